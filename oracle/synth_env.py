@@ -1,0 +1,200 @@
+"""ORACLE / TEST INFRASTRUCTURE — CPU (numpy) definition of the synthetic benchmark envs.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+The GPU path (xuanpolicy_amd/csrc/rollout.hip: xpa_synthbox_step) implements the same math;
+this file is the checker and the CPU baseline's environment.
+
+The reference ships no synthetic env; BASELINE.md / SURVEY.md §8(d) define `SynthBox(D, A)` to be
+plugged in through the reference's `NewEnv` hook (xuance/environment/__init__.py:76-78) with the
+`New_Env` step contract (xuance/environment/new_env/new_env.py:27-42):
+    reset() -> (obs, info{episode_step})
+    step(a) -> (obs, reward, terminated, truncated, info{episode_step, episode_score})
+
+Dynamics (all randomness from a stateless counter hash so CPU and GPU agree):
+    x   = W s + U clip(a, -1, 1) + NOISE * xi          (Box actions)
+    x   = W s + U[:, a] + NOISE * xi                     (Discrete actions)
+    s'  = tanh(x);  r = -mean(s'^2);  terminated = s'[0] > TERM_THRESH
+    truncated = episode_step >= max_episode_steps
+    reset: s0 = 0.1 * (2u - 1)
+    xi_d = sqrt(3) * (u1 + u2 + u3 + u4 - 2)   (mean 0, var 1),  u_j = hash_u01(seed, env, episode, (t*D+d)*4+j)
+"""
+import numpy as np
+
+MASK32 = 0xFFFFFFFF
+W_GAIN = 1.25
+U_GAIN = 0.6
+NOISE = 0.35
+TERM_THRESH = 0.92
+RESET_SCALE = 0.1
+SALT_W = 0x57A7E000
+SALT_U = 0x0AC7E000
+SALT_RESET = 0x5EED0000
+
+
+def mix32(x):
+    """murmur3 fmix32 over a uint32 numpy array (wrapping arithmetic)."""
+    x = np.asarray(x, dtype=np.uint32).copy()
+    with np.errstate(over="ignore"):
+        x ^= x >> np.uint32(16)
+        x *= np.uint32(0x85EBCA6B)
+        x ^= x >> np.uint32(13)
+        x *= np.uint32(0xC2B2AE35)
+        x ^= x >> np.uint32(16)
+    return x
+
+
+def hash4(seed, k0, k1, k2):
+    """h = mix(mix(mix(mix(seed) ^ k0) ^ k1) ^ k2), broadcasting uint32 keys."""
+    s = mix32(np.uint32(seed & MASK32))
+    h = mix32(s ^ np.asarray(k0, dtype=np.uint32))
+    h = mix32(h ^ np.asarray(k1, dtype=np.uint32))
+    h = mix32(h ^ np.asarray(k2, dtype=np.uint32))
+    return h
+
+
+def u01(h):
+    """Top 24 bits of a uint32 hash -> float32 uniform in [0, 1) (exact on CPU and GPU)."""
+    return (np.asarray(h, dtype=np.uint32) >> np.uint32(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+
+
+def synthbox_params(seed, obs_dim, act_dim, discrete=False):
+    """Dynamics matrices W [D, D] and U [D, A] (float32), drawn from the hash."""
+    D, A = obs_dim, act_dim
+    i = np.arange(D, dtype=np.uint32)[:, None]
+    j = np.arange(D, dtype=np.uint32)[None, :]
+    W = (2.0 * u01(hash4(seed, SALT_W, i, j)) - 1.0) * np.sqrt(3.0 / D) * W_GAIN
+    ja = np.arange(A, dtype=np.uint32)[None, :]
+    gain = U_GAIN if not discrete else 1.0
+    U = (2.0 * u01(hash4(seed, SALT_U, i, ja)) - 1.0) * np.sqrt(3.0 / max(A if not discrete else 1, 1)) * gain
+    return W.astype(np.float32), U.astype(np.float32)
+
+
+def synthbox_noise(seed, env, episode, t, D):
+    """xi [.., D] float32 for (env, episode, t) arrays of equal shape."""
+    env = np.asarray(env, dtype=np.uint32)[..., None]
+    ep = np.asarray(episode, dtype=np.uint32)[..., None]
+    t = np.asarray(t, dtype=np.uint32)[..., None]
+    d = np.arange(D, dtype=np.uint32)
+    base = (t * np.uint32(D) + d) * np.uint32(4)
+    acc = np.zeros(np.broadcast(env, d).shape, np.float32)
+    for k in range(4):
+        acc = acc + u01(hash4(seed, env, ep, base + np.uint32(k)))
+    return (acc - np.float32(2.0)) * np.float32(np.sqrt(3.0))
+
+
+def synthbox_reset_state(seed, env, episode, D):
+    env = np.asarray(env, dtype=np.uint32)[..., None]
+    ep = np.asarray(episode, dtype=np.uint32)[..., None]
+    d = np.arange(D, dtype=np.uint32)
+    return ((2.0 * u01(hash4(seed ^ SALT_RESET, env, ep, d)) - 1.0) * RESET_SCALE).astype(np.float32)
+
+
+class _Box:
+    def __init__(self, low, high, shape):
+        self.low = np.full(shape, low, np.float32)
+        self.high = np.full(shape, high, np.float32)
+        self.shape = tuple(shape)
+        self.dtype = np.float32
+
+
+class _Discrete:
+    def __init__(self, n):
+        self.n = int(n)
+        self.shape = ()
+        self.dtype = np.int64
+
+
+class SynthBoxEnv:
+    """One environment instance (stepped one at a time, like the reference's DummyVecEnv_Gym,
+    xuance/environment/gym/gym_vec_env.py:201-212)."""
+
+    def __init__(self, obs_dim, act_dim, seed=1, env_index=0, discrete=False, max_episode_steps=1000,
+                 spaces=None):
+        self.D, self.A, self.seed, self.index = obs_dim, act_dim, seed, env_index
+        self.discrete = discrete
+        self.W, self.U = synthbox_params(seed, obs_dim, act_dim, discrete)
+        self.max_episode_steps = max_episode_steps
+        if spaces is not None:
+            self.observation_space, self.action_space = spaces
+        else:
+            self.observation_space = _Box(-1.0, 1.0, (obs_dim,))
+            self.action_space = _Discrete(act_dim) if discrete else _Box(-1.0, 1.0, (act_dim,))
+        self.episode = -1
+        self._episode_step = 0
+        self._episode_score = 0.0
+        self.state = None
+
+    def close(self):
+        pass
+
+    def render(self, *a, **k):
+        pass
+
+    def reset(self):
+        self.episode += 1
+        self._episode_step = 0
+        self._episode_score = 0.0
+        self.state = synthbox_reset_state(self.seed, self.index, self.episode, self.D)
+        return self.state.copy(), {"episode_step": 0}
+
+    def step(self, action):
+        W, U = self.W, self.U
+        if self.discrete:
+            drive = U[:, int(action)]
+        else:
+            drive = U @ np.clip(np.asarray(action, np.float32), -1.0, 1.0)
+        xi = synthbox_noise(self.seed, self.index, self.episode, self._episode_step, self.D)
+        x = W @ self.state + drive + np.float32(NOISE) * xi
+        s = np.tanh(x.astype(np.float32))
+        r = float(-np.mean(s * s))
+        self._episode_step += 1
+        self._episode_score += r
+        term = bool(s[0] > TERM_THRESH)
+        trunc = bool(self._episode_step >= self.max_episode_steps)
+        self.state = s
+        info = {"episode_step": self._episode_step, "episode_score": self._episode_score}
+        return s.copy(), r, term, trunc, info
+
+
+class SynthBoxVec:
+    """numpy-vectorised variant of the same env ('second CPU variant with the env
+    vectorised in numpy').  Same semantics as N SynthBoxEnv instances in a DummyVecEnv."""
+
+    def __init__(self, n_envs, obs_dim, act_dim, seed=1, discrete=False, max_episode_steps=1000):
+        self.N, self.D, self.A, self.seed = n_envs, obs_dim, act_dim, seed
+        self.discrete = discrete
+        self.W, self.U = synthbox_params(seed, obs_dim, act_dim, discrete)
+        self.max_episode_steps = max_episode_steps
+        self.env_ids = np.arange(n_envs, dtype=np.uint32)
+        self.episode = np.zeros(n_envs, np.uint32)
+        self.ep_step = np.zeros(n_envs, np.int64)
+        self.ep_score = np.zeros(n_envs, np.float64)
+        self.state = synthbox_reset_state(seed, self.env_ids, self.episode, obs_dim)
+        self.num_envs = n_envs
+
+    def reset(self):
+        return self.state.copy()
+
+    def step(self, actions):
+        if self.discrete:
+            drive = self.U.T[np.asarray(actions, np.int64)]
+        else:
+            drive = np.clip(np.asarray(actions, np.float32), -1.0, 1.0) @ self.U.T
+        xi = synthbox_noise(self.seed, self.env_ids, self.episode, self.ep_step.astype(np.uint32), self.D)
+        x = self.state @ self.W.T + drive + np.float32(NOISE) * xi
+        s = np.tanh(x.astype(np.float32))
+        r = -np.mean(s * s, axis=1).astype(np.float32)
+        self.ep_step += 1
+        self.ep_score += r
+        term = s[:, 0] > TERM_THRESH
+        trunc = self.ep_step >= self.max_episode_steps
+        final = s.copy()
+        done = term | trunc
+        self.state = s
+        if done.any():
+            ids = np.nonzero(done)[0]
+            self.episode[ids] += 1
+            self.ep_step[ids] = 0
+            self.ep_score[ids] = 0.0
+            self.state[ids] = synthbox_reset_state(self.seed, self.env_ids[ids], self.episode[ids], self.D)
+        return final, r, term, trunc, self.state.copy()

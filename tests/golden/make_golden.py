@@ -1,0 +1,300 @@
+"""Capture golden vectors from the reference (XuanCe 1.0.5 fork at /root/reference).
+
+Run in the build container only (the reference never travels to the GPU box):
+    cd /tmp && python /root/repo/tests/golden/make_golden.py
+Writes small .npz fixtures next to this file (data only: inputs and the reference's outputs).
+
+Fixtures:
+  gae.npz      G1/G2  DummyOnPolicyBuffer store/finish_path/sample (memory_tools.py:143-245) under the
+                      agent's closure rules (ppoclip_agent.py:69-101): plain and Atari life-loss modes,
+                      use_gae on/off, plus sample() of two minibatches with adv-norm.
+  loss.npz     G3/G4  PPOCLIP_Learner.update / A2C_Learner.update (ppoclip_learner.py:24-65,
+                      a2c_learner.py:19-50) on Gaussian (A=6, 17) and Categorical (K=2, 6) heads:
+                      inputs, head outputs, d loss/d head (captured before grad clipping), info dict,
+                      parameters before and after the Adam step.
+  agent_*.npz  G5     two seeded iterations of PPOCLIP_Agent.train / A2C_Agent.train on SynthBox envs
+                      (oracle/synth_env.py) in the reference's DummyVecEnv_Gym: every stored step,
+                      every closure, the permutations, learner infos, initial and final parameters.
+  rms.npz      G7     RunningMeanStd (statistic_tools.py:35-112) update sequences.
+"""
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, REPO)
+
+import ref_loader  # noqa: E402
+
+xuance = ref_loader.import_reference()
+import torch  # noqa: E402
+import gym  # noqa: E402  (stub)
+from xuance.common.memory_tools import DummyOnPolicyBuffer  # noqa: E402
+from xuance.common.statistic_tools import RunningMeanStd  # noqa: E402
+from xuance.torch.representations import Basic_MLP  # noqa: E402
+from xuance.torch.policies import Gaussian_AC_Policy, Categorical_AC_Policy  # noqa: E402
+from xuance.torch.learners import PPOCLIP_Learner, A2C_Learner  # noqa: E402
+from xuance.torch.agents import PPOCLIP_Agent, A2C_Agent  # noqa: E402
+from xuance.environment.gym.gym_vec_env import DummyVecEnv_Gym  # noqa: E402
+from oracle.synth_env import SynthBoxEnv  # noqa: E402
+
+torch.set_num_threads(1)
+
+
+# ----------------------------------------------------------------------------------------------
+def capture_gae(seed=0, N=64, T=128, obs_dim=3, act_dim=2):
+    out = {}
+    rng = np.random.default_rng(seed)
+    for atari in (False, True):
+        for use_gae in (True, False):
+            tag = ("atari" if atari else "plain") + ("_gae" if use_gae else "_nogae")
+            buf = DummyOnPolicyBuffer(gym.spaces.Box(-1, 1, (obs_dim,)), gym.spaces.Box(-1, 1, (act_dim,)),
+                                      {"old_logp": ()}, N, T, use_gae, True, 0.99, 0.95)
+            closed = np.zeros((N, T), np.uint8)
+            boot = np.zeros((N, T), np.float32)
+            term_all = rng.random((N, T)) < 0.01
+            trunc_all = rng.random((N, T)) < 0.01
+            boot_all = rng.normal(0, 1, (N, T)).astype(np.float32)
+            for t in range(T):
+                obs = rng.normal(0, 1, (N, obs_dim)).astype(np.float32)
+                act = rng.normal(0, 1, (N, act_dim)).astype(np.float32)
+                rew = rng.normal(0, 1, N).astype(np.float32)
+                val = rng.normal(0, 1, N).astype(np.float32)
+                lp = rng.normal(-3, 1, N).astype(np.float32)
+                term, trunc = term_all[:, t], trunc_all[:, t]
+                buf.store(obs, act, rew, val, term, {"old_logp": lp})
+                if buf.full:
+                    # ppoclip_agent.py:69-75: close every env's path at buffer-full.
+                    for i in range(N):
+                        v = 0.0 if term[i] else boot_all[i, t]
+                        buf.finish_path(v, i)
+                        closed[i, T - 1], boot[i, T - 1] = 1, v
+                    break
+                for i in range(N):  # ppoclip_agent.py:89-101
+                    if term[i] or trunc[i]:
+                        if atari and not trunc[i]:
+                            continue  # life loss: masked d=1 mid-path, no closure
+                        v = 0.0 if term[i] else boot_all[i, t]
+                        buf.finish_path(v, i)
+                        closed[i, t], boot[i, t] = 1, v
+            out[tag + "/rew"] = buf.rewards.copy()
+            out[tag + "/val"] = buf.values.copy()
+            out[tag + "/term"] = buf.terminals.copy()
+            out[tag + "/closed"] = closed
+            out[tag + "/boot"] = boot
+            out[tag + "/adv"] = buf.advantages.copy()
+            out[tag + "/ret"] = buf.returns.copy()
+            if tag == "plain_gae":
+                out[tag + "/obs"] = buf.observations.copy()
+                out[tag + "/act"] = buf.actions.copy()
+                out[tag + "/logp"] = buf.auxiliary_infos["old_logp"].copy()
+                perm = np.arange(N * T)
+                rng.shuffle(perm)
+                B = N * T // 4
+                for k in range(2):
+                    idx = perm[k * B:(k + 1) * B]
+                    o, a, r, v, ad, ax = buf.sample(idx)
+                    out["sample%d/idx" % k] = idx.astype(np.int64)
+                    out["sample%d/obs" % k] = o
+                    out["sample%d/act" % k] = a
+                    out["sample%d/ret" % k] = r
+                    out["sample%d/val" % k] = v
+                    out["sample%d/adv" % k] = ad.astype(np.float32)
+                    out["sample%d/logp" % k] = ax["old_logp"]
+    np.savez_compressed(os.path.join(HERE, "gae.npz"), **out)
+    print("gae.npz", len(out))
+
+
+# ----------------------------------------------------------------------------------------------
+def _policy(D, A, discrete, hidden=(64,), seed=0):
+    torch.manual_seed(seed)
+    act = torch.nn.LeakyReLU
+    rep = Basic_MLP((D,), list(hidden), None, torch.nn.init.orthogonal_, act, "cpu")
+    if discrete:
+        return Categorical_AC_Policy(gym.spaces.Discrete(A), rep, list(hidden), list(hidden), None,
+                                     torch.nn.init.orthogonal_, act, "cpu")
+    return Gaussian_AC_Policy(gym.spaces.Box(-1, 1, (A,)), rep, list(hidden), list(hidden), None,
+                              torch.nn.init.orthogonal_, act, "cpu")
+
+
+def _sd(prefix, policy, out):
+    for k, v in policy.state_dict().items():
+        out[prefix + k] = v.detach().cpu().numpy().copy()
+
+
+def capture_loss(B=512, D=11):
+    out = {}
+    cases = [("ppo", "gaussian", 6), ("ppo", "gaussian", 17), ("ppo", "categorical", 2), ("ppo", "categorical", 6),
+             ("a2c", "gaussian", 6), ("a2c", "categorical", 6)]
+    for ci, (algo, dist, A) in enumerate(cases):
+        tag = "%s_%s_%d" % (algo, dist, A)
+        discrete = dist == "categorical"
+        policy = _policy(D, A, discrete, seed=100 + ci)
+        rng = np.random.default_rng(200 + ci)
+        obs = rng.normal(0, 1, (B, D)).astype(np.float32)
+        with torch.no_grad():
+            _, d0, v0 = policy(obs)
+            act = d0.stochastic_sample()
+            lp0 = d0.log_prob(act).numpy()
+        act = act.numpy().astype(np.float32)
+        old_logp = (lp0 + rng.normal(0, 0.3, B)).astype(np.float32)
+        adv = rng.normal(0, 1, B).astype(np.float32)
+        ret = rng.normal(0, 1, B).astype(np.float32)
+        val = rng.normal(0, 1, B).astype(np.float32)
+        _sd(tag + "/sd0/", policy, out)
+        opt = torch.optim.Adam(policy.parameters(), 4e-4, eps=1e-5)
+        sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.0, total_iters=1000)
+        cap = {}
+        head_mod = policy.actor.model if discrete else policy.actor.mu
+
+        def hook_head(m, i, o):
+            o.retain_grad()
+            cap["head"] = o
+
+        def hook_v(m, i, o):
+            o.retain_grad()
+            cap["v"] = o
+        h1 = head_mod.register_forward_hook(hook_head)
+        h2 = policy.critic.register_forward_hook(hook_v)
+        if not discrete:
+            h3 = policy.actor.logstd.register_hook(lambda g: cap.__setitem__("dlogstd", g.clone()))
+        ent_coef = 0.01
+        if algo == "ppo":
+            learner = PPOCLIP_Learner(policy, opt, sch, "cpu", "./", vf_coef=0.25, ent_coef=ent_coef, clip_range=0.2,
+                                      clip_grad_norm=0.5, use_grad_clip=True)
+            info = learner.update(obs, act, ret, val, adv, old_logp)
+        else:
+            learner = A2C_Learner(policy, opt, sch, "cpu", "./", vf_coef=0.25, ent_coef=ent_coef, clip_grad=0.5)
+            info = learner.update(obs, act, ret, adv)
+        h1.remove()
+        h2.remove()
+        if not discrete:
+            h3.remove()
+            out[tag + "/dlogstd"] = cap["dlogstd"].numpy()
+            out[tag + "/logstd0"] = out[tag + "/sd0/actor.logstd"]
+        out[tag + "/obs"] = obs
+        out[tag + "/act"] = act
+        out[tag + "/old_logp"] = old_logp
+        out[tag + "/adv"] = adv
+        out[tag + "/ret"] = ret
+        out[tag + "/val"] = val
+        out[tag + "/head"] = cap["head"].detach().numpy()
+        out[tag + "/dhead"] = cap["head"].grad.numpy()
+        out[tag + "/v"] = cap["v"].detach().numpy()
+        out[tag + "/dv"] = cap["v"].grad.numpy()
+        for k, v in info.items():
+            out[tag + "/info/" + k] = np.asarray(float(v))
+        _sd(tag + "/sd1/", policy, out)
+    np.savez_compressed(os.path.join(HERE, "loss.npz"), **out)
+    print("loss.npz", len(out))
+
+
+# ----------------------------------------------------------------------------------------------
+def capture_agent(algo, discrete, D, A, N=8, T=128, iters=2, max_ep=50, seed=7):
+    tag = "agent_%s_%s" % (algo, "cat" if discrete else "gauss")
+    cfg = types.SimpleNamespace(render=False, n_steps=T, n_minibatch=4, n_epoch=2, gamma=0.99, gae_lambda=0.95,
+                                env_name="SynthBox", use_gae=True, use_advnorm=True, device="cpu", model_dir="./models/",
+                                log_dir="./logs/", vf_coef=0.25, ent_coef=0.01, clip_range=0.2, clip_grad_norm=0.5,
+                                use_grad_clip=True, clip_grad=0.5, use_obsnorm=True, use_rewnorm=True,
+                                obsnorm_range=5, rewnorm_range=5, seed=seed, logger="tensorboard", test_mode=False)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    spaces = (gym.spaces.Box(-1, 1, (D,)), gym.spaces.Discrete(A) if discrete else gym.spaces.Box(-1, 1, (A,)))
+    envs = DummyVecEnv_Gym([(lambda i=i: SynthBoxEnv(D, A, seed=seed, env_index=i, discrete=discrete,
+                                                     max_episode_steps=max_ep, spaces=spaces)) for i in range(N)])
+    policy = _policy(D, A, discrete, seed=seed)
+    out = {}
+    _sd("sd0/", policy, out)
+    opt = torch.optim.Adam(policy.parameters(), 4e-4, eps=1e-5)
+    sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.0, total_iters=10000)
+    Agent = PPOCLIP_Agent if algo == "ppo" else A2C_Agent
+    agent = Agent(cfg, envs, policy, opt, sch, "cpu")
+    envs.reset()
+    rec = {"closed": np.zeros((iters, N, T), np.uint8), "boot": np.zeros((iters, N, T), np.float32)}
+    snaps, perms, infos = [], [], []
+    mem = agent.memory
+    it = {"k": 0}
+    orig_fp, orig_clear, orig_update = mem.finish_path, mem.clear, agent.learner.update
+    orig_shuffle = np.random.shuffle
+
+    def finish_path(val, i):
+        end = mem.n_size if mem.full else mem.ptr
+        if end > mem.start_ids[i] and it["k"] < iters:
+            rec["closed"][it["k"], i, end - 1] = 1
+            rec["boot"][it["k"], i, end - 1] = val
+        return orig_fp(val, i)
+
+    def clear():
+        snaps.append({"obs": mem.observations.copy(), "act": mem.actions.copy(), "rew": mem.rewards.copy(),
+                      "val": mem.values.copy(), "term": mem.terminals.copy(), "ret": mem.returns.copy(),
+                      "adv": mem.advantages.copy(),
+                      "logp": mem.auxiliary_infos["old_logp"].copy() if algo == "ppo" else np.zeros((N, T), np.float32)})
+        it["k"] += 1
+        return orig_clear()
+
+    def update(*a):
+        info = orig_update(*a)
+        infos.append([float(info[k]) for k in ("actor-loss", "critic-loss", "entropy", "learning_rate",
+                                                "predict_value")] + [float(info.get("clip_ratio", np.nan))])
+        return info
+
+    def shuffle(x):
+        orig_shuffle(x)
+        perms.append(x.copy())
+
+    mem.finish_path, mem.clear, agent.learner.update = finish_path, clear, update
+    np.random.shuffle = shuffle
+    try:
+        agent.train(iters * T)
+    finally:
+        np.random.shuffle = orig_shuffle
+    for k in ("obs", "act", "rew", "val", "term", "ret", "adv", "logp"):
+        out[k] = np.stack([s[k] for s in snaps])
+    out["closed"], out["boot"] = rec["closed"], rec["boot"]
+    out["perms"] = np.stack(perms).astype(np.int64)
+    out["infos"] = np.asarray(infos, np.float64)
+    out["config"] = np.asarray([N, T, D, A, cfg.n_epoch, cfg.n_minibatch, int(discrete), max_ep, seed], np.int64)
+    _sd("sd1/", policy, out)
+    np.savez_compressed(os.path.join(HERE, tag + ".npz"), **out)
+    print(tag, len(out), "closures", int(out["closed"].sum()))
+
+
+# ----------------------------------------------------------------------------------------------
+def capture_rms(seed=3):
+    rng = np.random.default_rng(seed)
+    out = {}
+    rms = RunningMeanStd((5,), comm=None, use_mpi=False)
+    xs, means, vars_, counts = [], [], [], []
+    for k in range(20):
+        x = (rng.normal(0, 1, (64, 5)) * (1 + k % 3) + k * 0.1).astype(np.float32)
+        rms.update(x)
+        xs.append(x)
+        means.append(rms.mean.copy())
+        vars_.append(rms.var.copy())
+        counts.append(rms.count)
+    out["obs/x"], out["obs/mean"], out["obs/var"] = np.stack(xs), np.stack(means), np.stack(vars_)
+    out["obs/count"] = np.asarray(counts, np.float64)
+    ret = RunningMeanStd((), comm=None, use_mpi=False)
+    rs = rng.normal(0, 3, 200).astype(np.float32)
+    rm, rv = [], []
+    for r in rs:
+        ret.update(np.asarray([r], np.float32))
+        rm.append(float(ret.mean))
+        rv.append(float(ret.var))
+    out["ret/x"], out["ret/mean"], out["ret/var"] = rs, np.asarray(rm), np.asarray(rv)
+    np.savez_compressed(os.path.join(HERE, "rms.npz"), **out)
+    print("rms.npz", len(out))
+
+
+if __name__ == "__main__":
+    os.makedirs("/tmp/xref_run", exist_ok=True)
+    os.chdir("/tmp/xref_run")
+    capture_gae()
+    capture_loss()
+    capture_agent("ppo", False, 17, 6)
+    capture_agent("a2c", True, 4, 2)
+    capture_rms()
