@@ -1,0 +1,163 @@
+/*
+ * xuanpolicy_amd — C ABI of the MI355X (gfx950) on-policy PPO-Clip / A2C hot path.
+ *
+ * Library: xuanpolicy_amd/libxuanpolicy_amd.so (hipcc --offload-arch=gfx950).
+ * Conventions (all entry points):
+ *   - every pointer is a device pointer owned by the caller (torch tensors on the Python side);
+ *     nothing is allocated, freed or synchronised inside, so every call is hipGraph-capturable;
+ *   - calls are ordered on `stream` (a hipStream_t; NULL = the legacy default stream);
+ *   - the return value is a hipError_t as int: 0 = success, 1 (hipErrorInvalidValue) = bad
+ *     arguments (nothing launched), anything else = the launch error;
+ *   - [n_envs, horizon] arrays are row-major: element (env n, step t) at n*horizon + t, the layout
+ *     of the reference's DummyOnPolicyBuffer (memory_tools.py:12-36, flat index env*T + step at
+ *     memory_tools.py:234).
+ *
+ * The reference (XuanCe 1.0.5 fork, pure Python) has no C ABI; each entry point names the
+ * reference function it replaces (paths relative to the reference root).
+ */
+#ifndef XUANPOLICY_AMD_H
+#define XUANPOLICY_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t *xpa_stream_t; /* == hipStream_t */
+
+#define XPA_ABI_VERSION 1
+
+/* Device-resident rollout cursor read by the per-step kernels, so a captured step replays
+ * without host-side arguments changing: ptr = buffer column being written (DummyOnPolicyBuffer.ptr,
+ * memory_tools.py:203), step = global env-step counter (RNG key). */
+typedef struct {
+    int32_t ptr;
+    uint32_t step;
+    int32_t reserved[2];
+} xpa_cursor_t;
+
+enum { XPA_ALGO_PPO = 0, XPA_ALGO_A2C = 1 };
+enum { XPA_DIST_GAUSSIAN = 0, XPA_DIST_CATEGORICAL = 1 };
+
+/* Loss scalars written by xpa_policy_loss_finalize, in this order. */
+enum {
+    XPA_OUT_ACTOR_LOSS = 0, /* -mean(min(clip(r)A, rA))  or  -mean(A logp)                        */
+    XPA_OUT_CRITIC_LOSS = 1, /* mean((v - R)^2)                                                    */
+    XPA_OUT_ENTROPY = 2,     /* mean(entropy)                                                       */
+    XPA_OUT_LOSS = 3,        /* actor - ent_coef*entropy + vf_coef*critic                           */
+    XPA_OUT_CLIP_RATIO = 4,  /* frac(r < 1-eps or r > 1+eps)   (PPO only, 0 for A2C)                */
+    XPA_OUT_VALUE_MEAN = 5,  /* mean(v)                                                              */
+    XPA_OUT_COUNT = 6
+};
+
+int xpa_abi_version(void);
+
+/* K1 — GAE / discounted returns over a whole [n_envs, horizon] buffer.
+ * Replaces DummyOnPolicyBuffer.finish_path (xuance/common/memory_tools.py:206-229) called for
+ * every path the agent closes (xuance/torch/agents/policy_gradient/ppoclip_agent.py:69-101,
+ * a2c_agent.py:66-98).  closed[n,t] != 0 marks the last step of a path closed with bootstrap
+ * value boot[n,t]; positions after a row's last closure are not written (as in the reference).
+ * use_gae = 0 selects the discount_cumsum branch (memory_tools.py:222-225).
+ * Reads rew/val/term (f32), closed (u8), boot (f32, only where closed); writes adv, ret (f32). */
+int xpa_gae_scan(const float *rew, const float *val, const float *term, const uint8_t *closed,
+                 const float *boot, int64_t n_envs, int64_t horizon, float gamma, float gae_lambda,
+                 int use_gae, float *adv, float *ret, xpa_stream_t stream);
+
+/* K4 — minibatch gather.  Replaces the fancy-index gather of DummyOnPolicyBuffer.sample
+ * (memory_tools.py:231-240) for the observation rows (the rest is read through `idx` by the loss
+ * kernel), and produces the per-minibatch advantage moments for adv-norm (memory_tools.py:241-242).
+ * obs_out[b] = obs[idx[b]] (row_bytes each); adv_partials[g] = (sum, sum of squares) in f64 over
+ * rows [g*256, (g+1)*256); xpa_gather_num_partials(batch) rows.  adv/adv_partials may be NULL.
+ * n_rows = rows of obs/adv: an index outside [0, n_rows) is never dereferenced (its output row is
+ * zeroed and it adds nothing to the moments). */
+int64_t xpa_gather_num_partials(int64_t batch);
+int xpa_gather_minibatch(const int64_t *idx, int64_t batch, int64_t n_rows, const void *obs,
+                         int64_t obs_row_bytes, void *obs_out, const float *adv, double *adv_partials,
+                         xpa_stream_t stream);
+
+/* K2 — fused policy/value loss forward + backward for one minibatch.
+ * Replaces PPOCLIP_Learner.update's loss (xuance/torch/learners/policy_gradient/ppoclip_learner.py:32-44)
+ * and A2C_Learner.update's loss (a2c_learner.py:24-31), with DiagGaussianDistribution /
+ * CategoricalDistribution log_prob and entropy (xuance/torch/utils/distributions.py:39-101).
+ * head: mu [batch, act_dim] (Gaussian, with logstd [act_dim]) or logits [batch, act_dim] (Categorical).
+ * v: predicted values [batch].  Per-sample inputs act/old_logp/adv/ret are read at row idx[b]
+ * (idx == NULL: row b; an idx outside [0, n_rows) is never dereferenced and the sample contributes
+ * nothing); act is [n_rows, act_dim] (Gaussian) or [n_rows] float-coded indices (Categorical).
+ * adv_partials (from xpa_gather_minibatch, n_adv_partials rows) != NULL applies per-minibatch
+ * normalisation (adv - mean) / (std_pop + 1e-8) (memory_tools.py:241-242); NULL uses adv as given.
+ * Writes d loss/d head [batch, act_dim], d loss/d v [batch] and per-block partial sums
+ * (xpa_loss_num_partials(batch) rows of xpa_loss_partial_width(act_dim) floats). */
+int64_t xpa_loss_num_partials(int64_t batch);
+int64_t xpa_loss_partial_width(int64_t act_dim);
+int xpa_policy_loss_fwd_bwd(int algo, int dist, int64_t batch, int64_t act_dim, const float *head,
+                            const float *logstd, const float *v, const int64_t *idx, int64_t n_rows,
+                            const float *act,
+                            const float *old_logp, const float *adv, const float *ret,
+                            const double *adv_partials, int64_t n_adv_partials, float clip_range,
+                            float vf_coef, float ent_coef, float *d_head, float *d_v, float *partials,
+                            xpa_stream_t stream);
+/* Deterministic reduction of the partials: scalars[XPA_OUT_COUNT] (the info dict of
+ * ppoclip_learner.py:53-63 / a2c_learner.py:36-47) and d loss/d logstd [act_dim] (Gaussian). */
+int xpa_policy_loss_finalize(int algo, int dist, int64_t batch, int64_t act_dim, const float *partials,
+                             int64_t n_partials, float vf_coef, float ent_coef, float *scalars,
+                             float *d_logstd, xpa_stream_t stream);
+
+/* K5 — RunningMeanStd over observations (xuance/common/statistic_tools.py:63-112) and observation
+ * normalisation (xuance/torch/agents/agent.py:104-116).
+ * xpa_rms_partials: per-block (mean, M2) in f64 over x[n, dim] (row stride ld floats).
+ * xpa_rms_merge: Chan merge of the partials into the batch moments, then update_from_moments into
+ * mean/var (f32 [dim]) and *count (f64) — one block.
+ * xpa_obs_normalize: out = clip((x - mean) / (sqrt(var) + 1e-8), -clip_range, clip_range);
+ * also copied to col_out + cursor->ptr*dim (row stride col_ld) when col_out != NULL. */
+int64_t xpa_rms_num_partials(int64_t n);
+int xpa_rms_partials(const float *x, int64_t n, int64_t dim, int64_t ld, double *partials,
+                     xpa_stream_t stream);
+int xpa_rms_merge(const double *partials, int64_t n_partials, int64_t n, int64_t dim, float *mean,
+                  float *var, double *count, xpa_stream_t stream);
+int xpa_obs_normalize(const float *x, int64_t n, int64_t dim, int64_t ldx, const float *mean,
+                      const float *var, float clip_range, float *out, int64_t ldo, float *col_out,
+                      int64_t col_ld, const xpa_cursor_t *cursor, xpa_stream_t stream);
+
+/* K3 — rollout action sampling + log-prob + store.  Replaces PPOCLIP_Agent._action
+ * (ppoclip_agent.py:50-57: stochastic_sample + log_prob + three D2H copies) and the action/value/
+ * log-prob part of DummyOnPolicyBuffer.store (memory_tools.py:196-204).
+ * Gaussian: a = mu + exp(logstd) * eps, eps ~ N(0,1) from a counter hash of (seed, cursor->step, env, dim).
+ * Categorical: inverse-CDF sample of softmax(logits) from one hashed uniform per env.
+ * Stores act [n_envs, horizon, act_dim] (float-coded index for Categorical), logp and val
+ * [n_envs, horizon] at column cursor->ptr, and the env input into env_in (row stride ld_env):
+ * clip(a, -act_clip, act_clip) (Gaussian) or one-hot(a) (Categorical). */
+int xpa_rollout_sample(int dist, int64_t n_envs, int64_t act_dim, int64_t horizon, const float *head,
+                       const float *logstd, const float *v, const xpa_cursor_t *cursor, uint32_t seed,
+                       float act_clip, float *buf_act, float *buf_logp, float *buf_val, float *env_in,
+                       int64_t ld_env, xpa_stream_t stream);
+
+/* K7 — SynthBox environment step (the synthetic env plugged in through the reference's NewEnv hook,
+ * xuance/environment/__init__.py:76-78, replacing DummyVecEnv_Gym.step_wait, gym_vec_env.py:201-212).
+ * pre[n, :] = W s_n + U a_n (a GEMM the caller runs on X = [s | env action] with Wcat = [W | U]).
+ * s' = tanh(pre + noise * xi), r = -mean(s'^2), terminated = s'[0] > term_thresh,
+ * truncated = episode_step + 1 >= max_episode_steps; done envs auto-reset (reset_obs semantics).
+ * Writes final_obs (s'), state (X[:, :obs_dim], row stride ld_state: s' or the reset state),
+ * rew, term, trunc, and the per-env episode counters. */
+int xpa_synthbox_step(int64_t n_envs, int64_t obs_dim, const float *pre, uint32_t seed,
+                      int32_t max_episode_steps, float noise, float term_thresh, float reset_scale,
+                      float *state, int64_t ld_state, float *final_obs, float *rew, uint8_t *term,
+                      uint8_t *trunc, int32_t *ep_step, uint32_t *ep_index, float *ep_score,
+                      float *ep_last_score, int32_t *ep_last_len, xpa_stream_t stream);
+
+/* K8 — rollout post-step bookkeeping (one block).  Replaces, per step, DummyOnPolicyBuffer.store of
+ * rewards/terminals (memory_tools.py:196-204) with reward normalisation (agent.py:118-123), the
+ * return tracker and ret_rms update (ppoclip_agent.py:87-92 with the (1-term) mask; a2c_agent.py:84
+ * without), and the agent's path closing (ppoclip_agent.py:69-75, 89-101): closed/boot columns for
+ * xpa_gae_scan (atari_lifeloss = 1: a terminal without truncation does not close the path,
+ * ppoclip_agent.py:93-94).  Advances cursor->ptr (mod horizon) and cursor->step. */
+int xpa_rollout_post(int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term,
+                     const uint8_t *trunc, const float *v_boot, xpa_cursor_t *cursor, float *ret_mean,
+                     float *ret_var, double *ret_count, float *returns, float *buf_rew, float *buf_term,
+                     uint8_t *buf_closed, float *buf_boot, float gamma, int mask_returns,
+                     int use_rewnorm, float rew_range, int atari_lifeloss, xpa_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XUANPOLICY_AMD_H */

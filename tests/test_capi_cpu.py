@@ -1,0 +1,107 @@
+"""CPU tests of the drop-in boundary: the C-ABI library builds, loads and exports every symbol that
+include/xuanpolicy_amd.h declares; the Python bindings cover them; no compute call without a GPU."""
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+from xuanpolicy_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_functions():
+    src = open(os.path.join(REPO, "include", "xuanpolicy_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(xpa_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    _lib.build_library()
+    return _lib.load()
+
+
+def test_header_symbols_exported(lib):
+    names = _header_functions()
+    assert len(names) >= 15
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (xpa_\w+)", out))
+    assert set(names) == exported, (set(names) ^ exported)
+    for n in names:
+        assert hasattr(lib, n)
+
+
+def test_bindings_cover_header():
+    assert set(_header_functions()) == set(_lib.SIGNATURES)
+
+
+def test_abi_version_and_size_helpers(lib):
+    assert lib.xpa_abi_version() == _lib.ABI_VERSION
+    assert lib.xpa_loss_num_partials(65536) == 256
+    assert lib.xpa_loss_partial_width(6) == 11
+    assert lib.xpa_gather_num_partials(65537) == 257
+    assert lib.xpa_rms_num_partials(4096) == 64
+
+
+def test_invalid_arguments_rejected_before_launch(lib):
+    # null pointers / bad shapes return hipErrorInvalidValue (1) without touching a device
+    assert lib.xpa_gae_scan(None, None, None, None, None, 4, 4, 0.99, 0.95, 1, None, None, None) == 1
+    assert lib.xpa_gae_scan(None, None, None, None, None, -1, 4, 0.99, 0.95, 1, None, None, None) == 1
+    assert lib.xpa_policy_loss_fwd_bwd(0, 0, 0, 6, *([None] * 4), 1, *([None] * 5), 0, 0.2, 0.25, 0.0,
+                                       None, None, None, None) == 1
+    assert lib.xpa_policy_loss_fwd_bwd(0, 1, 8, 1, *([None] * 4), 8, *([None] * 5), 0, 0.2, 0.25, 0.0,
+                                       None, None, None, None) == 1
+    assert lib.xpa_gather_minibatch(None, 8, 8, None, 4, None, None, None, None) == 1
+    assert lib.xpa_rms_merge(None, 3, 100, 4, None, None, None, None) == 1
+
+
+def test_ops_refuse_cpu_tensors():
+    from xuanpolicy_amd import ops
+    x = torch.zeros(4, 8)
+    with pytest.raises(ValueError, match="ROCm device"):
+        ops.gae_scan(x, x, x, torch.zeros(4, 8, dtype=torch.uint8), x, 0.99, 0.95)
+    with pytest.raises(ValueError, match="ROCm device"):
+        ops.policy_loss("ppo", "gaussian", torch.zeros(4, 2), torch.zeros(2), torch.zeros(4), torch.zeros(8),
+                        torch.zeros(4), torch.zeros(4), old_logp=torch.zeros(4))
+
+
+def test_config_cascade():
+    from xuanpolicy_amd.runner import get_arguments
+    a = get_arguments("ppo", "synthbox", "SynthBox-v0")
+    assert (a.agent, a.parallels, a.n_steps, a.n_epoch, a.n_minibatch) == ("PPO_Clip", 4096, 128, 16, 8)
+    assert a.representation_hidden_size == [256] and a.clip_grad_norm == 0.5 and a.use_obsnorm
+    b = get_arguments("a2c", "synthbox", "SynthBox-v0")
+    assert b.agent == "A2C" and b.discrete and b.clip_grad == 0.5
+
+
+def test_registries_match_reference_names():
+    from xuanpolicy_amd import agents, learners, policies
+    assert set(agents.REGISTRY) == {"PPO_Clip", "A2C"}
+    assert set(learners.REGISTRY) == {"PPO_Clip", "A2C"}
+    assert {"Gaussian_AC", "Categorical_AC"} <= set(policies.REGISTRY)
+
+
+def test_policy_state_dict_keys_match_reference(golden):
+    """Our Gaussian/Categorical AC modules load the reference's state_dict (checkpoint interchange)."""
+    from xuanpolicy_amd.policies import Basic_MLP, Categorical_AC_Policy, Gaussian_AC_Policy
+
+    class Box:
+        shape = (6,)
+
+    class Disc:
+        n, shape = 6, ()
+    g = golden("loss.npz")
+    for tag, cls, space in (("ppo_gaussian_6", Gaussian_AC_Policy, Box()),
+                            ("ppo_categorical_6", Categorical_AC_Policy, Disc())):
+        D = g[tag + "/obs"].shape[1]
+        rep = Basic_MLP((D,), [64], None, torch.nn.init.orthogonal_, torch.nn.LeakyReLU, "cpu")
+        pol = cls(space, rep, [64], [64], None, torch.nn.init.orthogonal_, torch.nn.LeakyReLU, "cpu")
+        sd = {k[len(tag) + 5:]: torch.as_tensor(v) for k, v in g.items() if k.startswith(tag + "/sd0/")}
+        pol.load_state_dict(sd)
+        out, dist, v = pol(g[tag + "/obs"])
+        head = dist.mu if hasattr(dist, "mu") else dist.logits
+        assert torch.allclose(head, torch.as_tensor(g[tag + "/head"]), atol=1e-5)
+        assert torch.allclose(v, torch.as_tensor(g[tag + "/v"]), atol=1e-5)

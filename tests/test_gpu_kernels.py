@@ -1,0 +1,353 @@
+"""GPU parity tests: every HIP kernel through the C ABI vs the CPU oracle / reference golden vectors.
+Run on the MI355X box (pytest -m gpu)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cpu_ref, synth_env
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _setup():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cpu_ref.build_oracle()
+    from xuanpolicy_amd import _lib
+    _lib.load()
+
+
+def _d(x, dtype=None):
+    t = torch.as_tensor(np.ascontiguousarray(x))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.to(DEV)
+
+
+def _h(t):
+    return t.detach().cpu().numpy()
+
+
+# ---------------------------------------------------------------------------------------------- K1
+@pytest.mark.parametrize("tag", ["plain_gae", "plain_nogae", "atari_gae", "atari_nogae"])
+def test_gae_kernel_golden(golden, tag):
+    from xuanpolicy_amd import ops
+    g = golden("gae.npz")
+    use_gae = tag.endswith("_gae")
+    adv, ret = ops.gae_scan(_d(g[tag + "/rew"]), _d(g[tag + "/val"]), _d(g[tag + "/term"]), _d(g[tag + "/closed"]),
+                            _d(g[tag + "/boot"]), 0.99, 0.95, use_gae)
+    np.testing.assert_allclose(_h(adv), g[tag + "/adv"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(_h(ret), g[tag + "/ret"], rtol=1e-5, atol=1e-5)
+
+
+def _random_gae_case(rng, N, T, p_close=0.02, p_term=0.02, close_last=True):
+    rew = rng.normal(0, 1, (N, T)).astype(np.float32)
+    val = rng.normal(0, 1, (N, T)).astype(np.float32)
+    term = (rng.random((N, T)) < p_term).astype(np.float32)
+    closed = (rng.random((N, T)) < p_close).astype(np.uint8)
+    if close_last:
+        closed[:, -1] = 1
+    boot = np.where(closed > 0, rng.normal(0, 1, (N, T)), 0).astype(np.float32)
+    boot[term > 0] = 0.0
+    return rew, val, term, closed, boot
+
+
+@pytest.mark.parametrize("N,T", [(1, 1), (7, 63), (64, 128), (33, 129), (5, 1024), (130, 4), (3, 257), (1000, 128)])
+@pytest.mark.parametrize("use_gae", [True, False])
+def test_gae_kernel_random_shapes(N, T, use_gae):
+    from xuanpolicy_amd import ops
+    rng = np.random.default_rng(N * 1000 + T)
+    # open tails: about a third of the rows are not closed at T-1
+    rew, val, term, closed, boot = _random_gae_case(rng, N, T, close_last=False)
+    closed[rng.random(N) < 0.66, -1] = 1
+    ref_adv = np.full((N, T), -7.0, np.float32)
+    ref_ret = np.full((N, T), -7.0, np.float32)
+    cpu_ref.gae_rows(rew, val, term, closed, boot, 0.99, 0.95, use_gae, adv=ref_adv, ret=ref_ret)
+    adv = torch.full((N, T), -7.0, device=DEV)
+    ret = torch.full((N, T), -7.0, device=DEV)
+    ops.gae_scan(_d(rew), _d(val), _d(term), _d(closed), _d(boot), 0.99, 0.95, use_gae, adv=adv, ret=ret)
+    np.testing.assert_allclose(_h(adv), ref_adv, rtol=1e-5, atol=2e-5)
+    np.testing.assert_allclose(_h(ret), ref_ret, rtol=1e-5, atol=2e-5)
+
+
+def test_gae_kernel_unaligned_views():
+    """float4 path needs 16-B alignment; an offset view must take the scalar path and stay correct."""
+    from xuanpolicy_amd import ops
+    rng = np.random.default_rng(5)
+    N, T = 17, 128
+    rew, val, term, closed, boot = _random_gae_case(rng, N, T)
+    big = torch.zeros(N * T + 1, device=DEV)
+    r_view = big[1:].view(N, T)
+    r_view.copy_(_d(rew))
+    adv, ret = ops.gae_scan(r_view, _d(val), _d(term), _d(closed), _d(boot), 0.98, 0.9)
+    ref_adv, ref_ret = cpu_ref.gae_rows(rew, val, term, closed, boot, 0.98, 0.9)
+    np.testing.assert_allclose(_h(adv), ref_adv, rtol=1e-5, atol=2e-5)
+    np.testing.assert_allclose(_h(ret), ref_ret, rtol=1e-5, atol=2e-5)
+
+
+def test_gae_kernel_full_size_properties():
+    """BASELINE sizes (4096 x 128 and 262144 x 128): sampled rows vs the oracle, plus the
+    size-independent identity ret = adv + v."""
+    from xuanpolicy_amd import ops
+    for N in (4096, 262144):
+        T = 128
+        g = torch.Generator(device=DEV).manual_seed(N)
+        rew = torch.randn(N, T, device=DEV, generator=g)
+        val = torch.randn(N, T, device=DEV, generator=g)
+        term = (torch.rand(N, T, device=DEV, generator=g) < 0.01).float()
+        closed = (torch.rand(N, T, device=DEV, generator=g) < 0.001).to(torch.uint8)
+        closed[:, -1] = 1
+        boot = torch.randn(N, T, device=DEV, generator=g) * closed
+        adv, ret = ops.gae_scan(rew, val, term, closed, boot, 0.99, 0.95)
+        np.testing.assert_allclose(_h(ret), _h(adv + val), rtol=0, atol=1e-6)
+        rows = torch.randint(0, N, (256,), generator=torch.Generator().manual_seed(1)).to(DEV)
+        ra, rr = cpu_ref.gae_rows(_h(rew[rows]), _h(val[rows]), _h(term[rows]), _h(closed[rows]), _h(boot[rows]),
+                                  0.99, 0.95)
+        np.testing.assert_allclose(_h(adv[rows]), ra, rtol=1e-5, atol=2e-5)
+
+
+# ---------------------------------------------------------------------------------------------- K2
+LOSS_CASES = ["ppo_gaussian_6", "ppo_gaussian_17", "ppo_categorical_2", "ppo_categorical_6", "a2c_gaussian_6",
+              "a2c_categorical_6"]
+
+
+@pytest.mark.parametrize("tag", LOSS_CASES)
+def test_loss_kernel_golden(golden, tag):
+    from xuanpolicy_amd import ops
+    g = golden("loss.npz")
+    algo, dist, _ = tag.split("_")
+    sc, dh, dls, dv = ops.policy_loss(algo, dist, _d(g[tag + "/head"]),
+                                      _d(g[tag + "/logstd0"]) if dist == "gaussian" else None, _d(g[tag + "/v"]),
+                                      _d(g[tag + "/act"]), _d(g[tag + "/adv"]), _d(g[tag + "/ret"]),
+                                      old_logp=_d(g[tag + "/old_logp"]) if algo == "ppo" else None,
+                                      clip_range=0.2, vf_coef=0.25, ent_coef=0.01)
+    sc = _h(sc)
+    info = {k: float(g[tag + "/info/" + k]) for k in ("actor-loss", "critic-loss", "entropy", "predict_value")}
+    assert abs(sc[0] - info["actor-loss"]) < 1e-5
+    assert abs(sc[1] - info["critic-loss"]) < 1e-5
+    assert abs(sc[2] - info["entropy"]) < 1e-5
+    assert abs(sc[5] - info["predict_value"]) < 1e-6
+    loss = info["actor-loss"] - 0.01 * info["entropy"] + 0.25 * info["critic-loss"]
+    assert abs(sc[3] - loss) < 1e-4
+    if algo == "ppo":
+        assert abs(sc[4] - float(g[tag + "/info/clip_ratio"])) < 1e-7
+    np.testing.assert_allclose(_h(dh), g[tag + "/dhead"], rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(_h(dv), g[tag + "/dv"], rtol=1e-4, atol=1e-8)
+    if dist == "gaussian":
+        np.testing.assert_allclose(_h(dls), g[tag + "/dlogstd"], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("algo,dist,A,B", [("ppo", "gaussian", 17, 65536), ("ppo", "categorical", 18, 4097),
+                                           ("a2c", "gaussian", 6, 1000), ("a2c", "categorical", 6, 257)])
+def test_loss_kernel_indexed_advnorm(algo, dist, A, B):
+    """idx-gathered inputs + per-minibatch adv-norm from the gather kernel's moments vs the oracle."""
+    from xuanpolicy_amd import ops
+    rng = np.random.default_rng(A * 7 + B)
+    rows = 3 * B
+    head = rng.normal(0, 0.5, (B, A)).astype(np.float32)
+    logstd = (-1 + rng.normal(0, 0.1, A)).astype(np.float32)
+    v = rng.normal(0, 1, B).astype(np.float32)
+    if dist == "gaussian":
+        act_all = rng.normal(0, 0.6, (rows, A)).astype(np.float32)
+    else:
+        act_all = rng.integers(0, A, rows).astype(np.float32)
+    adv_all = (rng.normal(0.3, 2.0, rows)).astype(np.float32)
+    ret_all = rng.normal(0, 1, rows).astype(np.float32)
+    logp_all = rng.normal(-3, 1, rows).astype(np.float32)
+    idx = rng.permutation(rows)[:B].astype(np.int64)
+    obs_all = rng.normal(0, 1, (rows, 5)).astype(np.float32)
+    idx_d = _d(idx)
+    obs_mb, part = ops.gather_minibatch(idx_d, _d(obs_all), adv=_d(adv_all))
+    np.testing.assert_array_equal(_h(obs_mb), obs_all[idx])
+    a = adv_all[idx].astype(np.float64)
+    np.testing.assert_allclose(_h(part).sum(0), [a.sum(), (a * a).sum()], rtol=1e-9)
+    sc, dh, dls, dv = ops.policy_loss(algo, dist, _d(head), _d(logstd) if dist == "gaussian" else None, _d(v),
+                                      _d(act_all), _d(adv_all), _d(ret_all), old_logp=_d(logp_all), idx=idx_d,
+                                      adv_partials=part, clip_range=0.2, vf_coef=0.5, ent_coef=0.01)
+    adv_n = (adv_all[idx] - adv_all[idx].mean()) / (adv_all[idx].std() + 1e-8)
+    if dist == "gaussian":
+        # old_logp near the current logp so ratios straddle the clip range
+        sc_s = np.exp(logstd)
+        lp = (-(act_all[idx] - head) ** 2 / (2 * sc_s ** 2) - logstd - 0.5 * np.log(2 * np.pi)).sum(-1)
+        logp_all[idx] = lp + rng.normal(0, 0.3, B)
+        sc, dh, dls, dv = ops.policy_loss(algo, dist, _d(head), _d(logstd), _d(v), _d(act_all), _d(adv_all),
+                                          _d(ret_all), old_logp=_d(logp_all), idx=idx_d, adv_partials=part,
+                                          clip_range=0.2, vf_coef=0.5, ent_coef=0.01)
+    info, rdh, rdls, rdv = cpu_ref.loss_grads_ref(algo, dist, head, logstd, v, act_all[idx], adv_n, ret_all[idx],
+                                                  logp_all[idx], 0.2, 0.5, 0.01)
+    sc = _h(sc)
+    assert abs(sc[3] - info["loss"]) < 1e-4, (sc, info)
+    assert abs(sc[0] - info["actor-loss"]) < 1e-4
+    np.testing.assert_allclose(_h(dh), rdh, rtol=2e-4, atol=1e-8)
+    np.testing.assert_allclose(_h(dv), rdv, rtol=1e-4, atol=1e-9)
+    if dist == "gaussian":
+        np.testing.assert_allclose(_h(dls), rdls, rtol=2e-4, atol=1e-5)
+    if algo == "ppo":
+        assert abs(sc[4] - info["clip_ratio"]) < 2.0 / B
+
+
+def test_loss_kernel_out_of_range_idx_is_inert():
+    from xuanpolicy_amd import ops
+    B, A = 64, 3
+    head = torch.randn(B, A, device=DEV)
+    idx = torch.arange(B, device=DEV)
+    idx[5] = 10_000
+    idx[9] = -3
+    sc, dh, dls, dv = ops.policy_loss("a2c", "gaussian", head, torch.zeros(A, device=DEV), torch.zeros(B, device=DEV),
+                                      torch.zeros(B * A, device=DEV), torch.ones(B, device=DEV),
+                                      torch.zeros(B, device=DEV), idx=idx)
+    assert float(dh[5].abs().sum()) == 0.0 and float(dh[9].abs().sum()) == 0.0
+    assert torch.isfinite(sc).all()
+
+
+# ---------------------------------------------------------------------------------------------- K5
+def test_rms_kernel_golden(golden):
+    from xuanpolicy_amd import ops
+    g = golden("rms.npz")
+    mean = torch.zeros(5, device=DEV)
+    var = torch.ones(5, device=DEV)
+    cnt = torch.full((1,), 1e-4, dtype=torch.float64, device=DEV)
+    for k in range(g["obs/x"].shape[0]):
+        ops.rms_update(_d(g["obs/x"][k]), mean, var, cnt)
+        np.testing.assert_allclose(_h(mean), g["obs/mean"][k], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(_h(var), g["obs/var"][k], rtol=1e-5, atol=1e-6)
+        assert abs(float(cnt) - g["obs/count"][k]) < 1e-6
+
+
+@pytest.mark.parametrize("N,D", [(4096, 17), (1000, 376), (3, 2)])
+def test_rms_and_normalize_strided(N, D):
+    from xuanpolicy_amd import ops
+    rng = np.random.default_rng(N + D)
+    X = _d(rng.normal(1.0, 3.0, (N, D + 5)).astype(np.float32))
+    x = X[:, :D]
+    ref = cpu_ref.RunningMeanStdRef((D,))
+    mean = torch.zeros(D, device=DEV)
+    var = torch.ones(D, device=DEV)
+    cnt = torch.full((1,), 1e-4, dtype=torch.float64, device=DEV)
+    for _ in range(3):
+        ops.rms_update(x, mean, var, cnt)
+        ref.update(_h(x))
+    np.testing.assert_allclose(_h(mean), ref.mean, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(_h(var), ref.var, rtol=1e-4, atol=1e-5)
+    out = torch.empty(N, D, device=DEV)
+    T = 4
+    col = torch.zeros(N, T, D, device=DEV)
+    cur = torch.tensor([2, 0, 0, 0], dtype=torch.int32, device=DEV)
+    ops.obs_normalize(x, mean, var, 5.0, out, col_out=col, col_ld=T * D, cursor=cur)
+    exp = np.clip((_h(x) - _h(mean)) / (np.sqrt(_h(var)) + 1e-8), -5, 5)
+    np.testing.assert_allclose(_h(out), exp, rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(_h(col[:, 2]), _h(out))
+    assert float(col[:, [0, 1, 3]].abs().sum()) == 0.0
+
+
+# ---------------------------------------------------------------------------------------------- K7
+@pytest.mark.parametrize("D,A,discrete", [(17, 6, False), (376, 17, False), (4, 2, True)])
+def test_synthbox_step_matches_oracle(D, A, discrete):
+    from xuanpolicy_amd.envs import SynthBoxVecEnv
+    N = 512
+    env = SynthBoxVecEnv(N, D, A, seed=11, discrete=discrete, max_episode_steps=7, device=DEV)
+    ref = synth_env.SynthBoxVec(N, D, A, seed=11, discrete=discrete, max_episode_steps=7)
+    np.testing.assert_array_equal(_h(env.obs), ref.state)
+    rng = np.random.default_rng(0)
+    for step in range(12):
+        acts = rng.integers(0, A, N) if discrete else rng.normal(0, 1, (N, A)).astype(np.float32)
+        ref.state = _h(env.obs).copy()  # re-sync: compare one step at a time (tanh dynamics amplify ulps)
+        fin, r, te, tr, nxt = ref.step(acts)
+        g_fin, g_r, g_te, g_tr, _ = env.step(acts)
+        np.testing.assert_allclose(g_fin, fin, rtol=1e-5, atol=2e-6)
+        np.testing.assert_allclose(g_r, r, rtol=1e-5, atol=1e-6)
+        near = np.abs(fin[:, 0] - synth_env.TERM_THRESH) < 1e-5
+        np.testing.assert_array_equal(g_te[~near], te[~near])
+        np.testing.assert_array_equal(g_tr, tr)
+        done = te | tr
+        np.testing.assert_array_equal(_h(env.obs)[done & ~near], nxt[done & ~near])  # reset states are exact
+    assert int(env.ep_index.sum()) > 0
+
+
+# ---------------------------------------------------------------------------------------------- K3
+def test_rollout_sample_gaussian_and_categorical():
+    from xuanpolicy_amd import ops
+    N, T, A = 20000, 4, 3
+    cur = torch.tensor([1, 77, 0, 0], dtype=torch.int32, device=DEV)
+    mu = torch.randn(N, A, device=DEV) * 0.3
+    logstd = torch.tensor([-1.0, -0.5, 0.2], device=DEV)
+    v = torch.randn(N, device=DEV)
+    act = torch.zeros(N, T, A, device=DEV)
+    logp = torch.zeros(N, T, device=DEV)
+    val = torch.zeros(N, T, device=DEV)
+    env_in = torch.zeros(N, A + 2, device=DEV)
+    ops.rollout_sample("gaussian", mu, logstd, v, cur, 5, act, logp, val, env_in[:, :A], act_clip=1.0)
+    a1 = act[:, 1]
+    eps = (a1 - mu) / torch.exp(logstd)
+    assert abs(float(eps.mean())) < 0.02 and abs(float(eps.std()) - 1.0) < 0.02
+    ref_lp = torch.distributions.Normal(mu, torch.exp(logstd)).log_prob(a1).sum(-1)
+    np.testing.assert_allclose(_h(logp[:, 1]), _h(ref_lp), rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(_h(val[:, 1]), _h(v))
+    np.testing.assert_array_equal(_h(env_in[:, :A]), np.clip(_h(a1), -1, 1))
+    assert float(act[:, [0, 2, 3]].abs().sum()) == 0.0
+    # same cursor.step -> same draws; different step -> different draws
+    act2 = torch.zeros_like(act)
+    ops.rollout_sample("gaussian", mu, logstd, v, cur, 5, act2, logp, val, env_in[:, :A])
+    assert torch.equal(act2[:, 1], a1)
+    K = 5
+    logits = torch.randn(N, K, device=DEV)
+    cact = torch.zeros(N, T, device=DEV)
+    onehot = torch.zeros(N, K, device=DEV)
+    ops.rollout_sample("categorical", logits, None, v, cur, 9, cact, logp, val, onehot)
+    k = cact[:, 1].long()
+    np.testing.assert_allclose(_h(logp[:, 1]), _h(torch.log_softmax(logits, -1).gather(1, k[:, None])[:, 0]),
+                               rtol=1e-5, atol=1e-5)
+    assert torch.equal(onehot.argmax(1), k) and torch.equal(onehot.sum(1), torch.ones(N, device=DEV))
+    freq = torch.bincount(k, minlength=K).float() / N
+    np.testing.assert_allclose(_h(freq), _h(torch.softmax(logits, -1).mean(0)), atol=0.015)
+
+
+# ---------------------------------------------------------------------------------------------- K8
+@pytest.mark.parametrize("algo,atari", [("ppo", False), ("a2c", False), ("ppo", True)])
+def test_rollout_post_matches_reference_rules(algo, atari):
+    from xuanpolicy_amd import ops
+    rng = np.random.default_rng(3)
+    N, T = 300, 5
+    returns = rng.normal(0, 1, N).astype(np.float32)
+    ret_rms = cpu_ref.RunningMeanStdRef(())
+    ret_rms.mean, ret_rms.var, ret_rms.count = np.float32(0.3), np.float32(2.0), 17.0
+    rm = torch.tensor([0.3], device=DEV)
+    rv = torch.tensor([2.0], device=DEV)
+    rc = torch.tensor([17.0], dtype=torch.float64, device=DEV)
+    rt = _d(returns)
+    bufs = {k: torch.zeros(N, T, device=DEV) for k in ("rew", "term", "boot")}
+    closed = torch.zeros(N, T, dtype=torch.uint8, device=DEV)
+    cur = torch.tensor([0, 0, 0, 0], dtype=torch.int32, device=DEV)
+    for t in range(T):
+        rew = rng.normal(0, 2, N).astype(np.float32)
+        term = rng.random(N) < 0.2
+        trunc = rng.random(N) < 0.1
+        vb = rng.normal(0, 1, N).astype(np.float32)
+        # reference rules (agent.py:118-123, ppoclip_agent.py:69-101 / a2c_agent.py:84)
+        exp_rew = np.clip(rew / np.clip(np.sqrt(ret_rms.var), 0.1, 100), -5, 5)
+        if algo == "ppo":
+            returns = (1 - term) * 0.99 * returns + rew
+        else:
+            returns = 0.99 * returns + rew
+        done = term | trunc
+        for i in np.nonzero(done)[0]:
+            ret_rms.update(returns[i:i + 1])
+        returns = np.where(done, 0, returns).astype(np.float32)
+        last = t == T - 1
+        close = np.full(N, True) if last else (done & ~(atari & ~trunc))
+        exp_boot = np.where(close, np.where(term, 0, vb), 0)
+        ops.rollout_post(_d(rew), _d(term.astype(np.uint8)), _d(trunc.astype(np.uint8)), _d(vb), cur, rm, rv, rc, rt,
+                         bufs["rew"], bufs["term"], closed, bufs["boot"], 0.99, mask_returns=(algo == "ppo"),
+                         use_rewnorm=True, rew_range=5.0, atari_lifeloss=atari)
+        np.testing.assert_allclose(_h(bufs["rew"][:, t]), exp_rew, rtol=1e-5, atol=1e-6)
+        np.testing.assert_array_equal(_h(bufs["term"][:, t]), term.astype(np.float32))
+        np.testing.assert_array_equal(_h(closed[:, t]).astype(bool), close)
+        np.testing.assert_allclose(_h(bufs["boot"][:, t]), exp_boot, rtol=0, atol=0)
+        np.testing.assert_allclose(_h(rt), returns, rtol=1e-5, atol=1e-5)
+        assert abs(float(rm) - float(ret_rms.mean)) < 1e-5 * max(1, abs(float(ret_rms.mean)))
+        assert abs(float(rv) - float(ret_rms.var)) < 1e-4 * max(1, abs(float(ret_rms.var)))
+        assert abs(float(rc) - ret_rms.count) < 1e-9
+    assert _h(cur)[0] == 0 and _h(cur)[1] == T

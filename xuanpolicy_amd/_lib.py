@@ -1,0 +1,100 @@
+"""ctypes binding of the C ABI in include/xuanpolicy_amd.h (libxuanpolicy_amd.so, gfx950).
+
+The library is built in-tree by `build_library()` (hipcc, --offload-arch=gfx950) and loaded after
+`import torch`, so its NEEDED libamdhip64.so.7 resolves to the HIP runtime torch already mapped
+(same SONAME) and torch's device pointers and hipStream_t handles are valid in it.
+
+There is no CPU fallback: every entry point raises if the library is missing or a call fails.
+"""
+import ctypes
+import os
+import subprocess
+
+import torch  # noqa: F401  (must be loaded first: see module docstring)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "libxuanpolicy_amd.so")
+CSRC = os.path.join(PKG_DIR, "csrc")
+SOURCES = ["gae.hip", "loss.hip", "rollout.hip"]
+HEADER = os.path.join(REPO_DIR, "include", "xuanpolicy_amd.h")
+
+ABI_VERSION = 1
+
+c_i32, c_i64, c_u32, c_f32, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
+
+# name -> (restype, argtypes); mirrors include/xuanpolicy_amd.h one-for-one.
+SIGNATURES = {
+    "xpa_abi_version": (ctypes.c_int, []),
+    "xpa_gae_scan": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, ctypes.c_int, c_p, c_p, c_p]),
+    "xpa_gather_num_partials": (c_i64, [c_i64]),
+    "xpa_gather_minibatch": (ctypes.c_int, [c_p, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p]),
+    "xpa_loss_num_partials": (c_i64, [c_i64]),
+    "xpa_loss_partial_width": (c_i64, [c_i64]),
+    "xpa_policy_loss_fwd_bwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p,
+                                               c_p, c_p, c_p, c_p, c_i64, c_f32, c_f32, c_f32, c_p, c_p, c_p, c_p]),
+    "xpa_policy_loss_finalize": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_f32, c_f32,
+                                                c_p, c_p, c_p]),
+    "xpa_rms_num_partials": (c_i64, [c_i64]),
+    "xpa_rms_partials": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_p, c_p]),
+    "xpa_rms_merge": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p]),
+    "xpa_obs_normalize": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_f32, c_p, c_i64, c_p, c_i64, c_p, c_p]),
+    "xpa_rollout_sample": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_u32, c_f32, c_p, c_p,
+                                          c_p, c_p, c_i64, c_p]),
+    "xpa_synthbox_step": (ctypes.c_int, [c_i64, c_i64, c_p, c_u32, c_i32, c_f32, c_f32, c_f32, c_p, c_i64, c_p, c_p,
+                                         c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "xpa_rollout_post": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                                        c_f32, ctypes.c_int, ctypes.c_int, c_f32, ctypes.c_int, c_p]),
+}
+
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall"]
+
+_lib = None
+
+
+class XpaError(RuntimeError):
+    pass
+
+
+def build_library(force=False, verbose=False):
+    """Compile csrc/*.hip into libxuanpolicy_amd.so for gfx950 (cross-compiles without a GPU)."""
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    deps = srcs + [os.path.join(CSRC, "xpa_common.h"), HEADER]
+    if not force and os.path.exists(LIB_PATH):
+        lib_m = os.path.getmtime(LIB_PATH)
+        if all(os.path.getmtime(d) <= lib_m for d in deps):
+            return LIB_PATH
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    tmp = LIB_PATH + ".tmp"
+    cmd = [hipcc] + HIPCC_FLAGS + ["-o", tmp] + srcs
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+def load(path=None):
+    """Load the library (once) and bind every exported symbol's signature."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise XpaError("libxuanpolicy_amd.so not built (%s); run __graft_entry__.build() or "
+                       "xuanpolicy_amd._lib.build_library()" % path)
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    v = lib.xpa_abi_version()
+    if v != ABI_VERSION:
+        raise XpaError("ABI version mismatch: library %d, bindings %d" % (v, ABI_VERSION))
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        raise XpaError("%s failed: hipError %d%s" % (what, rc, " (invalid argument)" if rc == 1 else ""))

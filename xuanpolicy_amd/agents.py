@@ -1,0 +1,281 @@
+"""PPO-Clip and A2C agents: the reference's on-policy training loop, device-resident on one GPU.
+
+Mirrors (reference paths):
+  Agent base            xuance/torch/agents/agent.py:7-141 (obs/reward normalisation, logging, save/load)
+  PPOCLIP_Agent.train   xuance/torch/agents/policy_gradient/ppoclip_agent.py:59-111
+  A2C_Agent.train       xuance/torch/agents/policy_gradient/a2c_agent.py:57-107
+  REGISTRY              xuance/torch/agents/__init__.py:68-111 ("PPO_Clip", "A2C")
+Same constructor (config, envs, policy, optimizer, scheduler, device) and config keys
+(n_steps, n_epoch, n_minibatch, gamma, gae_lambda, use_gae, use_advnorm, use_obsnorm, use_rewnorm,
+obsnorm_range, rewnorm_range, vf_coef, ent_coef, clip_range, clip_grad_norm / clip_grad, ...).
+
+One env step of the hot loop (device env, no host sync):
+   K5  RunningMeanStd.update(obs) + normalise -> policy input and buffer column
+   --  policy heads forward (PyTorch-ROCm GEMMs, no autograd)
+   K3  sample action, log-prob, store act/logp/value
+   K7  env step (GEMM + xpa_synthbox_step, auto-reset)
+   K5c normalise the final obs with the same statistics -> critic forward (truncation bootstrap)
+   K8  reward norm, return tracker, ret_rms, terminals, path closures; cursor += 1
+When the buffer is full: K1 GAE over [n_envs, n_steps]; then n_epoch x n_minibatch updates of
+K4 gather -> heads forward -> K2 loss fwd+bwd -> autograd backward -> [all-reduce] -> clip -> Adam.
+Host-side envs (numpy VecEnvs) are supported through the same kernels with per-step H2D/D2H copies.
+
+Semantic notes: action sampling uses the counter-hash RNG on device, not torch's
+CPU generator; the truncation bootstrap value V(norm(final obs)) is computed for every env each step
+(the reference recomputes a full batch once per truncated env, ppoclip_agent.py:99-100); ret_rms merges
+all finished envs of a step in one Chan update (mathematically equal to the reference's sequential
+single-value updates).
+"""
+import time
+
+import numpy as np
+import torch
+
+from . import ops
+from .buffer import DummyOnPolicyBuffer, DummyOnPolicyBuffer_Atari
+from .learners import A2C_Learner, PPOCLIP_Learner
+from .policies import policy_heads, space_shape
+
+FLOAT_MAX = 3.0e38
+
+
+def _cfg(config, name, default):
+    return getattr(config, name, default)
+
+
+class _OnPolicyAgent:
+    algo = "ppo"
+
+    def __init__(self, config, envs, policy, optimizer, scheduler=None, device=None):
+        self.config = config
+        self.envs = envs
+        self.policy = policy
+        self.render = _cfg(config, "render", False)
+        self.n_envs = envs.num_envs
+        self.n_steps = config.n_steps
+        self.n_minibatch = config.n_minibatch
+        self.n_epoch = config.n_epoch
+        self.gamma = config.gamma
+        self.gae_lam = config.gae_lambda
+        self.atari = _cfg(config, "env_name", "") == "Atari"
+        self.observation_space = envs.observation_space
+        self.action_space = envs.action_space
+        self.device = next(policy.parameters()).device
+        self.discrete = bool(getattr(policy, "discrete", not hasattr(policy.actor, "logstd")))
+        self.dist = "categorical" if self.discrete else "gaussian"
+        self.auxiliary_info_shape = {"old_logp": ()} if self.algo == "ppo" else {}
+        Buffer = DummyOnPolicyBuffer_Atari if self.atari else DummyOnPolicyBuffer
+        self.buffer_size = self.n_envs * self.n_steps
+        self.batch_size = self.buffer_size // self.n_minibatch
+        self.memory = Buffer(self.observation_space, self.action_space, self.auxiliary_info_shape, self.n_envs,
+                             self.n_steps, _cfg(config, "use_gae", True), _cfg(config, "use_advnorm", True),
+                             self.gamma, self.gae_lam, device=self.device)
+        self.learner = self._make_learner(config, policy, optimizer, scheduler)
+        self.use_obsnorm = bool(_cfg(config, "use_obsnorm", False))
+        self.use_rewnorm = bool(_cfg(config, "use_rewnorm", False))
+        self.obsnorm_range = float(_cfg(config, "obsnorm_range", 5))
+        self.rewnorm_range = float(_cfg(config, "rewnorm_range", 5))
+        dev, N, T = self.device, self.n_envs, self.n_steps
+        self.obs_shape = space_shape(self.observation_space)
+        D = int(np.prod(self.obs_shape)) if len(self.obs_shape) else 1
+        self.obs_dim = D
+        f32 = dict(dtype=torch.float32, device=dev)
+        # RunningMeanStd state (statistic_tools.py:35-60): mean 0, var 1, count 1e-4
+        self.obs_mean = torch.zeros((D,), **f32)
+        self.obs_var = torch.ones((D,), **f32)
+        self.obs_count = torch.full((1,), 1e-4, dtype=torch.float64, device=dev)
+        self.ret_mean = torch.zeros((1,), **f32)
+        self.ret_var = torch.ones((1,), **f32)
+        self.ret_count = torch.full((1,), 1e-4, dtype=torch.float64, device=dev)
+        self.returns = torch.zeros((N,), **f32)
+        self.cursor = ops.new_cursor(dev)
+        self.obs_norm = torch.empty((N, D), **f32)
+        self.boot_obs = torch.empty((N, D), **f32)
+        self.rms_part = torch.empty((2 * ops.rms_num_partials(N), D), dtype=torch.float64, device=dev)
+        self.logp_scratch = None if self.algo == "ppo" else torch.zeros((N, T), **f32)
+        self.obs_mb = None
+        self.adv_part = None
+        self.seed = int(_cfg(config, "seed", 1))
+        self.gen = torch.Generator(device=dev)
+        self.gen.manual_seed(self.seed)
+        self.device_env = hasattr(envs, "step_device")
+        self.current_step = 0
+        self.current_episode = np.zeros((N,), np.int32)
+        self.iterations = 0
+        self.last_info = None
+        self.infos = []          # host copies, one dict per buffer-full phase
+        self.log_hook = None     # optional callable(info: dict, step: int) (tensorboard/wandb adapter)
+        self.timers = {"rollout": 0.0, "update": 0.0}
+        self._t = 0
+        self._host_obs = None
+
+    def _make_learner(self, config, policy, optimizer, scheduler):
+        raise NotImplementedError
+
+    # ---- normalisation (agent.py:104-123) -----------------------------------------------------------
+    def _obs_clip(self):
+        return self.obsnorm_range if self.use_obsnorm else FLOAT_MAX
+
+    def _normalize_into(self, x, out, to_buffer):
+        mem = self.memory
+        if to_buffer:
+            T, D = self.n_steps, self.obs_dim
+            ops.obs_normalize(x, self.obs_mean, self.obs_var, self._obs_clip(), out, col_out=mem.observations,
+                              col_ld=T * D, cursor=self.cursor)
+        else:
+            ops.obs_normalize(x, self.obs_mean, self.obs_var, self._obs_clip(), out)
+
+    # ---- one env step ---------------------------------------------------------------------------------
+    def _sample_into_buffer(self):
+        mem = self.memory
+        with torch.no_grad():
+            head, logstd, v = policy_heads(self.policy, self.obs_norm)
+        logp_buf = mem.auxiliary_infos["old_logp"] if self.algo == "ppo" else self.logp_scratch
+        env_in = self.envs.act_in if self.device_env else self._act_scratch()
+        ops.rollout_sample(self.dist, head.contiguous(), logstd, v.contiguous(), self.cursor, self.seed,
+                           mem.actions, logp_buf, mem.values, env_in, act_clip=1.0)
+
+    def _act_scratch(self):
+        if getattr(self, "_env_in", None) is None:
+            A = self.action_space.n if self.discrete else int(np.prod(self.action_space.shape))
+            self._env_in = torch.zeros((self.n_envs, A), dtype=torch.float32, device=self.device)
+        return self._env_in
+
+    def _post(self, rew, term, trunc, final_obs):
+        mem = self.memory
+        self._normalize_into(final_obs, self.boot_obs, False)
+        with torch.no_grad():
+            v_boot = policy_heads(self.policy, self.boot_obs)[2]
+        ops.rollout_post(rew, term, trunc, v_boot.contiguous(), self.cursor, self.ret_mean, self.ret_var,
+                         self.ret_count, self.returns, mem.rewards, mem.terminals, mem.closed, mem.boot, self.gamma,
+                         mask_returns=(self.algo == "ppo"), use_rewnorm=self.use_rewnorm,
+                         rew_range=self.rewnorm_range, atari_lifeloss=self.atari)
+
+    def _rollout_step_device(self):
+        env = self.envs
+        x = env.obs
+        if self.use_obsnorm:
+            ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count, partials=self.rms_part)
+        self._normalize_into(x, self.obs_norm, True)
+        self._sample_into_buffer()
+        env.step_device()
+        self._post(env.rew, env.term, env.trunc, env.final_obs)
+
+    def _rollout_step_host(self):
+        """Same kernels around a host VecEnv (numpy in/out, reset_obs in infos)."""
+        env, dev = self.envs, self.device
+        if self._host_obs is None:
+            self._host_obs = np.asarray(env.buf_obs, np.float32).reshape(self.n_envs, -1)
+        x = torch.as_tensor(self._host_obs, device=dev)
+        if self.use_obsnorm:
+            ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count, partials=self.rms_part)
+        self._normalize_into(x, self.obs_norm, True)
+        self._sample_into_buffer()
+        t = self._t
+        acts = (self.memory.actions[:, t]).cpu().numpy()
+        if self.discrete:
+            acts = acts.astype(np.int64)
+        next_obs, rews, terms, truncs, infos = env.step(acts)
+        next_obs = np.asarray(next_obs, np.float32).reshape(self.n_envs, -1)
+        self._post(torch.as_tensor(np.asarray(rews, np.float32), device=dev),
+                   torch.as_tensor(np.asarray(terms, np.uint8), device=dev),
+                   torch.as_tensor(np.asarray(truncs, np.uint8), device=dev), torch.as_tensor(next_obs, device=dev))
+        obs = next_obs.copy()
+        for i in range(self.n_envs):
+            if terms[i] or truncs[i]:
+                if self.atari and not truncs[i]:
+                    continue
+                obs[i] = np.asarray(infos[i]["reset_obs"], np.float32).reshape(-1)
+                self.current_episode[i] += 1
+        self._host_obs = obs
+
+    # ---- buffer-full phase ------------------------------------------------------------------------------
+    def _update_phase(self):
+        mem = self.memory
+        mem.size = self.n_steps
+        mem.compute_advantages()
+        NT, B = self.buffer_size, self.batch_size
+        obs_flat = mem.observations.reshape((NT,) + tuple(mem.observations.shape[2:]))
+        act_flat = mem.actions.reshape(-1)
+        adv_flat = mem.advantages.reshape(-1)
+        ret_flat = mem.returns.reshape(-1)
+        logp_flat = mem.auxiliary_infos["old_logp"].reshape(-1) if self.algo == "ppo" else None
+        use_advnorm = mem.use_advnorm
+        scalars = None
+        for _ in range(self.n_epoch):
+            perm = torch.randperm(NT, device=self.device, generator=self.gen)
+            for start in range(0, NT, B):
+                idx = perm[start:start + B]
+                b = idx.shape[0]
+                if self.obs_mb is None or self.obs_mb.shape[0] != b:
+                    self.obs_mb = torch.empty((b,) + tuple(obs_flat.shape[1:]), dtype=obs_flat.dtype,
+                                              device=self.device)
+                    self.adv_part = torch.empty((ops.gather_num_partials(b), 2), dtype=torch.float64,
+                                                device=self.device)
+                obs_mb, part = ops.gather_minibatch(idx, obs_flat, adv=adv_flat if use_advnorm else None,
+                                                    obs_out=self.obs_mb,
+                                                    adv_partials=self.adv_part if use_advnorm else None)
+                scalars = self.learner.update_fused(obs_mb, idx, act_flat, adv_flat, ret_flat, logp_flat, part)
+        self.last_info = scalars
+        self.iterations += 1
+
+    def log_infos(self, info, x_index):
+        if self.log_hook is not None:
+            self.log_hook(info, x_index)
+
+    def _host_info(self):
+        info = self.learner._info(self.last_info)
+        info["iteration"] = self.iterations
+        info["step"] = self.current_step
+        return info
+
+    # ---- public API (ppoclip_agent.py:59-111) -------------------------------------------------------------
+    def train(self, train_steps, log=True):
+        step_fn = self._rollout_step_device if self.device_env else self._rollout_step_host
+        for _ in range(train_steps):
+            t0 = time.perf_counter()
+            step_fn()
+            self._t += 1
+            self.memory.ptr = self._t % self.n_steps
+            self.memory.size = min(self.memory.size + 1, self.n_steps)
+            self.current_step += self.n_envs
+            t1 = time.perf_counter()
+            self.timers["rollout"] += t1 - t0
+            if self._t == self.n_steps:
+                self._update_phase()
+                self._t = 0
+                self.memory.ptr, self.memory.size = 0, 0
+                if log:
+                    info = self._host_info()
+                    self.infos.append(info)
+                    self.log_infos(info, self.current_step)
+                self.timers["update"] += time.perf_counter() - t1
+
+    def save_model(self, model_path):
+        self.learner.save_model(model_path)
+
+    def load_model(self, path, seed=1):
+        self.learner.load_model(path, seed)
+
+    def finish(self):
+        pass
+
+
+class PPOCLIP_Agent(_OnPolicyAgent):
+    algo = "ppo"
+
+    def _make_learner(self, config, policy, optimizer, scheduler):
+        return PPOCLIP_Learner(policy, optimizer, scheduler, _cfg(config, "device", None), _cfg(config, "model_dir", "./"),
+                               vf_coef=config.vf_coef, ent_coef=config.ent_coef, clip_range=config.clip_range,
+                               clip_grad_norm=config.clip_grad_norm, use_grad_clip=_cfg(config, "use_grad_clip", True))
+
+
+class A2C_Agent(_OnPolicyAgent):
+    algo = "a2c"
+
+    def _make_learner(self, config, policy, optimizer, scheduler):
+        return A2C_Learner(policy, optimizer, scheduler, _cfg(config, "device", None), _cfg(config, "model_dir", "./"),
+                           config.vf_coef, config.ent_coef, config.clip_grad)
+
+
+REGISTRY = {"PPO_Clip": PPOCLIP_Agent, "A2C": A2C_Agent}

@@ -1,0 +1,266 @@
+// K2 — fused PPO-Clip / A2C policy + value + entropy loss, forward and backward, one minibatch (gfx950).
+//
+// Replaces (reference paths):
+//   PPOCLIP_Learner.update loss     xuance/torch/learners/policy_gradient/ppoclip_learner.py:32-44
+//   A2C_Learner.update loss         xuance/torch/learners/policy_gradient/a2c_learner.py:24-31
+//   DiagGaussian/Categorical        xuance/torch/utils/distributions.py:39-101 (torch Normal / Categorical)
+//   per-minibatch adv-norm          xuance/common/memory_tools.py:241-242
+// One thread per sample: reads the policy head row (mu or logits), its value, and — through the
+// minibatch permutation idx — act/old_logp/adv/ret straight from the [n_envs, horizon] buffer (no
+// gathered copies), writes d loss/d head and d loss/d v, and one row of block partial sums
+// (surrogate, squared error, entropy, clip count, value, d loss/d logstd[A]).  The partials are
+// reduced in a fixed order by xpa_policy_loss_finalize (no float atomics -> bit-reproducible).
+// Closed-form gradients follow torch autograd's tie rules: clamp passes the
+// gradient on [1-eps, 1+eps] inclusive; minimum() splits an exact tie half/half.
+// HBM-bound elementwise work: Gaussian 4(3A+5) B/sample, Categorical 4(2K+6) B/sample.
+#include "xpa_common.h"
+
+namespace {
+
+constexpr int kLossThreads = 256;
+constexpr int kLossWaves = kLossThreads / 64;
+constexpr int kPartBase = 5;  // surrogate, sq-err, entropy, clip count, value
+constexpr int kMaxAct = 64;
+constexpr float kLogSqrt2Pi = 0.91893853320467274178f;  // log(sqrt(2*pi))
+constexpr float kHalfLog2PiPlusHalf = 1.41893853320467274178f;  // 0.5 + 0.5*log(2*pi)
+
+__device__ __forceinline__ void adv_moments(const double *partials, int64_t n_partials, int64_t batch,
+                                            float *s_mean, float *s_inv) {
+    // Wave 0 reduces the gather kernel's (sum, sumsq) rows in a fixed order.
+    if (threadIdx.x < 64) {
+        double s = 0.0, q = 0.0;
+        for (int64_t k = threadIdx.x; k < n_partials; k += 64) {
+            s += partials[2 * k];
+            q += partials[2 * k + 1];
+        }
+        s = xpa_wave_sum(s);
+        q = xpa_wave_sum(q);
+        if (threadIdx.x == 0) {
+            const double mean = s / (double)batch;
+            const double var = fmax(q / (double)batch - mean * mean, 0.0);
+            *s_mean = (float)mean;
+            *s_inv = (float)(1.0 / ((double)(float)sqrt(var) + 1e-8));
+        }
+    }
+}
+
+template <int DIST, int ALGO>
+__global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
+    int64_t batch, int A, const float *__restrict__ head, const float *__restrict__ logstd,
+    const float *__restrict__ v, const int64_t *__restrict__ idx, int64_t n_rows, const float *__restrict__ act,
+    const float *__restrict__ old_logp, const float *__restrict__ adv, const float *__restrict__ ret,
+    const double *__restrict__ adv_partials, int64_t n_adv_partials, float clip_range, float vf_coef,
+    float ent_coef, float *__restrict__ d_head, float *__restrict__ d_v, float *__restrict__ partials, int width) {
+    __shared__ float s_scale[kMaxAct], s_logscale[kMaxAct], s_var[kMaxAct];
+    __shared__ float s_ent;
+    __shared__ float s_mean, s_inv;
+    __shared__ float s_red[kLossWaves];
+
+    const int tid = threadIdx.x;
+    if (DIST == XPA_DIST_GAUSSIAN) {
+        for (int a = tid; a < A; a += kLossThreads) {
+            const float sc = expf(logstd[a]);   // std = logstd.exp() (gaussian.py:29)
+            s_scale[a] = sc;
+            s_logscale[a] = logf(sc);           // Normal.log_prob uses scale.log()
+            s_var[a] = sc * sc;
+        }
+    }
+    if (adv_partials) {
+        adv_moments(adv_partials, n_adv_partials, batch, &s_mean, &s_inv);
+    } else if (tid == 0) {
+        s_mean = 0.f;
+        s_inv = 1.f;
+    }
+    __syncthreads();
+    if (DIST == XPA_DIST_GAUSSIAN && tid == 0) {
+        float e = 0.f;
+        for (int a = 0; a < A; ++a) e += kHalfLog2PiPlusHalf + s_logscale[a];
+        s_ent = e;
+    }
+    __syncthreads();
+
+    const int64_t b = (int64_t)blockIdx.x * kLossThreads + tid;
+    int64_t row = b < batch ? (idx ? idx[b] : b) : 0;
+    const bool valid = b < batch && row >= 0 && row < n_rows;
+    if (!valid) row = 0;
+    if (b < batch && !valid) {  // out-of-range index: zero gradient, no contribution
+        d_v[b] = 0.f;
+        for (int a = 0; a < A; ++a) d_head[b * A + a] = 0.f;
+    }
+    const float inv_b = 1.0f / (float)batch;
+
+    float surr = 0.f, sq = 0.f, ent = 0.f, clipc = 0.f, vv = 0.f;
+    float dlogp = 0.f;
+    float lse = 0.f, H = 0.f;  // categorical
+    int ai = 0;
+    if (valid) {
+        const float A_n = (adv[row] - s_mean) * s_inv;
+        const float vb = v[b];
+        const float diffv = vb - ret[row];
+        sq = diffv * diffv;
+        vv = vb;
+        d_v[b] = vf_coef * 2.0f * diffv * inv_b;
+        float logp = 0.f;
+        if (DIST == XPA_DIST_GAUSSIAN) {
+            const float *mu = head + b * A;
+            const float *x = act + row * A;
+            for (int a = 0; a < A; ++a) {
+                const float diff = x[a] - mu[a];
+                logp += -(diff * diff) / (2.0f * s_var[a]) - s_logscale[a] - kLogSqrt2Pi;
+            }
+            ent = s_ent;
+        } else {
+            const float *z = head + b * A;
+            float m = z[0];
+            for (int k = 1; k < A; ++k) m = fmaxf(m, z[k]);
+            float se = 0.f;
+            for (int k = 0; k < A; ++k) se += expf(z[k] - m);
+            lse = m + logf(se);
+            ai = (int)act[row];
+            ai = ai < 0 ? 0 : (ai >= A ? A - 1 : ai);
+            logp = z[ai] - lse;
+            for (int k = 0; k < A; ++k) {
+                const float ln = z[k] - lse;
+                H -= expf(ln) * ln;
+            }
+            ent = H;
+        }
+        if (ALGO == XPA_ALGO_PPO) {
+            const float ratio = expf(logp - old_logp[row]);
+            const float lo = 1.0f - clip_range, hi = 1.0f + clip_range;
+            const float cr = fminf(fmaxf(ratio, lo), hi);
+            const float s1 = cr * A_n;
+            const float s2 = A_n * ratio;
+            surr = fminf(s1, s2);
+            const bool inr = (ratio >= lo) && (ratio <= hi);
+            const float g1 = inr ? A_n : 0.f;
+            const float w1 = (s1 < s2) ? 1.f : ((s1 == s2) ? 0.5f : 0.f);
+            const float w2 = (s2 < s1) ? 1.f : ((s1 == s2) ? 0.5f : 0.f);
+            dlogp = -inv_b * (w1 * g1 + w2 * A_n) * ratio;
+            clipc = ((ratio < lo) || (ratio > hi)) ? 1.f : 0.f;
+        } else {
+            surr = A_n * logp;
+            dlogp = -A_n * inv_b;
+        }
+        if (DIST == XPA_DIST_GAUSSIAN) {
+            const float *mu = head + b * A;
+            const float *x = act + row * A;
+            float *dm = d_head + b * A;
+            for (int a = 0; a < A; ++a) dm[a] = dlogp * (x[a] - mu[a]) / s_var[a];
+        } else {
+            const float *z = head + b * A;
+            float *dz = d_head + b * A;
+            const float ec = ent_coef * inv_b;
+            for (int k = 0; k < A; ++k) {
+                const float ln = z[k] - lse;
+                const float p = expf(ln);
+                const float oh = (k == ai) ? 1.f : 0.f;
+                dz[k] = dlogp * (oh - p) + ec * p * (ln + H);
+            }
+        }
+    }
+    float *prow = partials + (int64_t)blockIdx.x * width;
+    float t0 = xpa_block_sum(surr, s_red, kLossWaves);
+    float t1 = xpa_block_sum(sq, s_red, kLossWaves);
+    float t2 = xpa_block_sum(ent, s_red, kLossWaves);
+    float t3 = xpa_block_sum(clipc, s_red, kLossWaves);
+    float t4 = xpa_block_sum(vv, s_red, kLossWaves);
+    if (tid == 0) {
+        prow[0] = t0; prow[1] = t1; prow[2] = t2; prow[3] = t3; prow[4] = t4;
+    }
+    if (DIST == XPA_DIST_GAUSSIAN) {
+        const float *mu = head + b * A;
+        const float *x = act + row * A;
+        for (int a = 0; a < A; ++a) {
+            float g = 0.f;
+            if (valid) {
+                const float diff = x[a] - mu[a];
+                g = dlogp * (diff * diff / s_var[a] - 1.0f);
+            }
+            const float tg = xpa_block_sum(g, s_red, kLossWaves);
+            if (tid == 0) prow[kPartBase + a] = tg;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void policy_loss_finalize_kernel(int algo, int dist, int64_t batch, int A,
+                                                                   const float *__restrict__ partials,
+                                                                   int64_t n_partials, int width, float vf_coef,
+                                                                   float ent_coef, float *__restrict__ scalars,
+                                                                   float *__restrict__ d_logstd) {
+    __shared__ double s_red[4];
+    const int ncols = kPartBase + (dist == XPA_DIST_GAUSSIAN ? A : 0);
+    double tot[kPartBase];
+    for (int j = 0; j < ncols; ++j) {
+        double s = 0.0;
+        for (int64_t k = threadIdx.x; k < n_partials; k += 256) s += (double)partials[k * width + j];
+        s = xpa_block_sum(s, s_red, 4);
+        if (j < kPartBase) tot[j] = s;
+        else if (threadIdx.x == 0) d_logstd[j - kPartBase] = (float)(s - (double)ent_coef);
+    }
+    if (threadIdx.x == 0) {
+        const double B = (double)batch;
+        const double actor = -tot[0] / B;
+        const double critic = tot[1] / B;
+        const double entropy = tot[2] / B;
+        scalars[XPA_OUT_ACTOR_LOSS] = (float)actor;
+        scalars[XPA_OUT_CRITIC_LOSS] = (float)critic;
+        scalars[XPA_OUT_ENTROPY] = (float)entropy;
+        scalars[XPA_OUT_LOSS] = (float)(actor - (double)ent_coef * entropy + (double)vf_coef * critic);
+        scalars[XPA_OUT_CLIP_RATIO] = algo == XPA_ALGO_PPO ? (float)(tot[3] / B) : 0.f;
+        scalars[XPA_OUT_VALUE_MEAN] = (float)(tot[4] / B);
+    }
+}
+
+}  // namespace
+
+XPA_API int64_t xpa_loss_num_partials(int64_t batch) { return (batch + kLossThreads - 1) / kLossThreads; }
+
+XPA_API int64_t xpa_loss_partial_width(int64_t act_dim) { return kPartBase + act_dim; }
+
+XPA_API int xpa_policy_loss_fwd_bwd(int algo, int dist, int64_t batch, int64_t act_dim, const float *head,
+                                    const float *logstd, const float *v, const int64_t *idx, int64_t n_rows,
+                                    const float *act,
+                                    const float *old_logp, const float *adv, const float *ret,
+                                    const double *adv_partials, int64_t n_adv_partials, float clip_range,
+                                    float vf_coef, float ent_coef, float *d_head, float *d_v, float *partials,
+                                    xpa_stream_t stream) {
+    if (batch <= 0 || act_dim <= 0 || act_dim > kMaxAct) return (int)hipErrorInvalidValue;
+    if (algo != XPA_ALGO_PPO && algo != XPA_ALGO_A2C) return (int)hipErrorInvalidValue;
+    if (dist != XPA_DIST_GAUSSIAN && dist != XPA_DIST_CATEGORICAL) return (int)hipErrorInvalidValue;
+    if (dist == XPA_DIST_CATEGORICAL && act_dim < 2) return (int)hipErrorInvalidValue;
+    if (!head || !v || !act || !adv || !ret || !d_head || !d_v || !partials) return (int)hipErrorInvalidValue;
+    if (n_rows <= 0 || (!idx && n_rows < batch)) return (int)hipErrorInvalidValue;
+    if (dist == XPA_DIST_GAUSSIAN && !logstd) return (int)hipErrorInvalidValue;
+    if (algo == XPA_ALGO_PPO && !old_logp) return (int)hipErrorInvalidValue;
+    const int64_t blocks = xpa_loss_num_partials(batch);
+    if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+    const int width = (int)xpa_loss_partial_width(act_dim);
+    const int A = (int)act_dim;
+    hipStream_t s = (hipStream_t)stream;
+#define XPA_LOSS_LAUNCH(D_, A_)                                                                                    \
+    hipLaunchKernelGGL((policy_loss_kernel<D_, A_>), dim3((unsigned)blocks), dim3(kLossThreads), 0, s, batch, A,  \
+                       head, logstd, v, idx, n_rows, act, old_logp, adv, ret, adv_partials, n_adv_partials, clip_range,   \
+                       vf_coef, ent_coef, d_head, d_v, partials, width)
+    if (dist == XPA_DIST_GAUSSIAN) {
+        if (algo == XPA_ALGO_PPO) XPA_LOSS_LAUNCH(XPA_DIST_GAUSSIAN, XPA_ALGO_PPO);
+        else XPA_LOSS_LAUNCH(XPA_DIST_GAUSSIAN, XPA_ALGO_A2C);
+    } else {
+        if (algo == XPA_ALGO_PPO) XPA_LOSS_LAUNCH(XPA_DIST_CATEGORICAL, XPA_ALGO_PPO);
+        else XPA_LOSS_LAUNCH(XPA_DIST_CATEGORICAL, XPA_ALGO_A2C);
+    }
+#undef XPA_LOSS_LAUNCH
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_policy_loss_finalize(int algo, int dist, int64_t batch, int64_t act_dim, const float *partials,
+                                     int64_t n_partials, float vf_coef, float ent_coef, float *scalars,
+                                     float *d_logstd, xpa_stream_t stream) {
+    if (batch <= 0 || act_dim <= 0 || act_dim > kMaxAct || n_partials <= 0 || !partials || !scalars)
+        return (int)hipErrorInvalidValue;
+    if (dist == XPA_DIST_GAUSSIAN && !d_logstd) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(policy_loss_finalize_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, algo, dist, batch,
+                       (int)act_dim, partials, n_partials, (int)xpa_loss_partial_width(act_dim), vf_coef, ent_coef,
+                       scalars, d_logstd);
+    return xpa_launch_status();
+}

@@ -1,0 +1,421 @@
+// Rollout-side kernels of the fused on-policy pipeline (gfx950):
+//   K4 xpa_gather_minibatch  minibatch row gather + advantage moments (memory_tools.py:231-242)
+//   K5 xpa_rms_*             RunningMeanStd + obs normalisation (statistic_tools.py:63-112, agent.py:104-116)
+//   K3 xpa_rollout_sample    action sample + log-prob + buffer store (ppoclip_agent.py:50-57, memory_tools.py:196-204)
+//   K7 xpa_synthbox_step     synthetic env step with auto-reset (gym_vec_env.py:201-212 contract)
+//   K8 xpa_rollout_post      reward norm, return tracker, ret_rms, path closures (ppoclip_agent.py:68-101)
+// All per-step kernels read the buffer column from a device cursor so a whole env step can be
+// captured once in a hipGraph and replayed.
+#include "xpa_common.h"
+
+namespace {
+
+constexpr int kGatherRows = 256;  // rows per gather block == rows per adv partial
+constexpr int kRmsRows = 64;      // rows per RMS partial block
+constexpr uint32_t kSaltAct = 0xAC7105EDu;
+constexpr uint32_t kSaltReset = 0x5EED0000u;  // oracle/synth_env.py SALT_RESET
+
+// ---------------------------------------------------------------------------------------------
+// K4 gather
+// ---------------------------------------------------------------------------------------------
+template <typename V>
+__global__ __launch_bounds__(256) void gather_rows_kernel(const int64_t *__restrict__ idx, int64_t batch,
+                                                          int64_t n_rows, const V *__restrict__ src, int64_t row_vecs,
+                                                          V *__restrict__ dst, const float *__restrict__ adv,
+                                                          double *__restrict__ adv_partials) {
+    __shared__ double s_red[4];
+    const int64_t r0 = (int64_t)blockIdx.x * kGatherRows;
+    const int64_t r1 = r0 + kGatherRows < batch ? r0 + kGatherRows : batch;
+    const int64_t n = (r1 - r0) * row_vecs;
+    for (int64_t e = threadIdx.x; e < n; e += 256) {
+        const int64_t r = r0 + e / row_vecs;
+        const int64_t c = e % row_vecs;
+        const int64_t sr = idx[r];
+        dst[r * row_vecs + c] = (sr >= 0 && sr < n_rows) ? src[sr * row_vecs + c] : V{};
+    }
+    if (adv_partials) {
+        double s = 0.0, q = 0.0;
+        const int64_t r = r0 + threadIdx.x;
+        const int64_t sr = r < r1 ? idx[r] : -1;
+        if (sr >= 0 && sr < n_rows) {
+            const double a = (double)adv[sr];
+            s = a;
+            q = a * a;
+        }
+        s = xpa_block_sum(s, s_red, 4);
+        q = xpa_block_sum(q, s_red, 4);
+        if (threadIdx.x == 0) {
+            adv_partials[2 * blockIdx.x] = s;
+            adv_partials[2 * blockIdx.x + 1] = q;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K5 RunningMeanStd
+// ---------------------------------------------------------------------------------------------
+// One thread per column, kRmsRows rows per block: Welford in f64 -> (mean, M2) per (block, column).
+__global__ __launch_bounds__(256) void rms_partials_kernel(const float *__restrict__ x, int64_t n, int64_t dim,
+                                                           int64_t ld, double *__restrict__ part) {
+    const int64_t r0 = (int64_t)blockIdx.x * kRmsRows;
+    const int64_t r1 = r0 + kRmsRows < n ? r0 + kRmsRows : n;
+    const int64_t np = gridDim.x;
+    for (int64_t d = (int64_t)blockIdx.y * blockDim.x + threadIdx.x; d < dim; d += (int64_t)gridDim.y * blockDim.x) {
+        double mean = 0.0, m2 = 0.0;
+        int k = 0;
+        for (int64_t r = r0; r < r1; ++r) {
+            const double xv = (double)x[r * ld + d];
+            ++k;
+            const double delta = xv - mean;
+            mean += delta / k;
+            m2 += delta * (xv - mean);
+        }
+        part[(int64_t)blockIdx.x * dim + d] = mean;
+        part[(np + blockIdx.x) * dim + d] = m2;
+    }
+}
+
+// Chan merge of the partials (fixed order) then update_from_moments (statistic_tools.py:86-112).
+__global__ __launch_bounds__(256) void rms_merge_kernel(const double *__restrict__ part, int64_t np, int64_t n,
+                                                        int64_t dim, float *__restrict__ mean, float *__restrict__ var,
+                                                        double *__restrict__ count) {
+    const double c0 = *count;
+    __syncthreads();
+    for (int64_t d = threadIdx.x; d < dim; d += blockDim.x) {
+        double bm = 0.0, bm2 = 0.0, bn = 0.0;
+        for (int64_t p = 0; p < np; ++p) {
+            const double nb = (double)((p + 1) * kRmsRows < n ? kRmsRows : n - p * kRmsRows);
+            const double pm = part[p * dim + d];
+            const double pm2 = part[(np + p) * dim + d];
+            const double tot = bn + nb;
+            const double delta = pm - bm;
+            bm += delta * nb / tot;
+            bm2 += pm2 + delta * delta * bn * nb / tot;
+            bn = tot;
+        }
+        const double bvar = bm2 / (double)n;  // np.std(x, axis=0)**2 (ddof 0)
+        const double m0 = (double)mean[d], v0 = (double)var[d];
+        const double tot = c0 + (double)n;
+        const double delta = bm - m0;
+        const double new_mean = m0 + delta * (double)n / tot;
+        const double m2 = v0 * c0 + bvar * (double)n + delta * delta * c0 * (double)n / tot;
+        mean[d] = (float)new_mean;
+        var[d] = (float)(m2 / tot);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *count = c0 + (double)n;
+}
+
+__global__ __launch_bounds__(256) void obs_normalize_kernel(const float *__restrict__ x, int64_t n, int64_t dim,
+                                                            int64_t ldx, const float *__restrict__ mean,
+                                                            const float *__restrict__ var, float clip_range,
+                                                            float *__restrict__ out, int64_t ldo,
+                                                            float *__restrict__ col_out, int64_t col_ld,
+                                                            const xpa_cursor_t *__restrict__ cursor) {
+    const int64_t total = n * dim;
+    const int64_t coff = (col_out && cursor) ? (int64_t)cursor->ptr * dim : 0;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = e / dim, d = e % dim;
+        const float sd = sqrtf(var[d]);
+        float y = (x[r * ldx + d] - mean[d]) / (sd + 1e-8f);
+        y = fminf(fmaxf(y, -clip_range), clip_range);
+        out[r * ldo + d] = y;
+        if (col_out) col_out[r * col_ld + coff + d] = y;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K3 sample + log-prob + store
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rollout_sample_gauss_kernel(
+    int64_t n_envs, int A, int64_t T, const float *__restrict__ mu, const float *__restrict__ logstd,
+    const float *__restrict__ v, const xpa_cursor_t *__restrict__ cur, uint32_t seed, float act_clip,
+    float *__restrict__ buf_act, float *__restrict__ buf_logp, float *__restrict__ buf_val, float *__restrict__ env_in,
+    int64_t ld_env) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_envs) return;
+    const int64_t t = cur->ptr;
+    const uint32_t step = cur->step;
+    const int64_t cell = n * T + t;
+    float logp = 0.f;
+    for (int a = 0; a < A; ++a) {
+        const uint32_t h1 = xpa_hash4(seed ^ kSaltAct, step, (uint32_t)n, (uint32_t)(2 * a));
+        const uint32_t h2 = xpa_hash4(seed ^ kSaltAct, step, (uint32_t)n, (uint32_t)(2 * a + 1));
+        const float u1 = 1.0f - xpa_u01(h1);  // (0, 1]
+        const float u2 = xpa_u01(h2);
+        const float eps = sqrtf(-2.0f * logf(u1)) * cosf(6.28318530717958647692f * u2);
+        const float sc = expf(logstd[a]);
+        const float m = mu[n * A + a];
+        const float x = m + sc * eps;
+        const float diff = x - m;
+        logp += -(diff * diff) / (2.0f * sc * sc) - logf(sc) - 0.91893853320467274178f;
+        buf_act[cell * A + a] = x;
+        env_in[n * ld_env + a] = fminf(fmaxf(x, -act_clip), act_clip);
+    }
+    buf_logp[cell] = logp;
+    buf_val[cell] = v[n];
+}
+
+__global__ __launch_bounds__(256) void rollout_sample_cat_kernel(
+    int64_t n_envs, int K, int64_t T, const float *__restrict__ logits, const float *__restrict__ v,
+    const xpa_cursor_t *__restrict__ cur, uint32_t seed, float *__restrict__ buf_act, float *__restrict__ buf_logp,
+    float *__restrict__ buf_val, float *__restrict__ env_in, int64_t ld_env) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_envs) return;
+    const int64_t t = cur->ptr;
+    const uint32_t step = cur->step;
+    const int64_t cell = n * T + t;
+    const float *z = logits + n * K;
+    float m = z[0];
+    for (int k = 1; k < K; ++k) m = fmaxf(m, z[k]);
+    float se = 0.f;
+    for (int k = 0; k < K; ++k) se += expf(z[k] - m);
+    const float lse = m + logf(se);
+    const float u = xpa_u01(xpa_hash4(seed ^ kSaltAct, step, (uint32_t)n, 0u));
+    int pick = K - 1;
+    float cdf = 0.f;
+    for (int k = 0; k < K; ++k) {
+        cdf += expf(z[k] - lse);
+        if (u < cdf) {
+            pick = k;
+            break;
+        }
+    }
+    buf_act[cell] = (float)pick;
+    buf_logp[cell] = z[pick] - lse;
+    buf_val[cell] = v[n];
+    for (int k = 0; k < K; ++k) env_in[n * ld_env + k] = (k == pick) ? 1.f : 0.f;
+}
+
+// ---------------------------------------------------------------------------------------------
+// K7 SynthBox env step (one wave per env, lanes over the state dims)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void synthbox_step_kernel(
+    int64_t n_envs, int D, const float *__restrict__ pre, uint32_t seed, int max_steps, float noise, float thresh,
+    float reset_scale, float *__restrict__ state, int64_t ld_state, float *__restrict__ final_obs,
+    float *__restrict__ rew, uint8_t *__restrict__ term, uint8_t *__restrict__ trunc, int32_t *__restrict__ ep_step,
+    uint32_t *__restrict__ ep_index, float *__restrict__ ep_score, float *__restrict__ ep_last_score,
+    int32_t *__restrict__ ep_last_len) {
+    const int64_t n = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (n >= n_envs) return;  // wave-uniform
+    const int t = ep_step[n];
+    const uint32_t ep = ep_index[n];
+    float sumsq = 0.f, s0 = 0.f;
+    for (int d = lane; d < D; d += 64) {
+        const uint32_t base = ((uint32_t)t * (uint32_t)D + (uint32_t)d) * 4u;
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc += xpa_u01(xpa_hash4(seed, (uint32_t)n, ep, base + (uint32_t)j));
+        const float xi = (acc - 2.0f) * 1.7320508075688772f;
+        const float s = tanhf(pre[n * D + d] + noise * xi);
+        final_obs[n * D + d] = s;
+        sumsq += s * s;
+        if (d == 0) s0 = s;
+    }
+    sumsq = xpa_wave_sum(sumsq);
+    s0 = __shfl(s0, 0, 64);
+    const float r = -sumsq / (float)D;
+    const bool te = s0 > thresh;
+    const int t1 = t + 1;
+    const bool tr = t1 >= max_steps;
+    const bool done = te || tr;
+    const float score = ep_score[n] + r;
+    for (int d = lane; d < D; d += 64) {
+        float sn;
+        if (done) {
+            const uint32_t h = xpa_hash4(seed ^ kSaltReset, (uint32_t)n, ep + 1u, (uint32_t)d);
+            sn = (2.0f * xpa_u01(h) - 1.0f) * reset_scale;
+        } else {
+            sn = final_obs[n * D + d];
+        }
+        state[n * ld_state + d] = sn;
+    }
+    if (lane == 0) {
+        rew[n] = r;
+        term[n] = te ? 1 : 0;
+        trunc[n] = tr ? 1 : 0;
+        if (done) {
+            ep_last_score[n] = score;
+            ep_last_len[n] = t1;
+            ep_index[n] = ep + 1u;
+            ep_step[n] = 0;
+            ep_score[n] = 0.f;
+        } else {
+            ep_step[n] = t1;
+            ep_score[n] = score;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K8 post-step bookkeeping (single block)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void rollout_post_kernel(
+    int64_t n_envs, int64_t T, const float *__restrict__ rew, const uint8_t *__restrict__ term,
+    const uint8_t *__restrict__ trunc, const float *__restrict__ v_boot, xpa_cursor_t *__restrict__ cur,
+    float *__restrict__ ret_mean, float *__restrict__ ret_var, double *__restrict__ ret_count,
+    float *__restrict__ returns, float *__restrict__ buf_rew, float *__restrict__ buf_term,
+    uint8_t *__restrict__ buf_closed, float *__restrict__ buf_boot, float gamma, int mask_returns, int use_rewnorm,
+    float rew_range, int atari_lifeloss) {
+    __shared__ double s_red[16];
+    const int32_t t = cur->ptr;
+    const float rstd = fminf(fmaxf(sqrtf(*ret_var), 0.1f), 100.0f);
+    const bool last = (t == (int32_t)(T - 1));
+    double cnt = 0.0, sum = 0.0, sumsq = 0.0;
+    for (int64_t n = threadIdx.x; n < n_envs; n += blockDim.x) {
+        const float r = rew[n];
+        const bool te = term[n] != 0, tr = trunc[n] != 0;
+        const int64_t cell = n * T + t;
+        buf_rew[cell] = use_rewnorm ? fminf(fmaxf(r / rstd, -rew_range), rew_range) : r;
+        buf_term[cell] = te ? 1.f : 0.f;
+        const bool done = te || tr;
+        const bool close = last || (done && !(atari_lifeloss && !tr));
+        buf_closed[cell] = close ? 1 : 0;
+        buf_boot[cell] = close ? (te ? 0.f : v_boot[n]) : 0.f;
+        float R = returns[n];
+        R = mask_returns ? (te ? 0.f : gamma * R) + r : gamma * R + r;
+        if (done) {
+            cnt += 1.0;
+            sum += (double)R;
+            sumsq += (double)R * (double)R;
+            R = 0.f;
+        }
+        returns[n] = R;
+    }
+    const int nw = blockDim.x >> 6;
+    cnt = xpa_block_sum(cnt, s_red, nw);
+    sum = xpa_block_sum(sum, s_red, nw);
+    sumsq = xpa_block_sum(sumsq, s_red, nw);
+    if (threadIdx.x == 0) {
+        if (cnt > 0.0) {
+            const double bm = sum / cnt;
+            const double bvar = fmax(sumsq / cnt - bm * bm, 0.0);
+            const double c0 = *ret_count, m0 = (double)*ret_mean, v0 = (double)*ret_var;
+            const double tot = c0 + cnt;
+            const double delta = bm - m0;
+            *ret_mean = (float)(m0 + delta * cnt / tot);
+            *ret_var = (float)((v0 * c0 + bvar * cnt + delta * delta * c0 * cnt / tot) / tot);
+            *ret_count = tot;
+        }
+        cur->ptr = (int32_t)((t + 1) % T);
+        cur->step = cur->step + 1u;
+    }
+}
+
+}  // namespace
+
+// ---- K4 --------------------------------------------------------------------------------------------
+XPA_API int64_t xpa_gather_num_partials(int64_t batch) { return (batch + kGatherRows - 1) / kGatherRows; }
+
+XPA_API int xpa_gather_minibatch(const int64_t *idx, int64_t batch, int64_t n_rows, const void *obs,
+                                 int64_t obs_row_bytes, void *obs_out, const float *adv, double *adv_partials,
+                                 xpa_stream_t stream) {
+    if (batch <= 0 || n_rows <= 0 || obs_row_bytes < 0 || !idx) return (int)hipErrorInvalidValue;
+    if (obs_row_bytes > 0 && (!obs || !obs_out)) return (int)hipErrorInvalidValue;
+    if (adv_partials && !adv) return (int)hipErrorInvalidValue;
+    const int64_t blocks = xpa_gather_num_partials(batch);
+    hipStream_t s = (hipStream_t)stream;
+    const uintptr_t al = (uintptr_t)obs | (uintptr_t)obs_out;
+    if (obs_row_bytes % 16 == 0 && al % 16 == 0)
+        hipLaunchKernelGGL(gather_rows_kernel<uint4>, dim3((unsigned)blocks), dim3(256), 0, s, idx, batch,
+                           n_rows, (const uint4 *)obs, obs_row_bytes / 16, (uint4 *)obs_out, adv, adv_partials);
+    else if (obs_row_bytes % 4 == 0 && al % 4 == 0)
+        hipLaunchKernelGGL(gather_rows_kernel<uint32_t>, dim3((unsigned)blocks), dim3(256), 0, s, idx, batch,
+                           n_rows, (const uint32_t *)obs, obs_row_bytes / 4, (uint32_t *)obs_out, adv, adv_partials);
+    else
+        hipLaunchKernelGGL(gather_rows_kernel<uint8_t>, dim3((unsigned)blocks), dim3(256), 0, s, idx, batch,
+                           n_rows, (const uint8_t *)obs, obs_row_bytes, (uint8_t *)obs_out, adv, adv_partials);
+    return xpa_launch_status();
+}
+
+// ---- K5 --------------------------------------------------------------------------------------------
+XPA_API int64_t xpa_rms_num_partials(int64_t n) { return (n + kRmsRows - 1) / kRmsRows; }
+
+XPA_API int xpa_rms_partials(const float *x, int64_t n, int64_t dim, int64_t ld, double *partials,
+                             xpa_stream_t stream) {
+    if (n <= 0 || dim <= 0 || ld < dim || !x || !partials) return (int)hipErrorInvalidValue;
+    const int64_t np = xpa_rms_num_partials(n);
+    const int threads = dim >= 256 ? 256 : (int)((dim + 63) / 64 * 64);
+    const int64_t ycols = (dim + threads - 1) / threads;
+    hipLaunchKernelGGL(rms_partials_kernel, dim3((unsigned)np, (unsigned)(ycols < 65535 ? ycols : 65535)),
+                       dim3(threads), 0, (hipStream_t)stream, x, n, dim, ld, partials);
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_rms_merge(const double *partials, int64_t n_partials, int64_t n, int64_t dim, float *mean,
+                          float *var, double *count, xpa_stream_t stream) {
+    if (n <= 0 || dim <= 0 || n_partials != xpa_rms_num_partials(n) || !partials || !mean || !var || !count)
+        return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(rms_merge_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, partials, n_partials, n, dim,
+                       mean, var, count);
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_obs_normalize(const float *x, int64_t n, int64_t dim, int64_t ldx, const float *mean,
+                              const float *var, float clip_range, float *out, int64_t ldo, float *col_out,
+                              int64_t col_ld, const xpa_cursor_t *cursor, xpa_stream_t stream) {
+    if (n <= 0 || dim <= 0 || ldx < dim || ldo < dim || !x || !mean || !var || !out) return (int)hipErrorInvalidValue;
+    if (col_out && (!cursor || col_ld < dim)) return (int)hipErrorInvalidValue;
+    const int64_t total = n * dim;
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(obs_normalize_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, n, dim, ldx,
+                       mean, var, clip_range, out, ldo, col_out, col_ld, cursor);
+    return xpa_launch_status();
+}
+
+// ---- K3 --------------------------------------------------------------------------------------------
+XPA_API int xpa_rollout_sample(int dist, int64_t n_envs, int64_t act_dim, int64_t horizon, const float *head,
+                               const float *logstd, const float *v, const xpa_cursor_t *cursor, uint32_t seed,
+                               float act_clip, float *buf_act, float *buf_logp, float *buf_val, float *env_in,
+                               int64_t ld_env, xpa_stream_t stream) {
+    if (n_envs <= 0 || act_dim <= 0 || horizon <= 0 || !head || !v || !cursor || !buf_act || !buf_logp ||
+        !buf_val || !env_in || ld_env < act_dim)
+        return (int)hipErrorInvalidValue;
+    const unsigned blocks = (unsigned)((n_envs + 255) / 256);
+    hipStream_t s = (hipStream_t)stream;
+    if (dist == XPA_DIST_GAUSSIAN) {
+        if (!logstd) return (int)hipErrorInvalidValue;
+        hipLaunchKernelGGL(rollout_sample_gauss_kernel, dim3(blocks), dim3(256), 0, s, n_envs, (int)act_dim, horizon,
+                           head, logstd, v, cursor, seed, act_clip, buf_act, buf_logp, buf_val, env_in, ld_env);
+    } else if (dist == XPA_DIST_CATEGORICAL) {
+        if (act_dim < 2) return (int)hipErrorInvalidValue;
+        hipLaunchKernelGGL(rollout_sample_cat_kernel, dim3(blocks), dim3(256), 0, s, n_envs, (int)act_dim, horizon,
+                           head, v, cursor, seed, buf_act, buf_logp, buf_val, env_in, ld_env);
+    } else {
+        return (int)hipErrorInvalidValue;
+    }
+    return xpa_launch_status();
+}
+
+// ---- K7 --------------------------------------------------------------------------------------------
+XPA_API int xpa_synthbox_step(int64_t n_envs, int64_t obs_dim, const float *pre, uint32_t seed,
+                              int32_t max_episode_steps, float noise, float term_thresh, float reset_scale,
+                              float *state, int64_t ld_state, float *final_obs, float *rew, uint8_t *term,
+                              uint8_t *trunc, int32_t *ep_step, uint32_t *ep_index, float *ep_score,
+                              float *ep_last_score, int32_t *ep_last_len, xpa_stream_t stream) {
+    if (n_envs <= 0 || obs_dim <= 0 || ld_state < obs_dim || !pre || !state || !final_obs || !rew || !term ||
+        !trunc || !ep_step || !ep_index || !ep_score || !ep_last_score || !ep_last_len)
+        return (int)hipErrorInvalidValue;
+    const unsigned blocks = (unsigned)((n_envs + 3) / 4);
+    hipLaunchKernelGGL(synthbox_step_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, n_envs, (int)obs_dim, pre,
+                       seed, max_episode_steps, noise, term_thresh, reset_scale, state, ld_state, final_obs, rew, term,
+                       trunc, ep_step, ep_index, ep_score, ep_last_score, ep_last_len);
+    return xpa_launch_status();
+}
+
+// ---- K8 --------------------------------------------------------------------------------------------
+XPA_API int xpa_rollout_post(int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term,
+                             const uint8_t *trunc, const float *v_boot, xpa_cursor_t *cursor, float *ret_mean,
+                             float *ret_var, double *ret_count, float *returns, float *buf_rew, float *buf_term,
+                             uint8_t *buf_closed, float *buf_boot, float gamma, int mask_returns, int use_rewnorm,
+                             float rew_range, int atari_lifeloss, xpa_stream_t stream) {
+    if (n_envs <= 0 || horizon <= 0 || !rew || !term || !trunc || !v_boot || !cursor || !ret_mean || !ret_var ||
+        !ret_count || !returns || !buf_rew || !buf_term || !buf_closed || !buf_boot)
+        return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(rollout_post_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, n_envs, horizon, rew, term,
+                       trunc, v_boot, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term, buf_closed,
+                       buf_boot, gamma, mask_returns, use_rewnorm, rew_range, atari_lifeloss);
+    return xpa_launch_status();
+}

@@ -1,0 +1,168 @@
+"""Device-resident synthetic vector environments for the on-policy benchmark (BASELINE.json configs).
+
+SynthBoxVecEnv(n_envs, D, A) is the SynthBox(D, A) env of SURVEY.md §8(d), plugged in where the
+reference builds envs (xuance/environment/__init__.py:76-78 NewEnv hook; DummyVecEnv_Gym contract of
+xuance/environment/gym/gym_vec_env.py:148-231).  The state lives in HBM and a step is one GEMM
+(X @ Wcat^T, hipBLASLt) plus the xpa_synthbox_step kernel, with auto-reset on done.
+
+Dynamics (spec shared with the CPU checker oracle/synth_env.py; all randomness from a counter hash):
+    x = W s + U clip(a, -1, 1) + NOISE * xi      (Discrete: U[:, a] via a one-hot row)
+    s' = tanh(x), r = -mean(s'^2), terminated = s'[0] > TERM_THRESH, truncated at max_episode_steps
+    reset s0 = RESET_SCALE * (2u - 1)
+The host-facing step(actions) -> (obs, rew, term, trunc, infos) exists for the VecEnv contract and
+tests; the agent's hot loop uses step_device() and never leaves the GPU.
+"""
+import numpy as np
+import torch
+
+from . import _lib, ops
+
+W_GAIN, U_GAIN, NOISE, TERM_THRESH, RESET_SCALE = 1.25, 0.6, 0.35, 0.92, 0.1
+SALT_W, SALT_U, SALT_RESET = 0x57A7E000, 0x0AC7E000, 0x5EED0000
+
+
+def _mix32(x):
+    x = np.asarray(x, dtype=np.uint32).copy()
+    with np.errstate(over="ignore"):
+        x ^= x >> np.uint32(16)
+        x *= np.uint32(0x85EBCA6B)
+        x ^= x >> np.uint32(13)
+        x *= np.uint32(0xC2B2AE35)
+        x ^= x >> np.uint32(16)
+    return x
+
+
+def _hash4(seed, k0, k1, k2):
+    h = _mix32(_mix32(np.uint32(seed & 0xFFFFFFFF)) ^ np.asarray(k0, np.uint32))
+    h = _mix32(h ^ np.asarray(k1, np.uint32))
+    return _mix32(h ^ np.asarray(k2, np.uint32))
+
+
+def _u01(h):
+    return (np.asarray(h, np.uint32) >> np.uint32(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+
+
+def synthbox_matrices(seed, D, A, discrete=False):
+    i = np.arange(D, dtype=np.uint32)[:, None]
+    W = (2.0 * _u01(_hash4(seed, SALT_W, i, np.arange(D, dtype=np.uint32)[None, :])) - 1.0) * np.sqrt(3.0 / D) * W_GAIN
+    gain, fan = (1.0, 1) if discrete else (U_GAIN, A)
+    U = (2.0 * _u01(_hash4(seed, SALT_U, i, np.arange(A, dtype=np.uint32)[None, :])) - 1.0) * np.sqrt(3.0 / fan) * gain
+    return W.astype(np.float32), U.astype(np.float32)
+
+
+def synthbox_reset_states(seed, env_ids, episodes, D):
+    e = np.asarray(env_ids, np.uint32)[:, None]
+    ep = np.asarray(episodes, np.uint32)[:, None]
+    d = np.arange(D, dtype=np.uint32)[None, :]
+    return ((2.0 * _u01(_hash4(seed ^ SALT_RESET, e, ep, d)) - 1.0) * RESET_SCALE).astype(np.float32)
+
+
+class _Box:
+    def __init__(self, shape):
+        self.shape = tuple(shape)
+        self.low = -np.ones(shape, np.float32)
+        self.high = np.ones(shape, np.float32)
+        self.dtype = np.float32
+
+
+class _Discrete:
+    def __init__(self, n):
+        self.n, self.shape, self.dtype = int(n), (), np.int64
+
+
+class SynthBoxVecEnv:
+    """n_envs SynthBox(D, A) environments resident on one GPU."""
+
+    def __init__(self, n_envs, obs_dim, act_dim, seed=1, discrete=False, max_episode_steps=1000, device=None,
+                 shard=0):
+        self.num_envs, self.D, self.A = int(n_envs), int(obs_dim), int(act_dim)
+        self.seed, self.discrete, self.max_episode_steps = int(seed), bool(discrete), int(max_episode_steps)
+        self.max_episode_length = self.max_episode_steps
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        # Data-parallel shards share the dynamics (W, U from `seed`) but draw noise/reset states from a
+        # per-shard stream; shard 0 is bit-identical to the CPU checker.
+        self.shard = int(shard)
+        self.noise_seed = (self.seed ^ ((0x9E3779B9 * self.shard) & 0xFFFFFFFF)) & 0xFFFFFFFF
+        self.observation_space = _Box((self.D,))
+        self.action_space = _Discrete(self.A) if discrete else _Box((self.A,))
+        W, U = synthbox_matrices(self.seed, self.D, self.A, self.discrete)
+        dev, N, D, A = self.device, self.num_envs, self.D, self.A
+        self.Wcat_t = torch.as_tensor(np.concatenate([W, U], axis=1).T.copy(), device=dev)  # [D + A, D]
+        self.X = torch.zeros((N, D + A), dtype=torch.float32, device=dev)                   # [state | action]
+        self.pre = torch.empty((N, D), dtype=torch.float32, device=dev)
+        self.final_obs = torch.empty((N, D), dtype=torch.float32, device=dev)
+        self.rew = torch.zeros((N,), dtype=torch.float32, device=dev)
+        self.term = torch.zeros((N,), dtype=torch.uint8, device=dev)
+        self.trunc = torch.zeros((N,), dtype=torch.uint8, device=dev)
+        self.ep_step = torch.zeros((N,), dtype=torch.int32, device=dev)
+        self.ep_index = torch.zeros((N,), dtype=torch.int32, device=dev)  # read as uint32 by the kernel
+        self.ep_score = torch.zeros((N,), dtype=torch.float32, device=dev)
+        self.ep_last_score = torch.zeros((N,), dtype=torch.float32, device=dev)
+        self.ep_last_len = torch.zeros((N,), dtype=torch.int32, device=dev)
+        self.reset()
+
+    @property
+    def obs(self):
+        """Current observation [N, D] (a strided view of X)."""
+        return self.X[:, :self.D]
+
+    @property
+    def act_in(self):
+        """Env action input [N, A] (a strided view of X): clipped action or one-hot."""
+        return self.X[:, self.D:]
+
+    @property
+    def buf_obs(self):
+        return self.obs
+
+    def reset(self):
+        ids = np.arange(self.num_envs)
+        s0 = synthbox_reset_states(self.noise_seed, ids, np.zeros(self.num_envs), self.D)
+        self.X.zero_()
+        self.X[:, :self.D] = torch.as_tensor(s0, device=self.device)
+        for t in (self.ep_step, self.ep_index, self.ep_score, self.ep_last_score, self.ep_last_len, self.rew,
+                  self.term, self.trunc):
+            t.zero_()
+        return self.obs.clone(), [{} for _ in range(self.num_envs)]
+
+    def step_device(self):
+        """One env step for all envs from the action already written into act_in."""
+        torch.mm(self.X, self.Wcat_t, out=self.pre)
+        rc = ops.lib().xpa_synthbox_step(self.num_envs, self.D, ops._p(self.pre), self.noise_seed,
+                                         self.max_episode_steps, NOISE, TERM_THRESH, RESET_SCALE, ops._p(self.X),
+                                         self.X.stride(0), ops._p(self.final_obs), ops._p(self.rew),
+                                         ops._p(self.term), ops._p(self.trunc), ops._p(self.ep_step),
+                                         ops._p(self.ep_index), ops._p(self.ep_score), ops._p(self.ep_last_score),
+                                         ops._p(self.ep_last_len), ops._stream(self.device))
+        _lib.check(rc, "xpa_synthbox_step")
+
+    def step(self, actions):
+        """VecEnv contract (gym_vec_env.py:201-212): returns host copies of (obs, rew, term, trunc, infos)
+        with infos[i]['reset_obs'] for done envs."""
+        a = torch.as_tensor(np.asarray(actions) if not isinstance(actions, torch.Tensor) else actions,
+                            device=self.device)
+        if self.discrete:
+            self.act_in.zero_()
+            self.act_in.scatter_(1, a.long().reshape(-1, 1), 1.0)
+        else:
+            self.act_in.copy_(torch.clamp(a.float().reshape(self.num_envs, self.A), -1.0, 1.0))
+        self.step_device()
+        obs = self.final_obs.cpu().numpy()
+        rew = self.rew.cpu().numpy()
+        term = self.term.cpu().numpy().astype(bool)
+        trunc = self.trunc.cpu().numpy().astype(bool)
+        nxt = self.obs.cpu().numpy()
+        lens, scores = self.ep_step.cpu().numpy(), self.ep_score.cpu().numpy()
+        last_len, last_score = self.ep_last_len.cpu().numpy(), self.ep_last_score.cpu().numpy()
+        infos = []
+        for i in range(self.num_envs):
+            done = term[i] or trunc[i]
+            info = {"episode_step": int(last_len[i] if done else lens[i]),
+                    "episode_score": float(last_score[i] if done else scores[i])}
+            if done:
+                info["reset_obs"] = nxt[i].copy()
+            infos.append(info)
+        return obs, rew, term, trunc, infos
+
+    def close(self):
+        pass

@@ -1,0 +1,148 @@
+"""PPO-Clip and A2C learners whose loss forward+backward is one HIP kernel (K2).
+
+Mirrors (reference paths):
+  Learner               xuance/torch/learners/learner.py:10-52 (save_model / load_model / update)
+  PPOCLIP_Learner       xuance/torch/learners/policy_gradient/ppoclip_learner.py:4-65
+  A2C_Learner           xuance/torch/learners/policy_gradient/a2c_learner.py:4-50
+Same constructor arguments, same update() signature and the same info-dict keys.
+
+Per update: policy heads forward (PyTorch-ROCm GEMMs) -> xpa_policy_loss_fwd_bwd +
+xpa_policy_loss_finalize (loss scalars, d loss/d mu|logits, d loss/d logstd, d loss/d v) ->
+torch.autograd.backward of those head gradients through the MLP -> [one flat gradient all-reduce
+when data-parallel] -> clip_grad_norm_ -> optimizer.step -> scheduler.step, matching
+ppoclip_learner.py:45-51.  update() returns host floats like the reference (one sync);
+update_fused() keeps everything on device for the agent's hot loop.
+"""
+import os
+
+import torch
+
+from . import ops
+from .policies import policy_heads
+
+
+class Learner:
+    def __init__(self, policy, optimizer, scheduler=None, device=None, model_dir="./"):
+        self.policy = policy
+        self.optimizer = optimizer
+        self.scheduler = scheduler
+        self.device = device
+        self.model_dir = model_dir
+        self.iterations = 0
+        self.grad_sync = None  # set by xuanpolicy_amd.distributed for data-parallel training
+
+    def save_model(self, model_path):
+        torch.save(self.policy.state_dict(), model_path)
+
+    def load_model(self, path, seed=1):
+        """learner.py:27-48: newest file of the seed_<seed> directory."""
+        for f in os.listdir(path):
+            if "seed_%d" % seed in f:
+                path = os.path.join(path, f)
+                break
+        names = sorted(n for n in os.listdir(path) if n != "obs_rms.npy")
+        dev = self.device if self.device is not None else "cpu"
+        self.policy.load_state_dict(torch.load(os.path.join(path, names[-1]), map_location=dev, weights_only=True))
+
+    def update(self, *args):
+        raise NotImplementedError
+
+
+def _dist_of(policy):
+    return "categorical" if getattr(policy, "discrete", not hasattr(policy.actor, "logstd")) else "gaussian"
+
+
+class _FusedPolicyGradient(Learner):
+    algo = "ppo"
+
+    def __init__(self, policy, optimizer, scheduler, device, model_dir, vf_coef, ent_coef, clip_range, max_grad_norm,
+                 use_grad_clip):
+        super().__init__(policy, optimizer, scheduler, device, model_dir)
+        self.vf_coef, self.ent_coef, self.clip_range = vf_coef, ent_coef, clip_range
+        self._max_norm, self._use_clip = max_grad_norm, use_grad_clip
+        self.dist = _dist_of(policy)
+        self._ws = None
+        self._params = [p for p in policy.parameters()]
+
+    def _backward_and_step(self, head, logstd, v, d_head, d_logstd, d_v):
+        self.optimizer.zero_grad(set_to_none=True)
+        tensors, grads = [head, v], [d_head, d_v]
+        if logstd is not None:
+            tensors.append(logstd)
+            grads.append(d_logstd)
+        torch.autograd.backward(tensors, grads)
+        if self.grad_sync is not None:
+            self.grad_sync(self._params)
+        if self._use_clip:
+            torch.nn.utils.clip_grad_norm_(self._params, self._max_norm)
+        self.optimizer.step()
+        if self.scheduler is not None:
+            self.scheduler.step()
+
+    def update_fused(self, obs, idx, act, adv, ret, old_logp=None, adv_partials=None):
+        """One minibatch update reading act/adv/ret/old_logp from the flattened rollout buffer at idx
+        (idx=None: already gathered).  Returns the device tensor of loss scalars (ops.OUT_KEYS)."""
+        self.iterations += 1
+        head, logstd, v = policy_heads(self.policy, obs)
+        if self._ws is None or self._ws.batch != head.shape[0]:
+            self._ws = ops.LossWorkspace(head.shape[0], head.shape[1], head.device, self.dist)
+        scalars, dh, dls, dv = ops.policy_loss(self.algo, self.dist, head.contiguous(), logstd, v.contiguous(), act, adv,
+                                               ret, old_logp=old_logp, idx=idx, adv_partials=adv_partials,
+                                               clip_range=self.clip_range, vf_coef=self.vf_coef,
+                                               ent_coef=self.ent_coef, ws=self._ws)
+        self._backward_and_step(head, logstd, v, dh, dls, dv)
+        return scalars
+
+    def _info(self, scalars):
+        s = scalars.detach().cpu().tolist()
+        info = {"actor-loss": s[0], "critic-loss": s[1], "entropy": s[2],
+                "learning_rate": self.optimizer.param_groups[0]["lr"], "predict_value": s[5]}
+        if self.algo == "ppo":
+            info["clip_ratio"] = s[4]
+        return info
+
+    @staticmethod
+    def _t(x, device, dtype=torch.float32):
+        if isinstance(x, torch.Tensor):
+            return x.to(device=device, dtype=dtype).contiguous()
+        import numpy as np
+        return torch.as_tensor(np.asarray(x), dtype=dtype, device=device).contiguous()
+
+    def _device(self):
+        return next(self.policy.parameters()).device
+
+
+class PPOCLIP_Learner(_FusedPolicyGradient):
+    """ppoclip_learner.py:4-65."""
+    algo = "ppo"
+
+    def __init__(self, policy, optimizer, scheduler=None, device=None, model_dir="./", vf_coef=0.25, ent_coef=0.005,
+                 clip_range=0.25, clip_grad_norm=0.25, use_grad_clip=True):
+        super().__init__(policy, optimizer, scheduler, device, model_dir, vf_coef, ent_coef, clip_range,
+                         clip_grad_norm, use_grad_clip)
+        self.clip_grad_norm, self.use_grad_clip = clip_grad_norm, use_grad_clip
+
+    def update(self, obs_batch, act_batch, ret_batch, value_batch, adv_batch, old_logp):
+        dev = self._device()
+        scalars = self.update_fused(self._t(obs_batch, dev), None, self._t(act_batch, dev).reshape(-1),
+                                    self._t(adv_batch, dev), self._t(ret_batch, dev), self._t(old_logp, dev))
+        return self._info(scalars)
+
+
+class A2C_Learner(_FusedPolicyGradient):
+    """a2c_learner.py:4-50 (always clips the gradient norm, a2c_learner.py:34)."""
+    algo = "a2c"
+
+    def __init__(self, policy, optimizer, scheduler=None, device=None, model_dir="./", vf_coef=0.25, ent_coef=0.005,
+                 clip_grad=None):
+        super().__init__(policy, optimizer, scheduler, device, model_dir, vf_coef, ent_coef, 0.0, clip_grad, True)
+        self.clip_grad = clip_grad
+
+    def update(self, obs_batch, act_batch, ret_batch, adv_batch):
+        dev = self._device()
+        scalars = self.update_fused(self._t(obs_batch, dev), None, self._t(act_batch, dev).reshape(-1),
+                                    self._t(adv_batch, dev), self._t(ret_batch, dev))
+        return self._info(scalars)
+
+
+REGISTRY = {"PPO_Clip": PPOCLIP_Learner, "A2C": A2C_Learner}

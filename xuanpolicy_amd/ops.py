@@ -1,0 +1,255 @@
+"""Torch-tensor front end of the C ABI (include/xuanpolicy_amd.h).
+
+Every op validates device/dtype/shape/contiguity on the host (a wrong shape never reaches a kernel),
+passes raw device pointers plus torch's current hipStream_t, and raises XpaError on any failure.
+There is no CPU path: tensors must live on a ROCm device.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+ALGO = {"ppo": 0, "a2c": 1}
+DIST = {"gaussian": 0, "categorical": 1}
+N_OUT = 6
+OUT_KEYS = ("actor-loss", "critic-loss", "entropy", "loss", "clip_ratio", "predict_value")
+
+
+def lib():
+    return _lib.load()
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _req(t, name, dtype, shape=None, contiguous=True):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError("%s must be a torch.Tensor" % name)
+    if t.device.type != "cuda":
+        raise ValueError("%s must be on a ROCm device (got %s); xuanpolicy_amd has no CPU path" % (name, t.device))
+    if t.dtype != dtype:
+        raise TypeError("%s must be %s (got %s)" % (name, dtype, t.dtype))
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError("%s must have shape %s (got %s)" % (name, tuple(shape), tuple(t.shape)))
+    if contiguous and not t.is_contiguous():
+        raise ValueError("%s must be contiguous" % name)
+    return t
+
+
+def _row_stride(t, name, cols):
+    """2-D float tensor whose rows may be strided (e.g. a column block of a wider matrix)."""
+    if t.dim() != 2 or t.stride(1) != 1 or t.shape[1] != cols or t.stride(0) < cols:
+        raise ValueError("%s must be 2-D [n, %d] with unit column stride" % (name, cols))
+    return t.stride(0)
+
+
+# ------------------------------------------------------------------------------------------------
+def gae_scan(rew, val, term, closed, boot, gamma, gae_lambda, use_gae=True, adv=None, ret=None):
+    """K1.  All [n_envs, horizon]; closed uint8, the rest float32.  Returns (adv, ret)."""
+    N, T = rew.shape
+    for name, t, dt in (("rew", rew, torch.float32), ("val", val, torch.float32), ("term", term, torch.float32),
+                        ("closed", closed, torch.uint8), ("boot", boot, torch.float32)):
+        _req(t, name, dt, (N, T))
+    adv = torch.empty_like(rew) if adv is None else _req(adv, "adv", torch.float32, (N, T))
+    ret = torch.empty_like(rew) if ret is None else _req(ret, "ret", torch.float32, (N, T))
+    rc = lib().xpa_gae_scan(_p(rew), _p(val), _p(term), _p(closed), _p(boot), N, T, float(gamma), float(gae_lambda),
+                            int(bool(use_gae)), _p(adv), _p(ret), _stream(rew.device))
+    _lib.check(rc, "xpa_gae_scan")
+    return adv, ret
+
+
+def gather_num_partials(batch):
+    return int(lib().xpa_gather_num_partials(batch))
+
+
+def gather_minibatch(idx, obs, adv=None, obs_out=None, adv_partials=None):
+    """K4.  idx int64 [B] flat indices into obs rows ([n_rows, ...] any dtype, contiguous).
+    Returns (obs_out [B, ...], adv_partials float64 [n_partials, 2] or None)."""
+    _req(idx, "idx", torch.int64)
+    if idx.dim() != 1:
+        raise ValueError("idx must be 1-D")
+    B = idx.shape[0]
+    if not obs.is_contiguous() or obs.device.type != "cuda":
+        raise ValueError("obs must be a contiguous device tensor")
+    row_shape = tuple(obs.shape[1:])
+    row_bytes = obs[0].numel() * obs.element_size() if obs.shape[0] > 0 else 0
+    if obs_out is None:
+        obs_out = torch.empty((B,) + row_shape, dtype=obs.dtype, device=obs.device)
+    elif tuple(obs_out.shape) != (B,) + row_shape or obs_out.dtype != obs.dtype or not obs_out.is_contiguous():
+        raise ValueError("obs_out must be contiguous %s %s" % ((B,) + row_shape, obs.dtype))
+    if adv is not None:
+        _req(adv, "adv", torch.float32)
+        if adv.numel() != obs.shape[0]:
+            raise ValueError("adv must have one entry per obs row")
+        if adv_partials is None:
+            adv_partials = torch.empty((gather_num_partials(B), 2), dtype=torch.float64, device=obs.device)
+        else:
+            _req(adv_partials, "adv_partials", torch.float64, (gather_num_partials(B), 2))
+    rc = lib().xpa_gather_minibatch(_p(idx), B, obs.shape[0], _p(obs), row_bytes, _p(obs_out), _p(adv) if adv is not None else None,
+                                    _p(adv_partials) if adv is not None else None, _stream(obs.device))
+    _lib.check(rc, "xpa_gather_minibatch")
+    return obs_out, (adv_partials if adv is not None else None)
+
+
+class LossWorkspace:
+    """Reusable outputs of K2 for a fixed (batch, act_dim) (keeps the update step allocation-free)."""
+
+    def __init__(self, batch, act_dim, device, dist):
+        n = int(lib().xpa_loss_num_partials(batch))
+        w = int(lib().xpa_loss_partial_width(act_dim))
+        self.batch, self.act_dim = batch, act_dim
+        self.partials = torch.empty((n, w), dtype=torch.float32, device=device)
+        self.d_head = torch.empty((batch, act_dim), dtype=torch.float32, device=device)
+        self.d_v = torch.empty((batch,), dtype=torch.float32, device=device)
+        self.scalars = torch.empty((N_OUT,), dtype=torch.float32, device=device)
+        self.d_logstd = torch.empty((act_dim,), dtype=torch.float32, device=device) if dist == "gaussian" else None
+
+
+def policy_loss(algo, dist, head, logstd, v, act, adv, ret, old_logp=None, idx=None, adv_partials=None,
+                clip_range=0.2, vf_coef=0.25, ent_coef=0.0, ws=None):
+    """K2 + finalize.  Returns (scalars[6] device tensor, d_head, d_logstd or None, d_v).
+
+    head [B, A] float32; logstd [A] (gaussian); v [B].  act/old_logp/adv/ret are read at idx[b]
+    (idx int64 [B]) or at b when idx is None.  adv_partials (float64 [*, 2]) => per-minibatch adv-norm."""
+    if algo not in ALGO or dist not in DIST:
+        raise ValueError("algo must be ppo|a2c and dist gaussian|categorical")
+    _req(head, "head", torch.float32)
+    if head.dim() != 2:
+        raise ValueError("head must be [B, A]")
+    B, A = head.shape
+    _req(v, "v", torch.float32, (B,))
+    if dist == "gaussian":
+        _req(logstd, "logstd", torch.float32, (A,))
+    if idx is not None:
+        _req(idx, "idx", torch.int64, (B,))
+    rows = adv.numel()
+    _req(adv, "adv", torch.float32)
+    _req(ret, "ret", torch.float32)
+    if ret.numel() != rows:
+        raise ValueError("ret and adv must have the same number of rows")
+    if idx is None and rows != B:
+        raise ValueError("without idx, adv/ret must have B rows")
+    _req(act, "act", torch.float32)
+    if act.numel() != rows * (A if dist == "gaussian" else 1):
+        raise ValueError("act has %d elements, expected %d" % (act.numel(), rows * (A if dist == "gaussian" else 1)))
+    if algo == "ppo":
+        if old_logp is None:
+            raise ValueError("PPO needs old_logp")
+        _req(old_logp, "old_logp", torch.float32)
+        if old_logp.numel() != rows:
+            raise ValueError("old_logp must have one entry per row")
+    if adv_partials is not None:
+        _req(adv_partials, "adv_partials", torch.float64)
+    if ws is None or ws.batch != B or ws.act_dim != A:
+        ws = LossWorkspace(B, A, head.device, dist)
+    s = _stream(head.device)
+    L = lib()
+    rc = L.xpa_policy_loss_fwd_bwd(ALGO[algo], DIST[dist], B, A, _p(head), _p(logstd) if dist == "gaussian" else None,
+                                   _p(v), _p(idx), rows, _p(act), _p(old_logp) if algo == "ppo" else None, _p(adv), _p(ret),
+                                   _p(adv_partials), adv_partials.shape[0] if adv_partials is not None else 0,
+                                   float(clip_range), float(vf_coef), float(ent_coef), _p(ws.d_head), _p(ws.d_v),
+                                   _p(ws.partials), s)
+    _lib.check(rc, "xpa_policy_loss_fwd_bwd")
+    rc = L.xpa_policy_loss_finalize(ALGO[algo], DIST[dist], B, A, _p(ws.partials), ws.partials.shape[0],
+                                    float(vf_coef), float(ent_coef), _p(ws.scalars), _p(ws.d_logstd), s)
+    _lib.check(rc, "xpa_policy_loss_finalize")
+    return ws.scalars, ws.d_head, ws.d_logstd, ws.d_v
+
+
+# ------------------------------------------------------------------------------------------------
+def rms_num_partials(n):
+    return int(lib().xpa_rms_num_partials(n))
+
+
+def rms_update(x, mean, var, count, partials=None):
+    """K5a+b: RunningMeanStd.update(x) on device.  x [n, dim] float32 (row stride may exceed dim);
+    mean/var float32 [dim], count float64 [1] — all updated in place."""
+    n, dim = x.shape
+    ld = _row_stride(x, "x", dim)
+    _req(mean, "mean", torch.float32, (dim,))
+    _req(var, "var", torch.float32, (dim,))
+    _req(count, "count", torch.float64, (1,))
+    np_ = rms_num_partials(n)
+    if partials is None:
+        partials = torch.empty((2 * np_, dim), dtype=torch.float64, device=x.device)
+    else:
+        _req(partials, "partials", torch.float64, (2 * np_, dim))
+    s = _stream(x.device)
+    _lib.check(lib().xpa_rms_partials(_p(x), n, dim, ld, _p(partials), s), "xpa_rms_partials")
+    _lib.check(lib().xpa_rms_merge(_p(partials), np_, n, dim, _p(mean), _p(var), _p(count), s), "xpa_rms_merge")
+
+
+def obs_normalize(x, mean, var, clip_range, out, col_out=None, col_ld=0, cursor=None):
+    """K5c: out = clip((x - mean)/(sqrt(var)+1e-8)); optionally also into a buffer column."""
+    n, dim = x.shape
+    ldx = _row_stride(x, "x", dim)
+    ldo = _row_stride(out, "out", dim)
+    _req(mean, "mean", torch.float32, (dim,))
+    _req(var, "var", torch.float32, (dim,))
+    if col_out is not None:
+        _req(col_out, "col_out", torch.float32)
+        _req(cursor, "cursor", torch.int32, (4,))
+    rc = lib().xpa_obs_normalize(_p(x), n, dim, ldx, _p(mean), _p(var), float(clip_range), _p(out), ldo, _p(col_out),
+                                 int(col_ld), _p(cursor), _stream(x.device))
+    _lib.check(rc, "xpa_obs_normalize")
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+def new_cursor(device):
+    """xpa_cursor_t {ptr, step, reserved[2]} as an int32[4] device tensor."""
+    return torch.zeros((4,), dtype=torch.int32, device=device)
+
+
+def rollout_sample(dist, head, logstd, v, cursor, seed, buf_act, buf_logp, buf_val, env_in, act_clip=1.0):
+    """K3: sample actions for every env, store act/logp/val at column cursor.ptr, write env input."""
+    _req(head, "head", torch.float32)
+    N, A = head.shape
+    _req(v, "v", torch.float32, (N,))
+    _req(cursor, "cursor", torch.int32, (4,))
+    _req(buf_logp, "buf_logp", torch.float32)
+    _req(buf_val, "buf_val", torch.float32)
+    if buf_logp.dim() != 2 or buf_logp.shape[0] != N or tuple(buf_val.shape) != tuple(buf_logp.shape):
+        raise ValueError("buf_logp/buf_val must be [n_envs, horizon]")
+    T = buf_logp.shape[1]
+    _req(buf_act, "buf_act", torch.float32, (N, T, A) if dist == "gaussian" else (N, T))
+    ld_env = _row_stride(env_in, "env_in", A)
+    if env_in.dtype != torch.float32 or env_in.shape[0] != N:
+        raise ValueError("env_in must be float32 [n_envs, act_dim]")
+    if dist == "gaussian":
+        _req(logstd, "logstd", torch.float32, (A,))
+    rc = lib().xpa_rollout_sample(DIST[dist], N, A, T, _p(head), _p(logstd) if dist == "gaussian" else None, _p(v),
+                                  _p(cursor), int(seed) & 0xFFFFFFFF, float(act_clip), _p(buf_act), _p(buf_logp),
+                                  _p(buf_val), _p(env_in), ld_env, _stream(head.device))
+    _lib.check(rc, "xpa_rollout_sample")
+
+
+def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term,
+                 buf_closed, buf_boot, gamma, mask_returns=True, use_rewnorm=True, rew_range=5.0, atari_lifeloss=False):
+    """K8: reward normalisation, return tracker + ret_rms, rewards/terminals/closures into the buffer
+    column cursor.ptr, then cursor.ptr = (ptr + 1) % horizon, cursor.step += 1."""
+    N = rew.shape[0]
+    _req(rew, "rew", torch.float32, (N,))
+    _req(term, "term", torch.uint8, (N,))
+    _req(trunc, "trunc", torch.uint8, (N,))
+    _req(v_boot, "v_boot", torch.float32, (N,))
+    _req(cursor, "cursor", torch.int32, (4,))
+    for name, t in (("ret_mean", ret_mean), ("ret_var", ret_var)):
+        _req(t, name, torch.float32, (1,))
+    _req(ret_count, "ret_count", torch.float64, (1,))
+    _req(returns, "returns", torch.float32, (N,))
+    T = buf_rew.shape[1]
+    for name, t in (("buf_rew", buf_rew), ("buf_term", buf_term), ("buf_boot", buf_boot)):
+        _req(t, name, torch.float32, (N, T))
+    _req(buf_closed, "buf_closed", torch.uint8, (N, T))
+    rc = lib().xpa_rollout_post(N, T, _p(rew), _p(term), _p(trunc), _p(v_boot), _p(cursor), _p(ret_mean), _p(ret_var),
+                                _p(ret_count), _p(returns), _p(buf_rew), _p(buf_term), _p(buf_closed), _p(buf_boot),
+                                float(gamma), int(bool(mask_returns)), int(bool(use_rewnorm)), float(rew_range),
+                                int(bool(atari_lifeloss)), _stream(rew.device))
+    _lib.check(rc, "xpa_rollout_post")

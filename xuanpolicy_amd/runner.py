@@ -1,0 +1,96 @@
+"""Config surface and runner for the on-policy path.
+
+Mirrors (reference paths):
+  get_arguments / recursive_dict_update   xuance/common/common_tools.py:13-83 (basic.yaml -> algo/env yaml ->
+                                          user yaml -> parser args, as a SimpleNamespace)
+  Runner_DRL.__init__ / run               xuance/torch/runners/runner_drl.py:15-98 (representation, policy,
+                                          Adam(eps=1e-5), LinearLR(end_factor=0, total_iters=running_steps),
+                                          REGISTRY_Agent[...](args, envs, policy, optimizer, scheduler, device))
+The YAML files under xuanpolicy_amd/configs/ carry the reference's key names; env_name "SynthBox"
+selects the device-resident SynthBox env (BASELINE.json configs).
+"""
+import os
+from copy import deepcopy
+from types import SimpleNamespace
+
+import torch
+import yaml
+
+from . import agents
+from .envs import SynthBoxVecEnv
+from .policies import (ActivationFunctions, Basic_MLP, REGISTRY as REGISTRY_Policy, REGISTRY_Representation)
+
+CONFIG_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "configs")
+
+
+def recursive_dict_update(basic, target):
+    out = deepcopy(basic)
+    for k, v in target.items():
+        out[k] = recursive_dict_update(out.get(k, {}), v) if isinstance(v, dict) else v
+    return out
+
+
+def get_config(path):
+    with open(path) as f:
+        return yaml.safe_load(f)
+
+
+def get_arguments(method, env, env_id, config_path=None, parser_args=None):
+    """common_tools.py:32-83 for a single method: basic.yaml, then <method>/<env>.yaml, then the user
+    YAML, then parser args."""
+    cfg = get_config(os.path.join(CONFIG_DIR, "basic.yaml"))
+    algo = os.path.join(CONFIG_DIR, method, env + ".yaml")
+    if os.path.exists(algo):
+        cfg = recursive_dict_update(cfg, get_config(algo))
+    if config_path is not None:
+        cfg = recursive_dict_update(cfg, get_config(config_path))
+    if parser_args is not None:
+        cfg = recursive_dict_update(cfg, dict(vars(parser_args)))
+    args = SimpleNamespace(**cfg)
+    args.env_id = env_id
+    return args
+
+
+def make_envs(config, device=None, shard=0):
+    if config.env_name == "SynthBox":
+        return SynthBoxVecEnv(config.parallels, config.obs_dim, config.act_dim, seed=config.seed,
+                              discrete=bool(getattr(config, "discrete", False)),
+                              max_episode_steps=getattr(config, "max_episode_steps", 1000), device=device, shard=shard)
+    raise NotImplementedError("env_name %r: only the device-resident SynthBox env is built in; pass any VecEnv "
+                              "with the reference's step contract to the agent directly" % config.env_name)
+
+
+def build_agent(config, device=None, envs=None, shard=0):
+    """runner_drl.py:15-75 for PPO_Clip / A2C."""
+    device = torch.device(device if device is not None else config.device)
+    envs = envs if envs is not None else make_envs(config, device, shard)
+    config.observation_space, config.action_space = envs.observation_space, envs.action_space
+    act = ActivationFunctions[config.activation]
+    init = torch.nn.init.orthogonal_
+    if config.representation == "Basic_MLP":
+        rep = Basic_MLP(envs.observation_space.shape, config.representation_hidden_size, None, init, act, device)
+    else:
+        rep = REGISTRY_Representation[config.representation](envs.observation_space.shape, device)
+    policy = REGISTRY_Policy[config.policy](envs.action_space, rep, config.actor_hidden_size, config.critic_hidden_size,
+                                            None, init, act, device)
+    opt_kw = {"fused": True} if getattr(config, "fused_adam", True) and device.type == "cuda" else {}
+    optimizer = torch.optim.Adam(policy.parameters(), config.learning_rate, eps=1e-5, **opt_kw)
+    scheduler = torch.optim.lr_scheduler.LinearLR(optimizer, start_factor=1.0, end_factor=0.0,
+                                                  total_iters=config.running_steps)
+    return agents.REGISTRY[config.agent](config, envs, policy, optimizer, scheduler, device)
+
+
+def build_synthbox_ppo(n_envs=4096, n_steps=128, obs_dim=17, act_dim=6, hidden=256, n_epoch=16, n_minibatch=8,
+                       seed=1, device="cuda:0", agent="PPO_Clip", discrete=False, **overrides):
+    """The BASELINE.json C2 configuration (ppo/mujoco.yaml hyper-parameters on SynthBox(17, 6))."""
+    method = "ppo" if agent == "PPO_Clip" else "a2c"
+    cfg = get_arguments(method, "synthbox", "SynthBox-v0")
+    cfg.agent = agent
+    cfg.parallels, cfg.n_steps, cfg.obs_dim, cfg.act_dim = n_envs, n_steps, obs_dim, act_dim
+    cfg.n_epoch, cfg.n_minibatch, cfg.seed, cfg.discrete = n_epoch, n_minibatch, seed, discrete
+    cfg.policy = "Categorical_AC" if discrete else "Gaussian_AC"
+    cfg.representation_hidden_size = cfg.actor_hidden_size = cfg.critic_hidden_size = [hidden]
+    for k, v in overrides.items():
+        setattr(cfg, k, v)
+    torch.manual_seed(seed)
+    return build_agent(cfg, device)
