@@ -1,0 +1,227 @@
+#!/usr/bin/env python
+"""Benchmark: end-to-end PPO-Clip env-steps/s at num_envs=4096, horizon=128 (BASELINE.json config C2:
+SynthBox(obs=17, act=6), ppo/mujoco.yaml hyper-parameters: n_epoch 16, n_minibatch 8, [256] nets,
+LeakyReLU, Adam eps=1e-5, LinearLR) plus the GAE kernel's HBM roofline.
+
+A "step" is one PPO iteration on every rank: 128 env steps of the 4096-env device-resident rollout
+(obs-RMS + normalise, policy forward, action sample, env step, bootstrap critic, bookkeeping), the GAE
+scan over [4096, 128], then 16 epochs x 8 minibatches of 65 536 (gather, heads forward, fused loss
+fwd+bwd kernel, MLP backward, [RCCL all-reduce], grad-clip, Adam, LinearLR).  Inputs start resident in
+HBM (the env lives on the GPU).  value = env-steps processed by all ranks / max-over-ranks wall time.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N ... bench.py --gpus N ...     (one process per GPU, RCCL)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=8)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--n-envs", type=int, default=4096)
+    p.add_argument("--horizon", type=int, default=128)
+    p.add_argument("--obs-dim", type=int, default=17)
+    p.add_argument("--act-dim", type=int, default=6)
+    p.add_argument("--hidden", type=int, default=256)
+    p.add_argument("--n-epoch", type=int, default=16)
+    p.add_argument("--n-minibatch", type=int, default=8)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-updates", type=int, default=8, help="updates timed in the bounded CPU sample")
+    p.add_argument("--no-sweep", action="store_true")
+    p.add_argument("--no-kernel-timing", action="store_true")
+    p.add_argument("--out", default=None, help="also write the JSON line to this file")
+    return p.parse_args()
+
+
+def gae_bytes(n_envs, horizon, mid_truncations):
+    """20 B per (env, step) + 4 B per env (last bootstrap) + 4 B per mid-buffer
+    truncation bootstrap."""
+    return 20.0 * n_envs * horizon + 4.0 * n_envs + 4.0 * mid_truncations
+
+
+def loss_bytes_gauss(batch, act_dim):
+    """Gaussian loss fwd+bwd = 4 (3A + 5) B per sample."""
+    return 4.0 * (3 * act_dim + 5) * batch
+
+
+def gae_sweep(device, sizes=(4096, 65536, 262144, 1048576), horizon=128, reps=7):
+    """GAE kernel alone, Infinity Cache flushed (512 MiB write) before each timed launch."""
+    import torch
+    from xuanpolicy_amd import ops
+    flush = torch.empty(512 * 1024 * 1024 // 4, dtype=torch.float32, device=device)
+    out = []
+    for N in sizes:
+        g = torch.Generator(device=device).manual_seed(N)
+        rew = torch.randn(N, horizon, device=device, generator=g)
+        val = torch.randn(N, horizon, device=device, generator=g)
+        term = (torch.rand(N, horizon, device=device, generator=g) < 0.01).float()
+        closed = (torch.rand(N, horizon, device=device, generator=g) < 0.001).to(torch.uint8)
+        closed[:, -1] = 1
+        boot = torch.randn(N, horizon, device=device, generator=g) * closed
+        adv = torch.empty_like(rew)
+        ret = torch.empty_like(rew)
+        mid = int((closed[:, :-1] > 0).sum())
+        times = []
+        for _ in range(reps):
+            flush.fill_(1.0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ops.gae_scan(rew, val, term, closed, boot, 0.99, 0.95, True, adv=adv, ret=ret)
+            e1.record()
+            e1.synchronize()
+            times.append(e0.elapsed_time(e1))
+        times.sort()
+        ms = times[len(times) // 2]
+        b = gae_bytes(N, horizon, mid)
+        out.append({"n_envs": N, "horizon": horizon, "ms": round(ms, 5), "GB/s": round(b / ms / 1e6, 1),
+                    "frac": round(b / ms / 1e6 / HBM_PEAK_GBS, 3), "algorithmic_bytes": int(b)})
+        del rew, val, term, closed, boot, adv, ret
+    del flush
+    torch.cuda.empty_cache()
+    return out
+
+
+def cpu_baseline(args, cores):
+    """The oracle's restatement of the reference loop (oracle/cpu_ref.AgentLoopRef: per-env
+    DummyVecEnv stepping, per-env finish_path, numpy fancy-index sampling, torch-CPU learner with
+    Adam(eps=1e-5) + LinearLR) on a bounded sample of the same workload."""
+    import numpy as np
+    import torch
+    from oracle import cpu_ref, synth_env
+    torch.set_num_threads(cores)
+    N, T, D, A, H = args.n_envs, args.horizon, args.obs_dim, args.act_dim, args.hidden
+    torch.manual_seed(1)
+    np.random.seed(1)
+    envs = [synth_env.SynthBoxEnv(D, A, seed=1, env_index=i) for i in range(N)]
+    pol = cpu_ref.build_actor_critic_ref(D, A, [H], [H], [H])
+    opt = torch.optim.Adam(pol.parameters(), 4e-4, eps=1e-5)
+    sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.0, total_iters=100000000)
+    lrn = cpu_ref.LearnerRef(pol, opt, sch, "ppo", 0.25, 0.0, 0.2, 0.5, True)
+    loop = cpu_ref.AgentLoopRef(envs, pol, lrn, T, args.n_epoch, args.n_minibatch, 0.99, 0.95)
+    t0 = time.perf_counter()
+    loop.run_steps(T, max_updates=args.cpu_updates)
+    wall = time.perf_counter() - t0
+    tm = loop.timers
+    per_update = (tm["sample"] + tm["update"]) / max(loop.n_updates, 1)
+    n_updates_full = args.n_epoch * ((N * T + (N * T // args.n_minibatch) - 1) // (N * T // args.n_minibatch))
+    rollout = tm["act"] + tm["env"] + tm["store"]
+    iteration = rollout + tm["gae"] + n_updates_full * per_update
+    return {"value": round(N * T / iteration, 1), "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "sample": ("one %dx%d rollout (per-env SynthBoxEnv stepping as DummyVecEnv_Gym) + per-env finish_path "
+                       "GAE + %d of the %d minibatch updates (B=%d) timed in %.1f s; iteration time = rollout %.2f s "
+                       "+ GAE %.2f s + %d x %.3f s per update (sample + learner.update) = %.2f s"
+                       % (N, T, loop.n_updates, n_updates_full, N * T // args.n_minibatch, wall, rollout, tm["gae"],
+                          n_updates_full, per_update, iteration))}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from xuanpolicy_amd import ops
+    from xuanpolicy_amd.distributed import attach_flat_grads, broadcast_parameters, init_from_env
+    from xuanpolicy_amd.runner import build_synthbox_ppo
+
+    rank, local, world = init_from_env()
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    N, T = args.n_envs, args.horizon
+    agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=args.obs_dim, act_dim=args.act_dim, hidden=args.hidden,
+                               n_epoch=args.n_epoch, n_minibatch=args.n_minibatch, seed=1, device=device,
+                               shard=rank)
+    if world > 1:
+        broadcast_parameters(agent.policy)
+    attach_flat_grads(agent.learner, allreduce=world > 1)
+
+    for _ in range(args.warmup):
+        agent.train(T)
+    torch.cuda.synchronize()
+    ops.TIMER.enabled = not args.no_kernel_timing
+    ops.TIMER.reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        agent.train(T)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ops.TIMER.enabled = False
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e)
+
+    gae_ms = ops.TIMER.mean_ms("gae")
+    loss_ms = ops.TIMER.mean_ms("loss")
+    mem = agent.memory
+    mid_trunc = int(((mem.closed[:, :-1] > 0) & (mem.terminals[:, :-1] == 0)).sum())
+    B = N * T // args.n_minibatch
+    result = None
+    if rank == 0:
+        value = world * N * T * args.steps / elapsed
+        roofline = None
+        if gae_ms:
+            gb = gae_bytes(N, T, mid_trunc)
+            ach = gb / gae_ms / 1e6
+            traffic = None
+            pmc = os.path.join(REPO, "profiles", "pmc_gae_r01.json")
+            if os.path.exists(pmc):
+                with open(pmc) as f:
+                    traffic = json.load(f).get("hbm_bytes_per_launch")
+            roofline = {"kernel": "xpa_gae_scan (gae_scan_kernel<4>)", "bound": "hbm", "achieved": round(ach, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "avg_launch_us": round(gae_ms * 1e3, 3), "algorithmic_bytes_per_launch": int(gb),
+                        "launches": len(ops.TIMER.events.get("gae", []))}
+        loss_kernel = None
+        if loss_ms:
+            lb = loss_bytes_gauss(B, args.act_dim)
+            loss_kernel = {"kernel": "xpa_policy_loss_fwd_bwd (gaussian, ppo)", "avg_launch_us": round(loss_ms * 1e3, 3),
+                           "achieved": round(lb / loss_ms / 1e6, 1), "unit": "GB/s",
+                           "frac": round(lb / loss_ms / 1e6 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": int(lb),
+                           "launches": len(ops.TIMER.events.get("loss", []))}
+        result = {
+            "metric": "env-steps/sec at num_envs=4096, horizon=128; GAE kernel HBM GB/s vs peak",
+            "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "PPO-Clip SynthBox(obs=17,act=6) num_envs=%d/GPU horizon=%d, ppo/mujoco.yaml "
+                                   "(n_epoch %d, n_minibatch %d, nets [%d] LeakyReLU)" %
+                                   (N, T, args.n_epoch, args.n_minibatch, args.hidden),
+                       "num_envs_per_gpu": N, "horizon": T, "global_envs": N * world, "minibatch": B,
+                       "updates_per_step": args.n_epoch * args.n_minibatch,
+                       "parallelism": "dp%d (env shards, 1 RCCL all-reduce per minibatch)" % world},
+            "roofline": roofline,
+            "loss_kernel": loss_kernel,
+        }
+        if not args.no_sweep and world == 1:
+            result["gae_sweep_flushed"] = gae_sweep(device, horizon=T)
+        if not args.no_cpu_baseline and world == 1:
+            cores = min(16, len(os.sched_getaffinity(0)))
+            result["cpu_baseline"] = cpu_baseline(args, cores)
+            result["speedup_vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
+        line = json.dumps(result)
+        print(line, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

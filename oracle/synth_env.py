@@ -130,12 +130,30 @@ class SynthBoxEnv:
     def render(self, *a, **k):
         pass
 
+    NOISE_CHUNK = 64  # NOISE * xi drawn for 64 steps at a time (same values, amortised hashing)
+
     def reset(self):
         self.episode += 1
         self._episode_step = 0
         self._episode_score = 0.0
+        self._chunk_t0, self._chunk = -1, None
         self.state = synthbox_reset_state(self.seed, self.index, self.episode, self.D)
         return self.state.copy(), {"episode_step": 0}
+
+    def _noise(self, t):
+        # hash4(seed, env, ep, k) == mix32(prefix ^ k) with prefix = mix(mix(mix(seed) ^ env) ^ ep):
+        # the prefix is fixed per episode, so a chunk costs one vectorised mix32 (same values).
+        if self._chunk is None or not (0 <= t - self._chunk_t0 < self.NOISE_CHUNK):
+            if self._chunk is None:
+                self._prefix = mix32(mix32(mix32(np.uint32(self.seed & MASK32)) ^ np.uint32(self.index))
+                                     ^ np.uint32(self.episode))
+            k = (np.arange(t * self.D * 4, (t + self.NOISE_CHUNK) * self.D * 4, dtype=np.uint64)
+                 & MASK32).astype(np.uint32)
+            u = u01(mix32(self._prefix ^ k)).reshape(self.NOISE_CHUNK, self.D, 4)
+            xi = (u[..., 0] + u[..., 1] + u[..., 2] + u[..., 3] - np.float32(2.0)) * np.float32(np.sqrt(3.0))
+            self._chunk_t0 = t
+            self._chunk = np.float32(NOISE) * xi
+        return self._chunk[t - self._chunk_t0]
 
     def step(self, action):
         W, U = self.W, self.U
@@ -143,10 +161,9 @@ class SynthBoxEnv:
             drive = U[:, int(action)]
         else:
             drive = U @ np.clip(np.asarray(action, np.float32), -1.0, 1.0)
-        xi = synthbox_noise(self.seed, self.index, self.episode, self._episode_step, self.D)
-        x = W @ self.state + drive + np.float32(NOISE) * xi
-        s = np.tanh(x.astype(np.float32))
-        r = float(-np.mean(s * s))
+        xi = self._noise(self._episode_step)
+        s = np.tanh(W @ self.state + drive + xi)
+        r = -float(s @ s) / self.D
         self._episode_step += 1
         self._episode_score += r
         term = bool(s[0] > TERM_THRESH)

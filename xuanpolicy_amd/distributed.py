@@ -1,0 +1,94 @@
+"""Data-parallel on-policy training across the GPUs of one node (one process per GPU).
+
+The reference has no multi-device path (its only collective, comm.Allreduce in
+xuance/common/statistic_tools.py:16, is never enabled).  Here env shards partition across ranks
+(each rank owns its own envs, rollout buffer, GAE, permutation and minibatches: no exchange), and the
+only collective is ONE all-reduce (average) of the flat fp32 gradient per minibatch, before
+clip_grad_norm_, so the clipped norm is the global one.
+
+FlatGrads makes every parameter's .grad a view into one contiguous buffer, so autograd accumulates
+straight into it and the all-reduce is a single RCCL call over xGMI (latency-bound at 0.04-1 MiB;
+one bucket, no overlap needed).  Backend "nccl" is RCCL on ROCm; "gloo" is used by the CPU tests.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class FlatGrads:
+    """Owns a flat gradient buffer; params' .grad are views into it (kept across zero_grad)."""
+
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        for p in self.params:
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+
+    def zero_(self):
+        self.flat.zero_()
+
+    def ensure_views(self):
+        off = 0
+        for p in self.params:
+            if p.grad is None or p.grad.data_ptr() != self.flat[off:].data_ptr():
+                g = p.grad
+                p.grad = self.flat[off:off + p.numel()].view_as(p)
+                if g is not None:
+                    p.grad.copy_(g)
+            off += p.numel()
+
+
+class GradAllReduce:
+    """learner.grad_sync hook: average the flat gradient over the process group (one collective)."""
+
+    def __init__(self, flat_grads, group=None):
+        self.fg = flat_grads
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.avg = dist.get_backend(group) == "nccl"
+        self.calls = 0
+
+    def __call__(self, params):
+        self.fg.ensure_views()
+        if self.avg:
+            dist.all_reduce(self.fg.flat, op=dist.ReduceOp.AVG, group=self.group)
+        else:
+            dist.all_reduce(self.fg.flat, op=dist.ReduceOp.SUM, group=self.group)
+            self.fg.flat.div_(self.world)
+        self.calls += 1
+
+
+def attach_flat_grads(learner, allreduce=True, group=None):
+    """Give a learner flat gradients (and the all-reduce hook when a process group is initialised)."""
+    fg = FlatGrads(learner.policy.parameters())
+    learner.flat_grads = fg
+    if allreduce and dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        learner.grad_sync = GradAllReduce(fg, group)
+    return fg
+
+
+def broadcast_parameters(module, src=0, group=None):
+    """Start every rank from rank src's weights (one broadcast per tensor, at setup only)."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        with torch.no_grad():
+            for t in list(module.parameters()) + list(module.buffers()):
+                dist.broadcast(t, src, group=group)
+
+
+def init_from_env(backend=None):
+    """torchrun-style init (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    return rank, local, world

@@ -65,7 +65,11 @@ class _FusedPolicyGradient(Learner):
         self._params = [p for p in policy.parameters()]
 
     def _backward_and_step(self, head, logstd, v, d_head, d_logstd, d_v):
-        self.optimizer.zero_grad(set_to_none=True)
+        fg = getattr(self, "flat_grads", None)
+        if fg is not None:
+            fg.zero_()  # grads are views into one flat buffer (xuanpolicy_amd.distributed.FlatGrads)
+        else:
+            self.optimizer.zero_grad(set_to_none=True)
         tensors, grads = [head, v], [d_head, d_v]
         if logstd is not None:
             tensors.append(logstd)

@@ -20,6 +20,42 @@ def lib():
     return _lib.load()
 
 
+class KernelTimer:
+    """Optional per-launch HIP-event timing of the hot kernels on the stream they are launched on
+    (bench.py's live roofline).  Disabled by default: no events in the hot loop."""
+
+    def __init__(self):
+        self.enabled = False
+        self.events = {}
+
+    def start(self, name):
+        if not self.enabled:
+            return None
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        return e0
+
+    def stop(self, name, e0):
+        if e0 is None:
+            return
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self.events.setdefault(name, []).append((e0, e1))
+
+    def reset(self):
+        self.events = {}
+
+    def mean_ms(self, name):
+        ev = self.events.get(name, [])
+        if not ev:
+            return None
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+
+
+TIMER = KernelTimer()
+
+
 def _p(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
@@ -58,8 +94,10 @@ def gae_scan(rew, val, term, closed, boot, gamma, gae_lambda, use_gae=True, adv=
         _req(t, name, dt, (N, T))
     adv = torch.empty_like(rew) if adv is None else _req(adv, "adv", torch.float32, (N, T))
     ret = torch.empty_like(rew) if ret is None else _req(ret, "ret", torch.float32, (N, T))
+    ev = TIMER.start("gae")
     rc = lib().xpa_gae_scan(_p(rew), _p(val), _p(term), _p(closed), _p(boot), N, T, float(gamma), float(gae_lambda),
                             int(bool(use_gae)), _p(adv), _p(ret), _stream(rew.device))
+    TIMER.stop("gae", ev)
     _lib.check(rc, "xpa_gae_scan")
     return adv, ret
 
@@ -150,11 +188,13 @@ def policy_loss(algo, dist, head, logstd, v, act, adv, ret, old_logp=None, idx=N
         ws = LossWorkspace(B, A, head.device, dist)
     s = _stream(head.device)
     L = lib()
+    ev = TIMER.start("loss")
     rc = L.xpa_policy_loss_fwd_bwd(ALGO[algo], DIST[dist], B, A, _p(head), _p(logstd) if dist == "gaussian" else None,
                                    _p(v), _p(idx), rows, _p(act), _p(old_logp) if algo == "ppo" else None, _p(adv), _p(ret),
                                    _p(adv_partials), adv_partials.shape[0] if adv_partials is not None else 0,
                                    float(clip_range), float(vf_coef), float(ent_coef), _p(ws.d_head), _p(ws.d_v),
                                    _p(ws.partials), s)
+    TIMER.stop("loss", ev)
     _lib.check(rc, "xpa_policy_loss_fwd_bwd")
     rc = L.xpa_policy_loss_finalize(ALGO[algo], DIST[dist], B, A, _p(ws.partials), ws.partials.shape[0],
                                     float(vf_coef), float(ent_coef), _p(ws.scalars), _p(ws.d_logstd), s)

@@ -63,6 +63,7 @@ def make_envs(config, device=None, shard=0):
 def build_agent(config, device=None, envs=None, shard=0):
     """runner_drl.py:15-75 for PPO_Clip / A2C."""
     device = torch.device(device if device is not None else config.device)
+    shard = getattr(config, "shard", shard)
     envs = envs if envs is not None else make_envs(config, device, shard)
     config.observation_space, config.action_space = envs.observation_space, envs.action_space
     act = ActivationFunctions[config.activation]
