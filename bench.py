@@ -130,7 +130,7 @@ def main():
     import torch
     import torch.distributed as dist
     from xuanpolicy_amd import ops
-    from xuanpolicy_amd.distributed import attach_flat_grads, broadcast_parameters, init_from_env
+    from xuanpolicy_amd.distributed import broadcast_parameters, init_from_env
     from xuanpolicy_amd.runner import build_synthbox_ppo
 
     rank, local, world = init_from_env()
@@ -140,9 +140,9 @@ def main():
     agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=args.obs_dim, act_dim=args.act_dim, hidden=args.hidden,
                                n_epoch=args.n_epoch, n_minibatch=args.n_minibatch, seed=1, device=device,
                                shard=rank)
+    agent.learner.enable_fast_path()  # flat params/grads, fused clip+Adam, RCCL hook when world > 1
     if world > 1:
         broadcast_parameters(agent.policy)
-    attach_flat_grads(agent.learner, allreduce=world > 1)
 
     for _ in range(args.warmup):
         agent.train(T)

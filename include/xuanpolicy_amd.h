@@ -157,6 +157,17 @@ int xpa_rollout_post(int64_t n_envs, int64_t horizon, const float *rew, const ui
                      uint8_t *buf_closed, float *buf_boot, float gamma, int mask_returns,
                      int use_rewnorm, float rew_range, int atari_lifeloss, xpa_stream_t stream);
 
+/* K9 — fused global-norm gradient clipping + Adam over flat fp32 buffers (all 16-B aligned).
+ * Replaces torch.nn.utils.clip_grad_norm_ + torch.optim.Adam.step in PPOCLIP_Learner.update /
+ * A2C_Learner.update (ppoclip_learner.py:47-49, a2c_learner.py:34-35) for the Adam(eps=1e-5) the runner
+ * builds (xuance/torch/runners/runner_drl.py:71).  max_norm <= 0 disables clipping.  step is the
+ * 1-based Adam step count.  norm_partials: xpa_grad_norm_num_partials(n) doubles of scratch.
+ * Writes the pre-clip total norm to *total_norm_out when non-NULL. */
+int64_t xpa_grad_norm_num_partials(int64_t n);
+int xpa_clip_adam_step(float *param, float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+                       double *norm_partials, float max_norm, float lr, float beta1, float beta2, float eps,
+                       int64_t step, float *total_norm_out, xpa_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -181,7 +181,7 @@ def test_fused_agent_iteration_matches_cpu_replay():
     from xuanpolicy_amd.runner import build_synthbox_ppo
     N, T, D, A = 128, 32, 17, 6
     agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=D, act_dim=A, hidden=64, n_epoch=2, n_minibatch=4,
-                               seed=9, device=DEV, ent_coef=0.01, fused_adam=False)
+                               seed=9, device=DEV, ent_coef=0.01)
     pol = cpu_ref.build_actor_critic_ref(D, A, [64], [64], [64])
     pol.load_state_dict({k: v.cpu() for k, v in agent.policy.state_dict().items()})
     agent.train(T - 1, log=False)

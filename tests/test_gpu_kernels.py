@@ -351,3 +351,56 @@ def test_rollout_post_matches_reference_rules(algo, atari):
         assert abs(float(rv) - float(ret_rms.var)) < 1e-4 * max(1, abs(float(ret_rms.var)))
         assert abs(float(rc) - ret_rms.count) < 1e-9
     assert _h(cur)[0] == 0 and _h(cur)[1] == T
+
+
+# ---------------------------------------------------------------------------------------------- K9
+@pytest.mark.parametrize("max_norm", [0.5, 0.0, 1e9])
+def test_fused_clip_adam_matches_torch(max_norm):
+    """xpa_clip_adam_step == clip_grad_norm_ + torch.optim.Adam (foreach) over several steps, with
+    optimizer.state_dict() still describing the moments."""
+    from xuanpolicy_amd.flat import FlatState, FusedClipAdam
+    torch.manual_seed(0)
+    net_a = torch.nn.Sequential(torch.nn.Linear(17, 33), torch.nn.LeakyReLU(), torch.nn.Linear(33, 7)).to(DEV)
+    net_b = torch.nn.Sequential(torch.nn.Linear(17, 33), torch.nn.LeakyReLU(), torch.nn.Linear(33, 7)).to(DEV)
+    net_b.load_state_dict(net_a.state_dict())
+    opt_a = torch.optim.Adam(net_a.parameters(), 4e-4, eps=1e-5, foreach=True)
+    opt_b = torch.optim.Adam(net_b.parameters(), 4e-4, eps=1e-5)
+    fs = FlatState(net_b.parameters())
+    fused = FusedClipAdam(opt_b, fs)
+    for step in range(6):
+        x = torch.randn(64, 17, device=DEV)
+        opt_a.zero_grad()
+        (net_a(x) ** 2).mean().backward()
+        if max_norm > 0:
+            torch.nn.utils.clip_grad_norm_(net_a.parameters(), max_norm)
+        opt_a.step()
+        fs.zero_()
+        (net_b(x) ** 2).mean().backward()
+        fused.step(max_norm)
+        for pa, pb in zip(net_a.parameters(), net_b.parameters()):
+            np.testing.assert_allclose(_h(pb), _h(pa), rtol=1e-5, atol=1e-7)
+    sa, sb = opt_a.state_dict()["state"], opt_b.state_dict()["state"]
+    for k in sa:
+        np.testing.assert_allclose(_h(sb[k]["exp_avg"]), _h(sa[k]["exp_avg"]), rtol=1e-5, atol=1e-9)
+        np.testing.assert_allclose(_h(sb[k]["exp_avg_sq"]), _h(sa[k]["exp_avg_sq"]), rtol=1e-4, atol=1e-10)
+        assert float(sb[k]["step"]) == float(sa[k]["step"]) == 6.0
+
+
+def test_splitk_linear_matches_linear():
+    from xuanpolicy_amd.policies import FastLinear
+    torch.manual_seed(1)
+    for (n_in, n_out) in [(17, 256), (256, 256), (256, 6), (256, 1)]:
+        lin = FastLinear(n_in, n_out).to(DEV)
+        ref = torch.nn.Linear(n_in, n_out).to(DEV)
+        ref.load_state_dict(lin.state_dict())
+        x = torch.randn(65536, n_in, device=DEV, requires_grad=True)
+        gy = torch.randn(65536, n_out, device=DEV)
+        lin(x).backward(gy)
+        gx = x.grad.clone()
+        x.grad = None
+        ref(x).backward(gy)
+        np.testing.assert_allclose(_h(gx), _h(x.grad), rtol=1e-5, atol=1e-5)
+        # fp32 sums over K = 65536 in a different order: compare relative to the gradient's scale
+        for a, b in ((lin.weight.grad, ref.weight.grad), (lin.bias.grad, ref.bias.grad)):
+            a, b = _h(a).astype(np.float64), _h(b).astype(np.float64)
+            assert np.abs(a - b).max() <= 2e-5 * np.abs(b).max(), (np.abs(a - b).max(), np.abs(b).max())

@@ -6,41 +6,16 @@ xuance/common/statistic_tools.py:16, is never enabled).  Here env shards partiti
 only collective is ONE all-reduce (average) of the flat fp32 gradient per minibatch, before
 clip_grad_norm_, so the clipped norm is the global one.
 
-FlatGrads makes every parameter's .grad a view into one contiguous buffer, so autograd accumulates
-straight into it and the all-reduce is a single RCCL call over xGMI (latency-bound at 0.04-1 MiB;
-one bucket, no overlap needed).  Backend "nccl" is RCCL on ROCm; "gloo" is used by the CPU tests.
+FlatState (xuanpolicy_amd.flat) makes every parameter's .grad a view into one contiguous buffer, so
+autograd accumulates straight into it and the all-reduce is a single RCCL call over xGMI
+(latency-bound at 0.04-1 MiB; one bucket, no overlap needed).  Backend "nccl" is RCCL on ROCm; "gloo" is used by the CPU tests.
 """
 import os
 
 import torch
 import torch.distributed as dist
 
-
-class FlatGrads:
-    """Owns a flat gradient buffer; params' .grad are views into it (kept across zero_grad)."""
-
-    def __init__(self, params):
-        self.params = [p for p in params if p.requires_grad]
-        n = sum(p.numel() for p in self.params)
-        dev = self.params[0].device
-        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
-        off = 0
-        for p in self.params:
-            p.grad = self.flat[off:off + p.numel()].view_as(p)
-            off += p.numel()
-
-    def zero_(self):
-        self.flat.zero_()
-
-    def ensure_views(self):
-        off = 0
-        for p in self.params:
-            if p.grad is None or p.grad.data_ptr() != self.flat[off:].data_ptr():
-                g = p.grad
-                p.grad = self.flat[off:off + p.numel()].view_as(p)
-                if g is not None:
-                    p.grad.copy_(g)
-            off += p.numel()
+from .flat import FlatState, FusedClipAdam, fused_adam_compatible
 
 
 class GradAllReduce:
@@ -63,13 +38,17 @@ class GradAllReduce:
         self.calls += 1
 
 
-def attach_flat_grads(learner, allreduce=True, group=None):
-    """Give a learner flat gradients (and the all-reduce hook when a process group is initialised)."""
-    fg = FlatGrads(learner.policy.parameters())
-    learner.flat_grads = fg
+def attach_flat_grads(learner, allreduce=True, group=None, fused_optimizer=True):
+    """Give a learner flat parameters/gradients, the fused clip+Adam step when its optimizer allows,
+    and the all-reduce hook when a process group of more than one rank is initialised."""
+    fs = FlatState(learner.policy.parameters())
+    learner.flat_grads = fs
+    learner._params = fs.params
+    if fused_optimizer and fused_adam_compatible(learner.optimizer):
+        learner.fused_opt = FusedClipAdam(learner.optimizer, fs)
     if allreduce and dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        learner.grad_sync = GradAllReduce(fg, group)
-    return fg
+        learner.grad_sync = GradAllReduce(fs, group)
+    return fs
 
 
 def broadcast_parameters(module, src=0, group=None):

@@ -1,0 +1,103 @@
+"""Flat parameter / gradient / optimizer-state buffers for the learner's hot path.
+
+Every parameter of the policy becomes a view into one contiguous fp32 buffer, and so does its .grad
+(autograd accumulates straight into the views).  That gives:
+  * one RCCL all-reduce per minibatch over the whole gradient (xuanpolicy_amd.distributed);
+  * one fused clip_grad_norm_ + Adam launch pair over all parameters (xpa_clip_adam_step), replacing
+    torch's per-tensor multi_tensor_apply kernels (ppoclip_learner.py:47-49 semantics, see optim.hip).
+The torch.optim.Adam object handed in by the runner (runner_drl.py:71) stays the source of truth for
+hyper-parameters (lr as stepped by LinearLR, betas, eps) and its .state holds views of the flat moment
+buffers, so optimizer.state_dict() / load_state_dict() keep working.
+"""
+import torch
+
+from . import _lib, ops
+
+
+class FlatState:
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.numel = n
+        self.param = torch.empty(n, dtype=torch.float32, device=dev)
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)  # gradients
+        off = 0
+        with torch.no_grad():
+            for p in self.params:
+                k = p.numel()
+                self.param[off:off + k].copy_(p.detach().reshape(-1))
+                p.data = self.param[off:off + k].view_as(p)
+                p.grad = self.flat[off:off + k].view_as(p)
+                off += k
+
+    def zero_(self):
+        self.flat.zero_()
+
+    def ensure_views(self):
+        """Re-point .grad at the flat buffer if anything replaced it (e.g. zero_grad(set_to_none=True))."""
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            view = self.flat[off:off + k]
+            if p.grad is None or p.grad.data_ptr() != view.data_ptr():
+                g = p.grad
+                p.grad = view.view_as(p)
+                if g is None:
+                    p.grad.zero_()
+                else:
+                    p.grad.copy_(g)
+            off += k
+
+
+def fused_adam_compatible(optimizer):
+    if type(optimizer) is not torch.optim.Adam or len(optimizer.param_groups) != 1:
+        return False
+    g = optimizer.param_groups[0]
+    return (not g.get("amsgrad", False) and not g.get("maximize", False) and g.get("weight_decay", 0) == 0
+            and not g.get("differentiable", False))
+
+
+class FusedClipAdam:
+    """clip_grad_norm_(max_norm) + Adam.step() as two HIP launches over a FlatState."""
+
+    def __init__(self, optimizer, flat: FlatState):
+        if not fused_adam_compatible(optimizer):
+            raise ValueError("FusedClipAdam needs torch.optim.Adam with one param group, no weight decay/amsgrad")
+        group_params = set(id(p) for p in optimizer.param_groups[0]["params"])
+        if group_params != set(id(p) for p in flat.params):
+            raise ValueError("optimizer parameters differ from the flat state's parameters")
+        self.optimizer, self.fs = optimizer, flat
+        dev, n = flat.param.device, flat.numel
+        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.partials = torch.empty(int(ops.lib().xpa_grad_norm_num_partials(n)), dtype=torch.float64, device=dev)
+        self.total_norm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.step_count = 0
+        self._step_t = torch.zeros((), dtype=torch.float32)  # shared CPU 'step' like torch's Adam state
+        off = 0
+        for p in flat.params:
+            k = p.numel()
+            st = optimizer.state.get(p, {})
+            if "exp_avg" in st:  # migrate existing state
+                self.exp_avg[off:off + k].copy_(st["exp_avg"].reshape(-1))
+                self.exp_avg_sq[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+                self.step_count = int(float(st["step"]))
+            optimizer.state[p] = {"step": self._step_t, "exp_avg": self.exp_avg[off:off + k].view_as(p),
+                                  "exp_avg_sq": self.exp_avg_sq[off:off + k].view_as(p)}
+            off += k
+        self._step_t.fill_(float(self.step_count))
+
+    def step(self, max_norm):
+        g = self.optimizer.param_groups[0]
+        self.step_count += 1
+        b1, b2 = g["betas"]
+        lr = g["lr"]
+        lr = float(lr) if not isinstance(lr, torch.Tensor) else float(lr.item())
+        rc = ops.lib().xpa_clip_adam_step(ops._p(self.fs.param), ops._p(self.fs.flat), ops._p(self.exp_avg),
+                                          ops._p(self.exp_avg_sq), self.fs.numel, ops._p(self.partials),
+                                          float(max_norm) if max_norm else 0.0, lr, float(b1), float(b2),
+                                          float(g["eps"]), self.step_count, ops._p(self.total_norm),
+                                          ops._stream(self.fs.param.device))
+        _lib.check(rc, "xpa_clip_adam_step")
+        self._step_t.fill_(float(self.step_count))

@@ -77,9 +77,13 @@ class _FusedPolicyGradient(Learner):
         torch.autograd.backward(tensors, grads)
         if self.grad_sync is not None:
             self.grad_sync(self._params)
-        if self._use_clip:
-            torch.nn.utils.clip_grad_norm_(self._params, self._max_norm)
-        self.optimizer.step()
+        fused = getattr(self, "fused_opt", None)
+        if fused is not None:
+            fused.step(self._max_norm if self._use_clip else 0.0)  # xpa_clip_adam_step (K9)
+        else:
+            if self._use_clip:
+                torch.nn.utils.clip_grad_norm_(self._params, self._max_norm)
+            self.optimizer.step()
         if self.scheduler is not None:
             self.scheduler.step()
 
@@ -96,6 +100,13 @@ class _FusedPolicyGradient(Learner):
                                                ent_coef=self.ent_coef, ws=self._ws)
         self._backward_and_step(head, logstd, v, dh, dls, dv)
         return scalars
+
+    def enable_fast_path(self, fused_optimizer=True):
+        """Flat parameters/gradients and the fused clip+Adam kernel (xuanpolicy_amd.flat)."""
+        from .distributed import attach_flat_grads
+        if getattr(self, "flat_grads", None) is None:
+            attach_flat_grads(self, allreduce=True, fused_optimizer=fused_optimizer)
+        return self
 
     def _info(self, scalars):
         s = scalars.detach().cpu().tolist()

@@ -37,10 +37,62 @@ def space_shape(space):
     return tuple(space.shape)
 
 
+def _splitk_splits(batch, n_out, n_in):
+    """Split count for the weight-gradient GEMM dW = dY^T X with K = batch.  hipBLASLt runs these
+    long-K, small-M*N shapes without split-K (~32 workgroups on a 256-CU chip: 39 TF/s at 256x256,
+    <3 TF/s at 256x17, measured r01); a batched GEMM over S slices of K + a sum fills the chip
+    (S chosen so S x tiles >= ~512 workgroups, 32x64 tiles)."""
+    tiles = max(1, -(-n_out // 32)) * max(1, -(-n_in // 64))
+    s = 1
+    while s * tiles < 512 and s < 64:
+        s *= 2
+    while s > 1 and (batch % s or batch // s < 512):
+        s //= 2
+    return s
+
+
+class _SplitKLinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return torch.nn.functional.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = gy.mm(w)
+        if ctx.needs_input_grad[1]:
+            B, n_out, n_in = x.shape[0], w.shape[0], w.shape[1]
+            s = _splitk_splits(B, n_out, n_in)
+            if s > 1:
+                gyc, xc = gy.contiguous(), x.contiguous()
+                gw = torch.bmm(gyc.view(s, B // s, n_out).transpose(1, 2), xc.view(s, B // s, n_in)).sum(0)
+            else:
+                gw = gy.t().mm(x)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gy.sum(0)
+        return gx, gw, gb
+
+
+class FastLinear(nn.Linear):
+    """nn.Linear (same parameters and state_dict) whose backward computes the weight gradient of
+    large batches as a split-K batched GEMM (see _splitk_splits)."""
+
+    min_batch = 8192
+
+    def forward(self, x):
+        if x.dim() == 2 and x.shape[0] >= self.min_batch and torch.is_grad_enabled() and x.is_cuda:
+            return _SplitKLinearFn.apply(x, self.weight, self.bias)
+        return torch.nn.functional.linear(x, self.weight, self.bias)
+
+
 def mlp_block(input_dim, output_dim, normalize=None, activation=None, initialize=None, device=None):
     """Linear -> activation -> normalize (layers.py:8-24)."""
     block = []
-    linear = nn.Linear(input_dim, output_dim, device=device)
+    linear = FastLinear(input_dim, output_dim, device=device)
     if initialize is not None:
         initialize(linear.weight)
         nn.init.constant_(linear.bias, 0)

@@ -78,7 +78,10 @@ def build_agent(config, device=None, envs=None, shard=0):
     optimizer = torch.optim.Adam(policy.parameters(), config.learning_rate, eps=1e-5, **opt_kw)
     scheduler = torch.optim.lr_scheduler.LinearLR(optimizer, start_factor=1.0, end_factor=0.0,
                                                   total_iters=config.running_steps)
-    return agents.REGISTRY[config.agent](config, envs, policy, optimizer, scheduler, device)
+    agent = agents.REGISTRY[config.agent](config, envs, policy, optimizer, scheduler, device)
+    if getattr(config, "fast_path", True) and device.type == "cuda":
+        agent.learner.enable_fast_path(fused_optimizer=getattr(config, "fused_adam", True))
+    return agent
 
 
 def build_synthbox_ppo(n_envs=4096, n_steps=128, obs_dim=17, act_dim=6, hidden=256, n_epoch=16, n_minibatch=8,
