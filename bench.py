@@ -130,11 +130,11 @@ def main():
     import torch
     import torch.distributed as dist
     from xuanpolicy_amd import ops
-    from xuanpolicy_amd.distributed import broadcast_parameters, init_from_env
+    from xuanpolicy_amd.distributed import broadcast_parameters, init_from_env, local_device
     from xuanpolicy_amd.runner import build_synthbox_ppo
 
     rank, local, world = init_from_env()
-    device = torch.device("cuda", local)
+    device = local_device(local)
     torch.cuda.set_device(device)
     N, T = args.n_envs, args.horizon
     agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=args.obs_dim, act_dim=args.act_dim, hidden=args.hidden,

@@ -105,14 +105,15 @@ int xpa_policy_loss_finalize(int algo, int dist, int64_t batch, int64_t act_dim,
 
 /* K5 — RunningMeanStd over observations (xuance/common/statistic_tools.py:63-112) and observation
  * normalisation (xuance/torch/agents/agent.py:104-116).
- * xpa_rms_partials: per-block (mean, M2) in f64 over x[n, dim] (row stride ld floats).
- * xpa_rms_merge: Chan merge of the partials into the batch moments, then update_from_moments into
- * mean/var (f32 [dim]) and *count (f64) — one block.
+ * xpa_rms_partials: per-block f64 sums of (x - shift) and (x - shift)^2 over x[n, dim] (row stride
+ * ld floats); shift must be the `mean` array later passed to xpa_rms_merge (the running mean).
+ * xpa_rms_merge: batch moments from the partials, then update_from_moments into mean/var
+ * (f32 [dim]) and *count (f64) — one block.
  * xpa_obs_normalize: out = clip((x - mean) / (sqrt(var) + 1e-8), -clip_range, clip_range);
  * also copied to col_out + cursor->ptr*dim (row stride col_ld) when col_out != NULL. */
 int64_t xpa_rms_num_partials(int64_t n);
-int xpa_rms_partials(const float *x, int64_t n, int64_t dim, int64_t ld, double *partials,
-                     xpa_stream_t stream);
+int xpa_rms_partials(const float *x, int64_t n, int64_t dim, int64_t ld, const float *shift,
+                     double *partials, xpa_stream_t stream);
 int xpa_rms_merge(const double *partials, int64_t n_partials, int64_t n, int64_t dim, float *mean,
                   float *var, double *count, xpa_stream_t stream);
 int xpa_obs_normalize(const float *x, int64_t n, int64_t dim, int64_t ldx, const float *mean,

@@ -43,7 +43,7 @@ def test_abi_version_and_size_helpers(lib):
     assert lib.xpa_loss_num_partials(65536) == 256
     assert lib.xpa_loss_partial_width(6) == 11
     assert lib.xpa_gather_num_partials(65537) == 257
-    assert lib.xpa_rms_num_partials(4096) == 64
+    assert lib.xpa_rms_num_partials(4096) == 16
 
 
 def test_invalid_arguments_rejected_before_launch(lib):

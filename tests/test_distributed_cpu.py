@@ -1,0 +1,88 @@
+"""Data-parallel path on CPU with the gloo backend (world_size 2): the flat-gradient all-reduce used per
+minibatch (one collective), parameter broadcast at start-up, and torchrun-style initialisation."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _net(seed):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Linear(5, 16), torch.nn.LeakyReLU(), torch.nn.Linear(16, 3))
+
+
+def _data(rank):
+    g = torch.Generator().manual_seed(100 + rank)
+    return torch.randn(32, 5, generator=g), torch.randn(32, 3, generator=g)
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    try:
+        from xuanpolicy_amd.distributed import GradAllReduce, broadcast_parameters, init_from_env
+        from xuanpolicy_amd.flat import FlatState
+        r, local, w = init_from_env(backend="gloo")
+        assert (r, w) == (rank, world) and dist.get_backend() == "gloo"
+        net = _net(seed=rank)           # ranks start different ...
+        broadcast_parameters(net)       # ... and leave identical (rank 0's weights)
+        ref0 = _net(seed=0)
+        for a, b in zip(net.parameters(), ref0.parameters()):
+            assert torch.equal(a, b)
+        fs = FlatState(net.parameters())
+        ar = GradAllReduce(fs)
+        x, y = _data(rank)
+        fs.zero_()
+        ((net(x) - y) ** 2).mean().backward()
+        ar(fs.params)
+        assert ar.calls == 1
+        # expected: mean over ranks of each rank's local gradient
+        exp = []
+        for rr in range(world):
+            m = _net(seed=0)
+            xx, yy = _data(rr)
+            ((m(xx) - yy) ** 2).mean().backward()
+            exp.append(torch.cat([p.grad.reshape(-1) for p in m.parameters()]))
+        exp = torch.stack(exp).mean(0)
+        torch.testing.assert_close(fs.flat, exp, rtol=1e-6, atol=1e-7)
+        # the .grad views still alias the flat buffer after the collective
+        off = 0
+        for p in fs.params:
+            assert p.grad.data_ptr() == fs.flat[off:].data_ptr()
+            off += p.numel()
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_flat_grad_allreduce_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=110) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+    assert res == {0: "ok", 1: "ok"}, res
+
+
+def test_init_from_env_single_process_is_noop(monkeypatch):
+    from xuanpolicy_amd.distributed import init_from_env
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    assert init_from_env() == (0, 0, 1)
+    assert not dist.is_initialized()

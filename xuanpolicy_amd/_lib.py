@@ -36,7 +36,7 @@ SIGNATURES = {
     "xpa_policy_loss_finalize": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_f32, c_f32,
                                                 c_p, c_p, c_p]),
     "xpa_rms_num_partials": (c_i64, [c_i64]),
-    "xpa_rms_partials": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_p, c_p]),
+    "xpa_rms_partials": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
     "xpa_rms_merge": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p]),
     "xpa_obs_normalize": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_f32, c_p, c_i64, c_p, c_i64, c_p, c_p]),
     "xpa_rollout_sample": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_u32, c_f32, c_p, c_p,

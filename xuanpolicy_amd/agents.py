@@ -108,6 +108,9 @@ class _OnPolicyAgent:
         self.timers = {"rollout": 0.0, "update": 0.0}
         self._t = 0
         self._host_obs = None
+        self.use_graph = bool(_cfg(config, "cuda_graph", True)) and self.device.type == "cuda"
+        self._graph = None
+        self._graph_pool = None
 
     def _make_learner(self, config, policy, optimizer, scheduler):
         raise NotImplementedError
@@ -160,6 +163,26 @@ class _OnPolicyAgent:
         self._sample_into_buffer()
         env.step_device()
         self._post(env.rew, env.term, env.trunc, env.final_obs)
+
+    def _rollout_step_graph(self):
+        """The device env step captured once into a hipGraph and replayed: every per-step argument
+        (buffer column, RNG step) lives in the device cursor, so the same graph serves all steps."""
+        key = tuple(p.data_ptr() for p in self.policy.parameters())
+        if self._graph is not None and key != self._graph_key:
+            self._graph = None  # parameters were re-homed (e.g. flat buffers attached): re-capture
+        if self._graph is None:
+            self._graph_key = key
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):
+                self._rollout_step_device()        # a real step (also warms up BLAS handles)
+            torch.cuda.current_stream(self.device).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self._graph_pool):
+                self._rollout_step_device()        # recorded, not executed
+            self._graph = g
+            return
+        self._graph.replay()
 
     def _rollout_step_host(self):
         """Same kernels around a host VecEnv (numpy in/out, reset_obs in infos)."""
@@ -231,7 +254,10 @@ class _OnPolicyAgent:
 
     # ---- public API (ppoclip_agent.py:59-111) -------------------------------------------------------------
     def train(self, train_steps, log=True):
-        step_fn = self._rollout_step_device if self.device_env else self._rollout_step_host
+        if not self.device_env:
+            step_fn = self._rollout_step_host
+        else:
+            step_fn = self._rollout_step_graph if self.use_graph else self._rollout_step_device
         for _ in range(train_steps):
             t0 = time.perf_counter()
             step_fn()

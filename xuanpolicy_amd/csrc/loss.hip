@@ -54,7 +54,7 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
     __shared__ float s_scale[kMaxAct], s_logscale[kMaxAct], s_var[kMaxAct];
     __shared__ float s_ent;
     __shared__ float s_mean, s_inv;
-    __shared__ float s_red[kLossWaves];
+    __shared__ float s_red[(kPartBase + kMaxAct) * kLossWaves];
 
     const int tid = threadIdx.x;
     if (DIST == XPA_DIST_GAUSSIAN) {
@@ -159,14 +159,20 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
             }
         }
     }
-    float *prow = partials + (int64_t)blockIdx.x * width;
-    float t0 = xpa_block_sum(surr, s_red, kLossWaves);
-    float t1 = xpa_block_sum(sq, s_red, kLossWaves);
-    float t2 = xpa_block_sum(ent, s_red, kLossWaves);
-    float t3 = xpa_block_sum(clipc, s_red, kLossWaves);
-    float t4 = xpa_block_sum(vv, s_red, kLossWaves);
-    if (tid == 0) {
-        prow[0] = t0; prow[1] = t1; prow[2] = t2; prow[3] = t3; prow[4] = t4;
+    // Block partial sums: every value is wave-reduced by shuffles into its own LDS slot row, then ONE
+    // barrier and a fixed-order sum over the waves (deterministic, no per-value barriers).
+    const int w = tid >> 6;
+    const bool lane0 = (tid & 63) == 0;
+    {
+        const float r0 = xpa_wave_sum(surr), r1 = xpa_wave_sum(sq), r2 = xpa_wave_sum(ent);
+        const float r3 = xpa_wave_sum(clipc), r4 = xpa_wave_sum(vv);
+        if (lane0) {
+            s_red[0 * kLossWaves + w] = r0;
+            s_red[1 * kLossWaves + w] = r1;
+            s_red[2 * kLossWaves + w] = r2;
+            s_red[3 * kLossWaves + w] = r3;
+            s_red[4 * kLossWaves + w] = r4;
+        }
     }
     if (DIST == XPA_DIST_GAUSSIAN) {
         const float *mu = head + b * A;
@@ -177,9 +183,18 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
                 const float diff = x[a] - mu[a];
                 g = dlogp * (diff * diff / s_var[a] - 1.0f);
             }
-            const float tg = xpa_block_sum(g, s_red, kLossWaves);
-            if (tid == 0) prow[kPartBase + a] = tg;
+            g = xpa_wave_sum(g);
+            if (lane0) s_red[(kPartBase + a) * kLossWaves + w] = g;
         }
+    }
+    __syncthreads();
+    const int nvals = kPartBase + (DIST == XPA_DIST_GAUSSIAN ? A : 0);
+    float *prow = partials + (int64_t)blockIdx.x * width;
+    for (int j = tid; j < nvals; j += kLossThreads) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < kLossWaves; ++k) s += s_red[j * kLossWaves + k];
+        prow[j] = s;
     }
 }
 
@@ -188,16 +203,19 @@ __global__ __launch_bounds__(256) void policy_loss_finalize_kernel(int algo, int
                                                                    int64_t n_partials, int width, float vf_coef,
                                                                    float ent_coef, float *__restrict__ scalars,
                                                                    float *__restrict__ d_logstd) {
-    __shared__ double s_red[4];
+    __shared__ double tot[kPartBase];
     const int ncols = kPartBase + (dist == XPA_DIST_GAUSSIAN ? A : 0);
-    double tot[kPartBase];
-    for (int j = 0; j < ncols; ++j) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int j = w; j < ncols; j += 4) {  // one wave per column, fixed lane order -> deterministic
         double s = 0.0;
-        for (int64_t k = threadIdx.x; k < n_partials; k += 256) s += (double)partials[k * width + j];
-        s = xpa_block_sum(s, s_red, 4);
-        if (j < kPartBase) tot[j] = s;
-        else if (threadIdx.x == 0) d_logstd[j - kPartBase] = (float)(s - (double)ent_coef);
+        for (int64_t k = lane; k < n_partials; k += 64) s += (double)partials[k * width + j];
+        s = xpa_wave_sum(s);
+        if (lane == 0) {
+            if (j < kPartBase) tot[j] = s;
+            else d_logstd[j - kPartBase] = (float)(s - (double)ent_coef);
+        }
     }
+    __syncthreads();
     if (threadIdx.x == 0) {
         const double B = (double)batch;
         const double actor = -tot[0] / B;

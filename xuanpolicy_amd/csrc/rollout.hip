@@ -11,7 +11,7 @@
 namespace {
 
 constexpr int kGatherRows = 256;  // rows per gather block == rows per adv partial
-constexpr int kRmsRows = 64;      // rows per RMS partial block
+constexpr int kRmsRows = 256;     // rows per RMS partial block
 constexpr uint32_t kSaltAct = 0xAC7105EDu;
 constexpr uint32_t kSaltReset = 0x5EED0000u;  // oracle/synth_env.py SALT_RESET
 
@@ -24,19 +24,26 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const int64_t *__restr
                                                           V *__restrict__ dst, const float *__restrict__ adv,
                                                           double *__restrict__ adv_partials) {
     __shared__ double s_red[4];
+    __shared__ int64_t s_src[kGatherRows];
     const int64_t r0 = (int64_t)blockIdx.x * kGatherRows;
     const int64_t r1 = r0 + kGatherRows < batch ? r0 + kGatherRows : batch;
-    const int64_t n = (r1 - r0) * row_vecs;
-    for (int64_t e = threadIdx.x; e < n; e += 256) {
-        const int64_t r = r0 + e / row_vecs;
-        const int64_t c = e % row_vecs;
-        const int64_t sr = idx[r];
-        dst[r * row_vecs + c] = (sr >= 0 && sr < n_rows) ? src[sr * row_vecs + c] : V{};
+    const int nr = (int)(r1 - r0);
+    if ((int)threadIdx.x < nr) s_src[threadIdx.x] = idx[r0 + threadIdx.x];
+    __syncthreads();
+    // Consecutive lanes copy consecutive vectors of a row (32-bit index math; the row's source offset
+    // comes from LDS), so each row is one contiguous burst.
+    const uint32_t rv = (uint32_t)row_vecs;
+    const uint32_t n = (uint32_t)nr * rv;
+    V *out = dst + r0 * row_vecs;
+    for (uint32_t e = threadIdx.x; e < n; e += 256) {
+        const uint32_t r = e / rv;
+        const uint32_t c = e - r * rv;
+        const int64_t sr = s_src[r];
+        out[e] = (sr >= 0 && sr < n_rows) ? src[sr * row_vecs + c] : V{};
     }
     if (adv_partials) {
         double s = 0.0, q = 0.0;
-        const int64_t r = r0 + threadIdx.x;
-        const int64_t sr = r < r1 ? idx[r] : -1;
+        const int64_t sr = (int)threadIdx.x < nr ? s_src[threadIdx.x] : -1;
         if (sr >= 0 && sr < n_rows) {
             const double a = (double)adv[sr];
             s = a;
@@ -54,47 +61,65 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const int64_t *__restr
 // ---------------------------------------------------------------------------------------------
 // K5 RunningMeanStd
 // ---------------------------------------------------------------------------------------------
-// One thread per column, kRmsRows rows per block: Welford in f64 -> (mean, M2) per (block, column).
+// Block g sums rows [g*kRmsRows, (g+1)*kRmsRows) of (x - shift) and (x - shift)^2 in f64 per column
+// (shift = the running mean, so the one-pass variance does not cancel).  Threads cover a
+// (row group x column) tile, all row loads of a thread are independent (no serial latency chain),
+// and the row groups are combined through LDS in a fixed order.
 __global__ __launch_bounds__(256) void rms_partials_kernel(const float *__restrict__ x, int64_t n, int64_t dim,
-                                                           int64_t ld, double *__restrict__ part) {
+                                                           int64_t ld, const float *__restrict__ shift,
+                                                           double *__restrict__ part) {
+    __shared__ double s_sum[256], s_sq[256];
     const int64_t r0 = (int64_t)blockIdx.x * kRmsRows;
     const int64_t r1 = r0 + kRmsRows < n ? r0 + kRmsRows : n;
     const int64_t np = gridDim.x;
-    for (int64_t d = (int64_t)blockIdx.y * blockDim.x + threadIdx.x; d < dim; d += (int64_t)gridDim.y * blockDim.x) {
-        double mean = 0.0, m2 = 0.0;
-        int k = 0;
-        for (int64_t r = r0; r < r1; ++r) {
-            const double xv = (double)x[r * ld + d];
-            ++k;
-            const double delta = xv - mean;
-            mean += delta / k;
-            m2 += delta * (xv - mean);
+    for (int64_t c0 = 0; c0 < dim; c0 += 256) {
+        const int dc = (int)(dim - c0 < 256 ? dim - c0 : 256);  // columns in this tile
+        const int groups = 256 / dc;                            // row groups
+        const int c = threadIdx.x % dc, gsub = threadIdx.x / dc;
+        double s = 0.0, q = 0.0;
+        if (gsub < groups) {
+            const float sh = shift ? shift[c0 + c] : 0.f;
+#pragma unroll 4
+            for (int64_t r = r0 + gsub; r < r1; r += groups) {
+                const double v = (double)x[r * ld + c0 + c] - (double)sh;
+                s += v;
+                q += v * v;
+            }
         }
-        part[(int64_t)blockIdx.x * dim + d] = mean;
-        part[(np + blockIdx.x) * dim + d] = m2;
+        s_sum[threadIdx.x] = s;
+        s_sq[threadIdx.x] = q;
+        __syncthreads();
+        if ((int)threadIdx.x < dc) {
+            double ts = 0.0, tq = 0.0;
+            for (int k = 0; k < groups; ++k) {
+                ts += s_sum[k * dc + threadIdx.x];
+                tq += s_sq[k * dc + threadIdx.x];
+            }
+            part[(int64_t)blockIdx.x * dim + c0 + threadIdx.x] = ts;
+            part[(np + blockIdx.x) * dim + c0 + threadIdx.x] = tq;
+        }
+        __syncthreads();
     }
 }
 
-// Chan merge of the partials (fixed order) then update_from_moments (statistic_tools.py:86-112).
+// Sum of the partials (fixed order) -> batch mean/var, then update_from_moments
+// (statistic_tools.py:86-112) into mean/var (f32) and count (f64).  mean doubles as the shift the
+// partials were taken around.
 __global__ __launch_bounds__(256) void rms_merge_kernel(const double *__restrict__ part, int64_t np, int64_t n,
                                                         int64_t dim, float *__restrict__ mean, float *__restrict__ var,
                                                         double *__restrict__ count) {
     const double c0 = *count;
     __syncthreads();
     for (int64_t d = threadIdx.x; d < dim; d += blockDim.x) {
-        double bm = 0.0, bm2 = 0.0, bn = 0.0;
+        double s = 0.0, q = 0.0;
         for (int64_t p = 0; p < np; ++p) {
-            const double nb = (double)((p + 1) * kRmsRows < n ? kRmsRows : n - p * kRmsRows);
-            const double pm = part[p * dim + d];
-            const double pm2 = part[(np + p) * dim + d];
-            const double tot = bn + nb;
-            const double delta = pm - bm;
-            bm += delta * nb / tot;
-            bm2 += pm2 + delta * delta * bn * nb / tot;
-            bn = tot;
+            s += part[p * dim + d];
+            q += part[(np + p) * dim + d];
         }
-        const double bvar = bm2 / (double)n;  // np.std(x, axis=0)**2 (ddof 0)
+        const double ms = s / (double)n;
         const double m0 = (double)mean[d], v0 = (double)var[d];
+        const double bm = m0 + ms;                               // batch mean
+        const double bvar = fmax(q / (double)n - ms * ms, 0.0);  // np.std(x, axis=0)**2 (ddof 0)
         const double tot = c0 + (double)n;
         const double delta = bm - m0;
         const double new_mean = m0 + delta * (double)n / tot;
@@ -263,25 +288,42 @@ __global__ __launch_bounds__(1024) void rollout_post_kernel(
     const float rstd = fminf(fmaxf(sqrtf(*ret_var), 0.1f), 100.0f);
     const bool last = (t == (int32_t)(T - 1));
     double cnt = 0.0, sum = 0.0, sumsq = 0.0;
-    for (int64_t n = threadIdx.x; n < n_envs; n += blockDim.x) {
-        const float r = rew[n];
-        const bool te = term[n] != 0, tr = trunc[n] != 0;
-        const int64_t cell = n * T + t;
-        buf_rew[cell] = use_rewnorm ? fminf(fmaxf(r / rstd, -rew_range), rew_range) : r;
-        buf_term[cell] = te ? 1.f : 0.f;
-        const bool done = te || tr;
-        const bool close = last || (done && !(atari_lifeloss && !tr));
-        buf_closed[cell] = close ? 1 : 0;
-        buf_boot[cell] = close ? (te ? 0.f : v_boot[n]) : 0.f;
-        float R = returns[n];
-        R = mask_returns ? (te ? 0.f : gamma * R) + r : gamma * R + r;
-        if (done) {
-            cnt += 1.0;
-            sum += (double)R;
-            sumsq += (double)R * (double)R;
-            R = 0.f;
+    constexpr int U = 4;  // envs per thread per pass, all loads issued before use
+    const int64_t stride = (int64_t)blockDim.x;
+    for (int64_t base = threadIdx.x; base < n_envs; base += stride * U) {
+        float r[U], vb[U], R[U];
+        uint8_t te8[U], tr8[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int64_t n = base + k * stride;
+            const bool ok = n < n_envs;
+            r[k] = ok ? rew[n] : 0.f;
+            vb[k] = ok ? v_boot[n] : 0.f;
+            R[k] = ok ? returns[n] : 0.f;
+            te8[k] = ok ? term[n] : 0;
+            tr8[k] = ok ? trunc[n] : 0;
         }
-        returns[n] = R;
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int64_t n = base + k * stride;
+            if (n >= n_envs) continue;
+            const bool te = te8[k] != 0, tr = tr8[k] != 0;
+            const int64_t cell = n * T + t;
+            buf_rew[cell] = use_rewnorm ? fminf(fmaxf(r[k] / rstd, -rew_range), rew_range) : r[k];
+            buf_term[cell] = te ? 1.f : 0.f;
+            const bool done = te || tr;
+            const bool close = last || (done && !(atari_lifeloss && !tr));
+            buf_closed[cell] = close ? 1 : 0;
+            buf_boot[cell] = close ? (te ? 0.f : vb[k]) : 0.f;
+            float Rk = mask_returns ? (te ? 0.f : gamma * R[k]) + r[k] : gamma * R[k] + r[k];
+            if (done) {
+                cnt += 1.0;
+                sum += (double)Rk;
+                sumsq += (double)Rk * (double)Rk;
+                Rk = 0.f;
+            }
+            returns[n] = Rk;
+        }
     }
     const int nw = blockDim.x >> 6;
     cnt = xpa_block_sum(cnt, s_red, nw);
@@ -332,14 +374,12 @@ XPA_API int xpa_gather_minibatch(const int64_t *idx, int64_t batch, int64_t n_ro
 // ---- K5 --------------------------------------------------------------------------------------------
 XPA_API int64_t xpa_rms_num_partials(int64_t n) { return (n + kRmsRows - 1) / kRmsRows; }
 
-XPA_API int xpa_rms_partials(const float *x, int64_t n, int64_t dim, int64_t ld, double *partials,
-                             xpa_stream_t stream) {
+XPA_API int xpa_rms_partials(const float *x, int64_t n, int64_t dim, int64_t ld, const float *shift,
+                             double *partials, xpa_stream_t stream) {
     if (n <= 0 || dim <= 0 || ld < dim || !x || !partials) return (int)hipErrorInvalidValue;
     const int64_t np = xpa_rms_num_partials(n);
-    const int threads = dim >= 256 ? 256 : (int)((dim + 63) / 64 * 64);
-    const int64_t ycols = (dim + threads - 1) / threads;
-    hipLaunchKernelGGL(rms_partials_kernel, dim3((unsigned)np, (unsigned)(ycols < 65535 ? ycols : 65535)),
-                       dim3(threads), 0, (hipStream_t)stream, x, n, dim, ld, partials);
+    hipLaunchKernelGGL(rms_partials_kernel, dim3((unsigned)np), dim3(256), 0, (hipStream_t)stream, x, n, dim, ld,
+                       shift, partials);
     return xpa_launch_status();
 }
 

@@ -65,9 +65,17 @@ def init_from_env(backend=None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
+        backend = backend or os.environ.get("XPA_DIST_BACKEND")  # e.g. gloo for a 1-GPU rehearsal
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = "nccl" if torch.cuda.device_count() > 0 else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend, rank=rank, world_size=world)
     return rank, local, world
+
+
+def local_device(local_rank):
+    """cuda:<local_rank>, wrapped onto the visible devices (several ranks may share one GPU in a
+    gloo rehearsal; with RCCL every rank has its own GPU)."""
+    n = torch.cuda.device_count()
+    return torch.device("cuda", local_rank % n) if n else torch.device("cpu")

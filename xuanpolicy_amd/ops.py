@@ -227,7 +227,7 @@ def rms_update(x, mean, var, count, partials=None):
     else:
         _req(partials, "partials", torch.float64, (2 * np_, dim))
     s = _stream(x.device)
-    _lib.check(lib().xpa_rms_partials(_p(x), n, dim, ld, _p(partials), s), "xpa_rms_partials")
+    _lib.check(lib().xpa_rms_partials(_p(x), n, dim, ld, _p(mean), _p(partials), s), "xpa_rms_partials")
     _lib.check(lib().xpa_rms_merge(_p(partials), np_, n, dim, _p(mean), _p(var), _p(count), s), "xpa_rms_merge")
 
 
