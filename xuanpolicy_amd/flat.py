@@ -101,3 +101,4 @@ class FusedClipAdam:
                                           ops._stream(self.fs.param.device))
         _lib.check(rc, "xpa_clip_adam_step")
         self._step_t.fill_(float(self.step_count))
+        self.optimizer._opt_called = True  # the LR scheduler checks that an optimizer step happened
