@@ -169,6 +169,30 @@ int xpa_clip_adam_step(float *param, float *grad, float *exp_avg, float *exp_avg
                        double *norm_partials, float max_norm, float lr, float beta1, float beta2, float eps,
                        int64_t step, float *total_norm_out, xpa_stream_t stream);
 
+/* K10 — activation backward fused with bias-gradient column sums for one MLP layer (row-major
+ * [rows, cols]).  Replaces the activation backward and the bias-gradient reduction torch autograd runs
+ * per mlp_block (xuance/torch/utils/layers.py:8-24) inside loss.backward() (ppoclip_learner.py:46).
+ * act: 0 = identity (column sums of dh only; dz unused), 1 = LeakyReLU/ReLU (mask from the activation
+ * output h, slope), 2 = tanh (1 - h^2).  dz = dh * act'(h) (dz may alias dh; NULL = do not store);
+ * partials: xpa_act_bwd_num_partials(rows) x cols floats; xpa_colsum_finalize sums them in a fixed
+ * order into out[cols] (the bias gradient). */
+int64_t xpa_act_bwd_num_partials(int64_t rows);
+int xpa_act_bwd_colsum(int act, const float *dh, const float *h, int64_t rows, int64_t cols, float slope,
+                       float *dz, float *partials, xpa_stream_t stream);
+int xpa_colsum_finalize(const float *partials, int64_t n_partials, int64_t cols, float *out,
+                        xpa_stream_t stream);
+
+/* K11 — backward of a thin output layer (k <= 32 outputs, weight w [k, hidden], no activation) fused
+ * with the activation backward of the hidden layer feeding it (output h [rows, hidden]): the tail
+ * of the actor / critic heads (gaussian.py:8-51, categorical.py:16-58).  Given d_head [rows, k]
+ * (row stride ldd): dz = (d_head w) * act'(h) [rows, hidden]; per-block partials of
+ * dW = d_head^T h (xpa_head_bwd_num_partials(rows) x k x hidden), of the hidden bias gradient (x hidden)
+ * and of the output bias gradient (x k; NULL = skip); reduce each with xpa_colsum_finalize. */
+int64_t xpa_head_bwd_num_partials(int64_t rows);
+int xpa_head_backward(int act, int64_t k, const float *d_head, int64_t ldd, const float *h, const float *w,
+                      int64_t rows, int64_t hidden, float slope, float *dz, float *partial_dw,
+                      float *partial_db_hidden, float *partial_db_out, xpa_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

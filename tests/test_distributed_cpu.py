@@ -53,12 +53,12 @@ def _worker(rank, world, port, q):
             ((m(xx) - yy) ** 2).mean().backward()
             exp.append(torch.cat([p.grad.reshape(-1) for p in m.parameters()]))
         exp = torch.stack(exp).mean(0)
-        torch.testing.assert_close(fs.flat, exp, rtol=1e-6, atol=1e-7)
-        # the .grad views still alias the flat buffer after the collective
-        off = 0
-        for p in fs.params:
-            assert p.grad.data_ptr() == fs.flat[off:].data_ptr()
-            off += p.numel()
+        got = torch.cat([p.grad.reshape(-1) for p in fs.params])
+        torch.testing.assert_close(got, exp, rtol=1e-6, atol=1e-7)
+        # the .grad views still alias the (256-B aligned, zero-padded) flat buffer after the collective
+        for p, off in zip(fs.params, fs.offsets):
+            assert p.grad.data_ptr() == fs.flat[off:].data_ptr() and off % 64 == 0
+        assert float(fs.flat.abs().sum()) == float(got.abs().sum())  # padding stays zero
         q.put((rank, "ok"))
     except Exception as e:  # pragma: no cover - reported to the parent
         q.put((rank, repr(e)))

@@ -1,0 +1,337 @@
+// K10 — activation backward fused with the bias-gradient column sums of an MLP layer (gfx950).
+//
+// Replaces, in the learner's backward through the actor-critic (PPOCLIP_Learner.update's
+// loss.backward(), xuance/torch/learners/policy_gradient/ppoclip_learner.py:46, through the
+// mlp_block Linear -> activation layers of xuance/torch/utils/layers.py:8-24), the two torch passes
+// over each [B, C] hidden activation: the activation backward (dz = dh * act'(h)) and the bias
+// gradient reduction (db = sum_b dz).  One pass reads dh and h, writes dz (may alias dh) and per-block
+// column partial sums; xpa_colsum_finalize reduces the partials (fixed order) into db.
+// act: 0 = identity (output layers: only the column sums), 1 = LeakyReLU/ReLU with `slope`
+// (the mask is taken from the activation OUTPUT h: h > 0 <=> z > 0 for slope >= 0), 2 = tanh (1 - h^2).
+// HBM-bound: 12 B per element (dh, h read; dz written) + C*4 B per 256 rows of partials.
+#include "xpa_common.h"
+
+namespace {
+
+constexpr int kRowsPerBlock = 64;  // 1024 blocks at B = 65 536: ~4 blocks per CU to hide HBM latency
+
+template <int ACT>
+__device__ __forceinline__ float act_grad(float dh, float h, float slope) {
+    if (ACT == 1) return h > 0.f ? dh : dh * slope;
+    if (ACT == 2) return dh * (1.0f - h * h);
+    return dh;
+}
+
+// C % 4 == 0: each thread owns 4 consecutive columns of its row group (16-B accesses).
+// dh and dz may alias (in-place): no __restrict__ on them.
+template <int ACT>
+__global__ __launch_bounds__(256) void act_bwd_colsum_vec4(const float *dh, const float *__restrict__ h, int64_t B,
+                                                           int C, float slope, float *dz,
+                                                           float *__restrict__ partials) {
+    extern __shared__ __attribute__((aligned(16))) float4 s_acc[];  // [groups][C/4]
+    const int cq = C / 4;                                            // <= 256 (checked by the launcher)
+    const int groups = 256 / cq;
+    const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock;
+    const int64_t r1 = r0 + kRowsPerBlock < B ? r0 + kRowsPerBlock : B;
+    const int c4 = threadIdx.x % cq, g = threadIdx.x / cq;
+    if (g < groups) {
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+        for (int64_t r = r0 + g; r < r1; r += groups) {
+            const int64_t off = r * C + 4 * c4;
+            float4 d = *reinterpret_cast<const float4 *>(dh + off);
+            if (ACT != 0) {
+                const float4 hv = *reinterpret_cast<const float4 *>(h + off);
+                d.x = act_grad<ACT>(d.x, hv.x, slope);
+                d.y = act_grad<ACT>(d.y, hv.y, slope);
+                d.z = act_grad<ACT>(d.z, hv.z, slope);
+                d.w = act_grad<ACT>(d.w, hv.w, slope);
+                if (dz) *reinterpret_cast<float4 *>(dz + off) = d;
+            }
+            acc.x += d.x; acc.y += d.y; acc.z += d.z; acc.w += d.w;
+        }
+        s_acc[g * cq + c4] = acc;
+    }
+    __syncthreads();
+    for (int c4 = threadIdx.x; c4 < cq; c4 += 256) {
+        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int g = 0; g < groups; ++g) {
+            const float4 a = s_acc[g * cq + c4];
+            t.x += a.x; t.y += a.y; t.z += a.z; t.w += a.w;
+        }
+        *reinterpret_cast<float4 *>(partials + (int64_t)blockIdx.x * C + 4 * c4) = t;
+    }
+}
+
+// Generic C (e.g. 1 value column, 6 action logits): threads over (row group, column), LDS combine.
+template <int ACT>
+__global__ __launch_bounds__(256) void act_bwd_colsum_scalar(const float *dh, const float *__restrict__ h, int64_t B,
+                                                             int C, float slope, float *dz,
+                                                             float *__restrict__ partials) {
+    __shared__ float s_acc[256];
+    const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock;
+    const int64_t r1 = r0 + kRowsPerBlock < B ? r0 + kRowsPerBlock : B;
+    for (int cbase = 0; cbase < C; cbase += 256) {
+        const int dc = C - cbase < 256 ? C - cbase : 256;
+        const int groups = 256 / dc;
+        const int c = threadIdx.x % dc, g = threadIdx.x / dc;
+        float acc = 0.f;
+        if (g < groups) {
+#pragma unroll 4
+            for (int64_t r = r0 + g; r < r1; r += groups) {
+                const int64_t off = r * C + cbase + c;
+                float d = dh[off];
+                if (ACT != 0) {
+                    d = act_grad<ACT>(d, h[off], slope);
+                    if (dz) dz[off] = d;
+                }
+                acc += d;
+            }
+        }
+        s_acc[threadIdx.x] = acc;
+        __syncthreads();
+        if ((int)threadIdx.x < dc) {
+            float t = 0.f;
+            for (int k = 0; k < groups; ++k) t += s_acc[k * dc + threadIdx.x];
+            partials[(int64_t)blockIdx.x * C + cbase + threadIdx.x] = t;
+        }
+        __syncthreads();
+    }
+}
+
+// K11: backward of a thin output layer (K outputs, no activation) and the activation of the hidden
+// layer that feeds it, in one pass.  Thread = hidden column i, block = kHeadRows rows:
+//   dh[b,i]  = sum_o d_head[b,o] W[o,i]           (the output layer's dX)
+//   dz[b,i]  = dh[b,i] * act'(h[b,i])               (hidden activation backward)
+//   dW[o,i] += d_head[b,o] h[b,i];  db_h[i] += dz[b,i];  db_o[o] += d_head[b,o]
+// W's column and the K accumulators live in registers (KMAX compile-time, K <= KMAX runtime);
+// d_head rows are staged in LDS.  Per-block partials are reduced by xpa_colsum_finalize.
+constexpr int kHeadRows = 128;
+
+template <int KMAX, int ACT>
+__global__ __launch_bounds__(256) void head_backward_kernel(int K, const float *__restrict__ d_head, int64_t ldd,
+                                                            const float *__restrict__ h, const float *__restrict__ W,
+                                                            int64_t B, int H, float slope, float *__restrict__ dz,
+                                                            float *__restrict__ p_dw, float *__restrict__ p_dbh,
+                                                            float *__restrict__ p_dbo) {
+    __shared__ float s_dh[kHeadRows * KMAX];
+    const int64_t r0 = (int64_t)blockIdx.x * kHeadRows;
+    const int nr = (int)(B - r0 < kHeadRows ? B - r0 : kHeadRows);
+    for (int e = threadIdx.x; e < nr * K; e += 256) {
+        const int r = e / K, o = e - r * K;
+        s_dh[r * KMAX + o] = d_head[(r0 + r) * ldd + o];
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < K && p_dbo) {  // output-layer bias gradient partial
+        float s = 0.f;
+        for (int r = 0; r < nr; ++r) s += s_dh[r * KMAX + threadIdx.x];
+        p_dbo[(int64_t)blockIdx.x * K + threadIdx.x] = s;
+    }
+    for (int i = threadIdx.x; i < H; i += 256) {
+        float w[KMAX], acc[KMAX];
+#pragma unroll
+        for (int o = 0; o < KMAX; ++o) {
+            w[o] = o < K ? W[(int64_t)o * H + i] : 0.f;
+            acc[o] = 0.f;
+        }
+        float dbh = 0.f;
+#pragma unroll 4
+        for (int r = 0; r < nr; ++r) {
+            const int64_t off = (r0 + r) * H + i;
+            const float hv = h[off];
+            float d = 0.f;
+#pragma unroll
+            for (int o = 0; o < KMAX; ++o) {
+                if (o < K) {
+                    const float g = s_dh[r * KMAX + o];
+                    d += g * w[o];
+                    acc[o] += g * hv;
+                }
+            }
+            d = act_grad<ACT>(d, hv, slope);
+            dz[off] = d;
+            dbh += d;
+        }
+#pragma unroll
+        for (int o = 0; o < KMAX; ++o)
+            if (o < K) p_dw[((int64_t)blockIdx.x * K + o) * H + i] = acc[o];
+        p_dbh[(int64_t)blockIdx.x * H + i] = dbh;
+    }
+}
+
+// Same computation with 16-B accesses for K <= KMAX <= 8 and hidden % 4 == 0, hidden / 4 <= 256:
+// a thread owns 4 consecutive columns of one of (256 / (hidden/4)) row groups, the groups' partial
+// accumulators are combined through LDS in a fixed order.
+template <int KMAX, int ACT>
+__global__ __launch_bounds__(256) void head_backward_vec4_kernel(int K, const float *__restrict__ d_head, int64_t ldd,
+                                                                 const float *__restrict__ h,
+                                                                 const float *__restrict__ W, int64_t B, int H,
+                                                                 float slope, float *__restrict__ dz,
+                                                                 float *__restrict__ p_dw, float *__restrict__ p_dbh,
+                                                                 float *__restrict__ p_dbo) {
+    __shared__ float s_dh[kHeadRows * KMAX];
+    __shared__ __attribute__((aligned(16))) float4 s_red[256];
+    const int64_t r0 = (int64_t)blockIdx.x * kHeadRows;
+    const int nr = (int)(B - r0 < kHeadRows ? B - r0 : kHeadRows);
+    for (int e = threadIdx.x; e < nr * K; e += 256) {
+        const int r = e / K, o = e - r * K;
+        s_dh[r * KMAX + o] = d_head[(r0 + r) * ldd + o];
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < K && p_dbo) {
+        float s = 0.f;
+        for (int r = 0; r < nr; ++r) s += s_dh[r * KMAX + threadIdx.x];
+        p_dbo[(int64_t)blockIdx.x * K + threadIdx.x] = s;
+    }
+    const int cq = H / 4, groups = 256 / cq;
+    const int c4 = threadIdx.x % cq, grp = threadIdx.x / cq;
+    float4 w[KMAX], acc[KMAX];
+#pragma unroll
+    for (int o = 0; o < KMAX; ++o) {
+        w[o] = o < K ? *reinterpret_cast<const float4 *>(W + (int64_t)o * H + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        acc[o] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float4 dbh = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (grp < groups) {
+#pragma unroll 8
+        for (int r = grp; r < nr; r += groups) {
+            const int64_t off = (r0 + r) * H + 4 * c4;
+            const float4 hv = *reinterpret_cast<const float4 *>(h + off);
+            float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int o = 0; o < KMAX; ++o) {
+                if (o < K) {
+                    const float g = s_dh[r * KMAX + o];
+                    d.x += g * w[o].x; d.y += g * w[o].y; d.z += g * w[o].z; d.w += g * w[o].w;
+                    acc[o].x += g * hv.x; acc[o].y += g * hv.y; acc[o].z += g * hv.z; acc[o].w += g * hv.w;
+                }
+            }
+            d.x = act_grad<ACT>(d.x, hv.x, slope);
+            d.y = act_grad<ACT>(d.y, hv.y, slope);
+            d.z = act_grad<ACT>(d.z, hv.z, slope);
+            d.w = act_grad<ACT>(d.w, hv.w, slope);
+            *reinterpret_cast<float4 *>(dz + off) = d;
+            dbh.x += d.x; dbh.y += d.y; dbh.z += d.z; dbh.w += d.w;
+        }
+    }
+    // Combine the row groups: one LDS round per accumulator (fixed group order).
+    auto combine = [&](float4 v, float *dst) {
+        s_red[threadIdx.x] = v;
+        __syncthreads();
+        if (grp == 0) {
+            float4 t = s_red[c4];
+            for (int g2 = 1; g2 < groups; ++g2) {
+                const float4 a = s_red[g2 * cq + c4];
+                t.x += a.x; t.y += a.y; t.z += a.z; t.w += a.w;
+            }
+            *reinterpret_cast<float4 *>(dst + 4 * c4) = t;
+        }
+        __syncthreads();
+    };
+#pragma unroll
+    for (int o = 0; o < KMAX; ++o)
+        if (o < K) combine(acc[o], p_dw + ((int64_t)blockIdx.x * K + o) * H);
+    combine(dbh, p_dbh + (int64_t)blockIdx.x * H);
+}
+
+__global__ __launch_bounds__(256) void colsum_finalize_kernel(const float *__restrict__ partials, int64_t G, int C,
+                                                              float *__restrict__ out) {
+    // one wave per column, lanes over partial rows, fixed order -> deterministic
+    const int w = (blockIdx.x * 256 + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+    if (w >= C) return;
+    double s = 0.0;
+    for (int64_t k = lane; k < G; k += 64) s += (double)partials[k * C + w];
+    s = xpa_wave_sum(s);
+    if (lane == 0) out[w] = (float)s;
+}
+
+}  // namespace
+
+XPA_API int64_t xpa_act_bwd_num_partials(int64_t rows) { return (rows + kRowsPerBlock - 1) / kRowsPerBlock; }
+
+XPA_API int xpa_act_bwd_colsum(int act, const float *dh, const float *h, int64_t rows, int64_t cols, float slope,
+                               float *dz, float *partials, xpa_stream_t stream) {
+    if (rows <= 0 || cols <= 0 || cols > (1 << 20) || !dh || !partials || act < 0 || act > 2)
+        return (int)hipErrorInvalidValue;
+    if (act != 0 && !h) return (int)hipErrorInvalidValue;
+    const int64_t G = xpa_act_bwd_num_partials(rows);
+    const int C = (int)cols;
+    hipStream_t s = (hipStream_t)stream;
+    const bool vec = (C % 4 == 0) && (C / 4 <= 256) &&
+                     (((uintptr_t)dh | (uintptr_t)(h ? h : dh) | (uintptr_t)(dz ? dz : dh) | (uintptr_t)partials) % 16 == 0);
+    if (vec) {
+        const int cq = C / 4;
+        const int groups = 256 / cq;
+        const size_t lds = (size_t)groups * cq * sizeof(float4);
+#define XPA_ACT_LAUNCH(A_)                                                                                        \
+    hipLaunchKernelGGL((act_bwd_colsum_vec4<A_>), dim3((unsigned)G), dim3(256), lds, s, dh, h, rows, C, slope, dz, \
+                       partials)
+        if (act == 0) XPA_ACT_LAUNCH(0);
+        else if (act == 1) XPA_ACT_LAUNCH(1);
+        else XPA_ACT_LAUNCH(2);
+#undef XPA_ACT_LAUNCH
+    } else {
+#define XPA_ACT_LAUNCH(A_)                                                                                          \
+    hipLaunchKernelGGL((act_bwd_colsum_scalar<A_>), dim3((unsigned)G), dim3(256), 0, s, dh, h, rows, C, slope, dz, \
+                       partials)
+        if (act == 0) XPA_ACT_LAUNCH(0);
+        else if (act == 1) XPA_ACT_LAUNCH(1);
+        else XPA_ACT_LAUNCH(2);
+#undef XPA_ACT_LAUNCH
+    }
+    return xpa_launch_status();
+}
+
+XPA_API int64_t xpa_head_bwd_num_partials(int64_t rows) { return (rows + kHeadRows - 1) / kHeadRows; }
+
+XPA_API int xpa_head_backward(int act, int64_t k, const float *d_head, int64_t ldd, const float *h, const float *w,
+                              int64_t rows, int64_t hidden, float slope, float *dz, float *partial_dw,
+                              float *partial_db_hidden, float *partial_db_out, xpa_stream_t stream) {
+    if (rows <= 0 || hidden <= 0 || k <= 0 || k > 32 || ldd < k || act < 0 || act > 2 || !d_head || !h || !w ||
+        !dz || !partial_dw || !partial_db_hidden)
+        return (int)hipErrorInvalidValue;
+    const unsigned G = (unsigned)xpa_head_bwd_num_partials(rows);
+    hipStream_t s = (hipStream_t)stream;
+    const int K = (int)k, H = (int)hidden;
+#define XPA_HEAD_LAUNCH(KM_, A_)                                                                                    \
+    hipLaunchKernelGGL((head_backward_kernel<KM_, A_>), dim3(G), dim3(256), 0, s, K, d_head, ldd, h, w, rows, H,   \
+                       slope, dz, partial_dw, partial_db_hidden, partial_db_out)
+#define XPA_HEAD_ACT(KM_)                 \
+    do {                                  \
+        if (act == 0) XPA_HEAD_LAUNCH(KM_, 0); \
+        else if (act == 1) XPA_HEAD_LAUNCH(KM_, 1); \
+        else XPA_HEAD_LAUNCH(KM_, 2);     \
+    } while (0)
+    const bool vec = (H % 4 == 0) && (H / 4 <= 256) && K <= 8 &&
+                     (((uintptr_t)h | (uintptr_t)w | (uintptr_t)dz | (uintptr_t)partial_dw | (uintptr_t)partial_db_hidden) %
+                      16 == 0);
+    if (vec) {
+#undef XPA_HEAD_LAUNCH
+#define XPA_HEAD_LAUNCH(KM_, A_)                                                                                     \
+    hipLaunchKernelGGL((head_backward_vec4_kernel<KM_, A_>), dim3(G), dim3(256), 0, s, K, d_head, ldd, h, w, rows, H, \
+                       slope, dz, partial_dw, partial_db_hidden, partial_db_out)
+        if (K == 1) XPA_HEAD_ACT(1);
+        else if (K <= 2) XPA_HEAD_ACT(2);
+        else XPA_HEAD_ACT(8);
+    } else {
+#undef XPA_HEAD_LAUNCH
+#define XPA_HEAD_LAUNCH(KM_, A_)                                                                                    \
+    hipLaunchKernelGGL((head_backward_kernel<KM_, A_>), dim3(G), dim3(256), 0, s, K, d_head, ldd, h, w, rows, H,   \
+                       slope, dz, partial_dw, partial_db_hidden, partial_db_out)
+        if (K == 1) XPA_HEAD_ACT(1);
+        else if (K <= 8) XPA_HEAD_ACT(8);
+        else XPA_HEAD_ACT(32);
+    }
+#undef XPA_HEAD_ACT
+#undef XPA_HEAD_LAUNCH
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_colsum_finalize(const float *partials, int64_t n_partials, int64_t cols, float *out,
+                                xpa_stream_t stream) {
+    if (n_partials <= 0 || cols <= 0 || !partials || !out) return (int)hipErrorInvalidValue;
+    const unsigned blocks = (unsigned)((cols * 64 + 255) / 256);
+    hipLaunchKernelGGL(colsum_finalize_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, partials, n_partials,
+                       (int)cols, out);
+    return xpa_launch_status();
+}

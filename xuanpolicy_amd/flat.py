@@ -14,30 +14,40 @@ import torch
 from . import _lib, ops
 
 
+ALIGN = 64  # floats: every segment starts on a 256-B boundary (16-B vector kernels on the views)
+
+
+def _aligned(n):
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
 class FlatState:
     def __init__(self, params):
         self.params = [p for p in params if p.requires_grad]
-        n = sum(p.numel() for p in self.params)
+        self.offsets = []
+        off = 0
+        for p in self.params:
+            self.offsets.append(off)
+            off += _aligned(p.numel())
+        n = off
         dev = self.params[0].device
         self.numel = n
-        self.param = torch.empty(n, dtype=torch.float32, device=dev)
+        # padding between segments stays zero in param, grad and Adam moments (zero grad -> zero step)
+        self.param = torch.zeros(n, dtype=torch.float32, device=dev)
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)  # gradients
-        off = 0
         with torch.no_grad():
-            for p in self.params:
+            for p, off in zip(self.params, self.offsets):
                 k = p.numel()
                 self.param[off:off + k].copy_(p.detach().reshape(-1))
                 p.data = self.param[off:off + k].view_as(p)
                 p.grad = self.flat[off:off + k].view_as(p)
-                off += k
 
     def zero_(self):
         self.flat.zero_()
 
     def ensure_views(self):
         """Re-point .grad at the flat buffer if anything replaced it (e.g. zero_grad(set_to_none=True))."""
-        off = 0
-        for p in self.params:
+        for p, off in zip(self.params, self.offsets):
             k = p.numel()
             view = self.flat[off:off + k]
             if p.grad is None or p.grad.data_ptr() != view.data_ptr():
@@ -47,7 +57,6 @@ class FlatState:
                     p.grad.zero_()
                 else:
                     p.grad.copy_(g)
-            off += k
 
 
 def fused_adam_compatible(optimizer):
@@ -75,8 +84,7 @@ class FusedClipAdam:
         self.total_norm = torch.zeros(1, dtype=torch.float32, device=dev)
         self.step_count = 0
         self._step_t = torch.zeros((), dtype=torch.float32)  # shared CPU 'step' like torch's Adam state
-        off = 0
-        for p in flat.params:
+        for p, off in zip(flat.params, flat.offsets):
             k = p.numel()
             st = optimizer.state.get(p, {})
             if "exp_avg" in st:  # migrate existing state
@@ -85,7 +93,6 @@ class FusedClipAdam:
                 self.step_count = int(float(st["step"]))
             optimizer.state[p] = {"step": self._step_t, "exp_avg": self.exp_avg[off:off + k].view_as(p),
                                   "exp_avg_sq": self.exp_avg_sq[off:off + k].view_as(p)}
-            off += k
         self._step_t.fill_(float(self.step_count))
 
     def step(self, max_norm):

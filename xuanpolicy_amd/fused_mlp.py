@@ -1,0 +1,189 @@
+"""Explicit forward/backward of the actor-critic MLP for the learner's hot path (no autograd graph).
+
+Reference network: representation Basic_MLP -> ActorNet (mu or logits) and CriticNet, each a chain of
+mlp_block = Linear -> activation (xuance/torch/representations/mlp.py:21-51,
+xuance/torch/policies/gaussian.py:8-51, categorical.py:16-58, xuance/torch/utils/layers.py:8-24).
+PPOCLIP_Learner.update runs loss.backward() through it (ppoclip_learner.py:46); here the loss kernel
+(K2) hands d loss/d head and d loss/d v straight to this backward, which writes every parameter
+gradient into the flat gradient buffer (flat.FlatState) with:
+  * hipBLASLt GEMMs for dX (the trunk's two heads accumulate with one addmm: no separate add pass);
+  * split-K batched GEMMs for dW = dZ^T X written with sum(out=grad view) (see policies._splitk_splits);
+  * K10 xpa_act_bwd_colsum: activation backward + bias-gradient column sums in one pass over [B, H]
+    (output layers: column sums only), xpa_colsum_finalize into the bias-gradient views.
+Forward: F.linear (GEMM + bias epilogue) then the activation in place; the activation OUTPUTS are
+kept (LeakyReLU/ReLU/tanh derivatives are functions of the output), no pre-activation copies.
+Every parameter gradient is overwritten each update, so no zeroing pass is needed.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib, ops
+from .policies import Basic_Identical, Basic_MLP, _splitk_splits
+
+
+def _act_code(m):
+    if m is None:
+        return 0, 0.0
+    if isinstance(m, nn.LeakyReLU):
+        return 1, float(m.negative_slope)
+    if isinstance(m, nn.ReLU):
+        return 1, 0.0
+    if isinstance(m, nn.Tanh):
+        return 2, 0.0
+    raise ValueError("unsupported activation %r" % type(m).__name__)
+
+
+def _parse(seq):
+    mods = list(seq)
+    layers, i = [], 0
+    while i < len(mods):
+        lin = mods[i]
+        if not isinstance(lin, nn.Linear) or lin.bias is None:
+            raise ValueError("expected Linear with bias, got %r" % type(lin).__name__)
+        act = None
+        if i + 1 < len(mods) and not isinstance(mods[i + 1], nn.Linear):
+            act = mods[i + 1]
+            i += 2
+        else:
+            i += 1
+        layers.append((lin,) + _act_code(act))
+    return layers
+
+
+class FusedActorCritic:
+    """Built from a Gaussian/Categorical actor-critic policy whose parameters live in a FlatState."""
+
+    def __init__(self, policy):
+        rep = policy.representation
+        if isinstance(rep, Basic_MLP):
+            self.rep = _parse(rep.model)
+        elif isinstance(rep, Basic_Identical):
+            self.rep = []
+        else:
+            raise ValueError("representation %r has no explicit backward" % type(rep).__name__)
+        self.discrete = bool(getattr(policy, "discrete", False))
+        self.actor = _parse(policy.actor.model if self.discrete else policy.actor.mu)
+        self.critic = _parse(policy.critic.model)
+        self.logstd = None if self.discrete else policy.actor.logstd
+        self.use_head_kernel = True
+        n_params = sum(1 for _ in policy.parameters())
+        n_cov = 2 * (len(self.rep) + len(self.actor) + len(self.critic)) + (0 if self.discrete else 1)
+        if n_params != n_cov:
+            raise ValueError("policy has parameters outside the Linear chains")
+        self._partials = {}
+
+    # ------------------------------------------------------------------------------------------------
+    @staticmethod
+    def _chain_forward(layers, x):
+        outs = []
+        h = x
+        for lin, code, slope in layers:
+            h = F.linear(h, lin.weight, lin.bias)
+            if code == 1:
+                F.leaky_relu(h, slope, inplace=True)
+            elif code == 2:
+                h.tanh_()
+            outs.append(h)
+        return outs
+
+    @torch.no_grad()
+    def forward(self, x):
+        rep_outs = self._chain_forward(self.rep, x)
+        s = rep_outs[-1] if rep_outs else x
+        a_outs = self._chain_forward(self.actor, s)
+        c_outs = self._chain_forward(self.critic, s)
+        v = c_outs[-1][:, 0]
+        return a_outs[-1], self.logstd, v, (x, rep_outs, s, a_outs, c_outs)
+
+    # ------------------------------------------------------------------------------------------------
+    def _bias_grad(self, code, g, h, slope, out):
+        rows, cols = g.shape
+        key = (rows, cols)
+        part = self._partials.get(key)
+        if part is None:
+            part = torch.empty((int(ops.lib().xpa_act_bwd_num_partials(rows)), cols), dtype=torch.float32,
+                               device=g.device)
+            self._partials[key] = part
+        s = ops._stream(g.device)
+        L = ops.lib()
+        _lib.check(L.xpa_act_bwd_colsum(code, ops._p(g), ops._p(h) if code else None, rows, cols, slope,
+                                        ops._p(g) if code else None, ops._p(part), s), "xpa_act_bwd_colsum")
+        _lib.check(L.xpa_colsum_finalize(ops._p(part), part.shape[0], cols, ops._p(out), s), "xpa_colsum_finalize")
+
+    @staticmethod
+    def _weight_grad(dz, x, out):
+        B, n_out = dz.shape
+        n_in = x.shape[1]
+        s = _splitk_splits(B, n_out, n_in)
+        if s > 1:
+            torch.sum(torch.bmm(dz.view(s, B // s, n_out).transpose(1, 2), x.reshape(s, B // s, n_in)), dim=0, out=out)
+        else:
+            torch.mm(dz.t(), x, out=out)
+
+    def _head_tail(self, layers, outs, g):
+        """K11 for [hidden Linear + act] -> [output Linear, no act]: returns dz of the hidden layer."""
+        lin_o, code_o, _ = layers[-1]
+        lin_h, code_h, slope = layers[-2]
+        h = outs[-2]
+        B, H = h.shape
+        K = g.shape[1]
+        key = ("head", B, H, K)
+        ws = self._partials.get(key)
+        L = ops.lib()
+        if ws is None:
+            G = int(L.xpa_head_bwd_num_partials(B))
+            dev = g.device
+            ws = (torch.empty((G, K * H), device=dev), torch.empty((G, H), device=dev), torch.empty((G, K), device=dev),
+                  torch.empty((B, H), device=dev))
+            self._partials[key] = ws
+        p_dw, p_dbh, p_dbo, dz = ws
+        s = ops._stream(g.device)
+        _lib.check(L.xpa_head_backward(code_h, K, ops._p(g), g.stride(0), ops._p(h), ops._p(lin_o.weight), B, H, slope,
+                                       ops._p(dz), ops._p(p_dw), ops._p(p_dbh), ops._p(p_dbo), s), "xpa_head_backward")
+        G = p_dw.shape[0]
+        _lib.check(L.xpa_colsum_finalize(ops._p(p_dw), G, K * H, ops._p(lin_o.weight.grad), s), "colsum dW")
+        _lib.check(L.xpa_colsum_finalize(ops._p(p_dbh), G, H, ops._p(lin_h.bias.grad), s), "colsum db_h")
+        _lib.check(L.xpa_colsum_finalize(ops._p(p_dbo), G, K, ops._p(lin_o.bias.grad), s), "colsum db_o")
+        return dz
+
+    def _chain_backward(self, layers, inputs, outs, g, need_dx, accumulate=None):
+        """g: grad w.r.t. the chain's last output (contiguous [B, n_out]); returns grad w.r.t. its input
+        (added to `accumulate` through the GEMM's C operand when given)."""
+        top = len(layers) - 1
+        if (len(layers) >= 2 and layers[-1][1] == 0 and layers[-2][1] != 0 and g.shape[1] <= 32
+                and g.stride(1) == 1 and self.use_head_kernel):
+            g = self._head_tail(layers, outs, g)   # output layer + hidden activation done by K11
+            lin, _, _ = layers[-2]
+            self._weight_grad(g, inputs[-2], lin.weight.grad)
+            top = len(layers) - 2
+            if top > 0 or need_dx:
+                if top == 0 and accumulate is not None:
+                    g = accumulate.addmm_(g, lin.weight)
+                else:
+                    g = torch.mm(g, lin.weight)
+            top -= 1
+        for j in range(top, -1, -1):
+            lin, code, slope = layers[j]
+            h = outs[j]
+            x = inputs[j]
+            self._bias_grad(code, g, h, slope, lin.bias.grad)   # g <- g * act'(h) in place (code != 0)
+            self._weight_grad(g, x, lin.weight.grad)
+            if j > 0 or need_dx:
+                if j == 0 and accumulate is not None:
+                    g = accumulate.addmm_(g, lin.weight)   # C += g W in the GEMM (C aliases D: no copy)
+                else:
+                    g = torch.mm(g, lin.weight)
+        return g
+
+    @torch.no_grad()
+    def backward(self, ctx, d_head, d_v):
+        x, rep_outs, s, a_outs, c_outs = ctx
+        have_rep = len(self.rep) > 0
+        a_in = [s] + a_outs[:-1]
+        c_in = [s] + c_outs[:-1]
+        ds = self._chain_backward(self.actor, a_in, a_outs, d_head, need_dx=have_rep)
+        ds = self._chain_backward(self.critic, c_in, c_outs, d_v.view(-1, 1), need_dx=have_rep, accumulate=ds)
+        if have_rep:
+            r_in = [x] + rep_outs[:-1]
+            self._chain_backward(self.rep, r_in, rep_outs, ds, need_dx=False)

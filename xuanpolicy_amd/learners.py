@@ -75,6 +75,21 @@ class _FusedPolicyGradient(Learner):
             tensors.append(logstd)
             grads.append(d_logstd)
         torch.autograd.backward(tensors, grads)
+        self._sync_clip_step()
+
+    def _fused_mlp(self):
+        """Explicit actor-critic backward (fused_mlp.FusedActorCritic) once gradients live in flat views."""
+        fm = getattr(self, "_fm", None)
+        if fm is None and getattr(self, "flat_grads", None) is not None and getattr(self, "fused_mlp_enabled", True):
+            from .fused_mlp import FusedActorCritic
+            try:
+                fm = FusedActorCritic(self.policy)
+            except ValueError:
+                fm = False
+            self._fm = fm
+        return fm or None
+
+    def _sync_clip_step(self):
         if self.grad_sync is not None:
             self.grad_sync(self._params)
         fused = getattr(self, "fused_opt", None)
@@ -91,6 +106,19 @@ class _FusedPolicyGradient(Learner):
         """One minibatch update reading act/adv/ret/old_logp from the flattened rollout buffer at idx
         (idx=None: already gathered).  Returns the device tensor of loss scalars (ops.OUT_KEYS)."""
         self.iterations += 1
+        fm = self._fused_mlp()
+        if fm is not None:
+            head, logstd, v, ctx = fm.forward(obs)
+            if self._ws is None or self._ws.batch != head.shape[0]:
+                self._ws = ops.LossWorkspace(head.shape[0], head.shape[1], head.device, self.dist)
+            scalars, dh, _, dv = ops.policy_loss(self.algo, self.dist, head, logstd, v, act, adv, ret,
+                                                 old_logp=old_logp, idx=idx, adv_partials=adv_partials,
+                                                 clip_range=self.clip_range, vf_coef=self.vf_coef,
+                                                 ent_coef=self.ent_coef, ws=self._ws,
+                                                 d_logstd_out=logstd.grad if logstd is not None else None)
+            fm.backward(ctx, dh, dv)       # writes every parameter gradient into the flat buffer
+            self._sync_clip_step()
+            return scalars
         head, logstd, v = policy_heads(self.policy, obs)
         if self._ws is None or self._ws.batch != head.shape[0]:
             self._ws = ops.LossWorkspace(head.shape[0], head.shape[1], head.device, self.dist)

@@ -156,7 +156,7 @@ class LossWorkspace:
 
 
 def policy_loss(algo, dist, head, logstd, v, act, adv, ret, old_logp=None, idx=None, adv_partials=None,
-                clip_range=0.2, vf_coef=0.25, ent_coef=0.0, ws=None):
+                clip_range=0.2, vf_coef=0.25, ent_coef=0.0, ws=None, d_logstd_out=None):
     """K2 + finalize.  Returns (scalars[6] device tensor, d_head, d_logstd or None, d_v).
 
     head [B, A] float32; logstd [A] (gaussian); v [B].  act/old_logp/adv/ret are read at idx[b]
@@ -202,10 +202,14 @@ def policy_loss(algo, dist, head, logstd, v, act, adv, ret, old_logp=None, idx=N
                                    _p(ws.partials), s)
     TIMER.stop("loss", ev)
     _lib.check(rc, "xpa_policy_loss_fwd_bwd")
+    d_logstd = ws.d_logstd
+    if d_logstd_out is not None and dist == "gaussian":
+        _req(d_logstd_out, "d_logstd_out", torch.float32, (A,))
+        d_logstd = d_logstd_out
     rc = L.xpa_policy_loss_finalize(ALGO[algo], DIST[dist], B, A, _p(ws.partials), ws.partials.shape[0],
-                                    float(vf_coef), float(ent_coef), _p(ws.scalars), _p(ws.d_logstd), s)
+                                    float(vf_coef), float(ent_coef), _p(ws.scalars), _p(d_logstd), s)
     _lib.check(rc, "xpa_policy_loss_finalize")
-    return ws.scalars, ws.d_head, ws.d_logstd, ws.d_v
+    return ws.scalars, ws.d_head, d_logstd, ws.d_v
 
 
 # ------------------------------------------------------------------------------------------------

@@ -60,9 +60,28 @@ def make_envs(config, device=None, shard=0):
                               "with the reference's step contract to the agent directly" % config.env_name)
 
 
+TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning", "tunableop_results0.csv")
+
+
+def enable_tuned_gemms(path=TUNED_GEMMS):
+    """Use the committed TunableOp table (tools/tune_gemms.py: hipBLASLt/rocBLAS solutions measured on
+    MI355X for the update's GEMM shapes).  Lookup only (no tuning at run time); shapes not in the table
+    fall back to the default heuristics.  Returns True when the table was loaded."""
+    if not os.path.exists(path) or not torch.cuda.is_available():
+        return False
+    tun = torch.cuda.tunable
+    tun.enable(True)
+    tun.tuning_enable(False)
+    tun.read_file(path)
+    return True
+
+
 def build_agent(config, device=None, envs=None, shard=0):
     """runner_drl.py:15-75 for PPO_Clip / A2C."""
     device = torch.device(device if device is not None else config.device)
+    # Opt-in: the r01 table gave no end-to-end gain (123.0 vs 123.4 ms/iteration, tools/tune_gemms.py check).
+    if getattr(config, "tunableop", False) and device.type == "cuda":
+        enable_tuned_gemms()
     shard = getattr(config, "shard", shard)
     envs = envs if envs is not None else make_envs(config, device, shard)
     config.observation_space, config.action_space = envs.observation_space, envs.action_space
