@@ -193,6 +193,32 @@ int xpa_head_backward(int act, int64_t k, const float *d_head, int64_t ldd, cons
                       int64_t rows, int64_t hidden, float slope, float *dz, float *partial_dw,
                       float *partial_db_hidden, float *partial_db_out, xpa_stream_t stream);
 
+/* K12 — fused head: hidden activation + output Linear + loss + backward in one pass per head.
+ * Replaces, for a head [Linear(., 256) + act] -> [Linear(256, K)], the tail of the forward
+ * (gaussian.py:8-51 / categorical.py:16-58), the loss of PPOCLIP_Learner.update
+ * (ppoclip_learner.py:32-44) / A2C_Learner.update (a2c_learner.py:24-31) and autograd's backward down
+ * to the hidden pre-activation z [batch, 256] (ppoclip_learner.py:46).  Per-row inputs
+ * (act, old_logp, adv, ret) are read at idx[b] (idx NULL: at b) with the same adv normalisation,
+ * tie rules and invalid-index behaviour as xpa_policy_loss_fwd_bwd.  Outputs: dz [batch, 256]; per-block
+ * partials (xpa_head_fused_num_partials(batch) rows) of dW_out (x K*256), db_hidden (x 256) and db_out
+ * (x K) for xpa_colsum_finalize, and one loss-partials row per block in xpa_policy_loss_fwd_bwd's
+ * layout (width >= xpa_loss_partial_width(K)): the actor kernel fills the surrogate / entropy / clip /
+ * dlogstd columns, the critic kernel the squared-error / value columns, so one
+ * xpa_policy_loss_finalize over the shared array yields the loss scalars and d logstd.
+ * act: 0 identity, 1 LeakyReLU(slope) / ReLU (slope 0), 2 tanh.  K <= 8; hidden must be 256;
+ * z, w, dz and the dW / db_hidden partials 16-B aligned. */
+int64_t xpa_head_fused_num_partials(int64_t batch);
+int xpa_head_fused_actor(int algo, int dist, int act, int64_t batch, int64_t act_dim, int64_t hidden,
+                         const float *z, const float *w, const float *b, float slope, const float *logstd,
+                         const int64_t *idx, int64_t n_rows, const float *act_buf, const float *old_logp,
+                         const float *adv, const double *adv_partials, int64_t n_adv_partials, float clip_range,
+                         float ent_coef, float *dz, float *partial_dw, float *partial_db_hidden,
+                         float *partial_db_out, float *loss_partials, int64_t loss_width, xpa_stream_t stream);
+int xpa_head_fused_critic(int act, int64_t batch, int64_t hidden, const float *z, const float *w, const float *b,
+                          float slope, const int64_t *idx, int64_t n_rows, const float *ret, float vf_coef,
+                          float *dz, float *partial_dw, float *partial_db_hidden, float *partial_db_out,
+                          float *loss_partials, int64_t loss_width, xpa_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -89,3 +89,61 @@ def test_explicit_backward_matches_autograd(discrete, act, rep_hidden):
         ga, gb = a.grad.double(), b.grad.double()
         scale = ga.abs().max().item() + 1e-12
         assert (ga - gb).abs().max().item() <= 2e-5 * scale, (n1, (ga - gb).abs().max().item(), scale)
+
+
+@pytest.mark.parametrize("algo,discrete,act,rep_hidden,ent", [
+    ("ppo", False, torch.nn.LeakyReLU, [256], 0.0), ("ppo", True, torch.nn.LeakyReLU, [256], 0.01),
+    ("a2c", False, torch.nn.Tanh, [64], 0.005), ("a2c", True, torch.nn.ReLU, [], 0.01),
+    ("ppo", False, torch.nn.LeakyReLU, [], 0.0)])
+def test_fused_heads_match_loss_kernel_path(algo, discrete, act, rep_hidden, ent):
+    """K12 (heads + loss + head backward in one pass) == K2 loss kernel + explicit backward, which the
+    drop-in tests pin to the reference's fixtures: loss scalars and every parameter gradient."""
+    from xuanpolicy_amd import ops
+    from xuanpolicy_amd.flat import FlatState
+    from xuanpolicy_amd.fused_mlp import FusedActorCritic
+    torch.manual_seed(1)
+    D, A, B, R = 17, 6, 8192 + 37, 20000
+    p1 = _policy(D, A, discrete, act, rep_hidden)
+    p2 = _policy(D, A, discrete, act, rep_hidden)
+    p2.load_state_dict(p1.state_dict())
+    fs1, fs2 = FlatState(p1.parameters()), FlatState(p2.parameters())
+    fm1, fm2 = FusedActorCritic(p1), FusedActorCritic(p2)
+    assert fm2.fused_heads
+    obs_all = torch.randn(R, D, device=DEV)
+    idx = torch.randperm(R, device=DEV)[:B].contiguous()
+    idx[5] = R + 3          # invalid rows contribute nothing
+    idx[B - 1] = -1
+    adv = torch.randn(R, device=DEV)
+    ret = torch.randn(R, device=DEV)
+    if discrete:
+        act_buf = torch.randint(0, A, (R,), device=DEV).float()
+    else:
+        act_buf = torch.randn(R, A, device=DEV)
+    with torch.no_grad():
+        h0, _, _ = p1.heads(obs_all)
+        if discrete:
+            old = torch.distributions.Categorical(logits=h0).log_prob(act_buf.long())
+        else:
+            old = torch.distributions.Normal(h0, p1.actor.logstd.exp()).log_prob(act_buf).sum(-1)
+        old = (old + 0.05 * torch.randn(R, device=DEV)).contiguous()   # ratios on both sides of the clip
+    obs, part = ops.gather_minibatch(idx.clamp(0, R - 1), obs_all, adv=adv)
+    # both paths read the same adv-norm partials
+    dist = "categorical" if discrete else "gaussian"
+    kw = dict(old_logp=old if algo == "ppo" else None, idx=idx, adv_partials=part, clip_range=0.2, vf_coef=0.25,
+              ent_coef=ent)
+    fs1.flat.fill_(7.0)
+    fs2.flat.fill_(-7.0)
+    head, logstd, v, ctx = fm1.forward(obs)
+    s1, dh, _, dv = ops.policy_loss(algo, dist, head, logstd, v, act_buf, adv, ret,
+                                    d_logstd_out=logstd.grad if logstd is not None else None, **kw)
+    fm1.backward(ctx, dh, dv)
+    ctx2 = fm2.forward_hidden(obs)
+    s2 = fm2.loss_backward(ctx2, algo, dist, act_buf, adv, ret, **kw)
+    torch.cuda.synchronize()
+    a, b = s1.double().cpu(), s2.double().cpu()
+    assert torch.allclose(a, b, rtol=2e-5, atol=2e-6), (a, b)
+    for (n1, x1), (n2, x2) in zip(p1.named_parameters(), p2.named_parameters()):
+        ga, gb = x1.grad.double(), x2.grad.double()
+        scale = ga.abs().max().item() + 1e-12
+        assert (ga - gb).abs().max().item() <= 5e-5 * scale, (n1, (ga - gb).abs().max().item(), scale)
+        assert not bool((x2.grad == -7.0).any()), n2   # every gradient written

@@ -16,7 +16,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "libxuanpolicy_amd.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
-SOURCES = ["gae.hip", "loss.hip", "rollout.hip", "optim.hip", "mlp.hip"]
+SOURCES = ["gae.hip", "loss.hip", "rollout.hip", "optim.hip", "mlp.hip", "head.hip"]
 HEADER = os.path.join(REPO_DIR, "include", "xuanpolicy_amd.h")
 
 ABI_VERSION = 1
@@ -51,6 +51,12 @@ SIGNATURES = {
     "xpa_head_bwd_num_partials": (c_i64, [c_i64]),
     "xpa_head_backward": (ctypes.c_int, [ctypes.c_int, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_f32, c_p, c_p, c_p,
                                          c_p, c_p]),
+    "xpa_head_fused_num_partials": (c_i64, [c_i64]),
+    "xpa_head_fused_actor": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_p, c_p,
+                                            c_f32, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_f32, c_f32, c_p, c_p,
+                                            c_p, c_p, c_p, c_i64, c_p]),
+    "xpa_head_fused_critic": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_p, c_p, c_p, c_f32, c_p, c_i64, c_p, c_f32,
+                                             c_p, c_p, c_p, c_p, c_p, c_i64, c_p]),
     "xpa_grad_norm_num_partials": (c_i64, [c_i64]),
     "xpa_clip_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_p, c_f32, c_f32, c_f32, c_f32, c_f32, c_i64, c_p,
                                           c_p]),

@@ -1,0 +1,451 @@
+// K12 — fused actor / critic head: hidden activation + output layer + PPO-Clip / A2C loss + backward,
+// one pass per minibatch and head (gfx950).
+//
+// Replaces, for the MLP actor-critic (xuance/torch/policies/gaussian.py:8-51, categorical.py:16-58;
+// mlp_block xuance/torch/utils/layers.py:8-24), the tail of the forward (activation of the last hidden
+// layer, the output Linear), the loss of PPOCLIP_Learner.update / A2C_Learner.update
+// (ppoclip_learner.py:32-44, a2c_learner.py:24-31, distributions.py:39-101) and the backward down to the
+// hidden pre-activation (torch autograd in loss.backward(), ppoclip_learner.py:46).
+//
+// Outputs: dz [batch, 256]; per-block partials dW_o [K*256], db_h [256], db_o [K] (reduced by
+// xpa_colsum_finalize) and one row of the K2 loss-partials layout (surrogate, sq-err, entropy, clip
+// count, value sum, dlogstd[K]; reduced by xpa_policy_loss_finalize).  The actor launch fills the actor
+// columns, the critic launch the critic columns of the same partials array.
+// HBM: reads z (4 B/elem), writes dz (4 B/elem): 2 KiB per row at H = 256, plus the per-row inputs.
+#include "xpa_common.h"
+
+namespace {
+
+constexpr int kWaves = 4;
+constexpr int kH = 256;  // hidden width handled
+constexpr int kPartBase = 5;
+constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
+constexpr float kHalfLog2PiPlusHalf = 1.41893853320467274178f;
+
+template <int ACT>
+__device__ __forceinline__ float act_f(float z, float slope) {
+    if (ACT == 1) return z > 0.f ? z : z * slope;
+    if (ACT == 2) return tanhf(z);
+    return z;
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_g(float h, float slope) {  // d act / d z as a function of the output
+    if (ACT == 1) return h > 0.f ? 1.f : slope;
+    if (ACT == 2) return 1.0f - h * h;
+    return 1.f;
+}
+
+__device__ __forceinline__ void adv_stats(const double *partials, int64_t n, int64_t batch, float *mean, float *inv) {
+    if (threadIdx.x < 64) {
+        double s = 0.0, q = 0.0;
+        for (int64_t k = threadIdx.x; k < n; k += 64) {
+            s += partials[2 * k];
+            q += partials[2 * k + 1];
+        }
+        s = xpa_wave_sum(s);
+        q = xpa_wave_sum(q);
+        if (threadIdx.x == 0) {
+            const double m = s / (double)batch;
+            const double var = fmax(q / (double)batch - m * m, 0.0);
+            *mean = (float)m;
+            *inv = (float)(1.0 / ((double)(float)sqrt(var) + 1e-8));
+        }
+    }
+}
+
+// Tiled formulation: a block walks tiles of kTile = 64 rows (grid-stride, next tile's z prefetched into
+// registers while the current one is processed):
+//   stage    256 threads load the [64 x 256] z tile coalesced (16-B loads), apply the activation and
+//            store h into LDS (row stride kS = 260 floats);
+//   phase 1  row owners: thread (wave q, lane r) dots h[r, 64q : 64q + 64] with the output weights
+//            (wave-uniform scalar loads) -> per-quarter partials in LDS;
+//   loss     wave 0, lane r: head[r] = sum of the 4 quarters + bias, the row's loss terms and d head
+//            (once per row, no redundant lanes) -> LDS;
+//   phase 2  column owners: thread c walks the tile's rows: dz[r, c] = (d_head[r] . w[:, c]) * act'(h),
+//            accumulating dW_out[:, c] and db_hidden[c] in registers.
+// LDS banks: phase-1 ds_read_b128 of lanes r = 16g..16g+15 start at dword 4r + c (mod 64): the 16-lane
+// group covers the 64 banks once; phase-2 ds_read_b32 of consecutive columns hits consecutive banks.
+typedef float f4v __attribute__((ext_vector_type(4)));
+constexpr int kTile = 64;
+constexpr int kS = 260;
+constexpr int kGridMax = 512;  // 2 blocks per CU (77 KiB LDS each) x 256 CUs
+
+struct HeadArgs {
+    int64_t batch;
+    int K;
+    const float *z;
+    const float *W;
+    const float *bias;
+    float slope;
+    const float *logstd;
+    const int64_t *idx;
+    int64_t n_rows;
+    const float *act;
+    const float *old_logp;
+    const float *adv;
+    const float *ret;
+    const double *adv_partials;
+    int64_t n_adv_partials;
+    float clip_range, ent_coef, vf_coef;
+    float *dz, *p_dw, *p_dbh, *p_dbo, *p_loss;
+    int loss_width;
+};
+
+__device__ __forceinline__ void load_tile(float4 (&zq)[16], const float *__restrict__ z, int64_t tile, int64_t batch) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int lin = i * 256 + (int)threadIdx.x;
+        const int64_t row = tile * kTile + (lin >> 6);
+        if (row < batch) {
+            const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(z + row * kH) + (lin & 63));
+            zq[i] = make_float4(v.x, v.y, v.z, v.w);
+        } else {
+            zq[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+}
+
+// MODE: 0 Gaussian actor, 1 Categorical actor, 2 critic.  ALGO: 0 PPO, 1 A2C (actor only).
+template <int MODE, int ALGO, int ACT, int KMAX>
+__global__ __launch_bounds__(256, 2) void head_tile_kernel(
+    int64_t batch, int K_in, const float *__restrict__ z, const float *__restrict__ W, const float *__restrict__ bias,
+    float slope, const float *__restrict__ logstd, const int64_t *__restrict__ idx, int64_t n_rows,
+    const float *__restrict__ act, const float *__restrict__ old_logp, const float *__restrict__ adv,
+    const float *__restrict__ ret, const double *__restrict__ adv_partials, int64_t n_adv_partials, float clip_range,
+    float ent_coef, float vf_coef, float *__restrict__ dz, float *__restrict__ p_dw, float *__restrict__ p_dbh,
+    float *__restrict__ p_dbo, float *__restrict__ p_loss, int loss_width) {
+    __shared__ __attribute__((aligned(16))) float s_h[kTile * kS];
+    __shared__ __attribute__((aligned(16))) float s_part[kWaves][kTile][KMAX];
+    __shared__ __attribute__((aligned(16))) float s_dh[kTile][KMAX];
+    __shared__ float s_mean, s_inv;
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int K = MODE == 2 ? 1 : K_in;
+    if (MODE != 2 && adv_partials) {
+        adv_stats(adv_partials, n_adv_partials, batch, &s_mean, &s_inv);
+    } else if (t == 0) {
+        s_mean = 0.f;
+        s_inv = 1.f;
+    }
+    const int64_t ntiles = (batch + kTile - 1) / kTile;
+    int64_t tile = blockIdx.x;
+    float4 zq[16];
+    load_tile(zq, z, tile, batch);
+
+    // phase-2 constants / accumulators (column t)
+    float wc[KMAX], acc_dw[KMAX];
+#pragma unroll
+    for (int o = 0; o < KMAX; ++o) {
+        wc[o] = o < K ? W[o * kH + t] : 0.f;
+        acc_dw[o] = 0.f;
+    }
+    float acc_dbh = 0.f;
+    // wave-0 (row owner) accumulators
+    float acc_dbo[KMAX], acc_dls[KMAX], var_[KMAX], logsc[KMAX];
+    float sum0 = 0.f, sum1 = 0.f, sum2 = 0.f, ent_const = 0.f;
+#pragma unroll
+    for (int o = 0; o < KMAX; ++o) {
+        acc_dbo[o] = acc_dls[o] = 0.f;
+        if (MODE == 0) {
+            const float sc = o < K ? expf(logstd[o]) : 1.f;
+            var_[o] = sc * sc;
+            logsc[o] = logf(sc);
+            if (o < K) ent_const += kHalfLog2PiPlusHalf + logsc[o];
+        }
+    }
+    const float inv_b = 1.0f / (float)batch;
+    const float lo = 1.0f - clip_range, hi = 1.0f + clip_range;
+    __syncthreads();
+    const float a_mean = s_mean, a_inv = s_inv;
+
+    for (; tile < ntiles; tile += gridDim.x) {
+        // ---- stage h = act(z) into LDS ----
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int lin = i * 256 + t;
+            float4 h;
+            h.x = act_f<ACT>(zq[i].x, slope); h.y = act_f<ACT>(zq[i].y, slope);
+            h.z = act_f<ACT>(zq[i].z, slope); h.w = act_f<ACT>(zq[i].w, slope);
+            *reinterpret_cast<float4 *>(s_h + (lin >> 6) * kS + 4 * (lin & 63)) = h;
+        }
+        // ---- wave 0: this tile's per-row inputs (lane = row) ----
+        bool valid = false;
+        float my_x = 0.f, my_old = 0.f, my_act[KMAX];
+#pragma unroll
+        for (int o = 0; o < KMAX; ++o) my_act[o] = 0.f;
+        if (wave == 0) {
+            const int64_t b = tile * kTile + lane;
+            if (b < batch) {
+                const int64_t row = idx ? idx[b] : b;
+                valid = row >= 0 && row < n_rows;
+                if (valid) {
+                    if (MODE == 2) {
+                        my_x = ret[row];
+                    } else {
+                        my_x = adv[row];
+                        if (ALGO == 0) my_old = old_logp[row];
+                        if (MODE == 0) {
+#pragma unroll
+                            for (int o = 0; o < KMAX; ++o)
+                                if (o < K) my_act[o] = act[row * K + o];
+                        } else {
+                            my_act[0] = act[row];
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        const int64_t next = tile + gridDim.x;
+        if (next < ntiles) load_tile(zq, z, next, batch);  // in flight during phases 1-2
+        // ---- phase 1: partial dot products, row = lane, quarter = wave ----
+        {
+            float p[KMAX];
+#pragma unroll
+            for (int o = 0; o < KMAX; ++o) p[o] = 0.f;
+            const float *hrow = s_h + lane * kS + wave * 64;
+            const float *wq = W + wave * 64;
+#pragma unroll 4
+            for (int j = 0; j < 16; ++j) {
+                const float4 hv = *reinterpret_cast<const float4 *>(hrow + 4 * j);
+#pragma unroll
+                for (int o = 0; o < KMAX; ++o) {
+                    if (o < K) {
+                        const float4 w4 = *reinterpret_cast<const float4 *>(wq + o * kH + 4 * j);
+                        p[o] += hv.x * w4.x + hv.y * w4.y + hv.z * w4.z + hv.w * w4.w;
+                    }
+                }
+            }
+#pragma unroll
+            for (int o = 0; o < KMAX; ++o) s_part[wave][lane][o] = p[o];
+        }
+        __syncthreads();
+        // ---- loss: wave 0, one lane per row ----
+        if (wave == 0) {
+            float dh_[KMAX];
+#pragma unroll
+            for (int o = 0; o < KMAX; ++o) dh_[o] = 0.f;
+            if (valid) {
+                float hd[KMAX];
+#pragma unroll
+                for (int o = 0; o < KMAX; ++o)
+                    hd[o] = o < K ? ((s_part[0][lane][o] + s_part[1][lane][o]) + (s_part[2][lane][o] + s_part[3][lane][o])) +
+                                        bias[o]
+                                  : 0.f;
+                if (MODE == 2) {
+                    const float diffv = hd[0] - my_x;
+                    sum0 += diffv * diffv;
+                    sum1 += hd[0];
+                    dh_[0] = vf_coef * 2.0f * diffv * inv_b;
+                    acc_dbo[0] += dh_[0];
+                } else {
+                    const float A_n = (my_x - a_mean) * a_inv;
+                    float logp = 0.f, ent = 0.f, lse = 0.f;
+                    int ai = 0;
+                    float diff[KMAX];
+                    if (MODE == 0) {
+#pragma unroll
+                        for (int o = 0; o < KMAX; ++o) {
+                            diff[o] = 0.f;
+                            if (o < K) {
+                                diff[o] = my_act[o] - hd[o];
+                                logp += -(diff[o] * diff[o]) / (2.0f * var_[o]) - logsc[o] - kLogSqrt2Pi;
+                            }
+                        }
+                        ent = ent_const;
+                    } else {
+                        float m = hd[0];
+#pragma unroll
+                        for (int o = 1; o < KMAX; ++o)
+                            if (o < K) m = fmaxf(m, hd[o]);
+                        float se = 0.f;
+#pragma unroll
+                        for (int o = 0; o < KMAX; ++o)
+                            if (o < K) se += expf(hd[o] - m);
+                        lse = m + logf(se);
+                        ai = (int)my_act[0];
+                        ai = ai < 0 ? 0 : (ai >= K ? K - 1 : ai);
+#pragma unroll
+                        for (int o = 0; o < KMAX; ++o) {
+                            if (o < K) {
+                                const float ln = hd[o] - lse;
+                                ent -= expf(ln) * ln;
+                                if (o == ai) logp = ln;
+                            }
+                        }
+                    }
+                    float dlogp;
+                    if (ALGO == 0) {
+                        const float ratio = expf(logp - my_old);
+                        const float cr = fminf(fmaxf(ratio, lo), hi);
+                        const float s1 = cr * A_n, s2 = A_n * ratio;
+                        sum0 += fminf(s1, s2);
+                        const bool inr = (ratio >= lo) && (ratio <= hi);
+                        const float g1 = inr ? A_n : 0.f;
+                        const float w1 = (s1 < s2) ? 1.f : ((s1 == s2) ? 0.5f : 0.f);
+                        const float w2 = (s2 < s1) ? 1.f : ((s1 == s2) ? 0.5f : 0.f);
+                        dlogp = -inv_b * (w1 * g1 + w2 * A_n) * ratio;
+                        sum2 += ((ratio < lo) || (ratio > hi)) ? 1.f : 0.f;
+                    } else {
+                        sum0 += A_n * logp;
+                        dlogp = -A_n * inv_b;
+                    }
+                    sum1 += ent;
+                    const float ec = ent_coef * inv_b;
+#pragma unroll
+                    for (int o = 0; o < KMAX; ++o) {
+                        if (o < K) {
+                            if (MODE == 0) {
+                                dh_[o] = dlogp * diff[o] / var_[o];
+                                acc_dls[o] += dlogp * (diff[o] * diff[o] / var_[o] - 1.0f);
+                            } else {
+                                const float ln = hd[o] - lse;
+                                const float p = expf(ln);
+                                dh_[o] = dlogp * ((o == ai ? 1.f : 0.f) - p) + ec * p * (ln + ent);
+                            }
+                            acc_dbo[o] += dh_[o];
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int o = 0; o < KMAX; ++o) s_dh[lane][o] = dh_[o];
+        }
+        __syncthreads();
+        // ---- phase 2: column owner t ----
+        const int nr = (int)min((int64_t)kTile, batch - tile * kTile);
+        float *dzt = dz + tile * kTile * kH + t;
+        for (int r = 0; r < nr; ++r) {
+            const float h = s_h[r * kS + t];
+            float d = 0.f;
+#pragma unroll
+            for (int o = 0; o < KMAX; ++o) {  // o >= K: s_dh and wc are 0 (accumulator unused)
+                const float g = s_dh[r][o];
+                d += g * wc[o];
+                acc_dw[o] += g * h;
+            }
+            d *= act_g<ACT>(h, slope);
+            __builtin_nontemporal_store(d, dzt + r * kH);
+            acc_dbh += d;
+        }
+        __syncthreads();  // s_h / s_dh reused by the next tile
+    }
+    // ---- block partials ----
+    const int64_t blk = blockIdx.x;
+#pragma unroll
+    for (int o = 0; o < KMAX; ++o)
+        if (o < K) p_dw[(blk * K + o) * kH + t] = acc_dw[o];
+    p_dbh[blk * kH + t] = acc_dbh;
+    if (wave == 0) {
+        sum0 = xpa_wave_sum(sum0);
+        sum1 = xpa_wave_sum(sum1);
+        sum2 = xpa_wave_sum(sum2);
+#pragma unroll
+        for (int o = 0; o < KMAX; ++o) {
+            if (o < K) {
+                acc_dbo[o] = xpa_wave_sum(acc_dbo[o]);
+                if (MODE == 0) acc_dls[o] = xpa_wave_sum(acc_dls[o]);
+            }
+        }
+        if (lane == 0) {
+            float *prow = p_loss + blk * loss_width;
+            if (MODE == 2) {
+                prow[1] = sum0;
+                prow[4] = sum1;
+            } else {
+                prow[0] = sum0;
+                prow[2] = sum1;
+                prow[3] = sum2;
+            }
+#pragma unroll
+            for (int o = 0; o < KMAX; ++o) {
+                if (o < K) {
+                    p_dbo[blk * K + o] = acc_dbo[o];
+                    if (MODE == 0) prow[kPartBase + o] = acc_dls[o];
+                }
+            }
+        }
+    }
+}
+
+}  // namespace
+
+XPA_API int64_t xpa_head_fused_num_partials(int64_t batch) {
+    const int64_t tiles = (batch + kTile - 1) / kTile;
+    return tiles < kGridMax ? tiles : kGridMax;
+}
+
+namespace {
+#define XPA_HEAD_ARGS(a) a.batch, a.K, a.z, a.W, a.bias, a.slope, a.logstd, a.idx, a.n_rows, a.act, a.old_logp, a.adv, a.ret, a.adv_partials, a.n_adv_partials, a.clip_range, a.ent_coef, a.vf_coef, a.dz, a.p_dw, a.p_dbh, a.p_dbo, a.p_loss, a.loss_width
+template <int MODE, int ALGO>
+void launch_head(const HeadArgs &a, int act_code, hipStream_t s) {
+    const dim3 grid((unsigned)xpa_head_fused_num_partials(a.batch)), block(256);
+    if constexpr (MODE == 2) {
+        if (act_code == 0) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 0, 1>), grid, block, 0, s, XPA_HEAD_ARGS(a));
+        else if (act_code == 1) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 1, 1>), grid, block, 0, s, XPA_HEAD_ARGS(a));
+        else hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 2, 1>), grid, block, 0, s, XPA_HEAD_ARGS(a));
+    } else if (a.K <= 4) {  // KMAX 8 (K <= 8); the K <= 4 instantiation keeps fewer live registers
+        if (act_code == 0) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 0, 4>), grid, block, 0, s, XPA_HEAD_ARGS(a));
+        else if (act_code == 1) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 1, 4>), grid, block, 0, s, XPA_HEAD_ARGS(a));
+        else hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 2, 4>), grid, block, 0, s, XPA_HEAD_ARGS(a));
+    } else {
+        if (act_code == 0) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 0, 8>), grid, block, 0, s, XPA_HEAD_ARGS(a));
+        else if (act_code == 1) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 1, 8>), grid, block, 0, s, XPA_HEAD_ARGS(a));
+        else hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 2, 8>), grid, block, 0, s, XPA_HEAD_ARGS(a));
+    }
+}
+#undef XPA_HEAD_ARGS
+}  // namespace
+
+XPA_API int xpa_head_fused_actor(int algo, int dist, int act_code, int64_t batch, int64_t act_dim, int64_t hidden,
+                                 const float *z, const float *w, const float *b, float slope, const float *logstd,
+                                 const int64_t *idx, int64_t n_rows, const float *act, const float *old_logp,
+                                 const float *adv, const double *adv_partials, int64_t n_adv_partials,
+                                 float clip_range, float ent_coef, float *dz, float *partial_dw,
+                                 float *partial_db_hidden, float *partial_db_out, float *loss_partials,
+                                 int64_t loss_width, xpa_stream_t stream) {
+    if (batch <= 0 || hidden != kH || act_dim < 1 || act_dim > 8 || act_code < 0 || act_code > 2 || !z || !w || !b ||
+        !act || !adv || !dz || !partial_dw || !partial_db_hidden || !partial_db_out || !loss_partials ||
+        loss_width < kPartBase + act_dim || n_rows <= 0 || (!idx && n_rows < batch))
+        return (int)hipErrorInvalidValue;
+    if ((algo != XPA_ALGO_PPO && algo != XPA_ALGO_A2C) || (dist != XPA_DIST_GAUSSIAN && dist != XPA_DIST_CATEGORICAL))
+        return (int)hipErrorInvalidValue;
+    if ((dist == XPA_DIST_GAUSSIAN && !logstd) || (algo == XPA_ALGO_PPO && !old_logp) ||
+        (dist == XPA_DIST_CATEGORICAL && act_dim < 2))
+        return (int)hipErrorInvalidValue;
+    if (((uintptr_t)z | (uintptr_t)w) % 16) return (int)hipErrorInvalidValue;
+    HeadArgs a{};
+    a.batch = batch; a.K = (int)act_dim; a.z = z; a.W = w; a.bias = b; a.slope = slope; a.logstd = logstd;
+    a.idx = idx; a.n_rows = n_rows; a.act = act; a.old_logp = old_logp; a.adv = adv; a.ret = nullptr;
+    a.adv_partials = adv_partials; a.n_adv_partials = n_adv_partials; a.clip_range = clip_range;
+    a.ent_coef = ent_coef; a.vf_coef = 0.f; a.dz = dz; a.p_dw = partial_dw; a.p_dbh = partial_db_hidden;
+    a.p_dbo = partial_db_out; a.p_loss = loss_partials; a.loss_width = (int)loss_width;
+    hipStream_t s = (hipStream_t)stream;
+    if (dist == XPA_DIST_GAUSSIAN) {
+        if (algo == XPA_ALGO_PPO) launch_head<0, 0>(a, act_code, s);
+        else launch_head<0, 1>(a, act_code, s);
+    } else {
+        if (algo == XPA_ALGO_PPO) launch_head<1, 0>(a, act_code, s);
+        else launch_head<1, 1>(a, act_code, s);
+    }
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_head_fused_critic(int act_code, int64_t batch, int64_t hidden, const float *z, const float *w,
+                                  const float *b, float slope, const int64_t *idx, int64_t n_rows, const float *ret,
+                                  float vf_coef, float *dz, float *partial_dw, float *partial_db_hidden,
+                                  float *partial_db_out, float *loss_partials, int64_t loss_width,
+                                  xpa_stream_t stream) {
+    if (batch <= 0 || hidden != kH || act_code < 0 || act_code > 2 || !z || !w || !b || !ret || !dz || !partial_dw ||
+        !partial_db_hidden || !partial_db_out || !loss_partials || loss_width < kPartBase || n_rows <= 0 ||
+        (!idx && n_rows < batch))
+        return (int)hipErrorInvalidValue;
+    if (((uintptr_t)z | (uintptr_t)w) % 16) return (int)hipErrorInvalidValue;
+    HeadArgs a{};
+    a.batch = batch; a.K = 1; a.z = z; a.W = w; a.bias = b; a.slope = slope; a.idx = idx; a.n_rows = n_rows;
+    a.ret = ret; a.vf_coef = vf_coef; a.dz = dz; a.p_dw = partial_dw; a.p_dbh = partial_db_hidden;
+    a.p_dbo = partial_db_out; a.p_loss = loss_partials; a.loss_width = (int)loss_width;
+    launch_head<2, 0>(a, act_code, (hipStream_t)stream);
+    return xpa_launch_status();
+}

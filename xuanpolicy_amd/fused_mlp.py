@@ -67,11 +67,21 @@ class FusedActorCritic:
         self.critic = _parse(policy.critic.model)
         self.logstd = None if self.discrete else policy.actor.logstd
         self.use_head_kernel = True
+        # K12 (fused head + loss + backward) when both heads end in [Linear(., 256) + act] -> Linear(256, K)
+        k = self.actor[-1][0].out_features
+        self.fused_heads = (self._head_fusable(self.actor) and self._head_fusable(self.critic)
+                            and k <= 8 and (k >= 2 or not self.discrete))
+        self._hws = None
         n_params = sum(1 for _ in policy.parameters())
         n_cov = 2 * (len(self.rep) + len(self.actor) + len(self.critic)) + (0 if self.discrete else 1)
         if n_params != n_cov:
             raise ValueError("policy has parameters outside the Linear chains")
         self._partials = {}
+
+    @staticmethod
+    def _head_fusable(layers):
+        return (len(layers) >= 2 and layers[-1][1] == 0 and layers[-2][0].out_features == ops.HEAD_HIDDEN
+                and layers[-1][0].in_features == ops.HEAD_HIDDEN)
 
     # ------------------------------------------------------------------------------------------------
     @staticmethod
@@ -95,6 +105,63 @@ class FusedActorCritic:
         c_outs = self._chain_forward(self.critic, s)
         v = c_outs[-1][:, 0]
         return a_outs[-1], self.logstd, v, (x, rep_outs, s, a_outs, c_outs)
+
+    @torch.no_grad()
+    def forward_hidden(self, x):
+        """Forward up to the heads' last hidden pre-activations (K12 does the rest)."""
+        rep_outs = self._chain_forward(self.rep, x)
+        s = rep_outs[-1] if rep_outs else x
+        heads = []
+        for layers in (self.actor, self.critic):
+            outs = self._chain_forward(layers[:-2], s)
+            lin = layers[-2][0]
+            x_h = outs[-1] if outs else s
+            heads.append((outs, x_h, F.linear(x_h, lin.weight, lin.bias)))
+        return (x, rep_outs, s, heads)
+
+    @torch.no_grad()
+    def loss_backward(self, ctx, algo, dist, act, adv, ret, old_logp=None, idx=None, adv_partials=None,
+                      clip_range=0.2, vf_coef=0.25, ent_coef=0.0):
+        """K12 loss + head backward, then the hidden / trunk GEMMs.  Writes every parameter gradient;
+        returns the loss-scalars device tensor (ops.OUT_KEYS)."""
+        x, rep_outs, s, ((a_outs, a_xh, z_a), (c_outs, c_xh, z_c)) = ctx
+        B = z_a.shape[0]
+        lin_ao, _, _ = self.actor[-1]
+        lin_ah, a_code, a_slope = self.actor[-2]
+        lin_co, _, _ = self.critic[-1]
+        lin_ch, c_code, c_slope = self.critic[-2]
+        K = lin_ao.out_features
+        if self._hws is None or self._hws.batch != B:
+            self._hws = ops.HeadWorkspace(B, K, z_a.device)
+        grads = {"w_actor": lin_ao.weight.grad, "b_actor": lin_ao.bias.grad, "bh_actor": lin_ah.bias.grad,
+                 "w_critic": lin_co.weight.grad, "b_critic": lin_co.bias.grad, "bh_critic": lin_ch.bias.grad}
+        if self.logstd is not None:
+            grads["logstd"] = self.logstd.grad
+        scalars, dz_a, dz_c = ops.fused_heads(algo, dist, self._hws, z_a, lin_ao.weight, lin_ao.bias, (a_code, a_slope),
+                                              z_c, lin_co.weight, lin_co.bias, (c_code, c_slope), self.logstd, act,
+                                              adv, ret, old_logp=old_logp, idx=idx, adv_partials=adv_partials,
+                                              clip_range=clip_range, vf_coef=vf_coef, ent_coef=ent_coef, grads=grads)
+        have_rep = len(self.rep) > 0
+        ds = self._from_dz(self.actor[:-1], [s] + a_outs, a_outs, dz_a, need_dx=have_rep)
+        ds = self._from_dz(self.critic[:-1], [s] + c_outs, c_outs, dz_c, need_dx=have_rep, accumulate=ds)
+        if have_rep:
+            r_in = [x] + rep_outs[:-1]
+            self._chain_backward(self.rep, r_in, rep_outs, ds, need_dx=False)
+        return scalars
+
+    def _from_dz(self, layers, inputs, outs, dz, need_dx, accumulate=None):
+        """Backward from the pre-activation gradient dz of layers[-1] (its bias gradient already
+        written): weight gradient, dX, then the earlier layers of the chain."""
+        lin = layers[-1][0]
+        self._weight_grad(dz, inputs[len(layers) - 1], lin.weight.grad)
+        if len(layers) == 1:
+            if not need_dx:
+                return None
+            return accumulate.addmm_(dz, lin.weight) if accumulate is not None else torch.mm(dz, lin.weight)
+        g = torch.mm(dz, lin.weight)
+        prev = layers[:-1]
+        return self._chain_backward(prev, inputs[:len(prev)], outs[:len(prev)], g, need_dx, accumulate,
+                                    allow_head=False)
 
     # ------------------------------------------------------------------------------------------------
     def _bias_grad(self, code, g, h, slope, out):
@@ -147,12 +214,12 @@ class FusedActorCritic:
         _lib.check(L.xpa_colsum_finalize(ops._p(p_dbo), G, K, ops._p(lin_o.bias.grad), s), "colsum db_o")
         return dz
 
-    def _chain_backward(self, layers, inputs, outs, g, need_dx, accumulate=None):
+    def _chain_backward(self, layers, inputs, outs, g, need_dx, accumulate=None, allow_head=True):
         """g: grad w.r.t. the chain's last output (contiguous [B, n_out]); returns grad w.r.t. its input
         (added to `accumulate` through the GEMM's C operand when given)."""
         top = len(layers) - 1
         if (len(layers) >= 2 and layers[-1][1] == 0 and layers[-2][1] != 0 and g.shape[1] <= 32
-                and g.stride(1) == 1 and self.use_head_kernel):
+                and g.stride(1) == 1 and self.use_head_kernel and allow_head):
             g = self._head_tail(layers, outs, g)   # output layer + hidden activation done by K11
             lin, _, _ = layers[-2]
             self._weight_grad(g, inputs[-2], lin.weight.grad)

@@ -107,6 +107,13 @@ class _FusedPolicyGradient(Learner):
         (idx=None: already gathered).  Returns the device tensor of loss scalars (ops.OUT_KEYS)."""
         self.iterations += 1
         fm = self._fused_mlp()
+        if fm is not None and fm.fused_heads:
+            ctx = fm.forward_hidden(obs)   # K12: heads, loss and head backward in one pass per head
+            scalars = fm.loss_backward(ctx, self.algo, self.dist, act, adv, ret, old_logp=old_logp, idx=idx,
+                                       adv_partials=adv_partials, clip_range=self.clip_range, vf_coef=self.vf_coef,
+                                       ent_coef=self.ent_coef)
+            self._sync_clip_step()
+            return scalars
         if fm is not None:
             head, logstd, v, ctx = fm.forward(obs)
             if self._ws is None or self._ws.batch != head.shape[0]:

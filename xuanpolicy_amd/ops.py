@@ -213,6 +213,94 @@ def policy_loss(algo, dist, head, logstd, v, act, adv, ret, old_logp=None, idx=N
 
 
 # ------------------------------------------------------------------------------------------------
+HEAD_HIDDEN = 256  # hidden width K12 handles (64 lanes x 4 columns)
+
+
+class HeadWorkspace:
+    """Outputs and per-block partials of K12 for a fixed (batch, K)."""
+
+    def __init__(self, batch, k, device):
+        H = HEAD_HIDDEN
+        G = int(lib().xpa_head_fused_num_partials(batch))
+        self.batch, self.k, self.G = batch, k, G
+        f32 = dict(dtype=torch.float32, device=device)
+        self.dz_actor = torch.empty((batch, H), **f32)
+        self.dz_critic = torch.empty((batch, H), **f32)
+        self.p_dw_actor = torch.empty((G, k * H), **f32)
+        self.p_dbh_actor = torch.empty((G, H), **f32)
+        self.p_dbo_actor = torch.empty((G, k), **f32)
+        self.p_dw_critic = torch.empty((G, H), **f32)
+        self.p_dbh_critic = torch.empty((G, H), **f32)
+        self.p_dbo_critic = torch.empty((G, 1), **f32)
+        self.loss_partials = torch.zeros((G, int(lib().xpa_loss_partial_width(k))), **f32)
+        self.scalars = torch.empty((N_OUT,), **f32)
+
+
+def _colsum(part, out, s):
+    _lib.check(lib().xpa_colsum_finalize(_p(part), part.shape[0], part.shape[1], _p(out), s), "xpa_colsum_finalize")
+
+
+def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, w_critic, b_critic, act_critic,
+                logstd, act, adv, ret, old_logp=None, idx=None, adv_partials=None, clip_range=0.2, vf_coef=0.25,
+                ent_coef=0.0, grads=None):
+    """K12 actor + critic heads, loss finalize and the column-sum finalizes.
+
+    z_*: hidden pre-activations [B, 256]; w_*/b_*: output layer (K x 256 / 1 x 256); act_*: (code, slope)
+    of the hidden activation.  grads: dict with the gradient views to write — 'w_actor', 'b_actor',
+    'bh_actor', 'w_critic', 'b_critic', 'bh_critic', 'logstd' (gaussian).  Returns (scalars, dz_actor,
+    dz_critic)."""
+    if algo not in ALGO or dist not in DIST:
+        raise ValueError("algo must be ppo|a2c and dist gaussian|categorical")
+    B, H = z_actor.shape
+    K = w_actor.shape[0]
+    if H != HEAD_HIDDEN or ws.batch != B or ws.k != K:
+        raise ValueError("fused heads need hidden width %d and a matching workspace" % HEAD_HIDDEN)
+    _req(z_actor, "z_actor", torch.float32, (B, H))
+    _req(z_critic, "z_critic", torch.float32, (B, H))
+    _req(w_actor, "w_actor", torch.float32, (K, H))
+    _req(w_critic, "w_critic", torch.float32, (1, H))
+    if idx is not None:
+        _req(idx, "idx", torch.int64, (B,))
+    rows = adv.numel()
+    _req(adv, "adv", torch.float32)
+    _req(ret, "ret", torch.float32, (rows,))
+    _req(act, "act", torch.float32)
+    if act.numel() != rows * (K if dist == "gaussian" else 1):
+        raise ValueError("act has %d elements, expected %d" % (act.numel(), rows * (K if dist == "gaussian" else 1)))
+    if algo == "ppo":
+        _req(old_logp, "old_logp", torch.float32, (rows,))
+    if adv_partials is not None:
+        _req(adv_partials, "adv_partials", torch.float64)
+    s = _stream(z_actor.device)
+    L = lib()
+    W = ws.loss_partials.shape[1]
+    ev = TIMER.start("heads")
+    rc = L.xpa_head_fused_actor(ALGO[algo], DIST[dist], act_actor[0], B, K, H, _p(z_actor), _p(w_actor), _p(b_actor),
+                                float(act_actor[1]), _p(logstd) if dist == "gaussian" else None, _p(idx), rows, _p(act),
+                                _p(old_logp) if algo == "ppo" else None, _p(adv), _p(adv_partials),
+                                adv_partials.shape[0] if adv_partials is not None else 0, float(clip_range),
+                                float(ent_coef), _p(ws.dz_actor), _p(ws.p_dw_actor), _p(ws.p_dbh_actor),
+                                _p(ws.p_dbo_actor), _p(ws.loss_partials), W, s)
+    _lib.check(rc, "xpa_head_fused_actor")
+    rc = L.xpa_head_fused_critic(act_critic[0], B, H, _p(z_critic), _p(w_critic), _p(b_critic), float(act_critic[1]),
+                                 _p(idx), rows, _p(ret), float(vf_coef), _p(ws.dz_critic), _p(ws.p_dw_critic),
+                                 _p(ws.p_dbh_critic), _p(ws.p_dbo_critic), _p(ws.loss_partials), W, s)
+    TIMER.stop("heads", ev)
+    _lib.check(rc, "xpa_head_fused_critic")
+    g = grads or {}
+    d_logstd = g.get("logstd")
+    if dist == "gaussian" and d_logstd is None:
+        d_logstd = torch.empty((K,), dtype=torch.float32, device=z_actor.device)
+    _lib.check(L.xpa_policy_loss_finalize(ALGO[algo], DIST[dist], B, K, _p(ws.loss_partials), ws.G, float(vf_coef),
+                                          float(ent_coef), _p(ws.scalars), _p(d_logstd), s), "xpa_policy_loss_finalize")
+    for key, part in (("w_actor", ws.p_dw_actor), ("b_actor", ws.p_dbo_actor), ("bh_actor", ws.p_dbh_actor),
+                      ("w_critic", ws.p_dw_critic), ("b_critic", ws.p_dbo_critic), ("bh_critic", ws.p_dbh_critic)):
+        if key in g:
+            _colsum(part, g[key], s)
+    return ws.scalars, ws.dz_actor, ws.dz_critic
+
+
+# ------------------------------------------------------------------------------------------------
 def rms_num_partials(n):
     return int(lib().xpa_rms_num_partials(n))
 
