@@ -205,19 +205,39 @@ int xpa_head_backward(int act, int64_t k, const float *d_head, int64_t ldd, cons
  * layout (width >= xpa_loss_partial_width(K)): the actor kernel fills the surrogate / entropy / clip /
  * dlogstd columns, the critic kernel the squared-error / value columns, so one
  * xpa_policy_loss_finalize over the shared array yields the loss scalars and d logstd.
- * act: 0 identity, 1 LeakyReLU(slope) / ReLU (slope 0), 2 tanh.  K <= 8; hidden must be 256;
- * z, w, dz and the dW / db_hidden partials 16-B aligned. */
+ * act: 0 identity, 1 LeakyReLU(slope) / ReLU (slope 0), 2 tanh.  K <= 8; hidden must be 256; z and dz
+ * rows have stride ld (>= 256, multiple of 4); z and w 16-B aligned. */
 int64_t xpa_head_fused_num_partials(int64_t batch);
-int xpa_head_fused_actor(int algo, int dist, int act, int64_t batch, int64_t act_dim, int64_t hidden,
+int xpa_head_fused_actor(int algo, int dist, int act, int64_t batch, int64_t act_dim, int64_t hidden, int64_t ld,
                          const float *z, const float *w, const float *b, float slope, const float *logstd,
                          const int64_t *idx, int64_t n_rows, const float *act_buf, const float *old_logp,
                          const float *adv, const double *adv_partials, int64_t n_adv_partials, float clip_range,
                          float ent_coef, float *dz, float *partial_dw, float *partial_db_hidden,
                          float *partial_db_out, float *loss_partials, int64_t loss_width, xpa_stream_t stream);
-int xpa_head_fused_critic(int act, int64_t batch, int64_t hidden, const float *z, const float *w, const float *b,
+int xpa_head_fused_critic(int act, int64_t batch, int64_t hidden, int64_t ld, const float *z, const float *w, const float *b,
                           float slope, const int64_t *idx, int64_t n_rows, const float *ret, float vf_coef,
                           float *dz, float *partial_dw, float *partial_db_hidden, float *partial_db_out,
                           float *loss_partials, int64_t loss_width, xpa_stream_t stream);
+
+/* Batched xpa_colsum_finalize: out_i[c] = sum over the n_partials[i] rows of partials_i[:, c] for
+ * up to 16 segments in one launch (host arrays of n_segs entries; the pointers they hold are device
+ * pointers).  Same fixed-order f64 sums as xpa_colsum_finalize. */
+int xpa_colsum_finalize_batch(int n_segs, const float *const *partials, const int64_t *n_partials,
+                              const int64_t *cols, float *const *outs, xpa_stream_t stream);
+
+/* K13 — first representation layer Linear(d_in, 256) + activation for a small d_in (<= 64): Basic_MLP's
+ * first mlp_block (xuance/torch/representations/mlp.py:21-51, utils/layers.py:8-24) as HBM-streaming
+ * kernels.  Forward: h = act(x W^T + b), x [rows, d_in] (row stride ldx), w [256, d_in], h [rows, 256]
+ * (row stride ldh).  Backward (the layer is the first of the network, so no dX): from g = d loss/d h
+ * and h, per-block partials of dW (xpa_thin_bwd_num_partials(rows) rows of 256*d_in, laid out as w) and
+ * of db (rows of 256), each reduced by xpa_colsum_finalize.  act: 0 identity, 1 LeakyReLU(slope) /
+ * ReLU, 2 tanh. */
+int64_t xpa_thin_bwd_num_partials(int64_t rows);
+int xpa_thin_linear_act_fwd(int act, const float *x, int64_t ldx, int64_t rows, int64_t d_in, int64_t d_out,
+                            const float *w, const float *b, float slope, float *h, int64_t ldh, xpa_stream_t stream);
+int xpa_thin_linear_act_bwd(int act, const float *g, int64_t ldg, const float *h, int64_t ldh, int64_t rows,
+                            const float *x, int64_t ldx, int64_t d_in, int64_t d_out, float slope, float *partial_dw,
+                            float *partial_db, xpa_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -105,3 +105,33 @@ def test_policy_state_dict_keys_match_reference(golden):
         head = dist.mu if hasattr(dist, "mu") else dist.logits
         assert torch.allclose(head, torch.as_tensor(g[tag + "/head"]), atol=1e-5)
         assert torch.allclose(v, torch.as_tensor(g[tag + "/v"]), atol=1e-5)
+
+
+def test_flat_state_placement_groups():
+    """FlatState keeps parameter order/offsets per parameter but lays placement groups back to back
+    (the paired actor|critic hidden layer of fused_mlp.head_placement)."""
+    from xuanpolicy_amd.flat import ALIGN, FlatState
+    from xuanpolicy_amd.fused_mlp import head_placement
+    from xuanpolicy_amd.policies import Basic_MLP, Gaussian_AC_Policy
+
+    class Box:
+        shape = (6,)
+    torch.manual_seed(0)
+    rep = Basic_MLP((17,), [256], None, torch.nn.init.orthogonal_, torch.nn.LeakyReLU, "cpu")
+    pol = Gaussian_AC_Policy(Box(), rep, [256], [256], None, torch.nn.init.orthogonal_, torch.nn.LeakyReLU, "cpu")
+    before = {k: v.clone() for k, v in pol.state_dict().items()}
+    groups = head_placement(pol)
+    assert len(groups) == 2
+    fs = FlatState(pol.parameters(), placement=groups)
+    assert [id(p) for p in fs.params] == [id(p) for p in pol.parameters()]
+    assert all(o % ALIGN == 0 for o in fs.offsets)
+    for g in groups:
+        pv, gv = fs.span(g)
+        assert pv.numel() == sum(p.numel() for p in g)
+        assert pv.data_ptr() == g[0].data_ptr() and gv.data_ptr() == g[0].grad.data_ptr()
+    assert fs.span([groups[0][1], groups[0][0]]) is None   # wrong order is not back to back
+    for k, v in pol.state_dict().items():
+        assert torch.equal(v, before[k]), k
+    # offsets are unique and do not overlap
+    spans = sorted((o, o + p.numel()) for p, o in zip(fs.params, fs.offsets))
+    assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:]))

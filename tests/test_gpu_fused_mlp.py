@@ -71,6 +71,13 @@ def test_explicit_backward_matches_autograd(discrete, act, rep_hidden):
     x = torch.randn(B, D, device=DEV)
     dh = torch.randn(B, A, device=DEV) * 1e-3
     dv = torch.randn(B, device=DEV) * 1e-3
+    import copy
+    p3 = copy.deepcopy(p1).double()   # fp64 truth for the gradient check
+    rep3 = p3.representation.model if rep_hidden else torch.nn.Identity()   # Basic_MLP casts to f32: run
+    s3 = rep3(x.double())                                                 # the Sequential chains directly
+    h3 = (p3.actor.model if discrete else p3.actor.mu)(s3)
+    v3 = p3.critic.model(s3)[:, 0]
+    torch.autograd.backward([h3, v3], [dh.double(), dv.double()])
     head, logstd, v = p1.heads(x)
     tensors, grads = [head, v], [dh, dv]
     torch.autograd.backward(tensors, grads)
@@ -83,19 +90,24 @@ def test_explicit_backward_matches_autograd(discrete, act, rep_hidden):
     if ls2 is not None:
         ls2.grad.zero_()   # logstd's gradient comes from the loss finalize, not from this backward
     fm.backward(ctx, dh.clone(), dv.clone())
-    for (n1, a), (n2, b) in zip(p1.named_parameters(), p2.named_parameters()):
+    # random-sign head gradients summed over 65536 rows cancel heavily, so two fp32 summation orders
+    # differ well above 1e-5 relative; the bar is: no further from the fp64 gradient than torch's own
+    # fp32 autograd (x2), or within 2e-5 of the gradient's scale
+    for (n1, a), (n2, b), (n3, c) in zip(p1.named_parameters(), p2.named_parameters(), p3.named_parameters()):
         if n1.endswith("logstd"):
             continue
-        ga, gb = a.grad.double(), b.grad.double()
-        scale = ga.abs().max().item() + 1e-12
-        assert (ga - gb).abs().max().item() <= 2e-5 * scale, (n1, (ga - gb).abs().max().item(), scale)
+        ga, gb, gc = a.grad.double(), b.grad.double(), c.grad
+        scale = gc.abs().max().item() + 1e-12
+        e_torch = (ga - gc).abs().max().item()
+        e_ours = (gb - gc).abs().max().item()
+        assert e_ours <= max(2 * e_torch, 2e-5 * scale), (n1, e_ours, e_torch, scale)
 
 
-@pytest.mark.parametrize("algo,discrete,act,rep_hidden,ent", [
-    ("ppo", False, torch.nn.LeakyReLU, [256], 0.0), ("ppo", True, torch.nn.LeakyReLU, [256], 0.01),
-    ("a2c", False, torch.nn.Tanh, [64], 0.005), ("a2c", True, torch.nn.ReLU, [], 0.01),
-    ("ppo", False, torch.nn.LeakyReLU, [], 0.0)])
-def test_fused_heads_match_loss_kernel_path(algo, discrete, act, rep_hidden, ent):
+@pytest.mark.parametrize("algo,discrete,act,rep_hidden,ent,paired", [
+    ("ppo", False, torch.nn.LeakyReLU, [256], 0.0, True), ("ppo", False, torch.nn.LeakyReLU, [256], 0.0, False),
+    ("ppo", True, torch.nn.LeakyReLU, [256], 0.01, True), ("a2c", False, torch.nn.Tanh, [64], 0.005, True),
+    ("a2c", True, torch.nn.ReLU, [], 0.01, False), ("ppo", False, torch.nn.LeakyReLU, [], 0.0, True)])
+def test_fused_heads_match_loss_kernel_path(algo, discrete, act, rep_hidden, ent, paired):
     """K12 (heads + loss + head backward in one pass) == K2 loss kernel + explicit backward, which the
     drop-in tests pin to the reference's fixtures: loss scalars and every parameter gradient."""
     from xuanpolicy_amd import ops
@@ -106,9 +118,11 @@ def test_fused_heads_match_loss_kernel_path(algo, discrete, act, rep_hidden, ent
     p1 = _policy(D, A, discrete, act, rep_hidden)
     p2 = _policy(D, A, discrete, act, rep_hidden)
     p2.load_state_dict(p1.state_dict())
-    fs1, fs2 = FlatState(p1.parameters()), FlatState(p2.parameters())
-    fm1, fm2 = FusedActorCritic(p1), FusedActorCritic(p2)
-    assert fm2.fused_heads
+    from xuanpolicy_amd.fused_mlp import head_placement
+    fs1 = FlatState(p1.parameters())
+    fs2 = FlatState(p2.parameters(), placement=head_placement(p2) if paired else None)
+    fm1, fm2 = FusedActorCritic(p1), FusedActorCritic(p2, flat=fs2)
+    assert fm2.fused_heads and (fm2.pair is not None) == paired
     obs_all = torch.randn(R, D, device=DEV)
     idx = torch.randperm(R, device=DEV)[:B].contiguous()
     idx[5] = R + 3          # invalid rows contribute nothing
@@ -147,3 +161,65 @@ def test_fused_heads_match_loss_kernel_path(algo, discrete, act, rep_hidden, ent
         scale = ga.abs().max().item() + 1e-12
         assert (ga - gb).abs().max().item() <= 5e-5 * scale, (n1, (ga - gb).abs().max().item(), scale)
         assert not bool((x2.grad == -7.0).any()), n2   # every gradient written
+
+
+@pytest.mark.parametrize("rows,din,code", [(1000, 17, 1), (65536 + 5, 17, 1), (77, 4, 2), (4096, 33, 0),
+                                           (3000, 64, 1), (129, 8, 2)])
+def test_thin_first_layer_kernels(rows, din, code):
+    """K13 forward / backward vs torch fp32 (F.linear + activation, autograd)."""
+    from xuanpolicy_amd import ops
+    L = ops.lib()
+    torch.manual_seed(rows + din)
+    slope = 0.01
+    x = torch.randn(rows, din, device=DEV)
+    lin = torch.nn.Linear(din, 256).to(DEV)
+    act = {0: lambda z: z, 1: lambda z: torch.nn.functional.leaky_relu(z, slope), 2: torch.tanh}[code]
+    xr = x.clone().requires_grad_(False)
+    h_ref = act(torch.nn.functional.linear(xr, lin.weight, lin.bias))
+    h = torch.empty(rows, 256, device=DEV)
+    s = ops._stream()
+    assert L.xpa_thin_linear_act_fwd(code, ops._p(x), din, rows, din, 256, ops._p(lin.weight), ops._p(lin.bias),
+                                     slope, ops._p(h), 256, s) == 0
+    torch.testing.assert_close(h, h_ref.detach(), rtol=1e-5, atol=1e-5)
+    g = torch.randn(rows, 256, device=DEV) * 1e-2
+    h_ref.backward(g)
+    G = int(L.xpa_thin_bwd_num_partials(rows))
+    pdw = torch.empty(G, 256 * din, device=DEV)
+    pdb = torch.empty(G, 256, device=DEV)
+    dw = torch.empty(256, din, device=DEV)
+    db = torch.empty(256, device=DEV)
+    assert L.xpa_thin_linear_act_bwd(code, ops._p(g), 256, ops._p(h), 256, rows, ops._p(x), din, din, 256, slope,
+                                     ops._p(pdw), ops._p(pdb), s) == 0
+    assert L.xpa_colsum_finalize(ops._p(pdw), G, 256 * din, ops._p(dw), s) == 0
+    assert L.xpa_colsum_finalize(ops._p(pdb), G, 256, ops._p(db), s) == 0
+    for got, exp in ((dw, lin.weight.grad), (db, lin.bias.grad)):
+        scale = exp.abs().max().item()
+        assert (got - exp).abs().max().item() <= 2e-5 * scale + 1e-6
+    # invalid arguments launch nothing
+    assert L.xpa_thin_linear_act_fwd(code, ops._p(x), din, rows, 65, 256, ops._p(lin.weight), ops._p(lin.bias),
+                                     slope, ops._p(h), 256, s) != 0
+
+
+def test_colsum_finalize_batch_matches_single():
+    """xpa_colsum_finalize_batch == per-segment xpa_colsum_finalize (bitwise: same fixed-order f64 sums),
+    more segments than one launch holds."""
+    from xuanpolicy_amd import ops
+    L = ops.lib()
+    torch.manual_seed(3)
+    shapes = [(512, 1536), (512, 6), (256, 4352), (1, 3), (700, 1), (64, 256)] * 3
+    q = ops.ColsumQueue()
+    outs, refs = [], []
+    s = ops._stream()
+    for G, C in shapes:
+        part = torch.randn(G, C, device=DEV)
+        out = torch.full((C,), 9.0, device=DEV)
+        ref = torch.empty(C, device=DEV)
+        assert L.xpa_colsum_finalize(ops._p(part), G, C, ops._p(ref), s) == 0
+        q.add(part, out)
+        outs.append(out)
+        refs.append(ref)
+    q.flush()
+    q.items = [(torch.zeros(2, 2, device=DEV), torch.zeros(2, device=DEV))]
+    q.flush()                      # a second plan
+    for o, r in zip(outs, refs):
+        assert torch.equal(o, r)

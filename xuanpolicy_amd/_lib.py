@@ -16,7 +16,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "libxuanpolicy_amd.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
-SOURCES = ["gae.hip", "loss.hip", "rollout.hip", "optim.hip", "mlp.hip", "head.hip"]
+SOURCES = ["gae.hip", "loss.hip", "rollout.hip", "optim.hip", "mlp.hip", "head.hip", "thin.hip"]
 HEADER = os.path.join(REPO_DIR, "include", "xuanpolicy_amd.h")
 
 ABI_VERSION = 1
@@ -52,11 +52,18 @@ SIGNATURES = {
     "xpa_head_backward": (ctypes.c_int, [ctypes.c_int, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_f32, c_p, c_p, c_p,
                                          c_p, c_p]),
     "xpa_head_fused_num_partials": (c_i64, [c_i64]),
-    "xpa_head_fused_actor": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_p, c_p,
+    "xpa_head_fused_actor": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_i64, c_i64, c_p, c_p,
+                                            c_p,
                                             c_f32, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_f32, c_f32, c_p, c_p,
                                             c_p, c_p, c_p, c_i64, c_p]),
-    "xpa_head_fused_critic": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_p, c_p, c_p, c_f32, c_p, c_i64, c_p, c_f32,
+    "xpa_head_fused_critic": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_f32, c_p, c_i64, c_p, c_f32,
                                              c_p, c_p, c_p, c_p, c_p, c_i64, c_p]),
+    "xpa_colsum_finalize_batch": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p]),
+    "xpa_thin_bwd_num_partials": (c_i64, [c_i64]),
+    "xpa_thin_linear_act_fwd": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f32, c_p, c_i64,
+                                               c_p]),
+    "xpa_thin_linear_act_bwd": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_f32,
+                                               c_p, c_p, c_p]),
     "xpa_grad_norm_num_partials": (c_i64, [c_i64]),
     "xpa_clip_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_p, c_f32, c_f32, c_f32, c_f32, c_f32, c_i64, c_p,
                                           c_p]),

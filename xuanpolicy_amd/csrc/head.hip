@@ -7,7 +7,8 @@
 // (ppoclip_learner.py:32-44, a2c_learner.py:24-31, distributions.py:39-101) and the backward down to the
 // hidden pre-activation (torch autograd in loss.backward(), ppoclip_learner.py:46).
 //
-// Outputs: dz [batch, 256]; per-block partials dW_o [K*256], db_h [256], db_o [K] (reduced by
+// z and dz rows have stride ld (>= 256, multiple of 4: e.g. the halves of a [batch, 512] actor|critic
+// pair).  Outputs: dz [batch, 256]; per-block partials dW_o [K*256], db_h [256], db_o [K] (reduced by
 // xpa_colsum_finalize) and one row of the K2 loss-partials layout (surrogate, sq-err, entropy, clip
 // count, value sum, dlogstd[K]; reduced by xpa_policy_loss_finalize).  The actor launch fills the actor
 // columns, the critic launch the critic columns of the same partials array.
@@ -74,6 +75,7 @@ constexpr int kGridMax = 512;  // 2 blocks per CU (77 KiB LDS each) x 256 CUs
 struct HeadArgs {
     int64_t batch;
     int K;
+    int64_t ld;
     const float *z;
     const float *W;
     const float *bias;
@@ -92,13 +94,14 @@ struct HeadArgs {
     int loss_width;
 };
 
-__device__ __forceinline__ void load_tile(float4 (&zq)[16], const float *__restrict__ z, int64_t tile, int64_t batch) {
+__device__ __forceinline__ void load_tile(float4 (&zq)[16], const float *__restrict__ z, int64_t ld, int64_t tile,
+                                          int64_t batch) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int lin = i * 256 + (int)threadIdx.x;
         const int64_t row = tile * kTile + (lin >> 6);
         if (row < batch) {
-            const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(z + row * kH) + (lin & 63));
+            const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(z + row * ld) + (lin & 63));
             zq[i] = make_float4(v.x, v.y, v.z, v.w);
         } else {
             zq[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -109,7 +112,7 @@ __device__ __forceinline__ void load_tile(float4 (&zq)[16], const float *__restr
 // MODE: 0 Gaussian actor, 1 Categorical actor, 2 critic.  ALGO: 0 PPO, 1 A2C (actor only).
 template <int MODE, int ALGO, int ACT, int KMAX>
 __global__ __launch_bounds__(256, 2) void head_tile_kernel(
-    int64_t batch, int K_in, const float *__restrict__ z, const float *__restrict__ W, const float *__restrict__ bias,
+    int64_t batch, int K_in, int64_t ld, const float *__restrict__ z, const float *__restrict__ W, const float *__restrict__ bias,
     float slope, const float *__restrict__ logstd, const int64_t *__restrict__ idx, int64_t n_rows,
     const float *__restrict__ act, const float *__restrict__ old_logp, const float *__restrict__ adv,
     const float *__restrict__ ret, const double *__restrict__ adv_partials, int64_t n_adv_partials, float clip_range,
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(
     const int64_t ntiles = (batch + kTile - 1) / kTile;
     int64_t tile = blockIdx.x;
     float4 zq[16];
-    load_tile(zq, z, tile, batch);
+    load_tile(zq, z, ld, tile, batch);
 
     // phase-2 constants / accumulators (column t)
     float wc[KMAX], acc_dw[KMAX];
@@ -198,7 +201,7 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(
         }
         __syncthreads();
         const int64_t next = tile + gridDim.x;
-        if (next < ntiles) load_tile(zq, z, next, batch);  // in flight during phases 1-2
+        if (next < ntiles) load_tile(zq, z, ld, next, batch);  // in flight during phases 1-2
         // ---- phase 1: partial dot products, row = lane, quarter = wave ----
         {
             float p[KMAX];
@@ -315,7 +318,7 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(
         __syncthreads();
         // ---- phase 2: column owner t ----
         const int nr = (int)min((int64_t)kTile, batch - tile * kTile);
-        float *dzt = dz + tile * kTile * kH + t;
+        float *dzt = dz + tile * kTile * ld + t;
         for (int r = 0; r < nr; ++r) {
             const float h = s_h[r * kS + t];
             float d = 0.f;
@@ -326,7 +329,7 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(
                 acc_dw[o] += g * h;
             }
             d *= act_g<ACT>(h, slope);
-            __builtin_nontemporal_store(d, dzt + r * kH);
+            __builtin_nontemporal_store(d, dzt + r * ld);
             acc_dbh += d;
         }
         __syncthreads();  // s_h / s_dh reused by the next tile
@@ -377,7 +380,7 @@ XPA_API int64_t xpa_head_fused_num_partials(int64_t batch) {
 }
 
 namespace {
-#define XPA_HEAD_ARGS(a) a.batch, a.K, a.z, a.W, a.bias, a.slope, a.logstd, a.idx, a.n_rows, a.act, a.old_logp, a.adv, a.ret, a.adv_partials, a.n_adv_partials, a.clip_range, a.ent_coef, a.vf_coef, a.dz, a.p_dw, a.p_dbh, a.p_dbo, a.p_loss, a.loss_width
+#define XPA_HEAD_ARGS(a) a.batch, a.K, a.ld, a.z, a.W, a.bias, a.slope, a.logstd, a.idx, a.n_rows, a.act, a.old_logp, a.adv, a.ret, a.adv_partials, a.n_adv_partials, a.clip_range, a.ent_coef, a.vf_coef, a.dz, a.p_dw, a.p_dbh, a.p_dbo, a.p_loss, a.loss_width
 template <int MODE, int ALGO>
 void launch_head(const HeadArgs &a, int act_code, hipStream_t s) {
     const dim3 grid((unsigned)xpa_head_fused_num_partials(a.batch)), block(256);
@@ -399,7 +402,7 @@ void launch_head(const HeadArgs &a, int act_code, hipStream_t s) {
 }  // namespace
 
 XPA_API int xpa_head_fused_actor(int algo, int dist, int act_code, int64_t batch, int64_t act_dim, int64_t hidden,
-                                 const float *z, const float *w, const float *b, float slope, const float *logstd,
+                                 int64_t ld, const float *z, const float *w, const float *b, float slope, const float *logstd,
                                  const int64_t *idx, int64_t n_rows, const float *act, const float *old_logp,
                                  const float *adv, const double *adv_partials, int64_t n_adv_partials,
                                  float clip_range, float ent_coef, float *dz, float *partial_dw,
@@ -414,9 +417,9 @@ XPA_API int xpa_head_fused_actor(int algo, int dist, int act_code, int64_t batch
     if ((dist == XPA_DIST_GAUSSIAN && !logstd) || (algo == XPA_ALGO_PPO && !old_logp) ||
         (dist == XPA_DIST_CATEGORICAL && act_dim < 2))
         return (int)hipErrorInvalidValue;
-    if (((uintptr_t)z | (uintptr_t)w) % 16) return (int)hipErrorInvalidValue;
+    if (((uintptr_t)z | (uintptr_t)w) % 16 || ld < kH || ld % 4) return (int)hipErrorInvalidValue;
     HeadArgs a{};
-    a.batch = batch; a.K = (int)act_dim; a.z = z; a.W = w; a.bias = b; a.slope = slope; a.logstd = logstd;
+    a.batch = batch; a.K = (int)act_dim; a.ld = ld; a.z = z; a.W = w; a.bias = b; a.slope = slope; a.logstd = logstd;
     a.idx = idx; a.n_rows = n_rows; a.act = act; a.old_logp = old_logp; a.adv = adv; a.ret = nullptr;
     a.adv_partials = adv_partials; a.n_adv_partials = n_adv_partials; a.clip_range = clip_range;
     a.ent_coef = ent_coef; a.vf_coef = 0.f; a.dz = dz; a.p_dw = partial_dw; a.p_dbh = partial_db_hidden;
@@ -432,7 +435,7 @@ XPA_API int xpa_head_fused_actor(int algo, int dist, int act_code, int64_t batch
     return xpa_launch_status();
 }
 
-XPA_API int xpa_head_fused_critic(int act_code, int64_t batch, int64_t hidden, const float *z, const float *w,
+XPA_API int xpa_head_fused_critic(int act_code, int64_t batch, int64_t hidden, int64_t ld, const float *z, const float *w,
                                   const float *b, float slope, const int64_t *idx, int64_t n_rows, const float *ret,
                                   float vf_coef, float *dz, float *partial_dw, float *partial_db_hidden,
                                   float *partial_db_out, float *loss_partials, int64_t loss_width,
@@ -441,9 +444,9 @@ XPA_API int xpa_head_fused_critic(int act_code, int64_t batch, int64_t hidden, c
         !partial_db_hidden || !partial_db_out || !loss_partials || loss_width < kPartBase || n_rows <= 0 ||
         (!idx && n_rows < batch))
         return (int)hipErrorInvalidValue;
-    if (((uintptr_t)z | (uintptr_t)w) % 16) return (int)hipErrorInvalidValue;
+    if (((uintptr_t)z | (uintptr_t)w) % 16 || ld < kH || ld % 4) return (int)hipErrorInvalidValue;
     HeadArgs a{};
-    a.batch = batch; a.K = 1; a.z = z; a.W = w; a.bias = b; a.slope = slope; a.idx = idx; a.n_rows = n_rows;
+    a.batch = batch; a.K = 1; a.ld = ld; a.z = z; a.W = w; a.bias = b; a.slope = slope; a.idx = idx; a.n_rows = n_rows;
     a.ret = ret; a.vf_coef = vf_coef; a.dz = dz; a.p_dw = partial_dw; a.p_dbh = partial_db_hidden;
     a.p_dbo = partial_db_out; a.p_loss = loss_partials; a.loss_width = (int)loss_width;
     launch_head<2, 0>(a, act_code, (hipStream_t)stream);

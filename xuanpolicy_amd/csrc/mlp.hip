@@ -245,6 +245,29 @@ __global__ __launch_bounds__(256) void colsum_finalize_kernel(const float *__res
     if (lane == 0) out[w] = (float)s;
 }
 
+constexpr int kMaxSegs = 16;
+struct ColsumBatch {
+    const float *part[kMaxSegs];
+    float *out[kMaxSegs];
+    int64_t G[kMaxSegs];
+    int C[kMaxSegs];
+    int start[kMaxSegs + 1];  // first global column of each segment
+    int n;
+};
+
+__global__ __launch_bounds__(256) void colsum_finalize_batch_kernel(ColsumBatch b) {
+    const int w = (blockIdx.x * 256 + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+    if (w >= b.start[b.n]) return;
+    int sg = 0;
+    while (w >= b.start[sg + 1]) ++sg;
+    const int col = w - b.start[sg], C = b.C[sg];
+    const float *__restrict__ part = b.part[sg];
+    double s = 0.0;
+    for (int64_t k = lane; k < b.G[sg]; k += 64) s += (double)part[k * C + col];
+    s = xpa_wave_sum(s);
+    if (lane == 0) b.out[sg][col] = (float)s;
+}
+
 }  // namespace
 
 XPA_API int64_t xpa_act_bwd_num_partials(int64_t rows) { return (rows + kRowsPerBlock - 1) / kRowsPerBlock; }
@@ -333,5 +356,27 @@ XPA_API int xpa_colsum_finalize(const float *partials, int64_t n_partials, int64
     const unsigned blocks = (unsigned)((cols * 64 + 255) / 256);
     hipLaunchKernelGGL(colsum_finalize_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, partials, n_partials,
                        (int)cols, out);
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_colsum_finalize_batch(int n_segs, const float *const *partials, const int64_t *n_partials,
+                                      const int64_t *cols, float *const *outs, xpa_stream_t stream) {
+    if (n_segs <= 0 || n_segs > kMaxSegs || !partials || !n_partials || !cols || !outs) return (int)hipErrorInvalidValue;
+    ColsumBatch b{};
+    b.n = n_segs;
+    int64_t total = 0;
+    for (int i = 0; i < n_segs; ++i) {
+        if (!partials[i] || !outs[i] || n_partials[i] <= 0 || cols[i] <= 0) return (int)hipErrorInvalidValue;
+        b.part[i] = partials[i];
+        b.out[i] = outs[i];
+        b.G[i] = n_partials[i];
+        b.C[i] = (int)cols[i];
+        b.start[i] = (int)total;
+        total += cols[i];
+        if (total > (1 << 24)) return (int)hipErrorInvalidValue;
+    }
+    b.start[n_segs] = (int)total;
+    const unsigned blocks = (unsigned)((total * 64 + 255) / 256);
+    hipLaunchKernelGGL(colsum_finalize_batch_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, b);
     return xpa_launch_status();
 }

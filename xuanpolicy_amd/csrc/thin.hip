@@ -1,0 +1,227 @@
+// K13 — the representation's first layer, Linear(d_in, 256) + activation with a small d_in (the
+// observation width: 17 for the C2 MuJoCo shape), forward and backward as streaming kernels (gfx950).
+//
+// Reference: Basic_MLP's first mlp_block (xuance/torch/representations/mlp.py:21-51,
+// xuance/torch/utils/layers.py:8-24); forward in policy(obs) and backward in loss.backward()
+// (ppoclip_learner.py:30-46).  With K = d_in <= 64 the GEMM has ~17 FMAs per output element, so the
+// layer is bound by HBM (writing / re-reading the [B, 256] activations), not by the matrix cores.
+//
+//   forward : h[b, c] = act(sum_k x[b, k] W[c, k] + bias[c])      (writes h: 1 KiB per row)
+//   backward: dz = g * act'(h);  dW[c, k] = sum_b dz[b, c] x[b, k];  db[c] = sum_b dz[b, c]
+//             (reads g and h: 2 KiB per row; dz itself is never stored — nothing below the first
+//             layer needs it)
+// Mapping: 256 threads, thread t owns output column t (its d_in weights / accumulators in registers);
+// a block walks 64-row tiles (grid-stride); the tile's x rows are staged in LDS and read as
+// wave-uniform broadcasts; h / g rows are read and written as whole coalesced 1-KiB rows.
+#include "xpa_common.h"
+
+namespace {
+
+constexpr int kCols = 256;
+constexpr int kTile = 64;
+constexpr int kMaxIn = 64;
+constexpr int kFwdGrid = 1024;
+constexpr int kBwdGrid = 256;
+
+template <int ACT>
+__device__ __forceinline__ float act_f(float z, float slope) {
+    if (ACT == 1) return z > 0.f ? z : z * slope;
+    if (ACT == 2) return tanhf(z);
+    return z;
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_g(float h, float slope) {
+    if (ACT == 1) return h > 0.f ? 1.f : slope;
+    if (ACT == 2) return 1.0f - h * h;
+    return 1.f;
+}
+
+template <int ACT, int DMAX>
+__global__ __launch_bounds__(256) void thin_fwd_kernel(const float *__restrict__ x, int64_t ldx, int64_t rows, int din,
+                                                       const float *__restrict__ W, const float *__restrict__ bias,
+                                                       float slope, float *__restrict__ h, int64_t ldh) {
+    constexpr int kPad = DMAX + 4;  // row stride of the staged x tile (16-B aligned rows)
+    __shared__ __attribute__((aligned(16))) float s_x[kTile * kPad];
+    const int t = threadIdx.x;
+    float w[DMAX];
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) w[k] = k < din ? W[t * din + k] : 0.f;
+    const float bc = bias[t];
+    const int64_t ntiles = (rows + kTile - 1) / kTile;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t r0 = tile * kTile;
+        __syncthreads();
+        // zero-padded columns din..DMAX-1 stay 0 from this loop's (r, k < DMAX) writes
+        for (int i = t; i < kTile * DMAX; i += 256) {
+            const int r = i / DMAX, k = i - r * DMAX;
+            s_x[r * kPad + k] = (k < din && r0 + r < rows) ? x[(r0 + r) * ldx + k] : 0.f;
+        }
+        __syncthreads();
+        const int nr = (int)min((int64_t)kTile, rows - r0);
+        for (int r = 0; r < nr; ++r) {
+            const float *xr = s_x + r * kPad;
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < DMAX; k += 4) {
+                const float4 xv = *reinterpret_cast<const float4 *>(xr + k);
+                acc = fmaf(xv.x, w[k], acc);
+                acc = fmaf(xv.y, w[k + 1], acc);
+                acc = fmaf(xv.z, w[k + 2], acc);
+                acc = fmaf(xv.w, w[k + 3], acc);
+            }
+            __builtin_nontemporal_store(act_f<ACT>(acc + bc, slope), h + (r0 + r) * ldh + t);
+        }
+    }
+}
+
+// 1024 threads = 4 groups of 256 (group = one 64-row tile at a time, thread = column), 8 rows of g / h
+// in flight per thread; the groups' accumulators are combined through LDS (fixed order) at the end.
+constexpr int kBwdGroups = 4;
+constexpr int kBwdU = 8;
+
+template <int ACT, int DMAX>
+__global__ __launch_bounds__(1024) void thin_bwd_kernel(const float *__restrict__ g, int64_t ldg,
+                                                        const float *__restrict__ h, int64_t ldh, int64_t rows,
+                                                        const float *__restrict__ x, int64_t ldx, int din, float slope,
+                                                        float *__restrict__ partial_dw, float *__restrict__ partial_db) {
+    constexpr int kPad = DMAX + 4;
+    constexpr int kXs = kTile * kPad;                                        // one group's x tile
+    constexpr int kLds = kBwdGroups * kXs > kCols * (DMAX + 1) ? kBwdGroups * kXs : kCols * (DMAX + 1);
+    __shared__ __attribute__((aligned(16))) float s_buf[kLds];
+    const int grp = threadIdx.x >> 8, t = threadIdx.x & 255;
+    float *s_x = s_buf + grp * kXs;
+    float acc[DMAX];
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) acc[k] = 0.f;
+    float accb = 0.f;
+    const int64_t ntiles = (rows + kTile - 1) / kTile;
+    for (int64_t base = (int64_t)blockIdx.x * kBwdGroups; base < ntiles; base += (int64_t)gridDim.x * kBwdGroups) {
+        const int64_t tile = base + grp;  // uniform trip count for the whole block (barriers)
+        const int64_t r0 = tile * kTile;
+        __syncthreads();
+        if (tile < ntiles) {
+            for (int i = t; i < kTile * DMAX; i += 256) {
+                const int r = i / DMAX, k = i - r * DMAX;
+                s_x[r * kPad + k] = (k < din && r0 + r < rows) ? x[(r0 + r) * ldx + k] : 0.f;
+            }
+        }
+        __syncthreads();
+        if (tile >= ntiles) continue;
+        const int nr = (int)min((int64_t)kTile, rows - r0);
+        int r = 0;
+        for (; r + kBwdU <= nr; r += kBwdU) {
+            float gv[kBwdU], hv[kBwdU];
+#pragma unroll
+            for (int u = 0; u < kBwdU; ++u) {
+                gv[u] = __builtin_nontemporal_load(g + (r0 + r + u) * ldg + t);
+                hv[u] = __builtin_nontemporal_load(h + (r0 + r + u) * ldh + t);
+            }
+#pragma unroll
+            for (int u = 0; u < kBwdU; ++u) {
+                const float dz = gv[u] * act_g<ACT>(hv[u], slope);
+                accb += dz;
+                const float *xr = s_x + (r + u) * kPad;
+#pragma unroll
+                for (int k = 0; k < DMAX; k += 4) {
+                    const float4 xv = *reinterpret_cast<const float4 *>(xr + k);
+                    acc[k] = fmaf(dz, xv.x, acc[k]);
+                    acc[k + 1] = fmaf(dz, xv.y, acc[k + 1]);
+                    acc[k + 2] = fmaf(dz, xv.z, acc[k + 2]);
+                    acc[k + 3] = fmaf(dz, xv.w, acc[k + 3]);
+                }
+            }
+        }
+        for (; r < nr; ++r) {
+            const float dz = g[(r0 + r) * ldg + t] * act_g<ACT>(h[(r0 + r) * ldh + t], slope);
+            accb += dz;
+            const float *xr = s_x + r * kPad;
+#pragma unroll
+            for (int k = 0; k < DMAX; ++k) acc[k] = fmaf(dz, xr[k], acc[k]);
+        }
+    }
+    // combine groups 1..3 into group 0 (fixed order), through LDS [256][DMAX + 1]
+    for (int src = 1; src < kBwdGroups; ++src) {
+        __syncthreads();
+        if (grp == src) {
+#pragma unroll
+            for (int k = 0; k < DMAX; ++k) s_buf[t * (DMAX + 1) + k] = acc[k];
+            s_buf[t * (DMAX + 1) + DMAX] = accb;
+        }
+        __syncthreads();
+        if (grp == 0) {
+#pragma unroll
+            for (int k = 0; k < DMAX; ++k) acc[k] += s_buf[t * (DMAX + 1) + k];
+            accb += s_buf[t * (DMAX + 1) + DMAX];
+        }
+    }
+    if (grp != 0) return;
+    // partial row layout = the weight layout [256, din] (row-major), so a column sum over the
+    // partials lands directly in W.grad
+    float *pw = partial_dw + (int64_t)blockIdx.x * kCols * din + (int64_t)t * din;
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k)
+        if (k < din) pw[k] = acc[k];
+    partial_db[(int64_t)blockIdx.x * kCols + t] = accb;
+}
+
+template <int ACT>
+void launch_fwd(int dmax, dim3 grid, hipStream_t s, const float *x, int64_t ldx, int64_t rows, int din,
+                const float *W, const float *b, float slope, float *h, int64_t ldh) {
+    if (dmax == 8) hipLaunchKernelGGL((thin_fwd_kernel<ACT, 8>), grid, dim3(256), 0, s, x, ldx, rows, din, W, b, slope, h, ldh);
+    else if (dmax == 20) hipLaunchKernelGGL((thin_fwd_kernel<ACT, 20>), grid, dim3(256), 0, s, x, ldx, rows, din, W, b, slope, h, ldh);
+    else if (dmax == 32) hipLaunchKernelGGL((thin_fwd_kernel<ACT, 32>), grid, dim3(256), 0, s, x, ldx, rows, din, W, b, slope, h, ldh);
+    else hipLaunchKernelGGL((thin_fwd_kernel<ACT, 64>), grid, dim3(256), 0, s, x, ldx, rows, din, W, b, slope, h, ldh);
+}
+
+template <int ACT>
+void launch_bwd(int dmax, dim3 grid, hipStream_t s, const float *g, int64_t ldg, const float *h, int64_t ldh,
+                int64_t rows, const float *x, int64_t ldx, int din, float slope, float *pdw, float *pdb) {
+#define XPA_BWD(D_) \
+    hipLaunchKernelGGL((thin_bwd_kernel<ACT, D_>), grid, dim3(1024), 0, s, g, ldg, h, ldh, rows, x, ldx, din, slope, pdw, pdb)
+    if (dmax == 8) XPA_BWD(8);
+    else if (dmax == 20) XPA_BWD(20);
+    else if (dmax == 32) XPA_BWD(32);
+    else XPA_BWD(64);
+#undef XPA_BWD
+}
+
+int dmax_for(int din) { return din <= 8 ? 8 : din <= 20 ? 20 : din <= 32 ? 32 : 64; }
+
+}  // namespace
+
+XPA_API int64_t xpa_thin_bwd_num_partials(int64_t rows) {
+    const int64_t blocks = ((rows + kTile - 1) / kTile + 3) / 4;  // 4 tiles per block-iteration
+    return blocks < kBwdGrid ? (blocks > 0 ? blocks : 1) : kBwdGrid;
+}
+
+XPA_API int xpa_thin_linear_act_fwd(int act, const float *x, int64_t ldx, int64_t rows, int64_t d_in, int64_t d_out,
+                                    const float *w, const float *b, float slope, float *h, int64_t ldh,
+                                    xpa_stream_t stream) {
+    if (rows <= 0 || d_in < 1 || d_in > kMaxIn || d_out != kCols || act < 0 || act > 2 || !x || !w || !b || !h ||
+        ldx < d_in || ldh < d_out)
+        return (int)hipErrorInvalidValue;
+    const int64_t tiles = (rows + kTile - 1) / kTile;
+    const dim3 grid((unsigned)(tiles < kFwdGrid ? tiles : kFwdGrid));
+    hipStream_t s = (hipStream_t)stream;
+    const int dm = dmax_for((int)d_in);
+    if (act == 0) launch_fwd<0>(dm, grid, s, x, ldx, rows, (int)d_in, w, b, slope, h, ldh);
+    else if (act == 1) launch_fwd<1>(dm, grid, s, x, ldx, rows, (int)d_in, w, b, slope, h, ldh);
+    else launch_fwd<2>(dm, grid, s, x, ldx, rows, (int)d_in, w, b, slope, h, ldh);
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_thin_linear_act_bwd(int act, const float *g, int64_t ldg, const float *h, int64_t ldh, int64_t rows,
+                                    const float *x, int64_t ldx, int64_t d_in, int64_t d_out, float slope,
+                                    float *partial_dw, float *partial_db, xpa_stream_t stream) {
+    if (rows <= 0 || d_in < 1 || d_in > kMaxIn || d_out != kCols || act < 0 || act > 2 || !g || !h || !x ||
+        !partial_dw || !partial_db || ldg < d_out || ldh < d_out || ldx < d_in)
+        return (int)hipErrorInvalidValue;
+    const dim3 grid((unsigned)xpa_thin_bwd_num_partials(rows));
+    hipStream_t s = (hipStream_t)stream;
+    const int dm = dmax_for((int)d_in);
+    if (act == 0) launch_bwd<0>(dm, grid, s, g, ldg, h, ldh, rows, x, ldx, (int)d_in, slope, partial_dw, partial_db);
+    else if (act == 1) launch_bwd<1>(dm, grid, s, g, ldg, h, ldh, rows, x, ldx, (int)d_in, slope, partial_dw, partial_db);
+    else launch_bwd<2>(dm, grid, s, g, ldg, h, ldh, rows, x, ldx, (int)d_in, slope, partial_dw, partial_db);
+    return xpa_launch_status();
+}

@@ -41,7 +41,8 @@ class GradAllReduce:
 def attach_flat_grads(learner, allreduce=True, group=None, fused_optimizer=True):
     """Give a learner flat parameters/gradients, the fused clip+Adam step when its optimizer allows,
     and the all-reduce hook when a process group of more than one rank is initialised."""
-    fs = FlatState(learner.policy.parameters())
+    from .fused_mlp import head_placement
+    fs = FlatState(learner.policy.parameters(), placement=head_placement(learner.policy))
     learner.flat_grads = fs
     learner._params = fs.params
     if fused_optimizer and fused_adam_compatible(learner.optimizer):

@@ -22,13 +22,30 @@ def _aligned(n):
 
 
 class FlatState:
-    def __init__(self, params):
+    """params: the parameters (their order is kept in .params / .offsets).  placement: optional groups
+    of parameters laid out back to back in the given order (each member but the last a multiple of
+    ALIGN elements), so a group can be used as one tensor — e.g. the actor and critic hidden layers
+    that read the same input become one [512, 256] weight (fused_mlp.head_placement)."""
+
+    def __init__(self, params, placement=None):
         self.params = [p for p in params if p.requires_grad]
-        self.offsets = []
+        index = {id(p): i for i, p in enumerate(self.params)}
+        group_of = {}
+        for g in placement or []:
+            ok = (all(id(p) in index for p in g) and len(set(id(p) for p in g)) == len(g)
+                  and all(p.numel() % ALIGN == 0 for p in g[:-1]) and not any(id(p) in group_of for p in g))
+            if ok:
+                for p in g:
+                    group_of[id(p)] = g
+        offsets = [None] * len(self.params)
         off = 0
         for p in self.params:
-            self.offsets.append(off)
-            off += _aligned(p.numel())
+            if offsets[index[id(p)]] is not None:
+                continue
+            for q in group_of.get(id(p), [p]):
+                offsets[index[id(q)]] = off
+                off += _aligned(q.numel())
+        self.offsets = offsets
         n = off
         dev = self.params[0].device
         self.numel = n
@@ -44,6 +61,21 @@ class FlatState:
 
     def zero_(self):
         self.flat.zero_()
+
+    def span(self, group):
+        """(param view, grad view) covering a placement group as one flat span, or None if the members
+        are not back to back."""
+        offs = []
+        for p in group:
+            i = next((k for k, q in enumerate(self.params) if q is p), None)
+            if i is None:
+                return None
+            offs.append((self.offsets[i], p.numel()))
+        for (o0, n0), (o1, _) in zip(offs, offs[1:]):
+            if o1 != o0 + n0:
+                return None
+        start, total = offs[0][0], sum(n for _, n in offs)
+        return self.param[start:start + total], self.flat[start:start + total]
 
     def ensure_views(self):
         """Re-point .grad at the flat buffer if anything replaced it (e.g. zero_grad(set_to_none=True))."""

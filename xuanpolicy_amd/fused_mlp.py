@@ -51,10 +51,32 @@ def _parse(seq):
     return layers
 
 
-class FusedActorCritic:
-    """Built from a Gaussian/Categorical actor-critic policy whose parameters live in a FlatState."""
+def _head_layers(policy):
+    discrete = bool(getattr(policy, "discrete", False))
+    actor = [m for m in (policy.actor.model if discrete else policy.actor.mu) if isinstance(m, nn.Linear)]
+    critic = [m for m in policy.critic.model if isinstance(m, nn.Linear)]
+    return actor, critic
 
-    def __init__(self, policy):
+
+def head_placement(policy):
+    """FlatState placement groups that let the actor's and the critic's hidden layer run as one
+    [512, in] layer: both heads must be [Linear(in, 256) + act] -> Linear(256, K) on the same input."""
+    try:
+        actor, critic = _head_layers(policy)
+    except AttributeError:
+        return []
+    if (len(actor) != 2 or len(critic) != 2 or actor[0].in_features != critic[0].in_features
+            or actor[0].out_features != ops.HEAD_HIDDEN or critic[0].out_features != ops.HEAD_HIDDEN
+            or actor[0].bias is None or critic[0].bias is None):
+        return []
+    return [[actor[0].weight, critic[0].weight], [actor[0].bias, critic[0].bias]]
+
+
+class FusedActorCritic:
+    """Built from a Gaussian/Categorical actor-critic policy whose parameters live in a FlatState
+    (pass it as `flat` to use the paired actor|critic hidden layer when head_placement applied)."""
+
+    def __init__(self, policy, flat=None):
         rep = policy.representation
         if isinstance(rep, Basic_MLP):
             self.rep = _parse(rep.model)
@@ -72,11 +94,24 @@ class FusedActorCritic:
         self.fused_heads = (self._head_fusable(self.actor) and self._head_fusable(self.critic)
                             and k <= 8 and (k >= 2 or not self.discrete))
         self._hws = None
+        # K13 for the first representation layer when its input is narrow (observation width <= 64)
+        self.thin0 = (len(self.rep) > 0 and self.rep[0][0].in_features <= 64
+                      and self.rep[0][0].out_features == ops.HEAD_HIDDEN)
+        self.pair = None
+        if self.fused_heads and flat is not None and len(self.actor) == 2 and len(self.critic) == 2:
+            la, lc = self.actor[0][0], self.critic[0][0]
+            if la.in_features == lc.in_features:
+                w = flat.span([la.weight, lc.weight])
+                b = flat.span([la.bias, lc.bias])
+                if w is not None and b is not None:
+                    n_in = la.in_features
+                    self.pair = (w[0].view(2 * ops.HEAD_HIDDEN, n_in), b[0], w[1].view(2 * ops.HEAD_HIDDEN, n_in), b[1])
         n_params = sum(1 for _ in policy.parameters())
         n_cov = 2 * (len(self.rep) + len(self.actor) + len(self.critic)) + (0 if self.discrete else 1)
         if n_params != n_cov:
             raise ValueError("policy has parameters outside the Linear chains")
         self._partials = {}
+        self._cq = ops.ColsumQueue()
 
     @staticmethod
     def _head_fusable(layers):
@@ -97,9 +132,39 @@ class FusedActorCritic:
             outs.append(h)
         return outs
 
+    def _rep_forward(self, x):
+        if self.thin0 and x.dim() == 2 and x.dtype == torch.float32 and x.stride(1) == 1:
+            lin, code, slope = self.rep[0]
+            h = torch.empty((x.shape[0], lin.out_features), dtype=torch.float32, device=x.device)
+            _lib.check(ops.lib().xpa_thin_linear_act_fwd(code, ops._p(x), x.stride(0), x.shape[0], lin.in_features,
+                                                         lin.out_features, ops._p(lin.weight), ops._p(lin.bias), slope,
+                                                         ops._p(h), h.stride(0), ops._stream(x.device)),
+                       "xpa_thin_linear_act_fwd")
+            return [h] + self._chain_forward(self.rep[1:], h)
+        return self._chain_forward(self.rep, x)
+
+    def _thin_backward(self, layer, g, h, x):
+        lin, code, slope = layer
+        rows, din = x.shape[0], lin.in_features
+        L = ops.lib()
+        key = ("thin", rows, din)
+        ws = self._partials.get(key)
+        if ws is None:
+            G = int(L.xpa_thin_bwd_num_partials(rows))
+            ws = (torch.empty((G, lin.out_features * din), device=g.device),
+                  torch.empty((G, lin.out_features), device=g.device))
+            self._partials[key] = ws
+        pdw, pdb = ws
+        s = ops._stream(g.device)
+        _lib.check(L.xpa_thin_linear_act_bwd(code, ops._p(g), g.stride(0), ops._p(h), h.stride(0), rows, ops._p(x),
+                                             x.stride(0), din, lin.out_features, slope, ops._p(pdw), ops._p(pdb), s),
+                   "xpa_thin_linear_act_bwd")
+        self._cq.add(pdw, lin.weight.grad)
+        self._cq.add(pdb, lin.bias.grad)
+
     @torch.no_grad()
     def forward(self, x):
-        rep_outs = self._chain_forward(self.rep, x)
+        rep_outs = self._rep_forward(x)
         s = rep_outs[-1] if rep_outs else x
         a_outs = self._chain_forward(self.actor, s)
         c_outs = self._chain_forward(self.critic, s)
@@ -109,8 +174,12 @@ class FusedActorCritic:
     @torch.no_grad()
     def forward_hidden(self, x):
         """Forward up to the heads' last hidden pre-activations (K12 does the rest)."""
-        rep_outs = self._chain_forward(self.rep, x)
+        rep_outs = self._rep_forward(x)
         s = rep_outs[-1] if rep_outs else x
+        if self.pair is not None:   # one GEMM for both hidden layers: [B, 512] = actor | critic
+            H = ops.HEAD_HIDDEN
+            z = F.linear(s, self.pair[0], self.pair[1])
+            return (x, rep_outs, s, (([], s, z[:, :H]), ([], s, z[:, H:])))
         heads = []
         for layers in (self.actor, self.critic):
             outs = self._chain_forward(layers[:-2], s)
@@ -131,8 +200,9 @@ class FusedActorCritic:
         lin_co, _, _ = self.critic[-1]
         lin_ch, c_code, c_slope = self.critic[-2]
         K = lin_ao.out_features
+        paired = self.pair is not None
         if self._hws is None or self._hws.batch != B:
-            self._hws = ops.HeadWorkspace(B, K, z_a.device)
+            self._hws = ops.HeadWorkspace(B, K, z_a.device, paired=paired)
         grads = {"w_actor": lin_ao.weight.grad, "b_actor": lin_ao.bias.grad, "bh_actor": lin_ah.bias.grad,
                  "w_critic": lin_co.weight.grad, "b_critic": lin_co.bias.grad, "bh_critic": lin_ch.bias.grad}
         if self.logstd is not None:
@@ -140,13 +210,23 @@ class FusedActorCritic:
         scalars, dz_a, dz_c = ops.fused_heads(algo, dist, self._hws, z_a, lin_ao.weight, lin_ao.bias, (a_code, a_slope),
                                               z_c, lin_co.weight, lin_co.bias, (c_code, c_slope), self.logstd, act,
                                               adv, ret, old_logp=old_logp, idx=idx, adv_partials=adv_partials,
-                                              clip_range=clip_range, vf_coef=vf_coef, ent_coef=ent_coef, grads=grads)
+                                              clip_range=clip_range, vf_coef=vf_coef, ent_coef=ent_coef, grads=grads,
+                                              colsum_queue=self._cq)
         have_rep = len(self.rep) > 0
+        if paired:   # dW of both hidden layers and dX (K = 512, no accumulate pass) as single GEMMs
+            dz = self._hws.dz_pair
+            self._weight_grad(dz, s, self.pair[2])
+            if have_rep:
+                self._chain_backward(self.rep, [x] + rep_outs[:-1], rep_outs, torch.mm(dz, self.pair[0]),
+                                     need_dx=False, thin_first=self.thin0)
+            self._cq.flush(z_a.device)   # every deferred column-sum finalize in one launch
+            return scalars
         ds = self._from_dz(self.actor[:-1], [s] + a_outs, a_outs, dz_a, need_dx=have_rep)
         ds = self._from_dz(self.critic[:-1], [s] + c_outs, c_outs, dz_c, need_dx=have_rep, accumulate=ds)
         if have_rep:
             r_in = [x] + rep_outs[:-1]
-            self._chain_backward(self.rep, r_in, rep_outs, ds, need_dx=False)
+            self._chain_backward(self.rep, r_in, rep_outs, ds, need_dx=False, thin_first=self.thin0)
+        self._cq.flush(z_a.device)
         return scalars
 
     def _from_dz(self, layers, inputs, outs, dz, need_dx, accumulate=None):
@@ -214,7 +294,7 @@ class FusedActorCritic:
         _lib.check(L.xpa_colsum_finalize(ops._p(p_dbo), G, K, ops._p(lin_o.bias.grad), s), "colsum db_o")
         return dz
 
-    def _chain_backward(self, layers, inputs, outs, g, need_dx, accumulate=None, allow_head=True):
+    def _chain_backward(self, layers, inputs, outs, g, need_dx, accumulate=None, allow_head=True, thin_first=False):
         """g: grad w.r.t. the chain's last output (contiguous [B, n_out]); returns grad w.r.t. its input
         (added to `accumulate` through the GEMM's C operand when given)."""
         top = len(layers) - 1
@@ -234,6 +314,9 @@ class FusedActorCritic:
             lin, code, slope = layers[j]
             h = outs[j]
             x = inputs[j]
+            if j == 0 and thin_first and not need_dx and g.stride(1) == 1 and x.stride(1) == 1:
+                self._thin_backward(layers[0], g, h, x)   # K13: act backward + dW + db, no dz pass
+                break
             self._bias_grad(code, g, h, slope, lin.bias.grad)   # g <- g * act'(h) in place (code != 0)
             self._weight_grad(g, x, lin.weight.grad)
             if j > 0 or need_dx:
@@ -253,4 +336,5 @@ class FusedActorCritic:
         ds = self._chain_backward(self.critic, c_in, c_outs, d_v.view(-1, 1), need_dx=have_rep, accumulate=ds)
         if have_rep:
             r_in = [x] + rep_outs[:-1]
-            self._chain_backward(self.rep, r_in, rep_outs, ds, need_dx=False)
+            self._chain_backward(self.rep, r_in, rep_outs, ds, need_dx=False, thin_first=self.thin0)
+        self._cq.flush(d_head.device)

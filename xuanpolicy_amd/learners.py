@@ -83,7 +83,7 @@ class _FusedPolicyGradient(Learner):
         if fm is None and getattr(self, "flat_grads", None) is not None and getattr(self, "fused_mlp_enabled", True):
             from .fused_mlp import FusedActorCritic
             try:
-                fm = FusedActorCritic(self.policy)
+                fm = FusedActorCritic(self.policy, flat=self.flat_grads)
             except ValueError:
                 fm = False
             self._fm = fm

@@ -219,13 +219,18 @@ HEAD_HIDDEN = 256  # hidden width K12 handles (64 lanes x 4 columns)
 class HeadWorkspace:
     """Outputs and per-block partials of K12 for a fixed (batch, K)."""
 
-    def __init__(self, batch, k, device):
+    def __init__(self, batch, k, device, paired=False):
         H = HEAD_HIDDEN
         G = int(lib().xpa_head_fused_num_partials(batch))
-        self.batch, self.k, self.G = batch, k, G
+        self.batch, self.k, self.G, self.paired = batch, k, G, paired
         f32 = dict(dtype=torch.float32, device=device)
-        self.dz_actor = torch.empty((batch, H), **f32)
-        self.dz_critic = torch.empty((batch, H), **f32)
+        if paired:   # actor | critic halves of one [batch, 512] gradient (one dX / dW GEMM downstream)
+            self.dz_pair = torch.empty((batch, 2 * H), **f32)
+            self.dz_actor, self.dz_critic = self.dz_pair[:, :H], self.dz_pair[:, H:]
+        else:
+            self.dz_pair = None
+            self.dz_actor = torch.empty((batch, H), **f32)
+            self.dz_critic = torch.empty((batch, H), **f32)
         self.p_dw_actor = torch.empty((G, k * H), **f32)
         self.p_dbh_actor = torch.empty((G, H), **f32)
         self.p_dbo_actor = torch.empty((G, k), **f32)
@@ -240,13 +245,54 @@ def _colsum(part, out, s):
     _lib.check(lib().xpa_colsum_finalize(_p(part), part.shape[0], part.shape[1], _p(out), s), "xpa_colsum_finalize")
 
 
+class ColsumQueue:
+    """Collects column-sum finalizes (partials [G, C] -> out [C]) and launches them together with
+    xpa_colsum_finalize_batch (16 segments per launch).  The ctypes argument arrays are cached per
+    set of buffers, so a steady-state update re-uses them."""
+
+    MAX_SEGS = 16
+
+    def __init__(self):
+        self.items = []
+        self._plans = {}
+
+    def add(self, part, out):
+        _req(part, "partials", torch.float32)
+        _req(out, "out", torch.float32)
+        if part.dim() != 2 or out.numel() != part.shape[1]:
+            raise ValueError("partials must be [G, C] and out must have C elements")
+        self.items.append((part, out))
+
+    def flush(self, device=None):
+        if not self.items:
+            return
+        key = tuple((p.data_ptr(), p.shape[0], p.shape[1], o.data_ptr()) for p, o in self.items)
+        plan = self._plans.get(key)
+        if plan is None:
+            plan = []
+            for i in range(0, len(key), self.MAX_SEGS):
+                chunk = key[i:i + self.MAX_SEGS]
+                n = len(chunk)
+                arrs = ((ctypes.c_void_p * n)(*[c[0] for c in chunk]), (ctypes.c_int64 * n)(*[c[1] for c in chunk]),
+                        (ctypes.c_int64 * n)(*[c[2] for c in chunk]), (ctypes.c_void_p * n)(*[c[3] for c in chunk]))
+                plan.append((n, arrs, [ctypes.cast(a, ctypes.c_void_p) for a in arrs]))
+            self._plans[key] = plan
+        s = _stream(device if device is not None else self.items[0][0].device)
+        L = lib()
+        for n, _keep, args in plan:
+            _lib.check(L.xpa_colsum_finalize_batch(n, *args, s), "xpa_colsum_finalize_batch")
+        self.items = []
+
+
 def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, w_critic, b_critic, act_critic,
                 logstd, act, adv, ret, old_logp=None, idx=None, adv_partials=None, clip_range=0.2, vf_coef=0.25,
-                ent_coef=0.0, grads=None):
+                ent_coef=0.0, grads=None, colsum_queue=None):
     """K12 actor + critic heads, loss finalize and the column-sum finalizes.
 
-    z_*: hidden pre-activations [B, 256]; w_*/b_*: output layer (K x 256 / 1 x 256); act_*: (code, slope)
-    of the hidden activation.  grads: dict with the gradient views to write — 'w_actor', 'b_actor',
+    z_*: hidden pre-activations [B, 256] (unit column stride; row stride = the workspace dz row stride,
+    e.g. the halves of a [B, 512] actor|critic pre-activation with a paired workspace); w_*/b_*: output layer (K x 256 / 1 x 256); act_*: (code, slope)
+    of the hidden activation.  colsum_queue: an ops.ColsumQueue to defer the column-sum finalizes into
+    (flushed by the caller), else they run here.  grads: dict with the gradient views to write — 'w_actor', 'b_actor',
     'bh_actor', 'w_critic', 'b_critic', 'bh_critic', 'logstd' (gaussian).  Returns (scalars, dz_actor,
     dz_critic)."""
     if algo not in ALGO or dist not in DIST:
@@ -255,8 +301,11 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
     K = w_actor.shape[0]
     if H != HEAD_HIDDEN or ws.batch != B or ws.k != K:
         raise ValueError("fused heads need hidden width %d and a matching workspace" % HEAD_HIDDEN)
-    _req(z_actor, "z_actor", torch.float32, (B, H))
-    _req(z_critic, "z_critic", torch.float32, (B, H))
+    ld = ws.dz_actor.stride(0)
+    for name, zz in (("z_actor", z_actor), ("z_critic", z_critic)):
+        _req(zz, name, torch.float32, contiguous=False)
+        if tuple(zz.shape) != (B, H) or zz.stride() != (ld, 1):
+            raise ValueError("%s must be [%d, %d] with row stride %d" % (name, B, H, ld))
     _req(w_actor, "w_actor", torch.float32, (K, H))
     _req(w_critic, "w_critic", torch.float32, (1, H))
     if idx is not None:
@@ -275,14 +324,14 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
     L = lib()
     W = ws.loss_partials.shape[1]
     ev = TIMER.start("heads")
-    rc = L.xpa_head_fused_actor(ALGO[algo], DIST[dist], act_actor[0], B, K, H, _p(z_actor), _p(w_actor), _p(b_actor),
+    rc = L.xpa_head_fused_actor(ALGO[algo], DIST[dist], act_actor[0], B, K, H, ld, _p(z_actor), _p(w_actor), _p(b_actor),
                                 float(act_actor[1]), _p(logstd) if dist == "gaussian" else None, _p(idx), rows, _p(act),
                                 _p(old_logp) if algo == "ppo" else None, _p(adv), _p(adv_partials),
                                 adv_partials.shape[0] if adv_partials is not None else 0, float(clip_range),
                                 float(ent_coef), _p(ws.dz_actor), _p(ws.p_dw_actor), _p(ws.p_dbh_actor),
                                 _p(ws.p_dbo_actor), _p(ws.loss_partials), W, s)
     _lib.check(rc, "xpa_head_fused_actor")
-    rc = L.xpa_head_fused_critic(act_critic[0], B, H, _p(z_critic), _p(w_critic), _p(b_critic), float(act_critic[1]),
+    rc = L.xpa_head_fused_critic(act_critic[0], B, H, ld, _p(z_critic), _p(w_critic), _p(b_critic), float(act_critic[1]),
                                  _p(idx), rows, _p(ret), float(vf_coef), _p(ws.dz_critic), _p(ws.p_dw_critic),
                                  _p(ws.p_dbh_critic), _p(ws.p_dbo_critic), _p(ws.loss_partials), W, s)
     TIMER.stop("heads", ev)
@@ -293,10 +342,13 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
         d_logstd = torch.empty((K,), dtype=torch.float32, device=z_actor.device)
     _lib.check(L.xpa_policy_loss_finalize(ALGO[algo], DIST[dist], B, K, _p(ws.loss_partials), ws.G, float(vf_coef),
                                           float(ent_coef), _p(ws.scalars), _p(d_logstd), s), "xpa_policy_loss_finalize")
+    queue = colsum_queue if colsum_queue is not None else ColsumQueue()
     for key, part in (("w_actor", ws.p_dw_actor), ("b_actor", ws.p_dbo_actor), ("bh_actor", ws.p_dbh_actor),
                       ("w_critic", ws.p_dw_critic), ("b_critic", ws.p_dbo_critic), ("bh_critic", ws.p_dbh_critic)):
         if key in g:
-            _colsum(part, g[key], s)
+            queue.add(part, g[key])
+    if colsum_queue is None:
+        queue.flush(z_actor.device)
     return ws.scalars, ws.dz_actor, ws.dz_critic
 
 
