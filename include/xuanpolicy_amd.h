@@ -225,6 +225,23 @@ int xpa_head_fused_critic(int act, int64_t batch, int64_t hidden, int64_t ld, co
 int xpa_colsum_finalize_batch(int n_segs, const float *const *partials, const int64_t *n_partials,
                               const int64_t *cols, float *const *outs, xpa_stream_t stream);
 
+/* K14 — rollout policy head: the last hidden activation and both output layers of the actor-critic
+ * (gaussian.py:8-51 / categorical.py:16-58 forward in PPOCLIP_Agent._action, ppoclip_agent.py:50-57)
+ * fused with xpa_rollout_sample: z_actor / z_critic [n_envs, 256] are the hidden pre-activations
+ * (row stride ld, e.g. the halves of a paired [n, 512] GEMM output); the value and mu / logits are
+ * formed in the kernel and the sample / log-prob / value / env input are stored exactly as
+ * xpa_rollout_sample does (same RNG stream).  act_dim <= 8.
+ * xpa_value_head: v_out[n] = act(z_critic) . w_critic + b_critic alone (the bootstrap value of
+ * ppoclip_agent.py:77-81 on the normalised final observations). */
+int xpa_rollout_policy_head(int dist, int act, int64_t n_envs, int64_t act_dim, int64_t horizon, int64_t hidden,
+                            int64_t ld, const float *z_actor, const float *z_critic, float slope,
+                            const float *w_actor, const float *b_actor, const float *w_critic,
+                            const float *b_critic, const float *logstd, const xpa_cursor_t *cursor, uint32_t seed,
+                            float act_clip, float *buf_act, float *buf_logp, float *buf_val, float *env_in,
+                            int64_t ld_env, xpa_stream_t stream);
+int xpa_value_head(int act, int64_t n, int64_t hidden, int64_t ld, const float *z_critic, float slope,
+                   const float *w_critic, const float *b_critic, float *v_out, xpa_stream_t stream);
+
 /* K13 — first representation layer Linear(d_in, 256) + activation for a small d_in (<= 64): Basic_MLP's
  * first mlp_block (xuance/torch/representations/mlp.py:21-51, utils/layers.py:8-24) as HBM-streaming
  * kernels.  Forward: h = act(x W^T + b), x [rows, d_in] (row stride ldx), w [256, d_in], h [rows, 256]

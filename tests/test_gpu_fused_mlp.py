@@ -223,3 +223,48 @@ def test_colsum_finalize_batch_matches_single():
     q.flush()                      # a second plan
     for o, r in zip(outs, refs):
         assert torch.equal(o, r)
+
+
+@pytest.mark.parametrize("discrete,act", [(False, torch.nn.LeakyReLU), (True, torch.nn.LeakyReLU),
+                                          (False, torch.nn.Tanh)])
+def test_rollout_policy_head_matches_sample_kernel(discrete, act):
+    """K14 (trunk + paired hidden GEMM + heads + sample/store) == policy_heads (nn modules) + K3 on the
+    same cursor/seed: same RNG draws, so actions / log-probs / values agree to fp32 rounding."""
+    from xuanpolicy_amd import ops
+    from xuanpolicy_amd.flat import FlatState
+    from xuanpolicy_amd.fused_mlp import FusedActorCritic, head_placement
+    from xuanpolicy_amd.policies import policy_heads
+    torch.manual_seed(5)
+    D, A, N, T = 17, 6, 4096 + 3, 8
+    pol = _policy(D, A, discrete, act, [256])
+    fs = FlatState(pol.parameters(), placement=head_placement(pol))
+    fm = FusedActorCritic(pol, flat=fs)
+    assert fm.rollout_ok
+    x = torch.randn(N, D, device=DEV)
+    cur = torch.tensor([3, 77, 0, 0], dtype=torch.int32, device=DEV)
+    dist = "categorical" if discrete else "gaussian"
+    bufs = []
+    for path in ("k3", "k14"):
+        ba = torch.zeros((N, T) if discrete else (N, T, A), device=DEV)
+        bl, bv = torch.zeros(N, T, device=DEV), torch.zeros(N, T, device=DEV)
+        env_in = torch.zeros(N, A, device=DEV)
+        if path == "k3":
+            with torch.no_grad():
+                head, logstd, v = policy_heads(pol, x)
+            ops.rollout_sample(dist, head.contiguous(), logstd, v.contiguous(), cur, 1234, ba, bl, bv, env_in)
+        else:
+            fm.rollout_act(x, dist, cur, 1234, ba, bl, bv, env_in)
+        bufs.append((ba, bl, bv, env_in))
+    (a1, l1, v1, e1), (a2, l2, v2, e2) = bufs
+    torch.testing.assert_close(v2, v1, rtol=1e-5, atol=1e-5)
+    if discrete:   # inverse-CDF picks agree except where u sits within rounding of a CDF boundary
+        assert (a1 != a2).float().mean().item() < 1e-3
+        same = (a1 == a2)
+        torch.testing.assert_close(l2[same], l1[same], rtol=1e-5, atol=1e-5)
+    else:
+        torch.testing.assert_close(a2, a1, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(l2, l1, rtol=1e-5, atol=1e-4)
+        torch.testing.assert_close(e2, e1, rtol=1e-5, atol=1e-5)
+    vb = fm.rollout_value(x)
+    with torch.no_grad():
+        torch.testing.assert_close(vb, policy_heads(pol, x)[2], rtol=1e-5, atol=1e-5)

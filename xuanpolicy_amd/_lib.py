@@ -58,6 +58,10 @@ SIGNATURES = {
                                             c_p, c_p, c_p, c_i64, c_p]),
     "xpa_head_fused_critic": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_f32, c_p, c_i64, c_p, c_f32,
                                              c_p, c_p, c_p, c_p, c_p, c_i64, c_p]),
+    "xpa_rollout_policy_head": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p,
+                                               c_f32, c_p, c_p, c_p, c_p, c_p, c_p, c_u32, c_f32, c_p, c_p, c_p, c_p,
+                                               c_i64, c_p]),
+    "xpa_value_head": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_f32, c_p, c_p, c_p, c_p]),
     "xpa_colsum_finalize_batch": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p]),
     "xpa_thin_bwd_num_partials": (c_i64, [c_i64]),
     "xpa_thin_linear_act_fwd": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f32, c_p, c_i64,

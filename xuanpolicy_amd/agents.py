@@ -129,12 +129,23 @@ class _OnPolicyAgent:
             ops.obs_normalize(x, self.obs_mean, self.obs_var, self._obs_clip(), out)
 
     # ---- one env step ---------------------------------------------------------------------------------
+    def _rollout_mlp(self):
+        """The learner's FusedActorCritic when it can drive the rollout forward (K14), else None."""
+        fm_get = getattr(self.learner, "_fused_mlp", None)
+        fm = fm_get() if fm_get is not None else None
+        return fm if fm is not None and fm.rollout_ok else None
+
     def _sample_into_buffer(self):
         mem = self.memory
-        with torch.no_grad():
-            head, logstd, v = policy_heads(self.policy, self.obs_norm)
         logp_buf = mem.auxiliary_infos["old_logp"] if self.algo == "ppo" else self.logp_scratch
         env_in = self.envs.act_in if self.device_env else self._act_scratch()
+        fm = self._rollout_mlp()
+        if fm is not None:
+            fm.rollout_act(self.obs_norm, self.dist, self.cursor, self.seed, mem.actions, logp_buf, mem.values, env_in,
+                           act_clip=1.0)
+            return
+        with torch.no_grad():
+            head, logstd, v = policy_heads(self.policy, self.obs_norm)
         ops.rollout_sample(self.dist, head.contiguous(), logstd, v.contiguous(), self.cursor, self.seed,
                            mem.actions, logp_buf, mem.values, env_in, act_clip=1.0)
 
@@ -147,8 +158,12 @@ class _OnPolicyAgent:
     def _post(self, rew, term, trunc, final_obs):
         mem = self.memory
         self._normalize_into(final_obs, self.boot_obs, False)
-        with torch.no_grad():
-            v_boot = policy_heads(self.policy, self.boot_obs)[2]
+        fm = self._rollout_mlp()
+        if fm is not None:
+            v_boot = fm.rollout_value(self.boot_obs)
+        else:
+            with torch.no_grad():
+                v_boot = policy_heads(self.policy, self.boot_obs)[2]
         ops.rollout_post(rew, term, trunc, v_boot.contiguous(), self.cursor, self.ret_mean, self.ret_var,
                          self.ret_count, self.returns, mem.rewards, mem.terminals, mem.closed, mem.boot, self.gamma,
                          mask_returns=(self.algo == "ppo"), use_rewnorm=self.use_rewnorm,

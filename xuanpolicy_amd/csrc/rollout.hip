@@ -152,13 +152,12 @@ __global__ __launch_bounds__(256) void obs_normalize_kernel(const float *__restr
 // ---------------------------------------------------------------------------------------------
 // K3 sample + log-prob + store
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void rollout_sample_gauss_kernel(
-    int64_t n_envs, int A, int64_t T, const float *__restrict__ mu, const float *__restrict__ logstd,
-    const float *__restrict__ v, const xpa_cursor_t *__restrict__ cur, uint32_t seed, float act_clip,
-    float *__restrict__ buf_act, float *__restrict__ buf_logp, float *__restrict__ buf_val, float *__restrict__ env_in,
-    int64_t ld_env) {
-    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (n >= n_envs) return;
+__device__ __forceinline__ void gauss_sample_store(int64_t n, int A, int64_t T, const float *mu_row,
+                                                   const float *__restrict__ logstd, float v,
+                                                   const xpa_cursor_t *__restrict__ cur, uint32_t seed, float act_clip,
+                                                   float *__restrict__ buf_act, float *__restrict__ buf_logp,
+                                                   float *__restrict__ buf_val, float *__restrict__ env_in,
+                                                   int64_t ld_env) {
     const int64_t t = cur->ptr;
     const uint32_t step = cur->step;
     const int64_t cell = n * T + t;
@@ -170,7 +169,7 @@ __global__ __launch_bounds__(256) void rollout_sample_gauss_kernel(
         const float u2 = xpa_u01(h2);
         const float eps = sqrtf(-2.0f * logf(u1)) * cosf(6.28318530717958647692f * u2);
         const float sc = expf(logstd[a]);
-        const float m = mu[n * A + a];
+        const float m = mu_row[a];
         const float x = m + sc * eps;
         const float diff = x - m;
         logp += -(diff * diff) / (2.0f * sc * sc) - logf(sc) - 0.91893853320467274178f;
@@ -178,19 +177,17 @@ __global__ __launch_bounds__(256) void rollout_sample_gauss_kernel(
         env_in[n * ld_env + a] = fminf(fmaxf(x, -act_clip), act_clip);
     }
     buf_logp[cell] = logp;
-    buf_val[cell] = v[n];
+    buf_val[cell] = v;
 }
 
-__global__ __launch_bounds__(256) void rollout_sample_cat_kernel(
-    int64_t n_envs, int K, int64_t T, const float *__restrict__ logits, const float *__restrict__ v,
-    const xpa_cursor_t *__restrict__ cur, uint32_t seed, float *__restrict__ buf_act, float *__restrict__ buf_logp,
-    float *__restrict__ buf_val, float *__restrict__ env_in, int64_t ld_env) {
-    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (n >= n_envs) return;
+__device__ __forceinline__ void cat_sample_store(int64_t n, int K, int64_t T, const float *z, float v,
+                                                 const xpa_cursor_t *__restrict__ cur, uint32_t seed,
+                                                 float *__restrict__ buf_act, float *__restrict__ buf_logp,
+                                                 float *__restrict__ buf_val, float *__restrict__ env_in,
+                                                 int64_t ld_env) {
     const int64_t t = cur->ptr;
     const uint32_t step = cur->step;
     const int64_t cell = n * T + t;
-    const float *z = logits + n * K;
     float m = z[0];
     for (int k = 1; k < K; ++k) m = fmaxf(m, z[k]);
     float se = 0.f;
@@ -208,8 +205,83 @@ __global__ __launch_bounds__(256) void rollout_sample_cat_kernel(
     }
     buf_act[cell] = (float)pick;
     buf_logp[cell] = z[pick] - lse;
-    buf_val[cell] = v[n];
+    buf_val[cell] = v;
     for (int k = 0; k < K; ++k) env_in[n * ld_env + k] = (k == pick) ? 1.f : 0.f;
+}
+
+__global__ __launch_bounds__(256) void rollout_sample_gauss_kernel(
+    int64_t n_envs, int A, int64_t T, const float *__restrict__ mu, const float *__restrict__ logstd,
+    const float *__restrict__ v, const xpa_cursor_t *__restrict__ cur, uint32_t seed, float act_clip,
+    float *__restrict__ buf_act, float *__restrict__ buf_logp, float *__restrict__ buf_val, float *__restrict__ env_in,
+    int64_t ld_env) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_envs) return;
+    gauss_sample_store(n, A, T, mu + n * A, logstd, v[n], cur, seed, act_clip, buf_act, buf_logp, buf_val, env_in,
+                       ld_env);
+}
+
+__global__ __launch_bounds__(256) void rollout_sample_cat_kernel(
+    int64_t n_envs, int K, int64_t T, const float *__restrict__ logits, const float *__restrict__ v,
+    const xpa_cursor_t *__restrict__ cur, uint32_t seed, float *__restrict__ buf_act, float *__restrict__ buf_logp,
+    float *__restrict__ buf_val, float *__restrict__ env_in, int64_t ld_env) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_envs) return;
+    cat_sample_store(n, K, T, logits + n * K, v[n], cur, seed, buf_act, buf_logp, buf_val, env_in, ld_env);
+}
+
+// ---------------------------------------------------------------------------------------------
+// K14 rollout policy head: hidden activation + output layers (one wave per env, lane l owns hidden
+// columns [4l, 4l + 4), butterfly dot products) + the K3 sample/store above, or the value alone.
+// ---------------------------------------------------------------------------------------------
+template <int ACT>
+__device__ __forceinline__ float4 act4(float4 z, float slope) {
+    if (ACT == 1) {
+        z.x = z.x > 0.f ? z.x : z.x * slope; z.y = z.y > 0.f ? z.y : z.y * slope;
+        z.z = z.z > 0.f ? z.z : z.z * slope; z.w = z.w > 0.f ? z.w : z.w * slope;
+    } else if (ACT == 2) {
+        z.x = tanhf(z.x); z.y = tanhf(z.y); z.z = tanhf(z.z); z.w = tanhf(z.w);
+    }
+    return z;
+}
+
+__device__ __forceinline__ float dot4(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
+
+__device__ __forceinline__ float wave_allsum_f(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// MODE: 0 Gaussian sample, 1 Categorical sample, 2 value only (v_out[n]).
+template <int MODE, int ACT>
+__global__ __launch_bounds__(256) void rollout_policy_head_kernel(
+    int64_t n_envs, int K, int64_t T, const float *__restrict__ za, const float *__restrict__ zc, int64_t ld,
+    float slope, const float *__restrict__ Wa, const float *__restrict__ ba, const float *__restrict__ Wc,
+    const float *__restrict__ bc, const float *__restrict__ logstd, const xpa_cursor_t *__restrict__ cur,
+    uint32_t seed, float act_clip, float *__restrict__ buf_act, float *__restrict__ buf_logp,
+    float *__restrict__ buf_val, float *__restrict__ env_in, int64_t ld_env, float *__restrict__ v_out) {
+    __shared__ float s_head[4][8];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t n = (int64_t)blockIdx.x * 4 + wave;
+    if (n >= n_envs) return;  // wave-uniform
+    const float4 hc = act4<ACT>(*reinterpret_cast<const float4 *>(zc + n * ld + 4 * lane), slope);
+    const float v = wave_allsum_f(dot4(hc, *reinterpret_cast<const float4 *>(Wc + 4 * lane))) + bc[0];
+    if (MODE == 2) {
+        if (lane == 0) v_out[n] = v;
+        return;
+    }
+    const float4 h = act4<ACT>(*reinterpret_cast<const float4 *>(za + n * ld + 4 * lane), slope);
+    for (int o = 0; o < K; ++o) {
+        const float p = wave_allsum_f(dot4(h, *reinterpret_cast<const float4 *>(Wa + o * 256 + 4 * lane))) + ba[o];
+        if (lane == 0) s_head[wave][o] = p;
+    }
+    if (lane == 0) {
+        if (MODE == 0)
+            gauss_sample_store(n, K, T, s_head[wave], logstd, v, cur, seed, act_clip, buf_act, buf_logp, buf_val,
+                               env_in, ld_env);
+        else
+            cat_sample_store(n, K, T, s_head[wave], v, cur, seed, buf_act, buf_logp, buf_val, env_in, ld_env);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -457,5 +529,59 @@ XPA_API int xpa_rollout_post(int64_t n_envs, int64_t horizon, const float *rew, 
     hipLaunchKernelGGL(rollout_post_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, n_envs, horizon, rew, term,
                        trunc, v_boot, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term, buf_closed,
                        buf_boot, gamma, mask_returns, use_rewnorm, rew_range, atari_lifeloss);
+    return xpa_launch_status();
+}
+
+// ---- K14 -------------------------------------------------------------------------------------------
+XPA_API int xpa_rollout_policy_head(int dist, int act, int64_t n_envs, int64_t act_dim, int64_t horizon,
+                                    int64_t hidden, int64_t ld, const float *z_actor, const float *z_critic,
+                                    float slope, const float *w_actor, const float *b_actor, const float *w_critic,
+                                    const float *b_critic, const float *logstd, const xpa_cursor_t *cursor,
+                                    uint32_t seed, float act_clip, float *buf_act, float *buf_logp, float *buf_val,
+                                    float *env_in, int64_t ld_env, xpa_stream_t stream) {
+    if (n_envs <= 0 || act_dim < 1 || act_dim > 8 || horizon <= 0 || hidden != 256 || ld < 256 || ld % 4 ||
+        act < 0 || act > 2 || !z_actor || !z_critic || !w_actor || !b_actor || !w_critic || !b_critic || !cursor ||
+        !buf_act || !buf_logp || !buf_val || !env_in || ld_env < act_dim)
+        return (int)hipErrorInvalidValue;
+    if (((uintptr_t)z_actor | (uintptr_t)z_critic | (uintptr_t)w_actor | (uintptr_t)w_critic) % 16)
+        return (int)hipErrorInvalidValue;
+    if ((dist == XPA_DIST_GAUSSIAN && !logstd) || (dist == XPA_DIST_CATEGORICAL && act_dim < 2) ||
+        (dist != XPA_DIST_GAUSSIAN && dist != XPA_DIST_CATEGORICAL))
+        return (int)hipErrorInvalidValue;
+    const unsigned blocks = (unsigned)((n_envs + 3) / 4);
+    hipStream_t s = (hipStream_t)stream;
+#define XPA_K14(M_, A_)                                                                                          \
+    hipLaunchKernelGGL((rollout_policy_head_kernel<M_, A_>), dim3(blocks), dim3(256), 0, s, n_envs, (int)act_dim, \
+                       horizon, z_actor, z_critic, ld, slope, w_actor, b_actor, w_critic, b_critic, logstd, cursor,   \
+                       seed, act_clip, buf_act, buf_logp, buf_val, env_in, ld_env, (float *)nullptr)
+    if (dist == XPA_DIST_GAUSSIAN) {
+        if (act == 0) XPA_K14(0, 0);
+        else if (act == 1) XPA_K14(0, 1);
+        else XPA_K14(0, 2);
+    } else {
+        if (act == 0) XPA_K14(1, 0);
+        else if (act == 1) XPA_K14(1, 1);
+        else XPA_K14(1, 2);
+    }
+#undef XPA_K14
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_value_head(int act, int64_t n, int64_t hidden, int64_t ld, const float *z_critic, float slope,
+                           const float *w_critic, const float *b_critic, float *v_out, xpa_stream_t stream) {
+    if (n <= 0 || hidden != 256 || ld < 256 || ld % 4 || act < 0 || act > 2 || !z_critic || !w_critic ||
+        !b_critic || !v_out || ((uintptr_t)z_critic | (uintptr_t)w_critic) % 16)
+        return (int)hipErrorInvalidValue;
+    const unsigned blocks = (unsigned)((n + 3) / 4);
+    hipStream_t s = (hipStream_t)stream;
+#define XPA_VH(A_)                                                                                                 \
+    hipLaunchKernelGGL((rollout_policy_head_kernel<2, A_>), dim3(blocks), dim3(256), 0, s, n, 1, (int64_t)1,        \
+                       z_critic, z_critic, ld, slope, w_critic, b_critic, w_critic, b_critic, (const float *)nullptr, \
+                       (const xpa_cursor_t *)nullptr, 0u, 0.f, (float *)nullptr, (float *)nullptr, (float *)nullptr, \
+                       (float *)nullptr, (int64_t)0, v_out)
+    if (act == 0) XPA_VH(0);
+    else if (act == 1) XPA_VH(1);
+    else XPA_VH(2);
+#undef XPA_VH
     return xpa_launch_status();
 }

@@ -171,6 +171,36 @@ class FusedActorCritic:
         v = c_outs[-1][:, 0]
         return a_outs[-1], self.logstd, v, (x, rep_outs, s, a_outs, c_outs)
 
+    # ---- rollout-side forwards (K14) ---------------------------------------------------------------
+    @property
+    def rollout_ok(self):
+        return self.pair is not None
+
+    @torch.no_grad()
+    def rollout_act(self, x, dist, cursor, seed, buf_act, buf_logp, buf_val, env_in, act_clip=1.0):
+        """Policy step of the rollout: trunk, paired hidden GEMM, then K14 (heads + sample + store)."""
+        rep_outs = self._rep_forward(x)
+        s = rep_outs[-1] if rep_outs else x
+        z = F.linear(s, self.pair[0], self.pair[1])
+        H = ops.HEAD_HIDDEN
+        lin_ao = self.actor[-1][0]
+        lin_co = self.critic[-1][0]
+        _, code, slope = self.actor[-2]
+        if self.critic[-2][1:] != (code, slope):
+            raise ValueError("actor and critic hidden activations differ")
+        ops.rollout_policy_head(dist, z[:, :H], z[:, H:], (code, slope), lin_ao.weight, lin_ao.bias, lin_co.weight,
+                                lin_co.bias, self.logstd, cursor, seed, buf_act, buf_logp, buf_val, env_in, act_clip)
+
+    @torch.no_grad()
+    def rollout_value(self, x, out=None):
+        """Critic only (bootstrap values): trunk, critic hidden GEMM, K14 value head."""
+        rep_outs = self._rep_forward(x)
+        s = rep_outs[-1] if rep_outs else x
+        lin_ch, code, slope = self.critic[-2]
+        lin_co = self.critic[-1][0]
+        z = F.linear(s, lin_ch.weight, lin_ch.bias)
+        return ops.value_head(z, (code, slope), lin_co.weight, lin_co.bias, out=out)
+
     @torch.no_grad()
     def forward_hidden(self, x):
         """Forward up to the heads' last hidden pre-activations (K12 does the rest)."""

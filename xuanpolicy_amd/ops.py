@@ -420,6 +420,51 @@ def rollout_sample(dist, head, logstd, v, cursor, seed, buf_act, buf_logp, buf_v
     _lib.check(rc, "xpa_rollout_sample")
 
 
+def rollout_policy_head(dist, z_actor, z_critic, act, w_actor, b_actor, w_critic, b_critic, logstd, cursor, seed,
+                        buf_act, buf_logp, buf_val, env_in, act_clip=1.0):
+    """K14: hidden activation + output layers + K3 sampling/store in one launch.  z_* [N, 256] hidden
+    pre-activations with unit column stride and a common row stride; act = (code, slope)."""
+    N, H = z_actor.shape
+    ld = z_actor.stride(0)
+    for name, z in (("z_actor", z_actor), ("z_critic", z_critic)):
+        _req(z, name, torch.float32, contiguous=False)
+        if tuple(z.shape) != (N, HEAD_HIDDEN) or z.stride() != (ld, 1):
+            raise ValueError("%s must be [N, %d] with the same row stride" % (name, HEAD_HIDDEN))
+    A = w_actor.shape[0]
+    _req(w_actor, "w_actor", torch.float32, (A, H))
+    _req(w_critic, "w_critic", torch.float32, (1, H))
+    _req(cursor, "cursor", torch.int32, (4,))
+    _req(buf_logp, "buf_logp", torch.float32)
+    _req(buf_val, "buf_val", torch.float32)
+    if buf_logp.dim() != 2 or buf_logp.shape[0] != N or tuple(buf_val.shape) != tuple(buf_logp.shape):
+        raise ValueError("buf_logp/buf_val must be [n_envs, horizon]")
+    T = buf_logp.shape[1]
+    _req(buf_act, "buf_act", torch.float32, (N, T, A) if dist == "gaussian" else (N, T))
+    ld_env = _row_stride(env_in, "env_in", A)
+    if dist == "gaussian":
+        _req(logstd, "logstd", torch.float32, (A,))
+    rc = lib().xpa_rollout_policy_head(DIST[dist], act[0], N, A, T, H, ld, _p(z_actor), _p(z_critic), float(act[1]),
+                                       _p(w_actor), _p(b_actor), _p(w_critic), _p(b_critic),
+                                       _p(logstd) if dist == "gaussian" else None, _p(cursor), int(seed) & 0xFFFFFFFF,
+                                       float(act_clip), _p(buf_act), _p(buf_logp), _p(buf_val), _p(env_in), ld_env,
+                                       _stream(z_actor.device))
+    _lib.check(rc, "xpa_rollout_policy_head")
+
+
+def value_head(z_critic, act, w_critic, b_critic, out=None):
+    """K14 value-only: v = act(z_critic) . w + b for every row."""
+    N, H = z_critic.shape
+    _req(z_critic, "z_critic", torch.float32, contiguous=False)
+    if H != HEAD_HIDDEN or z_critic.stride(1) != 1:
+        raise ValueError("z_critic must be [N, %d] with unit column stride" % HEAD_HIDDEN)
+    _req(w_critic, "w_critic", torch.float32, (1, H))
+    out = torch.empty((N,), dtype=torch.float32, device=z_critic.device) if out is None else out
+    _req(out, "out", torch.float32, (N,))
+    _lib.check(lib().xpa_value_head(act[0], N, H, z_critic.stride(0), _p(z_critic), float(act[1]), _p(w_critic),
+                                    _p(b_critic), _p(out), _stream(z_critic.device)), "xpa_value_head")
+    return out
+
+
 def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term,
                  buf_closed, buf_boot, gamma, mask_returns=True, use_rewnorm=True, rew_range=5.0, atari_lifeloss=False):
     """K8: reward normalisation, return tracker + ret_rms, rewards/terminals/closures into the buffer
