@@ -22,6 +22,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+FP32_MFMA_PEAK_TFLOPS = 157.3  # dense f32-input MFMA (= f32 vector rate; no xf32 on gfx950), same table
 
 
 def parse():
@@ -37,7 +38,7 @@ def parse():
     p.add_argument("--n-epoch", type=int, default=16)
     p.add_argument("--n-minibatch", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-updates", type=int, default=8, help="updates timed in the bounded CPU sample")
+    p.add_argument("--cpu-updates", type=int, default=16, help="updates timed in the bounded CPU sample")
     p.add_argument("--no-sweep", action="store_true")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
@@ -53,6 +54,44 @@ def gae_bytes(n_envs, horizon, mid_truncations):
 def loss_bytes_gauss(batch, act_dim):
     """Gaussian loss fwd+bwd = 4 (3A + 5) B per sample."""
     return 4.0 * (3 * act_dim + 5) * batch
+
+
+def heads_bytes(batch, act_dim, hidden=256):
+    """K12 actor + critic launches per minibatch: each reads its hidden
+    pre-activations and writes dz (2 x 4 x hidden B per row); the actor reads act (4A), old_logp,
+    adv and idx (4 + 4 + 8), the critic ret and idx (4 + 8)."""
+    return batch * (2 * 2 * 4 * hidden + 4 * act_dim + 16 + 12)
+
+
+def pair_gemm_flops(batch, d_in, hidden=256):
+    """Paired actor|critic hidden-layer forward GEMM: [B, d_in] x [d_in, 2 hidden]."""
+    return 2.0 * batch * d_in * 2 * hidden
+
+
+def gae_graph_replay_us(mem, reps=50):
+    """K1 alone, `reps` launches on the agent's live buffers captured back to back in one hipGraph
+    (no host dispatch gaps between launches), timed with events on the replay stream."""
+    import torch
+    from xuanpolicy_amd import ops
+    args = (mem.rewards, mem.values, mem.terminals, mem.closed, mem.boot, mem.gamma, mem.gae_lam, mem.use_gae)
+    adv, ret = torch.empty_like(mem.rewards), torch.empty_like(mem.rewards)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        ops.gae_scan(*args, adv=adv, ret=ret)        # warm
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            for _ in range(reps):
+                ops.gae_scan(*args, adv=adv, ret=ret)
+        g.replay()
+        side.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(200000)
+        e0.record(side)
+        g.replay()
+        e1.record(side)
+        e1.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
 
 
 def gae_sweep(device, sizes=(4096, 65536, 262144, 1048576), horizon=128, reps=7):
@@ -167,20 +206,12 @@ def main():
 
     gae_ms = ops.TIMER.mean_ms("gae")
     loss_ms = ops.TIMER.mean_ms("loss")
+    heads_ms = ops.TIMER.mean_ms("heads")
+    gemm_ms = ops.TIMER.mean_ms("gemm_pair")
     mem = agent.memory
     # Back-to-back replay of the same GAE launch on the agent's live buffers (after the timed region):
     # per-launch time without the event/dispatch overhead a single bracketed launch carries.
-    replay_us = None
-    if not args.no_kernel_timing:
-        reps = 50
-        torch.cuda._sleep(200000)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            mem.compute_advantages()
-        e1.record()
-        e1.synchronize()
-        replay_us = e0.elapsed_time(e1) / reps * 1e3
+    replay_us = None if args.no_kernel_timing else gae_graph_replay_us(mem)
     mid_trunc = int(((mem.closed[:, :-1] > 0) & (mem.terminals[:, :-1] == 0)).sum())
     B = N * T // args.n_minibatch
     result = None
@@ -198,11 +229,11 @@ def main():
             roofline = {"kernel": "xpa_gae_scan (gae_scan_kernel<4>)", "bound": "hbm", "achieved": round(ach, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "avg_launch_us": round(gae_ms * 1e3, 3), "algorithmic_bytes_per_launch": int(gb),
-                        "launches": len(ops.TIMER.events.get("gae", [])),
-                        "timing": "HIP events bracketing each in-loop launch (includes ~2-3 us of event/dispatch "
-                                  "latency at this size)",
-                        "replay_back_to_back_us": round(replay_us, 3) if replay_us else None,
-                        "replay_achieved": round(gb / replay_us / 1e3, 1) if replay_us else None}
+                        "launches": ops.TIMER.count("gae"),
+                        "timing": "HIP events recorded by each in-loop dispatch at the kernel's own start and end "
+                                  "(hipExtLaunchKernel), on the launch stream, inside the timed region",
+                        "graph_replay_us": round(replay_us, 3) if replay_us else None,
+                        "graph_replay_achieved": round(gb / replay_us / 1e3, 1) if replay_us else None}
         loss_kernel = None
         if loss_ms:
             lb = loss_bytes_gauss(B, args.act_dim)
@@ -210,6 +241,21 @@ def main():
                            "achieved": round(lb / loss_ms / 1e6, 1), "unit": "GB/s",
                            "frac": round(lb / loss_ms / 1e6 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": int(lb),
                            "launches": len(ops.TIMER.events.get("loss", []))}
+        update_kernels = {}
+        if heads_ms:
+            hb = heads_bytes(B, args.act_dim, args.hidden)
+            update_kernels["heads"] = {
+                "kernel": "xpa_head_fused_actor + xpa_head_fused_critic (K12, per minibatch)", "bound": "hbm",
+                "avg_us": round(heads_ms * 1e3, 3), "algorithmic_bytes": int(hb),
+                "achieved": round(hb / heads_ms / 1e6, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(hb / heads_ms / 1e6 / HBM_PEAK_GBS, 4), "launches": ops.TIMER.count("heads")}
+        if gemm_ms:
+            fl = pair_gemm_flops(B, args.hidden, args.hidden)
+            update_kernels["gemm_pair"] = {
+                "kernel": "paired actor|critic hidden-layer forward GEMM (hipBLASLt, fp32 MFMA)", "bound": "mfma",
+                "avg_us": round(gemm_ms * 1e3, 3), "flops": fl, "achieved": round(fl / gemm_ms / 1e9, 1),
+                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(fl / gemm_ms / 1e9 / FP32_MFMA_PEAK_TFLOPS, 4)}
         result = {
             "metric": "env-steps/sec at num_envs=4096, horizon=128; GAE kernel HBM GB/s vs peak",
             "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
@@ -224,6 +270,7 @@ def main():
                            world, "RCCL" if world == 1 or dist.get_backend() == "nccl" else dist.get_backend())},
             "roofline": roofline,
             "loss_kernel": loss_kernel,
+            "update_kernels": update_kernels or None,
         }
         if not args.no_sweep and world == 1:
             result["gae_sweep_flushed"] = gae_sweep(device, horizon=T)

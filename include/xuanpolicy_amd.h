@@ -63,6 +63,12 @@ int xpa_abi_version(void);
 int xpa_gae_scan(const float *rew, const float *val, const float *term, const uint8_t *closed,
                  const float *boot, int64_t n_envs, int64_t horizon, float gamma, float gae_lambda,
                  int use_gae, float *adv, float *ret, xpa_stream_t stream);
+/* The same launch with two HIP events (hipEvent_t, created by the caller with timing enabled) recorded
+ * at the kernel's own start and end (hipExtLaunchKernel): the live per-launch duration bench.py's
+ * roofline uses.  NULL events = xpa_gae_scan. */
+int xpa_gae_scan_timed(const float *rew, const float *val, const float *term, const uint8_t *closed,
+                       const float *boot, int64_t n_envs, int64_t horizon, float gamma, float gae_lambda,
+                       int use_gae, float *adv, float *ret, void *ev_start, void *ev_stop, xpa_stream_t stream);
 
 /* K4 — minibatch gather.  Replaces the fancy-index gather of DummyOnPolicyBuffer.sample
  * (memory_tools.py:231-240) for the observation rows (the rest is read through `idx` by the loss

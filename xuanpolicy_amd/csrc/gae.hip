@@ -26,6 +26,8 @@
 // kernel moves 21 B (+1 B closure flag) plus 4 B per closed path.
 #include <stdlib.h>
 
+#include <hip/hip_ext.h>
+
 #include "xpa_common.h"
 
 namespace {
@@ -187,9 +189,31 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float *__restrict__
 
 XPA_API int xpa_abi_version(void) { return XPA_ABI_VERSION; }
 
+namespace {
+template <int VEC, int NT>
+void launch_gae(dim3 grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1, const float *rew, const float *val,
+                const float *term, const uint8_t *closed, const float *boot, int64_t n_envs, int T, int seg_log2,
+                float gamma, float gl, int use_gae, float *adv, float *ret) {
+    if (e0 || e1)  // events recorded by the dispatch itself: the kernel's own start / end
+        hipExtLaunchKernelGGL((gae_scan_kernel<VEC, NT>), grid, dim3(256), 0, s, e0, e1, 0, rew, val, term, closed,
+                              boot, n_envs, T, seg_log2, gamma, gl, use_gae, adv, ret);
+    else
+        hipLaunchKernelGGL((gae_scan_kernel<VEC, NT>), grid, dim3(256), 0, s, rew, val, term, closed, boot, n_envs, T,
+                           seg_log2, gamma, gl, use_gae, adv, ret);
+}
+}  // namespace
+
 XPA_API int xpa_gae_scan(const float *rew, const float *val, const float *term, const uint8_t *closed,
                          const float *boot, int64_t n_envs, int64_t horizon, float gamma, float gae_lambda,
                          int use_gae, float *adv, float *ret, xpa_stream_t stream) {
+    return xpa_gae_scan_timed(rew, val, term, closed, boot, n_envs, horizon, gamma, gae_lambda, use_gae, adv, ret,
+                              nullptr, nullptr, stream);
+}
+
+XPA_API int xpa_gae_scan_timed(const float *rew, const float *val, const float *term, const uint8_t *closed,
+                               const float *boot, int64_t n_envs, int64_t horizon, float gamma, float gae_lambda,
+                               int use_gae, float *adv, float *ret, void *ev_start, void *ev_stop,
+                               xpa_stream_t stream) {
     if (n_envs < 0 || horizon < 0 || horizon > (1 << 30)) return (int)hipErrorInvalidValue;
     if (n_envs == 0 || horizon == 0) return 0;
     if (!rew || !val || !term || !closed || !boot || !adv || !ret) return (int)hipErrorInvalidValue;
@@ -215,14 +239,13 @@ XPA_API int xpa_gae_scan(const float *rew, const float *val, const float *term, 
     }();
     const bool nt = nt_env != 0;
     hipStream_t s = (hipStream_t)stream;
+    hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
+    const dim3 grid((unsigned)blocks);
     if (vec4 && nt)
-        hipLaunchKernelGGL((gae_scan_kernel<4, 1>), dim3((unsigned)blocks), dim3(256), 0, s, rew, val, term, closed,
-                           boot, n_envs, T, seg_log2, gamma, gl, use_gae, adv, ret);
+        launch_gae<4, 1>(grid, s, e0, e1, rew, val, term, closed, boot, n_envs, T, seg_log2, gamma, gl, use_gae, adv, ret);
     else if (vec4)
-        hipLaunchKernelGGL((gae_scan_kernel<4, 0>), dim3((unsigned)blocks), dim3(256), 0, s, rew, val, term, closed,
-                           boot, n_envs, T, seg_log2, gamma, gl, use_gae, adv, ret);
+        launch_gae<4, 0>(grid, s, e0, e1, rew, val, term, closed, boot, n_envs, T, seg_log2, gamma, gl, use_gae, adv, ret);
     else
-        hipLaunchKernelGGL((gae_scan_kernel<1, 0>), dim3((unsigned)blocks), dim3(256), 0, s, rew, val, term, closed,
-                           boot, n_envs, T, seg_log2, gamma, gl, use_gae, adv, ret);
+        launch_gae<1, 0>(grid, s, e0, e1, rew, val, term, closed, boot, n_envs, T, seg_log2, gamma, gl, use_gae, adv, ret);
     return xpa_launch_status();
 }

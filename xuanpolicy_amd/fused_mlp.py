@@ -208,7 +208,9 @@ class FusedActorCritic:
         s = rep_outs[-1] if rep_outs else x
         if self.pair is not None:   # one GEMM for both hidden layers: [B, 512] = actor | critic
             H = ops.HEAD_HIDDEN
+            ev = ops.TIMER.start("gemm_pair")
             z = F.linear(s, self.pair[0], self.pair[1])
+            ops.TIMER.stop("gemm_pair", ev)
             return (x, rep_outs, s, (([], s, z[:, :H]), ([], s, z[:, H:])))
         heads = []
         for layers in (self.actor, self.critic):

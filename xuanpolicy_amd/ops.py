@@ -27,9 +27,10 @@ class KernelTimer:
     def __init__(self):
         self.enabled = False
         self.events = {}
+        self.hip_pairs = {}
         # GPU spin (clock cycles) queued before the start event, so the kernel is already enqueued when
         # the start event completes and the host launch latency is not counted as kernel time.
-        self.pad_cycles = {"gae": 200000}
+        self.pad_cycles = {}
 
     def start(self, name):
         if not self.enabled:
@@ -48,15 +49,64 @@ class KernelTimer:
         e1.record()
         self.events.setdefault(name, []).append((e0, e1))
 
+    # ---- dispatch-attached events (hipExtLaunchKernel): the kernel's own start / end ---------------
+    _rt = None
+
+    @classmethod
+    def _hip(cls):
+        if cls._rt is None:
+            rt = ctypes.CDLL("libamdhip64.so.7")   # the HIP runtime torch already loaded (same SONAME)
+            rt.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+            rt.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+            rt.hipEventSynchronize.argtypes = [ctypes.c_void_p]
+            rt.hipEventDestroy.argtypes = [ctypes.c_void_p]
+            cls._rt = rt
+        return cls._rt
+
+    def kernel_events(self, name):
+        """(start, stop) hipEvent_t handles for a launch whose kernel records them itself, or None when
+        timing is off."""
+        if not self.enabled:
+            return None
+        rt = self._hip()
+        pair = []
+        for _ in range(2):
+            ev = ctypes.c_void_p()
+            if rt.hipEventCreate(ctypes.byref(ev)) != 0:
+                raise RuntimeError("hipEventCreate failed")
+            pair.append(ev)
+        self.hip_pairs.setdefault(name, []).append(tuple(pair))
+        return pair
+
     def reset(self):
         self.events = {}
+        rt = self._rt
+        for pairs in getattr(self, "hip_pairs", {}).values():
+            for a, b in pairs:
+                rt.hipEventDestroy(a)
+                rt.hipEventDestroy(b)
+        self.hip_pairs = {}
 
     def mean_ms(self, name):
+        pairs = getattr(self, "hip_pairs", {}).get(name, [])
+        if pairs:
+            rt = self._hip()
+            tot = 0.0
+            for a, b in pairs:
+                rt.hipEventSynchronize(b)
+                ms = ctypes.c_float()
+                if rt.hipEventElapsedTime(ctypes.byref(ms), a, b) != 0:
+                    raise RuntimeError("hipEventElapsedTime failed")
+                tot += ms.value
+            return tot / len(pairs)
         ev = self.events.get(name, [])
         if not ev:
             return None
         torch.cuda.synchronize()
         return sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+
+    def count(self, name):
+        return len(getattr(self, "hip_pairs", {}).get(name, [])) or len(self.events.get(name, []))
 
 
 TIMER = KernelTimer()
@@ -100,10 +150,14 @@ def gae_scan(rew, val, term, closed, boot, gamma, gae_lambda, use_gae=True, adv=
         _req(t, name, dt, (N, T))
     adv = torch.empty_like(rew) if adv is None else _req(adv, "adv", torch.float32, (N, T))
     ret = torch.empty_like(rew) if ret is None else _req(ret, "ret", torch.float32, (N, T))
-    ev = TIMER.start("gae")
-    rc = lib().xpa_gae_scan(_p(rew), _p(val), _p(term), _p(closed), _p(boot), N, T, float(gamma), float(gae_lambda),
-                            int(bool(use_gae)), _p(adv), _p(ret), _stream(rew.device))
-    TIMER.stop("gae", ev)
+    ev = TIMER.kernel_events("gae")
+    if ev is None:
+        rc = lib().xpa_gae_scan(_p(rew), _p(val), _p(term), _p(closed), _p(boot), N, T, float(gamma), float(gae_lambda),
+                                int(bool(use_gae)), _p(adv), _p(ret), _stream(rew.device))
+    else:
+        rc = lib().xpa_gae_scan_timed(_p(rew), _p(val), _p(term), _p(closed), _p(boot), N, T, float(gamma),
+                                      float(gae_lambda), int(bool(use_gae)), _p(adv), _p(ret), ev[0], ev[1],
+                                      _stream(rew.device))
     _lib.check(rc, "xpa_gae_scan")
     return adv, ret
 
