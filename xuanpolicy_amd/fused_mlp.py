@@ -3,9 +3,12 @@
 Reference network: representation Basic_MLP -> ActorNet (mu or logits) and CriticNet, each a chain of
 mlp_block = Linear -> activation (xuance/torch/representations/mlp.py:21-51,
 xuance/torch/policies/gaussian.py:8-51, categorical.py:16-58, xuance/torch/utils/layers.py:8-24).
-PPOCLIP_Learner.update runs loss.backward() through it (ppoclip_learner.py:46); here the loss kernel
-(K2) hands d loss/d head and d loss/d v straight to this backward, which writes every parameter
-gradient into the flat gradient buffer (flat.FlatState) with:
+PPOCLIP_Learner.update runs loss.backward() through it (ppoclip_learner.py:46).  Two explicit paths
+write every parameter gradient into the flat gradient buffer (flat.FlatState):
+  * forward_hidden() + loss_backward() (the learner's fast path): K13 for the first layer, ONE GEMM
+    for the actor|critic hidden layers when FlatState placed them back to back (head_placement), K12
+    for both heads (activation, output layer, loss, head backward), then one dW and one dX GEMM;
+  * forward() + backward(d_head, d_v) after the K2 loss kernel, for other shapes, with:
   * hipBLASLt GEMMs for dX (the trunk's two heads accumulate with one addmm: no separate add pass);
   * split-K batched GEMMs for dW = dZ^T X written with sum(out=grad view) (see policies._splitk_splits);
   * K10 xpa_act_bwd_colsum: activation backward + bias-gradient column sums in one pass over [B, H]

@@ -1,4 +1,4 @@
-"""PPO-Clip and A2C learners whose loss forward+backward is one HIP kernel (K2).
+"""PPO-Clip and A2C learners whose loss forward+backward runs in hand-written HIP kernels (K2 / K12).
 
 Mirrors (reference paths):
   Learner               xuance/torch/learners/learner.py:10-52 (save_model / load_model / update)
@@ -6,11 +6,14 @@ Mirrors (reference paths):
   A2C_Learner           xuance/torch/learners/policy_gradient/a2c_learner.py:4-50
 Same constructor arguments, same update() signature and the same info-dict keys.
 
-Per update: policy heads forward (PyTorch-ROCm GEMMs) -> xpa_policy_loss_fwd_bwd +
-xpa_policy_loss_finalize (loss scalars, d loss/d mu|logits, d loss/d logstd, d loss/d v) ->
-torch.autograd.backward of those head gradients through the MLP -> [one flat gradient all-reduce
-when data-parallel] -> clip_grad_norm_ -> optimizer.step -> scheduler.step, matching
-ppoclip_learner.py:45-51.  update() returns host floats like the reference (one sync);
+Per update (reference order, ppoclip_learner.py:45-51): forward, loss, backward -> [one flat gradient
+all-reduce when data-parallel] -> clip_grad_norm_ -> optimizer.step -> scheduler.step.
+  * update(): policy heads forward (PyTorch-ROCm GEMMs) -> K2 xpa_policy_loss_fwd_bwd + finalize
+    (loss scalars, d loss/d mu|logits, d loss/d logstd, d loss/d v) -> autograd backward of those
+    head gradients -> K9 fused clip + Adam when the parameters are flat.
+  * update_fused() (the agent's hot loop, MLP policies with flat parameters): fused_mlp's explicit
+    forward/backward with K13 (first layer), one paired hidden GEMM, K12 (heads + loss + head
+    backward) and K9 — no autograd graph (DESIGN.md §3).  update() returns host floats like the reference (one sync);
 update_fused() keeps everything on device for the agent's hot loop.
 """
 import os
