@@ -40,6 +40,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-updates", type=int, default=16, help="updates timed in the bounded CPU sample")
     p.add_argument("--no-sweep", action="store_true")
+    p.add_argument("--no-per", action="store_true", help="skip the C5 PER (K6) measurement")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
     return p.parse_args()
@@ -129,6 +130,89 @@ def gae_sweep(device, sizes=(4096, 65536, 262144, 1048576), horizon=128, reps=7)
     del flush
     torch.cuda.empty_cache()
     return out
+
+
+def per_bench(device, n_envs=8, n_size=131072, batch=2048, frames=True, reps=50):
+    """C5 (BASELINE.json configs[4]): K6 on 8 x 131 072 = 1 M transitions, batch 2048, f64 trees.
+    Times xpa_per_sample and xpa_per_update_priorities (HIP events over `reps` back-to-back calls on
+    the launch stream), the K4 gather of 2048 uint8 4x84x84 frame pairs (obs + next obs) out of the
+    1 M-transition replay, and the restated reference (oracle/per_ref.py, the reference's Python trees)
+    on one host core for the same sample + update."""
+    import torch
+    from xuanpolicy_amd import ops
+    from xuanpolicy_amd.per import PerOffPolicyBuffer
+
+    class _Space:
+        def __init__(self, shape):
+            self.shape = shape
+    buf = PerOffPolicyBuffer(_Space((4, 84, 84) if frames else (1,)), _Space(()), {}, n_envs, n_size, batch, 0.6,
+                             device=device, obs_dtype=torch.uint8)
+    cap = buf.capacity
+    g = torch.Generator(device=device).manual_seed(0)
+    buf.sum_tree[:, cap:] = torch.rand((n_envs, cap), generator=g, device=device, dtype=torch.float64) + 0.05
+    buf.min_tree[:, cap:] = buf.sum_tree[:, cap:]
+    lvl = cap
+    while lvl > 1:
+        half = lvl // 2
+        buf.sum_tree[:, half:lvl] = buf.sum_tree[:, lvl:2 * lvl:2] + buf.sum_tree[:, lvl + 1:2 * lvl:2]
+        buf.min_tree[:, half:lvl] = torch.minimum(buf.min_tree[:, lvl:2 * lvl:2], buf.min_tree[:, lvl + 1:2 * lvl:2])
+        lvl = half
+    buf.size, buf.ptr = n_size, 0
+    prio = torch.rand(batch, generator=g, device=device) * 4
+    steps, flat, _ = buf.sample_indices(0.4)
+    torch.cuda.synchronize()
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e3
+    t_sample = timed(lambda: buf.sample_indices(0.4))
+    t_update = timed(lambda: buf.update_priorities(steps, prio, check=False))
+    res = {"config": "C5: %d envs x %d slots (%d transitions, capacity 2^%d per env), batch %d, f64 trees" %
+                     (n_envs, n_size, n_envs * n_size, cap.bit_length() - 1, batch),
+           "sample_us": round(t_sample, 2), "update_priorities_us": round(t_update, 2),
+           "bound": "latency (log2(capacity) dependent tree levels per draw / update)"}
+    if frames:
+        obs_rows = buf.observations.reshape(n_envs * n_size, -1)
+        out = torch.empty((batch, obs_rows.shape[1]), dtype=torch.uint8, device=device)
+        t_gather = timed(lambda: (ops.gather_minibatch(flat, obs_rows, obs_out=out),
+                                  ops.gather_minibatch(flat, buf.next_observations.reshape(n_envs * n_size, -1),
+                                                       obs_out=out)))
+        gb = 2 * 2 * batch * obs_rows.shape[1]
+        res.update({"gather_frames_us": round(t_gather, 2), "gather_bytes": gb,
+                    "gather_GBps": round(gb / t_gather / 1e3, 1), "gather_frac_of_hbm_peak":
+                    round(gb / t_gather / 1e3 / HBM_PEAK_GBS, 4)})
+    del buf
+    torch.cuda.empty_cache()
+    # restated reference on the host (one core, the reference is single-threaded Python)
+    sys.path.insert(0, REPO)
+    import numpy as np
+    from oracle.per_ref import PerBufferRef
+    ref = PerBufferRef(n_envs, n_size, batch, 0.6, obs_shape=(1,))
+    rng = np.random.default_rng(0)
+    for i in range(n_envs):
+        vals = list(rng.random(cap) + 0.05)
+        ref.it_sum[i].value[cap:] = vals
+        ref.it_min[i].value[cap:] = vals
+        for node in range(cap - 1, 0, -1):
+            ref.it_sum[i].value[node] = ref.it_sum[i].value[2 * node] + ref.it_sum[i].value[2 * node + 1]
+            ref.it_min[i].value[node] = min(ref.it_min[i].value[2 * node], ref.it_min[i].value[2 * node + 1])
+    ref.size = n_size
+    t0 = time.perf_counter()
+    st, _ = ref.sample_indices(0.4, rng.random(batch))
+    t1 = time.perf_counter()
+    ref.update_priorities(st.astype(np.int64), rng.random(batch).astype(np.float32) * 4)
+    t2 = time.perf_counter()
+    res["cpu_reference_restated"] = {"sample_us": round((t1 - t0) * 1e6, 1), "update_priorities_us":
+                                     round((t2 - t1) * 1e6, 1), "cores": 1, "kind": "port"}
+    res["speedup_sample_update"] = round(((t2 - t0) * 1e6) / (t_sample + t_update), 1)
+    return res
 
 
 def cpu_baseline(args, cores):
@@ -274,6 +358,8 @@ def main():
         }
         if not args.no_sweep and world == 1:
             result["gae_sweep_flushed"] = gae_sweep(device, horizon=T)
+        if not args.no_per and world == 1:
+            result["per_kernels"] = per_bench(device)
         if not args.no_cpu_baseline and world == 1:
             cores = min(16, len(os.sched_getaffinity(0)))
             result["cpu_baseline"] = cpu_baseline(args, cores)

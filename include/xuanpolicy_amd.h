@@ -248,6 +248,33 @@ int xpa_rollout_policy_head(int dist, int act, int64_t n_envs, int64_t act_dim, 
 int xpa_value_head(int act, int64_t n, int64_t hidden, int64_t ld, const float *z_critic, float slope,
                    const float *w_critic, const float *b_critic, float *v_out, xpa_stream_t stream);
 
+/* K6 — prioritized replay (PerOffPolicyBuffer, memory_tools.py:369-492; Sum/MinSegmentTree,
+ * segtree_tool.py:4-86) with f64 trees on device: one [n_envs, 2*capacity] array per tree (node 1 =
+ * root, leaf i at capacity + i; neutral 0 / +inf), capacity = next power of two >= n_size.
+ * xpa_per_store: leaf ptr of every env = max_priority[e] ** alpha, ancestors updated (store, :437-439).
+ * xpa_per_update_priorities: for each env e, entries k of idx / priorities [n_envs, batch_per_env]:
+ *   leaf = (p == 0 ? 1e-8 : p) ** alpha (a repeated index keeps its last entry, as the sequential
+ *   reference loop does), max_priority[e] = max(max_priority[e], p); ancestors rebuilt level by
+ *   level.  An index outside [0, size) is skipped and counted in *err (the reference asserts).
+ *   scratch: int32 [n_envs, capacity] filled with -1 once; left at -1.
+ * xpa_per_sample: per env, batch_per_env stratified draws mass = u*len + k*len with len =
+ *   sum(0, size - 1) / batch_per_env (leaves [0, size-2]: the reference's exclusive end), the
+ *   prefix-sum descent, and the IS weights (p_sample * size^-beta) / (p_min * size^-beta).  u from
+ *   `uniforms` (f64 [n_envs*batch_per_env], e.g. the reference's recorded random.random() draws) or, if
+ *   NULL, a counter hash of (seed, counter, env, k).  steps = index (wrap_uint8 != 0: index & 255, the
+ *   reference's astype(np.uint8)), flat_index (optional) = env * n_size + step for
+ *   xpa_gather_minibatch.  size >= 2 (the reference recurses forever at size 1). */
+int xpa_per_store(double *sum_tree, double *min_tree, const double *max_priority, int64_t n_envs,
+                  int64_t capacity, int64_t ptr, double alpha, xpa_stream_t stream);
+int xpa_per_update_priorities(double *sum_tree, double *min_tree, double *max_priority, int *scratch,
+                              int64_t n_envs, int64_t capacity, int64_t size, const int64_t *idx,
+                              const float *priorities, int64_t batch_per_env, double alpha, int *err,
+                              xpa_stream_t stream);
+int xpa_per_sample(const double *sum_tree, const double *min_tree, int64_t n_envs, int64_t capacity, int64_t size,
+                   int64_t batch_per_env, int64_t n_size, const double *uniforms, uint32_t seed, uint32_t counter,
+                   double beta, int wrap_uint8, int64_t *steps, int64_t *flat_index, double *weights,
+                   xpa_stream_t stream);
+
 /* K13 — first representation layer Linear(d_in, 256) + activation for a small d_in (<= 64): Basic_MLP's
  * first mlp_block (xuance/torch/representations/mlp.py:21-51, utils/layers.py:8-24) as HBM-streaming
  * kernels.  Forward: h = act(x W^T + b), x [rows, d_in] (row stride ldx), w [256, d_in], h [rows, 256]

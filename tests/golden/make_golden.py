@@ -16,6 +16,10 @@ Fixtures:
                       (oracle/synth_env.py) in the reference's DummyVecEnv_Gym: every stored step,
                       every closure, the permutations, learner infos, initial and final parameters.
   rms.npz      G7     RunningMeanStd (statistic_tools.py:35-112) update sequences.
+  per.npz      G6     PerOffPolicyBuffer (memory_tools.py:369-492) + Sum/MinSegmentTree (segtree_tool.py):
+                      store / sample(beta) / update_priorities rounds with every uniform random.random()
+                      returned to the sampler recorded, the trees after every call, max priorities, the
+                      sampled indices (incl. the uint8 wrap for n_size > 256), IS weights and batches.
 """
 import os
 import sys
@@ -290,6 +294,68 @@ def capture_rms(seed=3):
     print("rms.npz", len(out))
 
 
+# ----------------------------------------------------------------------------------------------
+def capture_per():
+    import random
+    import xuance.common.memory_tools as mt
+    out = {}
+    cases = [("small", 2, 100, 32, 0.6, [40, 40, 40], 0.4), ("wrap", 1, 300, 16, 0.5, [290, 20], 0.7)]
+    for tag, n_envs, n_size, batch, alpha, stores, beta in cases:
+        rng = np.random.default_rng(11)
+        random.seed(5)
+        uniforms = []
+        orig = random.random
+
+        def rec():
+            u = orig()
+            uniforms.append(u)
+            return u
+        mt.random.random = rec
+        buf = mt.PerOffPolicyBuffer(gym.spaces.Box(-1, 1, (3,)), gym.spaces.Discrete(4), {}, n_envs, n_size, batch,
+                                    alpha)
+        cap = buf._it_sum[0]._capacity
+        pre = "%s/" % tag
+        out[pre + "config"] = np.asarray([n_envs, n_size, batch, cap], np.int64)
+        out[pre + "alpha_beta"] = np.asarray([alpha, beta], np.float64)
+        step_obs, step_act, step_rew, step_term, step_next = [], [], [], [], []
+        for r, n_store in enumerate(stores):
+            for _ in range(n_store):
+                o = rng.normal(0, 1, (n_envs, 3)).astype(np.float32)
+                a = rng.integers(0, 4, n_envs)
+                rw = rng.normal(0, 1, n_envs).astype(np.float32)
+                te = (rng.random(n_envs) < 0.1).astype(np.float32)
+                nx = rng.normal(0, 1, (n_envs, 3)).astype(np.float32)
+                buf.store(o, a, rw, te, nx)
+                step_obs.append(o), step_act.append(a), step_rew.append(rw), step_term.append(te), step_next.append(nx)
+            pr = "%sr%d/" % (pre, r)
+            out[pr + "n_store"] = np.asarray(n_store)
+            out[pr + "tree_sum_after_store"] = np.stack([np.asarray(t._value, np.float64) for t in buf._it_sum])
+            out[pr + "tree_min_after_store"] = np.stack([np.asarray(t._value, np.float64) for t in buf._it_min])
+            n_u = len(uniforms)
+            ob, ac, rw, te, nx, w, idx = buf.sample(beta)
+            out[pr + "uniforms"] = np.asarray(uniforms[n_u:], np.float64)
+            out[pr + "step_choices"] = np.asarray(idx)
+            out[pr + "weights"] = np.asarray(w, np.float64)
+            out[pr + "obs"], out[pr + "act"], out[pr + "rew"] = ob, ac, rw
+            out[pr + "term"], out[pr + "next"] = te, nx
+            prio = (rng.random(batch) * 2.0).astype(np.float32)
+            prio[::7] = 0.0
+            out[pr + "priorities"] = prio
+            # The sampled indices are uint8 (memory_tools.py:465).  Under the pinned NumPy 1.21,
+            # `idx += capacity` in SegmentTree.__setitem__ promotes uint8 + int to int64; NumPy 2 raises
+            # OverflowError once capacity > 255.  Pass the same (wrapped) values as int64 = NumPy 1.21.
+            buf.update_priorities(np.asarray(idx).astype(np.int64), prio)
+            out[pr + "tree_sum_after_update"] = np.stack([np.asarray(t._value, np.float64) for t in buf._it_sum])
+            out[pr + "tree_min_after_update"] = np.stack([np.asarray(t._value, np.float64) for t in buf._it_min])
+            out[pr + "max_priority"] = np.array(buf._max_priority, np.float64, copy=True)
+            out[pr + "size_ptr"] = np.asarray([buf.size, buf.ptr], np.int64)
+        out[pre + "obs"], out[pre + "act"] = np.stack(step_obs), np.stack(step_act)
+        out[pre + "rew"], out[pre + "term"], out[pre + "next"] = np.stack(step_rew), np.stack(step_term), np.stack(step_next)
+        mt.random.random = orig
+    np.savez_compressed(os.path.join(HERE, "per.npz"), **out)
+    print("per.npz", len(out))
+
+
 if __name__ == "__main__":
     os.makedirs("/tmp/xref_run", exist_ok=True)
     os.chdir("/tmp/xref_run")
@@ -298,3 +364,4 @@ if __name__ == "__main__":
     capture_agent("ppo", False, 17, 6)
     capture_agent("a2c", True, 4, 2)
     capture_rms()
+    capture_per()

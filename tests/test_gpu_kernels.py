@@ -404,3 +404,29 @@ def test_splitk_linear_matches_linear():
         for a, b in ((lin.weight.grad, ref.weight.grad), (lin.bias.grad, ref.bias.grad)):
             a, b = _h(a).astype(np.float64), _h(b).astype(np.float64)
             assert np.abs(a - b).max() <= 2e-5 * np.abs(b).max(), (np.abs(a - b).max(), np.abs(b).max())
+
+
+@pytest.mark.parametrize("row_shape,dtype", [((4, 84, 84), torch.uint8), ((17,), torch.float32), ((3,), torch.uint8),
+                                             ((1024,), torch.float32), ((4, 84, 84), torch.float32)])
+def test_gather_minibatch_row_shapes(row_shape, dtype):
+    """K4 for narrow rows, 4-byte and byte rows and the wide-row path (>= 4 KiB, Atari frames), with
+    out-of-range indices zeroed and the adv moments computed alongside."""
+    from xuanpolicy_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(1)
+    R, B = 3000, 777
+    if dtype == torch.uint8:
+        src = torch.randint(0, 256, (R,) + row_shape, generator=g, device="cuda", dtype=torch.int64).to(torch.uint8)
+    else:
+        src = torch.randn((R,) + row_shape, generator=g, device="cuda")
+    idx = torch.randint(0, R, (B,), generator=g, device="cuda")
+    idx[3] = R + 1
+    idx[10] = -5
+    adv = torch.randn(R, generator=g, device="cuda")
+    out, part = ops.gather_minibatch(idx, src, adv=adv)
+    ok = (idx >= 0) & (idx < R)
+    exp = torch.zeros_like(out)
+    exp[ok] = src[idx[ok]]
+    assert torch.equal(out, exp)
+    a = adv[idx[ok]].double()
+    np.testing.assert_allclose(part[:, 0].sum().item(), a.sum().item(), rtol=1e-12, atol=1e-9)
+    np.testing.assert_allclose(part[:, 1].sum().item(), (a * a).sum().item(), rtol=1e-12)

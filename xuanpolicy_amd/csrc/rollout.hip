@@ -58,6 +58,30 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const int64_t *__restr
     }
 }
 
+// Wide rows (>= 4 KiB, e.g. 4x84x84 uint8 frames of the replay buffer): one block per (row, 16 KiB
+// chunk), four independent 16-B non-temporal loads per thread in flight.
+constexpr int kWideU = 4;
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void gather_wide_kernel(const int64_t *__restrict__ idx, int64_t n_rows,
+                                                          const u4v *__restrict__ src, int64_t row_vecs,
+                                                          int64_t chunks, u4v *__restrict__ dst) {
+    const int64_t row = (int64_t)blockIdx.x / chunks, chunk = (int64_t)blockIdx.x - row * chunks;
+    const int64_t sr = idx[row];
+    const bool ok = sr >= 0 && sr < n_rows;
+    const int64_t c0 = chunk * 256 * kWideU + threadIdx.x;
+    u4v v[kWideU];
+#pragma unroll
+    for (int u = 0; u < kWideU; ++u) {
+        const int64_t c = c0 + u * 256;
+        v[u] = (ok && c < row_vecs) ? __builtin_nontemporal_load(src + sr * row_vecs + c) : u4v{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < kWideU; ++u) {
+        const int64_t c = c0 + u * 256;
+        if (c < row_vecs) __builtin_nontemporal_store(v[u], dst + row * row_vecs + c);
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // K5 RunningMeanStd
 // ---------------------------------------------------------------------------------------------
@@ -431,7 +455,15 @@ XPA_API int xpa_gather_minibatch(const int64_t *idx, int64_t batch, int64_t n_ro
     const int64_t blocks = xpa_gather_num_partials(batch);
     hipStream_t s = (hipStream_t)stream;
     const uintptr_t al = (uintptr_t)obs | (uintptr_t)obs_out;
-    if (obs_row_bytes % 16 == 0 && al % 16 == 0)
+    if (obs_row_bytes >= 4096 && obs_row_bytes % 16 == 0 && al % 16 == 0) {
+        const int64_t rv = obs_row_bytes / 16, chunks = (rv + 256 * kWideU - 1) / (256 * kWideU);
+        if (batch * chunks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+        hipLaunchKernelGGL(gather_wide_kernel, dim3((unsigned)(batch * chunks)), dim3(256), 0, s, idx, n_rows,
+                           (const u4v *)obs, rv, chunks, (u4v *)obs_out);
+        if (adv_partials)  // the moments alone (no row copy)
+            hipLaunchKernelGGL(gather_rows_kernel<uint4>, dim3((unsigned)blocks), dim3(256), 0, s, idx, batch, n_rows,
+                               (const uint4 *)obs, (int64_t)0, (uint4 *)obs_out, adv, adv_partials);
+    } else if (obs_row_bytes % 16 == 0 && al % 16 == 0)
         hipLaunchKernelGGL(gather_rows_kernel<uint4>, dim3((unsigned)blocks), dim3(256), 0, s, idx, batch,
                            n_rows, (const uint4 *)obs, obs_row_bytes / 16, (uint4 *)obs_out, adv, adv_partials);
     else if (obs_row_bytes % 4 == 0 && al % 4 == 0)
