@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--cpu-updates", type=int, default=16, help="updates timed in the bounded CPU sample")
     p.add_argument("--no-sweep", action="store_true")
     p.add_argument("--no-per", action="store_true", help="skip the C5 PER (K6) measurement")
+    p.add_argument("--no-c3", action="store_true", help="skip the C3 Atari A2C measurement")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
     return p.parse_args()
@@ -215,6 +216,31 @@ def per_bench(device, n_envs=8, n_size=131072, batch=2048, frames=True, reps=50)
     return res
 
 
+def c3_bench(device, n_envs=1024, n_steps=128, steps=2, warmup=1):
+    """C3 (BASELINE.json configs[2]): A2C, SynthAtari uint8 4x84x84 frames, AC_CNN_Atari, 1024 envs x
+    128 steps (a2c/atari.yaml: 4 epochs x 8 minibatches of 16 384), everything resident on the GPU."""
+    import torch
+    from xuanpolicy_amd.runner import build_atari_a2c
+    agent = build_atari_a2c(n_envs=n_envs, n_steps=n_steps, device=device)
+    for _ in range(warmup):
+        agent.train(n_steps)
+    torch.cuda.synchronize()
+    agent.timers = {"rollout": 0.0, "update": 0.0}
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        agent.train(n_steps)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    res = {"workload": "A2C SynthAtari(4x84x84 uint8, 6 actions) num_envs=%d horizon=%d, a2c/atari.yaml (n_epoch 4, "
+                       "n_minibatch 8), AC_CNN_Atari [32,64,64]/[8,4,3]/[4,2,1] + fc 512" % (n_envs, n_steps),
+           "metric": "env-steps/s", "value": round(n_envs * n_steps * steps / el, 1),
+           "ms_per_iteration": round(el / steps * 1e3, 2), "iterations": steps, "dtype": "f32 (uint8 frames)",
+           "host_timer_split_ms": {k: round(v / steps * 1e3, 2) for k, v in agent.timers.items()}}
+    del agent
+    torch.cuda.empty_cache()
+    return res
+
+
 def cpu_baseline(args, cores):
     """The oracle's restatement of the reference loop (oracle/cpu_ref.AgentLoopRef: per-env
     DummyVecEnv stepping, per-env finish_path, numpy fancy-index sampling, torch-CPU learner with
@@ -358,6 +384,8 @@ def main():
         }
         if not args.no_sweep and world == 1:
             result["gae_sweep_flushed"] = gae_sweep(device, horizon=T)
+        if not args.no_c3 and world == 1:
+            result["c3_atari_a2c"] = c3_bench(device)
         if not args.no_per and world == 1:
             result["per_kernels"] = per_bench(device)
         if not args.no_cpu_baseline and world == 1:

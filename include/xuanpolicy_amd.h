@@ -275,6 +275,28 @@ int xpa_per_sample(const double *sum_tree, const double *min_tree, int64_t n_env
                    double beta, int wrap_uint8, int64_t *steps, int64_t *flat_index, double *weights,
                    xpa_stream_t stream);
 
+/* Column store of raw observation rows into the rollout buffer at the device cursor:
+ * dst[(i * horizon + cursor->ptr) * row_bytes ...] = src[i * row_bytes ...] for i < n (the uint8 Atari
+ * frames of DummyOnPolicyBuffer_Atari.store, memory_tools.py:196-204, 526-560).  row_bytes % 16 == 0,
+ * 16-B aligned pointers. */
+int xpa_store_column(const void *src, int64_t n, int64_t row_bytes, void *dst, int64_t horizon,
+                     const xpa_cursor_t *cursor, xpa_stream_t stream);
+
+/* K15 — SynthAtari env step (the Atari-shaped synthetic env of SURVEY.md §8(d); spec + CPU checker
+ * oracle/synth_env.py SynthAtariEnv), replacing DummyVecEnv_Atari / Atari_Env stepping for the benchmark
+ * (gym_vec_env.py:201-212, 234-238; gym_env.py:186-241).  stack / final_obs: uint8 [n_envs, 84, 84, 4]
+ * (channel 3 newest); the action is the one-hot row of act_in (row stride ld_act) written by the
+ * sampler.  Writes the stepped stack to final_obs, reward sign, terminated (life lost or game over),
+ * truncated (game over or step limit); on game over the env resets (stack = 4 copies of the new
+ * episode's first frame).  Per-env int32 state: ep_step, ep_index, lives, paddle; f32 scores.
+ * xpa_synthatari_reset: stack = the first frame of episode ep_index[n], 4 times. */
+int xpa_synthatari_step(int64_t n_envs, int64_t n_actions, const float *act_in, int64_t ld_act, uint32_t seed,
+                        int32_t max_episode_steps, uint8_t *stack, uint8_t *final_obs, float *rew, uint8_t *term,
+                        uint8_t *trunc, int32_t *ep_step, int32_t *ep_index, int32_t *lives, int32_t *paddle,
+                        float *ep_score, float *ep_last_score, int32_t *ep_last_len, xpa_stream_t stream);
+int xpa_synthatari_reset(int64_t n_envs, uint32_t seed, uint8_t *stack, const int32_t *ep_index,
+                         xpa_stream_t stream);
+
 /* K13 — first representation layer Linear(d_in, 256) + activation for a small d_in (<= 64): Basic_MLP's
  * first mlp_block (xuance/torch/representations/mlp.py:21-51, utils/layers.py:8-24) as HBM-streaming
  * kernels.  Forward: h = act(x W^T + b), x [rows, d_in] (row stride ldx), w [256, d_in], h [rows, 256]

@@ -215,3 +215,86 @@ class SynthBoxVec:
             self.ep_score[ids] = 0.0
             self.state[ids] = synthbox_reset_state(self.seed, self.env_ids[ids], self.episode[ids], self.D)
         return final, r, term, trunc, self.state.copy()
+
+
+# ------------------------------------------------------------------------------------------------
+# SynthAtari: the Atari-shaped synthetic env of SURVEY.md §8(d) (C3 / C5 shapes).
+# Observation uint8 [84, 84, 4] (HWC frame stack, channel 3 = newest, as Atari_Env's LazyFrames
+# concatenation, xuance/environment/gym/gym_env.py:212-241), Discrete(n_actions), reward in {-1, 0, 1}
+# (np.sign, gym_env.py:230), lives with the reference's flag rules (gym_env.py:193-209):
+#   life lost (lives > 0 left): terminated = True, truncated = False (the episode continues)
+#   game over / step limit:     terminated = True, truncated = True  (reset)
+# Dynamics (counter hash only):
+#   dx(a) = ((a + 1) % 3 - 1) * 3;  px = clip(px + dx(a), 0, 76)                  (paddle column)
+#   ball column bx(t) = hash4(seed ^ SALT_BALL, env, ep, t >> 4) % 77, row by(t) = (t & 15) * 5
+#   at t & 15 == 15: r = +1 if |px - bx(t)| <= 8 else -1 (a life lost); else r = 0
+#   frame(ep, t, px)[y, x] = hash4(seed ^ SALT_PIX, env, ep, y*84 + x) >> 27    (static noise 0..31)
+#                            255 inside the 8x8 ball at (by(t), bx(t)), 200 on the paddle rows 78..81
+#   step: t = ep_step; ... ep_step += 1; new frame(ep, ep_step, px) pushed onto the stack
+#   reset: lives 5, px 38, ep_step 0, stack = 4 copies of frame(ep, 0, 38)
+# ------------------------------------------------------------------------------------------------
+ATARI_HW = 84
+ATARI_STACK = 4
+ATARI_LIVES = 5
+ATARI_PX0 = 38
+SALT_PIX = 0xA7A21000
+SALT_BALL = 0xBA11B000
+
+
+def atari_dx(a):
+    return ((np.asarray(a, np.int64) + 1) % 3 - 1) * 3
+
+
+def atari_ball(seed, env, ep, t):
+    bx = hash4(seed ^ SALT_BALL, env, ep, np.uint32(int(t) >> 4)) % np.uint32(77)
+    return int(bx), (int(t) & 15) * 5
+
+
+def atari_frame(seed, env, ep, t, px):
+    p = np.arange(ATARI_HW * ATARI_HW, dtype=np.uint32)
+    f = (hash4(seed ^ SALT_PIX, env, ep, p) >> np.uint32(27)).astype(np.uint8).reshape(ATARI_HW, ATARI_HW)
+    bx, by = atari_ball(seed, env, ep, t)
+    f[by:by + 8, bx:bx + 8] = 255
+    f[78:82, px:px + 8] = 200
+    return f
+
+
+class SynthAtariEnv:
+    """One SynthAtari env with the Atari_Env step contract (obs, reward, terminated, truncated, info)."""
+
+    def __init__(self, env_id, seed=1, n_actions=6, max_episode_steps=27000):
+        self.env_id, self.seed, self.n_actions, self.max_episode_steps = int(env_id), int(seed), n_actions, max_episode_steps
+        self.ep = 0
+        self._reset_state()
+
+    def _reset_state(self):
+        self.lives, self.px, self.ep_step, self.score = ATARI_LIVES, ATARI_PX0, 0, 0.0
+        f = atari_frame(self.seed, self.env_id, self.ep, 0, self.px)
+        self.stack = np.repeat(f[:, :, None], ATARI_STACK, axis=2)
+
+    def reset(self):
+        return self.stack.copy(), {"episode_step": 0}
+
+    def step(self, a):
+        t = self.ep_step
+        self.px = int(np.clip(self.px + int(atari_dx(a)), 0, 76))
+        r = 0.0
+        if (t & 15) == 15:
+            bx, _ = atari_ball(self.seed, self.env_id, self.ep, t)
+            r = 1.0 if abs(self.px - bx) <= 8 else -1.0
+        self.ep_step += 1
+        self.score += r
+        if r < 0:
+            self.lives -= 1
+        game_over = self.lives == 0 or self.ep_step >= self.max_episode_steps
+        terminated = bool(game_over or r < 0)
+        truncated = bool(game_over)
+        f = atari_frame(self.seed, self.env_id, self.ep, self.ep_step, self.px)
+        self.stack = np.concatenate([self.stack[:, :, 1:], f[:, :, None]], axis=2)
+        obs = self.stack.copy()
+        info = {"episode_step": self.ep_step, "episode_score": self.score}
+        if game_over:
+            self.ep += 1
+            self._reset_state()
+            info["reset_obs"] = self.stack.copy()
+        return obs, np.float32(r), terminated, truncated, info

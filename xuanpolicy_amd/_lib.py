@@ -16,7 +16,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "libxuanpolicy_amd.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
-SOURCES = ["gae.hip", "loss.hip", "rollout.hip", "optim.hip", "mlp.hip", "head.hip", "thin.hip", "per.hip"]
+SOURCES = ["gae.hip", "loss.hip", "rollout.hip", "optim.hip", "mlp.hip", "head.hip", "thin.hip", "per.hip", "atari.hip"]
 HEADER = os.path.join(REPO_DIR, "include", "xuanpolicy_amd.h")
 
 ABI_VERSION = 1
@@ -70,6 +70,10 @@ SIGNATURES = {
                                                  c_p, c_p]),
     "xpa_per_sample": (ctypes.c_int, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_u32, c_u32, ctypes.c_double,
                                       ctypes.c_int, c_p, c_p, c_p, c_p]),
+    "xpa_store_column": (ctypes.c_int, [c_p, c_i64, c_i64, c_p, c_i64, c_p, c_p]),
+    "xpa_synthatari_step": (ctypes.c_int, [c_i64, c_i64, c_p, c_i64, c_u32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                                           c_p, c_p, c_p, c_p, c_p]),
+    "xpa_synthatari_reset": (ctypes.c_int, [c_i64, c_u32, c_p, c_p, c_p]),
     "xpa_thin_bwd_num_partials": (c_i64, [c_i64]),
     "xpa_thin_linear_act_fwd": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f32, c_p, c_i64,
                                                c_p]),

@@ -89,9 +89,14 @@ class _OnPolicyAgent:
         self.ret_count = torch.full((1,), 1e-4, dtype=torch.float64, device=dev)
         self.returns = torch.zeros((N,), **f32)
         self.cursor = ops.new_cursor(dev)
-        self.obs_norm = torch.empty((N, D), **f32)
-        self.boot_obs = torch.empty((N, D), **f32)
-        self.rms_part = torch.empty((2 * ops.rms_num_partials(N), D), dtype=torch.float64, device=dev)
+        # Raw observations (uint8 Atari frames without obs normalisation, DummyOnPolicyBuffer_Atari): stored
+        # and fed to the policy as they are (AC_CNN_Atari scales by 1/255 on device).
+        self.raw_obs = self.memory.observations.dtype == torch.uint8 and not self.use_obsnorm
+        self.obs_norm = None if self.raw_obs else torch.empty((N, D), **f32)
+        self.boot_obs = None if self.raw_obs else torch.empty((N, D), **f32)
+        self.rms_part = (torch.empty((2 * ops.rms_num_partials(N), D), dtype=torch.float64, device=dev)
+                         if self.use_obsnorm else None)
+        self._policy_in = self.obs_norm
         self.logp_scratch = None if self.algo == "ppo" else torch.zeros((N, T), **f32)
         self.obs_mb = None
         self.adv_part = None
@@ -141,11 +146,11 @@ class _OnPolicyAgent:
         env_in = self.envs.act_in if self.device_env else self._act_scratch()
         fm = self._rollout_mlp()
         if fm is not None:
-            fm.rollout_act(self.obs_norm, self.dist, self.cursor, self.seed, mem.actions, logp_buf, mem.values, env_in,
-                           act_clip=1.0)
+            fm.rollout_act(self._policy_in, self.dist, self.cursor, self.seed, mem.actions, logp_buf, mem.values,
+                           env_in, act_clip=1.0)
             return
         with torch.no_grad():
-            head, logstd, v = policy_heads(self.policy, self.obs_norm)
+            head, logstd, v = policy_heads(self.policy, self._policy_in)
         ops.rollout_sample(self.dist, head.contiguous(), logstd, v.contiguous(), self.cursor, self.seed,
                            mem.actions, logp_buf, mem.values, env_in, act_clip=1.0)
 
@@ -157,6 +162,11 @@ class _OnPolicyAgent:
 
     def _post(self, rew, term, trunc, final_obs):
         mem = self.memory
+        if self.raw_obs:
+            with torch.no_grad():
+                v_boot = policy_heads(self.policy, final_obs)[2]
+            self._post_kernel(rew, term, trunc, v_boot)
+            return
         self._normalize_into(final_obs, self.boot_obs, False)
         fm = self._rollout_mlp()
         if fm is not None:
@@ -164,6 +174,10 @@ class _OnPolicyAgent:
         else:
             with torch.no_grad():
                 v_boot = policy_heads(self.policy, self.boot_obs)[2]
+        self._post_kernel(rew, term, trunc, v_boot)
+
+    def _post_kernel(self, rew, term, trunc, v_boot):
+        mem = self.memory
         ops.rollout_post(rew, term, trunc, v_boot.contiguous(), self.cursor, self.ret_mean, self.ret_var,
                          self.ret_count, self.returns, mem.rewards, mem.terminals, mem.closed, mem.boot, self.gamma,
                          mask_returns=(self.algo == "ppo"), use_rewnorm=self.use_rewnorm,
@@ -172,9 +186,13 @@ class _OnPolicyAgent:
     def _rollout_step_device(self):
         env = self.envs
         x = env.obs
-        if self.use_obsnorm:
-            ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count, partials=self.rms_part)
-        self._normalize_into(x, self.obs_norm, True)
+        if self.raw_obs:
+            ops.store_column(x, self.memory.observations, self.cursor)
+            self._policy_in = x
+        else:
+            if self.use_obsnorm:
+                ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count, partials=self.rms_part)
+            self._normalize_into(x, self.obs_norm, True)
         self._sample_into_buffer()
         env.step_device()
         self._post(env.rew, env.term, env.trunc, env.final_obs)
@@ -202,19 +220,25 @@ class _OnPolicyAgent:
     def _rollout_step_host(self):
         """Same kernels around a host VecEnv (numpy in/out, reset_obs in infos)."""
         env, dev = self.envs, self.device
+        dt = np.uint8 if self.raw_obs else np.float32
+        shape = (self.n_envs,) + (tuple(self.obs_shape) if self.raw_obs else (-1,))
         if self._host_obs is None:
-            self._host_obs = np.asarray(env.buf_obs, np.float32).reshape(self.n_envs, -1)
+            self._host_obs = np.asarray(env.buf_obs, dt).reshape(shape)
         x = torch.as_tensor(self._host_obs, device=dev)
-        if self.use_obsnorm:
-            ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count, partials=self.rms_part)
-        self._normalize_into(x, self.obs_norm, True)
+        if self.raw_obs:
+            ops.store_column(x.contiguous(), self.memory.observations, self.cursor)
+            self._policy_in = x
+        else:
+            if self.use_obsnorm:
+                ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count, partials=self.rms_part)
+            self._normalize_into(x, self.obs_norm, True)
         self._sample_into_buffer()
         t = self._t
         acts = (self.memory.actions[:, t]).cpu().numpy()
         if self.discrete:
             acts = acts.astype(np.int64)
         next_obs, rews, terms, truncs, infos = env.step(acts)
-        next_obs = np.asarray(next_obs, np.float32).reshape(self.n_envs, -1)
+        next_obs = np.asarray(next_obs, dt).reshape(shape)
         self._post(torch.as_tensor(np.asarray(rews, np.float32), device=dev),
                    torch.as_tensor(np.asarray(terms, np.uint8), device=dev),
                    torch.as_tensor(np.asarray(truncs, np.uint8), device=dev), torch.as_tensor(next_obs, device=dev))
@@ -223,7 +247,7 @@ class _OnPolicyAgent:
             if terms[i] or truncs[i]:
                 if self.atari and not truncs[i]:
                     continue
-                obs[i] = np.asarray(infos[i]["reset_obs"], np.float32).reshape(-1)
+                obs[i] = np.asarray(infos[i]["reset_obs"], dt).reshape(obs[i].shape)
                 self.current_episode[i] += 1
         self._host_obs = obs
 

@@ -82,6 +82,19 @@ __global__ __launch_bounds__(256) void gather_wide_kernel(const int64_t *__restr
     }
 }
 
+// Column store: dst[(n * horizon + cursor->ptr) * row_vecs + c] = src[n * row_vecs + c] (raw uint8
+// Atari observations into the rollout buffer, DummyOnPolicyBuffer_Atari.store, memory_tools.py:196-204).
+__global__ __launch_bounds__(256) void store_column_kernel(const u4v *__restrict__ src, int64_t n, int64_t row_vecs,
+                                                           u4v *__restrict__ dst, int64_t horizon,
+                                                           const xpa_cursor_t *__restrict__ cur) {
+    const int64_t t = cur->ptr;
+    const int64_t total = n * row_vecs;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+        const int64_t r = e / row_vecs, c = e - r * row_vecs;
+        __builtin_nontemporal_store(__builtin_nontemporal_load(src + e), dst + (r * horizon + t) * row_vecs + c);
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // K5 RunningMeanStd
 // ---------------------------------------------------------------------------------------------
@@ -615,5 +628,18 @@ XPA_API int xpa_value_head(int act, int64_t n, int64_t hidden, int64_t ld, const
     else if (act == 1) XPA_VH(1);
     else XPA_VH(2);
 #undef XPA_VH
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_store_column(const void *src, int64_t n, int64_t row_bytes, void *dst, int64_t horizon,
+                             const xpa_cursor_t *cursor, xpa_stream_t stream) {
+    if (n <= 0 || row_bytes <= 0 || row_bytes % 16 || horizon <= 0 || !src || !dst || !cursor ||
+        ((uintptr_t)src | (uintptr_t)dst) % 16)
+        return (int)hipErrorInvalidValue;
+    const int64_t rv = row_bytes / 16;
+    int64_t blocks = (n * rv + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(store_column_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const u4v *)src, n, rv, (u4v *)dst, horizon, cursor);
     return xpa_launch_status();
 }

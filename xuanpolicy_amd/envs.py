@@ -166,3 +166,105 @@ class SynthBoxVecEnv:
 
     def close(self):
         pass
+
+
+class _ImageBox:
+    def __init__(self, shape):
+        self.shape = tuple(shape)
+        self.low = np.zeros(shape, np.uint8)
+        self.high = np.full(shape, 255, np.uint8)
+        self.dtype = np.uint8
+
+
+class SynthAtariVecEnv:
+    """n_envs SynthAtari envs (uint8 4x84x84 frame stacks, Discrete(n_actions), reward sign, lives) resident
+    on one GPU — the C3 / C5 shapes of BASELINE.json.  Spec and CPU checker: oracle/synth_env.py
+    (SynthAtariEnv); kernel: csrc/atari.hip (K15).  Same interface as SynthBoxVecEnv: obs, act_in,
+    final_obs, rew/term/trunc, step_device(), host step() with the DummyVecEnv_Atari contract."""
+
+    HW, STACK = 84, 4
+
+    def __init__(self, n_envs, n_actions=6, seed=1, max_episode_steps=27000, device=None, shard=0):
+        self.num_envs, self.n_actions = int(n_envs), int(n_actions)
+        self.seed, self.max_episode_steps = int(seed), int(max_episode_steps)
+        self.max_episode_length = self.max_episode_steps
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.shard = int(shard)
+        self.noise_seed = (self.seed ^ ((0x9E3779B9 * self.shard) & 0xFFFFFFFF)) & 0xFFFFFFFF
+        shape = (self.HW, self.HW, self.STACK)
+        self.observation_space = _ImageBox(shape)
+        self.action_space = _Discrete(self.n_actions)
+        dev, N = self.device, self.num_envs
+        self.stack = torch.zeros((N,) + shape, dtype=torch.uint8, device=dev)
+        self.final_obs = torch.zeros((N,) + shape, dtype=torch.uint8, device=dev)
+        self._act = torch.zeros((N, self.n_actions), dtype=torch.float32, device=dev)
+        self.rew = torch.zeros((N,), dtype=torch.float32, device=dev)
+        self.term = torch.zeros((N,), dtype=torch.uint8, device=dev)
+        self.trunc = torch.zeros((N,), dtype=torch.uint8, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.ep_step, self.ep_index = torch.zeros((N,), **i32), torch.zeros((N,), **i32)
+        self.lives, self.paddle = torch.zeros((N,), **i32), torch.zeros((N,), **i32)
+        self.ep_last_len = torch.zeros((N,), **i32)
+        self.ep_score = torch.zeros((N,), dtype=torch.float32, device=dev)
+        self.ep_last_score = torch.zeros((N,), dtype=torch.float32, device=dev)
+        self.reset()
+
+    @property
+    def obs(self):
+        return self.stack
+
+    @property
+    def act_in(self):
+        return self._act
+
+    @property
+    def buf_obs(self):
+        return self.stack
+
+    def reset(self):
+        for t in (self.ep_step, self.ep_index, self.ep_score, self.ep_last_score, self.ep_last_len, self.rew,
+                  self.term, self.trunc, self._act):
+            t.zero_()
+        self.lives.fill_(5)
+        self.paddle.fill_(38)
+        _lib.check(ops.lib().xpa_synthatari_reset(self.num_envs, self.noise_seed, ops._p(self.stack),
+                                                  ops._p(self.ep_index), ops._stream(self.device)),
+                   "xpa_synthatari_reset")
+        return self.stack.clone(), [{} for _ in range(self.num_envs)]
+
+    def step_device(self):
+        rc = ops.lib().xpa_synthatari_step(self.num_envs, self.n_actions, ops._p(self._act), self._act.stride(0),
+                                           self.noise_seed, self.max_episode_steps, ops._p(self.stack),
+                                           ops._p(self.final_obs), ops._p(self.rew), ops._p(self.term),
+                                           ops._p(self.trunc), ops._p(self.ep_step), ops._p(self.ep_index),
+                                           ops._p(self.lives), ops._p(self.paddle), ops._p(self.ep_score),
+                                           ops._p(self.ep_last_score), ops._p(self.ep_last_len),
+                                           ops._stream(self.device))
+        _lib.check(rc, "xpa_synthatari_step")
+
+    def step(self, actions):
+        """DummyVecEnv_Atari contract (gym_vec_env.py:201-212): host copies of (obs, rew, term, trunc, infos);
+        infos[i]['reset_obs'] after a game over."""
+        a = torch.as_tensor(np.asarray(actions) if not isinstance(actions, torch.Tensor) else actions,
+                            device=self.device).long().reshape(-1, 1)
+        self._act.zero_()
+        self._act.scatter_(1, a, 1.0)
+        self.step_device()
+        obs = self.final_obs.cpu().numpy()
+        rew = self.rew.cpu().numpy()
+        term = self.term.cpu().numpy().astype(bool)
+        trunc = self.trunc.cpu().numpy().astype(bool)
+        nxt = self.stack.cpu().numpy()
+        lens, scores = self.ep_step.cpu().numpy(), self.ep_score.cpu().numpy()
+        last_len, last_score = self.ep_last_len.cpu().numpy(), self.ep_last_score.cpu().numpy()
+        infos = []
+        for i in range(self.num_envs):
+            info = {"episode_step": int(last_len[i] if trunc[i] else lens[i]),
+                    "episode_score": float(last_score[i] if trunc[i] else scores[i])}
+            if trunc[i]:
+                info["reset_obs"] = nxt[i].copy()
+            infos.append(info)
+        return obs, rew, term, trunc, infos
+
+    def close(self):
+        pass

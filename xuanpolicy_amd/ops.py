@@ -429,6 +429,19 @@ def rms_update(x, mean, var, count, partials=None):
     _lib.check(lib().xpa_rms_merge(_p(partials), np_, n, dim, _p(mean), _p(var), _p(count), s), "xpa_rms_merge")
 
 
+def store_column(x, buf, cursor):
+    """Raw observation rows x [N, ...] into buf [N, T, ...] at column cursor.ptr (graph-capturable)."""
+    N = x.shape[0]
+    if not x.is_contiguous() or not buf.is_contiguous() or x.device.type != "cuda" or buf.dtype != x.dtype:
+        raise ValueError("store_column: contiguous device tensors of one dtype")
+    if buf.shape[0] != N or tuple(buf.shape[2:]) != tuple(x.shape[1:]):
+        raise ValueError("store_column: buf must be [N, T] + x.shape[1:]")
+    _req(cursor, "cursor", torch.int32, (4,))
+    row_bytes = x[0].numel() * x.element_size()
+    _lib.check(lib().xpa_store_column(_p(x), N, row_bytes, _p(buf), buf.shape[1], _p(cursor), _stream(x.device)),
+               "xpa_store_column")
+
+
 def obs_normalize(x, mean, var, clip_range, out, col_out=None, col_ld=0, cursor=None):
     """K5c: out = clip((x - mean)/(sqrt(var)+1e-8)); optionally also into a buffer column."""
     n, dim = x.shape

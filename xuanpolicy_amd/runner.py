@@ -17,8 +17,9 @@ import torch
 import yaml
 
 from . import agents
-from .envs import SynthBoxVecEnv
-from .policies import (ActivationFunctions, Basic_MLP, REGISTRY as REGISTRY_Policy, REGISTRY_Representation)
+from .envs import SynthAtariVecEnv, SynthBoxVecEnv
+from .policies import (AC_CNN_Atari, ActivationFunctions, Basic_MLP, REGISTRY as REGISTRY_Policy,
+                       REGISTRY_Representation)
 
 CONFIG_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "configs")
 
@@ -56,8 +57,12 @@ def make_envs(config, device=None, shard=0):
         return SynthBoxVecEnv(config.parallels, config.obs_dim, config.act_dim, seed=config.seed,
                               discrete=bool(getattr(config, "discrete", False)),
                               max_episode_steps=getattr(config, "max_episode_steps", 1000), device=device, shard=shard)
-    raise NotImplementedError("env_name %r: only the device-resident SynthBox env is built in; pass any VecEnv "
-                              "with the reference's step contract to the agent directly" % config.env_name)
+    if config.env_name == "Atari" and str(getattr(config, "env_id", "")).startswith("SynthAtari"):
+        return SynthAtariVecEnv(config.parallels, getattr(config, "n_actions", 6), seed=config.seed,
+                                max_episode_steps=getattr(config, "max_episode_steps", 27000), device=device,
+                                shard=shard)
+    raise NotImplementedError("env_name %r: only the device-resident SynthBox / SynthAtari envs are built in; pass "
+                              "any VecEnv with the reference's step contract to the agent directly" % config.env_name)
 
 
 TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning", "tunableop_results0.csv")
@@ -89,6 +94,9 @@ def build_agent(config, device=None, envs=None, shard=0):
     init = torch.nn.init.orthogonal_
     if config.representation == "Basic_MLP":
         rep = Basic_MLP(envs.observation_space.shape, config.representation_hidden_size, None, init, act, device)
+    elif config.representation == "AC_CNN_Atari":   # input_reformat.py:20-35 argument set
+        rep = AC_CNN_Atari(envs.observation_space.shape, config.kernels, config.strides, config.filters, None, init,
+                           act, device, config.fc_hidden_sizes)
     else:
         rep = REGISTRY_Representation[config.representation](envs.observation_space.shape, device)
     policy = REGISTRY_Policy[config.policy](envs.action_space, rep, config.actor_hidden_size, config.critic_hidden_size,
@@ -113,6 +121,16 @@ def build_synthbox_ppo(n_envs=4096, n_steps=128, obs_dim=17, act_dim=6, hidden=2
     cfg.n_epoch, cfg.n_minibatch, cfg.seed, cfg.discrete = n_epoch, n_minibatch, seed, discrete
     cfg.policy = "Categorical_AC" if discrete else "Gaussian_AC"
     cfg.representation_hidden_size = cfg.actor_hidden_size = cfg.critic_hidden_size = [hidden]
+    for k, v in overrides.items():
+        setattr(cfg, k, v)
+    torch.manual_seed(seed)
+    return build_agent(cfg, device)
+
+
+def build_atari_a2c(n_envs=1024, n_steps=128, seed=1, device="cuda:0", **overrides):
+    """The BASELINE.json C3 configuration: A2C, AC_CNN_Atari, SynthAtari 4x84x84 uint8 frames, 6 actions."""
+    cfg = get_arguments("a2c", "atari", "SynthAtari-v0")
+    cfg.parallels, cfg.n_steps, cfg.seed = n_envs, n_steps, seed
     for k, v in overrides.items():
         setattr(cfg, k, v)
     torch.manual_seed(seed)
