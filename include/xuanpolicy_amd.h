@@ -114,7 +114,8 @@ int xpa_policy_loss_finalize(int algo, int dist, int64_t batch, int64_t act_dim,
  * xpa_rms_partials: per-block f64 sums of (x - shift) and (x - shift)^2 over x[n, dim] (row stride
  * ld floats); shift must be the `mean` array later passed to xpa_rms_merge (the running mean).
  * xpa_rms_merge: batch moments from the partials, then update_from_moments into mean/var
- * (f32 [dim]) and *count (f64) — one block.
+ * (f32 [dim]) and *count (f64) — one block.  n = rows the partials cover (n_partials * 256 or fewer
+ * for one rank; the global row count when the partials were SUM-reduced across ranks).
  * xpa_obs_normalize: out = clip((x - mean) / (sqrt(var) + 1e-8), -clip_range, clip_range);
  * also copied to col_out + cursor->ptr*dim (row stride col_ld) when col_out != NULL. */
 int64_t xpa_rms_num_partials(int64_t n);

@@ -1,0 +1,106 @@
+"""GPU: the data-parallel normalisation variants of SURVEY.md §8(e) with 2 ranks sharing the box's one
+GPU over gloo (the RCCL path is the same code with backend "nccl", one GPU per rank):
+  * sync_obs_rms   — RMS partials SUM-reduced before the merge == one RunningMeanStd over all ranks' rows;
+  * global_advnorm — minibatch advantage moments averaged == adv-norm over the concatenated minibatch;
+  * a 2-rank PPO run with both keeps obs statistics and parameters identical on every rank."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), XPA_DIST_BACKEND="gloo")
+    import torch.distributed as dist
+    try:
+        from xuanpolicy_amd import ops
+        from xuanpolicy_amd.distributed import init_from_env
+        init_from_env()
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        # ---- synchronised RMS ----
+        N, D = 300, 17
+        xs = [torch.randn(N, D, generator=torch.Generator().manual_seed(10 + r)).to(dev) * (1 + r) + r for r in
+              range(world)]
+        mean, var = torch.zeros(D, device=dev), torch.ones(D, device=dev)
+        count = torch.full((1,), 1e-4, dtype=torch.float64, device=dev)
+        for _ in range(3):
+            ops.rms_update(xs[rank], mean, var, count,
+                           reduce_partials=lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM), world=world)
+        m1, v1 = torch.zeros(D, device=dev), torch.ones(D, device=dev)
+        c1 = torch.full((1,), 1e-4, dtype=torch.float64, device=dev)
+        for _ in range(3):
+            ops.rms_update(torch.cat(xs), m1, v1, c1)
+        torch.testing.assert_close(mean, m1, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(var, v1, rtol=1e-5, atol=1e-6)
+        assert float(count) == float(c1)
+        # ---- global adv-norm ----
+        B, R, A = 256, 1000, 6
+        g = torch.Generator().manual_seed(99)
+        adv_all = torch.randn(R, generator=g).to(dev) * 3 + 1
+        ret_all = torch.randn(R, generator=g).to(dev)
+        act_all = torch.randn(R, A, generator=g).to(dev)
+        logp_all = torch.randn(R, generator=g).to(dev) * 0.1 - 5
+        idx_all = torch.randperm(R, generator=g)[:B * world].to(dev)
+        head_all = torch.randn(B * world, A, generator=g).to(dev) * 0.3
+        v_all = torch.randn(B * world, generator=g).to(dev)
+        logstd = torch.full((A,), -1.0, device=dev)
+        obs_all = torch.randn(R, 3, generator=g).to(dev)
+        sl = slice(rank * B, (rank + 1) * B)
+        _, part = ops.gather_minibatch(idx_all[sl].contiguous(), obs_all, adv=adv_all)
+        dist.all_reduce(part, op=dist.ReduceOp.SUM)
+        part.div_(world)
+        _, dh, _, _ = ops.policy_loss("ppo", "gaussian", head_all[sl].contiguous(), logstd, v_all[sl].contiguous(),
+                                      act_all, adv_all, ret_all, old_logp=logp_all, idx=idx_all[sl].contiguous(),
+                                      adv_partials=part)
+        dh = dh.clone()
+        _, part_c = ops.gather_minibatch(idx_all, obs_all, adv=adv_all)
+        _, dh_c, _, _ = ops.policy_loss("ppo", "gaussian", head_all, logstd, v_all, act_all, adv_all, ret_all,
+                                        old_logp=logp_all, idx=idx_all, adv_partials=part_c)
+        torch.testing.assert_close(dh, dh_c[sl] * world, rtol=1e-5, atol=1e-7)
+        # ---- 2-rank PPO with both variants ----
+        from xuanpolicy_amd.distributed import broadcast_parameters
+        from xuanpolicy_amd.runner import build_synthbox_ppo
+        agent = build_synthbox_ppo(n_envs=64, n_steps=16, n_epoch=2, n_minibatch=2, device=dev, shard=rank,
+                                   sync_obs_rms=True, global_advnorm=True)
+        broadcast_parameters(agent.policy)
+        assert agent.sync_obs_rms and agent.global_advnorm and not agent.use_graph
+        agent.train(32)
+        for t in (agent.obs_mean, agent.obs_var, torch.cat([p.detach().reshape(-1) for p in agent.policy.parameters()])):
+            got = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(got, t.contiguous())
+            assert torch.equal(got[0], got[1])
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_dp_normalisation_variants_two_ranks_one_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=580) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: "ok", 1: "ok"}, res

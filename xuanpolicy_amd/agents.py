@@ -114,6 +114,18 @@ class _OnPolicyAgent:
         self._t = 0
         self._host_obs = None
         self.use_graph = bool(_cfg(config, "cuda_graph", True)) and self.device.type == "cuda"
+        # Data-parallel normalisation variants; default = per-shard statistics with one
+        # gradient all-reduce per minibatch.
+        #   sync_obs_rms:   SUM the per-step RMS partials across ranks (identical obs statistics everywhere)
+        #   global_advnorm: AVG each minibatch's advantage moments across ranks (global adv-norm)
+        self.world = 1
+        import torch.distributed as tdist
+        if tdist.is_available() and tdist.is_initialized():
+            self.world = tdist.get_world_size()
+        self.sync_obs_rms = bool(_cfg(config, "sync_obs_rms", False)) and self.world > 1 and self.use_obsnorm
+        self.global_advnorm = bool(_cfg(config, "global_advnorm", False)) and self.world > 1
+        if self.sync_obs_rms:
+            self.use_graph = False  # the per-step collective runs outside a captured graph
         self._graph = None
         self._graph_pool = None
 
@@ -183,6 +195,14 @@ class _OnPolicyAgent:
                          mask_returns=(self.algo == "ppo"), use_rewnorm=self.use_rewnorm,
                          rew_range=self.rewnorm_range, atari_lifeloss=self.atari)
 
+    def _rms_update(self, x):
+        if self.sync_obs_rms:
+            import torch.distributed as tdist
+            ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count, partials=self.rms_part,
+                           reduce_partials=lambda t: tdist.all_reduce(t, op=tdist.ReduceOp.SUM), world=self.world)
+        else:
+            ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count, partials=self.rms_part)
+
     def _rollout_step_device(self):
         env = self.envs
         x = env.obs
@@ -191,7 +211,7 @@ class _OnPolicyAgent:
             self._policy_in = x
         else:
             if self.use_obsnorm:
-                ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count, partials=self.rms_part)
+                self._rms_update(x)
             self._normalize_into(x, self.obs_norm, True)
         self._sample_into_buffer()
         env.step_device()
@@ -230,7 +250,7 @@ class _OnPolicyAgent:
             self._policy_in = x
         else:
             if self.use_obsnorm:
-                ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count, partials=self.rms_part)
+                self._rms_update(x)
             self._normalize_into(x, self.obs_norm, True)
         self._sample_into_buffer()
         t = self._t
@@ -277,6 +297,10 @@ class _OnPolicyAgent:
                 obs_mb, part = ops.gather_minibatch(idx, obs_flat, adv=adv_flat if use_advnorm else None,
                                                     obs_out=self.obs_mb,
                                                     adv_partials=self.adv_part if use_advnorm else None)
+                if self.global_advnorm and part is not None:
+                    import torch.distributed as tdist
+                    tdist.all_reduce(part, op=tdist.ReduceOp.SUM)   # (sum, sumsq) over all ranks' minibatches,
+                    part.div_(self.world)                           # averaged: mean / var of the global minibatch
                 scalars = self.learner.update_fused(obs_mb, idx, act_flat, adv_flat, ret_flat, logp_flat, part)
         self.last_info = scalars
         self.iterations += 1

@@ -411,9 +411,12 @@ def rms_num_partials(n):
     return int(lib().xpa_rms_num_partials(n))
 
 
-def rms_update(x, mean, var, count, partials=None):
+def rms_update(x, mean, var, count, partials=None, reduce_partials=None, world=1):
     """K5a+b: RunningMeanStd.update(x) on device.  x [n, dim] float32 (row stride may exceed dim);
-    mean/var float32 [dim], count float64 [1] — all updated in place."""
+    mean/var float32 [dim], count float64 [1] — all updated in place.
+    reduce_partials(partials): optional in-place SUM across ranks of the f64 partials (the
+    mpi_moments-style synchronised statistics, statistic_tools.py:20-32); the merge then counts
+    n * world rows.  All ranks must hold the same running mean (it is the partials' shift)."""
     n, dim = x.shape
     ld = _row_stride(x, "x", dim)
     _req(mean, "mean", torch.float32, (dim,))
@@ -426,6 +429,9 @@ def rms_update(x, mean, var, count, partials=None):
         _req(partials, "partials", torch.float64, (2 * np_, dim))
     s = _stream(x.device)
     _lib.check(lib().xpa_rms_partials(_p(x), n, dim, ld, _p(mean), _p(partials), s), "xpa_rms_partials")
+    if reduce_partials is not None:
+        reduce_partials(partials)
+        n = n * int(world)
     _lib.check(lib().xpa_rms_merge(_p(partials), np_, n, dim, _p(mean), _p(var), _p(count), s), "xpa_rms_merge")
 
 
