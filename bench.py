@@ -266,12 +266,26 @@ def cpu_baseline(args, cores):
     n_updates_full = args.n_epoch * ((N * T + (N * T // args.n_minibatch) - 1) // (N * T // args.n_minibatch))
     rollout = tm["act"] + tm["env"] + tm["store"]
     iteration = rollout + tm["gae"] + n_updates_full * per_update
-    return {"value": round(N * T / iteration, 1), "unit": "env-steps/s", "cores": cores, "kind": "port",
-            "sample": ("one %dx%d rollout (per-env SynthBoxEnv stepping as DummyVecEnv_Gym) + per-env finish_path "
-                       "GAE + %d of the %d minibatch updates (B=%d) timed in %.1f s; iteration time = rollout %.2f s "
-                       "+ GAE %.2f s + %d x %.3f s per update (sample + learner.update) = %.2f s"
-                       % (N, T, loop.n_updates, n_updates_full, N * T // args.n_minibatch, wall, rollout, tm["gae"],
-                          n_updates_full, per_update, iteration))}
+    res = {"value": round(N * T / iteration, 1), "unit": "env-steps/s", "cores": cores, "kind": "port",
+           "sample": ("one %dx%d rollout (per-env SynthBoxEnv stepping as DummyVecEnv_Gym) + per-env finish_path "
+                      "GAE + %d of the %d minibatch updates (B=%d) timed in %.1f s; iteration time = rollout %.2f s "
+                      "+ GAE %.2f s + %d x %.3f s per update (sample + learner.update) = %.2f s"
+                      % (N, T, loop.n_updates, n_updates_full, N * T // args.n_minibatch, wall, rollout, tm["gae"],
+                         n_updates_full, per_update, iteration))}
+    # the same loop with the env vectorised in numpy (synth_env.SynthBoxVec), so the
+    # speedup is not credited only to removing the per-env Python stepping; the updates cost the same.
+    venv = synth_env.SynthBoxVec(N, D, A, seed=1)
+    loop2 = cpu_ref.AgentLoopRef(None, pol, lrn, T, args.n_epoch, args.n_minibatch, 0.99, 0.95, vectorized_env=venv)
+    loop2.run_steps(T, max_updates=0)
+    tm2 = loop2.timers
+    rollout2 = tm2["act"] + tm2["env"] + tm2["store"]
+    iteration2 = rollout2 + tm2["gae"] + n_updates_full * per_update
+    res["vectorized_env_variant"] = {
+        "value": round(N * T / iteration2, 1), "unit": "env-steps/s", "cores": cores,
+        "sample": "rollout with the numpy-vectorised env %.2f s (act %.2f, env %.2f, store %.2f) + GAE %.2f s + the "
+                  "same %d x %.3f s updates = %.2f s" % (rollout2, tm2["act"], tm2["env"], tm2["store"], tm2["gae"],
+                                                          n_updates_full, per_update, iteration2)}
+    return res
 
 
 def main():
@@ -392,6 +406,8 @@ def main():
             cores = min(16, len(os.sched_getaffinity(0)))
             result["cpu_baseline"] = cpu_baseline(args, cores)
             result["speedup_vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
+            result["speedup_vs_cpu_vectorized_env"] = round(
+                value / result["cpu_baseline"]["vectorized_env_variant"]["value"], 1)
         line = json.dumps(result)
         print(line, flush=True)
         if args.out:
