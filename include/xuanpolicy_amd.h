@@ -298,6 +298,23 @@ int xpa_synthatari_step(int64_t n_envs, int64_t n_actions, const float *act_in, 
 int xpa_synthatari_reset(int64_t n_envs, uint32_t seed, uint8_t *stack, const int32_t *ep_index,
                          xpa_stream_t stream);
 
+/* K8 with deferred bootstrap values (valid when an env truncates at most once per rollout, i.e.
+ * max_episode_steps >= horizon): instead of v_boot, a mid-buffer truncation of env n (a path closed
+ * with a bootstrap, ppoclip_agent.py:95-100) stores its normalised final-observation row
+ * boot_obs[n] (row stride ld_boot, obs_dim floats) into slot_obs[n] and sets slot_t[n] = t (slot_t
+ * starts at -1; a second truncation in the same rollout counts in *overflow).  After the last step,
+ * values = V([slot_obs; boot_obs]) ([2 n_envs]: the truncation slots, then the last step's final
+ * observations, ppoclip_agent.py:69-75) and xpa_rollout_bootstrap_fixup writes buf_boot at every
+ * recorded truncation and at the last column (0 where terminal), resetting slot_t to -1. */
+int xpa_rollout_post_deferred(int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term,
+                              const uint8_t *trunc, const float *boot_obs, int64_t ld_boot, int64_t obs_dim,
+                              float *slot_obs, int32_t *slot_t, int32_t *overflow, xpa_cursor_t *cursor,
+                              float *ret_mean, float *ret_var, double *ret_count, float *returns, float *buf_rew,
+                              float *buf_term, uint8_t *buf_closed, float *buf_boot, float gamma, int mask_returns,
+                              int use_rewnorm, float rew_range, int atari_lifeloss, xpa_stream_t stream);
+int xpa_rollout_bootstrap_fixup(int64_t n_envs, int64_t horizon, const float *values, int32_t *slot_t,
+                                const float *buf_term, float *buf_boot, xpa_stream_t stream);
+
 /* K13 — first representation layer Linear(d_in, 256) + activation for a small d_in (<= 64): Basic_MLP's
  * first mlp_block (xuance/torch/representations/mlp.py:21-51, utils/layers.py:8-24) as HBM-streaming
  * kernels.  Forward: h = act(x W^T + b), x [rows, d_in] (row stride ldx), w [256, d_in], h [rows, 256]

@@ -126,6 +126,16 @@ class _OnPolicyAgent:
         self.global_advnorm = bool(_cfg(config, "global_advnorm", False)) and self.world > 1
         if self.sync_obs_rms:
             self.use_graph = False  # the per-step collective runs outside a captured graph
+        # Deferred truncation bootstraps: valid when an env truncates at most once per
+        # rollout; the critic then runs once per iteration on [truncation slots; last-step obs] instead of
+        # on every env at every step.
+        max_ep = getattr(envs, "max_episode_steps", getattr(envs, "max_episode_length", 0)) or 0
+        self.defer_boot = (bool(_cfg(config, "defer_bootstrap", True)) and not self.raw_obs
+                           and int(max_ep) >= self.n_steps)
+        if self.defer_boot:
+            self.slot_obs = torch.zeros((N, D), **f32)
+            self.slot_t = torch.full((N,), -1, dtype=torch.int32, device=dev)
+            self.slot_overflow = torch.zeros((1,), dtype=torch.int32, device=dev)
         self._graph = None
         self._graph_pool = None
 
@@ -180,6 +190,14 @@ class _OnPolicyAgent:
             self._post_kernel(rew, term, trunc, v_boot)
             return
         self._normalize_into(final_obs, self.boot_obs, False)
+        if self.defer_boot:
+            mem = self.memory
+            ops.rollout_post(rew, term, trunc, None, self.cursor, self.ret_mean, self.ret_var, self.ret_count,
+                             self.returns, mem.rewards, mem.terminals, mem.closed, mem.boot, self.gamma,
+                             mask_returns=(self.algo == "ppo"), use_rewnorm=self.use_rewnorm,
+                             rew_range=self.rewnorm_range, atari_lifeloss=self.atari,
+                             deferred=(self.boot_obs, self.slot_obs, self.slot_t, self.slot_overflow))
+            return
         fm = self._rollout_mlp()
         if fm is not None:
             v_boot = fm.rollout_value(self.boot_obs)
@@ -272,8 +290,25 @@ class _OnPolicyAgent:
         self._host_obs = obs
 
     # ---- buffer-full phase ------------------------------------------------------------------------------
+    def _deferred_bootstraps(self):
+        """V([truncation slots; last-step final obs]) in one critic pass, written into the buffer's
+        bootstrap column by xpa_rollout_bootstrap_fixup."""
+        x = torch.cat([self.slot_obs, self.boot_obs], dim=0)
+        fm = self._rollout_mlp()
+        if fm is not None:
+            v = fm.rollout_value(x)
+        else:
+            with torch.no_grad():
+                v = policy_heads(self.policy, x)[2].contiguous()
+        mem = self.memory
+        ops.bootstrap_fixup(v, self.slot_t, mem.terminals, mem.boot)
+        if int(self.slot_overflow.item()):
+            raise RuntimeError("an env truncated twice within one rollout; set config.defer_bootstrap = False")
+
     def _update_phase(self):
         mem = self.memory
+        if self.defer_boot:
+            self._deferred_bootstraps()
         mem.size = self.n_steps
         mem.compute_advantages()
         NT, B = self.buffer_size, self.batch_size

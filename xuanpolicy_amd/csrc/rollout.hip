@@ -385,13 +385,18 @@ __global__ __launch_bounds__(256) void synthbox_step_kernel(
 // ---------------------------------------------------------------------------------------------
 // K8 post-step bookkeeping (single block)
 // ---------------------------------------------------------------------------------------------
+// DEFER: no v_boot; a mid-buffer truncation of env n copies its normalised final observation row
+// (boot_obs) into slot_obs[n] and records slot_t[n] = t (a second one in the same rollout counts in
+// *overflow); bootstraps are written afterwards by xpa_rollout_bootstrap_fixup.
+template <bool DEFER>
 __global__ __launch_bounds__(1024) void rollout_post_kernel(
     int64_t n_envs, int64_t T, const float *__restrict__ rew, const uint8_t *__restrict__ term,
     const uint8_t *__restrict__ trunc, const float *__restrict__ v_boot, xpa_cursor_t *__restrict__ cur,
     float *__restrict__ ret_mean, float *__restrict__ ret_var, double *__restrict__ ret_count,
     float *__restrict__ returns, float *__restrict__ buf_rew, float *__restrict__ buf_term,
     uint8_t *__restrict__ buf_closed, float *__restrict__ buf_boot, float gamma, int mask_returns, int use_rewnorm,
-    float rew_range, int atari_lifeloss) {
+    float rew_range, int atari_lifeloss, const float *__restrict__ boot_obs, int64_t ld_boot, int64_t dim,
+    float *__restrict__ slot_obs, int *__restrict__ slot_t, int *__restrict__ overflow) {
     __shared__ double s_red[16];
     const int32_t t = cur->ptr;
     const float rstd = fminf(fmaxf(sqrtf(*ret_var), 0.1f), 100.0f);
@@ -407,7 +412,7 @@ __global__ __launch_bounds__(1024) void rollout_post_kernel(
             const int64_t n = base + k * stride;
             const bool ok = n < n_envs;
             r[k] = ok ? rew[n] : 0.f;
-            vb[k] = ok ? v_boot[n] : 0.f;
+            vb[k] = (ok && !DEFER) ? v_boot[n] : 0.f;
             R[k] = ok ? returns[n] : 0.f;
             te8[k] = ok ? term[n] : 0;
             tr8[k] = ok ? trunc[n] : 0;
@@ -424,6 +429,11 @@ __global__ __launch_bounds__(1024) void rollout_post_kernel(
             const bool close = last || (done && !(atari_lifeloss && !tr));
             buf_closed[cell] = close ? 1 : 0;
             buf_boot[cell] = close ? (te ? 0.f : vb[k]) : 0.f;
+            if (DEFER && close && !te && !last) {  // mid-buffer truncation: keep the row for later
+                if (slot_t[n] >= 0) atomicAdd(overflow, 1);
+                slot_t[n] = (int)t;
+                for (int64_t d = 0; d < dim; ++d) slot_obs[n * dim + d] = boot_obs[n * ld_boot + d];
+            }
             float Rk = mask_returns ? (te ? 0.f : gamma * R[k]) + r[k] : gamma * R[k] + r[k];
             if (done) {
                 cnt += 1.0;
@@ -571,9 +581,54 @@ XPA_API int xpa_rollout_post(int64_t n_envs, int64_t horizon, const float *rew, 
     if (n_envs <= 0 || horizon <= 0 || !rew || !term || !trunc || !v_boot || !cursor || !ret_mean || !ret_var ||
         !ret_count || !returns || !buf_rew || !buf_term || !buf_closed || !buf_boot)
         return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(rollout_post_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, n_envs, horizon, rew, term,
-                       trunc, v_boot, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term, buf_closed,
-                       buf_boot, gamma, mask_returns, use_rewnorm, rew_range, atari_lifeloss);
+    hipLaunchKernelGGL(rollout_post_kernel<false>, dim3(1), dim3(1024), 0, (hipStream_t)stream, n_envs, horizon, rew,
+                       term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term,
+                       buf_closed, buf_boot, gamma, mask_returns, use_rewnorm, rew_range, atari_lifeloss,
+                       (const float *)nullptr, (int64_t)0, (int64_t)0, (float *)nullptr, (int *)nullptr,
+                       (int *)nullptr);
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_rollout_post_deferred(int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term,
+                                      const uint8_t *trunc, const float *boot_obs, int64_t ld_boot, int64_t obs_dim,
+                                      float *slot_obs, int32_t *slot_t, int32_t *overflow, xpa_cursor_t *cursor,
+                                      float *ret_mean, float *ret_var, double *ret_count, float *returns,
+                                      float *buf_rew, float *buf_term, uint8_t *buf_closed, float *buf_boot,
+                                      float gamma, int mask_returns, int use_rewnorm, float rew_range,
+                                      int atari_lifeloss, xpa_stream_t stream) {
+    if (n_envs <= 0 || horizon <= 0 || obs_dim <= 0 || ld_boot < obs_dim || !rew || !term || !trunc || !boot_obs ||
+        !slot_obs || !slot_t || !overflow || !cursor || !ret_mean || !ret_var || !ret_count || !returns || !buf_rew ||
+        !buf_term || !buf_closed || !buf_boot)
+        return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(rollout_post_kernel<true>, dim3(1), dim3(1024), 0, (hipStream_t)stream, n_envs, horizon, rew,
+                       term, trunc, (const float *)nullptr, cursor, ret_mean, ret_var, ret_count, returns, buf_rew,
+                       buf_term, buf_closed, buf_boot, gamma, mask_returns, use_rewnorm, rew_range, atari_lifeloss,
+                       boot_obs, ld_boot, obs_dim, slot_obs, slot_t, overflow);
+    return xpa_launch_status();
+}
+
+namespace {
+__global__ __launch_bounds__(256) void bootstrap_fixup_kernel(int64_t n_envs, int64_t T, const float *__restrict__ v,
+                                                              int *__restrict__ slot_t,
+                                                              const float *__restrict__ buf_term,
+                                                              float *__restrict__ buf_boot) {
+    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (n >= n_envs) return;
+    const int t = slot_t[n];
+    if (t >= 0) {
+        buf_boot[n * T + t] = v[n];
+        slot_t[n] = -1;
+    }
+    const int64_t last = n * T + T - 1;
+    buf_boot[last] = buf_term[last] != 0.f ? 0.f : v[n_envs + n];
+}
+}  // namespace
+
+XPA_API int xpa_rollout_bootstrap_fixup(int64_t n_envs, int64_t horizon, const float *values, int32_t *slot_t,
+                                        const float *buf_term, float *buf_boot, xpa_stream_t stream) {
+    if (n_envs <= 0 || horizon <= 0 || !values || !slot_t || !buf_term || !buf_boot) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(bootstrap_fixup_kernel, dim3((unsigned)((n_envs + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, n_envs, horizon, values, slot_t, buf_term, buf_boot);
     return xpa_launch_status();
 }
 

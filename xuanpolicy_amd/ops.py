@@ -539,14 +539,18 @@ def value_head(z_critic, act, w_critic, b_critic, out=None):
 
 
 def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term,
-                 buf_closed, buf_boot, gamma, mask_returns=True, use_rewnorm=True, rew_range=5.0, atari_lifeloss=False):
+                 buf_closed, buf_boot, gamma, mask_returns=True, use_rewnorm=True, rew_range=5.0, atari_lifeloss=False,
+                 deferred=None):
     """K8: reward normalisation, return tracker + ret_rms, rewards/terminals/closures into the buffer
-    column cursor.ptr, then cursor.ptr = (ptr + 1) % horizon, cursor.step += 1."""
+    column cursor.ptr, then cursor.ptr = (ptr + 1) % horizon, cursor.step += 1.
+    deferred = (boot_obs [N, D] (row stride may exceed D), slot_obs [N, D], slot_t int32 [N], overflow
+    int32 [1]): no v_boot; truncation rows are kept for bootstrap_fixup after the rollout."""
     N = rew.shape[0]
     _req(rew, "rew", torch.float32, (N,))
     _req(term, "term", torch.uint8, (N,))
     _req(trunc, "trunc", torch.uint8, (N,))
-    _req(v_boot, "v_boot", torch.float32, (N,))
+    if deferred is None:
+        _req(v_boot, "v_boot", torch.float32, (N,))
     _req(cursor, "cursor", torch.int32, (4,))
     for name, t in (("ret_mean", ret_mean), ("ret_var", ret_var)):
         _req(t, name, torch.float32, (1,))
@@ -556,8 +560,34 @@ def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count,
     for name, t in (("buf_rew", buf_rew), ("buf_term", buf_term), ("buf_boot", buf_boot)):
         _req(t, name, torch.float32, (N, T))
     _req(buf_closed, "buf_closed", torch.uint8, (N, T))
+    if deferred is not None:
+        boot_obs, slot_obs, slot_t, overflow = deferred
+        D = slot_obs.shape[1]
+        ld = _row_stride(boot_obs, "boot_obs", D)
+        _req(slot_obs, "slot_obs", torch.float32, (N, D))
+        _req(slot_t, "slot_t", torch.int32, (N,))
+        _req(overflow, "overflow", torch.int32, (1,))
+        rc = lib().xpa_rollout_post_deferred(N, T, _p(rew), _p(term), _p(trunc), _p(boot_obs), ld, D, _p(slot_obs),
+                                             _p(slot_t), _p(overflow), _p(cursor), _p(ret_mean), _p(ret_var),
+                                             _p(ret_count), _p(returns), _p(buf_rew), _p(buf_term), _p(buf_closed),
+                                             _p(buf_boot), float(gamma), int(bool(mask_returns)),
+                                             int(bool(use_rewnorm)), float(rew_range), int(bool(atari_lifeloss)),
+                                             _stream(rew.device))
+        _lib.check(rc, "xpa_rollout_post_deferred")
+        return
     rc = lib().xpa_rollout_post(N, T, _p(rew), _p(term), _p(trunc), _p(v_boot), _p(cursor), _p(ret_mean), _p(ret_var),
                                 _p(ret_count), _p(returns), _p(buf_rew), _p(buf_term), _p(buf_closed), _p(buf_boot),
                                 float(gamma), int(bool(mask_returns)), int(bool(use_rewnorm)), float(rew_range),
                                 int(bool(atari_lifeloss)), _stream(rew.device))
     _lib.check(rc, "xpa_rollout_post")
+
+
+def bootstrap_fixup(values, slot_t, buf_term, buf_boot):
+    """After a deferred rollout: values [2N] = V(slot rows) then V(last-step final obs)."""
+    N, T = buf_boot.shape
+    _req(values, "values", torch.float32, (2 * N,))
+    _req(slot_t, "slot_t", torch.int32, (N,))
+    _req(buf_term, "buf_term", torch.float32, (N, T))
+    _req(buf_boot, "buf_boot", torch.float32, (N, T))
+    _lib.check(lib().xpa_rollout_bootstrap_fixup(N, T, _p(values), _p(slot_t), _p(buf_term), _p(buf_boot),
+                                                 _stream(values.device)), "xpa_rollout_bootstrap_fixup")
