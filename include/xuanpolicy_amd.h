@@ -153,17 +153,21 @@ int xpa_synthbox_step(int64_t n_envs, int64_t obs_dim, const float *pre, uint32_
                       uint8_t *trunc, int32_t *ep_step, uint32_t *ep_index, float *ep_score,
                       float *ep_last_score, int32_t *ep_last_len, xpa_stream_t stream);
 
-/* K8 — rollout post-step bookkeeping (one block).  Replaces, per step, DummyOnPolicyBuffer.store of
+/* K8 — rollout post-step bookkeeping.  Replaces, per step, DummyOnPolicyBuffer.store of
  * rewards/terminals (memory_tools.py:196-204) with reward normalisation (agent.py:118-123), the
  * return tracker and ret_rms update (ppoclip_agent.py:87-92 with the (1-term) mask; a2c_agent.py:84
  * without), and the agent's path closing (ppoclip_agent.py:69-75, 89-101): closed/boot columns for
  * xpa_gae_scan (atari_lifeloss = 1: a terminal without truncation does not close the path,
- * ppoclip_agent.py:93-94).  Advances cursor->ptr (mod horizon) and cursor->step. */
+ * ppoclip_agent.py:93-94).  Advances cursor->ptr (mod horizon) and cursor->step.
+ * Workspace: partials = 3 * xpa_rollout_post_num_blocks(n_envs) doubles, ticket = one uint32 that is
+ * 0 before the first call (the kernel leaves it at 0). */
+int64_t xpa_rollout_post_num_blocks(int64_t n_envs);
 int xpa_rollout_post(int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term,
                      const uint8_t *trunc, const float *v_boot, xpa_cursor_t *cursor, float *ret_mean,
                      float *ret_var, double *ret_count, float *returns, float *buf_rew, float *buf_term,
-                     uint8_t *buf_closed, float *buf_boot, float gamma, int mask_returns,
-                     int use_rewnorm, float rew_range, int atari_lifeloss, xpa_stream_t stream);
+                     uint8_t *buf_closed, float *buf_boot, float gamma, int mask_returns, int use_rewnorm,
+                     float rew_range, int atari_lifeloss, double *partials, uint32_t *ticket,
+                     xpa_stream_t stream);
 
 /* K9 — fused global-norm gradient clipping + Adam over flat fp32 buffers (all 16-B aligned).
  * Replaces torch.nn.utils.clip_grad_norm_ + torch.optim.Adam.step in PPOCLIP_Learner.update /
@@ -311,7 +315,8 @@ int xpa_rollout_post_deferred(int64_t n_envs, int64_t horizon, const float *rew,
                               float *slot_obs, int32_t *slot_t, int32_t *overflow, xpa_cursor_t *cursor,
                               float *ret_mean, float *ret_var, double *ret_count, float *returns, float *buf_rew,
                               float *buf_term, uint8_t *buf_closed, float *buf_boot, float gamma, int mask_returns,
-                              int use_rewnorm, float rew_range, int atari_lifeloss, xpa_stream_t stream);
+                              int use_rewnorm, float rew_range, int atari_lifeloss, double *partials,
+                              uint32_t *ticket, xpa_stream_t stream);
 int xpa_rollout_bootstrap_fixup(int64_t n_envs, int64_t horizon, const float *values, int32_t *slot_t,
                                 const float *buf_term, float *buf_boot, xpa_stream_t stream);
 

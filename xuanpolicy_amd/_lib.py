@@ -45,8 +45,9 @@ SIGNATURES = {
                                           c_p, c_p, c_i64, c_p]),
     "xpa_synthbox_step": (ctypes.c_int, [c_i64, c_i64, c_p, c_u32, c_i32, c_f32, c_f32, c_f32, c_p, c_i64, c_p, c_p,
                                          c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "xpa_rollout_post_num_blocks": (c_i64, [c_i64]),
     "xpa_rollout_post": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
-                                        c_f32, ctypes.c_int, ctypes.c_int, c_f32, ctypes.c_int, c_p]),
+                                        c_f32, ctypes.c_int, ctypes.c_int, c_f32, ctypes.c_int, c_p, c_p, c_p]),
     "xpa_act_bwd_num_partials": (c_i64, [c_i64]),
     "xpa_act_bwd_colsum": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_i64, c_i64, c_f32, c_p, c_p, c_p]),
     "xpa_colsum_finalize": (ctypes.c_int, [c_p, c_i64, c_i64, c_p, c_p]),
@@ -76,7 +77,7 @@ SIGNATURES = {
     "xpa_synthatari_reset": (ctypes.c_int, [c_i64, c_u32, c_p, c_p, c_p]),
     "xpa_rollout_post_deferred": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p,
                                                  c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, ctypes.c_int, ctypes.c_int,
-                                                 c_f32, ctypes.c_int, c_p]),
+                                                 c_f32, ctypes.c_int, c_p, c_p, c_p]),
     "xpa_rollout_bootstrap_fixup": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_p]),
     "xpa_thin_bwd_num_partials": (c_i64, [c_i64]),
     "xpa_thin_linear_act_fwd": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f32, c_p, c_i64,

@@ -89,6 +89,7 @@ class _OnPolicyAgent:
         self.ret_count = torch.full((1,), 1e-4, dtype=torch.float64, device=dev)
         self.returns = torch.zeros((N,), **f32)
         self.cursor = ops.new_cursor(dev)
+        self.post_ws = ops.post_workspace(N, dev)
         # Raw observations (uint8 Atari frames without obs normalisation, DummyOnPolicyBuffer_Atari): stored
         # and fed to the policy as they are (AC_CNN_Atari scales by 1/255 on device).
         self.raw_obs = self.memory.observations.dtype == torch.uint8 and not self.use_obsnorm
@@ -196,7 +197,8 @@ class _OnPolicyAgent:
                              self.returns, mem.rewards, mem.terminals, mem.closed, mem.boot, self.gamma,
                              mask_returns=(self.algo == "ppo"), use_rewnorm=self.use_rewnorm,
                              rew_range=self.rewnorm_range, atari_lifeloss=self.atari,
-                             deferred=(self.boot_obs, self.slot_obs, self.slot_t, self.slot_overflow))
+                             deferred=(self.boot_obs, self.slot_obs, self.slot_t, self.slot_overflow),
+                             workspace=self.post_ws)
             return
         fm = self._rollout_mlp()
         if fm is not None:
@@ -211,7 +213,7 @@ class _OnPolicyAgent:
         ops.rollout_post(rew, term, trunc, v_boot.contiguous(), self.cursor, self.ret_mean, self.ret_var,
                          self.ret_count, self.returns, mem.rewards, mem.terminals, mem.closed, mem.boot, self.gamma,
                          mask_returns=(self.algo == "ppo"), use_rewnorm=self.use_rewnorm,
-                         rew_range=self.rewnorm_range, atari_lifeloss=self.atari)
+                         rew_range=self.rewnorm_range, atari_lifeloss=self.atari, workspace=self.post_ws)
 
     def _rms_update(self, x):
         if self.sync_obs_rms:

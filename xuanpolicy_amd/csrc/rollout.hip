@@ -308,16 +308,40 @@ __global__ __launch_bounds__(256) void rollout_policy_head_kernel(
         return;
     }
     const float4 h = act4<ACT>(*reinterpret_cast<const float4 *>(za + n * ld + 4 * lane), slope);
+    float mine = 0.f;  // lane o keeps head[o]
     for (int o = 0; o < K; ++o) {
         const float p = wave_allsum_f(dot4(h, *reinterpret_cast<const float4 *>(Wa + o * 256 + 4 * lane))) + ba[o];
-        if (lane == 0) s_head[wave][o] = p;
+        if (lane == o) mine = p;
+        if (MODE == 1 && lane == 0) s_head[wave][o] = p;
     }
+    if (MODE == 1) {
+        if (lane == 0) cat_sample_store(n, K, T, s_head[wave], v, cur, seed, buf_act, buf_logp, buf_val, env_in, ld_env);
+        return;
+    }
+    // Gaussian: lane a draws dimension a (the K3 arithmetic); lane 0 adds the log-prob terms in
+    // dimension order, so the sum is bitwise K3's sequential one.
+    const int64_t cell = n * T + cur->ptr;
+    float term_a = 0.f;
+    if (lane < K) {
+        const int a = lane;
+        const uint32_t step = cur->step;
+        const uint32_t h1 = xpa_hash4(seed ^ kSaltAct, step, (uint32_t)n, (uint32_t)(2 * a));
+        const uint32_t h2 = xpa_hash4(seed ^ kSaltAct, step, (uint32_t)n, (uint32_t)(2 * a + 1));
+        const float u1 = 1.0f - xpa_u01(h1);
+        const float u2 = xpa_u01(h2);
+        const float eps = sqrtf(-2.0f * logf(u1)) * cosf(6.28318530717958647692f * u2);
+        const float sc = expf(logstd[a]);
+        const float x = mine + sc * eps;
+        const float diff = x - mine;
+        term_a = -(diff * diff) / (2.0f * sc * sc) - logf(sc) - 0.91893853320467274178f;
+        buf_act[cell * K + a] = x;
+        env_in[n * ld_env + a] = fminf(fmaxf(x, -act_clip), act_clip);
+    }
+    float logp = 0.f;
+    for (int a = 0; a < K; ++a) logp += __shfl(term_a, a, 64);
     if (lane == 0) {
-        if (MODE == 0)
-            gauss_sample_store(n, K, T, s_head[wave], logstd, v, cur, seed, act_clip, buf_act, buf_logp, buf_val,
-                               env_in, ld_env);
-        else
-            cat_sample_store(n, K, T, s_head[wave], v, cur, seed, buf_act, buf_logp, buf_val, env_in, ld_env);
+        buf_logp[cell] = logp;
+        buf_val[cell] = v;
     }
 }
 
@@ -385,83 +409,90 @@ __global__ __launch_bounds__(256) void synthbox_step_kernel(
 // ---------------------------------------------------------------------------------------------
 // K8 post-step bookkeeping (single block)
 // ---------------------------------------------------------------------------------------------
+// One env per thread over ceil(n_envs / 256) blocks (the scattered column writes spread over the chip);
+// each block writes its finished-return moments (count, sum, sum of squares; f64) to `partials`, and
+// the last block to arrive (atomic ticket) merges them in block order into ret_rms, advances the
+// cursor and resets the ticket to 0 (graph replays see a fresh ticket).
 // DEFER: no v_boot; a mid-buffer truncation of env n copies its normalised final observation row
 // (boot_obs) into slot_obs[n] and records slot_t[n] = t (a second one in the same rollout counts in
 // *overflow); bootstraps are written afterwards by xpa_rollout_bootstrap_fixup.
+constexpr int kPostThreads = 256;
 template <bool DEFER>
-__global__ __launch_bounds__(1024) void rollout_post_kernel(
+__global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
     int64_t n_envs, int64_t T, const float *__restrict__ rew, const uint8_t *__restrict__ term,
     const uint8_t *__restrict__ trunc, const float *__restrict__ v_boot, xpa_cursor_t *__restrict__ cur,
     float *__restrict__ ret_mean, float *__restrict__ ret_var, double *__restrict__ ret_count,
     float *__restrict__ returns, float *__restrict__ buf_rew, float *__restrict__ buf_term,
     uint8_t *__restrict__ buf_closed, float *__restrict__ buf_boot, float gamma, int mask_returns, int use_rewnorm,
     float rew_range, int atari_lifeloss, const float *__restrict__ boot_obs, int64_t ld_boot, int64_t dim,
-    float *__restrict__ slot_obs, int *__restrict__ slot_t, int *__restrict__ overflow) {
-    __shared__ double s_red[16];
+    float *__restrict__ slot_obs, int *__restrict__ slot_t, int *__restrict__ overflow, double *__restrict__ partials,
+    unsigned int *__restrict__ ticket) {
+    __shared__ double s_red[kPostThreads / 64];
+    __shared__ bool s_last;
     const int32_t t = cur->ptr;
     const float rstd = fminf(fmaxf(sqrtf(*ret_var), 0.1f), 100.0f);
     const bool last = (t == (int32_t)(T - 1));
     double cnt = 0.0, sum = 0.0, sumsq = 0.0;
-    constexpr int U = 4;  // envs per thread per pass, all loads issued before use
-    const int64_t stride = (int64_t)blockDim.x;
-    for (int64_t base = threadIdx.x; base < n_envs; base += stride * U) {
-        float r[U], vb[U], R[U];
-        uint8_t te8[U], tr8[U];
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            const int64_t n = base + k * stride;
-            const bool ok = n < n_envs;
-            r[k] = ok ? rew[n] : 0.f;
-            vb[k] = (ok && !DEFER) ? v_boot[n] : 0.f;
-            R[k] = ok ? returns[n] : 0.f;
-            te8[k] = ok ? term[n] : 0;
-            tr8[k] = ok ? trunc[n] : 0;
+    const int64_t n = (int64_t)blockIdx.x * kPostThreads + threadIdx.x;
+    if (n < n_envs) {
+        const float r = rew[n];
+        const float vb = DEFER ? 0.f : v_boot[n];
+        const float R = returns[n];
+        const bool te = term[n] != 0, tr = trunc[n] != 0;
+        const int64_t cell = n * T + t;
+        buf_rew[cell] = use_rewnorm ? fminf(fmaxf(r / rstd, -rew_range), rew_range) : r;
+        buf_term[cell] = te ? 1.f : 0.f;
+        const bool done = te || tr;
+        const bool close = last || (done && !(atari_lifeloss && !tr));
+        buf_closed[cell] = close ? 1 : 0;
+        buf_boot[cell] = close ? (te ? 0.f : vb) : 0.f;
+        if (DEFER && close && !te && !last) {  // mid-buffer truncation: keep the row for later
+            if (slot_t[n] >= 0) atomicAdd(overflow, 1);
+            slot_t[n] = (int)t;
+            for (int64_t d = 0; d < dim; ++d) slot_obs[n * dim + d] = boot_obs[n * ld_boot + d];
         }
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            const int64_t n = base + k * stride;
-            if (n >= n_envs) continue;
-            const bool te = te8[k] != 0, tr = tr8[k] != 0;
-            const int64_t cell = n * T + t;
-            buf_rew[cell] = use_rewnorm ? fminf(fmaxf(r[k] / rstd, -rew_range), rew_range) : r[k];
-            buf_term[cell] = te ? 1.f : 0.f;
-            const bool done = te || tr;
-            const bool close = last || (done && !(atari_lifeloss && !tr));
-            buf_closed[cell] = close ? 1 : 0;
-            buf_boot[cell] = close ? (te ? 0.f : vb[k]) : 0.f;
-            if (DEFER && close && !te && !last) {  // mid-buffer truncation: keep the row for later
-                if (slot_t[n] >= 0) atomicAdd(overflow, 1);
-                slot_t[n] = (int)t;
-                for (int64_t d = 0; d < dim; ++d) slot_obs[n * dim + d] = boot_obs[n * ld_boot + d];
-            }
-            float Rk = mask_returns ? (te ? 0.f : gamma * R[k]) + r[k] : gamma * R[k] + r[k];
-            if (done) {
-                cnt += 1.0;
-                sum += (double)Rk;
-                sumsq += (double)Rk * (double)Rk;
-                Rk = 0.f;
-            }
-            returns[n] = Rk;
+        float Rk = mask_returns ? (te ? 0.f : gamma * R) + r : gamma * R + r;
+        if (done) {
+            cnt = 1.0;
+            sum = (double)Rk;
+            sumsq = (double)Rk * (double)Rk;
+            Rk = 0.f;
         }
+        returns[n] = Rk;
     }
-    const int nw = blockDim.x >> 6;
+    constexpr int nw = kPostThreads / 64;
     cnt = xpa_block_sum(cnt, s_red, nw);
     sum = xpa_block_sum(sum, s_red, nw);
     sumsq = xpa_block_sum(sumsq, s_red, nw);
     if (threadIdx.x == 0) {
-        if (cnt > 0.0) {
-            const double bm = sum / cnt;
-            const double bvar = fmax(sumsq / cnt - bm * bm, 0.0);
-            const double c0 = *ret_count, m0 = (double)*ret_mean, v0 = (double)*ret_var;
-            const double tot = c0 + cnt;
-            const double delta = bm - m0;
-            *ret_mean = (float)(m0 + delta * cnt / tot);
-            *ret_var = (float)((v0 * c0 + bvar * cnt + delta * delta * c0 * cnt / tot) / tot);
-            *ret_count = tot;
-        }
-        cur->ptr = (int32_t)((t + 1) % T);
-        cur->step = cur->step + 1u;
+        partials[3 * blockIdx.x] = cnt;
+        partials[3 * blockIdx.x + 1] = sum;
+        partials[3 * blockIdx.x + 2] = sumsq;
+        __threadfence();
+        s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
     }
+    __syncthreads();
+    if (!s_last || threadIdx.x != 0) return;
+    __threadfence();
+    double c = 0.0, s1 = 0.0, s2 = 0.0;
+    for (unsigned g = 0; g < gridDim.x; ++g) {  // fixed order -> deterministic
+        c += ((volatile double *)partials)[3 * g];
+        s1 += ((volatile double *)partials)[3 * g + 1];
+        s2 += ((volatile double *)partials)[3 * g + 2];
+    }
+    if (c > 0.0) {
+        const double bm = s1 / c;
+        const double bvar = fmax(s2 / c - bm * bm, 0.0);
+        const double c0 = *ret_count, m0 = (double)*ret_mean, v0 = (double)*ret_var;
+        const double tot = c0 + c;
+        const double delta = bm - m0;
+        *ret_mean = (float)(m0 + delta * c / tot);
+        *ret_var = (float)((v0 * c0 + bvar * c + delta * delta * c0 * c / tot) / tot);
+        *ret_count = tot;
+    }
+    cur->ptr = (int32_t)((t + 1) % T);
+    cur->step = cur->step + 1u;
+    *ticket = 0u;
 }
 
 }  // namespace
@@ -573,19 +604,25 @@ XPA_API int xpa_synthbox_step(int64_t n_envs, int64_t obs_dim, const float *pre,
 }
 
 // ---- K8 --------------------------------------------------------------------------------------------
+XPA_API int64_t xpa_rollout_post_num_blocks(int64_t n_envs) {
+    return (n_envs + kPostThreads - 1) / kPostThreads;
+}
+
 XPA_API int xpa_rollout_post(int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term,
                              const uint8_t *trunc, const float *v_boot, xpa_cursor_t *cursor, float *ret_mean,
                              float *ret_var, double *ret_count, float *returns, float *buf_rew, float *buf_term,
                              uint8_t *buf_closed, float *buf_boot, float gamma, int mask_returns, int use_rewnorm,
-                             float rew_range, int atari_lifeloss, xpa_stream_t stream) {
+                             float rew_range, int atari_lifeloss, double *partials, uint32_t *ticket,
+                             xpa_stream_t stream) {
     if (n_envs <= 0 || horizon <= 0 || !rew || !term || !trunc || !v_boot || !cursor || !ret_mean || !ret_var ||
-        !ret_count || !returns || !buf_rew || !buf_term || !buf_closed || !buf_boot)
+        !ret_count || !returns || !buf_rew || !buf_term || !buf_closed || !buf_boot || !partials || !ticket ||
+        xpa_rollout_post_num_blocks(n_envs) > 0x7fffffff)
         return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(rollout_post_kernel<false>, dim3(1), dim3(1024), 0, (hipStream_t)stream, n_envs, horizon, rew,
-                       term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term,
-                       buf_closed, buf_boot, gamma, mask_returns, use_rewnorm, rew_range, atari_lifeloss,
-                       (const float *)nullptr, (int64_t)0, (int64_t)0, (float *)nullptr, (int *)nullptr,
-                       (int *)nullptr);
+    hipLaunchKernelGGL(rollout_post_kernel<false>, dim3((unsigned)xpa_rollout_post_num_blocks(n_envs)),
+                       dim3(kPostThreads), 0, (hipStream_t)stream, n_envs, horizon, rew, term, trunc, v_boot, cursor,
+                       ret_mean, ret_var, ret_count, returns, buf_rew, buf_term, buf_closed, buf_boot, gamma,
+                       mask_returns, use_rewnorm, rew_range, atari_lifeloss, (const float *)nullptr, (int64_t)0,
+                       (int64_t)0, (float *)nullptr, (int *)nullptr, (int *)nullptr, partials, (unsigned *)ticket);
     return xpa_launch_status();
 }
 
@@ -595,15 +632,16 @@ XPA_API int xpa_rollout_post_deferred(int64_t n_envs, int64_t horizon, const flo
                                       float *ret_mean, float *ret_var, double *ret_count, float *returns,
                                       float *buf_rew, float *buf_term, uint8_t *buf_closed, float *buf_boot,
                                       float gamma, int mask_returns, int use_rewnorm, float rew_range,
-                                      int atari_lifeloss, xpa_stream_t stream) {
+                                      int atari_lifeloss, double *partials, uint32_t *ticket, xpa_stream_t stream) {
     if (n_envs <= 0 || horizon <= 0 || obs_dim <= 0 || ld_boot < obs_dim || !rew || !term || !trunc || !boot_obs ||
         !slot_obs || !slot_t || !overflow || !cursor || !ret_mean || !ret_var || !ret_count || !returns || !buf_rew ||
-        !buf_term || !buf_closed || !buf_boot)
+        !buf_term || !buf_closed || !buf_boot || !partials || !ticket || xpa_rollout_post_num_blocks(n_envs) > 0x7fffffff)
         return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(rollout_post_kernel<true>, dim3(1), dim3(1024), 0, (hipStream_t)stream, n_envs, horizon, rew,
-                       term, trunc, (const float *)nullptr, cursor, ret_mean, ret_var, ret_count, returns, buf_rew,
-                       buf_term, buf_closed, buf_boot, gamma, mask_returns, use_rewnorm, rew_range, atari_lifeloss,
-                       boot_obs, ld_boot, obs_dim, slot_obs, slot_t, overflow);
+    hipLaunchKernelGGL(rollout_post_kernel<true>, dim3((unsigned)xpa_rollout_post_num_blocks(n_envs)),
+                       dim3(kPostThreads), 0, (hipStream_t)stream, n_envs, horizon, rew, term, trunc,
+                       (const float *)nullptr, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term,
+                       buf_closed, buf_boot, gamma, mask_returns, use_rewnorm, rew_range, atari_lifeloss, boot_obs,
+                       ld_boot, obs_dim, slot_obs, slot_t, overflow, partials, (unsigned *)ticket);
     return xpa_launch_status();
 }
 

@@ -37,28 +37,28 @@ __device__ __forceinline__ float act_g(float h, float slope) {
     return 1.f;
 }
 
-template <int ACT, int DMAX>
+template <int ACT, int DMAX, int TILE>
 __global__ __launch_bounds__(256) void thin_fwd_kernel(const float *__restrict__ x, int64_t ldx, int64_t rows, int din,
                                                        const float *__restrict__ W, const float *__restrict__ bias,
                                                        float slope, float *__restrict__ h, int64_t ldh) {
     constexpr int kPad = DMAX + 4;  // row stride of the staged x tile (16-B aligned rows)
-    __shared__ __attribute__((aligned(16))) float s_x[kTile * kPad];
+    __shared__ __attribute__((aligned(16))) float s_x[TILE * kPad];
     const int t = threadIdx.x;
     float w[DMAX];
 #pragma unroll
     for (int k = 0; k < DMAX; ++k) w[k] = k < din ? W[t * din + k] : 0.f;
     const float bc = bias[t];
-    const int64_t ntiles = (rows + kTile - 1) / kTile;
+    const int64_t ntiles = (rows + TILE - 1) / TILE;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t r0 = tile * kTile;
+        const int64_t r0 = tile * TILE;
         __syncthreads();
         // zero-padded columns din..DMAX-1 stay 0 from this loop's (r, k < DMAX) writes
-        for (int i = t; i < kTile * DMAX; i += 256) {
+        for (int i = t; i < TILE * DMAX; i += 256) {
             const int r = i / DMAX, k = i - r * DMAX;
             s_x[r * kPad + k] = (k < din && r0 + r < rows) ? x[(r0 + r) * ldx + k] : 0.f;
         }
         __syncthreads();
-        const int nr = (int)min((int64_t)kTile, rows - r0);
+        const int nr = (int)min((int64_t)TILE, rows - r0);
         for (int r = 0; r < nr; ++r) {
             const float *xr = s_x + r * kPad;
             float acc = 0.f;
@@ -165,13 +165,30 @@ __global__ __launch_bounds__(1024) void thin_bwd_kernel(const float *__restrict_
     partial_db[(int64_t)blockIdx.x * kCols + t] = accb;
 }
 
+template <int ACT, int TILE>
+void launch_fwd_t(int dmax, dim3 grid, hipStream_t s, const float *x, int64_t ldx, int64_t rows, int din,
+                  const float *W, const float *b, float slope, float *h, int64_t ldh) {
+#define XPA_FWD(D_) \
+    hipLaunchKernelGGL((thin_fwd_kernel<ACT, D_, TILE>), grid, dim3(256), 0, s, x, ldx, rows, din, W, b, slope, h, ldh)
+    if (dmax == 8) XPA_FWD(8);
+    else if (dmax == 20) XPA_FWD(20);
+    else if (dmax == 32) XPA_FWD(32);
+    else XPA_FWD(64);
+#undef XPA_FWD
+}
+
+// 64-row tiles for update-sized batches; 8-row tiles when fewer than 1024 x 64 rows (e.g. the rollout's
+// 4096 envs) so the grid still covers the chip.
 template <int ACT>
-void launch_fwd(int dmax, dim3 grid, hipStream_t s, const float *x, int64_t ldx, int64_t rows, int din,
-                const float *W, const float *b, float slope, float *h, int64_t ldh) {
-    if (dmax == 8) hipLaunchKernelGGL((thin_fwd_kernel<ACT, 8>), grid, dim3(256), 0, s, x, ldx, rows, din, W, b, slope, h, ldh);
-    else if (dmax == 20) hipLaunchKernelGGL((thin_fwd_kernel<ACT, 20>), grid, dim3(256), 0, s, x, ldx, rows, din, W, b, slope, h, ldh);
-    else if (dmax == 32) hipLaunchKernelGGL((thin_fwd_kernel<ACT, 32>), grid, dim3(256), 0, s, x, ldx, rows, din, W, b, slope, h, ldh);
-    else hipLaunchKernelGGL((thin_fwd_kernel<ACT, 64>), grid, dim3(256), 0, s, x, ldx, rows, din, W, b, slope, h, ldh);
+void launch_fwd(int dmax, hipStream_t s, const float *x, int64_t ldx, int64_t rows, int din, const float *W,
+                const float *b, float slope, float *h, int64_t ldh) {
+    if (rows >= (int64_t)kTile * kFwdGrid) {
+        launch_fwd_t<ACT, kTile>(dmax, dim3(kFwdGrid), s, x, ldx, rows, din, W, b, slope, h, ldh);
+    } else {
+        const int64_t tiles = (rows + 7) / 8;
+        launch_fwd_t<ACT, 8>(dmax, dim3((unsigned)(tiles < kFwdGrid ? tiles : kFwdGrid)), s, x, ldx, rows, din, W, b,
+                             slope, h, ldh);
+    }
 }
 
 template <int ACT>
@@ -201,13 +218,11 @@ XPA_API int xpa_thin_linear_act_fwd(int act, const float *x, int64_t ldx, int64_
     if (rows <= 0 || d_in < 1 || d_in > kMaxIn || d_out != kCols || act < 0 || act > 2 || !x || !w || !b || !h ||
         ldx < d_in || ldh < d_out)
         return (int)hipErrorInvalidValue;
-    const int64_t tiles = (rows + kTile - 1) / kTile;
-    const dim3 grid((unsigned)(tiles < kFwdGrid ? tiles : kFwdGrid));
     hipStream_t s = (hipStream_t)stream;
     const int dm = dmax_for((int)d_in);
-    if (act == 0) launch_fwd<0>(dm, grid, s, x, ldx, rows, (int)d_in, w, b, slope, h, ldh);
-    else if (act == 1) launch_fwd<1>(dm, grid, s, x, ldx, rows, (int)d_in, w, b, slope, h, ldh);
-    else launch_fwd<2>(dm, grid, s, x, ldx, rows, (int)d_in, w, b, slope, h, ldh);
+    if (act == 0) launch_fwd<0>(dm, s, x, ldx, rows, (int)d_in, w, b, slope, h, ldh);
+    else if (act == 1) launch_fwd<1>(dm, s, x, ldx, rows, (int)d_in, w, b, slope, h, ldh);
+    else launch_fwd<2>(dm, s, x, ldx, rows, (int)d_in, w, b, slope, h, ldh);
     return xpa_launch_status();
 }
 

@@ -538,13 +538,20 @@ def value_head(z_critic, act, w_critic, b_critic, out=None):
     return out
 
 
+def post_workspace(n_envs, device):
+    """K8 workspace: (partials f64 [3 * blocks], ticket int32 [1] = 0)."""
+    g = int(lib().xpa_rollout_post_num_blocks(n_envs))
+    return (torch.zeros(3 * g, dtype=torch.float64, device=device), torch.zeros(1, dtype=torch.int32, device=device))
+
+
 def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term,
                  buf_closed, buf_boot, gamma, mask_returns=True, use_rewnorm=True, rew_range=5.0, atari_lifeloss=False,
-                 deferred=None):
+                 deferred=None, workspace=None):
     """K8: reward normalisation, return tracker + ret_rms, rewards/terminals/closures into the buffer
     column cursor.ptr, then cursor.ptr = (ptr + 1) % horizon, cursor.step += 1.
     deferred = (boot_obs [N, D] (row stride may exceed D), slot_obs [N, D], slot_t int32 [N], overflow
-    int32 [1]): no v_boot; truncation rows are kept for bootstrap_fixup after the rollout."""
+    int32 [1]): no v_boot; truncation rows are kept for bootstrap_fixup after the rollout.
+    workspace = post_workspace(N) (kept by the caller across steps; allocated here when None)."""
     N = rew.shape[0]
     _req(rew, "rew", torch.float32, (N,))
     _req(term, "term", torch.uint8, (N,))
@@ -560,6 +567,7 @@ def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count,
     for name, t in (("buf_rew", buf_rew), ("buf_term", buf_term), ("buf_boot", buf_boot)):
         _req(t, name, torch.float32, (N, T))
     _req(buf_closed, "buf_closed", torch.uint8, (N, T))
+    part, ticket = workspace if workspace is not None else post_workspace(N, rew.device)
     if deferred is not None:
         boot_obs, slot_obs, slot_t, overflow = deferred
         D = slot_obs.shape[1]
@@ -572,13 +580,13 @@ def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count,
                                              _p(ret_count), _p(returns), _p(buf_rew), _p(buf_term), _p(buf_closed),
                                              _p(buf_boot), float(gamma), int(bool(mask_returns)),
                                              int(bool(use_rewnorm)), float(rew_range), int(bool(atari_lifeloss)),
-                                             _stream(rew.device))
+                                             _p(part), _p(ticket), _stream(rew.device))
         _lib.check(rc, "xpa_rollout_post_deferred")
         return
     rc = lib().xpa_rollout_post(N, T, _p(rew), _p(term), _p(trunc), _p(v_boot), _p(cursor), _p(ret_mean), _p(ret_var),
                                 _p(ret_count), _p(returns), _p(buf_rew), _p(buf_term), _p(buf_closed), _p(buf_boot),
                                 float(gamma), int(bool(mask_returns)), int(bool(use_rewnorm)), float(rew_range),
-                                int(bool(atari_lifeloss)), _stream(rew.device))
+                                int(bool(atari_lifeloss)), _p(part), _p(ticket), _stream(rew.device))
     _lib.check(rc, "xpa_rollout_post")
 
 
