@@ -109,6 +109,11 @@ int xpa_policy_loss_finalize(int algo, int dist, int64_t batch, int64_t act_dim,
                              int64_t n_partials, float vf_coef, float ent_coef, float *scalars,
                              float *d_logstd, xpa_stream_t stream);
 
+/* Epoch permutation for minibatch sampling (replaces the np.random.shuffle of an arange(buffer_size),
+ * ppoclip_agent.py:76-81): out = a pseudo-random permutation of [0, n) keyed by (seed, counter)
+ * (4-round Feistel over 2h >= log2(n) bits with cycle walking), n <= 2^31. */
+int xpa_random_permutation(int64_t n, uint32_t seed, uint32_t counter, int64_t *out, xpa_stream_t stream);
+
 /* K5 — RunningMeanStd over observations (xuance/common/statistic_tools.py:63-112) and observation
  * normalisation (xuance/torch/agents/agent.py:104-116).
  * xpa_rms_partials: per-block f64 sums of (x - shift) and (x - shift)^2 over x[n, dim] (row stride

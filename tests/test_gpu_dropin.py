@@ -200,11 +200,9 @@ def test_fused_agent_iteration_matches_cpu_replay():
     buf.returns[:], buf.advantages[:] = ret, adv
     buf.auxiliary_infos["old_logp"][:] = mem.auxiliary_infos["old_logp"].cpu().numpy()
     buf.size = T
-    gen = torch.Generator(device=DEV)
-    gen.manual_seed(agent.seed)
     B = N * T // 4
-    for _ in range(2):
-        perm = torch.randperm(N * T, device=DEV, generator=gen).cpu().numpy()
+    for e in range(2):
+        perm = agent.epoch_permutation(N * T, counter=e).cpu().numpy()
         for s in range(0, N * T, B):
             o, a, r, v, ad, ax = buf.sample(perm[s:s + B])
             info = lrn.update(o, a, r, ad, ax["old_logp"])

@@ -430,3 +430,18 @@ def test_gather_minibatch_row_shapes(row_shape, dtype):
     a = adv[idx[ok]].double()
     np.testing.assert_allclose(part[:, 0].sum().item(), a.sum().item(), rtol=1e-12, atol=1e-9)
     np.testing.assert_allclose(part[:, 1].sum().item(), (a * a).sum().item(), rtol=1e-12)
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 1000, 524288, 65536 * 8 + 3])
+def test_random_permutation_is_a_bijection(n):
+    from xuanpolicy_amd import ops
+    p0 = ops.random_permutation(n, 1, 0)
+    assert torch.equal(torch.sort(p0).values, torch.arange(n, device=p0.device))
+    if n >= 1000:
+        p1 = ops.random_permutation(n, 1, 1)
+        assert not torch.equal(p0, p1)                                   # a new epoch reshuffles
+        assert torch.equal(p0, ops.random_permutation(n, 1, 0))          # deterministic per (seed, counter)
+        # no positional structure: correlation between position and value is small
+        pos = torch.arange(n, device=p0.device, dtype=torch.float64)
+        c = torch.corrcoef(torch.stack([pos, p0.double()]))[0, 1].item()
+        assert abs(c) < 0.05

@@ -102,8 +102,8 @@ class _OnPolicyAgent:
         self.obs_mb = None
         self.adv_part = None
         self.seed = int(_cfg(config, "seed", 1))
-        self.gen = torch.Generator(device=dev)
-        self.gen.manual_seed(self.seed)
+        self._perm_counter = 0
+        self._perm_buf = None
         self.device_env = hasattr(envs, "step_device")
         self.current_step = 0
         self.current_episode = np.zeros((N,), np.int32)
@@ -292,6 +292,16 @@ class _OnPolicyAgent:
         self._host_obs = obs
 
     # ---- buffer-full phase ------------------------------------------------------------------------------
+    def epoch_permutation(self, n, counter=None):
+        """The minibatch permutation of the next epoch (ppoclip_agent.py:76-81): a device Feistel
+        permutation keyed by (config.seed, epoch counter) — one launch instead of a sort."""
+        if counter is None:
+            counter = self._perm_counter
+            self._perm_counter += 1
+        if self._perm_buf is None or self._perm_buf.shape[0] != n:
+            self._perm_buf = torch.empty(n, dtype=torch.int64, device=self.device)
+        return ops.random_permutation(n, self.seed, counter, out=self._perm_buf)
+
     def _deferred_bootstraps(self):
         """V([truncation slots; last-step final obs]) in one critic pass, written into the buffer's
         bootstrap column by xpa_rollout_bootstrap_fixup."""
@@ -322,7 +332,7 @@ class _OnPolicyAgent:
         use_advnorm = mem.use_advnorm
         scalars = None
         for _ in range(self.n_epoch):
-            perm = torch.randperm(NT, device=self.device, generator=self.gen)
+            perm = self.epoch_permutation(NT)
             for start in range(0, NT, B):
                 idx = perm[start:start + B]
                 b = idx.shape[0]

@@ -95,6 +95,34 @@ __global__ __launch_bounds__(256) void store_column_kernel(const u4v *__restrict
     }
 }
 
+// Epoch permutation of [0, n) (the np.random.shuffle of ppoclip_agent.py:76-81): a 4-round Feistel
+// network over 2h bits (2^(2h) >= n) keyed by a counter hash of (seed, counter), cycle-walked into
+// [0, n) — a bijection computed independently per element, one launch, no sort.
+constexpr uint32_t kSaltPerm = 0x9E2A0000u;
+__device__ __forceinline__ uint32_t feistel(uint32_t x, int h, uint32_t seed, uint32_t counter) {
+    const uint32_t mask = (1u << h) - 1u;
+    uint32_t L = x >> h, R = x & mask;
+#pragma unroll
+    for (uint32_t r = 0; r < 4; ++r) {
+        const uint32_t F = xpa_hash4(seed ^ kSaltPerm, counter, r, R) & mask;
+        const uint32_t nl = R;
+        R = L ^ F;
+        L = nl;
+    }
+    return (L << h) | R;
+}
+
+__global__ __launch_bounds__(256) void permutation_kernel(int64_t n, int h, uint32_t seed, uint32_t counter,
+                                                          int64_t *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint32_t x = (uint32_t)i;
+    do {
+        x = feistel(x, h, seed, counter);
+    } while ((int64_t)x >= n);
+    out[i] = (int64_t)x;
+}
+
 // ---------------------------------------------------------------------------------------------
 // K5 RunningMeanStd
 // ---------------------------------------------------------------------------------------------
@@ -734,5 +762,14 @@ XPA_API int xpa_store_column(const void *src, int64_t n, int64_t row_bytes, void
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(store_column_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                        (const u4v *)src, n, rv, (u4v *)dst, horizon, cursor);
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_random_permutation(int64_t n, uint32_t seed, uint32_t counter, int64_t *out, xpa_stream_t stream) {
+    if (n <= 0 || n > (1LL << 31) || !out) return (int)hipErrorInvalidValue;
+    int h = 1;
+    while ((1LL << (2 * h)) < n) ++h;
+    hipLaunchKernelGGL(permutation_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, h,
+                       seed, counter, out);
     return xpa_launch_status();
 }

@@ -162,6 +162,16 @@ def gae_scan(rew, val, term, closed, boot, gamma, gae_lambda, use_gae=True, adv=
     return adv, ret
 
 
+def random_permutation(n, seed, counter, out=None, device=None):
+    """Pseudo-random permutation of [0, n) keyed by (seed, counter) on device (int64 [n])."""
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=device if device is not None else "cuda")
+    _req(out, "out", torch.int64, (n,))
+    _lib.check(lib().xpa_random_permutation(n, int(seed) & 0xFFFFFFFF, int(counter) & 0xFFFFFFFF, _p(out),
+                                            _stream(out.device)), "xpa_random_permutation")
+    return out
+
+
 def gather_num_partials(batch):
     return int(lib().xpa_gather_num_partials(batch))
 
