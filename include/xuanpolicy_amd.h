@@ -74,7 +74,7 @@ int xpa_gae_scan_timed(const float *rew, const float *val, const float *term, co
  * (memory_tools.py:231-240) for the observation rows (the rest is read through `idx` by the loss
  * kernel), and produces the per-minibatch advantage moments for adv-norm (memory_tools.py:241-242).
  * obs_out[b] = obs[idx[b]] (row_bytes each); adv_partials[g] = (sum, sum of squares) in f64 over
- * rows [g*256, (g+1)*256); xpa_gather_num_partials(batch) rows.  adv/adv_partials may be NULL.
+ * rows [g*64, (g+1)*64); xpa_gather_num_partials(batch) rows.  adv/adv_partials may be NULL.
  * n_rows = rows of obs/adv: an index outside [0, n_rows) is never dereferenced (its output row is
  * zeroed and it adds nothing to the moments). */
 int64_t xpa_gather_num_partials(int64_t batch);

@@ -120,7 +120,8 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(
     float *__restrict__ p_dbo, float *__restrict__ p_loss, int loss_width) {
     __shared__ __attribute__((aligned(16))) float s_h[kTile * kS];
     __shared__ __attribute__((aligned(16))) float s_part[kWaves][kTile][KMAX];
-    __shared__ __attribute__((aligned(16))) float s_dh[kTile][KMAX];
+    constexpr int KP = (KMAX + 3) & ~3;  // 16-B aligned d-head rows
+    __shared__ __attribute__((aligned(16))) float s_dh[kTile][KP];
     __shared__ float s_mean, s_inv;
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -388,10 +389,14 @@ void launch_head(const HeadArgs &a, int act_code, hipStream_t s) {
         if (act_code == 0) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 0, 1>), grid, block, 0, s, XPA_HEAD_ARGS(a));
         else if (act_code == 1) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 1, 1>), grid, block, 0, s, XPA_HEAD_ARGS(a));
         else hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 2, 1>), grid, block, 0, s, XPA_HEAD_ARGS(a));
-    } else if (a.K <= 4) {  // KMAX 8 (K <= 8); the K <= 4 instantiation keeps fewer live registers
+    } else if (a.K <= 4) {  // KMAX = the smallest of 4 / 6 / 8 >= K (fewer live registers and FMAs)
         if (act_code == 0) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 0, 4>), grid, block, 0, s, XPA_HEAD_ARGS(a));
         else if (act_code == 1) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 1, 4>), grid, block, 0, s, XPA_HEAD_ARGS(a));
         else hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 2, 4>), grid, block, 0, s, XPA_HEAD_ARGS(a));
+    } else if (a.K <= 6) {
+        if (act_code == 0) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 0, 6>), grid, block, 0, s, XPA_HEAD_ARGS(a));
+        else if (act_code == 1) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 1, 6>), grid, block, 0, s, XPA_HEAD_ARGS(a));
+        else hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 2, 6>), grid, block, 0, s, XPA_HEAD_ARGS(a));
     } else {
         if (act_code == 0) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 0, 8>), grid, block, 0, s, XPA_HEAD_ARGS(a));
         else if (act_code == 1) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 1, 8>), grid, block, 0, s, XPA_HEAD_ARGS(a));

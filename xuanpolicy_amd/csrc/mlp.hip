@@ -234,15 +234,43 @@ __global__ __launch_bounds__(256) void head_backward_vec4_kernel(int K, const fl
     combine(dbh, p_dbh + (int64_t)blockIdx.x * H);
 }
 
-__global__ __launch_bounds__(256) void colsum_finalize_kernel(const float *__restrict__ partials, int64_t G, int C,
-                                                              float *__restrict__ out) {
-    // one wave per column, lanes over partial rows, fixed order -> deterministic
-    const int w = (blockIdx.x * 256 + threadIdx.x) >> 6, lane = threadIdx.x & 63;
-    if (w >= C) return;
+// Column sums of per-block partials [G, C] -> out [C]: a block owns 64 columns (coalesced 256-B row
+// reads) x 16 row groups (thread (g, c) sums rows g, g + 16, ... in order, f64); the groups are combined
+// through LDS in a fixed order -> deterministic, and identical for the single and the batched entry.
+constexpr int kColTile = 64;
+constexpr int kColGroups = 16;
+
+__device__ __forceinline__ void colsum_tile(const float *__restrict__ part, int64_t G, int C, int c0,
+                                            float *__restrict__ out, double (*s_red)[kColTile]) {
+    const int lane = threadIdx.x & (kColTile - 1), grp = threadIdx.x / kColTile;
+    const int c = c0 + lane;
     double s = 0.0;
-    for (int64_t k = lane; k < G; k += 64) s += (double)partials[k * C + w];
-    s = xpa_wave_sum(s);
-    if (lane == 0) out[w] = (float)s;
+    if (c < C) {
+        int64_t k = grp;
+        for (; k + 3 * kColGroups < G; k += 4 * kColGroups) {  // 4 independent loads in flight
+            const float a0 = part[k * C + c], a1 = part[(k + kColGroups) * C + c];
+            const float a2 = part[(k + 2 * kColGroups) * C + c], a3 = part[(k + 3 * kColGroups) * C + c];
+            s += (double)a0;
+            s += (double)a1;
+            s += (double)a2;
+            s += (double)a3;
+        }
+        for (; k < G; k += kColGroups) s += (double)part[k * C + c];
+    }
+    s_red[grp][lane] = s;
+    __syncthreads();
+    if (grp == 0 && c < C) {
+        double t = s_red[0][lane];
+        for (int g = 1; g < kColGroups; ++g) t += s_red[g][lane];
+        out[c] = (float)t;
+    }
+}
+
+__global__ __launch_bounds__(kColTile * kColGroups) void colsum_finalize_kernel(const float *__restrict__ partials,
+                                                                               int64_t G, int C,
+                                                                               float *__restrict__ out) {
+    __shared__ double s_red[kColGroups][kColTile];
+    colsum_tile(partials, G, C, (int)blockIdx.x * kColTile, out, s_red);
 }
 
 constexpr int kMaxSegs = 16;
@@ -251,21 +279,16 @@ struct ColsumBatch {
     float *out[kMaxSegs];
     int64_t G[kMaxSegs];
     int C[kMaxSegs];
-    int start[kMaxSegs + 1];  // first global column of each segment
+    int tile0[kMaxSegs + 1];  // first column tile of each segment
     int n;
 };
 
-__global__ __launch_bounds__(256) void colsum_finalize_batch_kernel(ColsumBatch b) {
-    const int w = (blockIdx.x * 256 + threadIdx.x) >> 6, lane = threadIdx.x & 63;
-    if (w >= b.start[b.n]) return;
+__global__ __launch_bounds__(kColTile * kColGroups) void colsum_finalize_batch_kernel(ColsumBatch b) {
+    __shared__ double s_red[kColGroups][kColTile];
+    const int tile = blockIdx.x;
     int sg = 0;
-    while (w >= b.start[sg + 1]) ++sg;
-    const int col = w - b.start[sg], C = b.C[sg];
-    const float *__restrict__ part = b.part[sg];
-    double s = 0.0;
-    for (int64_t k = lane; k < b.G[sg]; k += 64) s += (double)part[k * C + col];
-    s = xpa_wave_sum(s);
-    if (lane == 0) b.out[sg][col] = (float)s;
+    while (tile >= b.tile0[sg + 1]) ++sg;
+    colsum_tile(b.part[sg], b.G[sg], b.C[sg], (tile - b.tile0[sg]) * kColTile, b.out[sg], s_red);
 }
 
 }  // namespace
@@ -353,9 +376,9 @@ XPA_API int xpa_head_backward(int act, int64_t k, const float *d_head, int64_t l
 XPA_API int xpa_colsum_finalize(const float *partials, int64_t n_partials, int64_t cols, float *out,
                                 xpa_stream_t stream) {
     if (n_partials <= 0 || cols <= 0 || !partials || !out) return (int)hipErrorInvalidValue;
-    const unsigned blocks = (unsigned)((cols * 64 + 255) / 256);
-    hipLaunchKernelGGL(colsum_finalize_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, partials, n_partials,
-                       (int)cols, out);
+    const unsigned blocks = (unsigned)((cols + kColTile - 1) / kColTile);
+    hipLaunchKernelGGL(colsum_finalize_kernel, dim3(blocks), dim3(kColTile * kColGroups), 0, (hipStream_t)stream,
+                       partials, n_partials, (int)cols, out);
     return xpa_launch_status();
 }
 
@@ -364,19 +387,19 @@ XPA_API int xpa_colsum_finalize_batch(int n_segs, const float *const *partials, 
     if (n_segs <= 0 || n_segs > kMaxSegs || !partials || !n_partials || !cols || !outs) return (int)hipErrorInvalidValue;
     ColsumBatch b{};
     b.n = n_segs;
-    int64_t total = 0;
+    int64_t tiles = 0;
     for (int i = 0; i < n_segs; ++i) {
-        if (!partials[i] || !outs[i] || n_partials[i] <= 0 || cols[i] <= 0) return (int)hipErrorInvalidValue;
+        if (!partials[i] || !outs[i] || n_partials[i] <= 0 || cols[i] <= 0 || cols[i] > (1 << 24))
+            return (int)hipErrorInvalidValue;
         b.part[i] = partials[i];
         b.out[i] = outs[i];
         b.G[i] = n_partials[i];
         b.C[i] = (int)cols[i];
-        b.start[i] = (int)total;
-        total += cols[i];
-        if (total > (1 << 24)) return (int)hipErrorInvalidValue;
+        b.tile0[i] = (int)tiles;
+        tiles += (cols[i] + kColTile - 1) / kColTile;
     }
-    b.start[n_segs] = (int)total;
-    const unsigned blocks = (unsigned)((total * 64 + 255) / 256);
-    hipLaunchKernelGGL(colsum_finalize_batch_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, b);
+    b.tile0[n_segs] = (int)tiles;
+    hipLaunchKernelGGL(colsum_finalize_batch_kernel, dim3((unsigned)tiles), dim3(kColTile * kColGroups), 0,
+                       (hipStream_t)stream, b);
     return xpa_launch_status();
 }

@@ -10,7 +10,7 @@
 
 namespace {
 
-constexpr int kGatherRows = 256;  // rows per gather block == rows per adv partial
+constexpr int kGatherRows = 64;  // rows per gather block == rows per adv partial (1024 blocks at B = 65 536)
 constexpr int kRmsRows = 256;     // rows per RMS partial block
 constexpr uint32_t kSaltAct = 0xAC7105EDu;
 constexpr uint32_t kSaltReset = 0x5EED0000u;  // oracle/synth_env.py SALT_RESET
