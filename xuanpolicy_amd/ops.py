@@ -26,14 +26,18 @@ class KernelTimer:
 
     def __init__(self):
         self.enabled = False
+        self.only = None          # optional set of names to time (others pass through untimed)
         self.events = {}
         self.hip_pairs = {}
         # GPU spin (clock cycles) queued before the start event, so the kernel is already enqueued when
         # the start event completes and the host launch latency is not counted as kernel time.
         self.pad_cycles = {}
 
+    def _on(self, name):
+        return self.enabled and (self.only is None or name in self.only)
+
     def start(self, name):
-        if not self.enabled:
+        if not self._on(name):
             return None
         pad = self.pad_cycles.get(name, 0)
         if pad:
@@ -66,7 +70,7 @@ class KernelTimer:
     def kernel_events(self, name):
         """(start, stop) hipEvent_t handles for a launch whose kernel records them itself, or None when
         timing is off."""
-        if not self.enabled:
+        if not self._on(name):
             return None
         rt = self._hip()
         pair = []
