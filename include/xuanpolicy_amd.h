@@ -258,6 +258,24 @@ int xpa_rollout_policy_head(int dist, int act, int64_t n_envs, int64_t act_dim, 
 int xpa_value_head(int act, int64_t n, int64_t hidden, int64_t ld, const float *z_critic, float slope,
                    const float *w_critic, const float *b_critic, float *v_out, xpa_stream_t stream);
 
+/* K16 — K12 with the hidden layer's GEMM on the fp32 matrix cores (v_mfma_f32_32x32x2_f32): the
+ * pre-activations z = x w_hidden^T + b_hidden of each [64 x 256] tile are formed in registers and never
+ * written to HBM; the rest is exactly K12 (same outputs, partial layouts and loss-partials columns).
+ * x: the hidden layer's input [batch, 256] (row stride ldx); w_hidden [256, 256] row-major (the
+ * Linear's weight), b_hidden [256]; dz rows have stride ld_dz. */
+int xpa_head_gemm_actor(int algo, int dist, int act, int64_t batch, int64_t act_dim, int64_t hidden, const float *x,
+                        int64_t ldx, const float *w_hidden, const float *b_hidden, int64_t ld_dz, const float *w,
+                        const float *b, float slope, const float *logstd, const int64_t *idx, int64_t n_rows,
+                        const float *act_buf, const float *old_logp, const float *adv, const double *adv_partials,
+                        int64_t n_adv_partials, float clip_range, float ent_coef, float *dz, float *partial_dw,
+                        float *partial_db_hidden, float *partial_db_out, float *loss_partials, int64_t loss_width,
+                        xpa_stream_t stream);
+int xpa_head_gemm_critic(int act, int64_t batch, int64_t hidden, const float *x, int64_t ldx, const float *w_hidden,
+                         const float *b_hidden, int64_t ld_dz, const float *w, const float *b, float slope,
+                         const int64_t *idx, int64_t n_rows, const float *ret, float vf_coef, float *dz,
+                         float *partial_dw, float *partial_db_hidden, float *partial_db_out, float *loss_partials,
+                         int64_t loss_width, xpa_stream_t stream);
+
 /* K6 — prioritized replay (PerOffPolicyBuffer, memory_tools.py:369-492; Sum/MinSegmentTree,
  * segtree_tool.py:4-86) with f64 trees on device: one [n_envs, 2*capacity] array per tree (node 1 =
  * root, leaf i at capacity + i; neutral 0 / +inf), capacity = next power of two >= n_size.

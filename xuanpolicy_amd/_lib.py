@@ -85,6 +85,11 @@ SIGNATURES = {
                                                c_p]),
     "xpa_thin_linear_act_bwd": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_f32,
                                                c_p, c_p, c_p]),
+    "xpa_head_gemm_actor": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_i64, c_p,
+                                           c_p, c_i64, c_p, c_p, c_f32, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_f32,
+                                           c_f32, c_p, c_p, c_p, c_p, c_p, c_i64, c_p]),
+    "xpa_head_gemm_critic": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_f32, c_p,
+                                            c_i64, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64, c_p]),
     "xpa_grad_norm_num_partials": (c_i64, [c_i64]),
     "xpa_clip_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_p, c_f32, c_f32, c_f32, c_f32, c_f32, c_i64, c_p,
                                           c_p]),

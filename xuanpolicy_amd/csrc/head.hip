@@ -76,7 +76,9 @@ struct HeadArgs {
     int64_t batch;
     int K;
     int64_t ld;
-    const float *z;
+    const float *z;  // K12: hidden pre-activations; K16: the hidden layer's input x
+    int64_t ldx;
+    const float *Wh, *bh;  // K16: hidden layer weight [256, 256] and bias
     const float *W;
     const float *bias;
     float slope;
@@ -109,100 +111,106 @@ __device__ __forceinline__ void load_tile(float4 (&zq)[16], const float *__restr
     }
 }
 
+// ---- shared epilogue: everything after h = act(z) of a 64-row tile is in LDS ----------------------
 // MODE: 0 Gaussian actor, 1 Categorical actor, 2 critic.  ALGO: 0 PPO, 1 A2C (actor only).
+template <int KMAX>
+struct RowIn {  // wave 0, lane = row of the tile
+    bool valid;
+    float x, old, act[KMAX];
+};
+
 template <int MODE, int ALGO, int ACT, int KMAX>
-__global__ __launch_bounds__(256, 2) void head_tile_kernel(
-    int64_t batch, int K_in, int64_t ld, const float *__restrict__ z, const float *__restrict__ W, const float *__restrict__ bias,
-    float slope, const float *__restrict__ logstd, const int64_t *__restrict__ idx, int64_t n_rows,
-    const float *__restrict__ act, const float *__restrict__ old_logp, const float *__restrict__ adv,
-    const float *__restrict__ ret, const double *__restrict__ adv_partials, int64_t n_adv_partials, float clip_range,
-    float ent_coef, float vf_coef, float *__restrict__ dz, float *__restrict__ p_dw, float *__restrict__ p_dbh,
-    float *__restrict__ p_dbo, float *__restrict__ p_loss, int loss_width) {
-    __shared__ __attribute__((aligned(16))) float s_h[kTile * kS];
-    __shared__ __attribute__((aligned(16))) float s_part[kWaves][kTile][KMAX];
-    constexpr int KP = (KMAX + 3) & ~3;  // 16-B aligned d-head rows
-    __shared__ __attribute__((aligned(16))) float s_dh[kTile][KP];
-    __shared__ float s_mean, s_inv;
-    const int t = threadIdx.x, lane = t & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int K = MODE == 2 ? 1 : K_in;
-    if (MODE != 2 && adv_partials) {
-        adv_stats(adv_partials, n_adv_partials, batch, &s_mean, &s_inv);
-    } else if (t == 0) {
-        s_mean = 0.f;
-        s_inv = 1.f;
-    }
-    const int64_t ntiles = (batch + kTile - 1) / kTile;
-    int64_t tile = blockIdx.x;
-    float4 zq[16];
-    load_tile(zq, z, ld, tile, batch);
-
-    // phase-2 constants / accumulators (column t)
-    float wc[KMAX], acc_dw[KMAX];
-#pragma unroll
-    for (int o = 0; o < KMAX; ++o) {
-        wc[o] = o < K ? W[o * kH + t] : 0.f;
-        acc_dw[o] = 0.f;
-    }
-    float acc_dbh = 0.f;
-    // wave-0 (row owner) accumulators
+struct HeadEpi {
+    static constexpr int KP = (KMAX + 3) & ~3;  // 16-B aligned d-head rows
+    float wc[KMAX], acc_dw[KMAX], acc_dbh;      // phase 2 (column t)
     float acc_dbo[KMAX], acc_dls[KMAX], var_[KMAX], logsc[KMAX];
-    float sum0 = 0.f, sum1 = 0.f, sum2 = 0.f, ent_const = 0.f;
-#pragma unroll
-    for (int o = 0; o < KMAX; ++o) {
-        acc_dbo[o] = acc_dls[o] = 0.f;
-        if (MODE == 0) {
-            const float sc = o < K ? expf(logstd[o]) : 1.f;
-            var_[o] = sc * sc;
-            logsc[o] = logf(sc);
-            if (o < K) ent_const += kHalfLog2PiPlusHalf + logsc[o];
-        }
-    }
-    const float inv_b = 1.0f / (float)batch;
-    const float lo = 1.0f - clip_range, hi = 1.0f + clip_range;
-    __syncthreads();
-    const float a_mean = s_mean, a_inv = s_inv;
+    float sum0, sum1, sum2, ent_const, inv_b, lo, hi, a_mean, a_inv, slope;
+    int K;
 
-    for (; tile < ntiles; tile += gridDim.x) {
-        // ---- stage h = act(z) into LDS ----
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int lin = i * 256 + t;
-            float4 h;
-            h.x = act_f<ACT>(zq[i].x, slope); h.y = act_f<ACT>(zq[i].y, slope);
-            h.z = act_f<ACT>(zq[i].z, slope); h.w = act_f<ACT>(zq[i].w, slope);
-            *reinterpret_cast<float4 *>(s_h + (lin >> 6) * kS + 4 * (lin & 63)) = h;
+    // W: output layer [K, 256]; s_stats: 2 floats of LDS.  Ends with a block barrier.
+    __device__ __forceinline__ void init(int K_in, const float *__restrict__ W, const float *__restrict__ logstd,
+                                         const double *__restrict__ adv_partials, int64_t n_adv_partials,
+                                         int64_t batch, float clip_range, float slope_, float *s_stats) {
+        const int t = threadIdx.x;
+        K = MODE == 2 ? 1 : K_in;
+        slope = slope_;
+        if (MODE != 2 && adv_partials) {
+            adv_stats(adv_partials, n_adv_partials, batch, s_stats, s_stats + 1);
+        } else if (t == 0) {
+            s_stats[0] = 0.f;
+            s_stats[1] = 1.f;
         }
-        // ---- wave 0: this tile's per-row inputs (lane = row) ----
-        bool valid = false;
-        float my_x = 0.f, my_old = 0.f, my_act[KMAX];
 #pragma unroll
-        for (int o = 0; o < KMAX; ++o) my_act[o] = 0.f;
-        if (wave == 0) {
+        for (int o = 0; o < KMAX; ++o) {
+            wc[o] = o < K ? W[o * kH + t] : 0.f;
+            acc_dw[o] = 0.f;
+            acc_dbo[o] = acc_dls[o] = 0.f;
+            var_[o] = 1.f;
+            logsc[o] = 0.f;
+        }
+        acc_dbh = 0.f;
+        sum0 = sum1 = sum2 = ent_const = 0.f;
+        if (MODE == 0) {
+#pragma unroll
+            for (int o = 0; o < KMAX; ++o) {
+                const float sc = o < K ? expf(logstd[o]) : 1.f;
+                var_[o] = sc * sc;
+                logsc[o] = logf(sc);
+                if (o < K) ent_const += kHalfLog2PiPlusHalf + logsc[o];
+            }
+        }
+        inv_b = 1.0f / (float)batch;
+        lo = 1.0f - clip_range;
+        hi = 1.0f + clip_range;
+        __syncthreads();
+        a_mean = s_stats[0];
+        a_inv = s_stats[1];
+    }
+
+    __device__ __forceinline__ RowIn<KMAX> rows(int64_t tile, int64_t batch, const int64_t *__restrict__ idx,
+                                                int64_t n_rows, const float *__restrict__ act,
+                                                const float *__restrict__ old_logp, const float *__restrict__ adv,
+                                                const float *__restrict__ ret) const {
+        RowIn<KMAX> in;
+        in.valid = false;
+        in.x = in.old = 0.f;
+#pragma unroll
+        for (int o = 0; o < KMAX; ++o) in.act[o] = 0.f;
+        const int lane = threadIdx.x & 63;
+        if ((threadIdx.x >> 6) == 0) {
             const int64_t b = tile * kTile + lane;
             if (b < batch) {
                 const int64_t row = idx ? idx[b] : b;
-                valid = row >= 0 && row < n_rows;
-                if (valid) {
+                in.valid = row >= 0 && row < n_rows;
+                if (in.valid) {
                     if (MODE == 2) {
-                        my_x = ret[row];
+                        in.x = ret[row];
                     } else {
-                        my_x = adv[row];
-                        if (ALGO == 0) my_old = old_logp[row];
+                        in.x = adv[row];
+                        if (ALGO == 0) in.old = old_logp[row];
                         if (MODE == 0) {
 #pragma unroll
                             for (int o = 0; o < KMAX; ++o)
-                                if (o < K) my_act[o] = act[row * K + o];
+                                if (o < K) in.act[o] = act[row * K + o];
                         } else {
-                            my_act[0] = act[row];
+                            in.act[0] = act[row];
                         }
                     }
                 }
             }
         }
+        return in;
+    }
+
+    // s_h holds h = act(z) of rows [tile*64, tile*64 + 64) (row stride kS).  Starts with a barrier
+    // (s_h complete), ends with one (s_h / s_dh free for the next tile).
+    __device__ __forceinline__ void tile(const float *s_h, float (*s_part)[kTile][KMAX], float (*s_dh)[KP],
+                                         const RowIn<KMAX> &in, int64_t tile, int64_t batch,
+                                         const float *__restrict__ W, const float *__restrict__ bias,
+                                         float *__restrict__ dz, int64_t ld, float ent_coef, float vf_coef) {
+        const int t = threadIdx.x, lane = t & 63;
+        const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
         __syncthreads();
-        const int64_t next = tile + gridDim.x;
-        if (next < ntiles) load_tile(zq, z, ld, next, batch);  // in flight during phases 1-2
         // ---- phase 1: partial dot products, row = lane, quarter = wave ----
         {
             float p[KMAX];
@@ -230,7 +238,7 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(
             float dh_[KMAX];
 #pragma unroll
             for (int o = 0; o < KMAX; ++o) dh_[o] = 0.f;
-            if (valid) {
+            if (in.valid) {
                 float hd[KMAX];
 #pragma unroll
                 for (int o = 0; o < KMAX; ++o)
@@ -238,13 +246,13 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(
                                         bias[o]
                                   : 0.f;
                 if (MODE == 2) {
-                    const float diffv = hd[0] - my_x;
+                    const float diffv = hd[0] - in.x;
                     sum0 += diffv * diffv;
                     sum1 += hd[0];
                     dh_[0] = vf_coef * 2.0f * diffv * inv_b;
                     acc_dbo[0] += dh_[0];
                 } else {
-                    const float A_n = (my_x - a_mean) * a_inv;
+                    const float A_n = (in.x - a_mean) * a_inv;
                     float logp = 0.f, ent = 0.f, lse = 0.f;
                     int ai = 0;
                     float diff[KMAX];
@@ -253,7 +261,7 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(
                         for (int o = 0; o < KMAX; ++o) {
                             diff[o] = 0.f;
                             if (o < K) {
-                                diff[o] = my_act[o] - hd[o];
+                                diff[o] = in.act[o] - hd[o];
                                 logp += -(diff[o] * diff[o]) / (2.0f * var_[o]) - logsc[o] - kLogSqrt2Pi;
                             }
                         }
@@ -268,7 +276,7 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(
                         for (int o = 0; o < KMAX; ++o)
                             if (o < K) se += expf(hd[o] - m);
                         lse = m + logf(se);
-                        ai = (int)my_act[0];
+                        ai = (int)in.act[0];
                         ai = ai < 0 ? 0 : (ai >= K ? K - 1 : ai);
 #pragma unroll
                         for (int o = 0; o < KMAX; ++o) {
@@ -281,7 +289,7 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(
                     }
                     float dlogp;
                     if (ALGO == 0) {
-                        const float ratio = expf(logp - my_old);
+                        const float ratio = expf(logp - in.old);
                         const float cr = fminf(fmaxf(ratio, lo), hi);
                         const float s1 = cr * A_n, s2 = A_n * ratio;
                         sum0 += fminf(s1, s2);
@@ -335,42 +343,214 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(
         }
         __syncthreads();  // s_h / s_dh reused by the next tile
     }
-    // ---- block partials ----
-    const int64_t blk = blockIdx.x;
+
+    __device__ __forceinline__ void finish(float *__restrict__ p_dw, float *__restrict__ p_dbh,
+                                           float *__restrict__ p_dbo, float *__restrict__ p_loss, int loss_width) {
+        const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+        const int64_t blk = blockIdx.x;
 #pragma unroll
-    for (int o = 0; o < KMAX; ++o)
-        if (o < K) p_dw[(blk * K + o) * kH + t] = acc_dw[o];
-    p_dbh[blk * kH + t] = acc_dbh;
-    if (wave == 0) {
-        sum0 = xpa_wave_sum(sum0);
-        sum1 = xpa_wave_sum(sum1);
-        sum2 = xpa_wave_sum(sum2);
-#pragma unroll
-        for (int o = 0; o < KMAX; ++o) {
-            if (o < K) {
-                acc_dbo[o] = xpa_wave_sum(acc_dbo[o]);
-                if (MODE == 0) acc_dls[o] = xpa_wave_sum(acc_dls[o]);
-            }
-        }
-        if (lane == 0) {
-            float *prow = p_loss + blk * loss_width;
-            if (MODE == 2) {
-                prow[1] = sum0;
-                prow[4] = sum1;
-            } else {
-                prow[0] = sum0;
-                prow[2] = sum1;
-                prow[3] = sum2;
-            }
+        for (int o = 0; o < KMAX; ++o)
+            if (o < K) p_dw[(blk * K + o) * kH + t] = acc_dw[o];
+        p_dbh[blk * kH + t] = acc_dbh;
+        if (wave == 0) {
+            sum0 = xpa_wave_sum(sum0);
+            sum1 = xpa_wave_sum(sum1);
+            sum2 = xpa_wave_sum(sum2);
 #pragma unroll
             for (int o = 0; o < KMAX; ++o) {
                 if (o < K) {
-                    p_dbo[blk * K + o] = acc_dbo[o];
-                    if (MODE == 0) prow[kPartBase + o] = acc_dls[o];
+                    acc_dbo[o] = xpa_wave_sum(acc_dbo[o]);
+                    if (MODE == 0) acc_dls[o] = xpa_wave_sum(acc_dls[o]);
+                }
+            }
+            if (lane == 0) {
+                float *prow = p_loss + blk * loss_width;
+                if (MODE == 2) {
+                    prow[1] = sum0;
+                    prow[4] = sum1;
+                } else {
+                    prow[0] = sum0;
+                    prow[2] = sum1;
+                    prow[3] = sum2;
+                }
+#pragma unroll
+                for (int o = 0; o < KMAX; ++o) {
+                    if (o < K) {
+                        p_dbo[blk * K + o] = acc_dbo[o];
+                        if (MODE == 0) prow[kPartBase + o] = acc_dls[o];
+                    }
                 }
             }
         }
     }
+};
+
+#define XPA_HEAD_KERNEL_PARAMS                                                                                     \
+    int64_t batch, int K_in, int64_t ld, const float *__restrict__ z, int64_t ldx, const float *__restrict__ Wh,   \
+        const float *__restrict__ bh, const float *__restrict__ W, const float *__restrict__ bias, float slope,     \
+        const float *__restrict__ logstd, const int64_t *__restrict__ idx, int64_t n_rows,                         \
+        const float *__restrict__ act, const float *__restrict__ old_logp, const float *__restrict__ adv,          \
+        const float *__restrict__ ret, const double *__restrict__ adv_partials, int64_t n_adv_partials,            \
+        float clip_range, float ent_coef, float vf_coef, float *__restrict__ dz, float *__restrict__ p_dw,         \
+        float *__restrict__ p_dbh, float *__restrict__ p_dbo, float *__restrict__ p_loss, int loss_width
+
+// K12: z (the hidden pre-activations, row stride ld == ldx) streamed from HBM.
+template <int MODE, int ALGO, int ACT, int KMAX>
+__global__ __launch_bounds__(256, 2) void head_tile_kernel(XPA_HEAD_KERNEL_PARAMS) {
+    using Epi = HeadEpi<MODE, ALGO, ACT, KMAX>;
+    __shared__ __attribute__((aligned(16))) float s_h[kTile * kS];
+    __shared__ __attribute__((aligned(16))) float s_part[kWaves][kTile][KMAX];
+    __shared__ __attribute__((aligned(16))) float s_dh[kTile][Epi::KP];
+    __shared__ float s_stats[2];
+    const int t = threadIdx.x;
+    const int64_t ntiles = (batch + kTile - 1) / kTile;
+    int64_t tile = blockIdx.x;
+    float4 zq[16];
+    load_tile(zq, z, ldx, tile, batch);
+    Epi epi;
+    epi.init(K_in, W, logstd, adv_partials, n_adv_partials, batch, clip_range, slope, s_stats);
+    for (; tile < ntiles; tile += gridDim.x) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {  // stage h = act(z)
+            const int lin = i * 256 + t;
+            float4 h;
+            h.x = act_f<ACT>(zq[i].x, slope); h.y = act_f<ACT>(zq[i].y, slope);
+            h.z = act_f<ACT>(zq[i].z, slope); h.w = act_f<ACT>(zq[i].w, slope);
+            *reinterpret_cast<float4 *>(s_h + (lin >> 6) * kS + 4 * (lin & 63)) = h;
+        }
+        const RowIn<KMAX> in = epi.rows(tile, batch, idx, n_rows, act, old_logp, adv, ret);
+        const int64_t next = tile + gridDim.x;
+        if (next < ntiles) load_tile(zq, z, ldx, next, batch);  // in flight during the epilogue
+        epi.tile(s_h, s_part, s_dh, in, tile, batch, W, bias, dz, ld, ent_coef, vf_coef);
+    }
+    epi.finish(p_dw, p_dbh, p_dbo, p_loss, loss_width);
+}
+
+// K16: the hidden layer's GEMM itself on the fp32 matrix cores, z = x Wh^T + bh for a [64 x 256] tile
+// (v_mfma_f32_32x32x2_f32: exact f32 fma chains), then the K12 epilogue on the tile in LDS — z never
+// goes to HBM.  Wave w owns columns [64w, 64w + 64) as 2 x 2 tiles of 32 x 32 (64 accumulator regs);
+// k runs in chunks of 16, double-buffered in LDS as [k parity h][row][k / 2] images (row stride 12
+// floats: the 16-lane groups of each ds_read_b128 hit 16 distinct 4-bank slots), the next chunk's
+// global loads in flight during the current chunk's 32 MFMAs per wave.
+constexpr int kKin = 256;
+constexpr int kKC = 16;
+constexpr int kPS = 12;
+constexpr int kAImg = 2 * kTile * kPS;
+constexpr int kBImg = 2 * kH * kPS;
+constexpr int kStage = kAImg + kBImg;
+static_assert(2 * kStage <= kTile * kS, "operand stages share the epilogue tile");
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void gemm_load(const float *__restrict__ x, int64_t ldx, const float *__restrict__ Wh,
+                                          int64_t r0, int64_t batch, int k0, float4 &ra, float4 (&rb)[4]) {
+    const int t = threadIdx.x;
+    const int row = t >> 2, q = t & 3;
+    ra = (r0 + row < batch) ? *reinterpret_cast<const float4 *>(x + (r0 + row) * ldx + k0 + 4 * q)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int lin = j * 256 + t, c = lin >> 2, q2 = lin & 3;
+        rb[j] = *reinterpret_cast<const float4 *>(Wh + c * kKin + k0 + 4 * q2);
+    }
+}
+
+__device__ __forceinline__ void gemm_store(float *st, const float4 &ra, const float4 (&rb)[4]) {
+    const int t = threadIdx.x;
+    const int row = t >> 2, q = t & 3;
+    float *A = st, *B = st + kAImg;
+    *reinterpret_cast<float2 *>(A + row * kPS + 2 * q) = make_float2(ra.x, ra.z);            // k even
+    *reinterpret_cast<float2 *>(A + (kTile + row) * kPS + 2 * q) = make_float2(ra.y, ra.w);  // k odd
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int lin = j * 256 + t, c = lin >> 2, q2 = lin & 3;
+        *reinterpret_cast<float2 *>(B + c * kPS + 2 * q2) = make_float2(rb[j].x, rb[j].z);
+        *reinterpret_cast<float2 *>(B + (kH + c) * kPS + 2 * q2) = make_float2(rb[j].y, rb[j].w);
+    }
+}
+
+__device__ __forceinline__ void gemm_chunk(const float *st, f32x16 (&acc)[2][2], int lane, int wave) {
+    const float *A = st, *B = st + kAImg;
+    const int h = lane >> 5, i = lane & 31;
+    float4 alo[2], ahi[2], blo[2], bhi[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+        const float *pa = A + (h * kTile + rt * 32 + i) * kPS;
+        alo[rt] = *reinterpret_cast<const float4 *>(pa);
+        ahi[rt] = *reinterpret_cast<const float4 *>(pa + 4);
+    }
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+        const float *pb = B + (h * kH + wave * 64 + ct * 32 + i) * kPS;
+        blo[ct] = *reinterpret_cast<const float4 *>(pb);
+        bhi[ct] = *reinterpret_cast<const float4 *>(pb + 4);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 8; ++s2) {
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+            const float4 &av = s2 < 4 ? alo[rt] : ahi[rt];
+            const float a = (s2 & 3) == 0 ? av.x : (s2 & 3) == 1 ? av.y : (s2 & 3) == 2 ? av.z : av.w;
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                const float4 &bv = s2 < 4 ? blo[ct] : bhi[ct];
+                const float b = (s2 & 3) == 0 ? bv.x : (s2 & 3) == 1 ? bv.y : (s2 & 3) == 2 ? bv.z : bv.w;
+                acc[rt][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[rt][ct], 0, 0, 0);
+            }
+        }
+    }
+}
+
+template <int MODE, int ALGO, int ACT, int KMAX>
+__global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAMS) {
+    using Epi = HeadEpi<MODE, ALGO, ACT, KMAX>;
+    __shared__ __attribute__((aligned(16))) float smem[kTile * kS];  // operand stages, then the h tile
+    __shared__ __attribute__((aligned(16))) float s_part[kWaves][kTile][KMAX];
+    __shared__ __attribute__((aligned(16))) float s_dh[kTile][Epi::KP];
+    __shared__ float s_stats[2];
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int64_t ntiles = (batch + kTile - 1) / kTile;
+    Epi epi;
+    epi.init(K_in, W, logstd, adv_partials, n_adv_partials, batch, clip_range, slope, s_stats);
+    const float bh0 = bh[wave * 64 + (lane & 31)], bh1 = bh[wave * 64 + 32 + (lane & 31)];
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t r0 = tile * kTile;
+        const RowIn<KMAX> in = epi.rows(tile, batch, idx, n_rows, act, old_logp, adv, ret);
+        f32x16 acc[2][2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[rt][ct][r] = 0.f;
+        float4 ra, rb[4];
+        __syncthreads();  // the previous tile's epilogue is done with smem
+        gemm_load(z, ldx, Wh, r0, batch, 0, ra, rb);
+        gemm_store(smem, ra, rb);
+        __syncthreads();
+        for (int c = 0; c < kKin / kKC; ++c) {
+            const bool more = c + 1 < kKin / kKC;
+            if (more) gemm_load(z, ldx, Wh, r0, batch, (c + 1) * kKC, ra, rb);
+            gemm_chunk(smem + (c & 1) * kStage, acc, lane, wave);
+            if (more) gemm_store(smem + ((c + 1) & 1) * kStage, ra, rb);
+            __syncthreads();
+        }
+        // h = act(z + bh) into the tile image: C/D map row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col = lane & 31
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                const int col = wave * 64 + ct * 32 + (lane & 31);
+                const float bc = ct ? bh1 : bh0;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    smem[row * kS + col] = act_f<ACT>(acc[rt][ct][r] + bc, slope);
+                }
+            }
+        epi.tile(smem, s_part, s_dh, in, tile, batch, W, bias, dz, ld, ent_coef, vf_coef);
+    }
+    epi.finish(p_dw, p_dbh, p_dbo, p_loss, loss_width);
 }
 
 }  // namespace
@@ -381,29 +561,61 @@ XPA_API int64_t xpa_head_fused_num_partials(int64_t batch) {
 }
 
 namespace {
-#define XPA_HEAD_ARGS(a) a.batch, a.K, a.ld, a.z, a.W, a.bias, a.slope, a.logstd, a.idx, a.n_rows, a.act, a.old_logp, a.adv, a.ret, a.adv_partials, a.n_adv_partials, a.clip_range, a.ent_coef, a.vf_coef, a.dz, a.p_dw, a.p_dbh, a.p_dbo, a.p_loss, a.loss_width
-template <int MODE, int ALGO>
-void launch_head(const HeadArgs &a, int act_code, hipStream_t s) {
+#define XPA_HEAD_ARGS(a) a.batch, a.K, a.ld, a.z, a.ldx, a.Wh, a.bh, a.W, a.bias, a.slope, a.logstd, a.idx, a.n_rows, a.act, a.old_logp, a.adv, a.ret, a.adv_partials, a.n_adv_partials, a.clip_range, a.ent_coef, a.vf_coef, a.dz, a.p_dw, a.p_dbh, a.p_dbo, a.p_loss, a.loss_width
+template <bool GEMM, int MODE, int ALGO, int ACT, int KMAX>
+void launch_one(const HeadArgs &a, hipStream_t s) {
     const dim3 grid((unsigned)xpa_head_fused_num_partials(a.batch)), block(256);
-    if constexpr (MODE == 2) {
-        if (act_code == 0) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 0, 1>), grid, block, 0, s, XPA_HEAD_ARGS(a));
-        else if (act_code == 1) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 1, 1>), grid, block, 0, s, XPA_HEAD_ARGS(a));
-        else hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 2, 1>), grid, block, 0, s, XPA_HEAD_ARGS(a));
-    } else if (a.K <= 4) {  // KMAX = the smallest of 4 / 6 / 8 >= K (fewer live registers and FMAs)
-        if (act_code == 0) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 0, 4>), grid, block, 0, s, XPA_HEAD_ARGS(a));
-        else if (act_code == 1) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 1, 4>), grid, block, 0, s, XPA_HEAD_ARGS(a));
-        else hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 2, 4>), grid, block, 0, s, XPA_HEAD_ARGS(a));
-    } else if (a.K <= 6) {
-        if (act_code == 0) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 0, 6>), grid, block, 0, s, XPA_HEAD_ARGS(a));
-        else if (act_code == 1) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 1, 6>), grid, block, 0, s, XPA_HEAD_ARGS(a));
-        else hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 2, 6>), grid, block, 0, s, XPA_HEAD_ARGS(a));
-    } else {
-        if (act_code == 0) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 0, 8>), grid, block, 0, s, XPA_HEAD_ARGS(a));
-        else if (act_code == 1) hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 1, 8>), grid, block, 0, s, XPA_HEAD_ARGS(a));
-        else hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, 2, 8>), grid, block, 0, s, XPA_HEAD_ARGS(a));
-    }
+    if constexpr (GEMM)
+        hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX>), grid, block, 0, s, XPA_HEAD_ARGS(a));
+    else
+        hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, ACT, KMAX>), grid, block, 0, s, XPA_HEAD_ARGS(a));
+}
+
+template <bool GEMM, int MODE, int ALGO, int KMAX>
+void launch_act(const HeadArgs &a, int act_code, hipStream_t s) {
+    if (act_code == 0) launch_one<GEMM, MODE, ALGO, 0, KMAX>(a, s);
+    else if (act_code == 1) launch_one<GEMM, MODE, ALGO, 1, KMAX>(a, s);
+    else launch_one<GEMM, MODE, ALGO, 2, KMAX>(a, s);
+}
+
+template <bool GEMM, int MODE, int ALGO>
+void launch_head(const HeadArgs &a, int act_code, hipStream_t s) {
+    if constexpr (MODE == 2) launch_act<GEMM, MODE, ALGO, 1>(a, act_code, s);
+    else if (a.K <= 4) launch_act<GEMM, MODE, ALGO, 4>(a, act_code, s);  // KMAX = smallest of 4 / 6 / 8 >= K
+    else if (a.K <= 6) launch_act<GEMM, MODE, ALGO, 6>(a, act_code, s);
+    else launch_act<GEMM, MODE, ALGO, 8>(a, act_code, s);
 }
 #undef XPA_HEAD_ARGS
+
+template <bool GEMM>
+int actor_entry(int algo, int dist, int act_code, HeadArgs &a, hipStream_t s) {
+    if (dist == XPA_DIST_GAUSSIAN) {
+        if (algo == XPA_ALGO_PPO) launch_head<GEMM, 0, 0>(a, act_code, s);
+        else launch_head<GEMM, 0, 1>(a, act_code, s);
+    } else {
+        if (algo == XPA_ALGO_PPO) launch_head<GEMM, 1, 0>(a, act_code, s);
+        else launch_head<GEMM, 1, 1>(a, act_code, s);
+    }
+    return xpa_launch_status();
+}
+
+int check_actor(int algo, int dist, int act_code, int64_t batch, int64_t act_dim, int64_t hidden, const float *w,
+                const float *b, const float *logstd, int64_t n_rows, const int64_t *idx, const float *act,
+                const float *old_logp, const float *adv, const float *dz, const float *partial_dw,
+                const float *partial_db_hidden, const float *partial_db_out, const float *loss_partials,
+                int64_t loss_width) {
+    if (batch <= 0 || hidden != kH || act_dim < 1 || act_dim > 8 || act_code < 0 || act_code > 2 || !w || !b ||
+        !act || !adv || !dz || !partial_dw || !partial_db_hidden || !partial_db_out || !loss_partials ||
+        loss_width < kPartBase + act_dim || n_rows <= 0 || (!idx && n_rows < batch))
+        return (int)hipErrorInvalidValue;
+    if ((algo != XPA_ALGO_PPO && algo != XPA_ALGO_A2C) || (dist != XPA_DIST_GAUSSIAN && dist != XPA_DIST_CATEGORICAL))
+        return (int)hipErrorInvalidValue;
+    if ((dist == XPA_DIST_GAUSSIAN && !logstd) || (algo == XPA_ALGO_PPO && !old_logp) ||
+        (dist == XPA_DIST_CATEGORICAL && act_dim < 2))
+        return (int)hipErrorInvalidValue;
+    if ((uintptr_t)w % 16) return (int)hipErrorInvalidValue;
+    return 0;
+}
 }  // namespace
 
 XPA_API int xpa_head_fused_actor(int algo, int dist, int act_code, int64_t batch, int64_t act_dim, int64_t hidden,
@@ -413,31 +625,17 @@ XPA_API int xpa_head_fused_actor(int algo, int dist, int act_code, int64_t batch
                                  float clip_range, float ent_coef, float *dz, float *partial_dw,
                                  float *partial_db_hidden, float *partial_db_out, float *loss_partials,
                                  int64_t loss_width, xpa_stream_t stream) {
-    if (batch <= 0 || hidden != kH || act_dim < 1 || act_dim > 8 || act_code < 0 || act_code > 2 || !z || !w || !b ||
-        !act || !adv || !dz || !partial_dw || !partial_db_hidden || !partial_db_out || !loss_partials ||
-        loss_width < kPartBase + act_dim || n_rows <= 0 || (!idx && n_rows < batch))
-        return (int)hipErrorInvalidValue;
-    if ((algo != XPA_ALGO_PPO && algo != XPA_ALGO_A2C) || (dist != XPA_DIST_GAUSSIAN && dist != XPA_DIST_CATEGORICAL))
-        return (int)hipErrorInvalidValue;
-    if ((dist == XPA_DIST_GAUSSIAN && !logstd) || (algo == XPA_ALGO_PPO && !old_logp) ||
-        (dist == XPA_DIST_CATEGORICAL && act_dim < 2))
-        return (int)hipErrorInvalidValue;
-    if (((uintptr_t)z | (uintptr_t)w) % 16 || ld < kH || ld % 4) return (int)hipErrorInvalidValue;
+    int rc = check_actor(algo, dist, act_code, batch, act_dim, hidden, w, b, logstd, n_rows, idx, act, old_logp, adv, dz,
+                         partial_dw, partial_db_hidden, partial_db_out, loss_partials, loss_width);
+    if (rc) return rc;
+    if (!z || (uintptr_t)z % 16 || ld < kH || ld % 4) return (int)hipErrorInvalidValue;
     HeadArgs a{};
-    a.batch = batch; a.K = (int)act_dim; a.ld = ld; a.z = z; a.W = w; a.bias = b; a.slope = slope; a.logstd = logstd;
-    a.idx = idx; a.n_rows = n_rows; a.act = act; a.old_logp = old_logp; a.adv = adv; a.ret = nullptr;
-    a.adv_partials = adv_partials; a.n_adv_partials = n_adv_partials; a.clip_range = clip_range;
+    a.batch = batch; a.K = (int)act_dim; a.ld = ld; a.z = z; a.ldx = ld; a.W = w; a.bias = b; a.slope = slope;
+    a.logstd = logstd; a.idx = idx; a.n_rows = n_rows; a.act = act; a.old_logp = old_logp; a.adv = adv;
+    a.ret = nullptr; a.adv_partials = adv_partials; a.n_adv_partials = n_adv_partials; a.clip_range = clip_range;
     a.ent_coef = ent_coef; a.vf_coef = 0.f; a.dz = dz; a.p_dw = partial_dw; a.p_dbh = partial_db_hidden;
     a.p_dbo = partial_db_out; a.p_loss = loss_partials; a.loss_width = (int)loss_width;
-    hipStream_t s = (hipStream_t)stream;
-    if (dist == XPA_DIST_GAUSSIAN) {
-        if (algo == XPA_ALGO_PPO) launch_head<0, 0>(a, act_code, s);
-        else launch_head<0, 1>(a, act_code, s);
-    } else {
-        if (algo == XPA_ALGO_PPO) launch_head<1, 0>(a, act_code, s);
-        else launch_head<1, 1>(a, act_code, s);
-    }
-    return xpa_launch_status();
+    return actor_entry<false>(algo, dist, act_code, a, (hipStream_t)stream);
 }
 
 XPA_API int xpa_head_fused_critic(int act_code, int64_t batch, int64_t hidden, int64_t ld, const float *z, const float *w,
@@ -451,9 +649,52 @@ XPA_API int xpa_head_fused_critic(int act_code, int64_t batch, int64_t hidden, i
         return (int)hipErrorInvalidValue;
     if (((uintptr_t)z | (uintptr_t)w) % 16 || ld < kH || ld % 4) return (int)hipErrorInvalidValue;
     HeadArgs a{};
-    a.batch = batch; a.K = 1; a.ld = ld; a.z = z; a.W = w; a.bias = b; a.slope = slope; a.idx = idx; a.n_rows = n_rows;
-    a.ret = ret; a.vf_coef = vf_coef; a.dz = dz; a.p_dw = partial_dw; a.p_dbh = partial_db_hidden;
+    a.batch = batch; a.K = 1; a.ld = ld; a.z = z; a.ldx = ld; a.W = w; a.bias = b; a.slope = slope; a.idx = idx;
+    a.n_rows = n_rows; a.ret = ret; a.vf_coef = vf_coef; a.dz = dz; a.p_dw = partial_dw; a.p_dbh = partial_db_hidden;
     a.p_dbo = partial_db_out; a.p_loss = loss_partials; a.loss_width = (int)loss_width;
-    launch_head<2, 0>(a, act_code, (hipStream_t)stream);
+    launch_head<false, 2, 0>(a, act_code, (hipStream_t)stream);
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_head_gemm_actor(int algo, int dist, int act_code, int64_t batch, int64_t act_dim, int64_t hidden,
+                                const float *x, int64_t ldx, const float *w_hidden, const float *b_hidden, int64_t ld_dz,
+                                const float *w, const float *b, float slope, const float *logstd, const int64_t *idx,
+                                int64_t n_rows, const float *act, const float *old_logp, const float *adv,
+                                const double *adv_partials, int64_t n_adv_partials, float clip_range, float ent_coef,
+                                float *dz, float *partial_dw, float *partial_db_hidden, float *partial_db_out,
+                                float *loss_partials, int64_t loss_width, xpa_stream_t stream) {
+    int rc = check_actor(algo, dist, act_code, batch, act_dim, hidden, w, b, logstd, n_rows, idx, act, old_logp, adv, dz,
+                         partial_dw, partial_db_hidden, partial_db_out, loss_partials, loss_width);
+    if (rc) return rc;
+    if (!x || !w_hidden || !b_hidden || ((uintptr_t)x | (uintptr_t)w_hidden) % 16 || ldx < kKin || ldx % 4 ||
+        ld_dz < kH)
+        return (int)hipErrorInvalidValue;
+    HeadArgs a{};
+    a.batch = batch; a.K = (int)act_dim; a.ld = ld_dz; a.z = x; a.ldx = ldx; a.Wh = w_hidden; a.bh = b_hidden;
+    a.W = w; a.bias = b; a.slope = slope; a.logstd = logstd; a.idx = idx; a.n_rows = n_rows; a.act = act;
+    a.old_logp = old_logp; a.adv = adv; a.ret = nullptr; a.adv_partials = adv_partials;
+    a.n_adv_partials = n_adv_partials; a.clip_range = clip_range; a.ent_coef = ent_coef; a.vf_coef = 0.f; a.dz = dz;
+    a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
+    a.loss_width = (int)loss_width;
+    return actor_entry<true>(algo, dist, act_code, a, (hipStream_t)stream);
+}
+
+XPA_API int xpa_head_gemm_critic(int act_code, int64_t batch, int64_t hidden, const float *x, int64_t ldx,
+                                 const float *w_hidden, const float *b_hidden, int64_t ld_dz, const float *w,
+                                 const float *b, float slope, const int64_t *idx, int64_t n_rows, const float *ret,
+                                 float vf_coef, float *dz, float *partial_dw, float *partial_db_hidden,
+                                 float *partial_db_out, float *loss_partials, int64_t loss_width, xpa_stream_t stream) {
+    if (batch <= 0 || hidden != kH || act_code < 0 || act_code > 2 || !x || !w_hidden || !b_hidden || !w || !b ||
+        !ret || !dz || !partial_dw || !partial_db_hidden || !partial_db_out || !loss_partials ||
+        loss_width < kPartBase || n_rows <= 0 || (!idx && n_rows < batch))
+        return (int)hipErrorInvalidValue;
+    if (((uintptr_t)x | (uintptr_t)w_hidden | (uintptr_t)w) % 16 || ldx < kKin || ldx % 4 || ld_dz < kH)
+        return (int)hipErrorInvalidValue;
+    HeadArgs a{};
+    a.batch = batch; a.K = 1; a.ld = ld_dz; a.z = x; a.ldx = ldx; a.Wh = w_hidden; a.bh = b_hidden; a.W = w;
+    a.bias = b; a.slope = slope; a.idx = idx; a.n_rows = n_rows; a.ret = ret; a.vf_coef = vf_coef; a.dz = dz;
+    a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
+    a.loss_width = (int)loss_width;
+    launch_head<true, 2, 0>(a, act_code, (hipStream_t)stream);
     return xpa_launch_status();
 }

@@ -109,6 +109,9 @@ class FusedActorCritic:
                 if w is not None and b is not None:
                     n_in = la.in_features
                     self.pair = (w[0].view(2 * ops.HEAD_HIDDEN, n_in), b[0], w[1].view(2 * ops.HEAD_HIDDEN, n_in), b[1])
+        # K16: the paired hidden layers' forward GEMM inside the head kernels (fp32 MFMA), when their
+        # input is 256 wide; z is then never materialised.
+        self.gemm_heads = self.pair is not None and self.actor[0][0].in_features == ops.HEAD_HIDDEN
         n_params = sum(1 for _ in policy.parameters())
         n_cov = 2 * (len(self.rep) + len(self.actor) + len(self.critic)) + (0 if self.discrete else 1)
         if n_params != n_cov:
@@ -209,6 +212,8 @@ class FusedActorCritic:
         """Forward up to the heads' last hidden pre-activations (K12 does the rest)."""
         rep_outs = self._rep_forward(x)
         s = rep_outs[-1] if rep_outs else x
+        if self.pair is not None and self.gemm_heads:   # K16 forms z inside the head kernels
+            return (x, rep_outs, s, (([], s, None), ([], s, None)))
         if self.pair is not None:   # one GEMM for both hidden layers: [B, 512] = actor | critic
             H = ops.HEAD_HIDDEN
             ev = ops.TIMER.start("gemm_pair")
@@ -229,7 +234,7 @@ class FusedActorCritic:
         """K12 loss + head backward, then the hidden / trunk GEMMs.  Writes every parameter gradient;
         returns the loss-scalars device tensor (ops.OUT_KEYS)."""
         x, rep_outs, s, ((a_outs, a_xh, z_a), (c_outs, c_xh, z_c)) = ctx
-        B = z_a.shape[0]
+        B = s.shape[0]
         lin_ao, _, _ = self.actor[-1]
         lin_ah, a_code, a_slope = self.actor[-2]
         lin_co, _, _ = self.critic[-1]
@@ -237,7 +242,10 @@ class FusedActorCritic:
         K = lin_ao.out_features
         paired = self.pair is not None
         if self._hws is None or self._hws.batch != B:
-            self._hws = ops.HeadWorkspace(B, K, z_a.device, paired=paired)
+            self._hws = ops.HeadWorkspace(B, K, s.device, paired=paired)
+        gemm = None
+        if z_a is None:   # K16
+            gemm = (s, (lin_ah.weight, lin_ah.bias), (lin_ch.weight, lin_ch.bias))
         grads = {"w_actor": lin_ao.weight.grad, "b_actor": lin_ao.bias.grad, "bh_actor": lin_ah.bias.grad,
                  "w_critic": lin_co.weight.grad, "b_critic": lin_co.bias.grad, "bh_critic": lin_ch.bias.grad}
         if self.logstd is not None:
@@ -246,7 +254,7 @@ class FusedActorCritic:
                                               z_c, lin_co.weight, lin_co.bias, (c_code, c_slope), self.logstd, act,
                                               adv, ret, old_logp=old_logp, idx=idx, adv_partials=adv_partials,
                                               clip_range=clip_range, vf_coef=vf_coef, ent_coef=ent_coef, grads=grads,
-                                              colsum_queue=self._cq)
+                                              colsum_queue=self._cq, gemm=gemm)
         have_rep = len(self.rep) > 0
         if paired:   # dW of both hidden layers and dX (K = 512, no accumulate pass) as single GEMMs
             dz = self._hws.dz_pair
@@ -254,14 +262,14 @@ class FusedActorCritic:
             if have_rep:
                 self._chain_backward(self.rep, [x] + rep_outs[:-1], rep_outs, torch.mm(dz, self.pair[0]),
                                      need_dx=False, thin_first=self.thin0)
-            self._cq.flush(z_a.device)   # every deferred column-sum finalize in one launch
+            self._cq.flush(s.device)   # every deferred column-sum finalize in one launch
             return scalars
         ds = self._from_dz(self.actor[:-1], [s] + a_outs, a_outs, dz_a, need_dx=have_rep)
         ds = self._from_dz(self.critic[:-1], [s] + c_outs, c_outs, dz_c, need_dx=have_rep, accumulate=ds)
         if have_rep:
             r_in = [x] + rep_outs[:-1]
             self._chain_backward(self.rep, r_in, rep_outs, ds, need_dx=False, thin_first=self.thin0)
-        self._cq.flush(z_a.device)
+        self._cq.flush(s.device)
         return scalars
 
     def _from_dz(self, layers, inputs, outs, dz, need_dx, accumulate=None):

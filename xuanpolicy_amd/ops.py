@@ -354,26 +354,37 @@ class ColsumQueue:
 
 def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, w_critic, b_critic, act_critic,
                 logstd, act, adv, ret, old_logp=None, idx=None, adv_partials=None, clip_range=0.2, vf_coef=0.25,
-                ent_coef=0.0, grads=None, colsum_queue=None):
+                ent_coef=0.0, grads=None, colsum_queue=None, gemm=None):
     """K12 actor + critic heads, loss finalize and the column-sum finalizes.
 
     z_*: hidden pre-activations [B, 256] (unit column stride; row stride = the workspace dz row stride,
-    e.g. the halves of a [B, 512] actor|critic pre-activation with a paired workspace); w_*/b_*: output layer (K x 256 / 1 x 256); act_*: (code, slope)
+    e.g. the halves of a [B, 512] actor|critic pre-activation with a paired workspace); w_*/b_*: output layer
+    gemm = (x [B, 256], (w_h_actor, b_h_actor), (w_h_critic, b_h_critic)): K16 — the hidden layers' GEMMs
+    run inside the head kernels on the matrix cores and z_actor / z_critic are not used (pass None). (K x 256 / 1 x 256); act_*: (code, slope)
     of the hidden activation.  colsum_queue: an ops.ColsumQueue to defer the column-sum finalizes into
     (flushed by the caller), else they run here.  grads: dict with the gradient views to write — 'w_actor', 'b_actor',
     'bh_actor', 'w_critic', 'b_critic', 'bh_critic', 'logstd' (gaussian).  Returns (scalars, dz_actor,
     dz_critic)."""
     if algo not in ALGO or dist not in DIST:
         raise ValueError("algo must be ppo|a2c and dist gaussian|categorical")
-    B, H = z_actor.shape
+    H = HEAD_HIDDEN
+    B = gemm[0].shape[0] if gemm is not None else z_actor.shape[0]
     K = w_actor.shape[0]
-    if H != HEAD_HIDDEN or ws.batch != B or ws.k != K:
-        raise ValueError("fused heads need hidden width %d and a matching workspace" % HEAD_HIDDEN)
+    if ws.batch != B or ws.k != K:
+        raise ValueError("fused heads need a matching workspace")
     ld = ws.dz_actor.stride(0)
-    for name, zz in (("z_actor", z_actor), ("z_critic", z_critic)):
-        _req(zz, name, torch.float32, contiguous=False)
-        if tuple(zz.shape) != (B, H) or zz.stride() != (ld, 1):
-            raise ValueError("%s must be [%d, %d] with row stride %d" % (name, B, H, ld))
+    if gemm is not None:
+        x, (wha, bha), (whc, bhc) = gemm
+        _req(x, "x", torch.float32, contiguous=False)
+        if tuple(x.shape) != (B, H) or x.stride(1) != 1:
+            raise ValueError("x must be [%d, %d] with unit column stride" % (B, H))
+        for name, w_ in (("w_h_actor", wha), ("w_h_critic", whc)):
+            _req(w_, name, torch.float32, (H, H))
+    else:
+        for name, zz in (("z_actor", z_actor), ("z_critic", z_critic)):
+            _req(zz, name, torch.float32, contiguous=False)
+            if tuple(zz.shape) != (B, H) or zz.stride() != (ld, 1):
+                raise ValueError("%s must be [%d, %d] with row stride %d" % (name, B, H, ld))
     _req(w_actor, "w_actor", torch.float32, (K, H))
     _req(w_critic, "w_critic", torch.float32, (1, H))
     if idx is not None:
@@ -388,26 +399,39 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
         _req(old_logp, "old_logp", torch.float32, (rows,))
     if adv_partials is not None:
         _req(adv_partials, "adv_partials", torch.float64)
-    s = _stream(z_actor.device)
+    dev = w_actor.device
+    s = _stream(dev)
     L = lib()
     W = ws.loss_partials.shape[1]
     ev = TIMER.start("heads")
-    rc = L.xpa_head_fused_actor(ALGO[algo], DIST[dist], act_actor[0], B, K, H, ld, _p(z_actor), _p(w_actor), _p(b_actor),
-                                float(act_actor[1]), _p(logstd) if dist == "gaussian" else None, _p(idx), rows, _p(act),
-                                _p(old_logp) if algo == "ppo" else None, _p(adv), _p(adv_partials),
-                                adv_partials.shape[0] if adv_partials is not None else 0, float(clip_range),
-                                float(ent_coef), _p(ws.dz_actor), _p(ws.p_dw_actor), _p(ws.p_dbh_actor),
-                                _p(ws.p_dbo_actor), _p(ws.loss_partials), W, s)
-    _lib.check(rc, "xpa_head_fused_actor")
-    rc = L.xpa_head_fused_critic(act_critic[0], B, H, ld, _p(z_critic), _p(w_critic), _p(b_critic), float(act_critic[1]),
-                                 _p(idx), rows, _p(ret), float(vf_coef), _p(ws.dz_critic), _p(ws.p_dw_critic),
-                                 _p(ws.p_dbh_critic), _p(ws.p_dbo_critic), _p(ws.loss_partials), W, s)
+    n_adv = adv_partials.shape[0] if adv_partials is not None else 0
+    p_logstd = _p(logstd) if dist == "gaussian" else None
+    p_old = _p(old_logp) if algo == "ppo" else None
+    if gemm is not None:
+        _lib.check(L.xpa_head_gemm_actor(ALGO[algo], DIST[dist], act_actor[0], B, K, H, _p(x), x.stride(0), _p(wha),
+                                         _p(bha), ld, _p(w_actor), _p(b_actor), float(act_actor[1]), p_logstd, _p(idx),
+                                         rows, _p(act), p_old, _p(adv), _p(adv_partials), n_adv, float(clip_range),
+                                         float(ent_coef), _p(ws.dz_actor), _p(ws.p_dw_actor), _p(ws.p_dbh_actor),
+                                         _p(ws.p_dbo_actor), _p(ws.loss_partials), W, s), "xpa_head_gemm_actor")
+        _lib.check(L.xpa_head_gemm_critic(act_critic[0], B, H, _p(x), x.stride(0), _p(whc), _p(bhc), ld, _p(w_critic),
+                                          _p(b_critic), float(act_critic[1]), _p(idx), rows, _p(ret), float(vf_coef),
+                                          _p(ws.dz_critic), _p(ws.p_dw_critic), _p(ws.p_dbh_critic),
+                                          _p(ws.p_dbo_critic), _p(ws.loss_partials), W, s), "xpa_head_gemm_critic")
+    else:
+        _lib.check(L.xpa_head_fused_actor(ALGO[algo], DIST[dist], act_actor[0], B, K, H, ld, _p(z_actor), _p(w_actor),
+                                          _p(b_actor), float(act_actor[1]), p_logstd, _p(idx), rows, _p(act), p_old,
+                                          _p(adv), _p(adv_partials), n_adv, float(clip_range), float(ent_coef),
+                                          _p(ws.dz_actor), _p(ws.p_dw_actor), _p(ws.p_dbh_actor), _p(ws.p_dbo_actor),
+                                          _p(ws.loss_partials), W, s), "xpa_head_fused_actor")
+        _lib.check(L.xpa_head_fused_critic(act_critic[0], B, H, ld, _p(z_critic), _p(w_critic), _p(b_critic),
+                                           float(act_critic[1]), _p(idx), rows, _p(ret), float(vf_coef),
+                                           _p(ws.dz_critic), _p(ws.p_dw_critic), _p(ws.p_dbh_critic),
+                                           _p(ws.p_dbo_critic), _p(ws.loss_partials), W, s), "xpa_head_fused_critic")
     TIMER.stop("heads", ev)
-    _lib.check(rc, "xpa_head_fused_critic")
     g = grads or {}
     d_logstd = g.get("logstd")
     if dist == "gaussian" and d_logstd is None:
-        d_logstd = torch.empty((K,), dtype=torch.float32, device=z_actor.device)
+        d_logstd = torch.empty((K,), dtype=torch.float32, device=dev)
     _lib.check(L.xpa_policy_loss_finalize(ALGO[algo], DIST[dist], B, K, _p(ws.loss_partials), ws.G, float(vf_coef),
                                           float(ent_coef), _p(ws.scalars), _p(d_logstd), s), "xpa_policy_loss_finalize")
     queue = colsum_queue if colsum_queue is not None else ColsumQueue()
@@ -416,7 +440,7 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
         if key in g:
             queue.add(part, g[key])
     if colsum_queue is None:
-        queue.flush(z_actor.device)
+        queue.flush(dev)
     return ws.scalars, ws.dz_actor, ws.dz_critic
 
 
