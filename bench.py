@@ -348,6 +348,7 @@ def main():
     # Back-to-back replay of the same GAE launch on the agent's live buffers (after the timed region):
     # per-launch time without the event/dispatch overhead a single bracketed launch carries.
     replay_us = None if args.no_kernel_timing else gae_graph_replay_us(mem)
+    floor_us = None if args.no_kernel_timing else ops.dispatch_floor_us(device)
     mid_trunc = int(((mem.closed[:, :-1] > 0) & (mem.terminals[:, :-1] == 0)).sum())
     B = N * T // args.n_minibatch
     result = None
@@ -369,7 +370,11 @@ def main():
                         "timing": "HIP events recorded by each in-loop dispatch at the kernel's own start and end "
                                   "(hipExtLaunchKernel), on the launch stream, inside the timed region",
                         "graph_replay_us": round(replay_us, 3) if replay_us else None,
-                        "graph_replay_achieved": round(gb / replay_us / 1e3, 1) if replay_us else None}
+                        "graph_replay_achieved": round(gb / replay_us / 1e3, 1) if replay_us else None,
+                        # An empty one-wave launch on the same clock: no kernel of this launch's bytes can
+                        # measure above gb / floor (tools/gae_floor.hip).
+                        "dispatch_floor_us": round(floor_us, 3) if floor_us else None,
+                        "frac_ceiling_at_floor": round(gb / floor_us / 1e3 / HBM_PEAK_GBS, 4) if floor_us else None}
         loss_kernel = None
         if loss_ms:
             lb = loss_bytes_gauss(B, args.act_dim)
@@ -378,7 +383,16 @@ def main():
                            "frac": round(lb / loss_ms / 1e6 / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": int(lb),
                            "launches": len(ops.TIMER.events.get("loss", []))}
         update_kernels = {}
-        if heads_ms:
+        if heads_ms and getattr(agent.learner._fused_mlp(), "gemm_heads", False):
+            fl = pair_gemm_flops(B, args.hidden, args.hidden)
+            update_kernels["heads"] = {
+                "kernel": "xpa_head_gemm_actor + xpa_head_gemm_critic (K16: hidden-layer GEMM on fp32 MFMA "
+                          "+ fused head epilogue, per minibatch)", "bound": "mfma",
+                "avg_us": round(heads_ms * 1e3, 3), "flops": fl, "achieved": round(fl / heads_ms / 1e9, 1),
+                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(fl / heads_ms / 1e9 / FP32_MFMA_PEAK_TFLOPS, 4), "launches": ops.TIMER.count("heads"),
+                "timing": "event pairs on the launch stream in one extra iteration after the timed region"}
+        elif heads_ms:
             hb = heads_bytes(B, args.act_dim, args.hidden)
             update_kernels["heads"] = {
                 "kernel": "xpa_head_fused_actor + xpa_head_fused_critic (K12, per minibatch)", "bound": "hbm",

@@ -59,7 +59,8 @@ int xpa_abi_version(void);
  * a2c_agent.py:66-98).  closed[n,t] != 0 marks the last step of a path closed with bootstrap
  * value boot[n,t]; positions after a row's last closure are not written (as in the reference).
  * use_gae = 0 selects the discount_cumsum branch (memory_tools.py:222-225).
- * Reads rew/val/term (f32), closed (u8), boot (f32, only where closed); writes adv, ret (f32). */
+ * Reads rew/val/term (f32), closed (u8), boot (f32 [n_envs, horizon]: streamed densely, its values
+ * used only where closed); writes adv, ret (f32). */
 int xpa_gae_scan(const float *rew, const float *val, const float *term, const uint8_t *closed,
                  const float *boot, int64_t n_envs, int64_t horizon, float gamma, float gae_lambda,
                  int use_gae, float *adv, float *ret, xpa_stream_t stream);
@@ -69,6 +70,10 @@ int xpa_gae_scan(const float *rew, const float *val, const float *term, const ui
 int xpa_gae_scan_timed(const float *rew, const float *val, const float *term, const uint8_t *closed,
                        const float *boot, int64_t n_envs, int64_t horizon, float gamma, float gae_lambda,
                        int use_gae, float *adv, float *ret, void *ev_start, void *ev_stop, xpa_stream_t stream);
+
+/* Measurement aid (no reference counterpart): an empty one-wave kernel launched with the same
+ * dispatch-attached events as xpa_gae_scan_timed — the fixed per-launch cost of that clock. */
+int xpa_dispatch_floor_timed(void *ev_start, void *ev_stop, xpa_stream_t stream);
 
 /* K4 — minibatch gather.  Replaces the fancy-index gather of DummyOnPolicyBuffer.sample
  * (memory_tools.py:231-240) for the observation rows (the rest is read through `idx` by the loss

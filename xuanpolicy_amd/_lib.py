@@ -29,6 +29,7 @@ SIGNATURES = {
     "xpa_gae_scan": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, ctypes.c_int, c_p, c_p, c_p]),
     "xpa_gae_scan_timed": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, ctypes.c_int, c_p, c_p,
                                           c_p, c_p, c_p]),
+    "xpa_dispatch_floor_timed": (ctypes.c_int, [c_p, c_p, c_p]),
     "xpa_random_permutation": (ctypes.c_int, [c_i64, c_u32, c_u32, c_p, c_p]),
     "xpa_gather_num_partials": (c_i64, [c_i64]),
     "xpa_gather_minibatch": (ctypes.c_int, [c_p, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p]),

@@ -22,8 +22,11 @@
 //     its 4 outputs; rows longer than 64*VEC loop over chunks from the end with a register carry;
 //   * the boot value is read only where closed (sparse); positions after the last closure of a row
 //     (an open path) are not written, exactly like the reference.
+//   * boot is streamed densely alongside r, v, d (vector path): reading it only where closed made a
+//     dependent second memory round trip in every wave (each row closes at its last step at rollout
+//     end) — 0.9-2.1 us of a 5-7 us launch at 4096 x 128 (tools/gae_floor.hip, r01).
 // Algorithmic bytes: 20 B per (env, step) (r, v, d read; adv, ret written); this
-// kernel moves 21 B (+1 B closure flag) plus 4 B per closed path.
+// kernel moves 25 B (+1 B closure flag, +4 B boot).
 #include <stdlib.h>
 
 #include <hip/hip_ext.h>
@@ -76,7 +79,7 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float *__restrict__
 
     for (int c = nchunks - 1; c >= 0; --c) {
         const int t0 = c * C + sl * VEC;
-        float r[VEC], v[VEC], d[VEC];
+        float r[VEC], v[VEC], d[VEC], bt[VEC];
         int cl[VEC];
         const bool full = row_ok && (t0 + VEC <= T);
         if (VEC == 4 && full) {
@@ -84,6 +87,10 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float *__restrict__
             const float4 v4 = ld4<NT>(val + base + t0);
             const float4 d4 = ld4<NT>(term + base + t0);
             const uint32_t c4 = *reinterpret_cast<const uint32_t *>(closed + base + t0);  // one dword, 4 flags
+            // boot is read densely with the other streams: +4 B per step, but no dependent second
+            // round trip after the flags land (every row closes at its last step at rollout end).
+            const float4 q4 = ld4<NT>(boot + base + t0);
+            bt[0] = q4.x; bt[1] = q4.y; bt[2] = q4.z; bt[3] = q4.w;
             r[0] = r4.x; r[1] = r4.y; r[2] = r4.z; r[3] = r4.w;
             v[0] = v4.x; v[1] = v4.y; v[2] = v4.z; v[3] = v4.w;
             d[0] = d4.x; d[1] = d4.y; d[2] = d4.z; d[3] = d4.w;
@@ -97,6 +104,7 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float *__restrict__
                 v[e] = ok ? val[base + t] : 0.f;
                 d[e] = ok ? term[base + t] : 0.f;
                 cl[e] = ok ? (int)closed[base + t] : 0;
+                bt[e] = cl[e] ? boot[base + t] : 0.f;
             }
         }
         // v_{t+1} of this lane's last element: the next lane's first v, or the later chunk's.
@@ -109,14 +117,13 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float *__restrict__
             const int t = t0 + e;
             const bool ok = row_ok && t < T;
             const float vnext = (e < VEC - 1) ? v[e + 1] : vn_lane;
-            const float bt = cl[e] ? boot[base + t] : 0.f;
-            const float nv = cl[e] ? bt : vnext;
+            const float nv = cl[e] ? bt[e] : vnext;
             const float nd = 1.0f - d[e];
             if (use_gae) {
                 b[e] = r[e] + gamma * nd * nv - v[e];
                 a[e] = cl[e] ? 0.f : gl * nd;
             } else {
-                b[e] = r[e] + (cl[e] ? gamma * bt : 0.f);
+                b[e] = r[e] + (cl[e] ? gamma * bt[e] : 0.f);
                 a[e] = cl[e] ? 0.f : gamma;
                 adv_direct[e] = r[e] + gamma * nv - v[e];
             }
@@ -190,6 +197,22 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float *__restrict__
 XPA_API int xpa_abi_version(void) { return XPA_ABI_VERSION; }
 
 namespace {
+__global__ __launch_bounds__(64) void dispatch_floor_kernel(float *p) {
+    if (p) p[threadIdx.x] = 0.f;
+}
+}  // namespace
+
+// An empty one-wave launch timed by the same dispatch-attached events as xpa_gae_scan_timed: the fixed
+// cost (dispatch, cache fences, timestamps) that every launch carries on this clock, whatever its grid
+// (flat 4.1-4.2 us for 1 x 64 up to 2048 x 1024 threads on MI355X, tools/gae_floor.hip, r01).
+XPA_API int xpa_dispatch_floor_timed(void *ev_start, void *ev_stop, xpa_stream_t stream) {
+    if (!ev_start || !ev_stop) return (int)hipErrorInvalidValue;
+    hipExtLaunchKernelGGL(dispatch_floor_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
+                          (hipEvent_t)ev_stop, 0, (float *)nullptr);
+    return xpa_launch_status();
+}
+
+namespace {
 template <int VEC, int NT>
 void launch_gae(dim3 grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1, const float *rew, const float *val,
                 const float *term, const uint8_t *closed, const float *boot, int64_t n_envs, int T, int seg_log2,
@@ -219,7 +242,8 @@ XPA_API int xpa_gae_scan_timed(const float *rew, const float *val, const float *
     if (!rew || !val || !term || !closed || !boot || !adv || !ret) return (int)hipErrorInvalidValue;
     const int T = (int)horizon;
     const bool vec4 = (T % 4 == 0) && ((uintptr_t)rew % 16 == 0) && ((uintptr_t)val % 16 == 0) &&
-                      ((uintptr_t)term % 16 == 0) && ((uintptr_t)adv % 16 == 0) && ((uintptr_t)ret % 16 == 0) &&
+                      ((uintptr_t)term % 16 == 0) && ((uintptr_t)boot % 16 == 0) && ((uintptr_t)adv % 16 == 0) &&
+                      ((uintptr_t)ret % 16 == 0) &&
                       ((uintptr_t)closed % 4 == 0);
     const int VEC = vec4 ? 4 : 1;
     int per_lane = (T + VEC - 1) / VEC;

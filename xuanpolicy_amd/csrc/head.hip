@@ -15,6 +15,10 @@
 // HBM: reads z (4 B/elem), writes dz (4 B/elem): 2 KiB per row at H = 256, plus the per-row inputs.
 #include "xpa_common.h"
 
+#ifndef XPA_HEAD_PROBE  // tools/head_probe.py builds variants with parts compiled out
+#define XPA_HEAD_PROBE 0
+#endif
+
 namespace {
 
 constexpr int kWaves = 4;
@@ -525,16 +529,22 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
                 for (int r = 0; r < 16; ++r) acc[rt][ct][r] = 0.f;
         float4 ra, rb[4];
         __syncthreads();  // the previous tile's epilogue is done with smem
+#if XPA_HEAD_PROBE != 2  // tools/head_probe.py: 2 = epilogue alone
         gemm_load(z, ldx, Wh, r0, batch, 0, ra, rb);
         gemm_store(smem, ra, rb);
         __syncthreads();
         for (int c = 0; c < kKin / kKC; ++c) {
             const bool more = c + 1 < kKin / kKC;
             if (more) gemm_load(z, ldx, Wh, r0, batch, (c + 1) * kKC, ra, rb);
+#if XPA_HEAD_PROBE != 3  // 3 = operand staging alone (its results kept live)
             gemm_chunk(smem + (c & 1) * kStage, acc, lane, wave);
+#else
+            asm volatile("" ::"v"(ra.x), "v"(rb[0].y));
+#endif
             if (more) gemm_store(smem + ((c + 1) & 1) * kStage, ra, rb);
             __syncthreads();
         }
+#endif
         // h = act(z + bh) into the tile image: C/D map row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col = lane & 31
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
@@ -548,7 +558,12 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
                     smem[row * kS + col] = act_f<ACT>(acc[rt][ct][r] + bc, slope);
                 }
             }
+#if XPA_HEAD_PROBE == 1 || XPA_HEAD_PROBE == 3  // the GEMM alone: keep its result live
+        __syncthreads();
+        if (r0 + (t >> 2) < batch) dz[(r0 + (t >> 2)) * ld + (t & 3)] = smem[(t >> 2) * kS + (t & 3)];
+#else
         epi.tile(smem, s_part, s_dh, in, tile, batch, W, bias, dz, ld, ent_coef, vf_coef);
+#endif
     }
     epi.finish(p_dw, p_dbh, p_dbo, p_loss, loss_width);
 }

@@ -166,6 +166,32 @@ def gae_scan(rew, val, term, closed, boot, gamma, gae_lambda, use_gae=True, adv=
     return adv, ret
 
 
+def dispatch_floor_us(device, reps=50):
+    """Median duration (us) of an empty one-wave launch timed by dispatch-attached events, the clock
+    xpa_gae_scan_timed uses: the fixed cost every launch carries on it (bench.py reports it beside K1)."""
+    rt = TIMER._hip()
+    lib_ = lib()
+    e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
+    for ev in (e0, e1):
+        if rt.hipEventCreate(ctypes.byref(ev)) != 0:
+            raise RuntimeError("hipEventCreate failed")
+    times = []
+    try:
+        for i in range(reps + 3):
+            _lib.check(lib_.xpa_dispatch_floor_timed(e0, e1, _stream(device)), "xpa_dispatch_floor_timed")
+            rt.hipEventSynchronize(e1)
+            ms = ctypes.c_float()
+            if rt.hipEventElapsedTime(ctypes.byref(ms), e0, e1) != 0:
+                raise RuntimeError("hipEventElapsedTime failed")
+            if i >= 3:
+                times.append(ms.value * 1e3)
+    finally:
+        rt.hipEventDestroy(e0)
+        rt.hipEventDestroy(e1)
+    times.sort()
+    return times[len(times) // 2]
+
+
 def random_permutation(n, seed, counter, out=None, device=None):
     """Pseudo-random permutation of [0, n) keyed by (seed, counter) on device (int64 [n])."""
     if out is None:
