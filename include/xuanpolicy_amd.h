@@ -71,6 +71,19 @@ int xpa_gae_scan_timed(const float *rew, const float *val, const float *term, co
                        const float *boot, int64_t n_envs, int64_t horizon, float gamma, float gae_lambda,
                        int use_gae, float *adv, float *ret, void *ev_start, void *ev_stop, xpa_stream_t stream);
 
+/* K1, compact closures: the fused agent's form (non-Atari, at most one mid-buffer truncation per env
+ * per rollout — K8's deferred bootstrap slots).  A row closes at its terminals (term != 0), at step
+ * slot_t[n] (>= 0: the env's truncation) and at its last step; the bootstraps are
+ * vboot[n] (truncation) and vboot[n_envs + n] (last step; 0 when terminal) — the critic values of the
+ * deferred pass.  Fuses xpa_rollout_bootstrap_fixup: writes both bootstraps into boot[n, t] and resets
+ * slot_t[n] = -1, so the buffer ends in the state of fixup + xpa_gae_scan.  Reads exactly the
+ * algorithmic r, v, d (f32) + 12 B per env; no closure-flag or dense boot stream.
+ * ev_start / ev_stop as in xpa_gae_scan_timed (NULL: untimed). */
+int xpa_gae_scan_compact(const float *rew, const float *val, const float *term, int32_t *slot_t,
+                         const float *vboot, int64_t n_envs, int64_t horizon, float gamma, float gae_lambda,
+                         int use_gae, float *adv, float *ret, float *boot, void *ev_start, void *ev_stop,
+                         xpa_stream_t stream);
+
 /* Measurement aid (no reference counterpart): an empty one-wave kernel launched with the same
  * dispatch-attached events as xpa_gae_scan_timed — the fixed per-launch cost of that clock. */
 int xpa_dispatch_floor_timed(void *ev_start, void *ev_stop, xpa_stream_t stream);

@@ -55,7 +55,8 @@ def _random_gae_case(rng, N, T, p_close=0.02, p_term=0.02, close_last=True):
     return rew, val, term, closed, boot
 
 
-@pytest.mark.parametrize("N,T", [(1, 1), (7, 63), (64, 128), (33, 129), (5, 1024), (130, 4), (3, 257), (1000, 128)])
+@pytest.mark.parametrize("N,T", [(1, 1), (7, 63), (64, 128), (33, 129), (5, 1024), (130, 4), (3, 257), (1000, 128),
+                                 (9, 36), (2, 64), (70, 96), (11, 200), (6, 516), (5, 256)])
 @pytest.mark.parametrize("use_gae", [True, False])
 def test_gae_kernel_random_shapes(N, T, use_gae):
     from xuanpolicy_amd import ops
@@ -71,6 +72,50 @@ def test_gae_kernel_random_shapes(N, T, use_gae):
     ops.gae_scan(_d(rew), _d(val), _d(term), _d(closed), _d(boot), 0.99, 0.95, use_gae, adv=adv, ret=ret)
     np.testing.assert_allclose(_h(adv), ref_adv, rtol=1e-5, atol=2e-5)
     np.testing.assert_allclose(_h(ret), ref_ret, rtol=1e-5, atol=2e-5)
+
+
+def _compact_case(rng, N, T, p_term=0.02, p_slot=0.3):
+    rew = rng.normal(0, 1, (N, T)).astype(np.float32)
+    val = rng.normal(0, 1, (N, T)).astype(np.float32)
+    term = (rng.random((N, T)) < p_term).astype(np.float32)
+    term[rng.random(N) < 0.1, -1] = 1.0                        # some rows end on a terminal
+    slot = np.where(rng.random(N) < p_slot, rng.integers(0, max(T - 1, 1), N), -1).astype(np.int32)
+    if T > 1:
+        slot[:: 7] = T - 2                                    # truncation right before the last step
+        term[np.arange(N)[slot >= 0], slot[slot >= 0]] = 0.0  # a truncation slot is not a terminal (K8)
+    vboot = rng.normal(0, 1, 2 * N).astype(np.float32)
+    # the equivalent dense closure record (K8 flags + xpa_rollout_bootstrap_fixup)
+    closed = (term > 0).astype(np.uint8)
+    closed[:, -1] = 1
+    boot = np.zeros((N, T), np.float32)
+    rows = np.nonzero(slot >= 0)[0]
+    closed[rows, slot[rows]] = 1
+    boot[rows, slot[rows]] = vboot[rows]
+    boot[:, -1] = np.where(term[:, -1] > 0, 0.0, vboot[N:])
+    return rew, val, term, slot, vboot, closed, boot
+
+
+@pytest.mark.parametrize("N,T", [(1000, 128), (4096, 128), (33, 36), (5, 516), (7, 130), (3, 20), (11, 256), (2, 1)])
+@pytest.mark.parametrize("use_gae", [True, False])
+def test_gae_compact_matches_fixup_plus_scan(N, T, use_gae):
+    """xpa_gae_scan_compact (the fused agent's form) == xpa_rollout_bootstrap_fixup + xpa_gae_scan ==
+    the oracle, including the boot column it writes and the slot reset."""
+    from xuanpolicy_amd import ops
+    rng = np.random.default_rng(N * 7 + T)
+    rew, val, term, slot, vboot, closed, boot = _compact_case(rng, N, T)
+    ref_adv, ref_ret = cpu_ref.gae_rows(rew, val, term, closed, boot, 0.99, 0.95, use_gae)
+    slot_d = _d(slot)
+    boot_d = torch.zeros(N, T, device=DEV)
+    adv, ret = ops.gae_scan_compact(_d(rew), _d(val), _d(term), slot_d, _d(vboot), 0.99, 0.95, use_gae,
+                                    boot=boot_d)
+    np.testing.assert_allclose(_h(adv), ref_adv, rtol=1e-5, atol=2e-5)
+    np.testing.assert_allclose(_h(ret), ref_ret, rtol=1e-5, atol=2e-5)
+    np.testing.assert_array_equal(_h(boot_d), boot)
+    assert (_h(slot_d) == -1).all()
+    # the dense path on the same record agrees to the bit pattern of the scan order
+    a2, r2 = ops.gae_scan(_d(rew), _d(val), _d(term), _d(closed), _d(boot), 0.99, 0.95, use_gae)
+    np.testing.assert_allclose(_h(adv), _h(a2), rtol=0, atol=1e-6)
+    np.testing.assert_allclose(_h(ret), _h(r2), rtol=0, atol=1e-6)
 
 
 def test_gae_kernel_unaligned_views():

@@ -27,6 +27,8 @@ c_i32, c_i64, c_u32, c_f32, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint3
 SIGNATURES = {
     "xpa_abi_version": (ctypes.c_int, []),
     "xpa_gae_scan": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, ctypes.c_int, c_p, c_p, c_p]),
+    "xpa_gae_scan_compact": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, ctypes.c_int, c_p, c_p,
+                                            c_p, c_p, c_p, c_p]),
     "xpa_gae_scan_timed": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, ctypes.c_int, c_p, c_p,
                                           c_p, c_p, c_p]),
     "xpa_dispatch_floor_timed": (ctypes.c_int, [c_p, c_p, c_p]),

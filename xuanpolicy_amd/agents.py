@@ -312,17 +312,25 @@ class _OnPolicyAgent:
         else:
             with torch.no_grad():
                 v = policy_heads(self.policy, x)[2].contiguous()
-        mem = self.memory
-        ops.bootstrap_fixup(v, self.slot_t, mem.terminals, mem.boot)
         if int(self.slot_overflow.item()):
             raise RuntimeError("an env truncated twice within one rollout; set config.defer_bootstrap = False")
+        return v.reshape(-1)
 
     def _update_phase(self):
         mem = self.memory
-        if self.defer_boot:
-            self._deferred_bootstraps()
         mem.size = self.n_steps
-        mem.compute_advantages()
+        if self.defer_boot:
+            vboot = self._deferred_bootstraps()
+            if not self.atari and not mem._pending:
+                # one launch: the fixup's bootstrap writes fused into the compact-closure GAE scan
+                ops.gae_scan_compact(mem.rewards, mem.values, mem.terminals, self.slot_t, vboot, mem.gamma,
+                                     mem.gae_lam, mem.use_gae, adv=mem._advantages, ret=mem._returns, boot=mem.boot)
+                mem._dirty = False
+            else:
+                ops.bootstrap_fixup(vboot, self.slot_t, mem.terminals, mem.boot)
+                mem.compute_advantages()
+        else:
+            mem.compute_advantages()
         NT, B = self.buffer_size, self.batch_size
         obs_flat = mem.observations.reshape((NT,) + tuple(mem.observations.shape[2:]))
         act_flat = mem.actions.reshape(-1)

@@ -56,13 +56,23 @@ __device__ __forceinline__ void st4(float *p, float4 v) {
     }
 }
 
-template <int VEC, int NT>
+// COMPACT = 1 (the fused agent's rollout with deferred truncation bootstraps, non-Atari): no closure
+// flags and no dense boot stream.  A row closes at its terminals (d != 0), at its one mid-buffer
+// truncation slot_t[row] (K8 records at most one per rollout) and at its last step; the bootstraps are
+// the critic values vboot[row] (truncation slot) and vboot[n_rows + row] (last step, 0 when terminal),
+// loaded once per row next to the r/v/d streams.  The kernel writes those two bootstraps into `boot`
+// (the buffer's state is that of xpa_rollout_bootstrap_fixup + xpa_gae_scan) and resets slot_t.
+// Bytes: exactly the algorithmic 20 B per (env, step) + 12 B per env (+8 B sparse boot writes).
+template <int VEC, int NT, int COMPACT = 0>
 __global__ __launch_bounds__(256) void gae_scan_kernel(const float *__restrict__ rew, const float *__restrict__ val,
                                                        const float *__restrict__ term,
                                                        const uint8_t *__restrict__ closed,
                                                        const float *__restrict__ boot, int64_t n_rows, int T,
                                                        int seg_log2, float gamma, float gl, int use_gae,
-                                                       float *__restrict__ adv, float *__restrict__ ret) {
+                                                       float *__restrict__ adv, float *__restrict__ ret,
+                                                       int *__restrict__ slot_t = nullptr,
+                                                       const float *__restrict__ vboot = nullptr,
+                                                       float *__restrict__ boot_out = nullptr) {
     const int L = 1 << seg_log2;
     const int lane = threadIdx.x & 63;
     const int sl = lane & (L - 1);
@@ -73,6 +83,14 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float *__restrict__
     const int C = L * VEC;
     const int nchunks = (T + C - 1) / C;
 
+    int st = -1;
+    float vs = 0.f, vl = 0.f;
+    if (COMPACT && row_ok) {
+        st = slot_t[row];
+        vs = vboot[row];
+        vl = vboot[n_rows + row];
+    }
+
     float carry = 0.f;   // A (or R) at the first element of the later chunk
     float carry_v = 0.f; // v at that element
     int carry_any = 0;   // a closure exists at or after the later chunk's first element
@@ -82,7 +100,33 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float *__restrict__
         float r[VEC], v[VEC], d[VEC], bt[VEC];
         int cl[VEC];
         const bool full = row_ok && (t0 + VEC <= T);
-        if (VEC == 4 && full) {
+        if (COMPACT && VEC == 4 && full) {
+            const float4 r4 = ld4<NT>(rew + base + t0);
+            const float4 v4 = ld4<NT>(val + base + t0);
+            const float4 d4 = ld4<NT>(term + base + t0);
+            r[0] = r4.x; r[1] = r4.y; r[2] = r4.z; r[3] = r4.w;
+            v[0] = v4.x; v[1] = v4.y; v[2] = v4.z; v[3] = v4.w;
+            d[0] = d4.x; d[1] = d4.y; d[2] = d4.z; d[3] = d4.w;
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+                const int t = t0 + e;
+                const bool lt = (t == T - 1);
+                cl[e] = lt || d[e] != 0.f || t == st;
+                bt[e] = lt ? (d[e] != 0.f ? 0.f : vl) : (t == st ? vs : 0.f);
+            }
+        } else if (COMPACT) {
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+                const int t = t0 + e;
+                const bool ok = row_ok && t < T;
+                r[e] = ok ? rew[base + t] : 0.f;
+                v[e] = ok ? val[base + t] : 0.f;
+                d[e] = ok ? term[base + t] : 0.f;
+                const bool lt = (t == T - 1);
+                cl[e] = ok && (lt || d[e] != 0.f || t == st);
+                bt[e] = lt ? (d[e] != 0.f ? 0.f : vl) : (t == st ? vs : 0.f);
+            }
+        } else if (VEC == 4 && full) {
             const float4 r4 = ld4<NT>(rew + base + t0);
             const float4 v4 = ld4<NT>(val + base + t0);
             const float4 d4 = ld4<NT>(term + base + t0);
@@ -190,8 +234,193 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float *__restrict__
         carry_v = __shfl(v[0], 0, L);
         carry_any = __shfl(any_first, 0, L);
     }
+    if (COMPACT && row_ok && sl == 0) {  // the fixup's writes: the two bootstraps, slot reset
+        if (st >= 0 && st < T - 1) boot_out[base + st] = vs;
+        const float dl = term[base + T - 1];
+        boot_out[base + T - 1] = dl != 0.f ? 0.f : vl;
+        if (st >= 0) slot_t[row] = -1;
+    }
 }
 
+
+// ---- DPP form (T > 32, 16-B aligned, T % 4 == 0: every rollout buffer) --------------------------------
+// The same affine scan with the lane order reversed inside a row segment: lane sl owns the 4 steps
+// starting at c*C + (L-1-sl)*4, so the reverse-in-time scan is a forward scan in lane order and runs
+// on DPP (row_shr:1/2/4/8, row_bcast:15/31 — ALU-latency lane moves) instead of ds_bpermute round
+// trips; the closure "any later" flags come from one ballot, the neighbour values from wave_shr:1.
+// (The ds_bpermute form made the 4096 x 128 launch 1.7 us slower than a copy of its bytes, r01 probe
+// tools/gae_modes.hip.)
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp_mov(float old, float src) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
+                                                                 __builtin_bit_cast(int, src), CTRL, ROW_MASK, 0xf,
+                                                                 false));
+}
+constexpr int kDppRowShr = 0x110, kDppWaveShr1 = 0x138, kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143;
+
+template <int O, int CTRL, int ROW_MASK>
+__device__ __forceinline__ void dpp_combine(float &LA, float &LB) {
+    const float oA = dpp_mov<CTRL, ROW_MASK>(1.f, LA);  // disabled / out-of-row lanes: the identity map
+    const float oB = dpp_mov<CTRL, ROW_MASK>(0.f, LB);
+    LB = LB + LA * oB;
+    LA = LA * oA;
+}
+
+template <int SEG_LOG2, int COMPACT>
+__global__ __launch_bounds__(256) void gae_dpp_kernel(const float *__restrict__ rew, const float *__restrict__ val,
+                                                      const float *__restrict__ term,
+                                                      const uint8_t *__restrict__ closed,
+                                                      const float *__restrict__ boot, int64_t n_rows, int T,
+                                                      float gamma, float gl, int use_gae, float *__restrict__ adv,
+                                                      float *__restrict__ ret, int *__restrict__ slot_t,
+                                                      const float *__restrict__ vboot, float *__restrict__ boot_out) {
+    constexpr int L = 1 << SEG_LOG2;
+    constexpr int C = 4 * L;
+    const int lane = threadIdx.x & 63;
+    const int sl = lane & (L - 1);
+    const int seg_base = lane & ~(L - 1);
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t row = wave * (64 / L) + (lane >> SEG_LOG2);
+    const bool row_ok = row < n_rows;
+    const int64_t base = row_ok ? row * (int64_t)T : 0;
+    const int nchunks = (T + C - 1) / C;
+    const uint64_t seg_mask = (L == 64) ? ~0ull : ((1ull << L) - 1ull);
+
+    int st = -1;
+    float vs = 0.f, vl = 0.f;
+    if (COMPACT && row_ok) {
+        st = slot_t[row];
+        vs = vboot[row];
+        vl = vboot[n_rows + row];
+    }
+    float carry = 0.f, carry_v = 0.f;
+    bool carry_any = false;
+    for (int c = nchunks - 1; c >= 0; --c) {
+        const int t0 = c * C + (L - 1 - sl) * 4;
+        const bool in = row_ok && t0 < T;  // T % 4 == 0: a lane's 4 steps are all in or all out
+        float r[4] = {0.f, 0.f, 0.f, 0.f}, v[4] = {0.f, 0.f, 0.f, 0.f}, d[4] = {0.f, 0.f, 0.f, 0.f};
+        float bt[4] = {0.f, 0.f, 0.f, 0.f};
+        bool cl[4] = {false, false, false, false};
+        if (in) {
+            const float4 r4 = ld4<1>(rew + base + t0);
+            const float4 v4 = ld4<1>(val + base + t0);
+            const float4 d4 = ld4<1>(term + base + t0);
+            r[0] = r4.x; r[1] = r4.y; r[2] = r4.z; r[3] = r4.w;
+            v[0] = v4.x; v[1] = v4.y; v[2] = v4.z; v[3] = v4.w;
+            d[0] = d4.x; d[1] = d4.y; d[2] = d4.z; d[3] = d4.w;
+            if (COMPACT) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int t = t0 + e;
+                    const bool lt = (t == T - 1);
+                    cl[e] = lt || d[e] != 0.f || t == st;
+                    bt[e] = lt ? (d[e] != 0.f ? 0.f : vl) : (t == st ? vs : 0.f);
+                }
+            } else {
+                const uint32_t c4 = *reinterpret_cast<const uint32_t *>(closed + base + t0);
+                const float4 q4 = ld4<1>(boot + base + t0);
+                bt[0] = q4.x; bt[1] = q4.y; bt[2] = q4.z; bt[3] = q4.w;
+                cl[0] = (c4 & 0xff) != 0; cl[1] = ((c4 >> 8) & 0xff) != 0;
+                cl[2] = ((c4 >> 16) & 0xff) != 0; cl[3] = (c4 >> 24) != 0;
+            }
+        }
+        // v_{t+1} of this lane's last step = v[0] of the lane below it (it owns the following steps)
+        float vn = dpp_mov<kDppWaveShr1>(0.f, v[0]);
+        if (sl == 0) vn = carry_v;
+        float a[4], b[4], adv_direct[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float vnext = (e < 3) ? v[e + 1] : vn;
+            const float nv = cl[e] ? bt[e] : vnext;
+            const float nd = 1.0f - d[e];
+            if (use_gae) {
+                b[e] = r[e] + gamma * nd * nv - v[e];
+                a[e] = cl[e] ? 0.f : gl * nd;
+            } else {
+                b[e] = r[e] + (cl[e] ? gamma * bt[e] : 0.f);
+                a[e] = cl[e] ? 0.f : gamma;
+            }
+            adv_direct[e] = r[e] + gamma * nv - v[e];
+            if (!in) { a[e] = 1.f; b[e] = 0.f; }
+        }
+        float LA = 1.f, LB = 0.f;
+        bool lany = false;
+#pragma unroll
+        for (int e = 3; e >= 0; --e) {
+            LB = b[e] + a[e] * LB;
+            LA = a[e] * LA;
+            lany |= cl[e];
+        }
+        // inclusive scan in lane order inside the segment (lower lanes = later steps)
+        dpp_combine<1, kDppRowShr + 1, 0xf>(LA, LB);
+        dpp_combine<2, kDppRowShr + 2, 0xf>(LA, LB);
+        dpp_combine<4, kDppRowShr + 4, 0xf>(LA, LB);
+        dpp_combine<8, kDppRowShr + 8, 0xf>(LA, LB);
+        if (L >= 32) dpp_combine<16, kDppRowBcast15, 0xa>(LA, LB);
+        if (L == 64) dpp_combine<32, kDppRowBcast31, 0xc>(LA, LB);
+        const float first = LB + LA * carry;  // A (or R) at this lane's first step
+        const uint64_t segbits = (__ballot(lany) >> seg_base) & seg_mask;
+        bool nany = carry_any || (segbits & ((1ull << sl) - 1ull)) != 0;
+        float nxt = dpp_mov<kDppWaveShr1>(0.f, first);
+        if (sl == 0) nxt = carry;
+        float oa[4], orr[4];
+        bool wr[4];
+#pragma unroll
+        for (int e = 3; e >= 0; --e) {
+            const float x = b[e] + a[e] * nxt;
+            const bool anyc = cl[e] || nany;
+            oa[e] = use_gae ? x : adv_direct[e];
+            orr[e] = use_gae ? x + v[e] : x;
+            wr[e] = anyc && in;
+            nxt = x;
+            nany = anyc;
+        }
+        if (wr[0] && wr[1] && wr[2] && wr[3]) {
+            st4<1>(adv + base + t0, make_float4(oa[0], oa[1], oa[2], oa[3]));
+            st4<1>(ret + base + t0, make_float4(orr[0], orr[1], orr[2], orr[3]));
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (wr[e]) {
+                    adv[base + t0 + e] = oa[e];
+                    ret[base + t0 + e] = orr[e];
+                }
+        }
+        if (c > 0) {  // the earlier chunk continues from this chunk's first step (lane L-1)
+            carry = __shfl(first, L - 1, L);
+            carry_v = __shfl(v[0], L - 1, L);
+            carry_any = carry_any || segbits != 0;
+        }
+    }
+    if (COMPACT && row_ok && sl == 0) {  // xpa_rollout_bootstrap_fixup's writes: both bootstraps, slot reset
+        if (st >= 0 && st < T - 1) boot_out[base + st] = vs;
+        boot_out[base + T - 1] = term[base + T - 1] != 0.f ? 0.f : vl;
+        if (st >= 0) slot_t[row] = -1;
+    }
+}
+
+template <int COMPACT>
+bool launch_gae_dpp(int seg_log2, dim3 grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1, const float *rew,
+                    const float *val, const float *term, const uint8_t *closed, const float *boot, int64_t n_envs,
+                    int T, float gamma, float gl, int use_gae, float *adv, float *ret, int *slot_t,
+                    const float *vboot, float *boot_out) {
+#define XPA_GAE_DPP(S_)                                                                                              \
+    do {                                                                                                             \
+        if (e0 || e1)                                                                                                \
+            hipExtLaunchKernelGGL((gae_dpp_kernel<S_, COMPACT>), grid, dim3(256), 0, s, e0, e1, 0, rew, val, term,    \
+                                  closed, boot, n_envs, T, gamma, gl, use_gae, adv, ret, slot_t, vboot, boot_out);   \
+        else                                                                                                         \
+            hipLaunchKernelGGL((gae_dpp_kernel<S_, COMPACT>), grid, dim3(256), 0, s, rew, val, term, closed, boot,    \
+                               n_envs, T, gamma, gl, use_gae, adv, ret, slot_t, vboot, boot_out);                    \
+    } while (0)
+    switch (seg_log2) {
+        case 4: XPA_GAE_DPP(4); return true;
+        case 5: XPA_GAE_DPP(5); return true;
+        case 6: XPA_GAE_DPP(6); return true;
+        default: return false;
+    }
+#undef XPA_GAE_DPP
+}
 }  // namespace
 
 XPA_API int xpa_abi_version(void) { return XPA_ABI_VERSION; }
@@ -219,10 +448,12 @@ void launch_gae(dim3 grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1, const fl
                 float gamma, float gl, int use_gae, float *adv, float *ret) {
     if (e0 || e1)  // events recorded by the dispatch itself: the kernel's own start / end
         hipExtLaunchKernelGGL((gae_scan_kernel<VEC, NT>), grid, dim3(256), 0, s, e0, e1, 0, rew, val, term, closed,
-                              boot, n_envs, T, seg_log2, gamma, gl, use_gae, adv, ret);
+                              boot, n_envs, T, seg_log2, gamma, gl, use_gae, adv, ret, (int *)nullptr,
+                              (const float *)nullptr, (float *)nullptr);
     else
         hipLaunchKernelGGL((gae_scan_kernel<VEC, NT>), grid, dim3(256), 0, s, rew, val, term, closed, boot, n_envs, T,
-                           seg_log2, gamma, gl, use_gae, adv, ret);
+                           seg_log2, gamma, gl, use_gae, adv, ret, (int *)nullptr, (const float *)nullptr,
+                           (float *)nullptr);
 }
 }  // namespace
 
@@ -265,11 +496,65 @@ XPA_API int xpa_gae_scan_timed(const float *rew, const float *val, const float *
     hipStream_t s = (hipStream_t)stream;
     hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
     const dim3 grid((unsigned)blocks);
+    static const int dpp_env = [] {
+        const char *e = getenv("XPA_GAE_DPP");
+        return e ? atoi(e) : -1;
+    }();
+    if (vec4 && nt && dpp_env != 0 &&
+        launch_gae_dpp<0>(seg_log2, grid, s, e0, e1, rew, val, term, closed, boot, n_envs, T, gamma, gl, use_gae, adv,
+                          ret, nullptr, nullptr, nullptr))
+        return xpa_launch_status();
     if (vec4 && nt)
         launch_gae<4, 1>(grid, s, e0, e1, rew, val, term, closed, boot, n_envs, T, seg_log2, gamma, gl, use_gae, adv, ret);
     else if (vec4)
         launch_gae<4, 0>(grid, s, e0, e1, rew, val, term, closed, boot, n_envs, T, seg_log2, gamma, gl, use_gae, adv, ret);
     else
         launch_gae<1, 0>(grid, s, e0, e1, rew, val, term, closed, boot, n_envs, T, seg_log2, gamma, gl, use_gae, adv, ret);
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_gae_scan_compact(const float *rew, const float *val, const float *term, int32_t *slot_t,
+                                 const float *vboot, int64_t n_envs, int64_t horizon, float gamma, float gae_lambda,
+                                 int use_gae, float *adv, float *ret, float *boot, void *ev_start, void *ev_stop,
+                                 xpa_stream_t stream) {
+    if (n_envs < 0 || horizon < 0 || horizon > (1 << 30)) return (int)hipErrorInvalidValue;
+    if (n_envs == 0 || horizon == 0) return 0;
+    if (!rew || !val || !term || !slot_t || !vboot || !adv || !ret || !boot) return (int)hipErrorInvalidValue;
+    const int T = (int)horizon;
+    const bool vec4 = (T % 4 == 0) && ((uintptr_t)rew % 16 == 0) && ((uintptr_t)val % 16 == 0) &&
+                      ((uintptr_t)term % 16 == 0) && ((uintptr_t)adv % 16 == 0) && ((uintptr_t)ret % 16 == 0);
+    const int VEC = vec4 ? 4 : 1;
+    const int per_lane = (T + VEC - 1) / VEC;
+    int seg_log2 = 0;
+    while ((1 << seg_log2) < per_lane && seg_log2 < 6) ++seg_log2;
+    const int64_t rows_per_wave = 64 >> seg_log2;
+    const int64_t blocks = ((n_envs + rows_per_wave - 1) / rows_per_wave + 3) / 4;
+    if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+    const float gl = gamma * gae_lambda;
+    hipStream_t s = (hipStream_t)stream;
+    hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
+    const dim3 grid((unsigned)blocks);
+#define XPA_GAEC(V_, NT_)                                                                                            \
+    do {                                                                                                             \
+        if (e0 || e1)                                                                                                \
+            hipExtLaunchKernelGGL((gae_scan_kernel<V_, NT_, 1>), grid, dim3(256), 0, s, e0, e1, 0, rew, val, term,     \
+                                  (const uint8_t *)nullptr, (const float *)nullptr, n_envs, T, seg_log2, gamma, gl,  \
+                                  use_gae, adv, ret, slot_t, vboot, boot);                                           \
+        else                                                                                                         \
+            hipLaunchKernelGGL((gae_scan_kernel<V_, NT_, 1>), grid, dim3(256), 0, s, rew, val, term,                   \
+                               (const uint8_t *)nullptr, (const float *)nullptr, n_envs, T, seg_log2, gamma, gl,     \
+                               use_gae, adv, ret, slot_t, vboot, boot);                                              \
+    } while (0)
+    static const int dpp_env = [] {
+        const char *e = getenv("XPA_GAE_DPP");
+        return e ? atoi(e) : -1;
+    }();
+    if (vec4 && dpp_env != 0 &&
+        launch_gae_dpp<1>(seg_log2, grid, s, e0, e1, rew, val, term, nullptr, nullptr, n_envs, T, gamma, gl, use_gae,
+                          adv, ret, slot_t, vboot, boot))
+        return xpa_launch_status();
+    if (vec4) XPA_GAEC(4, 1);
+    else XPA_GAEC(1, 0);
+#undef XPA_GAEC
     return xpa_launch_status();
 }

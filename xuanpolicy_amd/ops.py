@@ -166,6 +166,28 @@ def gae_scan(rew, val, term, closed, boot, gamma, gae_lambda, use_gae=True, adv=
     return adv, ret
 
 
+def gae_scan_compact(rew, val, term, slot_t, vboot, gamma, gae_lambda, use_gae=True, adv=None, ret=None, boot=None):
+    """K1, compact closures (xpa_gae_scan_compact): rows close at terminals, at slot_t[n] (one deferred
+    truncation per env, -1 = none) and at the last step, bootstrapped by vboot = [V(truncation slots);
+    V(last obs)] ([2 n_envs]).  Writes the two bootstraps into `boot` and resets slot_t (the state
+    xpa_rollout_bootstrap_fixup + xpa_gae_scan leave).  Returns (adv, ret)."""
+    N, T = rew.shape
+    for name, t, dt in (("rew", rew, torch.float32), ("val", val, torch.float32), ("term", term, torch.float32),
+                        ("boot", boot, torch.float32)):
+        _req(t, name, dt, (N, T))
+    _req(slot_t, "slot_t", torch.int32, (N,))
+    _req(vboot, "vboot", torch.float32, (2 * N,))
+    adv = torch.empty_like(rew) if adv is None else _req(adv, "adv", torch.float32, (N, T))
+    ret = torch.empty_like(rew) if ret is None else _req(ret, "ret", torch.float32, (N, T))
+    ev = TIMER.kernel_events("gae")
+    e0, e1 = (None, None) if ev is None else ev
+    rc = lib().xpa_gae_scan_compact(_p(rew), _p(val), _p(term), _p(slot_t), _p(vboot), N, T, float(gamma),
+                                    float(gae_lambda), int(bool(use_gae)), _p(adv), _p(ret), _p(boot), e0, e1,
+                                    _stream(rew.device))
+    _lib.check(rc, "xpa_gae_scan_compact")
+    return adv, ret
+
+
 def dispatch_floor_us(device, reps=50):
     """Median duration (us) of an empty one-wave launch timed by dispatch-attached events, the clock
     xpa_gae_scan_timed uses: the fixed cost every launch carries on it (bench.py reports it beside K1)."""
