@@ -75,16 +75,22 @@ def gae_graph_replay_us(mem, reps=50):
     (no host dispatch gaps between launches), timed with events on the replay stream."""
     import torch
     from xuanpolicy_amd import ops
-    args = (mem.rewards, mem.values, mem.terminals, mem.closed, mem.boot, mem.gamma, mem.gae_lam, mem.use_gae)
     adv, ret = torch.empty_like(mem.rewards), torch.empty_like(mem.rewards)
+    slot = torch.full((mem.n_envs,), -1, dtype=torch.int32, device=mem.rewards.device)
+    vboot = torch.zeros(2 * mem.n_envs, device=mem.rewards.device)
+    boot = torch.empty_like(mem.rewards)
+
+    def launch():  # the in-loop form (compact closures); slots empty after the rollout's GAE
+        ops.gae_scan_compact(mem.rewards, mem.values, mem.terminals, slot, vboot, mem.gamma, mem.gae_lam,
+                             mem.use_gae, adv=adv, ret=ret, boot=boot)
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
-        ops.gae_scan(*args, adv=adv, ret=ret)        # warm
+        launch()        # warm
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=side):
             for _ in range(reps):
-                ops.gae_scan(*args, adv=adv, ret=ret)
+                launch()
         g.replay()
         side.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -97,7 +103,8 @@ def gae_graph_replay_us(mem, reps=50):
 
 
 def gae_sweep(device, sizes=(4096, 65536, 262144, 1048576), horizon=128, reps=7):
-    """GAE kernel alone, Infinity Cache flushed (512 MiB write) before each timed launch."""
+    """GAE kernel alone (the in-loop compact form, ~1/8 of the rows with a mid-buffer truncation),
+    Infinity Cache flushed (512 MiB write) before each timed launch."""
     import torch
     from xuanpolicy_amd import ops
     flush = torch.empty(512 * 1024 * 1024 // 4, dtype=torch.float32, device=device)
@@ -107,18 +114,21 @@ def gae_sweep(device, sizes=(4096, 65536, 262144, 1048576), horizon=128, reps=7)
         rew = torch.randn(N, horizon, device=device, generator=g)
         val = torch.randn(N, horizon, device=device, generator=g)
         term = (torch.rand(N, horizon, device=device, generator=g) < 0.01).float()
-        closed = (torch.rand(N, horizon, device=device, generator=g) < 0.001).to(torch.uint8)
-        closed[:, -1] = 1
-        boot = torch.randn(N, horizon, device=device, generator=g) * closed
+        vboot = torch.randn(2 * N, device=device, generator=g)
+        slot0 = torch.where(torch.rand(N, device=device, generator=g) < 0.125,
+                            torch.randint(0, horizon - 1, (N,), device=device, generator=g), -1).to(torch.int32)
+        slot = torch.empty_like(slot0)
         adv = torch.empty_like(rew)
         ret = torch.empty_like(rew)
-        mid = int((closed[:, :-1] > 0).sum())
+        boot = torch.empty_like(rew)
+        mid = int((slot0 >= 0).sum())
         times = []
         for _ in range(reps):
+            slot.copy_(slot0)
             flush.fill_(1.0)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            ops.gae_scan(rew, val, term, closed, boot, 0.99, 0.95, True, adv=adv, ret=ret)
+            ops.gae_scan_compact(rew, val, term, slot, vboot, 0.99, 0.95, True, adv=adv, ret=ret, boot=boot)
             e1.record()
             e1.synchronize()
             times.append(e0.elapsed_time(e1))
@@ -127,7 +137,7 @@ def gae_sweep(device, sizes=(4096, 65536, 262144, 1048576), horizon=128, reps=7)
         b = gae_bytes(N, horizon, mid)
         out.append({"n_envs": N, "horizon": horizon, "ms": round(ms, 5), "GB/s": round(b / ms / 1e6, 1),
                     "frac": round(b / ms / 1e6 / HBM_PEAK_GBS, 3), "algorithmic_bytes": int(b)})
-        del rew, val, term, closed, boot, adv, ret
+        del rew, val, term, vboot, slot0, slot, adv, ret, boot
     del flush
     torch.cuda.empty_cache()
     return out
@@ -349,6 +359,7 @@ def main():
     # per-launch time without the event/dispatch overhead a single bracketed launch carries.
     replay_us = None if args.no_kernel_timing else gae_graph_replay_us(mem)
     floor_us = None if args.no_kernel_timing else ops.dispatch_floor_us(device)
+    copy_us = None if args.no_kernel_timing else ops.stream_copy_us(mem.rewards, mem.values, mem.terminals)
     mid_trunc = int(((mem.closed[:, :-1] > 0) & (mem.terminals[:, :-1] == 0)).sum())
     B = N * T // args.n_minibatch
     result = None
@@ -359,11 +370,11 @@ def main():
             gb = gae_bytes(N, T, mid_trunc)
             ach = gb / gae_ms / 1e6
             traffic = None
-            pmc = os.path.join(REPO, "profiles", "pmc_gae_r01.json")
+            pmc = os.path.join(REPO, "profiles", "pmc_gae_compact_r01.json")
             if os.path.exists(pmc):
                 with open(pmc) as f:
                     traffic = json.load(f).get("hbm_bytes_per_launch")
-            roofline = {"kernel": "xpa_gae_scan (gae_scan_kernel<4>)", "bound": "hbm", "achieved": round(ach, 1),
+            roofline = {"kernel": "xpa_gae_scan_compact (gae_dpp_kernel<5, 1>)", "bound": "hbm", "achieved": round(ach, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "avg_launch_us": round(gae_ms * 1e3, 3), "algorithmic_bytes_per_launch": int(gb),
                         "launches": gae_launches,
@@ -374,7 +385,11 @@ def main():
                         # An empty one-wave launch on the same clock: no kernel of this launch's bytes can
                         # measure above gb / floor (tools/gae_floor.hip).
                         "dispatch_floor_us": round(floor_us, 3) if floor_us else None,
-                        "frac_ceiling_at_floor": round(gb / floor_us / 1e3 / HBM_PEAK_GBS, 4) if floor_us else None}
+                        "frac_ceiling_at_floor": round(gb / floor_us / 1e3 / HBM_PEAK_GBS, 4) if floor_us else None,
+                        # the same bytes streamed with no scan (3 loads + 2 stores of 16 B per 4 elements), same
+                        # clock, same buffers: what any kernel moving K1's bytes in one launch takes here
+                        "same_bytes_copy_us": round(copy_us, 3) if copy_us else None,
+                        "frac_of_copy": round(copy_us / (gae_ms * 1e3), 3) if copy_us else None}
         loss_kernel = None
         if loss_ms:
             lb = loss_bytes_gauss(B, args.act_dim)

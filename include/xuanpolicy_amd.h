@@ -87,6 +87,10 @@ int xpa_gae_scan_compact(const float *rew, const float *val, const float *term, 
 /* Measurement aid (no reference counterpart): an empty one-wave kernel launched with the same
  * dispatch-attached events as xpa_gae_scan_timed — the fixed per-launch cost of that clock. */
 int xpa_dispatch_floor_timed(void *ev_start, void *ev_stop, xpa_stream_t stream);
+/* Measurement aid: K1's algorithmic bytes moved with no scan (3 f32 streams read, 2 written, n elements,
+ * 16-B aligned, n % 4 == 0), timed by the same dispatch-attached events: the copy floor K1 is held to. */
+int xpa_stream_copy_timed(const float *r, const float *v, const float *d, float *a, float *o, int64_t n,
+                          void *ev_start, void *ev_stop, xpa_stream_t stream);
 
 /* K4 — minibatch gather.  Replaces the fancy-index gather of DummyOnPolicyBuffer.sample
  * (memory_tools.py:231-240) for the observation rows (the rest is read through `idx` by the loss

@@ -2,7 +2,8 @@
 1 M envs, Infinity Cache flushed before every launch.  Run under:
   rocprofv3 --pmc FETCH_SIZE --output-format csv -d <dir> -- python tools/gae_pmc.py
   rocprofv3 --pmc WRITE_SIZE --output-format csv -d <dir> -- python tools/gae_pmc.py
-tools/pmc_summary.py turns the two passes into profiles/pmc_gae_r01.json (per-launch HBM bytes)."""
+tools/pmc_summary.py turns the two passes into profiles/pmc_gae_compact_r01.json (per-launch HBM bytes of
+the dense and the compact form)."""
 import os
 import sys
 
@@ -25,9 +26,15 @@ def main():
         closed[:, -1] = 1
         boot = torch.randn(N, T, device=dev, generator=g) * closed
         adv, ret = torch.empty_like(rew), torch.empty_like(rew)
-        for _ in range(5):
+        vboot = torch.randn(2 * N, device=dev, generator=g)
+        for _ in range(5):   # dense form (xpa_gae_scan: closure flags + boot streams)
             flush.fill_(1.0)
             ops.gae_scan(rew, val, term, closed, boot, 0.99, 0.95, True, adv=adv, ret=ret)
+        for _ in range(5):   # compact form (the fused agent's in-loop launch), ~1/8 of the rows truncated
+            slot = torch.where(torch.rand(N, device=dev, generator=g) < 0.125,
+                               torch.randint(0, T - 1, (N,), device=dev, generator=g), -1).to(torch.int32)
+            flush.fill_(1.0)
+            ops.gae_scan_compact(rew, val, term, slot, vboot, 0.99, 0.95, True, adv=adv, ret=ret, boot=boot)
         torch.cuda.synchronize()
         print("N", N, "mid closures", int((closed[:, :-1] > 0).sum()), flush=True)
 

@@ -12,10 +12,12 @@ def per_kernel(pass_dir, counter):
     vals = defaultdict(list)
     for f in glob.glob(pass_dir + "/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if r.get("Counter_Name") != counter or "gae_scan" not in r.get("Kernel_Name", ""):
+            name = r.get("Kernel_Name", "")
+            if r.get("Counter_Name") != counter or ("gae_scan" not in name and "gae_dpp" not in name):
                 continue
             grid = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)
-            vals[grid].append(float(r["Counter_Value"]))
+            form = "compact" if (", 1>" in name) else "dense"
+            vals["%s/%d" % (form, grid)].append(float(r["Counter_Value"]))
     return vals
 
 
@@ -23,14 +25,14 @@ def main(fetch_dir, write_dir, out):
     fetch, write = per_kernel(fetch_dir, "FETCH_SIZE"), per_kernel(write_dir, "WRITE_SIZE")
     res = {"method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), KiB x 1024, FETCH x2 (gfx950)",
            "launches": {}}
-    for grid in sorted(set(fetch) | set(write)):
+    for grid in sorted(set(fetch) | set(write)):  # key = form/grid
         f = sorted(fetch.get(grid, [0]))[len(fetch.get(grid, [0])) // 2] * 1024 * 2
         w = sorted(write.get(grid, [0]))[len(write.get(grid, [0])) // 2] * 1024
         res["launches"][str(grid)] = {"fetch_bytes": f, "write_bytes": w, "hbm_bytes": f + w}
-    grids = sorted(res["launches"], key=int)
-    if grids:
-        res["hbm_bytes_per_launch"] = res["launches"][grids[0]]["hbm_bytes"]   # bench size (4096 x 128)
-        res["hbm_bytes_per_launch_1M"] = res["launches"][grids[-1]]["hbm_bytes"]
+    comp = sorted((k for k in res["launches"] if k.startswith("compact/")), key=lambda k: int(k.split("/")[1]))
+    if comp:   # the in-loop (compact) form: bench size (4096 x 128) and 1 M envs
+        res["hbm_bytes_per_launch"] = res["launches"][comp[0]]["hbm_bytes"]
+        res["hbm_bytes_per_launch_1M"] = res["launches"][comp[-1]]["hbm_bytes"]
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

@@ -442,6 +442,33 @@ XPA_API int xpa_dispatch_floor_timed(void *ev_start, void *ev_stop, xpa_stream_t
 }
 
 namespace {
+__global__ __launch_bounds__(256) void stream_copy_kernel(const f4v *__restrict__ r, const f4v *__restrict__ v,
+                                                          const f4v *__restrict__ d, f4v *__restrict__ a,
+                                                          f4v *__restrict__ o, int64_t n4) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n4) return;
+    const f4v x = __builtin_nontemporal_load(r + i);
+    const f4v y = __builtin_nontemporal_load(v + i);
+    const f4v z = __builtin_nontemporal_load(d + i);
+    __builtin_nontemporal_store(x + y * z, a + i);
+    __builtin_nontemporal_store(x * y + z, o + i);
+}
+}  // namespace
+
+// Measurement aid: K1's algorithmic traffic with no scan — three 16-B streaming loads and two 16-B
+// streaming stores per 4 elements (20 B per element) — timed by the same dispatch-attached events.
+XPA_API int xpa_stream_copy_timed(const float *r, const float *v, const float *d, float *a, float *o, int64_t n,
+                                  void *ev_start, void *ev_stop, xpa_stream_t stream) {
+    if (n <= 0 || n % 4 || !r || !v || !d || !a || !o || !ev_start || !ev_stop) return (int)hipErrorInvalidValue;
+    if (((uintptr_t)r | (uintptr_t)v | (uintptr_t)d | (uintptr_t)a | (uintptr_t)o) % 16) return (int)hipErrorInvalidValue;
+    const int64_t n4 = n / 4;
+    hipExtLaunchKernelGGL(stream_copy_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                          (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0, (const f4v *)r, (const f4v *)v, (const f4v *)d,
+                          (f4v *)a, (f4v *)o, n4);
+    return xpa_launch_status();
+}
+
+namespace {
 template <int VEC, int NT>
 void launch_gae(dim3 grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1, const float *rew, const float *val,
                 const float *term, const uint8_t *closed, const float *boot, int64_t n_envs, int T, int seg_log2,

@@ -188,11 +188,10 @@ def gae_scan_compact(rew, val, term, slot_t, vboot, gamma, gae_lambda, use_gae=T
     return adv, ret
 
 
-def dispatch_floor_us(device, reps=50):
-    """Median duration (us) of an empty one-wave launch timed by dispatch-attached events, the clock
-    xpa_gae_scan_timed uses: the fixed cost every launch carries on it (bench.py reports it beside K1)."""
+def _event_timed_median_us(launch, reps):
+    """Median duration (us) of `launch(ev_start, ev_stop)` over `reps` synchronised launches, each timed by
+    dispatch-attached events (the clock xpa_gae_scan_timed uses)."""
     rt = TIMER._hip()
-    lib_ = lib()
     e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
     for ev in (e0, e1):
         if rt.hipEventCreate(ctypes.byref(ev)) != 0:
@@ -200,7 +199,7 @@ def dispatch_floor_us(device, reps=50):
     times = []
     try:
         for i in range(reps + 3):
-            _lib.check(lib_.xpa_dispatch_floor_timed(e0, e1, _stream(device)), "xpa_dispatch_floor_timed")
+            launch(e0, e1)
             rt.hipEventSynchronize(e1)
             ms = ctypes.c_float()
             if rt.hipEventElapsedTime(ctypes.byref(ms), e0, e1) != 0:
@@ -212,6 +211,27 @@ def dispatch_floor_us(device, reps=50):
         rt.hipEventDestroy(e1)
     times.sort()
     return times[len(times) // 2]
+
+
+def dispatch_floor_us(device, reps=50):
+    """Median duration (us) of an empty one-wave launch timed by dispatch-attached events, the clock
+    xpa_gae_scan_timed uses: the fixed cost every launch carries on it (bench.py reports it beside K1)."""
+    st = _stream(device)
+    return _event_timed_median_us(
+        lambda e0, e1: _lib.check(lib().xpa_dispatch_floor_timed(e0, e1, st), "xpa_dispatch_floor_timed"), reps)
+
+
+def stream_copy_us(rew, val, term, reps=50):
+    """Median duration (us) of a plain streaming copy of K1's algorithmic bytes (read rew/val/term, write
+    two arrays of the same shape; 20 B per element) on the same clock: the floor K1 is held to."""
+    n = rew.numel()
+    a, o = torch.empty_like(rew), torch.empty_like(rew)
+    st = _stream(rew.device)
+
+    def launch(e0, e1):
+        _lib.check(lib().xpa_stream_copy_timed(_p(rew), _p(val), _p(term), _p(a), _p(o), n, e0, e1, st),
+                   "xpa_stream_copy_timed")
+    return _event_timed_median_us(launch, reps)
 
 
 def random_permutation(n, seed, counter, out=None, device=None):
