@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--no-sweep", action="store_true")
     p.add_argument("--no-per", action="store_true", help="skip the C5 PER (K6) measurement")
     p.add_argument("--no-c3", action="store_true", help="skip the C3 Atari A2C measurement")
+    p.add_argument("--no-c4", action="store_true", help="skip the C4 Box(376,17) measurement")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
     return p.parse_args()
@@ -251,6 +252,45 @@ def c3_bench(device, n_envs=1024, n_steps=128, steps=2, warmup=1):
     return res
 
 
+def c4_bench(device, rank, world, n_envs=4096, n_steps=128, steps=2, warmup=1):
+    """C4 (BASELINE.json configs[3]): PPO-Clip SynthBox(obs=376, act=17), 4096 envs per GPU, the env shards
+    of all ranks trained together with one all-reduce of the flat gradient per minibatch (every rank runs
+    this; max-over-ranks wall time).  At world = 1 it is one GPU's shard of the 8-GPU configuration."""
+    import torch
+    import torch.distributed as dist
+    from xuanpolicy_amd.distributed import broadcast_parameters
+    from xuanpolicy_amd.runner import build_synthbox_ppo
+    agent = build_synthbox_ppo(n_envs=n_envs, n_steps=n_steps, obs_dim=376, act_dim=17, hidden=256, seed=2,
+                               device=device, shard=rank)
+    agent.learner.enable_fast_path()
+    if world > 1:
+        broadcast_parameters(agent.policy)
+    for _ in range(warmup):
+        agent.train(n_steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        agent.train(n_steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([el], dtype=torch.float64, device=device)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el = float(e)
+    res = {"workload": "PPO-Clip SynthBox(obs=376,act=17) num_envs=%d/GPU x %d GPU horizon=%d, ppo/mujoco.yaml, "
+                       "nets [256] LeakyReLU" % (n_envs, world, n_steps),
+           "metric": "env-steps/s", "value": round(world * n_envs * n_steps * steps / el, 1),
+           "ms_per_iteration": round(el / steps * 1e3, 2), "iterations": steps, "n_gpus": world,
+           "fused_heads": bool(getattr(agent.learner._fused_mlp(), "fused_heads", False))}
+    del agent
+    torch.cuda.empty_cache()
+    return res
+
+
 def cpu_baseline(args, cores):
     """The oracle's restatement of the reference loop (oracle/cpu_ref.AgentLoopRef: per-env
     DummyVecEnv stepping, per-env finish_path, numpy fancy-index sampling, torch-CPU learner with
@@ -362,6 +402,7 @@ def main():
     copy_us = None if args.no_kernel_timing else ops.stream_copy_us(mem.rewards, mem.values, mem.terminals)
     mid_trunc = int(((mem.closed[:, :-1] > 0) & (mem.terminals[:, :-1] == 0)).sum())
     B = N * T // args.n_minibatch
+    c4 = None if args.no_c4 else c4_bench(device, rank, world)   # collective: every rank
     result = None
     if rank == 0:
         value = world * N * T * args.steps / elapsed
@@ -438,6 +479,8 @@ def main():
             "loss_kernel": loss_kernel,
             "update_kernels": update_kernels or None,
         }
+        if c4 is not None:
+            result["c4_box376"] = c4
         if not args.no_sweep and world == 1:
             result["gae_sweep_flushed"] = gae_sweep(device, horizon=T)
         if not args.no_c3 and world == 1:

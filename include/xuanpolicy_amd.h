@@ -243,7 +243,7 @@ int xpa_head_backward(int act, int64_t k, const float *d_head, int64_t ldd, cons
  * layout (width >= xpa_loss_partial_width(K)): the actor kernel fills the surrogate / entropy / clip /
  * dlogstd columns, the critic kernel the squared-error / value columns, so one
  * xpa_policy_loss_finalize over the shared array yields the loss scalars and d logstd.
- * act: 0 identity, 1 LeakyReLU(slope) / ReLU (slope 0), 2 tanh.  K <= 8; hidden must be 256; z and dz
+ * act: 0 identity, 1 LeakyReLU(slope) / ReLU (slope 0), 2 tanh.  K <= 18; hidden must be 256; z and dz
  * rows have stride ld (>= 256, multiple of 4); z and w 16-B aligned. */
 int64_t xpa_head_fused_num_partials(int64_t batch);
 int xpa_head_fused_actor(int algo, int dist, int act, int64_t batch, int64_t act_dim, int64_t hidden, int64_t ld,
@@ -268,7 +268,7 @@ int xpa_colsum_finalize_batch(int n_segs, const float *const *partials, const in
  * fused with xpa_rollout_sample: z_actor / z_critic [n_envs, 256] are the hidden pre-activations
  * (row stride ld, e.g. the halves of a paired [n, 512] GEMM output); the value and mu / logits are
  * formed in the kernel and the sample / log-prob / value / env input are stored exactly as
- * xpa_rollout_sample does (same RNG stream).  act_dim <= 8.
+ * xpa_rollout_sample does (same RNG stream).  act_dim <= 32.
  * xpa_value_head: v_out[n] = act(z_critic) . w_critic + b_critic alone (the bootstrap value of
  * ppoclip_agent.py:77-81 on the normalised final observations). */
 int xpa_rollout_policy_head(int dist, int act, int64_t n_envs, int64_t act_dim, int64_t horizon, int64_t hidden,

@@ -103,18 +103,20 @@ def test_explicit_backward_matches_autograd(discrete, act, rep_hidden):
         assert e_ours <= max(2 * e_torch, 2e-5 * scale), (n1, e_ours, e_torch, scale)
 
 
-@pytest.mark.parametrize("algo,discrete,act,rep_hidden,ent,paired", [
-    ("ppo", False, torch.nn.LeakyReLU, [256], 0.0, True), ("ppo", False, torch.nn.LeakyReLU, [256], 0.0, False),
-    ("ppo", True, torch.nn.LeakyReLU, [256], 0.01, True), ("a2c", False, torch.nn.Tanh, [64], 0.005, True),
-    ("a2c", True, torch.nn.ReLU, [], 0.01, False), ("ppo", False, torch.nn.LeakyReLU, [], 0.0, True)])
-def test_fused_heads_match_loss_kernel_path(algo, discrete, act, rep_hidden, ent, paired):
+@pytest.mark.parametrize("algo,discrete,act,rep_hidden,ent,paired,D,A", [
+    ("ppo", False, torch.nn.LeakyReLU, [256], 0.0, True, 17, 6), ("ppo", False, torch.nn.LeakyReLU, [256], 0.0, False, 17, 6),
+    ("ppo", True, torch.nn.LeakyReLU, [256], 0.01, True, 17, 6), ("a2c", False, torch.nn.Tanh, [64], 0.005, True, 17, 6),
+    ("a2c", True, torch.nn.ReLU, [], 0.01, False, 17, 6), ("ppo", False, torch.nn.LeakyReLU, [], 0.0, True, 17, 6),
+    ("ppo", False, torch.nn.LeakyReLU, [256], 0.0, True, 376, 17),     # C4 shapes (KMAX 18 bucket)
+    ("ppo", True, torch.nn.LeakyReLU, [256], 0.01, True, 33, 18), ("a2c", False, torch.nn.Tanh, [256], 0.01, False, 20, 9)])
+def test_fused_heads_match_loss_kernel_path(algo, discrete, act, rep_hidden, ent, paired, D, A):
     """K12 (heads + loss + head backward in one pass) == K2 loss kernel + explicit backward, which the
     drop-in tests pin to the reference's fixtures: loss scalars and every parameter gradient."""
     from xuanpolicy_amd import ops
     from xuanpolicy_amd.flat import FlatState
     from xuanpolicy_amd.fused_mlp import FusedActorCritic
     torch.manual_seed(1)
-    D, A, B, R = 17, 6, 8192 + 37, 20000
+    B, R = 8192 + 37, 20000
     p1 = _policy(D, A, discrete, act, rep_hidden)
     p2 = _policy(D, A, discrete, act, rep_hidden)
     p2.load_state_dict(p1.state_dict())
@@ -238,9 +240,10 @@ def test_colsum_finalize_batch_matches_single():
         assert torch.equal(o, r)
 
 
-@pytest.mark.parametrize("discrete,act", [(False, torch.nn.LeakyReLU), (True, torch.nn.LeakyReLU),
-                                          (False, torch.nn.Tanh)])
-def test_rollout_policy_head_matches_sample_kernel(discrete, act):
+@pytest.mark.parametrize("discrete,act,D,A", [(False, torch.nn.LeakyReLU, 17, 6), (True, torch.nn.LeakyReLU, 17, 6),
+                                              (False, torch.nn.Tanh, 17, 6), (False, torch.nn.LeakyReLU, 376, 17),
+                                              (True, torch.nn.LeakyReLU, 40, 18)])
+def test_rollout_policy_head_matches_sample_kernel(discrete, act, D, A):
     """K14 (trunk + paired hidden GEMM + heads + sample/store) == policy_heads (nn modules) + K3 on the
     same cursor/seed: same RNG draws, so actions / log-probs / values agree to fp32 rounding."""
     from xuanpolicy_amd import ops
@@ -248,7 +251,7 @@ def test_rollout_policy_head_matches_sample_kernel(discrete, act):
     from xuanpolicy_amd.fused_mlp import FusedActorCritic, head_placement
     from xuanpolicy_amd.policies import policy_heads
     torch.manual_seed(5)
-    D, A, N, T = 17, 6, 4096 + 3, 8
+    N, T = 4096 + 3, 8
     pol = _policy(D, A, discrete, act, [256])
     fs = FlatState(pol.parameters(), placement=head_placement(pol))
     fm = FusedActorCritic(pol, flat=fs)

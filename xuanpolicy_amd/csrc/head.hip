@@ -24,6 +24,7 @@ namespace {
 constexpr int kWaves = 4;
 constexpr int kH = 256;  // hidden width handled
 constexpr int kPartBase = 5;
+constexpr int kHeadKMax = 18;  // largest head width of the fused head kernels (KMAX buckets 4 / 6 / 8 / 18)
 constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
 constexpr float kHalfLog2PiPlusHalf = 1.41893853320467274178f;
 
@@ -598,7 +599,8 @@ void launch_head(const HeadArgs &a, int act_code, hipStream_t s) {
     if constexpr (MODE == 2) launch_act<GEMM, MODE, ALGO, 1>(a, act_code, s);
     else if (a.K <= 4) launch_act<GEMM, MODE, ALGO, 4>(a, act_code, s);  // KMAX = smallest of 4 / 6 / 8 >= K
     else if (a.K <= 6) launch_act<GEMM, MODE, ALGO, 6>(a, act_code, s);
-    else launch_act<GEMM, MODE, ALGO, 8>(a, act_code, s);
+    else if (a.K <= 8) launch_act<GEMM, MODE, ALGO, 8>(a, act_code, s);
+    else launch_act<GEMM, MODE, ALGO, 18>(a, act_code, s);  // C4 (A = 17), 18-way categorical
 }
 #undef XPA_HEAD_ARGS
 
@@ -619,7 +621,7 @@ int check_actor(int algo, int dist, int act_code, int64_t batch, int64_t act_dim
                 const float *old_logp, const float *adv, const float *dz, const float *partial_dw,
                 const float *partial_db_hidden, const float *partial_db_out, const float *loss_partials,
                 int64_t loss_width) {
-    if (batch <= 0 || hidden != kH || act_dim < 1 || act_dim > 8 || act_code < 0 || act_code > 2 || !w || !b ||
+    if (batch <= 0 || hidden != kH || act_dim < 1 || act_dim > kHeadKMax || act_code < 0 || act_code > 2 || !w || !b ||
         !act || !adv || !dz || !partial_dw || !partial_db_hidden || !partial_db_out || !loss_partials ||
         loss_width < kPartBase + act_dim || n_rows <= 0 || (!idx && n_rows < batch))
         return (int)hipErrorInvalidValue;

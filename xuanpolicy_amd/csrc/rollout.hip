@@ -318,6 +318,7 @@ __device__ __forceinline__ float wave_allsum_f(float v) {
 }
 
 // MODE: 0 Gaussian sample, 1 Categorical sample, 2 value only (v_out[n]).
+constexpr int kRolloutKMax = 32;  // head width limit of K14 (lanes < K draw the Gaussian dimensions)
 template <int MODE, int ACT>
 __global__ __launch_bounds__(256) void rollout_policy_head_kernel(
     int64_t n_envs, int K, int64_t T, const float *__restrict__ za, const float *__restrict__ zc, int64_t ld,
@@ -325,7 +326,7 @@ __global__ __launch_bounds__(256) void rollout_policy_head_kernel(
     const float *__restrict__ bc, const float *__restrict__ logstd, const xpa_cursor_t *__restrict__ cur,
     uint32_t seed, float act_clip, float *__restrict__ buf_act, float *__restrict__ buf_logp,
     float *__restrict__ buf_val, float *__restrict__ env_in, int64_t ld_env, float *__restrict__ v_out) {
-    __shared__ float s_head[4][8];
+    __shared__ float s_head[4][kRolloutKMax];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t n = (int64_t)blockIdx.x * 4 + wave;
     if (n >= n_envs) return;  // wave-uniform
@@ -705,7 +706,7 @@ XPA_API int xpa_rollout_policy_head(int dist, int act, int64_t n_envs, int64_t a
                                     const float *b_critic, const float *logstd, const xpa_cursor_t *cursor,
                                     uint32_t seed, float act_clip, float *buf_act, float *buf_logp, float *buf_val,
                                     float *env_in, int64_t ld_env, xpa_stream_t stream) {
-    if (n_envs <= 0 || act_dim < 1 || act_dim > 8 || horizon <= 0 || hidden != 256 || ld < 256 || ld % 4 ||
+    if (n_envs <= 0 || act_dim < 1 || act_dim > kRolloutKMax || horizon <= 0 || hidden != 256 || ld < 256 || ld % 4 ||
         act < 0 || act > 2 || !z_actor || !z_critic || !w_actor || !b_actor || !w_critic || !b_critic || !cursor ||
         !buf_act || !buf_logp || !buf_val || !env_in || ld_env < act_dim)
         return (int)hipErrorInvalidValue;

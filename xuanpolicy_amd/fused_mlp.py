@@ -95,7 +95,7 @@ class FusedActorCritic:
         # K12 (fused head + loss + backward) when both heads end in [Linear(., 256) + act] -> Linear(256, K)
         k = self.actor[-1][0].out_features
         self.fused_heads = (self._head_fusable(self.actor) and self._head_fusable(self.critic)
-                            and k <= 8 and (k >= 2 or not self.discrete))
+                            and k <= ops.HEAD_KMAX and (k >= 2 or not self.discrete))
         self._hws = None
         # K13 for the first representation layer when its input is narrow (observation width <= 64)
         self.thin0 = (len(self.rep) > 0 and self.rep[0][0].in_features <= 64

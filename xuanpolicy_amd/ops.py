@@ -350,6 +350,7 @@ def policy_loss(algo, dist, head, logstd, v, act, adv, ret, old_logp=None, idx=N
 
 # ------------------------------------------------------------------------------------------------
 HEAD_HIDDEN = 256  # hidden width K12 handles (64 lanes x 4 columns)
+HEAD_KMAX = 18   # widest head of the fused head kernels K12 / K16 (and K14's rollout head)
 
 
 class HeadWorkspace:
