@@ -381,12 +381,24 @@ def main():
         elapsed = float(e)
     gae_ms_timed = ops.TIMER.mean_ms("gae")
     gae_launches = ops.TIMER.count("gae")
-    # One more (untimed) iteration with event pairs around the K12 launches and the paired GEMM.
+    # One more (untimed) iteration with event pairs around the K12 launches and the paired GEMM, and
+    # events at the iteration's rollout | update boundary.
+    phase_ms = None
     if not args.no_kernel_timing:
         ops.TIMER.reset()
         ops.TIMER.only = {"heads", "gemm_pair"}
+        e_start = torch.cuda.Event(enable_timing=True)
+        agent.phase_events = []
+        e_start.record()
         agent.train(T)
         torch.cuda.synchronize()
+        ev = dict(agent.phase_events)
+        agent.phase_events = None
+        if "rollout_end" in ev and "update_end" in ev:
+            phase_ms = {"rollout": round(e_start.elapsed_time(ev["rollout_end"]), 3),
+                        "update_incl_gae": round(ev["rollout_end"].elapsed_time(ev["update_end"]), 3),
+                        "note": "device events at the iteration's phase boundaries, one extra iteration after the "
+                                "timed region (the heads/GEMM event pairs of that iteration included)"}
     ops.TIMER.enabled = False
     ops.TIMER.only = None
 
@@ -476,6 +488,7 @@ def main():
                        "parallelism": "dp%d (env shards, 1 %s all-reduce per minibatch)" % (
                            world, "RCCL" if world == 1 or dist.get_backend() == "nccl" else dist.get_backend())},
             "roofline": roofline,
+            "phase_split_ms": phase_ms,
             "loss_kernel": loss_kernel,
             "update_kernels": update_kernels or None,
         }

@@ -150,6 +150,12 @@ int xpa_rms_partials(const float *x, int64_t n, int64_t dim, int64_t ld, const f
                      double *partials, xpa_stream_t stream);
 int xpa_rms_merge(const double *partials, int64_t n_partials, int64_t n, int64_t dim, float *mean,
                   float *var, double *count, xpa_stream_t stream);
+/* xpa_rms_partials + xpa_rms_merge in one launch (shift = mean): the last block to finish (an atomic
+ * ticket, int32 [1], zero-initialised by the caller and left at zero) merges every block's partials in
+ * block order — the same arithmetic and order as xpa_rms_merge.  partials: xpa_rms_num_partials(n) x 2 x
+ * dim doubles. */
+int xpa_rms_update(const float *x, int64_t n, int64_t dim, int64_t ld, float *mean, float *var, double *count,
+                   double *partials, int32_t *ticket, xpa_stream_t stream);
 int xpa_obs_normalize(const float *x, int64_t n, int64_t dim, int64_t ldx, const float *mean,
                       const float *var, float clip_range, float *out, int64_t ldo, float *col_out,
                       int64_t col_ld, const xpa_cursor_t *cursor, xpa_stream_t stream);
@@ -362,6 +368,18 @@ int xpa_rollout_post_deferred(int64_t n_envs, int64_t horizon, const float *rew,
                               float *buf_term, uint8_t *buf_closed, float *buf_boot, float gamma, int mask_returns,
                               int use_rewnorm, float rew_range, int atari_lifeloss, double *partials,
                               uint32_t *ticket, xpa_stream_t stream);
+/* xpa_rollout_post_deferred with the normalisation of the final observations folded in: final_obs holds
+ * the RAW observations; a kept truncation row is normalised with obs_mean / obs_var (clip obs_clip,
+ * xpa_obs_normalize's arithmetic) into slot_obs, and at the rollout's last step every env's normalised
+ * final observation is written into boot_norm [n_envs, ld_norm] (the input of the deferred critic pass). */
+int xpa_rollout_post_deferred_norm(int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term,
+                                   const uint8_t *trunc, const float *final_obs, int64_t ld_final, int64_t obs_dim,
+                                   const float *obs_mean, const float *obs_var, float obs_clip, float *boot_norm,
+                                   int64_t ld_norm, float *slot_obs, int32_t *slot_t, int32_t *overflow,
+                                   xpa_cursor_t *cursor, float *ret_mean, float *ret_var, double *ret_count,
+                                   float *returns, float *buf_rew, float *buf_term, uint8_t *buf_closed,
+                                   float *buf_boot, float gamma, int mask_returns, int use_rewnorm, float rew_range,
+                                   int atari_lifeloss, double *partials, uint32_t *ticket, xpa_stream_t stream);
 int xpa_rollout_bootstrap_fixup(int64_t n_envs, int64_t horizon, const float *values, int32_t *slot_t,
                                 const float *buf_term, float *buf_boot, xpa_stream_t stream);
 

@@ -288,6 +288,26 @@ def test_rms_and_normalize_strided(N, D):
     assert float(col[:, [0, 1, 3]].abs().sum()) == 0.0
 
 
+@pytest.mark.parametrize("N,D", [(4096, 17), (1000, 376), (3, 2), (70000, 5)])
+def test_rms_update_single_launch_equals_two_launch(N, D):
+    """xpa_rms_update (last-arriving block merges, ticket) == xpa_rms_partials + xpa_rms_merge, bit for
+    bit, over consecutive updates; the ticket is back at zero after every launch."""
+    from xuanpolicy_amd import ops
+    rng = np.random.default_rng(N * 3 + D)
+    X = _d(rng.normal(1.0, 3.0, (N, D + 3)).astype(np.float32))
+    x = X[:, :D]
+    st = [(torch.zeros(D, device=DEV), torch.ones(D, device=DEV),
+           torch.full((1,), 1e-4, dtype=torch.float64, device=DEV)) for _ in range(2)]
+    ticket = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for k in range(4):
+        xk = x * (1.0 + 0.1 * k)
+        ops.rms_update(xk, *st[0])
+        ops.rms_update(xk, *st[1], ticket=ticket)
+        for a, b in zip(st[0], st[1]):
+            assert torch.equal(a, b)
+        assert int(ticket.item()) == 0
+
+
 # ---------------------------------------------------------------------------------------------- K7
 @pytest.mark.parametrize("D,A,discrete", [(17, 6, False), (376, 17, False), (4, 2, True)])
 def test_synthbox_step_matches_oracle(D, A, discrete):

@@ -44,6 +44,7 @@ SIGNATURES = {
                                                 c_p, c_p, c_p]),
     "xpa_rms_num_partials": (c_i64, [c_i64]),
     "xpa_rms_partials": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
+    "xpa_rms_update": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p]),
     "xpa_rms_merge": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p]),
     "xpa_obs_normalize": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_f32, c_p, c_i64, c_p, c_i64, c_p, c_p]),
     "xpa_rollout_sample": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_u32, c_f32, c_p, c_p,
@@ -80,6 +81,10 @@ SIGNATURES = {
     "xpa_synthatari_step": (ctypes.c_int, [c_i64, c_i64, c_p, c_i64, c_u32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                                            c_p, c_p, c_p, c_p, c_p]),
     "xpa_synthatari_reset": (ctypes.c_int, [c_i64, c_u32, c_p, c_p, c_p]),
+    "xpa_rollout_post_deferred_norm": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_f32,
+                                                      c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                                                      c_p, c_f32, ctypes.c_int, ctypes.c_int, c_f32, ctypes.c_int, c_p,
+                                                      c_p, c_p]),
     "xpa_rollout_post_deferred": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p,
                                                  c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, ctypes.c_int, ctypes.c_int,
                                                  c_f32, ctypes.c_int, c_p, c_p, c_p]),

@@ -97,6 +97,7 @@ class _OnPolicyAgent:
         self.boot_obs = None if self.raw_obs else torch.empty((N, D), **f32)
         self.rms_part = (torch.empty((2 * ops.rms_num_partials(N), D), dtype=torch.float64, device=dev)
                          if self.use_obsnorm else None)
+        self._rms_ticket = torch.zeros((1,), dtype=torch.int32, device=dev)   # xpa_rms_update's arrival count
         self._policy_in = self.obs_norm
         self.logp_scratch = None if self.algo == "ppo" else torch.zeros((N, T), **f32)
         self.obs_mb = None
@@ -112,6 +113,7 @@ class _OnPolicyAgent:
         self.infos = []          # host copies, one dict per buffer-full phase
         self.log_hook = None     # optional callable(info: dict, step: int) (tensorboard/wandb adapter)
         self.timers = {"rollout": 0.0, "update": 0.0}
+        self.phase_events = None
         self._t = 0
         self._host_obs = None
         self.use_graph = bool(_cfg(config, "cuda_graph", True)) and self.device.type == "cuda"
@@ -190,16 +192,19 @@ class _OnPolicyAgent:
                 v_boot = policy_heads(self.policy, final_obs)[2]
             self._post_kernel(rew, term, trunc, v_boot)
             return
-        self._normalize_into(final_obs, self.boot_obs, False)
         if self.defer_boot:
+            # final-obs normalisation folded into K8: kept truncation rows and, at the last step, every env's
+            # normalised final observation (boot_obs) — no separate normalise launch per step
             mem = self.memory
             ops.rollout_post(rew, term, trunc, None, self.cursor, self.ret_mean, self.ret_var, self.ret_count,
                              self.returns, mem.rewards, mem.terminals, mem.closed, mem.boot, self.gamma,
                              mask_returns=(self.algo == "ppo"), use_rewnorm=self.use_rewnorm,
                              rew_range=self.rewnorm_range, atari_lifeloss=self.atari,
-                             deferred=(self.boot_obs, self.slot_obs, self.slot_t, self.slot_overflow),
+                             deferred=(final_obs, self.slot_obs, self.slot_t, self.slot_overflow, self.obs_mean,
+                                       self.obs_var, self._obs_clip(), self.boot_obs),
                              workspace=self.post_ws)
             return
+        self._normalize_into(final_obs, self.boot_obs, False)
         fm = self._rollout_mlp()
         if fm is not None:
             v_boot = fm.rollout_value(self.boot_obs)
@@ -221,7 +226,8 @@ class _OnPolicyAgent:
             ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count, partials=self.rms_part,
                            reduce_partials=lambda t: tdist.all_reduce(t, op=tdist.ReduceOp.SUM), world=self.world)
         else:
-            ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count, partials=self.rms_part)
+            ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count, partials=self.rms_part,
+                           ticket=self._rms_ticket)
 
     def _rollout_step_device(self):
         env = self.envs
@@ -386,7 +392,13 @@ class _OnPolicyAgent:
             t1 = time.perf_counter()
             self.timers["rollout"] += t1 - t0
             if self._t == self.n_steps:
+                if self.phase_events is not None:   # measurement hook (bench.py): rollout | update split
+                    self.phase_events.append(("rollout_end", torch.cuda.Event(enable_timing=True)))
+                    self.phase_events[-1][1].record()
                 self._update_phase()
+                if self.phase_events is not None:
+                    self.phase_events.append(("update_end", torch.cuda.Event(enable_timing=True)))
+                    self.phase_events[-1][1].record()
                 self._t = 0
                 self.memory.ptr, self.memory.size = 0, 0
                 if log:

@@ -130,10 +130,19 @@ __global__ __launch_bounds__(256) void permutation_kernel(int64_t n, int h, uint
 // (shift = the running mean, so the one-pass variance does not cancel).  Threads cover a
 // (row group x column) tile, all row loads of a thread are independent (no serial latency chain),
 // and the row groups are combined through LDS in a fixed order.
+__device__ void rms_merge_body(const double *part, int64_t np, int64_t n, int64_t dim, float *__restrict__ mean,
+                               float *__restrict__ var, double *__restrict__ count);
+
+// MERGE: the last block to finish (atomic ticket) also runs the merge below over all blocks' partials in
+// block order (deterministic, = xpa_rms_merge) and resets the ticket: one launch per obs-RMS update.
+template <bool MERGE>
 __global__ __launch_bounds__(256) void rms_partials_kernel(const float *__restrict__ x, int64_t n, int64_t dim,
-                                                           int64_t ld, const float *__restrict__ shift,
-                                                           double *__restrict__ part) {
+                                                           int64_t ld, const float *shift,  // may alias mean
+                                                           double *__restrict__ part, float *mean,
+                                                           float *__restrict__ var, double *__restrict__ count,
+                                                           unsigned int *__restrict__ ticket) {
     __shared__ double s_sum[256], s_sq[256];
+    __shared__ bool s_last;
     const int64_t r0 = (int64_t)blockIdx.x * kRmsRows;
     const int64_t r1 = r0 + kRmsRows < n ? r0 + kRmsRows : n;
     const int64_t np = gridDim.x;
@@ -165,21 +174,29 @@ __global__ __launch_bounds__(256) void rms_partials_kernel(const float *__restri
         }
         __syncthreads();
     }
+    if (MERGE) {
+        __threadfence();  // this block's partials visible device-wide before its ticket
+        if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1u) == (unsigned)(np - 1);
+        __syncthreads();
+        if (!s_last) return;
+        __threadfence();
+        rms_merge_body(part, np, n, dim, mean, var, count);
+        if (threadIdx.x == 0) *ticket = 0u;
+    }
 }
 
 // Sum of the partials (fixed order) -> batch mean/var, then update_from_moments
 // (statistic_tools.py:86-112) into mean/var (f32) and count (f64).  mean doubles as the shift the
 // partials were taken around.
-__global__ __launch_bounds__(256) void rms_merge_kernel(const double *__restrict__ part, int64_t np, int64_t n,
-                                                        int64_t dim, float *__restrict__ mean, float *__restrict__ var,
-                                                        double *__restrict__ count) {
+__device__ void rms_merge_body(const double *part, int64_t np, int64_t n, int64_t dim, float *__restrict__ mean,
+                               float *__restrict__ var, double *__restrict__ count) {
     const double c0 = *count;
     __syncthreads();
     for (int64_t d = threadIdx.x; d < dim; d += blockDim.x) {
         double s = 0.0, q = 0.0;
-        for (int64_t p = 0; p < np; ++p) {
-            s += part[p * dim + d];
-            q += part[(np + p) * dim + d];
+        for (int64_t p = 0; p < np; ++p) {  // volatile: other blocks' partials (ticketed merge), never stale L1
+            s += ((const volatile double *)part)[p * dim + d];
+            q += ((const volatile double *)part)[(np + p) * dim + d];
         }
         const double ms = s / (double)n;
         const double m0 = (double)mean[d], v0 = (double)var[d];
@@ -194,6 +211,12 @@ __global__ __launch_bounds__(256) void rms_merge_kernel(const double *__restrict
     }
     __syncthreads();
     if (threadIdx.x == 0) *count = c0 + (double)n;
+}
+
+__global__ __launch_bounds__(256) void rms_merge_kernel(const double *__restrict__ part, int64_t np, int64_t n,
+                                                        int64_t dim, float *__restrict__ mean, float *__restrict__ var,
+                                                        double *__restrict__ count) {
+    rms_merge_body(part, np, n, dim, mean, var, count);
 }
 
 __global__ __launch_bounds__(256) void obs_normalize_kernel(const float *__restrict__ x, int64_t n, int64_t dim,
@@ -446,7 +469,17 @@ __global__ __launch_bounds__(256) void synthbox_step_kernel(
 // (boot_obs) into slot_obs[n] and records slot_t[n] = t (a second one in the same rollout counts in
 // *overflow); bootstraps are written afterwards by xpa_rollout_bootstrap_fixup.
 constexpr int kPostThreads = 256;
-template <bool DEFER>
+// NORM (with DEFER): boot_obs holds the RAW final observations; the kernel normalises them with the obs
+// running statistics (obs_normalize_kernel's exact arithmetic) where it keeps a truncation row, and at the
+// rollout's last step writes every env's normalised final observation into boot_norm — the second
+// normalise launch of each env step is folded in here.
+__device__ __forceinline__ float obs_norm1(float x, float m, float v, float clip) {
+    const float sd = sqrtf(v);
+    const float y = (x - m) / (sd + 1e-8f);
+    return fminf(fmaxf(y, -clip), clip);
+}
+
+template <bool DEFER, bool NORM = false>
 __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
     int64_t n_envs, int64_t T, const float *__restrict__ rew, const uint8_t *__restrict__ term,
     const uint8_t *__restrict__ trunc, const float *__restrict__ v_boot, xpa_cursor_t *__restrict__ cur,
@@ -455,7 +488,9 @@ __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
     uint8_t *__restrict__ buf_closed, float *__restrict__ buf_boot, float gamma, int mask_returns, int use_rewnorm,
     float rew_range, int atari_lifeloss, const float *__restrict__ boot_obs, int64_t ld_boot, int64_t dim,
     float *__restrict__ slot_obs, int *__restrict__ slot_t, int *__restrict__ overflow, double *__restrict__ partials,
-    unsigned int *__restrict__ ticket) {
+    unsigned int *__restrict__ ticket, const float *__restrict__ obs_mean = nullptr,
+    const float *__restrict__ obs_var = nullptr, float obs_clip = 0.f, float *__restrict__ boot_norm = nullptr,
+    int64_t ld_norm = 0) {
     __shared__ double s_red[kPostThreads / 64];
     __shared__ bool s_last;
     const int32_t t = cur->ptr;
@@ -478,8 +513,13 @@ __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
         if (DEFER && close && !te && !last) {  // mid-buffer truncation: keep the row for later
             if (slot_t[n] >= 0) atomicAdd(overflow, 1);
             slot_t[n] = (int)t;
-            for (int64_t d = 0; d < dim; ++d) slot_obs[n * dim + d] = boot_obs[n * ld_boot + d];
+            for (int64_t d = 0; d < dim; ++d)
+                slot_obs[n * dim + d] = NORM ? obs_norm1(boot_obs[n * ld_boot + d], obs_mean[d], obs_var[d], obs_clip)
+                                             : boot_obs[n * ld_boot + d];
         }
+        if (NORM && last)
+            for (int64_t d = 0; d < dim; ++d)
+                boot_norm[n * ld_norm + d] = obs_norm1(boot_obs[n * ld_boot + d], obs_mean[d], obs_var[d], obs_clip);
         float Rk = mask_returns ? (te ? 0.f : gamma * R) + r : gamma * R + r;
         if (done) {
             cnt = 1.0;
@@ -565,8 +605,19 @@ XPA_API int xpa_rms_partials(const float *x, int64_t n, int64_t dim, int64_t ld,
                              double *partials, xpa_stream_t stream) {
     if (n <= 0 || dim <= 0 || ld < dim || !x || !partials) return (int)hipErrorInvalidValue;
     const int64_t np = xpa_rms_num_partials(n);
-    hipLaunchKernelGGL(rms_partials_kernel, dim3((unsigned)np), dim3(256), 0, (hipStream_t)stream, x, n, dim, ld,
-                       shift, partials);
+    hipLaunchKernelGGL(rms_partials_kernel<false>, dim3((unsigned)np), dim3(256), 0, (hipStream_t)stream, x, n, dim,
+                       ld, shift, partials, (float *)nullptr, (float *)nullptr, (double *)nullptr,
+                       (unsigned int *)nullptr);
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_rms_update(const float *x, int64_t n, int64_t dim, int64_t ld, float *mean, float *var,
+                           double *count, double *partials, int32_t *ticket, xpa_stream_t stream) {
+    if (n <= 0 || dim <= 0 || ld < dim || !x || !mean || !var || !count || !partials || !ticket)
+        return (int)hipErrorInvalidValue;
+    const int64_t np = xpa_rms_num_partials(n);
+    hipLaunchKernelGGL(rms_partials_kernel<true>, dim3((unsigned)np), dim3(256), 0, (hipStream_t)stream, x, n, dim, ld,
+                       (const float *)mean, partials, mean, var, count, (unsigned int *)ticket);
     return xpa_launch_status();
 }
 
@@ -651,7 +702,7 @@ XPA_API int xpa_rollout_post(int64_t n_envs, int64_t horizon, const float *rew, 
                        dim3(kPostThreads), 0, (hipStream_t)stream, n_envs, horizon, rew, term, trunc, v_boot, cursor,
                        ret_mean, ret_var, ret_count, returns, buf_rew, buf_term, buf_closed, buf_boot, gamma,
                        mask_returns, use_rewnorm, rew_range, atari_lifeloss, (const float *)nullptr, (int64_t)0,
-                       (int64_t)0, (float *)nullptr, (int *)nullptr, (int *)nullptr, partials, (unsigned *)ticket);
+                       (int64_t)0, (float *)nullptr, (int *)nullptr, (int *)nullptr, partials, (unsigned *)ticket, (const float *)nullptr, (const float *)nullptr, 0.f, (float *)nullptr, (int64_t)0);
     return xpa_launch_status();
 }
 
@@ -670,7 +721,30 @@ XPA_API int xpa_rollout_post_deferred(int64_t n_envs, int64_t horizon, const flo
                        dim3(kPostThreads), 0, (hipStream_t)stream, n_envs, horizon, rew, term, trunc,
                        (const float *)nullptr, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term,
                        buf_closed, buf_boot, gamma, mask_returns, use_rewnorm, rew_range, atari_lifeloss, boot_obs,
-                       ld_boot, obs_dim, slot_obs, slot_t, overflow, partials, (unsigned *)ticket);
+                       ld_boot, obs_dim, slot_obs, slot_t, overflow, partials, (unsigned *)ticket, (const float *)nullptr, (const float *)nullptr, 0.f, (float *)nullptr, (int64_t)0);
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_rollout_post_deferred_norm(int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term,
+                                           const uint8_t *trunc, const float *final_obs, int64_t ld_final,
+                                           int64_t obs_dim, const float *obs_mean, const float *obs_var,
+                                           float obs_clip, float *boot_norm, int64_t ld_norm, float *slot_obs,
+                                           int32_t *slot_t, int32_t *overflow, xpa_cursor_t *cursor, float *ret_mean,
+                                           float *ret_var, double *ret_count, float *returns, float *buf_rew,
+                                           float *buf_term, uint8_t *buf_closed, float *buf_boot, float gamma,
+                                           int mask_returns, int use_rewnorm, float rew_range, int atari_lifeloss,
+                                           double *partials, uint32_t *ticket, xpa_stream_t stream) {
+    if (n_envs <= 0 || horizon <= 0 || obs_dim <= 0 || ld_final < obs_dim || ld_norm < obs_dim || !rew || !term ||
+        !trunc || !final_obs || !obs_mean || !obs_var || !boot_norm || !slot_obs || !slot_t || !overflow || !cursor ||
+        !ret_mean || !ret_var || !ret_count || !returns || !buf_rew || !buf_term || !buf_closed || !buf_boot ||
+        !partials || !ticket || xpa_rollout_post_num_blocks(n_envs) > 0x7fffffff)
+        return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((rollout_post_kernel<true, true>), dim3((unsigned)xpa_rollout_post_num_blocks(n_envs)),
+                       dim3(kPostThreads), 0, (hipStream_t)stream, n_envs, horizon, rew, term, trunc,
+                       (const float *)nullptr, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term,
+                       buf_closed, buf_boot, gamma, mask_returns, use_rewnorm, rew_range, atari_lifeloss, final_obs,
+                       ld_final, obs_dim, slot_obs, slot_t, overflow, partials, (unsigned *)ticket, obs_mean, obs_var,
+                       obs_clip, boot_norm, ld_norm);
     return xpa_launch_status();
 }
 

@@ -518,12 +518,13 @@ def rms_num_partials(n):
     return int(lib().xpa_rms_num_partials(n))
 
 
-def rms_update(x, mean, var, count, partials=None, reduce_partials=None, world=1):
+def rms_update(x, mean, var, count, partials=None, reduce_partials=None, world=1, ticket=None):
     """K5a+b: RunningMeanStd.update(x) on device.  x [n, dim] float32 (row stride may exceed dim);
     mean/var float32 [dim], count float64 [1] — all updated in place.
     reduce_partials(partials): optional in-place SUM across ranks of the f64 partials (the
     mpi_moments-style synchronised statistics, statistic_tools.py:20-32); the merge then counts
-    n * world rows.  All ranks must hold the same running mean (it is the partials' shift)."""
+    n * world rows.  All ranks must hold the same running mean (it is the partials' shift).
+    ticket (int32 [1], zeroed once): single-launch form (xpa_rms_update: the last block merges)."""
     n, dim = x.shape
     ld = _row_stride(x, "x", dim)
     _req(mean, "mean", torch.float32, (dim,))
@@ -535,6 +536,11 @@ def rms_update(x, mean, var, count, partials=None, reduce_partials=None, world=1
     else:
         _req(partials, "partials", torch.float64, (2 * np_, dim))
     s = _stream(x.device)
+    if ticket is not None and reduce_partials is None:
+        _req(ticket, "ticket", torch.int32, (1,))
+        _lib.check(lib().xpa_rms_update(_p(x), n, dim, ld, _p(mean), _p(var), _p(count), _p(partials), _p(ticket), s),
+                   "xpa_rms_update")
+        return
     _lib.check(lib().xpa_rms_partials(_p(x), n, dim, ld, _p(mean), _p(partials), s), "xpa_rms_partials")
     if reduce_partials is not None:
         reduce_partials(partials)
@@ -675,6 +681,26 @@ def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count,
         _req(t, name, torch.float32, (N, T))
     _req(buf_closed, "buf_closed", torch.uint8, (N, T))
     part, ticket = workspace if workspace is not None else post_workspace(N, rew.device)
+    if deferred is not None and len(deferred) == 8:
+        # (final_obs RAW, slot_obs, slot_t, overflow, obs_mean, obs_var, obs_clip, boot_norm): normalisation
+        # of the final observations folded into K8 (xpa_rollout_post_deferred_norm)
+        final_obs, slot_obs, slot_t, overflow, obs_mean, obs_var, obs_clip, boot_norm = deferred
+        D = slot_obs.shape[1]
+        ldf = _row_stride(final_obs, "final_obs", D)
+        ldn = _row_stride(boot_norm, "boot_norm", D)
+        _req(slot_obs, "slot_obs", torch.float32, (N, D))
+        _req(slot_t, "slot_t", torch.int32, (N,))
+        _req(overflow, "overflow", torch.int32, (1,))
+        _req(obs_mean, "obs_mean", torch.float32, (D,))
+        _req(obs_var, "obs_var", torch.float32, (D,))
+        rc = lib().xpa_rollout_post_deferred_norm(
+            N, T, _p(rew), _p(term), _p(trunc), _p(final_obs), ldf, D, _p(obs_mean), _p(obs_var), float(obs_clip),
+            _p(boot_norm), ldn, _p(slot_obs), _p(slot_t), _p(overflow), _p(cursor), _p(ret_mean), _p(ret_var),
+            _p(ret_count), _p(returns), _p(buf_rew), _p(buf_term), _p(buf_closed), _p(buf_boot), float(gamma),
+            int(bool(mask_returns)), int(bool(use_rewnorm)), float(rew_range), int(bool(atari_lifeloss)), _p(part),
+            _p(ticket), _stream(rew.device))
+        _lib.check(rc, "xpa_rollout_post_deferred_norm")
+        return
     if deferred is not None:
         boot_obs, slot_obs, slot_t, overflow = deferred
         D = slot_obs.shape[1]
