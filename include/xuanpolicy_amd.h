@@ -393,6 +393,14 @@ int xpa_rollout_bootstrap_fixup(int64_t n_envs, int64_t horizon, const float *va
 int64_t xpa_thin_bwd_num_partials(int64_t rows);
 int xpa_thin_linear_act_fwd(int act, const float *x, int64_t ldx, int64_t rows, int64_t d_in, int64_t d_out,
                             const float *w, const float *b, float slope, float *h, int64_t ldh, xpa_stream_t stream);
+/* The rollout's forward with the observation normalisation fused in: x holds RAW observations;
+ * xn = clip((x - mean) / (sqrt(var) + 1e-8), +-clip) (xpa_obs_normalize's arithmetic) is written to xn
+ * [rows, ldn] and, when col != NULL, into the rollout buffer column cursor->ptr of col (row stride col_ld
+ * floats, as xpa_obs_normalize's col_out), and h = act(xn W^T + b) as xpa_thin_linear_act_fwd. */
+int xpa_thin_linear_act_fwd_norm(int act, const float *x, int64_t ldx, int64_t rows, int64_t d_in, int64_t d_out,
+                                 const float *w, const float *b, float slope, float *h, int64_t ldh,
+                                 const float *mean, const float *var, float clip, float *xn, int64_t ldn,
+                                 float *col, int64_t col_ld, const xpa_cursor_t *cursor, xpa_stream_t stream);
 int xpa_thin_linear_act_bwd(int act, const float *g, int64_t ldg, const float *h, int64_t ldh, int64_t rows,
                             const float *x, int64_t ldx, int64_t d_in, int64_t d_out, float slope, float *partial_dw,
                             float *partial_db, xpa_stream_t stream);

@@ -215,6 +215,39 @@ def test_thin_first_layer_kernels(rows, din, code):
                                      slope, ops._p(h), 256, s) != 0
 
 
+@pytest.mark.parametrize("rows,din,code", [(4096, 17, 1), (1001, 8, 2), (77, 33, 0)])
+def test_thin_forward_with_fused_normalisation(rows, din, code):
+    """xpa_thin_linear_act_fwd_norm == xpa_obs_normalize (into xn and the buffer column) followed by
+    xpa_thin_linear_act_fwd: identical normalised rows, h within fp32 rounding."""
+    from xuanpolicy_amd import ops
+    torch.manual_seed(rows + din)
+    X = torch.randn(rows, din + 3, device=DEV) * 3 + 1
+    x = X[:, :din]
+    mean, var = torch.randn(din, device=DEV), torch.rand(din, device=DEV) + 0.1
+    W, b = torch.randn(256, din, device=DEV) * 0.2, torch.randn(256, device=DEV) * 0.1
+    T = 5
+    cur = torch.tensor([3, 0, 0, 0], dtype=torch.int32, device=DEV)
+    L = ops.lib()
+    s = ops._stream()
+    outs = []
+    for fused in (False, True):
+        xn = torch.zeros(rows, din, device=DEV)
+        col = torch.zeros(rows, T, din, device=DEV)
+        h = torch.empty(rows, 256, device=DEV)
+        if fused:
+            assert L.xpa_thin_linear_act_fwd_norm(code, ops._p(x), x.stride(0), rows, din, 256, ops._p(W), ops._p(b),
+                                                   0.01, ops._p(h), 256, ops._p(mean), ops._p(var), 5.0, ops._p(xn),
+                                                   din, ops._p(col), T * din, ops._p(cur), s) == 0
+        else:
+            ops.obs_normalize(x, mean, var, 5.0, xn, col_out=col, col_ld=T * din, cursor=cur)
+            assert L.xpa_thin_linear_act_fwd(code, ops._p(xn), din, rows, din, 256, ops._p(W), ops._p(b), 0.01,
+                                             ops._p(h), 256, s) == 0
+        outs.append((xn, col, h))
+    (xa, ca, ha), (xb, cb, hb) = outs
+    assert torch.equal(xa, xb) and torch.equal(ca, cb)
+    torch.testing.assert_close(hb, ha, rtol=1e-6, atol=1e-6)
+
+
 def test_colsum_finalize_batch_matches_single():
     """xpa_colsum_finalize_batch == per-segment xpa_colsum_finalize (bitwise: same fixed-order f64 sums),
     more segments than one launch holds."""

@@ -165,11 +165,18 @@ class _OnPolicyAgent:
         fm = fm_get() if fm_get is not None else None
         return fm if fm is not None and fm.rollout_ok else None
 
-    def _sample_into_buffer(self):
+    def _sample_into_buffer(self, raw_x=None):
+        """raw_x: the raw observations, normalised inside the fused trunk (see _rollout_step_device)."""
         mem = self.memory
         logp_buf = mem.auxiliary_infos["old_logp"] if self.algo == "ppo" else self.logp_scratch
         env_in = self.envs.act_in if self.device_env else self._act_scratch()
         fm = self._rollout_mlp()
+        if raw_x is not None:
+            T, D = self.n_steps, self.obs_dim
+            fm.rollout_act(raw_x, self.dist, self.cursor, self.seed, mem.actions, logp_buf, mem.values, env_in,
+                           act_clip=1.0, norm=(self.obs_mean, self.obs_var, self._obs_clip(), self.obs_norm,
+                                               mem.observations, T * D, self.cursor))
+            return
         if fm is not None:
             fm.rollout_act(self._policy_in, self.dist, self.cursor, self.seed, mem.actions, logp_buf, mem.values,
                            env_in, act_clip=1.0)
@@ -238,6 +245,12 @@ class _OnPolicyAgent:
         else:
             if self.use_obsnorm:
                 self._rms_update(x)
+            fm = self._rollout_mlp()
+            if fm is not None and fm.thin0 and x.stride(1) == 1:
+                self._sample_into_buffer(raw_x=x)   # normalisation fused into the trunk's first layer
+                env.step_device()
+                self._post(env.rew, env.term, env.trunc, env.final_obs)
+                return
             self._normalize_into(x, self.obs_norm, True)
         self._sample_into_buffer()
         env.step_device()

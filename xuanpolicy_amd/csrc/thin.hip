@@ -75,6 +75,63 @@ __global__ __launch_bounds__(256) void thin_fwd_kernel(const float *__restrict__
     }
 }
 
+// Rollout form with the observation normalisation fused in (K5c + K13): the raw observation rows are
+// normalised while the x tile is staged — clip((x - mean) / (sqrt(var) + 1e-8)), xpa_obs_normalize's
+// arithmetic — and the normalised rows are also written to `xn` (the policy input) and into the
+// rollout buffer column cursor.ptr of `col` ([rows, T, din] at col_ld floats per row).  8-row tiles.
+template <int ACT, int DMAX>
+__global__ __launch_bounds__(256) void thin_fwd_norm_kernel(const float *__restrict__ x, int64_t ldx, int64_t rows,
+                                                            int din, const float *__restrict__ W,
+                                                            const float *__restrict__ bias, float slope,
+                                                            float *__restrict__ h, int64_t ldh,
+                                                            const float *__restrict__ mean,
+                                                            const float *__restrict__ var, float clip,
+                                                            float *__restrict__ xn, int64_t ldn,
+                                                            float *__restrict__ col, int64_t col_ld,
+                                                            const xpa_cursor_t *__restrict__ cursor) {
+    constexpr int TILE = 8;
+    constexpr int kPad = DMAX + 4;
+    __shared__ __attribute__((aligned(16))) float s_x[TILE * kPad];
+    const int t = threadIdx.x;
+    float w[DMAX];
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) w[k] = k < din ? W[t * din + k] : 0.f;
+    const float bc = bias[t];
+    const int64_t coff = col ? (int64_t)cursor->ptr * din : 0;
+    const int64_t ntiles = (rows + TILE - 1) / TILE;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t r0 = tile * TILE;
+        __syncthreads();
+        for (int i = t; i < TILE * DMAX; i += 256) {
+            const int r = i / DMAX, k = i - r * DMAX;
+            float y = 0.f;
+            if (k < din && r0 + r < rows) {
+                const float sd = sqrtf(var[k]);
+                y = (x[(r0 + r) * ldx + k] - mean[k]) / (sd + 1e-8f);
+                y = fminf(fmaxf(y, -clip), clip);
+                xn[(r0 + r) * ldn + k] = y;
+                if (col) col[(r0 + r) * col_ld + coff + k] = y;
+            }
+            s_x[r * kPad + k] = y;
+        }
+        __syncthreads();
+        const int nr = (int)min((int64_t)TILE, rows - r0);
+        for (int r = 0; r < nr; ++r) {
+            const float *xr = s_x + r * kPad;
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < DMAX; k += 4) {
+                const float4 xv = *reinterpret_cast<const float4 *>(xr + k);
+                acc = fmaf(xv.x, w[k], acc);
+                acc = fmaf(xv.y, w[k + 1], acc);
+                acc = fmaf(xv.z, w[k + 2], acc);
+                acc = fmaf(xv.w, w[k + 3], acc);
+            }
+            __builtin_nontemporal_store(act_f<ACT>(acc + bc, slope), h + (r0 + r) * ldh + t);
+        }
+    }
+}
+
 // 1024 threads = 4 groups of 256 (group = one 64-row tile at a time, thread = column), 8 rows of g / h
 // in flight per thread; the groups' accumulators are combined through LDS (fixed order) at the end.
 constexpr int kBwdGroups = 4;
@@ -238,5 +295,33 @@ XPA_API int xpa_thin_linear_act_bwd(int act, const float *g, int64_t ldg, const 
     if (act == 0) launch_bwd<0>(dm, grid, s, g, ldg, h, ldh, rows, x, ldx, (int)d_in, slope, partial_dw, partial_db);
     else if (act == 1) launch_bwd<1>(dm, grid, s, g, ldg, h, ldh, rows, x, ldx, (int)d_in, slope, partial_dw, partial_db);
     else launch_bwd<2>(dm, grid, s, g, ldg, h, ldh, rows, x, ldx, (int)d_in, slope, partial_dw, partial_db);
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_thin_linear_act_fwd_norm(int act, const float *x, int64_t ldx, int64_t rows, int64_t d_in,
+                                         int64_t d_out, const float *w, const float *b, float slope, float *h,
+                                         int64_t ldh, const float *mean, const float *var, float clip, float *xn,
+                                         int64_t ldn, float *col, int64_t col_ld, const xpa_cursor_t *cursor,
+                                         xpa_stream_t stream) {
+    if (rows <= 0 || d_in < 1 || d_in > kMaxIn || d_out != kCols || act < 0 || act > 2 || !x || !w || !b || !h ||
+        !mean || !var || !xn || ldx < d_in || ldh < d_out || ldn < d_in || (col && (!cursor || col_ld < d_in)))
+        return (int)hipErrorInvalidValue;
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t tiles = (rows + 7) / 8;
+    const dim3 grid((unsigned)(tiles < kFwdGrid ? tiles : kFwdGrid));
+    const int dm = dmax_for((int)d_in);
+#define XPA_FWDN(A_, D_)                                                                                            \
+    hipLaunchKernelGGL((thin_fwd_norm_kernel<A_, D_>), grid, dim3(256), 0, s, x, ldx, rows, (int)d_in, w, b, slope, h, \
+                       ldh, mean, var, clip, xn, ldn, col, col_ld, cursor)
+#define XPA_FWDN_D(A_)              \
+    if (dm == 8) XPA_FWDN(A_, 8);   \
+    else if (dm == 20) XPA_FWDN(A_, 20); \
+    else if (dm == 32) XPA_FWDN(A_, 32); \
+    else XPA_FWDN(A_, 64);
+    if (act == 0) { XPA_FWDN_D(0) }
+    else if (act == 1) { XPA_FWDN_D(1) }
+    else { XPA_FWDN_D(2) }
+#undef XPA_FWDN_D
+#undef XPA_FWDN
     return xpa_launch_status();
 }

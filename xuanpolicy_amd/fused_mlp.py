@@ -138,7 +138,21 @@ class FusedActorCritic:
             outs.append(h)
         return outs
 
-    def _rep_forward(self, x):
+    def _rep_forward(self, x, norm=None):
+        if norm is not None:
+            # x RAW: observation normalisation fused into the first layer (xpa_thin_linear_act_fwd_norm);
+            # norm = (mean, var, clip, xn_out, col, col_ld, cursor)
+            if not self.thin0:
+                raise ValueError("fused normalisation needs the thin first layer (K13)")
+            lin, code, slope = self.rep[0]
+            mean, var, clip, xn, col, col_ld, cursor = norm
+            h = torch.empty((x.shape[0], lin.out_features), dtype=torch.float32, device=x.device)
+            _lib.check(ops.lib().xpa_thin_linear_act_fwd_norm(
+                code, ops._p(x), x.stride(0), x.shape[0], lin.in_features, lin.out_features, ops._p(lin.weight),
+                ops._p(lin.bias), slope, ops._p(h), h.stride(0), ops._p(mean), ops._p(var), float(clip), ops._p(xn),
+                xn.stride(0), ops._p(col), int(col_ld), ops._p(cursor), ops._stream(x.device)),
+                "xpa_thin_linear_act_fwd_norm")
+            return [h] + self._chain_forward(self.rep[1:], h)
         if self.thin0 and x.dim() == 2 and x.dtype == torch.float32 and x.stride(1) == 1:
             lin, code, slope = self.rep[0]
             h = torch.empty((x.shape[0], lin.out_features), dtype=torch.float32, device=x.device)
@@ -183,9 +197,10 @@ class FusedActorCritic:
         return self.pair is not None
 
     @torch.no_grad()
-    def rollout_act(self, x, dist, cursor, seed, buf_act, buf_logp, buf_val, env_in, act_clip=1.0):
-        """Policy step of the rollout: trunk, paired hidden GEMM, then K14 (heads + sample + store)."""
-        rep_outs = self._rep_forward(x)
+    def rollout_act(self, x, dist, cursor, seed, buf_act, buf_logp, buf_val, env_in, act_clip=1.0, norm=None):
+        """Policy step of the rollout: trunk, paired hidden GEMM, then K14 (heads + sample + store).
+        norm: see _rep_forward (x is then the raw observation)."""
+        rep_outs = self._rep_forward(x, norm=norm)
         s = rep_outs[-1] if rep_outs else x
         z = F.linear(s, self.pair[0], self.pair[1])
         H = ops.HEAD_HIDDEN
