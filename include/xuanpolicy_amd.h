@@ -130,6 +130,11 @@ int xpa_policy_loss_fwd_bwd(int algo, int dist, int64_t batch, int64_t act_dim, 
 int xpa_policy_loss_finalize(int algo, int dist, int64_t batch, int64_t act_dim, const float *partials,
                              int64_t n_partials, float vf_coef, float ent_coef, float *scalars,
                              float *d_logstd, xpa_stream_t stream);
+/* The same, also writing sum(d_logstd^2) (0 for Categorical) into *sq_out (nullable): that gradient's
+ * share of the clip norm for xpa_clip_adam_step_partials. */
+int xpa_policy_loss_finalize_sq(int algo, int dist, int64_t batch, int64_t act_dim, const float *partials,
+                                int64_t n_partials, float vf_coef, float ent_coef, float *scalars, float *d_logstd,
+                                double *sq_out, xpa_stream_t stream);
 
 /* Epoch permutation for minibatch sampling (replaces the np.random.shuffle of an arange(buffer_size),
  * ppoclip_agent.py:76-81): out = a pseudo-random permutation of [0, n) keyed by (seed, counter)
@@ -212,6 +217,13 @@ int64_t xpa_grad_norm_num_partials(int64_t n);
 int xpa_clip_adam_step(float *param, float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
                        double *norm_partials, float max_norm, float lr, float beta1, float beta2, float eps,
                        int64_t step, float *total_norm_out, xpa_stream_t stream);
+/* K9 from squared-norm partials already written by the gradient producers (world size 1: the batched
+ * column-sum finalize's per-tile partials + the loss finalize's d logstd share): no norm pass over the
+ * flat gradient.  sq_partials: n_sq doubles summing to |grad|^2; the clip + Adam arithmetic is
+ * xpa_clip_adam_step's. */
+int xpa_clip_adam_step_partials(float *param, float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+                                const double *sq_partials, int64_t n_sq, float max_norm, float lr, float beta1,
+                                float beta2, float eps, int64_t step, float *total_norm_out, xpa_stream_t stream);
 
 /* K10 — activation backward fused with bias-gradient column sums for one MLP layer (row-major
  * [rows, cols]).  Replaces the activation backward and the bias-gradient reduction torch autograd runs
@@ -268,6 +280,16 @@ int xpa_head_fused_critic(int act, int64_t batch, int64_t hidden, int64_t ld, co
  * pointers).  Same fixed-order f64 sums as xpa_colsum_finalize. */
 int xpa_colsum_finalize_batch(int n_segs, const float *const *partials, const int64_t *n_partials,
                               const int64_t *cols, float *const *outs, xpa_stream_t stream);
+/* Column tiles (= blocks) of one batched finalize over these segments (n_partials rows x cols). */
+int64_t xpa_colsum_batch_tiles(int n_segs, const int64_t *n_partials, const int64_t *cols);
+/* xpa_colsum_finalize_batch that also produces the clip norm of its outputs: sq (nullable; tiles + 2
+ * doubles) holds at sq[0] a share written beforehand (e.g. xpa_policy_loss_finalize_sq's d logstd); each
+ * tile writes its sum of squared outputs to sq[1 + tile], and the last block to finish (atomic ticket,
+ * int32 [1], zero-initialised and left at zero) writes the fixed-order total of sq[0 .. tiles] to
+ * sq[1 + tiles] — the single partial xpa_clip_adam_step_partials then reads. */
+int xpa_colsum_finalize_batch_sq(int n_segs, const float *const *partials, const int64_t *n_partials,
+                                 const int64_t *cols, float *const *outs, double *sq, int32_t *ticket,
+                                 xpa_stream_t stream);
 
 /* K14 — rollout policy head: the last hidden activation and both output layers of the actor-critic
  * (gaussian.py:8-51 / categorical.py:16-58 forward in PPOCLIP_Agent._action, ppoclip_agent.py:50-57)

@@ -176,6 +176,14 @@ def test_fused_heads_match_loss_kernel_path(algo, discrete, act, rep_hidden, ent
         scale = ga.abs().max().item() + 1e-12
         assert (ga - gb).abs().max().item() <= 5e-5 * scale, (n1, (ga - gb).abs().max().item(), scale)
         assert not bool((x2.grad == -7.0).any()), n2   # every gradient written
+    # the clip norm's squared-sum partials written beside the gradients (xpa_clip_adam_step_partials)
+    if fm2.sq_ready is not None:
+        buf, cnt = fm2.sq_ready
+        sq_fused = float(buf[:cnt].sum())
+        sq_true = sum(float((x.grad.double() ** 2).sum()) for x in p2.parameters())
+        assert abs(sq_fused - sq_true) <= 1e-9 * sq_true, (sq_fused, sq_true)
+    else:   # the C2 / C4 fast path (paired heads on a [256] thin trunk) must cover every gradient
+        assert not (paired and rep_hidden == [256] and D <= 64)
 
 
 @pytest.mark.parametrize("rows,din,code", [(1000, 17, 1), (65536 + 5, 17, 1), (77, 4, 2), (4096, 33, 0),

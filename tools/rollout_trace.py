@@ -50,6 +50,26 @@ def summarize(db):
         print("%-60s dur %6.2f  gap-before %6.2f" % (k, statistics.median(d), statistics.median(g)))
     up = [r for r in it[posts[-1] + 1:]]
     print("update phase: %d kernels, span %.1f ms" % (len(up), (up[-1][2] - up[0][1]) / 1e6 if up else 0))
+    # one update = the kernels after one clip_adam launch up to the next update's last clip_adam
+    ends = [i for i, r in enumerate(up) if "clip_adam" in r[0]]
+    ends = ends[1::2] if len(ends) > 2 and "clip_adam" in up[ends[0] + 1][0] else ends
+    per = {}
+    spans = []
+    for a, b in zip(ends[4:-1], ends[5:]):
+        seg = up[a + 1:b + 1]
+        spans.append((seg[-1][2] - seg[0][1]) / 1e3)
+        prev_end = up[a][2]
+        for j, (n, s_, e) in enumerate(seg):
+            key = "%02d %s" % (j, n.split("(")[0][-50:])
+            d = per.setdefault(key, [[], []])
+            d[0].append((e - s_) / 1e3)
+            d[1].append((s_ - prev_end) / 1e3)
+            prev_end = e
+    if spans:
+        print("update span us: median %.1f over %d updates" % (statistics.median(spans), len(spans)))
+        for k, (d, g) in sorted(per.items()):
+            if len(d) >= len(spans) // 2:
+                print("%-60s dur %7.2f  gap-before %6.2f" % (k, statistics.median(d), statistics.median(g)))
 
 
 if __name__ == "__main__":

@@ -202,8 +202,10 @@ __global__ __launch_bounds__(256) void policy_loss_finalize_kernel(int algo, int
                                                                    const float *__restrict__ partials,
                                                                    int64_t n_partials, int width, float vf_coef,
                                                                    float ent_coef, float *__restrict__ scalars,
-                                                                   float *__restrict__ d_logstd) {
+                                                                   float *__restrict__ d_logstd,
+                                                                   double *__restrict__ sq_out) {
     __shared__ double tot[kPartBase];
+    __shared__ float s_dls[kMaxAct];
     const int ncols = kPartBase + (dist == XPA_DIST_GAUSSIAN ? A : 0);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int j = w; j < ncols; j += 4) {  // one wave per column, fixed lane order -> deterministic
@@ -212,10 +214,16 @@ __global__ __launch_bounds__(256) void policy_loss_finalize_kernel(int algo, int
         s = xpa_wave_sum(s);
         if (lane == 0) {
             if (j < kPartBase) tot[j] = s;
-            else d_logstd[j - kPartBase] = (float)(s - (double)ent_coef);
+            else d_logstd[j - kPartBase] = s_dls[j - kPartBase] = (float)(s - (double)ent_coef);
         }
     }
     __syncthreads();
+    if (threadIdx.x == 0 && sq_out) {  // this gradient's share of the clip norm (xpa_clip_adam_step_partials)
+        double q = 0.0;
+        if (dist == XPA_DIST_GAUSSIAN)
+            for (int a = 0; a < A; ++a) q += (double)s_dls[a] * (double)s_dls[a];
+        *sq_out = q;
+    }
     if (threadIdx.x == 0) {
         const double B = (double)batch;
         const double actor = -tot[0] / B;
@@ -271,14 +279,21 @@ XPA_API int xpa_policy_loss_fwd_bwd(int algo, int dist, int64_t batch, int64_t a
     return xpa_launch_status();
 }
 
-XPA_API int xpa_policy_loss_finalize(int algo, int dist, int64_t batch, int64_t act_dim, const float *partials,
-                                     int64_t n_partials, float vf_coef, float ent_coef, float *scalars,
-                                     float *d_logstd, xpa_stream_t stream) {
+XPA_API int xpa_policy_loss_finalize_sq(int algo, int dist, int64_t batch, int64_t act_dim, const float *partials,
+                                        int64_t n_partials, float vf_coef, float ent_coef, float *scalars,
+                                        float *d_logstd, double *sq_out, xpa_stream_t stream) {
     if (batch <= 0 || act_dim <= 0 || act_dim > kMaxAct || n_partials <= 0 || !partials || !scalars)
         return (int)hipErrorInvalidValue;
     if (dist == XPA_DIST_GAUSSIAN && !d_logstd) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(policy_loss_finalize_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, algo, dist, batch,
                        (int)act_dim, partials, n_partials, (int)xpa_loss_partial_width(act_dim), vf_coef, ent_coef,
-                       scalars, d_logstd);
+                       scalars, d_logstd, sq_out);
     return xpa_launch_status();
+}
+
+XPA_API int xpa_policy_loss_finalize(int algo, int dist, int64_t batch, int64_t act_dim, const float *partials,
+                                     int64_t n_partials, float vf_coef, float ent_coef, float *scalars,
+                                     float *d_logstd, xpa_stream_t stream) {
+    return xpa_policy_loss_finalize_sq(algo, dist, batch, act_dim, partials, n_partials, vf_coef, ent_coef, scalars,
+                                       d_logstd, nullptr, stream);
 }

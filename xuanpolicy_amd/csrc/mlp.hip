@@ -240,8 +240,11 @@ __global__ __launch_bounds__(256) void head_backward_vec4_kernel(int K, const fl
 constexpr int kColTile = 64;
 constexpr int kColGroups = 16;
 
+// sq != nullptr: also the tile's sum of squared outputs (f64, wave 0) into *sq — the gradient-norm
+// partial the clip + Adam step reads (xpa_clip_adam_step_partials), in place of a separate norm pass.
 __device__ __forceinline__ void colsum_tile(const float *__restrict__ part, int64_t G, int C, int c0,
-                                            float *__restrict__ out, double (*s_red)[kColTile]) {
+                                            float *__restrict__ out, double (*s_red)[kColTile],
+                                            double *__restrict__ sq = nullptr) {
     const int lane = threadIdx.x & (kColTile - 1), grp = threadIdx.x / kColTile;
     const int c = c0 + lane;
     double s = 0.0;
@@ -259,10 +262,18 @@ __device__ __forceinline__ void colsum_tile(const float *__restrict__ part, int6
     }
     s_red[grp][lane] = s;
     __syncthreads();
-    if (grp == 0 && c < C) {
-        double t = s_red[0][lane];
-        for (int g = 1; g < kColGroups; ++g) t += s_red[g][lane];
-        out[c] = (float)t;
+    if (grp == 0) {
+        float o = 0.f;
+        if (c < C) {
+            double t = s_red[0][lane];
+            for (int g = 1; g < kColGroups; ++g) t += s_red[g][lane];
+            o = (float)t;
+            out[c] = o;
+        }
+        if (sq) {  // grp 0 is wave 0 (kColTile == 64)
+            const double q = xpa_wave_sum((double)o * (double)o);
+            if (lane == 0) xpa_store_agent(sq, q);
+        }
     }
 }
 
@@ -274,6 +285,16 @@ __global__ __launch_bounds__(kColTile * kColGroups) void colsum_finalize_kernel(
 }
 
 constexpr int kMaxSegs = 16;
+// Segments with few partial rows (G <= kWideMaxG, e.g. the split-K slices of a weight gradient: G = 8,
+// C = 131 072) use 1024-column tiles, one column per thread summed over G in order; the others 64-column
+// tiles with 16 row groups (colsum_tile).
+constexpr int kWideTile = kColTile * kColGroups;
+constexpr int kWideMaxG = 32;
+
+__host__ __device__ inline int64_t seg_tiles(int64_t G, int64_t C) {
+    return G <= kWideMaxG ? (C + kWideTile - 1) / kWideTile : (C + kColTile - 1) / kColTile;
+}
+
 struct ColsumBatch {
     const float *part[kMaxSegs];
     float *out[kMaxSegs];
@@ -281,14 +302,67 @@ struct ColsumBatch {
     int C[kMaxSegs];
     int tile0[kMaxSegs + 1];  // first column tile of each segment
     int n;
+    // nullable: clip-norm partials.  sq[0] = a share written beforehand (d logstd, loss finalize),
+    // sq[1 + tile] = each tile's sum of squared outputs, and the last block to finish (ticket) writes
+    // the fixed-order total of sq[0 .. tiles] into sq[1 + tiles] and resets the ticket.
+    double *sq;
+    unsigned int *ticket;
 };
 
 __global__ __launch_bounds__(kColTile * kColGroups) void colsum_finalize_batch_kernel(ColsumBatch b) {
     __shared__ double s_red[kColGroups][kColTile];
+    __shared__ bool s_last;
     const int tile = blockIdx.x;
     int sg = 0;
     while (tile >= b.tile0[sg + 1]) ++sg;
-    colsum_tile(b.part[sg], b.G[sg], b.C[sg], (tile - b.tile0[sg]) * kColTile, b.out[sg], s_red);
+    double *sq = b.sq ? b.sq + 1 + tile : nullptr;
+    if (b.G[sg] <= kWideMaxG) {
+        const int64_t G = b.G[sg];
+        const int C = b.C[sg];
+        const int c = (tile - b.tile0[sg]) * kWideTile + (int)threadIdx.x;
+        const float *part = b.part[sg];
+        double acc = 0.0;
+        float o = 0.f;
+        if (c < C) {
+            for (int64_t k = 0; k < G; ++k) acc += (double)part[k * C + c];
+            o = (float)acc;
+            b.out[sg][c] = o;
+        }
+        if (sq) {
+            const double q = xpa_wave_sum((double)o * (double)o);
+            if ((threadIdx.x & 63) == 0) s_red[0][threadIdx.x >> 6] = q;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                double t = 0.0;
+                for (int w = 0; w < kWideTile / 64; ++w) t += s_red[0][w];
+                xpa_store_agent(sq, t);
+            }
+        }
+    } else {
+        colsum_tile(b.part[sg], b.G[sg], b.C[sg], (tile - b.tile0[sg]) * kColTile, b.out[sg], s_red, sq);
+    }
+    if (!b.sq) return;
+    xpa_drain();  // this block's partial (sc1 store) complete before its ticket
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = xpa_ticket(b.ticket) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    const int n = (int)gridDim.x + 1;  // sq[0 .. tiles]
+    // thread t sums a contiguous run of the partials in order, then the runs in thread order (fixed)
+    const int per = (n + kWideTile - 1) / kWideTile;
+    double acc = 0.0;
+    for (int i = threadIdx.x * per; i < n && i < ((int)threadIdx.x + 1) * per; ++i) acc += xpa_load_agent(b.sq + i);
+    __shared__ double s_all[kWideTile];
+    s_all[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = kWideTile / 2; off > 0; off >>= 1) {  // fixed-shape tree: deterministic
+        if ((int)threadIdx.x < off) s_all[threadIdx.x] += s_all[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        b.sq[n] = s_all[0];
+        *b.ticket = 0u;
+    }
 }
 
 }  // namespace
@@ -382,10 +456,20 @@ XPA_API int xpa_colsum_finalize(const float *partials, int64_t n_partials, int64
     return xpa_launch_status();
 }
 
-XPA_API int xpa_colsum_finalize_batch(int n_segs, const float *const *partials, const int64_t *n_partials,
-                                      const int64_t *cols, float *const *outs, xpa_stream_t stream) {
+XPA_API int64_t xpa_colsum_batch_tiles(int n_segs, const int64_t *n_partials, const int64_t *cols) {
+    int64_t tiles = 0;
+    for (int i = 0; i < n_segs; ++i) tiles += seg_tiles(n_partials[i], cols[i]);
+    return tiles;
+}
+
+XPA_API int xpa_colsum_finalize_batch_sq(int n_segs, const float *const *partials, const int64_t *n_partials,
+                                         const int64_t *cols, float *const *outs, double *sq, int32_t *ticket,
+                                         xpa_stream_t stream) {
     if (n_segs <= 0 || n_segs > kMaxSegs || !partials || !n_partials || !cols || !outs) return (int)hipErrorInvalidValue;
+    if (sq && !ticket) return (int)hipErrorInvalidValue;
     ColsumBatch b{};
+    b.sq = sq;
+    b.ticket = (unsigned int *)ticket;
     b.n = n_segs;
     int64_t tiles = 0;
     for (int i = 0; i < n_segs; ++i) {
@@ -396,10 +480,15 @@ XPA_API int xpa_colsum_finalize_batch(int n_segs, const float *const *partials, 
         b.G[i] = n_partials[i];
         b.C[i] = (int)cols[i];
         b.tile0[i] = (int)tiles;
-        tiles += (cols[i] + kColTile - 1) / kColTile;
+        tiles += seg_tiles(n_partials[i], cols[i]);
     }
     b.tile0[n_segs] = (int)tiles;
     hipLaunchKernelGGL(colsum_finalize_batch_kernel, dim3((unsigned)tiles), dim3(kColTile * kColGroups), 0,
                        (hipStream_t)stream, b);
     return xpa_launch_status();
+}
+
+XPA_API int xpa_colsum_finalize_batch(int n_segs, const float *const *partials, const int64_t *n_partials,
+                                      const int64_t *cols, float *const *outs, xpa_stream_t stream) {
+    return xpa_colsum_finalize_batch_sq(n_segs, partials, n_partials, cols, outs, nullptr, nullptr, stream);
 }

@@ -94,6 +94,31 @@ inline int64_t norm_blocks(int64_t n) {
 
 XPA_API int64_t xpa_grad_norm_num_partials(int64_t n) { return norm_blocks(n); }
 
+// The clip + Adam step from squared-norm partials the gradient producers already wrote (the batched
+// column-sum finalize's per-tile partials and the loss finalize's d logstd share, world size 1): the norm
+// pass over the flat gradient is skipped.  sq_partials: n_sq doubles whose sum is |grad|^2.
+XPA_API int xpa_clip_adam_step_partials(float *param, float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+                                        const double *sq_partials, int64_t n_sq, float max_norm, float lr,
+                                        float beta1, float beta2, float eps, int64_t step, float *total_norm_out,
+                                        xpa_stream_t stream) {
+    if (n <= 0 || step < 1 || !param || !grad || !exp_avg || !exp_avg_sq || !sq_partials || n_sq <= 0 ||
+        n_sq > 0x7fffffff)
+        return (int)hipErrorInvalidValue;
+    if (((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16)
+        return (int)hipErrorInvalidValue;
+    const double bc1 = 1.0 - pow((double)beta1, (double)step);
+    const double bc2 = 1.0 - pow((double)beta2, (double)step);
+    const float step_size = (float)((double)lr / bc1);
+    const float inv_bc2_sqrt = (float)(1.0 / sqrt(bc2));
+    int64_t ab = (n / 4 + kOptThreads - 1) / kOptThreads;
+    if (ab < 1) ab = 1;
+    if (ab > 2048) ab = 2048;
+    hipLaunchKernelGGL(clip_adam_kernel, dim3((unsigned)ab), dim3(kOptThreads), 0, (hipStream_t)stream, param, grad,
+                       exp_avg, exp_avg_sq, n, sq_partials, (int)n_sq, max_norm, beta1, beta2, step_size,
+                       inv_bc2_sqrt, eps, total_norm_out);
+    return xpa_launch_status();
+}
+
 XPA_API int xpa_clip_adam_step(float *param, float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
                                double *norm_partials, float max_norm, float lr, float beta1, float beta2, float eps,
                                int64_t step, float *total_norm_out, xpa_stream_t stream) {

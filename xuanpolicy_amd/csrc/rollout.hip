@@ -169,17 +169,17 @@ __global__ __launch_bounds__(256) void rms_partials_kernel(const float *__restri
                 ts += s_sum[k * dc + threadIdx.x];
                 tq += s_sq[k * dc + threadIdx.x];
             }
-            part[(int64_t)blockIdx.x * dim + c0 + threadIdx.x] = ts;
-            part[(np + blockIdx.x) * dim + c0 + threadIdx.x] = tq;
+            xpa_store_agent(part + (int64_t)blockIdx.x * dim + c0 + threadIdx.x, ts);  // sc1: handed to the
+            xpa_store_agent(part + (np + blockIdx.x) * dim + c0 + threadIdx.x, tq);    // merging block
         }
         __syncthreads();
     }
     if (MERGE) {
-        __threadfence();  // this block's partials visible device-wide before its ticket
-        if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1u) == (unsigned)(np - 1);
+        xpa_drain();
+        __syncthreads();
+        if (threadIdx.x == 0) s_last = xpa_ticket(ticket) == (unsigned)(np - 1);
         __syncthreads();
         if (!s_last) return;
-        __threadfence();
         rms_merge_body(part, np, n, dim, mean, var, count);
         if (threadIdx.x == 0) *ticket = 0u;
     }
@@ -188,9 +188,9 @@ __global__ __launch_bounds__(256) void rms_partials_kernel(const float *__restri
 // Sum of the partials (fixed order) -> batch mean/var, then update_from_moments
 // (statistic_tools.py:86-112) into mean/var (f32) and count (f64).  mean doubles as the shift the
 // partials were taken around.
-// Every (partial, column) sum / square is loaded by its own thread into LDS in one round trip (plain loads:
-// the caller has passed an agent-scope acquire fence when the partials come from other blocks of the
-// same launch), then each column is summed over the partials in block order (deterministic).
+// Every (partial, column) sum / square is loaded by its own thread into LDS in one round trip (sc1 loads:
+// the partials may come from other blocks of the same launch), then each column is summed over the
+// partials in block order (deterministic).
 constexpr int kMergeLds = 2048;  // doubles of LDS staging: np * dim <= 1024 (else per-column global loads)
 __device__ void rms_merge_body(const double *part, int64_t np, int64_t n, int64_t dim, float *__restrict__ mean,
                                float *__restrict__ var, double *__restrict__ count) {
@@ -198,13 +198,13 @@ __device__ void rms_merge_body(const double *part, int64_t np, int64_t n, int64_
     const double c0 = *count;
     const bool staged = np * dim * 2 <= kMergeLds;
     if (staged)
-        for (int64_t i = threadIdx.x; i < 2 * np * dim; i += blockDim.x) s_part[i] = part[i];
+        for (int64_t i = threadIdx.x; i < 2 * np * dim; i += blockDim.x) s_part[i] = xpa_load_agent(part + i);
     __syncthreads();
     for (int64_t d = threadIdx.x; d < dim; d += blockDim.x) {
         double s = 0.0, q = 0.0;
         for (int64_t p = 0; p < np; ++p) {
-            s += staged ? s_part[p * dim + d] : part[p * dim + d];
-            q += staged ? s_part[(np + p) * dim + d] : part[(np + p) * dim + d];
+            s += staged ? s_part[p * dim + d] : xpa_load_agent(part + p * dim + d);
+            q += staged ? s_part[(np + p) * dim + d] : xpa_load_agent(part + (np + p) * dim + d);
         }
         const double ms = s / (double)n;
         const double m0 = (double)mean[d], v0 = (double)var[d];
@@ -541,29 +541,28 @@ __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
     cnt = xpa_block_sum(cnt, s_red, nw);
     sum = xpa_block_sum(sum, s_red, nw);
     sumsq = xpa_block_sum(sumsq, s_red, nw);
-    if (threadIdx.x == 0) {
-        partials[3 * blockIdx.x] = cnt;
-        partials[3 * blockIdx.x + 1] = sum;
-        partials[3 * blockIdx.x + 2] = sumsq;
-        __threadfence();
-        s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    if (threadIdx.x == 0) {  // sc1 stores, drained before the ticket (no L2 write-back fence)
+        xpa_store_agent(partials + 3 * blockIdx.x, cnt);
+        xpa_store_agent(partials + 3 * blockIdx.x + 1, sum);
+        xpa_store_agent(partials + 3 * blockIdx.x + 2, sumsq);
+        xpa_drain();
+        s_last = xpa_ticket(ticket) == gridDim.x - 1;
     }
     __syncthreads();
     if (!s_last) return;
-    __threadfence();  // agent-scope acquire: the other blocks' partials, plain loads below
     // all of the last block's threads load the partials at once (one round trip), thread 0 sums them in
     // block order (deterministic)
     __shared__ double s_pp[3 * 1024];
     const bool staged = gridDim.x <= 1024;
     if (staged)
-        for (unsigned i = threadIdx.x; i < 3 * gridDim.x; i += kPostThreads) s_pp[i] = partials[i];
+        for (unsigned i = threadIdx.x; i < 3 * gridDim.x; i += kPostThreads) s_pp[i] = xpa_load_agent(partials + i);
     __syncthreads();
     if (threadIdx.x != 0) return;
     double c = 0.0, s1 = 0.0, s2 = 0.0;
     for (unsigned g = 0; g < gridDim.x; ++g) {  // fixed order -> deterministic
-        c += staged ? s_pp[3 * g] : partials[3 * g];
-        s1 += staged ? s_pp[3 * g + 1] : partials[3 * g + 1];
-        s2 += staged ? s_pp[3 * g + 2] : partials[3 * g + 2];
+        c += staged ? s_pp[3 * g] : xpa_load_agent(partials + 3 * g);
+        s1 += staged ? s_pp[3 * g + 1] : xpa_load_agent(partials + 3 * g + 1);
+        s2 += staged ? s_pp[3 * g + 2] : xpa_load_agent(partials + 3 * g + 2);
     }
     if (c > 0.0) {
         const double bm = s1 / c;

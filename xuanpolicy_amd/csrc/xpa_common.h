@@ -57,3 +57,21 @@ __device__ __forceinline__ T xpa_block_sum(T v, T *scratch, int nwaves) {
     for (int i = 0; i < nwaves; ++i) s += scratch[i];
     return s;
 }
+
+// ---- inter-workgroup hand-off inside one launch (ticketed "last block merges") -------------------
+// Producer: xpa_store_agent for every handed-off value (write-through, sc1), then xpa_drain() and the
+// block barrier, then one lane takes the ticket (xpa_ticket).  Consumer (the last block): xpa_load_agent
+// (sc1 loads).  No __threadfence(): on gfx950 an agent-scope release is a full L2 write-back
+// (buffer_wbl2 sc1) per block — 76 us for a ~150-block finalize behind the update's GEMMs (r01).
+template <typename T>
+__device__ __forceinline__ void xpa_store_agent(T *p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T xpa_load_agent(const T *p) {
+    return __hip_atomic_load(const_cast<T *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void xpa_drain() { __builtin_amdgcn_s_waitcnt(0); }
+__device__ __forceinline__ unsigned xpa_ticket(unsigned *t) {
+    return __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}

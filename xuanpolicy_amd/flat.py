@@ -127,17 +127,27 @@ class FusedClipAdam:
                                   "exp_avg_sq": self.exp_avg_sq[off:off + k].view_as(p)}
         self._step_t.fill_(float(self.step_count))
 
-    def step(self, max_norm):
+    def step(self, max_norm, sq=None):
+        """sq = (float64 partials, count) summing to |grad|^2, written by the gradient producers: one launch
+        (xpa_clip_adam_step_partials) instead of the norm pass + step."""
         g = self.optimizer.param_groups[0]
         self.step_count += 1
         b1, b2 = g["betas"]
         lr = g["lr"]
         lr = float(lr) if not isinstance(lr, torch.Tensor) else float(lr.item())
-        rc = ops.lib().xpa_clip_adam_step(ops._p(self.fs.param), ops._p(self.fs.flat), ops._p(self.exp_avg),
-                                          ops._p(self.exp_avg_sq), self.fs.numel, ops._p(self.partials),
-                                          float(max_norm) if max_norm else 0.0, lr, float(b1), float(b2),
-                                          float(g["eps"]), self.step_count, ops._p(self.total_norm),
-                                          ops._stream(self.fs.param.device))
-        _lib.check(rc, "xpa_clip_adam_step")
+        if sq is not None:
+            buf, count = sq
+            rc = ops.lib().xpa_clip_adam_step_partials(
+                ops._p(self.fs.param), ops._p(self.fs.flat), ops._p(self.exp_avg), ops._p(self.exp_avg_sq),
+                self.fs.numel, ops._p(buf), int(count), float(max_norm) if max_norm else 0.0, lr, float(b1),
+                float(b2), float(g["eps"]), self.step_count, ops._p(self.total_norm), ops._stream(self.fs.param.device))
+            _lib.check(rc, "xpa_clip_adam_step_partials")
+        else:
+            rc = ops.lib().xpa_clip_adam_step(ops._p(self.fs.param), ops._p(self.fs.flat), ops._p(self.exp_avg),
+                                              ops._p(self.exp_avg_sq), self.fs.numel, ops._p(self.partials),
+                                              float(max_norm) if max_norm else 0.0, lr, float(b1), float(b2),
+                                              float(g["eps"]), self.step_count, ops._p(self.total_norm),
+                                              ops._stream(self.fs.param.device))
+            _lib.check(rc, "xpa_clip_adam_step")
         self._step_t.fill_(float(self.step_count))
         self.optimizer._opt_called = True  # the LR scheduler checks that an optimizer step happened

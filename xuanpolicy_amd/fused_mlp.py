@@ -118,6 +118,10 @@ class FusedActorCritic:
             raise ValueError("policy has parameters outside the Linear chains")
         self._partials = {}
         self._cq = ops.ColsumQueue()
+        self._sq = None
+        self.sq_ready = None
+        self._params = list(policy.parameters())
+        self._n_params = None
 
     @staticmethod
     def _head_fusable(layers):
@@ -265,27 +269,42 @@ class FusedActorCritic:
                  "w_critic": lin_co.weight.grad, "b_critic": lin_co.bias.grad, "bh_critic": lin_ch.bias.grad}
         if self.logstd is not None:
             grads["logstd"] = self.logstd.grad
+        if self._sq is None:
+            self._sq = torch.zeros(self.SQ_SLOTS, dtype=torch.float64, device=s.device)
+        self.sq_ready = None
         scalars, dz_a, dz_c = ops.fused_heads(algo, dist, self._hws, z_a, lin_ao.weight, lin_ao.bias, (a_code, a_slope),
                                               z_c, lin_co.weight, lin_co.bias, (c_code, c_slope), self.logstd, act,
                                               adv, ret, old_logp=old_logp, idx=idx, adv_partials=adv_partials,
                                               clip_range=clip_range, vf_coef=vf_coef, ent_coef=ent_coef, grads=grads,
-                                              colsum_queue=self._cq, gemm=gemm)
+                                              colsum_queue=self._cq, gemm=gemm, sq_logstd=self._sq.data_ptr())
         have_rep = len(self.rep) > 0
         if paired:   # dW of both hidden layers and dX (K = 512, no accumulate pass) as single GEMMs
             dz = self._hws.dz_pair
-            self._weight_grad(dz, s, self.pair[2])
+            self._weight_grad(dz, s, self.pair[2], queue=self._cq)
             if have_rep:
                 self._chain_backward(self.rep, [x] + rep_outs[:-1], rep_outs, torch.mm(dz, self.pair[0]),
                                      need_dx=False, thin_first=self.thin0)
-            self._cq.flush(s.device)   # every deferred column-sum finalize in one launch
+            self._flush_with_norm(s.device)   # every deferred column-sum finalize in one launch
             return scalars
         ds = self._from_dz(self.actor[:-1], [s] + a_outs, a_outs, dz_a, need_dx=have_rep)
         ds = self._from_dz(self.critic[:-1], [s] + c_outs, c_outs, dz_c, need_dx=have_rep, accumulate=ds)
         if have_rep:
             r_in = [x] + rep_outs[:-1]
             self._chain_backward(self.rep, r_in, rep_outs, ds, need_dx=False, thin_first=self.thin0)
-        self._cq.flush(s.device)
+        self._flush_with_norm(s.device)
         return scalars
+
+    SQ_SLOTS = 16384   # clip-norm partials: slot 0 = d logstd, then one per finalize column tile
+
+    def _flush_with_norm(self, device):
+        """Flush the column-sum finalizes, writing the clip norm's squared-sum partials beside them.  When
+        those outputs plus d logstd are every parameter's gradient, sq_ready = (partials, count) lets the
+        clip + Adam step skip its norm pass (xpa_clip_adam_step_partials)."""
+        total, written = self._cq.flush(device, sq=self._sq)
+        covered = written + (self.logstd.numel() if self.logstd is not None else 0)
+        if self._n_params is None:
+            self._n_params = sum(p.numel() for p in self._params)
+        self.sq_ready = (total, 1) if total is not None and covered == self._n_params else None
 
     def _from_dz(self, layers, inputs, outs, dz, need_dx, accumulate=None):
         """Backward from the pre-activation gradient dz of layers[-1] (its bias gradient already
@@ -316,13 +335,28 @@ class FusedActorCritic:
                                         ops._p(g) if code else None, ops._p(part), s), "xpa_act_bwd_colsum")
         _lib.check(L.xpa_colsum_finalize(ops._p(part), part.shape[0], cols, ops._p(out), s), "xpa_colsum_finalize")
 
-    @staticmethod
-    def _weight_grad(dz, x, out):
+    def _weight_grad(self, dz, x, out, queue=None):
+        """dW = dz^T x.  Split-K (a batched GEMM over slices of the batch) when the GEMM alone would not
+        fill the chip; with `queue` the slice sum is one more segment of the batched column-sum finalize
+        (f64, fixed order) instead of its own reduction launch."""
         B, n_out = dz.shape
         n_in = x.shape[1]
         s = _splitk_splits(B, n_out, n_in)
+        if queue is not None:   # (s == 1: the finalize only copies, so every gradient still passes through it)
+            key = ("splitk", s, n_out, n_in)
+            ws = self._partials.get(key)
+            if ws is None:
+                ws = torch.empty((s, n_out, n_in), dtype=torch.float32, device=dz.device)
+                self._partials[key] = ws
+            if s > 1:
+                torch.bmm(dz.view(s, B // s, n_out).transpose(1, 2), x.reshape(s, B // s, n_in), out=ws)
+            else:
+                torch.mm(dz.t(), x, out=ws[0])
+            queue.add(ws.view(s, n_out * n_in), out.view(-1))
+            return
         if s > 1:
-            torch.sum(torch.bmm(dz.view(s, B // s, n_out).transpose(1, 2), x.reshape(s, B // s, n_in)), dim=0, out=out)
+            torch.sum(torch.bmm(dz.view(s, B // s, n_out).transpose(1, 2), x.reshape(s, B // s, n_in)), dim=0,
+                      out=out)
         else:
             torch.mm(dz.t(), x, out=out)
 

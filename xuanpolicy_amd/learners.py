@@ -92,12 +92,15 @@ class _FusedPolicyGradient(Learner):
             self._fm = fm
         return fm or None
 
-    def _sync_clip_step(self):
+    def _sync_clip_step(self, sq=None):
+        """sq = (partials, count): squared-norm partials of the complete gradient written by its producers
+        (valid only without a gradient all-reduce): the fused step skips its norm pass."""
         if self.grad_sync is not None:
             self.grad_sync(self._params)
+            sq = None
         fused = getattr(self, "fused_opt", None)
         if fused is not None:
-            fused.step(self._max_norm if self._use_clip else 0.0)  # xpa_clip_adam_step (K9)
+            fused.step(self._max_norm if self._use_clip else 0.0, sq=sq)  # xpa_clip_adam_step (K9)
         else:
             if self._use_clip:
                 torch.nn.utils.clip_grad_norm_(self._params, self._max_norm)
@@ -115,7 +118,7 @@ class _FusedPolicyGradient(Learner):
             scalars = fm.loss_backward(ctx, self.algo, self.dist, act, adv, ret, old_logp=old_logp, idx=idx,
                                        adv_partials=adv_partials, clip_range=self.clip_range, vf_coef=self.vf_coef,
                                        ent_coef=self.ent_coef)
-            self._sync_clip_step()
+            self._sync_clip_step(sq=fm.sq_ready)
             return scalars
         if fm is not None:
             head, logstd, v, ctx = fm.forward(obs)

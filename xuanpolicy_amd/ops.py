@@ -392,6 +392,7 @@ class ColsumQueue:
     def __init__(self):
         self.items = []
         self._plans = {}
+        self._ticket = None
 
     def add(self, part, out):
         _req(part, "partials", torch.float32)
@@ -400,9 +401,12 @@ class ColsumQueue:
             raise ValueError("partials must be [G, C] and out must have C elements")
         self.items.append((part, out))
 
-    def flush(self, device=None):
+    def flush(self, device=None, sq=None):
+        """Launch the queued finalizes.  sq (float64 tensor, >= tiles + 2 entries, sq[0] written beforehand):
+        when the queue fits one launch, also the clip norm of the outputs + sq[0], left at sq[1 + tiles]
+        (xpa_colsum_finalize_batch_sq).  Returns (that total's view or None, output elements written)."""
         if not self.items:
-            return
+            return None, 0
         key = tuple((p.data_ptr(), p.shape[0], p.shape[1], o.data_ptr()) for p, o in self.items)
         plan = self._plans.get(key)
         if plan is None:
@@ -412,18 +416,32 @@ class ColsumQueue:
                 n = len(chunk)
                 arrs = ((ctypes.c_void_p * n)(*[c[0] for c in chunk]), (ctypes.c_int64 * n)(*[c[1] for c in chunk]),
                         (ctypes.c_int64 * n)(*[c[2] for c in chunk]), (ctypes.c_void_p * n)(*[c[3] for c in chunk]))
-                plan.append((n, arrs, [ctypes.cast(a, ctypes.c_void_p) for a in arrs]))
+                tiles = int(lib().xpa_colsum_batch_tiles(n, ctypes.cast(arrs[1], ctypes.c_void_p),
+                                                         ctypes.cast(arrs[2], ctypes.c_void_p)))
+                plan.append((n, arrs, [ctypes.cast(a, ctypes.c_void_p) for a in arrs], tiles))
             self._plans[key] = plan
-        s = _stream(device if device is not None else self.items[0][0].device)
+        dev = device if device is not None else self.items[0][0].device
+        s = _stream(dev)
         L = lib()
-        for n, _keep, args in plan:
-            _lib.check(L.xpa_colsum_finalize_batch(n, *args, s), "xpa_colsum_finalize_batch")
+        total = None
+        if sq is not None and len(plan) == 1 and plan[0][3] + 2 <= sq.numel():
+            if self._ticket is None:
+                self._ticket = torch.zeros((1,), dtype=torch.int32, device=dev)
+            n, _keep, args, tiles = plan[0]
+            _lib.check(L.xpa_colsum_finalize_batch_sq(n, *args, _p(sq), _p(self._ticket), s),
+                       "xpa_colsum_finalize_batch_sq")
+            total = sq[1 + tiles:2 + tiles]
+        else:
+            for n, _keep, args, _tiles in plan:
+                _lib.check(L.xpa_colsum_finalize_batch(n, *args, s), "xpa_colsum_finalize_batch")
+        written = sum(o.numel() for _, o in self.items)
         self.items = []
+        return total, written
 
 
 def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, w_critic, b_critic, act_critic,
                 logstd, act, adv, ret, old_logp=None, idx=None, adv_partials=None, clip_range=0.2, vf_coef=0.25,
-                ent_coef=0.0, grads=None, colsum_queue=None, gemm=None):
+                ent_coef=0.0, grads=None, colsum_queue=None, gemm=None, sq_logstd=None):
     """K12 actor + critic heads, loss finalize and the column-sum finalizes.
 
     z_*: hidden pre-activations [B, 256] (unit column stride; row stride = the workspace dz row stride,
@@ -501,8 +519,10 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
     d_logstd = g.get("logstd")
     if dist == "gaussian" and d_logstd is None:
         d_logstd = torch.empty((K,), dtype=torch.float32, device=dev)
-    _lib.check(L.xpa_policy_loss_finalize(ALGO[algo], DIST[dist], B, K, _p(ws.loss_partials), ws.G, float(vf_coef),
-                                          float(ent_coef), _p(ws.scalars), _p(d_logstd), s), "xpa_policy_loss_finalize")
+    # sq_logstd: device address of one double receiving sum(d_logstd^2) (the clip norm's share of logstd)
+    _lib.check(L.xpa_policy_loss_finalize_sq(ALGO[algo], DIST[dist], B, K, _p(ws.loss_partials), ws.G,
+                                             float(vf_coef), float(ent_coef), _p(ws.scalars), _p(d_logstd),
+                                             sq_logstd, s), "xpa_policy_loss_finalize")
     queue = colsum_queue if colsum_queue is not None else ColsumQueue()
     for key, part in (("w_actor", ws.p_dw_actor), ("b_actor", ws.p_dbo_actor), ("bh_actor", ws.p_dbh_actor),
                       ("w_critic", ws.p_dw_critic), ("b_critic", ws.p_dbo_critic), ("bh_critic", ws.p_dbh_critic)):
