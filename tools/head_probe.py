@@ -22,7 +22,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 sys.path.insert(0, REPO)
 OUT = os.path.join(HERE, "_probe")
-VARIANTS = {0: "full", 1: "gemm only", 2: "epilogue only", 3: "staging only"}
+VARIANTS = {0: "full", 1: "gemm only", 2: "epilogue only", 3: "staging only", 4: "epilogue without dz stores",
+            5: "epilogue without phase 2", 6: "gemm without operand DMAs"}
 
 
 def build():

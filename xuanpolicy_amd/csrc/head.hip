@@ -226,12 +226,12 @@ struct HeadEpi {
 #pragma unroll 4
             for (int j = 0; j < 16; ++j) {
                 const float4 hv = *reinterpret_cast<const float4 *>(hrow + 4 * j);
+                // unconditional (rows o >= K re-read row 0; their sums are never used): the KMAX scalar
+                // loads of a step issue together instead of one branch + load + wait per output
 #pragma unroll
                 for (int o = 0; o < KMAX; ++o) {
-                    if (o < K) {
-                        const float4 w4 = *reinterpret_cast<const float4 *>(wq + o * kH + 4 * j);
-                        p[o] += hv.x * w4.x + hv.y * w4.y + hv.z * w4.z + hv.w * w4.w;
-                    }
+                    const float4 w4 = *reinterpret_cast<const float4 *>(wq + (o < K ? o : 0) * kH + 4 * j);
+                    p[o] += hv.x * w4.x + hv.y * w4.y + hv.z * w4.z + hv.w * w4.w;
                 }
             }
 #pragma unroll
@@ -331,19 +331,58 @@ struct HeadEpi {
         }
         __syncthreads();
         // ---- phase 2: column owner t ----
+#if XPA_HEAD_PROBE == 5  // 5 = epilogue alone without phase 2
+        const int nr = 0;
+#else
         const int nr = (int)min((int64_t)kTile, batch - tile * kTile);
+#endif
         float *dzt = dz + tile * kTile * ld + t;
-        for (int r = 0; r < nr; ++r) {
+        // rows in groups of 4: every LDS read of the group (h, and the d-head rows as 16-B broadcasts)
+        // issued before the arithmetic, which keeps the row order of the accumulations (bitwise the
+        // same sums as one row at a time)
+        int r = 0;
+        for (; r + 4 <= nr; r += 4) {
+            float hv[4], gq[4][KP];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                hv[u] = s_h[(r + u) * kS + t];
+#pragma unroll
+                for (int q = 0; q < KP; q += 4) {
+                    const float4 g4 = *reinterpret_cast<const float4 *>(&s_dh[r + u][q]);
+                    gq[u][q] = g4.x;
+                    gq[u][q + 1] = g4.y;
+                    gq[u][q + 2] = g4.z;
+                    gq[u][q + 3] = g4.w;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                float d = 0.f;
+#pragma unroll
+                for (int o = 0; o < KMAX; ++o) {  // o >= K: s_dh and wc are 0 (accumulator unused)
+                    d += gq[u][o] * wc[o];
+                    acc_dw[o] += gq[u][o] * hv[u];
+                }
+                d *= act_g<ACT>(hv[u], slope);
+#if XPA_HEAD_PROBE != 4  // 4 = epilogue alone without the dz stores
+                __builtin_nontemporal_store(d, dzt + (r + u) * ld);
+#endif
+                acc_dbh += d;
+            }
+        }
+        for (; r < nr; ++r) {
             const float h = s_h[r * kS + t];
             float d = 0.f;
 #pragma unroll
-            for (int o = 0; o < KMAX; ++o) {  // o >= K: s_dh and wc are 0 (accumulator unused)
+            for (int o = 0; o < KMAX; ++o) {
                 const float g = s_dh[r][o];
                 d += g * wc[o];
                 acc_dw[o] += g * h;
             }
             d *= act_g<ACT>(h, slope);
+#if XPA_HEAD_PROBE != 4
             __builtin_nontemporal_store(d, dzt + r * ld);
+#endif
             acc_dbh += d;
         }
         __syncthreads();  // s_h / s_dh reused by the next tile
@@ -433,61 +472,74 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(XPA_HEAD_KERNEL_PARAM
 
 // K16: the hidden layer's GEMM itself on the fp32 matrix cores, z = x Wh^T + bh for a [64 x 256] tile
 // (v_mfma_f32_32x32x2_f32: exact f32 fma chains), then the K12 epilogue on the tile in LDS — z never
-// goes to HBM.  Wave w owns columns [64w, 64w + 64) as 2 x 2 tiles of 32 x 32 (64 accumulator regs);
-// k runs in chunks of 16, double-buffered in LDS as [k parity h][row][k / 2] images (row stride 12
-// floats: the 16-lane groups of each ds_read_b128 hit 16 distinct 4-bank slots), the next chunk's
-// global loads in flight during the current chunk's 32 MFMAs per wave.
+// goes to HBM.  Wave w owns columns [64w, 64w + 64) as 2 x 2 tiles of 32 x 32 (64 accumulator regs).
+// Operands are staged by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip) in chunks of 16 k
+// through a 3-stage ring: chunk c + 2 is in flight while chunk c feeds the MFMAs, each wave waits only
+// for its own chunk-c DMAs (counted vmcnt) before the one barrier per chunk.  A stage holds the A image
+// (64 rows of x) and the B image (256 rows of Wh), every row 64 B = four 16-B slots, slot p of row r
+// holding k quad q = p ^ ((r >> 2) & 3) — the swizzle is applied to the per-lane GLOBAL address (the DMA
+// writes lane-linear), and makes the 16-lane groups of each ds_read_b128 cover the 16 slots of a bank
+// row once.  Lane (i, h) reads quads h and h + 2 of its row; component s of quad q is k = 4q + s and is
+// fed to the MFMA as its k = h: any k order is exact as long as A and B agree.
 constexpr int kKin = 256;
 constexpr int kKC = 16;
-constexpr int kPS = 12;
-constexpr int kAImg = 2 * kTile * kPS;
-constexpr int kBImg = 2 * kH * kPS;
-constexpr int kStage = kAImg + kBImg;
-static_assert(2 * kStage <= kTile * kS, "operand stages share the epilogue tile");
+constexpr int kAImg = kTile * kKC;  // floats
+constexpr int kBImg = kH * kKC;
+constexpr int kStage = kAImg + kBImg;  // 20 KiB
+constexpr int kStages = 3;
+constexpr int kChunks = kKin / kKC;
+static_assert(kStages * kStage <= kTile * kS, "operand stages share the epilogue tile");
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) char lds_char_t;
 
-__device__ __forceinline__ void gemm_load(const float *__restrict__ x, int64_t ldx, const float *__restrict__ Wh,
-                                          int64_t r0, int64_t batch, int k0, float4 &ra, float4 (&rb)[4]) {
-    const int t = threadIdx.x;
-    const int row = t >> 2, q = t & 3;
-    ra = (r0 + row < batch) ? *reinterpret_cast<const float4 *>(x + (r0 + row) * ldx + k0 + 4 * q)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int lin = j * 256 + t, c = lin >> 2, q2 = lin & 3;
-        rb[j] = *reinterpret_cast<const float4 *>(Wh + c * kKin + k0 + 4 * q2);
-    }
+// One global_load_lds_dwordx4 (lane l's 16 B land at lds_wave_base + 16 l).  Issued from inline asm: the
+// builtin form makes hipcc wait vmcnt(0) before every ds_read it cannot prove disjoint from an in-flight
+// DMA — i.e. before each chunk's fragment reads, draining the ring; here the waits are the counted ones
+// of the k-loop (and its last chunk waits vmcnt(0), so no compiler-counted wait after the loop is short).
+__device__ __forceinline__ void glds16(const float *g, unsigned lds_wave_base) {
+#if XPA_HEAD_PROBE == 6  // 6 = the GEMM without its operand DMAs (MFMA stream on stale LDS)
+    asm volatile("" ::"v"(g), "s"(lds_wave_base) : "memory");
+    return;
+#endif
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds_wave_base)
+                 : "memory", "m0");
 }
 
-__device__ __forceinline__ void gemm_store(float *st, const float4 &ra, const float4 (&rb)[4]) {
-    const int t = threadIdx.x;
-    const int row = t >> 2, q = t & 3;
-    float *A = st, *B = st + kAImg;
-    *reinterpret_cast<float2 *>(A + row * kPS + 2 * q) = make_float2(ra.x, ra.z);            // k even
-    *reinterpret_cast<float2 *>(A + (kTile + row) * kPS + 2 * q) = make_float2(ra.y, ra.w);  // k odd
+// A chunk's 5 DMAs of wave w: A rows 16w .. 16w + 15, B rows 64w .. 64w + 63 (16 rows = 1 KiB each).
+// st: LDS byte address of the stage.  Rows past the batch re-read the last row (results never used).
+__device__ __forceinline__ void gemm_issue(unsigned st, const float *__restrict__ x, int64_t ldx,
+                                           const float *__restrict__ Wh, int64_t r0, int64_t batch, int k0,
+                                           int lane, int wave) {
+    const int rr = lane >> 2, p = lane & 3;
+    const int q = p ^ ((rr >> 2) & 3);  // (row >> 2) & 3 == (rr >> 2) & 3: row bases are multiples of 16
+    int64_t grow = r0 + wave * 16 + rr;
+    grow = grow < batch ? grow : batch - 1;
+    glds16(x + grow * ldx + k0 + 4 * q, st + (unsigned)(wave * 16 * kKC * 4));
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int lin = j * 256 + t, c = lin >> 2, q2 = lin & 3;
-        *reinterpret_cast<float2 *>(B + c * kPS + 2 * q2) = make_float2(rb[j].x, rb[j].z);
-        *reinterpret_cast<float2 *>(B + (kH + c) * kPS + 2 * q2) = make_float2(rb[j].y, rb[j].w);
+        const int row = wave * 64 + j * 16 + rr;
+        glds16(Wh + row * kKin + k0 + 4 * q, st + (unsigned)((kAImg + (wave * 64 + j * 16) * kKC) * 4));
     }
 }
+constexpr int kDmaPerChunk = 5;  // per wave: the vmcnt count that leaves one chunk in flight
 
 __device__ __forceinline__ void gemm_chunk(const float *st, f32x16 (&acc)[2][2], int lane, int wave) {
     const float *A = st, *B = st + kAImg;
     const int h = lane >> 5, i = lane & 31;
+    const int sw = (i >> 2) & 3;
+    const int olo = 4 * (h ^ sw), ohi = 4 * ((h + 2) ^ sw);
     float4 alo[2], ahi[2], blo[2], bhi[2];
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
-        const float *pa = A + (h * kTile + rt * 32 + i) * kPS;
-        alo[rt] = *reinterpret_cast<const float4 *>(pa);
-        ahi[rt] = *reinterpret_cast<const float4 *>(pa + 4);
+        const float *pa = A + (rt * 32 + i) * kKC;
+        alo[rt] = *reinterpret_cast<const float4 *>(pa + olo);
+        ahi[rt] = *reinterpret_cast<const float4 *>(pa + ohi);
     }
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) {
-        const float *pb = B + (h * kH + wave * 64 + ct * 32 + i) * kPS;
-        blo[ct] = *reinterpret_cast<const float4 *>(pb);
-        bhi[ct] = *reinterpret_cast<const float4 *>(pb + 4);
+        const float *pb = B + (wave * 64 + ct * 32 + i) * kKC;
+        blo[ct] = *reinterpret_cast<const float4 *>(pb + olo);
+        bhi[ct] = *reinterpret_cast<const float4 *>(pb + ohi);
     }
 #pragma unroll
     for (int s2 = 0; s2 < 8; ++s2) {
@@ -508,10 +560,16 @@ __device__ __forceinline__ void gemm_chunk(const float *st, f32x16 (&acc)[2][2],
 template <int MODE, int ALGO, int ACT, int KMAX>
 __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAMS) {
     using Epi = HeadEpi<MODE, ALGO, ACT, KMAX>;
-    __shared__ __attribute__((aligned(16))) float smem[kTile * kS];  // operand stages, then the h tile
-    __shared__ __attribute__((aligned(16))) float s_part[kWaves][kTile][KMAX];
-    __shared__ __attribute__((aligned(16))) float s_dh[kTile][Epi::KP];
-    __shared__ float s_stats[2];
+    // ONE LDS array (a second __shared__ object beside the DMA target can make hipcc wait vmcnt(0) before
+    // every chunk's ds_reads): operand stages / h tile, then the epilogue's partials, d head and stats.
+    constexpr int kPartOff = kTile * kS, kDhOff = kPartOff + kWaves * kTile * KMAX;
+    constexpr int kStatsOff = kDhOff + kTile * Epi::KP;
+    __shared__ __attribute__((aligned(16))) float lds[kStatsOff + 4];
+    float *smem = lds;
+    auto s_part = reinterpret_cast<float(*)[kTile][KMAX]>(lds + kPartOff);
+    auto s_dh = reinterpret_cast<float(*)[Epi::KP]>(lds + kDhOff);
+    float *s_stats = lds + kStatsOff;
+    const unsigned lds_base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int64_t ntiles = (batch + kTile - 1) / kTile;
@@ -528,23 +586,24 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
             for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[rt][ct][r] = 0.f;
-        float4 ra, rb[4];
         __syncthreads();  // the previous tile's epilogue is done with smem
-#if XPA_HEAD_PROBE != 2  // tools/head_probe.py: 2 = epilogue alone
-        gemm_load(z, ldx, Wh, r0, batch, 0, ra, rb);
-        gemm_store(smem, ra, rb);
-        __syncthreads();
-        for (int c = 0; c < kKin / kKC; ++c) {
-            const bool more = c + 1 < kKin / kKC;
-            if (more) gemm_load(z, ldx, Wh, r0, batch, (c + 1) * kKC, ra, rb);
-#if XPA_HEAD_PROBE != 3  // 3 = operand staging alone (its results kept live)
-            gemm_chunk(smem + (c & 1) * kStage, acc, lane, wave);
-#else
-            asm volatile("" ::"v"(ra.x), "v"(rb[0].y));
+#if XPA_HEAD_PROBE != 2 && XPA_HEAD_PROBE != 4 && XPA_HEAD_PROBE != 5  // tools/head_probe.py: 2 = epilogue alone (4, 5: parts of it)
+        gemm_issue(lds_base, z, ldx, Wh, r0, batch, 0, lane, wave);
+        gemm_issue(lds_base + kStage * 4, z, ldx, Wh, r0, batch, kKC, lane, wave);
+#pragma unroll 1
+        for (int c = 0; c < kChunks; ++c) {
+            // own DMAs of chunk c landed (chunk c + 1's may still fly), then every wave's: chunk c is in
+            // LDS and chunk c - 1's stage — the one chunk c + 2 refills — has been read by all waves
+            if (c + 1 < kChunks) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kDmaPerChunk) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            if (c + 2 < kChunks)
+                gemm_issue(lds_base + ((c + 2) % kStages) * kStage * 4, z, ldx, Wh, r0, batch, (c + 2) * kKC, lane,
+                           wave);
+#if XPA_HEAD_PROBE != 3  // 3 = operand staging alone
+            gemm_chunk(smem + (c % kStages) * kStage, acc, lane, wave);
 #endif
-            if (more) gemm_store(smem + ((c + 1) & 1) * kStage, ra, rb);
-            __syncthreads();
         }
+        __syncthreads();  // every wave done with the stages before the h tile overwrites them
 #endif
         // h = act(z + bh) into the tile image: C/D map row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col = lane & 31
 #pragma unroll
@@ -559,7 +618,7 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
                     smem[row * kS + col] = act_f<ACT>(acc[rt][ct][r] + bc, slope);
                 }
             }
-#if XPA_HEAD_PROBE == 1 || XPA_HEAD_PROBE == 3  // the GEMM alone: keep its result live
+#if XPA_HEAD_PROBE == 1 || XPA_HEAD_PROBE == 3 || XPA_HEAD_PROBE == 6  // the GEMM alone: keep its result live
         __syncthreads();
         if (r0 + (t >> 2) < batch) dz[(r0 + (t >> 2)) * ld + (t & 3)] = smem[(t >> 2) * kS + (t & 3)];
 #else
