@@ -1,16 +1,23 @@
 """Where K16's time goes: the fused hidden-GEMM + head kernels timed whole and with parts compiled out.
 
-    python tools/head_probe.py build        # here (no GPU): tools/_probe/libxpa_probe{0,1,2,3}.so
+    python tools/head_probe.py build        # here (no GPU): tools/_probe/libxpa_probe{0..6}.so
     python tools/head_probe.py run          # on the GPU box: one child process per variant
 
 Variants (head.hip, XPA_HEAD_PROBE): 0 the product kernel, 1 the GEMM alone (staging + MFMA, result
-kept live), 2 the epilogue alone (no GEMM), 3 operand staging alone (no MFMA).
+kept live), 2 the epilogue alone (no GEMM), 3 operand staging alone (no MFMA), 4 the epilogue without its
+dz stores, 5 the epilogue without phase 2, 6 the GEMM without its operand DMAs (MFMA stream on stale LDS).
 
-r01 findings (65 536 rows, fp32 MFMA floor 54.6 us per head): LDS-staged K16 actor 134 / critic 99 us
-= GEMM 92 (staging 37, not overlapped with the MFMAs) + epilogue 40 / 16 (not overlapped either).  A
-register-direct variant (no LDS staging, k permuted so each lane's fragments are contiguous) ran its
-GEMM in 110-122 us: SQ_WAIT_INST_ANY 88 % of wave cycles with the MFMA pipe ~50 % busy — in-loop
-VGPR-destination loads stall MFMA issue (the same MFMA stream with operands reused ran in 73-76 us).  Shape: the C2
+r01 findings (65 536 rows, fp32 MFMA floor 54.6 us per head at 2.4 GHz): register-staged K16 actor 134 /
+critic 99 us = GEMM 92 (staging 37, not overlapped with the MFMAs) + epilogue 40 / 16 (not overlapped
+either).  A register-direct variant (no LDS staging) ran its GEMM in 110-122 us: SQ_WAIT_INST_ANY 88 % of
+wave cycles — in-loop VGPR-destination loads stall MFMA issue.
+LDS-DMA 3-stage ring (current): actor 121-124 / critic 92-94; GEMM alone 89-92 / 84-88; MFMA stream without
+the DMAs 68-74 (so the loop itself reaches ~80 % of the floor and the DMAs add ~17 us); staging alone
+26-31; epilogue alone 39 / 15 (phase 1 + loss 20 / 9 after batching the head-weight scalar loads, which
+had been one branch + load + wait per output).  Rejected: per-wave private operand rings (each wave
+DMAs its own A copy + its B rows, no k-loop barrier): GEMM 100 / 92, worse — the 4x A re-reads cost more
+than the barriers (MFMA stream alone only 70 / 66 without them).
+Shape: the C2
 minibatch (65 536 rows, hidden 256, Gaussian actor K = 6, PPO); per-launch device time from events
 around `reps` back-to-back launches."""
 import json
@@ -24,6 +31,7 @@ sys.path.insert(0, REPO)
 OUT = os.path.join(HERE, "_probe")
 VARIANTS = {0: "full", 1: "gemm only", 2: "epilogue only", 3: "staging only", 4: "epilogue without dz stores",
             5: "epilogue without phase 2", 6: "gemm without operand DMAs"}
+FLAGS = {}   # variant -> hipcc defines, when not just -DXPA_HEAD_PROBE=<variant>
 
 
 def build():
@@ -31,7 +39,7 @@ def build():
     os.makedirs(OUT, exist_ok=True)
     procs = []
     for v in VARIANTS:
-        cmd = ([os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")] + _lib.HIPCC_FLAGS + ["-DXPA_HEAD_PROBE=%d" % v, "-o",
+        cmd = ([os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")] + _lib.HIPCC_FLAGS + FLAGS.get(v, ["-DXPA_HEAD_PROBE=%d" % v]) + ["-o",
                os.path.join(OUT, "libxpa_probe%d.so" % v)] + [os.path.join(_lib.CSRC, s) for s in _lib.SOURCES])
         procs.append(subprocess.Popen(cmd))
     for p in procs:
