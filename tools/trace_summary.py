@@ -22,7 +22,10 @@ def main(trace, bench, out=None, live=None):
     rows = list(csv.DictReader(open(trace)))
     b = json.load(open(bench))
     iters = b["warmup"] + b["steps"]
-    gae = [r for r in rows if "gae_scan_kernel" in r["Kernel_Name"]]
+    # the in-loop GAE kernel bench.py names in roofline.kernel, e.g. "xpa_gae_scan_compact (gae_dpp_kernel<5, 1>)"
+    m = re.search(r"\(([^()]+)\)\s*$", (b.get("roofline") or {}).get("kernel", ""))
+    pat = m.group(1) if m else "gae_scan_kernel"
+    gae = [r for r in rows if pat in r["Kernel_Name"]]
     gae.sort(key=lambda r: int(r["Start_Timestamp"]))
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in gae]
     timed = dur[b["warmup"]:iters]
@@ -35,6 +38,7 @@ def main(trace, bench, out=None, live=None):
     top = sorted(per.items(), key=lambda kv: -kv[1][1])[:30]
     res = {
         "bench_value": b["value"], "bench_ms_per_step": b["ms_per_step"],
+        "gae_kernel": pat,
         "gae_inloop_timed_launches_us": timed,
         "gae_inloop_avg_us": sum(timed) / len(timed) if timed else None,
         "profiled_run_live_avg_launch_us": (b.get("roofline") or {}).get("avg_launch_us"),
