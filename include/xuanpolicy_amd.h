@@ -307,6 +307,22 @@ int xpa_rollout_policy_head(int dist, int act, int64_t n_envs, int64_t act_dim, 
                             int64_t ld_env, xpa_stream_t stream);
 int xpa_value_head(int act, int64_t n, int64_t hidden, int64_t ld, const float *z_critic, float slope,
                    const float *w_critic, const float *b_critic, float *v_out, xpa_stream_t stream);
+/* K14 (Gaussian) with the SynthBox env step of the same env fused after the sample (K7's arithmetic; the
+ * env pre-activation [W | U] (s | clip(a)) as a fixed-order fmaf chain from the state row and the sampled
+ * actions instead of the env GEMM): one launch in place of K14 + env GEMM + xpa_synthbox_step.  state: the
+ * env's [n_envs, ld_state] input rows (s | a), obs_dim <= 64 state columns followed by act_dim action
+ * columns (written with the clipped actions, as env_in); wcat_t: [W | U]^T, [obs_dim + act_dim, obs_dim];
+ * the env arguments are xpa_synthbox_step's. */
+int xpa_rollout_policy_head_synthbox(int act, int64_t n_envs, int64_t act_dim, int64_t horizon, int64_t hidden,
+                                     int64_t ld, const float *z_actor, const float *z_critic, float slope,
+                                     const float *w_actor, const float *b_actor, const float *w_critic,
+                                     const float *b_critic, const float *logstd, const xpa_cursor_t *cursor,
+                                     uint32_t seed, float act_clip, float *buf_act, float *buf_logp, float *buf_val,
+                                     int64_t obs_dim, const float *wcat_t, uint32_t env_seed,
+                                     int32_t max_episode_steps, float noise, float term_thresh, float reset_scale,
+                                     float *state, int64_t ld_state, float *final_obs, float *rew, uint8_t *term,
+                                     uint8_t *trunc, int32_t *ep_step, uint32_t *ep_index, float *ep_score,
+                                     float *ep_last_score, int32_t *ep_last_len, xpa_stream_t stream);
 
 /* K16 — K12 with the hidden layer's GEMM on the fp32 matrix cores (v_mfma_f32_32x32x2_f32): the
  * pre-activations z = x w_hidden^T + b_hidden of each [64 x 256] tile are formed in registers and never

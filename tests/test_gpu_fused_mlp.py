@@ -325,3 +325,47 @@ def test_rollout_policy_head_matches_sample_kernel(discrete, act, D, A):
     vb = fm.rollout_value(x)
     with torch.no_grad():
         torch.testing.assert_close(vb, policy_heads(pol, x)[2], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("D,A,act", [(17, 6, torch.nn.LeakyReLU), (64, 3, torch.nn.Tanh), (5, 17, torch.nn.LeakyReLU)])
+def test_rollout_head_with_fused_env_step(D, A, act):
+    """K14 with the SynthBox env step fused in (xpa_rollout_policy_head_synthbox) == K14 followed by the env's
+    own step (env GEMM + K7): the buffers bitwise, the env's outputs to fp32 rounding of its pre-activation
+    (a fixed-order chain instead of the GEMM), its flags and episode counters exactly away from the
+    termination threshold."""
+    from xuanpolicy_amd.envs import SynthBoxVecEnv
+    from xuanpolicy_amd.flat import FlatState
+    from xuanpolicy_amd.fused_mlp import FusedActorCritic, head_placement
+    from oracle import synth_env
+    torch.manual_seed(7)
+    N, T = 4096 + 3, 8
+    pol = _policy(D, A, False, act, [256])
+    fs = FlatState(pol.parameters(), placement=head_placement(pol))
+    fm = FusedActorCritic(pol, flat=fs)
+    envs = [SynthBoxVecEnv(N, D, A, seed=3, max_episode_steps=4, device=DEV) for _ in range(2)]
+    for step in range(6):
+        x = envs[0].obs.clone()
+        cur = torch.tensor([step % T, 100 + step, 0, 0], dtype=torch.int32, device=DEV)
+        outs = []
+        for fused, env in zip((False, True), envs):
+            ba = torch.zeros(N, T, A, device=DEV)
+            bl, bv = torch.zeros(N, T, device=DEV), torch.zeros(N, T, device=DEV)
+            if fused:
+                assert env.fusable_with_policy_step("gaussian")
+                fm.rollout_act(x, "gaussian", cur, 99, ba, bl, bv, env.act_in, env=env)
+            else:
+                fm.rollout_act(x, "gaussian", cur, 99, ba, bl, bv, env.act_in)
+                env.step_device()
+            outs.append((ba, bl, bv, env))
+        (a1, l1, v1, e1), (a2, l2, v2, e2) = outs
+        assert torch.equal(a1, a2) and torch.equal(l1, l2) and torch.equal(v1, v2)
+        assert torch.equal(e1.act_in, e2.act_in)
+        torch.testing.assert_close(e2.final_obs, e1.final_obs, rtol=1e-5, atol=2e-6)
+        torch.testing.assert_close(e2.rew, e1.rew, rtol=1e-5, atol=1e-6)
+        near = (e1.final_obs[:, 0] - synth_env.TERM_THRESH).abs() < 1e-5
+        assert torch.equal(e1.term[~near], e2.term[~near]) and torch.equal(e1.trunc, e2.trunc)
+        assert torch.equal(e1.ep_step[~near], e2.ep_step[~near])
+        e2.X.copy_(e1.X)   # re-sync the states (tanh dynamics amplify ulps over steps)
+        for name in ("ep_step", "ep_index", "ep_score", "ep_last_score", "ep_last_len"):
+            getattr(e2, name).copy_(getattr(e1, name))
+    assert int(envs[0].ep_index.sum()) > 0

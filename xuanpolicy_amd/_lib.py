@@ -70,6 +70,10 @@ SIGNATURES = {
     "xpa_rollout_policy_head": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p,
                                                c_f32, c_p, c_p, c_p, c_p, c_p, c_p, c_u32, c_f32, c_p, c_p, c_p, c_p,
                                                c_i64, c_p]),
+    "xpa_rollout_policy_head_synthbox": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f32,
+                                                        c_p, c_p, c_p, c_p, c_p, c_p, c_u32, c_f32, c_p, c_p, c_p,
+                                                        c_i64, c_p, c_u32, ctypes.c_int32, c_f32, c_f32, c_f32, c_p,
+                                                        c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "xpa_value_head": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_f32, c_p, c_p, c_p, c_p]),
     "xpa_colsum_batch_tiles": (c_i64, [ctypes.c_int, c_p, c_p]),
     "xpa_colsum_finalize_batch_sq": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),

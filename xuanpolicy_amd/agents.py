@@ -106,6 +106,7 @@ class _OnPolicyAgent:
         self._perm_counter = 0
         self._perm_buf = None
         self.device_env = hasattr(envs, "step_device")
+        self.fuse_env_step = True   # device SynthBox env stepped inside K14 when possible (_env_fused)
         self.current_step = 0
         self.current_episode = np.zeros((N,), np.int32)
         self.iterations = 0
@@ -165,21 +166,29 @@ class _OnPolicyAgent:
         fm = fm_get() if fm_get is not None else None
         return fm if fm is not None and fm.rollout_ok else None
 
-    def _sample_into_buffer(self, raw_x=None):
-        """raw_x: the raw observations, normalised inside the fused trunk (see _rollout_step_device)."""
+    def _env_fused(self, fm):
+        """True when the device env's step runs inside the rollout's K14 launch (ops.rollout_policy_head_synthbox);
+        fuse_env_step = False keeps the separate env GEMM + K7 launches."""
+        ok = getattr(self.envs, "fusable_with_policy_step", None)
+        return bool(fm is not None and self.fuse_env_step and ok is not None and ok(self.dist))
+
+    def _sample_into_buffer(self, raw_x=None, fuse_env=False):
+        """raw_x: the raw observations, normalised inside the fused trunk (see _rollout_step_device).
+        fuse_env: also step the device env inside K14 (the caller then skips env.step_device())."""
         mem = self.memory
         logp_buf = mem.auxiliary_infos["old_logp"] if self.algo == "ppo" else self.logp_scratch
         env_in = self.envs.act_in if self.device_env else self._act_scratch()
         fm = self._rollout_mlp()
+        env = self.envs if fuse_env else None
         if raw_x is not None:
             T, D = self.n_steps, self.obs_dim
             fm.rollout_act(raw_x, self.dist, self.cursor, self.seed, mem.actions, logp_buf, mem.values, env_in,
                            act_clip=1.0, norm=(self.obs_mean, self.obs_var, self._obs_clip(), self.obs_norm,
-                                               mem.observations, T * D, self.cursor))
+                                               mem.observations, T * D, self.cursor), env=env)
             return
         if fm is not None:
             fm.rollout_act(self._policy_in, self.dist, self.cursor, self.seed, mem.actions, logp_buf, mem.values,
-                           env_in, act_clip=1.0)
+                           env_in, act_clip=1.0, env=env)
             return
         with torch.no_grad():
             head, logstd, v = policy_heads(self.policy, self._policy_in)
@@ -247,13 +256,17 @@ class _OnPolicyAgent:
                 self._rms_update(x)
             fm = self._rollout_mlp()
             if fm is not None and fm.thin0 and x.stride(1) == 1:
-                self._sample_into_buffer(raw_x=x)   # normalisation fused into the trunk's first layer
-                env.step_device()
+                fuse = self._env_fused(fm)
+                self._sample_into_buffer(raw_x=x, fuse_env=fuse)   # normalisation fused into the trunk's first layer
+                if not fuse:
+                    env.step_device()
                 self._post(env.rew, env.term, env.trunc, env.final_obs)
                 return
             self._normalize_into(x, self.obs_norm, True)
-        self._sample_into_buffer()
-        env.step_device()
+        fuse = self._env_fused(self._rollout_mlp())
+        self._sample_into_buffer(fuse_env=fuse)
+        if not fuse:
+            env.step_device()
         self._post(env.rew, env.term, env.trunc, env.final_obs)
 
     def _rollout_step_graph(self):

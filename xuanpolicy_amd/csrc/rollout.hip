@@ -329,6 +329,76 @@ __global__ __launch_bounds__(256) void rollout_sample_cat_kernel(
 // K14 rollout policy head: hidden activation + output layers (one wave per env, lane l owns hidden
 // columns [4l, 4l + 4), butterfly dot products) + the K3 sample/store above, or the value alone.
 // ---------------------------------------------------------------------------------------------
+// K7's per-env body, shared by the standalone env step and K14's fused form: one wave per env, lanes over
+// the state dims; pre(d) = the env's pre-activation for state dim d (row d of [W | U] (s | a)).
+struct SynthEnvArgs {
+    int D;
+    uint32_t seed;
+    int max_steps;
+    float noise, thresh, reset_scale;
+    float *state;
+    int64_t ld_state;
+    float *final_obs, *rew;
+    uint8_t *term, *trunc;
+    int32_t *ep_step;
+    uint32_t *ep_index;
+    float *ep_score, *ep_last_score;
+    int32_t *ep_last_len;
+    const float *wt;  // fused form: [W | U]^T, [D + A, D] row-major
+};
+
+template <class PreFn>
+__device__ __forceinline__ void synthbox_env_row(int64_t n, int lane, const SynthEnvArgs &e, PreFn pre) {
+    const int D = e.D;
+    const int t = e.ep_step[n];
+    const uint32_t ep = e.ep_index[n];
+    float sumsq = 0.f, s0 = 0.f;
+    for (int d = lane; d < D; d += 64) {
+        const uint32_t base = ((uint32_t)t * (uint32_t)D + (uint32_t)d) * 4u;
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc += xpa_u01(xpa_hash4(e.seed, (uint32_t)n, ep, base + (uint32_t)j));
+        const float xi = (acc - 2.0f) * 1.7320508075688772f;
+        const float sv = tanhf(pre(d) + e.noise * xi);
+        e.final_obs[n * D + d] = sv;
+        sumsq += sv * sv;
+        if (d == 0) s0 = sv;
+    }
+    sumsq = xpa_wave_sum(sumsq);
+    s0 = __shfl(s0, 0, 64);
+    const float r = -sumsq / (float)D;
+    const bool te = s0 > e.thresh;
+    const int t1 = t + 1;
+    const bool tr = t1 >= e.max_steps;
+    const bool done = te || tr;
+    const float score = e.ep_score[n] + r;
+    for (int d = lane; d < D; d += 64) {
+        float sn;
+        if (done) {
+            const uint32_t h = xpa_hash4(e.seed ^ kSaltReset, (uint32_t)n, ep + 1u, (uint32_t)d);
+            sn = (2.0f * xpa_u01(h) - 1.0f) * e.reset_scale;
+        } else {
+            sn = e.final_obs[n * D + d];
+        }
+        e.state[n * e.ld_state + d] = sn;
+    }
+    if (lane == 0) {
+        e.rew[n] = r;
+        e.term[n] = te ? 1 : 0;
+        e.trunc[n] = tr ? 1 : 0;
+        if (done) {
+            e.ep_last_score[n] = score;
+            e.ep_last_len[n] = t1;
+            e.ep_index[n] = ep + 1u;
+            e.ep_step[n] = 0;
+            e.ep_score[n] = 0.f;
+        } else {
+            e.ep_step[n] = t1;
+            e.ep_score[n] = score;
+        }
+    }
+}
+
 template <int ACT>
 __device__ __forceinline__ float4 act4(float4 z, float slope) {
     if (ACT == 1) {
@@ -350,13 +420,17 @@ __device__ __forceinline__ float wave_allsum_f(float v) {
 
 // MODE: 0 Gaussian sample, 1 Categorical sample, 2 value only (v_out[n]).
 constexpr int kRolloutKMax = 32;  // head width limit of K14 (lanes < K draw the Gaussian dimensions)
-template <int MODE, int ACT>
+// ENV (Gaussian only): the SynthBox env step of the same env fused after the sample — pre = [W | U] (s | clip(a))
+// from the state row and the lanes' clipped actions (fixed k order), then K7's body: no env GEMM and no K7
+// launch.  Needs D <= 64 (one state dim per lane).
+template <int MODE, int ACT, bool ENV = false>
 __global__ __launch_bounds__(256) void rollout_policy_head_kernel(
     int64_t n_envs, int K, int64_t T, const float *__restrict__ za, const float *__restrict__ zc, int64_t ld,
     float slope, const float *__restrict__ Wa, const float *__restrict__ ba, const float *__restrict__ Wc,
     const float *__restrict__ bc, const float *__restrict__ logstd, const xpa_cursor_t *__restrict__ cur,
     uint32_t seed, float act_clip, float *__restrict__ buf_act, float *__restrict__ buf_logp,
-    float *__restrict__ buf_val, float *__restrict__ env_in, int64_t ld_env, float *__restrict__ v_out) {
+    float *__restrict__ buf_val, float *__restrict__ env_in, int64_t ld_env, float *__restrict__ v_out,
+    SynthEnvArgs env) {
     __shared__ float s_head[4][kRolloutKMax];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t n = (int64_t)blockIdx.x * 4 + wave;
@@ -381,7 +455,7 @@ __global__ __launch_bounds__(256) void rollout_policy_head_kernel(
     // Gaussian: lane a draws dimension a (the K3 arithmetic); lane 0 adds the log-prob terms in
     // dimension order, so the sum is bitwise K3's sequential one.
     const int64_t cell = n * T + cur->ptr;
-    float term_a = 0.f;
+    float term_a = 0.f, xclip = 0.f;
     if (lane < K) {
         const int a = lane;
         const uint32_t step = cur->step;
@@ -395,7 +469,8 @@ __global__ __launch_bounds__(256) void rollout_policy_head_kernel(
         const float diff = x - mine;
         term_a = -(diff * diff) / (2.0f * sc * sc) - logf(sc) - 0.91893853320467274178f;
         buf_act[cell * K + a] = x;
-        env_in[n * ld_env + a] = fminf(fmaxf(x, -act_clip), act_clip);
+        xclip = fminf(fmaxf(x, -act_clip), act_clip);
+        env_in[n * ld_env + a] = xclip;
     }
     float logp = 0.f;
     for (int a = 0; a < K; ++a) logp += __shfl(term_a, a, 64);
@@ -403,67 +478,31 @@ __global__ __launch_bounds__(256) void rollout_policy_head_kernel(
         buf_logp[cell] = logp;
         buf_val[cell] = v;
     }
+    if constexpr (ENV) {
+        const int D = env.D;
+        const float xs = lane < D ? env.state[n * env.ld_state + lane] : 0.f;
+        float pre = 0.f;
+        for (int k = 0; k < D; ++k) {  // every lane shuffles; lanes < D accumulate
+            const float xk = __shfl(xs, k, 64);
+            if (lane < D) pre = fmaf(xk, env.wt[k * D + lane], pre);
+        }
+        for (int a = 0; a < K; ++a) {
+            const float av = __shfl(xclip, a, 64);
+            if (lane < D) pre = fmaf(av, env.wt[(D + a) * D + lane], pre);
+        }
+        synthbox_env_row(n, lane, env, [&](int) { return pre; });
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
 // K7 SynthBox env step (one wave per env, lanes over the state dims)
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void synthbox_step_kernel(
-    int64_t n_envs, int D, const float *__restrict__ pre, uint32_t seed, int max_steps, float noise, float thresh,
-    float reset_scale, float *__restrict__ state, int64_t ld_state, float *__restrict__ final_obs,
-    float *__restrict__ rew, uint8_t *__restrict__ term, uint8_t *__restrict__ trunc, int32_t *__restrict__ ep_step,
-    uint32_t *__restrict__ ep_index, float *__restrict__ ep_score, float *__restrict__ ep_last_score,
-    int32_t *__restrict__ ep_last_len) {
+__global__ __launch_bounds__(256) void synthbox_step_kernel(const float *__restrict__ pre, SynthEnvArgs e,
+                                                            int64_t n_envs) {
     const int64_t n = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (n >= n_envs) return;  // wave-uniform
-    const int t = ep_step[n];
-    const uint32_t ep = ep_index[n];
-    float sumsq = 0.f, s0 = 0.f;
-    for (int d = lane; d < D; d += 64) {
-        const uint32_t base = ((uint32_t)t * (uint32_t)D + (uint32_t)d) * 4u;
-        float acc = 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc += xpa_u01(xpa_hash4(seed, (uint32_t)n, ep, base + (uint32_t)j));
-        const float xi = (acc - 2.0f) * 1.7320508075688772f;
-        const float s = tanhf(pre[n * D + d] + noise * xi);
-        final_obs[n * D + d] = s;
-        sumsq += s * s;
-        if (d == 0) s0 = s;
-    }
-    sumsq = xpa_wave_sum(sumsq);
-    s0 = __shfl(s0, 0, 64);
-    const float r = -sumsq / (float)D;
-    const bool te = s0 > thresh;
-    const int t1 = t + 1;
-    const bool tr = t1 >= max_steps;
-    const bool done = te || tr;
-    const float score = ep_score[n] + r;
-    for (int d = lane; d < D; d += 64) {
-        float sn;
-        if (done) {
-            const uint32_t h = xpa_hash4(seed ^ kSaltReset, (uint32_t)n, ep + 1u, (uint32_t)d);
-            sn = (2.0f * xpa_u01(h) - 1.0f) * reset_scale;
-        } else {
-            sn = final_obs[n * D + d];
-        }
-        state[n * ld_state + d] = sn;
-    }
-    if (lane == 0) {
-        rew[n] = r;
-        term[n] = te ? 1 : 0;
-        trunc[n] = tr ? 1 : 0;
-        if (done) {
-            ep_last_score[n] = score;
-            ep_last_len[n] = t1;
-            ep_index[n] = ep + 1u;
-            ep_step[n] = 0;
-            ep_score[n] = 0.f;
-        } else {
-            ep_step[n] = t1;
-            ep_score[n] = score;
-        }
-    }
+    synthbox_env_row(n, lane, e, [&](int d) { return pre[n * e.D + d]; });
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -691,10 +730,10 @@ XPA_API int xpa_synthbox_step(int64_t n_envs, int64_t obs_dim, const float *pre,
     if (n_envs <= 0 || obs_dim <= 0 || ld_state < obs_dim || !pre || !state || !final_obs || !rew || !term ||
         !trunc || !ep_step || !ep_index || !ep_score || !ep_last_score || !ep_last_len)
         return (int)hipErrorInvalidValue;
+    SynthEnvArgs e{(int)obs_dim, seed, max_episode_steps, noise, term_thresh, reset_scale, state, ld_state, final_obs,
+                   rew, term, trunc, ep_step, ep_index, ep_score, ep_last_score, ep_last_len, nullptr};
     const unsigned blocks = (unsigned)((n_envs + 3) / 4);
-    hipLaunchKernelGGL(synthbox_step_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, n_envs, (int)obs_dim, pre,
-                       seed, max_episode_steps, noise, term_thresh, reset_scale, state, ld_state, final_obs, rew, term,
-                       trunc, ep_step, ep_index, ep_score, ep_last_score, ep_last_len);
+    hipLaunchKernelGGL(synthbox_step_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, pre, e, n_envs);
     return xpa_launch_status();
 }
 
@@ -809,7 +848,7 @@ XPA_API int xpa_rollout_policy_head(int dist, int act, int64_t n_envs, int64_t a
 #define XPA_K14(M_, A_)                                                                                          \
     hipLaunchKernelGGL((rollout_policy_head_kernel<M_, A_>), dim3(blocks), dim3(256), 0, s, n_envs, (int)act_dim, \
                        horizon, z_actor, z_critic, ld, slope, w_actor, b_actor, w_critic, b_critic, logstd, cursor,   \
-                       seed, act_clip, buf_act, buf_logp, buf_val, env_in, ld_env, (float *)nullptr)
+                       seed, act_clip, buf_act, buf_logp, buf_val, env_in, ld_env, (float *)nullptr, SynthEnvArgs{})
     if (dist == XPA_DIST_GAUSSIAN) {
         if (act == 0) XPA_K14(0, 0);
         else if (act == 1) XPA_K14(0, 1);
@@ -834,7 +873,7 @@ XPA_API int xpa_value_head(int act, int64_t n, int64_t hidden, int64_t ld, const
     hipLaunchKernelGGL((rollout_policy_head_kernel<2, A_>), dim3(blocks), dim3(256), 0, s, n, 1, (int64_t)1,        \
                        z_critic, z_critic, ld, slope, w_critic, b_critic, w_critic, b_critic, (const float *)nullptr, \
                        (const xpa_cursor_t *)nullptr, 0u, 0.f, (float *)nullptr, (float *)nullptr, (float *)nullptr, \
-                       (float *)nullptr, (int64_t)0, v_out)
+                       (float *)nullptr, (int64_t)0, v_out, SynthEnvArgs{})
     if (act == 0) XPA_VH(0);
     else if (act == 1) XPA_VH(1);
     else XPA_VH(2);
@@ -861,5 +900,42 @@ XPA_API int xpa_random_permutation(int64_t n, uint32_t seed, uint32_t counter, i
     while ((1LL << (2 * h)) < n) ++h;
     hipLaunchKernelGGL(permutation_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, h,
                        seed, counter, out);
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_rollout_policy_head_synthbox(int act, int64_t n_envs, int64_t act_dim, int64_t horizon, int64_t hidden,
+                                             int64_t ld, const float *z_actor, const float *z_critic, float slope,
+                                             const float *w_actor, const float *b_actor, const float *w_critic,
+                                             const float *b_critic, const float *logstd, const xpa_cursor_t *cursor,
+                                             uint32_t seed, float act_clip, float *buf_act, float *buf_logp,
+                                             float *buf_val, int64_t obs_dim, const float *wcat_t, uint32_t env_seed,
+                                             int32_t max_episode_steps, float noise, float term_thresh,
+                                             float reset_scale, float *state, int64_t ld_state, float *final_obs,
+                                             float *rew, uint8_t *term, uint8_t *trunc, int32_t *ep_step,
+                                             uint32_t *ep_index, float *ep_score, float *ep_last_score,
+                                             int32_t *ep_last_len, xpa_stream_t stream) {
+    if (n_envs <= 0 || act_dim < 1 || act_dim > kRolloutKMax || horizon <= 0 || hidden != 256 || ld < 256 || ld % 4 ||
+        act < 0 || act > 2 || !z_actor || !z_critic || !w_actor || !b_actor || !w_critic || !b_critic || !cursor ||
+        !logstd || !buf_act || !buf_logp || !buf_val)
+        return (int)hipErrorInvalidValue;
+    if (((uintptr_t)z_actor | (uintptr_t)z_critic | (uintptr_t)w_actor | (uintptr_t)w_critic) % 16)
+        return (int)hipErrorInvalidValue;
+    if (obs_dim < 1 || obs_dim > 64 || !wcat_t || !state || ld_state < obs_dim + act_dim || !final_obs || !rew ||
+        !term || !trunc || !ep_step || !ep_index || !ep_score || !ep_last_score || !ep_last_len)
+        return (int)hipErrorInvalidValue;
+    SynthEnvArgs e{(int)obs_dim, env_seed, max_episode_steps, noise, term_thresh, reset_scale, state, ld_state,
+                   final_obs, rew, term, trunc, ep_step, ep_index, ep_score, ep_last_score, ep_last_len, wcat_t};
+    float *env_in = state + obs_dim;  // the action columns of the env's input rows (s | a)
+    const unsigned blocks = (unsigned)((n_envs + 3) / 4);
+    hipStream_t s = (hipStream_t)stream;
+#define XPA_K14E(A_)                                                                                              \
+    hipLaunchKernelGGL((rollout_policy_head_kernel<0, A_, true>), dim3(blocks), dim3(256), 0, s, n_envs,           \
+                       (int)act_dim, horizon, z_actor, z_critic, ld, slope, w_actor, b_actor, w_critic, b_critic,     \
+                       logstd, cursor, seed, act_clip, buf_act, buf_logp, buf_val, env_in, ld_state, (float *)nullptr, \
+                       e)
+    if (act == 0) XPA_K14E(0);
+    else if (act == 1) XPA_K14E(1);
+    else XPA_K14E(2);
+#undef XPA_K14E
     return xpa_launch_status();
 }

@@ -125,6 +125,11 @@ class SynthBoxVecEnv:
             t.zero_()
         return self.obs.clone(), [{} for _ in range(self.num_envs)]
 
+    def fusable_with_policy_step(self, dist):
+        """True when the rollout's K14 can run this env's step in the same launch
+        (ops.rollout_policy_head_synthbox): continuous actions and at most 64 state dims."""
+        return dist == "gaussian" and not self.discrete and self.D <= 64
+
     def step_device(self):
         """One env step for all envs from the action already written into act_in."""
         torch.mm(self.X, self.Wcat_t, out=self.pre)

@@ -201,9 +201,11 @@ class FusedActorCritic:
         return self.pair is not None
 
     @torch.no_grad()
-    def rollout_act(self, x, dist, cursor, seed, buf_act, buf_logp, buf_val, env_in, act_clip=1.0, norm=None):
+    def rollout_act(self, x, dist, cursor, seed, buf_act, buf_logp, buf_val, env_in, act_clip=1.0, norm=None,
+                    env=None):
         """Policy step of the rollout: trunk, paired hidden GEMM, then K14 (heads + sample + store).
-        norm: see _rep_forward (x is then the raw observation)."""
+        norm: see _rep_forward (x is then the raw observation).  env: a device SynthBox env whose step runs
+        inside the same K14 launch (ops.rollout_policy_head_synthbox; the caller skips env.step_device())."""
         rep_outs = self._rep_forward(x, norm=norm)
         s = rep_outs[-1] if rep_outs else x
         z = F.linear(s, self.pair[0], self.pair[1])
@@ -213,6 +215,11 @@ class FusedActorCritic:
         _, code, slope = self.actor[-2]
         if self.critic[-2][1:] != (code, slope):
             raise ValueError("actor and critic hidden activations differ")
+        if env is not None:
+            ops.rollout_policy_head_synthbox(z[:, :H], z[:, H:], (code, slope), lin_ao.weight, lin_ao.bias,
+                                             lin_co.weight, lin_co.bias, self.logstd, cursor, seed, buf_act, buf_logp,
+                                             buf_val, env, act_clip)
+            return
         ops.rollout_policy_head(dist, z[:, :H], z[:, H:], (code, slope), lin_ao.weight, lin_ao.bias, lin_co.weight,
                                 lin_co.bias, self.logstd, cursor, seed, buf_act, buf_logp, buf_val, env_in, act_clip)
 

@@ -657,6 +657,38 @@ def rollout_policy_head(dist, z_actor, z_critic, act, w_actor, b_actor, w_critic
     _lib.check(rc, "xpa_rollout_policy_head")
 
 
+def rollout_policy_head_synthbox(z_actor, z_critic, act, w_actor, b_actor, w_critic, b_critic, logstd, cursor, seed,
+                                 buf_act, buf_logp, buf_val, env, act_clip=1.0):
+    """K14 (Gaussian) + the SynthBox env step of envs.SynthBoxVecEnv `env` in one launch
+    (xpa_rollout_policy_head_synthbox): same buffers as rollout_policy_head, then the env's state, final
+    obs, reward, flags and episode counters exactly as env.step_device() after K14 would write them (the
+    env pre-activation as a fixed-order chain instead of the GEMM: ulp-level differences)."""
+    N, H = z_actor.shape
+    ld = z_actor.stride(0)
+    for name, z in (("z_actor", z_actor), ("z_critic", z_critic)):
+        _req(z, name, torch.float32, contiguous=False)
+        if tuple(z.shape) != (N, HEAD_HIDDEN) or z.stride() != (ld, 1):
+            raise ValueError("%s must be [N, %d] with the same row stride" % (name, HEAD_HIDDEN))
+    A = w_actor.shape[0]
+    _req(w_actor, "w_actor", torch.float32, (A, H))
+    _req(w_critic, "w_critic", torch.float32, (1, H))
+    _req(cursor, "cursor", torch.int32, (4,))
+    _req(logstd, "logstd", torch.float32, (A,))
+    T = buf_logp.shape[1]
+    _req(buf_act, "buf_act", torch.float32, (N, T, A))
+    if env.num_envs != N or env.A != A or env.discrete:
+        raise ValueError("the fused env step needs a continuous-action env of matching shape")
+    from .envs import NOISE, TERM_THRESH, RESET_SCALE
+    rc = lib().xpa_rollout_policy_head_synthbox(
+        act[0], N, A, T, H, ld, _p(z_actor), _p(z_critic), float(act[1]), _p(w_actor), _p(b_actor), _p(w_critic),
+        _p(b_critic), _p(logstd), _p(cursor), int(seed) & 0xFFFFFFFF, float(act_clip), _p(buf_act), _p(buf_logp),
+        _p(buf_val), env.D, _p(env.Wcat_t), env.noise_seed, env.max_episode_steps, NOISE, TERM_THRESH,
+        RESET_SCALE, _p(env.X), env.X.stride(0), _p(env.final_obs), _p(env.rew), _p(env.term), _p(env.trunc),
+        _p(env.ep_step), _p(env.ep_index), _p(env.ep_score), _p(env.ep_last_score), _p(env.ep_last_len),
+        _stream(z_actor.device))
+    _lib.check(rc, "xpa_rollout_policy_head_synthbox")
+
+
 def value_head(z_critic, act, w_critic, b_critic, out=None):
     """K14 value-only: v = act(z_critic) . w + b for every row."""
     N, H = z_critic.shape
