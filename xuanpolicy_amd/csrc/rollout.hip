@@ -347,11 +347,11 @@ struct SynthEnvArgs {
     const float *wt;  // fused form: [W | U]^T, [D + A, D] row-major
 };
 
+// t, ep, score0: the env's ep_step / ep_index / ep_score (loaded by the caller, early in the fused form)
 template <class PreFn>
-__device__ __forceinline__ void synthbox_env_row(int64_t n, int lane, const SynthEnvArgs &e, PreFn pre) {
+__device__ __forceinline__ void synthbox_env_row(int64_t n, int lane, const SynthEnvArgs &e, PreFn pre, int t,
+                                                 uint32_t ep, float score0) {
     const int D = e.D;
-    const int t = e.ep_step[n];
-    const uint32_t ep = e.ep_index[n];
     float sumsq = 0.f, s0 = 0.f;
     for (int d = lane; d < D; d += 64) {
         const uint32_t base = ((uint32_t)t * (uint32_t)D + (uint32_t)d) * 4u;
@@ -371,7 +371,7 @@ __device__ __forceinline__ void synthbox_env_row(int64_t n, int lane, const Synt
     const int t1 = t + 1;
     const bool tr = t1 >= e.max_steps;
     const bool done = te || tr;
-    const float score = e.ep_score[n] + r;
+    const float score = score0 + r;
     for (int d = lane; d < D; d += 64) {
         float sn;
         if (done) {
@@ -435,6 +435,26 @@ __global__ __launch_bounds__(256) void rollout_policy_head_kernel(
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t n = (int64_t)blockIdx.x * 4 + wave;
     if (n >= n_envs) return;  // wave-uniform
+    // ENV: the env's state row, counters and the first kPreW rows of [W | U]^T are loaded first, so their
+    // latency hides under the head arithmetic
+    constexpr int kPreW = 24;
+    float xs = 0.f, wreg[ENV ? kPreW : 1];
+    int e_t = 0;
+    uint32_t e_ep = 0u;
+    float e_score = 0.f;
+    int dl = 0;
+    if constexpr (ENV) {
+        dl = lane < env.D ? lane : 0;
+        xs = lane < env.D ? env.state[n * env.ld_state + lane] : 0.f;
+        e_t = env.ep_step[n];
+        e_ep = env.ep_index[n];
+        e_score = env.ep_score[n];
+#pragma unroll
+        for (int j = 0; j < kPreW; ++j) {  // unconditional loads (clamped row): no branch + wait per element
+            const int jj = j < env.D + K ? j : env.D + K - 1;
+            wreg[j] = env.wt[jj * env.D + dl];
+        }
+    }
     const float4 hc = act4<ACT>(*reinterpret_cast<const float4 *>(zc + n * ld + 4 * lane), slope);
     const float v = wave_allsum_f(dot4(hc, *reinterpret_cast<const float4 *>(Wc + 4 * lane))) + bc[0];
     if (MODE == 2) {
@@ -479,18 +499,22 @@ __global__ __launch_bounds__(256) void rollout_policy_head_kernel(
         buf_val[cell] = v;
     }
     if constexpr (ENV) {
-        const int D = env.D;
-        const float xs = lane < D ? env.state[n * env.ld_state + lane] : 0.f;
+        // pre = [W | U] (s | clip(a)) for state dim `lane`: one fmaf chain over j < D + K in order
+        const int D = env.D, J = D + K;
         float pre = 0.f;
-        for (int k = 0; k < D; ++k) {  // every lane shuffles; lanes < D accumulate
-            const float xk = __shfl(xs, k, 64);
-            if (lane < D) pre = fmaf(xk, env.wt[k * D + lane], pre);
+#pragma unroll
+        for (int j = 0; j < kPreW; ++j) {
+            if (j < J) {  // uniform
+                const float v = __shfl(j < D ? xs : xclip, j < D ? j : j - D, 64);
+                if (lane < D) pre = fmaf(v, wreg[j], pre);
+            }
         }
-        for (int a = 0; a < K; ++a) {
-            const float av = __shfl(xclip, a, 64);
-            if (lane < D) pre = fmaf(av, env.wt[(D + a) * D + lane], pre);
+        for (int j = kPreW; j < J; ++j) {
+            const float v = __shfl(j < D ? xs : xclip, j < D ? j : j - D, 64);
+            const float w = env.wt[j * D + dl];
+            if (lane < D) pre = fmaf(v, w, pre);
         }
-        synthbox_env_row(n, lane, env, [&](int) { return pre; });
+        synthbox_env_row(n, lane, env, [&](int) { return pre; }, e_t, e_ep, e_score);
     }
 }
 
@@ -502,7 +526,7 @@ __global__ __launch_bounds__(256) void synthbox_step_kernel(const float *__restr
     const int64_t n = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (n >= n_envs) return;  // wave-uniform
-    synthbox_env_row(n, lane, e, [&](int d) { return pre[n * e.D + d]; });
+    synthbox_env_row(n, lane, e, [&](int d) { return pre[n * e.D + d]; }, e.ep_step[n], e.ep_index[n], e.ep_score[n]);
 }
 
 // ---------------------------------------------------------------------------------------------
