@@ -131,7 +131,8 @@ int xpa_policy_loss_finalize(int algo, int dist, int64_t batch, int64_t act_dim,
                              int64_t n_partials, float vf_coef, float ent_coef, float *scalars,
                              float *d_logstd, xpa_stream_t stream);
 /* The same, also writing sum(d_logstd^2) (0 for Categorical) into *sq_out (nullable): that gradient's
- * share of the clip norm for xpa_clip_adam_step_partials. */
+ * share of the clip norm for xpa_clip_adam_step_partials (the norm torch.nn.utils.clip_grad_norm_ takes
+ * over all parameters in ppoclip_learner.py:47-48, a2c_learner.py:34). */
 int xpa_policy_loss_finalize_sq(int algo, int dist, int64_t batch, int64_t act_dim, const float *partials,
                                 int64_t n_partials, float vf_coef, float ent_coef, float *scalars, float *d_logstd,
                                 double *sq_out, xpa_stream_t stream);
@@ -219,7 +220,8 @@ int xpa_clip_adam_step(float *param, float *grad, float *exp_avg, float *exp_avg
                        int64_t step, float *total_norm_out, xpa_stream_t stream);
 /* K9 from squared-norm partials already written by the gradient producers (world size 1: the batched
  * column-sum finalize's per-tile partials + the loss finalize's d logstd share): no norm pass over the
- * flat gradient.  sq_partials: n_sq doubles summing to |grad|^2; the clip + Adam arithmetic is
+ * flat gradient.  Same clip_grad_norm_ + Adam.step as xpa_clip_adam_step (ppoclip_learner.py:47-49,
+ * a2c_learner.py:34-35).  sq_partials: n_sq doubles summing to |grad|^2; the clip + Adam arithmetic is
  * xpa_clip_adam_step's. */
 int xpa_clip_adam_step_partials(float *param, float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
                                 const double *sq_partials, int64_t n_sq, float max_norm, float lr, float beta1,
@@ -307,7 +309,8 @@ int xpa_rollout_policy_head(int dist, int act, int64_t n_envs, int64_t act_dim, 
                             int64_t ld_env, xpa_stream_t stream);
 int xpa_value_head(int act, int64_t n, int64_t hidden, int64_t ld, const float *z_critic, float slope,
                    const float *w_critic, const float *b_critic, float *v_out, xpa_stream_t stream);
-/* K14 (Gaussian) with the SynthBox env step of the same env fused after the sample (K7's arithmetic; the
+/* K14 (Gaussian) with the SynthBox env step of the same env fused after the sample — the agent's
+ * `self.envs.step(acts)` right after `self._action(obs)` (ppoclip_agent.py:65-66) in one launch (K7's arithmetic; the
  * env pre-activation [W | U] (s | clip(a)) as a fixed-order fmaf chain from the state row and the sampled
  * actions instead of the env GEMM): one launch in place of K14 + env GEMM + xpa_synthbox_step.  state: the
  * env's [n_envs, ld_state] input rows (s | a), obs_dim <= 64 state columns followed by act_dim action
