@@ -1,5 +1,6 @@
 """Data-parallel path on CPU with the gloo backend (world_size 2): the flat-gradient all-reduce used per
-minibatch (one collective), parameter broadcast at start-up, and torchrun-style initialisation."""
+minibatch (one collective, or an early slice + the rest), parameter broadcast at start-up, and torchrun-style
+initialisation."""
 import os
 import socket
 
@@ -59,6 +60,18 @@ def _worker(rank, world, port, q):
         for p, off in zip(fs.params, fs.offsets):
             assert p.grad.data_ptr() == fs.flat[off:].data_ptr() and off % 64 == 0
         assert float(fs.flat.abs().sum()) == float(got.abs().sum())  # padding stays zero
+        # early slice (GradAllReduce.begin, as the fused MLP update starts its hidden-pair dW): the same
+        # average, element for element, as the single collective
+        fs.zero_()
+        ((net(x) - y) ** 2).mean().backward()
+        whole = fs.flat.clone()
+        dist.all_reduce(whole, op=dist.ReduceOp.SUM)
+        whole.div_(world)
+        w0 = fs.params[2].grad                    # the second Linear's weight: a slice inside the buffer
+        assert ar.begin(w0) and not ar.begin(w0)  # one early slice per update
+        ar(fs.params)
+        assert ar.calls == 2 and ar._early is None
+        assert torch.equal(fs.flat, whole)
         q.put((rank, "ok"))
     except Exception as e:  # pragma: no cover - reported to the parent
         q.put((rank, repr(e)))

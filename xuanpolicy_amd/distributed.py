@@ -7,8 +7,10 @@ only collective is ONE all-reduce (average) of the flat fp32 gradient per miniba
 clip_grad_norm_, so the clipped norm is the global one.
 
 FlatState (xuanpolicy_amd.flat) makes every parameter's .grad a view into one contiguous buffer, so
-autograd accumulates straight into it and the all-reduce is a single RCCL call over xGMI
-(latency-bound at 0.04-1 MiB; one bucket, no overlap needed).  Backend "nccl" is RCCL on ROCm; "gloo" is used by the CPU tests.
+autograd accumulates straight into it and the all-reduce is one RCCL call over xGMI per minibatch
+(latency-bound at 0.04-1 MiB; one bucket) — or, on the fused MLP path, two: the paired hidden layers' dW
+slice is started as soon as its GEMM has written it and overlaps the rest of the backward
+(GradAllReduce.begin).  Backend "nccl" is RCCL on ROCm; "gloo" is used by the CPU tests.
 """
 import os
 
@@ -19,7 +21,13 @@ from .flat import FlatState, FusedClipAdam, fused_adam_compatible
 
 
 class GradAllReduce:
-    """learner.grad_sync hook: average the flat gradient over the process group (one collective)."""
+    """learner.grad_sync hook: average the flat gradient over the process group.
+
+    begin(region): start the all-reduce of one contiguous slice of the flat gradient early (async, on the
+    collective's own stream) as soon as its producer has written it — the fused MLP update hands over the
+    paired hidden layers' dW (0.5 MB of C2's 0.55 MB) right after its GEMM, so the transfer overlaps the dX
+    GEMM and the trunk backward.  __call__ then reduces the rest of the buffer and waits for the early
+    slice: every element is still averaged exactly once, before the clip."""
 
     def __init__(self, flat_grads, group=None):
         self.fg = flat_grads
@@ -27,14 +35,39 @@ class GradAllReduce:
         self.world = dist.get_world_size(group)
         self.avg = dist.get_backend(group) == "nccl"
         self.calls = 0
+        self._early = None   # (offset, numel, work)
+
+    def _reduce(self, t, async_op=False):
+        op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
+        return dist.all_reduce(t, op=op, group=self.group, async_op=async_op)
+
+    def begin(self, region):
+        """Start the async all-reduce of `region` (a contiguous view into the flat gradient)."""
+        flat = self.fg.flat
+        off = (region.data_ptr() - flat.data_ptr()) // flat.element_size()
+        n = region.numel()
+        if (self._early is not None or not region.is_contiguous() or off < 0 or off + n > flat.numel()
+                or region.dtype != flat.dtype):
+            return False
+        self._early = (off, n, self._reduce(flat[off:off + n], async_op=True))
+        return True
 
     def __call__(self, params):
         self.fg.ensure_views()
-        if self.avg:
-            dist.all_reduce(self.fg.flat, op=dist.ReduceOp.AVG, group=self.group)
+        flat = self.fg.flat
+        if self._early is None:
+            self._reduce(flat)
+            if not self.avg:
+                flat.div_(self.world)
         else:
-            dist.all_reduce(self.fg.flat, op=dist.ReduceOp.SUM, group=self.group)
-            self.fg.flat.div_(self.world)
+            off, n, work = self._early
+            self._early = None
+            for lo, hi in ((0, off), (off + n, flat.numel())):
+                if hi > lo:
+                    self._reduce(flat[lo:hi])
+            work.wait()   # NCCL: the current stream waits for the early slice (no host sync)
+            if not self.avg:
+                flat.div_(self.world)
         self.calls += 1
 
 

@@ -118,6 +118,8 @@ class FusedActorCritic:
             raise ValueError("policy has parameters outside the Linear chains")
         self._partials = {}
         self._cq = ops.ColsumQueue()
+        self._cq_early = ops.ColsumQueue()
+        self.early_grad_sync = None   # data-parallel: callable(grad_view) starting an early all-reduce
         self._sq = None
         self.sq_ready = None
         self._params = list(policy.parameters())
@@ -287,7 +289,14 @@ class FusedActorCritic:
         have_rep = len(self.rep) > 0
         if paired:   # dW of both hidden layers and dX (K = 512, no accumulate pass) as single GEMMs
             dz = self._hws.dz_pair
-            self._weight_grad(dz, s, self.pair[2], queue=self._cq)
+            if self.early_grad_sync is not None:
+                # data-parallel: finalize this 0.5 MB slice now and start its all-reduce, which then overlaps
+                # the dX GEMM and the trunk backward (distributed.GradAllReduce.begin)
+                self._weight_grad(dz, s, self.pair[2], queue=self._cq_early)
+                self._cq_early.flush(s.device)
+                self.early_grad_sync(self.pair[2])
+            else:
+                self._weight_grad(dz, s, self.pair[2], queue=self._cq)
             if have_rep:
                 self._chain_backward(self.rep, [x] + rep_outs[:-1], rep_outs, torch.mm(dz, self.pair[0]),
                                      need_dx=False, thin_first=self.thin0)

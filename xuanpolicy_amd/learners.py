@@ -114,6 +114,7 @@ class _FusedPolicyGradient(Learner):
         self.iterations += 1
         fm = self._fused_mlp()
         if fm is not None and fm.fused_heads:
+            fm.early_grad_sync = getattr(self.grad_sync, "begin", None) if self.grad_sync is not None else None
             ctx = fm.forward_hidden(obs)   # K12: heads, loss and head backward in one pass per head
             scalars = fm.loss_backward(ctx, self.algo, self.dist, act, adv, ret, old_logp=old_logp, idx=idx,
                                        adv_partials=adv_partials, clip_range=self.clip_range, vf_coef=self.vf_coef,
