@@ -103,6 +103,50 @@ def gae_graph_replay_us(mem, reps=50):
     return e0.elapsed_time(e1) / reps * 1e3
 
 
+def loss_sweep(device, sizes=(65536, 262144, 1048576, 4194304), act_dim=6, reps=7):
+    """K2 alone (xpa_policy_loss_fwd_bwd, Gaussian PPO, rows in order: the drop-in learners' form; the C2
+    fast path fuses the loss into K16's epilogue instead), Infinity Cache flushed before each timed launch.
+    Inputs as SURVEY.md §8(d): mu ~ N(0, 0.5), logstd = -1 + N(0, 0.1), actions drawn around mu, adv / ret / v
+    ~ N(0, 1)."""
+    import torch
+    from xuanpolicy_amd import _lib, ops
+    flush = torch.empty(512 * 1024 * 1024 // 4, dtype=torch.float32, device=device)
+    L = ops.lib()
+    s = ops._stream(device)
+    out = []
+    A = act_dim
+    for B in sizes:
+        g = torch.Generator(device=device).manual_seed(B + 1)
+        mu = torch.randn(B, A, device=device, generator=g) * 0.5
+        logstd = -1.0 + 0.1 * torch.randn(A, device=device, generator=g)
+        act = mu + torch.exp(logstd) * torch.randn(B, A, device=device, generator=g)
+        old = torch.randn(B, device=device, generator=g) * 0.3 - 2.0
+        adv, ret, v = (torch.randn(B, device=device, generator=g) for _ in range(3))
+        ws = ops.LossWorkspace(B, A, device, "gaussian")
+        times = []
+        for _ in range(reps):
+            flush.fill_(1.0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = L.xpa_policy_loss_fwd_bwd(ops.ALGO["ppo"], ops.DIST["gaussian"], B, A, ops._p(mu), ops._p(logstd),
+                                           ops._p(v), None, B, ops._p(act), ops._p(old), ops._p(adv), ops._p(ret),
+                                           None, 0, 0.2, 0.25, 0.0, ops._p(ws.d_head), ops._p(ws.d_v),
+                                           ops._p(ws.partials), s)
+            e1.record()
+            _lib.check(rc, "xpa_policy_loss_fwd_bwd")
+            e1.synchronize()
+            times.append(e0.elapsed_time(e1))
+        times.sort()
+        ms = times[len(times) // 2]
+        b = loss_bytes_gauss(B, A)
+        out.append({"batch": B, "act_dim": A, "ms": round(ms, 5), "GB/s": round(b / ms / 1e6, 1),
+                    "frac": round(b / ms / 1e6 / HBM_PEAK_GBS, 3), "algorithmic_bytes": int(b)})
+        del mu, logstd, act, old, adv, ret, v, ws
+    del flush
+    torch.cuda.empty_cache()
+    return out
+
+
 def gae_sweep(device, sizes=(4096, 65536, 262144, 1048576), horizon=128, reps=7):
     """GAE kernel alone (the in-loop compact form, ~1/8 of the rows with a mid-buffer truncation),
     Infinity Cache flushed (512 MiB write) before each timed launch."""
@@ -496,6 +540,17 @@ def main():
             result["c4_box376"] = c4
         if not args.no_sweep and world == 1:
             result["gae_sweep_flushed"] = gae_sweep(device, horizon=T)
+            ls = loss_sweep(device, act_dim=args.act_dim)
+            result["loss_sweep_flushed"] = ls
+            if result["loss_kernel"] is None and ls:
+                k2 = ls[0]   # the C2 minibatch size
+                result["loss_kernel"] = {
+                    "kernel": "xpa_policy_loss_fwd_bwd (K2, gaussian, ppo; standalone: the C2 fast path fuses the "
+                              "loss into K16's epilogue)", "bound": "hbm", "batch": k2["batch"],
+                    "avg_launch_us": round(k2["ms"] * 1e3, 3), "achieved": k2["GB/s"], "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": k2["frac"], "algorithmic_bytes_per_launch": k2["algorithmic_bytes"],
+                    "timing": "host-recorded events around one launch after a 512 MiB cache flush (median of 7); "
+                              "see loss_sweep_flushed for larger batches"}
         if not args.no_c3 and world == 1:
             result["c3_atari_a2c"] = c3_bench(device)
         if not args.no_per and world == 1:

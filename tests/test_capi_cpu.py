@@ -40,7 +40,7 @@ def test_bindings_cover_header():
 
 def test_abi_version_and_size_helpers(lib):
     assert lib.xpa_abi_version() == _lib.ABI_VERSION
-    assert lib.xpa_loss_num_partials(65536) == 256
+    assert lib.xpa_loss_num_partials(65536) == 256 and lib.xpa_loss_num_partials(1 << 22) == 2048
     assert lib.xpa_loss_partial_width(6) == 11
     assert lib.xpa_gather_num_partials(65537) == 1025
     assert lib.xpa_rms_num_partials(4096) == 16

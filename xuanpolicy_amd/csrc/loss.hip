@@ -44,7 +44,13 @@ __device__ __forceinline__ void adv_moments(const double *partials, int64_t n_pa
     }
 }
 
-template <int DIST, int ALGO>
+// Grid-stride form: at most kLossMaxBlocks blocks (8 per CU), each thread walks rows b, b + grid * 256, ...
+// accumulating its loss terms (and, Gaussian, its d logstd terms: KM registers, KM >= A) before ONE block
+// reduction — the per-block prologue (exp/log of logstd, the adv moments) and the reduction are paid once
+// per ~B / 2048 rows instead of once per 256.  Per-row arithmetic (d_head, d_v) is unchanged.
+constexpr int64_t kLossMaxBlocks = 2048;
+
+template <int DIST, int ALGO, int KM>
 __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
     int64_t batch, int A, const float *__restrict__ head, const float *__restrict__ logstd,
     const float *__restrict__ v, const int64_t *__restrict__ idx, int64_t n_rows, const float *__restrict__ act,
@@ -78,37 +84,51 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
         s_ent = e;
     }
     __syncthreads();
-
-    const int64_t b = (int64_t)blockIdx.x * kLossThreads + tid;
-    int64_t row = b < batch ? (idx ? idx[b] : b) : 0;
-    const bool valid = b < batch && row >= 0 && row < n_rows;
-    if (!valid) row = 0;
-    if (b < batch && !valid) {  // out-of-range index: zero gradient, no contribution
-        d_v[b] = 0.f;
-        for (int a = 0; a < A; ++a) d_head[b * A + a] = 0.f;
-    }
     const float inv_b = 1.0f / (float)batch;
+    const float mean_a = s_mean, inv_a = s_inv;
+    float var_r[KM], logsc_r[KM];
+#pragma unroll
+    for (int a = 0; a < KM; ++a) {
+        var_r[a] = (DIST == XPA_DIST_GAUSSIAN && a < A) ? s_var[a] : 1.f;
+        logsc_r[a] = (DIST == XPA_DIST_GAUSSIAN && a < A) ? s_logscale[a] : 0.f;
+    }
+    const float ent_g = DIST == XPA_DIST_GAUSSIAN ? s_ent : 0.f;
 
-    float surr = 0.f, sq = 0.f, ent = 0.f, clipc = 0.f, vv = 0.f;
-    float dlogp = 0.f;
-    float lse = 0.f, H = 0.f;  // categorical
-    int ai = 0;
-    if (valid) {
-        const float A_n = (adv[row] - s_mean) * s_inv;
+    float surr_t = 0.f, sq_t = 0.f, ent_t = 0.f, clip_t = 0.f, vv_t = 0.f;
+    float dls_t[KM];
+#pragma unroll
+    for (int a = 0; a < KM; ++a) dls_t[a] = 0.f;
+
+    const int64_t stride = (int64_t)gridDim.x * kLossThreads;
+    for (int64_t b = (int64_t)blockIdx.x * kLossThreads + tid; b < batch; b += stride) {
+        int64_t row = idx ? idx[b] : b;
+        const bool valid = row >= 0 && row < n_rows;
+        if (!valid) {  // out-of-range index: zero gradient, no contribution
+            d_v[b] = 0.f;
+            for (int a = 0; a < A; ++a) d_head[b * A + a] = 0.f;
+            continue;
+        }
+        const float A_n = (adv[row] - mean_a) * inv_a;
         const float vb = v[b];
         const float diffv = vb - ret[row];
-        sq = diffv * diffv;
-        vv = vb;
+        sq_t += diffv * diffv;
+        vv_t += vb;
         d_v[b] = vf_coef * 2.0f * diffv * inv_b;
-        float logp = 0.f;
+        float logp = 0.f, lse = 0.f, H = 0.f;
+        int ai = 0;
+        float diff_r[KM];
         if (DIST == XPA_DIST_GAUSSIAN) {
             const float *mu = head + b * A;
             const float *x = act + row * A;
-            for (int a = 0; a < A; ++a) {
-                const float diff = x[a] - mu[a];
-                logp += -(diff * diff) / (2.0f * s_var[a]) - s_logscale[a] - kLogSqrt2Pi;
+#pragma unroll
+            for (int a = 0; a < KM; ++a) {
+                diff_r[a] = 0.f;
+                if (a < A) {
+                    diff_r[a] = x[a] - mu[a];
+                    logp += -(diff_r[a] * diff_r[a]) / (2.0f * var_r[a]) - logsc_r[a] - kLogSqrt2Pi;
+                }
             }
-            ent = s_ent;
+            ent_t += ent_g;
         } else {
             const float *z = head + b * A;
             float m = z[0];
@@ -123,30 +143,35 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
                 const float ln = z[k] - lse;
                 H -= expf(ln) * ln;
             }
-            ent = H;
+            ent_t += H;
         }
+        float dlogp;
         if (ALGO == XPA_ALGO_PPO) {
             const float ratio = expf(logp - old_logp[row]);
             const float lo = 1.0f - clip_range, hi = 1.0f + clip_range;
             const float cr = fminf(fmaxf(ratio, lo), hi);
             const float s1 = cr * A_n;
             const float s2 = A_n * ratio;
-            surr = fminf(s1, s2);
+            surr_t += fminf(s1, s2);
             const bool inr = (ratio >= lo) && (ratio <= hi);
             const float g1 = inr ? A_n : 0.f;
             const float w1 = (s1 < s2) ? 1.f : ((s1 == s2) ? 0.5f : 0.f);
             const float w2 = (s2 < s1) ? 1.f : ((s1 == s2) ? 0.5f : 0.f);
             dlogp = -inv_b * (w1 * g1 + w2 * A_n) * ratio;
-            clipc = ((ratio < lo) || (ratio > hi)) ? 1.f : 0.f;
+            clip_t += ((ratio < lo) || (ratio > hi)) ? 1.f : 0.f;
         } else {
-            surr = A_n * logp;
+            surr_t += A_n * logp;
             dlogp = -A_n * inv_b;
         }
         if (DIST == XPA_DIST_GAUSSIAN) {
-            const float *mu = head + b * A;
-            const float *x = act + row * A;
             float *dm = d_head + b * A;
-            for (int a = 0; a < A; ++a) dm[a] = dlogp * (x[a] - mu[a]) / s_var[a];
+#pragma unroll
+            for (int a = 0; a < KM; ++a) {
+                if (a < A) {
+                    dm[a] = dlogp * diff_r[a] / var_r[a];
+                    dls_t[a] += dlogp * (diff_r[a] * diff_r[a] / var_r[a] - 1.0f);
+                }
+            }
         } else {
             const float *z = head + b * A;
             float *dz = d_head + b * A;
@@ -164,8 +189,8 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
     const int w = tid >> 6;
     const bool lane0 = (tid & 63) == 0;
     {
-        const float r0 = xpa_wave_sum(surr), r1 = xpa_wave_sum(sq), r2 = xpa_wave_sum(ent);
-        const float r3 = xpa_wave_sum(clipc), r4 = xpa_wave_sum(vv);
+        const float r0 = xpa_wave_sum(surr_t), r1 = xpa_wave_sum(sq_t), r2 = xpa_wave_sum(ent_t);
+        const float r3 = xpa_wave_sum(clip_t), r4 = xpa_wave_sum(vv_t);
         if (lane0) {
             s_red[0 * kLossWaves + w] = r0;
             s_red[1 * kLossWaves + w] = r1;
@@ -175,16 +200,12 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
         }
     }
     if (DIST == XPA_DIST_GAUSSIAN) {
-        const float *mu = head + b * A;
-        const float *x = act + row * A;
-        for (int a = 0; a < A; ++a) {
-            float g = 0.f;
-            if (valid) {
-                const float diff = x[a] - mu[a];
-                g = dlogp * (diff * diff / s_var[a] - 1.0f);
+#pragma unroll
+        for (int a = 0; a < KM; ++a) {
+            if (a < A) {
+                const float g = xpa_wave_sum(dls_t[a]);
+                if (lane0) s_red[(kPartBase + a) * kLossWaves + w] = g;
             }
-            g = xpa_wave_sum(g);
-            if (lane0) s_red[(kPartBase + a) * kLossWaves + w] = g;
         }
     }
     __syncthreads();
@@ -240,7 +261,10 @@ __global__ __launch_bounds__(256) void policy_loss_finalize_kernel(int algo, int
 
 }  // namespace
 
-XPA_API int64_t xpa_loss_num_partials(int64_t batch) { return (batch + kLossThreads - 1) / kLossThreads; }
+XPA_API int64_t xpa_loss_num_partials(int64_t batch) {
+    const int64_t blocks = (batch + kLossThreads - 1) / kLossThreads;
+    return blocks < kLossMaxBlocks ? blocks : kLossMaxBlocks;
+}
 
 XPA_API int64_t xpa_loss_partial_width(int64_t act_dim) { return kPartBase + act_dim; }
 
@@ -264,17 +288,22 @@ XPA_API int xpa_policy_loss_fwd_bwd(int algo, int dist, int64_t batch, int64_t a
     const int width = (int)xpa_loss_partial_width(act_dim);
     const int A = (int)act_dim;
     hipStream_t s = (hipStream_t)stream;
-#define XPA_LOSS_LAUNCH(D_, A_)                                                                                    \
-    hipLaunchKernelGGL((policy_loss_kernel<D_, A_>), dim3((unsigned)blocks), dim3(kLossThreads), 0, s, batch, A,  \
-                       head, logstd, v, idx, n_rows, act, old_logp, adv, ret, adv_partials, n_adv_partials, clip_range,   \
-                       vf_coef, ent_coef, d_head, d_v, partials, width)
+#define XPA_LOSS_LAUNCH(D_, A_, KM_)                                                                              \
+    hipLaunchKernelGGL((policy_loss_kernel<D_, A_, KM_>), dim3((unsigned)blocks), dim3(kLossThreads), 0, s, batch,  \
+                       A, head, logstd, v, idx, n_rows, act, old_logp, adv, ret, adv_partials, n_adv_partials,       \
+                       clip_range, vf_coef, ent_coef, d_head, d_v, partials, width)
+#define XPA_LOSS_GAUSS(A_)                                                \
+    if (A <= 8) XPA_LOSS_LAUNCH(XPA_DIST_GAUSSIAN, A_, 8);                \
+    else if (A <= 20) XPA_LOSS_LAUNCH(XPA_DIST_GAUSSIAN, A_, 20);         \
+    else XPA_LOSS_LAUNCH(XPA_DIST_GAUSSIAN, A_, kMaxAct);
     if (dist == XPA_DIST_GAUSSIAN) {
-        if (algo == XPA_ALGO_PPO) XPA_LOSS_LAUNCH(XPA_DIST_GAUSSIAN, XPA_ALGO_PPO);
-        else XPA_LOSS_LAUNCH(XPA_DIST_GAUSSIAN, XPA_ALGO_A2C);
+        if (algo == XPA_ALGO_PPO) { XPA_LOSS_GAUSS(XPA_ALGO_PPO) }
+        else { XPA_LOSS_GAUSS(XPA_ALGO_A2C) }
     } else {
-        if (algo == XPA_ALGO_PPO) XPA_LOSS_LAUNCH(XPA_DIST_CATEGORICAL, XPA_ALGO_PPO);
-        else XPA_LOSS_LAUNCH(XPA_DIST_CATEGORICAL, XPA_ALGO_A2C);
+        if (algo == XPA_ALGO_PPO) XPA_LOSS_LAUNCH(XPA_DIST_CATEGORICAL, XPA_ALGO_PPO, 1);
+        else XPA_LOSS_LAUNCH(XPA_DIST_CATEGORICAL, XPA_ALGO_A2C, 1);
     }
+#undef XPA_LOSS_GAUSS
 #undef XPA_LOSS_LAUNCH
     return xpa_launch_status();
 }
