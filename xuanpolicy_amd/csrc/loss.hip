@@ -99,13 +99,48 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
 #pragma unroll
     for (int a = 0; a < KM; ++a) dls_t[a] = 0.f;
 
-    const int64_t stride = (int64_t)gridDim.x * kLossThreads;
-    for (int64_t b = (int64_t)blockIdx.x * kLossThreads + tid; b < batch; b += stride) {
+    // Gaussian, KM <= 20: the tile's head rows (and act rows when they are read in order) are staged through
+    // LDS with 16-B loads and d_head leaves through LDS with 16-B stores — the rows are A floats (24 B at
+    // A = 6), so per-thread row accesses would be 4-B loads strided by the row (a TA-bound pattern).
+    constexpr bool kStage = DIST == XPA_DIST_GAUSSIAN && KM <= 20;
+    __shared__ __attribute__((aligned(16))) float s_rows[kStage ? 3 * kLossThreads * KM : 4];
+    const bool stage = kStage && (((uintptr_t)head | (uintptr_t)d_head) % 16 == 0) && (A % 4 == 0 || true);
+    const bool stage_act = stage && idx == nullptr && ((uintptr_t)act % 16 == 0);
+    const int64_t ntiles = (batch + kLossThreads - 1) / kLossThreads;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t b = tile * kLossThreads + tid;
+        const int64_t t0 = tile * kLossThreads;
+        const int nt = (int)(batch - t0 < kLossThreads ? batch - t0 : kLossThreads);  // rows in this tile
+        float *s_mu = s_rows, *s_x = s_rows + kLossThreads * KM, *s_dm = s_rows + 2 * kLossThreads * KM;
+        if (stage) {
+            __syncthreads();  // the previous tile's d_head is out of LDS
+            const int n = nt * A;  // floats of the tile's rows (contiguous in head / act)
+            const float *gm = head + t0 * A, *gx = act + t0 * A;
+            const int n4 = (t0 * A) % 4 == 0 ? n / 4 : 0;  // 16-B aligned tile start: vector part
+            for (int i = tid; i < n4; i += kLossThreads) {
+                reinterpret_cast<float4 *>(s_mu)[i] = reinterpret_cast<const float4 *>(gm)[i];
+                if (stage_act) reinterpret_cast<float4 *>(s_x)[i] = reinterpret_cast<const float4 *>(gx)[i];
+            }
+            for (int i = 4 * n4 + tid; i < n; i += kLossThreads) {
+                s_mu[i] = gm[i];
+                if (stage_act) s_x[i] = gx[i];
+            }
+            __syncthreads();
+        }
+        if (b >= batch) {
+            if (stage) goto store_tile;
+            continue;
+        }
+        {
         int64_t row = idx ? idx[b] : b;
         const bool valid = row >= 0 && row < n_rows;
         if (!valid) {  // out-of-range index: zero gradient, no contribution
             d_v[b] = 0.f;
-            for (int a = 0; a < A; ++a) d_head[b * A + a] = 0.f;
+            if (stage)
+                for (int a = 0; a < A; ++a) s_dm[tid * A + a] = 0.f;
+            else
+                for (int a = 0; a < A; ++a) d_head[b * A + a] = 0.f;
+            if (stage) goto store_tile;
             continue;
         }
         const float A_n = (adv[row] - mean_a) * inv_a;
@@ -118,8 +153,8 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
         int ai = 0;
         float diff_r[KM];
         if (DIST == XPA_DIST_GAUSSIAN) {
-            const float *mu = head + b * A;
-            const float *x = act + row * A;
+            const float *mu = stage ? s_mu + tid * A : head + b * A;
+            const float *x = stage_act ? s_x + tid * A : act + row * A;
 #pragma unroll
             for (int a = 0; a < KM; ++a) {
                 diff_r[a] = 0.f;
@@ -164,7 +199,7 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
             dlogp = -A_n * inv_b;
         }
         if (DIST == XPA_DIST_GAUSSIAN) {
-            float *dm = d_head + b * A;
+            float *dm = stage ? s_dm + tid * A : d_head + b * A;
 #pragma unroll
             for (int a = 0; a < KM; ++a) {
                 if (a < A) {
@@ -182,6 +217,17 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
                 const float oh = (k == ai) ? 1.f : 0.f;
                 dz[k] = dlogp * (oh - p) + ec * p * (ln + H);
             }
+        }
+        }
+    store_tile:
+        if (stage) {  // the tile's d_head rows: LDS -> HBM with 16-B stores
+            __syncthreads();
+            const int n = nt * A;
+            float *gd = d_head + t0 * A;
+            const int n4 = (t0 * A) % 4 == 0 ? n / 4 : 0;
+            for (int i = tid; i < n4; i += kLossThreads)
+                reinterpret_cast<float4 *>(gd)[i] = reinterpret_cast<const float4 *>(s_dm)[i];
+            for (int i = 4 * n4 + tid; i < n; i += kLossThreads) gd[i] = s_dm[i];
         }
     }
     // Block partial sums: every value is wave-reduced by shuffles into its own LDS slot row, then ONE
