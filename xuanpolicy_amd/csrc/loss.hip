@@ -112,6 +112,16 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
         const int64_t t0 = tile * kLossThreads;
         const int nt = (int)(batch - t0 < kLossThreads ? batch - t0 : kLossThreads);  // rows in this tile
         float *s_mu = s_rows, *s_x = s_rows + kLossThreads * KM, *s_dm = s_rows + 2 * kLossThreads * KM;
+        // this row's scalars are requested before the tile staging (one HBM round trip for both)
+        int64_t row = b < batch ? (idx ? idx[b] : b) : -1;
+        const bool valid = row >= 0 && row < n_rows;
+        float p_adv = 0.f, p_v = 0.f, p_ret = 0.f, p_old = 0.f;
+        if (valid) {
+            p_adv = adv[row];
+            p_v = v[b];
+            p_ret = ret[row];
+            if (ALGO == XPA_ALGO_PPO) p_old = old_logp[row];
+        }
         if (stage) {
             __syncthreads();  // the previous tile's d_head is out of LDS
             const int n = nt * A;  // floats of the tile's rows (contiguous in head / act)
@@ -132,8 +142,6 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
             continue;
         }
         {
-        int64_t row = idx ? idx[b] : b;
-        const bool valid = row >= 0 && row < n_rows;
         if (!valid) {  // out-of-range index: zero gradient, no contribution
             d_v[b] = 0.f;
             if (stage)
@@ -143,9 +151,9 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
             if (stage) goto store_tile;
             continue;
         }
-        const float A_n = (adv[row] - mean_a) * inv_a;
-        const float vb = v[b];
-        const float diffv = vb - ret[row];
+        const float A_n = (p_adv - mean_a) * inv_a;
+        const float vb = p_v;
+        const float diffv = vb - p_ret;
         sq_t += diffv * diffv;
         vv_t += vb;
         d_v[b] = vf_coef * 2.0f * diffv * inv_b;
@@ -182,7 +190,7 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
         }
         float dlogp;
         if (ALGO == XPA_ALGO_PPO) {
-            const float ratio = expf(logp - old_logp[row]);
+            const float ratio = expf(logp - p_old);
             const float lo = 1.0f - clip_range, hi = 1.0f + clip_range;
             const float cr = fminf(fmaxf(ratio, lo), hi);
             const float s1 = cr * A_n;
