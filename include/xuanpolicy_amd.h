@@ -292,6 +292,14 @@ int64_t xpa_colsum_batch_tiles(int n_segs, const int64_t *n_partials, const int6
 int xpa_colsum_finalize_batch_sq(int n_segs, const float *const *partials, const int64_t *n_partials,
                                  const int64_t *cols, float *const *outs, double *sq, int32_t *ticket,
                                  xpa_stream_t stream);
+/* xpa_colsum_finalize_batch_sq with xpa_policy_loss_finalize_sq run by one extra (last) block of the same
+ * launch: the loss scalars and d logstd as that call writes them, its d logstd share of the clip norm in
+ * sq[0] (so sq[0] need not be written beforehand).  sq and ticket are required. */
+int xpa_colsum_finalize_batch_sq_loss(int n_segs, const float *const *partials, const int64_t *n_partials,
+                                      const int64_t *cols, float *const *outs, double *sq, int32_t *ticket, int algo,
+                                      int dist, int64_t batch, int64_t act_dim, const float *loss_partials,
+                                      int64_t n_loss_partials, float vf_coef, float ent_coef, float *scalars,
+                                      float *d_logstd, xpa_stream_t stream);
 
 /* K14 — rollout policy head: the last hidden activation and both output layers of the actor-critic
  * (gaussian.py:8-51 / categorical.py:16-58 forward in PPOCLIP_Agent._action, ppoclip_agent.py:50-57)

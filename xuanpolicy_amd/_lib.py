@@ -77,6 +77,9 @@ SIGNATURES = {
     "xpa_value_head": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_f32, c_p, c_p, c_p, c_p]),
     "xpa_colsum_batch_tiles": (c_i64, [ctypes.c_int, c_p, c_p]),
     "xpa_colsum_finalize_batch_sq": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "xpa_colsum_finalize_batch_sq_loss": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p, c_p, ctypes.c_int,
+                                                         ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_f32, c_f32, c_p,
+                                                         c_p, c_p]),
     "xpa_policy_loss_finalize_sq": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_f32, c_f32,
                                                    c_p, c_p, c_p, c_p]),
     "xpa_clip_adam_step_partials": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_f32, c_f32, c_f32, c_f32,

@@ -14,6 +14,7 @@
 // gradient on [1-eps, 1+eps] inclusive; minimum() splits an exact tie half/half.
 // HBM-bound elementwise work: Gaussian 4(3A+5) B/sample, Categorical 4(2K+6) B/sample.
 #include "xpa_common.h"
+#include "loss_finalize.h"
 
 namespace {
 
@@ -273,44 +274,10 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
     }
 }
 
-__global__ __launch_bounds__(256) void policy_loss_finalize_kernel(int algo, int dist, int64_t batch, int A,
-                                                                   const float *__restrict__ partials,
-                                                                   int64_t n_partials, int width, float vf_coef,
-                                                                   float ent_coef, float *__restrict__ scalars,
-                                                                   float *__restrict__ d_logstd,
-                                                                   double *__restrict__ sq_out) {
+__global__ __launch_bounds__(256) void policy_loss_finalize_kernel(XpaLossFinalizeArgs args, double *sq_out) {
     __shared__ double tot[kPartBase];
     __shared__ float s_dls[kMaxAct];
-    const int ncols = kPartBase + (dist == XPA_DIST_GAUSSIAN ? A : 0);
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int j = w; j < ncols; j += 4) {  // one wave per column, fixed lane order -> deterministic
-        double s = 0.0;
-        for (int64_t k = lane; k < n_partials; k += 64) s += (double)partials[k * width + j];
-        s = xpa_wave_sum(s);
-        if (lane == 0) {
-            if (j < kPartBase) tot[j] = s;
-            else d_logstd[j - kPartBase] = s_dls[j - kPartBase] = (float)(s - (double)ent_coef);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0 && sq_out) {  // this gradient's share of the clip norm (xpa_clip_adam_step_partials)
-        double q = 0.0;
-        if (dist == XPA_DIST_GAUSSIAN)
-            for (int a = 0; a < A; ++a) q += (double)s_dls[a] * (double)s_dls[a];
-        *sq_out = q;
-    }
-    if (threadIdx.x == 0) {
-        const double B = (double)batch;
-        const double actor = -tot[0] / B;
-        const double critic = tot[1] / B;
-        const double entropy = tot[2] / B;
-        scalars[XPA_OUT_ACTOR_LOSS] = (float)actor;
-        scalars[XPA_OUT_CRITIC_LOSS] = (float)critic;
-        scalars[XPA_OUT_ENTROPY] = (float)entropy;
-        scalars[XPA_OUT_LOSS] = (float)(actor - (double)ent_coef * entropy + (double)vf_coef * critic);
-        scalars[XPA_OUT_CLIP_RATIO] = algo == XPA_ALGO_PPO ? (float)(tot[3] / B) : 0.f;
-        scalars[XPA_OUT_VALUE_MEAN] = (float)(tot[4] / B);
-    }
+    xpa_loss_finalize_body(args, sq_out, tot, s_dls);
 }
 
 }  // namespace
@@ -368,9 +335,9 @@ XPA_API int xpa_policy_loss_finalize_sq(int algo, int dist, int64_t batch, int64
     if (batch <= 0 || act_dim <= 0 || act_dim > kMaxAct || n_partials <= 0 || !partials || !scalars)
         return (int)hipErrorInvalidValue;
     if (dist == XPA_DIST_GAUSSIAN && !d_logstd) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(policy_loss_finalize_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, algo, dist, batch,
-                       (int)act_dim, partials, n_partials, (int)xpa_loss_partial_width(act_dim), vf_coef, ent_coef,
-                       scalars, d_logstd, sq_out);
+    const XpaLossFinalizeArgs args{algo, dist, batch, (int)act_dim, partials, n_partials,
+                                   (int)xpa_loss_partial_width(act_dim), vf_coef, ent_coef, scalars, d_logstd};
+    hipLaunchKernelGGL(policy_loss_finalize_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, args, sq_out);
     return xpa_launch_status();
 }
 

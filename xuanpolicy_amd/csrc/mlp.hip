@@ -10,6 +10,7 @@
 // (the mask is taken from the activation OUTPUT h: h > 0 <=> z > 0 for slope >= 0), 2 = tanh (1 - h^2).
 // HBM-bound: 12 B per element (dh, h read; dz written) + C*4 B per 256 rows of partials.
 #include "xpa_common.h"
+#include "loss_finalize.h"
 
 namespace {
 
@@ -307,6 +308,10 @@ struct ColsumBatch {
     // the fixed-order total of sq[0 .. tiles] into sq[1 + tiles] and resets the ticket.
     double *sq;
     unsigned int *ticket;
+    // has_loss: the LAST block runs the loss finalize (xpa_loss_finalize_body) instead of a column tile,
+    // writing its d logstd share into sq[0] before taking its ticket
+    int has_loss;
+    XpaLossFinalizeArgs loss;
 };
 
 __global__ __launch_bounds__(kColTile * kColGroups) void colsum_finalize_batch_kernel(ColsumBatch b) {
@@ -314,8 +319,13 @@ __global__ __launch_bounds__(kColTile * kColGroups) void colsum_finalize_batch_k
     __shared__ bool s_last;
     const int tile = blockIdx.x;
     int sg = 0;
-    while (tile >= b.tile0[sg + 1]) ++sg;
     double *sq = b.sq ? b.sq + 1 + tile : nullptr;
+    if (b.has_loss && tile == (int)gridDim.x - 1) {
+        __shared__ double s_tot[kXpaLossPartBase];
+        __shared__ float s_dls[kXpaLossMaxAct];
+        xpa_loss_finalize_body(b.loss, b.sq, s_tot, s_dls);
+    } else {
+    while (tile >= b.tile0[sg + 1]) ++sg;
     if (b.G[sg] <= kWideMaxG) {
         const int64_t G = b.G[sg];
         const int C = b.C[sg];
@@ -341,13 +351,14 @@ __global__ __launch_bounds__(kColTile * kColGroups) void colsum_finalize_batch_k
     } else {
         colsum_tile(b.part[sg], b.G[sg], b.C[sg], (tile - b.tile0[sg]) * kColTile, b.out[sg], s_red, sq);
     }
+    }
     if (!b.sq) return;
     xpa_drain();  // this block's partial (sc1 store) complete before its ticket
     __syncthreads();
     if (threadIdx.x == 0) s_last = xpa_ticket(b.ticket) == gridDim.x - 1;
     __syncthreads();
     if (!s_last) return;
-    const int n = (int)gridDim.x + 1;  // sq[0 .. tiles]
+    const int n = (int)gridDim.x + (b.has_loss ? 0 : 1);  // sq[0 .. tiles]
     // thread t sums a contiguous run of the partials in order, then the runs in thread order (fixed)
     const int per = (n + kWideTile - 1) / kWideTile;
     double acc = 0.0;
@@ -462,14 +473,19 @@ XPA_API int64_t xpa_colsum_batch_tiles(int n_segs, const int64_t *n_partials, co
     return tiles;
 }
 
-XPA_API int xpa_colsum_finalize_batch_sq(int n_segs, const float *const *partials, const int64_t *n_partials,
-                                         const int64_t *cols, float *const *outs, double *sq, int32_t *ticket,
-                                         xpa_stream_t stream) {
+namespace {
+int colsum_batch_launch(int n_segs, const float *const *partials, const int64_t *n_partials, const int64_t *cols,
+                        float *const *outs, double *sq, int32_t *ticket, const XpaLossFinalizeArgs *loss,
+                        xpa_stream_t stream) {
     if (n_segs <= 0 || n_segs > kMaxSegs || !partials || !n_partials || !cols || !outs) return (int)hipErrorInvalidValue;
     if (sq && !ticket) return (int)hipErrorInvalidValue;
     ColsumBatch b{};
     b.sq = sq;
     b.ticket = (unsigned int *)ticket;
+    if (loss) {
+        b.has_loss = 1;
+        b.loss = *loss;
+    }
     b.n = n_segs;
     int64_t tiles = 0;
     for (int i = 0; i < n_segs; ++i) {
@@ -483,9 +499,30 @@ XPA_API int xpa_colsum_finalize_batch_sq(int n_segs, const float *const *partial
         tiles += seg_tiles(n_partials[i], cols[i]);
     }
     b.tile0[n_segs] = (int)tiles;
-    hipLaunchKernelGGL(colsum_finalize_batch_kernel, dim3((unsigned)tiles), dim3(kColTile * kColGroups), 0,
-                       (hipStream_t)stream, b);
+    hipLaunchKernelGGL(colsum_finalize_batch_kernel, dim3((unsigned)(tiles + (loss ? 1 : 0))),
+                       dim3(kColTile * kColGroups), 0, (hipStream_t)stream, b);
     return xpa_launch_status();
+}
+}  // namespace
+
+XPA_API int xpa_colsum_finalize_batch_sq(int n_segs, const float *const *partials, const int64_t *n_partials,
+                                         const int64_t *cols, float *const *outs, double *sq, int32_t *ticket,
+                                         xpa_stream_t stream) {
+    return colsum_batch_launch(n_segs, partials, n_partials, cols, outs, sq, ticket, nullptr, stream);
+}
+
+XPA_API int xpa_colsum_finalize_batch_sq_loss(int n_segs, const float *const *partials, const int64_t *n_partials,
+                                              const int64_t *cols, float *const *outs, double *sq, int32_t *ticket,
+                                              int algo, int dist, int64_t batch, int64_t act_dim,
+                                              const float *loss_partials, int64_t n_loss_partials, float vf_coef,
+                                              float ent_coef, float *scalars, float *d_logstd,
+                                              xpa_stream_t stream) {
+    if (!sq || !ticket || batch <= 0 || act_dim <= 0 || act_dim > kXpaLossMaxAct || n_loss_partials <= 0 ||
+        !loss_partials || !scalars || (dist == XPA_DIST_GAUSSIAN && !d_logstd))
+        return (int)hipErrorInvalidValue;
+    const XpaLossFinalizeArgs loss{algo, dist, batch, (int)act_dim, loss_partials, n_loss_partials,
+                                   (int)xpa_loss_partial_width(act_dim), vf_coef, ent_coef, scalars, d_logstd};
+    return colsum_batch_launch(n_segs, partials, n_partials, cols, outs, sq, ticket, &loss, stream);
 }
 
 XPA_API int xpa_colsum_finalize_batch(int n_segs, const float *const *partials, const int64_t *n_partials,

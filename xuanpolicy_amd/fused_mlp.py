@@ -285,7 +285,8 @@ class FusedActorCritic:
                                               z_c, lin_co.weight, lin_co.bias, (c_code, c_slope), self.logstd, act,
                                               adv, ret, old_logp=old_logp, idx=idx, adv_partials=adv_partials,
                                               clip_range=clip_range, vf_coef=vf_coef, ent_coef=ent_coef, grads=grads,
-                                              colsum_queue=self._cq, gemm=gemm, sq_logstd=self._sq.data_ptr())
+                                              colsum_queue=self._cq, gemm=gemm, sq_logstd=self._sq.data_ptr(),
+                                              defer_loss=True)
         have_rep = len(self.rep) > 0
         if paired:   # dW of both hidden layers and dX (K = 512, no accumulate pass) as single GEMMs
             dz = self._hws.dz_pair

@@ -393,6 +393,12 @@ class ColsumQueue:
         self.items = []
         self._plans = {}
         self._ticket = None
+        self.loss = None   # deferred loss finalize (defer_loss): run as one extra block of the flush
+
+    def defer_loss(self, algo, dist, batch, act_dim, loss_partials, vf_coef, ent_coef, scalars, d_logstd):
+        """Queue xpa_policy_loss_finalize_sq for the flush (its d logstd share of the clip norm lands in sq[0])."""
+        self.loss = (int(algo), int(dist), int(batch), int(act_dim), loss_partials, float(vf_coef), float(ent_coef),
+                     scalars, d_logstd)
 
     def add(self, part, out):
         _req(part, "partials", torch.float32)
@@ -424,12 +430,26 @@ class ColsumQueue:
         s = _stream(dev)
         L = lib()
         total = None
-        if sq is not None and len(plan) == 1 and plan[0][3] + 2 <= sq.numel():
+        loss, self.loss = self.loss, None
+        one = sq is not None and len(plan) == 1 and plan[0][3] + 2 <= sq.numel()
+        if loss is not None and not one:   # the loss finalize on its own (d logstd share into sq[0] if any)
+            a, d, B, K, lp, vf, ent, sc, dls = loss
+            _lib.check(L.xpa_policy_loss_finalize_sq(a, d, B, K, _p(lp), lp.shape[0], vf, ent, _p(sc), _p(dls),
+                                                     _p(sq) if sq is not None else None, s),
+                       "xpa_policy_loss_finalize")
+            loss = None
+        if one:
             if self._ticket is None:
                 self._ticket = torch.zeros((1,), dtype=torch.int32, device=dev)
             n, _keep, args, tiles = plan[0]
-            _lib.check(L.xpa_colsum_finalize_batch_sq(n, *args, _p(sq), _p(self._ticket), s),
-                       "xpa_colsum_finalize_batch_sq")
+            if loss is not None:   # one launch: the column tiles + the loss finalize block
+                a, d, B, K, lp, vf, ent, sc, dls = loss
+                _lib.check(L.xpa_colsum_finalize_batch_sq_loss(n, *args, _p(sq), _p(self._ticket), a, d, B, K, _p(lp),
+                                                               lp.shape[0], vf, ent, _p(sc), _p(dls), s),
+                           "xpa_colsum_finalize_batch_sq_loss")
+            else:
+                _lib.check(L.xpa_colsum_finalize_batch_sq(n, *args, _p(sq), _p(self._ticket), s),
+                           "xpa_colsum_finalize_batch_sq")
             total = sq[1 + tiles:2 + tiles]
         else:
             for n, _keep, args, _tiles in plan:
@@ -441,7 +461,7 @@ class ColsumQueue:
 
 def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, w_critic, b_critic, act_critic,
                 logstd, act, adv, ret, old_logp=None, idx=None, adv_partials=None, clip_range=0.2, vf_coef=0.25,
-                ent_coef=0.0, grads=None, colsum_queue=None, gemm=None, sq_logstd=None):
+                ent_coef=0.0, grads=None, colsum_queue=None, gemm=None, sq_logstd=None, defer_loss=False):
     """K12 actor + critic heads, loss finalize and the column-sum finalizes.
 
     z_*: hidden pre-activations [B, 256] (unit column stride; row stride = the workspace dz row stride,
@@ -519,11 +539,15 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
     d_logstd = g.get("logstd")
     if dist == "gaussian" and d_logstd is None:
         d_logstd = torch.empty((K,), dtype=torch.float32, device=dev)
-    # sq_logstd: device address of one double receiving sum(d_logstd^2) (the clip norm's share of logstd)
-    _lib.check(L.xpa_policy_loss_finalize_sq(ALGO[algo], DIST[dist], B, K, _p(ws.loss_partials), ws.G,
-                                             float(vf_coef), float(ent_coef), _p(ws.scalars), _p(d_logstd),
-                                             sq_logstd, s), "xpa_policy_loss_finalize")
     queue = colsum_queue if colsum_queue is not None else ColsumQueue()
+    if defer_loss and colsum_queue is not None:
+        # run by the queue's flush (one extra block of the batched finalize launch; writes sq[0] there)
+        queue.defer_loss(ALGO[algo], DIST[dist], B, K, ws.loss_partials, vf_coef, ent_coef, ws.scalars, d_logstd)
+    else:
+        # sq_logstd: device address of one double receiving sum(d_logstd^2) (the clip norm's share of logstd)
+        _lib.check(L.xpa_policy_loss_finalize_sq(ALGO[algo], DIST[dist], B, K, _p(ws.loss_partials), ws.G,
+                                                 float(vf_coef), float(ent_coef), _p(ws.scalars), _p(d_logstd),
+                                                 sq_logstd, s), "xpa_policy_loss_finalize")
     for key, part in (("w_actor", ws.p_dw_actor), ("b_actor", ws.p_dbo_actor), ("bh_actor", ws.p_dbh_actor),
                       ("w_critic", ws.p_dw_critic), ("b_critic", ws.p_dbo_critic), ("bh_critic", ws.p_dbh_critic)):
         if key in g:
