@@ -369,3 +369,42 @@ def test_rollout_head_with_fused_env_step(D, A, act):
         for name in ("ep_step", "ep_index", "ep_score", "ep_last_score", "ep_last_len"):
             getattr(e2, name).copy_(getattr(e1, name))
     assert int(envs[0].ep_index.sum()) > 0
+
+
+@pytest.mark.parametrize("nseg,dist", [(3, 0), (17, 0), (3, 1)])
+def test_colsum_queue_deferred_loss_finalize(nseg, dist):
+    """ColsumQueue.defer_loss: the loss finalize run as the batched finalize's extra block (one plan) or on
+    its own ahead of it (more segments than one launch holds) == xpa_policy_loss_finalize_sq called
+    directly: loss scalars and d logstd bitwise, and the clip-norm total = the outputs' squares + d logstd's."""
+    from xuanpolicy_amd import ops
+    L, s = ops.lib(), ops._stream()
+    torch.manual_seed(nseg + dist)
+    B, K, G = 65536, 6, 512
+    W = int(L.xpa_loss_partial_width(K))
+    lp = torch.randn(G, W, device=DEV) * 0.01
+    sc_ref, dls_ref = torch.zeros(ops.N_OUT, device=DEV), torch.zeros(K, device=DEV)
+    sq_ref = torch.zeros(1, dtype=torch.float64, device=DEV)
+    assert L.xpa_policy_loss_finalize_sq(0, dist, B, K, ops._p(lp), G, 0.25, 0.01, ops._p(sc_ref), ops._p(dls_ref),
+                                         ops._p(sq_ref), s) == 0
+    q = ops.ColsumQueue()
+    outs = []
+    for i in range(nseg):
+        part = torch.randn(8 if i % 2 else 64, 300 + i, device=DEV)
+        out = torch.empty(300 + i, device=DEV)
+        q.add(part, out)
+        outs.append(out)
+    sc, dls = torch.zeros(ops.N_OUT, device=DEV), torch.zeros(K, device=DEV)
+    sq = torch.zeros(16384, dtype=torch.float64, device=DEV)
+    q.defer_loss(0, dist, B, K, lp, 0.25, 0.01, sc, dls)
+    total, written = q.flush(DEV, sq=sq)
+    torch.cuda.synchronize()
+    assert torch.equal(sc, sc_ref)
+    if dist == 0:
+        assert torch.equal(dls, dls_ref)
+    assert float(sq[0]) == float(sq_ref[0])
+    assert written == sum(o.numel() for o in outs) and q.loss is None
+    if nseg <= ops.ColsumQueue.MAX_SEGS:
+        exp = sum(float((o.double() ** 2).sum()) for o in outs) + float(sq_ref[0])
+        assert total is not None and abs(float(total) - exp) <= 1e-9 * max(exp, 1.0)
+    else:
+        assert total is None
