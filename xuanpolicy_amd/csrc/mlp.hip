@@ -314,17 +314,10 @@ struct ColsumBatch {
     XpaLossFinalizeArgs loss;
 };
 
-__global__ __launch_bounds__(kColTile * kColGroups) void colsum_finalize_batch_kernel(ColsumBatch b) {
-    __shared__ double s_red[kColGroups][kColTile];
-    __shared__ bool s_last;
-    const int tile = blockIdx.x;
+// One column tile of a batched finalize (sq: this tile's squared-sum slot or nullptr).
+__device__ __forceinline__ void colsum_batch_tile(const ColsumBatch &b, int tile, double *sq,
+                                                  double (*s_red)[kColTile]) {
     int sg = 0;
-    double *sq = b.sq ? b.sq + 1 + tile : nullptr;
-    if (b.has_loss && tile == (int)gridDim.x - 1) {
-        __shared__ double s_tot[kXpaLossPartBase];
-        __shared__ float s_dls[kXpaLossMaxAct];
-        xpa_loss_finalize_body(b.loss, b.sq, s_tot, s_dls);
-    } else {
     while (tile >= b.tile0[sg + 1]) ++sg;
     if (b.G[sg] <= kWideMaxG) {
         const int64_t G = b.G[sg];
@@ -351,6 +344,18 @@ __global__ __launch_bounds__(kColTile * kColGroups) void colsum_finalize_batch_k
     } else {
         colsum_tile(b.part[sg], b.G[sg], b.C[sg], (tile - b.tile0[sg]) * kColTile, b.out[sg], s_red, sq);
     }
+}
+
+__global__ __launch_bounds__(kColTile * kColGroups) void colsum_finalize_batch_kernel(ColsumBatch b) {
+    __shared__ double s_red[kColGroups][kColTile];
+    __shared__ bool s_last;
+    const int tile = blockIdx.x;
+    if (b.has_loss && tile == (int)gridDim.x - 1) {  // the loss finalize block (its share into sq[0])
+        __shared__ double s_tot[kXpaLossPartBase];
+        __shared__ float s_dls[kXpaLossMaxAct];
+        xpa_loss_finalize_body(b.loss, b.sq, s_tot, s_dls);
+    } else {
+        colsum_batch_tile(b, tile, b.sq ? b.sq + 1 + tile : nullptr, s_red);
     }
     if (!b.sq) return;
     xpa_drain();  // this block's partial (sc1 store) complete before its ticket
