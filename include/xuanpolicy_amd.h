@@ -211,7 +211,8 @@ int xpa_rollout_post(int64_t n_envs, int64_t horizon, const float *rew, const ui
 /* K9 — fused global-norm gradient clipping + Adam over flat fp32 buffers (all 16-B aligned).
  * Replaces torch.nn.utils.clip_grad_norm_ + torch.optim.Adam.step in PPOCLIP_Learner.update /
  * A2C_Learner.update (ppoclip_learner.py:47-49, a2c_learner.py:34-35) for the Adam(eps=1e-5) the runner
- * builds (xuance/torch/runners/runner_drl.py:71).  max_norm <= 0 disables clipping.  step is the
+ * builds (xuance/torch/runners/runner_drl.py:71).  max_norm < 0 disables clipping (max_norm = 0 zeroes the gradient,
+ * as clip_grad_norm_(params, 0) does).  step is the
  * 1-based Adam step count.  norm_partials: xpa_grad_norm_num_partials(n) doubles of scratch.
  * Writes the pre-clip total norm to *total_norm_out when non-NULL. */
 int64_t xpa_grad_norm_num_partials(int64_t n);

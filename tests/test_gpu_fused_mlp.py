@@ -371,7 +371,7 @@ def test_rollout_head_with_fused_env_step(D, A, act):
     assert int(envs[0].ep_index.sum()) > 0
 
 
-@pytest.mark.parametrize("nseg,dist", [(3, 0), (17, 0), (3, 1)])
+@pytest.mark.parametrize("nseg,dist", [(3, 0), (17, 0), (3, 1), (0, 0)])
 def test_colsum_queue_deferred_loss_finalize(nseg, dist):
     """ColsumQueue.defer_loss: the loss finalize run as the batched finalize's extra block (one plan) or on
     its own ahead of it (more segments than one launch holds) == xpa_policy_loss_finalize_sq called
@@ -403,8 +403,135 @@ def test_colsum_queue_deferred_loss_finalize(nseg, dist):
         assert torch.equal(dls, dls_ref)
     assert float(sq[0]) == float(sq_ref[0])
     assert written == sum(o.numel() for o in outs) and q.loss is None
-    if nseg <= ops.ColsumQueue.MAX_SEGS:
+    if nseg == 0:   # nothing queued but the loss: it still runs, no norm total
+        assert total is None
+    elif nseg <= ops.ColsumQueue.MAX_SEGS:
         exp = sum(float((o.double() ** 2).sum()) for o in outs) + float(sq_ref[0])
         assert total is not None and abs(float(total) - exp) <= 1e-9 * max(exp, 1.0)
     else:
         assert total is None
+
+
+@pytest.mark.parametrize("algo,dist,K,B,code", [
+    ("a2c", "categorical", 18, 777, 0),    # the r01 aperture-violation configuration
+    ("ppo", "gaussian", 17, 4133, 1),      # C4 head width, ragged tail (4133 = 64 * 64 + 37)
+    ("ppo", "categorical", 18, 193, 2),
+    ("a2c", "gaussian", 6, 65, 1),
+    ("ppo", "gaussian", 6, 64, 0),
+])
+def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code):
+    """K16 (xpa_head_gemm_actor / _critic) through the C ABI against float64 autograd of the same head:
+    z = x Wh^T + bh, h = act(z), head = h W^T + b, the PPO-Clip / A2C loss with Gaussian / Categorical
+    log-prob + entropy (ppoclip_learner.py:32-44, a2c_learner.py:24-31) and the critic's value loss.
+    Checked: dz (d loss / d z), the summed per-block partials (dW_out, db_out, db_hidden, loss sums) and
+    untouched memory around every output (canaries on both sides of dz and the partials)."""
+    from xuanpolicy_amd import ops
+    L, s = ops.lib(), ops._stream()
+    g = torch.Generator(device=DEV).manual_seed(B + K)
+    H, R = 256, B + 300
+    slope = 0.01
+    x = torch.randn(B, H, device=DEV, generator=g)
+    wh_a, wh_c = (torch.randn(H, H, device=DEV, generator=g) / 16 for _ in range(2))
+    bh_a, bh_c = (torch.randn(H, device=DEV, generator=g) * 0.1 for _ in range(2))
+    w_a = torch.randn(K, H, device=DEV, generator=g) / 16
+    b_a = torch.randn(K, device=DEV, generator=g) * 0.1
+    w_c = torch.randn(1, H, device=DEV, generator=g) / 16
+    b_c = torch.randn(1, device=DEV, generator=g) * 0.1
+    logstd = (-1 + 0.1 * torch.randn(K, device=DEV, generator=g)) if dist == "gaussian" else None
+    idx = torch.randperm(R, device=DEV, generator=g)[:B].contiguous()
+    idx[B // 2] = -1           # invalid rows contribute nothing
+    idx[B - 1] = R + 5
+    adv = torch.randn(R, device=DEV, generator=g)
+    ret = torch.randn(R, device=DEV, generator=g)
+    if dist == "gaussian":
+        act = torch.randn(R, K, device=DEV, generator=g) * 0.5
+    else:
+        act = torch.randint(0, K, (R,), device=DEV, generator=g).float()
+    old = -1.5 + 0.3 * torch.randn(R, device=DEV, generator=g) if algo == "ppo" else None
+    if code != 2:   # kinks: rows with a pre-activation within rounding of 0 take either branch -> invalid
+        with torch.no_grad():
+            near = ((x @ wh_a.t() + bh_a).abs() < 1e-5).any(1) | ((x @ wh_c.t() + bh_c).abs() < 1e-5).any(1)
+        idx[near] = -1
+    G = int(L.xpa_head_fused_num_partials(B))
+    W = int(L.xpa_loss_partial_width(K))
+    pad = 64
+    dz_buf = torch.full((B * 2 * H + 2 * pad,), 777.0, device=DEV)   # canaries around the [B, 512] pair
+    dz = dz_buf[pad:pad + B * 2 * H].view(B, 2 * H)
+
+    def canary(n):
+        return torch.full((n + 2 * pad,), 555.0, device=DEV)
+    p_dw_a, p_dbh_a, p_dbo_a = canary(G * K * H), canary(G * H), canary(G * K)
+    p_dw_c, p_dbh_c, p_dbo_c = canary(G * H), canary(G * H), canary(G)
+    lp = torch.zeros(G * W + 2 * pad, device=DEV)
+    lp[:pad] = 555.0
+    lp[pad + G * W:] = 555.0
+    v = lambda t: ops._p(t[pad:])   # noqa: E731
+    algo_c, dist_c = ops.ALGO[algo], ops.DIST[dist]
+    ent, clip, vf = 0.01, 0.2, 0.25
+    assert L.xpa_head_gemm_actor(algo_c, dist_c, code, B, K, H, ops._p(x), H, ops._p(wh_a), ops._p(bh_a), 2 * H,
+                                 ops._p(w_a), ops._p(b_a), slope, ops._p(logstd) if logstd is not None else None,
+                                 ops._p(idx), R, ops._p(act), ops._p(old) if old is not None else None, ops._p(adv),
+                                 None, 0, clip, ent, ops._p(dz), v(p_dw_a), v(p_dbh_a), v(p_dbo_a), v(lp), W, s) == 0
+    assert L.xpa_head_gemm_critic(code, B, H, ops._p(x), H, ops._p(wh_c), ops._p(bh_c), 2 * H, ops._p(w_c),
+                                  ops._p(b_c), slope, ops._p(idx), R, ops._p(ret), vf, ops._p(dz[:, H:]), v(p_dw_c),
+                                  v(p_dbh_c), v(p_dbo_c), v(lp), W, s) == 0
+    torch.cuda.synchronize()
+    for t in (p_dw_a, p_dbh_a, p_dbo_a, p_dw_c, p_dbh_c, p_dbo_c):
+        assert bool((t[:pad] == 555.0).all()) and bool((t[-pad:] == 555.0).all()), "partials written out of bounds"
+    assert bool((lp[:pad] == 555.0).all()) and bool((lp[-pad:] == 555.0).all()), "loss partials out of bounds"
+    assert bool((dz_buf[:pad] == 777.0).all()) and bool((dz_buf[-pad:] == 777.0).all()), "dz out of bounds"
+
+    # float64 autograd reference
+    d = lambda t: t.detach().double().cpu()   # noqa: E731
+    act_fn = {0: lambda z: z, 1: lambda z: torch.nn.functional.leaky_relu(z, slope), 2: torch.tanh}[code]
+    idx_c = idx.cpu()
+    valid = (idx_c >= 0) & (idx_c < R)
+    rows = idx_c.clamp(0, R - 1)
+    A_n = d(adv)[rows]
+    za = (d(x) @ d(wh_a).t() + d(bh_a)).requires_grad_(True)
+    zc = (d(x) @ d(wh_c).t() + d(bh_c)).requires_grad_(True)
+    wa, ba, wc, bc = (d(t).requires_grad_(True) for t in (w_a, b_a, w_c, b_c))
+    head = act_fn(za) @ wa.t() + ba
+    vv = (act_fn(zc) @ wc.t() + bc)[:, 0]
+    ls = d(logstd).requires_grad_(True) if logstd is not None else None
+    if dist == "gaussian":
+        nd = torch.distributions.Normal(head, ls.exp())
+        logp = nd.log_prob(d(act)[rows]).sum(-1)
+        entr = nd.entropy().sum(-1)
+    else:
+        cd = torch.distributions.Categorical(logits=head)
+        logp = cd.log_prob(d(act)[rows].long())
+        entr = cd.entropy()
+    m = valid.double()
+    if algo == "ppo":
+        ratio = (logp - d(old)[rows]).exp()
+        surr = torch.minimum(ratio.clamp(1 - clip, 1 + clip) * A_n, ratio * A_n)
+    else:
+        surr = A_n * logp
+    actor_loss = -(surr * m).sum() / B
+    entropy = (entr * m).sum() / B
+    critic = ((vv - d(ret)[rows]) ** 2 * m).sum() / B
+    total = actor_loss - ent * entropy + vf * critic
+    total.backward()
+
+    def close(got, exp, what, rel=2e-5):
+        scale = exp.abs().max().item() + 1e-12
+        err = (got.double().cpu() - exp).abs().max().item()
+        assert err <= rel * scale + 1e-9, (what, err, scale)
+    close(dz[:, :H], za.grad, "dz actor")
+    close(dz[:, H:], zc.grad, "dz critic")
+    close(p_dw_a[pad:-pad].view(G, K * H).double().sum(0).view(K, H), wa.grad, "dW_out actor")
+    close(p_dbo_a[pad:-pad].view(G, K).double().sum(0), ba.grad, "db_out actor")
+    close(p_dbh_a[pad:-pad].view(G, H).double().sum(0), za.grad.sum(0), "db_hidden actor")
+    close(p_dw_c[pad:-pad].view(G, H).double().sum(0).view(1, H), wc.grad, "dW_out critic")
+    close(p_dbo_c[pad:-pad].view(G, 1).double().sum(0), bc.grad, "db_out critic")
+    close(p_dbh_c[pad:-pad].view(G, H).double().sum(0), zc.grad.sum(0), "db_hidden critic")
+    sc = torch.zeros(ops.N_OUT, device=DEV)
+    dls = torch.zeros(K, device=DEV)
+    assert L.xpa_policy_loss_finalize(algo_c, dist_c, B, K, v(lp), G, vf, ent, ops._p(sc), ops._p(dls), s) == 0
+    torch.cuda.synchronize()
+    got = sc.double().cpu()
+    assert abs(got[0] - actor_loss.item()) < 1e-5 and abs(got[1] - critic.item() * 1.0 / 1.0) < 1e-5
+    assert abs(got[2] - entropy.item()) < 1e-5 and abs(got[3] - total.item()) < 1e-5
+    if ls is not None:
+        close(dls, ls.grad, "d logstd", rel=1e-5)

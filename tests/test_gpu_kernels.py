@@ -419,10 +419,11 @@ def test_rollout_post_matches_reference_rules(algo, atari):
 
 
 # ---------------------------------------------------------------------------------------------- K9
-@pytest.mark.parametrize("max_norm", [0.5, 0.0, 1e9])
+@pytest.mark.parametrize("max_norm", [0.5, None, 0.0, 1e9])
 def test_fused_clip_adam_matches_torch(max_norm):
     """xpa_clip_adam_step == clip_grad_norm_ + torch.optim.Adam (foreach) over several steps, with
-    optimizer.state_dict() still describing the moments."""
+    optimizer.state_dict() still describing the moments.  None = use_grad_clip False (no clip); 0.0 clips
+    to a zero gradient exactly as torch.nn.utils.clip_grad_norm_(params, 0) does."""
     from xuanpolicy_amd.flat import FlatState, FusedClipAdam
     torch.manual_seed(0)
     net_a = torch.nn.Sequential(torch.nn.Linear(17, 33), torch.nn.LeakyReLU(), torch.nn.Linear(33, 7)).to(DEV)
@@ -436,7 +437,7 @@ def test_fused_clip_adam_matches_torch(max_norm):
         x = torch.randn(64, 17, device=DEV)
         opt_a.zero_grad()
         (net_a(x) ** 2).mean().backward()
-        if max_norm > 0:
+        if max_norm is not None:
             torch.nn.utils.clip_grad_norm_(net_a.parameters(), max_norm)
         opt_a.step()
         fs.zero_()

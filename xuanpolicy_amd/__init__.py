@@ -18,6 +18,9 @@ __version__ = "0.1.0"
 def __getattr__(name):
     # Lazy submodule access keeps `import xuanpolicy_amd` cheap and CPU-safe.
     import importlib
-    if name in ("ops", "buffer", "learners", "agents", "policies", "envs", "distributed", "config", "runner"):
+    if name in ("ops", "buffer", "learners", "agents", "policies", "envs", "distributed", "config", "runner", "common",
+                "environment"):
         return importlib.import_module("." + name, __name__)
+    if name in ("get_arguments", "get_runner"):   # `from xuance import get_arguments, get_runner`
+        return getattr(importlib.import_module(".runner", __name__), name)
     raise AttributeError(name)

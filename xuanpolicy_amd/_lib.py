@@ -119,7 +119,8 @@ SIGNATURES = {
                                           c_p]),
 }
 
-HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall"]
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall"]
+OBJ_DIR = os.path.join(PKG_DIR, "_obj")
 
 _lib = None
 
@@ -128,19 +129,40 @@ class XpaError(RuntimeError):
     pass
 
 
-def build_library(force=False, verbose=False):
-    """Compile csrc/*.hip into libxuanpolicy_amd.so for gfx950 (cross-compiles without a GPU)."""
+def build_library(force=False, verbose=False, jobs=None):
+    """Compile csrc/*.hip into libxuanpolicy_amd.so for gfx950 (cross-compiles without a GPU).
+
+    One hipcc process per source file (in parallel, objects under xuanpolicy_amd/_obj/, rebuilt when the
+    source or a shared header is newer), then one link step."""
+    from concurrent.futures import ThreadPoolExecutor
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    deps = srcs + [os.path.join(CSRC, "xpa_common.h"), HEADER]
+    headers = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")] + [HEADER]
+    hdr_m = max(os.path.getmtime(h) for h in headers)
     if not force and os.path.exists(LIB_PATH):
         lib_m = os.path.getmtime(LIB_PATH)
-        if all(os.path.getmtime(d) <= lib_m for d in deps):
+        if all(os.path.getmtime(d) <= lib_m for d in srcs) and hdr_m <= lib_m:
             return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    os.makedirs(OBJ_DIR, exist_ok=True)
+
+    def compile_one(src):
+        obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+        if (not force and os.path.exists(obj) and os.path.getmtime(obj) >= os.path.getmtime(src)
+                and os.path.getmtime(obj) >= hdr_m):
+            return obj
+        cmd = [hipcc] + HIPCC_FLAGS + ["-c", "-o", obj + ".tmp", src]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(obj + ".tmp", obj)
+        return obj
+    jobs = jobs or min(len(srcs), max(1, min(16, os.cpu_count() or 1)))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, srcs))
     tmp = LIB_PATH + ".tmp"
-    cmd = [hipcc] + HIPCC_FLAGS + ["-o", tmp] + srcs
+    cmd = [hipcc, "--offload-arch=gfx950", "-fPIC", "-shared", "-o", tmp] + objs
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH

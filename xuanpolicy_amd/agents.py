@@ -26,6 +26,8 @@ CPU generator; the truncation bootstrap value V(norm(final obs)) is computed for
 all finished envs of a step in one Chan update (mathematically equal to the reference's sequential
 single-value updates).
 """
+import json
+import os
 import time
 
 import numpy as np
@@ -115,6 +117,7 @@ class _OnPolicyAgent:
         self.log_hook = None     # optional callable(info: dict, step: int) (tensorboard/wandb adapter)
         self.timers = {"rollout": 0.0, "update": 0.0}
         self.phase_events = None
+        self.update_log = None   # a list: every update's device loss scalars are appended (tests / diagnostics)
         self._t = 0
         self._host_obs = None
         self.use_graph = bool(_cfg(config, "cuda_graph", True)) and self.device.type == "cuda"
@@ -134,14 +137,35 @@ class _OnPolicyAgent:
         # rollout; the critic then runs once per iteration on [truncation slots; last-step obs] instead of
         # on every env at every step.
         max_ep = getattr(envs, "max_episode_steps", getattr(envs, "max_episode_length", 0)) or 0
+        # Only the device envs qualify: their one truncation source is the time limit, so max_ep >= n_steps
+        # bounds it to one per rollout; a host VecEnv may truncate for other reasons (per-step bootstraps).
         self.defer_boot = (bool(_cfg(config, "defer_bootstrap", True)) and not self.raw_obs
-                           and int(max_ep) >= self.n_steps)
+                           and hasattr(envs, "step_device") and int(max_ep) >= self.n_steps)
         if self.defer_boot:
             self.slot_obs = torch.zeros((N, D), **f32)
             self.slot_t = torch.full((N,), -1, dtype=torch.int32, device=dev)
             self.slot_overflow = torch.zeros((1,), dtype=torch.int32, device=dev)
         self._graph = None
         self._graph_pool = None
+        # Model / log directories and the logger (agent.py:33-70).  model_dir_save is seed_<seed>_<time>
+        # under model_dir, model_dir_load is model_dir itself (what load_model searches); both are created
+        # when first written, not at construction (tests and benches build many agents).
+        time_string = time.asctime().replace(" ", "").replace(":", "_")
+        seed_tag = "seed_%d_" % self.seed
+        model_dir = _cfg(config, "model_dir", "./models/")
+        self.log_dir = _cfg(config, "log_dir", "./logs/")
+        self.model_dir_save = os.path.join(os.getcwd(), model_dir, seed_tag + time_string)
+        self.model_dir_load = model_dir
+        self.writer = _make_writer(_cfg(config, "logger", "none"), os.path.join(os.getcwd(), self.log_dir,
+                                                                               seed_tag + time_string))
+        self.use_wandb = False
+        # The reference's runner hands over the policy and a torch Adam; the hot path re-homes the parameters
+        # into flat buffers (learner.enable_fast_path) so the fused kernels own the update.
+        if bool(_cfg(config, "fast_path", True)) and self.device.type == "cuda":
+            if bool(_cfg(config, "tunableop", True)):
+                from .runner import enable_tuned_gemms
+                enable_tuned_gemms()
+            self.learner.enable_fast_path(fused_optimizer=bool(_cfg(config, "fused_adam", True)))
 
     def _make_learner(self, config, policy, optimizer, scheduler):
         raise NotImplementedError
@@ -344,7 +368,8 @@ class _OnPolicyAgent:
         else:
             with torch.no_grad():
                 v = policy_heads(self.policy, x)[2].contiguous()
-        if int(self.slot_overflow.item()):
+        if int(self.slot_overflow.item()):   # cannot happen for the device envs (see __init__); never silent
+            self.slot_overflow.zero_()
             raise RuntimeError("an env truncated twice within one rollout; set config.defer_bootstrap = False")
         return v.reshape(-1)
 
@@ -389,12 +414,18 @@ class _OnPolicyAgent:
                     tdist.all_reduce(part, op=tdist.ReduceOp.SUM)   # (sum, sumsq) over all ranks' minibatches,
                     part.div_(self.world)                           # averaged: mean / var of the global minibatch
                 scalars = self.learner.update_fused(obs_mb, idx, act_flat, adv_flat, ret_flat, logp_flat, part)
+                if self.update_log is not None:
+                    self.update_log.append(scalars.clone())
         self.last_info = scalars
         self.iterations += 1
 
     def log_infos(self, info, x_index):
+        """agent.py:81-94: every entry to the logger (tensorboard when importable, else JSON lines in
+        log_dir) and to log_hook."""
         if self.log_hook is not None:
             self.log_hook(info, x_index)
+        if self.writer is not None:
+            self.writer.write(info, x_index)
 
     def _host_info(self):
         info = self.learner._info(self.last_info)
@@ -433,14 +464,72 @@ class _OnPolicyAgent:
                     self.log_infos(info, self.current_step)
                 self.timers["update"] += time.perf_counter() - t1
 
-    def save_model(self, model_path):
-        self.learner.save_model(model_path)
+    def save_model(self, model_name):
+        """agent.py:74-76: the policy's state_dict to model_dir_save/model_name."""
+        os.makedirs(self.model_dir_save, exist_ok=True)
+        self.learner.save_model(self.model_dir_save + "/" + model_name)
 
     def load_model(self, path, seed=1):
+        """agent.py:78-79 -> learner.py:27-48 (newest file of the seed_<seed> directory under path)."""
         self.learner.load_model(path, seed)
 
+    # ---- test (ppoclip_agent.py:113-165, a2c_agent.py:109-160) ----------------------------------------
+    @torch.no_grad()
+    def _test_action(self, x):
+        head, logstd, _ = policy_heads(self.policy, x)
+        if self.discrete:
+            a = torch.distributions.Categorical(logits=head).sample()
+        else:
+            a = head + logstd.exp() * torch.randn_like(head)   # stochastic_sample of Normal(mu, exp(logstd))
+        return a.cpu().numpy()
+
+    def _test_obs(self, obs):
+        """The reference updates obs_rms in test() too (ppoclip_agent.py:125) and normalises with it."""
+        x = obs if isinstance(obs, torch.Tensor) else torch.as_tensor(np.asarray(obs))
+        if self.raw_obs:
+            return x.to(self.device)
+        x = x.to(device=self.device, dtype=torch.float32).reshape(x.shape[0], -1).contiguous()
+        if self.use_obsnorm:
+            ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count)
+        out = torch.empty_like(x)
+        ops.obs_normalize(x, self.obs_mean, self.obs_var, self._obs_clip(), out)
+        return out
+
+    def test(self, env_fn, test_episode):
+        """Run the current policy (stochastic actions) on env_fn()'s envs until test_episode episodes have
+        ended; returns their scores (infos[i]['episode_score'])."""
+        test_envs = env_fn()
+        num_envs = test_envs.num_envs
+        current_episode, scores, best_score = 0, [], -np.inf
+        obs, _ = test_envs.reset()
+        obs = obs.cpu().numpy() if isinstance(obs, torch.Tensor) else np.asarray(obs)
+        verbose = bool(_cfg(self.config, "test_mode", False))
+        while current_episode < test_episode:
+            acts = self._test_action(self._test_obs(obs))
+            if self.discrete:
+                acts = acts.astype(np.int64)
+            next_obs, rewards, terminals, truncations, infos = test_envs.step(acts)
+            obs = np.array(next_obs, copy=True)
+            for i in range(num_envs):
+                if terminals[i] or truncations[i]:
+                    if self.atari and not truncations[i]:   # life loss: the game goes on
+                        continue
+                    obs[i] = infos[i]["reset_obs"]
+                    scores.append(infos[i]["episode_score"])
+                    current_episode += 1
+                    best_score = max(best_score, infos[i]["episode_score"])
+                    if verbose:
+                        print("Episode: %d, Score: %.2f" % (current_episode, infos[i]["episode_score"]))
+        if verbose:
+            print("Best Score: %.2f" % best_score)
+        self.log_infos({"Test-Episode-Rewards/Mean-Score": float(np.mean(scores)),
+                        "Test-Episode-Rewards/Std-Score": float(np.std(scores))}, self.current_step)
+        test_envs.close()
+        return scores
+
     def finish(self):
-        pass
+        if self.writer is not None:
+            self.writer.close()
 
 
 class PPOCLIP_Agent(_OnPolicyAgent):
@@ -461,3 +550,64 @@ class A2C_Agent(_OnPolicyAgent):
 
 
 REGISTRY = {"PPO_Clip": PPOCLIP_Agent, "A2C": A2C_Agent}
+Agent = _OnPolicyAgent
+
+
+def get_total_iters(agent_name, args):
+    """agent.py:144-145: the LinearLR horizon the runner and the examples use."""
+    return args.running_steps
+
+
+class _JsonlWriter:
+    """Scalar sink for log_infos when no tensorboard / wandb is importable: one JSON object per line."""
+
+    def __init__(self, log_dir):
+        self.path = os.path.join(log_dir, "scalars.jsonl")
+        self._f = None
+
+    def write(self, info, step):
+        if self._f is None:
+            os.makedirs(os.path.dirname(self.path), exist_ok=True)
+            self._f = open(self.path, "a")
+        rec = {"step": int(step)}
+        for k, v in info.items():
+            if isinstance(v, dict):
+                rec.update({"%s/%s" % (k, kk): float(vv) for kk, vv in v.items()})
+            elif isinstance(v, (int, float, np.floating, np.integer)):
+                rec[k] = float(v)
+        self._f.write(json.dumps(rec) + "\n")
+
+    def close(self):
+        if self._f is not None:
+            self._f.close()
+            self._f = None
+
+
+class _TensorboardWriter:
+    def __init__(self, writer):
+        self.w = writer
+
+    def write(self, info, step):
+        for k, v in info.items():
+            if isinstance(v, dict):
+                self.w.add_scalars(k, v, step)
+            else:
+                self.w.add_scalar(k, v, step)
+
+    def close(self):
+        self.w.close()
+
+
+def _make_writer(logger, log_dir):
+    """config.logger: 'tensorboard' / 'wandb' (the reference's choices) or 'none'.  tensorboard and wandb
+    are optional: without them the scalars go to log_dir/scalars.jsonl."""
+    if logger in (None, "none", "None", False):
+        return None
+    if logger == "tensorboard":
+        try:
+            from torch.utils.tensorboard import SummaryWriter
+            os.makedirs(log_dir, exist_ok=True)
+            return _TensorboardWriter(SummaryWriter(log_dir))
+        except ImportError:
+            pass
+    return _JsonlWriter(log_dir)

@@ -121,6 +121,7 @@ __device__ __forceinline__ void load_tile(float4 (&zq)[16], const float *__restr
 template <int KMAX>
 struct RowIn {  // wave 0, lane = row of the tile
     bool valid;
+    bool masked;  // a batch row whose index is out of range (contributes nothing)
     float x, old, act[KMAX];
 };
 
@@ -178,6 +179,7 @@ struct HeadEpi {
                                                 const float *__restrict__ ret) const {
         RowIn<KMAX> in;
         in.valid = false;
+        in.masked = false;
         in.x = in.old = 0.f;
 #pragma unroll
         for (int o = 0; o < KMAX; ++o) in.act[o] = 0.f;
@@ -187,6 +189,7 @@ struct HeadEpi {
             if (b < batch) {
                 const int64_t row = idx ? idx[b] : b;
                 in.valid = row >= 0 && row < n_rows;
+                in.masked = !in.valid;
                 if (in.valid) {
                     if (MODE == 2) {
                         in.x = ret[row];
@@ -325,6 +328,11 @@ struct HeadEpi {
                         }
                     }
                 }
+            }
+            if (MODE == 0 && in.masked) {  // hand back the ent_coef / B the finalize subtracts for every row
+#pragma unroll
+                for (int o = 0; o < KMAX; ++o)
+                    if (o < K) acc_dls[o] += ent_coef * inv_b;
             }
 #pragma unroll
             for (int o = 0; o < KMAX; ++o) s_dh[lane][o] = dh_[o];

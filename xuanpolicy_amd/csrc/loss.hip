@@ -145,6 +145,11 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
         {
         if (!valid) {  // out-of-range index: zero gradient, no contribution
             d_v[b] = 0.f;
+            // the finalize subtracts ent_coef (= ent_coef / B per row) from d logstd for every row of the
+            // batch: a masked row hands its share back, so it contributes nothing there either
+            if (DIST == XPA_DIST_GAUSSIAN)
+                for (int a = 0; a < KM; ++a)
+                    if (a < A) dls_t[a] += ent_coef * inv_b;
             if (stage)
                 for (int a = 0; a < A; ++a) s_dm[tid * A + a] = 0.f;
             else

@@ -6,6 +6,7 @@
 // runner_drl.py:71).  Semantics follow torch: total_norm = ||g||_2 over all parameters,
 // coef = min(max_norm / (total_norm + 1e-6), 1); g *= coef; then Adam:
 //   m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g^2;  p -= (lr / bc1) m / (sqrt(v) / sqrt(bc2) + eps).
+// max_norm < 0 means "no clipping" (use_grad_clip False); max_norm = 0 clips to zero as torch does.
 // Two launches: K_a per-block sum of squares (f64, fixed order), K_b every block re-reduces those
 // partials (deterministic, no atomics), scales g in place and applies the Adam update with 16-B
 // accesses.  HBM-bound: 4 B read (K_a) + 4x4 B read + 4x4 B write... per parameter (p, g, m, v).
@@ -55,8 +56,9 @@ __global__ __launch_bounds__(kOptThreads) void clip_adam_kernel(float *__restric
         s = xpa_wave_sum(s);
         if (threadIdx.x == 0) {
             const float total = (float)sqrt(s);
+            // max_norm < 0: no clipping; max_norm >= 0 clips exactly like clip_grad_norm_ (0 zeroes g)
             float coef = 1.0f;
-            if (max_norm > 0.f) coef = fminf(max_norm / (total + 1e-6f), 1.0f);
+            if (max_norm >= 0.f) coef = fminf(max_norm / (total + 1e-6f), 1.0f);
             s_coef = coef;
             if (blockIdx.x == 0 && norm_out) *norm_out = total;
         }

@@ -128,8 +128,12 @@ class FusedClipAdam:
         self._step_t.fill_(float(self.step_count))
 
     def step(self, max_norm, sq=None):
-        """sq = (float64 partials, count) summing to |grad|^2, written by the gradient producers: one launch
-        (xpa_clip_adam_step_partials) instead of the norm pass + step."""
+        """max_norm: the clip_grad_norm_ bound, or None for no clipping (max_norm = 0 zeroes the gradient,
+        as torch's clip_grad_norm_ does).  sq = (float64 partials, count) summing to |grad|^2, written by the
+        gradient producers: one launch (xpa_clip_adam_step_partials) instead of the norm pass + step."""
+        if max_norm is not None and float(max_norm) < 0:
+            raise ValueError("max_norm must be >= 0 (None: no clipping)")
+        max_norm = -1.0 if max_norm is None else float(max_norm)   # the kernels' "no clipping" code
         g = self.optimizer.param_groups[0]
         self.step_count += 1
         b1, b2 = g["betas"]
@@ -139,13 +143,13 @@ class FusedClipAdam:
             buf, count = sq
             rc = ops.lib().xpa_clip_adam_step_partials(
                 ops._p(self.fs.param), ops._p(self.fs.flat), ops._p(self.exp_avg), ops._p(self.exp_avg_sq),
-                self.fs.numel, ops._p(buf), int(count), float(max_norm) if max_norm else 0.0, lr, float(b1),
+                self.fs.numel, ops._p(buf), int(count), max_norm, lr, float(b1),
                 float(b2), float(g["eps"]), self.step_count, ops._p(self.total_norm), ops._stream(self.fs.param.device))
             _lib.check(rc, "xpa_clip_adam_step_partials")
         else:
             rc = ops.lib().xpa_clip_adam_step(ops._p(self.fs.param), ops._p(self.fs.flat), ops._p(self.exp_avg),
                                               ops._p(self.exp_avg_sq), self.fs.numel, ops._p(self.partials),
-                                              float(max_norm) if max_norm else 0.0, lr, float(b1), float(b2),
+                                              max_norm, lr, float(b1), float(b2),
                                               float(g["eps"]), self.step_count, ops._p(self.total_norm),
                                               ops._stream(self.fs.param.device))
             _lib.check(rc, "xpa_clip_adam_step")

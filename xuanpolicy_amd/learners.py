@@ -100,7 +100,7 @@ class _FusedPolicyGradient(Learner):
             sq = None
         fused = getattr(self, "fused_opt", None)
         if fused is not None:
-            fused.step(self._max_norm if self._use_clip else 0.0, sq=sq)  # xpa_clip_adam_step (K9)
+            fused.step(self._max_norm if self._use_clip else None, sq=sq)  # xpa_clip_adam_step (K9)
         else:
             if self._use_clip:
                 torch.nn.utils.clip_grad_norm_(self._params, self._max_norm)
@@ -192,6 +192,8 @@ class A2C_Learner(_FusedPolicyGradient):
 
     def __init__(self, policy, optimizer, scheduler=None, device=None, model_dir="./", vf_coef=0.25, ent_coef=0.005,
                  clip_grad=None):
+        if clip_grad is None:   # the reference's clip_grad_norm_(..., None) fails at its first update
+            raise ValueError("A2C_Learner needs clip_grad (a2c_learner.py:34 always clips)")
         super().__init__(policy, optimizer, scheduler, device, model_dir, vf_coef, ent_coef, 0.0, clip_grad, True)
         self.clip_grad = clip_grad
 

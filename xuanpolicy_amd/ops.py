@@ -412,6 +412,13 @@ class ColsumQueue:
         when the queue fits one launch, also the clip norm of the outputs + sq[0], left at sq[1 + tiles]
         (xpa_colsum_finalize_batch_sq).  Returns (that total's view or None, output elements written)."""
         if not self.items:
+            loss, self.loss = self.loss, None
+            if loss is not None:   # a deferred loss finalize with no column tiles to ride on: run it alone
+                a, d, B, K, lp, vf, ent, sc, dls = loss
+                dev = device if device is not None else lp.device
+                _lib.check(lib().xpa_policy_loss_finalize_sq(a, d, B, K, _p(lp), lp.shape[0], vf, ent, _p(sc), _p(dls),
+                                                             _p(sq) if sq is not None else None, _stream(dev)),
+                           "xpa_policy_loss_finalize")
             return None, 0
         key = tuple((p.data_ptr(), p.shape[0], p.shape[1], o.data_ptr()) for p, o in self.items)
         plan = self._plans.get(key)

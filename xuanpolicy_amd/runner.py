@@ -36,23 +36,46 @@ def get_config(path):
         return yaml.safe_load(f)
 
 
+FLAT_ENVS = ("atari", "mujoco", "Platform", "synthbox")   # <method>/<env>.yaml; others <method>/<env>/<env_id>.yaml
+
+
 def get_arguments(method, env, env_id, config_path=None, parser_args=None):
-    """common_tools.py:32-83 for a single method: basic.yaml, then <method>/<env>.yaml, then the user
-    YAML, then parser args."""
+    """common_tools.py:32-83 for a single method: basic.yaml, then the method's <env>.yaml (or
+    <env>/<env_id>.yaml) when it exists, then the user YAML (relative to the working directory), then the
+    parser args (their names override)."""
     cfg = get_config(os.path.join(CONFIG_DIR, "basic.yaml"))
-    algo = os.path.join(CONFIG_DIR, method, env + ".yaml")
+    file_name = env + ".yaml" if env in FLAT_ENVS else os.path.join(env, env_id + ".yaml")
+    algo = os.path.join(CONFIG_DIR, method, file_name)
     if os.path.exists(algo):
         cfg = recursive_dict_update(cfg, get_config(algo))
     if config_path is not None:
-        cfg = recursive_dict_update(cfg, get_config(config_path))
+        cfg = recursive_dict_update(cfg, get_config(os.path.join(os.getcwd(), config_path)))
     if parser_args is not None:
         cfg = recursive_dict_update(cfg, dict(vars(parser_args)))
     args = SimpleNamespace(**cfg)
-    args.env_id = env_id
+    if env in FLAT_ENVS or not hasattr(args, "env_id"):
+        args.env_id = env_id
     return args
 
 
+def set_seed(seed):
+    """xuance/torch/utils/operations.py:17-22."""
+    import random
+
+    import numpy as np
+    torch.manual_seed(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed(seed)
+        torch.cuda.manual_seed_all(seed)
+    np.random.seed(seed)
+    random.seed(seed)
+
+
 def make_envs(config, device=None, shard=0):
+    """xuance/environment/__init__.py:36-99 for the envs built in here: the device-resident SynthBox /
+    SynthAtari vector envs (config.parallels envs on config.device)."""
+    if device is None:
+        device = getattr(config, "device", None)
     if config.env_name == "SynthBox":
         return SynthBoxVecEnv(config.parallels, config.obs_dim, config.act_dim, seed=config.seed,
                               discrete=bool(getattr(config, "discrete", False)),
@@ -136,3 +159,80 @@ def build_atari_a2c(n_envs=1024, n_steps=128, seed=1, device="cuda:0", **overrid
         setattr(cfg, k, v)
     torch.manual_seed(seed)
     return build_agent(cfg, device)
+
+
+class Runner_DRL:
+    """runner_drl.py:15-134 (with runner_basic.py:5-13) for PPO_Clip / A2C: seed, envs, representation,
+    policy, Adam(eps=1e-5) + LinearLR, the agent; run() trains (or tests a saved model in test_mode) and
+    benchmark() alternates training and test episodes, keeping the best model."""
+
+    def __init__(self, args):
+        self.args = args
+        self.agent_name = args.agent
+        self.env_id = args.env_id
+        set_seed(args.seed)
+        self.envs = make_envs(args)
+        self.envs.reset()
+        self.n_envs = self.envs.num_envs
+        self.agent = build_agent(args, envs=self.envs)
+
+    def _test_env_fn(self, parallels):
+        def env_fn():
+            args_test = deepcopy(self.args)
+            args_test.parallels = parallels
+            return make_envs(args_test)
+        return env_fn
+
+    def run(self):
+        import numpy as np
+        if getattr(self.args, "test_mode", False):
+            self.agent.render = True
+            self.agent.load_model(self.agent.model_dir_load, self.args.seed)
+            scores = self.agent.test(self._test_env_fn(1), self.args.test_episode)
+            print(f"Mean Score: {np.mean(scores)}, Std: {np.std(scores)}")
+            print("Finish testing.")
+        else:
+            self.agent.train(self.args.running_steps // self.n_envs)
+            print("Finish training.")
+            self.agent.save_model("final_train_model.pth")
+        self.envs.close()
+        self.agent.finish()
+
+    def benchmark(self):
+        import numpy as np
+        env_fn = self._test_env_fn(self.args.test_episode)
+        train_steps = self.args.running_steps // self.n_envs
+        eval_interval = self.args.eval_interval // self.n_envs
+        test_episode = self.args.test_episode
+        num_epoch = int(train_steps / eval_interval)
+        test_scores = self.agent.test(env_fn, test_episode)
+        best = {"mean": np.mean(test_scores), "std": np.std(test_scores), "step": self.agent.current_step}
+        for i_epoch in range(num_epoch):
+            print("Epoch: %d/%d:" % (i_epoch, num_epoch))
+            self.agent.train(eval_interval)
+            test_scores = self.agent.test(env_fn, test_episode)
+            if np.mean(test_scores) > best["mean"]:
+                best = {"mean": np.mean(test_scores), "std": np.std(test_scores), "step": self.agent.current_step}
+                self.agent.save_model(model_name="best_model.pth")
+        print("Best Model Score: %.2f, std=%.2f" % (best["mean"], best["std"]))
+        self.envs.close()
+        self.agent.finish()
+        return best
+
+
+REGISTRY = {"DRL": Runner_DRL}
+
+
+def get_runner(method, env, env_id, config_path=None, parser_args=None, is_test=False):
+    """common_tools.py:86-167 for a single method."""
+    args = get_arguments(method, env, env_id, config_path, parser_args)
+    args.agent_name = method
+    args.model_dir = os.path.join(os.getcwd(), args.model_dir, args.dl_toolbox, args.env_id)
+    args.log_dir = os.path.join(args.log_dir, args.dl_toolbox + "/", args.env_id)
+    if is_test:
+        args.test_mode = int(is_test)
+        args.parallels = 1
+    print("Algorithm:", args.agent)
+    print("Environment:", args.env_name)
+    print("Scenario:", args.env_id)
+    return REGISTRY[args.runner](args)
