@@ -94,6 +94,8 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float *__restrict__
     float carry = 0.f;   // A (or R) at the first element of the later chunk
     float carry_v = 0.f; // v at that element
     int carry_any = 0;   // a closure exists at or after the later chunk's first element
+    bool has_last = false;  // compact form: this lane owns step T - 1 of its row
+    float last_boot = 0.f;
 
     for (int c = nchunks - 1; c >= 0; --c) {
         const int t0 = c * C + sl * VEC;
@@ -113,6 +115,10 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float *__restrict__
                 const bool lt = (t == T - 1);
                 cl[e] = lt || d[e] != 0.f || t == st;
                 bt[e] = lt ? (d[e] != 0.f ? 0.f : vl) : (t == st ? vs : 0.f);
+                if (lt) {
+                    has_last = true;
+                    last_boot = bt[e];
+                }
             }
         } else if (COMPACT) {
 #pragma unroll
@@ -125,6 +131,10 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float *__restrict__
                 const bool lt = (t == T - 1);
                 cl[e] = ok && (lt || d[e] != 0.f || t == st);
                 bt[e] = lt ? (d[e] != 0.f ? 0.f : vl) : (t == st ? vs : 0.f);
+                if (ok && lt) {
+                    has_last = true;
+                    last_boot = bt[e];
+                }
             }
         } else if (VEC == 4 && full) {
             const float4 r4 = ld4<NT>(rew + base + t0);
@@ -234,10 +244,9 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(const float *__restrict__
         carry_v = __shfl(v[0], 0, L);
         carry_any = __shfl(any_first, 0, L);
     }
+    if (COMPACT && has_last) boot_out[base + T - 1] = last_boot;  // from registers (see gae_dpp_kernel)
     if (COMPACT && row_ok && sl == 0) {  // the fixup's writes: the two bootstraps, slot reset
         if (st >= 0 && st < T - 1) boot_out[base + st] = vs;
-        const float dl = term[base + T - 1];
-        boot_out[base + T - 1] = dl != 0.f ? 0.f : vl;
         if (st >= 0) slot_t[row] = -1;
     }
 }
@@ -295,6 +304,8 @@ __global__ __launch_bounds__(256) void gae_dpp_kernel(const float *__restrict__ 
     }
     float carry = 0.f, carry_v = 0.f;
     bool carry_any = false;
+    bool has_last = false;   // this lane owns step T - 1 of its row (compact form)
+    float last_boot = 0.f;
     for (int c = nchunks - 1; c >= 0; --c) {
         const int t0 = c * C + (L - 1 - sl) * 4;
         const bool in = row_ok && t0 < T;  // T % 4 == 0: a lane's 4 steps are all in or all out
@@ -315,6 +326,10 @@ __global__ __launch_bounds__(256) void gae_dpp_kernel(const float *__restrict__ 
                     const bool lt = (t == T - 1);
                     cl[e] = lt || d[e] != 0.f || t == st;
                     bt[e] = lt ? (d[e] != 0.f ? 0.f : vl) : (t == st ? vs : 0.f);
+                }
+                if (t0 + 3 == T - 1) {
+                    has_last = true;
+                    last_boot = bt[3];
                 }
             } else {
                 const uint32_t c4 = *reinterpret_cast<const uint32_t *>(closed + base + t0);
@@ -390,12 +405,20 @@ __global__ __launch_bounds__(256) void gae_dpp_kernel(const float *__restrict__ 
             carry = __shfl(first, L - 1, L);
             carry_v = __shfl(v[0], L - 1, L);
             carry_any = carry_any || segbits != 0;
+        } else if (COMPACT) {
+            // xpa_rollout_bootstrap_fixup's writes (both bootstraps, slot reset), issued inside the loop where
+            // st / vs / vl are known to have landed, the last step's bootstrap from the registers of the lane
+            // that owns step T - 1.  (After the loop, re-reading term[T - 1] cost a dependent load whose
+            // vmcnt(0) also waited for every adv/ret store of the wave, then one more HBM round trip.)
+            if (has_last) boot_out[base + T - 1] = last_boot;
+            if (row_ok && sl == 0) {
+                int sw = st;
+                asm volatile("" : "+v"(sw));  // keeps the slot address math here: hoisted out of the loop it
+                                              // made every wave wait for slot_t before issuing r / v / d
+                if (sw >= 0 && sw < T - 1) boot_out[base + sw] = vs;
+                if (sw >= 0) slot_t[row] = -1;
+            }
         }
-    }
-    if (COMPACT && row_ok && sl == 0) {  // xpa_rollout_bootstrap_fixup's writes: both bootstraps, slot reset
-        if (st >= 0 && st < T - 1) boot_out[base + st] = vs;
-        boot_out[base + T - 1] = term[base + T - 1] != 0.f ? 0.f : vl;
-        if (st >= 0) slot_t[row] = -1;
     }
 }
 

@@ -76,6 +76,13 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 constexpr int kTile = 64;
 constexpr int kS = 260;
 constexpr int kGridMax = 512;  // 2 blocks per CU (77 KiB LDS each) x 256 CUs
+// Blocks own the per-block partial rows blockIdx.x of p_dw / p_dbh / p_dbo / p_loss, which hold
+// head_partials(batch) rows: a block beyond them must write nothing.  (r01: an uncommitted two-head
+// experiment launched 13 tiles x 512 = 6656 blocks for B = 777; its blocks >= 13 skipped the tile loop and
+// still wrote their partials in finish() — out of the buffers: HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION.)
+__host__ __device__ constexpr int64_t head_partials(int64_t batch) {
+    return (batch + kTile - 1) / kTile < kGridMax ? (batch + kTile - 1) / kTile : kGridMax;
+}
 
 struct HeadArgs {
     int64_t batch;
@@ -456,6 +463,7 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(XPA_HEAD_KERNEL_PARAM
     __shared__ float s_stats[2];
     const int t = threadIdx.x;
     const int64_t ntiles = (batch + kTile - 1) / kTile;
+    if ((int64_t)blockIdx.x >= head_partials(batch)) return;  // no partial row of its own (see kGridMax)
     int64_t tile = blockIdx.x;
     float4 zq[16];
     load_tile(zq, z, ldx, tile, batch);
@@ -581,6 +589,7 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int64_t ntiles = (batch + kTile - 1) / kTile;
+    if ((int64_t)blockIdx.x >= head_partials(batch)) return;  // no partial row of its own (see kGridMax)
     Epi epi;
     epi.init(K_in, W, logstd, adv_partials, n_adv_partials, batch, clip_range, slope, s_stats);
     const float bh0 = bh[wave * 64 + (lane & 31)], bh1 = bh[wave * 64 + 32 + (lane & 31)];
@@ -639,8 +648,7 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
 }  // namespace
 
 XPA_API int64_t xpa_head_fused_num_partials(int64_t batch) {
-    const int64_t tiles = (batch + kTile - 1) / kTile;
-    return tiles < kGridMax ? tiles : kGridMax;
+    return head_partials(batch);
 }
 
 namespace {
