@@ -103,14 +103,27 @@ def gae_graph_replay_us(mem, reps=50):
     return e0.elapsed_time(e1) / reps * 1e3
 
 
-def loss_sweep(device, sizes=(65536, 262144, 1048576, 4194304), act_dim=6, reps=7):
+def cache_flush(flush, mode):
+    """Evict the caches before a timed launch.  "read": sum a 512 MiB buffer (other data replaces ours in L2 and
+    the Infinity Cache and leaves nothing dirty); "write": fill it (the evicting lines are dirty, so the timed
+    kernel's own misses also pay their write-back to HBM); "none": nothing."""
+    if mode == "read":
+        flush.sum()
+    elif mode == "write":
+        flush.fill_(1.0)
+
+
+def loss_sweep(device, sizes=(65536, 262144, 1048576, 4194304), act_dim=6, reps=7, flush_mode="read"):
     """K2 alone (xpa_policy_loss_fwd_bwd, Gaussian PPO, rows in order: the drop-in learners' form; the C2
-    fast path fuses the loss into K16's epilogue instead), Infinity Cache flushed before each timed launch.
+    fast path fuses the loss into K16's epilogue instead), caches flushed (cache_flush: 512 MiB read) before each
+    timed launch.
     Inputs as SURVEY.md §8(d): mu ~ N(0, 0.5), logstd = -1 + N(0, 0.1), actions drawn around mu, adv / ret / v
     ~ N(0, 1)."""
     import torch
     from xuanpolicy_amd import _lib, ops
-    flush = torch.empty(512 * 1024 * 1024 // 4, dtype=torch.float32, device=device)
+    flush = torch.ones(512 * 1024 * 1024 // 4, dtype=torch.float32, device=device)
+    for _ in range(2):
+        flush.sum()   # written once; read passes leave it clean
     L = ops.lib()
     s = ops._stream(device)
     out = []
@@ -125,7 +138,7 @@ def loss_sweep(device, sizes=(65536, 262144, 1048576, 4194304), act_dim=6, reps=
         ws = ops.LossWorkspace(B, A, device, "gaussian")
         times = []
         for _ in range(reps):
-            flush.fill_(1.0)
+            cache_flush(flush, flush_mode)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             rc = L.xpa_policy_loss_fwd_bwd(ops.ALGO["ppo"], ops.DIST["gaussian"], B, A, ops._p(mu), ops._p(logstd),
@@ -147,12 +160,14 @@ def loss_sweep(device, sizes=(65536, 262144, 1048576, 4194304), act_dim=6, reps=
     return out
 
 
-def gae_sweep(device, sizes=(4096, 65536, 262144, 1048576), horizon=128, reps=7):
+def gae_sweep(device, sizes=(4096, 65536, 262144, 1048576), horizon=128, reps=7, flush_mode="read"):
     """GAE kernel alone (the in-loop compact form, ~1/8 of the rows with a mid-buffer truncation),
-    Infinity Cache flushed (512 MiB write) before each timed launch."""
+    caches flushed (cache_flush: 512 MiB read) before each timed launch."""
     import torch
     from xuanpolicy_amd import ops
-    flush = torch.empty(512 * 1024 * 1024 // 4, dtype=torch.float32, device=device)
+    flush = torch.ones(512 * 1024 * 1024 // 4, dtype=torch.float32, device=device)
+    for _ in range(2):
+        flush.sum()   # written once; read passes leave it clean
     out = []
     for N in sizes:
         g = torch.Generator(device=device).manual_seed(N)
@@ -170,7 +185,7 @@ def gae_sweep(device, sizes=(4096, 65536, 262144, 1048576), horizon=128, reps=7)
         times = []
         for _ in range(reps):
             slot.copy_(slot0)
-            flush.fill_(1.0)
+            cache_flush(flush, flush_mode)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             ops.gae_scan_compact(rew, val, term, slot, vboot, 0.99, 0.95, True, adv=adv, ret=ret, boot=boot)
@@ -549,7 +564,7 @@ def main():
                               "loss into K16's epilogue)", "bound": "hbm", "batch": k2["batch"],
                     "avg_launch_us": round(k2["ms"] * 1e3, 3), "achieved": k2["GB/s"], "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": k2["frac"], "algorithmic_bytes_per_launch": k2["algorithmic_bytes"],
-                    "timing": "host-recorded events around one launch after a 512 MiB cache flush (median of 7); "
+                    "timing": "host-recorded events around one launch after a 512 MiB cache-flush read (median of 7); "
                               "see loss_sweep_flushed for larger batches"}
         if not args.no_c3 and world == 1:
             result["c3_atari_a2c"] = c3_bench(device)

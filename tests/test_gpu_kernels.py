@@ -234,6 +234,49 @@ def test_loss_kernel_indexed_advnorm(algo, dist, A, B):
         assert abs(sc[4] - info["clip_ratio"]) < 2.0 / B
 
 
+@pytest.mark.parametrize("algo,A,B,advnorm", [
+    ("ppo", 6, 1024 * 256 * 2 + 77, False),   # pipelined K2: > 2 tiles per block, a ragged last tile
+    ("ppo", 6, 65536, True),                   # C2 minibatch, in order, adv-norm
+    ("a2c", 2, 256 * 1024 + 256, False),       # A2C slot count (2A + 3), exactly one extra tile
+    ("ppo", 8, 300, False),                    # one full tile + a 44-row tail
+    ("ppo", 1, 259, True),                     # 1-float rows; 3-row tail
+    ("a2c", 5, 1, False),                      # a single row (the generic kernel: B < one tile)
+    ("ppo", 17, 5000, False),                  # C4 head width (the straight-line K2, A > 8)
+])
+def test_loss_kernel_in_order_rows(algo, A, B, advnorm):
+    """K2 with the minibatch rows in order (idx = None: the LDS-DMA pipelined form for A <= 8) against the
+    oracle's closed-form loss and gradients (ppoclip_learner.py:32-44, a2c_learner.py:24-31)."""
+    from xuanpolicy_amd import ops
+    rng = np.random.default_rng(A * 13 + B)
+    head = rng.normal(0, 0.5, (B, A)).astype(np.float32)
+    logstd = (-1 + rng.normal(0, 0.1, A)).astype(np.float32)
+    v = rng.normal(0, 1, B).astype(np.float32)
+    act = (head + np.exp(logstd) * rng.normal(0, 1, (B, A))).astype(np.float32)
+    adv = rng.normal(0.3, 2.0, B).astype(np.float32)
+    ret = rng.normal(0, 1, B).astype(np.float32)
+    sc_s = np.exp(logstd)
+    lp = (-(act - head) ** 2 / (2 * sc_s ** 2) - logstd - 0.5 * np.log(2 * np.pi)).sum(-1)
+    old = (lp + rng.normal(0, 0.3, B)).astype(np.float32)
+    part = None
+    if advnorm:
+        a = adv.astype(np.float64)
+        part = torch.tensor([[a.sum(), (a * a).sum()]], dtype=torch.float64, device=DEV)
+    sc, dh, dls, dv = ops.policy_loss(algo, "gaussian", _d(head), _d(logstd), _d(v), _d(act), _d(adv), _d(ret),
+                                      old_logp=_d(old) if algo == "ppo" else None, adv_partials=part,
+                                      clip_range=0.2, vf_coef=0.5, ent_coef=0.01)
+    adv_n = (adv - adv.mean()) / (adv.std() + 1e-8) if advnorm else adv
+    info, rdh, rdls, rdv = cpu_ref.loss_grads_ref(algo, "gaussian", head, logstd, v, act, adv_n, ret,
+                                                  old if algo == "ppo" else None, 0.2, 0.5, 0.01)
+    sc = _h(sc)
+    assert abs(sc[3] - info["loss"]) < 1e-4, (sc, info)
+    assert abs(sc[0] - info["actor-loss"]) < 1e-4
+    np.testing.assert_allclose(_h(dh), rdh, rtol=2e-4, atol=1e-8)
+    np.testing.assert_allclose(_h(dv), rdv, rtol=1e-4, atol=1e-9)
+    np.testing.assert_allclose(_h(dls), rdls, rtol=2e-4, atol=1e-5)
+    if algo == "ppo":
+        assert abs(sc[4] - info["clip_ratio"]) < 2.0 / B
+
+
 def test_loss_kernel_out_of_range_idx_is_inert():
     from xuanpolicy_amd import ops
     B, A = 64, 3
