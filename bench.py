@@ -544,8 +544,10 @@ def main():
                                    (N, T, args.n_epoch, args.n_minibatch, args.hidden),
                        "num_envs_per_gpu": N, "horizon": T, "global_envs": N * world, "minibatch": B,
                        "updates_per_step": args.n_epoch * args.n_minibatch,
-                       "parallelism": "dp%d (env shards, 1 %s all-reduce per minibatch)" % (
-                           world, "RCCL" if world == 1 or dist.get_backend() == "nccl" else dist.get_backend())},
+                       "parallelism": ("dp1 (one env shard, no collective)" if world == 1 else
+                                       "dp%d (env shards; the flat gradient all-reduced per minibatch over %s: the "
+                                       "paired hidden dW slice early + the rest, 2 calls)" % (
+                                           world, "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()))},
             "roofline": roofline,
             "phase_split_ms": phase_ms,
             "loss_kernel": loss_kernel,

@@ -68,13 +68,30 @@ def _worker(rank, world, port, q):
         dist.all_reduce(whole, op=dist.ReduceOp.SUM)
         whole.div_(world)
         w0 = fs.params[2].grad                    # the second Linear's weight: a slice inside the buffer
+        c0 = ar.collectives
         assert ar.begin(w0) and not ar.begin(w0)  # one early slice per update
         ar(fs.params)
-        assert ar.calls == 2 and ar._early is None
+        assert ar.calls == 2 and ar._early is None and ar.collectives - c0 == 3   # slice inside: 3 calls
         assert torch.equal(fs.flat, whole)
+        # a placement group is laid out first: its slice is a prefix, so slice + rest = 2 collectives
+        torch.manual_seed(5)
+        net2 = torch.nn.Sequential(torch.nn.Linear(5, 16), torch.nn.LeakyReLU(), torch.nn.Linear(16, 4))
+        fs2 = FlatState(net2.parameters(), placement=[[net2[2].weight, net2[2].bias]])
+        assert fs2.offsets[2] == 0 and fs2.offsets[3] == 64 and fs2.offsets[0] > fs2.offsets[3]
+        ar2 = GradAllReduce(fs2)
+        fs2.zero_()
+        ((net2(x) - y.repeat(1, 2)[:, :4]) ** 2).mean().backward()
+        whole2 = fs2.flat.clone()
+        dist.all_reduce(whole2, op=dist.ReduceOp.SUM)
+        whole2.div_(world)
+        span = fs2.span([net2[2].weight, net2[2].bias])[1]
+        assert ar2.begin(span)
+        ar2(fs2.params)
+        assert ar2.collectives == 2 and torch.equal(fs2.flat, whole2)
         q.put((rank, "ok"))
     except Exception as e:  # pragma: no cover - reported to the parent
-        q.put((rank, repr(e)))
+        import traceback
+        q.put((rank, traceback.format_exc()))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()

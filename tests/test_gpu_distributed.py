@@ -104,3 +104,78 @@ def test_dp_normalisation_variants_two_ranks_one_gpu():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: "ok", 1: "ok"}, res
+
+
+def _fast_worker(rank, world, port, q):
+    """The C2 fast path (hidden [256]: K13 trunk, K14E, K16 heads, split-K dW with the early all-reduce of the
+    paired hidden slice) on 2 ranks sharing the GPU over gloo."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), XPA_DIST_BACKEND="gloo")
+    import torch.distributed as dist
+    try:
+        from xuanpolicy_amd.distributed import broadcast_parameters, init_from_env
+        from xuanpolicy_amd.runner import build_synthbox_ppo
+        init_from_env()
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        agent = build_synthbox_ppo(n_envs=128, n_steps=16, obs_dim=17, act_dim=6, hidden=256, n_epoch=2,
+                                   n_minibatch=2, seed=11, device=dev, shard=rank)
+        broadcast_parameters(agent.policy)
+        fm = agent.learner._fused_mlp()
+        assert fm is not None and fm.gemm_heads and fm.pair is not None, "fast path expected"
+        gs = agent.learner.grad_sync
+        assert gs is not None
+        agent.train(32)                     # two iterations of 16 steps, 4 updates each
+        torch.cuda.synchronize()
+        assert gs.calls == 8 and gs.collectives == 16, (gs.calls, gs.collectives)   # 2 per update
+        p = torch.cat([t.detach().reshape(-1) for t in agent.policy.parameters()])
+        got = [torch.empty_like(p) for _ in range(world)]
+        dist.all_gather(got, p)
+        assert torch.equal(got[0], got[1]) and torch.isfinite(p).all()
+        q.put((rank, "ok"))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_dp_fast_path_two_collectives_per_update_two_ranks_one_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fast_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=580) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: "ok", 1: "ok"}, res
+
+
+@pytest.mark.timeout(600)
+def test_bench_two_rank_rehearsal_one_gpu():
+    """`bench.py --gpus 2` as the driver launches it (torch.distributed.run, one process per rank), both ranks on
+    the box's one GPU over gloo: the JSON line reports the whole-job rate of 2 env shards."""
+    import json
+    import subprocess
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, XPA_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(repo, "bench.py"), "--gpus", "2", "--steps",
+           "2", "--warmup", "1", "--n-envs", "256", "--horizon", "32", "--n-epoch", "2", "--n-minibatch", "2",
+           "--no-sweep", "--no-per", "--no-c3", "--no-c4", "--no-cpu-baseline", "--no-kernel-timing"]
+    out = subprocess.run(cmd, cwd=repo, env=env, capture_output=True, text=True, timeout=560)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["steps"] == 2 and r["value"] > 0
+    assert r["config"]["global_envs"] == 512 and "dp2" in r["config"]["parallelism"]

@@ -145,6 +145,7 @@ class _OnPolicyAgent:
             self.slot_obs = torch.zeros((N, D), **f32)
             self.slot_t = torch.full((N,), -1, dtype=torch.int32, device=dev)
             self.slot_overflow = torch.zeros((1,), dtype=torch.int32, device=dev)
+            self._overflow_host = self._overflow_event = None
         self._graph = None
         self._graph_pool = None
         # Model / log directories and the logger (agent.py:33-70).  model_dir_save is seed_<seed>_<time>
@@ -368,9 +369,16 @@ class _OnPolicyAgent:
         else:
             with torch.no_grad():
                 v = policy_heads(self.policy, x)[2].contiguous()
-        if int(self.slot_overflow.item()):   # cannot happen for the device envs (see __init__); never silent
-            self.slot_overflow.zero_()
+        # An env truncating twice in one rollout cannot happen for the device envs (their one truncation source is
+        # the time limit and max_episode_steps >= n_steps, see __init__), so the flag is checked without a host
+        # sync: copied to pinned memory here and read one iteration later (never silent, never a stall).
+        if self._overflow_host is None:
+            self._overflow_host = torch.zeros((1,), dtype=torch.int32, pin_memory=True)
+            self._overflow_event = torch.cuda.Event()
+        elif self._overflow_event.query() and int(self._overflow_host[0]):
             raise RuntimeError("an env truncated twice within one rollout; set config.defer_bootstrap = False")
+        self._overflow_host.copy_(self.slot_overflow, non_blocking=True)
+        self._overflow_event.record()
         return v.reshape(-1)
 
     def _update_phase(self):

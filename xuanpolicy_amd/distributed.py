@@ -9,8 +9,9 @@ clip_grad_norm_, so the clipped norm is the global one.
 FlatState (xuanpolicy_amd.flat) makes every parameter's .grad a view into one contiguous buffer, so
 autograd accumulates straight into it and the all-reduce is one RCCL call over xGMI per minibatch
 (latency-bound at 0.04-1 MiB; one bucket) — or, on the fused MLP path, two: the paired hidden layers' dW
-slice is started as soon as its GEMM has written it and overlaps the rest of the backward
-(GradAllReduce.begin).  Backend "nccl" is RCCL on ROCm; "gloo" is used by the CPU tests.
+slice (the first 0.5 MB of the flat buffer) is started as soon as its GEMM has written it and overlaps the
+rest of the backward (GradAllReduce.begin); the rest is one more call.  The overlap is exercised with gloo
+(CPU, and 2 ranks on one GPU); its RCCL timing on xGMI is unmeasured (no multi-GPU box this round).  Backend "nccl" is RCCL on ROCm; "gloo" is used by the CPU tests.
 """
 import os
 
@@ -35,10 +36,12 @@ class GradAllReduce:
         self.world = dist.get_world_size(group)
         self.avg = dist.get_backend(group) == "nccl"
         self.calls = 0
+        self.collectives = 0  # all_reduce calls issued (the fused MLP update: 2 per minibatch)
         self._early = None   # (offset, numel, work)
 
     def _reduce(self, t, async_op=False):
         op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
+        self.collectives += 1
         return dist.all_reduce(t, op=op, group=self.group, async_op=async_op)
 
     def begin(self, region):
@@ -62,6 +65,8 @@ class GradAllReduce:
         else:
             off, n, work = self._early
             self._early = None
+            # FlatState lays the paired hidden layers out first, so the early slice is a prefix and the rest
+            # is ONE range; a slice elsewhere costs one more collective for the range before it
             for lo, hi in ((0, off), (off + n, flat.numel())):
                 if hi > lo:
                     self._reduce(flat[lo:hi])

@@ -37,14 +37,20 @@ class FlatState:
             if ok:
                 for p in g:
                     group_of[id(p)] = g
+        # placement groups first (from offset 0), then the other parameters in order: a group's gradient span
+        # is then a prefix of the flat buffer, so an early all-reduce of it plus one of the rest is two
+        # collectives per update (distributed.GradAllReduce), never three
         offsets = [None] * len(self.params)
         off = 0
+        for g in placement or []:
+            if g and id(g[0]) in group_of and group_of[id(g[0])] is g:
+                for q in g:
+                    offsets[index[id(q)]] = off
+                    off += _aligned(q.numel())
         for p in self.params:
-            if offsets[index[id(p)]] is not None:
-                continue
-            for q in group_of.get(id(p), [p]):
-                offsets[index[id(q)]] = off
-                off += _aligned(q.numel())
+            if offsets[index[id(p)]] is None:
+                offsets[index[id(p)]] = off
+                off += _aligned(p.numel())
         self.offsets = offsets
         n = off
         dev = self.params[0].device
