@@ -16,6 +16,12 @@ Fixtures:
                       (oracle/synth_env.py) in the reference's DummyVecEnv_Gym: every stored step,
                       every closure, the permutations, learner infos, initial and final parameters.
   rms.npz      G7     RunningMeanStd (statistic_tools.py:35-112) update sequences.
+  atari_a2c.npz G8    two seeded iterations of A2C_Agent.train (a2c_agent.py:57-107) with env_name "Atari":
+                      DummyOnPolicyBuffer_Atari (memory_tools.py:526-560, uint8 frames), AC_CNN_Atari
+                      (cnn.py:45-93) + Categorical_AC_Policy, DummyVecEnv_Atari over SynthAtari envs
+                      (oracle/synth_env.py; life losses keep the path open, game overs truncate).  Frames are
+                      NOT stored: the test regenerates them by stepping the oracle env with the recorded
+                      actions and checks them against the recorded per-step frame sums.
   per.npz      G6     PerOffPolicyBuffer (memory_tools.py:369-492) + Sum/MinSegmentTree (segtree_tool.py):
                       store / sample(beta) / update_priorities rounds with every uniform random.random()
                       returned to the sampler recorded, the trees after every call, max priorities, the
@@ -43,8 +49,9 @@ from xuance.torch.representations import Basic_MLP  # noqa: E402
 from xuance.torch.policies import Gaussian_AC_Policy, Categorical_AC_Policy  # noqa: E402
 from xuance.torch.learners import PPOCLIP_Learner, A2C_Learner  # noqa: E402
 from xuance.torch.agents import PPOCLIP_Agent, A2C_Agent  # noqa: E402
-from xuance.environment.gym.gym_vec_env import DummyVecEnv_Gym  # noqa: E402
-from oracle.synth_env import SynthBoxEnv  # noqa: E402
+from xuance.environment.gym.gym_vec_env import DummyVecEnv_Gym, DummyVecEnv_Atari  # noqa: E402
+from xuance.torch.representations import AC_CNN_Atari  # noqa: E402
+from oracle.synth_env import SynthAtariEnv, SynthBoxEnv  # noqa: E402
 
 torch.set_num_threads(1)
 
@@ -356,6 +363,96 @@ def capture_per():
     print("per.npz", len(out))
 
 
+# ----------------------------------------------------------------------------------------------
+ATARI_NET = dict(filters=[8, 8], kernels=[8, 4], strides=[4, 2], fc_hidden_sizes=[32])  # a small AC_CNN_Atari
+
+
+def capture_atari(N=4, T=16, iters=2, max_ep=20, n_actions=6, seed=5):
+    cfg = types.SimpleNamespace(render=False, n_steps=T, n_minibatch=2, n_epoch=2, gamma=0.99, gae_lambda=0.95,
+                                env_name="Atari", use_gae=True, use_advnorm=True, device="cpu", model_dir="./models/",
+                                log_dir="./logs/", vf_coef=0.25, ent_coef=0.01, clip_grad=0.2, use_obsnorm=False,
+                                use_rewnorm=False, obsnorm_range=5, rewnorm_range=5, seed=seed, logger="tensorboard",
+                                test_mode=False)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    obs_space, act_space = gym.spaces.Box(0, 255, (84, 84, 4)), gym.spaces.Discrete(n_actions)
+
+    class _Env(SynthAtariEnv):   # the reference's env contract: spaces on the instance
+        observation_space, action_space = obs_space, act_space
+
+        def close(self):
+            pass
+
+    envs = DummyVecEnv_Atari([(lambda i=i: _Env(i, seed=seed, n_actions=n_actions, max_episode_steps=max_ep))
+                              for i in range(N)])
+    torch.manual_seed(seed)
+    rep = AC_CNN_Atari((84, 84, 4), ATARI_NET["kernels"], ATARI_NET["strides"], ATARI_NET["filters"], None,
+                       torch.nn.init.orthogonal_, torch.nn.ReLU, "cpu", ATARI_NET["fc_hidden_sizes"])
+    policy = Categorical_AC_Policy(act_space, rep, [], [], None, torch.nn.init.orthogonal_, torch.nn.ReLU, "cpu")
+    out = {}
+    _sd("sd0/", policy, out)
+    opt = torch.optim.Adam(policy.parameters(), 7e-4, eps=1e-5)
+    sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.0, total_iters=10000)
+    agent = A2C_Agent(cfg, envs, policy, opt, sch, "cpu")
+    envs.reset()
+    rec = {"closed": np.zeros((iters, N, T), np.uint8), "boot": np.zeros((iters, N, T), np.float32)}
+    snaps, perms, infos, env_acts = [], [], [], []
+    mem = agent.memory
+    it = {"k": 0}
+    orig_fp, orig_clear, orig_update, orig_step = mem.finish_path, mem.clear, agent.learner.update, envs.step
+    orig_shuffle = np.random.shuffle
+
+    def finish_path(val, i):
+        end = mem.n_size if mem.full else mem.ptr
+        if end > mem.start_ids[i] and it["k"] < iters:
+            rec["closed"][it["k"], i, end - 1] = 1
+            rec["boot"][it["k"], i, end - 1] = val
+        return orig_fp(val, i)
+
+    def clear():
+        snaps.append({"act": mem.actions.copy(), "rew": mem.rewards.copy(), "val": mem.values.copy(),
+                      "term": mem.terminals.copy(), "ret": mem.returns.copy(), "adv": mem.advantages.copy(),
+                      "frame_sum": mem.observations.reshape(N, T, -1).astype(np.int64).sum(-1),
+                      "obs_dtype_u8": np.asarray(mem.observations.dtype == np.uint8)})
+        it["k"] += 1
+        return orig_clear()
+
+    def update(*a):
+        info = orig_update(*a)
+        infos.append([float(info[k]) for k in ("actor-loss", "critic-loss", "entropy", "learning_rate",
+                                                "predict_value")])
+        return info
+
+    def shuffle(x):
+        orig_shuffle(x)
+        perms.append(x.copy())
+
+    def step(acts):
+        env_acts.append(np.asarray(acts).copy())
+        return orig_step(acts)
+
+    mem.finish_path, mem.clear, agent.learner.update, envs.step = finish_path, clear, update, step
+    np.random.shuffle = shuffle
+    try:
+        agent.train(iters * T)
+    finally:
+        np.random.shuffle = orig_shuffle
+    for k in ("act", "rew", "val", "term", "ret", "adv", "frame_sum"):
+        out[k] = np.stack([s_[k] for s_ in snaps])
+    assert all(bool(s_["obs_dtype_u8"]) for s_ in snaps)
+    out["closed"], out["boot"] = rec["closed"], rec["boot"]
+    out["env_actions"] = np.stack(env_acts).astype(np.int64)
+    out["perms"] = np.stack(perms).astype(np.int64)
+    out["infos"] = np.asarray(infos, np.float64)
+    out["config"] = np.asarray([N, T, n_actions, cfg.n_epoch, cfg.n_minibatch, max_ep, seed], np.int64)
+    out["net"] = np.asarray(ATARI_NET["filters"] + ATARI_NET["kernels"] + ATARI_NET["strides"]
+                            + ATARI_NET["fc_hidden_sizes"], np.int64)
+    _sd("sd1/", policy, out)
+    np.savez_compressed(os.path.join(HERE, "atari_a2c.npz"), **out)
+    print("atari_a2c.npz", len(out), "closures", int(out["closed"].sum()), "life-loss terminals",
+          int(out["term"].sum()))
+
+
 if __name__ == "__main__":
     os.makedirs("/tmp/xref_run", exist_ok=True)
     os.chdir("/tmp/xref_run")
@@ -365,3 +462,4 @@ if __name__ == "__main__":
     capture_agent("a2c", True, 4, 2)
     capture_rms()
     capture_per()
+    capture_atari()

@@ -162,3 +162,37 @@ def test_agent_replay_oracle(golden, name):
                 u += 1
     for k, v in pol.state_dict().items():
         np.testing.assert_allclose(v.numpy(), g["sd1/" + k], rtol=1e-4, atol=1e-5, err_msg=k)
+
+
+def test_atari_fixture_frames_and_gae_from_oracle(golden):
+    """G8 pinned on CPU: stepping the oracle SynthAtari env with the recorded actions through the reference's
+    DummyVecEnv / A2C_Agent observation flow (gym_vec_env.py:201-212, a2c_agent.py:80-92) reproduces the
+    rewards, life-loss terminals and per-step frame sums the reference stored, and the oracle GAE over the
+    recorded Atari closures (life losses keep the path open) reproduces its advantages and returns."""
+    from oracle.synth_env import SynthAtariEnv
+    g = golden("atari_a2c.npz")
+    N, T, K, _, _, max_ep, seed = (int(x) for x in g["config"])
+    envs = [SynthAtariEnv(i, seed=seed, n_actions=K, max_episode_steps=max_ep) for i in range(N)]
+    obs = np.stack([e.reset()[0] for e in envs])
+    k = 0
+    for it in range(g["act"].shape[0]):
+        for t in range(T):
+            nxt, raw = obs.copy(), obs.copy()
+            for i, e in enumerate(envs):
+                o, r, te, tr, info = e.step(g["env_actions"][k][i])
+                assert r == g["rew"][it][i, t] and te == bool(g["term"][it][i, t])
+                if te or tr:
+                    info["reset_obs"] = e.reset()[0]
+                raw[i] = o
+                nxt[i] = info["reset_obs"] if tr else o
+            # the first step of train() stores the vec env's live buf_obs AFTER envs.step wrote into it
+            # (a2c_agent.py:59-66: obs aliases envs.buf_obs until the first obs = next_obs; no obsnorm copy)
+            stored = raw if (it, t) == (0, 0) else obs
+            assert np.array_equal(stored.reshape(N, -1).astype(np.int64).sum(-1), g["frame_sum"][it][:, t])
+            k += 1
+            obs = nxt
+        adv, ret = cpu_ref.gae_rows(g["rew"][it], g["val"][it], g["term"][it], g["closed"][it], g["boot"][it],
+                                    0.99, 0.95)
+        np.testing.assert_allclose(adv, g["adv"][it], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(ret, g["ret"][it], rtol=1e-5, atol=1e-5)
+    assert int(g["term"].sum()) > 0 and int(g["closed"].sum()) > 0
