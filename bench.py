@@ -38,7 +38,7 @@ def parse():
     p.add_argument("--n-epoch", type=int, default=16)
     p.add_argument("--n-minibatch", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-updates", type=int, default=16, help="updates timed in the bounded CPU sample")
+    p.add_argument("--cpu-updates", type=int, default=24, help="updates timed in the bounded CPU sample")
     p.add_argument("--no-sweep", action="store_true")
     p.add_argument("--no-per", action="store_true", help="skip the C5 PER (K6) measurement")
     p.add_argument("--no-c3", action="store_true", help="skip the C3 Atari A2C measurement")
@@ -350,6 +350,18 @@ def c4_bench(device, rank, world, n_envs=4096, n_steps=128, steps=2, warmup=1):
     return res
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(args, cores):
     """The oracle's restatement of the reference loop (oracle/cpu_ref.AgentLoopRef: per-env
     DummyVecEnv stepping, per-env finish_path, numpy fancy-index sampling, torch-CPU learner with
@@ -372,6 +384,7 @@ def cpu_baseline(args, cores):
     wall = time.perf_counter() - t0
     tm = loop.timers
     per_update = (tm["sample"] + tm["update"]) / max(loop.n_updates, 1)
+    ut = np.asarray(loop.update_times)
     n_updates_full = args.n_epoch * ((N * T + (N * T // args.n_minibatch) - 1) // (N * T // args.n_minibatch))
     rollout = tm["act"] + tm["env"] + tm["store"]
     iteration = rollout + tm["gae"] + n_updates_full * per_update
@@ -380,7 +393,12 @@ def cpu_baseline(args, cores):
                       "GAE + %d of the %d minibatch updates (B=%d) timed in %.1f s; iteration time = rollout %.2f s "
                       "+ GAE %.2f s + %d x %.3f s per update (sample + learner.update) = %.2f s"
                       % (N, T, loop.n_updates, n_updates_full, N * T // args.n_minibatch, wall, rollout, tm["gae"],
-                         n_updates_full, per_update, iteration))}
+                         n_updates_full, per_update, iteration)),
+           "per_update_s": {"mean": round(float(ut.mean()), 4), "std": round(float(ut.std()), 4),
+                            "min": round(float(ut.min()), 4), "max": round(float(ut.max()), 4), "n": int(ut.size)},
+           "cpu_model": _cpu_model(), "affinity_cpus": len(os.sched_getaffinity(0)),
+           "threads_note": "torch intra-op threads = the box's CPU share (OMP_NUM_THREADS, 16 on the GPU box; "
+                           "the affinity mask spans the whole host)"}
     # the same loop with the env vectorised in numpy (synth_env.SynthBoxVec), so the
     # speedup is not credited only to removing the per-env Python stepping; the updates cost the same.
     venv = synth_env.SynthBoxVec(N, D, A, seed=1)
@@ -573,7 +591,8 @@ def main():
         if not args.no_per and world == 1:
             result["per_kernels"] = per_bench(device)
         if not args.no_cpu_baseline and world == 1:
-            cores = min(16, len(os.sched_getaffinity(0)))
+            aff = len(os.sched_getaffinity(0))
+            cores = min(aff, int(os.environ.get("OMP_NUM_THREADS", aff)))   # the box's CPU share
             result["cpu_baseline"] = cpu_baseline(args, cores)
             result["speedup_vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
             result["speedup_vs_cpu_vectorized_env"] = round(

@@ -467,6 +467,7 @@ class AgentLoopRef:
         self.batch_size = self.buffer_size // n_minibatch
         self.timers = {k: 0.0 for k in ("act", "env", "store", "gae", "sample", "update")}
         self.n_updates = 0
+        self.update_times = []   # seconds per (sample + learner.update), for the baseline's spread
         if envs is not None:
             self.obs = np.stack([e.reset()[0] for e in envs]).astype(np.float32)
         else:
@@ -542,8 +543,10 @@ class AgentLoopRef:
                         ob, ac, rt, vl, ad, ax = self.memory.sample(idx[start:start + self.batch_size])
                         tu = time.perf_counter()
                         info = self.learner.update(ob, ac, rt, ad, ax.get("old_logp"))
+                        te = time.perf_counter()
                         tm["sample"] += tu - ts
-                        tm["update"] += time.perf_counter() - tu
+                        tm["update"] += te - tu
+                        self.update_times.append(te - ts)
                         done_updates += 1
                         self.n_updates += 1
                         if on_update is not None:
