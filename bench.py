@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--cpu-updates", type=int, default=24, help="updates timed in the bounded CPU sample")
     p.add_argument("--no-sweep", action="store_true")
     p.add_argument("--no-per", action="store_true", help="skip the C5 PER (K6) measurement")
+    p.add_argument("--no-c1", action="store_true", help="skip the C1 CartPole measurement")
     p.add_argument("--no-c3", action="store_true", help="skip the C3 Atari A2C measurement")
     p.add_argument("--no-c4", action="store_true", help="skip the C4 Box(376,17) measurement")
     p.add_argument("--no-kernel-timing", action="store_true")
@@ -283,6 +284,57 @@ def per_bench(device, n_envs=8, n_size=131072, batch=2048, frames=True, reps=50)
     res["cpu_reference_restated"] = {"sample_us": round((t1 - t0) * 1e6, 1), "update_priorities_us":
                                      round((t2 - t1) * 1e6, 1), "cores": 1, "kind": "port"}
     res["speedup_sample_update"] = round(((t2 - t0) * 1e6) / (t_sample + t_update), 1)
+    return res
+
+
+def c1_bench(device, n_envs=8, n_steps=128, hidden=64, steps=5, warmup=1, cpu=True):
+    """C1 (BASELINE.json configs[0]): PPO-Clip on CartPole-v1, 8 envs x 128 steps, ppo/classic_control/
+    CartPole-v1.yaml (8 epochs x 8 minibatches of 128), [64] nets, on device (K18 env, K3 sampling, K1 GAE,
+    K2 / K9 updates) — and the same loop on the host as the reference runs it (oracle/cpu_ref.AgentLoopRef over
+    per-env CartPoleEnv objects, torch-CPU learner): the reference's own CPU-runnable configuration."""
+    import numpy as np
+    import torch
+    from xuanpolicy_amd.runner import build_cartpole_ppo
+    agent = build_cartpole_ppo(n_envs=n_envs, n_steps=n_steps, hidden=hidden, device=device)
+    cfg = agent.config
+    for _ in range(warmup):
+        agent.train(n_steps, log=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        agent.train(n_steps, log=False)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    res = {"workload": "PPO-Clip CartPole-v1 num_envs=%d horizon=%d, ppo/classic_control/CartPole-v1.yaml (n_epoch %d, "
+                       "n_minibatch %d), nets [%d] LeakyReLU" % (n_envs, n_steps, cfg.n_epoch, cfg.n_minibatch,
+                                                               hidden),
+           "metric": "env-steps/s", "value": round(n_envs * n_steps * steps / el, 1),
+           "ms_per_iteration": round(el / steps * 1e3, 2), "iterations": steps, "dtype": "f32 (f64 env state)"}
+    del agent
+    if cpu:
+        from oracle import cpu_ref, synth_env
+        torch.manual_seed(1)
+        np.random.seed(1)
+        nthreads = torch.get_num_threads()
+        torch.set_num_threads(1)     # 128-row minibatches: one thread is the reference's fastest setting here
+        envs = [synth_env.CartPoleEnv(i, seed=1) for i in range(n_envs)]
+        pol = cpu_ref.build_actor_critic_ref(4, 2, [hidden], [hidden], [hidden], discrete=True)
+        opt = torch.optim.Adam(pol.parameters(), cfg.learning_rate, eps=1e-5)
+        sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.0, total_iters=cfg.running_steps)
+        lrn = cpu_ref.LearnerRef(pol, opt, sch, "ppo", cfg.vf_coef, cfg.ent_coef, cfg.clip_range, cfg.clip_grad_norm,
+                                 True)
+        loop = cpu_ref.AgentLoopRef(envs, pol, lrn, n_steps, cfg.n_epoch, cfg.n_minibatch, cfg.gamma, cfg.gae_lambda)
+        loop.run_steps(n_steps)          # warm-up iteration
+        t0 = time.perf_counter()
+        loop.run_steps(2 * n_steps)
+        el_cpu = time.perf_counter() - t0
+        torch.set_num_threads(nthreads)
+        res["cpu_reference_loop"] = {"value": round(n_envs * n_steps * 2 / el_cpu, 1), "unit": "env-steps/s",
+                                     "cores": 1, "kind": "port", "sample": "2 full iterations (%d updates) of the "
+                                     "restated reference loop after one warm-up iteration" % (2 * cfg.n_epoch *
+                                                                                            cfg.n_minibatch)}
+        res["speedup_vs_cpu"] = round(res["value"] / res["cpu_reference_loop"]["value"], 2)
+    torch.cuda.empty_cache()
     return res
 
 
@@ -586,6 +638,8 @@ def main():
                     "unit": "GB/s", "frac": k2["frac"], "algorithmic_bytes_per_launch": k2["algorithmic_bytes"],
                     "timing": "host-recorded events around one launch after a 512 MiB cache-flush read (median of 7); "
                               "see loss_sweep_flushed for larger batches"}
+        if not args.no_c1 and world == 1:
+            result["c1_cartpole"] = c1_bench(device)
         if not args.no_c3 and world == 1:
             result["c3_atari_a2c"] = c3_bench(device)
         if not args.no_per and world == 1:

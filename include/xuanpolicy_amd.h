@@ -192,6 +192,17 @@ int xpa_synthbox_step(int64_t n_envs, int64_t obs_dim, const float *pre, uint32_
                       uint8_t *trunc, int32_t *ep_step, uint32_t *ep_index, float *ep_score,
                       float *ep_last_score, int32_t *ep_last_len, xpa_stream_t stream);
 
+/* K18 — CartPole-v1 environment step (BASELINE.json configs[0]; replaces DummyVecEnv_Gym.step_wait over gym's
+ * CartPoleEnv, gym_vec_env.py:201-212; dynamics of gym 0.26.2 classic_control/cartpole.py with TimeLimit(500)).
+ * One thread per env: f64 state [n_envs, 4], action = act_in[n * ld_act + 1] > 0.5 (the one-hot env input the
+ * rollout kernels write), euler step, reward 1, terminated on |x| > 2.4 or |theta| > 12 deg, truncated at
+ * max_episode_steps; done envs auto-reset with hashed uniform(-0.05, 0.05) states.  Writes final_obs (f32 image
+ * of the stepped state), obs (row stride ld_obs: the state or the reset state), rew, term, trunc, counters. */
+int xpa_cartpole_step(int64_t n_envs, const float *act_in, int64_t ld_act, double *state, float *obs,
+                      int64_t ld_obs, float *final_obs, float *rew, uint8_t *term, uint8_t *trunc,
+                      int32_t *ep_step, uint32_t *ep_index, float *ep_score, float *ep_last_score,
+                      int32_t *ep_last_len, uint32_t seed, int32_t max_episode_steps, xpa_stream_t stream);
+
 /* K8 — rollout post-step bookkeeping.  Replaces, per step, DummyOnPolicyBuffer.store of
  * rewards/terminals (memory_tools.py:196-204) with reward normalisation (agent.py:118-123), the
  * return tracker and ret_rms update (ppoclip_agent.py:87-92 with the (1-term) mask; a2c_agent.py:84

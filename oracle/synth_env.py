@@ -298,3 +298,78 @@ class SynthAtariEnv:
             self._reset_state()
             info["reset_obs"] = self.stack.copy()
         return obs, np.float32(r), terminated, truncated, info
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# CartPole-v1 (BASELINE.json configs[0]).  gym is not installed here; this restates the published
+# gym 0.26.2 classic_control/cartpole.py dynamics (euler integrator, Python-float = f64 state, f32 observations)
+# under TimeLimit(max_episode_steps=500).  Delta: the reset state's uniform(-0.05, 0.05) draws come from the
+# counter hash (seed, env, episode, dim) instead of the env's np_random, so CPU and GPU agree.  Parity against
+# gym itself is unpinned (no gym, no recorded gym trajectories in the reference).
+CP_GRAVITY, CP_MASSCART, CP_MASSPOLE, CP_LENGTH, CP_FORCE, CP_TAU = 9.8, 1.0, 0.1, 0.5, 10.0, 0.02
+CP_TOTAL_MASS = CP_MASSPOLE + CP_MASSCART
+CP_POLEMASS_LENGTH = CP_MASSPOLE * CP_LENGTH
+CP_THETA_THRESHOLD = 12 * 2 * np.pi / 360
+CP_X_THRESHOLD = 2.4
+SALT_CARTPOLE = 0xCA27B01E
+
+
+def cartpole_reset_state(seed, env, episode):
+    """uniform(-0.05, 0.05) per dim: f32-exact hash uniform, then f64 (the device computes the same)."""
+    u = u01(hash4(seed ^ SALT_CARTPOLE, np.uint32(env), np.uint32(episode), np.arange(4, dtype=np.uint32)))
+    return u.astype(np.float64) * 0.1 - 0.05
+
+
+def cartpole_dynamics(state, action):
+    """One euler step of gym's CartPoleEnv.step (cartpole.py: force, temp, thetaacc, xacc, euler update) on f64
+    state arrays [..., 4]; returns (new_state, terminated)."""
+    x, x_dot, theta, theta_dot = (state[..., k] for k in range(4))
+    force = np.where(np.asarray(action) == 1, CP_FORCE, -CP_FORCE)
+    costheta, sintheta = np.cos(theta), np.sin(theta)
+    temp = (force + CP_POLEMASS_LENGTH * theta_dot ** 2 * sintheta) / CP_TOTAL_MASS
+    thetaacc = (CP_GRAVITY * sintheta - costheta * temp) / (
+        CP_LENGTH * (4.0 / 3.0 - CP_MASSPOLE * costheta ** 2 / CP_TOTAL_MASS))
+    xacc = temp - CP_POLEMASS_LENGTH * thetaacc * costheta / CP_TOTAL_MASS
+    x = x + CP_TAU * x_dot
+    x_dot = x_dot + CP_TAU * xacc
+    theta = theta + CP_TAU * theta_dot
+    theta_dot = theta_dot + CP_TAU * thetaacc
+    new = np.stack([x, x_dot, theta, theta_dot], axis=-1)
+    term = (x < -CP_X_THRESHOLD) | (x > CP_X_THRESHOLD) | (theta < -CP_THETA_THRESHOLD) | (theta > CP_THETA_THRESHOLD)
+    return new, term
+
+
+class CartPoleEnv:
+    """One CartPole-v1 env with the gym step contract the reference's DummyVecEnv_Gym drives (reward 1 per step,
+    terminated on the angle / position limits, truncated at 500 steps, auto-reset by the vec env)."""
+
+    def __init__(self, env_id, seed=1, max_episode_steps=500):
+        self.env_id, self.seed, self.max_episode_steps = int(env_id), int(seed), int(max_episode_steps)
+        self.ep = 0
+        self.D, self.A, self.discrete = 4, 2, True   # AgentLoopRef's env description
+        self.observation_space = _Box(-np.inf, np.inf, (4,))
+        self.action_space = _Discrete(2)
+        self._reset_state()
+
+    def _reset_state(self):
+        self.state = cartpole_reset_state(self.seed, self.env_id, self.ep)
+        self.ep_step, self.score = 0, 0.0
+
+    def reset(self):
+        return self.state.astype(np.float32), {"episode_step": self.ep_step}
+
+    def close(self):
+        pass
+
+    def step(self, a):
+        self.state, term = cartpole_dynamics(self.state, int(a))
+        self.ep_step += 1
+        self.score += 1.0
+        term = bool(term)
+        trunc = self.ep_step >= self.max_episode_steps   # gym TimeLimit: independent of terminated
+        obs = self.state.astype(np.float32)
+        info = {"episode_step": self.ep_step, "episode_score": self.score}
+        if term or trunc:
+            self.ep += 1
+            self._reset_state()
+        return obs, np.float32(1.0), term, trunc, info

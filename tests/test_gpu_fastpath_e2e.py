@@ -21,6 +21,7 @@ import pytest
 import torch
 
 from oracle import cpu_ref
+from tests._oracle_replay import replay_last_step_iteration
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -58,97 +59,4 @@ def test_fast_path_iteration_matches_oracle(agent_name, discrete, A, ent):
 
     agent.train(T, log=False)             # iteration 1 (episodes start together; time limit at step 81)
     agent.train(T - 1, log=False)         # iteration 2's rollout but its last step
-    pol = cpu_ref.build_actor_critic_ref(D, A, [H], [H], [H], discrete=discrete)
-    pol.load_state_dict({k: v.detach().cpu() for k, v in agent.policy.state_dict().items()})
-    pol.double()
-    # the optimizer / schedule state the 8 updates of iteration 2 start from (Adam moments + step, LinearLR)
-    opt_state = {n: {k: (v.detach().cpu().clone() if isinstance(v, torch.Tensor) else v)
-                     for k, v in agent.learner.optimizer.state[p].items()}
-                 for n, p in agent.policy.named_parameters()}
-    lr0 = agent.learner.optimizer.param_groups[0]["lr"]
-    sched_epoch = agent.learner.scheduler.last_epoch
-    perm_counter = agent._perm_counter
-    agent.update_log = []
-    agent.train(1, log=False)             # last env step -> deferred bootstraps + GAE -> 8 updates
-    torch.cuda.synchronize()
-    mem = agent.memory
-
-    # ---- rollout: values and old log-probs at the iteration's weights (f64 oracle) ----
-    obs = mem.observations.cpu().numpy().astype(np.float64)
-    act = mem.actions.cpu().numpy().astype(np.float64)
-    with torch.no_grad():
-        head, logstd, v = pol.heads(torch.as_tensor(obs.reshape(N * T, D)))
-        d = pol.dist(head, logstd)
-        if discrete:
-            lp = d.log_prob(torch.as_tensor(act.reshape(N * T)).long())
-        else:
-            lp = d.log_prob(torch.as_tensor(act.reshape(N * T, A))).sum(-1)
-    np.testing.assert_allclose(mem.values.cpu().numpy().reshape(-1), v.numpy(), rtol=1e-4, atol=1e-4)
-    if algo == "ppo":
-        np.testing.assert_allclose(mem.auxiliary_infos["old_logp"].cpu().numpy().reshape(-1), lp.numpy(),
-                                   rtol=1e-4, atol=2e-4)
-
-    # ---- bootstraps ----
-    term = mem.terminals.cpu().numpy()
-    closed = mem.closed.cpu().numpy().astype(bool)
-    boot = mem.boot.cpu().numpy()
-    with torch.no_grad():
-        v_last = pol.heads(torch.as_tensor(agent.boot_obs.cpu().numpy().astype(np.float64)))[2].numpy()
-        v_slot = pol.heads(torch.as_tensor(agent.slot_obs.cpu().numpy().astype(np.float64)))[2].numpy()
-    np.testing.assert_allclose(boot[:, T - 1], np.where(term[:, T - 1] != 0, 0.0, v_last), rtol=1e-4, atol=1e-4)
-    mid = closed[:, :T - 1] & (term[:, :T - 1] == 0)
-    rows, cols = np.nonzero(mid)
-    if not discrete:   # (the discrete SynthBox terminates its episodes well before the time limit)
-        assert len(rows) > 0, "the case must exercise mid-buffer truncation bootstraps"
-    assert len(np.unique(rows)) == len(rows)   # at most one per rollout (deferred path)
-    np.testing.assert_allclose(boot[rows, cols], v_slot[rows], rtol=1e-4, atol=1e-4)
-
-    # ---- GAE (north_star: 1e-5 on advantages / returns) ----
-    adv, ret = cpu_ref.gae_rows(mem.rewards.cpu().numpy(), mem.values.cpu().numpy(), term, closed.astype(np.uint8),
-                                boot, 0.99, 0.95)
-    np.testing.assert_allclose(mem.advantages.cpu().numpy(), adv, rtol=1e-5, atol=1e-5)
-    np.testing.assert_allclose(mem.returns.cpu().numpy(), ret, rtol=1e-5, atol=1e-5)
-
-    # ---- updates: the oracle learner replays the buffer with the device permutations ----
-    pol.float()
-    cfg = agent.config
-    opt = torch.optim.Adam(pol.parameters(), cfg.learning_rate, eps=1e-5)
-    sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.0, total_iters=cfg.running_steps)
-    # continue from the agent's Adam moments and LinearLR position (it steps once per update,
-    # ppoclip_learner.py:50-51)
-    named = dict(pol.named_parameters())
-    for n, st in opt_state.items():
-        opt.state[named[n]] = {"step": torch.tensor(float(st["step"])), "exp_avg": st["exp_avg"].float().clone(),
-                               "exp_avg_sq": st["exp_avg_sq"].float().clone()}
-    opt.param_groups[0]["lr"] = lr0
-    sch.last_epoch = sched_epoch
-    clip = cfg.clip_grad_norm if algo == "ppo" else cfg.clip_grad
-    lrn = cpu_ref.LearnerRef(pol, opt, sch, algo, cfg.vf_coef, ent, getattr(cfg, "clip_range", 0.2), clip, True)
-    buf = cpu_ref.BufferRef((D,), () if discrete else (A,), {"old_logp": ()} if algo == "ppo" else {}, N, T)
-    buf.observations[:] = mem.observations.cpu().numpy()
-    buf.actions[:] = mem.actions.cpu().numpy()
-    buf.values[:] = mem.values.cpu().numpy()
-    buf.returns[:], buf.advantages[:] = ret, adv
-    if algo == "ppo":
-        buf.auxiliary_infos["old_logp"][:] = mem.auxiliary_infos["old_logp"].cpu().numpy()
-    buf.size = T
-    B = N * T // n_mb
-    assert len(agent.update_log) == n_epoch * n_mb
-    u = 0
-    for e in range(n_epoch):
-        perm = agent.epoch_permutation(N * T, counter=perm_counter + e).cpu().numpy()
-        for s in range(0, N * T, B):
-            o, a, r, _, ad, ax = buf.sample(perm[s:s + B])
-            info = lrn.update(o, a, r, ad, ax.get("old_logp"))
-            got = agent.update_log[u].cpu().numpy()   # ops.OUT_KEYS order
-            ref_loss = info["actor-loss"] - ent * info["entropy"] + cfg.vf_coef * info["critic-loss"]
-            assert abs(got[3] - ref_loss) < 1e-4, ("loss", u, got[3], ref_loss)
-            for j, k in enumerate(("actor-loss", "critic-loss", "entropy")):
-                assert abs(got[j] - info[k]) < 1e-4 * max(1.0, abs(info[k])), (k, u, got[j], info[k])
-            assert abs(got[5] - info["predict_value"]) < 1e-4 * max(1.0, abs(info["predict_value"]))
-            if algo == "ppo":
-                assert abs(got[4] - info["clip_ratio"]) <= 2.0 / B + 1e-7, ("clip_ratio", u, got[4], info["clip_ratio"])
-            u += 1
-    for k, val in agent.policy.state_dict().items():
-        np.testing.assert_allclose(val.detach().cpu().numpy(), pol.state_dict()[k].numpy(), rtol=1e-3, atol=1e-4,
-                                   err_msg=k)
+    replay_last_step_iteration(agent, D, A, [H], discrete, algo, ent, n_epoch, n_mb, expect_mid_truncations=not discrete)

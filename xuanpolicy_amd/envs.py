@@ -273,3 +273,108 @@ class SynthAtariVecEnv:
 
     def close(self):
         pass
+
+
+# ---- CartPole-v1 (BASELINE.json configs[0]) -------------------------------------------------------------------
+SALT_CARTPOLE = 0xCA27B01E
+
+
+def cartpole_reset_states(seed, env_ids, episodes):
+    """uniform(-0.05, 0.05) per dim from the counter hash (f32-exact uniform, then f64), as K18 draws them."""
+    e = np.asarray(env_ids, np.uint32)[:, None]
+    ep = np.asarray(episodes, np.uint32)[:, None]
+    d = np.arange(4, dtype=np.uint32)[None, :]
+    return _u01(_hash4(seed ^ SALT_CARTPOLE, e, ep, d)).astype(np.float64) * 0.1 - 0.05
+
+
+class CartPoleVecEnv:
+    """n_envs CartPole-v1 envs resident on one GPU (K18 xpa_cartpole_step, csrc/classic.hip): gym 0.26.2's
+    dynamics with TimeLimit(500), f64 state, f32 observations, Discrete(2) actions read from the one-hot env
+    input the rollout kernels write.  Same interface as SynthBoxVecEnv (obs, act_in, final_obs, rew / term /
+    trunc, step_device(), host step() with DummyVecEnv_Gym's contract).  CPU checker:
+    oracle/synth_env.CartPoleEnv."""
+
+    def __init__(self, n_envs, seed=1, max_episode_steps=500, device=None, shard=0):
+        self.num_envs, self.seed, self.max_episode_steps = int(n_envs), int(seed), int(max_episode_steps)
+        self.max_episode_length = self.max_episode_steps
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.shard = int(shard)
+        self.noise_seed = (self.seed ^ ((0x9E3779B9 * self.shard) & 0xFFFFFFFF)) & 0xFFFFFFFF
+        self.observation_space = _Box((4,))
+        self.observation_space.low = np.full(4, -np.inf, np.float32)
+        self.observation_space.high = np.full(4, np.inf, np.float32)
+        self.action_space = _Discrete(2)
+        dev, N = self.device, self.num_envs
+        self.state = torch.zeros((N, 4), dtype=torch.float64, device=dev)
+        self._obs = torch.zeros((N, 4), dtype=torch.float32, device=dev)
+        self._act = torch.zeros((N, 2), dtype=torch.float32, device=dev)
+        self.final_obs = torch.zeros((N, 4), dtype=torch.float32, device=dev)
+        self.rew = torch.zeros((N,), dtype=torch.float32, device=dev)
+        self.term = torch.zeros((N,), dtype=torch.uint8, device=dev)
+        self.trunc = torch.zeros((N,), dtype=torch.uint8, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.ep_step, self.ep_index, self.ep_last_len = (torch.zeros((N,), **i32) for _ in range(3))
+        self.ep_score = torch.zeros((N,), dtype=torch.float32, device=dev)
+        self.ep_last_score = torch.zeros((N,), dtype=torch.float32, device=dev)
+        self.reset()
+
+    @property
+    def obs(self):
+        return self._obs
+
+    @property
+    def act_in(self):
+        """Env action input [N, 2]: the one-hot of the sampled action (K3 / K14 write it)."""
+        return self._act
+
+    @property
+    def buf_obs(self):
+        return self._obs
+
+    def reset(self):
+        s0 = cartpole_reset_states(self.noise_seed, np.arange(self.num_envs), np.zeros(self.num_envs))
+        self.state.copy_(torch.as_tensor(s0, device=self.device))
+        self._obs.copy_(self.state.float())
+        for t in (self.ep_step, self.ep_index, self.ep_score, self.ep_last_score, self.ep_last_len, self.rew,
+                  self.term, self.trunc):
+            t.zero_()
+        return self._obs.clone(), [{} for _ in range(self.num_envs)]
+
+    def fusable_with_policy_step(self, dist):
+        return False
+
+    def step_device(self):
+        rc = ops.lib().xpa_cartpole_step(self.num_envs, ops._p(self._act), self._act.stride(0), ops._p(self.state),
+                                         ops._p(self._obs), self._obs.stride(0), ops._p(self.final_obs),
+                                         ops._p(self.rew), ops._p(self.term), ops._p(self.trunc),
+                                         ops._p(self.ep_step), ops._p(self.ep_index), ops._p(self.ep_score),
+                                         ops._p(self.ep_last_score), ops._p(self.ep_last_len), self.noise_seed,
+                                         self.max_episode_steps, ops._stream(self.device))
+        _lib.check(rc, "xpa_cartpole_step")
+
+    def step(self, actions):
+        """VecEnv contract (gym_vec_env.py:201-212): host copies of (obs, rew, term, trunc, infos)."""
+        a = torch.as_tensor(np.asarray(actions) if not isinstance(actions, torch.Tensor) else actions,
+                            device=self.device).long().reshape(-1, 1)
+        self._act.zero_()
+        self._act.scatter_(1, a, 1.0)
+        self.step_device()
+        obs = self.final_obs.cpu().numpy()
+        rew = self.rew.cpu().numpy()
+        term = self.term.cpu().numpy().astype(bool)
+        trunc = self.trunc.cpu().numpy().astype(bool)
+        nxt = self._obs.cpu().numpy()
+        lens, scores = self.ep_step.cpu().numpy(), self.ep_score.cpu().numpy()
+        last_len, last_score = self.ep_last_len.cpu().numpy(), self.ep_last_score.cpu().numpy()
+        infos = []
+        for i in range(self.num_envs):
+            done = term[i] or trunc[i]
+            info = {"episode_step": int(last_len[i] if done else lens[i]),
+                    "episode_score": float(last_score[i] if done else scores[i])}
+            if done:
+                info["reset_obs"] = nxt[i].copy()
+            infos.append(info)
+        return obs, rew, term, trunc, infos
+
+    def close(self):
+        pass

@@ -17,7 +17,7 @@ import torch
 import yaml
 
 from . import agents
-from .envs import SynthAtariVecEnv, SynthBoxVecEnv
+from .envs import CartPoleVecEnv, SynthAtariVecEnv, SynthBoxVecEnv
 from .policies import (AC_CNN_Atari, ActivationFunctions, Basic_MLP, REGISTRY as REGISTRY_Policy,
                        REGISTRY_Representation)
 
@@ -80,11 +80,16 @@ def make_envs(config, device=None, shard=0):
         return SynthBoxVecEnv(config.parallels, config.obs_dim, config.act_dim, seed=config.seed,
                               discrete=bool(getattr(config, "discrete", False)),
                               max_episode_steps=getattr(config, "max_episode_steps", 1000), device=device, shard=shard)
+    if config.env_name == "Classic Control" and str(getattr(config, "env_id", "")) == "CartPole-v1":
+        return CartPoleVecEnv(config.parallels, seed=config.seed, max_episode_steps=getattr(config, "max_episode_steps",
+                                                                                            500),
+                              device=device, shard=shard)
     if config.env_name == "Atari" and str(getattr(config, "env_id", "")).startswith("SynthAtari"):
         return SynthAtariVecEnv(config.parallels, getattr(config, "n_actions", 6), seed=config.seed,
                                 max_episode_steps=getattr(config, "max_episode_steps", 27000), device=device,
                                 shard=shard)
-    raise NotImplementedError("env_name %r: only the device-resident SynthBox / SynthAtari envs are built in; pass "
+    raise NotImplementedError("env_name %r: only the device-resident SynthBox / SynthAtari / CartPole-v1 envs are "
+                              "built in; pass "
                               "any VecEnv with the reference's step contract to the agent directly" % config.env_name)
 
 
@@ -144,6 +149,19 @@ def build_synthbox_ppo(n_envs=4096, n_steps=128, obs_dim=17, act_dim=6, hidden=2
     cfg.parallels, cfg.n_steps, cfg.obs_dim, cfg.act_dim = n_envs, n_steps, obs_dim, act_dim
     cfg.n_epoch, cfg.n_minibatch, cfg.seed, cfg.discrete = n_epoch, n_minibatch, seed, discrete
     cfg.policy = "Categorical_AC" if discrete else "Gaussian_AC"
+    cfg.representation_hidden_size = cfg.actor_hidden_size = cfg.critic_hidden_size = [hidden]
+    for k, v in overrides.items():
+        setattr(cfg, k, v)
+    torch.manual_seed(seed)
+    return build_agent(cfg, device)
+
+
+def build_cartpole_ppo(n_envs=8, n_steps=128, hidden=64, seed=1, device="cuda:0", **overrides):
+    """The BASELINE.json C1 configuration: PPO-Clip on CartPole-v1 (ppo/classic_control/CartPole-v1.yaml keys),
+    8 envs x 128 steps, [64] hidden layers for the representation, actor and critic (SURVEY.md §8(d) reading of
+    "MLP[64,64]")."""
+    cfg = get_arguments("ppo", "classic_control", "CartPole-v1")
+    cfg.parallels, cfg.n_steps, cfg.seed = n_envs, n_steps, seed
     cfg.representation_hidden_size = cfg.actor_hidden_size = cfg.critic_hidden_size = [hidden]
     for k, v in overrides.items():
         setattr(cfg, k, v)
