@@ -203,6 +203,16 @@ int xpa_cartpole_step(int64_t n_envs, const float *act_in, int64_t ld_act, doubl
                       int32_t *ep_step, uint32_t *ep_index, float *ep_score, float *ep_last_score,
                       int32_t *ep_last_len, uint32_t seed, int32_t max_episode_steps, xpa_stream_t stream);
 
+/* K19 — PER-DQN TD target, loss, gradient and priorities (BASELINE.json configs[4]; replaces the tensor algebra
+ * of PerDQN_Learner.update, xuance/torch/learners/qlearning_family/perdqn_learner.py:23-30, 48).
+ * y = rew + (gamma * (1 - term)) * max_a targetQ[b, a]; p = evalQ[b, act[b]]; dQ[b, :] = one-hot(act[b]) * 2 (p - y) / B
+ * (d mse / d evalQ); td_abs[b] = |y - p| (the new priorities for xpa_per_update_priorities);
+ * scalars[0] = mean((p - y)^2) (Qloss), scalars[1] = mean(p) (predictQ).  act: float-coded indices; out-of-range
+ * ones are clamped and counted into *err (may be NULL).  One block; deterministic. */
+int xpa_dqn_td_loss(int64_t batch, int64_t n_actions, const float *evalQ, int64_t ld_eval, const float *targetQ,
+                    int64_t ld_tgt, const float *act, const float *rew, const float *term, float gamma, float *dQ,
+                    int64_t ld_dq, float *td_abs, float *scalars, int32_t *err, xpa_stream_t stream);
+
 /* K8 — rollout post-step bookkeeping.  Replaces, per step, DummyOnPolicyBuffer.store of
  * rewards/terminals (memory_tools.py:196-204) with reward normalisation (agent.py:118-123), the
  * return tracker and ret_rms update (ppoclip_agent.py:87-92 with the (1-term) mask; a2c_agent.py:84

@@ -16,6 +16,10 @@ Each piece cites the reference code it restates (paths relative to /root/referen
                        xuance/torch/representations/mlp.py:21-51, xuance/torch/utils/layers.py:8-24
   LearnerRef           ppoclip_learner.py:24-65, a2c_learner.py:19-50
   AgentLoopRef         ppoclip_agent.py:59-111, a2c_agent.py:57-107, xuance/torch/agents/agent.py:104-123
+  build_qnetwork_ref   xuance/torch/policies/deterministic.py:6-25 (BasicQhead), 148-182 (BasicQnetwork),
+                       xuance/torch/representations/cnn.py:5-40 (Basic_CNN)
+  dqn_td_ref           xuance/torch/learners/qlearning_family/perdqn_learner.py:23-30 (closed form)
+  PerDQNLearnerRef     perdqn_learner.py:17-48
 """
 import ctypes
 import math
@@ -568,3 +572,111 @@ class AgentLoopRef:
                         self.memory.finish_path(bv[i], i)
                     obs[i] = infos[i]["reset_obs"]
         self.obs = obs
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# PER-DQN (BASELINE.json configs[4]).
+def build_qnetwork_ref(n_actions, filters, kernels, strides, q_hidden, in_shape=(84, 84, 4)):
+    """BasicQnetwork over Basic_CNN with the reference's module layout / state_dict keys
+    (representation.model.*, target_representation.model.*, eval_Qhead.model.*, target_Qhead.model.*)."""
+    import copy
+    torch = _torch()
+    nn = torch.nn
+
+    class BasicCNNRef(nn.Module):   # cnn.py:5-40: conv blocks (padding (k - s) // 2) + ReLU, global max pool
+        def __init__(self):
+            super().__init__()
+            layers, (C, H, W) = [], (in_shape[2], in_shape[0], in_shape[1])
+            for k, st, f in zip(kernels, strides, filters):
+                pad = int((k - st) // 2)
+                layers += [nn.Conv2d(C, f, k, st, padding=pad), nn.ReLU()]
+                C = f
+            layers += [nn.AdaptiveMaxPool2d((1, 1)), nn.Flatten()]
+            self.model = nn.Sequential(*layers)
+
+        def forward(self, obs):   # obs / 255.0 on the host (f64), NHWC -> NCHW, float32
+            x = torch.as_tensor(np.transpose(np.asarray(obs) / 255.0, (0, 3, 1, 2)), dtype=torch.float32)
+            return {"state": self.model(x)}
+
+    class QheadRef(nn.Module):    # deterministic.py:6-25
+        def __init__(self):
+            super().__init__()
+            layers, d = [], filters[-1]
+            for h in q_hidden:
+                layers += [nn.Linear(d, h), nn.ReLU()]
+                d = h
+            layers += [nn.Linear(d, n_actions)]
+            self.model = nn.Sequential(*layers)
+
+        def forward(self, x):
+            return self.model(x)
+
+    class QnetRef(nn.Module):     # deterministic.py:148-182
+        def __init__(self):
+            super().__init__()
+            self.representation = BasicCNNRef()
+            self.target_representation = copy.deepcopy(self.representation)
+            self.eval_Qhead = QheadRef()
+            self.target_Qhead = copy.deepcopy(self.eval_Qhead)
+
+        def forward(self, obs):
+            q = self.eval_Qhead(self.representation(obs)["state"])
+            return None, q.argmax(dim=-1), q
+
+        def target(self, obs):
+            q = self.target_Qhead(self.target_representation(obs)["state"])
+            return None, q.argmax(dim=-1).detach(), q.detach()
+
+        def copy_target(self):
+            for ep, tp in zip(self.representation.parameters(), self.target_representation.parameters()):
+                tp.data.copy_(ep)
+            for ep, tp in zip(self.eval_Qhead.parameters(), self.target_Qhead.parameters()):
+                tp.data.copy_(ep)
+
+    return QnetRef()
+
+
+def dqn_td_ref(evalQ, targetQ, act, rew, term, gamma):
+    """perdqn_learner.py:23-30 in closed form (f32 numpy, torch's operation order):
+    y = rew + (gamma * (1 - term)) * max_a' targetQ,  p = evalQ[act],  loss = mean((p - y)^2),
+    d loss / d evalQ = 2 (p - y) / B at (b, act_b), |TD| = |y - p|."""
+    evalQ, targetQ = np.asarray(evalQ, np.float32), np.asarray(targetQ, np.float32)
+    a = np.asarray(act).astype(np.int64)
+    B = evalQ.shape[0]
+    y = np.asarray(rew, np.float32) + (np.float32(gamma) * (np.float32(1) - np.asarray(term, np.float32))) * \
+        targetQ.max(-1)
+    p = evalQ[np.arange(B), a]
+    d = (p - y).astype(np.float32)
+    dq = np.zeros_like(evalQ)
+    dq[np.arange(B), a] = np.float32(2.0) * d / np.float32(B)
+    return float(np.mean(d.astype(np.float64) ** 2)), np.abs(y - p).astype(np.float32), dq, float(p.mean())
+
+
+class PerDQNLearnerRef:
+    """perdqn_learner.py:17-48 on torch CPU: TD target from the target network, MSE, Adam, LinearLR, hard target
+    copy every sync_frequency updates; returns (|TD error|, info)."""
+
+    def __init__(self, policy, optimizer, scheduler, gamma=0.99, sync_frequency=100):
+        self.policy, self.optimizer, self.scheduler = policy, optimizer, scheduler
+        self.gamma, self.sync_frequency, self.iterations = gamma, sync_frequency, 0
+
+    def update(self, obs, act, rew, nxt, term):
+        torch = _torch()
+        self.iterations += 1
+        act, rew, term = torch.as_tensor(act), torch.as_tensor(rew), torch.as_tensor(term)
+        _, _, evalQ = self.policy(obs)
+        _, _, targetQ = self.policy.target(nxt)
+        targetQ = rew + self.gamma * (1 - term) * targetQ.max(dim=-1).values
+        predictQ = (evalQ * torch.nn.functional.one_hot(act.long(), evalQ.shape[1])).sum(dim=-1)
+        td = targetQ - predictQ
+        loss = torch.nn.functional.mse_loss(predictQ, targetQ)
+        self.optimizer.zero_grad()
+        loss.backward()
+        self.optimizer.step()
+        if self.scheduler is not None:
+            self.scheduler.step()
+        if self.iterations % self.sync_frequency == 0:
+            self.policy.copy_target()
+        info = {"Qloss": loss.item(), "learning_rate": self.optimizer.param_groups[0]["lr"],
+                "predictQ": predictQ.mean().item()}
+        return np.abs(td.detach().numpy()), info

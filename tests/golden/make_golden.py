@@ -22,6 +22,10 @@ Fixtures:
                       (oracle/synth_env.py; life losses keep the path open, game overs truncate).  Frames are
                       NOT stored: the test regenerates them by stepping the oracle env with the recorded
                       actions and checks them against the recorded per-step frame sums.
+  perdqn.npz   G9     PerDQN_Learner.update (perdqn_learner.py:17-48) on BasicQnetwork (deterministic.py:148-182)
+                      over a small Basic_CNN (cnn.py:5-40): 4 updates, sync_frequency 2 (target copies),
+                      uint8 4x84x84 batches regenerated from a recorded numpy seed (PCG64), 18 actions:
+                      |TD error| per sample, the info dict, and the parameters after every update.
   per.npz      G6     PerOffPolicyBuffer (memory_tools.py:369-492) + Sum/MinSegmentTree (segtree_tool.py):
                       store / sample(beta) / update_priorities rounds with every uniform random.random()
                       returned to the sampler recorded, the trees after every call, max priorities, the
@@ -453,6 +457,54 @@ def capture_atari(N=4, T=16, iters=2, max_ep=20, n_actions=6, seed=5):
           int(out["term"].sum()))
 
 
+# ----------------------------------------------------------------------------------------------
+PERDQN_NET = dict(filters=[8, 8], kernels=[8, 4], strides=[4, 2], q_hidden=[32])
+
+
+def perdqn_batch(seed, k, B, A):
+    """The k-th update's inputs, regenerated identically by the test (numpy PCG64 is stable)."""
+    rng = np.random.default_rng(seed * 1000 + k)
+    obs = rng.integers(0, 256, (B, 84, 84, 4), dtype=np.uint8)
+    nxt = rng.integers(0, 256, (B, 84, 84, 4), dtype=np.uint8)
+    act = rng.integers(0, A, B).astype(np.float32)
+    rew = rng.normal(0, 1, B).astype(np.float32)
+    term = (rng.random(B) < 0.2).astype(np.float32)
+    return obs, act, rew, nxt, term
+
+
+def capture_perdqn(B=32, A=18, n_updates=4, seed=9, sync=2, gamma=0.99):
+    from xuance.torch.representations import Basic_CNN
+    from xuance.torch.policies import BasicQnetwork
+    from xuance.torch.learners import PerDQN_Learner
+    torch.manual_seed(seed)
+    rep = Basic_CNN((84, 84, 4), PERDQN_NET["kernels"], PERDQN_NET["strides"], PERDQN_NET["filters"], None,
+                    torch.nn.init.orthogonal_, torch.nn.ReLU, "cpu")
+    policy = BasicQnetwork(gym.spaces.Discrete(A), rep, PERDQN_NET["q_hidden"], None, torch.nn.init.orthogonal_,
+                           torch.nn.ReLU, "cpu")
+    out = {}
+    _sd("sd0/", policy, out)
+    opt = torch.optim.Adam(policy.parameters(), 1e-3, eps=1e-5)
+    sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.5, total_iters=10)
+    lrn = PerDQN_Learner(policy, opt, sch, "cpu", "./", gamma, sync)
+    tds, infos, sums = [], [], []
+    for k in range(n_updates):
+        obs, act, rew, nxt, term = perdqn_batch(seed, k, B, A)
+        sums.append([int(obs.astype(np.int64).sum()), int(nxt.astype(np.int64).sum())])
+        td, info = lrn.update(obs, act, rew, nxt, term)
+        tds.append(np.asarray(td, np.float32))
+        infos.append([float(info["Qloss"]), float(info["learning_rate"]), float(info["predictQ"])])
+        _sd("sd%d/" % (k + 1), policy, out)
+    out["td_abs"] = np.stack(tds)
+    out["infos"] = np.asarray(infos, np.float64)
+    out["input_sums"] = np.asarray(sums, np.int64)
+    out["config"] = np.asarray([B, A, n_updates, seed, sync], np.int64)
+    out["gamma"] = np.asarray(gamma, np.float64)
+    out["net"] = np.asarray(PERDQN_NET["filters"] + PERDQN_NET["kernels"] + PERDQN_NET["strides"]
+                            + PERDQN_NET["q_hidden"], np.int64)
+    np.savez_compressed(os.path.join(HERE, "perdqn.npz"), **out)
+    print("perdqn.npz", len(out))
+
+
 if __name__ == "__main__":
     os.makedirs("/tmp/xref_run", exist_ok=True)
     os.chdir("/tmp/xref_run")
@@ -463,3 +515,4 @@ if __name__ == "__main__":
     capture_rms()
     capture_per()
     capture_atari()
+    capture_perdqn()

@@ -1,0 +1,106 @@
+"""GPU: C5 (BASELINE.json configs[4]) — PER-DQN on device.
+
+  * K19 (xpa_dqn_td_loss) against the oracle's closed form (oracle/cpu_ref.dqn_td_ref, perdqn_learner.py:23-30);
+  * G9: the reference's PerDQN_Learner.update (4 updates, target copies every 2) replayed through the device
+    PerDQN_Learner (BasicQnetwork over Basic_CNN on MIOpen / hipBLASLt + K19): |TD|, info, parameters;
+  * the device PerDQN_Agent loop (K15 SynthAtari env with 18 actions, K6 store / sample / priority update,
+    K4 uint8 frame gathers) runs and keeps its trees consistent."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cpu_ref
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _setup():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.mark.parametrize("B,A", [(2048, 18), (3, 2), (1500, 7)])
+def test_dqn_td_kernel_matches_oracle(B, A):
+    from xuanpolicy_amd import ops
+    rng = np.random.default_rng(B + A)
+    eq = rng.normal(0, 1, (B, A)).astype(np.float32)
+    tq = rng.normal(0, 1, (B, A)).astype(np.float32)
+    tq[::5, 0] = tq[::5].max(1)        # ties in the max
+    act = rng.integers(0, A, B).astype(np.float32)
+    rew = rng.normal(0, 1, B).astype(np.float32)
+    term = (rng.random(B) < 0.3).astype(np.float32)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    dq, td, sc = ops.dqn_td_loss(torch.as_tensor(eq, device=DEV), torch.as_tensor(tq, device=DEV),
+                                 torch.as_tensor(act, device=DEV), torch.as_tensor(rew, device=DEV),
+                                 torch.as_tensor(term, device=DEV), 0.99, err=err)
+    loss, rtd, rdq, pq = cpu_ref.dqn_td_ref(eq, tq, act, rew, term, 0.99)
+    np.testing.assert_array_equal(td.cpu().numpy(), rtd)            # f32 element ops in the same order: exact
+    np.testing.assert_allclose(dq.cpu().numpy(), rdq, rtol=1e-6, atol=0)
+    s = sc.cpu().numpy()
+    assert abs(s[0] - loss) <= 1e-6 * max(1.0, loss) and abs(s[1] - pq) <= 1e-6 * max(1.0, abs(pq))
+    assert int(err) == 0
+    bad = torch.as_tensor(act, device=DEV).clone()
+    bad[0], bad[1] = -1.0, float(A)                                 # out of range: clamped and counted
+    ops.dqn_td_loss(torch.as_tensor(eq, device=DEV), torch.as_tensor(tq, device=DEV), bad,
+                    torch.as_tensor(rew, device=DEV), torch.as_tensor(term, device=DEV), 0.99, err=err)
+    assert int(err) == 2
+
+
+def _perdqn_batch(seed, k, B, A):
+    rng = np.random.default_rng(seed * 1000 + k)
+    obs = rng.integers(0, 256, (B, 84, 84, 4), dtype=np.uint8)
+    nxt = rng.integers(0, 256, (B, 84, 84, 4), dtype=np.uint8)
+    act = rng.integers(0, A, B).astype(np.float32)
+    rew = rng.normal(0, 1, B).astype(np.float32)
+    term = (rng.random(B) < 0.2).astype(np.float32)
+    return obs, act, rew, nxt, term
+
+
+def test_perdqn_learner_replays_reference(golden):
+    from xuanpolicy_amd.learners import PerDQN_Learner
+    from xuanpolicy_amd.policies import BasicQnetwork, Basic_CNN
+    g = golden("perdqn.npz")
+    B, A, n_up, seed, sync = (int(x) for x in g["config"])
+    net = [int(x) for x in g["net"]]
+    nl = (len(net) - 1) // 3
+
+    class Disc:
+        n, shape = A, ()
+    rep = Basic_CNN((84, 84, 4), net[nl:2 * nl], net[2 * nl:3 * nl], net[:nl], None, None, torch.nn.ReLU, DEV)
+    pol = BasicQnetwork(Disc(), rep, net[3 * nl:], None, None, torch.nn.ReLU, DEV)
+    pol.load_state_dict({k[4:]: torch.as_tensor(v) for k, v in g.items() if k.startswith("sd0/")})
+    opt = torch.optim.Adam(pol.parameters(), 1e-3, eps=1e-5)
+    sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.5, total_iters=10)
+    lrn = PerDQN_Learner(pol, opt, sch, DEV, "./", float(g["gamma"]), sync)
+    for k in range(n_up):
+        obs, act, rew, nxt, term = _perdqn_batch(seed, k, B, A)
+        td, info = lrn.update(torch.as_tensor(obs, device=DEV), act, rew, torch.as_tensor(nxt, device=DEV), term)
+        assert td.device.type == "cuda" and td.dtype == torch.float32
+        np.testing.assert_allclose(td.cpu().numpy(), g["td_abs"][k], rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose([info["Qloss"], info["learning_rate"], info["predictQ"]], g["infos"][k],
+                                   rtol=1e-4, atol=1e-6)
+        for key, v in pol.state_dict().items():
+            np.testing.assert_allclose(v.cpu().numpy(), g["sd%d/%s" % (k + 1, key)], rtol=1e-3, atol=1e-5,
+                                       err_msg=key)
+
+
+def test_perdqn_agent_loop_on_device():
+    from xuanpolicy_amd.runner import build_perdqn
+    agent = build_perdqn(n_envs=4, n_size=256, batch_size=64, device=DEV, start_training=64, sync_frequency=20,
+                         filters=[8, 8], kernels=[8, 4], strides=[4, 2], q_hidden_size=[32], max_episode_steps=40)
+    assert agent.device_env and agent.memory.observations.dtype == torch.uint8
+    assert agent.envs.action_space.n == 18
+    agent.train(80, sync_info=True)
+    torch.cuda.synchronize()
+    assert agent.memory.size == 80 and len(agent.infos) > 0
+    for info in agent.infos:
+        assert np.isfinite([info["Qloss"], info["predictQ"]]).all()
+    assert agent.learner.iterations == len(agent.infos)
+    # the sum tree's root equals the sum of its leaves (p_i^alpha of every stored transition), every env
+    cap = agent.memory.capacity
+    st = agent.memory.sum_tree.cpu().numpy()
+    np.testing.assert_allclose(st[:, 1], st[:, cap:].sum(1), rtol=1e-12)
+    assert (st[:, cap:cap + 80] > 0).all() and (st[:, cap + 80:] == 0).all()
+    assert 0.4 < agent.PER_beta <= 1.0 and agent.egreedy < agent.start_greedy

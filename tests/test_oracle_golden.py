@@ -196,3 +196,44 @@ def test_atari_fixture_frames_and_gae_from_oracle(golden):
         np.testing.assert_allclose(adv, g["adv"][it], rtol=1e-5, atol=1e-5)
         np.testing.assert_allclose(ret, g["ret"][it], rtol=1e-5, atol=1e-5)
     assert int(g["term"].sum()) > 0 and int(g["closed"].sum()) > 0
+
+
+def _perdqn_batch(seed, k, B, A):
+    """tests/golden/make_golden.py perdqn_batch: the k-th update's inputs (numpy PCG64 is stable)."""
+    rng = np.random.default_rng(seed * 1000 + k)
+    obs = rng.integers(0, 256, (B, 84, 84, 4), dtype=np.uint8)
+    nxt = rng.integers(0, 256, (B, 84, 84, 4), dtype=np.uint8)
+    act = rng.integers(0, A, B).astype(np.float32)
+    rew = rng.normal(0, 1, B).astype(np.float32)
+    term = (rng.random(B) < 0.2).astype(np.float32)
+    return obs, act, rew, nxt, term
+
+
+def test_perdqn_learner_ref_matches_reference(golden):
+    """G9 pins the oracle's PER-DQN learner (perdqn_learner.py:17-48 over BasicQnetwork / Basic_CNN): |TD|, the
+    info dict and the parameters after each of 4 updates (target copies every 2), and the closed-form TD / loss
+    gradient (dqn_td_ref) against the autograd learner."""
+    g = golden("perdqn.npz")
+    B, A, n_up, seed, sync = (int(x) for x in g["config"])
+    net = [int(x) for x in g["net"]]
+    nl = (len(net) - 1) // 3
+    pol = cpu_ref.build_qnetwork_ref(A, net[:nl], net[nl:2 * nl], net[2 * nl:3 * nl], net[3 * nl:])
+    pol.load_state_dict({k[4:]: torch.as_tensor(v) for k, v in g.items() if k.startswith("sd0/")})
+    opt = torch.optim.Adam(pol.parameters(), 1e-3, eps=1e-5)
+    sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.5, total_iters=10)
+    lrn = cpu_ref.PerDQNLearnerRef(pol, opt, sch, float(g["gamma"]), sync)
+    for k in range(n_up):
+        obs, act, rew, nxt, term = _perdqn_batch(seed, k, B, A)
+        assert [int(obs.astype(np.int64).sum()), int(nxt.astype(np.int64).sum())] == list(g["input_sums"][k])
+        with torch.no_grad():
+            eq = pol(obs)[2].numpy()
+            tq = pol.target(nxt)[2].numpy()
+        loss, td, dq, pq = cpu_ref.dqn_td_ref(eq, tq, act, rew, term, float(g["gamma"]))
+        td_l, info = lrn.update(obs, act, rew, nxt, term)
+        np.testing.assert_allclose(td, td_l, rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(td_l, g["td_abs"][k], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose([info["Qloss"], info["learning_rate"], info["predictQ"]], g["infos"][k],
+                                   rtol=1e-5, atol=1e-7)
+        assert abs(loss - info["Qloss"]) <= 1e-5 * max(1.0, loss)
+        for key, v in pol.state_dict().items():
+            np.testing.assert_allclose(v.numpy(), g["sd%d/%s" % (k + 1, key)], rtol=1e-5, atol=1e-6, err_msg=key)

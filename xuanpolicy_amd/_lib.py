@@ -17,7 +17,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "libxuanpolicy_amd.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
 SOURCES = ["gae.hip", "loss.hip", "rollout.hip", "optim.hip", "mlp.hip", "head.hip", "thin.hip", "per.hip", "atari.hip",
-           "classic.hip"]
+           "classic.hip", "dqn.hip"]
 HEADER = os.path.join(REPO_DIR, "include", "xuanpolicy_amd.h")
 
 ABI_VERSION = 1
@@ -54,6 +54,8 @@ SIGNATURES = {
                                          c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "xpa_cartpole_step": (ctypes.c_int, [c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                                          c_p, c_u32, c_i32, c_p]),
+    "xpa_dqn_td_loss": (ctypes.c_int, [c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_f32, c_p, c_i64, c_p, c_p,
+                                       c_p, c_p]),
     "xpa_rollout_post_num_blocks": (c_i64, [c_i64]),
     "xpa_rollout_post": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                                         c_f32, ctypes.c_int, ctypes.c_int, c_f32, ctypes.c_int, c_p, c_p, c_p]),

@@ -35,7 +35,7 @@ import torch
 
 from . import ops
 from .buffer import DummyOnPolicyBuffer, DummyOnPolicyBuffer_Atari
-from .learners import A2C_Learner, PPOCLIP_Learner
+from .learners import A2C_Learner, PerDQN_Learner, PPOCLIP_Learner
 from .policies import policy_heads, space_shape
 
 FLOAT_MAX = 3.0e38
@@ -557,7 +557,95 @@ class A2C_Agent(_OnPolicyAgent):
                            config.vf_coef, config.ent_coef, config.clip_grad)
 
 
-REGISTRY = {"PPO_Clip": PPOCLIP_Agent, "A2C": A2C_Agent}
+class PerDQN_Agent:
+    """perdqn_agent.py:4-95 (BASELINE.json configs[4]): e-greedy DQN with prioritized replay, device-resident.
+
+    Same constructor and train(train_steps) loop as the reference: each step stores (obs, act, rew, term, next)
+    in the PER buffer (K6 store: the new leaf at max priority), and every training_frequency steps after
+    start_training samples a batch (K6 sample: stratified prefix-sum descent + IS weights; K4 gathers the uint8
+    frames), runs PerDQN_Learner.update (Q forwards / backward on PyTorch-ROCm, K19 TD / loss / gradient /
+    priorities) and writes the |TD| priorities back (K6 update) without leaving the GPU.  PER_beta and the
+    e-greedy rate follow perdqn_agent.py:74-95.  With a device env (step_device / act_in, e.g. the SynthAtari
+    vec env with 18 actions) the loop never copies frames to the host; the coin flip of the e-greedy choice is
+    the reference's np.random draw (one host draw per step, no sync)."""
+
+    def __init__(self, config, envs, policy, optimizer, scheduler=None, device=None):
+        from .per import PerOffPolicyBuffer
+        self.config = config
+        self.envs = envs
+        self.policy = policy
+        self.device = torch.device(device if device is not None else _cfg(config, "device", "cuda:0"))
+        self.n_envs = envs.num_envs
+        self.gamma = config.gamma
+        self.train_frequency = config.training_frequency
+        self.start_training = config.start_training
+        self.start_greedy, self.end_greedy = config.start_greedy, config.end_greedy
+        self.egreedy = config.start_greedy
+        self.decay_step_greedy = _cfg(config, "decay_step_greedy", 1)
+        self.observation_space, self.action_space = envs.observation_space, envs.action_space
+        self.PER_beta0 = self.PER_beta = config.PER_beta0
+        self.atari = _cfg(config, "env_name", "") == "Atari"
+        obs_dtype = torch.uint8 if self.atari else torch.float32
+        self.memory = PerOffPolicyBuffer(self.observation_space, self.action_space, {}, self.n_envs, config.n_size,
+                                         config.batch_size, config.PER_alpha, device=self.device,
+                                         seed=_cfg(config, "seed", 1), obs_dtype=obs_dtype)
+        self.learner = PerDQN_Learner(policy, optimizer, scheduler, self.device, _cfg(config, "model_dir", "./"),
+                                      config.gamma, config.sync_frequency)
+        self.device_env = hasattr(envs, "step_device")
+        self.current_step = 0
+        self.current_episode = np.zeros(self.n_envs, np.int32)
+        self.infos = []
+
+    def _action(self, obs, egreedy=0.0):
+        """perdqn_agent.py:47-54: argmax of the eval Q row, or (with probability egreedy, one draw for all envs)
+        uniform random actions from np.random, as the reference draws them."""
+        with torch.no_grad():
+            _, argmax_action, _ = self.policy(obs)
+        random_action = np.random.choice(self.action_space.n, self.n_envs)
+        if np.random.rand() < egreedy:
+            return torch.as_tensor(random_action, device=self.device)
+        return argmax_action
+
+    def _env_step(self, acts):
+        """(next observation to store, rew, term, trunc); the observation the policy sees next is env.obs (device
+        env: the kernel already continued done envs from their reset state) or self._host_obs."""
+        env = self.envs
+        if self.device_env:
+            env.act_in.zero_()
+            env.act_in.scatter_(1, acts.long().reshape(-1, 1), 1.0)
+            env.step_device()
+            return env.final_obs, env.rew, env.term, env.trunc
+        nxt, rew, term, trunc, infos = env.step(acts.cpu().numpy())
+        self._host_obs = np.array(nxt, copy=True)
+        for i in range(self.n_envs):   # perdqn_agent.py:76-83: continue from reset_obs (not on an Atari life loss)
+            if (term[i] or trunc[i]) and not (self.atari and not trunc[i]):
+                self._host_obs[i] = infos[i]["reset_obs"]
+        return nxt, rew, term, trunc
+
+    def train(self, train_steps, sync_info=False):
+        """perdqn_agent.py:56-95."""
+        env = self.envs
+        if not self.device_env and not hasattr(self, "_host_obs"):
+            self._host_obs = np.array(env.buf_obs, copy=True)
+        for _ in range(train_steps):
+            obs = env.obs.clone() if self.device_env else self._host_obs
+            acts = self._action(obs, self.egreedy)
+            nxt, rew, term, trunc = self._env_step(acts)
+            self.memory.store(obs, acts, rew, term, nxt)
+            if self.current_step > self.start_training and self.current_step % self.train_frequency == 0:
+                o, a, r, d, n, w, idxes = self.memory.sample(self.PER_beta)
+                td_abs, info = self.learner.update(o, a, r, n, d, sync_info=sync_info)
+                self.memory.update_priorities(idxes, td_abs, check=False)
+                info["epsilon-greedy"] = self.egreedy
+                self.infos.append(info)
+            self.PER_beta += (1 - self.PER_beta0) / train_steps
+            self.egreedy = self.egreedy - (self.start_greedy - self.end_greedy) / train_steps
+            self.current_step += self.n_envs
+            if self.egreedy > self.end_greedy:
+                self.egreedy = self.egreedy - (self.start_greedy - self.end_greedy) / self.decay_step_greedy
+
+
+REGISTRY = {"PPO_Clip": PPOCLIP_Agent, "A2C": A2C_Agent, "PerDQN": PerDQN_Agent}
 Agent = _OnPolicyAgent
 
 

@@ -205,3 +205,50 @@ class A2C_Learner(_FusedPolicyGradient):
 
 
 REGISTRY = {"PPO_Clip": PPOCLIP_Learner, "A2C": A2C_Learner}
+
+
+class PerDQN_Learner(Learner):
+    """perdqn_learner.py:4-48 (same constructor, update(obs, act, rew, next, terminal) -> (|TD|, info)).
+
+    The Q-network forwards (eval on obs, target on next) and the backward stay in PyTorch-ROCm (MIOpen
+    convolutions, hipBLASLt GEMMs); the tensor algebra between them — TD target with max over the target Q row,
+    the gathered prediction, MSE, its gradient w.r.t. evalQ and the |TD| priorities — is K19 (xpa_dqn_td_loss,
+    one launch).  |TD| stays on the device (a float32 tensor the device PerOffPolicyBuffer.update_priorities
+    takes as it is); the reference returns a NumPy array.  Hard target copy every sync_frequency updates."""
+
+    def __init__(self, policy, optimizer, scheduler=None, device=None, model_dir="./", gamma=0.99,
+                 sync_frequency=100):
+        self.gamma = gamma
+        self.sync_frequency = sync_frequency
+        super().__init__(policy, optimizer, scheduler, device, model_dir)
+        self._err = None
+
+    def _f32(self, x, dev):
+        if isinstance(x, torch.Tensor):
+            return x.to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+        return torch.as_tensor(x, dtype=torch.float32, device=dev).reshape(-1).contiguous()
+
+    def update(self, obs_batch, act_batch, rew_batch, next_batch, terminal_batch, sync_info=True):
+        self.iterations += 1
+        _, _, evalQ = self.policy(obs_batch)
+        dev = evalQ.device
+        with torch.no_grad():
+            _, _, targetQ = self.policy.target(next_batch)
+        if self._err is None:
+            self._err = torch.zeros(1, dtype=torch.int32, device=dev)
+        dQ, td_abs, sc = ops.dqn_td_loss(evalQ.detach(), targetQ, self._f32(act_batch, dev), self._f32(rew_batch, dev),
+                                         self._f32(terminal_batch, dev), self.gamma, err=self._err)
+        self.optimizer.zero_grad()
+        evalQ.backward(dQ)
+        self.optimizer.step()
+        if self.scheduler is not None:
+            self.scheduler.step()
+        if self.iterations % self.sync_frequency == 0:
+            self.policy.copy_target()
+        lr = self.optimizer.param_groups[0]["lr"]
+        if not sync_info:   # the agent's hot loop: scalars stay on the device
+            return td_abs, {"Qloss": sc[0], "learning_rate": lr, "predictQ": sc[1]}
+        q = sc.cpu().tolist()
+        return td_abs, {"Qloss": q[0], "learning_rate": lr, "predictQ": q[1]}
+
+REGISTRY["PerDQN"] = PerDQN_Learner

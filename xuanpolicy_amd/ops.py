@@ -815,3 +815,24 @@ def bootstrap_fixup(values, slot_t, buf_term, buf_boot):
     _req(buf_boot, "buf_boot", torch.float32, (N, T))
     _lib.check(lib().xpa_rollout_bootstrap_fixup(N, T, _p(values), _p(slot_t), _p(buf_term), _p(buf_boot),
                                                  _stream(values.device)), "xpa_rollout_bootstrap_fixup")
+
+
+def dqn_td_loss(evalQ, targetQ, act, rew, term, gamma, dQ=None, td_abs=None, scalars=None, err=None):
+    """K19 (xpa_dqn_td_loss): the PER-DQN TD target / MSE loss / d loss d evalQ / |TD| of one batch
+    (perdqn_learner.py:23-30).  evalQ / targetQ [B, A] f32 (row-strided allowed), act / rew / term [B] f32.
+    Returns (dQ [B, A], td_abs [B], scalars [2] = (Qloss, predictQ mean)), all on device."""
+    B, A = evalQ.shape
+    ld_e = _row_stride(evalQ, "evalQ", A)
+    ld_t = _row_stride(targetQ, "targetQ", A)
+    for name, t in (("act", act), ("rew", rew), ("term", term)):
+        _req(t, name, torch.float32, (B,))
+    dQ = torch.empty((B, A), dtype=torch.float32, device=evalQ.device) if dQ is None else _req(dQ, "dQ",
+                                                                                               torch.float32, (B, A))
+    td_abs = torch.empty(B, dtype=torch.float32, device=evalQ.device) if td_abs is None else \
+        _req(td_abs, "td_abs", torch.float32, (B,))
+    scalars = torch.empty(2, dtype=torch.float32, device=evalQ.device) if scalars is None else \
+        _req(scalars, "scalars", torch.float32, (2,))
+    rc = lib().xpa_dqn_td_loss(B, A, _p(evalQ), ld_e, _p(targetQ), ld_t, _p(act), _p(rew), _p(term), float(gamma),
+                               _p(dQ), A, _p(td_abs), _p(scalars), _p(err), _stream(evalQ.device))
+    _lib.check(rc, "xpa_dqn_td_loss")
+    return dQ, td_abs, scalars

@@ -191,6 +191,80 @@ class AC_CNN_Atari(nn.Module):
         return {"state": self.model(x.permute(0, 3, 1, 2))}
 
 
+class Basic_CNN(nn.Module):
+    """cnn.py:5-40: conv blocks (padding (k - s) // 2, activation) + global max pool + flatten; state dim =
+    filters[-1].  Input uint8 [B, 84, 84, C] (NHWC): /255 and the NCHW view happen on device."""
+
+    def __init__(self, input_shape, kernels, strides, filters, normalize=None, initialize=None, activation=None,
+                 device=None):
+        super().__init__()
+        self.input_shape = (input_shape[2], input_shape[0], input_shape[1])
+        self.device = device
+        self.output_shapes = {"state": (filters[-1],)}
+        layers, shape = [], self.input_shape
+        for k, s, f in zip(kernels, strides, filters):
+            cnn, shape = cnn_block(shape, f, k, s, normalize, activation, initialize, device)
+            layers.extend(cnn)
+        layers.append(nn.AdaptiveMaxPool2d((1, 1)))
+        layers.append(nn.Flatten())
+        self.model = nn.Sequential(*layers)
+
+    def forward(self, observations):
+        x = _as_input(observations, self.device, dtype=torch.float32) / 255.0
+        return {"state": self.model(x.permute(0, 3, 1, 2))}
+
+
+class BasicQhead(nn.Module):
+    """deterministic.py:6-25."""
+
+    def __init__(self, state_dim, action_dim, hidden_sizes, normalize=None, initialize=None, activation=None,
+                 device=None):
+        super().__init__()
+        layers, shape = [], (state_dim,)
+        for h in hidden_sizes:
+            mlp, shape = mlp_block(shape[0], h, normalize, activation, initialize, device)
+            layers.extend(mlp)
+        layers.extend(mlp_block(shape[0], action_dim, None, None, None, device)[0])
+        self.model = nn.Sequential(*layers)
+
+    def forward(self, x):
+        return self.model(x)
+
+
+class BasicQnetwork(nn.Module):
+    """deterministic.py:148-182 (the same module names, so the reference's checkpoints load): an evaluation
+    network, a target network (deep copies), copy_target() for the hard update."""
+
+    def __init__(self, action_space, representation, hidden_size=None, normalize=None, initialize=None,
+                 activation=None, device=None):
+        super().__init__()
+        import copy
+        self.action_dim = action_space.n
+        self.representation = representation
+        self.target_representation = copy.deepcopy(representation)
+        self.representation_info_shape = self.representation.output_shapes
+        self.eval_Qhead = BasicQhead(self.representation.output_shapes["state"][0], self.action_dim,
+                                     hidden_size or [], normalize, initialize, activation, device)
+        self.target_Qhead = copy.deepcopy(self.eval_Qhead)
+
+    def forward(self, observation):
+        outputs = self.representation(observation)
+        evalQ = self.eval_Qhead(outputs["state"])
+        return outputs, evalQ.argmax(dim=-1), evalQ
+
+    def target(self, observation):
+        outputs = self.target_representation(observation)
+        targetQ = self.target_Qhead(outputs["state"])
+        return outputs, targetQ.argmax(dim=-1).detach(), targetQ.detach()
+
+    def copy_target(self):
+        with torch.no_grad():
+            for ep, tp in zip(self.representation.parameters(), self.target_representation.parameters()):
+                tp.copy_(ep)
+            for ep, tp in zip(self.eval_Qhead.parameters(), self.target_Qhead.parameters()):
+                tp.copy_(ep)
+
+
 class CategoricalDistribution:
     """distributions.py:39-66."""
 
@@ -344,8 +418,9 @@ class Categorical_AC_Policy(_ActorCritic):
         self.critic = _Critic(d, critic_hidden_size or [], normalize, initialize, activation, device, init_last=True)
 
 
-REGISTRY = {"Gaussian_AC": Gaussian_AC_Policy, "Categorical_AC": Categorical_AC_Policy}
-REGISTRY_Representation = {"Basic_Identical": Basic_Identical, "Basic_MLP": Basic_MLP, "AC_CNN_Atari": AC_CNN_Atari}
+REGISTRY = {"Gaussian_AC": Gaussian_AC_Policy, "Categorical_AC": Categorical_AC_Policy, "Basic_Q_network": BasicQnetwork}
+REGISTRY_Representation = {"Basic_Identical": Basic_Identical, "Basic_MLP": Basic_MLP, "AC_CNN_Atari": AC_CNN_Atari,
+                           "Basic_CNN": Basic_CNN}
 
 
 def policy_heads(policy, x):

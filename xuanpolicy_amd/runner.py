@@ -36,7 +36,7 @@ def get_config(path):
         return yaml.safe_load(f)
 
 
-FLAT_ENVS = ("atari", "mujoco", "Platform", "synthbox")   # <method>/<env>.yaml; others <method>/<env>/<env_id>.yaml
+FLAT_ENVS = ("atari", "mujoco", "Platform", "synthbox")  # perdqn/atari.yaml too   # <method>/<env>.yaml; others <method>/<env>/<env_id>.yaml
 
 
 def get_arguments(method, env, env_id, config_path=None, parser_args=None):
@@ -167,6 +167,28 @@ def build_cartpole_ppo(n_envs=8, n_steps=128, hidden=64, seed=1, device="cuda:0"
         setattr(cfg, k, v)
     torch.manual_seed(seed)
     return build_agent(cfg, device)
+
+
+def build_perdqn(n_envs=8, n_size=131072, batch_size=2048, seed=1, device="cuda:0", **overrides):
+    """The BASELINE.json C5 configuration: PER-DQN (perdqn/atari.yaml keys) on SynthAtari frames with 18 actions,
+    replay n_envs x n_size (8 x 131 072 = 1 M transitions), batch 2048, BasicQnetwork over Basic_CNN; Adam(eps=1e-5)
+    + LinearLR as runner_drl.py:71-76 builds them."""
+    from .agents import PerDQN_Agent
+    from .policies import BasicQnetwork, Basic_CNN
+    cfg = get_arguments("perdqn", "atari", "SynthAtari-v0")
+    cfg.parallels, cfg.n_size, cfg.batch_size, cfg.seed = n_envs, n_size, batch_size, seed
+    for k, v in overrides.items():
+        setattr(cfg, k, v)
+    cfg.device = str(device)
+    torch.manual_seed(seed)
+    envs = make_envs(cfg, device=device)
+    act = ActivationFunctions[cfg.activation]
+    rep = Basic_CNN(envs.observation_space.shape, cfg.kernels, cfg.strides, cfg.filters, None,
+                    torch.nn.init.orthogonal_, act, device)
+    policy = BasicQnetwork(envs.action_space, rep, cfg.q_hidden_size, None, torch.nn.init.orthogonal_, act, device)
+    opt = torch.optim.Adam(policy.parameters(), cfg.learning_rate, eps=1e-5)
+    sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.0, total_iters=cfg.running_steps)
+    return PerDQN_Agent(cfg, envs, policy, opt, sch, device)
 
 
 def build_atari_a2c(n_envs=1024, n_steps=128, seed=1, device="cuda:0", **overrides):
