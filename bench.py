@@ -338,6 +338,76 @@ def c1_bench(device, n_envs=8, n_steps=128, hidden=64, steps=5, warmup=1, cpu=Tr
     return res
 
 
+def c5_bench(device, n_envs=8, n_size=131072, batch=2048, steps=20, warmup=3, cpu_updates=3, tree_cpu_us=None):
+    """C5 (BASELINE.json configs[4]): the PER-DQN training step at full size — replay 8 x 131 072 = 1 M uint8
+    4x84x84 transitions (obs + next: 56 GB in HBM), batch 2048, 18 actions, BasicQnetwork over Basic_CNN
+    [32, 64, 64] / q_hidden [512] (perdqn/atari.yaml).  One step = one env step of the 8 envs + store (K6 store)
+    + sample (K6) + K4 frame gathers + eval / target Q forwards + K19 + backward + Adam + K6 priority update, the
+    agent loop with start_training = 0 and train_frequency 1 over a replay pre-filled to capacity (frames and
+    leaf priorities synthetic).  CPU leg: the restated reference learner (oracle PerDQNLearnerRef, torch CPU)
+    on `cpu_updates` batches of 2048 plus the reference's Python trees (oracle/per_ref) for the same calls."""
+    import numpy as np
+    import torch
+    from xuanpolicy_amd.runner import build_perdqn
+    agent = build_perdqn(n_envs=n_envs, n_size=n_size, batch_size=batch, device=device, start_training=0,
+                         sync_frequency=500)
+    mem = agent.memory
+    cap = mem.capacity
+    g = torch.Generator(device=device).manual_seed(0)
+    mem.sum_tree[:, cap:cap + n_size] = torch.rand((n_envs, n_size), generator=g, device=device,
+                                                   dtype=torch.float64) + 0.05
+    mem.min_tree[:, cap:cap + n_size] = mem.sum_tree[:, cap:cap + n_size]
+    lvl = cap
+    while lvl > 1:
+        half = lvl // 2
+        mem.sum_tree[:, half:lvl] = mem.sum_tree[:, lvl:2 * lvl:2] + mem.sum_tree[:, lvl + 1:2 * lvl:2]
+        mem.min_tree[:, half:lvl] = torch.minimum(mem.min_tree[:, lvl:2 * lvl:2], mem.min_tree[:, lvl + 1:2 * lvl:2])
+        lvl = half
+    mem.size, mem.ptr = n_size, 0
+    agent.train(warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    agent.train(steps)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    res = {"workload": "PER-DQN SynthAtari(4x84x84 uint8, 18 actions), replay %d x %d = %d transitions, batch %d, "
+                       "BasicQnetwork Basic_CNN [32,64,64]/[8,4,3]/[4,2,1] + q [512], perdqn/atari.yaml" %
+                       (n_envs, n_size, n_envs * n_size, batch),
+           "metric": "learner steps/s (one env step of %d envs + one batch-%d update each)" % (n_envs, batch),
+           "value": round(steps / el, 2), "ms_per_step": round(el / steps * 1e3, 3),
+           "env_steps_per_s": round(steps * n_envs / el, 1), "steps": steps, "dtype": "f32 (uint8 frames)",
+           "replay_bytes_in_hbm": int(2 * mem.observations.numel())}
+    del agent, mem
+    torch.cuda.empty_cache()
+    if cpu_updates:
+        from oracle import cpu_ref
+        torch.manual_seed(0)
+        pol = cpu_ref.build_qnetwork_ref(18, [32, 64, 64], [8, 4, 3], [4, 2, 1], [512])
+        opt = torch.optim.Adam(pol.parameters(), 1e-4, eps=1e-5)
+        lrn = cpu_ref.PerDQNLearnerRef(pol, opt, None, 0.99, 500)
+        rng = np.random.default_rng(0)
+        obs = rng.integers(0, 256, (batch, 84, 84, 4), dtype=np.uint8)
+        nxt = rng.integers(0, 256, (batch, 84, 84, 4), dtype=np.uint8)
+        act = rng.integers(0, 18, batch).astype(np.float32)
+        rew = rng.normal(0, 1, batch).astype(np.float32)
+        term = np.zeros(batch, np.float32)
+        lrn.update(obs, act, rew, nxt, term)      # warm-up
+        t0 = time.perf_counter()
+        for _ in range(cpu_updates):
+            lrn.update(obs, act, rew, nxt, term)
+        t_upd = (time.perf_counter() - t0) / cpu_updates
+        t_tree = (tree_cpu_us or 0.0) * 1e-6
+        res["cpu_reference_step"] = {"value": round(1.0 / (t_upd + t_tree), 3), "unit": "learner steps/s",
+                                     "cores": torch.get_num_threads(), "kind": "port",
+                                     "sample": "%d batch-%d PerDQN_Learner updates (restated, torch CPU) %.3f s each "
+                                               "+ one PER sample + priority update of the reference's Python trees "
+                                               "%.3f s (per_kernels.cpu_reference_restated; the frame gather and "
+                                               "env step not counted)"
+                                               % (cpu_updates, batch, t_upd, t_tree)}
+        res["speedup_vs_cpu"] = round(res["value"] / res["cpu_reference_step"]["value"], 1)
+    return res
+
+
 def c3_bench(device, n_envs=1024, n_steps=128, steps=2, warmup=1):
     """C3 (BASELINE.json configs[2]): A2C, SynthAtari uint8 4x84x84 frames, AC_CNN_Atari, 1024 envs x
     128 steps (a2c/atari.yaml: 4 epochs x 8 minibatches of 16 384), everything resident on the GPU."""
@@ -644,6 +714,8 @@ def main():
             result["c3_atari_a2c"] = c3_bench(device)
         if not args.no_per and world == 1:
             result["per_kernels"] = per_bench(device)
+            cr = result["per_kernels"].get("cpu_reference_restated", {})
+            result["c5_perdqn"] = c5_bench(device, tree_cpu_us=cr.get("sample_us", 0) + cr.get("update_priorities_us", 0))
         if not args.no_cpu_baseline and world == 1:
             aff = len(os.sched_getaffinity(0))
             cores = min(aff, int(os.environ.get("OMP_NUM_THREADS", aff)))   # the box's CPU share
