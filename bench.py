@@ -72,19 +72,38 @@ def pair_gemm_flops(batch, d_in, hidden=256):
     return 2.0 * batch * d_in * 2 * hidden
 
 
-def gae_graph_replay_us(mem, reps=50):
-    """K1 alone, `reps` launches on the agent's live buffers captured back to back in one hipGraph
-    (no host dispatch gaps between launches), timed with events on the replay stream."""
+def gae_value_bytes(n_envs, horizon, mid_truncations, hidden=256):
+    """K1V (xpa_gae_scan_value): K1's bytes + the critic hidden pre-activations of the deferred pass it reads to
+    form the bootstrap values, 2 n_envs rows x hidden f32 (every env's truncation-slot row and last-step row:
+    the critic pass runs at a fixed [2N, D] shape) + the output layer."""
+    return gae_bytes(n_envs, horizon, mid_truncations) + 4.0 * (2 * n_envs * hidden + hidden + 1)
+
+
+def gae_graph_replay_us(agent, reps=50):
+    """The in-loop GAE launch alone (the form the agent ran), `reps` launches on the agent's live buffers captured
+    back to back in one hipGraph (no host dispatch gaps between launches), timed with events on the replay
+    stream."""
     import torch
     from xuanpolicy_amd import ops
+    mem = agent.memory
     adv, ret = torch.empty_like(mem.rewards), torch.empty_like(mem.rewards)
     slot = torch.full((mem.n_envs,), -1, dtype=torch.int32, device=mem.rewards.device)
     vboot = torch.zeros(2 * mem.n_envs, device=mem.rewards.device)
     boot = torch.empty_like(mem.rewards)
+    form = getattr(agent, "gae_form", "compact")
+    if form == "value":
+        fm = agent.learner._fused_mlp()
+        zc = fm.rollout_value_hidden(agent._boot_pair)
+        lin_co = fm.critic[-1][0]
+        act = fm.critic[-2][1:]
 
-    def launch():  # the in-loop form (compact closures); slots empty after the rollout's GAE
-        ops.gae_scan_compact(mem.rewards, mem.values, mem.terminals, slot, vboot, mem.gamma, mem.gae_lam,
-                             mem.use_gae, adv=adv, ret=ret, boot=boot)
+        def launch():  # slots empty after the rollout's GAE
+            ops.gae_scan_value(mem.rewards, mem.values, mem.terminals, slot, zc, act, lin_co.weight, lin_co.bias,
+                               mem.gamma, mem.gae_lam, mem.use_gae, adv=adv, ret=ret, boot=boot)
+    else:
+        def launch():  # the compact-closure form; slots empty after the rollout's GAE
+            ops.gae_scan_compact(mem.rewards, mem.values, mem.terminals, slot, vboot, mem.gamma, mem.gae_lam,
+                                 mem.use_gae, adv=adv, ret=ret, boot=boot)
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
@@ -608,7 +627,7 @@ def main():
     mem = agent.memory
     # Back-to-back replay of the same GAE launch on the agent's live buffers (after the timed region):
     # per-launch time without the event/dispatch overhead a single bracketed launch carries.
-    replay_us = None if args.no_kernel_timing else gae_graph_replay_us(mem)
+    replay_us = None if args.no_kernel_timing else gae_graph_replay_us(agent)
     floor_us = None if args.no_kernel_timing else ops.dispatch_floor_us(device)
     copy_us = None if args.no_kernel_timing else ops.stream_copy_us(mem.rewards, mem.values, mem.terminals)
     mid_trunc = int(((mem.closed[:, :-1] > 0) & (mem.terminals[:, :-1] == 0)).sum())
@@ -619,16 +638,29 @@ def main():
         value = world * N * T * args.steps / elapsed
         roofline = None
         if gae_ms:
-            gb = gae_bytes(N, T, mid_trunc)
+            form = getattr(agent, "gae_form", "compact")
+            gb = gae_value_bytes(N, T, mid_trunc, args.hidden) if form == "value" else gae_bytes(N, T, mid_trunc)
+            gb_k1 = gae_bytes(N, T, mid_trunc)
             ach = gb / gae_ms / 1e6
             traffic = None
             pmc = os.path.join(REPO, "profiles", "pmc_gae_compact_r01.json")
             if os.path.exists(pmc):
                 with open(pmc) as f:
                     traffic = json.load(f).get("hbm_bytes_per_launch")
-            roofline = {"kernel": "xpa_gae_scan_compact (gae_dpp_kernel<5, 1>)", "bound": "hbm", "achieved": round(ach, 1),
+            if form == "value":
+                act_code = agent.learner._fused_mlp().critic[-2][1]
+                kname = "xpa_gae_scan_value: critic output layer + bootstrap fixup + GAE (gae_dpp_kernel<5, 1, %d>)" \
+                    % act_code
+            else:
+                kname = "xpa_gae_scan_compact (gae_dpp_kernel<5, 1>)"
+            roofline = {"kernel": kname, "bound": "hbm", "achieved": round(ach, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "avg_launch_us": round(gae_ms * 1e3, 3), "algorithmic_bytes_per_launch": int(gb),
+                        "bytes_note": ("K1's 20 B per (env, step) + 4 B per bootstrap (%d B) + the critic hidden "
+                                       "pre-activations the fused value head reads, 2 x %d rows x %d f32 + the output "
+                                       "layer" % (int(gb_k1), N, args.hidden)) if form == "value" else
+                                      "20 B per (env, step) + 4 B per bootstrap (SURVEY.md §8(d))",
+                        "gae_only_bytes_frac": round(gb_k1 / gae_ms / 1e6 / HBM_PEAK_GBS, 4),
                         "launches": gae_launches,
                         "timing": "HIP events recorded by each in-loop dispatch at the kernel's own start and end "
                                   "(hipExtLaunchKernel), on the launch stream, inside the timed region",
@@ -640,8 +672,8 @@ def main():
                         "frac_ceiling_at_floor": round(gb / floor_us / 1e3 / HBM_PEAK_GBS, 4) if floor_us else None,
                         # the same bytes streamed with no scan (3 loads + 2 stores of 16 B per 4 elements), same
                         # clock, same buffers: what any kernel moving K1's bytes in one launch takes here
-                        "same_bytes_copy_us": round(copy_us, 3) if copy_us else None,
-                        "frac_of_copy": round(copy_us / (gae_ms * 1e3), 3) if copy_us else None}
+                        "k1_bytes_copy_us": round(copy_us, 3) if copy_us else None,
+                        "frac_of_copy": round(copy_us / (gae_ms * 1e3), 3) if copy_us and form != "value" else None}
         loss_kernel = None
         if loss_ms:
             lb = loss_bytes_gauss(B, args.act_dim)

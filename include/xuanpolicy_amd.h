@@ -84,6 +84,20 @@ int xpa_gae_scan_compact(const float *rew, const float *val, const float *term, 
                          int use_gae, float *adv, float *ret, float *boot, void *ev_start, void *ev_stop,
                          xpa_stream_t stream);
 
+/* K1V, value-fused compact scan: xpa_gae_scan_compact with the deferred pass's value head inside it.
+ * Replaces the critic's last layer on [truncation slots; last observations] (gaussian.py:73-77 /
+ * categorical.py:83-85: v = critic(state)[:, 0], as the agent bootstraps at ppoclip_agent.py:69-75, 95-100)
+ * plus the fixup + finish_path GAE (memory_tools.py:206-229).  z_critic [2 n_envs, ld] (row stride ld,
+ * 16-B aligned) holds the critic's hidden-layer pre-activations (rows [0, n) the truncation slots, [n, 2n)
+ * the last-step observations); V = act(z) . w_critic + b_critic[0] (act 0 identity, 1 LeakyReLU(slope),
+ * 2 tanh; hidden = 256), bitwise K14's xpa_value_head.  Then exactly xpa_gae_scan_compact with
+ * vboot = V.  horizon % 4 == 0 and >= 36.  ev_start / ev_stop as in xpa_gae_scan_timed. */
+int xpa_gae_scan_value(const float *rew, const float *val, const float *term, int32_t *slot_t, int act,
+                       const float *z_critic, int64_t ld, float slope, const float *w_critic,
+                       const float *b_critic, int64_t n_envs, int64_t horizon, int64_t hidden, float gamma,
+                       float gae_lambda, int use_gae, float *adv, float *ret, float *boot, void *ev_start,
+                       void *ev_stop, xpa_stream_t stream);
+
 /* Measurement aid (no reference counterpart): an empty one-wave kernel launched with the same
  * dispatch-attached events as xpa_gae_scan_timed — the fixed per-launch cost of that clock. */
 int xpa_dispatch_floor_timed(void *ev_start, void *ev_stop, xpa_stream_t stream);

@@ -118,6 +118,45 @@ def test_gae_compact_matches_fixup_plus_scan(N, T, use_gae):
     np.testing.assert_allclose(_h(ret), _h(r2), rtol=0, atol=1e-6)
 
 
+@pytest.mark.parametrize("N,T", [(4096, 128), (1000, 128), (777, 64), (33, 36), (5, 516), (7, 260), (11, 256)])
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_gae_value_fused_matches_value_head_plus_compact(N, T, act):
+    """xpa_gae_scan_value (value head inside the scan) == xpa_value_head + xpa_gae_scan_compact bit for bit (adv,
+    ret, the boot column, the slot reset), and the values it bootstraps with == the oracle's act(z) . w + b."""
+    from xuanpolicy_amd import ops
+    rng = np.random.default_rng(N * 13 + T + act)
+    rew, val, term, slot, _, closed, _ = _compact_case(rng, N, T)
+    H, slope = 256, 0.01
+    z = rng.normal(0, 1, (2 * N, H)).astype(np.float32)
+    w = (rng.normal(0, 1, (1, H)) / 16).astype(np.float32)
+    b = rng.normal(0, 1, (1,)).astype(np.float32)
+    z_d, w_d, b_d = _d(z), _d(w), _d(b)
+    vboot = ops.value_head(z_d, (act, slope), w_d, b_d)
+    boot_a, slot_a = torch.zeros(N, T, device=DEV), _d(slot)
+    adv_a, ret_a = ops.gae_scan_compact(_d(rew), _d(val), _d(term), slot_a, vboot, 0.99, 0.95, True, boot=boot_a)
+    boot_b, slot_b = torch.zeros(N, T, device=DEV), _d(slot)
+    adv_b = torch.full((N, T), -7.0, device=DEV)
+    ret_b = torch.full((N, T), -7.0, device=DEV)
+    ops.gae_scan_value(_d(rew), _d(val), _d(term), slot_b, z_d, (act, slope), w_d, b_d, 0.99, 0.95, True,
+                       adv=adv_b, ret=ret_b, boot=boot_b)
+    np.testing.assert_array_equal(_h(adv_b), _h(adv_a))
+    np.testing.assert_array_equal(_h(ret_b), _h(ret_a))
+    np.testing.assert_array_equal(_h(boot_b), _h(boot_a))
+    assert (_h(slot_b) == -1).all()
+    # the oracle: V in f64 from the same z, then the dense-closure GAE restatement
+    h = z.astype(np.float64)
+    h = np.where(h > 0, h, h * slope) if act == 1 else (np.tanh(h) if act == 2 else h)
+    v = (h @ w[0].astype(np.float64) + b[0]).astype(np.float32)
+    np.testing.assert_allclose(_h(vboot), v, rtol=1e-5, atol=1e-5)
+    ref_boot = np.zeros((N, T), np.float32)
+    rows = np.nonzero(slot >= 0)[0]
+    ref_boot[rows, slot[rows]] = v[rows]
+    ref_boot[:, -1] = np.where(term[:, -1] > 0, 0.0, v[N:])
+    ref_adv, ref_ret = cpu_ref.gae_rows(rew, val, term, closed, ref_boot, 0.99, 0.95, True)
+    np.testing.assert_allclose(_h(adv_b), ref_adv, rtol=1e-5, atol=2e-5)
+    np.testing.assert_allclose(_h(ret_b), ref_ret, rtol=1e-5, atol=2e-5)
+
+
 def test_gae_kernel_unaligned_views():
     """float4 path needs 16-B alignment; an offset view must take the scalar path and stay correct."""
     from xuanpolicy_amd import ops

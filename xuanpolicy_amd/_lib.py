@@ -30,6 +30,8 @@ SIGNATURES = {
     "xpa_gae_scan": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, ctypes.c_int, c_p, c_p, c_p]),
     "xpa_gae_scan_compact": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, ctypes.c_int, c_p, c_p,
                                             c_p, c_p, c_p, c_p]),
+    "xpa_gae_scan_value": (ctypes.c_int, [c_p, c_p, c_p, c_p, ctypes.c_int, c_p, c_i64, c_f32, c_p, c_p, c_i64, c_i64,
+                                          c_i64, c_f32, c_f32, ctypes.c_int, c_p, c_p, c_p, c_p, c_p, c_p]),
     "xpa_stream_copy_timed": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_p]),
     "xpa_gae_scan_timed": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, ctypes.c_int, c_p, c_p,
                                           c_p, c_p, c_p]),

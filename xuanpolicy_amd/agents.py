@@ -109,6 +109,7 @@ class _OnPolicyAgent:
         self._perm_buf = None
         self.device_env = hasattr(envs, "step_device")
         self.fuse_env_step = True   # device SynthBox env stepped inside K14 when possible (_env_fused)
+        self.fuse_value_gae = True  # deferred bootstraps' value head inside the GAE scan (xpa_gae_scan_value)
         self.current_step = 0
         self.current_episode = np.zeros((N,), np.int32)
         self.iterations = 0
@@ -142,7 +143,11 @@ class _OnPolicyAgent:
         self.defer_boot = (bool(_cfg(config, "defer_bootstrap", True)) and not self.raw_obs
                            and hasattr(envs, "step_device") and int(max_ep) >= self.n_steps)
         if self.defer_boot:
-            self.slot_obs = torch.zeros((N, D), **f32)
+            # [truncation slots; last-step observations] as the two halves of one buffer: the deferred critic
+            # pass reads it whole (no concatenation launch)
+            pair = torch.zeros((2 * N, D), **f32)
+            self.slot_obs, self.boot_obs = pair[:N], pair[N:]
+            self._boot_pair = pair
             self.slot_t = torch.full((N,), -1, dtype=torch.int32, device=dev)
             self.slot_overflow = torch.zeros((1,), dtype=torch.int32, device=dev)
             self._overflow_host = self._overflow_event = None
@@ -359,16 +364,23 @@ class _OnPolicyAgent:
             self._perm_buf = torch.empty(n, dtype=torch.int64, device=self.device)
         return ops.random_permutation(n, self.seed, counter, out=self._perm_buf)
 
-    def _deferred_bootstraps(self):
-        """V([truncation slots; last-step final obs]) in one critic pass, written into the buffer's
-        bootstrap column by xpa_rollout_bootstrap_fixup."""
-        x = torch.cat([self.slot_obs, self.boot_obs], dim=0)
+    def _deferred_bootstraps(self, hidden_only=False):
+        """V([truncation slots; last-step final obs]) in one critic pass ([2N] values), or with hidden_only the
+        critic's hidden pre-activations ([2N, 256], for the value-fused scan xpa_gae_scan_value; None when the
+        policy has no fused critic)."""
+        x = self._boot_pair
         fm = self._rollout_mlp()
+        self._check_overflow()
+        if hidden_only:
+            return fm.rollout_value_hidden(x)
         if fm is not None:
             v = fm.rollout_value(x)
         else:
             with torch.no_grad():
                 v = policy_heads(self.policy, x)[2].contiguous()
+        return v.reshape(-1)
+
+    def _check_overflow(self):
         # An env truncating twice in one rollout cannot happen for the device envs (their one truncation source is
         # the time limit and max_episode_steps >= n_steps, see __init__), so the flag is checked without a host
         # sync: copied to pinned memory here and read one iteration later (never silent, never a stall).
@@ -379,18 +391,32 @@ class _OnPolicyAgent:
             raise RuntimeError("an env truncated twice within one rollout; set config.defer_bootstrap = False")
         self._overflow_host.copy_(self.slot_overflow, non_blocking=True)
         self._overflow_event.record()
-        return v.reshape(-1)
 
     def _update_phase(self):
         mem = self.memory
         mem.size = self.n_steps
-        if self.defer_boot:
+        zc = None
+        if (self.defer_boot and not self.atari and not mem._pending and self.fuse_value_gae
+                and ops.gae_value_ok(self.n_steps) and self._rollout_mlp() is not None):
+            zc = self._deferred_bootstraps(hidden_only=True)
+        if zc is not None:
+            # one launch: the critic's output layer, the fixup's bootstrap writes and the compact GAE scan
+            fm = self._rollout_mlp()
+            lin_co = fm.critic[-1][0]
+            _, code, slope = fm.critic[-2]
+            ops.gae_scan_value(mem.rewards, mem.values, mem.terminals, self.slot_t, zc, (code, slope), lin_co.weight,
+                               lin_co.bias, mem.gamma, mem.gae_lam, mem.use_gae, adv=mem._advantages,
+                               ret=mem._returns, boot=mem.boot)
+            mem._dirty = False
+            self.gae_form = "value"
+        elif self.defer_boot:
             vboot = self._deferred_bootstraps()
             if not self.atari and not mem._pending:
                 # one launch: the fixup's bootstrap writes fused into the compact-closure GAE scan
                 ops.gae_scan_compact(mem.rewards, mem.values, mem.terminals, self.slot_t, vboot, mem.gamma,
                                      mem.gae_lam, mem.use_gae, adv=mem._advantages, ret=mem._returns, boot=mem.boot)
                 mem._dirty = False
+                self.gae_form = "compact"
             else:
                 ops.bootstrap_fixup(vboot, self.slot_t, mem.terminals, mem.boot)
                 mem.compute_advantages()

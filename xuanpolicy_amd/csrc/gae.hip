@@ -275,14 +275,32 @@ __device__ __forceinline__ void dpp_combine(float &LA, float &LB) {
     LA = LA * oA;
 }
 
-template <int SEG_LOG2, int COMPACT>
+// xor-butterfly partner inside a 32-lane group without an LDS round trip (ds_swizzle bitmask mode:
+// src lane = ((lane & 0x1f) | 0) ^ X)
+template <int X>
+__device__ __forceinline__ float swz_xor(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x1f | (X << 10)));
+}
+
+// Value-fused form (VACT >= 0, with COMPACT): the deferred bootstraps' critic values are formed here from the
+// critic's hidden pre-activations z [2 n_rows, ld] (rows [0, n) = truncation slots, [n, 2n) = last-step
+// observations) instead of by a separate value-head launch (K14 MODE 2) whose output the scan then loads.
+// V = sum_j act(z_j) w_j + b with K14's arithmetic bit for bit: virtual lane j (of K14's 64) owns columns
+// [4j, 4j + 4) and the sum runs K14's xor butterfly 32, 16, ..., 1 — lane sl of an L-lane row segment holds
+// virtual lanes sl + k L (k < 64 / L), so steps o >= L are in-lane and o < L cross lanes (ds_swizzle).
+template <int SEG_LOG2, int COMPACT, int VACT = -1>
 __global__ __launch_bounds__(256) void gae_dpp_kernel(const float *__restrict__ rew, const float *__restrict__ val,
                                                       const float *__restrict__ term,
                                                       const uint8_t *__restrict__ closed,
                                                       const float *__restrict__ boot, int64_t n_rows, int T,
                                                       float gamma, float gl, int use_gae, float *__restrict__ adv,
                                                       float *__restrict__ ret, int *__restrict__ slot_t,
-                                                      const float *__restrict__ vboot, float *__restrict__ boot_out) {
+                                                      const float *__restrict__ vboot, float *__restrict__ boot_out,
+                                                      const float *__restrict__ zc = nullptr, int64_t ldz = 0,
+                                                      float slope = 0.f, const float *__restrict__ wc = nullptr,
+                                                      const float *__restrict__ bc = nullptr) {
+    constexpr bool VALUE = VACT >= 0;
+    static_assert(!VALUE || COMPACT, "the value-fused scan is a compact-closure form");
     constexpr int L = 1 << SEG_LOG2;
     constexpr int C = 4 * L;
     const int lane = threadIdx.x & 63;
@@ -297,7 +315,23 @@ __global__ __launch_bounds__(256) void gae_dpp_kernel(const float *__restrict__ 
 
     int st = -1;
     float vs = 0.f, vl = 0.f;
-    if (COMPACT && row_ok) {
+    constexpr int KV = VALUE ? 64 / L : 1;
+    float4 zs[KV], zl[KV], wv[KV];
+    float bias = 0.f;
+    if constexpr (VALUE) {
+        // every load unconditional from a clamped address (no branch whose join would wait for them all)
+        const int64_t rs = row_ok ? row : 0;
+        st = slot_t[rs];
+        if (!row_ok) st = -1;
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            const int col = 4 * (sl + k * L);
+            zs[k] = *reinterpret_cast<const float4 *>(zc + rs * ldz + col);
+            zl[k] = *reinterpret_cast<const float4 *>(zc + (n_rows + rs) * ldz + col);
+            wv[k] = *reinterpret_cast<const float4 *>(wc + col);
+        }
+        bias = bc[0];
+    } else if (COMPACT && row_ok) {
         st = slot_t[row];
         vs = vboot[row];
         vl = vboot[n_rows + row];
@@ -312,7 +346,58 @@ __global__ __launch_bounds__(256) void gae_dpp_kernel(const float *__restrict__ 
         float r[4] = {0.f, 0.f, 0.f, 0.f}, v[4] = {0.f, 0.f, 0.f, 0.f}, d[4] = {0.f, 0.f, 0.f, 0.f};
         float bt[4] = {0.f, 0.f, 0.f, 0.f};
         bool cl[4] = {false, false, false, false};
-        if (in) {
+        if constexpr (VALUE) {
+            // unconditional loads (clamped step), validity by selects; then V(slot), V(last) from z
+            const int64_t o = base + (in ? t0 : 0);
+            const float4 r4 = ld4<1>(rew + o);
+            const float4 v4 = ld4<1>(val + o);
+            const float4 d4 = ld4<1>(term + o);
+            if (c == nchunks - 1) {
+                float ps[KV], pl[KV];
+#pragma unroll
+                for (int k = 0; k < KV; ++k) {
+                    ps[k] = xpa_dot4(xpa_act4<VACT>(zs[k], slope), wv[k]);
+                    pl[k] = xpa_dot4(xpa_act4<VACT>(zl[k], slope), wv[k]);
+                }
+#pragma unroll
+                for (int m = KV / 2; m >= 1; m >>= 1)  // butterfly steps o = m L >= L: in-lane
+#pragma unroll
+                    for (int k = 0; k < KV; ++k)
+                        if (k < (k ^ m)) {
+                            const float a0 = ps[k] + ps[k ^ m], b0 = pl[k] + pl[k ^ m];
+                            ps[k] = ps[k ^ m] = a0;
+                            pl[k] = pl[k ^ m] = b0;
+                        }
+                float xs = ps[0], xl = pl[0];
+                if constexpr (L == 64) {
+                    xs += __shfl_xor(xs, 32, 64);
+                    xl += __shfl_xor(xl, 32, 64);
+                }
+                if constexpr (L >= 32) { xs += swz_xor<16>(xs); xl += swz_xor<16>(xl); }
+                xs += swz_xor<8>(xs); xl += swz_xor<8>(xl);
+                xs += swz_xor<4>(xs); xl += swz_xor<4>(xl);
+                xs += swz_xor<2>(xs); xl += swz_xor<2>(xl);
+                xs += swz_xor<1>(xs); xl += swz_xor<1>(xl);
+                vs = xs + bias;
+                vl = xl + bias;
+            }
+            if (in) {
+                r[0] = r4.x; r[1] = r4.y; r[2] = r4.z; r[3] = r4.w;
+                v[0] = v4.x; v[1] = v4.y; v[2] = v4.z; v[3] = v4.w;
+                d[0] = d4.x; d[1] = d4.y; d[2] = d4.z; d[3] = d4.w;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int t = t0 + e;
+                    const bool lt = (t == T - 1);
+                    cl[e] = lt || d[e] != 0.f || t == st;
+                    bt[e] = lt ? (d[e] != 0.f ? 0.f : vl) : (t == st ? vs : 0.f);
+                }
+                if (t0 + 3 == T - 1) {
+                    has_last = true;
+                    last_boot = bt[3];
+                }
+            }
+        } else if (in) {
             const float4 r4 = ld4<1>(rew + base + t0);
             const float4 v4 = ld4<1>(val + base + t0);
             const float4 d4 = ld4<1>(term + base + t0);
@@ -431,10 +516,14 @@ bool launch_gae_dpp(int seg_log2, dim3 grid, hipStream_t s, hipEvent_t e0, hipEv
     do {                                                                                                             \
         if (e0 || e1)                                                                                                \
             hipExtLaunchKernelGGL((gae_dpp_kernel<S_, COMPACT>), grid, dim3(256), 0, s, e0, e1, 0, rew, val, term,    \
-                                  closed, boot, n_envs, T, gamma, gl, use_gae, adv, ret, slot_t, vboot, boot_out);   \
+                                  closed, boot, n_envs, T, gamma, gl, use_gae, adv, ret, slot_t, vboot, boot_out,    \
+                                  (const float *)nullptr, (int64_t)0, 0.f, (const float *)nullptr,                   \
+                                  (const float *)nullptr);                                                           \
         else                                                                                                         \
             hipLaunchKernelGGL((gae_dpp_kernel<S_, COMPACT>), grid, dim3(256), 0, s, rew, val, term, closed, boot,    \
-                               n_envs, T, gamma, gl, use_gae, adv, ret, slot_t, vboot, boot_out);                    \
+                               n_envs, T, gamma, gl, use_gae, adv, ret, slot_t, vboot, boot_out,                     \
+                               (const float *)nullptr, (int64_t)0, 0.f, (const float *)nullptr,                      \
+                               (const float *)nullptr);                                                              \
     } while (0)
     switch (seg_log2) {
         case 4: XPA_GAE_DPP(4); return true;
@@ -606,5 +695,64 @@ XPA_API int xpa_gae_scan_compact(const float *rew, const float *val, const float
     if (vec4) XPA_GAEC(4, 1);
     else XPA_GAEC(1, 0);
 #undef XPA_GAEC
+    return xpa_launch_status();
+}
+
+namespace {
+template <int S_, int A_>
+void launch_gae_value(dim3 grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1, const float *rew, const float *val,
+                      const float *term, int64_t n_envs, int T, float gamma, float gl, int use_gae, float *adv,
+                      float *ret, int *slot_t, float *boot, const float *z, int64_t ld, float slope, const float *w,
+                      const float *b) {
+    if (e0 || e1)
+        hipExtLaunchKernelGGL((gae_dpp_kernel<S_, 1, A_>), grid, dim3(256), 0, s, e0, e1, 0, rew, val, term,
+                              (const uint8_t *)nullptr, (const float *)nullptr, n_envs, T, gamma, gl, use_gae, adv, ret,
+                              slot_t, (const float *)nullptr, boot, z, ld, slope, w, b);
+    else
+        hipLaunchKernelGGL((gae_dpp_kernel<S_, 1, A_>), grid, dim3(256), 0, s, rew, val, term, (const uint8_t *)nullptr,
+                           (const float *)nullptr, n_envs, T, gamma, gl, use_gae, adv, ret, slot_t,
+                           (const float *)nullptr, boot, z, ld, slope, w, b);
+}
+}  // namespace
+
+XPA_API int xpa_gae_scan_value(const float *rew, const float *val, const float *term, int32_t *slot_t, int act,
+                               const float *z_critic, int64_t ld, float slope, const float *w_critic,
+                               const float *b_critic, int64_t n_envs, int64_t horizon, int64_t hidden, float gamma,
+                               float gae_lambda, int use_gae, float *adv, float *ret, float *boot, void *ev_start,
+                               void *ev_stop, xpa_stream_t stream) {
+    if (n_envs <= 0 || horizon < 36 || horizon > (1 << 30) || horizon % 4 || hidden != 256 || ld < 256 || ld % 4 ||
+        act < 0 || act > 2)
+        return (int)hipErrorInvalidValue;
+    if (!rew || !val || !term || !slot_t || !z_critic || !w_critic || !b_critic || !adv || !ret || !boot)
+        return (int)hipErrorInvalidValue;
+    if (((uintptr_t)rew | (uintptr_t)val | (uintptr_t)term | (uintptr_t)adv | (uintptr_t)ret | (uintptr_t)z_critic |
+         (uintptr_t)w_critic) % 16)
+        return (int)hipErrorInvalidValue;
+    const int T = (int)horizon;
+    int seg_log2 = 0;
+    while ((1 << seg_log2) < T / 4 && seg_log2 < 6) ++seg_log2;  // T >= 36: seg_log2 in [4, 6]
+    const int64_t rows_per_wave = 64 >> seg_log2;
+    const int64_t blocks = ((n_envs + rows_per_wave - 1) / rows_per_wave + 3) / 4;
+    if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+    const dim3 grid((unsigned)blocks);
+    hipStream_t s = (hipStream_t)stream;
+    hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
+    const float gl = gamma * gae_lambda;
+#define XPA_GAEV(S_, A_)                                                                                        \
+    launch_gae_value<S_, A_>(grid, s, e0, e1, rew, val, term, n_envs, T, gamma, gl, use_gae, adv, ret, slot_t, boot, \
+                             z_critic, ld, slope, w_critic, b_critic)
+#define XPA_GAEV_ACT(S_)             \
+    do {                             \
+        if (act == 0) XPA_GAEV(S_, 0); \
+        else if (act == 1) XPA_GAEV(S_, 1); \
+        else XPA_GAEV(S_, 2);        \
+    } while (0)
+    switch (seg_log2) {
+        case 4: XPA_GAEV_ACT(4); break;
+        case 5: XPA_GAEV_ACT(5); break;
+        default: XPA_GAEV_ACT(6); break;
+    }
+#undef XPA_GAEV_ACT
+#undef XPA_GAEV
     return xpa_launch_status();
 }

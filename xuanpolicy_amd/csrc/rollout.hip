@@ -399,19 +399,6 @@ __device__ __forceinline__ void synthbox_env_row(int64_t n, int lane, const Synt
     }
 }
 
-template <int ACT>
-__device__ __forceinline__ float4 act4(float4 z, float slope) {
-    if (ACT == 1) {
-        z.x = z.x > 0.f ? z.x : z.x * slope; z.y = z.y > 0.f ? z.y : z.y * slope;
-        z.z = z.z > 0.f ? z.z : z.z * slope; z.w = z.w > 0.f ? z.w : z.w * slope;
-    } else if (ACT == 2) {
-        z.x = tanhf(z.x); z.y = tanhf(z.y); z.z = tanhf(z.z); z.w = tanhf(z.w);
-    }
-    return z;
-}
-
-__device__ __forceinline__ float dot4(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
-
 __device__ __forceinline__ float wave_allsum_f(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -455,16 +442,16 @@ __global__ __launch_bounds__(256) void rollout_policy_head_kernel(
             wreg[j] = env.wt[jj * env.D + dl];
         }
     }
-    const float4 hc = act4<ACT>(*reinterpret_cast<const float4 *>(zc + n * ld + 4 * lane), slope);
-    const float v = wave_allsum_f(dot4(hc, *reinterpret_cast<const float4 *>(Wc + 4 * lane))) + bc[0];
+    const float4 hc = xpa_act4<ACT>(*reinterpret_cast<const float4 *>(zc + n * ld + 4 * lane), slope);
+    const float v = wave_allsum_f(xpa_dot4(hc, *reinterpret_cast<const float4 *>(Wc + 4 * lane))) + bc[0];
     if (MODE == 2) {
         if (lane == 0) v_out[n] = v;
         return;
     }
-    const float4 h = act4<ACT>(*reinterpret_cast<const float4 *>(za + n * ld + 4 * lane), slope);
+    const float4 h = xpa_act4<ACT>(*reinterpret_cast<const float4 *>(za + n * ld + 4 * lane), slope);
     float mine = 0.f;  // lane o keeps head[o]
     for (int o = 0; o < K; ++o) {
-        const float p = wave_allsum_f(dot4(h, *reinterpret_cast<const float4 *>(Wa + o * 256 + 4 * lane))) + ba[o];
+        const float p = wave_allsum_f(xpa_dot4(h, *reinterpret_cast<const float4 *>(Wa + o * 256 + 4 * lane))) + ba[o];
         if (lane == o) mine = p;
         if (MODE == 1 && lane == 0) s_head[wave][o] = p;
     }

@@ -45,6 +45,26 @@ __device__ __forceinline__ T xpa_wave_max(T v) {
     return v;
 }
 
+// ---- hidden activation + dot product of the rollout value / policy heads -------------------------
+// (shared so K14's value head and the value-fused GAE scan form V(s) with the same arithmetic, bit for bit)
+// ACT: 0 identity, 1 LeakyReLU(slope), 2 tanh.
+template <int ACT>
+__device__ __forceinline__ float4 xpa_act4(float4 z, float slope) {
+    if (ACT == 1) {
+        z.x = z.x > 0.f ? z.x : z.x * slope; z.y = z.y > 0.f ? z.y : z.y * slope;
+        z.z = z.z > 0.f ? z.z : z.z * slope; z.w = z.w > 0.f ? z.w : z.w * slope;
+    } else if (ACT == 2) {
+        z.x = tanhf(z.x); z.y = tanhf(z.y); z.z = tanhf(z.z); z.w = tanhf(z.w);
+    }
+    return z;
+}
+
+// explicit fma chain: left to fp-contract, hipcc picked fma(x, x', y y') in one kernel and fma(y, y', x x') in
+// another, so the "same" dot product differed by an ulp between K14 and the value-fused scan
+__device__ __forceinline__ float xpa_dot4(float4 a, float4 b) {
+    return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
+}
+
 // Block sum over `nwaves` waves through LDS scratch (nwaves entries); result valid in all threads.
 template <typename T>
 __device__ __forceinline__ T xpa_block_sum(T v, T *scratch, int nwaves) {

@@ -226,6 +226,15 @@ class FusedActorCritic:
                                 lin_co.bias, self.logstd, cursor, seed, buf_act, buf_logp, buf_val, env_in, act_clip)
 
     @torch.no_grad()
+    def rollout_value_hidden(self, x):
+        """Critic up to its last hidden pre-activation [n, 256] (the value-fused GAE scan applies the
+        activation and the output layer)."""
+        rep_outs = self._rep_forward(x)
+        s = rep_outs[-1] if rep_outs else x
+        lin_ch = self.critic[-2][0]
+        return F.linear(s, lin_ch.weight, lin_ch.bias)
+
+    @torch.no_grad()
     def rollout_value(self, x, out=None):
         """Critic only (bootstrap values): trunk, critic hidden GEMM, K14 value head."""
         rep_outs = self._rep_forward(x)

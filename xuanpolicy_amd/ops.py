@@ -188,6 +188,42 @@ def gae_scan_compact(rew, val, term, slot_t, vboot, gamma, gae_lambda, use_gae=T
     return adv, ret
 
 
+def gae_value_ok(T, z_critic=None):
+    """True when xpa_gae_scan_value covers horizon T (DPP row segments of 16-64 lanes)."""
+    return T % 4 == 0 and T >= 36 and (z_critic is None or z_critic.shape[1] == HEAD_HIDDEN)
+
+
+def gae_scan_value(rew, val, term, slot_t, z_critic, act, w_critic, b_critic, gamma, gae_lambda, use_gae=True,
+                   adv=None, ret=None, boot=None):
+    """K1V (xpa_gae_scan_value): gae_scan_compact with the deferred bootstrap values formed inside the scan from
+    the critic's hidden pre-activations z_critic [2 n_envs, 256] (rows: truncation slots, then last-step obs),
+    act = (code, slope) and the critic's output layer (w_critic [1, 256], b_critic [1]).  Returns (adv, ret)."""
+    N, T = rew.shape
+    for name, t, dt in (("rew", rew, torch.float32), ("val", val, torch.float32), ("term", term, torch.float32),
+                        ("boot", boot, torch.float32)):
+        _req(t, name, dt, (N, T))
+    _req(slot_t, "slot_t", torch.int32, (N,))
+    if z_critic.dtype != torch.float32 or z_critic.device.type != "cuda" or z_critic.shape[0] != 2 * N:
+        raise ValueError("z_critic must be a float32 ROCm tensor [2 n_envs, %d]" % HEAD_HIDDEN)
+    ld = _row_stride(z_critic, "z_critic", HEAD_HIDDEN)
+    _req(w_critic, "w_critic", torch.float32)
+    _req(b_critic, "b_critic", torch.float32)
+    if w_critic.numel() != HEAD_HIDDEN or b_critic.numel() != 1:
+        raise ValueError("the critic's output layer must be Linear(%d, 1)" % HEAD_HIDDEN)
+    if not gae_value_ok(T, z_critic):
+        raise ValueError("xpa_gae_scan_value needs horizon % 4 == 0 and >= 36 (got %d)" % T)
+    adv = torch.empty_like(rew) if adv is None else _req(adv, "adv", torch.float32, (N, T))
+    ret = torch.empty_like(rew) if ret is None else _req(ret, "ret", torch.float32, (N, T))
+    ev = TIMER.kernel_events("gae")
+    e0, e1 = (None, None) if ev is None else ev
+    rc = lib().xpa_gae_scan_value(_p(rew), _p(val), _p(term), _p(slot_t), int(act[0]), _p(z_critic), ld,
+                                  float(act[1]), _p(w_critic), _p(b_critic), N, T, HEAD_HIDDEN, float(gamma),
+                                  float(gae_lambda), int(bool(use_gae)), _p(adv), _p(ret), _p(boot), e0, e1,
+                                  _stream(rew.device))
+    _lib.check(rc, "xpa_gae_scan_value")
+    return adv, ret
+
+
 def _event_timed_median_us(launch, reps):
     """Median duration (us) of `launch(ev_start, ev_stop)` over `reps` synchronised launches, each timed by
     dispatch-attached events (the clock xpa_gae_scan_timed uses)."""
