@@ -153,6 +153,10 @@ class _OnPolicyAgent:
             self._overflow_host = self._overflow_event = None
         self._graph = None
         self._graph_pool = None
+        # device env steps per replayed graph (train() falls back to single-step replays at chunk boundaries it
+        # cannot meet); 1 = per-step graphs
+        self.graph_chunk = int(_cfg(config, "graph_chunk", min(self.n_steps, 128)))
+        self._chunk_graph = self._chunk_key = None
         # Model / log directories and the logger (agent.py:33-70).  model_dir_save is seed_<seed>_<time>
         # under model_dir, model_dir_load is model_dir itself (what load_model searches); both are created
         # when first written, not at construction (tests and benches build many agents).
@@ -319,6 +323,26 @@ class _OnPolicyAgent:
             return
         self._graph.replay()
 
+    def _rollout_chunk_graph(self, k):
+        """k consecutive device env steps captured into ONE hipGraph (k x 5 kernels) and replayed as a unit: a
+        per-step replay leaves the GPU idle ~8 us between graphs while the host launches the next (r02 trace:
+        127 such gaps = 1.0 ms of a 72 ms iteration).  Same replay invariance as _rollout_step_graph."""
+        key = (k,) + tuple(p.data_ptr() for p in self.policy.parameters())
+        if self._chunk_graph is not None and key != self._chunk_key:
+            self._chunk_graph = None
+        if self._chunk_graph is None:
+            if self._graph is None:
+                self._rollout_step_graph()   # a real first step + the single-step graph (warm-up, BLAS handles)
+                return 1
+            self._chunk_key = key
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self._graph_pool):
+                for _ in range(k):
+                    self._rollout_step_device()   # recorded, not executed
+            self._chunk_graph = g
+        self._chunk_graph.replay()
+        return k
+
     def _rollout_step_host(self):
         """Same kernels around a host VecEnv (numpy in/out, reset_obs in infos)."""
         env, dev = self.envs, self.device
@@ -473,13 +497,20 @@ class _OnPolicyAgent:
             step_fn = self._rollout_step_host
         else:
             step_fn = self._rollout_step_graph if self.use_graph else self._rollout_step_device
-        for _ in range(train_steps):
+        chunk = self.graph_chunk if (self.device_env and self.use_graph) else 1
+        left = train_steps
+        while left > 0:
             t0 = time.perf_counter()
-            step_fn()
-            self._t += 1
+            if chunk > 1 and left >= chunk and self._t % chunk == 0 and self.n_steps - self._t >= chunk:
+                k = self._rollout_chunk_graph(chunk)
+            else:
+                step_fn()
+                k = 1
+            left -= k
+            self._t += k
             self.memory.ptr = self._t % self.n_steps
-            self.memory.size = min(self.memory.size + 1, self.n_steps)
-            self.current_step += self.n_envs
+            self.memory.size = min(self.memory.size + k, self.n_steps)
+            self.current_step += self.n_envs * k
             t1 = time.perf_counter()
             self.timers["rollout"] += t1 - t0
             if self._t == self.n_steps:
