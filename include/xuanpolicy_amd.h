@@ -490,6 +490,22 @@ int xpa_thin_linear_act_bwd(int act, const float *g, int64_t ldg, const float *h
                             const float *x, int64_t ldx, int64_t d_in, int64_t d_out, float slope, float *partial_dw,
                             float *partial_db, xpa_stream_t stream);
 
+/* C3 / C5 convolutional trunk (AC_CNN_Atari xuance/torch/representations/cnn.py:45-93, Basic_CNN :5-40): the
+ * elementwise passes around the MIOpen convolutions, every tensor NHWC ([rows = B*H*W, C] row-major).
+ * K20: dst[i] = float32(src[i] / 255.0) with the reference's arithmetic (NumPy float64 division, then the
+ * float32 cast; cnn.py:89-92), bit for bit; n bytes in, n floats out (16-B aligned buffers take the vector path). */
+int xpa_frames_to_f32(const uint8_t *src, int64_t n, float *dst, xpa_stream_t stream);
+/* K21: y = act(y + bias) in place over [rows, cols] (bias [cols] or NULL): the conv / Linear bias and the
+ * activation of cnn_block / mlp_block (xuance/torch/utils/layers.py:8-57).  cols % 4 == 0 and cols / 4 must
+ * divide 256; act 0 identity, 1 LeakyReLU(slope) / ReLU, 2 tanh. */
+int xpa_bias_act(int act, float *y, int64_t rows, int64_t cols, const float *bias, float slope, xpa_stream_t stream);
+/* K22: dz = dh * act'(h) (dz may alias dh; NULL: not written) and per-block column sums of dz, the bias gradient
+ * (xpa_act_bwd_bias_num_partials(rows, cols) rows of cols, reduced by xpa_colsum_finalize): the backward of
+ * K21 over a conv / fc layer's output.  Same cols constraint as K21; 16-B aligned. */
+int64_t xpa_act_bwd_bias_num_partials(int64_t rows, int64_t cols);
+int xpa_act_bwd_bias(int act, const float *dh, const float *h, int64_t rows, int64_t cols, float slope, float *dz,
+                     float *partials, xpa_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

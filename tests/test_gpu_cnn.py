@@ -1,0 +1,137 @@
+"""GPU: the C3 CNN trunk kernels (K20 frames -> f32, K21 bias + activation, K22 activation backward + bias
+gradient) against their PyTorch definitions, and the explicit AC_CNN_Atari actor-critic forward/backward
+(fused_cnn.FusedCNNActorCritic) against autograd through the reference-layout modules."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _setup():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _lib():
+    from xuanpolicy_amd import _lib, ops
+    return _lib, ops
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 1000, 28224 * 3 + 5, 28224 * 64])
+def test_frames_to_f32_is_the_reference_division(n):
+    """K20 == float32(uint8 / 255.0 in float64) (cnn.py:89-92, NumPy semantics) bit for bit, ragged tails and an
+    unaligned source included."""
+    _l, ops = _lib()
+    g = torch.Generator(device="cpu").manual_seed(n)
+    x = torch.randint(0, 256, (n + 1,), generator=g, dtype=torch.int32).to(torch.uint8)
+    for src in (x[:n], x[1:]):
+        xd = src.to(DEV)
+        out = torch.full((n,), -1.0, device=DEV)
+        _l.check(ops.lib().xpa_frames_to_f32(ops._p(xd), n, ops._p(out), ops._stream(DEV)), "frames")
+        ref = (src.numpy() / 255.0).astype(np.float32)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("rows,cols", [(7, 32), (4096, 64), (100003, 32), (333, 512), (64, 4)])
+@pytest.mark.parametrize("act,slope", [(0, 0.0), (1, 0.0), (1, 0.01), (2, 0.0)])
+def test_bias_act_and_backward(rows, cols, act, slope):
+    _l, ops = _lib()
+    g = torch.Generator(device="cpu").manual_seed(rows + cols + act)
+    z = torch.randn(rows, cols, generator=g).to(DEV)
+    b = torch.randn(cols, generator=g).to(DEV)
+    y = z.clone()
+    _l.check(ops.lib().xpa_bias_act(act, ops._p(y), rows, cols, ops._p(b), slope, ops._stream(DEV)), "bias_act")
+    zb = z + b
+    ref = {0: zb, 1: torch.nn.functional.leaky_relu(zb, slope), 2: torch.tanh(zb)}[act]
+    torch.testing.assert_close(y, ref, rtol=1e-6, atol=1e-6)
+    # backward: dz = dh * act'(y), bias gradient = column sums of dz (f64 finalize)
+    dh = torch.randn(rows, cols, generator=g).to(DEV)
+    G = int(ops.lib().xpa_act_bwd_bias_num_partials(rows, cols))
+    part = torch.empty(G, cols, device=DEV)
+    dz = dh.clone()
+    _l.check(ops.lib().xpa_act_bwd_bias(act, ops._p(dz), ops._p(y), rows, cols, slope, ops._p(dz), ops._p(part),
+                                        ops._stream(DEV)), "act_bwd_bias")
+    db = torch.empty(cols, device=DEV)
+    _l.check(ops.lib().xpa_colsum_finalize(ops._p(part), G, cols, ops._p(db), ops._stream(DEV)), "finalize")
+    if act == 0:
+        rdz = dh
+    elif act == 1:
+        rdz = torch.where(y > 0, dh, dh * slope)
+    else:
+        rdz = dh * (1 - y * y)
+    if act == 1:
+        torch.testing.assert_close(dz, rdz, rtol=0, atol=0)
+    elif act == 2:   # dh * (1 - h^2): fp-contraction differs from torch's by an ulp
+        torch.testing.assert_close(dz, rdz, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(db.double(), rdz.double().sum(0), rtol=1e-5, atol=1e-4)
+
+
+def _c3_policy(K=6, seed=0):
+    from xuanpolicy_amd.policies import AC_CNN_Atari, Categorical_AC_Policy
+
+    class _Disc:
+        n, shape = K, ()
+    torch.manual_seed(seed)
+    rep = AC_CNN_Atari((84, 84, 4), [8, 4, 3], [4, 2, 1], [32, 64, 64], None, torch.nn.init.orthogonal_,
+                       torch.nn.ReLU, DEV, [512])
+    return Categorical_AC_Policy(_Disc(), rep, [], [], None, torch.nn.init.orthogonal_, torch.nn.ReLU, DEV)
+
+
+@pytest.mark.parametrize("B", [96, 257])
+def test_fused_cnn_matches_autograd(B):
+    """FusedCNNActorCritic forward (logits, v) and every parameter gradient for given d logits / d v == autograd
+    through the reference-layout modules (AC_CNN_Atari: uint8 / 255, NCHW convs with bias, ReLU, Flatten in
+    (C, H, W) order, fc, heads)."""
+    from xuanpolicy_amd.fused_cnn import FusedCNNActorCritic
+    pol = _c3_policy()
+    # non-trivial biases so the bias paths are exercised
+    with torch.no_grad():
+        for n, p in pol.named_parameters():
+            if n.endswith("bias"):
+                p.normal_(0, 0.1)
+    g = torch.Generator(device="cpu").manual_seed(B)
+    x = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.int32).to(torch.uint8).to(DEV)
+    d_head = (torch.randn(B, 6, generator=g) / B).to(DEV)
+    d_v = (torch.randn(B, generator=g) / B).to(DEV)
+    # explicit path
+    fc = FusedCNNActorCritic(pol)
+    for p in pol.parameters():
+        p.grad = torch.full_like(p, float("nan"))   # every gradient must be overwritten
+    h2, _, v2, ctx = fc.forward(x)
+    (hs, flat, fouts), s_state, _, _ = ctx
+    # float64 CPU reference through the reference-layout modules (NCHW convs with bias, Flatten in (C, H, W)
+    # order).  Its ReLUs take their masks from the explicit path's own activations: a unit within an ulp of the
+    # kink may flip between two f32 paths (different conv algorithms), which would move that unit's whole
+    # gradient contribution — the arithmetic under test is the backward, not the kink's side.
+    import copy
+    pol64 = copy.deepcopy(pol).to("cpu").double()
+    masks = [(y > 0).permute(0, 3, 1, 2).cpu().double() for y in hs[1:]] + [(f > 0).cpu().double() for f in fouts]
+    h = (x.cpu().double() / 255.0).permute(0, 3, 1, 2)
+    relu_plain = h.new_zeros(())
+    k = 0
+    for mod in pol64.representation.model:
+        if isinstance(mod, torch.nn.ReLU):
+            plain = torch.relu(h)
+            relu_plain = torch.maximum(relu_plain, (plain - h * masks[k]).abs().max().detach())
+            h = h * masks[k]
+            k += 1
+        else:
+            h = mod(h)
+    l64, v64 = pol64.actor.model(h), pol64.critic(h)
+    torch.testing.assert_close(h2.cpu().double(), l64.detach(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(v2.cpu().double(), v64.detach(), rtol=1e-4, atol=1e-5)
+    assert float(relu_plain) < 1e-5   # the borrowed masks differ from f64's own only at near-zero units
+    pol64.zero_grad()
+    torch.autograd.backward([l64, v64], [d_head.cpu().double(), d_v.cpu().double()])
+    ref = {n: p.grad.detach() for n, p in pol64.named_parameters()}
+    fc.backward(ctx, d_head, d_v)
+    bad = []
+    for n, p in pol.named_parameters():
+        scale = float(ref[n].abs().max()) + 1e-12
+        err = float((p.grad.cpu().double() - ref[n]).abs().max())
+        if not err <= 2e-5 * scale + 1e-8:
+            bad.append((n, err, scale))
+    assert not bad, bad

@@ -17,7 +17,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "libxuanpolicy_amd.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
 SOURCES = ["gae.hip", "loss.hip", "rollout.hip", "optim.hip", "mlp.hip", "head.hip", "thin.hip", "per.hip", "atari.hip",
-           "classic.hip", "dqn.hip"]
+           "classic.hip", "dqn.hip", "conv.hip"]
 HEADER = os.path.join(REPO_DIR, "include", "xuanpolicy_amd.h")
 
 ABI_VERSION = 1
@@ -64,6 +64,10 @@ SIGNATURES = {
     "xpa_act_bwd_num_partials": (c_i64, [c_i64]),
     "xpa_act_bwd_colsum": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_i64, c_i64, c_f32, c_p, c_p, c_p]),
     "xpa_colsum_finalize": (ctypes.c_int, [c_p, c_i64, c_i64, c_p, c_p]),
+    "xpa_frames_to_f32": (ctypes.c_int, [c_p, c_i64, c_p, c_p]),
+    "xpa_bias_act": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_p, c_f32, c_p]),
+    "xpa_act_bwd_bias_num_partials": (c_i64, [c_i64, c_i64]),
+    "xpa_act_bwd_bias": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_i64, c_i64, c_f32, c_p, c_p, c_p]),
     "xpa_head_bwd_num_partials": (c_i64, [c_i64]),
     "xpa_head_backward": (ctypes.c_int, [ctypes.c_int, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_f32, c_p, c_p, c_p,
                                          c_p, c_p]),

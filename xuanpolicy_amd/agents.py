@@ -151,6 +151,12 @@ class _OnPolicyAgent:
             self.slot_t = torch.full((N,), -1, dtype=torch.int32, device=dev)
             self.slot_overflow = torch.zeros((1,), dtype=torch.int32, device=dev)
             self._overflow_host = self._overflow_event = None
+        # Raw-frame device envs whose truncations are always terminal (SynthAtari): K8 gets no per-step bootstrap
+        # values (every mid-rollout close is terminal, boot 0) and the last step's are formed after the rollout —
+        # one critic forward per iteration instead of one per env step (a2c_agent.py:66-72, 86-98).
+        self.raw_defer = (self.raw_obs and self.device_env and bool(_cfg(config, "defer_bootstrap", True))
+                          and bool(getattr(envs, "truncation_implies_terminal", False)))
+        self._zero_vboot = torch.zeros((N,), **f32) if self.raw_defer else None
         self._graph = None
         self._graph_pool = None
         # device env steps per replayed graph (train() falls back to single-step replays at chunk boundaries it
@@ -224,10 +230,21 @@ class _OnPolicyAgent:
             fm.rollout_act(self._policy_in, self.dist, self.cursor, self.seed, mem.actions, logp_buf, mem.values,
                            env_in, act_clip=1.0, env=env)
             return
-        with torch.no_grad():
-            head, logstd, v = policy_heads(self.policy, self._policy_in)
+        head, logstd, v = self._heads(self._policy_in)
         ops.rollout_sample(self.dist, head.contiguous(), logstd, v.contiguous(), self.cursor, self.seed,
                            mem.actions, logp_buf, mem.values, env_in, act_clip=1.0)
+
+    def _rollout_cnn(self):
+        """The learner's explicit CNN forward (fused_cnn.FusedCNNActorCritic) for raw-frame policies, else None."""
+        get = getattr(self.learner, "_fused_cnn", None)
+        return get() if (get is not None and self.raw_obs) else None
+
+    @torch.no_grad()
+    def _heads(self, x):
+        fc = self._rollout_cnn() if x.dtype == torch.uint8 else None
+        if fc is not None:
+            return fc.heads(x)
+        return policy_heads(self.policy, x)
 
     def _act_scratch(self):
         if getattr(self, "_env_in", None) is None:
@@ -238,8 +255,7 @@ class _OnPolicyAgent:
     def _post(self, rew, term, trunc, final_obs):
         mem = self.memory
         if self.raw_obs:
-            with torch.no_grad():
-                v_boot = policy_heads(self.policy, final_obs)[2]
+            v_boot = self._zero_vboot if self.raw_defer else self._heads(final_obs)[2]
             self._post_kernel(rew, term, trunc, v_boot)
             return
         if self.defer_boot:
@@ -404,6 +420,23 @@ class _OnPolicyAgent:
                 v = policy_heads(self.policy, x)[2].contiguous()
         return v.reshape(-1)
 
+    def _raw_last_bootstraps(self):
+        """raw_defer: V(final frames of the last step) for the last column's bootstraps (0 where terminal), written
+        by xpa_rollout_bootstrap_fixup; a mid-rollout non-terminal close (which would have needed its own value)
+        contradicts the env's truncation_implies_terminal contract and raises."""
+        mem = self.memory
+        T = self.n_steps
+        bad = bool(((mem.closed[:, :T - 1] != 0) & (mem.terminals[:, :T - 1] == 0)).any())
+        if bad:
+            raise RuntimeError("a non-terminal truncation inside the rollout: the env breaks truncation_implies_"
+                               "terminal; set config.defer_bootstrap = False")
+        N = self.n_envs
+        if getattr(self, "_raw_vb", None) is None:
+            self._raw_vb = torch.zeros((2 * N,), dtype=torch.float32, device=self.device)
+            self._raw_slots = torch.full((N,), -1, dtype=torch.int32, device=self.device)
+        self._raw_vb[N:].copy_(self._heads(self.envs.final_obs)[2])
+        ops.bootstrap_fixup(self._raw_vb, self._raw_slots, mem.terminals, mem.boot)
+
     def _check_overflow(self):
         # An env truncating twice in one rollout cannot happen for the device envs (their one truncation source is
         # the time limit and max_episode_steps >= n_steps, see __init__), so the flag is checked without a host
@@ -419,6 +452,8 @@ class _OnPolicyAgent:
     def _update_phase(self):
         mem = self.memory
         mem.size = self.n_steps
+        if self.raw_defer:
+            self._raw_last_bootstraps()
         zc = None
         if (self.defer_boot and not self.atari and not mem._pending and self.fuse_value_gae
                 and ops.gae_value_ok(self.n_steps) and self._rollout_mlp() is not None):
@@ -501,6 +536,10 @@ class _OnPolicyAgent:
         left = train_steps
         while left > 0:
             t0 = time.perf_counter()
+            if self._t == 0:
+                fc = self._rollout_cnn()
+                if fc is not None:
+                    fc.refresh()   # outside any captured graph: the replays read the refreshed weight copy
             if chunk > 1 and left >= chunk and self._t % chunk == 0 and self.n_steps - self._t >= chunk:
                 k = self._rollout_chunk_graph(chunk)
             else:

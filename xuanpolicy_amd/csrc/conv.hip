@@ -1,0 +1,209 @@
+// C3 / C5 convolutional trunk (AC_CNN_Atari / Basic_CNN), the elementwise passes around the MIOpen
+// convolutions and hipBLASLt GEMMs, gfx950.  Every tensor is NHWC ([rows = B*H*W, C] row-major), the layout the
+// uint8 frames arrive in, so no pass needs a permute.
+//
+//   K20 xpa_frames_to_f32    uint8 frames -> float32 / 255, as the reference's `observations / 255.0` (NumPy
+//                            float64 division) + torch.as_tensor(..., float32) (xuance/torch/representations/
+//                            cnn.py:89-92): a 256-entry table of float32(i / 255.0) in LDS, so every value is the
+//                            reference's double-rounded one bit for bit.  1 B read + 4 B written per pixel.
+//   K21 xpa_bias_act         y = act(y + b) in place over [rows, C]: the conv's bias (run bias-free by MIOpen)
+//                            and the ReLU of cnn_block / mlp_block (xuance/torch/utils/layers.py:8-57) in one
+//                            pass instead of MIOpen's bias op + torch's activation (8 B per element).
+//   K22 xpa_act_bwd_bias     dz = dh * act'(h) in place + per-block column sums of dz (the bias gradient), one
+//                            pass over [rows, C] (12 B per element): the ReLU backward and the bias-gradient
+//                            reduction of the conv / fc layers; a fixed grid (<= 2048 blocks) so the f64 finalize
+//                            (xpa_colsum_finalize) reads few partials.  K10's form for conv-sized row counts.
+#include "xpa_common.h"
+
+namespace {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// Lane = one dword (4 pixels) per step of 64 dwords: every load instruction reads 256 contiguous bytes of the
+// wave and every store writes 1 KiB contiguous (a lane that converted 16 B and wrote 4 float4 made each store
+// instruction hit 64 B strides, 4.5x slower: r02 C3 trace); 4 dwords in flight per lane.
+__global__ __launch_bounds__(256) void frames_to_f32_kernel(const unsigned *__restrict__ src, int64_t n4,
+                                                            f4v *__restrict__ dst) {
+    __shared__ float lut[256];
+    lut[threadIdx.x] = (float)((double)threadIdx.x / 255.0);  // NumPy: uint8 / 255.0 in f64, then float32
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t base = wave * 256; base < n4; base += nw * 256) {  // a wave's 4 x 64 dwords per step
+        unsigned w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = base + k * 64 + lane;
+            w[k] = i < n4 ? __builtin_nontemporal_load(src + i) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = base + k * 64 + lane;
+            const unsigned x = w[k];
+            const f4v o = {lut[x & 0xffu], lut[(x >> 8) & 0xffu], lut[(x >> 16) & 0xffu], lut[x >> 24]};
+            if (i < n4) __builtin_nontemporal_store(o, dst + i);
+        }
+    }
+}
+
+// the scalar remainder (n % 16, or every element of a misaligned buffer)
+__global__ __launch_bounds__(256) void frames_to_f32_tail(const uint8_t *__restrict__ src, int64_t n0, int64_t n,
+                                                          float *__restrict__ dst) {
+    for (int64_t i = n0 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        dst[i] = (float)((double)src[i] / 255.0);
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_fwd(float z, float slope) {
+    if (ACT == 1) return z > 0.f ? z : z * slope;
+    if (ACT == 2) return tanhf(z);
+    return z;
+}
+
+// C % 4 == 0, C / 4 divides 256: a thread's column quad is fixed across the grid-stride loop (the stride,
+// gridDim * 256 quads, is a multiple of C / 4), so its bias quad is loaded once.
+template <int ACT, bool BIAS>
+__global__ __launch_bounds__(256) void bias_act_kernel(f4v *__restrict__ y, int64_t n4, int cq,
+                                                       const f4v *__restrict__ b, float slope) {
+    const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    f4v bq = {0.f, 0.f, 0.f, 0.f};
+    if (BIAS) bq = b[i0 % cq];
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = i0; i < n4; i += stride) {
+        f4v v = y[i];
+        if (BIAS) v += bq;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = act_fwd<ACT>(v[e], slope);
+        y[i] = v;
+    }
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_grad(float dh, float h, float slope) {
+    if (ACT == 1) return h > 0.f ? dh : dh * slope;  // mask from the OUTPUT: h > 0 <=> z > 0 for slope >= 0
+    if (ACT == 2) return dh * (1.0f - h * h);
+    return dh;
+}
+
+constexpr int kBiasGradBlocks = 2048;
+constexpr int kUnroll = 4;
+
+// Thread = (row group g, column quad c4); the block's row groups stride the rows by gridDim * groups; kUnroll
+// rows' loads are issued before any of their (in-place) stores.  LDS combine of the row groups in a fixed order.
+template <int ACT>
+__global__ __launch_bounds__(256) void act_bwd_bias_kernel(const float *dh, const float *__restrict__ h,
+                                                           int64_t rows, int C, float slope, float *dz,
+                                                           float *__restrict__ partials) {
+    extern __shared__ __attribute__((aligned(16))) f4v s_acc[];
+    const int cq = C / 4, groups = 256 / cq;
+    const int c4 = threadIdx.x % cq, g = threadIdx.x / cq;
+    f4v acc = {0.f, 0.f, 0.f, 0.f};
+    const int64_t stride = (int64_t)gridDim.x * groups;
+    for (int64_t r0 = (int64_t)blockIdx.x * groups + g; r0 < rows; r0 += kUnroll * stride) {
+        f4v d[kUnroll], hv[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t r = r0 + u * stride;
+            const int64_t off = (r < rows ? r : r0) * C + 4 * c4;
+            d[u] = *reinterpret_cast<const f4v *>(dh + off);
+            if (ACT != 0) hv[u] = *reinterpret_cast<const f4v *>(h + off);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t r = r0 + u * stride;
+            if (r < rows) {
+                f4v v = d[u];
+                if (ACT != 0) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = act_grad<ACT>(v[e], hv[u][e], slope);
+                    if (dz) *reinterpret_cast<f4v *>(dz + r * C + 4 * c4) = v;
+                }
+                acc += v;
+            }
+        }
+    }
+    s_acc[g * cq + c4] = acc;
+    __syncthreads();
+    if ((int)threadIdx.x < cq) {
+        f4v t = {0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < groups; ++k) t += s_acc[k * cq + threadIdx.x];
+        *reinterpret_cast<f4v *>(partials + (int64_t)blockIdx.x * C + 4 * threadIdx.x) = t;
+    }
+}
+
+int grid_for(int64_t work, int64_t per_block, int64_t cap) {
+    int64_t g = (work + per_block - 1) / per_block;
+    if (g > cap) g = cap;
+    return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace
+
+XPA_API int xpa_frames_to_f32(const uint8_t *src, int64_t n, float *dst, xpa_stream_t stream) {
+    if (n < 0 || (n > 0 && (!src || !dst))) return (int)hipErrorInvalidValue;
+    if (n == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    const bool vec = ((uintptr_t)src % 4 == 0) && ((uintptr_t)dst % 16 == 0);
+    const int64_t n4 = vec ? n / 4 : 0;
+    if (n4 > 0) {  // 1024 dwords per block per step, <= 8 blocks per CU, grid-stride beyond that
+        const int g = grid_for(n4, 1024, 256 * 8);
+        hipLaunchKernelGGL(frames_to_f32_kernel, dim3((unsigned)g), dim3(256), 0, s, (const unsigned *)src, n4,
+                           (f4v *)dst);
+    }
+    const int64_t n0 = n4 * 4;
+    if (n0 < n)
+        hipLaunchKernelGGL(frames_to_f32_tail, dim3((unsigned)grid_for(n - n0, 256, 4096)), dim3(256), 0, s, src, n0,
+                           n, dst);
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_bias_act(int act, float *y, int64_t rows, int64_t cols, const float *bias, float slope,
+                         xpa_stream_t stream) {
+    if (rows <= 0 || cols <= 0 || cols % 4 || 256 % (cols / 4) || !y || act < 0 || act > 2)
+        return (int)hipErrorInvalidValue;
+    if (((uintptr_t)y | (uintptr_t)(bias ? bias : y)) % 16) return (int)hipErrorInvalidValue;
+    const int cq = (int)(cols / 4);
+    const int64_t n4 = rows * cq;
+    const int g = grid_for(n4, 256, 256 * 8 * 4);
+    hipStream_t s = (hipStream_t)stream;
+#define XPA_BA(A_, B_)                                                                                          \
+    hipLaunchKernelGGL((bias_act_kernel<A_, B_>), dim3((unsigned)g), dim3(256), 0, s, (f4v *)y, n4, cq,          \
+                       (const f4v *)bias, slope)
+    if (bias) {
+        if (act == 0) XPA_BA(0, true);
+        else if (act == 1) XPA_BA(1, true);
+        else XPA_BA(2, true);
+    } else {
+        if (act == 0) return 0;
+        if (act == 1) XPA_BA(1, false);
+        else XPA_BA(2, false);
+    }
+#undef XPA_BA
+    return xpa_launch_status();
+}
+
+XPA_API int64_t xpa_act_bwd_bias_num_partials(int64_t rows, int64_t cols) {
+    if (rows <= 0 || cols <= 0 || cols % 4 || 256 % (cols / 4)) return 0;
+    const int64_t groups = 256 / (cols / 4);
+    return grid_for(rows, groups * kUnroll, kBiasGradBlocks);
+}
+
+XPA_API int xpa_act_bwd_bias(int act, const float *dh, const float *h, int64_t rows, int64_t cols, float slope,
+                             float *dz, float *partials, xpa_stream_t stream) {
+    const int64_t G = xpa_act_bwd_bias_num_partials(rows, cols);
+    if (G <= 0 || !dh || !partials || act < 0 || act > 2 || (act != 0 && !h)) return (int)hipErrorInvalidValue;
+    if (((uintptr_t)dh | (uintptr_t)(h ? h : dh) | (uintptr_t)(dz ? dz : dh) | (uintptr_t)partials) % 16)
+        return (int)hipErrorInvalidValue;
+    const int C = (int)cols;
+    const size_t lds = 256 * sizeof(f4v);
+    hipStream_t s = (hipStream_t)stream;
+#define XPA_ABB(A_)                                                                                               \
+    hipLaunchKernelGGL((act_bwd_bias_kernel<A_>), dim3((unsigned)G), dim3(256), lds, s, dh, h, rows, C, slope, dz, \
+                       partials)
+    if (act == 0) XPA_ABB(0);
+    else if (act == 1) XPA_ABB(1);
+    else XPA_ABB(2);
+#undef XPA_ABB
+    return xpa_launch_status();
+}

@@ -193,6 +193,10 @@ class SynthAtariVecEnv:
         self.num_envs, self.n_actions = int(n_envs), int(n_actions)
         self.seed, self.max_episode_steps = int(seed), int(max_episode_steps)
         self.max_episode_length = self.max_episode_steps
+        # the reference's Atari flag rules (gym_env.py:193-209): a game over or the step limit sets terminated AND
+        # truncated, so a truncation never needs a bootstrap value (finish_path(0)) — the agent then evaluates the
+        # critic only on the last step's observations, once per rollout
+        self.truncation_implies_terminal = True
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.shard = int(shard)
         self.noise_seed = (self.seed ^ ((0x9E3779B9 * self.shard) & 0xFFFFFFFF)) & 0xFFFFFFFF

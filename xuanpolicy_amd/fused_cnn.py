@@ -1,0 +1,250 @@
+"""Explicit (autograd-free) forward / backward of an actor-critic on the AC_CNN_Atari trunk (C3).
+
+Reference: AC_CNN_Atari xuance/torch/representations/cnn.py:45-93 (conv blocks with padding (k - s) // 2 + ReLU,
+Flatten, fc blocks), cnn_block / mlp_block xuance/torch/utils/layers.py:8-57, Categorical_AC_Policy
+xuance/torch/policies/categorical.py:61-85; the learner's loss.backward() a2c_learner.py:31-33.
+
+Every activation stays NHWC ([rows = B*H*W, C] row-major), the layout the uint8 frames arrive in:
+  forward   K20 xpa_frames_to_f32 (uint8 -> float32 / 255, the reference's arithmetic bit for bit)
+            -> per conv: MIOpen conv2d without bias on the channels-last view -> K21 xpa_bias_act (bias + ReLU
+               in place)
+            -> Flatten in NHWC order: the first fc layer uses its weight with the columns permuted from the
+               reference's (C, H, W) order to (H, W, C) (one 13 MB copy per parameter update, instead of an
+               NHWC -> NCHW copy of the [B, 6400] activations every forward)
+            -> fc: hipBLASLt GEMM (bias epilogue) -> K21 ReLU in place -> heads (GEMMs)
+  backward  heads: GEMMs + K10 bias column sums -> fc: K22 xpa_act_bwd_bias (ReLU backward + bias gradient) ->
+            dW GEMM (permuted back into the reference layout) + dX GEMM -> per conv: K22 then MIOpen
+            convolution_backward (data, weight; no dX for the first conv).
+Parameter gradients are written into the parameters' .grad views (the flat buffer of xuanpolicy_amd.flat).
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib, ops
+from .fused_mlp import _act_code, _parse
+from .policies import AC_CNN_Atari
+
+
+def _conv_layers(model):
+    convs, rest, i = [], [], 0
+    mods = list(model)
+    while i < len(mods) and isinstance(mods[i], nn.Conv2d):
+        conv = mods[i]
+        act = mods[i + 1] if i + 1 < len(mods) and not isinstance(mods[i + 1], (nn.Conv2d, nn.Flatten)) else None
+        if conv.bias is None or conv.groups != 1 or tuple(conv.dilation) != (1, 1):
+            raise ValueError("expected Conv2d with bias, groups 1, dilation 1")
+        convs.append((conv,) + _act_code(act))
+        i += 2 if act is not None else 1
+    if i >= len(mods) or not isinstance(mods[i], nn.Flatten):
+        raise ValueError("expected Flatten after the conv blocks")
+    return convs, _parse(mods[i + 1:])
+
+
+class FusedCNNActorCritic:
+    """Built from a Categorical/Gaussian actor-critic policy with an AC_CNN_Atari representation."""
+
+    def __init__(self, policy):
+        rep = policy.representation
+        if not isinstance(rep, AC_CNN_Atari):
+            raise ValueError("representation %r has no explicit CNN path" % type(rep).__name__)
+        self.convs, self.fc = _conv_layers(rep.model)
+        if not self.fc:
+            raise ValueError("AC_CNN_Atari without fc layers")
+        for conv, code, _ in self.convs:
+            if conv.out_channels % 4 or 256 % (conv.out_channels // 4):
+                raise ValueError("conv channels must be a multiple of 4 dividing 1024")
+        self.discrete = bool(getattr(policy, "discrete", False))
+        self.actor = _parse(policy.actor.model if self.discrete else policy.actor.mu)
+        self.critic = _parse(policy.critic.model)
+        self.logstd = None if self.discrete else policy.actor.logstd
+        C, H, W = rep.input_shape
+        self.in_hwc = (H, W, C)
+        shape = (C, H, W)
+        self.out_shapes = []
+        for conv, _, _ in self.convs:
+            k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+            Ho = (shape[1] + 2 * p - k) // s + 1
+            Wo = (shape[2] + 2 * p - k) // s + 1
+            shape = (conv.out_channels, Ho, Wo)
+            self.out_shapes.append(shape)
+        Cl, Hl, Wl = shape
+        fc0 = self.fc[0][0]
+        if fc0.in_features != Cl * Hl * Wl:
+            raise ValueError("fc input width does not match the conv output")
+        self._chw = (Cl, Hl, Wl)
+        self._w_hwc = None      # the first fc weight with (H, W, C)-ordered columns, refreshed after each update
+        self.stale = True
+        self._dw_tmp = None
+        self._partials = {}
+        n_params = sum(1 for _ in policy.parameters())
+        n_cov = 2 * (len(self.convs) + len(self.fc) + len(self.actor) + len(self.critic)) + (0 if self.discrete else 1)
+        if n_params != n_cov:
+            raise ValueError("policy has parameters outside the conv / Linear chains")
+
+    # ------------------------------------------------------------------------------------------------
+    def refresh(self):
+        """Re-derive the (H, W, C)-ordered first fc weight now (the agent calls it before a captured rollout, whose
+        graph must not contain the copy)."""
+        self.stale = True
+        self._fc0_weight()
+
+    def _fc0_weight(self):
+        if self.stale or self._w_hwc is None:
+            w = self.fc[0][0].weight
+            Cl, Hl, Wl = self._chw
+            if self._w_hwc is None:
+                self._w_hwc = torch.empty_like(w)
+            self._w_hwc.view(w.shape[0], Hl, Wl, Cl).copy_(w.view(w.shape[0], Cl, Hl, Wl).permute(0, 2, 3, 1))
+            self.stale = False
+        return self._w_hwc
+
+    @staticmethod
+    def _bias_act(code, y2d, bias, slope):
+        _lib.check(ops.lib().xpa_bias_act(code, ops._p(y2d), y2d.shape[0], y2d.shape[1],
+                                          ops._p(bias) if bias is not None else None, float(slope),
+                                          ops._stream(y2d.device)), "xpa_bias_act")
+
+    def frames(self, x):
+        """uint8 [B, H, W, C] -> float32 / 255 [B, H, W, C] (K20)."""
+        if x.dtype != torch.uint8 or x.device.type != "cuda" or not x.is_contiguous():
+            raise ValueError("frames must be a contiguous uint8 ROCm tensor [B, H, W, C]")
+        out = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+        _lib.check(ops.lib().xpa_frames_to_f32(ops._p(x), x.numel(), ops._p(out), ops._stream(x.device)),
+                   "xpa_frames_to_f32")
+        return out
+
+    @torch.no_grad()
+    def trunk(self, x):
+        """x uint8 [B, H, W, C] -> (state [B, d], context for backward)."""
+        B = x.shape[0]
+        h = self.frames(x.reshape((B,) + self.in_hwc))
+        hs = [h]
+        for conv, code, slope in self.convs:
+            z = F.conv2d(h.permute(0, 3, 1, 2), conv.weight, None, conv.stride, conv.padding)
+            y = z.permute(0, 2, 3, 1)
+            if not y.is_contiguous():
+                y = y.contiguous()
+            self._bias_act(code, y.view(-1, y.shape[3]), conv.bias, slope)
+            hs.append(y)
+            h = y
+        flat = h.reshape(B, -1)                  # (H, W, C) order: no copy
+        fouts = []
+        s = flat
+        for j, (lin, code, slope) in enumerate(self.fc):
+            w = self._fc0_weight() if j == 0 else lin.weight
+            s = F.linear(s, w, lin.bias)
+            if code:
+                self._bias_act(code, s, None, slope)
+            fouts.append(s)
+        return s, (hs, flat, fouts)
+
+    @staticmethod
+    def _chain(layers, x):
+        outs, h = [], x
+        for lin, code, slope in layers:
+            h = F.linear(h, lin.weight, lin.bias)
+            if code == 1:
+                F.leaky_relu(h, slope, inplace=True)
+            elif code == 2:
+                h.tanh_()
+            outs.append(h)
+        return outs
+
+    @torch.no_grad()
+    def forward(self, x):
+        """(logits or mu, logstd or None, v, ctx)."""
+        s, tctx = self.trunk(x)
+        a_outs = self._chain(self.actor, s)
+        c_outs = self._chain(self.critic, s)
+        return a_outs[-1], self.logstd, c_outs[-1][:, 0], (tctx, s, a_outs, c_outs)
+
+    @torch.no_grad()
+    def heads(self, x):
+        head, logstd, v, _ = self.forward(x)
+        return head, logstd, v
+
+    # ------------------------------------------------------------------------------------------------
+    def _part(self, rows, cols, device, k22):
+        key = (rows, cols, k22)
+        p = self._partials.get(key)
+        if p is None:
+            L = ops.lib()
+            G = int(L.xpa_act_bwd_bias_num_partials(rows, cols)) if k22 else int(L.xpa_act_bwd_num_partials(rows))
+            p = torch.empty((G, cols), dtype=torch.float32, device=device)
+            self._partials[key] = p
+        return p
+
+    def _act_bwd_bias(self, code, g2d, h2d, slope, bias_grad):
+        """g2d <- g2d * act'(h2d) in place; bias_grad <- column sums (K22, or K10 for widths K22 does not take)."""
+        rows, cols = g2d.shape
+        L, s = ops.lib(), ops._stream(g2d.device)
+        k22 = cols % 4 == 0 and 256 % (cols // 4) == 0 and g2d.is_contiguous()
+        part = self._part(rows, cols, g2d.device, k22)
+        hp = ops._p(h2d) if code else None
+        gp = ops._p(g2d) if code else None
+        if k22:
+            _lib.check(L.xpa_act_bwd_bias(code, ops._p(g2d), hp, rows, cols, float(slope), gp, ops._p(part), s),
+                       "xpa_act_bwd_bias")
+        else:
+            if not g2d.is_contiguous():
+                raise ValueError("gradient rows must be contiguous")
+            _lib.check(L.xpa_act_bwd_colsum(code, ops._p(g2d), hp, rows, cols, float(slope), gp, ops._p(part), s),
+                       "xpa_act_bwd_colsum")
+        _lib.check(L.xpa_colsum_finalize(ops._p(part), part.shape[0], cols, ops._p(bias_grad), s),
+                   "xpa_colsum_finalize")
+
+    def _chain_backward(self, layers, inputs, outs, g, acc=None):
+        """Linear(+act) chain backward; returns d(input) (added into acc when given)."""
+        for j in range(len(layers) - 1, -1, -1):
+            lin, code, slope = layers[j]
+            g = g.contiguous()
+            self._act_bwd_bias(code, g, outs[j], slope, lin.bias.grad)
+            torch.mm(g.t(), inputs[j], out=lin.weight.grad)
+            if j == 0 and acc is not None:
+                g = acc.addmm_(g, lin.weight)
+            else:
+                g = torch.mm(g, lin.weight)
+        return g
+
+    @torch.no_grad()
+    def backward(self, ctx, d_head, d_v):
+        """Writes every parameter gradient (d_head [B, K], d_v [B]: the loss kernel's outputs)."""
+        (hs, flat, fouts), s, a_outs, c_outs = ctx
+        ds = self._chain_backward(self.actor, [s] + a_outs[:-1], a_outs, d_head)
+        ds = self._chain_backward(self.critic, [s] + c_outs[:-1], c_outs, d_v.view(-1, 1), acc=ds)
+        # fc chain (the first layer's weight is used in (H, W, C) column order)
+        g = ds
+        for j in range(len(self.fc) - 1, -1, -1):
+            lin, code, slope = self.fc[j]
+            x_in = flat if j == 0 else fouts[j - 1]
+            g = g.contiguous()
+            self._act_bwd_bias(code, g, fouts[j], slope, lin.bias.grad)
+            if j == 0:
+                if self._dw_tmp is None:
+                    self._dw_tmp = torch.empty_like(lin.weight)
+                torch.mm(g.t(), x_in, out=self._dw_tmp)
+                Cl, Hl, Wl = self._chw
+                lin.weight.grad.view(lin.out_features, Cl, Hl, Wl).copy_(
+                    self._dw_tmp.view(lin.out_features, Hl, Wl, Cl).permute(0, 3, 1, 2))
+                g = torch.mm(g, self._fc0_weight())
+            else:
+                torch.mm(g.t(), x_in, out=lin.weight.grad)
+                g = torch.mm(g, lin.weight)
+        # conv blocks, last to first; g is the NHWC gradient of the last conv block's output
+        for i in range(len(self.convs) - 1, -1, -1):
+            conv, code, slope = self.convs[i]
+            y = hs[i + 1]
+            g = g.reshape(y.shape)
+            if not g.is_contiguous():
+                g = g.contiguous()
+            self._act_bwd_bias(code, g.view(-1, y.shape[3]), y.view(-1, y.shape[3]), slope, conv.bias.grad)
+            need_in = i > 0
+            gx, gw, _ = torch.ops.aten.convolution_backward(
+                g.permute(0, 3, 1, 2), hs[i].permute(0, 3, 1, 2), conv.weight, None, list(conv.stride),
+                list(conv.padding), [1, 1], False, [0, 0], 1, [need_in, True, False])
+            conv.weight.grad.copy_(gw)
+            if need_in:
+                g = gx.permute(0, 2, 3, 1)
+        self.stale = True   # the optimizer step that follows changes the fc weight
+

@@ -46,6 +46,9 @@ class Learner:
         names = sorted(n for n in os.listdir(path) if n != "obs_rms.npy")
         dev = self.device if self.device is not None else "cpu"
         self.policy.load_state_dict(torch.load(os.path.join(path, names[-1]), map_location=dev, weights_only=True))
+        fc = getattr(self, "_fc", None)
+        if fc:
+            fc.stale = True
 
     def update(self, *args):
         raise NotImplementedError
@@ -92,6 +95,20 @@ class _FusedPolicyGradient(Learner):
             self._fm = fm
         return fm or None
 
+    def _fused_cnn(self):
+        """Explicit CNN actor-critic forward/backward (fused_cnn.FusedCNNActorCritic) for AC_CNN_Atari policies."""
+        fc = getattr(self, "_fc", None)
+        if fc is None:
+            fc = False
+            if getattr(self, "fused_cnn_enabled", True) and self._device().type == "cuda":
+                from .fused_cnn import FusedCNNActorCritic
+                try:
+                    fc = FusedCNNActorCritic(self.policy)
+                except ValueError:
+                    fc = False
+            self._fc = fc
+        return fc or None
+
     def _sync_clip_step(self, sq=None):
         """sq = (partials, count): squared-norm partials of the complete gradient written by its producers
         (valid only without a gradient all-reduce): the fused step skips its norm pass."""
@@ -120,6 +137,25 @@ class _FusedPolicyGradient(Learner):
                                        adv_partials=adv_partials, clip_range=self.clip_range, vf_coef=self.vf_coef,
                                        ent_coef=self.ent_coef)
             self._sync_clip_step(sq=fm.sq_ready)
+            return scalars
+        fc = self._fused_cnn() if fm is None else None
+        if fc is not None and obs.dtype == torch.uint8:
+            # explicit CNN path: K20 frames, MIOpen convs + K21 bias/ReLU, K2 loss, K22 + conv/GEMM backward
+            head, logstd, v, ctx = fc.forward(obs)
+            if self._ws is None or self._ws.batch != head.shape[0]:
+                self._ws = ops.LossWorkspace(head.shape[0], head.shape[1], head.device, self.dist)
+            fg = getattr(self, "flat_grads", None)
+            if fg is None:
+                for p in self._params:
+                    if p.grad is None:
+                        p.grad = torch.zeros_like(p)
+            scalars, dh, _, dv = ops.policy_loss(self.algo, self.dist, head, logstd, v.contiguous(), act, adv, ret,
+                                                 old_logp=old_logp, idx=idx, adv_partials=adv_partials,
+                                                 clip_range=self.clip_range, vf_coef=self.vf_coef,
+                                                 ent_coef=self.ent_coef, ws=self._ws,
+                                                 d_logstd_out=logstd.grad if logstd is not None else None)
+            fc.backward(ctx, dh, dv)       # writes every parameter gradient
+            self._sync_clip_step()
             return scalars
         if fm is not None:
             head, logstd, v, ctx = fm.forward(obs)
@@ -165,6 +201,14 @@ class _FusedPolicyGradient(Learner):
         import numpy as np
         return torch.as_tensor(np.asarray(x), dtype=dtype, device=device).contiguous()
 
+    @classmethod
+    def _obs(cls, x, device):
+        """Observations: raw uint8 frames stay uint8 (the CNN path converts them on device, K20), the rest float32."""
+        import numpy as np
+        if (isinstance(x, torch.Tensor) and x.dtype == torch.uint8) or (isinstance(x, np.ndarray) and x.dtype == np.uint8):
+            return cls._t(x, device, torch.uint8)
+        return cls._t(x, device)
+
     def _device(self):
         return next(self.policy.parameters()).device
 
@@ -181,7 +225,7 @@ class PPOCLIP_Learner(_FusedPolicyGradient):
 
     def update(self, obs_batch, act_batch, ret_batch, value_batch, adv_batch, old_logp):
         dev = self._device()
-        scalars = self.update_fused(self._t(obs_batch, dev), None, self._t(act_batch, dev).reshape(-1),
+        scalars = self.update_fused(self._obs(obs_batch, dev), None, self._t(act_batch, dev).reshape(-1),
                                     self._t(adv_batch, dev), self._t(ret_batch, dev), self._t(old_logp, dev))
         return self._info(scalars)
 
@@ -199,7 +243,7 @@ class A2C_Learner(_FusedPolicyGradient):
 
     def update(self, obs_batch, act_batch, ret_batch, adv_batch):
         dev = self._device()
-        scalars = self.update_fused(self._t(obs_batch, dev), None, self._t(act_batch, dev).reshape(-1),
+        scalars = self.update_fused(self._obs(obs_batch, dev), None, self._t(act_batch, dev).reshape(-1),
                                     self._t(adv_batch, dev), self._t(ret_batch, dev))
         return self._info(scalars)
 
