@@ -427,7 +427,7 @@ def c5_bench(device, n_envs=8, n_size=131072, batch=2048, steps=20, warmup=3, cp
     return res
 
 
-def c3_bench(device, n_envs=1024, n_steps=128, steps=2, warmup=1):
+def c3_bench(device, n_envs=1024, n_steps=128, steps=2, warmup=1, cpu=True, kernels=True):
     """C3 (BASELINE.json configs[2]): A2C, SynthAtari uint8 4x84x84 frames, AC_CNN_Atari, 1024 envs x
     128 steps (a2c/atari.yaml: 4 epochs x 8 minibatches of 16 384), everything resident on the GPU."""
     import torch
@@ -449,7 +449,114 @@ def c3_bench(device, n_envs=1024, n_steps=128, steps=2, warmup=1):
            "host_timer_split_ms": {k: round(v / steps * 1e3, 2) for k, v in agent.timers.items()}}
     del agent
     torch.cuda.empty_cache()
+    if kernels:
+        res["roofline"] = c3_kernels(device)
+    if cpu:
+        res["cpu_baseline"] = c3_cpu_baseline(n_envs, n_steps)
+        res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
     return res
+
+
+def c3_cpu_baseline(n_envs=1024, n_steps=128, n_epoch=4, n_minibatch=8, steps_timed=3, updates_timed=2):
+    """The C3 loop as the reference runs it on the host (a2c_agent.py:57-107): per-env SynthAtari stepping
+    (DummyVecEnv_Atari), the AC_CNN_Atari policy forward on NumPy frames / 255.0 (cnn.py:89-92), the buffer column
+    store and fancy-index sample (memory_tools.py:526-560), and A2C_Learner.update (autograd, clip_grad_norm_,
+    Adam) on torch CPU — restated in oracle/cpu_ref (build_atari_ac_ref, LearnerRef).  Bounded sample:
+    `steps_timed` env steps of all envs and `updates_timed` minibatch updates (B = N T / n_minibatch), extrapolated
+    to one iteration (n_steps steps + n_epoch n_minibatch updates)."""
+    import numpy as np
+    import torch
+    from oracle import cpu_ref, synth_env
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    K = 6
+    pol = cpu_ref.build_atari_ac_ref(K)
+    opt = torch.optim.Adam(pol.parameters(), 7e-4, eps=1e-5)
+    lrn = cpu_ref.LearnerRef(pol, opt, None, "a2c", 0.25, 0.01, 0.0, 0.2, True)
+    envs = [synth_env.SynthAtariEnv(i, seed=1, n_actions=K, max_episode_steps=27000) for i in range(n_envs)]
+    obs = np.stack([e.reset()[0] for e in envs])
+    col = np.zeros_like(obs)
+    t_act = t_env = t_store = 0.0
+    for _ in range(steps_timed):
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            logits, _, v = pol.heads(obs)
+            a = torch.distributions.Categorical(logits=logits).sample().numpy()
+        t1 = time.perf_counter()
+        nxt = []
+        for i, e in enumerate(envs):
+            o, r, te, tr, info = e.step(int(a[i]))
+            if tr:
+                o = e.reset()[0]
+            nxt.append(o)
+        nxt = np.stack(nxt)
+        t2 = time.perf_counter()
+        col[:] = obs
+        t3 = time.perf_counter()
+        obs = nxt
+        t_act, t_env, t_store = t_act + t1 - t0, t_env + t2 - t1, t_store + t3 - t2
+    B = n_envs * n_steps // n_minibatch
+    rng = np.random.default_rng(0)
+    pool = rng.integers(0, 256, (2 * B,) + obs.shape[1:], dtype=np.uint8)
+    t_upd = []
+    for _ in range(updates_timed):
+        t0 = time.perf_counter()
+        idx = rng.permutation(2 * B)[:B]
+        ob = pool[idx]
+        act, ret, adv = rng.integers(0, K, B), rng.normal(0, 1, B).astype(np.float32), rng.normal(0, 1, B)
+        adv = ((adv - adv.mean()) / (adv.std() + 1e-8)).astype(np.float32)
+        lrn.update(ob, act, ret, adv)
+        t_upd.append(time.perf_counter() - t0)
+    step_s = (t_act + t_env + t_store) / steps_timed
+    upd_s = sum(t_upd) / len(t_upd)
+    it_s = n_steps * step_s + n_epoch * n_minibatch * upd_s
+    return {"value": round(n_envs * n_steps / it_s, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": "%d env steps of %d envs (policy forward %.3f s, per-env SynthAtari step %.3f s, store %.3f s per "
+                      "step) + %d A2C updates at B=%d (%.2f s each, incl. the fancy-index sample) -> iteration = %d x "
+                      "%.3f s + %d x %.2f s = %.1f s" % (steps_timed, n_envs, t_act / steps_timed, t_env / steps_timed,
+                                                         t_store / steps_timed, updates_timed, B, upd_s, n_steps,
+                                                         step_s, n_epoch * n_minibatch, upd_s, it_s)}
+
+
+def c3_kernels(device, batch=16384):
+    """K20 / K22 at the C3 update's shapes (minibatch of `batch` frames; conv1's [B*21*21, 32] output), HIP events
+    around single launches on the launch stream, median of 7 (the buffers exceed every cache)."""
+    import torch
+    from xuanpolicy_amd import _lib, ops
+    L = ops.lib()
+    st = ops._stream(device)
+    x = torch.randint(0, 256, (batch, 84, 84, 4), dtype=torch.uint8, device=device)
+    y = torch.empty(x.shape, dtype=torch.float32, device=device)
+    rows, C = batch * 21 * 21, 32
+    g = torch.randn(rows, C, device=device)
+    h = torch.relu(torch.randn(rows, C, device=device))
+    part = torch.empty(int(L.xpa_act_bwd_bias_num_partials(rows, C)), C, device=device)
+
+    def timed(fn, reps=7):
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        ts.sort()
+        return ts[len(ts) // 2]
+    f_us = timed(lambda: _lib.check(L.xpa_frames_to_f32(ops._p(x), x.numel(), ops._p(y), st), "frames"))
+    b_us = timed(lambda: _lib.check(L.xpa_act_bwd_bias(1, ops._p(g), ops._p(h), rows, C, 0.0, ops._p(g), ops._p(part),
+                                                       st), "act_bwd_bias"))
+    fb, bb = 5.0 * x.numel(), 12.0 * rows * C
+    return {"frames_to_f32": {"kernel": "xpa_frames_to_f32 (K20)", "bound": "hbm", "avg_launch_us": round(f_us, 2),
+                              "algorithmic_bytes_per_launch": int(fb), "achieved": round(fb / f_us / 1e3, 1),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(fb / f_us / 1e3 / HBM_PEAK_GBS, 4),
+                              "shape": "%d frames 84x84x4 uint8 -> f32 (1 B read + 4 B written per pixel)" % batch},
+            "act_bwd_bias": {"kernel": "xpa_act_bwd_bias (K22, ReLU)", "bound": "hbm", "avg_launch_us": round(b_us, 2),
+                             "algorithmic_bytes_per_launch": int(bb), "achieved": round(bb / b_us / 1e3, 1),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(bb / b_us / 1e3 / HBM_PEAK_GBS, 4),
+                             "shape": "conv1 output [%d x 21 x 21, 32] (dh, h read, dz written: 12 B per element)"
+                                      % batch}}
 
 
 def c4_bench(device, rank, world, n_envs=4096, n_steps=128, steps=2, warmup=1):
@@ -743,7 +850,7 @@ def main():
         if not args.no_c1 and world == 1:
             result["c1_cartpole"] = c1_bench(device)
         if not args.no_c3 and world == 1:
-            result["c3_atari_a2c"] = c3_bench(device)
+            result["c3_atari_a2c"] = c3_bench(device, cpu=not args.no_cpu_baseline, kernels=not args.no_kernel_timing)
         if not args.no_per and world == 1:
             result["per_kernels"] = per_bench(device)
             cr = result["per_kernels"].get("cpu_reference_restated", {})

@@ -392,6 +392,63 @@ def build_actor_critic_ref(obs_dim, act_dim, rep_hidden, actor_hidden, critic_hi
     return AC()
 
 
+def build_atari_ac_ref(n_actions, filters=(32, 64, 64), kernels=(8, 4, 3), strides=(4, 2, 1), fc=(512,),
+                       in_shape=(84, 84, 4)):
+    """Categorical actor-critic on AC_CNN_Atari with the reference's layout (cnn.py:45-93: conv blocks with padding
+    (k - s) // 2 + ReLU, Flatten in (C, H, W) order, fc blocks; categorical.py:61-85 with empty actor / critic hidden
+    lists) and its input arithmetic: observations / 255.0 in NumPy float64, transposed to NCHW, cast to float32."""
+    torch = _torch()
+    nn = torch.nn
+    C, H, W = in_shape[2], in_shape[0], in_shape[1]
+    layers, c, h, w = [], C, H, W
+    for f, k, s in zip(filters, kernels, strides):
+        p = (k - s) // 2
+        conv = nn.Conv2d(c, f, k, s, padding=p)
+        nn.init.orthogonal_(conv.weight, gain=np.sqrt(2))
+        nn.init.constant_(conv.bias, 0)
+        layers += [conv, nn.ReLU()]
+        c, h, w = f, (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    layers.append(nn.Flatten())
+    d = c * h * w
+    for hdim in fc:
+        lin = nn.Linear(d, hdim)
+        nn.init.orthogonal_(lin.weight, gain=np.sqrt(2))
+        nn.init.constant_(lin.bias, 0)
+        layers += [lin, nn.ReLU()]
+        d = hdim
+
+    class Rep(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.model = nn.Sequential(*layers)
+
+        def forward(self, obs):
+            x = np.asarray(obs) / 255.0
+            return {"state": self.model(torch.as_tensor(np.transpose(x, (0, 3, 1, 2)), dtype=torch.float32))}
+
+    class AC(nn.Module):
+        discrete = True
+
+        def __init__(self):
+            super().__init__()
+            self.representation = Rep()
+            self.actor = nn.Module()
+            self.actor.model = nn.Sequential(nn.Linear(d, n_actions))
+            self.critic_head = nn.Sequential(nn.Linear(d, 1))
+            for lin in (self.actor.model[0], self.critic_head[0]):
+                nn.init.orthogonal_(lin.weight)
+                nn.init.constant_(lin.bias, 0)
+
+        def heads(self, obs):
+            s = self.representation(obs)["state"]
+            return self.actor.model(s), None, self.critic_head(s)[:, 0]
+
+        def dist(self, head, logstd):
+            return torch.distributions.Categorical(logits=head)
+
+    return AC()
+
+
 class LearnerRef:
     """ppoclip_learner.py:24-65 / a2c_learner.py:19-50 on torch CPU (autograd, Adam, LinearLR)."""
 
@@ -405,7 +462,8 @@ class LearnerRef:
     def update(self, obs, act, ret, adv, old_logp=None):
         torch = _torch()
         self.iterations += 1
-        obs = torch.as_tensor(obs, dtype=torch.float32)
+        if not (isinstance(obs, np.ndarray) and obs.dtype == np.uint8):   # raw frames: the policy scales them
+            obs = torch.as_tensor(obs, dtype=torch.float32)
         act = torch.as_tensor(act)
         ret = torch.as_tensor(ret)
         adv = torch.as_tensor(adv)

@@ -1,4 +1,5 @@
-"""Run the C3 leg of bench.py alone (for rocprofv3 --kernel-trace): python tools/c3_run.py [iterations]"""
+"""Run the C3 leg of bench.py alone (for rocprofv3 --kernel-trace): python tools/c3_run.py [iterations] [--full]
+(--full adds the kernel roofline and the bounded CPU baseline)."""
 import json
 import os
 import sys
@@ -8,5 +9,6 @@ import bench  # noqa: E402
 
 if __name__ == "__main__":
     import torch
-    it = int(sys.argv[1]) if len(sys.argv) > 1 else 1
-    print(json.dumps(bench.c3_bench(torch.device("cuda:0"), steps=it, warmup=1)))
+    it = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 1
+    full = "--full" in sys.argv
+    print(json.dumps(bench.c3_bench(torch.device("cuda:0"), steps=it, warmup=1, cpu=full, kernels=full)))
