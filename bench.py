@@ -750,10 +750,10 @@ def main():
             gb_k1 = gae_bytes(N, T, mid_trunc)
             ach = gb / gae_ms / 1e6
             traffic = None
-            pmc = os.path.join(REPO, "profiles", "pmc_gae_compact_r01.json")
+            pmc = os.path.join(REPO, "profiles", "pmc_gae_r02.json")   # tools/gae_pmc.py + tools/pmc_summary.py
             if os.path.exists(pmc):
                 with open(pmc) as f:
-                    traffic = json.load(f).get("hbm_bytes_per_launch")
+                    traffic = json.load(f).get("hbm_bytes_per_launch_" + form)
             if form == "value":
                 act_code = agent.learner._fused_mlp().critic[-2][1]
                 kname = "xpa_gae_scan_value: critic output layer + bootstrap fixup + GAE (gae_dpp_kernel<5, 1, %d>)" \

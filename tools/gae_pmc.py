@@ -2,8 +2,10 @@
 1 M envs, Infinity Cache flushed before every launch.  Run under:
   rocprofv3 --pmc FETCH_SIZE --output-format csv -d <dir> -- python tools/gae_pmc.py
   rocprofv3 --pmc WRITE_SIZE --output-format csv -d <dir> -- python tools/gae_pmc.py
-tools/pmc_summary.py turns the two passes into profiles/pmc_gae_compact_r01.json (per-launch HBM bytes of
-the dense and the compact form)."""
+tools/pmc_summary.py turns the two passes into profiles/pmc_gae_*.json (per-launch HBM bytes of the dense, the
+compact and — since r02 — the value-fused form xpa_gae_scan_value, the in-loop launch of the C2 fast path: it also
+reads the critic's hidden pre-activations z [2N, 256]; caches evicted by a 512 MiB READ before each of its launches,
+so no dirty flush line is written back inside the measured kernel)."""
 import os
 import sys
 
@@ -35,6 +37,17 @@ def main():
                                torch.randint(0, T - 1, (N,), device=dev, generator=g), -1).to(torch.int32)
             flush.fill_(1.0)
             ops.gae_scan_compact(rew, val, term, slot, vboot, 0.99, 0.95, True, adv=adv, ret=ret, boot=boot)
+        if N <= 262144:   # value-fused form (z: 2N x 256 f32)
+            z = torch.randn(2 * N, 256, device=dev, generator=g)
+            w = torch.randn(1, 256, device=dev, generator=g) / 16
+            b = torch.zeros(1, device=dev)
+            for _ in range(5):
+                slot = torch.where(torch.rand(N, device=dev, generator=g) < 0.125,
+                                   torch.randint(0, T - 1, (N,), device=dev, generator=g), -1).to(torch.int32)
+                flush.sum()
+                ops.gae_scan_value(rew, val, term, slot, z, (1, 0.01), w, b, 0.99, 0.95, True, adv=adv, ret=ret,
+                                   boot=boot)
+            del z
         torch.cuda.synchronize()
         print("N", N, "mid closures", int((closed[:, :-1] > 0).sum()), flush=True)
 

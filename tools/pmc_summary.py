@@ -16,7 +16,13 @@ def per_kernel(pass_dir, counter):
             if r.get("Counter_Name") != counter or ("gae_scan" not in name and "gae_dpp" not in name):
                 continue
             grid = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)
-            form = "compact" if (", 1>" in name) else "dense"
+            targs = name[name.index("<") + 1:name.index(">")] if "<" in name else ""
+            parts = [x.strip() for x in targs.split(",")]
+            # gae_dpp_kernel<SEG, COMPACT, VACT>: VACT >= 0 = the value-fused form (-1 = none)
+            if len(parts) == 3 and parts[2] != "-1":
+                form = "value"
+            else:
+                form = "compact" if len(parts) >= 2 and parts[1] == "1" else "dense"
             vals["%s/%d" % (form, grid)].append(float(r["Counter_Value"]))
     return vals
 
@@ -29,10 +35,12 @@ def main(fetch_dir, write_dir, out):
         f = sorted(fetch.get(grid, [0]))[len(fetch.get(grid, [0])) // 2] * 1024 * 2
         w = sorted(write.get(grid, [0]))[len(write.get(grid, [0])) // 2] * 1024
         res["launches"][str(grid)] = {"fetch_bytes": f, "write_bytes": w, "hbm_bytes": f + w}
-    comp = sorted((k for k in res["launches"] if k.startswith("compact/")), key=lambda k: int(k.split("/")[1]))
-    if comp:   # the in-loop (compact) form: bench size (4096 x 128) and 1 M envs
-        res["hbm_bytes_per_launch"] = res["launches"][comp[0]]["hbm_bytes"]
-        res["hbm_bytes_per_launch_1M"] = res["launches"][comp[-1]]["hbm_bytes"]
+    for form in ("compact", "value"):
+        keys = sorted((k for k in res["launches"] if k.startswith(form + "/")), key=lambda k: int(k.split("/")[1]))
+        if keys:   # the bench size (4096 x 128) and the largest measured
+            res["hbm_bytes_per_launch_" + form] = res["launches"][keys[0]]["hbm_bytes"]
+            res["hbm_bytes_per_launch_%s_largest" % form] = res["launches"][keys[-1]]["hbm_bytes"]
+    res["hbm_bytes_per_launch"] = res.get("hbm_bytes_per_launch_value", res.get("hbm_bytes_per_launch_compact"))
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
