@@ -647,6 +647,7 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
 
 }  // namespace
 
+#ifndef XPA_HEAD_KERNELS_ONLY  // tools/_probe: include the kernels alone and instantiate one
 XPA_API int64_t xpa_head_fused_num_partials(int64_t batch) {
     return head_partials(batch);
 }
@@ -790,3 +791,4 @@ XPA_API int xpa_head_gemm_critic(int act_code, int64_t batch, int64_t hidden, co
     launch_head<true, 2, 0>(a, act_code, (hipStream_t)stream);
     return xpa_launch_status();
 }
+#endif  // XPA_HEAD_KERNELS_ONLY
