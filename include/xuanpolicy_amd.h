@@ -99,7 +99,8 @@ int xpa_gae_scan_value(const float *rew, const float *val, const float *term, in
                        void *ev_stop, xpa_stream_t stream);
 
 /* Measurement aid (no reference counterpart): an empty one-wave kernel launched with the same
- * dispatch-attached events as xpa_gae_scan_timed — the fixed per-launch cost of that clock. */
+ * dispatch-attached events as xpa_gae_scan_timed — the fixed per-launch cost of that clock (both events NULL:
+ * a plain empty launch, for other clocks). */
 int xpa_dispatch_floor_timed(void *ev_start, void *ev_stop, xpa_stream_t stream);
 /* Measurement aid: K1's algorithmic bytes moved with no scan (3 f32 streams read, 2 written, n elements,
  * 16-B aligned, n % 4 == 0), timed by the same dispatch-attached events: the copy floor K1 is held to. */

@@ -140,42 +140,64 @@ class XpaError(RuntimeError):
     pass
 
 
+def _digest(paths, extra=""):
+    import hashlib
+    h = hashlib.sha256(extra.encode())
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def build_library(force=False, verbose=False, jobs=None):
     """Compile csrc/*.hip into libxuanpolicy_amd.so for gfx950 (cross-compiles without a GPU).
 
-    One hipcc process per source file (in parallel, objects under xuanpolicy_amd/_obj/, rebuilt when the
-    source or a shared header is newer), then one link step."""
+    One hipcc process per source file (in parallel, objects under xuanpolicy_amd/_obj/), then one link step.
+    An object is rebuilt when the content hash of its source + the shared headers + the flags differs from the
+    one recorded beside it (mtimes raced: a source edited while a build was running kept a stale object that
+    looked newer than it)."""
     from concurrent.futures import ThreadPoolExecutor
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    headers = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")] + [HEADER]
-    hdr_m = max(os.path.getmtime(h) for h in headers)
-    if not force and os.path.exists(LIB_PATH):
-        lib_m = os.path.getmtime(LIB_PATH)
-        if all(os.path.getmtime(d) <= lib_m for d in srcs) and hdr_m <= lib_m:
-            return LIB_PATH
+    headers = sorted([os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")] + [HEADER])
+    hdr_digest = _digest(headers, " ".join(HIPCC_FLAGS))
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     os.makedirs(OBJ_DIR, exist_ok=True)
+    rebuilt = []
 
     def compile_one(src):
         obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
-        if (not force and os.path.exists(obj) and os.path.getmtime(obj) >= os.path.getmtime(src)
-                and os.path.getmtime(obj) >= hdr_m):
-            return obj
+        want = _digest([src], hdr_digest)
+        stamp = obj + ".sha256"
+        if not force and os.path.exists(obj) and os.path.exists(stamp):
+            with open(stamp) as f:
+                if f.read().strip() == want:
+                    return obj
         cmd = [hipcc] + HIPCC_FLAGS + ["-c", "-o", obj + ".tmp", src]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
         os.replace(obj + ".tmp", obj)
+        with open(stamp, "w") as f:
+            f.write(want)
+        rebuilt.append(obj)
         return obj
     jobs = jobs or min(len(srcs), max(1, min(16, os.cpu_count() or 1)))
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(compile_one, srcs))
+    link_stamp = LIB_PATH + ".sha256"
+    link_want = _digest(objs)
+    if not force and not rebuilt and os.path.exists(LIB_PATH) and os.path.exists(link_stamp):
+        with open(link_stamp) as f:
+            if f.read().strip() == link_want:
+                return LIB_PATH
     tmp = LIB_PATH + ".tmp"
     cmd = [hipcc, "--offload-arch=gfx950", "-fPIC", "-shared", "-o", tmp] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB_PATH)
+    with open(link_stamp, "w") as f:
+        f.write(link_want)
     return LIB_PATH
 
 

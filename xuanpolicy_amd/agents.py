@@ -410,7 +410,6 @@ class _OnPolicyAgent:
         policy has no fused critic)."""
         x = self._boot_pair
         fm = self._rollout_mlp()
-        self._check_overflow()
         if hidden_only:
             return fm.rollout_value_hidden(x)
         if fm is not None:
@@ -511,6 +510,10 @@ class _OnPolicyAgent:
                     self.update_log.append(scalars.clone())
         self.last_info = scalars
         self.iterations += 1
+        if self.defer_boot:
+            # after the whole update is enqueued: a D2H copy here no longer holds the host back before the critic
+            # pass + GAE (issued right after the rollout graph, it made the GPU idle 30-100 us before K1V)
+            self._check_overflow()
 
     def log_infos(self, info, x_index):
         """agent.py:81-94: every entry to the logger (tensorboard when importable, else JSON lines in

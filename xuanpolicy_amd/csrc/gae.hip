@@ -547,9 +547,12 @@ __global__ __launch_bounds__(64) void dispatch_floor_kernel(float *p) {
 // cost (dispatch, cache fences, timestamps) that every launch carries on this clock, whatever its grid
 // (flat 4.1-4.2 us for 1 x 64 up to 2048 x 1024 threads on MI355X, tools/gae_floor.hip, r01).
 XPA_API int xpa_dispatch_floor_timed(void *ev_start, void *ev_stop, xpa_stream_t stream) {
-    if (!ev_start || !ev_stop) return (int)hipErrorInvalidValue;
-    hipExtLaunchKernelGGL(dispatch_floor_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
-                          (hipEvent_t)ev_stop, 0, (float *)nullptr);
+    if (!ev_start != !ev_stop) return (int)hipErrorInvalidValue;
+    if (!ev_start)  // no events: a plain empty launch (for other clocks)
+        hipLaunchKernelGGL(dispatch_floor_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (float *)nullptr);
+    else
+        hipExtLaunchKernelGGL(dispatch_floor_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (hipEvent_t)ev_start,
+                              (hipEvent_t)ev_stop, 0, (float *)nullptr);
     return xpa_launch_status();
 }
 
