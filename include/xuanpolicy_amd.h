@@ -506,6 +506,16 @@ int xpa_bias_act(int act, float *y, int64_t rows, int64_t cols, const float *bia
 int64_t xpa_act_bwd_bias_num_partials(int64_t rows, int64_t cols);
 int xpa_act_bwd_bias(int act, const float *dh, const float *h, int64_t rows, int64_t cols, float slope, float *dz,
                      float *partials, xpa_stream_t stream);
+/* K23: out[b, c] = max over the hw positions of x [batch, hw, channels] (NHWC), argmax[b, c] its position — Basic_CNN's
+ * AdaptiveMaxPool2d((1, 1)) (cnn.py:5-40) with torch's rule: the first maximum wins, a NaN always replaces. */
+int xpa_global_maxpool(const float *x, int64_t batch, int64_t hw, int64_t channels, float *out, int32_t *argmax,
+                       xpa_stream_t stream);
+/* K24: the backward of K23 and of the activation before it, with the conv bias gradient: dz[b, p, c] =
+ * (p == argmax[b, c] ? dout[b, c] : 0) * act'(h[b, p, c]) over [batch * hw, channels], and the column-sum partials
+ * of dz as xpa_act_bwd_bias (xpa_act_bwd_bias_num_partials(batch * hw, channels) rows). */
+int xpa_maxpool_act_bwd_bias(int act, const float *dout, const int32_t *argmax, const float *h, int64_t batch,
+                             int64_t hw, int64_t channels, float slope, float *dz, float *partials,
+                             xpa_stream_t stream);
 
 #ifdef __cplusplus
 }

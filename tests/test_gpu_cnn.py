@@ -101,7 +101,7 @@ def test_fused_cnn_matches_autograd(B):
     for p in pol.parameters():
         p.grad = torch.full_like(p, float("nan"))   # every gradient must be overwritten
     h2, _, v2, ctx = fc.forward(x)
-    (hs, flat, fouts), s_state, _, _ = ctx
+    (hs, _, flat, fouts), s_state, _, _ = ctx
     # float64 CPU reference through the reference-layout modules (NCHW convs with bias, Flatten in (C, H, W)
     # order).  Its ReLUs take their masks from the explicit path's own activations: a unit within an ulp of the
     # kink may flip between two f32 paths (different conv algorithms), which would move that unit's whole
@@ -132,6 +132,94 @@ def test_fused_cnn_matches_autograd(B):
     for n, p in pol.named_parameters():
         scale = float(ref[n].abs().max()) + 1e-12
         err = float((p.grad.cpu().double() - ref[n]).abs().max())
+        if not err <= 2e-5 * scale + 1e-8:
+            bad.append((n, err, scale))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("B,HW,C", [(5, 100, 64), (2048, 100, 64), (3, 7, 32)])
+def test_global_maxpool_and_backward_match_torch(B, HW, C):
+    """K23 == torch's AdaptiveMaxPool2d((1, 1)) values and indices (first maximum wins: ties planted, incl. all-zero
+    ReLU channels), K24 == its backward routed through the ReLU, with the bias column sums."""
+    _l, ops = _lib()
+    g = torch.Generator(device="cpu").manual_seed(B + HW)
+    h = torch.relu(torch.randn(B, HW, C, generator=g))
+    h[:, :, 0] = 0.0                                 # dead channel: every position ties at 0
+    h[:, HW // 2, 1] = h[:, 0, 1] = 5.0              # a tie between two positions: the first must win
+    hd = h.to(DEV)
+    out = torch.empty(B, C, device=DEV)
+    am = torch.empty(B, C, dtype=torch.int32, device=DEV)
+    _l.check(ops.lib().xpa_global_maxpool(ops._p(hd), B, HW, C, ops._p(out), ops._p(am), ops._stream(DEV)), "maxpool")
+    x = hd.permute(0, 2, 1).reshape(B, C, HW, 1)     # NCHW view of the NHWC data, W = 1
+    ref, ridx = torch.nn.functional.adaptive_max_pool2d(x, (1, 1), return_indices=True)
+    torch.testing.assert_close(out, ref.view(B, C), rtol=0, atol=0)
+    assert torch.equal(am.long(), ridx.view(B, C))
+    dout = torch.randn(B, C, generator=g).to(DEV)
+    G = int(ops.lib().xpa_act_bwd_bias_num_partials(B * HW, C))
+    part = torch.empty(G, C, device=DEV)
+    dz = torch.empty(B, HW, C, device=DEV)
+    _l.check(ops.lib().xpa_maxpool_act_bwd_bias(1, ops._p(dout), ops._p(am), ops._p(hd), B, HW, C, 0.0, ops._p(dz),
+                                                ops._p(part), ops._stream(DEV)), "maxpool_bwd")
+    db = torch.empty(C, device=DEV)
+    _l.check(ops.lib().xpa_colsum_finalize(ops._p(part), G, C, ops._p(db), ops._stream(DEV)), "finalize")
+    xr = x.clone().requires_grad_(True)
+    torch.autograd.backward(torch.nn.functional.adaptive_max_pool2d(xr, (1, 1)), dout.view(B, C, 1, 1))
+    rdz = (xr.grad.view(B, C, HW).permute(0, 2, 1) * (hd > 0)).contiguous()
+    torch.testing.assert_close(dz, rdz, rtol=0, atol=0)
+    torch.testing.assert_close(db.double(), rdz.double().sum((0, 1)), rtol=1e-5, atol=1e-5)   # f32 block sums
+
+
+@pytest.mark.parametrize("B", [64, 300])
+def test_fused_qnetwork_matches_autograd(B):
+    """FusedQNetwork (Basic_CNN + Q head, C5): evalQ, targetQ and every eval-parameter gradient for a given d evalQ ==
+    float64 autograd through the reference-layout modules (ReLU masks and max-pool positions borrowed from the f32
+    path, as in test_fused_cnn_matches_autograd)."""
+    import copy
+    from xuanpolicy_amd.fused_cnn import FusedQNetwork
+    from xuanpolicy_amd.policies import Basic_CNN, BasicQnetwork
+
+    class _Disc:
+        n, shape = 18, ()
+    torch.manual_seed(B)
+    rep = Basic_CNN((84, 84, 4), [8, 4, 3], [4, 2, 1], [32, 64, 64], None, torch.nn.init.orthogonal_, torch.nn.ReLU,
+                    DEV)
+    pol = BasicQnetwork(_Disc(), rep, [512], None, torch.nn.init.orthogonal_, torch.nn.ReLU, DEV)
+    with torch.no_grad():
+        for n, p in pol.named_parameters():
+            if n.endswith("bias"):
+                p.normal_(0, 0.1)
+    pol.copy_target()
+    g = torch.Generator(device="cpu").manual_seed(B)
+    x = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.int32).to(torch.uint8).to(DEV)
+    dq = (torch.randn(B, 18, generator=g) / B).to(DEV)
+    fq = FusedQNetwork(pol)
+    q, ctx = fq.forward(x)
+    tq = fq.target(x)
+    torch.testing.assert_close(tq, q, rtol=1e-6, atol=1e-6)   # target = deep copy of eval at construction
+    (hs, am, _, _), s, outs = ctx
+    pol64 = copy.deepcopy(pol).to("cpu").double()
+    masks = [(y > 0).permute(0, 3, 1, 2).cpu().double() for y in hs[1:]]
+    h = (x.cpu().double() / 255.0).permute(0, 3, 1, 2)
+    k = 0
+    for mod in pol64.representation.model:
+        if isinstance(mod, torch.nn.ReLU):
+            h = h * masks[k]
+            k += 1
+        elif isinstance(mod, torch.nn.AdaptiveMaxPool2d):
+            Bc, Cc = h.shape[0], h.shape[1]
+            h = torch.gather(h.reshape(Bc, Cc, -1), 2, am.cpu().long().view(Bc, Cc, 1)).view(Bc, Cc, 1, 1)
+        else:
+            h = mod(h)
+    q64 = pol64.eval_Qhead(h)
+    torch.testing.assert_close(q.cpu().double(), q64.detach(), rtol=1e-4, atol=1e-5)
+    torch.autograd.backward(q64, dq.cpu().double())
+    fq.backward(ctx, dq)
+    bad = []
+    for (n, p), (n64, p64) in zip(pol.named_parameters(), pol64.named_parameters()):
+        if n.startswith("target"):
+            continue
+        scale = float(p64.grad.abs().max()) + 1e-12
+        err = float((p.grad.cpu().double() - p64.grad).abs().max())
         if not err <= 2e-5 * scale + 1e-8:
             bad.append((n, err, scale))
     assert not bad, bad

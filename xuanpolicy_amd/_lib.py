@@ -68,6 +68,9 @@ SIGNATURES = {
     "xpa_bias_act": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_p, c_f32, c_p]),
     "xpa_act_bwd_bias_num_partials": (c_i64, [c_i64, c_i64]),
     "xpa_act_bwd_bias": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_i64, c_i64, c_f32, c_p, c_p, c_p]),
+    "xpa_global_maxpool": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
+    "xpa_maxpool_act_bwd_bias": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_p, c_p,
+                                                c_p]),
     "xpa_head_bwd_num_partials": (c_i64, [c_i64]),
     "xpa_head_backward": (ctypes.c_int, [ctypes.c_int, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_f32, c_p, c_p, c_p,
                                          c_p, c_p]),

@@ -698,8 +698,8 @@ class PerDQN_Agent:
     def _action(self, obs, egreedy=0.0):
         """perdqn_agent.py:47-54: argmax of the eval Q row, or (with probability egreedy, one draw for all envs)
         uniform random actions from np.random, as the reference draws them."""
-        with torch.no_grad():
-            _, argmax_action, _ = self.policy(obs)
+        q = self.learner.q_values(obs)
+        argmax_action = q.argmax(dim=-1)
         random_action = np.random.choice(self.action_space.n, self.n_envs)
         if np.random.rand() < egreedy:
             return torch.as_tensor(random_action, device=self.device)

@@ -132,6 +132,78 @@ __global__ __launch_bounds__(256) void act_bwd_bias_kernel(const float *dh, cons
     }
 }
 
+// K23: global max over the HW positions of NHWC [B, HW, C] (Basic_CNN's AdaptiveMaxPool2d((1, 1))), thread = (b, c),
+// consecutive threads = consecutive channels (each hw step of a wave reads 256 contiguous bytes), 4 positions' loads
+// in flight.  torch's rule (AdaptiveMaxPooling2d.cu): max starts at -inf with index 0, and a position replaces it
+// when `val > max || isnan(val)` — the first maximum wins, the last NaN wins.
+__global__ __launch_bounds__(256) void global_maxpool_kernel(const float *__restrict__ x, int64_t B, int HW, int C,
+                                                             float *__restrict__ out, int32_t *__restrict__ argmax) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= B * C) return;
+    const int64_t b = i / C;
+    const int c = (int)(i - b * C);
+    const float *p = x + b * (int64_t)HW * C + c;
+    float m = -__builtin_inff();
+    int am = 0;
+    int hw = 0;
+    for (; hw + 4 <= HW; hw += 4) {
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = p[(int64_t)(hw + u) * C];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (v[u] > m || __builtin_isnan(v[u])) {
+                m = v[u];
+                am = hw + u;
+            }
+    }
+    for (; hw < HW; ++hw) {
+        const float v = p[(int64_t)hw * C];
+        if (v > m || __builtin_isnan(v)) {
+            m = v;
+            am = hw;
+        }
+    }
+    out[i] = m;
+    argmax[i] = am;
+}
+
+// K24: the backward of K23 fused into K22 — the pooled gradient routed to each (b, c)'s argmax position (0
+// elsewhere), times act'(h), written as the conv output's dz, with the bias-gradient partials (K22's grid / layout).
+template <int ACT>
+__global__ __launch_bounds__(256) void maxpool_act_bwd_bias_kernel(const float *__restrict__ dout,
+                                                                   const int32_t *__restrict__ argmax,
+                                                                   const float *__restrict__ h, int64_t rows, int HW,
+                                                                   int C, float slope, float *__restrict__ dz,
+                                                                   float *__restrict__ partials) {
+    extern __shared__ __attribute__((aligned(16))) f4v s_acc[];
+    const int cq = C / 4, groups = 256 / cq;
+    const int c4 = threadIdx.x % cq, g = threadIdx.x / cq;
+    f4v acc = {0.f, 0.f, 0.f, 0.f};
+    const int64_t stride = (int64_t)gridDim.x * groups;
+    for (int64_t r = (int64_t)blockIdx.x * groups + g; r < rows; r += stride) {
+        const int64_t b = r / HW;
+        const int hw = (int)(r - b * HW);
+        const f4v hv = *reinterpret_cast<const f4v *>(h + r * C + 4 * c4);
+        f4v v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t bc = b * C + 4 * c4 + e;
+            v[e] = argmax[bc] == hw ? dout[bc] : 0.f;
+            v[e] = act_grad<ACT>(v[e], hv[e], slope);
+        }
+        *reinterpret_cast<f4v *>(dz + r * C + 4 * c4) = v;
+        acc += v;
+    }
+    s_acc[g * cq + c4] = acc;
+    __syncthreads();
+    if ((int)threadIdx.x < cq) {
+        f4v t = {0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < groups; ++k) t += s_acc[k * cq + threadIdx.x];
+        *reinterpret_cast<f4v *>(partials + (int64_t)blockIdx.x * C + 4 * threadIdx.x) = t;
+    }
+}
+
 int grid_for(int64_t work, int64_t per_block, int64_t cap) {
     int64_t g = (work + per_block - 1) / per_block;
     if (g > cap) g = cap;
@@ -205,5 +277,35 @@ XPA_API int xpa_act_bwd_bias(int act, const float *dh, const float *h, int64_t r
     else if (act == 1) XPA_ABB(1);
     else XPA_ABB(2);
 #undef XPA_ABB
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_global_maxpool(const float *x, int64_t batch, int64_t hw, int64_t channels, float *out,
+                               int32_t *argmax, xpa_stream_t stream) {
+    if (batch <= 0 || hw <= 0 || channels <= 0 || hw > (1 << 30) || channels > (1 << 20) || !x || !out || !argmax)
+        return (int)hipErrorInvalidValue;
+    const int64_t n = batch * channels;
+    hipLaunchKernelGGL(global_maxpool_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                       batch, (int)hw, (int)channels, out, argmax);
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_maxpool_act_bwd_bias(int act, const float *dout, const int32_t *argmax, const float *h, int64_t batch,
+                                     int64_t hw, int64_t channels, float slope, float *dz, float *partials,
+                                     xpa_stream_t stream) {
+    const int64_t rows = batch * hw;
+    const int64_t G = xpa_act_bwd_bias_num_partials(rows, channels);
+    if (G <= 0 || hw > (1 << 30) || !dout || !argmax || !h || !dz || !partials || act < 0 || act > 2)
+        return (int)hipErrorInvalidValue;
+    if (((uintptr_t)h | (uintptr_t)dz | (uintptr_t)partials) % 16) return (int)hipErrorInvalidValue;
+    const size_t lds = 256 * sizeof(f4v);
+    hipStream_t s = (hipStream_t)stream;
+#define XPA_MPB(A_)                                                                                              \
+    hipLaunchKernelGGL((maxpool_act_bwd_bias_kernel<A_>), dim3((unsigned)G), dim3(256), lds, s, dout, argmax, h, \
+                       rows, (int)hw, (int)channels, slope, dz, partials)
+    if (act == 0) XPA_MPB(0);
+    else if (act == 1) XPA_MPB(1);
+    else XPA_MPB(2);
+#undef XPA_MPB
     return xpa_launch_status();
 }

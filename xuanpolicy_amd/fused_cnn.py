@@ -1,21 +1,26 @@
-"""Explicit (autograd-free) forward / backward of an actor-critic on the AC_CNN_Atari trunk (C3).
+"""Explicit (autograd-free) forward / backward of the convolutional policies: the AC_CNN_Atari actor-critic (C3) and
+the Basic_CNN Q-network of PER-DQN (C5).
 
 Reference: AC_CNN_Atari xuance/torch/representations/cnn.py:45-93 (conv blocks with padding (k - s) // 2 + ReLU,
-Flatten, fc blocks), cnn_block / mlp_block xuance/torch/utils/layers.py:8-57, Categorical_AC_Policy
-xuance/torch/policies/categorical.py:61-85; the learner's loss.backward() a2c_learner.py:31-33.
+Flatten, fc blocks), Basic_CNN cnn.py:5-40 (conv blocks, AdaptiveMaxPool2d((1, 1)), Flatten), cnn_block / mlp_block
+xuance/torch/utils/layers.py:8-57, Categorical_AC_Policy xuance/torch/policies/categorical.py:61-85, BasicQnetwork
+deterministic.py:148-182; the learners' loss.backward() (a2c_learner.py:31-33, perdqn_learner.py:37-40).
 
 Every activation stays NHWC ([rows = B*H*W, C] row-major), the layout the uint8 frames arrive in:
   forward   K20 xpa_frames_to_f32 (uint8 -> float32 / 255, the reference's arithmetic bit for bit)
             -> per conv: MIOpen conv2d without bias on the channels-last view -> K21 xpa_bias_act (bias + ReLU
                in place)
-            -> Flatten in NHWC order: the first fc layer uses its weight with the columns permuted from the
-               reference's (C, H, W) order to (H, W, C) (one 13 MB copy per parameter update, instead of an
-               NHWC -> NCHW copy of the [B, 6400] activations every forward)
-            -> fc: hipBLASLt GEMM (bias epilogue) -> K21 ReLU in place -> heads (GEMMs)
-  backward  heads: GEMMs + K10 bias column sums -> fc: K22 xpa_act_bwd_bias (ReLU backward + bias gradient) ->
-            dW GEMM (permuted back into the reference layout) + dX GEMM -> per conv: K22 then MIOpen
+            -> AC_CNN_Atari: Flatten in NHWC order — the first fc layer uses its weight with the columns permuted
+               from the reference's (C, H, W) order to (H, W, C) (one 13 MB copy per parameter update, instead of an
+               NHWC -> NCHW copy of the [B, 6400] activations every forward) -> fc: hipBLASLt GEMM (bias epilogue)
+               -> K21 ReLU in place;
+               Basic_CNN: K23 xpa_global_maxpool (max + argmax per (b, c), torch's tie rule)
+            -> heads / Q head (GEMMs)
+  backward  heads: GEMMs + K10 / K22 bias column sums -> AC_CNN_Atari fc: K22 xpa_act_bwd_bias (ReLU backward + bias
+            gradient) -> dW GEMM (permuted back into the reference layout) + dX GEMM; Basic_CNN: K24 (the pooled
+            gradient routed to the argmax, ReLU backward, bias gradient) -> per conv: K22 then MIOpen
             convolution_backward (data, weight; no dX for the first conv).
-Parameter gradients are written into the parameters' .grad views (the flat buffer of xuanpolicy_amd.flat).
+Parameter gradients are written into the parameters' .grad views (allocated when missing).
 """
 import torch
 import torch.nn as nn
@@ -23,71 +28,153 @@ import torch.nn.functional as F
 
 from . import _lib, ops
 from .fused_mlp import _act_code, _parse
-from .policies import AC_CNN_Atari
+from .policies import AC_CNN_Atari, Basic_CNN
 
 
 def _conv_layers(model):
-    convs, rest, i = [], [], 0
+    """(conv blocks [(conv, act code, slope)], tail, fc layers): tail "flatten" (AC_CNN_Atari) or "maxpool"
+    (Basic_CNN)."""
+    convs, i = [], 0
     mods = list(model)
     while i < len(mods) and isinstance(mods[i], nn.Conv2d):
         conv = mods[i]
-        act = mods[i + 1] if i + 1 < len(mods) and not isinstance(mods[i + 1], (nn.Conv2d, nn.Flatten)) else None
+        nxt = mods[i + 1] if i + 1 < len(mods) else None
+        act = nxt if isinstance(nxt, (nn.ReLU, nn.LeakyReLU, nn.Tanh)) else None
         if conv.bias is None or conv.groups != 1 or tuple(conv.dilation) != (1, 1):
             raise ValueError("expected Conv2d with bias, groups 1, dilation 1")
         convs.append((conv,) + _act_code(act))
         i += 2 if act is not None else 1
+    if not convs:
+        raise ValueError("no conv blocks")
+    if i < len(mods) and isinstance(mods[i], nn.AdaptiveMaxPool2d):
+        if tuple(nn.modules.utils._pair(mods[i].output_size)) != (1, 1) or i + 1 >= len(mods) \
+                or not isinstance(mods[i + 1], nn.Flatten) or i + 2 != len(mods):
+            raise ValueError("expected AdaptiveMaxPool2d((1, 1)) + Flatten as the tail")
+        return convs, "maxpool", []
     if i >= len(mods) or not isinstance(mods[i], nn.Flatten):
-        raise ValueError("expected Flatten after the conv blocks")
-    return convs, _parse(mods[i + 1:])
+        raise ValueError("expected Flatten (or a global max pool) after the conv blocks")
+    fc = _parse(mods[i + 1:])
+    if not fc:
+        raise ValueError("Flatten without fc layers")
+    return convs, "flatten", fc
 
 
-class FusedCNNActorCritic:
-    """Built from a Categorical/Gaussian actor-critic policy with an AC_CNN_Atari representation."""
+class _Part:
+    """Per-block partial buffers of the bias-gradient reductions, by shape."""
 
-    def __init__(self, policy):
-        rep = policy.representation
-        if not isinstance(rep, AC_CNN_Atari):
+    def __init__(self):
+        self.bufs = {}
+
+    def get(self, rows, cols, device, k22):
+        key = (rows, cols, k22)
+        p = self.bufs.get(key)
+        if p is None:
+            L = ops.lib()
+            G = int(L.xpa_act_bwd_bias_num_partials(rows, cols)) if k22 else int(L.xpa_act_bwd_num_partials(rows))
+            p = torch.empty((G, cols), dtype=torch.float32, device=device)
+            self.bufs[key] = p
+        return p
+
+
+def _bias_act(code, y2d, bias, slope):
+    _lib.check(ops.lib().xpa_bias_act(code, ops._p(y2d), y2d.shape[0], y2d.shape[1],
+                                      ops._p(bias) if bias is not None else None, float(slope),
+                                      ops._stream(y2d.device)), "xpa_bias_act")
+
+
+def _act_bwd_bias(parts, code, g2d, h2d, slope, bias_grad):
+    """g2d <- g2d * act'(h2d) in place; bias_grad <- column sums (K22, or K10 for widths K22 does not take)."""
+    rows, cols = g2d.shape
+    L, s = ops.lib(), ops._stream(g2d.device)
+    if not g2d.is_contiguous():
+        raise ValueError("gradient rows must be contiguous")
+    k22 = cols % 4 == 0 and 256 % (cols // 4) == 0
+    part = parts.get(rows, cols, g2d.device, k22)
+    hp = ops._p(h2d) if code else None
+    gp = ops._p(g2d) if code else None
+    if k22:
+        _lib.check(L.xpa_act_bwd_bias(code, ops._p(g2d), hp, rows, cols, float(slope), gp, ops._p(part), s),
+                   "xpa_act_bwd_bias")
+    else:
+        _lib.check(L.xpa_act_bwd_colsum(code, ops._p(g2d), hp, rows, cols, float(slope), gp, ops._p(part), s),
+                   "xpa_act_bwd_colsum")
+    _lib.check(L.xpa_colsum_finalize(ops._p(part), part.shape[0], cols, ops._p(bias_grad), s), "xpa_colsum_finalize")
+
+
+def _chain(layers, x):
+    outs, h = [], x
+    for lin, code, slope in layers:
+        h = F.linear(h, lin.weight, lin.bias)
+        if code and h.shape[1] % 4 == 0 and 256 % (h.shape[1] // 4) == 0:
+            _bias_act(code, h, None, slope)   # K21 in place
+        elif code == 1:
+            F.leaky_relu(h, slope, inplace=True)
+        elif code == 2:
+            h.tanh_()
+        outs.append(h)
+    return outs
+
+
+def _chain_backward(parts, layers, inputs, outs, g, acc=None, need_dx=True):
+    """Linear(+act) chain backward; returns d(input) (added into acc when given)."""
+    for j in range(len(layers) - 1, -1, -1):
+        lin, code, slope = layers[j]
+        g = g.contiguous()
+        _act_bwd_bias(parts, code, g, outs[j], slope, lin.bias.grad)
+        torch.mm(g.t(), inputs[j], out=lin.weight.grad)
+        if j == 0 and not need_dx:
+            return None
+        if j == 0 and acc is not None:
+            g = acc.addmm_(g, lin.weight)
+        else:
+            g = torch.mm(g, lin.weight)
+    return g
+
+
+def _ensure_grads(params):
+    for p in params:
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+
+
+class _Trunk:
+    """The explicit forward / backward of one AC_CNN_Atari or Basic_CNN representation."""
+
+    def __init__(self, rep, parts):
+        if not isinstance(rep, (AC_CNN_Atari, Basic_CNN)):
             raise ValueError("representation %r has no explicit CNN path" % type(rep).__name__)
-        self.convs, self.fc = _conv_layers(rep.model)
-        if not self.fc:
-            raise ValueError("AC_CNN_Atari without fc layers")
-        for conv, code, _ in self.convs:
+        self.rep = rep
+        self.convs, self.tail, self.fc = _conv_layers(rep.model)
+        for conv, _, _ in self.convs:
             if conv.out_channels % 4 or 256 % (conv.out_channels // 4):
                 raise ValueError("conv channels must be a multiple of 4 dividing 1024")
-        self.discrete = bool(getattr(policy, "discrete", False))
-        self.actor = _parse(policy.actor.model if self.discrete else policy.actor.mu)
-        self.critic = _parse(policy.critic.model)
-        self.logstd = None if self.discrete else policy.actor.logstd
         C, H, W = rep.input_shape
         self.in_hwc = (H, W, C)
         shape = (C, H, W)
-        self.out_shapes = []
         for conv, _, _ in self.convs:
             k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
-            Ho = (shape[1] + 2 * p - k) // s + 1
-            Wo = (shape[2] + 2 * p - k) // s + 1
-            shape = (conv.out_channels, Ho, Wo)
-            self.out_shapes.append(shape)
-        Cl, Hl, Wl = shape
-        fc0 = self.fc[0][0]
-        if fc0.in_features != Cl * Hl * Wl:
+            shape = (conv.out_channels, (shape[1] + 2 * p - k) // s + 1, (shape[2] + 2 * p - k) // s + 1)
+        self._chw = shape
+        if self.tail == "flatten" and self.fc[0][0].in_features != shape[0] * shape[1] * shape[2]:
             raise ValueError("fc input width does not match the conv output")
-        self._chw = (Cl, Hl, Wl)
         self._w_hwc = None      # the first fc weight with (H, W, C)-ordered columns, refreshed after each update
         self.stale = True
         self._dw_tmp = None
-        self._partials = {}
-        n_params = sum(1 for _ in policy.parameters())
-        n_cov = 2 * (len(self.convs) + len(self.fc) + len(self.actor) + len(self.critic)) + (0 if self.discrete else 1)
-        if n_params != n_cov:
-            raise ValueError("policy has parameters outside the conv / Linear chains")
+        self.parts = parts
+        self.n_params = 2 * (len(self.convs) + len(self.fc))
 
-    # ------------------------------------------------------------------------------------------------
+    def params(self):
+        out = []
+        for conv, _, _ in self.convs:
+            out += [conv.weight, conv.bias]
+        for lin, _, _ in self.fc:
+            out += [lin.weight, lin.bias]
+        return out
+
     def refresh(self):
-        """Re-derive the (H, W, C)-ordered first fc weight now (the agent calls it before a captured rollout, whose
-        graph must not contain the copy)."""
         self.stale = True
-        self._fc0_weight()
+        if self.tail == "flatten":
+            self._fc0_weight()
 
     def _fc0_weight(self):
         if self.stale or self._w_hwc is None:
@@ -100,12 +187,7 @@ class FusedCNNActorCritic:
         return self._w_hwc
 
     @staticmethod
-    def _bias_act(code, y2d, bias, slope):
-        _lib.check(ops.lib().xpa_bias_act(code, ops._p(y2d), y2d.shape[0], y2d.shape[1],
-                                          ops._p(bias) if bias is not None else None, float(slope),
-                                          ops._stream(y2d.device)), "xpa_bias_act")
-
-    def frames(self, x):
+    def frames(x):
         """uint8 [B, H, W, C] -> float32 / 255 [B, H, W, C] (K20)."""
         if x.dtype != torch.uint8 or x.device.type != "cuda" or not x.is_contiguous():
             raise ValueError("frames must be a contiguous uint8 ROCm tensor [B, H, W, C]")
@@ -115,7 +197,7 @@ class FusedCNNActorCritic:
         return out
 
     @torch.no_grad()
-    def trunk(self, x):
+    def forward(self, x):
         """x uint8 [B, H, W, C] -> (state [B, d], context for backward)."""
         B = x.shape[0]
         h = self.frames(x.reshape((B,) + self.in_hwc))
@@ -125,9 +207,16 @@ class FusedCNNActorCritic:
             y = z.permute(0, 2, 3, 1)
             if not y.is_contiguous():
                 y = y.contiguous()
-            self._bias_act(code, y.view(-1, y.shape[3]), conv.bias, slope)
+            _bias_act(code, y.view(-1, y.shape[3]), conv.bias, slope)
             hs.append(y)
             h = y
+        if self.tail == "maxpool":
+            Cl = h.shape[3]
+            s = torch.empty((B, Cl), dtype=torch.float32, device=x.device)
+            am = torch.empty((B, Cl), dtype=torch.int32, device=x.device)
+            _lib.check(ops.lib().xpa_global_maxpool(ops._p(h), B, h.shape[1] * h.shape[2], Cl, ops._p(s), ops._p(am),
+                                                    ops._stream(x.device)), "xpa_global_maxpool")
+            return s, (hs, am, None, [])
         flat = h.reshape(B, -1)                  # (H, W, C) order: no copy
         fouts = []
         s = flat
@@ -135,110 +224,56 @@ class FusedCNNActorCritic:
             w = self._fc0_weight() if j == 0 else lin.weight
             s = F.linear(s, w, lin.bias)
             if code:
-                self._bias_act(code, s, None, slope)
+                _bias_act(code, s, None, slope)
             fouts.append(s)
-        return s, (hs, flat, fouts)
-
-    @staticmethod
-    def _chain(layers, x):
-        outs, h = [], x
-        for lin, code, slope in layers:
-            h = F.linear(h, lin.weight, lin.bias)
-            if code == 1:
-                F.leaky_relu(h, slope, inplace=True)
-            elif code == 2:
-                h.tanh_()
-            outs.append(h)
-        return outs
+        return s, (hs, None, flat, fouts)
 
     @torch.no_grad()
-    def forward(self, x):
-        """(logits or mu, logstd or None, v, ctx)."""
-        s, tctx = self.trunk(x)
-        a_outs = self._chain(self.actor, s)
-        c_outs = self._chain(self.critic, s)
-        return a_outs[-1], self.logstd, c_outs[-1][:, 0], (tctx, s, a_outs, c_outs)
-
-    @torch.no_grad()
-    def heads(self, x):
-        head, logstd, v, _ = self.forward(x)
-        return head, logstd, v
-
-    # ------------------------------------------------------------------------------------------------
-    def _part(self, rows, cols, device, k22):
-        key = (rows, cols, k22)
-        p = self._partials.get(key)
-        if p is None:
-            L = ops.lib()
-            G = int(L.xpa_act_bwd_bias_num_partials(rows, cols)) if k22 else int(L.xpa_act_bwd_num_partials(rows))
-            p = torch.empty((G, cols), dtype=torch.float32, device=device)
-            self._partials[key] = p
-        return p
-
-    def _act_bwd_bias(self, code, g2d, h2d, slope, bias_grad):
-        """g2d <- g2d * act'(h2d) in place; bias_grad <- column sums (K22, or K10 for widths K22 does not take)."""
-        rows, cols = g2d.shape
-        L, s = ops.lib(), ops._stream(g2d.device)
-        k22 = cols % 4 == 0 and 256 % (cols // 4) == 0 and g2d.is_contiguous()
-        part = self._part(rows, cols, g2d.device, k22)
-        hp = ops._p(h2d) if code else None
-        gp = ops._p(g2d) if code else None
-        if k22:
-            _lib.check(L.xpa_act_bwd_bias(code, ops._p(g2d), hp, rows, cols, float(slope), gp, ops._p(part), s),
-                       "xpa_act_bwd_bias")
-        else:
-            if not g2d.is_contiguous():
-                raise ValueError("gradient rows must be contiguous")
-            _lib.check(L.xpa_act_bwd_colsum(code, ops._p(g2d), hp, rows, cols, float(slope), gp, ops._p(part), s),
-                       "xpa_act_bwd_colsum")
-        _lib.check(L.xpa_colsum_finalize(ops._p(part), part.shape[0], cols, ops._p(bias_grad), s),
-                   "xpa_colsum_finalize")
-
-    def _chain_backward(self, layers, inputs, outs, g, acc=None):
-        """Linear(+act) chain backward; returns d(input) (added into acc when given)."""
-        for j in range(len(layers) - 1, -1, -1):
-            lin, code, slope = layers[j]
-            g = g.contiguous()
-            self._act_bwd_bias(code, g, outs[j], slope, lin.bias.grad)
-            torch.mm(g.t(), inputs[j], out=lin.weight.grad)
-            if j == 0 and acc is not None:
-                g = acc.addmm_(g, lin.weight)
-            else:
-                g = torch.mm(g, lin.weight)
-        return g
-
-    @torch.no_grad()
-    def backward(self, ctx, d_head, d_v):
-        """Writes every parameter gradient (d_head [B, K], d_v [B]: the loss kernel's outputs)."""
-        (hs, flat, fouts), s, a_outs, c_outs = ctx
-        ds = self._chain_backward(self.actor, [s] + a_outs[:-1], a_outs, d_head)
-        ds = self._chain_backward(self.critic, [s] + c_outs[:-1], c_outs, d_v.view(-1, 1), acc=ds)
-        # fc chain (the first layer's weight is used in (H, W, C) column order)
+    def backward(self, ctx, ds):
+        """ds: d loss / d state [B, d]; writes every trunk parameter's gradient."""
+        hs, am, flat, fouts = ctx
+        B = hs[0].shape[0]
+        parts = self.parts
         g = ds
-        for j in range(len(self.fc) - 1, -1, -1):
-            lin, code, slope = self.fc[j]
-            x_in = flat if j == 0 else fouts[j - 1]
-            g = g.contiguous()
-            self._act_bwd_bias(code, g, fouts[j], slope, lin.bias.grad)
-            if j == 0:
-                if self._dw_tmp is None:
-                    self._dw_tmp = torch.empty_like(lin.weight)
-                torch.mm(g.t(), x_in, out=self._dw_tmp)
-                Cl, Hl, Wl = self._chw
-                lin.weight.grad.view(lin.out_features, Cl, Hl, Wl).copy_(
-                    self._dw_tmp.view(lin.out_features, Hl, Wl, Cl).permute(0, 3, 1, 2))
-                g = torch.mm(g, self._fc0_weight())
-            else:
-                torch.mm(g.t(), x_in, out=lin.weight.grad)
-                g = torch.mm(g, lin.weight)
-        # conv blocks, last to first; g is the NHWC gradient of the last conv block's output
+        if self.tail == "flatten":
+            for j in range(len(self.fc) - 1, -1, -1):
+                lin, code, slope = self.fc[j]
+                x_in = flat if j == 0 else fouts[j - 1]
+                g = g.contiguous()
+                _act_bwd_bias(parts, code, g, fouts[j], slope, lin.bias.grad)
+                if j == 0:
+                    if self._dw_tmp is None:
+                        self._dw_tmp = torch.empty_like(lin.weight)
+                    torch.mm(g.t(), x_in, out=self._dw_tmp)
+                    Cl, Hl, Wl = self._chw
+                    lin.weight.grad.view(lin.out_features, Cl, Hl, Wl).copy_(
+                        self._dw_tmp.view(lin.out_features, Hl, Wl, Cl).permute(0, 3, 1, 2))
+                    g = torch.mm(g, self._fc0_weight())
+                else:
+                    torch.mm(g.t(), x_in, out=lin.weight.grad)
+                    g = torch.mm(g, lin.weight)
+        # conv blocks, last to first; g is the NHWC gradient of the last conv block's output (flatten tail) or, for
+        # the max-pool tail, K24 forms the last block's dz from the pooled gradient
         for i in range(len(self.convs) - 1, -1, -1):
             conv, code, slope = self.convs[i]
             y = hs[i + 1]
-            g = g.reshape(y.shape)
-            if not g.is_contiguous():
-                g = g.contiguous()
-            self._act_bwd_bias(code, g.view(-1, y.shape[3]), y.view(-1, y.shape[3]), slope, conv.bias.grad)
+            Cy = y.shape[3]
+            if i == len(self.convs) - 1 and self.tail == "maxpool":
+                HW = y.shape[1] * y.shape[2]
+                dz = torch.empty_like(y)
+                part = parts.get(B * HW, Cy, y.device, True)
+                L, st = ops.lib(), ops._stream(y.device)
+                _lib.check(L.xpa_maxpool_act_bwd_bias(code, ops._p(ds.contiguous()), ops._p(am), ops._p(y), B, HW, Cy,
+                                                      float(slope), ops._p(dz), ops._p(part), st),
+                           "xpa_maxpool_act_bwd_bias")
+                _lib.check(L.xpa_colsum_finalize(ops._p(part), part.shape[0], Cy, ops._p(conv.bias.grad), st),
+                           "xpa_colsum_finalize")
+                g = dz
+            else:
+                g = g.reshape(y.shape)
+                if not g.is_contiguous():
+                    g = g.contiguous()
+                _act_bwd_bias(parts, code, g.view(-1, Cy), y.view(-1, Cy), slope, conv.bias.grad)
             need_in = i > 0
             gx, gw, _ = torch.ops.aten.convolution_backward(
                 g.permute(0, 3, 1, 2), hs[i].permute(0, 3, 1, 2), conv.weight, None, list(conv.stride),
@@ -248,3 +283,104 @@ class FusedCNNActorCritic:
                 g = gx.permute(0, 2, 3, 1)
         self.stale = True   # the optimizer step that follows changes the fc weight
 
+
+class FusedCNNActorCritic:
+    """Built from a Categorical/Gaussian actor-critic policy with an AC_CNN_Atari representation."""
+
+    def __init__(self, policy):
+        self.parts = _Part()
+        self.trunk_ = _Trunk(policy.representation, self.parts)
+        if self.trunk_.tail != "flatten":
+            raise ValueError("the actor-critic path expects AC_CNN_Atari")
+        self.discrete = bool(getattr(policy, "discrete", False))
+        self.actor = _parse(policy.actor.model if self.discrete else policy.actor.mu)
+        self.critic = _parse(policy.critic.model)
+        self.logstd = None if self.discrete else policy.actor.logstd
+        n_params = sum(1 for _ in policy.parameters())
+        n_cov = self.trunk_.n_params + 2 * (len(self.actor) + len(self.critic)) + (0 if self.discrete else 1)
+        if n_params != n_cov:
+            raise ValueError("policy has parameters outside the conv / Linear chains")
+
+    @property
+    def stale(self):
+        return self.trunk_.stale
+
+    @stale.setter
+    def stale(self, v):
+        self.trunk_.stale = v
+
+    def refresh(self):
+        """Re-derive the (H, W, C)-ordered first fc weight now (the agent calls it before a captured rollout, whose
+        graph must not contain the copy)."""
+        self.trunk_.refresh()
+
+    def frames(self, x):
+        return self.trunk_.frames(x)
+
+    @torch.no_grad()
+    def trunk(self, x):
+        return self.trunk_.forward(x)
+
+    @torch.no_grad()
+    def forward(self, x):
+        """(logits or mu, logstd or None, v, ctx)."""
+        s, tctx = self.trunk_.forward(x)
+        a_outs = _chain(self.actor, s)
+        c_outs = _chain(self.critic, s)
+        return a_outs[-1], self.logstd, c_outs[-1][:, 0], (tctx, s, a_outs, c_outs)
+
+    @torch.no_grad()
+    def heads(self, x):
+        head, logstd, v, _ = self.forward(x)
+        return head, logstd, v
+
+    @torch.no_grad()
+    def backward(self, ctx, d_head, d_v):
+        """Writes every parameter gradient (d_head [B, K], d_v [B]: the loss kernel's outputs)."""
+        tctx, s, a_outs, c_outs = ctx
+        ds = _chain_backward(self.parts, self.actor, [s] + a_outs[:-1], a_outs, d_head)
+        ds = _chain_backward(self.parts, self.critic, [s] + c_outs[:-1], c_outs, d_v.view(-1, 1), acc=ds)
+        self.trunk_.backward(tctx, ds)
+
+
+class FusedQNetwork:
+    """BasicQnetwork over a Basic_CNN (or AC_CNN_Atari) representation: explicit eval forward / backward and the
+    target forward (deterministic.py:148-182)."""
+
+    def __init__(self, policy):
+        self.parts = _Part()
+        self.eval_trunk = _Trunk(policy.representation, self.parts)
+        self.target_trunk = _Trunk(policy.target_representation, self.parts)
+        self.eval_head = _parse(policy.eval_Qhead.model)
+        self.target_head = _parse(policy.target_Qhead.model)
+        n_params = sum(1 for _ in policy.parameters())
+        n_cov = 2 * self.eval_trunk.n_params + 4 * len(self.eval_head)
+        if n_params != n_cov:
+            raise ValueError("Q-network has parameters outside the conv / Linear chains")
+        self.eval_params = self.eval_trunk.params() + [t for lin, _, _ in self.eval_head for t in (lin.weight, lin.bias)]
+
+    @torch.no_grad()
+    def forward(self, x):
+        """evalQ [B, A] and the backward context."""
+        s, tctx = self.eval_trunk.forward(x)
+        outs = _chain(self.eval_head, s)
+        return outs[-1], (tctx, s, outs)
+
+    @torch.no_grad()
+    def target(self, x):
+        if self.target_trunk.tail == "flatten":
+            self.target_trunk.stale = True   # copy_target() may have changed it since the last call
+        s, _ = self.target_trunk.forward(x)
+        return _chain(self.target_head, s)[-1]
+
+    @torch.no_grad()
+    def backward(self, ctx, dq):
+        """dq = d loss / d evalQ [B, A] (K19); writes every eval parameter's gradient."""
+        _ensure_grads(self.eval_params)
+        tctx, s, outs = ctx
+        ds = _chain_backward(self.parts, self.eval_head, [s] + outs[:-1], outs, dq.contiguous())
+        self.eval_trunk.backward(tctx, ds)
+
+    def refresh(self):
+        self.eval_trunk.refresh()
+        self.target_trunk.refresh()

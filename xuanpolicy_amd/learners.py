@@ -272,18 +272,51 @@ class PerDQN_Learner(Learner):
             return x.to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
         return torch.as_tensor(x, dtype=torch.float32, device=dev).reshape(-1).contiguous()
 
+    def _fused_q(self):
+        """Explicit Q-network forward / backward (fused_cnn.FusedQNetwork) for CNN Q-networks on uint8 frames."""
+        fq = getattr(self, "_fq", None)
+        if fq is None:
+            fq = False
+            dev = next(self.policy.parameters()).device
+            if getattr(self, "fused_cnn_enabled", True) and dev.type == "cuda" and hasattr(self.policy, "eval_Qhead"):
+                from .fused_cnn import FusedQNetwork
+                try:
+                    fq = FusedQNetwork(self.policy)
+                except ValueError:
+                    fq = False
+            self._fq = fq
+        return fq or None
+
+    def q_values(self, obs):
+        """evalQ of the eval network (the agent's action selection)."""
+        fq = self._fused_q()
+        if fq is not None and isinstance(obs, torch.Tensor) and obs.dtype == torch.uint8 and obs.is_cuda:
+            return fq.forward(obs.contiguous())[0]
+        with torch.no_grad():
+            return self.policy(obs)[2]
+
     def update(self, obs_batch, act_batch, rew_batch, next_batch, terminal_batch, sync_info=True):
         self.iterations += 1
-        _, _, evalQ = self.policy(obs_batch)
+        fq = self._fused_q()
+        fused = (fq is not None and isinstance(obs_batch, torch.Tensor) and obs_batch.dtype == torch.uint8
+                 and obs_batch.is_cuda and isinstance(next_batch, torch.Tensor) and next_batch.dtype == torch.uint8)
+        if fused:   # K20 frames, MIOpen convs + K21, K23 max pool, Q head GEMMs; backward K24 / K22 + MIOpen
+            evalQ, ctx = fq.forward(obs_batch.contiguous())
+            targetQ = fq.target(next_batch.contiguous())
+        else:
+            _, _, evalQ = self.policy(obs_batch)
+            with torch.no_grad():
+                _, _, targetQ = self.policy.target(next_batch)
         dev = evalQ.device
-        with torch.no_grad():
-            _, _, targetQ = self.policy.target(next_batch)
         if self._err is None:
             self._err = torch.zeros(1, dtype=torch.int32, device=dev)
         dQ, td_abs, sc = ops.dqn_td_loss(evalQ.detach(), targetQ, self._f32(act_batch, dev), self._f32(rew_batch, dev),
                                          self._f32(terminal_batch, dev), self.gamma, err=self._err)
-        self.optimizer.zero_grad()
-        evalQ.backward(dQ)
+        if fused:
+            fq.backward(ctx, dQ)           # overwrites every eval-network gradient
+        else:
+            self.optimizer.zero_grad()
+            evalQ.backward(dQ)
         self.optimizer.step()
         if self.scheduler is not None:
             self.scheduler.step()
