@@ -135,6 +135,9 @@ struct RowIn {  // wave 0, lane = row of the tile
 template <int MODE, int ALGO, int ACT, int KMAX>
 struct HeadEpi {
     static constexpr int KP = (KMAX + 3) & ~3;  // 16-B aligned d-head rows
+    // phase-1 partials per pass: heads wider than 8 (C4's 17 / 18) go through s_part in two halves, so the K16 block
+    // fits 80 KiB of LDS (2 blocks per CU; 90 KiB with all 18 at once)
+    static constexpr int PH = KMAX > 8 ? (KMAX + 1) / 2 : KMAX;
     float wc[KMAX], acc_dw[KMAX], acc_dbh;      // phase 2 (column t)
     float acc_dbo[KMAX], acc_dls[KMAX], var_[KMAX], logsc[KMAX];
     float sum0, sum1, sum2, ent_const, inv_b, lo, hi, a_mean, a_inv, slope;
@@ -219,7 +222,7 @@ struct HeadEpi {
 
     // s_h holds h = act(z) of rows [tile*64, tile*64 + 64) (row stride kS).  Starts with a barrier
     // (s_h complete), ends with one (s_h / s_dh free for the next tile).
-    __device__ __forceinline__ void tile(const float *s_h, float (*s_part)[kTile][KMAX], float (*s_dh)[KP],
+    __device__ __forceinline__ void tile(const float *s_h, float (*s_part)[kTile][PH], float (*s_dh)[KP],
                                          const RowIn<KMAX> &in, int64_t tile, int64_t batch,
                                          const float *__restrict__ W, const float *__restrict__ bias,
                                          float *__restrict__ dz, int64_t ld, float ent_coef, float vf_coef) {
@@ -227,39 +230,55 @@ struct HeadEpi {
         const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
         __syncthreads();
         // ---- phase 1: partial dot products, row = lane, quarter = wave ----
-        {
-            float p[KMAX];
+        // Outputs [o0, o0 + PH) per pass; wide heads take two passes (re-reading the row quarter from LDS) so that
+        // s_part and the live partials stay half-sized.
+#pragma unroll 1
+        for (int o0 = 0; o0 < KMAX; o0 += PH) {
+            if (o0 > 0) __syncthreads();  // wave 0 has read the previous pass
+            float p[PH];
 #pragma unroll
-            for (int o = 0; o < KMAX; ++o) p[o] = 0.f;
+            for (int o = 0; o < PH; ++o) p[o] = 0.f;
             const float *hrow = s_h + lane * kS + wave * 64;
             const float *wq = W + wave * 64;
 #pragma unroll 4
             for (int j = 0; j < 16; ++j) {
                 const float4 hv = *reinterpret_cast<const float4 *>(hrow + 4 * j);
-                // unconditional (rows o >= K re-read row 0; their sums are never used): the KMAX scalar
-                // loads of a step issue together instead of one branch + load + wait per output
+                // unconditional (rows o >= K re-read row 0; their sums are never used): the scalar loads of a
+                // step issue together instead of one branch + load + wait per output
 #pragma unroll
-                for (int o = 0; o < KMAX; ++o) {
-                    const float4 w4 = *reinterpret_cast<const float4 *>(wq + (o < K ? o : 0) * kH + 4 * j);
+                for (int o = 0; o < PH; ++o) {
+                    const int oo = o0 + o;
+                    const float4 w4 = *reinterpret_cast<const float4 *>(wq + (oo < K ? oo : 0) * kH + 4 * j);
                     p[o] += hv.x * w4.x + hv.y * w4.y + hv.z * w4.z + hv.w * w4.w;
                 }
             }
 #pragma unroll
-            for (int o = 0; o < KMAX; ++o) s_part[wave][lane][o] = p[o];
+            for (int o = 0; o < PH; ++o) s_part[wave][lane][o] = p[o];
+            __syncthreads();
+            // the head outputs of wave 0's row: the 4 quarters summed in a fixed order, + bias, parked in the row's
+            // s_dh slots (free until the loss below overwrites them with d-head) so nothing stays live across passes
+            if (wave == 0) {
+#pragma unroll
+                for (int o = 0; o < PH; ++o)
+                    if (o0 + o < KMAX)
+                        s_dh[lane][o0 + o] =
+                            o0 + o < K ? ((s_part[0][lane][o] + s_part[1][lane][o]) +
+                                          (s_part[2][lane][o] + s_part[3][lane][o])) +
+                                             bias[o0 + o]
+                                       : 0.f;
+            }
         }
-        __syncthreads();
+        float hd[KMAX];
+        if (wave == 0) {
+#pragma unroll
+            for (int o = 0; o < KMAX; ++o) hd[o] = s_dh[lane][o];
+        }
         // ---- loss: wave 0, one lane per row ----
         if (wave == 0) {
             float dh_[KMAX];
 #pragma unroll
             for (int o = 0; o < KMAX; ++o) dh_[o] = 0.f;
             if (in.valid) {
-                float hd[KMAX];
-#pragma unroll
-                for (int o = 0; o < KMAX; ++o)
-                    hd[o] = o < K ? ((s_part[0][lane][o] + s_part[1][lane][o]) + (s_part[2][lane][o] + s_part[3][lane][o])) +
-                                        bias[o]
-                                  : 0.f;
                 if (MODE == 2) {
                     const float diffv = hd[0] - in.x;
                     sum0 += diffv * diffv;
@@ -458,7 +477,7 @@ template <int MODE, int ALGO, int ACT, int KMAX>
 __global__ __launch_bounds__(256, 2) void head_tile_kernel(XPA_HEAD_KERNEL_PARAMS) {
     using Epi = HeadEpi<MODE, ALGO, ACT, KMAX>;
     __shared__ __attribute__((aligned(16))) float s_h[kTile * kS];
-    __shared__ __attribute__((aligned(16))) float s_part[kWaves][kTile][KMAX];
+    __shared__ __attribute__((aligned(16))) float s_part[kWaves][kTile][Epi::PH];
     __shared__ __attribute__((aligned(16))) float s_dh[kTile][Epi::KP];
     __shared__ float s_stats[2];
     const int t = threadIdx.x;
@@ -578,11 +597,12 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
     using Epi = HeadEpi<MODE, ALGO, ACT, KMAX>;
     // ONE LDS array (a second __shared__ object beside the DMA target can make hipcc wait vmcnt(0) before
     // every chunk's ds_reads): operand stages / h tile, then the epilogue's partials, d head and stats.
-    constexpr int kPartOff = kTile * kS, kDhOff = kPartOff + kWaves * kTile * KMAX;
+    constexpr int kPartOff = kTile * kS, kDhOff = kPartOff + kWaves * kTile * Epi::PH;
     constexpr int kStatsOff = kDhOff + kTile * Epi::KP;
+    static_assert(KMAX <= 8 || (kStatsOff + 4) * 4 <= 81920, "wide heads: 2 blocks per CU");
     __shared__ __attribute__((aligned(16))) float lds[kStatsOff + 4];
     float *smem = lds;
-    auto s_part = reinterpret_cast<float(*)[kTile][KMAX]>(lds + kPartOff);
+    auto s_part = reinterpret_cast<float(*)[kTile][Epi::PH]>(lds + kPartOff);
     auto s_dh = reinterpret_cast<float(*)[Epi::KP]>(lds + kDhOff);
     float *s_stats = lds + kStatsOff;
     const unsigned lds_base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
