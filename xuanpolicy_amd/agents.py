@@ -397,9 +397,11 @@ class _OnPolicyAgent:
     def epoch_permutation(self, n, counter=None):
         """The minibatch permutation of the next epoch (ppoclip_agent.py:76-81): a device Feistel
         permutation keyed by (config.seed, epoch counter) — one launch instead of a sort."""
-        if counter is None:
-            counter = self._perm_counter
-            self._perm_counter += 1
+        if counter is not None:   # an explicit epoch (tests, replays): a fresh tensor, no live buffer touched
+            return ops.random_permutation(n, self.seed, counter,
+                                          out=torch.empty(n, dtype=torch.int64, device=self.device))
+        counter = self._perm_counter
+        self._perm_counter += 1
         if self._perm_buf is None or self._perm_buf.shape[0] != n:
             self._perm_buf = torch.empty(n, dtype=torch.int64, device=self.device)
         return ops.random_permutation(n, self.seed, counter, out=self._perm_buf)
