@@ -496,6 +496,15 @@ int xpa_thin_linear_act_bwd(int act, const float *g, int64_t ldg, const float *h
  * K20: dst[i] = float32(src[i] / 255.0) with the reference's arithmetic (NumPy float64 division, then the
  * float32 cast; cnn.py:89-92), bit for bit; n bytes in, n floats out (16-B aligned buffers take the vector path). */
 int xpa_frames_to_f32(const uint8_t *src, int64_t n, float *dst, xpa_stream_t stream);
+/* K25 — the first conv block straight from the uint8 frames (C3 AC_CNN_Atari / C5 Basic_CNN: cnn_block
+ * xuance/torch/utils/layers.py:36-57 on observations / 255.0, cnn.py:89-92): y = act(conv2d(x / 255, w, stride, pad)
+ * + bias) with x uint8 NHWC [batch, height, width, 4] (4-B aligned), w [32, 4, 8, 8] (torch's Conv2d layout), y f32
+ * NHWC [batch, OH, OW, 32], OH = (height + 2 pad - 8) / stride + 1 (zero padding).  Computed as sum x (w / 255) on
+ * fp32 MFMA (exact f32 fma chains; the 1/255 rounds once on the weight instead of once on the frame value).  act as xpa_bias_act.  channels must be 4,
+ * kernel 8 and out_channels 32 (else hipErrorInvalidValue). */
+int xpa_conv1_u8_fwd(int act, const uint8_t *x, int64_t batch, int64_t height, int64_t width, int64_t channels,
+                     int64_t kernel, int64_t stride, int64_t pad, const float *w, const float *bias,
+                     int64_t out_channels, float slope, float *y, xpa_stream_t stream);
 /* K21: y = act(y + bias) in place over [rows, cols] (bias [cols] or NULL): the conv / Linear bias and the
  * activation of cnn_block / mlp_block (xuance/torch/utils/layers.py:8-57).  cols % 4 == 0 and cols / 4 must
  * divide 256; act 0 identity, 1 LeakyReLU(slope) / ReLU, 2 tanh. */

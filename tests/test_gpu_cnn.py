@@ -223,3 +223,49 @@ def test_fused_qnetwork_matches_autograd(B):
         if not err <= 2e-5 * scale + 1e-8:
             bad.append((n, err, scale))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("B,act,slope", [(3, 1, 0.0), (17, 0, 0.0), (64, 1, 0.01), (5, 2, 0.0)])
+def test_conv1_u8_matches_conv2d(B, act, slope):
+    """K25 (the first conv block straight from uint8 frames on fp32 MFMA) == conv2d(K20 frames) + bias + act within
+    fp32 summation-order rounding, at the AC_CNN_Atari / Basic_CNN shape (84 x 84 x 4, 8 x 8 stride 4 pad 2 -> 32)."""
+    _l, ops = _lib()
+    g = torch.Generator(device="cpu").manual_seed(B)
+    x = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.int32).to(torch.uint8).to(DEV)
+    w = (torch.randn(32, 4, 8, 8, generator=g) * 0.05).to(DEV)
+    b = (torch.randn(32, generator=g) * 0.1).to(DEV)
+    y = torch.full((B, 21, 21, 32), float("nan"), device=DEV)
+    _l.check(ops.lib().xpa_conv1_u8_fwd(act, ops._p(x), B, 84, 84, 4, 8, 4, 2, ops._p(w), ops._p(b), 32, slope,
+                                        ops._p(y), ops._stream(DEV)), "conv1_u8")
+    xf = x.double() / 255.0
+    z = torch.nn.functional.conv2d(xf.permute(0, 3, 1, 2), w.double(), b.double(), 4, 2).permute(0, 2, 3, 1)
+    ref = {0: z, 1: torch.nn.functional.leaky_relu(z, slope), 2: torch.tanh(z)}[act]
+    torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=2e-5)
+
+
+def test_conv1_u8_scale_within_one_rounding():
+    """K25 scales by 1/255 on the weight side (sum x (w / 255)): with one-hot weights (output n reads tap
+    (c, ky, kx) = (n % 4, 2 + n // 8, 2 + n % 8 // 4 * 3) with weight 1) every output is x * float32(1 / 255), within
+    one f32 rounding of the reference's float32(x / 255.0) (K20), for all 256 byte values."""
+    _l, ops = _lib()
+    B = 8
+    x = (torch.arange(B * 84 * 84 * 4, dtype=torch.int64) * 2654435761 % 256).to(torch.uint8).reshape(B, 84, 84, 4)
+    x = x.to(DEV)
+    w = torch.zeros(32, 4, 8, 8)
+    taps = [(n % 4, 2 + n // 8, 2 + (n % 8) // 4 * 3) for n in range(32)]
+    for n, (c, ky, kx) in enumerate(taps):
+        w[n, c, ky, kx] = 1.0
+    w, b = w.to(DEV), torch.zeros(32, device=DEV)
+    y = torch.empty((B, 21, 21, 32), device=DEV)
+    _l.check(ops.lib().xpa_conv1_u8_fwd(0, ops._p(x), B, 84, 84, 4, 8, 4, 2, ops._p(w), ops._p(b), 32, 0.0, ops._p(y),
+                                        ops._stream(DEV)), "conv1_u8")
+    f = torch.empty((B, 84, 84, 4), device=DEV)
+    _l.check(ops.lib().xpa_frames_to_f32(ops._p(x), x.numel(), ops._p(f), ops._stream(DEV)), "frames")
+    yc, fc, xc = y.cpu(), f.cpu(), x.cpu()
+    for n, (c, ky, kx) in enumerate(taps):
+        iy = torch.arange(21) * 4 - 2 + ky   # taps chosen inside the frame for every output position
+        ix = torch.arange(21) * 4 - 2 + kx
+        xs = xc[:, iy][:, :, ix][..., c].float()
+        assert torch.equal(yc[..., n], xs * torch.tensor(1.0 / 255.0, dtype=torch.float32)), n
+        torch.testing.assert_close(yc[..., n], fc[:, iy][:, :, ix][..., c], rtol=1.2e-7, atol=0)
+    assert len(torch.unique(xc)) == 256

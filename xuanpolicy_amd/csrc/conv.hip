@@ -210,6 +210,121 @@ int grid_for(int64_t work, int64_t per_block, int64_t cap) {
     return (int)(g < 1 ? 1 : g);
 }
 
+
+// ---- K25: the first conv straight from the uint8 frames, on the fp32 matrix cores -------------------------------
+// y[b, oy, ox, n] = act(sum_{ky, kx, c} (x[b, oy S - P + ky, ox S - P + kx, c] / 255) W[n, c, ky, kx] + bias[n]) for
+// C = 4 input channels (one pixel = one dword), an 8 x 8 kernel (K = 256) and 32 output channels (N = 32): the
+// implicit GEMM [rows = B OH OW, 256] x [256, 32] with v_mfma_f32_32x32x2_f32 (exact f32 fma chains).  Lane (h, i)
+// of a wave owns output row i of a 32-row tile and pixel 2 t + h of each pixel pair t: it loads that pixel's dword
+// (0 outside the frame: the zero padding) and feeds its 4 bytes, as exact f32 integers (v_cvt_f32_ubyte, one VALU
+// op per MFMA), as the MFMA's k = h for channels c = 0..3, with the matching weights W[n, c, ky, kx] / 255 read from
+// an LDS image [pixel][n][c] (one ds_read_b128 per pixel): sum x (w / 255) instead of the reference's
+// sum float(x / 255) w — one f32 rounding per term either way (the scale rounds on the weight instead of the
+// frame), the same order of difference as any fp32 summation order.  Replaces K20 + MIOpen's conv + K21 for the forward (the uint8 frames are read
+// once, the f32 frame copy is never written).  Wave = 2 row tiles (2 accumulators), block = 4 waves = 256 rows,
+// grid-stride over row blocks (<= 4 blocks per CU) so the weight image is staged once per block.
+constexpr int kC1Rows = 256;
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Loads: 4 chunks of 8 pixel pairs (two kernel rows); chunk c + 1's 16 dwords per lane are requested before chunk
+// c's 64 MFMAs (a two-buffer register ring, fully unrolled), addresses as 32-bit offsets from each row tile's frame.
+template <int ACT>
+__device__ __forceinline__ void conv1_load_chunk(unsigned (&v)[2][8], const unsigned *const (&xr)[2], const int (&by)[2],
+                                                 const int (&bx)[2], int H, int W, int chunk, int h) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int p = 16 * chunk + 2 * j + h, ky = p >> 3, kx = p & 7;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+            const int iy = by[rt] + ky, ix = bx[rt] + kx;
+            const bool inb = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+            const unsigned d = xr[rt][inb ? iy * W + ix : 0];
+            v[rt][j] = inb ? d : 0u;
+        }
+    }
+}
+
+__device__ __forceinline__ void conv1_mfma_chunk(f32x16 (&acc)[2], const unsigned (&v)[2][8], const float *sB, int chunk,
+                                                 int h, int i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int p = 16 * chunk + 2 * j + h;
+        const f4v b4 = *reinterpret_cast<const f4v *>(sB + (p * 32 + i) * 4);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) {
+                const float a = (float)((v[rt][j] >> (8 * c)) & 0xffu);  // v_cvt_f32_ubyte<c>
+                acc[rt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b4[c], acc[rt], 0, 0, 0);
+            }
+        }
+    }
+}
+
+template <int ACT>
+__global__ __launch_bounds__(256, 4) void conv1_u8_fwd_kernel(const unsigned *__restrict__ x, int64_t rows, int H,
+                                                              int W, int OH, int OW, int S, int P,
+                                                              const float *__restrict__ w, const float *__restrict__ bias,
+                                                              float slope, float *__restrict__ y) {
+    __shared__ __attribute__((aligned(16))) float sB[64 * 32 * 4];  // [pixel p = ky 8 + kx][n][c]
+    const int t = threadIdx.x;
+    for (int e = t; e < 64 * 32 * 4; e += 256) {
+        const int c = e & 3, n = (e >> 2) & 31, p = e >> 7;
+        sB[e] = w[((n * 4 + c) * 8 + (p >> 3)) * 8 + (p & 7)] / 255.0f;  // the 1 / 255 scale on the weight side
+    }
+    __syncthreads();
+    const int lane = t & 63, h = lane >> 5, i = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const float bc = bias[i];
+    const int64_t ohw = (int64_t)OH * OW;
+    for (int64_t blk = blockIdx.x; blk * kC1Rows < rows; blk += gridDim.x) {
+        const int64_t r0 = blk * kC1Rows + wave * 64;
+        int by[2], bx[2];
+        const unsigned *xr[2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+            const int64_t m = r0 + rt * 32 + i;
+            const int64_t mc = m < rows ? m : rows - 1;
+            const int64_t b = mc / ohw;
+            const int rem = (int)(mc - b * ohw);
+            const int oy = rem / OW, ox = rem - (rem / OW) * OW;
+            by[rt] = oy * S - P;
+            bx[rt] = ox * S - P;
+            xr[rt] = x + b * H * W;
+        }
+        f32x16 acc[2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[rt][r] = 0.f;
+        unsigned va[2][8], vb[2][8];
+        // sched_barrier: keep the ring order (hipcc otherwise hoists all 64 loads and their 64-bit addresses: 248
+        // VGPRs, 2 waves per SIMD)
+        conv1_load_chunk<ACT>(va, xr, by, bx, H, W, 0, h);
+        conv1_load_chunk<ACT>(vb, xr, by, bx, H, W, 1, h);
+        __builtin_amdgcn_sched_barrier(0);
+        conv1_mfma_chunk(acc, va, sB, 0, h, i);
+        __builtin_amdgcn_sched_barrier(0);
+        conv1_load_chunk<ACT>(va, xr, by, bx, H, W, 2, h);
+        __builtin_amdgcn_sched_barrier(0);
+        conv1_mfma_chunk(acc, vb, sB, 1, h, i);
+        __builtin_amdgcn_sched_barrier(0);
+        conv1_load_chunk<ACT>(vb, xr, by, bx, H, W, 3, h);
+        __builtin_amdgcn_sched_barrier(0);
+        conv1_mfma_chunk(acc, va, sB, 2, h, i);
+        __builtin_amdgcn_sched_barrier(0);
+        conv1_mfma_chunk(acc, vb, sB, 3, h, i);
+        // C/D map: row = (r & 3) + 8 (r >> 2) + 4 h, column n = i
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t m = r0 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m < rows) y[m * 32 + i] = act_fwd<ACT>(acc[rt][r] + bc, slope);
+            }
+    }
+}
 }  // namespace
 
 XPA_API int xpa_frames_to_f32(const uint8_t *src, int64_t n, float *dst, xpa_stream_t stream) {
@@ -307,5 +422,27 @@ XPA_API int xpa_maxpool_act_bwd_bias(int act, const float *dout, const int32_t *
     else if (act == 1) XPA_MPB(1);
     else XPA_MPB(2);
 #undef XPA_MPB
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_conv1_u8_fwd(int act, const uint8_t *x, int64_t batch, int64_t height, int64_t width, int64_t channels,
+                             int64_t kernel, int64_t stride, int64_t pad, const float *w, const float *bias,
+                             int64_t out_channels, float slope, float *y, xpa_stream_t stream) {
+    if (batch <= 0 || channels != 4 || kernel != 8 || out_channels != 32 || stride < 1 || pad < 0 || act < 0 ||
+        act > 2 || !x || !w || !bias || !y || ((uintptr_t)x % 4) || height + 2 * pad < kernel ||
+        width + 2 * pad < kernel || height * width > (1 << 30))
+        return (int)hipErrorInvalidValue;
+    const int64_t OH = (height + 2 * pad - kernel) / stride + 1, OW = (width + 2 * pad - kernel) / stride + 1;
+    const int64_t rows = batch * OH * OW;
+    const int64_t blocks = (rows + kC1Rows - 1) / kC1Rows;
+    const dim3 grid((unsigned)(blocks < 1024 ? blocks : 1024)), block(256);
+    hipStream_t s = (hipStream_t)stream;
+#define XPA_C1(A_)                                                                                                   \
+    hipLaunchKernelGGL((conv1_u8_fwd_kernel<A_>), grid, block, 0, s, (const unsigned *)x, rows, (int)height,           \
+                       (int)width, (int)OH, (int)OW, (int)stride, (int)pad, w, bias, slope, y)
+    if (act == 0) XPA_C1(0);
+    else if (act == 1) XPA_C1(1);
+    else XPA_C1(2);
+#undef XPA_C1
     return xpa_launch_status();
 }

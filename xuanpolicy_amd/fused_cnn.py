@@ -7,7 +7,9 @@ xuance/torch/utils/layers.py:8-57, Categorical_AC_Policy xuance/torch/policies/c
 deterministic.py:148-182; the learners' loss.backward() (a2c_learner.py:31-33, perdqn_learner.py:37-40).
 
 Every activation stays NHWC ([rows = B*H*W, C] row-major), the layout the uint8 frames arrive in:
-  forward   K20 xpa_frames_to_f32 (uint8 -> float32 / 255, the reference's arithmetic bit for bit)
+  forward   the first conv block: K25 xpa_conv1_u8_fwd (the 4 x 8 x 8 -> 32 conv on fp32 MFMA straight from the uint8
+            frames, x / 255 as the reference's arithmetic bit for bit, bias + ReLU in its epilogue); other first
+            layers: K20 xpa_frames_to_f32 then MIOpen as below
             -> per conv: MIOpen conv2d without bias on the channels-last view -> K21 xpa_bias_act (bias + ReLU
                in place)
             -> AC_CNN_Atari: Flatten in NHWC order — the first fc layer uses its weight with the columns permuted
@@ -19,7 +21,8 @@ Every activation stays NHWC ([rows = B*H*W, C] row-major), the layout the uint8 
   backward  heads: GEMMs + K10 / K22 bias column sums -> AC_CNN_Atari fc: K22 xpa_act_bwd_bias (ReLU backward + bias
             gradient) -> dW GEMM (permuted back into the reference layout) + dX GEMM; Basic_CNN: K24 (the pooled
             gradient routed to the argmax, ReLU backward, bias gradient) -> per conv: K22 then MIOpen
-            convolution_backward (data, weight; no dX for the first conv).
+            convolution_backward (data, weight; no dX for the first conv, whose f32 input K20 makes here when K25
+            ran the forward).
 Parameter gradients are written into the parameters' .grad views (allocated when missing).
 """
 import torch
@@ -162,6 +165,12 @@ class _Trunk:
         self._dw_tmp = None
         self.parts = parts
         self.n_params = 2 * (len(self.convs) + len(self.fc))
+        # K25: the first conv block straight from the uint8 frames (4 channels, 8 x 8 kernel, 32 outputs: the Nature
+        # CNN's first layer); the f32 frame copy (K20) is then only made in the backward, for MIOpen's weight gradient
+        c0 = self.convs[0][0]
+        self.u8_conv1 = (C == 4 and c0.in_channels == 4 and c0.out_channels == 32 and tuple(c0.kernel_size) == (8, 8)
+                         and c0.stride[0] == c0.stride[1] and c0.padding[0] == c0.padding[1]
+                         and c0.padding_mode == "zeros")
 
     def params(self):
         out = []
@@ -196,13 +205,33 @@ class _Trunk:
                    "xpa_frames_to_f32")
         return out
 
+    def _conv1_u8(self, xu):
+        """K25: act(conv1(x / 255) + b) from the uint8 frames xu [B, H, W, 4] -> NHWC f32."""
+        conv, code, slope = self.convs[0]
+        B, H, W, C = xu.shape
+        k, st, pd = 8, conv.stride[0], conv.padding[0]
+        OH, OW = (H + 2 * pd - k) // st + 1, (W + 2 * pd - k) // st + 1
+        w = conv.weight if conv.weight.is_contiguous() else conv.weight.contiguous()
+        y = torch.empty((B, OH, OW, 32), dtype=torch.float32, device=xu.device)
+        _lib.check(ops.lib().xpa_conv1_u8_fwd(code, ops._p(xu), B, H, W, C, k, st, pd, ops._p(w), ops._p(conv.bias), 32,
+                                              float(slope), ops._p(y), ops._stream(xu.device)), "xpa_conv1_u8_fwd")
+        return y
+
     @torch.no_grad()
     def forward(self, x):
-        """x uint8 [B, H, W, C] -> (state [B, d], context for backward)."""
+        """x uint8 [B, H, W, C] -> (state [B, d], context for backward).  With K25 the context keeps the uint8 frames
+        as its first entry (backward converts them for the first conv's weight gradient)."""
         B = x.shape[0]
-        h = self.frames(x.reshape((B,) + self.in_hwc))
-        hs = [h]
-        for conv, code, slope in self.convs:
+        xu = x.reshape((B,) + self.in_hwc)
+        if self.u8_conv1 and xu.dtype == torch.uint8 and xu.is_contiguous() and xu.device.type == "cuda":
+            h = self._conv1_u8(xu)
+            hs = [xu, h]
+            convs = self.convs[1:]
+        else:
+            h = self.frames(xu)
+            hs = [h]
+            convs = self.convs
+        for conv, code, slope in convs:
             z = F.conv2d(h.permute(0, 3, 1, 2), conv.weight, None, conv.stride, conv.padding)
             y = z.permute(0, 2, 3, 1)
             if not y.is_contiguous():
@@ -275,8 +304,9 @@ class _Trunk:
                     g = g.contiguous()
                 _act_bwd_bias(parts, code, g.view(-1, Cy), y.view(-1, Cy), slope, conv.bias.grad)
             need_in = i > 0
+            x_in = self.frames(hs[i]) if hs[i].dtype == torch.uint8 else hs[i]
             gx, gw, _ = torch.ops.aten.convolution_backward(
-                g.permute(0, 3, 1, 2), hs[i].permute(0, 3, 1, 2), conv.weight, None, list(conv.stride),
+                g.permute(0, 3, 1, 2), x_in.permute(0, 3, 1, 2), conv.weight, None, list(conv.stride),
                 list(conv.padding), [1, 1], False, [0, 0], 1, [need_in, True, False])
             conv.weight.grad.copy_(gw)
             if need_in:
