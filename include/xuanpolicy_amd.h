@@ -505,6 +505,14 @@ int xpa_frames_to_f32(const uint8_t *src, int64_t n, float *dst, xpa_stream_t st
 int xpa_conv1_u8_fwd(int act, const uint8_t *x, int64_t batch, int64_t height, int64_t width, int64_t channels,
                      int64_t kernel, int64_t stride, int64_t pad, const float *w, const float *bias,
                      int64_t out_channels, float slope, float *y, xpa_stream_t stream);
+/* K27 — the data gradient of a stride-s (1 or 2), 2s x 2s conv with 32 input / 64 output channels (the Nature CNN's
+ * second conv: 4 x 4 stride 2 pad 1, 32 -> 64; torch's convolution_backward input gradient inside loss.backward(),
+ * a2c_learner.py:31-33): dx NHWC [batch, in_h, in_w, 32] = conv_transpose(dy NHWC [batch, out_h, out_w, 64] (16-B
+ * aligned), w [64, 32, 2s, 2s]), every element written (no accumulation into dx).  fp32 MFMA, one implicit GEMM per
+ * stride residue class (K = 4 taps x 64 channels).  out_h / out_w must be the forward's output size. */
+int xpa_conv_dgrad_s2k(const float *dy, int64_t batch, int64_t out_h, int64_t out_w, int64_t out_channels,
+                       const float *w, int64_t in_channels, int64_t kernel, int64_t stride, int64_t pad, int64_t in_h,
+                       int64_t in_w, float *dx, xpa_stream_t stream);
 /* K21: y = act(y + bias) in place over [rows, cols] (bias [cols] or NULL): the conv / Linear bias and the
  * activation of cnn_block / mlp_block (xuance/torch/utils/layers.py:8-57).  cols % 4 == 0 and cols / 4 must
  * divide 256; act 0 identity, 1 LeakyReLU(slope) / ReLU, 2 tanh. */

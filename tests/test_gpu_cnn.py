@@ -269,3 +269,20 @@ def test_conv1_u8_scale_within_one_rounding():
         assert torch.equal(yc[..., n], xs * torch.tensor(1.0 / 255.0, dtype=torch.float32)), n
         torch.testing.assert_close(yc[..., n], fc[:, iy][:, :, ix][..., c], rtol=1.2e-7, atol=0)
     assert len(torch.unique(xc)) == 256
+
+
+@pytest.mark.parametrize("B,H,k,s,p", [(7, 21, 4, 2, 1), (64, 21, 4, 2, 1), (3, 20, 4, 2, 0), (5, 19, 4, 2, 3),
+                                       (2, 9, 2, 1, 0), (4, 11, 2, 1, 1)])
+def test_conv_dgrad_s2k_matches_conv2d_input(B, H, k, s, p):
+    """K27 (data gradient of a 2s x 2s stride-s conv, 32 -> 64 channels, one implicit GEMM per residue class) ==
+    torch.nn.grad.conv2d_input in float64, odd / even sizes, padding 0 .. 3 and stride 1 included."""
+    _l, ops = _lib()
+    g = torch.Generator(device="cpu").manual_seed(B * 100 + H)
+    OH = (H + 2 * p - k) // s + 1
+    dy = torch.randn(B, OH, OH, 64, generator=g).to(DEV)
+    w = (torch.randn(64, 32, k, k, generator=g) * 0.1).to(DEV)
+    dx = torch.full((B, H, H, 32), float("nan"), device=DEV)
+    _l.check(ops.lib().xpa_conv_dgrad_s2k(ops._p(dy), B, OH, OH, 64, ops._p(w), 32, k, s, p, H, H, ops._p(dx),
+                                          ops._stream(DEV)), "dgrad")
+    ref = torch.nn.grad.conv2d_input((B, 32, H, H), w.double(), dy.double().permute(0, 3, 1, 2), s, p)
+    torch.testing.assert_close(dx.double(), ref.permute(0, 2, 3, 1), rtol=1e-5, atol=1e-5)

@@ -65,6 +65,8 @@ SIGNATURES = {
     "xpa_act_bwd_colsum": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_i64, c_i64, c_f32, c_p, c_p, c_p]),
     "xpa_colsum_finalize": (ctypes.c_int, [c_p, c_i64, c_i64, c_p, c_p]),
     "xpa_frames_to_f32": (ctypes.c_int, [c_p, c_i64, c_p, c_p]),
+    "xpa_conv_dgrad_s2k": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64,
+                                           c_i64, c_p, c_p]),
     "xpa_conv1_u8_fwd": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p,
                                          c_i64, c_f32, c_p, c_p]),
     "xpa_bias_act": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_p, c_f32, c_p]),

@@ -325,6 +325,135 @@ __global__ __launch_bounds__(256, 4) void conv1_u8_fwd_kernel(const unsigned *__
             }
     }
 }
+
+// ---- K27: data gradient of a stride-s, 2s x 2s conv (the Nature CNN's second conv: 4 x 4 stride 2, 32 -> 64) ------
+// dX[b, iy, ix, n] = sum_{ky, kx, co} dY[b, oy, ox, co] W[co, n, ky, kx] over iy = oy s - P + ky, ix likewise.  With a
+// 2s kernel every input pixel takes exactly the taps (oy0 - dy, ky0 + dy s) x (ox0 - dx, kx0 + dx s), dy, dx in
+// {0, 1}, where oy0 = (iy + P) / s and ky0 = (iy + P) % s: the s x s residue classes (ky0, kx0) each form a plain
+// implicit GEMM [rows of the class, K = 4 taps x 64 co] x [K, 32] whose weight operand is uniform over the class.  A
+// block owns 256 rows of one class (waves of 2 x 32 rows, v_mfma_f32_32x32x2_f32 as K25): lane (h, i) loads, for its
+// row i and tap t, the dY quads 2 j + h (16 B: channels 4q .. 4q + 3; 0 where the tap's output pixel is outside the
+// map) and feeds their 4 components as the MFMA's k = h against W[4 q + c, n, ky_t, kx_t] from the class's LDS image
+// [tap][co quad][n][4].  Chunks of (tap, half of its 64 channels) in a two-buffer register ring.  Replaces MIOpen's
+// stride-2 backward-data kernel (27 % of the fp32 MFMA peak at the C3 update, r02 trace).
+constexpr int kDgRows = 256;
+
+struct DgradGeom {
+    int H, W, OH, OW, S, P;
+    int ny[2], nx[2], iy0[2], ix0[2];  // per residue (s <= 2): rows / first index of the class
+    int64_t tiles[4];                  // block-tile prefix ends of the (ry, rx) classes in order 00, 01, 10, 11
+    int64_t B;
+};
+
+__device__ __forceinline__ void dgrad_load_chunk(f4v (&v)[2][4], const float *const (&yr)[2], const bool (&ok)[2][4],
+                                                 int tap, int half, int h) {  // every load from a clamped address
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int q = 2 * (4 * half + j) + h;  // channel quad
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+            const f4v d = *reinterpret_cast<const f4v *>(yr[rt] + 4 * q);
+            const f4v z = {0.f, 0.f, 0.f, 0.f};
+            v[rt][j] = ok[rt][tap] ? d : z;
+        }
+    }
+}
+
+__device__ __forceinline__ void dgrad_mfma_chunk(f32x16 (&acc)[2], const f4v (&v)[2][4], const float *sB, int tap,
+                                                 int half, int h, int i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int q = 2 * (4 * half + j) + h;
+        const f4v b4 = *reinterpret_cast<const f4v *>(sB + ((tap * 16 + q) * 32 + i) * 4);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+                acc[rt] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[rt][j][c], b4[c], acc[rt], 0, 0, 0);
+    }
+}
+
+__global__ __launch_bounds__(256, 2) void conv_dgrad_s2k_kernel(const float *__restrict__ dy, const float *__restrict__ w,
+                                                                DgradGeom g, float *__restrict__ dx) {
+    __shared__ __attribute__((aligned(16))) float sB[4 * 16 * 32 * 4];  // [tap][co quad][n][4]
+    const int t = threadIdx.x;
+    const int64_t bid = blockIdx.x;
+    const int cls = bid < g.tiles[0] ? 0 : bid < g.tiles[1] ? 1 : bid < g.tiles[2] ? 2 : 3;
+    const int64_t tile = bid - (cls ? g.tiles[cls - 1] : 0);
+    const int ry = cls >> 1, rx = cls & 1;
+    const int K = 2 * g.S;
+    for (int e = t; e < 4 * 16 * 32 * 4; e += 256) {  // W [64 co][32 n][K][K]
+        const int c = e & 3, n = (e >> 2) & 31, q = (e >> 7) & 15, tap = e >> 11;
+        const int ky = ry + (tap >> 1) * g.S, kx = rx + (tap & 1) * g.S;
+        sB[e] = w[(((4 * q + c) * 32 + n) * K + ky) * K + kx];
+    }
+    __syncthreads();
+    const int lane = t & 63, h = lane >> 5, i = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int ny = g.ny[ry], nx = g.nx[rx];
+    const int64_t per_img = (int64_t)ny * nx, rows = g.B * per_img;
+    const int64_t r0 = tile * kDgRows + wave * 64;
+    const float *yr[2][4];
+    bool ok[2][4];
+    int64_t orow[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+        const int64_t m = r0 + rt * 32 + i;
+        const bool mv = m < rows;
+        const int64_t mc = mv ? m : 0;
+        const int64_t b = mc / per_img;
+        const int rem = (int)(mc - b * per_img);
+        const int ay = rem / nx, ax = rem - (rem / nx) * nx;
+        const int iy = g.iy0[ry] + g.S * ay, ix = g.ix0[rx] + g.S * ax;
+        orow[rt] = mv ? (b * g.H + iy) * g.W + ix : -1;
+        const int oy0 = (iy + g.P) / g.S, ox0 = (ix + g.P) / g.S;
+#pragma unroll
+        for (int tap = 0; tap < 4; ++tap) {
+            const int oy = oy0 - (tap >> 1), ox = ox0 - (tap & 1);
+            const bool v = mv && (unsigned)oy < (unsigned)g.OH && (unsigned)ox < (unsigned)g.OW;
+            ok[rt][tap] = v;
+            yr[rt][tap] = dy + ((b * g.OH + (v ? oy : 0)) * g.OW + (v ? ox : 0)) * 64;
+        }
+    }
+    f32x16 acc[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[rt][r] = 0.f;
+    f4v va[2][4], vb[2][4];
+    // 8 chunks (tap, half of the 64 channels): chunk k + 1 requested before chunk k's 32 MFMAs
+#pragma unroll
+    for (int tap = 0; tap < 4; ++tap) {
+        const float *ya[2] = {yr[0][tap], yr[1][tap]};
+        if (tap == 0) dgrad_load_chunk(va, ya, ok, tap, 0, h);
+        dgrad_load_chunk(vb, ya, ok, tap, 1, h);
+        __builtin_amdgcn_sched_barrier(0);
+        dgrad_mfma_chunk(acc, va, sB, tap, 0, h, i);
+        __builtin_amdgcn_sched_barrier(0);
+        if (tap + 1 < 4) {
+            const float *yn[2] = {yr[0][tap + 1], yr[1][tap + 1]};
+            dgrad_load_chunk(va, yn, ok, tap + 1, 0, h);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        dgrad_mfma_chunk(acc, vb, sB, tap, 1, h, i);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // C/D map: row = (r & 3) + 8 (r >> 2) + 4 h of the tile, column n = i; the tile's rows are scattered pixels
+    __shared__ int64_t s_orow[4][32];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+        // every lane learns the output offsets of its 16 rows from the row owners (lane i, h = 0)
+        __builtin_amdgcn_wave_barrier();
+        if (h == 0) s_orow[wave][i] = orow[rt];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int64_t o = s_orow[wave][row];
+            if (o >= 0) dx[o * 32 + i] = acc[rt][r];
+        }
+    }
+}
 }  // namespace
 
 XPA_API int xpa_frames_to_f32(const uint8_t *src, int64_t n, float *dst, xpa_stream_t stream) {
@@ -444,5 +573,34 @@ XPA_API int xpa_conv1_u8_fwd(int act, const uint8_t *x, int64_t batch, int64_t h
     else if (act == 1) XPA_C1(1);
     else XPA_C1(2);
 #undef XPA_C1
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_conv_dgrad_s2k(const float *dy, int64_t batch, int64_t out_h, int64_t out_w, int64_t out_channels,
+                               const float *w, int64_t in_channels, int64_t kernel, int64_t stride, int64_t pad,
+                               int64_t in_h, int64_t in_w, float *dx, xpa_stream_t stream) {
+    if (batch <= 0 || out_channels != 64 || in_channels != 32 || stride < 1 || stride > 2 || kernel != 2 * stride ||
+        pad < 0 || pad >= stride * 2 || in_h < 1 || in_w < 1 || !dy || !w || !dx || ((uintptr_t)dy % 16) ||
+        out_h != (in_h + 2 * pad - kernel) / stride + 1 || out_w != (in_w + 2 * pad - kernel) / stride + 1 ||
+        out_h < 1 || out_w < 1)
+        return (int)hipErrorInvalidValue;
+    DgradGeom g{};
+    g.H = (int)in_h; g.W = (int)in_w; g.OH = (int)out_h; g.OW = (int)out_w; g.S = (int)stride; g.P = (int)pad;
+    g.B = batch;
+    for (int r = 0; r < 2; ++r) {
+        const int s_ = (int)stride;
+        const int y0 = (((r - (int)pad) % s_) + s_) % s_, x0 = y0;
+        g.iy0[r] = y0; g.ix0[r] = x0;
+        g.ny[r] = (r < s_ && y0 < g.H) ? (g.H - y0 + s_ - 1) / s_ : 0;
+        g.nx[r] = (r < s_ && x0 < g.W) ? (g.W - x0 + s_ - 1) / s_ : 0;
+    }
+    int64_t acc = 0;
+    for (int c = 0; c < 4; ++c) {
+        const int64_t rows = batch * (int64_t)g.ny[c >> 1] * g.nx[c & 1];
+        acc += (rows + kDgRows - 1) / kDgRows;
+        g.tiles[c] = acc;
+    }
+    if (acc <= 0 || acc > 0x7fffffff) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(conv_dgrad_s2k_kernel, dim3((unsigned)acc), dim3(256), 0, (hipStream_t)stream, dy, w, g, dx);
     return xpa_launch_status();
 }

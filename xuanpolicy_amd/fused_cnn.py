@@ -8,8 +8,8 @@ deterministic.py:148-182; the learners' loss.backward() (a2c_learner.py:31-33, p
 
 Every activation stays NHWC ([rows = B*H*W, C] row-major), the layout the uint8 frames arrive in:
   forward   the first conv block: K25 xpa_conv1_u8_fwd (the 4 x 8 x 8 -> 32 conv on fp32 MFMA straight from the uint8
-            frames, x / 255 as the reference's arithmetic bit for bit, bias + ReLU in its epilogue); other first
-            layers: K20 xpa_frames_to_f32 then MIOpen as below
+            frames as sum x (w / 255) — one f32 rounding per term like the reference's sum float(x / 255) w —, bias
+            + ReLU in its epilogue); other first layers: K20 xpa_frames_to_f32 then MIOpen as below
             -> per conv: MIOpen conv2d without bias on the channels-last view -> K21 xpa_bias_act (bias + ReLU
                in place)
             -> AC_CNN_Atari: Flatten in NHWC order — the first fc layer uses its weight with the columns permuted
@@ -21,8 +21,9 @@ Every activation stays NHWC ([rows = B*H*W, C] row-major), the layout the uint8 
   backward  heads: GEMMs + K10 / K22 bias column sums -> AC_CNN_Atari fc: K22 xpa_act_bwd_bias (ReLU backward + bias
             gradient) -> dW GEMM (permuted back into the reference layout) + dX GEMM; Basic_CNN: K24 (the pooled
             gradient routed to the argmax, ReLU backward, bias gradient) -> per conv: K22 then MIOpen
-            convolution_backward (data, weight; no dX for the first conv, whose f32 input K20 makes here when K25
-            ran the forward).
+            convolution_backward (weight; data too except where K27 xpa_conv_dgrad_s2k takes the data gradient — the
+            4 x 4 stride-2 32 -> 64 conv; no dX for the first conv, whose f32 input K20 makes here when K25 ran the
+            forward).
 Parameter gradients are written into the parameters' .grad views (allocated when missing).
 """
 import torch
@@ -257,6 +258,24 @@ class _Trunk:
             fouts.append(s)
         return s, (hs, None, flat, fouts)
 
+    @staticmethod
+    def _dgrad_ok(conv):
+        """K27 takes the data gradient of 2s x 2s, stride-s (1, 2) convs with 32 -> 64 channels."""
+        k, st, pd = conv.kernel_size, conv.stride, conv.padding
+        return (conv.in_channels == 32 and conv.out_channels == 64 and k[0] == k[1] and st[0] == st[1]
+                and pd[0] == pd[1] and st[0] in (1, 2) and k[0] == 2 * st[0] and pd[0] < k[0]
+                and conv.padding_mode == "zeros" and conv.weight.is_contiguous())
+
+    @staticmethod
+    def _dgrad(conv, g, in_shape):
+        """K27: d input (NHWC [B, H, W, 32]) from g = d output (NHWC [B, OH, OW, 64], contiguous)."""
+        B, H, W = in_shape[0], in_shape[1], in_shape[2]
+        dx = torch.empty((B, H, W, 32), dtype=torch.float32, device=g.device)
+        _lib.check(ops.lib().xpa_conv_dgrad_s2k(ops._p(g), B, g.shape[1], g.shape[2], 64, ops._p(conv.weight), 32,
+                                                conv.kernel_size[0], conv.stride[0], conv.padding[0], H, W, ops._p(dx),
+                                                ops._stream(g.device)), "xpa_conv_dgrad_s2k")
+        return dx
+
     @torch.no_grad()
     def backward(self, ctx, ds):
         """ds: d loss / d state [B, d]; writes every trunk parameter's gradient."""
@@ -305,11 +324,14 @@ class _Trunk:
                 _act_bwd_bias(parts, code, g.view(-1, Cy), y.view(-1, Cy), slope, conv.bias.grad)
             need_in = i > 0
             x_in = self.frames(hs[i]) if hs[i].dtype == torch.uint8 else hs[i]
+            k27 = need_in and self._dgrad_ok(conv)
             gx, gw, _ = torch.ops.aten.convolution_backward(
                 g.permute(0, 3, 1, 2), x_in.permute(0, 3, 1, 2), conv.weight, None, list(conv.stride),
-                list(conv.padding), [1, 1], False, [0, 0], 1, [need_in, True, False])
+                list(conv.padding), [1, 1], False, [0, 0], 1, [need_in and not k27, True, False])
             conv.weight.grad.copy_(gw)
-            if need_in:
+            if k27:
+                g = self._dgrad(conv, g, x_in.shape)
+            elif need_in:
                 g = gx.permute(0, 2, 3, 1)
         self.stale = True   # the optimizer step that follows changes the fc weight
 
