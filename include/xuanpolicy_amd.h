@@ -513,6 +513,14 @@ int xpa_conv1_u8_fwd(int act, const uint8_t *x, int64_t batch, int64_t height, i
 int xpa_conv_dgrad_s2k(const float *dy, int64_t batch, int64_t out_h, int64_t out_w, int64_t out_channels,
                        const float *w, int64_t in_channels, int64_t kernel, int64_t stride, int64_t pad, int64_t in_h,
                        int64_t in_w, float *dx, xpa_stream_t stream);
+/* K26 — K25's weight gradient from the uint8 frames (the first conv's dW in loss.backward()): per-block partials
+ * [xpa_conv1_u8_wgrad_num_partials(), 32 * 4 * 8 * 8] in the weight layout [n][c][ky][kx] of
+ * sum_rows dz[row, n] x[row's tap] / 255 (dz NHWC [batch, OH, OW, 32] f32: the gradient at the conv's output after
+ * the activation backward; x as xpa_conv1_u8_fwd), reduced by xpa_colsum_finalize into the weight gradient. */
+int64_t xpa_conv1_u8_wgrad_num_partials(void);
+int xpa_conv1_u8_wgrad(const float *dz, const uint8_t *x, int64_t batch, int64_t height, int64_t width,
+                       int64_t channels, int64_t kernel, int64_t stride, int64_t pad, int64_t out_channels,
+                       float *partial, xpa_stream_t stream);
 /* K21: y = act(y + bias) in place over [rows, cols] (bias [cols] or NULL): the conv / Linear bias and the
  * activation of cnn_block / mlp_block (xuance/torch/utils/layers.py:8-57).  cols % 4 == 0 and cols / 4 must
  * divide 256; act 0 identity, 1 LeakyReLU(slope) / ReLU, 2 tanh. */

@@ -454,6 +454,118 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_s2k_kernel(const float *__r
         }
     }
 }
+
+// ---- K26: the first conv's weight gradient straight from the uint8 frames ----------------------------------------
+// dW[n, c, ky, kx] = sum_rows dz[row, n] x[row's pixel (ky, kx), c] / 255 for K25's conv (4 channels, 8 x 8, 32
+// outputs; dz NHWC [B, OH, OW, 32] after the activation backward).  Split over rows: wave w of a block streams its
+// share of rows two at a time (the MFMA's k = the row pair), A = dz^T (lane (h, i): dz[row 2s + h][n = i], one f32
+// load), B = the frames: lane (h, j) loads the dword of pixel 32 g + j (g = 0, 1) of its row and feeds byte c to output
+// tile (g, c) — so one load of dz + two pixel dwords feed 8 MFMAs into 8 32 x 32 tiles (128 accumulator registers):
+// [32 n] x [256 = (g, c, j)].  The block's 4 waves are added in order through LDS and the block writes one partial row
+// (8192 floats, the weight layout [n][c][ky][kx], divided by 255 once); xpa_colsum_finalize sums the partials in f64.
+constexpr int kWgBlocks = 512;
+
+__global__ __launch_bounds__(256, 2) void conv1_u8_wgrad_kernel(const float *__restrict__ dz, const unsigned *__restrict__ x,
+                                                                int64_t rows, int H, int W, int OH, int OW, int S,
+                                                                int P, float *__restrict__ partial) {
+    __shared__ __attribute__((aligned(16))) float s_red[64 * 16 * 8];  // one wave's accumulators, lane-major
+    const int t = threadIdx.x, lane = t & 63, h = lane >> 5, j = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    // this wave's row range (row pairs split evenly over every wave of the grid)
+    const int64_t pairs = (rows + 1) / 2, nw = (int64_t)gridDim.x * 4, gw = (int64_t)blockIdx.x * 4 + wave;
+    const int64_t p0 = pairs * gw / nw, p1 = pairs * (gw + 1) / nw;
+    f32x16 acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+    // this lane's row 2 p + h, tracked incrementally as (b, oy, ox); groups of 4 row pairs, the next group's loads
+    // (4 dz values + 8 pixel dwords per lane) requested before the current group's 32 MFMAs
+    int64_t m = 2 * p0 + h;
+    const int64_t ohw = (int64_t)OH * OW;
+    int64_t b = m / ohw;
+    int rem = (int)(m - b * ohw);
+    int oy = rem / OW, ox = rem - (rem / OW) * OW;
+    const int ky0 = j >> 3, kx = j & 7;  // pixel 32 g + j: ky = 4 g + ky0
+    constexpr int U = 4;
+    float an[U];
+    unsigned dn[U][2];
+    auto load_group = [&](int64_t pp) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool mv = pp + u < p1 && m < rows;
+            an[u] = dz[(mv ? m : 0) * 32 + j];
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+                const int iy = oy * S - P + 4 * g + ky0, ix = ox * S - P + kx;
+                const bool inb = mv && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+                const unsigned v = x[((mv ? b : 0) * H + (inb ? iy : 0)) * W + (inb ? ix : 0)];
+                dn[u][g] = inb ? v : 0u;
+            }
+            if (!mv) an[u] = 0.f;
+            m += 2;  // advance this lane's row by 2
+            ox += 2;
+            while (ox >= OW) {
+                ox -= OW;
+                if (++oy >= OH) {
+                    oy = 0;
+                    ++b;
+                }
+            }
+        }
+    };
+    if (p0 < p1) load_group(p0);
+    for (int64_t pp = p0; pp < p1; pp += U) {
+        float a[U];
+        unsigned d[U][2];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            a[u] = an[u];
+            d[u][0] = dn[u][0];
+            d[u][1] = dn[u][1];
+        }
+        if (pp + U < p1) load_group(pp + U);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    acc[4 * g + c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], (float)((d[u][g] >> (8 * c)) & 0xffu),
+                                                                          acc[4 * g + c], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // waves 1..3 added into wave 0 in order
+    for (int src = 1; src < 4; ++src) {
+        __syncthreads();
+        if (wave == src) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) s_red[(q * 16 + r) * 64 + lane] = acc[q][r];
+        }
+        __syncthreads();
+        if (wave == 0) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[q][r] += s_red[(q * 16 + r) * 64 + lane];
+        }
+    }
+    if (wave != 0) return;
+    // D of tile (g, c): row n = (r & 3) + 8 (r >> 2) + 4 h, column j = pixel 32 g + j -> W[n][c][ky][kx]
+    float *pr = partial + (int64_t)blockIdx.x * 8192;
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = (r & 3) + 8 * (r >> 2) + 4 * h;
+                pr[(n * 4 + c) * 64 + 32 * g + j] = acc[4 * g + c][r] / 255.0f;
+            }
+}
 }  // namespace
 
 XPA_API int xpa_frames_to_f32(const uint8_t *src, int64_t n, float *dst, xpa_stream_t stream) {
@@ -602,5 +714,20 @@ XPA_API int xpa_conv_dgrad_s2k(const float *dy, int64_t batch, int64_t out_h, in
     }
     if (acc <= 0 || acc > 0x7fffffff) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(conv_dgrad_s2k_kernel, dim3((unsigned)acc), dim3(256), 0, (hipStream_t)stream, dy, w, g, dx);
+    return xpa_launch_status();
+}
+
+XPA_API int64_t xpa_conv1_u8_wgrad_num_partials(void) { return kWgBlocks; }
+
+XPA_API int xpa_conv1_u8_wgrad(const float *dz, const uint8_t *x, int64_t batch, int64_t height, int64_t width,
+                               int64_t channels, int64_t kernel, int64_t stride, int64_t pad, int64_t out_channels,
+                               float *partial, xpa_stream_t stream) {
+    if (batch <= 0 || channels != 4 || kernel != 8 || out_channels != 32 || stride < 1 || pad < 0 || !dz || !x ||
+        !partial || ((uintptr_t)x % 4) || height + 2 * pad < kernel || width + 2 * pad < kernel)
+        return (int)hipErrorInvalidValue;
+    const int64_t OH = (height + 2 * pad - kernel) / stride + 1, OW = (width + 2 * pad - kernel) / stride + 1;
+    hipLaunchKernelGGL(conv1_u8_wgrad_kernel, dim3(kWgBlocks), dim3(256), 0, (hipStream_t)stream, dz,
+                       (const unsigned *)x, batch * OH * OW, (int)height, (int)width, (int)OH, (int)OW, (int)stride,
+                       (int)pad, partial);
     return xpa_launch_status();
 }

@@ -22,8 +22,8 @@ Every activation stays NHWC ([rows = B*H*W, C] row-major), the layout the uint8 
             gradient) -> dW GEMM (permuted back into the reference layout) + dX GEMM; Basic_CNN: K24 (the pooled
             gradient routed to the argmax, ReLU backward, bias gradient) -> per conv: K22 then MIOpen
             convolution_backward (weight; data too except where K27 xpa_conv_dgrad_s2k takes the data gradient — the
-            4 x 4 stride-2 32 -> 64 conv; no dX for the first conv, whose f32 input K20 makes here when K25 ran the
-            forward).
+            4 x 4 stride-2 32 -> 64 conv); the first conv (no dX) after K25: K26 xpa_conv1_u8_wgrad from the uint8
+            frames + the f64 column-sum finalize (no f32 frame copy anywhere).
 Parameter gradients are written into the parameters' .grad views (allocated when missing).
 """
 import torch
@@ -258,6 +258,19 @@ class _Trunk:
             fouts.append(s)
         return s, (hs, None, flat, fouts)
 
+    def _conv1_wgrad(self, conv, g, xu):
+        """K26 partials + the f64 column-sum finalize -> conv.weight.grad (g: NHWC d output after K22)."""
+        L, st = ops.lib(), ops._stream(g.device)
+        if getattr(self, "_wg_part", None) is None:
+            self._wg_part = torch.empty((int(L.xpa_conv1_u8_wgrad_num_partials()), 8192), dtype=torch.float32,
+                                        device=g.device)
+        g = g if g.is_contiguous() else g.contiguous()
+        B, H, W, C = xu.shape
+        _lib.check(L.xpa_conv1_u8_wgrad(ops._p(g), ops._p(xu), B, H, W, C, 8, conv.stride[0], conv.padding[0], 32,
+                                        ops._p(self._wg_part), st), "xpa_conv1_u8_wgrad")
+        _lib.check(L.xpa_colsum_finalize(ops._p(self._wg_part), self._wg_part.shape[0], 8192,
+                                         ops._p(conv.weight.grad), st), "xpa_colsum_finalize")
+
     @staticmethod
     def _dgrad_ok(conv):
         """K27 takes the data gradient of 2s x 2s, stride-s (1, 2) convs with 32 -> 64 channels."""
@@ -323,6 +336,9 @@ class _Trunk:
                     g = g.contiguous()
                 _act_bwd_bias(parts, code, g.view(-1, Cy), y.view(-1, Cy), slope, conv.bias.grad)
             need_in = i > 0
+            if i == 0 and hs[0].dtype == torch.uint8 and conv.weight.grad.is_contiguous():
+                self._conv1_wgrad(conv, g, hs[0])   # K26: from the uint8 frames, no f32 frame copy
+                break
             x_in = self.frames(hs[i]) if hs[i].dtype == torch.uint8 else hs[i]
             k27 = need_in and self._dgrad_ok(conv)
             gx, gw, _ = torch.ops.aten.convolution_backward(
