@@ -520,18 +520,25 @@ def c3_cpu_baseline(n_envs=1024, n_steps=128, n_epoch=4, n_minibatch=8, steps_ti
 
 
 def c3_kernels(device, batch=16384):
-    """K20 / K22 at the C3 update's shapes (minibatch of `batch` frames; conv1's [B*21*21, 32] output), HIP events
-    around single launches on the launch stream, median of 7 (the buffers exceed every cache)."""
+    """The C3 update's hand-written kernels at its shapes (minibatch of `batch` frames): K25 conv1 forward from uint8,
+    K26 conv1 weight gradient from uint8, K27 conv2 data gradient (fp32 MFMA: FLOP / time vs the fp32 matrix peak) and
+    K22 (ReLU backward + bias sums over conv1's [B*21*21, 32]; HBM).  HIP events around single launches on the launch
+    stream, median of 7 (the buffers exceed every cache)."""
     import torch
     from xuanpolicy_amd import _lib, ops
     L = ops.lib()
     st = ops._stream(device)
     x = torch.randint(0, 256, (batch, 84, 84, 4), dtype=torch.uint8, device=device)
-    y = torch.empty(x.shape, dtype=torch.float32, device=device)
     rows, C = batch * 21 * 21, 32
+    w1, b1 = torch.randn(32, 4, 8, 8, device=device) * 0.05, torch.zeros(32, device=device)
+    y1 = torch.empty((batch, 21, 21, 32), device=device)
     g = torch.randn(rows, C, device=device)
     h = torch.relu(torch.randn(rows, C, device=device))
     part = torch.empty(int(L.xpa_act_bwd_bias_num_partials(rows, C)), C, device=device)
+    wpart = torch.empty(int(L.xpa_conv1_u8_wgrad_num_partials()), 8192, device=device)
+    dy2 = torch.randn(batch, 10, 10, 64, device=device)
+    w2 = torch.randn(64, 32, 4, 4, device=device) * 0.05
+    dx2 = torch.empty((batch, 21, 21, 32), device=device)
 
     def timed(fn, reps=7):
         ts = []
@@ -544,14 +551,28 @@ def c3_kernels(device, batch=16384):
             ts.append(e0.elapsed_time(e1) * 1e3)
         ts.sort()
         return ts[len(ts) // 2]
-    f_us = timed(lambda: _lib.check(L.xpa_frames_to_f32(ops._p(x), x.numel(), ops._p(y), st), "frames"))
+    f_us = timed(lambda: _lib.check(L.xpa_conv1_u8_fwd(1, ops._p(x), batch, 84, 84, 4, 8, 4, 2, ops._p(w1), ops._p(b1),
+                                                       32, 0.0, ops._p(y1), st), "conv1_u8_fwd"))
+    w_us = timed(lambda: _lib.check(L.xpa_conv1_u8_wgrad(ops._p(g), ops._p(x), batch, 84, 84, 4, 8, 4, 2, 32,
+                                                         ops._p(wpart), st), "conv1_u8_wgrad"))
+    d_us = timed(lambda: _lib.check(L.xpa_conv_dgrad_s2k(ops._p(dy2), batch, 10, 10, 64, ops._p(w2), 32, 4, 2, 1, 21,
+                                                         21, ops._p(dx2), st), "conv_dgrad_s2k"))
     b_us = timed(lambda: _lib.check(L.xpa_act_bwd_bias(1, ops._p(g), ops._p(h), rows, C, 0.0, ops._p(g), ops._p(part),
                                                        st), "act_bwd_bias"))
-    fb, bb = 5.0 * x.numel(), 12.0 * rows * C
-    return {"frames_to_f32": {"kernel": "xpa_frames_to_f32 (K20)", "bound": "hbm", "avg_launch_us": round(f_us, 2),
-                              "algorithmic_bytes_per_launch": int(fb), "achieved": round(fb / f_us / 1e3, 1),
-                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(fb / f_us / 1e3 / HBM_PEAK_GBS, 4),
-                              "shape": "%d frames 84x84x4 uint8 -> f32 (1 B read + 4 B written per pixel)" % batch},
+    c1_flops = 2.0 * rows * 256 * 32            # [rows, 8*8*4] x [256, 32]
+    c2_flops = 2.0 * batch * 21 * 21 * 32 * 256  # every input pixel: 4 taps x 64 channels
+    bb = 12.0 * rows * C
+
+    def mfma(name, us, flops, shape):
+        return {"kernel": name, "bound": "mfma", "avg_launch_us": round(us, 2), "flops_per_launch": flops,
+                "achieved": round(flops / us / 1e6, 1), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(flops / us / 1e6 / FP32_MFMA_PEAK_TFLOPS, 4), "shape": shape}
+    return {"conv1_u8_fwd": mfma("xpa_conv1_u8_fwd (K25)", f_us, c1_flops,
+                                 "%d frames 84x84x4 uint8 -> [B, 21, 21, 32] (8x8 s4 p2, bias + ReLU)" % batch),
+            "conv1_u8_wgrad": mfma("xpa_conv1_u8_wgrad (K26, partials; + f64 finalize)", w_us, c1_flops,
+                                   "dW [32, 4, 8, 8] over %d x 441 rows" % batch),
+            "conv_dgrad_s2k": mfma("xpa_conv_dgrad_s2k (K27)", d_us, c2_flops,
+                                   "dX [B, 21, 21, 32] from dY [B, 10, 10, 64], 4x4 s2 p1"),
             "act_bwd_bias": {"kernel": "xpa_act_bwd_bias (K22, ReLU)", "bound": "hbm", "avg_launch_us": round(b_us, 2),
                              "algorithmic_bytes_per_launch": int(bb), "achieved": round(bb / b_us / 1e3, 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(bb / b_us / 1e3 / HBM_PEAK_GBS, 4),
