@@ -479,6 +479,20 @@ int xpa_rollout_bootstrap_fixup(int64_t n_envs, int64_t horizon, const float *va
 int64_t xpa_thin_bwd_num_partials(int64_t rows);
 int xpa_thin_linear_act_fwd(int act, const float *x, int64_t ldx, int64_t rows, int64_t d_in, int64_t d_out,
                             const float *w, const float *b, float slope, float *h, int64_t ldh, xpa_stream_t stream);
+/* K13 with K4's minibatch gather folded in (the update's fast path, ppoclip_agent.py:76-85 / memory_tools.py:231-242):
+ * the rows are x[idx[r]] of the full flattened rollout buffer x [n_rows, d_in] (an index outside [0, n_rows) gives a
+ * zero row), so the gathered minibatch never materialises; with adv_partials (f64 [xpa_gather_num_partials(rows), 2])
+ * the forward also writes xpa_gather_minibatch's per-minibatch advantage moments of adv[idx] bit for bit, and with
+ * x_out ([rows, d_in] contiguous) the gathered rows themselves (what the backward then reads contiguously).  The
+ * _bwd_gather form reads the rows through idx instead.  Otherwise as xpa_thin_linear_act_fwd / _bwd. */
+int xpa_thin_linear_act_fwd_gather(int act, const float *x, int64_t ldx, int64_t n_rows, const int64_t *idx,
+                                   int64_t rows, int64_t d_in, int64_t d_out, const float *w, const float *b,
+                                   float slope, float *h, int64_t ldh, const float *adv, double *adv_partials,
+                                   float *x_out, xpa_stream_t stream);
+int xpa_thin_linear_act_bwd_gather(int act, const float *g, int64_t ldg, const float *h, int64_t ldh, int64_t rows,
+                                   const float *x, int64_t ldx, int64_t n_rows, const int64_t *idx, int64_t d_in,
+                                   int64_t d_out, float slope, float *partial_dw, float *partial_db,
+                                   xpa_stream_t stream);
 /* The rollout's forward with the observation normalisation fused in: x holds RAW observations;
  * xn = clip((x - mean) / (sqrt(var) + 1e-8), +-clip) (xpa_obs_normalize's arithmetic) is written to xn
  * [rows, ldn] and, when col != NULL, into the rollout buffer column cursor->ptr of col (row stride col_ld

@@ -535,3 +535,42 @@ def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code):
     assert abs(got[2] - entropy.item()) < 1e-5 and abs(got[3] - total.item()) < 1e-5
     if ls is not None:
         close(dls, ls.grad, "d logstd", rel=1e-5)
+
+
+@pytest.mark.parametrize("rows,n_rows,din", [(65536, 524288, 17), (1000, 5000, 4), (77, 300, 17)])
+def test_thin_gather_forms_equal_k4_then_k13(rows, n_rows, din):
+    """K13 with K4's gather folded in (xpa_thin_linear_act_fwd_gather / _bwd_gather) == xpa_gather_minibatch then
+    the plain K13 forms, bit for bit: h, the gathered rows (x_out), the adv-moment partials, and the dW / db
+    partials; out-of-range indices give zero rows and add nothing."""
+    import torch
+    from xuanpolicy_amd import _lib, ops
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(rows)
+    flat = torch.randn(n_rows, din, generator=g).to(dev)
+    adv = torch.randn(n_rows, generator=g).to(dev)
+    idx = torch.randint(0, n_rows, (rows,), generator=g)
+    idx[::97] = -3            # masked rows
+    idx[5::131] = n_rows + 7
+    idx = idx.to(dev)
+    lin = torch.nn.Linear(din, 256).to(dev)
+    L, st = ops.lib(), ops._stream(dev)
+    xg, part = ops.gather_minibatch(idx, flat, adv=adv)
+    h_ref = torch.empty(rows, 256, device=dev)
+    _lib.check(L.xpa_thin_linear_act_fwd(1, ops._p(xg), din, rows, din, 256, ops._p(lin.weight), ops._p(lin.bias),
+                                         0.01, ops._p(h_ref), 256, st), "fwd")
+    h = torch.empty(rows, 256, device=dev)
+    part2 = torch.empty_like(part)
+    xo = torch.empty(rows, din, device=dev)
+    _lib.check(L.xpa_thin_linear_act_fwd_gather(1, ops._p(flat), din, n_rows, ops._p(idx), rows, din, 256,
+                                                ops._p(lin.weight), ops._p(lin.bias), 0.01, ops._p(h), 256, ops._p(adv),
+                                                ops._p(part2), ops._p(xo), st), "fwd_gather")
+    assert torch.equal(h, h_ref) and torch.equal(part2, part) and torch.equal(xo, xg)
+    gr = torch.randn(rows, 256, generator=g).to(dev)
+    G = int(L.xpa_thin_bwd_num_partials(rows))
+    pw, pb = torch.empty(G, 256 * din, device=dev), torch.empty(G, 256, device=dev)
+    pw2, pb2 = torch.empty_like(pw), torch.empty_like(pb)
+    _lib.check(L.xpa_thin_linear_act_bwd(1, ops._p(gr), 256, ops._p(h), 256, rows, ops._p(xg), din, din, 256, 0.01,
+                                         ops._p(pw), ops._p(pb), st), "bwd")
+    _lib.check(L.xpa_thin_linear_act_bwd_gather(1, ops._p(gr), 256, ops._p(h), 256, rows, ops._p(flat), din, n_rows,
+                                                ops._p(idx), din, 256, 0.01, ops._p(pw2), ops._p(pb2), st), "bwd_gather")
+    assert torch.equal(pw, pw2) and torch.equal(pb, pb2)

@@ -123,6 +123,10 @@ SIGNATURES = {
                                                  c_f32, ctypes.c_int, c_p, c_p, c_p]),
     "xpa_rollout_bootstrap_fixup": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_p]),
     "xpa_thin_bwd_num_partials": (c_i64, [c_i64]),
+    "xpa_thin_linear_act_fwd_gather": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_p,
+                                                       c_f32, c_p, c_i64, c_p, c_p, c_p, c_p]),
+    "xpa_thin_linear_act_bwd_gather": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_p,
+                                                       c_i64, c_i64, c_f32, c_p, c_p, c_p]),
     "xpa_thin_linear_act_fwd_norm": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f32,
                                                     c_p, c_i64, c_p, c_p, c_f32, c_p, c_i64, c_p, c_i64, c_p, c_p]),
     "xpa_thin_linear_act_fwd": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f32, c_p, c_i64,

@@ -35,6 +35,7 @@ import torch
 
 from . import ops
 from .buffer import DummyOnPolicyBuffer, DummyOnPolicyBuffer_Atari
+from .fused_mlp import Rows
 from .learners import A2C_Learner, PerDQN_Learner, PPOCLIP_Learner
 from .policies import policy_heads, space_shape
 
@@ -110,6 +111,7 @@ class _OnPolicyAgent:
         self.device_env = hasattr(envs, "step_device")
         self.fuse_env_step = True   # device SynthBox env stepped inside K14 when possible (_env_fused)
         self.fuse_value_gae = True  # deferred bootstraps' value head inside the GAE scan (xpa_gae_scan_value)
+        self.fuse_gather = True     # minibatch gather + adv moments inside the update's K13 (fused_mlp.Rows)
         self.current_step = 0
         self.current_episode = np.zeros((N,), np.int32)
         self.iterations = 0
@@ -490,11 +492,24 @@ class _OnPolicyAgent:
         logp_flat = mem.auxiliary_infos["old_logp"].reshape(-1) if self.algo == "ppo" else None
         use_advnorm = mem.use_advnorm
         scalars = None
+        fm = self._rollout_mlp() if not self.global_advnorm else None
+        rows_path = fm is not None and self.fuse_gather and fm.rows_ok(obs_flat)
         for _ in range(self.n_epoch):
             perm = self.epoch_permutation(NT)
             for start in range(0, NT, B):
                 idx = perm[start:start + B]
                 b = idx.shape[0]
+                if rows_path:
+                    # K4 folded into K13: the update reads the minibatch rows (and forms the adv moments) through idx
+                    if self.adv_part is None or self.adv_part.shape[0] != ops.gather_num_partials(b):
+                        self.adv_part = torch.empty((ops.gather_num_partials(b), 2), dtype=torch.float64,
+                                                    device=self.device)
+                    part = self.adv_part if use_advnorm else None
+                    scalars = self.learner.update_fused(Rows(obs_flat, idx), idx, act_flat, adv_flat, ret_flat,
+                                                        logp_flat, part)
+                    if self.update_log is not None:
+                        self.update_log.append(scalars.clone())
+                    continue
                 if self.obs_mb is None or self.obs_mb.shape[0] != b:
                     self.obs_mb = torch.empty((b,) + tuple(obs_flat.shape[1:]), dtype=obs_flat.dtype,
                                               device=self.device)

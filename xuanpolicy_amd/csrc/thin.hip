@@ -37,12 +37,22 @@ __device__ __forceinline__ float act_g(float h, float slope) {
     return 1.f;
 }
 
-template <int ACT, int DMAX, int TILE>
+// IDX: the rows are x[idx[r]] of the full rollout buffer (n_rows rows; an index outside [0, n_rows) gives a zero row
+// and adds nothing to the moments), i.e. K4's minibatch gather folded into the staging of the x tile, and with
+// adv_partials the K4 advantage moments of each 64-row tile (f64 (sum, sum of squares), thread t <-> row t and
+// xpa_block_sum: K4's partials bit for bit).  Only the 64-row tile form takes IDX.
+template <int ACT, int DMAX, int TILE, bool IDX = false>
 __global__ __launch_bounds__(256) void thin_fwd_kernel(const float *__restrict__ x, int64_t ldx, int64_t rows, int din,
                                                        const float *__restrict__ W, const float *__restrict__ bias,
-                                                       float slope, float *__restrict__ h, int64_t ldh) {
+                                                       float slope, float *__restrict__ h, int64_t ldh,
+                                                       const int64_t *__restrict__ idx = nullptr, int64_t n_rows = 0,
+                                                       const float *__restrict__ adv = nullptr,
+                                                       double *__restrict__ adv_partials = nullptr,
+                                                       float *__restrict__ x_out = nullptr) {
     constexpr int kPad = DMAX + 4;  // row stride of the staged x tile (16-B aligned rows)
     __shared__ __attribute__((aligned(16))) float s_x[TILE * kPad];
+    __shared__ int64_t s_src[IDX ? TILE : 1];
+    __shared__ double s_red[4];
     const int t = threadIdx.x;
     float w[DMAX];
 #pragma unroll
@@ -52,10 +62,39 @@ __global__ __launch_bounds__(256) void thin_fwd_kernel(const float *__restrict__
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t r0 = tile * TILE;
         __syncthreads();
+        if (IDX) {
+            if (t < TILE) {
+                const int64_t sr = r0 + t < rows ? idx[r0 + t] : -1;
+                s_src[t] = (sr >= 0 && sr < n_rows) ? sr : -1;
+            }
+            __syncthreads();
+        }
         // zero-padded columns din..DMAX-1 stay 0 from this loop's (r, k < DMAX) writes
         for (int i = t; i < TILE * DMAX; i += 256) {
             const int r = i / DMAX, k = i - r * DMAX;
-            s_x[r * kPad + k] = (k < din && r0 + r < rows) ? x[(r0 + r) * ldx + k] : 0.f;
+            if (IDX) {
+                const int64_t sr = s_src[r];
+                const float v = (k < din && sr >= 0) ? x[sr * ldx + k] : 0.f;
+                s_x[r * kPad + k] = v;
+                if (x_out && k < din && r0 + r < rows) x_out[(r0 + r) * din + k] = v;  // the gathered rows, for the backward
+            } else {
+                s_x[r * kPad + k] = (k < din && r0 + r < rows) ? x[(r0 + r) * ldx + k] : 0.f;
+            }
+        }
+        if (IDX && adv_partials) {  // K4's moments of this tile (thread t <-> row t)
+            double sm = 0.0, q = 0.0;
+            const int64_t sr = t < TILE ? s_src[t] : -1;
+            if (sr >= 0) {
+                const double a = (double)adv[sr];
+                sm = a;
+                q = a * a;
+            }
+            sm = xpa_block_sum(sm, s_red, 4);
+            q = xpa_block_sum(q, s_red, 4);
+            if (t == 0) {
+                adv_partials[2 * tile] = sm;
+                adv_partials[2 * tile + 1] = q;
+            }
         }
         __syncthreads();
         const int nr = (int)min((int64_t)TILE, rows - r0);
@@ -137,11 +176,12 @@ __global__ __launch_bounds__(256) void thin_fwd_norm_kernel(const float *__restr
 constexpr int kBwdGroups = 4;
 constexpr int kBwdU = 8;
 
-template <int ACT, int DMAX>
+template <int ACT, int DMAX, bool IDX = false>
 __global__ __launch_bounds__(1024) void thin_bwd_kernel(const float *__restrict__ g, int64_t ldg,
                                                         const float *__restrict__ h, int64_t ldh, int64_t rows,
                                                         const float *__restrict__ x, int64_t ldx, int din, float slope,
-                                                        float *__restrict__ partial_dw, float *__restrict__ partial_db) {
+                                                        float *__restrict__ partial_dw, float *__restrict__ partial_db,
+                                                        const int64_t *__restrict__ idx = nullptr, int64_t n_rows = 0) {
     constexpr int kPad = DMAX + 4;
     constexpr int kXs = kTile * kPad;                                        // one group's x tile
     constexpr int kLds = kBwdGroups * kXs > kCols * (DMAX + 1) ? kBwdGroups * kXs : kCols * (DMAX + 1);
@@ -160,7 +200,12 @@ __global__ __launch_bounds__(1024) void thin_bwd_kernel(const float *__restrict_
         if (tile < ntiles) {
             for (int i = t; i < kTile * DMAX; i += 256) {
                 const int r = i / DMAX, k = i - r * DMAX;
-                s_x[r * kPad + k] = (k < din && r0 + r < rows) ? x[(r0 + r) * ldx + k] : 0.f;
+                if (IDX) {  // the minibatch row r of the full buffer (K4's gather folded in; out of range: zero row)
+                    const int64_t sr = r0 + r < rows ? idx[r0 + r] : -1;
+                    s_x[r * kPad + k] = (k < din && sr >= 0 && sr < n_rows) ? x[sr * ldx + k] : 0.f;
+                } else {
+                    s_x[r * kPad + k] = (k < din && r0 + r < rows) ? x[(r0 + r) * ldx + k] : 0.f;
+                }
             }
         }
         __syncthreads();
@@ -323,5 +368,58 @@ XPA_API int xpa_thin_linear_act_fwd_norm(int act, const float *x, int64_t ldx, i
     else { XPA_FWDN_D(2) }
 #undef XPA_FWDN_D
 #undef XPA_FWDN
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_thin_linear_act_fwd_gather(int act, const float *x, int64_t ldx, int64_t n_rows, const int64_t *idx,
+                                           int64_t rows, int64_t d_in, int64_t d_out, const float *w, const float *b,
+                                           float slope, float *h, int64_t ldh, const float *adv, double *adv_partials,
+                                           float *x_out, xpa_stream_t stream) {
+    if (rows <= 0 || n_rows <= 0 || d_in < 1 || d_in > kMaxIn || d_out != kCols || act < 0 || act > 2 || !x || !idx ||
+        !w || !b || !h || ldx < d_in || ldh < d_out || (adv_partials && !adv))
+        return (int)hipErrorInvalidValue;
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t tiles = (rows + kTile - 1) / kTile;
+    const dim3 grid((unsigned)(tiles < kFwdGrid ? tiles : kFwdGrid));
+    const int dm = dmax_for((int)d_in);
+#define XPA_FWDG(A_, D_)                                                                                             \
+    hipLaunchKernelGGL((thin_fwd_kernel<A_, D_, kTile, true>), grid, dim3(256), 0, s, x, ldx, rows, (int)d_in, w, b,   \
+                       slope, h, ldh, idx, n_rows, adv, adv_partials, x_out)
+#define XPA_FWDG_D(A_)                 \
+    if (dm == 8) XPA_FWDG(A_, 8);      \
+    else if (dm == 20) XPA_FWDG(A_, 20); \
+    else if (dm == 32) XPA_FWDG(A_, 32); \
+    else XPA_FWDG(A_, 64);
+    if (act == 0) { XPA_FWDG_D(0) }
+    else if (act == 1) { XPA_FWDG_D(1) }
+    else { XPA_FWDG_D(2) }
+#undef XPA_FWDG_D
+#undef XPA_FWDG
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_thin_linear_act_bwd_gather(int act, const float *g, int64_t ldg, const float *h, int64_t ldh,
+                                           int64_t rows, const float *x, int64_t ldx, int64_t n_rows,
+                                           const int64_t *idx, int64_t d_in, int64_t d_out, float slope,
+                                           float *partial_dw, float *partial_db, xpa_stream_t stream) {
+    if (rows <= 0 || n_rows <= 0 || d_in < 1 || d_in > kMaxIn || d_out != kCols || act < 0 || act > 2 || !g || !h ||
+        !x || !idx || !partial_dw || !partial_db || ldg < d_out || ldh < d_out || ldx < d_in)
+        return (int)hipErrorInvalidValue;
+    const dim3 grid((unsigned)xpa_thin_bwd_num_partials(rows));
+    hipStream_t s = (hipStream_t)stream;
+    const int dm = dmax_for((int)d_in);
+#define XPA_BWDG(A_, D_)                                                                                            \
+    hipLaunchKernelGGL((thin_bwd_kernel<A_, D_, true>), grid, dim3(1024), 0, s, g, ldg, h, ldh, rows, x, ldx,         \
+                       (int)d_in, slope, partial_dw, partial_db, idx, n_rows)
+#define XPA_BWDG_D(A_)                 \
+    if (dm == 8) XPA_BWDG(A_, 8);      \
+    else if (dm == 20) XPA_BWDG(A_, 20); \
+    else if (dm == 32) XPA_BWDG(A_, 32); \
+    else XPA_BWDG(A_, 64);
+    if (act == 0) { XPA_BWDG_D(0) }
+    else if (act == 1) { XPA_BWDG_D(1) }
+    else { XPA_BWDG_D(2) }
+#undef XPA_BWDG_D
+#undef XPA_BWDG
     return xpa_launch_status();
 }

@@ -75,6 +75,18 @@ def head_placement(policy):
     return [[actor[0].weight, critic[0].weight], [actor[0].bias, critic[0].bias]]
 
 
+class Rows:
+    """The minibatch rows `idx` of a flat [n_rows, d] buffer, handed to the fused path instead of a gathered copy:
+    K13's gather forms (xpa_thin_linear_act_fwd_gather / _bwd_gather) read them through the permutation."""
+
+    def __init__(self, flat, idx):
+        self.flat, self.idx = flat, idx
+        self.gathered = None   # set by the gather forward: the rows as a contiguous [B, d] copy
+        self.shape = (idx.shape[0], flat.shape[1])
+        self.device = flat.device
+        self.dtype = flat.dtype
+
+
 class FusedActorCritic:
     """Built from a Gaussian/Categorical actor-critic policy whose parameters live in a FlatState
     (pass it as `flat` to use the paired actor|critic hidden layer when head_placement applied)."""
@@ -144,7 +156,27 @@ class FusedActorCritic:
             outs.append(h)
         return outs
 
-    def _rep_forward(self, x, norm=None):
+    def rows_ok(self, flat):
+        """True when the update can take Rows(flat, idx) (K13 with the gather folded in)."""
+        return (self.fused_heads and self.thin0 and flat.dim() == 2 and flat.dtype == torch.float32
+                and flat.stride(1) == 1 and flat.is_cuda)
+
+    def _rep_forward(self, x, norm=None, adv=None, adv_partials=None):
+        if isinstance(x, Rows):
+            # K4's gather folded into K13's x staging (+ the advantage moments when adv_partials is given)
+            lin, code, slope = self.rep[0]
+            B = x.idx.shape[0]
+            h = torch.empty((B, lin.out_features), dtype=torch.float32, device=x.device)
+            # the gathered rows are written beside h (4 B x d_in per row) so the backward reads them contiguously
+            # (reading them through idx again cost K13's backward 3.3 us per update)
+            x.gathered = torch.empty((B, lin.in_features), dtype=torch.float32, device=x.device)
+            _lib.check(ops.lib().xpa_thin_linear_act_fwd_gather(
+                code, ops._p(x.flat), x.flat.stride(0), x.flat.shape[0], ops._p(x.idx), B, lin.in_features,
+                lin.out_features, ops._p(lin.weight), ops._p(lin.bias), slope, ops._p(h), h.stride(0),
+                ops._p(adv) if adv_partials is not None else None,
+                ops._p(adv_partials) if adv_partials is not None else None, ops._p(x.gathered),
+                ops._stream(x.device)), "xpa_thin_linear_act_fwd_gather")
+            return [h] + self._chain_forward(self.rep[1:], h)
         if norm is not None:
             # x RAW: observation normalisation fused into the first layer (xpa_thin_linear_act_fwd_norm);
             # norm = (mean, var, clip, xn_out, col, col_ld, cursor)
@@ -182,9 +214,17 @@ class FusedActorCritic:
             self._partials[key] = ws
         pdw, pdb = ws
         s = ops._stream(g.device)
-        _lib.check(L.xpa_thin_linear_act_bwd(code, ops._p(g), g.stride(0), ops._p(h), h.stride(0), rows, ops._p(x),
-                                             x.stride(0), din, lin.out_features, slope, ops._p(pdw), ops._p(pdb), s),
-                   "xpa_thin_linear_act_bwd")
+        if isinstance(x, Rows) and getattr(x, "gathered", None) is not None:
+            x = x.gathered
+        if isinstance(x, Rows):
+            _lib.check(L.xpa_thin_linear_act_bwd_gather(code, ops._p(g), g.stride(0), ops._p(h), h.stride(0), rows,
+                                                        ops._p(x.flat), x.flat.stride(0), x.flat.shape[0],
+                                                        ops._p(x.idx), din, lin.out_features, slope, ops._p(pdw),
+                                                        ops._p(pdb), s), "xpa_thin_linear_act_bwd_gather")
+        else:
+            _lib.check(L.xpa_thin_linear_act_bwd(code, ops._p(g), g.stride(0), ops._p(h), h.stride(0), rows,
+                                                 ops._p(x), x.stride(0), din, lin.out_features, slope, ops._p(pdw),
+                                                 ops._p(pdb), s), "xpa_thin_linear_act_bwd")
         self._cq.add(pdw, lin.weight.grad)
         self._cq.add(pdb, lin.bias.grad)
 
@@ -245,9 +285,10 @@ class FusedActorCritic:
         return ops.value_head(z, (code, slope), lin_co.weight, lin_co.bias, out=out)
 
     @torch.no_grad()
-    def forward_hidden(self, x):
-        """Forward up to the heads' last hidden pre-activations (K12 does the rest)."""
-        rep_outs = self._rep_forward(x)
+    def forward_hidden(self, x, adv=None, adv_partials=None):
+        """Forward up to the heads' last hidden pre-activations (K12 does the rest).  x may be Rows(flat, idx); then
+        adv_partials (if given) receives the minibatch's advantage moments of adv[idx] (K4's partials)."""
+        rep_outs = self._rep_forward(x, adv=adv, adv_partials=adv_partials)
         s = rep_outs[-1] if rep_outs else x
         if self.pair is not None and self.gemm_heads:   # K16 forms z inside the head kernels
             return (x, rep_outs, s, (([], s, None), ([], s, None)))
@@ -432,7 +473,7 @@ class FusedActorCritic:
             lin, code, slope = layers[j]
             h = outs[j]
             x = inputs[j]
-            if j == 0 and thin_first and not need_dx and g.stride(1) == 1 and x.stride(1) == 1:
+            if j == 0 and thin_first and not need_dx and g.stride(1) == 1 and (isinstance(x, Rows) or x.stride(1) == 1):
                 self._thin_backward(layers[0], g, h, x)   # K13: act backward + dW + db, no dz pass
                 break
             self._bias_grad(code, g, h, slope, lin.bias.grad)   # g <- g * act'(h) in place (code != 0)

@@ -132,7 +132,10 @@ class _FusedPolicyGradient(Learner):
         fm = self._fused_mlp()
         if fm is not None and fm.fused_heads:
             fm.early_grad_sync = getattr(self.grad_sync, "begin", None) if self.grad_sync is not None else None
-            ctx = fm.forward_hidden(obs)   # K12: heads, loss and head backward in one pass per head
+            # obs may be fused_mlp.Rows(flat buffer, idx): K13 reads the minibatch through idx and, with adv_partials,
+            # writes the minibatch's advantage moments itself (no K4 launch)
+            rows = type(obs).__name__ == "Rows"
+            ctx = fm.forward_hidden(obs, adv=adv if rows else None, adv_partials=adv_partials if rows else None)
             scalars = fm.loss_backward(ctx, self.algo, self.dist, act, adv, ret, old_logp=old_logp, idx=idx,
                                        adv_partials=adv_partials, clip_range=self.clip_range, vf_coef=self.vf_coef,
                                        ent_coef=self.ent_coef)
