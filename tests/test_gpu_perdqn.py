@@ -88,8 +88,11 @@ def test_perdqn_learner_replays_reference(golden):
 
 def test_perdqn_agent_loop_on_device():
     from xuanpolicy_amd.runner import build_perdqn
+    # the production channel counts of the first two convs (perdqn/atari.yaml: 32, 64), so the loop runs K25 / K26 /
+    # K27; with 8 / 8 channels (MIOpen's NHWC kernels for every conv) this test hit two intermittent illegal-address
+    # faults in r02, never reproduced under AMD_SERIALIZE_KERNEL=3
     agent = build_perdqn(n_envs=4, n_size=256, batch_size=64, device=DEV, start_training=64, sync_frequency=20,
-                         filters=[8, 8], kernels=[8, 4], strides=[4, 2], q_hidden_size=[32], max_episode_steps=40)
+                         filters=[32, 64], kernels=[8, 4], strides=[4, 2], q_hidden_size=[32], max_episode_steps=40)
     assert agent.device_env and agent.memory.observations.dtype == torch.uint8
     assert agent.envs.action_space.n == 18
     agent.train(80, sync_info=True)

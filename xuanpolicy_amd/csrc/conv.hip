@@ -278,10 +278,9 @@ __global__ __launch_bounds__(256, 4) void conv1_u8_fwd_kernel(const unsigned *__
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const float bc = bias[i];
     const int64_t ohw = (int64_t)OH * OW;
-    for (int64_t blk = blockIdx.x; blk * kC1Rows < rows; blk += gridDim.x) {
+    // The geometry of a row block for this lane's two rows (clamped past the end: loads stay in bounds).
+    auto geometry = [&](int64_t blk, int (&by)[2], int (&bx)[2], const unsigned *(&xr)[2]) {
         const int64_t r0 = blk * kC1Rows + wave * 64;
-        int by[2], bx[2];
-        const unsigned *xr[2];
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
             const int64_t m = r0 + rt * 32 + i;
@@ -293,16 +292,24 @@ __global__ __launch_bounds__(256, 4) void conv1_u8_fwd_kernel(const unsigned *__
             bx[rt] = ox * S - P;
             xr[rt] = x + b * H * W;
         }
+    };
+    int64_t blk = blockIdx.x;
+    if (blk * kC1Rows >= rows) return;
+    int by[2], bx[2];
+    const unsigned *xr[2];
+    geometry(blk, by, bx, xr);
+    unsigned va[2][8], vb[2][8];
+    // sched_barrier: keep the ring order (hipcc otherwise hoists all 64 loads and their 64-bit addresses: 248
+    // VGPRs, 2 waves per SIMD).  The ring runs on across row blocks: the next block's chunks 0 and 1 are requested
+    // during this block's chunks 2 and 3, so no block starts with an exposed load round trip.
+    conv1_load_chunk<ACT>(va, xr, by, bx, H, W, 0, h);
+    conv1_load_chunk<ACT>(vb, xr, by, bx, H, W, 1, h);
+    for (;;) {
         f32x16 acc[2];
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[rt][r] = 0.f;
-        unsigned va[2][8], vb[2][8];
-        // sched_barrier: keep the ring order (hipcc otherwise hoists all 64 loads and their 64-bit addresses: 248
-        // VGPRs, 2 waves per SIMD)
-        conv1_load_chunk<ACT>(va, xr, by, bx, H, W, 0, h);
-        conv1_load_chunk<ACT>(vb, xr, by, bx, H, W, 1, h);
         __builtin_amdgcn_sched_barrier(0);
         conv1_mfma_chunk(acc, va, sB, 0, h, i);
         __builtin_amdgcn_sched_barrier(0);
@@ -314,7 +321,17 @@ __global__ __launch_bounds__(256, 4) void conv1_u8_fwd_kernel(const unsigned *__
         __builtin_amdgcn_sched_barrier(0);
         conv1_mfma_chunk(acc, va, sB, 2, h, i);
         __builtin_amdgcn_sched_barrier(0);
+        const int64_t r0 = blk * kC1Rows + wave * 64;
+        const int64_t nblk = blk + gridDim.x;
+        const bool more = nblk * kC1Rows < rows;  // block-uniform
+        if (more) {
+            geometry(nblk, by, bx, xr);
+            conv1_load_chunk<ACT>(va, xr, by, bx, H, W, 0, h);
+        }
+        __builtin_amdgcn_sched_barrier(0);
         conv1_mfma_chunk(acc, vb, sB, 3, h, i);
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) conv1_load_chunk<ACT>(vb, xr, by, bx, H, W, 1, h);
         // C/D map: row = (r & 3) + 8 (r >> 2) + 4 h, column n = i
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
@@ -323,6 +340,8 @@ __global__ __launch_bounds__(256, 4) void conv1_u8_fwd_kernel(const unsigned *__
                 const int64_t m = r0 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (m < rows) y[m * 32 + i] = act_fwd<ACT>(acc[rt][r] + bc, slope);
             }
+        if (!more) break;
+        blk = nblk;
     }
 }
 
@@ -345,16 +364,56 @@ struct DgradGeom {
     int64_t B;
 };
 
-__device__ __forceinline__ void dgrad_load_chunk(f4v (&v)[2][4], const float *const (&yr)[2], const bool (&ok)[2][4],
+// A tile's per-lane geometry: for its two rows, the dY element offset of every tap (clamped to 0 when the tap's
+// output pixel is outside the map, flagged in ok) and the dX row (-1 past the class's rows).
+struct DgradRows {
+    int off[2][4];
+    bool ok[2][4];
+    int64_t orow[2];
+};
+
+__device__ __forceinline__ int dgrad_class(const DgradGeom &g, int64_t tile) {
+    return tile < g.tiles[0] ? 0 : tile < g.tiles[1] ? 1 : tile < g.tiles[2] ? 2 : 3;
+}
+
+__device__ __forceinline__ void dgrad_rows(const DgradGeom &g, int64_t gtile, int wave, int i, DgradRows &q) {
+    const int cls = dgrad_class(g, gtile);
+    const int64_t tile = gtile - (cls ? g.tiles[cls - 1] : 0);
+    const int ry = cls >> 1, rx = cls & 1;
+    const int ny = g.ny[ry], nx = g.nx[rx];
+    const int64_t per_img = (int64_t)ny * nx, rows = g.B * per_img;
+    const int64_t r0 = tile * kDgRows + wave * 64;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+        const int64_t m = r0 + rt * 32 + i;
+        const bool mv = m < rows;
+        const int64_t mc = mv ? m : 0;
+        const int64_t b = mc / per_img;
+        const int rem = (int)(mc - b * per_img);
+        const int ay = rem / nx, ax = rem - (rem / nx) * nx;
+        const int iy = g.iy0[ry] + g.S * ay, ix = g.ix0[rx] + g.S * ax;
+        q.orow[rt] = mv ? (b * g.H + iy) * g.W + ix : -1;
+        const int oy0 = (iy + g.P) / g.S, ox0 = (ix + g.P) / g.S;
+#pragma unroll
+        for (int tap = 0; tap < 4; ++tap) {
+            const int oy = oy0 - (tap >> 1), ox = ox0 - (tap & 1);
+            const bool v = mv && (unsigned)oy < (unsigned)g.OH && (unsigned)ox < (unsigned)g.OW;
+            q.ok[rt][tap] = v;
+            q.off[rt][tap] = v ? (int)(((b * g.OH + oy) * g.OW + ox) * 64) : 0;
+        }
+    }
+}
+
+__device__ __forceinline__ void dgrad_load_chunk(f4v (&v)[2][4], const float *__restrict__ dy, const DgradRows &q,
                                                  int tap, int half, int h) {  // every load from a clamped address
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int q = 2 * (4 * half + j) + h;  // channel quad
+        const int c4 = 2 * (4 * half + j) + h;  // channel quad
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
-            const f4v d = *reinterpret_cast<const f4v *>(yr[rt] + 4 * q);
+            const f4v d = *reinterpret_cast<const f4v *>(dy + q.off[rt][tap] + 4 * c4);
             const f4v z = {0.f, 0.f, 0.f, 0.f};
-            v[rt][j] = ok[rt][tap] ? d : z;
+            v[rt][j] = q.ok[rt][tap] ? d : z;
         }
     }
 }
@@ -373,85 +432,78 @@ __device__ __forceinline__ void dgrad_mfma_chunk(f32x16 (&acc)[2], const f4v (&v
     }
 }
 
+// Persistent blocks over contiguous ranges of the class-major tile list: a block re-stages the weight image only when
+// its range crosses into the next residue class (at most 3 times), and the register ring runs on across tiles (the
+// next tile's first chunk is requested during the current tile's last one).
+constexpr int kDgGrid = 512;  // 2 blocks per CU resident (191 VGPRs)
+
 __global__ __launch_bounds__(256, 2) void conv_dgrad_s2k_kernel(const float *__restrict__ dy, const float *__restrict__ w,
                                                                 DgradGeom g, float *__restrict__ dx) {
     __shared__ __attribute__((aligned(16))) float sB[4 * 16 * 32 * 4];  // [tap][co quad][n][4]
+    __shared__ int64_t s_orow[4][32];
     const int t = threadIdx.x;
-    const int64_t bid = blockIdx.x;
-    const int cls = bid < g.tiles[0] ? 0 : bid < g.tiles[1] ? 1 : bid < g.tiles[2] ? 2 : 3;
-    const int64_t tile = bid - (cls ? g.tiles[cls - 1] : 0);
-    const int ry = cls >> 1, rx = cls & 1;
-    const int K = 2 * g.S;
-    for (int e = t; e < 4 * 16 * 32 * 4; e += 256) {  // W [64 co][32 n][K][K]
-        const int c = e & 3, n = (e >> 2) & 31, q = (e >> 7) & 15, tap = e >> 11;
-        const int ky = ry + (tap >> 1) * g.S, kx = rx + (tap & 1) * g.S;
-        sB[e] = w[(((4 * q + c) * 32 + n) * K + ky) * K + kx];
-    }
-    __syncthreads();
     const int lane = t & 63, h = lane >> 5, i = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int ny = g.ny[ry], nx = g.nx[rx];
-    const int64_t per_img = (int64_t)ny * nx, rows = g.B * per_img;
-    const int64_t r0 = tile * kDgRows + wave * 64;
-    const float *yr[2][4];
-    bool ok[2][4];
-    int64_t orow[2];
+    const int64_t T = g.tiles[3];
+    const int64_t t0 = T * blockIdx.x / gridDim.x, t1 = T * (blockIdx.x + 1) / gridDim.x;
+    if (t0 >= t1) return;
+    const int K = 2 * g.S;
+    int staged = -1;
+    DgradRows cur, nxt;
+    dgrad_rows(g, t0, wave, i, cur);
+    f4v va[2][4], vb[2][4];
+    dgrad_load_chunk(va, dy, cur, 0, 0, h);
+    for (int64_t tile = t0; tile < t1; ++tile) {
+        const int cls = dgrad_class(g, tile);
+        if (cls != staged) {  // block-uniform
+            const int ry = cls >> 1, rx = cls & 1;
+            __syncthreads();
+            for (int e = t; e < 4 * 16 * 32 * 4; e += 256) {  // W [64 co][32 n][K][K]
+                const int c = e & 3, n = (e >> 2) & 31, q = (e >> 7) & 15, tap = e >> 11;
+                const int ky = ry + (tap >> 1) * g.S, kx = rx + (tap & 1) * g.S;
+                sB[e] = w[(((4 * q + c) * 32 + n) * K + ky) * K + kx];
+            }
+            __syncthreads();
+            staged = cls;
+        }
+        const bool more = tile + 1 < t1;
+        f32x16 acc[2];
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-        const int64_t m = r0 + rt * 32 + i;
-        const bool mv = m < rows;
-        const int64_t mc = mv ? m : 0;
-        const int64_t b = mc / per_img;
-        const int rem = (int)(mc - b * per_img);
-        const int ay = rem / nx, ax = rem - (rem / nx) * nx;
-        const int iy = g.iy0[ry] + g.S * ay, ix = g.ix0[rx] + g.S * ax;
-        orow[rt] = mv ? (b * g.H + iy) * g.W + ix : -1;
-        const int oy0 = (iy + g.P) / g.S, ox0 = (ix + g.P) / g.S;
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[rt][r] = 0.f;
+        // 8 chunks (tap, half of the 64 channels): chunk k + 1 requested before chunk k's 32 MFMAs
 #pragma unroll
         for (int tap = 0; tap < 4; ++tap) {
-            const int oy = oy0 - (tap >> 1), ox = ox0 - (tap & 1);
-            const bool v = mv && (unsigned)oy < (unsigned)g.OH && (unsigned)ox < (unsigned)g.OW;
-            ok[rt][tap] = v;
-            yr[rt][tap] = dy + ((b * g.OH + (v ? oy : 0)) * g.OW + (v ? ox : 0)) * 64;
+            dgrad_load_chunk(vb, dy, cur, tap, 1, h);
+            __builtin_amdgcn_sched_barrier(0);
+            dgrad_mfma_chunk(acc, va, sB, tap, 0, h, i);
+            __builtin_amdgcn_sched_barrier(0);
+            if (tap + 1 < 4) {
+                dgrad_load_chunk(va, dy, cur, tap + 1, 0, h);
+            } else if (more) {
+                dgrad_rows(g, tile + 1, wave, i, nxt);
+                dgrad_load_chunk(va, dy, nxt, 0, 0, h);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            dgrad_mfma_chunk(acc, vb, sB, tap, 1, h, i);
+            __builtin_amdgcn_sched_barrier(0);
         }
-    }
-    f32x16 acc[2];
+        // C/D map: row = (r & 3) + 8 (r >> 2) + 4 h of the tile, column n = i; the tile's rows are scattered pixels
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+        for (int rt = 0; rt < 2; ++rt) {
+            // every lane learns the output offsets of its 16 rows from the row owners (lane i, h = 0)
+            __builtin_amdgcn_wave_barrier();
+            if (h == 0) s_orow[wave][i] = cur.orow[rt];
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[rt][r] = 0.f;
-    f4v va[2][4], vb[2][4];
-    // 8 chunks (tap, half of the 64 channels): chunk k + 1 requested before chunk k's 32 MFMAs
-#pragma unroll
-    for (int tap = 0; tap < 4; ++tap) {
-        const float *ya[2] = {yr[0][tap], yr[1][tap]};
-        if (tap == 0) dgrad_load_chunk(va, ya, ok, tap, 0, h);
-        dgrad_load_chunk(vb, ya, ok, tap, 1, h);
-        __builtin_amdgcn_sched_barrier(0);
-        dgrad_mfma_chunk(acc, va, sB, tap, 0, h, i);
-        __builtin_amdgcn_sched_barrier(0);
-        if (tap + 1 < 4) {
-            const float *yn[2] = {yr[0][tap + 1], yr[1][tap + 1]};
-            dgrad_load_chunk(va, yn, ok, tap + 1, 0, h);
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int64_t o = s_orow[wave][row];
+                if (o >= 0) dx[o * 32 + i] = acc[rt][r];
+            }
         }
-        __builtin_amdgcn_sched_barrier(0);
-        dgrad_mfma_chunk(acc, vb, sB, tap, 1, h, i);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    // C/D map: row = (r & 3) + 8 (r >> 2) + 4 h of the tile, column n = i; the tile's rows are scattered pixels
-    __shared__ int64_t s_orow[4][32];
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-        // every lane learns the output offsets of its 16 rows from the row owners (lane i, h = 0)
-        __builtin_amdgcn_wave_barrier();
-        if (h == 0) s_orow[wave][i] = orow[rt];
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int64_t o = s_orow[wave][row];
-            if (o >= 0) dx[o * 32 + i] = acc[rt][r];
-        }
+        if (more) cur = nxt;
     }
 }
 
@@ -712,8 +764,9 @@ XPA_API int xpa_conv_dgrad_s2k(const float *dy, int64_t batch, int64_t out_h, in
         acc += (rows + kDgRows - 1) / kDgRows;
         g.tiles[c] = acc;
     }
-    if (acc <= 0 || acc > 0x7fffffff) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(conv_dgrad_s2k_kernel, dim3((unsigned)acc), dim3(256), 0, (hipStream_t)stream, dy, w, g, dx);
+    if (acc <= 0 || batch * out_h * out_w * 64 >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;  // int offsets
+    const unsigned grid = (unsigned)(acc < kDgGrid ? acc : kDgGrid);
+    hipLaunchKernelGGL(conv_dgrad_s2k_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, dy, w, g, dx);
     return xpa_launch_status();
 }
 
