@@ -4,6 +4,8 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_final.log 2>&1 || { tail -5 $O/pytest_final.log; exit 1; }
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")" > $O/smoke_final.log 2>&1 || { tail -5 $O/smoke_final.log; exit 7; }
+tail -1 $O/smoke_final.log
 tail -1 $O/pytest_final.log
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o f -- python tools/gae_pmc.py > $O/pmc_fetch.log 2>&1 || exit 2
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o w -- python tools/gae_pmc.py > $O/pmc_write.log 2>&1 || exit 3
