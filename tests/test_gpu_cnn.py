@@ -288,19 +288,20 @@ def test_conv_dgrad_s2k_matches_conv2d_input(B, H, k, s, p):
     torch.testing.assert_close(dx.double(), ref.permute(0, 2, 3, 1), rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("B", [1, 6, 33])
-def test_conv1_u8_wgrad_matches_conv2d_weight(B):
+@pytest.mark.parametrize("B,H,s,p", [(1, 84, 4, 2), (6, 84, 4, 2), (33, 84, 4, 2), (5, 85, 3, 1)])
+def test_conv1_u8_wgrad_matches_conv2d_weight(B, H, s, p):
     """K26 partials + the f64 column-sum finalize == torch.nn.grad.conv2d_weight on (x / 255) in float64 (odd row
     counts: the last row pair half empty)."""
     _l, ops = _lib()
     L, st = ops.lib(), ops._stream(DEV)
     g = torch.Generator(device="cpu").manual_seed(7 * B)
-    x = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.int32).to(torch.uint8).to(DEV)
-    dz = torch.randn(B, 21, 21, 32, generator=g).to(DEV)
+    OH = (H + 2 * p - 8) // s + 1   # 84 / 4 / 2: the 8-B pixel-pair form; 85 / 3 / 1: the dword form
+    x = torch.randint(0, 256, (B, H, H, 4), generator=g, dtype=torch.int32).to(torch.uint8).to(DEV)
+    dz = torch.randn(B, OH, OH, 32, generator=g).to(DEV)
     part = torch.full((int(L.xpa_conv1_u8_wgrad_num_partials()), 8192), float("nan"), device=DEV)
-    _l.check(L.xpa_conv1_u8_wgrad(ops._p(dz), ops._p(x), B, 84, 84, 4, 8, 4, 2, 32, ops._p(part), st), "wgrad")
+    _l.check(L.xpa_conv1_u8_wgrad(ops._p(dz), ops._p(x), B, H, H, 4, 8, s, p, 32, ops._p(part), st), "wgrad")
     dw = torch.empty(32, 4, 8, 8, device=DEV)
     _l.check(L.xpa_colsum_finalize(ops._p(part), part.shape[0], 8192, ops._p(dw), st), "finalize")
     ref = torch.nn.grad.conv2d_weight((x.double() / 255.0).permute(0, 3, 1, 2), (32, 4, 8, 8),
-                                      dz.double().permute(0, 3, 1, 2), 4, 2)
+                                      dz.double().permute(0, 3, 1, 2), s, p)
     torch.testing.assert_close(dw.double(), ref, rtol=1e-5, atol=1e-4)

@@ -517,6 +517,10 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_s2k_kernel(const float *__r
 // (8192 floats, the weight layout [n][c][ky][kx], divided by 255 once); xpa_colsum_finalize sums the partials in f64.
 constexpr int kWgBlocks = 512;
 
+// X2 (even W, S, P and an 8-B aligned frame buffer: the Nature CNN's 84 / 4 / 2): lane j loads pixels 2j and 2j + 1 of
+// its row (kernel row j / 4, columns 2 (j % 4), + 1) as one 8-B load and feeds tile (parity, c) with byte c of pixel
+// 2j + parity — 2 load instructions per 8 MFMAs instead of 3 (r02: the dword form was address-unit bound).
+template <bool X2>
 __global__ __launch_bounds__(256, 2) void conv1_u8_wgrad_kernel(const float *__restrict__ dz, const unsigned *__restrict__ x,
                                                                 int64_t rows, int H, int W, int OH, int OW, int S,
                                                                 int P, float *__restrict__ partial) {
@@ -538,7 +542,8 @@ __global__ __launch_bounds__(256, 2) void conv1_u8_wgrad_kernel(const float *__r
     int64_t b = m / ohw;
     int rem = (int)(m - b * ohw);
     int oy = rem / OW, ox = rem - (rem / OW) * OW;
-    const int ky0 = j >> 3, kx = j & 7;  // pixel 32 g + j: ky = 4 g + ky0
+    // dword form: pixel 32 g + j (ky = 4 g + j / 8, kx = j % 8); X2: pixels 2j + g (ky = j / 4, kx = 2 (j % 4) + g)
+    const int ky0 = X2 ? (j >> 2) : (j >> 3), kx = X2 ? 2 * (j & 3) : (j & 7);
     constexpr int U = 4;
     float an[U];
     unsigned dn[U][2];
@@ -547,12 +552,21 @@ __global__ __launch_bounds__(256, 2) void conv1_u8_wgrad_kernel(const float *__r
         for (int u = 0; u < U; ++u) {
             const bool mv = pp + u < p1 && m < rows;
             an[u] = dz[(mv ? m : 0) * 32 + j];
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-                const int iy = oy * S - P + 4 * g + ky0, ix = ox * S - P + kx;
+            if (X2) {  // both pixels in or both out: ix even, W even
+                const int iy = oy * S - P + ky0, ix = ox * S - P + kx;
                 const bool inb = mv && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-                const unsigned v = x[((mv ? b : 0) * H + (inb ? iy : 0)) * W + (inb ? ix : 0)];
-                dn[u][g] = inb ? v : 0u;
+                const uint2 v = *reinterpret_cast<const uint2 *>(x + ((mv ? b : 0) * H + (inb ? iy : 0)) * W +
+                                                                 (inb ? ix : 0));
+                dn[u][0] = inb ? v.x : 0u;
+                dn[u][1] = inb ? v.y : 0u;
+            } else {
+#pragma unroll
+                for (int g = 0; g < 2; ++g) {
+                    const int iy = oy * S - P + 4 * g + ky0, ix = ox * S - P + kx;
+                    const bool inb = mv && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+                    const unsigned v = x[((mv ? b : 0) * H + (inb ? iy : 0)) * W + (inb ? ix : 0)];
+                    dn[u][g] = inb ? v : 0u;
+                }
             }
             if (!mv) an[u] = 0.f;
             m += 2;  // advance this lane's row by 2
@@ -606,7 +620,7 @@ __global__ __launch_bounds__(256, 2) void conv1_u8_wgrad_kernel(const float *__r
         }
     }
     if (wave != 0) return;
-    // D of tile (g, c): row n = (r & 3) + 8 (r >> 2) + 4 h, column j = pixel 32 g + j -> W[n][c][ky][kx]
+    // D of tile (g, c): row n = (r & 3) + 8 (r >> 2) + 4 h, column j = pixel 32 g + j (X2: 2 j + g) -> W[n][c][ky][kx]
     float *pr = partial + (int64_t)blockIdx.x * 8192;
 #pragma unroll
     for (int g = 0; g < 2; ++g)
@@ -615,7 +629,7 @@ __global__ __launch_bounds__(256, 2) void conv1_u8_wgrad_kernel(const float *__r
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int n = (r & 3) + 8 * (r >> 2) + 4 * h;
-                pr[(n * 4 + c) * 64 + 32 * g + j] = acc[4 * g + c][r] / 255.0f;
+                pr[(n * 4 + c) * 64 + (X2 ? 2 * j + g : 32 * g + j)] = acc[4 * g + c][r] / 255.0f;
             }
 }
 }  // namespace
@@ -779,8 +793,14 @@ XPA_API int xpa_conv1_u8_wgrad(const float *dz, const uint8_t *x, int64_t batch,
         !partial || ((uintptr_t)x % 4) || height + 2 * pad < kernel || width + 2 * pad < kernel)
         return (int)hipErrorInvalidValue;
     const int64_t OH = (height + 2 * pad - kernel) / stride + 1, OW = (width + 2 * pad - kernel) / stride + 1;
-    hipLaunchKernelGGL(conv1_u8_wgrad_kernel, dim3(kWgBlocks), dim3(256), 0, (hipStream_t)stream, dz,
-                       (const unsigned *)x, batch * OH * OW, (int)height, (int)width, (int)OH, (int)OW, (int)stride,
-                       (int)pad, partial);
+    const bool x2 = width % 2 == 0 && stride % 2 == 0 && pad % 2 == 0 && (uintptr_t)x % 8 == 0;
+    if (x2)
+        hipLaunchKernelGGL(conv1_u8_wgrad_kernel<true>, dim3(kWgBlocks), dim3(256), 0, (hipStream_t)stream, dz,
+                           (const unsigned *)x, batch * OH * OW, (int)height, (int)width, (int)OH, (int)OW,
+                           (int)stride, (int)pad, partial);
+    else
+        hipLaunchKernelGGL(conv1_u8_wgrad_kernel<false>, dim3(kWgBlocks), dim3(256), 0, (hipStream_t)stream, dz,
+                           (const unsigned *)x, batch * OH * OW, (int)height, (int)width, (int)OH, (int)OW,
+                           (int)stride, (int)pad, partial);
     return xpa_launch_status();
 }
