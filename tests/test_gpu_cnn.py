@@ -225,20 +225,22 @@ def test_fused_qnetwork_matches_autograd(B):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("B,act,slope", [(3, 1, 0.0), (17, 0, 0.0), (64, 1, 0.01), (5, 2, 0.0)])
-def test_conv1_u8_matches_conv2d(B, act, slope):
+@pytest.mark.parametrize("B,act,slope,H,s,p", [(3, 1, 0.0, 84, 4, 2), (17, 0, 0.0, 84, 4, 2), (64, 1, 0.01, 84, 4, 2),
+                                             (5, 2, 0.0, 84, 4, 2), (4, 1, 0.0, 85, 3, 1), (3, 0, 0.0, 86, 4, 1)])
+def test_conv1_u8_matches_conv2d(B, act, slope, H, s, p):
     """K25 (the first conv block straight from uint8 frames on fp32 MFMA) == conv2d(K20 frames) + bias + act within
     fp32 summation-order rounding, at the AC_CNN_Atari / Basic_CNN shape (84 x 84 x 4, 8 x 8 stride 4 pad 2 -> 32)."""
     _l, ops = _lib()
     g = torch.Generator(device="cpu").manual_seed(B)
-    x = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.int32).to(torch.uint8).to(DEV)
+    OH = (H + 2 * p - 8) // s + 1   # 84 / 4 / 2: the 8-B pixel-pair form; odd width / stride / pad: the dword form
+    x = torch.randint(0, 256, (B, H, H, 4), generator=g, dtype=torch.int32).to(torch.uint8).to(DEV)
     w = (torch.randn(32, 4, 8, 8, generator=g) * 0.05).to(DEV)
     b = (torch.randn(32, generator=g) * 0.1).to(DEV)
-    y = torch.full((B, 21, 21, 32), float("nan"), device=DEV)
-    _l.check(ops.lib().xpa_conv1_u8_fwd(act, ops._p(x), B, 84, 84, 4, 8, 4, 2, ops._p(w), ops._p(b), 32, slope,
+    y = torch.full((B, OH, OH, 32), float("nan"), device=DEV)
+    _l.check(ops.lib().xpa_conv1_u8_fwd(act, ops._p(x), B, H, H, 4, 8, s, p, ops._p(w), ops._p(b), 32, slope,
                                         ops._p(y), ops._stream(DEV)), "conv1_u8")
     xf = x.double() / 255.0
-    z = torch.nn.functional.conv2d(xf.permute(0, 3, 1, 2), w.double(), b.double(), 4, 2).permute(0, 2, 3, 1)
+    z = torch.nn.functional.conv2d(xf.permute(0, 3, 1, 2), w.double(), b.double(), s, p).permute(0, 2, 3, 1)
     ref = {0: z, 1: torch.nn.functional.leaky_relu(z, slope), 2: torch.tanh(z)}[act]
     torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=2e-5)
 

@@ -229,12 +229,35 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // Loads: 4 chunks of 8 pixel pairs (two kernel rows); chunk c + 1's 16 dwords per lane are requested before chunk
 // c's 64 MFMAs (a two-buffer register ring, fully unrolled), addresses as 32-bit offsets from each row tile's frame.
-template <int ACT>
+// Pixel of slot j (0..7) of a chunk for lane half h: the dword form pairs pixels 2j + h; X2 (even W, S and P, 8-B
+// aligned frames) loads pixels 4q + 2h and 4q + 2h + 1 (same kernel row, even column: both in or both out of the frame)
+// as one 8-B load into slots 2q, 2q + 1 — half the load instructions (the address units bound the dword form).
+template <bool X2>
+__device__ __forceinline__ int conv1_pix(int chunk, int j, int h) {
+    return X2 ? 16 * chunk + 4 * (j >> 1) + 2 * h + (j & 1) : 16 * chunk + 2 * j + h;
+}
+
+template <bool X2>
 __device__ __forceinline__ void conv1_load_chunk(unsigned (&v)[2][8], const unsigned *const (&xr)[2], const int (&by)[2],
                                                  const int (&bx)[2], int H, int W, int chunk, int h) {
+    if (X2) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int p = conv1_pix<true>(chunk, 2 * q, h), ky = p >> 3, kx = p & 7;
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) {
+                const int iy = by[rt] + ky, ix = bx[rt] + kx;
+                const bool inb = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+                const uint2 d = *reinterpret_cast<const uint2 *>(xr[rt] + (inb ? iy * W + ix : 0));
+                v[rt][2 * q] = inb ? d.x : 0u;
+                v[rt][2 * q + 1] = inb ? d.y : 0u;
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const int p = 16 * chunk + 2 * j + h, ky = p >> 3, kx = p & 7;
+        const int p = conv1_pix<false>(chunk, j, h), ky = p >> 3, kx = p & 7;
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
             const int iy = by[rt] + ky, ix = bx[rt] + kx;
@@ -245,11 +268,12 @@ __device__ __forceinline__ void conv1_load_chunk(unsigned (&v)[2][8], const unsi
     }
 }
 
+template <bool X2>
 __device__ __forceinline__ void conv1_mfma_chunk(f32x16 (&acc)[2], const unsigned (&v)[2][8], const float *sB, int chunk,
                                                  int h, int i) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const int p = 16 * chunk + 2 * j + h;
+        const int p = conv1_pix<X2>(chunk, j, h);
         const f4v b4 = *reinterpret_cast<const f4v *>(sB + (p * 32 + i) * 4);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -262,7 +286,7 @@ __device__ __forceinline__ void conv1_mfma_chunk(f32x16 (&acc)[2], const unsigne
     }
 }
 
-template <int ACT>
+template <int ACT, bool X2>
 __global__ __launch_bounds__(256, 4) void conv1_u8_fwd_kernel(const unsigned *__restrict__ x, int64_t rows, int H,
                                                               int W, int OH, int OW, int S, int P,
                                                               const float *__restrict__ w, const float *__restrict__ bias,
@@ -302,8 +326,8 @@ __global__ __launch_bounds__(256, 4) void conv1_u8_fwd_kernel(const unsigned *__
     // sched_barrier: keep the ring order (hipcc otherwise hoists all 64 loads and their 64-bit addresses: 248
     // VGPRs, 2 waves per SIMD).  The ring runs on across row blocks: the next block's chunks 0 and 1 are requested
     // during this block's chunks 2 and 3, so no block starts with an exposed load round trip.
-    conv1_load_chunk<ACT>(va, xr, by, bx, H, W, 0, h);
-    conv1_load_chunk<ACT>(vb, xr, by, bx, H, W, 1, h);
+    conv1_load_chunk<X2>(va, xr, by, bx, H, W, 0, h);
+    conv1_load_chunk<X2>(vb, xr, by, bx, H, W, 1, h);
     for (;;) {
         f32x16 acc[2];
 #pragma unroll
@@ -311,27 +335,27 @@ __global__ __launch_bounds__(256, 4) void conv1_u8_fwd_kernel(const unsigned *__
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[rt][r] = 0.f;
         __builtin_amdgcn_sched_barrier(0);
-        conv1_mfma_chunk(acc, va, sB, 0, h, i);
+        conv1_mfma_chunk<X2>(acc, va, sB, 0, h, i);
         __builtin_amdgcn_sched_barrier(0);
-        conv1_load_chunk<ACT>(va, xr, by, bx, H, W, 2, h);
+        conv1_load_chunk<X2>(va, xr, by, bx, H, W, 2, h);
         __builtin_amdgcn_sched_barrier(0);
-        conv1_mfma_chunk(acc, vb, sB, 1, h, i);
+        conv1_mfma_chunk<X2>(acc, vb, sB, 1, h, i);
         __builtin_amdgcn_sched_barrier(0);
-        conv1_load_chunk<ACT>(vb, xr, by, bx, H, W, 3, h);
+        conv1_load_chunk<X2>(vb, xr, by, bx, H, W, 3, h);
         __builtin_amdgcn_sched_barrier(0);
-        conv1_mfma_chunk(acc, va, sB, 2, h, i);
+        conv1_mfma_chunk<X2>(acc, va, sB, 2, h, i);
         __builtin_amdgcn_sched_barrier(0);
         const int64_t r0 = blk * kC1Rows + wave * 64;
         const int64_t nblk = blk + gridDim.x;
         const bool more = nblk * kC1Rows < rows;  // block-uniform
         if (more) {
             geometry(nblk, by, bx, xr);
-            conv1_load_chunk<ACT>(va, xr, by, bx, H, W, 0, h);
+            conv1_load_chunk<X2>(va, xr, by, bx, H, W, 0, h);
         }
         __builtin_amdgcn_sched_barrier(0);
-        conv1_mfma_chunk(acc, vb, sB, 3, h, i);
+        conv1_mfma_chunk<X2>(acc, vb, sB, 3, h, i);
         __builtin_amdgcn_sched_barrier(0);
-        if (more) conv1_load_chunk<ACT>(vb, xr, by, bx, H, W, 1, h);
+        if (more) conv1_load_chunk<X2>(vb, xr, by, bx, H, W, 1, h);
         // C/D map: row = (r & 3) + 8 (r >> 2) + 4 h, column n = i
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
@@ -744,9 +768,14 @@ XPA_API int xpa_conv1_u8_fwd(int act, const uint8_t *x, int64_t batch, int64_t h
     const int64_t blocks = (rows + kC1Rows - 1) / kC1Rows;
     const dim3 grid((unsigned)(blocks < 1024 ? blocks : 1024)), block(256);
     hipStream_t s = (hipStream_t)stream;
+    const bool x2 = width % 2 == 0 && stride % 2 == 0 && pad % 2 == 0 && (uintptr_t)x % 8 == 0;
 #define XPA_C1(A_)                                                                                                   \
-    hipLaunchKernelGGL((conv1_u8_fwd_kernel<A_>), grid, block, 0, s, (const unsigned *)x, rows, (int)height,           \
-                       (int)width, (int)OH, (int)OW, (int)stride, (int)pad, w, bias, slope, y)
+    if (x2)                                                                                                          \
+        hipLaunchKernelGGL((conv1_u8_fwd_kernel<A_, true>), grid, block, 0, s, (const unsigned *)x, rows,             \
+                           (int)height, (int)width, (int)OH, (int)OW, (int)stride, (int)pad, w, bias, slope, y);     \
+    else                                                                                                             \
+        hipLaunchKernelGGL((conv1_u8_fwd_kernel<A_, false>), grid, block, 0, s, (const unsigned *)x, rows,            \
+                           (int)height, (int)width, (int)OH, (int)OW, (int)stride, (int)pad, w, bias, slope, y)
     if (act == 0) XPA_C1(0);
     else if (act == 1) XPA_C1(1);
     else XPA_C1(2);
