@@ -535,6 +535,14 @@ int64_t xpa_conv1_u8_wgrad_num_partials(void);
 int xpa_conv1_u8_wgrad(const float *dz, const uint8_t *x, int64_t batch, int64_t height, int64_t width,
                        int64_t channels, int64_t kernel, int64_t stride, int64_t pad, int64_t out_channels,
                        float *partial, xpa_stream_t stream);
+/* K26 with the conv block's activation backward + bias gradient folded in (act >= 0: K22 on the first conv's output
+ * never runs): dz here is d loss / d y at the block's OUTPUT y (NHWC f32, the forward's K25 output), the kernel
+ * forms dh act'(y) itself (act as xpa_bias_act) and also writes per-block bias partials
+ * [xpa_conv1_u8_wgrad_num_partials(), 32] for xpa_colsum_finalize.  act = -1: exactly xpa_conv1_u8_wgrad. */
+int xpa_conv1_u8_wgrad_act(int act, const float *dz, const float *y, float slope, const uint8_t *x, int64_t batch,
+                           int64_t height, int64_t width, int64_t channels, int64_t kernel, int64_t stride,
+                           int64_t pad, int64_t out_channels, float *partial, float *bias_partial,
+                           xpa_stream_t stream);
 /* K21: y = act(y + bias) in place over [rows, cols] (bias [cols] or NULL): the conv / Linear bias and the
  * activation of cnn_block / mlp_block (xuance/torch/utils/layers.py:8-57).  cols % 4 == 0 and cols / 4 must
  * divide 256; act 0 identity, 1 LeakyReLU(slope) / ReLU, 2 tanh. */

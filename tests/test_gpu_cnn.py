@@ -307,3 +307,37 @@ def test_conv1_u8_wgrad_matches_conv2d_weight(B, H, s, p):
     ref = torch.nn.grad.conv2d_weight((x.double() / 255.0).permute(0, 3, 1, 2), (32, 4, 8, 8),
                                       dz.double().permute(0, 3, 1, 2), s, p)
     torch.testing.assert_close(dw.double(), ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("act,slope", [(1, 0.0), (1, 0.01), (2, 0.0), (0, 0.0)])
+def test_conv1_u8_wgrad_act_matches_k22_then_k26(act, slope):
+    """xpa_conv1_u8_wgrad_act (K26 with the activation backward + bias gradient folded in) == K22 on the conv's output
+    then K26: the same weight gradient (bitwise: the same dz values in the same order) and the bias gradient within
+    f32 summation-order rounding."""
+    _l, ops = _lib()
+    L, st = ops.lib(), ops._stream(DEV)
+    B = 9
+    g = torch.Generator(device="cpu").manual_seed(act * 10 + int(slope * 100))
+    x = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.int32).to(torch.uint8).to(DEV)
+    y = torch.randn(B, 21, 21, 32, generator=g).to(DEV)
+    y = torch.tanh(y) if act == 2 else (torch.relu(y) if act == 1 and slope == 0 else y)
+    dh = torch.randn(B, 21, 21, 32, generator=g).to(DEV)
+    G = int(L.xpa_conv1_u8_wgrad_num_partials())
+    pw, pb = torch.empty(G, 8192, device=DEV), torch.empty(G, 32, device=DEV)
+    _l.check(L.xpa_conv1_u8_wgrad_act(act, ops._p(dh), ops._p(y), slope, ops._p(x), B, 84, 84, 4, 8, 4, 2, 32,
+                                      ops._p(pw), ops._p(pb), st), "wgrad_act")
+    dw, db = torch.empty(8192, device=DEV), torch.empty(32, device=DEV)
+    _l.check(L.xpa_colsum_finalize(ops._p(pw), G, 8192, ops._p(dw), st), "f")
+    _l.check(L.xpa_colsum_finalize(ops._p(pb), G, 32, ops._p(db), st), "f")
+    dz = dh.clone()
+    rows = B * 441
+    kp = torch.empty(int(L.xpa_act_bwd_bias_num_partials(rows, 32)), 32, device=DEV)
+    _l.check(L.xpa_act_bwd_bias(act, ops._p(dz), ops._p(y), rows, 32, slope, ops._p(dz), ops._p(kp), st), "k22")
+    db_ref = torch.empty(32, device=DEV)
+    _l.check(L.xpa_colsum_finalize(ops._p(kp), kp.shape[0], 32, ops._p(db_ref), st), "f")
+    pw2 = torch.empty_like(pw)
+    _l.check(L.xpa_conv1_u8_wgrad(ops._p(dz), ops._p(x), B, 84, 84, 4, 8, 4, 2, 32, ops._p(pw2), st), "wgrad")
+    dw_ref = torch.empty(8192, device=DEV)
+    _l.check(L.xpa_colsum_finalize(ops._p(pw2), G, 8192, ops._p(dw_ref), st), "f")
+    assert torch.equal(dw, dw_ref)
+    torch.testing.assert_close(db, db_ref, rtol=1e-5, atol=1e-4)

@@ -68,6 +68,8 @@ SIGNATURES = {
     "xpa_conv_dgrad_s2k": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64,
                                            c_i64, c_p, c_p]),
     "xpa_conv1_u8_wgrad_num_partials": (c_i64, []),
+    "xpa_conv1_u8_wgrad_act": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_f32, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
+                                               c_i64, c_i64, c_p, c_p, c_p]),
     "xpa_conv1_u8_wgrad": (ctypes.c_int, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
     "xpa_conv1_u8_fwd": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p,
                                          c_i64, c_f32, c_p, c_p]),

@@ -544,11 +544,16 @@ constexpr int kWgBlocks = 512;
 // X2 (even W, S, P and an 8-B aligned frame buffer: the Nature CNN's 84 / 4 / 2): lane j loads pixels 2j and 2j + 1 of
 // its row (kernel row j / 4, columns 2 (j % 4), + 1) as one 8-B load and feeds tile (parity, c) with byte c of pixel
 // 2j + parity — 2 load instructions per 8 MFMAs instead of 3 (r02: the dword form was address-unit bound).
-template <bool X2>
+// ACT >= 0: dz is the gradient at the block's OUTPUT (before the activation) and the block's activation backward +
+// bias-gradient partials run here (K22 folded in: dz = dh act'(y) never goes to HBM); y = the forward's output.
+template <bool X2, int ACT>
 __global__ __launch_bounds__(256, 2) void conv1_u8_wgrad_kernel(const float *__restrict__ dz, const unsigned *__restrict__ x,
                                                                 int64_t rows, int H, int W, int OH, int OW, int S,
-                                                                int P, float *__restrict__ partial) {
+                                                                int P, float *__restrict__ partial,
+                                                                const float *__restrict__ y, float slope,
+                                                                float *__restrict__ bias_partial) {
     __shared__ __attribute__((aligned(16))) float s_red[64 * 16 * 8];  // one wave's accumulators, lane-major
+    float bsum = 0.f;
     const int t = threadIdx.x, lane = t & 63, h = lane >> 5, j = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     // this wave's row range (row pairs split evenly over every wave of the grid)
@@ -576,6 +581,7 @@ __global__ __launch_bounds__(256, 2) void conv1_u8_wgrad_kernel(const float *__r
         for (int u = 0; u < U; ++u) {
             const bool mv = pp + u < p1 && m < rows;
             an[u] = dz[(mv ? m : 0) * 32 + j];
+            if (ACT >= 0) an[u] = act_grad<ACT>(an[u], y[(mv ? m : 0) * 32 + j], slope);
             if (X2) {  // both pixels in or both out: ix even, W even
                 const int iy = oy * S - P + ky0, ix = ox * S - P + kx;
                 const bool inb = mv && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
@@ -615,6 +621,10 @@ __global__ __launch_bounds__(256, 2) void conv1_u8_wgrad_kernel(const float *__r
             d[u][1] = dn[u][1];
         }
         if (pp + U < p1) load_group(pp + U);
+        if (ACT >= 0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) bsum += a[u];
+        }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -625,6 +635,16 @@ __global__ __launch_bounds__(256, 2) void conv1_u8_wgrad_kernel(const float *__r
                     acc[4 * g + c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], (float)((d[u][g] >> (8 * c)) & 0xffu),
                                                                           acc[4 * g + c], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
+    }
+    if (ACT >= 0) {  // bias partial: lane (h, j)'s sums over its rows, both halves and the 4 waves in a fixed order
+        __shared__ float s_b[4][64];
+        s_b[wave][lane] = bsum;
+        __syncthreads();
+        if (t < 32) {
+            float tb = 0.f;
+            for (int w = 0; w < 4; ++w) tb += s_b[w][t] + s_b[w][t + 32];
+            bias_partial[(int64_t)blockIdx.x * 32 + t] = tb;
+        }
     }
     // waves 1..3 added into wave 0 in order
     for (int src = 1; src < 4; ++src) {
@@ -815,21 +835,36 @@ XPA_API int xpa_conv_dgrad_s2k(const float *dy, int64_t batch, int64_t out_h, in
 
 XPA_API int64_t xpa_conv1_u8_wgrad_num_partials(void) { return kWgBlocks; }
 
-XPA_API int xpa_conv1_u8_wgrad(const float *dz, const uint8_t *x, int64_t batch, int64_t height, int64_t width,
-                               int64_t channels, int64_t kernel, int64_t stride, int64_t pad, int64_t out_channels,
-                               float *partial, xpa_stream_t stream) {
+XPA_API int xpa_conv1_u8_wgrad_act(int act, const float *dz, const float *y, float slope, const uint8_t *x,
+                                   int64_t batch, int64_t height, int64_t width, int64_t channels, int64_t kernel,
+                                   int64_t stride, int64_t pad, int64_t out_channels, float *partial,
+                                   float *bias_partial, xpa_stream_t stream) {
     if (batch <= 0 || channels != 4 || kernel != 8 || out_channels != 32 || stride < 1 || pad < 0 || !dz || !x ||
-        !partial || ((uintptr_t)x % 4) || height + 2 * pad < kernel || width + 2 * pad < kernel)
+        !partial || ((uintptr_t)x % 4) || height + 2 * pad < kernel || width + 2 * pad < kernel || act < -1 ||
+        act > 2 || (act >= 0 && (!y || !bias_partial)))
         return (int)hipErrorInvalidValue;
     const int64_t OH = (height + 2 * pad - kernel) / stride + 1, OW = (width + 2 * pad - kernel) / stride + 1;
     const bool x2 = width % 2 == 0 && stride % 2 == 0 && pad % 2 == 0 && (uintptr_t)x % 8 == 0;
-    if (x2)
-        hipLaunchKernelGGL(conv1_u8_wgrad_kernel<true>, dim3(kWgBlocks), dim3(256), 0, (hipStream_t)stream, dz,
-                           (const unsigned *)x, batch * OH * OW, (int)height, (int)width, (int)OH, (int)OW,
-                           (int)stride, (int)pad, partial);
-    else
-        hipLaunchKernelGGL(conv1_u8_wgrad_kernel<false>, dim3(kWgBlocks), dim3(256), 0, (hipStream_t)stream, dz,
-                           (const unsigned *)x, batch * OH * OW, (int)height, (int)width, (int)OH, (int)OW,
-                           (int)stride, (int)pad, partial);
+    hipStream_t s = (hipStream_t)stream;
+#define XPA_WG(X_, A_)                                                                                             \
+    hipLaunchKernelGGL((conv1_u8_wgrad_kernel<X_, A_>), dim3(kWgBlocks), dim3(256), 0, s, dz, (const unsigned *)x, \
+                       batch * OH * OW, (int)height, (int)width, (int)OH, (int)OW, (int)stride, (int)pad, partial, y, \
+                       slope, bias_partial)
+#define XPA_WG_A(X_)                \
+    if (act < 0) XPA_WG(X_, -1);    \
+    else if (act == 0) XPA_WG(X_, 0); \
+    else if (act == 1) XPA_WG(X_, 1); \
+    else XPA_WG(X_, 2);
+    if (x2) { XPA_WG_A(true) }
+    else { XPA_WG_A(false) }
+#undef XPA_WG_A
+#undef XPA_WG
     return xpa_launch_status();
+}
+
+XPA_API int xpa_conv1_u8_wgrad(const float *dz, const uint8_t *x, int64_t batch, int64_t height, int64_t width,
+                               int64_t channels, int64_t kernel, int64_t stride, int64_t pad, int64_t out_channels,
+                               float *partial, xpa_stream_t stream) {
+    return xpa_conv1_u8_wgrad_act(-1, dz, nullptr, 0.f, x, batch, height, width, channels, kernel, stride, pad,
+                                  out_channels, partial, nullptr, stream);
 }

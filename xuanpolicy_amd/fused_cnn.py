@@ -22,8 +22,9 @@ Every activation stays NHWC ([rows = B*H*W, C] row-major), the layout the uint8 
             gradient) -> dW GEMM (permuted back into the reference layout) + dX GEMM; Basic_CNN: K24 (the pooled
             gradient routed to the argmax, ReLU backward, bias gradient) -> per conv: K22 then MIOpen
             convolution_backward (weight; data too except where K27 xpa_conv_dgrad_s2k takes the data gradient — the
-            4 x 4 stride-2 32 -> 64 conv); the first conv (no dX) after K25: K26 xpa_conv1_u8_wgrad from the uint8
-            frames + the f64 column-sum finalize (no f32 frame copy anywhere).
+            4 x 4 stride-2 32 -> 64 conv); the first conv (no dX) after K25: K26 xpa_conv1_u8_wgrad_act from the uint8
+            frames with its ReLU backward + bias gradient folded in (no K22 pass) + the f64 column-sum finalizes (no
+            f32 frame copy anywhere).
 Parameter gradients are written into the parameters' .grad views (allocated when missing).
 """
 import torch
@@ -258,18 +259,31 @@ class _Trunk:
             fouts.append(s)
         return s, (hs, None, flat, fouts)
 
-    def _conv1_wgrad(self, conv, g, xu):
-        """K26 partials + the f64 column-sum finalize -> conv.weight.grad (g: NHWC d output after K22)."""
+    @staticmethod
+    def _k26_ok(conv, x0):
+        return x0.dtype == torch.uint8 and conv.weight.grad.is_contiguous() and conv.bias.grad.is_contiguous()
+
+    def _conv1_wgrad(self, conv, g, xu, act=None):
+        """K26 partials + the f64 column-sum finalize -> conv.weight.grad.  act None: g is d output after the
+        activation backward (K22 / K24 ran); act = (code, slope, y): g is d loss / d y and K26 also forms the
+        activation backward and the bias-gradient partials (-> conv.bias.grad)."""
         L, st = ops.lib(), ops._stream(g.device)
+        G = int(L.xpa_conv1_u8_wgrad_num_partials())
         if getattr(self, "_wg_part", None) is None:
-            self._wg_part = torch.empty((int(L.xpa_conv1_u8_wgrad_num_partials()), 8192), dtype=torch.float32,
-                                        device=g.device)
+            self._wg_part = torch.empty((G, 8192), dtype=torch.float32, device=g.device)
+            self._wb_part = torch.empty((G, 32), dtype=torch.float32, device=g.device)
         g = g if g.is_contiguous() else g.contiguous()
         B, H, W, C = xu.shape
-        _lib.check(L.xpa_conv1_u8_wgrad(ops._p(g), ops._p(xu), B, H, W, C, 8, conv.stride[0], conv.padding[0], 32,
-                                        ops._p(self._wg_part), st), "xpa_conv1_u8_wgrad")
-        _lib.check(L.xpa_colsum_finalize(ops._p(self._wg_part), self._wg_part.shape[0], 8192,
-                                         ops._p(conv.weight.grad), st), "xpa_colsum_finalize")
+        code, slope, y = act if act is not None else (-1, 0.0, None)
+        _lib.check(L.xpa_conv1_u8_wgrad_act(code, ops._p(g), ops._p(y) if y is not None else None, float(slope),
+                                            ops._p(xu), B, H, W, C, 8, conv.stride[0], conv.padding[0], 32,
+                                            ops._p(self._wg_part), ops._p(self._wb_part) if y is not None else None,
+                                            st), "xpa_conv1_u8_wgrad_act")
+        _lib.check(L.xpa_colsum_finalize(ops._p(self._wg_part), G, 8192, ops._p(conv.weight.grad), st),
+                   "xpa_colsum_finalize")
+        if y is not None:
+            _lib.check(L.xpa_colsum_finalize(ops._p(self._wb_part), G, 32, ops._p(conv.bias.grad), st),
+                       "xpa_colsum_finalize")
 
     @staticmethod
     def _dgrad_ok(conv):
@@ -334,9 +348,13 @@ class _Trunk:
                 g = g.reshape(y.shape)
                 if not g.is_contiguous():
                     g = g.contiguous()
+                if i == 0 and self._k26_ok(conv, hs[0]):
+                    # K26 with the activation backward + bias gradient folded in (no K22 pass over conv1's output)
+                    self._conv1_wgrad(conv, g, hs[0], act=(code, slope, y))
+                    break
                 _act_bwd_bias(parts, code, g.view(-1, Cy), y.view(-1, Cy), slope, conv.bias.grad)
             need_in = i > 0
-            if i == 0 and hs[0].dtype == torch.uint8 and conv.weight.grad.is_contiguous():
+            if i == 0 and self._k26_ok(conv, hs[0]):
                 self._conv1_wgrad(conv, g, hs[0])   # K26: from the uint8 frames, no f32 frame copy
                 break
             x_in = self.frames(hs[i]) if hs[i].dtype == torch.uint8 else hs[i]
