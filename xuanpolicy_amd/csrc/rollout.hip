@@ -12,6 +12,8 @@ namespace {
 
 constexpr int kGatherRows = 64;  // rows per gather block == rows per adv partial (1024 blocks at B = 65 536)
 constexpr int kRmsRows = 256;     // rows per RMS partial block
+constexpr int kRmsThreads = 1024; // threads per RMS partial block (r02: 256 left wide observations, 376 columns at
+                                  // C4, with one thread per column walking all 256 rows: 43.8 us per env step)
 constexpr uint32_t kSaltAct = 0xAC7105EDu;
 constexpr uint32_t kSaltReset = 0x5EED0000u;  // oracle/synth_env.py SALT_RESET
 
@@ -136,19 +138,19 @@ __device__ void rms_merge_body(const double *part, int64_t np, int64_t n, int64_
 // MERGE: the last block to finish (atomic ticket) also runs the merge below over all blocks' partials in
 // block order (deterministic, = xpa_rms_merge) and resets the ticket: one launch per obs-RMS update.
 template <bool MERGE>
-__global__ __launch_bounds__(256) void rms_partials_kernel(const float *__restrict__ x, int64_t n, int64_t dim,
-                                                           int64_t ld, const float *shift,  // may alias mean
-                                                           double *__restrict__ part, float *mean,
-                                                           float *__restrict__ var, double *__restrict__ count,
-                                                           unsigned int *__restrict__ ticket) {
-    __shared__ double s_sum[256], s_sq[256];
+__global__ __launch_bounds__(kRmsThreads) void rms_partials_kernel(const float *__restrict__ x, int64_t n, int64_t dim,
+                                                                   int64_t ld, const float *shift,  // may alias mean
+                                                                   double *__restrict__ part, float *mean,
+                                                                   float *__restrict__ var, double *__restrict__ count,
+                                                                   unsigned int *__restrict__ ticket) {
+    __shared__ double s_sum[kRmsThreads], s_sq[kRmsThreads];
     __shared__ bool s_last;
     const int64_t r0 = (int64_t)blockIdx.x * kRmsRows;
     const int64_t r1 = r0 + kRmsRows < n ? r0 + kRmsRows : n;
     const int64_t np = gridDim.x;
     for (int64_t c0 = 0; c0 < dim; c0 += 256) {
         const int dc = (int)(dim - c0 < 256 ? dim - c0 : 256);  // columns in this tile
-        const int groups = 256 / dc;                            // row groups
+        const int groups = kRmsThreads / dc;                    // row groups
         const int c = threadIdx.x % dc, gsub = threadIdx.x / dc;
         double s = 0.0, q = 0.0;
         if (gsub < groups) {
@@ -670,7 +672,7 @@ XPA_API int xpa_rms_partials(const float *x, int64_t n, int64_t dim, int64_t ld,
                              double *partials, xpa_stream_t stream) {
     if (n <= 0 || dim <= 0 || ld < dim || !x || !partials) return (int)hipErrorInvalidValue;
     const int64_t np = xpa_rms_num_partials(n);
-    hipLaunchKernelGGL(rms_partials_kernel<false>, dim3((unsigned)np), dim3(256), 0, (hipStream_t)stream, x, n, dim,
+    hipLaunchKernelGGL(rms_partials_kernel<false>, dim3((unsigned)np), dim3(kRmsThreads), 0, (hipStream_t)stream, x, n, dim,
                        ld, shift, partials, (float *)nullptr, (float *)nullptr, (double *)nullptr,
                        (unsigned int *)nullptr);
     return xpa_launch_status();
@@ -681,7 +683,7 @@ XPA_API int xpa_rms_update(const float *x, int64_t n, int64_t dim, int64_t ld, f
     if (n <= 0 || dim <= 0 || ld < dim || !x || !mean || !var || !count || !partials || !ticket)
         return (int)hipErrorInvalidValue;
     const int64_t np = xpa_rms_num_partials(n);
-    hipLaunchKernelGGL(rms_partials_kernel<true>, dim3((unsigned)np), dim3(256), 0, (hipStream_t)stream, x, n, dim, ld,
+    hipLaunchKernelGGL(rms_partials_kernel<true>, dim3((unsigned)np), dim3(kRmsThreads), 0, (hipStream_t)stream, x, n, dim, ld,
                        (const float *)mean, partials, mean, var, count, (unsigned int *)ticket);
     return xpa_launch_status();
 }
