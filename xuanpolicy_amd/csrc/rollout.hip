@@ -12,8 +12,10 @@ namespace {
 
 constexpr int kGatherRows = 64;  // rows per gather block == rows per adv partial (1024 blocks at B = 65 536)
 constexpr int kRmsRows = 256;     // rows per RMS partial block
-constexpr int kRmsThreads = 1024; // threads per RMS partial block (r02: 256 left wide observations, 376 columns at
-                                  // C4, with one thread per column walking all 256 rows: 43.8 us per env step)
+// threads per RMS partial block: 1024 for wide observations (r02: with 256, C4's 376 columns had one thread per column
+// walking all 256 rows, 43.8 us per env step -> 17.9 us), 256 for narrow ones (C1 / C2: the reduction and the merge
+// stay as short as before)
+constexpr int kRmsWideDim = 64;
 constexpr uint32_t kSaltAct = 0xAC7105EDu;
 constexpr uint32_t kSaltReset = 0x5EED0000u;  // oracle/synth_env.py SALT_RESET
 
@@ -137,7 +139,7 @@ __device__ void rms_merge_body(const double *part, int64_t np, int64_t n, int64_
 
 // MERGE: the last block to finish (atomic ticket) also runs the merge below over all blocks' partials in
 // block order (deterministic, = xpa_rms_merge) and resets the ticket: one launch per obs-RMS update.
-template <bool MERGE>
+template <bool MERGE, int kRmsThreads>
 __global__ __launch_bounds__(kRmsThreads) void rms_partials_kernel(const float *__restrict__ x, int64_t n, int64_t dim,
                                                                    int64_t ld, const float *shift,  // may alias mean
                                                                    double *__restrict__ part, float *mean,
@@ -672,9 +674,14 @@ XPA_API int xpa_rms_partials(const float *x, int64_t n, int64_t dim, int64_t ld,
                              double *partials, xpa_stream_t stream) {
     if (n <= 0 || dim <= 0 || ld < dim || !x || !partials) return (int)hipErrorInvalidValue;
     const int64_t np = xpa_rms_num_partials(n);
-    hipLaunchKernelGGL(rms_partials_kernel<false>, dim3((unsigned)np), dim3(kRmsThreads), 0, (hipStream_t)stream, x, n, dim,
-                       ld, shift, partials, (float *)nullptr, (float *)nullptr, (double *)nullptr,
-                       (unsigned int *)nullptr);
+    if (dim > kRmsWideDim)
+        hipLaunchKernelGGL((rms_partials_kernel<false, 1024>), dim3((unsigned)np), dim3(1024), 0, (hipStream_t)stream, x,
+                           n, dim, ld, shift, partials, (float *)nullptr, (float *)nullptr, (double *)nullptr,
+                           (unsigned int *)nullptr);
+    else
+        hipLaunchKernelGGL((rms_partials_kernel<false, 256>), dim3((unsigned)np), dim3(256), 0, (hipStream_t)stream, x,
+                           n, dim, ld, shift, partials, (float *)nullptr, (float *)nullptr, (double *)nullptr,
+                           (unsigned int *)nullptr);
     return xpa_launch_status();
 }
 
@@ -683,8 +690,12 @@ XPA_API int xpa_rms_update(const float *x, int64_t n, int64_t dim, int64_t ld, f
     if (n <= 0 || dim <= 0 || ld < dim || !x || !mean || !var || !count || !partials || !ticket)
         return (int)hipErrorInvalidValue;
     const int64_t np = xpa_rms_num_partials(n);
-    hipLaunchKernelGGL(rms_partials_kernel<true>, dim3((unsigned)np), dim3(kRmsThreads), 0, (hipStream_t)stream, x, n, dim, ld,
-                       (const float *)mean, partials, mean, var, count, (unsigned int *)ticket);
+    if (dim > kRmsWideDim)
+        hipLaunchKernelGGL((rms_partials_kernel<true, 1024>), dim3((unsigned)np), dim3(1024), 0, (hipStream_t)stream, x,
+                           n, dim, ld, (const float *)mean, partials, mean, var, count, (unsigned int *)ticket);
+    else
+        hipLaunchKernelGGL((rms_partials_kernel<true, 256>), dim3((unsigned)np), dim3(256), 0, (hipStream_t)stream, x,
+                           n, dim, ld, (const float *)mean, partials, mean, var, count, (unsigned int *)ticket);
     return xpa_launch_status();
 }
 
