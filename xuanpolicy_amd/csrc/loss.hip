@@ -30,7 +30,18 @@ __device__ __forceinline__ void adv_moments(const double *partials, int64_t n_pa
     // Wave 0 reduces the gather kernel's (sum, sumsq) rows in a fixed order.
     if (threadIdx.x < 64) {
         double s = 0.0, q = 0.0;
-        for (int64_t k = threadIdx.x; k < n_partials; k += 64) {
+        int64_t k = threadIdx.x;
+        for (; k + 7 * 64 < n_partials; k += 8 * 64) {  // 8 x 16-B loads in flight, added in k order
+            double2 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const double2 *>(partials + 2 * (k + 64 * u));
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s += v[u].x;
+                q += v[u].y;
+            }
+        }
+        for (; k < n_partials; k += 64) {
             s += partials[2 * k];
             q += partials[2 * k + 1];
         }

@@ -27,7 +27,15 @@ __device__ inline void xpa_loss_finalize_body(const XpaLossFinalizeArgs &a, doub
     if (threadIdx.x < 256) {
         for (int j = w; j < ncols; j += 4) {  // one wave per column, fixed lane order -> deterministic
             double s = 0.0;
-            for (int64_t k = lane; k < a.n_partials; k += 64) s += (double)a.partials[k * a.width + j];
+            int64_t k = lane;
+            for (; k + 7 * 64 < a.n_partials; k += 8 * 64) {  // 8 loads in flight, added in k order
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = a.partials[(k + 64 * u) * a.width + j];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) s += (double)v[u];
+            }
+            for (; k < a.n_partials; k += 64) s += (double)a.partials[k * a.width + j];
             s = xpa_wave_sum(s);
             if (lane == 0) {
                 if (j < kXpaLossPartBase) s_tot[j] = s;

@@ -251,6 +251,13 @@ __device__ __forceinline__ void colsum_tile(const float *__restrict__ part, int6
     double s = 0.0;
     if (c < C) {
         int64_t k = grp;
+        for (; k + 15 * kColGroups < G; k += 16 * kColGroups) {  // 16 independent loads in flight (G = 512: 2 rounds)
+            float a[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) a[u] = part[(k + u * kColGroups) * C + c];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) s += (double)a[u];
+        }
         for (; k + 3 * kColGroups < G; k += 4 * kColGroups) {  // 4 independent loads in flight
             const float a0 = part[k * C + c], a1 = part[(k + kColGroups) * C + c];
             const float a2 = part[(k + 2 * kColGroups) * C + c], a3 = part[(k + 3 * kColGroups) * C + c];
@@ -327,7 +334,15 @@ __device__ __forceinline__ void colsum_batch_tile(const ColsumBatch &b, int tile
         double acc = 0.0;
         float o = 0.f;
         if (c < C) {
-            for (int64_t k = 0; k < G; ++k) acc += (double)part[k * C + c];
+            int64_t k = 0;
+            for (; k + 8 <= G; k += 8) {  // 8 loads in flight, added in row order
+                float a[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) a[u] = part[(k + u) * C + c];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc += (double)a[u];
+            }
+            for (; k < G; ++k) acc += (double)part[k * C + c];
             o = (float)acc;
             b.out[sg][c] = o;
         }
