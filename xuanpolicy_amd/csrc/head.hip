@@ -138,6 +138,7 @@ __device__ __forceinline__ void load_tile(float4 (&zq)[16], const float *__restr
 
 // ---- shared epilogue: everything after h = act(z) of a 64-row tile is in LDS ----------------------
 // MODE: 0 Gaussian actor, 1 Categorical actor, 2 critic.  ALGO: 0 PPO, 1 A2C (actor only).
+typedef float f2v __attribute__((ext_vector_type(2)));
 template <int KMAX>
 struct RowIn {  // wave 0, lane = row of the tile
     bool valid;
@@ -151,7 +152,12 @@ struct HeadEpi {
     // phase-1 partials per pass: heads wider than 8 (C4's 17 / 18) go through s_part in two halves, so the K16 block
     // fits 80 KiB of LDS (2 blocks per CU; 90 KiB with all 18 at once)
     static constexpr int PH = KMAX > 8 ? (KMAX + 1) / 2 : KMAX;
-    float wc[KMAX], acc_dw[KMAX], acc_dbh;      // phase 2 (column t)
+    // phase 2 (column t); dW_out accumulated in output pairs (v_pk_fma_f32: the same fused multiply-add per output,
+    // half the VALU issues)
+    static constexpr bool kPk = KMAX <= 8;  // the wide heads (C4) keep scalar accumulators (packed pairs spill there)
+    static constexpr int KH2 = (KMAX + 1) / 2;
+    float wc[KMAX], acc_dw[kPk ? 1 : KMAX], acc_dbh;
+    f2v acc_dw2[kPk ? KH2 : 1];
     float acc_dbo[KMAX], acc_dls[KMAX], var_[KMAX], logsc[KMAX];
     float sum0, sum1, sum2, ent_const, inv_b, lo, hi, a_mean, a_inv, slope;
     int K;
@@ -172,10 +178,16 @@ struct HeadEpi {
 #pragma unroll
         for (int o = 0; o < KMAX; ++o) {
             wc[o] = o < K ? W[o * kH + t] : 0.f;
-            acc_dw[o] = 0.f;
             acc_dbo[o] = acc_dls[o] = 0.f;
             var_[o] = 1.f;
             logsc[o] = 0.f;
+        }
+        if constexpr (kPk) {
+#pragma unroll
+            for (int o2 = 0; o2 < KH2; ++o2) acc_dw2[o2] = f2v{0.f, 0.f};
+        } else {
+#pragma unroll
+            for (int o = 0; o < KMAX; ++o) acc_dw[o] = 0.f;
         }
         acc_dbh = 0.f;
         sum0 = sum1 = sum2 = ent_const = 0.f;
@@ -405,10 +417,19 @@ struct HeadEpi {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 float d = 0.f;
+                if constexpr (kPk) {
 #pragma unroll
-                for (int o = 0; o < KMAX; ++o) {  // o >= K: s_dh and wc are 0 (accumulator unused)
-                    d += gq[u][o] * wc[o];
-                    acc_dw[o] += gq[u][o] * hv[u];
+                    for (int o = 0; o < KMAX; ++o) d += gq[u][o] * wc[o];  // o >= K: s_dh and wc are 0
+                    const f2v hh = {hv[u], hv[u]};
+#pragma unroll
+                    for (int o2 = 0; o2 < KH2; ++o2)  // KP >= 2 KH2: the pad slots of s_dh are 0
+                        acc_dw2[o2] = __builtin_elementwise_fma(f2v{gq[u][2 * o2], gq[u][2 * o2 + 1]}, hh, acc_dw2[o2]);
+                } else {
+#pragma unroll
+                    for (int o = 0; o < KMAX; ++o) {
+                        d += gq[u][o] * wc[o];
+                        acc_dw[o] += gq[u][o] * hv[u];
+                    }
                 }
                 d *= act_g<ACT>(hv[u], slope);
 #if XPA_HEAD_PROBE != 4  // 4 = epilogue alone without the dz stores
@@ -420,11 +441,20 @@ struct HeadEpi {
         for (; r < nr; ++r) {
             const float h = s_h[r * kS + t];
             float d = 0.f;
+            if constexpr (kPk) {
 #pragma unroll
-            for (int o = 0; o < KMAX; ++o) {
-                const float g = s_dh[r][o];
-                d += g * wc[o];
-                acc_dw[o] += g * h;
+                for (int o = 0; o < KMAX; ++o) d += s_dh[r][o] * wc[o];
+                const f2v hh = {h, h};
+#pragma unroll
+                for (int o2 = 0; o2 < KH2; ++o2)
+                    acc_dw2[o2] = __builtin_elementwise_fma(f2v{s_dh[r][2 * o2], s_dh[r][2 * o2 + 1]}, hh, acc_dw2[o2]);
+            } else {
+#pragma unroll
+                for (int o = 0; o < KMAX; ++o) {
+                    const float g = s_dh[r][o];
+                    d += g * wc[o];
+                    acc_dw[o] += g * h;
+                }
             }
             d *= act_g<ACT>(h, slope);
 #if XPA_HEAD_PROBE != 4
@@ -441,7 +471,7 @@ struct HeadEpi {
         const int64_t blk = blockIdx.x;
 #pragma unroll
         for (int o = 0; o < KMAX; ++o)
-            if (o < K) p_dw[(blk * K + o) * kH + t] = acc_dw[o];
+            if (o < K) p_dw[(blk * K + o) * kH + t] = kPk ? acc_dw2[o >> 1][o & 1] : acc_dw[kPk ? 0 : o];
         p_dbh[blk * kH + t] = acc_dbh;
         if (wave == 0) {
             sum0 = xpa_wave_sum(sum0);
