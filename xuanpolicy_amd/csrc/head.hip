@@ -396,6 +396,9 @@ struct HeadEpi {
         const int nr = (int)min((int64_t)kTile, batch - tile * kTile);
 #endif
         float *dzt = dz + tile * kTile * ld + t;
+        f2v wc2[KH2];
+#pragma unroll
+        for (int o2 = 0; o2 < KH2; ++o2) wc2[o2] = f2v{wc[2 * o2], 2 * o2 + 1 < KMAX ? wc[2 * o2 + 1] : 0.f};
         // rows in groups of 4: every LDS read of the group (h, and the d-head rows as 16-B broadcasts)
         // issued before the arithmetic, which keeps the row order of the accumulations (bitwise the
         // same sums as one row at a time)
@@ -418,8 +421,13 @@ struct HeadEpi {
             for (int u = 0; u < 4; ++u) {
                 float d = 0.f;
                 if constexpr (kPk) {
+                    // d head . w over the even and the odd outputs as one packed chain, then their sum (o >= K:
+                    // s_dh and wc are 0)
+                    f2v d2 = {0.f, 0.f};
 #pragma unroll
-                    for (int o = 0; o < KMAX; ++o) d += gq[u][o] * wc[o];  // o >= K: s_dh and wc are 0
+                    for (int o2 = 0; o2 < KH2; ++o2)
+                        d2 = __builtin_elementwise_fma(f2v{gq[u][2 * o2], gq[u][2 * o2 + 1]}, wc2[o2], d2);
+                    d = d2.x + d2.y;
                     const f2v hh = {hv[u], hv[u]};
 #pragma unroll
                     for (int o2 = 0; o2 < KH2; ++o2)  // KP >= 2 KH2: the pad slots of s_dh are 0
@@ -442,8 +450,11 @@ struct HeadEpi {
             const float h = s_h[r * kS + t];
             float d = 0.f;
             if constexpr (kPk) {
+                f2v d2 = {0.f, 0.f};
 #pragma unroll
-                for (int o = 0; o < KMAX; ++o) d += s_dh[r][o] * wc[o];
+                for (int o2 = 0; o2 < KH2; ++o2)
+                    d2 = __builtin_elementwise_fma(f2v{s_dh[r][2 * o2], s_dh[r][2 * o2 + 1]}, wc2[o2], d2);
+                d = d2.x + d2.y;
                 const f2v hh = {h, h};
 #pragma unroll
                 for (int o2 = 0; o2 < KH2; ++o2)
