@@ -212,6 +212,9 @@ __global__ __launch_bounds__(kLossThreads) void policy_loss_kernel(
             for (int k = 0; k < A; ++k) se += expf(z[k] - m);
             lse = m + logf(se);
             ai = (int)act[row];
+            // Deliberate divergence: torch's Categorical.log_prob raises on an action outside [0, A); the kernel
+            // clamps it (a bounded read instead of a fault). The device rollout only writes in-range actions, and
+            // the drop-in learner validates host-supplied categorical actions before the launch (learners.py).
             ai = ai < 0 ? 0 : (ai >= A ? A - 1 : ai);
             logp = z[ai] - lse;
             for (int k = 0; k < A; ++k) {

@@ -215,6 +215,18 @@ class _FusedPolicyGradient(Learner):
     def _device(self):
         return next(self.policy.parameters()).device
 
+    def _check_actions(self, act_batch):
+        """Categorical.log_prob validates its argument and raises on an action outside [0, n) (the loss kernel
+        clamps instead, loss.hip): host-supplied batches are checked here, before the upload.  Device tensors come
+        from the device rollout, which only writes in-range actions, and are not synced for the check."""
+        if self.dist != "categorical" or (isinstance(act_batch, torch.Tensor) and act_batch.is_cuda):
+            return
+        import numpy as np
+        a = act_batch.numpy() if isinstance(act_batch, torch.Tensor) else np.asarray(act_batch)
+        n = int(getattr(self.policy, "action_dim", 0) or 0)
+        if a.size and (not np.all(np.isfinite(a)) or a.min() < 0 or (n and a.max() >= n) or np.any(a != np.floor(a))):
+            raise ValueError(f"categorical actions must be integers in [0, {n}); got range [{a.min()}, {a.max()}]")
+
 
 class PPOCLIP_Learner(_FusedPolicyGradient):
     """ppoclip_learner.py:4-65."""
@@ -228,6 +240,7 @@ class PPOCLIP_Learner(_FusedPolicyGradient):
 
     def update(self, obs_batch, act_batch, ret_batch, value_batch, adv_batch, old_logp):
         dev = self._device()
+        self._check_actions(act_batch)
         scalars = self.update_fused(self._obs(obs_batch, dev), None, self._t(act_batch, dev).reshape(-1),
                                     self._t(adv_batch, dev), self._t(ret_batch, dev), self._t(old_logp, dev))
         return self._info(scalars)
@@ -246,6 +259,7 @@ class A2C_Learner(_FusedPolicyGradient):
 
     def update(self, obs_batch, act_batch, ret_batch, adv_batch):
         dev = self._device()
+        self._check_actions(act_batch)
         scalars = self.update_fused(self._obs(obs_batch, dev), None, self._t(act_batch, dev).reshape(-1),
                                     self._t(adv_batch, dev), self._t(ret_batch, dev))
         return self._info(scalars)
