@@ -64,3 +64,22 @@ def test_ppo_cartpole_iteration_matches_oracle():
     agent.train(T, log=False)
     agent.train(T - 1, log=False)
     replay_last_step_iteration(agent, 4, 2, [H], True, "ppo", agent.config.ent_coef, n_epoch, n_mb)
+
+
+def test_graphed_updates_match_eager():
+    """learners._graphed_mlp_update: the per-slot hipGraph replays give the eager update's parameters (two iterations,
+    8 epochs x 8 slots: warm-up, capture + replay, and replays)."""
+    from xuanpolicy_amd.runner import build_cartpole_ppo
+    out = []
+    for graphed in (False, True):
+        agent = build_cartpole_ppo(n_envs=8, n_steps=128, hidden=64, seed=4, device=DEV, graph_update=graphed)
+        for _ in range(2):
+            agent.train(128, log=False)
+        torch.cuda.synchronize()
+        graphs = getattr(agent.learner, "_slot_graphs", {})
+        n_graphs = sum(isinstance(v, tuple) for v in graphs.values())
+        assert (n_graphs == 8) if graphed else (n_graphs == 0), n_graphs
+        assert not getattr(agent.learner, "_graph_failed", False)
+        out.append([p.detach().cpu().numpy().copy() for p in agent.policy.parameters()])
+    for a, b in zip(*out):
+        np.testing.assert_allclose(b, a, rtol=1e-6, atol=1e-7)

@@ -184,6 +184,9 @@ class _OnPolicyAgent:
                 from .runner import enable_tuned_gemms
                 enable_tuned_gemms()
             self.learner.enable_fast_path(fused_optimizer=bool(_cfg(config, "fused_adam", True)))
+            # small minibatches: one hipGraph per minibatch slot (learners._graphed_mlp_update); the agent loop's
+            # inputs are persistent buffers, which the graphs need (the drop-in learner.update path keeps it off)
+            self.learner.graph_updates = bool(_cfg(config, "graph_update", True))
 
     def _make_learner(self, config, policy, optimizer, scheduler):
         raise NotImplementedError

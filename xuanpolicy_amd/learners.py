@@ -160,18 +160,12 @@ class _FusedPolicyGradient(Learner):
             fc.backward(ctx, dh, dv)       # writes every parameter gradient
             self._sync_clip_step()
             return scalars
-        if fm is not None:
-            head, logstd, v, ctx = fm.forward(obs)
-            if self._ws is None or self._ws.batch != head.shape[0]:
-                self._ws = ops.LossWorkspace(head.shape[0], head.shape[1], head.device, self.dist)
-            scalars, dh, _, dv = ops.policy_loss(self.algo, self.dist, head, logstd, v, act, adv, ret,
-                                                 old_logp=old_logp, idx=idx, adv_partials=adv_partials,
-                                                 clip_range=self.clip_range, vf_coef=self.vf_coef,
-                                                 ent_coef=self.ent_coef, ws=self._ws,
-                                                 d_logstd_out=logstd.grad if logstd is not None else None)
-            fm.backward(ctx, dh, dv)       # writes every parameter gradient into the flat buffer
+        if fm is not None and self._graph_ok(obs):
+            scalars = self._graphed_mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials)
             self._sync_clip_step()
             return scalars
+        if fm is not None:
+            return self._mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, step=True)
         head, logstd, v = policy_heads(self.policy, obs)
         if self._ws is None or self._ws.batch != head.shape[0]:
             self._ws = ops.LossWorkspace(head.shape[0], head.shape[1], head.device, self.dist)
@@ -180,6 +174,58 @@ class _FusedPolicyGradient(Learner):
                                                clip_range=self.clip_range, vf_coef=self.vf_coef,
                                                ent_coef=self.ent_coef, ws=self._ws)
         self._backward_and_step(head, logstd, v, dh, dls, dv)
+        return scalars
+
+    # Small minibatches (C1: 128 rows of a [64] net) are bound by host dispatch, ~20 launches of a few us each at
+    # ~15-20 us of host time apiece (profiles/r02f_c1_host_probe.txt).  The explicit forward + loss + backward of one
+    # minibatch slot is therefore captured once into a hipGraph and replayed.  Every input is a fixed buffer: the rollout
+    # columns, the persistent epoch permutation (idx is a slice of it) and the gathered obs rows.  The parameters are
+    # updated in place by K9.  K9 itself runs outside the graph, because lr and the Adam step count are kernel arguments
+    # that change every update.  Slot graphs are keyed by those pointers.  A slot's first update runs eagerly and warms
+    # up workspaces and BLAS handles; the second captures; later ones replay.
+    graph_max_rows = 8192
+
+    def _graph_ok(self, obs):
+        return (getattr(self, "graph_updates", False) and self.grad_sync is None and isinstance(obs, torch.Tensor)
+                and obs.is_cuda and obs.shape[0] <= self.graph_max_rows and not getattr(self, "_graph_failed", False))
+
+    def _graphed_mlp_update(self, fm, obs, idx, act, adv, ret, old_logp, adv_partials):
+        ptr = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+        key = (ptr(obs), tuple(obs.shape), ptr(idx), -1 if idx is None else idx.shape[0], ptr(act), ptr(adv), ptr(ret),
+               ptr(old_logp), ptr(adv_partials)) + tuple(p.data_ptr() for p in self._params)
+        graphs = self.__dict__.setdefault("_slot_graphs", {})
+        ent = graphs.get(key)
+        if ent is None:                     # first use of this slot: eager (warm-up)
+            graphs[key] = "warm"
+            return self._mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, step=False)
+        if ent == "warm":
+            if self.__dict__.get("_graph_pool") is None:
+                self._graph_pool = torch.cuda.graph_pool_handle()
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g, pool=self._graph_pool):
+                    out = self._mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, step=False)
+            except Exception:               # a launch that cannot be captured: stay eager from here on
+                self._graph_failed = True
+                torch.cuda.synchronize()
+                return self._mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, step=False)
+            graphs[key] = ent = (g, out, self._ws)   # the graph writes into this workspace: keep it alive
+        ent[0].replay()
+        return ent[1]
+
+    def _mlp_update(self, fm, obs, idx, act, adv, ret, old_logp, adv_partials, step):
+        """Explicit forward (fused_mlp) + K2 loss + explicit backward into the flat gradient (+ K9 when step)."""
+        head, logstd, v, ctx = fm.forward(obs)
+        if self._ws is None or self._ws.batch != head.shape[0]:
+            self._ws = ops.LossWorkspace(head.shape[0], head.shape[1], head.device, self.dist)
+        scalars, dh, _, dv = ops.policy_loss(self.algo, self.dist, head, logstd, v, act, adv, ret,
+                                             old_logp=old_logp, idx=idx, adv_partials=adv_partials,
+                                             clip_range=self.clip_range, vf_coef=self.vf_coef,
+                                             ent_coef=self.ent_coef, ws=self._ws,
+                                             d_logstd_out=logstd.grad if logstd is not None else None)
+        fm.backward(ctx, dh, dv)       # writes every parameter gradient into the flat buffer
+        if step:
+            self._sync_clip_step()
         return scalars
 
     def enable_fast_path(self, fused_optimizer=True):
