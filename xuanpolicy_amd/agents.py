@@ -518,10 +518,18 @@ class _OnPolicyAgent:
                                               device=self.device)
                     self.adv_part = torch.empty((ops.gather_num_partials(b), 2), dtype=torch.float64,
                                                 device=self.device)
-                obs_mb, part = ops.gather_minibatch(idx, obs_flat, adv=adv_flat if use_advnorm else None,
-                                                    obs_out=self.obs_mb,
-                                                    adv_partials=self.adv_part if use_advnorm else None)
-                if self.global_advnorm and part is not None:
+                def gather(idx=idx):
+                    return ops.gather_minibatch(idx, obs_flat, adv=adv_flat if use_advnorm else None,
+                                                obs_out=self.obs_mb, adv_partials=self.adv_part if use_advnorm else None)
+                if not self.global_advnorm:
+                    # the gather rides in the learner's slot graph when the update is graphed (writes obs_mb / adv_part)
+                    scalars = self.learner.update_fused(self.obs_mb, idx, act_flat, adv_flat, ret_flat, logp_flat,
+                                                        self.adv_part if use_advnorm else None, pre=gather)
+                    if self.update_log is not None:
+                        self.update_log.append(scalars.clone())
+                    continue
+                obs_mb, part = gather()
+                if part is not None:
                     import torch.distributed as tdist
                     tdist.all_reduce(part, op=tdist.ReduceOp.SUM)   # (sum, sumsq) over all ranks' minibatches,
                     part.div_(self.world)                           # averaged: mean / var of the global minibatch

@@ -125,10 +125,16 @@ class _FusedPolicyGradient(Learner):
         if self.scheduler is not None:
             self.scheduler.step()
 
-    def update_fused(self, obs, idx, act, adv, ret, old_logp=None, adv_partials=None):
+    def update_fused(self, obs, idx, act, adv, ret, old_logp=None, adv_partials=None, pre=None):
         """One minibatch update reading act/adv/ret/old_logp from the flattened rollout buffer at idx
-        (idx=None: already gathered).  Returns the device tensor of loss scalars (ops.OUT_KEYS)."""
+        (idx=None: already gathered).  pre: launches that produce obs / adv_partials (the agent's minibatch gather),
+        run first — inside the slot graph when the update is graphed.  Returns the device tensor of loss scalars
+        (ops.OUT_KEYS)."""
         self.iterations += 1
+        if pre is not None and not (self._fused_mlp() is not None and not self._fused_mlp().fused_heads
+                                    and self._graph_ok(obs)):
+            pre()
+            pre = None
         fm = self._fused_mlp()
         if fm is not None and fm.fused_heads:
             fm.early_grad_sync = getattr(self.grad_sync, "begin", None) if self.grad_sync is not None else None
@@ -161,7 +167,7 @@ class _FusedPolicyGradient(Learner):
             self._sync_clip_step()
             return scalars
         if fm is not None and self._graph_ok(obs):
-            scalars = self._graphed_mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials)
+            scalars = self._graphed_mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, pre)
             self._sync_clip_step()
             return scalars
         if fm is not None:
@@ -189,7 +195,7 @@ class _FusedPolicyGradient(Learner):
         return (getattr(self, "graph_updates", False) and self.grad_sync is None and isinstance(obs, torch.Tensor)
                 and obs.is_cuda and obs.shape[0] <= self.graph_max_rows and not getattr(self, "_graph_failed", False))
 
-    def _graphed_mlp_update(self, fm, obs, idx, act, adv, ret, old_logp, adv_partials):
+    def _graphed_mlp_update(self, fm, obs, idx, act, adv, ret, old_logp, adv_partials, pre=None):
         ptr = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
         key = (ptr(obs), tuple(obs.shape), ptr(idx), -1 if idx is None else idx.shape[0], ptr(act), ptr(adv), ptr(ret),
                ptr(old_logp), ptr(adv_partials)) + tuple(p.data_ptr() for p in self._params)
@@ -197,6 +203,8 @@ class _FusedPolicyGradient(Learner):
         ent = graphs.get(key)
         if ent is None:                     # first use of this slot: eager (warm-up)
             graphs[key] = "warm"
+            if pre is not None:
+                pre()
             return self._mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, step=False)
         if ent == "warm":
             if self.__dict__.get("_graph_pool") is None:
@@ -204,10 +212,14 @@ class _FusedPolicyGradient(Learner):
             g = torch.cuda.CUDAGraph()
             try:
                 with torch.cuda.graph(g, pool=self._graph_pool):
+                    if pre is not None:
+                        pre()
                     out = self._mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, step=False)
             except Exception:               # a launch that cannot be captured: stay eager from here on
                 self._graph_failed = True
                 torch.cuda.synchronize()
+                if pre is not None:
+                    pre()
                 return self._mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, step=False)
             graphs[key] = ent = (g, out, self._ws)   # the graph writes into this workspace: keep it alive
         ent[0].replay()
