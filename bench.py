@@ -306,11 +306,13 @@ def per_bench(device, n_envs=8, n_size=131072, batch=2048, frames=True, reps=50)
     return res
 
 
-def c1_bench(device, n_envs=8, n_steps=128, hidden=64, steps=5, warmup=1, cpu=True):
+def c1_bench(device, n_envs=8, n_steps=128, hidden=64, steps=5, warmup=3, cpu=True):
     """C1 (BASELINE.json configs[0]): PPO-Clip on CartPole-v1, 8 envs x 128 steps, ppo/classic_control/
     CartPole-v1.yaml (8 epochs x 8 minibatches of 128), [64] nets, on device (K18 env, K3 sampling, K1 GAE,
     K2 / K9 updates) — and the same loop on the host as the reference runs it (oracle/cpu_ref.AgentLoopRef over
-    per-env CartPoleEnv objects, torch-CPU learner): the reference's own CPU-runnable configuration."""
+    per-env CartPoleEnv objects, torch-CPU learner): the reference's own CPU-runnable configuration.  Three untimed
+    iterations first: the rollout chunk graph and the per-slot update graphs are captured there, not in the timed
+    region."""
     import numpy as np
     import torch
     from xuanpolicy_amd.runner import build_cartpole_ppo
