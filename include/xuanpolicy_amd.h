@@ -26,7 +26,11 @@ extern "C" {
 
 typedef struct ihipStream_t *xpa_stream_t; /* == hipStream_t */
 
-#define XPA_ABI_VERSION 1
+/* ABI 2 (round 3): n_slots added to xpa_rollout_post_deferred[_norm] / xpa_rollout_bootstrap_fixup; the error
+ * word `err` added to xpa_per_sample / xpa_gather_minibatch / xpa_synthatari_step / xpa_maxpool_act_bwd_bias; max_norm of
+ * xpa_clip_adam_step[_partials]: < 0 disables clipping, 0 zeroes the gradient (ABI 1 callers passing 0 to mean "no
+ * clipping" must pass -1). */
+#define XPA_ABI_VERSION 2
 
 /* Device-resident rollout cursor read by the per-step kernels, so a captured step replays
  * without host-side arguments changing: ptr = buffer column being written (DummyOnPolicyBuffer.ptr,
@@ -113,11 +117,11 @@ int xpa_stream_copy_timed(const float *r, const float *v, const float *d, float 
  * obs_out[b] = obs[idx[b]] (row_bytes each); adv_partials[g] = (sum, sum of squares) in f64 over
  * rows [g*64, (g+1)*64); xpa_gather_num_partials(batch) rows.  adv/adv_partials may be NULL.
  * n_rows = rows of obs/adv: an index outside [0, n_rows) is never dereferenced (its output row is
- * zeroed and it adds nothing to the moments). */
+ * zeroed, it adds nothing to the moments and, when err != NULL, it is counted in *err). */
 int64_t xpa_gather_num_partials(int64_t batch);
 int xpa_gather_minibatch(const int64_t *idx, int64_t batch, int64_t n_rows, const void *obs,
                          int64_t obs_row_bytes, void *obs_out, const float *adv, double *adv_partials,
-                         xpa_stream_t stream);
+                         int32_t *err, xpa_stream_t stream);
 
 /* K2 — fused policy/value loss forward + backward for one minibatch.
  * Replaces PPOCLIP_Learner.update's loss (xuance/torch/learners/policy_gradient/ppoclip_learner.py:32-44)
@@ -405,7 +409,9 @@ int xpa_head_gemm_critic(int act, int64_t batch, int64_t hidden, const float *x,
  *   `uniforms` (f64 [n_envs*batch_per_env], e.g. the reference's recorded random.random() draws) or, if
  *   NULL, a counter hash of (seed, counter, env, k).  steps = index (wrap_uint8 != 0: index & 255, the
  *   reference's astype(np.uint8)), flat_index (optional) = env * n_size + step for
- *   xpa_gather_minibatch.  size >= 2 (the reference recurses forever at size 1). */
+ *   xpa_gather_minibatch.  size >= 2 (the reference recurses forever at size 1).  A descent that lands past the
+ *   stored leaves (mass rounded to >= the stored total) is clamped to step size - 1 and counted in *err (if not
+ *   NULL): the reference would fail its update_priorities assert on it. */
 int xpa_per_store(double *sum_tree, double *min_tree, const double *max_priority, int64_t n_envs,
                   int64_t capacity, int64_t ptr, double alpha, xpa_stream_t stream);
 int xpa_per_update_priorities(double *sum_tree, double *min_tree, double *max_priority, int *scratch,
@@ -414,7 +420,7 @@ int xpa_per_update_priorities(double *sum_tree, double *min_tree, double *max_pr
                               xpa_stream_t stream);
 int xpa_per_sample(const double *sum_tree, const double *min_tree, int64_t n_envs, int64_t capacity, int64_t size,
                    int64_t batch_per_env, int64_t n_size, const double *uniforms, uint32_t seed, uint32_t counter,
-                   double beta, int wrap_uint8, int64_t *steps, int64_t *flat_index, double *weights,
+                   double beta, int wrap_uint8, int64_t *steps, int64_t *flat_index, double *weights, int32_t *err,
                    xpa_stream_t stream);
 
 /* Column store of raw observation rows into the rollout buffer at the device cursor:
@@ -431,29 +437,33 @@ int xpa_store_column(const void *src, int64_t n, int64_t row_bytes, void *dst, i
  * sampler.  Writes the stepped stack to final_obs, reward sign, terminated (life lost or game over),
  * truncated (game over or step limit); on game over the env resets (stack = 4 copies of the new
  * episode's first frame).  Per-env int32 state: ep_step, ep_index, lives, paddle; f32 scores.
+ * An act_in row with no entry > 0.5 steps action 0 and counts in *err (if not NULL).
  * xpa_synthatari_reset: stack = the first frame of episode ep_index[n], 4 times. */
 int xpa_synthatari_step(int64_t n_envs, int64_t n_actions, const float *act_in, int64_t ld_act, uint32_t seed,
                         int32_t max_episode_steps, uint8_t *stack, uint8_t *final_obs, float *rew, uint8_t *term,
                         uint8_t *trunc, int32_t *ep_step, int32_t *ep_index, int32_t *lives, int32_t *paddle,
-                        float *ep_score, float *ep_last_score, int32_t *ep_last_len, xpa_stream_t stream);
+                        float *ep_score, float *ep_last_score, int32_t *ep_last_len, int32_t *err,
+                        xpa_stream_t stream);
 int xpa_synthatari_reset(int64_t n_envs, uint32_t seed, uint8_t *stack, const int32_t *ep_index,
                          xpa_stream_t stream);
 
-/* K8 with deferred bootstrap values (valid when an env truncates at most once per rollout, i.e.
- * max_episode_steps >= horizon): instead of v_boot, a mid-buffer truncation of env n (a path closed
- * with a bootstrap, ppoclip_agent.py:95-100) stores its normalised final-observation row
- * boot_obs[n] (row stride ld_boot, obs_dim floats) into slot_obs[n] and sets slot_t[n] = t (slot_t
- * starts at -1; a second truncation in the same rollout counts in *overflow).  After the last step,
- * values = V([slot_obs; boot_obs]) ([2 n_envs]: the truncation slots, then the last step's final
- * observations, ppoclip_agent.py:69-75) and xpa_rollout_bootstrap_fixup writes buf_boot at every
- * recorded truncation and at the last column (0 where terminal), resetting slot_t to -1. */
+/* K8 with deferred bootstrap values: instead of v_boot, a mid-buffer truncation of env n (a path closed
+ * with a bootstrap, ppoclip_agent.py:95-100) stores its normalised final-observation row boot_obs[n]
+ * (row stride ld_boot, obs_dim floats) in the env's first free slot k < n_slots: slot_obs[k n_envs + n]
+ * ([n_slots n_envs, obs_dim]) and slot_t[k n_envs + n] = t (slot_t [n_slots, n_envs] starts at -1).  A
+ * truncation finding every slot taken counts in *overflow (and reuses the last slot).  The caller sizes n_slots
+ * so that this cannot happen: an env whose only truncation source is a time limit of L steps truncates at most
+ * ceil((horizon - 1) / L) times before the last step of a rollout.  After the last step,
+ * values = V([slot_obs; boot_obs]) ([(n_slots + 1) n_envs]: the truncation slots, then the last step's final
+ * observations, ppoclip_agent.py:69-75) and xpa_rollout_bootstrap_fixup writes buf_boot at every recorded
+ * truncation and at the last column (0 where terminal), resetting slot_t to -1. */
 int xpa_rollout_post_deferred(int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term,
                               const uint8_t *trunc, const float *boot_obs, int64_t ld_boot, int64_t obs_dim,
-                              float *slot_obs, int32_t *slot_t, int32_t *overflow, xpa_cursor_t *cursor,
-                              float *ret_mean, float *ret_var, double *ret_count, float *returns, float *buf_rew,
-                              float *buf_term, uint8_t *buf_closed, float *buf_boot, float gamma, int mask_returns,
-                              int use_rewnorm, float rew_range, int atari_lifeloss, double *partials,
-                              uint32_t *ticket, xpa_stream_t stream);
+                              float *slot_obs, int32_t *slot_t, int64_t n_slots, int32_t *overflow,
+                              xpa_cursor_t *cursor, float *ret_mean, float *ret_var, double *ret_count,
+                              float *returns, float *buf_rew, float *buf_term, uint8_t *buf_closed, float *buf_boot,
+                              float gamma, int mask_returns, int use_rewnorm, float rew_range, int atari_lifeloss,
+                              double *partials, uint32_t *ticket, xpa_stream_t stream);
 /* xpa_rollout_post_deferred with the normalisation of the final observations folded in: final_obs holds
  * the RAW observations; a kept truncation row is normalised with obs_mean / obs_var (clip obs_clip,
  * xpa_obs_normalize's arithmetic) into slot_obs, and at the rollout's last step every env's normalised
@@ -461,13 +471,14 @@ int xpa_rollout_post_deferred(int64_t n_envs, int64_t horizon, const float *rew,
 int xpa_rollout_post_deferred_norm(int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term,
                                    const uint8_t *trunc, const float *final_obs, int64_t ld_final, int64_t obs_dim,
                                    const float *obs_mean, const float *obs_var, float obs_clip, float *boot_norm,
-                                   int64_t ld_norm, float *slot_obs, int32_t *slot_t, int32_t *overflow,
-                                   xpa_cursor_t *cursor, float *ret_mean, float *ret_var, double *ret_count,
-                                   float *returns, float *buf_rew, float *buf_term, uint8_t *buf_closed,
-                                   float *buf_boot, float gamma, int mask_returns, int use_rewnorm, float rew_range,
-                                   int atari_lifeloss, double *partials, uint32_t *ticket, xpa_stream_t stream);
+                                   int64_t ld_norm, float *slot_obs, int32_t *slot_t, int64_t n_slots,
+                                   int32_t *overflow, xpa_cursor_t *cursor, float *ret_mean, float *ret_var,
+                                   double *ret_count, float *returns, float *buf_rew, float *buf_term,
+                                   uint8_t *buf_closed, float *buf_boot, float gamma, int mask_returns, int use_rewnorm,
+                                   float rew_range, int atari_lifeloss, double *partials, uint32_t *ticket,
+                                   xpa_stream_t stream);
 int xpa_rollout_bootstrap_fixup(int64_t n_envs, int64_t horizon, const float *values, int32_t *slot_t,
-                                const float *buf_term, float *buf_boot, xpa_stream_t stream);
+                                int64_t n_slots, const float *buf_term, float *buf_boot, xpa_stream_t stream);
 
 /* K13 — first representation layer Linear(d_in, 256) + activation for a small d_in (<= 64): Basic_MLP's
  * first mlp_block (xuance/torch/representations/mlp.py:21-51, utils/layers.py:8-24) as HBM-streaming
@@ -559,9 +570,10 @@ int xpa_global_maxpool(const float *x, int64_t batch, int64_t hw, int64_t channe
                        xpa_stream_t stream);
 /* K24: the backward of K23 and of the activation before it, with the conv bias gradient: dz[b, p, c] =
  * (p == argmax[b, c] ? dout[b, c] : 0) * act'(h[b, p, c]) over [batch * hw, channels], and the column-sum partials
- * of dz as xpa_act_bwd_bias (xpa_act_bwd_bias_num_partials(batch * hw, channels) rows). */
+ * of dz as xpa_act_bwd_bias (xpa_act_bwd_bias_num_partials(batch * hw, channels) rows).  An argmax outside
+ * [0, hw) routes nothing and counts in *err (if not NULL). */
 int xpa_maxpool_act_bwd_bias(int act, const float *dout, const int32_t *argmax, const float *h, int64_t batch,
-                             int64_t hw, int64_t channels, float slope, float *dz, float *partials,
+                             int64_t hw, int64_t channels, float slope, float *dz, float *partials, int32_t *err,
                              xpa_stream_t stream);
 
 #ifdef __cplusplus

@@ -65,8 +65,13 @@ def replay_last_step_iteration(agent, D, A, hidden, discrete, algo, ent, n_epoch
     rows, cols = np.nonzero(mid)
     if expect_mid_truncations:
         assert len(rows) > 0, "the case must exercise mid-buffer truncation bootstraps"
-    assert len(np.unique(rows)) == len(rows)   # at most one per rollout (deferred path)
-    np.testing.assert_allclose(boot[rows, cols], v_slot[rows], rtol=1e-4, atol=1e-4)
+    # the k-th mid-buffer truncation of env n (in time order) was kept in slot k (row k N + n of slot_obs)
+    S = agent.n_slots
+    k_of = np.zeros(len(rows), np.int64)
+    for j in range(len(rows)):
+        k_of[j] = int(np.sum(mid[rows[j], :cols[j]]))
+    assert (k_of < S).all(), "more mid-buffer truncations than deferred slots"
+    np.testing.assert_allclose(boot[rows, cols], v_slot[k_of * N + rows], rtol=1e-4, atol=1e-4)
 
     # ---- GAE (north_star: 1e-5 on advantages / returns) ----
     adv, ret = cpu_ref.gae_rows(mem.rewards.cpu().numpy(), mem.values.cpu().numpy(), term, closed.astype(np.uint8),

@@ -54,7 +54,7 @@ def test_invalid_arguments_rejected_before_launch(lib):
                                        None, None, None, None) == 1
     assert lib.xpa_policy_loss_fwd_bwd(0, 1, 8, 1, *([None] * 4), 8, *([None] * 5), 0, 0.2, 0.25, 0.0,
                                        None, None, None, None) == 1
-    assert lib.xpa_gather_minibatch(None, 8, 8, None, 4, None, None, None, None) == 1
+    assert lib.xpa_gather_minibatch(None, 8, 8, None, 4, None, None, None, None, None) == 1
     assert lib.xpa_rms_merge(None, 3, 100, 4, None, None, None, None) == 1
 
 

@@ -41,11 +41,13 @@ def _worker(rank, world, port, q):
             assert torch.equal(a, b)
         fs = FlatState(net.parameters())
         ar = GradAllReduce(fs)
+        assert not ar.early_slice and not ar.begin(fs.params[0].grad)   # default: one collective, no early slice
+        ar = GradAllReduce(fs, early_slice=True)
         x, y = _data(rank)
         fs.zero_()
         ((net(x) - y) ** 2).mean().backward()
         ar(fs.params)
-        assert ar.calls == 1
+        assert ar.calls == 1 and ar.collectives == 1
         # expected: mean over ranks of each rank's local gradient
         exp = []
         for rr in range(world):
@@ -78,7 +80,7 @@ def _worker(rank, world, port, q):
         net2 = torch.nn.Sequential(torch.nn.Linear(5, 16), torch.nn.LeakyReLU(), torch.nn.Linear(16, 4))
         fs2 = FlatState(net2.parameters(), placement=[[net2[2].weight, net2[2].bias]])
         assert fs2.offsets[2] == 0 and fs2.offsets[3] == 64 and fs2.offsets[0] > fs2.offsets[3]
-        ar2 = GradAllReduce(fs2)
+        ar2 = GradAllReduce(fs2, early_slice=True)
         fs2.zero_()
         ((net2(x) - y.repeat(1, 2)[:, :4]) ** 2).mean().backward()
         whole2 = fs2.flat.clone()
@@ -88,6 +90,34 @@ def _worker(rank, world, port, q):
         assert ar2.begin(span)
         ar2(fs2.params)
         assert ar2.collectives == 2 and torch.equal(fs2.flat, whole2)
+        # the learner-level hook (attach_flat_grads + _sync_clip_step, as every minibatch update ends): ONE
+        # collective per minibatch by default, and every rank steps to the same parameters
+        from xuanpolicy_amd.distributed import attach_flat_grads
+        from xuanpolicy_amd.learners import PPOCLIP_Learner
+        net3 = _net(seed=0)
+        opt = torch.optim.Adam(net3.parameters(), 1e-3, eps=1e-5)
+
+        class _Pol(torch.nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.actor = torch.nn.Module()
+                self.actor.logstd = torch.nn.Parameter(torch.zeros(1))
+                self.body = net3
+        pol = _Pol()
+        lrn = PPOCLIP_Learner(pol, opt, None, "cpu", "./", 0.25, 0.0, 0.2, 0.5, True)
+        attach_flat_grads(lrn, allreduce=True, fused_optimizer=False)
+        gs = lrn.grad_sync
+        assert gs is not None and not gs.early_slice
+        for k in range(3):                        # three minibatches
+            xk, yk = _data(rank + 10 * k)
+            lrn.flat_grads.zero_()
+            ((net3(xk) - yk) ** 2).mean().backward()
+            lrn._sync_clip_step()
+        assert gs.calls == 3 and gs.collectives == 3, (gs.calls, gs.collectives)
+        pv = torch.cat([p.detach().reshape(-1) for p in net3.parameters()])
+        allp = [torch.empty_like(pv) for _ in range(world)]
+        dist.all_gather(allp, pv)
+        assert torch.equal(allp[0], allp[1])
         q.put((rank, "ok"))
     except Exception as e:  # pragma: no cover - reported to the parent
         import traceback

@@ -83,3 +83,56 @@ def test_graphed_updates_match_eager():
         out.append([p.detach().cpu().numpy().copy() for p in agent.policy.parameters()])
     for a, b in zip(*out):
         np.testing.assert_allclose(b, a, rtol=1e-6, atol=1e-7)
+
+
+def test_graphed_updates_ragged_last_minibatch():
+    """N*T = 800 rows in minibatches of 133: six full slots and a ragged 2-row slot per epoch.  The agent keeps one
+    gather buffer per minibatch size, so the slot graphs are keyed by stable pointers: 7 graphs after three
+    iterations (no growth), and the parameters equal the eager run's."""
+    from xuanpolicy_amd.runner import build_cartpole_ppo
+    out = []
+    for graphed in (False, True):
+        agent = build_cartpole_ppo(n_envs=8, n_steps=100, hidden=64, seed=6, device=DEV, graph_update=graphed,
+                                   n_minibatch=6, n_epoch=2)
+        assert agent.batch_size == 133
+        for _ in range(3):
+            agent.train(100, log=False)
+        torch.cuda.synchronize()
+        graphs = getattr(agent.learner, "_slot_graphs", {})
+        assert len(graphs) == (7 if graphed else 0), len(graphs)
+        assert sum(isinstance(v, tuple) for v in graphs.values()) == (7 if graphed else 0)
+        out.append([p.detach().cpu().numpy().copy() for p in agent.policy.parameters()])
+    for a, b in zip(*out):
+        np.testing.assert_allclose(b, a, rtol=1e-6, atol=1e-7)
+
+
+def test_graph_capture_failure_falls_back_to_eager():
+    """A launch failing inside the slot capture (after the backward queued its column-sum finalizes): the learner
+    drops the aborted capture's queued work and workspaces, reruns the update eagerly and stays eager — the
+    parameters equal the eager run's (stale finalizes must not be flushed into the eager update)."""
+    from xuanpolicy_amd import ops
+    from xuanpolicy_amd.runner import build_cartpole_ppo
+    out = []
+    for inject in (False, True):
+        agent = build_cartpole_ppo(n_envs=8, n_steps=128, hidden=64, seed=4, device=DEV, graph_update=inject)
+        if inject:
+            fm = agent.learner._fused_mlp()
+            real = ops.ColsumQueue.flush
+            state = {"raised": 0}
+
+            def flaky(self, *a, **k):
+                if torch.cuda.is_current_stream_capturing() and not state["raised"]:
+                    state["raised"] = 1
+                    assert self.items, "the injected failure must find queued finalizes"
+                    raise RuntimeError("injected capture failure")
+                return real(self, *a, **k)
+            fm._cq.flush = flaky.__get__(fm._cq)
+        for _ in range(2):
+            agent.train(128, log=False)
+        torch.cuda.synchronize()
+        if inject:
+            assert state["raised"] == 1 and agent.learner._graph_failed
+            assert not any(isinstance(v, tuple) for v in agent.learner._slot_graphs.values())
+        out.append([p.detach().cpu().numpy().copy() for p in agent.policy.parameters()])
+    for a, b in zip(*out):
+        np.testing.assert_allclose(b, a, rtol=1e-6, atol=1e-7)

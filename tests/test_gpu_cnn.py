@@ -159,7 +159,7 @@ def test_global_maxpool_and_backward_match_torch(B, HW, C):
     part = torch.empty(G, C, device=DEV)
     dz = torch.empty(B, HW, C, device=DEV)
     _l.check(ops.lib().xpa_maxpool_act_bwd_bias(1, ops._p(dout), ops._p(am), ops._p(hd), B, HW, C, 0.0, ops._p(dz),
-                                                ops._p(part), ops._stream(DEV)), "maxpool_bwd")
+                                                ops._p(part), None, ops._stream(DEV)), "maxpool_bwd")
     db = torch.empty(C, device=DEV)
     _l.check(ops.lib().xpa_colsum_finalize(ops._p(part), G, C, ops._p(db), ops._stream(DEV)), "finalize")
     xr = x.clone().requires_grad_(True)

@@ -107,8 +107,9 @@ def test_dp_normalisation_variants_two_ranks_one_gpu():
 
 
 def _fast_worker(rank, world, port, q):
-    """The C2 fast path (hidden [256]: K13 trunk, K14E, K16 heads, split-K dW with the early all-reduce of the
-    paired hidden slice) on 2 ranks sharing the GPU over gloo."""
+    """The C2 fast path (hidden [256]: K13 trunk, K14E, K16 heads, split-K dW) on 2 ranks sharing the GPU over
+    gloo: ONE all-reduce of the flat gradient per minibatch (north_star), then the same with the opt-in early-slice
+    variant (two per minibatch), both leaving every rank with identical parameters."""
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), XPA_DIST_BACKEND="gloo")
     import torch.distributed as dist
@@ -118,20 +119,22 @@ def _fast_worker(rank, world, port, q):
         init_from_env()
         dev = torch.device("cuda:0")
         torch.cuda.set_device(dev)
-        agent = build_synthbox_ppo(n_envs=128, n_steps=16, obs_dim=17, act_dim=6, hidden=256, n_epoch=2,
-                                   n_minibatch=2, seed=11, device=dev, shard=rank)
-        broadcast_parameters(agent.policy)
-        fm = agent.learner._fused_mlp()
-        assert fm is not None and fm.gemm_heads and fm.pair is not None, "fast path expected"
-        gs = agent.learner.grad_sync
-        assert gs is not None
-        agent.train(32)                     # two iterations of 16 steps, 4 updates each
-        torch.cuda.synchronize()
-        assert gs.calls == 8 and gs.collectives == 16, (gs.calls, gs.collectives)   # 2 per update
-        p = torch.cat([t.detach().reshape(-1) for t in agent.policy.parameters()])
-        got = [torch.empty_like(p) for _ in range(world)]
-        dist.all_gather(got, p)
-        assert torch.equal(got[0], got[1]) and torch.isfinite(p).all()
+        for early, per_update in ((False, 1), (True, 2)):
+            agent = build_synthbox_ppo(n_envs=128, n_steps=16, obs_dim=17, act_dim=6, hidden=256, n_epoch=2,
+                                       n_minibatch=2, seed=11, device=dev, shard=rank)
+            broadcast_parameters(agent.policy)
+            fm = agent.learner._fused_mlp()
+            assert fm is not None and fm.gemm_heads and fm.pair is not None, "fast path expected"
+            gs = agent.learner.grad_sync
+            assert gs is not None and not gs.early_slice
+            gs.early_slice = early
+            agent.train(32)                     # two iterations of 16 steps, 4 updates each
+            torch.cuda.synchronize()
+            assert gs.calls == 8 and gs.collectives == 8 * per_update, (early, gs.calls, gs.collectives)
+            p = torch.cat([t.detach().reshape(-1) for t in agent.policy.parameters()])
+            got = [torch.empty_like(p) for _ in range(world)]
+            dist.all_gather(got, p)
+            assert torch.equal(got[0], got[1]) and torch.isfinite(p).all()
         q.put((rank, "ok"))
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
@@ -142,7 +145,7 @@ def _fast_worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(600)
-def test_dp_fast_path_two_collectives_per_update_two_ranks_one_gpu():
+def test_dp_fast_path_one_collective_per_update_two_ranks_one_gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ctx = mp.get_context("spawn")

@@ -60,3 +60,41 @@ def test_fast_path_iteration_matches_oracle(agent_name, discrete, A, ent):
     agent.train(T, log=False)             # iteration 1 (episodes start together; time limit at step 81)
     agent.train(T - 1, log=False)         # iteration 2's rollout but its last step
     replay_last_step_iteration(agent, D, A, [H], discrete, algo, ent, n_epoch, n_mb, expect_mid_truncations=not discrete)
+
+
+def test_c4_shape_iteration_matches_oracle():
+    """C4's per-shard shapes (BASELINE.json configs[3]: SynthBox(obs=376, act=17), ppo/mujoco.yaml, [256] nets) at a
+    reduced N x T: the 376-wide trunk (no K13: the first layer is a library GEMM), the non-K14E rollout (K14 policy
+    head + the separate env GEMM + K7), the 1024-thread K5 for wide observations, the KMAX-18 K16 bucket (A = 17)
+    and the K9 step — one whole iteration replayed against the oracle (values, old log-probs, bootstraps, GAE,
+    every update's loss scalars, final weights)."""
+    from xuanpolicy_amd.runner import build_synthbox_ppo
+    N, T, D, A, H = 512, 64, 376, 17, 256
+    n_epoch, n_mb = 2, 4
+    agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=D, act_dim=A, hidden=H, n_epoch=n_epoch,
+                               n_minibatch=n_mb, seed=17, device=DEV, max_episode_steps=T + 17)
+    fm = agent.learner._fused_mlp()
+    assert fm is not None and fm.fused_heads and fm.gemm_heads and not fm.thin0 and fm.pair is not None
+    assert agent.defer_boot and agent.n_slots == 1 and not agent._env_fused(fm)
+    agent.train(T, log=False)
+    agent.train(T - 1, log=False)
+    replay_last_step_iteration(agent, D, A, [H], False, "ppo", 0.0, n_epoch, n_mb, expect_mid_truncations=True)
+
+
+def test_deferred_bootstraps_with_several_truncations_per_rollout():
+    """A time limit shorter than the rollout (max_episode_steps 20 < n_steps 64): every env truncates up to
+    ceil(63 / 20) = 4 times before the last step.  K8 keeps one deferred slot per truncation (agent.n_slots = 4), the
+    fix-up writes each slot's V(norm(final obs)) at its own step, and the iteration replays against the oracle
+    (ppoclip_agent.py:95-101 closes every truncated path with its own bootstrap)."""
+    from xuanpolicy_amd.runner import build_synthbox_ppo
+    N, T, D, A, H = 256, 64, 17, 6, 256
+    agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=D, act_dim=A, hidden=H, n_epoch=2, n_minibatch=4,
+                               seed=19, device=DEV, max_episode_steps=20)
+    assert agent.defer_boot and agent.n_slots == 4
+    agent.train(T, log=False)
+    agent.train(T - 1, log=False)
+    replay_last_step_iteration(agent, D, A, [H], False, "ppo", 0.0, 2, 4, expect_mid_truncations=True)
+    mem = agent.memory
+    mid = (mem.closed[:, :T - 1] != 0) & (mem.terminals[:, :T - 1] == 0)
+    assert int(mid.sum(1).max()) >= 3              # several truncations of one env inside one rollout
+    assert int(agent.slot_overflow) == 0 and int(agent.slot_t.max()) == -1

@@ -86,17 +86,18 @@ def test_perdqn_learner_replays_reference(golden):
                                        err_msg=key)
 
 
-def test_perdqn_agent_loop_on_device():
+@pytest.mark.parametrize("filters", [[8, 8], [32, 64]])
+def test_perdqn_agent_loop_on_device(filters):
+    """[8, 8]: MIOpen's NHWC kernels for every conv (the r02 intermittent-fault configuration); [32, 64]: the production
+    first two convs (K25 / K26 / K27 + MIOpen's conv2 weight gradient).  Every device error word stays 0."""
     from xuanpolicy_amd.runner import build_perdqn
-    # the production channel counts of the first two convs (perdqn/atari.yaml: 32, 64), so the loop runs K25 / K26 /
-    # K27; with 8 / 8 channels (MIOpen's NHWC kernels for every conv) this test hit two intermittent illegal-address
-    # faults in r02, never reproduced under AMD_SERIALIZE_KERNEL=3
     agent = build_perdqn(n_envs=4, n_size=256, batch_size=64, device=DEV, start_training=64, sync_frequency=20,
-                         filters=[32, 64], kernels=[8, 4], strides=[4, 2], q_hidden_size=[32], max_episode_steps=40)
+                         filters=filters, kernels=[8, 4], strides=[4, 2], q_hidden_size=[32], max_episode_steps=40)
     assert agent.device_env and agent.memory.observations.dtype == torch.uint8
     assert agent.envs.action_space.n == 18
     agent.train(80, sync_info=True)
     torch.cuda.synchronize()
+    assert agent.check_errors() == {"per_sample": 0, "gather": 0, "env": 0, "td_action": 0, "maxpool": 0}
     assert agent.memory.size == 80 and len(agent.infos) > 0
     for info in agent.infos:
         assert np.isfinite([info["Qloss"], info["predictQ"]]).all()

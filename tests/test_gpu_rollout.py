@@ -14,14 +14,15 @@ def _setup():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("agent_name", ["PPO_Clip", "A2C"])
-def test_deferred_bootstrap_matches_per_step(agent_name):
+@pytest.mark.parametrize("agent_name,max_ep", [("PPO_Clip", 100), ("A2C", 100), ("PPO_Clip", 20)])
+def test_deferred_bootstrap_matches_per_step(agent_name, max_ep):
+    """max_ep 20 < n_steps 64: up to 4 truncations per env and rollout, each in its own deferred slot."""
     from xuanpolicy_amd.runner import build_synthbox_ppo
-    kw = dict(n_envs=512, n_steps=64, n_epoch=2, n_minibatch=4, device=DEV, agent=agent_name, max_episode_steps=100)
+    kw = dict(n_envs=512, n_steps=64, n_epoch=2, n_minibatch=4, device=DEV, agent=agent_name, max_episode_steps=max_ep)
     a = build_synthbox_ppo(defer_bootstrap=True, **kw)
     b = build_synthbox_ppo(defer_bootstrap=False, **kw)
     b.policy.load_state_dict(a.policy.state_dict())
-    assert a.defer_boot and not b.defer_boot
+    assert a.defer_boot and not b.defer_boot and a.n_slots == (1 if max_ep >= 64 else 4)
     for _ in range(3):   # 3 iterations: truncations (every 100 steps) fall mid-buffer
         for ag in (a, b):
             for _ in range(ag.n_steps - 1):

@@ -20,7 +20,7 @@ SOURCES = ["gae.hip", "loss.hip", "rollout.hip", "optim.hip", "mlp.hip", "head.h
            "classic.hip", "dqn.hip", "conv.hip"]
 HEADER = os.path.join(REPO_DIR, "include", "xuanpolicy_amd.h")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 c_i32, c_i64, c_u32, c_f32, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
 
@@ -38,7 +38,7 @@ SIGNATURES = {
     "xpa_dispatch_floor_timed": (ctypes.c_int, [c_p, c_p, c_p]),
     "xpa_random_permutation": (ctypes.c_int, [c_i64, c_u32, c_u32, c_p, c_p]),
     "xpa_gather_num_partials": (c_i64, [c_i64]),
-    "xpa_gather_minibatch": (ctypes.c_int, [c_p, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p]),
+    "xpa_gather_minibatch": (ctypes.c_int, [c_p, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_p]),
     "xpa_loss_num_partials": (c_i64, [c_i64]),
     "xpa_loss_partial_width": (c_i64, [c_i64]),
     "xpa_policy_loss_fwd_bwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p,
@@ -78,7 +78,7 @@ SIGNATURES = {
     "xpa_act_bwd_bias": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_i64, c_i64, c_f32, c_p, c_p, c_p]),
     "xpa_global_maxpool": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
     "xpa_maxpool_act_bwd_bias": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_p, c_p,
-                                                c_p]),
+                                                c_p, c_p]),
     "xpa_head_bwd_num_partials": (c_i64, [c_i64]),
     "xpa_head_backward": (ctypes.c_int, [ctypes.c_int, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_f32, c_p, c_p, c_p,
                                          c_p, c_p]),
@@ -111,19 +111,20 @@ SIGNATURES = {
     "xpa_per_update_priorities": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_i64, ctypes.c_double,
                                                  c_p, c_p]),
     "xpa_per_sample": (ctypes.c_int, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_u32, c_u32, ctypes.c_double,
-                                      ctypes.c_int, c_p, c_p, c_p, c_p]),
+                                      ctypes.c_int, c_p, c_p, c_p, c_p, c_p]),
     "xpa_store_column": (ctypes.c_int, [c_p, c_i64, c_i64, c_p, c_i64, c_p, c_p]),
     "xpa_synthatari_step": (ctypes.c_int, [c_i64, c_i64, c_p, c_i64, c_u32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
-                                           c_p, c_p, c_p, c_p, c_p]),
+                                           c_p, c_p, c_p, c_p, c_p, c_p]),
     "xpa_synthatari_reset": (ctypes.c_int, [c_i64, c_u32, c_p, c_p, c_p]),
     "xpa_rollout_post_deferred_norm": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_f32,
-                                                      c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
-                                                      c_p, c_f32, ctypes.c_int, ctypes.c_int, c_f32, ctypes.c_int, c_p,
-                                                      c_p, c_p]),
-    "xpa_rollout_post_deferred": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p,
+                                                      c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                                                      c_p, c_p, c_p, c_f32, ctypes.c_int, ctypes.c_int, c_f32,
+                                                      ctypes.c_int, c_p, c_p, c_p]),
+    "xpa_rollout_post_deferred": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_i64, c_p,
+                                                 c_p, c_p,
                                                  c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, ctypes.c_int, ctypes.c_int,
                                                  c_f32, ctypes.c_int, c_p, c_p, c_p]),
-    "xpa_rollout_bootstrap_fixup": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_p]),
+    "xpa_rollout_bootstrap_fixup": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p]),
     "xpa_thin_bwd_num_partials": (c_i64, [c_i64]),
     "xpa_thin_linear_act_fwd_gather": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_p,
                                                        c_f32, c_p, c_i64, c_p, c_p, c_p, c_p]),

@@ -136,21 +136,23 @@ class _OnPolicyAgent:
         self.global_advnorm = bool(_cfg(config, "global_advnorm", False)) and self.world > 1
         if self.sync_obs_rms:
             self.use_graph = False  # the per-step collective runs outside a captured graph
-        # Deferred truncation bootstraps: valid when an env truncates at most once per
-        # rollout; the critic then runs once per iteration on [truncation slots; last-step obs] instead of
-        # on every env at every step.
-        max_ep = getattr(envs, "max_episode_steps", getattr(envs, "max_episode_length", 0)) or 0
-        # Only the device envs qualify: their one truncation source is the time limit, so max_ep >= n_steps
-        # bounds it to one per rollout; a host VecEnv may truncate for other reasons (per-step bootstraps).
+        # Deferred truncation bootstraps: the critic runs once per iteration on [truncation slots;
+        # last-step obs] instead of on every env at every step.  Only the device envs qualify: their one truncation
+        # source is the time limit, so an env truncates at most ceil((T - 1) / max_episode_steps) times before the
+        # rollout's last step, and K8 keeps that many slots per env (1 when max_episode_steps >= n_steps, the C1 / C2
+        # / C4 case); a host VecEnv may truncate for other reasons (per-step bootstraps).
+        max_ep = int(getattr(envs, "max_episode_steps", getattr(envs, "max_episode_length", 0)) or 0)
         self.defer_boot = (bool(_cfg(config, "defer_bootstrap", True)) and not self.raw_obs
-                           and hasattr(envs, "step_device") and int(max_ep) >= self.n_steps)
+                           and hasattr(envs, "step_device") and max_ep > 0)
         if self.defer_boot:
-            # [truncation slots; last-step observations] as the two halves of one buffer: the deferred critic
+            S = max(1, -(-(T - 1) // max_ep))
+            self.n_slots = S
+            # [truncation slots (slot-major, S x N rows); last-step observations] as one buffer: the deferred critic
             # pass reads it whole (no concatenation launch)
-            pair = torch.zeros((2 * N, D), **f32)
-            self.slot_obs, self.boot_obs = pair[:N], pair[N:]
+            pair = torch.zeros(((S + 1) * N, D), **f32)
+            self.slot_obs, self.boot_obs = pair[:S * N], pair[S * N:]
             self._boot_pair = pair
-            self.slot_t = torch.full((N,), -1, dtype=torch.int32, device=dev)
+            self.slot_t = torch.full((S * N,), -1, dtype=torch.int32, device=dev)
             self.slot_overflow = torch.zeros((1,), dtype=torch.int32, device=dev)
             self._overflow_host = self._overflow_event = None
         # Raw-frame device envs whose truncations are always terminal (SynthAtari): K8 gets no per-step bootstrap
@@ -444,14 +446,15 @@ class _OnPolicyAgent:
         ops.bootstrap_fixup(self._raw_vb, self._raw_slots, mem.terminals, mem.boot)
 
     def _check_overflow(self):
-        # An env truncating twice in one rollout cannot happen for the device envs (their one truncation source is
-        # the time limit and max_episode_steps >= n_steps, see __init__), so the flag is checked without a host
-        # sync: copied to pinned memory here and read one iteration later (never silent, never a stall).
+        # More truncations per env than slots cannot happen for the device envs (their one truncation source is the
+        # time limit, and __init__ sizes n_slots from it), so this guard of the env contract is checked without a
+        # host sync: copied to pinned memory here and read one iteration later.
         if self._overflow_host is None:
             self._overflow_host = torch.zeros((1,), dtype=torch.int32, pin_memory=True)
             self._overflow_event = torch.cuda.Event()
         elif self._overflow_event.query() and int(self._overflow_host[0]):
-            raise RuntimeError("an env truncated twice within one rollout; set config.defer_bootstrap = False")
+            raise RuntimeError("an env truncated more often than its time limit allows within one rollout (device env "
+                               "contract broken); set config.defer_bootstrap = False")
         self._overflow_host.copy_(self.slot_overflow, non_blocking=True)
         self._overflow_event.record()
 
@@ -461,7 +464,8 @@ class _OnPolicyAgent:
         if self.raw_defer:
             self._raw_last_bootstraps()
         zc = None
-        if (self.defer_boot and not self.atari and not mem._pending and self.fuse_value_gae
+        one_slot = self.defer_boot and self.n_slots == 1   # the fused scans take one deferred truncation per env
+        if (one_slot and not self.atari and not mem._pending and self.fuse_value_gae
                 and ops.gae_value_ok(self.n_steps) and self._rollout_mlp() is not None):
             zc = self._deferred_bootstraps(hidden_only=True)
         if zc is not None:
@@ -476,7 +480,7 @@ class _OnPolicyAgent:
             self.gae_form = "value"
         elif self.defer_boot:
             vboot = self._deferred_bootstraps()
-            if not self.atari and not mem._pending:
+            if one_slot and not self.atari and not mem._pending:
                 # one launch: the fixup's bootstrap writes fused into the compact-closure GAE scan
                 ops.gae_scan_compact(mem.rewards, mem.values, mem.terminals, self.slot_t, vboot, mem.gamma,
                                      mem.gae_lam, mem.use_gae, adv=mem._advantages, ret=mem._returns, boot=mem.boot)
@@ -504,20 +508,26 @@ class _OnPolicyAgent:
                 b = idx.shape[0]
                 if rows_path:
                     # K4 folded into K13: the update reads the minibatch rows (and forms the adv moments) through idx
-                    if self.adv_part is None or self.adv_part.shape[0] != ops.gather_num_partials(b):
-                        self.adv_part = torch.empty((ops.gather_num_partials(b), 2), dtype=torch.float64,
-                                                    device=self.device)
+                    parts = self.__dict__.setdefault("_adv_parts", {})
+                    g = ops.gather_num_partials(b)
+                    if g not in parts:   # one per minibatch size (a ragged last minibatch keeps its own)
+                        parts[g] = torch.empty((g, 2), dtype=torch.float64, device=self.device)
+                    self.adv_part = parts[g]
                     part = self.adv_part if use_advnorm else None
                     scalars = self.learner.update_fused(Rows(obs_flat, idx), idx, act_flat, adv_flat, ret_flat,
                                                         logp_flat, part)
                     if self.update_log is not None:
                         self.update_log.append(scalars.clone())
                     continue
-                if self.obs_mb is None or self.obs_mb.shape[0] != b:
-                    self.obs_mb = torch.empty((b,) + tuple(obs_flat.shape[1:]), dtype=obs_flat.dtype,
-                                              device=self.device)
-                    self.adv_part = torch.empty((ops.gather_num_partials(b), 2), dtype=torch.float64,
-                                                device=self.device)
+                # one (obs_mb, adv_part) pair per minibatch size: a ragged last minibatch keeps its own buffers, so
+                # the pointers the learner's slot graphs are keyed by stay stable across epochs
+                mbs = self.__dict__.setdefault("_mb_bufs", {})
+                bufs = mbs.get((b, obs_flat.dtype, tuple(obs_flat.shape[1:])))
+                if bufs is None:
+                    bufs = (torch.empty((b,) + tuple(obs_flat.shape[1:]), dtype=obs_flat.dtype, device=self.device),
+                            torch.empty((ops.gather_num_partials(b), 2), dtype=torch.float64, device=self.device))
+                    mbs[(b, obs_flat.dtype, tuple(obs_flat.shape[1:]))] = bufs
+                self.obs_mb, self.adv_part = bufs
                 def gather(idx=idx):
                     return ops.gather_minibatch(idx, obs_flat, adv=adv_flat if use_advnorm else None,
                                                 obs_out=self.obs_mb, adv_partials=self.adv_part if use_advnorm else None)
@@ -770,6 +780,23 @@ class PerDQN_Agent:
             self.current_step += self.n_envs
             if self.egreedy > self.end_greedy:
                 self.egreedy = self.egreedy - (self.start_greedy - self.end_greedy) / self.decay_step_greedy
+
+
+    def check_errors(self):
+        """The device loop's error words since the last call (one host sync): PER sample draws clamped past the
+        stored leaves, gathered indices outside the replay buffer, env steps without an action, actions outside
+        [0, n) in the TD kernel, max-pool argmax outside the window.  All 0 unless something upstream is corrupt."""
+        out = dict(zip(("per_sample", "gather"), self.memory.check_errors()))
+        for name, t in (("env", getattr(self.envs, "err", None)), ("td_action", self.learner._err)):
+            out[name] = int(t.item()) if t is not None else 0
+            if t is not None:
+                t.zero_()
+        fq = self.learner._fused_q()
+        e = getattr(fq.eval_trunk, "err", None) if fq is not None else None
+        out["maxpool"] = int(e.item()) if e is not None else 0
+        if e is not None:
+            e.zero_()
+        return out
 
 
 REGISTRY = {"PPO_Clip": PPOCLIP_Agent, "A2C": A2C_Agent, "PerDQN": PerDQN_Agent}

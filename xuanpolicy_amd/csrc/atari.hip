@@ -43,18 +43,22 @@ __global__ __launch_bounds__(256) void synthatari_step_kernel(
     uint32_t *__restrict__ stack, uint32_t *__restrict__ final_obs, float *__restrict__ rew,
     uint8_t *__restrict__ term, uint8_t *__restrict__ trunc, int *__restrict__ ep_step, int *__restrict__ ep_index,
     int *__restrict__ lives, int *__restrict__ pxs, float *__restrict__ ep_score, float *__restrict__ ep_last_score,
-    int *__restrict__ ep_last_len) {
+    int *__restrict__ ep_last_len, int *__restrict__ err) {
     __shared__ int s_px, s_t, s_over, s_bx, s_by, s_bx0, s_by0;
     __shared__ uint32_t s_pre, s_pre0;
     const int64_t n = blockIdx.x;
     const uint32_t env = (uint32_t)n;
     if (threadIdx.x == 0) {
-        int a = 0;  // the env input is the one-hot written by the sampler
+        int a = -1;  // the env input is the one-hot written by the sampler
         for (int k = 0; k < K; ++k)
             if (act_in[n * ld_act + k] > 0.5f) {
                 a = k;
                 break;
             }
+        if (a < 0) {  // no action set: NOOP, counted
+            if (err) atomicAdd(err, 1);
+            a = 0;
+        }
         const uint32_t ep = (uint32_t)ep_index[n];
         const int t = ep_step[n];
         int px = pxs[n] + ((a + 1) % 3 - 1) * 3;
@@ -119,7 +123,7 @@ XPA_API int xpa_synthatari_step(int64_t n_envs, int64_t n_actions, const float *
                                 int32_t max_episode_steps, uint8_t *stack, uint8_t *final_obs, float *rew,
                                 uint8_t *term, uint8_t *trunc, int32_t *ep_step, int32_t *ep_index, int32_t *lives,
                                 int32_t *paddle, float *ep_score, float *ep_last_score, int32_t *ep_last_len,
-                                xpa_stream_t stream) {
+                                int32_t *err, xpa_stream_t stream) {
     if (n_envs <= 0 || n_envs > 0x7fffffff || n_actions < 1 || ld_act < n_actions || max_episode_steps <= 0 ||
         !act_in || !stack || !final_obs || !rew || !term || !trunc || !ep_step || !ep_index || !lives || !paddle ||
         !ep_score || !ep_last_score || !ep_last_len || ((uintptr_t)stack | (uintptr_t)final_obs) % 4)
@@ -127,7 +131,7 @@ XPA_API int xpa_synthatari_step(int64_t n_envs, int64_t n_actions, const float *
     hipLaunchKernelGGL(synthatari_step_kernel, dim3((unsigned)n_envs), dim3(256), 0, (hipStream_t)stream,
                        (int)n_actions, act_in, ld_act, seed, (int)max_episode_steps, (uint32_t *)stack,
                        (uint32_t *)final_obs, rew, term, trunc, ep_step, ep_index, lives, paddle, ep_score,
-                       ep_last_score, ep_last_len);
+                       ep_last_score, ep_last_len, err);
     return xpa_launch_status();
 }
 

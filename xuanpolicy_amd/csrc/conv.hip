@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void maxpool_act_bwd_bias_kernel(const float *
                                                                    const int32_t *__restrict__ argmax,
                                                                    const float *__restrict__ h, int64_t rows, int HW,
                                                                    int C, float slope, float *__restrict__ dz,
-                                                                   float *__restrict__ partials) {
+                                                                   float *__restrict__ partials, int *__restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) f4v s_acc[];
     const int cq = C / 4, groups = 256 / cq;
     const int c4 = threadIdx.x % cq, g = threadIdx.x / cq;
@@ -189,7 +189,9 @@ __global__ __launch_bounds__(256) void maxpool_act_bwd_bias_kernel(const float *
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int64_t bc = b * C + 4 * c4 + e;
-            v[e] = argmax[bc] == hw ? dout[bc] : 0.f;
+            const int am = argmax[bc];
+            if (err && hw == 0 && (am < 0 || am >= HW)) atomicAdd(err, 1);  // K23 writes only in-range indices
+            v[e] = am == hw ? dout[bc] : 0.f;
             v[e] = act_grad<ACT>(v[e], hv[e], slope);
         }
         *reinterpret_cast<f4v *>(dz + r * C + 4 * c4) = v;
@@ -758,7 +760,7 @@ XPA_API int xpa_global_maxpool(const float *x, int64_t batch, int64_t hw, int64_
 
 XPA_API int xpa_maxpool_act_bwd_bias(int act, const float *dout, const int32_t *argmax, const float *h, int64_t batch,
                                      int64_t hw, int64_t channels, float slope, float *dz, float *partials,
-                                     xpa_stream_t stream) {
+                                     int32_t *err, xpa_stream_t stream) {
     const int64_t rows = batch * hw;
     const int64_t G = xpa_act_bwd_bias_num_partials(rows, channels);
     if (G <= 0 || hw > (1 << 30) || !dout || !argmax || !h || !dz || !partials || act < 0 || act > 2)
@@ -768,7 +770,7 @@ XPA_API int xpa_maxpool_act_bwd_bias(int act, const float *dout, const int32_t *
     hipStream_t s = (hipStream_t)stream;
 #define XPA_MPB(A_)                                                                                              \
     hipLaunchKernelGGL((maxpool_act_bwd_bias_kernel<A_>), dim3((unsigned)G), dim3(256), lds, s, dout, argmax, h, \
-                       rows, (int)hw, (int)channels, slope, dz, partials)
+                       rows, (int)hw, (int)channels, slope, dz, partials, err)
     if (act == 0) XPA_MPB(0);
     else if (act == 1) XPA_MPB(1);
     else XPA_MPB(2);

@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256) void per_sample_kernel(const double *__restric
                                                          const double *__restrict__ uniforms, uint32_t seed,
                                                          uint32_t counter, double beta, int wrap_uint8,
                                                          int64_t *__restrict__ steps, int64_t *__restrict__ flat,
-                                                         double *__restrict__ weights) {
+                                                         double *__restrict__ weights, int *__restrict__ err) {
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (g >= n_envs * b) return;
     const int64_t e = g / b, k = g - e * b;
@@ -157,7 +157,12 @@ __global__ __launch_bounds__(256) void per_sample_kernel(const double *__restric
             node = 2 * node + 1;
         }
     }
-    const int64_t idx = node - cap;
+    int64_t idx = node - cap;
+    if (idx >= size) {  // mass at or past the stored total (rounding of u*len + k*len): a zero leaf — the reference
+        if (err) atomicAdd(err, 1);  // would then assert in update_priorities; clamped to the last stored step
+        idx = size - 1;
+        node = cap + idx;
+    }
     const double total = s[1];
     const double scale = pow((double)size, -beta);
     const double max_weight = (m[1] / total) * scale;
@@ -199,13 +204,13 @@ XPA_API int xpa_per_update_priorities(double *sum_tree, double *min_tree, double
 XPA_API int xpa_per_sample(const double *sum_tree, const double *min_tree, int64_t n_envs, int64_t capacity,
                            int64_t size, int64_t batch_per_env, int64_t n_size, const double *uniforms, uint32_t seed,
                            uint32_t counter, double beta, int wrap_uint8, int64_t *steps, int64_t *flat_index,
-                           double *weights, xpa_stream_t stream) {
+                           double *weights, int32_t *err, xpa_stream_t stream) {
     if (n_envs <= 0 || capacity <= 0 || (capacity & (capacity - 1)) || size < 2 || size > capacity ||
         n_size < size || batch_per_env <= 0 || !(beta > 0) || !sum_tree || !min_tree || !steps || !weights)
         return (int)hipErrorInvalidValue;
     const int64_t total = n_envs * batch_per_env;
     hipLaunchKernelGGL(per_sample_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        sum_tree, min_tree, n_envs, capacity, size, batch_per_env, n_size, uniforms, seed, counter, beta,
-                       wrap_uint8, steps, flat_index, weights);
+                       wrap_uint8, steps, flat_index, weights, err);
     return xpa_launch_status();
 }

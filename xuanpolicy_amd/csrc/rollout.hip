@@ -26,13 +26,17 @@ template <typename V>
 __global__ __launch_bounds__(256) void gather_rows_kernel(const int64_t *__restrict__ idx, int64_t batch,
                                                           int64_t n_rows, const V *__restrict__ src, int64_t row_vecs,
                                                           V *__restrict__ dst, const float *__restrict__ adv,
-                                                          double *__restrict__ adv_partials) {
+                                                          double *__restrict__ adv_partials, int *__restrict__ err) {
     __shared__ double s_red[4];
     __shared__ int64_t s_src[kGatherRows];
     const int64_t r0 = (int64_t)blockIdx.x * kGatherRows;
     const int64_t r1 = r0 + kGatherRows < batch ? r0 + kGatherRows : batch;
     const int nr = (int)(r1 - r0);
-    if ((int)threadIdx.x < nr) s_src[threadIdx.x] = idx[r0 + threadIdx.x];
+    if ((int)threadIdx.x < nr) {
+        const int64_t sr = idx[r0 + threadIdx.x];
+        s_src[threadIdx.x] = sr;
+        if (err && (sr < 0 || sr >= n_rows)) atomicAdd(err, 1);  // the row is zero-filled, and counted
+    }
     __syncthreads();
     // Consecutive lanes copy consecutive vectors of a row (32-bit index math; the row's source offset
     // comes from LDS), so each row is one contiguous burst.
@@ -68,10 +72,11 @@ constexpr int kWideU = 4;
 typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void gather_wide_kernel(const int64_t *__restrict__ idx, int64_t n_rows,
                                                           const u4v *__restrict__ src, int64_t row_vecs,
-                                                          int64_t chunks, u4v *__restrict__ dst) {
+                                                          int64_t chunks, u4v *__restrict__ dst, int *__restrict__ err) {
     const int64_t row = (int64_t)blockIdx.x / chunks, chunk = (int64_t)blockIdx.x - row * chunks;
     const int64_t sr = idx[row];
     const bool ok = sr >= 0 && sr < n_rows;
+    if (err && !ok && chunk == 0 && threadIdx.x == 0) atomicAdd(err, 1);
     const int64_t c0 = chunk * 256 * kWideU + threadIdx.x;
     u4v v[kWideU];
 #pragma unroll
@@ -528,8 +533,10 @@ __global__ __launch_bounds__(256) void synthbox_step_kernel(const float *__restr
 // the last block to arrive (atomic ticket) merges them in block order into ret_rms, advances the
 // cursor and resets the ticket to 0 (graph replays see a fresh ticket).
 // DEFER: no v_boot; a mid-buffer truncation of env n copies its normalised final observation row
-// (boot_obs) into slot_obs[n] and records slot_t[n] = t (a second one in the same rollout counts in
-// *overflow); bootstraps are written afterwards by xpa_rollout_bootstrap_fixup.
+// (boot_obs) into the env's first free slot k < n_slots (slot_obs[k n_envs + n], slot_t[k n_envs + n] = t);
+// with every slot taken it counts in *overflow (the agent sizes n_slots from the env's time limit so that
+// this cannot happen: at most ceil((T - 1) / max_episode_steps) mid-buffer truncations per rollout);
+// bootstraps are written afterwards by xpa_rollout_bootstrap_fixup.
 constexpr int kPostThreads = 256;
 // NORM (with DEFER): boot_obs holds the RAW final observations; the kernel normalises them with the obs
 // running statistics (obs_normalize_kernel's exact arithmetic) where it keeps a truncation row, and at the
@@ -549,7 +556,8 @@ __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
     float *__restrict__ returns, float *__restrict__ buf_rew, float *__restrict__ buf_term,
     uint8_t *__restrict__ buf_closed, float *__restrict__ buf_boot, float gamma, int mask_returns, int use_rewnorm,
     float rew_range, int atari_lifeloss, const float *__restrict__ boot_obs, int64_t ld_boot, int64_t dim,
-    float *__restrict__ slot_obs, int *__restrict__ slot_t, int *__restrict__ overflow, double *__restrict__ partials,
+    float *__restrict__ slot_obs, int *__restrict__ slot_t, int n_slots, int *__restrict__ overflow,
+    double *__restrict__ partials,
     unsigned int *__restrict__ ticket, const float *__restrict__ obs_mean = nullptr,
     const float *__restrict__ obs_var = nullptr, float obs_clip = 0.f, float *__restrict__ boot_norm = nullptr,
     int64_t ld_norm = 0) {
@@ -573,11 +581,17 @@ __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
         buf_closed[cell] = close ? 1 : 0;
         buf_boot[cell] = close ? (te ? 0.f : vb) : 0.f;
         if (DEFER && close && !te && !last) {  // mid-buffer truncation: keep the row for later
-            if (slot_t[n] >= 0) atomicAdd(overflow, 1);
-            slot_t[n] = (int)t;
+            int k = 0;
+            while (k < n_slots && slot_t[(int64_t)k * n_envs + n] >= 0) ++k;
+            if (k == n_slots) {  // contract broken: counted (the agent raises), the last slot is reused
+                atomicAdd(overflow, 1);
+                k = n_slots - 1;
+            }
+            const int64_t sl = (int64_t)k * n_envs + n;
+            slot_t[sl] = (int)t;
             for (int64_t d = 0; d < dim; ++d)
-                slot_obs[n * dim + d] = NORM ? obs_norm1(boot_obs[n * ld_boot + d], obs_mean[d], obs_var[d], obs_clip)
-                                             : boot_obs[n * ld_boot + d];
+                slot_obs[sl * dim + d] = NORM ? obs_norm1(boot_obs[n * ld_boot + d], obs_mean[d], obs_var[d], obs_clip)
+                                              : boot_obs[n * ld_boot + d];
         }
         if (NORM && last)
             for (int64_t d = 0; d < dim; ++d)
@@ -640,7 +654,7 @@ XPA_API int64_t xpa_gather_num_partials(int64_t batch) { return (batch + kGather
 
 XPA_API int xpa_gather_minibatch(const int64_t *idx, int64_t batch, int64_t n_rows, const void *obs,
                                  int64_t obs_row_bytes, void *obs_out, const float *adv, double *adv_partials,
-                                 xpa_stream_t stream) {
+                                 int32_t *err, xpa_stream_t stream) {
     if (batch <= 0 || n_rows <= 0 || obs_row_bytes < 0 || !idx) return (int)hipErrorInvalidValue;
     if (obs_row_bytes > 0 && (!obs || !obs_out)) return (int)hipErrorInvalidValue;
     if (adv_partials && !adv) return (int)hipErrorInvalidValue;
@@ -651,19 +665,21 @@ XPA_API int xpa_gather_minibatch(const int64_t *idx, int64_t batch, int64_t n_ro
         const int64_t rv = obs_row_bytes / 16, chunks = (rv + 256 * kWideU - 1) / (256 * kWideU);
         if (batch * chunks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
         hipLaunchKernelGGL(gather_wide_kernel, dim3((unsigned)(batch * chunks)), dim3(256), 0, s, idx, n_rows,
-                           (const u4v *)obs, rv, chunks, (u4v *)obs_out);
+                           (const u4v *)obs, rv, chunks, (u4v *)obs_out, err);
         if (adv_partials)  // the moments alone (no row copy)
             hipLaunchKernelGGL(gather_rows_kernel<uint4>, dim3((unsigned)blocks), dim3(256), 0, s, idx, batch, n_rows,
-                               (const uint4 *)obs, (int64_t)0, (uint4 *)obs_out, adv, adv_partials);
+                               (const uint4 *)obs, (int64_t)0, (uint4 *)obs_out, adv, adv_partials,
+                               (int *)nullptr);
     } else if (obs_row_bytes % 16 == 0 && al % 16 == 0)
         hipLaunchKernelGGL(gather_rows_kernel<uint4>, dim3((unsigned)blocks), dim3(256), 0, s, idx, batch,
-                           n_rows, (const uint4 *)obs, obs_row_bytes / 16, (uint4 *)obs_out, adv, adv_partials);
+                           n_rows, (const uint4 *)obs, obs_row_bytes / 16, (uint4 *)obs_out, adv, adv_partials, err);
     else if (obs_row_bytes % 4 == 0 && al % 4 == 0)
         hipLaunchKernelGGL(gather_rows_kernel<uint32_t>, dim3((unsigned)blocks), dim3(256), 0, s, idx, batch,
-                           n_rows, (const uint32_t *)obs, obs_row_bytes / 4, (uint32_t *)obs_out, adv, adv_partials);
+                           n_rows, (const uint32_t *)obs, obs_row_bytes / 4, (uint32_t *)obs_out, adv, adv_partials,
+                           err);
     else
         hipLaunchKernelGGL(gather_rows_kernel<uint8_t>, dim3((unsigned)blocks), dim3(256), 0, s, idx, batch,
-                           n_rows, (const uint8_t *)obs, obs_row_bytes, (uint8_t *)obs_out, adv, adv_partials);
+                           n_rows, (const uint8_t *)obs, obs_row_bytes, (uint8_t *)obs_out, adv, adv_partials, err);
     return xpa_launch_status();
 }
 
@@ -780,18 +796,21 @@ XPA_API int xpa_rollout_post(int64_t n_envs, int64_t horizon, const float *rew, 
                        dim3(kPostThreads), 0, (hipStream_t)stream, n_envs, horizon, rew, term, trunc, v_boot, cursor,
                        ret_mean, ret_var, ret_count, returns, buf_rew, buf_term, buf_closed, buf_boot, gamma,
                        mask_returns, use_rewnorm, rew_range, atari_lifeloss, (const float *)nullptr, (int64_t)0,
-                       (int64_t)0, (float *)nullptr, (int *)nullptr, (int *)nullptr, partials, (unsigned *)ticket, (const float *)nullptr, (const float *)nullptr, 0.f, (float *)nullptr, (int64_t)0);
+                       (int64_t)0, (float *)nullptr, (int *)nullptr, 0, (int *)nullptr, partials, (unsigned *)ticket,
+                       (const float *)nullptr, (const float *)nullptr, 0.f, (float *)nullptr, (int64_t)0);
     return xpa_launch_status();
 }
 
 XPA_API int xpa_rollout_post_deferred(int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term,
                                       const uint8_t *trunc, const float *boot_obs, int64_t ld_boot, int64_t obs_dim,
-                                      float *slot_obs, int32_t *slot_t, int32_t *overflow, xpa_cursor_t *cursor,
-                                      float *ret_mean, float *ret_var, double *ret_count, float *returns,
-                                      float *buf_rew, float *buf_term, uint8_t *buf_closed, float *buf_boot,
-                                      float gamma, int mask_returns, int use_rewnorm, float rew_range,
-                                      int atari_lifeloss, double *partials, uint32_t *ticket, xpa_stream_t stream) {
-    if (n_envs <= 0 || horizon <= 0 || obs_dim <= 0 || ld_boot < obs_dim || !rew || !term || !trunc || !boot_obs ||
+                                      float *slot_obs, int32_t *slot_t, int64_t n_slots, int32_t *overflow,
+                                      xpa_cursor_t *cursor, float *ret_mean, float *ret_var, double *ret_count,
+                                      float *returns, float *buf_rew, float *buf_term, uint8_t *buf_closed,
+                                      float *buf_boot, float gamma, int mask_returns, int use_rewnorm,
+                                      float rew_range, int atari_lifeloss, double *partials, uint32_t *ticket,
+                                      xpa_stream_t stream) {
+    if (n_envs <= 0 || horizon <= 0 || obs_dim <= 0 || ld_boot < obs_dim || n_slots < 1 || n_slots > horizon ||
+        !rew || !term || !trunc || !boot_obs ||
         !slot_obs || !slot_t || !overflow || !cursor || !ret_mean || !ret_var || !ret_count || !returns || !buf_rew ||
         !buf_term || !buf_closed || !buf_boot || !partials || !ticket || xpa_rollout_post_num_blocks(n_envs) > 0x7fffffff)
         return (int)hipErrorInvalidValue;
@@ -799,7 +818,8 @@ XPA_API int xpa_rollout_post_deferred(int64_t n_envs, int64_t horizon, const flo
                        dim3(kPostThreads), 0, (hipStream_t)stream, n_envs, horizon, rew, term, trunc,
                        (const float *)nullptr, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term,
                        buf_closed, buf_boot, gamma, mask_returns, use_rewnorm, rew_range, atari_lifeloss, boot_obs,
-                       ld_boot, obs_dim, slot_obs, slot_t, overflow, partials, (unsigned *)ticket, (const float *)nullptr, (const float *)nullptr, 0.f, (float *)nullptr, (int64_t)0);
+                       ld_boot, obs_dim, slot_obs, slot_t, (int)n_slots, overflow, partials, (unsigned *)ticket,
+                       (const float *)nullptr, (const float *)nullptr, 0.f, (float *)nullptr, (int64_t)0);
     return xpa_launch_status();
 }
 
@@ -807,12 +827,14 @@ XPA_API int xpa_rollout_post_deferred_norm(int64_t n_envs, int64_t horizon, cons
                                            const uint8_t *trunc, const float *final_obs, int64_t ld_final,
                                            int64_t obs_dim, const float *obs_mean, const float *obs_var,
                                            float obs_clip, float *boot_norm, int64_t ld_norm, float *slot_obs,
-                                           int32_t *slot_t, int32_t *overflow, xpa_cursor_t *cursor, float *ret_mean,
+                                           int32_t *slot_t, int64_t n_slots, int32_t *overflow,
+                                           xpa_cursor_t *cursor, float *ret_mean,
                                            float *ret_var, double *ret_count, float *returns, float *buf_rew,
                                            float *buf_term, uint8_t *buf_closed, float *buf_boot, float gamma,
                                            int mask_returns, int use_rewnorm, float rew_range, int atari_lifeloss,
                                            double *partials, uint32_t *ticket, xpa_stream_t stream) {
-    if (n_envs <= 0 || horizon <= 0 || obs_dim <= 0 || ld_final < obs_dim || ld_norm < obs_dim || !rew || !term ||
+    if (n_envs <= 0 || horizon <= 0 || obs_dim <= 0 || ld_final < obs_dim || ld_norm < obs_dim || n_slots < 1 ||
+        n_slots > horizon || !rew || !term ||
         !trunc || !final_obs || !obs_mean || !obs_var || !boot_norm || !slot_obs || !slot_t || !overflow || !cursor ||
         !ret_mean || !ret_var || !ret_count || !returns || !buf_rew || !buf_term || !buf_closed || !buf_boot ||
         !partials || !ticket || xpa_rollout_post_num_blocks(n_envs) > 0x7fffffff)
@@ -821,33 +843,38 @@ XPA_API int xpa_rollout_post_deferred_norm(int64_t n_envs, int64_t horizon, cons
                        dim3(kPostThreads), 0, (hipStream_t)stream, n_envs, horizon, rew, term, trunc,
                        (const float *)nullptr, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term,
                        buf_closed, buf_boot, gamma, mask_returns, use_rewnorm, rew_range, atari_lifeloss, final_obs,
-                       ld_final, obs_dim, slot_obs, slot_t, overflow, partials, (unsigned *)ticket, obs_mean, obs_var,
+                       ld_final, obs_dim, slot_obs, slot_t, (int)n_slots, overflow, partials, (unsigned *)ticket,
+                       obs_mean, obs_var,
                        obs_clip, boot_norm, ld_norm);
     return xpa_launch_status();
 }
 
 namespace {
-__global__ __launch_bounds__(256) void bootstrap_fixup_kernel(int64_t n_envs, int64_t T, const float *__restrict__ v,
-                                                              int *__restrict__ slot_t,
+// v = V([slot rows (n_slots x n_envs); last-step rows (n_envs)]): every used slot's bootstrap, then the last column's.
+__global__ __launch_bounds__(256) void bootstrap_fixup_kernel(int64_t n_envs, int64_t T, int n_slots,
+                                                              const float *__restrict__ v, int *__restrict__ slot_t,
                                                               const float *__restrict__ buf_term,
                                                               float *__restrict__ buf_boot) {
     const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (n >= n_envs) return;
-    const int t = slot_t[n];
-    if (t >= 0) {
-        buf_boot[n * T + t] = v[n];
-        slot_t[n] = -1;
+    for (int k = 0; k < n_slots; ++k) {
+        const int64_t sl = (int64_t)k * n_envs + n;
+        const int t = slot_t[sl];
+        if (t >= 0 && t < T) buf_boot[n * T + t] = v[sl];
+        slot_t[sl] = -1;
     }
     const int64_t last = n * T + T - 1;
-    buf_boot[last] = buf_term[last] != 0.f ? 0.f : v[n_envs + n];
+    buf_boot[last] = buf_term[last] != 0.f ? 0.f : v[(int64_t)n_slots * n_envs + n];
 }
 }  // namespace
 
 XPA_API int xpa_rollout_bootstrap_fixup(int64_t n_envs, int64_t horizon, const float *values, int32_t *slot_t,
-                                        const float *buf_term, float *buf_boot, xpa_stream_t stream) {
-    if (n_envs <= 0 || horizon <= 0 || !values || !slot_t || !buf_term || !buf_boot) return (int)hipErrorInvalidValue;
+                                        int64_t n_slots, const float *buf_term, float *buf_boot, xpa_stream_t stream) {
+    if (n_envs <= 0 || horizon <= 0 || n_slots < 1 || n_slots > horizon || !values || !slot_t || !buf_term ||
+        !buf_boot)
+        return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(bootstrap_fixup_kernel, dim3((unsigned)((n_envs + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, n_envs, horizon, values, slot_t, buf_term, buf_boot);
+                       (hipStream_t)stream, n_envs, horizon, (int)n_slots, values, slot_t, buf_term, buf_boot);
     return xpa_launch_status();
 }
 

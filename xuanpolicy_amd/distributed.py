@@ -8,10 +8,12 @@ clip_grad_norm_, so the clipped norm is the global one.
 
 FlatState (xuanpolicy_amd.flat) makes every parameter's .grad a view into one contiguous buffer, so
 autograd accumulates straight into it and the all-reduce is one RCCL call over xGMI per minibatch
-(latency-bound at 0.04-1 MiB; one bucket) — or, on the fused MLP path, two: the paired hidden layers' dW
-slice (the first 0.5 MB of the flat buffer) is started as soon as its GEMM has written it and overlaps the
-rest of the backward (GradAllReduce.begin); the rest is one more call.  The overlap is exercised with gloo
-(CPU, and 2 ranks on one GPU); its RCCL timing on xGMI is unmeasured (no multi-GPU box this round).  Backend "nccl" is RCCL on ROCm; "gloo" is used by the CPU tests.
+(latency-bound at 0.04-1 MiB; one bucket).  That single collective is the default (north_star: "a single
+RCCL all-reduce of gradients per minibatch").  GradAllReduce(early_slice=True) is an opt-in variant for the
+fused MLP path that issues two: the paired hidden layers' dW slice (the first 0.5 MB of the flat buffer) is
+started as soon as its GEMM has written it and overlaps the rest of the backward (GradAllReduce.begin), the
+rest is one more call.  That overlap is exercised with gloo only; no RCCL measurement justifies it yet, so it
+stays off.  Backend "nccl" is RCCL on ROCm; "gloo" is used by the CPU tests.
 """
 import os
 
@@ -30,13 +32,14 @@ class GradAllReduce:
     GEMM and the trunk backward.  __call__ then reduces the rest of the buffer and waits for the early
     slice: every element is still averaged exactly once, before the clip."""
 
-    def __init__(self, flat_grads, group=None):
+    def __init__(self, flat_grads, group=None, early_slice=False):
         self.fg = flat_grads
+        self.early_slice = bool(early_slice)
         self.group = group
         self.world = dist.get_world_size(group)
         self.avg = dist.get_backend(group) == "nccl"
         self.calls = 0
-        self.collectives = 0  # all_reduce calls issued (the fused MLP update: 2 per minibatch)
+        self.collectives = 0  # all_reduce calls issued: 1 per minibatch (2 with early_slice on the fused MLP path)
         self._early = None   # (offset, numel, work)
 
     def _reduce(self, t, async_op=False):
@@ -45,7 +48,10 @@ class GradAllReduce:
         return dist.all_reduce(t, op=op, group=self.group, async_op=async_op)
 
     def begin(self, region):
-        """Start the async all-reduce of `region` (a contiguous view into the flat gradient)."""
+        """Start the async all-reduce of `region` (a contiguous view into the flat gradient).  Returns False (and
+        does nothing) unless early_slice is on."""
+        if not self.early_slice:
+            return False
         flat = self.fg.flat
         off = (region.data_ptr() - flat.data_ptr()) // flat.element_size()
         n = region.numel()
@@ -76,9 +82,10 @@ class GradAllReduce:
         self.calls += 1
 
 
-def attach_flat_grads(learner, allreduce=True, group=None, fused_optimizer=True):
+def attach_flat_grads(learner, allreduce=True, group=None, fused_optimizer=True, early_slice=False):
     """Give a learner flat parameters/gradients, the fused clip+Adam step when its optimizer allows,
-    and the all-reduce hook when a process group of more than one rank is initialised."""
+    and the all-reduce hook when a process group of more than one rank is initialised (one collective per
+    minibatch; early_slice=True: the two-collective overlapped variant)."""
     from .fused_mlp import head_placement
     fs = FlatState(learner.policy.parameters(), placement=head_placement(learner.policy))
     learner.flat_grads = fs
@@ -86,7 +93,7 @@ def attach_flat_grads(learner, allreduce=True, group=None, fused_optimizer=True)
     if fused_optimizer and fused_adam_compatible(learner.optimizer):
         learner.fused_opt = FusedClipAdam(learner.optimizer, fs)
     if allreduce and dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        learner.grad_sync = GradAllReduce(fs, group)
+        learner.grad_sync = GradAllReduce(fs, group, early_slice=early_slice)
     return fs
 
 

@@ -216,6 +216,7 @@ class SynthAtariVecEnv:
         self.ep_last_len = torch.zeros((N,), **i32)
         self.ep_score = torch.zeros((N,), dtype=torch.float32, device=dev)
         self.ep_last_score = torch.zeros((N,), dtype=torch.float32, device=dev)
+        self.err = torch.zeros((1,), dtype=torch.int32, device=dev)   # steps taken with no action set (K15)
         self.reset()
 
     @property
@@ -248,7 +249,7 @@ class SynthAtariVecEnv:
                                            ops._p(self.trunc), ops._p(self.ep_step), ops._p(self.ep_index),
                                            ops._p(self.lives), ops._p(self.paddle), ops._p(self.ep_score),
                                            ops._p(self.ep_last_score), ops._p(self.ep_last_len),
-                                           ops._stream(self.device))
+                                           ops._p(self.err), ops._stream(self.device))
         _lib.check(rc, "xpa_synthatari_step")
 
     def step(self, actions):

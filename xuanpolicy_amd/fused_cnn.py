@@ -338,8 +338,10 @@ class _Trunk:
                 dz = torch.empty_like(y)
                 part = parts.get(B * HW, Cy, y.device, True)
                 L, st = ops.lib(), ops._stream(y.device)
+                if getattr(self, "err", None) is None:
+                    self.err = torch.zeros((1,), dtype=torch.int32, device=y.device)   # argmax outside [0, HW)
                 _lib.check(L.xpa_maxpool_act_bwd_bias(code, ops._p(ds.contiguous()), ops._p(am), ops._p(y), B, HW, Cy,
-                                                      float(slope), ops._p(dz), ops._p(part), st),
+                                                      float(slope), ops._p(dz), ops._p(part), ops._p(self.err), st),
                            "xpa_maxpool_act_bwd_bias")
                 _lib.check(L.xpa_colsum_finalize(ops._p(part), part.shape[0], Cy, ops._p(conv.bias.grad), st),
                            "xpa_colsum_finalize")

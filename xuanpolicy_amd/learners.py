@@ -137,7 +137,7 @@ class _FusedPolicyGradient(Learner):
             pre = None
         fm = self._fused_mlp()
         if fm is not None and fm.fused_heads:
-            fm.early_grad_sync = getattr(self.grad_sync, "begin", None) if self.grad_sync is not None else None
+            fm.early_grad_sync = (self.grad_sync.begin if getattr(self.grad_sync, "early_slice", False) else None)
             # obs may be fused_mlp.Rows(flat buffer, idx): K13 reads the minibatch through idx and, with adv_partials,
             # writes the minibatch's advantage moments itself (no K4 launch)
             rows = type(obs).__name__ == "Rows"
@@ -190,15 +190,21 @@ class _FusedPolicyGradient(Learner):
     # that change every update.  Slot graphs are keyed by those pointers.  A slot's first update runs eagerly and warms
     # up workspaces and BLAS handles; the second captures; later ones replay.
     graph_max_rows = 8192
+    graph_max_slots = 64   # captured slot graphs per learner; beyond it (e.g. unstable input pointers) stay eager
 
     def _graph_ok(self, obs):
+        # not while ops.TIMER records events: a captured record would be replayed without re-appending its event
         return (getattr(self, "graph_updates", False) and self.grad_sync is None and isinstance(obs, torch.Tensor)
-                and obs.is_cuda and obs.shape[0] <= self.graph_max_rows and not getattr(self, "_graph_failed", False))
+                and obs.is_cuda and obs.shape[0] <= self.graph_max_rows and not getattr(self, "_graph_failed", False)
+                and not ops.TIMER.enabled
+                and len(self.__dict__.get("_slot_graphs", ())) < self.graph_max_slots)
 
     def _graphed_mlp_update(self, fm, obs, idx, act, adv, ret, old_logp, adv_partials, pre=None):
         ptr = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+        # the loss coefficients are kernel arguments baked into a capture: part of the key
         key = (ptr(obs), tuple(obs.shape), ptr(idx), -1 if idx is None else idx.shape[0], ptr(act), ptr(adv), ptr(ret),
-               ptr(old_logp), ptr(adv_partials)) + tuple(p.data_ptr() for p in self._params)
+               ptr(old_logp), ptr(adv_partials), float(self.clip_range), float(self.vf_coef), float(self.ent_coef)) \
+            + tuple(p.data_ptr() for p in self._params)
         graphs = self.__dict__.setdefault("_slot_graphs", {})
         ent = graphs.get(key)
         if ent is None:                     # first use of this slot: eager (warm-up)
@@ -210,6 +216,8 @@ class _FusedPolicyGradient(Learner):
             if self.__dict__.get("_graph_pool") is None:
                 self._graph_pool = torch.cuda.graph_pool_handle()
             g = torch.cuda.CUDAGraph()
+            # host-side state a failed capture could leave half-built: restored before the eager retry
+            saved = (self._ws, dict(fm._partials), fm._hws)
             try:
                 with torch.cuda.graph(g, pool=self._graph_pool):
                     if pre is not None:
@@ -218,6 +226,10 @@ class _FusedPolicyGradient(Learner):
             except Exception:               # a launch that cannot be captured: stay eager from here on
                 self._graph_failed = True
                 torch.cuda.synchronize()
+                self._ws, fm._partials, fm._hws = saved[0], saved[1], saved[2]
+                fm._cq.reset()              # queued finalizes of the aborted capture (capture-pool partials)
+                fm._cq_early.reset()
+                del graphs[key]
                 if pre is not None:
                     pre()
                 return self._mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, step=False)

@@ -284,8 +284,9 @@ def gather_num_partials(batch):
     return int(lib().xpa_gather_num_partials(batch))
 
 
-def gather_minibatch(idx, obs, adv=None, obs_out=None, adv_partials=None):
-    """K4.  idx int64 [B] flat indices into obs rows ([n_rows, ...] any dtype, contiguous).
+def gather_minibatch(idx, obs, adv=None, obs_out=None, adv_partials=None, err=None):
+    """K4.  idx int64 [B] flat indices into obs rows ([n_rows, ...] any dtype, contiguous).  err (int32 [1], optional):
+    counts indices outside [0, n_rows) (their rows are zero-filled).
     Returns (obs_out [B, ...], adv_partials float64 [n_partials, 2] or None)."""
     _req(idx, "idx", torch.int64)
     if idx.dim() != 1:
@@ -308,7 +309,8 @@ def gather_minibatch(idx, obs, adv=None, obs_out=None, adv_partials=None):
         else:
             _req(adv_partials, "adv_partials", torch.float64, (gather_num_partials(B), 2))
     rc = lib().xpa_gather_minibatch(_p(idx), B, obs.shape[0], _p(obs), row_bytes, _p(obs_out), _p(adv) if adv is not None else None,
-                                    _p(adv_partials) if adv is not None else None, _stream(obs.device))
+                                    _p(adv_partials) if adv is not None else None,
+                                    _p(_req(err, "err", torch.int32, (1,))) if err is not None else None, _stream(obs.device))
     _lib.check(rc, "xpa_gather_minibatch")
     return obs_out, (adv_partials if adv is not None else None)
 
@@ -430,6 +432,11 @@ class ColsumQueue:
         self._plans = {}
         self._ticket = None
         self.loss = None   # deferred loss finalize (defer_loss): run as one extra block of the flush
+
+    def reset(self):
+        """Drop queued finalizes (e.g. those of an aborted graph capture) without launching them."""
+        self.items = []
+        self.loss = None
 
     def defer_loss(self, algo, dist, batch, act_dim, loss_partials, vf_coef, ent_coef, scalars, d_logstd):
         """Queue xpa_policy_loss_finalize_sq for the flush (its d logstd share of the clip norm lands in sq[0])."""
@@ -781,8 +788,8 @@ def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count,
                  deferred=None, workspace=None):
     """K8: reward normalisation, return tracker + ret_rms, rewards/terminals/closures into the buffer
     column cursor.ptr, then cursor.ptr = (ptr + 1) % horizon, cursor.step += 1.
-    deferred = (boot_obs [N, D] (row stride may exceed D), slot_obs [N, D], slot_t int32 [N], overflow
-    int32 [1]): no v_boot; truncation rows are kept for bootstrap_fixup after the rollout.
+    deferred = (boot_obs [N, D] (row stride may exceed D), slot_obs [S N, D], slot_t int32 [S N], overflow
+    int32 [1]): no v_boot; truncation rows are kept (up to S per env) for bootstrap_fixup after the rollout.
     workspace = post_workspace(N) (kept by the caller across steps; allocated here when None)."""
     N = rew.shape[0]
     _req(rew, "rew", torch.float32, (N,))
@@ -805,16 +812,16 @@ def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count,
         # of the final observations folded into K8 (xpa_rollout_post_deferred_norm)
         final_obs, slot_obs, slot_t, overflow, obs_mean, obs_var, obs_clip, boot_norm = deferred
         D = slot_obs.shape[1]
+        S = _n_slots(slot_t, N)
         ldf = _row_stride(final_obs, "final_obs", D)
         ldn = _row_stride(boot_norm, "boot_norm", D)
-        _req(slot_obs, "slot_obs", torch.float32, (N, D))
-        _req(slot_t, "slot_t", torch.int32, (N,))
+        _req(slot_obs, "slot_obs", torch.float32, (S * N, D))
         _req(overflow, "overflow", torch.int32, (1,))
         _req(obs_mean, "obs_mean", torch.float32, (D,))
         _req(obs_var, "obs_var", torch.float32, (D,))
         rc = lib().xpa_rollout_post_deferred_norm(
             N, T, _p(rew), _p(term), _p(trunc), _p(final_obs), ldf, D, _p(obs_mean), _p(obs_var), float(obs_clip),
-            _p(boot_norm), ldn, _p(slot_obs), _p(slot_t), _p(overflow), _p(cursor), _p(ret_mean), _p(ret_var),
+            _p(boot_norm), ldn, _p(slot_obs), _p(slot_t), S, _p(overflow), _p(cursor), _p(ret_mean), _p(ret_var),
             _p(ret_count), _p(returns), _p(buf_rew), _p(buf_term), _p(buf_closed), _p(buf_boot), float(gamma),
             int(bool(mask_returns)), int(bool(use_rewnorm)), float(rew_range), int(bool(atari_lifeloss)), _p(part),
             _p(ticket), _stream(rew.device))
@@ -823,12 +830,12 @@ def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count,
     if deferred is not None:
         boot_obs, slot_obs, slot_t, overflow = deferred
         D = slot_obs.shape[1]
+        S = _n_slots(slot_t, N)
         ld = _row_stride(boot_obs, "boot_obs", D)
-        _req(slot_obs, "slot_obs", torch.float32, (N, D))
-        _req(slot_t, "slot_t", torch.int32, (N,))
+        _req(slot_obs, "slot_obs", torch.float32, (S * N, D))
         _req(overflow, "overflow", torch.int32, (1,))
         rc = lib().xpa_rollout_post_deferred(N, T, _p(rew), _p(term), _p(trunc), _p(boot_obs), ld, D, _p(slot_obs),
-                                             _p(slot_t), _p(overflow), _p(cursor), _p(ret_mean), _p(ret_var),
+                                             _p(slot_t), S, _p(overflow), _p(cursor), _p(ret_mean), _p(ret_var),
                                              _p(ret_count), _p(returns), _p(buf_rew), _p(buf_term), _p(buf_closed),
                                              _p(buf_boot), float(gamma), int(bool(mask_returns)),
                                              int(bool(use_rewnorm)), float(rew_range), int(bool(atari_lifeloss)),
@@ -842,14 +849,23 @@ def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count,
     _lib.check(rc, "xpa_rollout_post")
 
 
+def _n_slots(slot_t, N):
+    """Deferred truncation slots per env of a slot_t buffer ([S N] or [S, N] int32, contiguous)."""
+    _req(slot_t, "slot_t", torch.int32)
+    if slot_t.numel() == 0 or slot_t.numel() % N:
+        raise ValueError("slot_t must hold n_slots x n_envs entries")
+    return slot_t.numel() // N
+
+
 def bootstrap_fixup(values, slot_t, buf_term, buf_boot):
-    """After a deferred rollout: values [2N] = V(slot rows) then V(last-step final obs)."""
+    """After a deferred rollout: values [(S + 1) N] = V(slot rows, slot-major) then V(last-step final obs);
+    slot_t [S N] (S = slots per env)."""
     N, T = buf_boot.shape
-    _req(values, "values", torch.float32, (2 * N,))
-    _req(slot_t, "slot_t", torch.int32, (N,))
+    S = _n_slots(slot_t, N)
+    _req(values, "values", torch.float32, ((S + 1) * N,))
     _req(buf_term, "buf_term", torch.float32, (N, T))
     _req(buf_boot, "buf_boot", torch.float32, (N, T))
-    _lib.check(lib().xpa_rollout_bootstrap_fixup(N, T, _p(values), _p(slot_t), _p(buf_term), _p(buf_boot),
+    _lib.check(lib().xpa_rollout_bootstrap_fixup(N, T, _p(values), _p(slot_t), S, _p(buf_term), _p(buf_boot),
                                                  _stream(values.device)), "xpa_rollout_bootstrap_fixup")
 
 

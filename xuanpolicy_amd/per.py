@@ -71,6 +71,10 @@ class PerOffPolicyBuffer:
         self._max_priority = torch.ones(N, dtype=torch.float64, device=dev)
         self._scratch = torch.full((N, cap), -1, dtype=torch.int32, device=dev)
         self._err = torch.zeros(1, dtype=torch.int32, device=dev)
+        # error words of the sample descent (draws clamped to the last stored step) and of the row gathers (an index
+        # outside the buffer): counted on device, read by check_errors() (one sync, at the caller's choice)
+        self._sample_err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._gather_err = torch.zeros(1, dtype=torch.int32, device=dev)
 
     # ---- memory_tools.py:429-443 ----------------------------------------------------------------
     def _put(self, dst, data):
@@ -107,12 +111,13 @@ class PerOffPolicyBuffer:
         _lib.check(ops.lib().xpa_per_sample(ops._p(self.sum_tree), ops._p(self.min_tree), self.n_envs, self.capacity,
                                             self.size, b, self.n_size, ops._p(uniforms), self.seed & 0xFFFFFFFF,
                                             self._calls & 0xFFFFFFFF, float(beta), int(self.wrap_uint8), ops._p(steps),
-                                            ops._p(flat), ops._p(weights), ops._stream(self.device)), "xpa_per_sample")
+                                            ops._p(flat), ops._p(weights), ops._p(self._sample_err),
+                                            ops._stream(self.device)), "xpa_per_sample")
         return steps, flat, weights
 
     def _gather(self, arr, flat):
         rows = arr.reshape((self.n_envs * self.n_size,) + tuple(arr.shape[2:]))
-        out, _ = ops.gather_minibatch(flat, rows)
+        out, _ = ops.gather_minibatch(flat, rows, err=self._gather_err)
         return out
 
     def sample(self, beta, uniforms=None):
@@ -141,6 +146,14 @@ class PerOffPolicyBuffer:
                    "xpa_per_update_priorities")
         if check and int(self._err.item()):
             raise AssertionError("update_priorities: index outside [0, size)")
+
+    def check_errors(self):
+        """(sample draws clamped past the stored leaves, gathered indices outside the buffer) since the last call;
+        one host sync.  Both are 0 unless the trees or indices are corrupt."""
+        out = (int(self._sample_err.item()), int(self._gather_err.item()))
+        self._sample_err.zero_()
+        self._gather_err.zero_()
+        return out
 
     def clear(self):
         self._alloc()
