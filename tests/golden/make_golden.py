@@ -369,11 +369,38 @@ def capture_per():
 
 # ----------------------------------------------------------------------------------------------
 ATARI_NET = dict(filters=[8, 8], kernels=[8, 4], strides=[4, 2], fc_hidden_sizes=[32])  # a small AC_CNN_Atari
+# the production nets (a2c/atari.yaml + ppo/atari.yaml's AC_CNN_Atari, perdqn/atari.yaml's Basic_CNN + q 512)
+ATARI_PROD_NET = dict(filters=[32, 64, 64], kernels=[8, 4, 3], strides=[4, 2, 1], fc_hidden_sizes=[512])
+PERDQN_PROD_NET = dict(filters=[32, 64, 64], kernels=[8, 4, 3], strides=[4, 2, 1], q_hidden=[512])
 
 
-def capture_atari(N=4, T=16, iters=2, max_ep=20, n_actions=6, seed=5):
-    cfg = types.SimpleNamespace(render=False, n_steps=T, n_minibatch=2, n_epoch=2, gamma=0.99, gae_lambda=0.95,
-                                env_name="Atari", use_gae=True, use_advnorm=True, device="cpu", model_dir="./models/",
+def _sd_compact(prefix, policy, out):
+    """state_dict into out; tensors above fixture_init.BIG elements as every 16th row + per-row f64 sums."""
+    from fixture_init import BIG
+    for k, v in policy.state_dict().items():
+        a = v.detach().cpu().numpy()
+        if a.size > BIG:
+            out[prefix + k + "::rows16"] = a[::16].copy()
+            out[prefix + k + "::rowsum"] = a.reshape(a.shape[0], -1).astype(np.float64).sum(1)
+        else:
+            out[prefix + k] = a.copy()
+
+
+def _uniform_init(policy, seed, out):
+    """Overwrite the freshly built policy with fixture_init.uniform_state(seed); record seed + checksums."""
+    from fixture_init import checksum, uniform_state
+    sd = policy.state_dict()
+    vals = uniform_state([(k, v.shape) for k, v in sd.items()], seed)
+    policy.load_state_dict({k: torch.as_tensor(v) for k, v in vals.items()})
+    out["init_seed"] = np.asarray(seed, np.int64)
+    for k, v in vals.items():
+        out["sd0sum/" + k] = checksum(v)
+
+
+def capture_atari(N=4, T=16, iters=2, max_ep=20, n_actions=6, seed=5, net=ATARI_NET, n_minibatch=2, n_epoch=2,
+                  fname="atari_a2c.npz", init_seed=None):
+    cfg = types.SimpleNamespace(render=False, n_steps=T, n_minibatch=n_minibatch, n_epoch=n_epoch, gamma=0.99,
+                                gae_lambda=0.95, env_name="Atari", use_gae=True, use_advnorm=True, device="cpu", model_dir="./models/",
                                 log_dir="./logs/", vf_coef=0.25, ent_coef=0.01, clip_grad=0.2, use_obsnorm=False,
                                 use_rewnorm=False, obsnorm_range=5, rewnorm_range=5, seed=seed, logger="tensorboard",
                                 test_mode=False)
@@ -390,11 +417,14 @@ def capture_atari(N=4, T=16, iters=2, max_ep=20, n_actions=6, seed=5):
     envs = DummyVecEnv_Atari([(lambda i=i: _Env(i, seed=seed, n_actions=n_actions, max_episode_steps=max_ep))
                               for i in range(N)])
     torch.manual_seed(seed)
-    rep = AC_CNN_Atari((84, 84, 4), ATARI_NET["kernels"], ATARI_NET["strides"], ATARI_NET["filters"], None,
-                       torch.nn.init.orthogonal_, torch.nn.ReLU, "cpu", ATARI_NET["fc_hidden_sizes"])
+    rep = AC_CNN_Atari((84, 84, 4), net["kernels"], net["strides"], net["filters"], None,
+                       torch.nn.init.orthogonal_, torch.nn.ReLU, "cpu", net["fc_hidden_sizes"])
     policy = Categorical_AC_Policy(act_space, rep, [], [], None, torch.nn.init.orthogonal_, torch.nn.ReLU, "cpu")
     out = {}
-    _sd("sd0/", policy, out)
+    if init_seed is None:
+        _sd("sd0/", policy, out)
+    else:
+        _uniform_init(policy, init_seed, out)
     opt = torch.optim.Adam(policy.parameters(), 7e-4, eps=1e-5)
     sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.0, total_iters=10000)
     agent = A2C_Agent(cfg, envs, policy, opt, sch, "cpu")
@@ -449,12 +479,10 @@ def capture_atari(N=4, T=16, iters=2, max_ep=20, n_actions=6, seed=5):
     out["perms"] = np.stack(perms).astype(np.int64)
     out["infos"] = np.asarray(infos, np.float64)
     out["config"] = np.asarray([N, T, n_actions, cfg.n_epoch, cfg.n_minibatch, max_ep, seed], np.int64)
-    out["net"] = np.asarray(ATARI_NET["filters"] + ATARI_NET["kernels"] + ATARI_NET["strides"]
-                            + ATARI_NET["fc_hidden_sizes"], np.int64)
-    _sd("sd1/", policy, out)
-    np.savez_compressed(os.path.join(HERE, "atari_a2c.npz"), **out)
-    print("atari_a2c.npz", len(out), "closures", int(out["closed"].sum()), "life-loss terminals",
-          int(out["term"].sum()))
+    out["net"] = np.asarray(net["filters"] + net["kernels"] + net["strides"] + net["fc_hidden_sizes"], np.int64)
+    _sd_compact("sd1/", policy, out)
+    np.savez_compressed(os.path.join(HERE, fname), **out)
+    print(fname, len(out), "closures", int(out["closed"].sum()), "life-loss terminals", int(out["term"].sum()))
 
 
 # ----------------------------------------------------------------------------------------------
@@ -472,14 +500,15 @@ def perdqn_batch(seed, k, B, A):
     return obs, act, rew, nxt, term
 
 
-def capture_perdqn(B=32, A=18, n_updates=4, seed=9, sync=2, gamma=0.99):
+def capture_perdqn(B=32, A=18, n_updates=4, seed=9, sync=2, gamma=0.99, net=PERDQN_NET, fname="perdqn.npz",
+                   every_sd=True):
     from xuance.torch.representations import Basic_CNN
     from xuance.torch.policies import BasicQnetwork
     from xuance.torch.learners import PerDQN_Learner
     torch.manual_seed(seed)
-    rep = Basic_CNN((84, 84, 4), PERDQN_NET["kernels"], PERDQN_NET["strides"], PERDQN_NET["filters"], None,
+    rep = Basic_CNN((84, 84, 4), net["kernels"], net["strides"], net["filters"], None,
                     torch.nn.init.orthogonal_, torch.nn.ReLU, "cpu")
-    policy = BasicQnetwork(gym.spaces.Discrete(A), rep, PERDQN_NET["q_hidden"], None, torch.nn.init.orthogonal_,
+    policy = BasicQnetwork(gym.spaces.Discrete(A), rep, net["q_hidden"], None, torch.nn.init.orthogonal_,
                            torch.nn.ReLU, "cpu")
     out = {}
     _sd("sd0/", policy, out)
@@ -493,26 +522,146 @@ def capture_perdqn(B=32, A=18, n_updates=4, seed=9, sync=2, gamma=0.99):
         td, info = lrn.update(obs, act, rew, nxt, term)
         tds.append(np.asarray(td, np.float32))
         infos.append([float(info["Qloss"]), float(info["learning_rate"]), float(info["predictQ"])])
-        _sd("sd%d/" % (k + 1), policy, out)
+        if every_sd or k == n_updates - 1:
+            _sd("sd%d/" % (k + 1), policy, out)
     out["td_abs"] = np.stack(tds)
     out["infos"] = np.asarray(infos, np.float64)
     out["input_sums"] = np.asarray(sums, np.int64)
     out["config"] = np.asarray([B, A, n_updates, seed, sync], np.int64)
     out["gamma"] = np.asarray(gamma, np.float64)
-    out["net"] = np.asarray(PERDQN_NET["filters"] + PERDQN_NET["kernels"] + PERDQN_NET["strides"]
-                            + PERDQN_NET["q_hidden"], np.int64)
-    np.savez_compressed(os.path.join(HERE, "perdqn.npz"), **out)
-    print("perdqn.npz", len(out))
+    out["net"] = np.asarray(net["filters"] + net["kernels"] + net["strides"] + net["q_hidden"], np.int64)
+    np.savez_compressed(os.path.join(HERE, fname), **out)
+    print(fname, len(out))
+
+
+def capture_perdqn_agent(N=4, n_size=128, batch=64, A=18, steps=48, seed=13, max_ep=60, net=PERDQN_PROD_NET,
+                         fname="perdqn_agent.npz"):
+    """G10: PerDQN_Agent.train (perdqn_agent.py:56-95) on N SynthAtari envs (18 actions, DummyVecEnv_Atari) with the
+    production Basic_CNN + q 512: e-greedy draws from np.random (the MT19937 state before train() is recorded, so
+    the replay makes the same draws), PerOffPolicyBuffer store / sample(beta) / update_priorities with every
+    random.random() uniform recorded, PerDQN_Learner updates with target copies.  Records every env action, every
+    update's sampled steps, |TD| priorities and info, the beta / epsilon schedules, the final trees and weights.
+    update_priorities receives int64 indices and float64 priorities: the pinned NumPy 1.21 arithmetic
+    (np.float32 ** float -> float64 leaves; uint8 + int -> int64), which NumPy 2 would otherwise change."""
+    import random
+    import xuance.common.memory_tools as mt
+    from xuance.torch.representations import Basic_CNN
+    from xuance.torch.policies import BasicQnetwork
+    from xuance.torch.agents import PerDQN_Agent
+    cfg = types.SimpleNamespace(render=False, training_frequency=1, start_training=64, start_greedy=0.5,
+                                end_greedy=0.05, decay_step_greedy=200, PER_beta0=0.4, env_name="Atari",
+                                n_size=n_size, batch_size=batch, PER_alpha=0.5, device="cpu", model_dir="./models/",
+                                log_dir="./logs/", gamma=0.99, sync_frequency=5, use_obsnorm=False,
+                                use_rewnorm=False, obsnorm_range=5, rewnorm_range=5, seed=seed, logger="tensorboard",
+                                test_mode=False)
+    obs_space, act_space = gym.spaces.Box(0, 255, (84, 84, 4)), gym.spaces.Discrete(A)
+
+    class _Env(SynthAtariEnv):
+        observation_space, action_space = obs_space, act_space
+
+        def close(self):
+            pass
+    envs = DummyVecEnv_Atari([(lambda i=i: _Env(i, seed=seed, n_actions=A, max_episode_steps=max_ep))
+                              for i in range(N)])
+    torch.manual_seed(seed)
+    rep = Basic_CNN((84, 84, 4), net["kernels"], net["strides"], net["filters"], None, torch.nn.init.orthogonal_,
+                    torch.nn.ReLU, "cpu")
+    policy = BasicQnetwork(act_space, rep, net["q_hidden"], None, torch.nn.init.orthogonal_, torch.nn.ReLU, "cpu")
+    out = {}
+    _sd("sd0/", policy, out)
+    opt = torch.optim.Adam(policy.parameters(), 1e-4, eps=1e-5)
+    sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.5, total_iters=100)
+    agent = PerDQN_Agent(cfg, envs, policy, opt, sch, "cpu")
+    envs.reset()
+    mem = agent.memory
+    uniforms, env_acts, upd = [], [], {"steps": [], "td": [], "info": [], "beta": [], "u0": []}
+    sched = {"beta": [], "eps": []}
+    orig_rand, orig_step = random.random, envs.step
+    orig_sample, orig_update, orig_prio = mem.sample, agent.learner.update, mem.update_priorities
+
+    def rec_rand():
+        u = orig_rand()
+        uniforms.append(u)
+        return u
+
+    def step(acts):
+        env_acts.append(np.asarray(acts).astype(np.int64).copy())
+        sched["beta"].append(agent.PER_beta)
+        sched["eps"].append(agent.egreedy)
+        return orig_step(acts)
+
+    def sample(beta):
+        upd["beta"].append(beta)
+        upd["u0"].append(len(uniforms))
+        res = orig_sample(beta)
+        upd["steps"].append(np.asarray(res[-1]).astype(np.int64).copy())
+        return res
+
+    def update(*a):
+        td, info = orig_update(*a)
+        upd["td"].append(np.asarray(td, np.float32).copy())
+        upd["info"].append([float(info["Qloss"]), float(info["learning_rate"]), float(info["predictQ"])])
+        return td, info
+
+    def update_priorities(idxes, priorities):
+        return orig_prio(np.asarray(idxes).astype(np.int64), np.asarray(priorities).astype(np.float64))
+
+    mt.random.random = rec_rand
+    envs.step = step
+    mem.sample, agent.learner.update, mem.update_priorities = sample, update, update_priorities
+    np.random.seed(seed)
+    st = np.random.get_state()
+    out["np_state_keys"] = np.asarray(st[1], np.uint32)
+    out["np_state_pos"] = np.asarray([st[2], st[3]], np.int64)
+    out["np_state_gauss"] = np.asarray(st[4], np.float64)
+    try:
+        agent.train(steps)
+    finally:
+        mt.random.random = orig_rand
+    n_up = len(upd["td"])
+    assert n_up > 10, n_up
+    b = batch // N
+    out["env_actions"] = np.stack(env_acts)
+    out["sched_beta"], out["sched_eps"] = np.asarray(sched["beta"]), np.asarray(sched["eps"])
+    out["upd_steps"] = np.stack(upd["steps"])
+    out["upd_td"] = np.stack(upd["td"])
+    out["upd_info"] = np.asarray(upd["info"], np.float64)
+    out["upd_beta"] = np.asarray(upd["beta"], np.float64)
+    out["upd_uniforms"] = np.stack([np.asarray(uniforms[u0:u0 + batch], np.float64).reshape(N, b)
+                                    for u0 in upd["u0"]])
+    assert len(uniforms) == n_up * batch
+    out["tree_sum"] = np.stack([np.asarray(t._value, np.float64) for t in mem._it_sum])
+    out["tree_min"] = np.stack([np.asarray(t._value, np.float64) for t in mem._it_min])
+    out["max_priority"] = np.array(mem._max_priority, np.float64, copy=True)
+    out["size_ptr"] = np.asarray([mem.size, mem.ptr], np.int64)
+    out["final_beta_eps"] = np.asarray([agent.PER_beta, agent.egreedy], np.float64)
+    out["config"] = np.asarray([N, n_size, batch, A, steps, seed, max_ep, cfg.start_training, cfg.sync_frequency,
+                                cfg.decay_step_greedy], np.int64)
+    out["hyper"] = np.asarray([cfg.start_greedy, cfg.end_greedy, cfg.PER_beta0, cfg.PER_alpha, cfg.gamma, 1e-4, 0.5],
+                              np.float64)
+    out["net"] = np.asarray(net["filters"] + net["kernels"] + net["strides"] + net["q_hidden"], np.int64)
+    _sd("sd1/", policy, out)
+    np.savez_compressed(os.path.join(HERE, fname), **out)
+    print(fname, len(out), "updates", n_up)
 
 
 if __name__ == "__main__":
     os.makedirs("/tmp/xref_run", exist_ok=True)
     os.chdir("/tmp/xref_run")
-    capture_gae()
-    capture_loss()
-    capture_agent("ppo", False, 17, 6)
-    capture_agent("a2c", True, 4, 2)
-    capture_rms()
-    capture_per()
-    capture_atari()
-    capture_perdqn()
+    which = set(sys.argv[1:]) or {"base"}
+    if "base" in which:
+        capture_gae()
+        capture_loss()
+        capture_agent("ppo", False, 17, 6)
+        capture_agent("a2c", True, 4, 2)
+        capture_rms()
+        capture_per()
+        capture_atari()
+        capture_perdqn()
+    if "prod" in which:   # round 3: the production CNN nets (G8P, G9P) and the PerDQN agent loop (G10)
+        torch.set_num_threads(8)
+        capture_atari(N=8, T=64, iters=2, max_ep=40, net=ATARI_PROD_NET, n_minibatch=2, n_epoch=2,
+                      fname="atari_a2c_prod.npz", init_seed=21)
+        capture_perdqn(B=2048, n_updates=3, seed=23, sync=2, net=PERDQN_PROD_NET, fname="perdqn_prod.npz",
+                       every_sd=False)
+        capture_perdqn_agent()

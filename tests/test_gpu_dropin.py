@@ -129,8 +129,10 @@ def test_fused_agent_rollout_step_parity():
     env dynamics, reward normalisation, return tracker, ret_rms, closures)."""
     from xuanpolicy_amd.runner import build_synthbox_ppo
     N, T, D, A = 256, 16, 17, 6
+    # per-step bootstraps (defer_bootstrap=False): every closed column's V(norm(final obs)) is written as the step runs
     agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=D, act_dim=A, hidden=64, n_epoch=1, n_minibatch=2,
-                               seed=5, device=DEV, max_episode_steps=6)
+                               seed=5, device=DEV, max_episode_steps=6, defer_bootstrap=False)
+    assert not agent.defer_boot
     env, mem = agent.envs, agent.memory
     obs_rms = cpu_ref.RunningMeanStdRef((D,))
     ret_rms = cpu_ref.RunningMeanStdRef(())

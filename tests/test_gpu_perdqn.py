@@ -58,10 +58,14 @@ def _perdqn_batch(seed, k, B, A):
     return obs, act, rew, nxt, term
 
 
-def test_perdqn_learner_replays_reference(golden):
+@pytest.mark.parametrize("fixture", ["perdqn.npz", "perdqn_prod.npz"])
+def test_perdqn_learner_replays_reference(golden, fixture):
+    """G9 / G9P: the reference's PerDQN_Learner updates replayed.  perdqn_prod.npz is the production Basic_CNN
+    ([32, 64, 64] / [8, 4, 3] / [4, 2, 1] + q 512) at the C5 batch of 2048: K25 conv1 from the uint8 frames, K23 / K24
+    max pool, K26 / K27 in the backward, K19."""
     from xuanpolicy_amd.learners import PerDQN_Learner
     from xuanpolicy_amd.policies import BasicQnetwork, Basic_CNN
-    g = golden("perdqn.npz")
+    g = golden(fixture)
     B, A, n_up, seed, sync = (int(x) for x in g["config"])
     net = [int(x) for x in g["net"]]
     nl = (len(net) - 1) // 3
@@ -74,6 +78,10 @@ def test_perdqn_learner_replays_reference(golden):
     opt = torch.optim.Adam(pol.parameters(), 1e-3, eps=1e-5)
     sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.5, total_iters=10)
     lrn = PerDQN_Learner(pol, opt, sch, DEV, "./", float(g["gamma"]), sync)
+    fq = lrn._fused_q()
+    assert fq is not None
+    if net[:2] == [32, 64]:
+        assert fq.eval_trunk.u8_conv1 and fq.eval_trunk._dgrad_ok(fq.eval_trunk.convs[1][0])
     for k in range(n_up):
         obs, act, rew, nxt, term = _perdqn_batch(seed, k, B, A)
         td, info = lrn.update(torch.as_tensor(obs, device=DEV), act, rew, torch.as_tensor(nxt, device=DEV), term)
@@ -82,8 +90,10 @@ def test_perdqn_learner_replays_reference(golden):
         np.testing.assert_allclose([info["Qloss"], info["learning_rate"], info["predictQ"]], g["infos"][k],
                                    rtol=1e-4, atol=1e-6)
         for key, v in pol.state_dict().items():
-            np.testing.assert_allclose(v.cpu().numpy(), g["sd%d/%s" % (k + 1, key)], rtol=1e-3, atol=1e-5,
-                                       err_msg=key)
+            if "sd%d/%s" % (k + 1, key) in g:
+                np.testing.assert_allclose(v.cpu().numpy(), g["sd%d/%s" % (k + 1, key)], rtol=1e-3, atol=1e-5,
+                                           err_msg=key)
+    assert all(("sd%d/%s" % (n_up, key)) in g for key in pol.state_dict())
 
 
 @pytest.mark.parametrize("filters", [[8, 8], [32, 64]])
@@ -108,3 +118,77 @@ def test_perdqn_agent_loop_on_device(filters):
     np.testing.assert_allclose(st[:, 1], st[:, cap:].sum(1), rtol=1e-12)
     assert (st[:, cap:cap + 80] > 0).all() and (st[:, cap + 80:] == 0).all()
     assert 0.4 < agent.PER_beta <= 1.0 and agent.egreedy < agent.start_greedy
+
+
+def test_perdqn_agent_train_replays_reference(golden):
+    """G10: the reference's PerDQN_Agent.train (perdqn_agent.py:56-95) replayed through the device agent — SynthAtari
+    device envs (18 actions), the production Basic_CNN + q 512, PER buffer with K6 store / sample / priority update, K4
+    frame gathers, PerDQN_Learner (K25 / K23 / K19 / K24 / K26 / K27 + MIOpen / hipBLASLt), target copies every 5
+    updates.  np.random is set to the recorded MT19937 state, so the e-greedy coins and random actions are the
+    reference's; each PER sample takes the recorded random.random() uniforms.  Checked: every env action, every
+    update's sampled steps, |TD| priorities and info dict, the beta / epsilon schedules, the final sum / min trees,
+    max priorities and weights (eval and target)."""
+    from xuanpolicy_amd.runner import build_perdqn
+    g = golden("perdqn_agent.npz")
+    N, n_size, batch, A, steps, seed, max_ep, start, sync, decay = (int(x) for x in g["config"])
+    eps0, eps1, beta0, alpha, gamma, lr, lr_end = (float(x) for x in g["hyper"])
+    net = [int(x) for x in g["net"]]
+    nl = (len(net) - 1) // 3
+    agent = build_perdqn(n_envs=N, n_size=n_size, batch_size=batch, seed=seed, device=DEV, start_training=start,
+                         sync_frequency=sync, decay_step_greedy=decay, PER_alpha=alpha, PER_beta0=beta0,
+                         start_greedy=eps0, end_greedy=eps1, training_frequency=1, gamma=gamma, learning_rate=lr,
+                         max_episode_steps=max_ep, filters=net[:nl], kernels=net[nl:2 * nl], strides=net[2 * nl:3 * nl],
+                         q_hidden_size=net[3 * nl:])
+    assert agent.device_env and agent.envs.action_space.n == A and agent.alias_first_obs
+    agent.policy.load_state_dict({k[4:]: torch.as_tensor(v) for k, v in g.items() if k.startswith("sd0/")})
+    opt = agent.learner.optimizer
+    agent.learner.scheduler = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=lr_end,
+                                                                total_iters=100)
+    fq = agent.learner._fused_q()
+    assert fq is not None and fq.eval_trunk.u8_conv1
+    # recorded draws: the MT19937 state before train(), the PER uniforms of every sample
+    np.random.set_state(("MT19937", g["np_state_keys"], int(g["np_state_pos"][0]), int(g["np_state_pos"][1]),
+                         float(g["np_state_gauss"])))
+    uni = iter(g["upd_uniforms"])
+    agent.uniform_source = lambda: next(uni)
+    acts, samples, betas = [], [], []
+    real_step, real_sample = agent._env_step, agent.memory.sample
+
+    def env_step(a):
+        acts.append(a.cpu().numpy().astype(np.int64))
+        return real_step(a)
+
+    def sample(beta, uniforms=None):
+        betas.append(beta)
+        out = real_sample(beta, uniforms=uniforms)
+        samples.append(out[-1].cpu().numpy())
+        return out
+    agent._env_step, agent.memory.sample = env_step, sample
+    tds = []
+    real_prio = agent.memory.update_priorities
+
+    def prio(idx, td, check=True):
+        tds.append(td.cpu().numpy().copy())
+        return real_prio(idx, td, check=True)
+    agent.memory.update_priorities = prio
+    agent.train(steps, sync_info=True)
+    torch.cuda.synchronize()
+    assert agent.check_errors() == {"per_sample": 0, "gather": 0, "env": 0, "td_action": 0, "maxpool": 0}
+    np.testing.assert_array_equal(np.stack(acts), g["env_actions"])
+    n_up = g["upd_td"].shape[0]
+    assert len(samples) == n_up and len(agent.infos) == n_up
+    np.testing.assert_array_equal(np.asarray(betas), g["upd_beta"])
+    for k in range(n_up):
+        np.testing.assert_array_equal(samples[k], g["upd_steps"][k], err_msg="sampled steps, update %d" % k)
+        np.testing.assert_allclose(tds[k], g["upd_td"][k], rtol=1e-4, atol=1e-5, err_msg="|TD|, update %d" % k)
+        info = agent.infos[k]
+        np.testing.assert_allclose([info["Qloss"], info["learning_rate"], info["predictQ"]], g["upd_info"][k],
+                                   rtol=1e-4, atol=1e-6, err_msg="info, update %d" % k)
+    np.testing.assert_allclose([agent.PER_beta, agent.egreedy], g["final_beta_eps"], rtol=1e-12)
+    mem = agent.memory
+    assert [mem.size, mem.ptr] == list(g["size_ptr"])
+    np.testing.assert_allclose(mem.sum_tree.cpu().numpy(), g["tree_sum"], rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(mem.min_tree.cpu().numpy(), g["tree_min"], rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(mem.max_priority.cpu().numpy(), g["max_priority"], rtol=1e-4)
+    for key, v in agent.policy.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), g["sd1/" + key], rtol=1e-3, atol=5e-5, err_msg=key)

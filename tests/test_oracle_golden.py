@@ -1,5 +1,7 @@
 """Pin the CPU oracle (oracle/) against golden vectors captured from the reference itself
 (tests/golden/make_golden.py).  CPU only."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -164,13 +166,14 @@ def test_agent_replay_oracle(golden, name):
         np.testing.assert_allclose(v.numpy(), g["sd1/" + k], rtol=1e-4, atol=1e-5, err_msg=k)
 
 
-def test_atari_fixture_frames_and_gae_from_oracle(golden):
+@pytest.mark.parametrize("fixture", ["atari_a2c.npz", "atari_a2c_prod.npz"])
+def test_atari_fixture_frames_and_gae_from_oracle(golden, fixture):
     """G8 pinned on CPU: stepping the oracle SynthAtari env with the recorded actions through the reference's
     DummyVecEnv / A2C_Agent observation flow (gym_vec_env.py:201-212, a2c_agent.py:80-92) reproduces the
     rewards, life-loss terminals and per-step frame sums the reference stored, and the oracle GAE over the
     recorded Atari closures (life losses keep the path open) reproduces its advantages and returns."""
     from oracle.synth_env import SynthAtariEnv
-    g = golden("atari_a2c.npz")
+    g = golden(fixture)
     N, T, K, _, _, max_ep, seed = (int(x) for x in g["config"])
     envs = [SynthAtariEnv(i, seed=seed, n_actions=K, max_episode_steps=max_ep) for i in range(N)]
     obs = np.stack([e.reset()[0] for e in envs])
@@ -209,11 +212,12 @@ def _perdqn_batch(seed, k, B, A):
     return obs, act, rew, nxt, term
 
 
-def test_perdqn_learner_ref_matches_reference(golden):
+@pytest.mark.parametrize("fixture", ["perdqn.npz", "perdqn_prod.npz"])
+def test_perdqn_learner_ref_matches_reference(golden, fixture):
     """G9 pins the oracle's PER-DQN learner (perdqn_learner.py:17-48 over BasicQnetwork / Basic_CNN): |TD|, the
     info dict and the parameters after each of 4 updates (target copies every 2), and the closed-form TD / loss
     gradient (dqn_td_ref) against the autograd learner."""
-    g = golden("perdqn.npz")
+    g = golden(fixture)
     B, A, n_up, seed, sync = (int(x) for x in g["config"])
     net = [int(x) for x in g["net"]]
     nl = (len(net) - 1) // 3
@@ -236,4 +240,49 @@ def test_perdqn_learner_ref_matches_reference(golden):
                                    rtol=1e-5, atol=1e-7)
         assert abs(loss - info["Qloss"]) <= 1e-5 * max(1.0, loss)
         for key, v in pol.state_dict().items():
-            np.testing.assert_allclose(v.numpy(), g["sd%d/%s" % (k + 1, key)], rtol=1e-5, atol=1e-6, err_msg=key)
+            if "sd%d/%s" % (k + 1, key) in g:   # perdqn_prod.npz keeps only the last update's weights
+                np.testing.assert_allclose(v.numpy(), g["sd%d/%s" % (k + 1, key)], rtol=1e-5, atol=1e-6, err_msg=key)
+
+
+def test_fixture_init_regenerates_recorded_start():
+    """G8P's starting weights are regenerated (tests/golden/fixture_init.py), not stored: the regenerated tensors
+    match the checksums recorded when the reference trained from them, and the generator is the PCG64 stream."""
+    import numpy as np
+    from tests.golden.fixture_init import checksum, uniform_state
+    g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "atari_a2c_prod.npz"), allow_pickle=False))
+    shapes = [(k[len("sd0sum/"):], None) for k in g if k.startswith("sd0sum/")]
+    assert len(shapes) == 12    # 3 conv + 1 fc (weight, bias) + actor / critic output layers
+    from xuanpolicy_amd.policies import AC_CNN_Atari, Categorical_AC_Policy
+
+    class _Disc:
+        n, shape = 6, ()
+    torch.manual_seed(0)
+    rep = AC_CNN_Atari((84, 84, 4), [8, 4, 3], [4, 2, 1], [32, 64, 64], None, torch.nn.init.orthogonal_,
+                       torch.nn.ReLU, "cpu", [512])
+    pol = Categorical_AC_Policy(_Disc(), rep, [], [], None, torch.nn.init.orthogonal_, torch.nn.ReLU, "cpu")
+    vals = uniform_state([(k, v.shape) for k, v in pol.state_dict().items()], int(g["init_seed"]))
+    assert set(vals) == {k for k, _ in shapes}
+    for k, v in vals.items():
+        np.testing.assert_array_equal(checksum(v), g["sd0sum/" + k], err_msg=k)
+
+
+def test_perdqn_agent_fixture_schedules():
+    """G10 (PerDQN_Agent.train) on CPU: the recorded epsilon / beta schedules follow perdqn_agent.py:74-95 step by step,
+    every update's uniforms lie in [0, 1), and the recorded trees are consistent (root = sum of leaves)."""
+    import numpy as np
+    g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "perdqn_agent.npz"), allow_pickle=False))
+    N, n_size, batch, A, steps, seed, max_ep, start, sync, decay = (int(x) for x in g["config"])
+    eps0, eps1, beta0 = (float(x) for x in g["hyper"][:3])
+    eps, beta = eps0, beta0
+    for k in range(steps):
+        assert g["sched_eps"][k] == eps and g["sched_beta"][k] == beta
+        beta += (1 - beta0) / steps
+        eps = eps - (eps0 - eps1) / steps
+        if eps > eps1:
+            eps = eps - (eps0 - eps1) / decay
+    assert list(g["final_beta_eps"]) == [beta, eps]
+    u = g["upd_uniforms"]
+    assert u.shape == (g["upd_td"].shape[0], N, batch // N) and (u >= 0).all() and (u < 1).all()
+    cap = g["tree_sum"].shape[1] // 2
+    np.testing.assert_allclose(g["tree_sum"][:, 1], g["tree_sum"][:, cap:].sum(1), rtol=1e-12)
+    assert (g["env_actions"] >= 0).all() and (g["env_actions"] < A).all()

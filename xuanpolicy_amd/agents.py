@@ -732,6 +732,13 @@ class PerDQN_Agent:
         self.current_step = 0
         self.current_episode = np.zeros(self.n_envs, np.int32)
         self.infos = []
+        # perdqn_agent.py:57-66: train() starts from `obs = self.envs.buf_obs`, which aliases the vec env's buffer
+        # (no obsnorm copy), so the first store of every train() call holds the frames envs.step just wrote.
+        # Reproduced by default (a drop-in stores what the reference stores); False stores the pre-step frames.
+        self.alias_first_obs = bool(_cfg(config, "alias_first_obs", True))
+        # optional callable() -> uniforms [n_envs, batch / n_envs] for the next PER sample (e.g. the reference's
+        # recorded random.random() draws, memory_tools.py:415); None: the buffer's counter-hash uniforms
+        self.uniform_source = None
 
     def _action(self, obs, egreedy=0.0):
         """perdqn_agent.py:47-54: argmax of the eval Q row, or (with probability egreedy, one draw for all envs)
@@ -764,13 +771,14 @@ class PerDQN_Agent:
         env = self.envs
         if not self.device_env and not hasattr(self, "_host_obs"):
             self._host_obs = np.array(env.buf_obs, copy=True)
-        for _ in range(train_steps):
+        for k in range(train_steps):
             obs = env.obs.clone() if self.device_env else self._host_obs
             acts = self._action(obs, self.egreedy)
             nxt, rew, term, trunc = self._env_step(acts)
-            self.memory.store(obs, acts, rew, term, nxt)
+            self.memory.store(nxt if (k == 0 and self.alias_first_obs) else obs, acts, rew, term, nxt)
             if self.current_step > self.start_training and self.current_step % self.train_frequency == 0:
-                o, a, r, d, n, w, idxes = self.memory.sample(self.PER_beta)
+                u = self.uniform_source() if self.uniform_source is not None else None
+                o, a, r, d, n, w, idxes = self.memory.sample(self.PER_beta, uniforms=u)
                 td_abs, info = self.learner.update(o, a, r, n, d, sync_info=sync_info)
                 self.memory.update_priorities(idxes, td_abs, check=False)
                 info["epsilon-greedy"] = self.egreedy
