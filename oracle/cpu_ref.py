@@ -422,9 +422,10 @@ def build_atari_ac_ref(n_actions, filters=(32, 64, 64), kernels=(8, 4, 3), strid
             super().__init__()
             self.model = nn.Sequential(*layers)
 
-        def forward(self, obs):
+        def forward(self, obs):   # float32 as the reference; the parameters' dtype when the oracle runs in f64
             x = np.asarray(obs) / 255.0
-            return {"state": self.model(torch.as_tensor(np.transpose(x, (0, 3, 1, 2)), dtype=torch.float32))}
+            dt = next(self.parameters()).dtype
+            return {"state": self.model(torch.as_tensor(np.transpose(x, (0, 3, 1, 2)), dtype=dt))}
 
     class AC(nn.Module):
         discrete = True
@@ -465,9 +466,9 @@ class LearnerRef:
         if not (isinstance(obs, np.ndarray) and obs.dtype == np.uint8):   # raw frames: the policy scales them
             obs = torch.as_tensor(obs, dtype=torch.float32)
         act = torch.as_tensor(act)
-        ret = torch.as_tensor(ret)
-        adv = torch.as_tensor(adv)
         head, logstd, v = self.policy.heads(obs)
+        ret = torch.as_tensor(ret).to(v.dtype)   # (the parameters' dtype: f32, or f64 for precision envelopes)
+        adv = torch.as_tensor(adv).to(v.dtype)
         d = self.policy.dist(head, logstd)
         if self.policy.discrete:
             logp, ent = d.log_prob(act), d.entropy()
@@ -652,8 +653,9 @@ def build_qnetwork_ref(n_actions, filters, kernels, strides, q_hidden, in_shape=
             layers += [nn.AdaptiveMaxPool2d((1, 1)), nn.Flatten()]
             self.model = nn.Sequential(*layers)
 
-        def forward(self, obs):   # obs / 255.0 on the host (f64), NHWC -> NCHW, float32
-            x = torch.as_tensor(np.transpose(np.asarray(obs) / 255.0, (0, 3, 1, 2)), dtype=torch.float32)
+        def forward(self, obs):   # obs / 255.0 on the host (f64), NHWC -> NCHW, float32 (parameters' dtype in f64 runs)
+            dt = next(self.parameters()).dtype
+            x = torch.as_tensor(np.transpose(np.asarray(obs) / 255.0, (0, 3, 1, 2)), dtype=dt)
             return {"state": self.model(x)}
 
     class QheadRef(nn.Module):    # deterministic.py:6-25
@@ -723,6 +725,7 @@ class PerDQNLearnerRef:
         self.iterations += 1
         act, rew, term = torch.as_tensor(act), torch.as_tensor(rew), torch.as_tensor(term)
         _, _, evalQ = self.policy(obs)
+        rew, term = rew.to(evalQ.dtype), term.to(evalQ.dtype)
         _, _, targetQ = self.policy.target(nxt)
         targetQ = rew + self.gamma * (1 - term) * targetQ.max(dim=-1).values
         predictQ = (evalQ * torch.nn.functional.one_hot(act.long(), evalQ.shape[1])).sum(dim=-1)

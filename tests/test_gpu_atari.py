@@ -84,18 +84,22 @@ def _load_sd0(pol, g):
     pol.load_state_dict({k: torch.as_tensor(v) for k, v in vals.items()})
 
 
-def _check_sd1(pol, g, rtol, atol):
+def _check_sd1(pol, g, rtol, atol, env=None):
     """Final weights against the fixture: whole tensors, or (tensors above fixture_init.BIG) every 16th row + every
-    row's sum."""
+    row's sum.  env (tests/golden/make_envelopes.py): per tensor, how far the exact f64 replay lands from the f32
+    reference; the tolerance is max(atol, 3 x that)."""
+    env = env or {}
     for key, v in pol.state_dict().items():
         a = v.detach().cpu().numpy()
         if "sd1/" + key in g:
-            np.testing.assert_allclose(a, g["sd1/" + key], rtol=rtol, atol=atol, err_msg=key)
+            tol = max(atol, 3 * float(env.get("sd/" + key, 0)))
+            np.testing.assert_allclose(a, g["sd1/" + key], rtol=rtol, atol=tol, err_msg=key)
             continue
-        np.testing.assert_allclose(a[::16], g["sd1/" + key + "::rows16"], rtol=rtol, atol=atol, err_msg=key)
+        tol = max(atol, 3 * float(env.get("sd/" + key + "::rows16", 0)))
+        np.testing.assert_allclose(a[::16], g["sd1/" + key + "::rows16"], rtol=rtol, atol=tol, err_msg=key)
         rs = a.reshape(a.shape[0], -1).astype(np.float64).sum(1)
-        np.testing.assert_allclose(rs, g["sd1/" + key + "::rowsum"], rtol=rtol, atol=atol * a[0].size ** 0.5,
-                                   err_msg=key + " row sums")
+        tol = max(atol * a[0].size ** 0.5, 3 * float(env.get("sd/" + key + "::rowsum", 0)))
+        np.testing.assert_allclose(rs, g["sd1/" + key + "::rowsum"], rtol=rtol, atol=tol, err_msg=key + " row sums")
 
 
 @pytest.mark.parametrize("fixture", ["atari_a2c.npz", "atari_a2c_prod.npz"])
@@ -110,12 +114,16 @@ def test_a2c_atari_replays_reference_agent(golden, fixture):
     atari_a2c_prod.npz (G8P) is the production net (filters [32, 64, 64], kernels [8, 4, 3], strides [4, 2, 1], fc
     512; 8 envs x 64 steps, minibatches of 256): the fused path of the C3 bench — K25 conv1 from the uint8 frames,
     MIOpen conv2 / conv3, the (H, W, C)-permuted fc0 weight, K2, K26 conv1 weight gradient with the folded ReLU
-    backward + bias, K27 stride-2 data gradient — replayed update by update."""
+    backward + bias, K27 stride-2 data gradient — replayed update by update.  A few Adam steps of an f32 net are
+    chaotic in the last bits (tests/golden/make_envelopes.py): the prod fixture carries, per update and per tensor, how
+    far the exact f64 replay lands from the reference, and the tolerances are max(base, 3 x that envelope) — update 0
+    (identical starting weights) is held to the base tolerances."""
     from oracle.synth_env import SynthAtariEnv
     from xuanpolicy_amd.buffer import DummyOnPolicyBuffer_Atari
     from xuanpolicy_amd.learners import A2C_Learner
     from xuanpolicy_amd.policies import AC_CNN_Atari, Categorical_AC_Policy
     g = golden(fixture)
+    env = golden(fixture.replace(".npz", "_env.npz")) if "init_seed" in g else None
     N, T, K, n_epoch, n_mb, max_ep, seed = (int(x) for x in g["config"])
     net = [int(x) for x in g["net"]]
     nl = (len(net) - 1) // 3
@@ -174,11 +182,14 @@ def test_a2c_atari_replays_reference_agent(golden, fixture):
                 info = lrn.update(o, a, r, ad)
                 got = [info["actor-loss"], info["critic-loss"], info["entropy"], info["learning_rate"],
                        info["predict_value"]]
-                np.testing.assert_allclose(got, g["infos"][u], rtol=2e-4, atol=2e-5)
+                atol = np.maximum(2e-5, 3 * env["info"][u]) if env is not None else 2e-5
+                if env is not None and u == 0:
+                    assert (atol == 2e-5).all()   # the first update starts from identical weights: base tolerance
+                np.testing.assert_allclose(got, g["infos"][u], rtol=2e-4, atol=atol, err_msg="update %d" % u)
                 u += 1
         buf.clear()
     assert u == len(g["infos"])
-    _check_sd1(pol, g, rtol=1e-3, atol=5e-5)
+    _check_sd1(pol, g, rtol=1e-3, atol=5e-5, env=env)
 
 
 def test_atari_deferred_last_bootstrap_matches_per_step():

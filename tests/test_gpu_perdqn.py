@@ -66,6 +66,9 @@ def test_perdqn_learner_replays_reference(golden, fixture):
     from xuanpolicy_amd.learners import PerDQN_Learner
     from xuanpolicy_amd.policies import BasicQnetwork, Basic_CNN
     g = golden(fixture)
+    # G9P: per-update envelopes of the exact f64 replay's distance from the f32 reference (make_envelopes.py); the
+    # tolerances are max(base, 3 x envelope), so update 0 is held to the base tolerances
+    env = golden(fixture.replace(".npz", "_env.npz")) if fixture != "perdqn.npz" else None
     B, A, n_up, seed, sync = (int(x) for x in g["config"])
     net = [int(x) for x in g["net"]]
     nl = (len(net) - 1) // 3
@@ -86,12 +89,15 @@ def test_perdqn_learner_replays_reference(golden, fixture):
         obs, act, rew, nxt, term = _perdqn_batch(seed, k, B, A)
         td, info = lrn.update(torch.as_tensor(obs, device=DEV), act, rew, torch.as_tensor(nxt, device=DEV), term)
         assert td.device.type == "cuda" and td.dtype == torch.float32
-        np.testing.assert_allclose(td.cpu().numpy(), g["td_abs"][k], rtol=1e-4, atol=1e-5)
+        td_tol = max(1e-5, 3 * float(env["td"][k])) if env is not None else 1e-5
+        info_tol = np.maximum(1e-6, 3 * env["info"][k]) if env is not None else 1e-6
+        np.testing.assert_allclose(td.cpu().numpy(), g["td_abs"][k], rtol=1e-4, atol=td_tol, err_msg="update %d" % k)
         np.testing.assert_allclose([info["Qloss"], info["learning_rate"], info["predictQ"]], g["infos"][k],
-                                   rtol=1e-4, atol=1e-6)
+                                   rtol=1e-4, atol=info_tol, err_msg="update %d" % k)
         for key, v in pol.state_dict().items():
             if "sd%d/%s" % (k + 1, key) in g:
-                np.testing.assert_allclose(v.cpu().numpy(), g["sd%d/%s" % (k + 1, key)], rtol=1e-3, atol=1e-5,
+                tol = max(1e-5, 3 * float(env["sd/" + key])) if env is not None else 1e-5
+                np.testing.assert_allclose(v.cpu().numpy(), g["sd%d/%s" % (k + 1, key)], rtol=1e-3, atol=tol,
                                            err_msg=key)
     assert all(("sd%d/%s" % (n_up, key)) in g for key in pol.state_dict())
 
@@ -187,8 +193,9 @@ def test_perdqn_agent_train_replays_reference(golden):
     np.testing.assert_allclose([agent.PER_beta, agent.egreedy], g["final_beta_eps"], rtol=1e-12)
     mem = agent.memory
     assert [mem.size, mem.ptr] == list(g["size_ptr"])
-    np.testing.assert_allclose(mem.sum_tree.cpu().numpy(), g["tree_sum"], rtol=1e-5, atol=1e-9)
-    np.testing.assert_allclose(mem.min_tree.cpu().numpy(), g["tree_min"], rtol=1e-5, atol=1e-9)
+    # leaves are |TD|^alpha of priorities matched at rtol 1e-4 / atol 1e-5 above
+    np.testing.assert_allclose(mem.sum_tree.cpu().numpy(), g["tree_sum"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(mem.min_tree.cpu().numpy(), g["tree_min"], rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(mem.max_priority.cpu().numpy(), g["max_priority"], rtol=1e-4)
     for key, v in agent.policy.state_dict().items():
         np.testing.assert_allclose(v.cpu().numpy(), g["sd1/" + key], rtol=1e-3, atol=5e-5, err_msg=key)
