@@ -46,6 +46,10 @@ def parse():
     p.add_argument("--no-c4", action="store_true", help="skip the C4 Box(376,17) measurement")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
+    p.add_argument("--gae-form", choices=("value", "split"), default="split",
+                   help="value: the deferred bootstraps' value head fused into the GAE scan (K1V, one launch); "
+                        "split: value head (K14) then the compact GAE scan (K1)")
+    p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc HBM-traffic passes")
     return p.parse_args()
 
 
@@ -121,6 +125,46 @@ def gae_graph_replay_us(agent, reps=50):
         e1.record(side)
         e1.synchronize()
     return e0.elapsed_time(e1) / reps * 1e3
+
+
+def live_gae_traffic(form, timeout_s=150):
+    """roofline.traffic measured in this run: two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: separate passes,
+    the TCC block cannot hold both) over tools/gae_pmc.py --quick (the GAE launch at the bench size, 4096 x 128,
+    caches evicted by a 512 MiB read before each launch), each in a child process under `timeout -s KILL`; the
+    gfx950 corrections of MI355X_MICROARCH.md §HBM (FETCH_SIZE in KiB, half of a wide streaming read -> x2;
+    WRITE_SIZE exact for 16-B stores) applied by tools/pmc_summary.py.  Returns (per-launch HBM bytes or None,
+    note)."""
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not found"
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import pmc_summary
+    tmp = tempfile.mkdtemp(prefix="xpa_pmc_")
+    dirs = {}
+    env = dict(os.environ, TMPDIR="/tmp")
+    for ctr, tag in (("FETCH_SIZE", "f"), ("WRITE_SIZE", "w")):
+        d = os.path.join(tmp, tag)
+        cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o",
+               tag, "--", sys.executable, os.path.join(REPO, "tools", "gae_pmc.py"), "--quick"]
+        try:
+            r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=timeout_s + 30)
+        except Exception as e:   # noqa: BLE001 - reported, never fatal to the bench line
+            return None, "pmc pass %s failed: %r" % (ctr, e)
+        if r.returncode != 0:
+            return None, "pmc pass %s exited %d: %s" % (ctr, r.returncode, r.stderr[-300:])
+        dirs[ctr] = d
+    out = os.path.join(tmp, "pmc.json")
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        pmc_summary.main(dirs["FETCH_SIZE"], dirs["WRITE_SIZE"], out)
+    with open(out) as f:
+        res = json.load(f)
+    key = "hbm_bytes_per_launch_" + ("value" if form == "value" else "compact")
+    return res.get(key), "live rocprofv3 --pmc passes over tools/gae_pmc.py --quick (%s form, 4096 x 128)" % form
 
 
 def cache_flush(flush, mode):
@@ -702,6 +746,7 @@ def main():
                                n_epoch=args.n_epoch, n_minibatch=args.n_minibatch, seed=1, device=device,
                                shard=rank)
     agent.learner.enable_fast_path()  # flat params/grads, fused clip+Adam, RCCL hook when world > 1
+    agent.fuse_value_gae = args.gae_form == "value"
     if world > 1:
         broadcast_parameters(agent.policy)
 
@@ -772,11 +817,7 @@ def main():
             gb = gae_value_bytes(N, T, mid_trunc, args.hidden) if form == "value" else gae_bytes(N, T, mid_trunc)
             gb_k1 = gae_bytes(N, T, mid_trunc)
             ach = gb / gae_ms / 1e6
-            traffic = None
-            pmc = os.path.join(REPO, "profiles", "pmc_gae_r02.json")   # tools/gae_pmc.py + tools/pmc_summary.py
-            if os.path.exists(pmc):
-                with open(pmc) as f:
-                    traffic = json.load(f).get("hbm_bytes_per_launch_" + form)
+            traffic, traffic_note = (None, "skipped (--no-pmc)") if args.no_pmc else live_gae_traffic(form)
             if form == "value":
                 act_code = agent.learner._fused_mlp().critic[-2][1]
                 kname = "xpa_gae_scan_value: critic output layer + bootstrap fixup + GAE (gae_dpp_kernel<5, 1, %d>)" \
@@ -785,6 +826,8 @@ def main():
                 kname = "xpa_gae_scan_compact (gae_dpp_kernel<5, 1>)"
             roofline = {"kernel": kname, "bound": "hbm", "achieved": round(ach, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "traffic_note": traffic_note,
+                        "traffic_over_algorithmic": round(traffic / gb, 3) if traffic else None,
                         "avg_launch_us": round(gae_ms * 1e3, 3), "algorithmic_bytes_per_launch": int(gb),
                         "bytes_note": ("K1's 20 B per (env, step) + 4 B per bootstrap (%d B) + the critic hidden "
                                        "pre-activations the fused value head reads, 2 x %d rows x %d f32 + the output "
@@ -847,8 +890,8 @@ def main():
                        "num_envs_per_gpu": N, "horizon": T, "global_envs": N * world, "minibatch": B,
                        "updates_per_step": args.n_epoch * args.n_minibatch,
                        "parallelism": ("dp1 (one env shard, no collective)" if world == 1 else
-                                       "dp%d (env shards; the flat gradient all-reduced per minibatch over %s: the "
-                                       "paired hidden dW slice early + the rest, 2 calls)" % (
+                                       "dp%d (env shards; ONE all-reduce of the flat gradient per minibatch over "
+                                       "%s)" % (
                                            world, "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()))},
             "roofline": roofline,
             "phase_split_ms": phase_ms,

@@ -18,7 +18,8 @@ from xuanpolicy_amd import ops  # noqa: E402
 def main():
     dev = torch.device("cuda:0")
     flush = torch.empty(512 * 1024 * 1024 // 4, device=dev)
-    for N in (4096, 1048576):
+    quick = "--quick" in sys.argv   # bench.py's live pass: the bench size (4096 x 128) only
+    for N in ((4096,) if quick else (4096, 1048576)):
         T = 128
         g = torch.Generator(device=dev).manual_seed(N)
         rew = torch.randn(N, T, device=dev, generator=g)
