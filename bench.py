@@ -46,10 +46,12 @@ def parse():
     p.add_argument("--no-c4", action="store_true", help="skip the C4 Box(376,17) measurement")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
-    p.add_argument("--gae-form", choices=("value", "split"), default="split",
+    p.add_argument("--gae-form", choices=("value", "split"), default="value",
                    help="value: the deferred bootstraps' value head fused into the GAE scan (K1V, one launch); "
                         "split: value head (K14) then the compact GAE scan (K1)")
     p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc HBM-traffic passes")
+    p.add_argument("--no-rocprof", action="store_true",
+                   help="skip the child rocprofv3 --kernel-trace run that times the in-loop GAE launches")
     return p.parse_args()
 
 
@@ -165,6 +167,44 @@ def live_gae_traffic(form, timeout_s=150):
         res = json.load(f)
     key = "hbm_bytes_per_launch_" + ("value" if form == "value" else "compact")
     return res.get(key), "live rocprofv3 --pmc passes over tools/gae_pmc.py --quick (%s form, 4096 x 128)" % form
+
+
+def live_gae_rocprof(args, timeout_s=300):
+    """The in-loop GAE launch timed by the profiler: a child `rocprofv3 --kernel-trace` run of this bench (same
+    workload and GAE form, 2 warmup + 3 timed iterations, no side measurements); the average kernel-trace duration of
+    the 3 timed in-loop GAE launches.  Returns (avg us, [us, ...], note) or (None, None, note)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, None, "rocprofv3 not found"
+    tmp = tempfile.mkdtemp(prefix="xpa_kt_")
+    cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--kernel-trace", "--output-format", "csv", "-d", tmp, "-o",
+           "run", "--", sys.executable, os.path.abspath(__file__), "--steps", "3", "--warmup", "2", "--gae-form",
+           args.gae_form, "--n-envs", str(args.n_envs), "--horizon", str(args.horizon), "--obs-dim", str(args.obs_dim),
+           "--act-dim", str(args.act_dim), "--hidden", str(args.hidden), "--n-epoch", str(args.n_epoch),
+           "--n-minibatch", str(args.n_minibatch), "--no-pmc", "--no-rocprof", "--no-cpu-baseline", "--no-sweep",
+           "--no-per", "--no-c1", "--no-c3", "--no-c4", "--no-kernel-timing"]
+    try:
+        r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), capture_output=True, text=True,
+                           timeout=timeout_s + 30)
+    except Exception as e:   # noqa: BLE001 - reported, never fatal to the bench line
+        return None, None, "rocprofv3 child run failed: %r" % (e,)
+    files = glob.glob(os.path.join(tmp, "**", "*kernel_trace.csv"), recursive=True)
+    if r.returncode != 0 or not files:
+        return None, None, "rocprofv3 child run exited %d: %s" % (r.returncode, r.stderr[-300:])
+    rows = [x for x in csv.DictReader(open(files[0])) if "gae_dpp_kernel" in x["Kernel_Name"]]
+    rows.sort(key=lambda x: int(x["Start_Timestamp"]))
+    dur = [(int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e3 for x in rows[:5]]
+    if len(dur) < 5:
+        return None, None, "expected 5 in-loop GAE launches in the trace, found %d" % len(dur)
+    timed = dur[2:5]
+    return sum(timed) / 3, [round(d, 3) for d in timed], (
+        "rocprofv3 --kernel-trace of a child run of this bench (same workload, --gae-form %s; 2 warmup + 3 timed "
+        "iterations): the 3 timed in-loop GAE launches" % args.gae_form)
 
 
 def cache_flush(flush, mode):
@@ -818,6 +858,8 @@ def main():
             gb_k1 = gae_bytes(N, T, mid_trunc)
             ach = gb / gae_ms / 1e6
             traffic, traffic_note = (None, "skipped (--no-pmc)") if args.no_pmc else live_gae_traffic(form)
+            rp_us, rp_list, rp_note = (None, None, "skipped") if args.no_rocprof or world > 1 else \
+                live_gae_rocprof(args)
             if form == "value":
                 act_code = agent.learner._fused_mlp().critic[-2][1]
                 kname = "xpa_gae_scan_value: critic output layer + bootstrap fixup + GAE (gae_dpp_kernel<5, 1, %d>)" \
@@ -834,6 +876,13 @@ def main():
                                        "layer" % (int(gb_k1), N, args.hidden)) if form == "value" else
                                       "20 B per (env, step) + 4 B per bootstrap (SURVEY.md §8(d))",
                         "gae_only_bytes_frac": round(gb_k1 / gae_ms / 1e6 / HBM_PEAK_GBS, 4),
+                        # the profiler's duration of the same in-loop launch (child run): frac against the §8(d)
+                        # 20 B/unit bytes and against every byte the launch reads and writes
+                        "rocprof_inloop_us": round(rp_us, 3) if rp_us else None,
+                        "rocprof_inloop_launches_us": rp_list,
+                        "rocprof_frac_sec8d_bytes": round(gb_k1 / rp_us / 1e3 / HBM_PEAK_GBS, 4) if rp_us else None,
+                        "rocprof_frac_launch_bytes": round(gb / rp_us / 1e3 / HBM_PEAK_GBS, 4) if rp_us else None,
+                        "rocprof_note": rp_note,
                         "launches": gae_launches,
                         "timing": "HIP events recorded by each in-loop dispatch at the kernel's own start and end "
                                   "(hipExtLaunchKernel), on the launch stream, inside the timed region",

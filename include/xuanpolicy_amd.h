@@ -576,6 +576,34 @@ int xpa_maxpool_act_bwd_bias(int act, const float *dout, const int32_t *argmax, 
                              int64_t hw, int64_t channels, float slope, float *dz, float *partials, int32_t *err,
                              xpa_stream_t stream);
 
+/* K28 / K29 — generic NHWC convolutions of the CNN trunks as implicit GEMMs on the fp32 matrix cores (exact f32
+ * fma chains), replacing MIOpen on the explicit CNN path (conv blocks of AC_CNN_Atari / Basic_CNN,
+ * xuance/torch/utils/layers.py:27-57, xuance/torch/representations/cnn.py:5-93, and their backward in
+ * loss.backward(), a2c_learner.py:31-33 / perdqn_learner.py:37-40).  Tensors NHWC f32; w in torch's layout
+ * [out_c][in_c][kernel][kernel]; in_c a multiple of 4, <= 64; out_c <= 64; xpa_conv_igemm_ok(in_c, out_c, kernel)
+ * tells whether the weight image fits the 160 KiB LDS (the forward and, with the channel counts swapped, the data
+ * gradient).  act: 0 identity, 1 LeakyReLU(slope) / ReLU (slope 0), 2 tanh.
+ * xpa_conv_fwd: y = act(conv(x, w) + bias) [batch, OH, OW, out_c] (bias nullable).
+ * xpa_conv_dgrad: dx [batch, in_h, in_w, in_c] = the data gradient of the conv from dy [batch, out_h, out_w, out_c]
+ *   (stride 1 or 2); with act_prev >= 0, dx = that * act'(y_prev) (the previous block's activation backward, act' from
+ *   its OUTPUT y_prev) and, when bias_partial != NULL, its column sums per block
+ *   ([xpa_conv_dgrad_num_partials(batch, in_h, in_w)][in_c], xpa_colsum_finalize -> the previous block's bias grad).
+ * xpa_conv_wgrad: per-block partials [xpa_conv_wgrad_num_partials()][out_c][in_c][kernel][kernel] of
+ *   dW = sum over output pixels of dz x (xpa_colsum_finalize -> the weight gradient, weight layout); dz = g, or with
+ *   act >= 0, g * act'(y) (y = the block's forward output) and then bias_partial [num_partials][out_c] too. */
+int xpa_conv_igemm_ok(int64_t in_channels, int64_t out_channels, int64_t kernel);
+int xpa_conv_fwd(int act, const float *x, int64_t batch, int64_t in_h, int64_t in_w, int64_t in_c, const float *w,
+                 const float *bias, int64_t out_c, int64_t kernel, int64_t stride, int64_t pad, float slope, float *y,
+                 xpa_stream_t stream);
+int64_t xpa_conv_dgrad_num_partials(int64_t batch, int64_t in_h, int64_t in_w);
+int xpa_conv_dgrad(const float *dy, int64_t batch, int64_t out_h, int64_t out_w, int64_t out_c, const float *w,
+                   int64_t in_c, int64_t kernel, int64_t stride, int64_t pad, int64_t in_h, int64_t in_w, int act_prev,
+                   const float *y_prev, float slope, float *dx, float *bias_partial, xpa_stream_t stream);
+int64_t xpa_conv_wgrad_num_partials(void);
+int xpa_conv_wgrad(int act, const float *g, const float *y, float slope, const float *x, int64_t batch, int64_t in_h,
+                   int64_t in_w, int64_t in_c, int64_t out_c, int64_t kernel, int64_t stride, int64_t pad,
+                   float *partial, float *bias_partial, xpa_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,7 +17,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "libxuanpolicy_amd.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
 SOURCES = ["gae.hip", "loss.hip", "rollout.hip", "optim.hip", "mlp.hip", "head.hip", "thin.hip", "per.hip", "atari.hip",
-           "classic.hip", "dqn.hip", "conv.hip"]
+           "classic.hip", "dqn.hip", "conv.hip", "igemm.hip"]
 HEADER = os.path.join(REPO_DIR, "include", "xuanpolicy_amd.h")
 
 ABI_VERSION = 2
@@ -124,6 +124,15 @@ SIGNATURES = {
                                                  c_p, c_p,
                                                  c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, ctypes.c_int, ctypes.c_int,
                                                  c_f32, ctypes.c_int, c_p, c_p, c_p]),
+    "xpa_conv_igemm_ok": (ctypes.c_int, [c_i64, c_i64, c_i64]),
+    "xpa_conv_fwd": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i64,
+                                    c_f32, c_p, c_p]),
+    "xpa_conv_dgrad_num_partials": (c_i64, [c_i64, c_i64, c_i64]),
+    "xpa_conv_dgrad": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
+                                      ctypes.c_int, c_p, c_f32, c_p, c_p, c_p]),
+    "xpa_conv_wgrad_num_partials": (c_i64, []),
+    "xpa_conv_wgrad": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_f32, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
+                                      c_i64, c_p, c_p, c_p]),
     "xpa_rollout_bootstrap_fixup": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p]),
     "xpa_thin_bwd_num_partials": (c_i64, [c_i64]),
     "xpa_thin_linear_act_fwd_gather": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_p,

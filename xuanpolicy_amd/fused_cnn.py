@@ -70,6 +70,14 @@ class _Part:
     def __init__(self):
         self.bufs = {}
 
+    def buf(self, key, shape, device):
+        """A cached float32 buffer by key (K28 / K29 partials)."""
+        p = self.bufs.get(key)
+        if p is None:
+            p = torch.empty(shape, dtype=torch.float32, device=device)
+            self.bufs[key] = p
+        return p
+
     def get(self, rows, cols, device, k22):
         key = (rows, cols, k22)
         p = self.bufs.get(key)
@@ -234,11 +242,14 @@ class _Trunk:
             hs = [h]
             convs = self.convs
         for conv, code, slope in convs:
-            z = F.conv2d(h.permute(0, 3, 1, 2), conv.weight, None, conv.stride, conv.padding)
-            y = z.permute(0, 2, 3, 1)
-            if not y.is_contiguous():
-                y = y.contiguous()
-            _bias_act(code, y.view(-1, y.shape[3]), conv.bias, slope)
+            if self._igemm_ok(conv):   # K28: implicit GEMM on the fp32 matrix cores, bias + activation fused
+                y = self._conv_fwd(conv, code, slope, h)
+            else:
+                z = F.conv2d(h.permute(0, 3, 1, 2), conv.weight, None, conv.stride, conv.padding)
+                y = z.permute(0, 2, 3, 1)
+                if not y.is_contiguous():
+                    y = y.contiguous()
+                _bias_act(code, y.view(-1, y.shape[3]), conv.bias, slope)
             hs.append(y)
             h = y
         if self.tail == "maxpool":
@@ -258,6 +269,68 @@ class _Trunk:
                 _bias_act(code, s, None, slope)
             fouts.append(s)
         return s, (hs, None, flat, fouts)
+
+    use_igemm = True   # K28 / K29 for every conv they take (False: MIOpen, the r02 path)
+
+    def _igemm_ok(self, conv):
+        k, st, pd = conv.kernel_size, conv.stride, conv.padding
+        return (self.use_igemm and k[0] == k[1] and st[0] == st[1] and pd[0] == pd[1] and conv.padding_mode == "zeros"
+                and conv.in_channels % 4 == 0 and conv.weight.is_contiguous()
+                and bool(ops.lib().xpa_conv_igemm_ok(conv.in_channels, conv.out_channels, k[0])))
+
+    def _igemm_dgrad_ok(self, conv):
+        k, st = conv.kernel_size, conv.stride
+        return (self._igemm_ok(conv) and st[0] <= 2 and conv.out_channels % 4 == 0
+                and bool(ops.lib().xpa_conv_igemm_ok(conv.out_channels, conv.in_channels, k[0])))
+
+    @staticmethod
+    def _conv_fwd(conv, code, slope, h):
+        """K28 forward: act(conv(h) + b), h NHWC f32 [B, H, W, C] -> NHWC [B, OH, OW, out]."""
+        B, H, W, C = h.shape
+        k, st, pd = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        OH, OW = (H + 2 * pd - k) // st + 1, (W + 2 * pd - k) // st + 1
+        h = h if h.is_contiguous() else h.contiguous()
+        y = torch.empty((B, OH, OW, conv.out_channels), dtype=torch.float32, device=h.device)
+        _lib.check(ops.lib().xpa_conv_fwd(code, ops._p(h), B, H, W, C, ops._p(conv.weight), ops._p(conv.bias),
+                                          conv.out_channels, k, st, pd, float(slope), ops._p(y), ops._stream(h.device)),
+                   "xpa_conv_fwd")
+        return y
+
+    def _conv_wgrad(self, conv, g, act, slope, y, x):
+        """K29: conv.weight.grad (and with act >= 0: g * act'(y) is the operand and conv.bias.grad is written too) from
+        g NHWC [B, OH, OW, out] and the block's input x NHWC f32 [B, H, W, in]."""
+        L, st = ops.lib(), ops._stream(g.device)
+        B, H, W, C = x.shape
+        k = conv.kernel_size[0]
+        cout, cols = conv.out_channels, k * k * C
+        G = int(L.xpa_conv_wgrad_num_partials())
+        part = self.parts.buf(("wg", cout, cols), (G, cout * cols), g.device)
+        bpart = self.parts.buf(("wgb", cout), (G, cout), g.device) if act >= 0 else None
+        g = g if g.is_contiguous() else g.contiguous()
+        _lib.check(L.xpa_conv_wgrad(act, ops._p(g), ops._p(y) if act >= 0 else None, float(slope), ops._p(x), B, H, W, C,
+                                    cout, k, conv.stride[0], conv.padding[0], ops._p(part), ops._p(bpart), st),
+                   "xpa_conv_wgrad")
+        _lib.check(L.xpa_colsum_finalize(ops._p(part), G, cout * cols, ops._p(conv.weight.grad), st), "colsum dW")
+        if act >= 0:
+            _lib.check(L.xpa_colsum_finalize(ops._p(bpart), G, cout, ops._p(conv.bias.grad), st), "colsum db")
+
+    def _conv_dgrad(self, conv, dz, x_shape, prev):
+        """K28 data gradient from dz (the block's pre-activation gradient, NHWC) into the block's input; prev = (code,
+        slope, y_prev, bias_grad_prev) of the previous block: its activation backward and bias gradient fused in (the
+        result is then that block's dz)."""
+        L, st = ops.lib(), ops._stream(dz.device)
+        B, H, W, Cin = x_shape
+        k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        OH, OW = dz.shape[1], dz.shape[2]
+        dx = torch.empty((B, H, W, Cin), dtype=torch.float32, device=dz.device)
+        code, slope, y_prev, bgrad = prev
+        G = int(L.xpa_conv_dgrad_num_partials(B, H, W))
+        bpart = self.parts.buf(("dgb", B * H * W, Cin), (G, Cin), dz.device)
+        dz = dz if dz.is_contiguous() else dz.contiguous()
+        _lib.check(L.xpa_conv_dgrad(ops._p(dz), B, OH, OW, conv.out_channels, ops._p(conv.weight), Cin, k, s, p, H, W,
+                                    code, ops._p(y_prev), float(slope), ops._p(dx), ops._p(bpart), st), "xpa_conv_dgrad")
+        _lib.check(L.xpa_colsum_finalize(ops._p(bpart), G, Cin, ops._p(bgrad), st), "colsum db (dgrad)")
+        return dx
 
     @staticmethod
     def _k26_ok(conv, x0):
@@ -327,8 +400,10 @@ class _Trunk:
                 else:
                     torch.mm(g.t(), x_in, out=lin.weight.grad)
                     g = torch.mm(g, lin.weight)
-        # conv blocks, last to first; g is the NHWC gradient of the last conv block's output (flatten tail) or, for
-        # the max-pool tail, K24 forms the last block's dz from the pooled gradient
+        # conv blocks, last to first.  g is the NHWC gradient of the block's output (after its activation), or — once
+        # a fused step has applied the activation backward (K24 for the max-pool tail, K28's data gradient epilogue) —
+        # its pre-activation gradient dz (g_dz), with that block's bias gradient already written.
+        g_dz = False
         for i in range(len(self.convs) - 1, -1, -1):
             conv, code, slope = self.convs[i]
             y = hs[i + 1]
@@ -345,30 +420,42 @@ class _Trunk:
                            "xpa_maxpool_act_bwd_bias")
                 _lib.check(L.xpa_colsum_finalize(ops._p(part), part.shape[0], Cy, ops._p(conv.bias.grad), st),
                            "xpa_colsum_finalize")
-                g = dz
+                g, g_dz = dz, True
             else:
                 g = g.reshape(y.shape)
                 if not g.is_contiguous():
                     g = g.contiguous()
-                if i == 0 and self._k26_ok(conv, hs[0]):
-                    # K26 with the activation backward + bias gradient folded in (no K22 pass over conv1's output)
-                    self._conv1_wgrad(conv, g, hs[0], act=(code, slope, y))
-                    break
-                _act_bwd_bias(parts, code, g.view(-1, Cy), y.view(-1, Cy), slope, conv.bias.grad)
-            need_in = i > 0
             if i == 0 and self._k26_ok(conv, hs[0]):
-                self._conv1_wgrad(conv, g, hs[0])   # K26: from the uint8 frames, no f32 frame copy
+                # K26 from the uint8 frames: with the activation backward + bias gradient folded in unless done
+                self._conv1_wgrad(conv, g, hs[0], act=None if g_dz else (code, slope, y))
                 break
             x_in = self.frames(hs[i]) if hs[i].dtype == torch.uint8 else hs[i]
-            k27 = need_in and self._dgrad_ok(conv)
-            gx, gw, _ = torch.ops.aten.convolution_backward(
-                g.permute(0, 3, 1, 2), x_in.permute(0, 3, 1, 2), conv.weight, None, list(conv.stride),
-                list(conv.padding), [1, 1], False, [0, 0], 1, [need_in and not k27, True, False])
-            conv.weight.grad.copy_(gw)
-            if k27:
-                g = self._dgrad(conv, g, x_in.shape)
-            elif need_in:
-                g = gx.permute(0, 2, 3, 1)
+            ig = self._igemm_ok(conv)
+            need_in = i > 0
+            if not g_dz and (need_in or not ig):
+                # the data gradient (and the library weight gradient) read dz: K22 in place, + the bias gradient
+                _act_bwd_bias(parts, code, g.view(-1, Cy), y.view(-1, Cy), slope, conv.bias.grad)
+                g_dz = True
+            if ig:   # K29 (with the activation backward + bias gradient folded in when g is not dz yet)
+                self._conv_wgrad(conv, g, -1 if g_dz else code, slope, y, x_in)
+            if not ig or (need_in and not self._dgrad_ok(conv) and not self._igemm_dgrad_ok(conv)):
+                k27 = need_in and self._dgrad_ok(conv)
+                gx, gw, _ = torch.ops.aten.convolution_backward(
+                    g.permute(0, 3, 1, 2), x_in.permute(0, 3, 1, 2), conv.weight, None, list(conv.stride),
+                    list(conv.padding), [1, 1], False, [0, 0], 1, [need_in and not k27, not ig, False])
+                if not ig:
+                    conv.weight.grad.copy_(gw)
+                if need_in and not k27:
+                    g, g_dz = gx.permute(0, 2, 3, 1), False
+                    continue
+            if not need_in:
+                break
+            if self._dgrad_ok(conv):   # K27 (the stride-2 32 -> 64 conv): the previous block's g, not dz
+                g, g_dz = self._dgrad(conv, g, x_in.shape), False
+            else:                      # K28's data gradient with the previous block's activation backward + bias
+                pconv, pcode, pslope = self.convs[i - 1]
+                g = self._conv_dgrad(conv, g, tuple(x_in.shape), (pcode, pslope, hs[i], pconv.bias.grad))
+                g_dz = True
         self.stale = True   # the optimizer step that follows changes the fc weight
 
 
