@@ -583,6 +583,7 @@ int xpa_maxpool_act_bwd_bias(int act, const float *dout, const int32_t *argmax, 
  * [out_c][in_c][kernel][kernel]; in_c a multiple of 4, <= 64; out_c <= 64; xpa_conv_igemm_ok(in_c, out_c, kernel)
  * tells whether the weight image fits the 160 KiB LDS (the forward and, with the channel counts swapped, the data
  * gradient).  act: 0 identity, 1 LeakyReLU(slope) / ReLU (slope 0), 2 tanh.
+ * The operands must each be under 2 GiB (32-bit buffer offsets).
  * xpa_conv_fwd: y = act(conv(x, w) + bias) [batch, OH, OW, out_c] (bias nullable).
  * xpa_conv_dgrad: dx [batch, in_h, in_w, in_c] = the data gradient of the conv from dy [batch, out_h, out_w, out_c]
  *   (stride 1 or 2); with act_prev >= 0, dx = that * act'(y_prev) (the previous block's activation backward, act' from
@@ -603,6 +604,9 @@ int64_t xpa_conv_wgrad_num_partials(void);
 int xpa_conv_wgrad(int act, const float *g, const float *y, float slope, const float *x, int64_t batch, int64_t in_h,
                    int64_t in_w, int64_t in_c, int64_t out_c, int64_t kernel, int64_t stride, int64_t pad,
                    float *partial, float *bias_partial, xpa_stream_t stream);
+/* Diagnostics: on != 0 makes xpa_conv_wgrad take its streaming form (operands straight from global memory) even where
+ * the LDS-slab form applies (both give the same sums up to f32 association; process-global, not thread-safe). */
+void xpa_conv_wgrad_force_stream(int on);
 
 #ifdef __cplusplus
 }

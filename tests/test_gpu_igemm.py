@@ -55,8 +55,8 @@ def test_conv_dgrad_matches_f64(shape):
     from xuanpolicy_amd import _lib, ops
     B, H, W, Cin, Cout, k, s = shape
     p = (k - s) // 2
-    if not ops.lib().xpa_conv_igemm_ok(Cout, Cin, k):
-        pytest.skip("weight image of the data gradient does not fit the LDS")
+    if not ops.lib().xpa_conv_igemm_ok(Cout, Cin, k) or s > 2:
+        pytest.skip("data gradient taken by K28 for stride <= 2 and a weight image that fits the LDS")
     x, w, _ = _data(*shape, seed=2)
     OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
     g = torch.Generator().manual_seed(3)
@@ -83,9 +83,12 @@ def test_conv_dgrad_matches_f64(shape):
 
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("fold_act", [False, True])
-def test_conv_wgrad_matches_f64(shape, fold_act):
-    """dW = sum over output pixels of dz x; fold_act: the operand is g * act'(y) and the bias gradient comes too."""
+@pytest.mark.parametrize("form", ["slab", "stream"])
+def test_conv_wgrad_matches_f64(shape, fold_act, form):
+    """dW = sum over output pixels of dz x; fold_act: the operand is g * act'(y) and the bias gradient comes too.  Both
+    K29 forms: the LDS-slab one (every shape here) and the streaming one (forced)."""
     from xuanpolicy_amd import _lib, ops
+    ops.lib().xpa_conv_wgrad_force_stream(1 if form == "stream" else 0)
     B, H, W, Cin, Cout, k, s = shape
     p = (k - s) // 2
     x, w, b = _data(*shape, seed=4)
@@ -103,9 +106,12 @@ def test_conv_wgrad_matches_f64(shape, fold_act):
     part = torch.full((G, cols), float("nan"), device=DEV)
     bpart = torch.full((G, Cout), float("nan"), device=DEV)
     xd, gd, yd = x.to(DEV), gr.to(DEV), y.to(DEV)
-    _lib.check(L.xpa_conv_wgrad(1 if fold_act else -1, ops._p(gd), ops._p(yd) if fold_act else None, 0.0, ops._p(xd), B,
-                                H, W, Cin, Cout, k, s, p, ops._p(part), ops._p(bpart) if fold_act else None,
-                                ops._stream(DEV)), "xpa_conv_wgrad")
+    try:
+        _lib.check(L.xpa_conv_wgrad(1 if fold_act else -1, ops._p(gd), ops._p(yd) if fold_act else None, 0.0,
+                                    ops._p(xd), B, H, W, Cin, Cout, k, s, p, ops._p(part),
+                                    ops._p(bpart) if fold_act else None, ops._stream(DEV)), "xpa_conv_wgrad")
+    finally:
+        L.xpa_conv_wgrad_force_stream(0)
     dw = torch.empty(Cout, Cin, k, k, device=DEV)
     _lib.check(L.xpa_colsum_finalize(ops._p(part), G, cols, ops._p(dw), ops._stream(DEV)), "finalize")
     tol = 2e-6 * float(dw_ref.abs().max()) + 1e-6 * (B * OH * OW) ** 0.5

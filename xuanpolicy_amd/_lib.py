@@ -131,6 +131,7 @@ SIGNATURES = {
     "xpa_conv_dgrad": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
                                       ctypes.c_int, c_p, c_f32, c_p, c_p, c_p]),
     "xpa_conv_wgrad_num_partials": (c_i64, []),
+    "xpa_conv_wgrad_force_stream": (None, [ctypes.c_int]),
     "xpa_conv_wgrad": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_f32, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
                                       c_i64, c_p, c_p, c_p]),
     "xpa_rollout_bootstrap_fixup": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p]),

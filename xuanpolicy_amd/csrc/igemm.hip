@@ -21,11 +21,11 @@
 //   (a register ring that runs on across row blocks).
 // K29 xpa_conv_wgrad: dW[n, c, tap] = sum_m dz[m, n] in[pixel(m, tap), c] (the forward's pixel map): a long-K GEMM
 //   over the rows, split over the grid (one partial [COUT, CIN, K, K] per block, summed in f64 by xpa_colsum_finalize
-//   straight into the weight-gradient layout).  Wave = COUTP x (CTW column tiles of 32 (tap, channel) columns); every
-//   wave of a block streams the block's rows two at a time (the MFMA's k = the row pair: lane (h, i) loads dz[row 2p + h,
-//   32 nt + i] and in[pixel(row 2p + h, tap_j), c_j] for its column j = i), four row pairs prefetched.  With act >= 0 the
-//   operand is g * act'(y) (the block's own activation backward folded in: K22 is not run) and wave 0 also writes the
-//   bias-gradient partials.
+//   straight into the weight-gradient layout).  Wave = COUT x (TC column tiles of 16 (tap, channel) columns); every
+//   wave of a block streams the block's rows four at a time (v_mfma_f32_16x16x4_f32, the MFMA's k = 4 rows: lane (kk, i)
+//   loads dz[row 4q + kk, 16 nt + i] and in[pixel(row 4q + kk, tap_j), c_j] for its column j = i), two quads prefetched.
+//   With act >= 0 the operand is g * act'(y) (the block's own activation backward folded in: K22 is not run) and wave 0
+//   also writes the bias-gradient partials.
 #include "xpa_common.h"
 
 namespace {
@@ -33,8 +33,9 @@ namespace {
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kIgThreads = 512;
-constexpr int kIgRows = 512;             // rows per block step (8 waves x 64)
+constexpr int kIgThreads = 1024;         // 16 waves: 4 per SIMD (load latency hidden by the other waves)
+constexpr int kIgMT = 1;                 // 32-row m-tiles per wave
+constexpr int kIgRows = kIgThreads / 64 * 32 * kIgMT;  // rows per block step
 constexpr int kIgLdsFloats = 40960;      // 160 KiB: the whole weight image
 constexpr int kIgGrid = 256;             // one block per CU
 
@@ -54,6 +55,7 @@ __device__ __forceinline__ float ig_grad(float d, float y, float slope) {  // d 
 
 struct IgArgs {
     const float *in;     // NHWC [B, IH, IW, CIN]
+    int64_t in_bytes;    // < 2^31: the loads use 32-bit buffer offsets
     const float *w;      // torch layout: forward [COUT][CIN][K][K]; dgrad [CIN][COUT][K][K] (= the forward weight)
     const float *bias;   // forward: [COUT] (nullable)
     const float *yprev;  // dgrad: the previous block's output, NHWC like out (nullable: no activation backward)
@@ -102,13 +104,22 @@ __global__ __launch_bounds__(kIgThreads, 1) void conv_igemm_kernel(IgArgs a) {
     const int nch = taps * CPT;
     // ---- the weight image [tap][q][n][4] ----
     const int img = taps * CQ * COUTP * 4;
-    for (int e = t; e < img; e += kIgThreads) {
-        const int cc = e & 3, n = (e >> 2) % COUTP, q = ((e >> 2) / COUTP) % CQ, tap = e / (4 * COUTP * CQ);
-        const int c = 4 * q + cc, ky = tap / a.K, kx = tap - (tap / a.K) * a.K;
-        float v = 0.f;
-        if (n < a.COUT && c < a.CIN)
-            v = MODE == 0 ? a.w[((n * a.CIN + c) * a.K + ky) * a.K + kx] : a.w[((c * a.COUT + n) * a.K + ky) * a.K + kx];
-        sB[e] = v;
+    // 8 loads in flight per thread (a load-wait-store loop here costs ~36 serial L2 latencies per block)
+    for (int e0 = t; e0 < img; e0 += 8 * kIgThreads) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + u * kIgThreads;
+            const int cc = e & 3, n = (e >> 2) % COUTP, q = ((e >> 2) / COUTP) % CQ, tap = e / (4 * COUTP * CQ);
+            const int c = 4 * q + cc, ky = tap / a.K, kx = tap - (tap / a.K) * a.K;
+            v[u] = 0.f;
+            if (e < img && n < a.COUT && c < a.CIN)
+                v[u] = MODE == 0 ? a.w[((n * a.CIN + c) * a.K + ky) * a.K + kx]
+                                 : a.w[((c * a.COUT + n) * a.K + ky) * a.K + kx];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (e0 + u * kIgThreads < img) sB[e0 + u * kIgThreads] = v[u];
     }
     __syncthreads();
     const int64_t g0 = a.nblk * blockIdx.x / gridDim.x, g1 = a.nblk * (blockIdx.x + 1) / gridDim.x;
@@ -123,10 +134,10 @@ __global__ __launch_bounds__(kIgThreads, 1) void conv_igemm_kernel(IgArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) bsum[nt] = 0.f;
     const int64_t ohw = (int64_t)a.OH * a.OW;
-    auto geometry = [&](int64_t blk, IgRow (&rr)[2]) {
+    auto geometry = [&](int64_t blk, IgRow (&rr)[kIgMT]) {
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-            const int64_t m = blk * kIgRows + wave * 64 + mt * 32 + i;
+        for (int mt = 0; mt < kIgMT; ++mt) {
+            const int64_t m = blk * kIgRows + wave * 32 * kIgMT + mt * 32 + i;
             const bool ok = m < a.rows;
             const int64_t mc = ok ? m : 0;
             const int64_t b = mc / ohw;
@@ -137,34 +148,47 @@ __global__ __launch_bounds__(kIgThreads, 1) void conv_igemm_kernel(IgArgs a) {
             rr[mt].ok = ok;
         }
     };
-    auto load_chunk = [&](f4v (&v)[2][CJ], const IgRow (&rr)[2], int k) {
+    // A operand through a range-checked buffer descriptor: a padding tap or a ragged row gets an offset past the
+    // record count and the hardware returns zeros, so no select sits between the load and its use and the wait for
+    // chunk k + 1 lands after chunk k's MFMAs (a select right after the load would expose the whole load latency)
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(a.in), 0, (int)a.in_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, (int)(a.rows * a.COUT * 4),
+                                                                          0x00020000);
+    auto load_chunk = [&](f4v (&v)[kIgMT][CJ], const IgRow (&rr)[kIgMT], int k) {
         const int tap = k / CPT, jb = (k - tap * CPT) * CJ;
         const int ky = tap / a.K, kx = tap - (tap / a.K) * a.K;
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
+        for (int mt = 0; mt < kIgMT; ++mt) {
             bool valid;
             const int pix = ig_pixel<MODE>(a, rr[mt], ky, kx, valid);
-            const float *p = a.in + (int64_t)pix * a.CIN;
+            const int off = valid ? pix * a.CIN * 4 : INT32_MIN;
 #pragma unroll
             for (int j = 0; j < CJ; ++j) {
                 const int q = 2 * (jb + j) + h;
-                const bool qv = valid && 4 * q < a.CIN;
-                const f4v d = *reinterpret_cast<const f4v *>(p + (qv ? 4 * q : 0));
-                const f4v z = {0.f, 0.f, 0.f, 0.f};
-                v[mt][j] = qv ? d : z;
+                const int o = 4 * q < a.CIN ? off + 16 * q : INT32_MIN;
+                v[mt][j] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, 0));
             }
         }
     };
     if (g0 >= g1) return;
-    IgRow cur[2], nxt[2];
+    IgRow cur[kIgMT], nxt[kIgMT];
     geometry(g0, cur);
-    f4v va[2][CJ], vb[2][CJ];
+    f4v va[kIgMT][CJ], vb[kIgMT][CJ];
     load_chunk(va, cur, 0);
+    // The first chunk is waited for here, before the loop: with its loads still pending at the loop header the
+    // compiler's wait for them (merged with the back edge) becomes vmcnt(0) at the first MFMA of EVERY chunk, which
+    // drains the prefetch of chunk k + 1 too and exposes its whole latency.  Inside the loop the only wait is then at
+    // the va <- vb copy after chunk k's MFMAs.
+#pragma unroll
+    for (int mt = 0; mt < kIgMT; ++mt)
+#pragma unroll
+        for (int j = 0; j < CJ; ++j) asm volatile("" ::"v"(va[mt][j]));
     for (int64_t blk = g0; blk < g1; ++blk) {
         const bool more = blk + 1 < g1;
-        f32x16 acc[2][NT];
+        f32x16 acc[kIgMT][NT];
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
+        for (int mt = 0; mt < kIgMT; ++mt)
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -190,7 +214,7 @@ __global__ __launch_bounds__(kIgThreads, 1) void conv_igemm_kernel(IgArgs a) {
 #pragma unroll
                 for (int cc = 0; cc < 4; ++cc)
 #pragma unroll
-                    for (int mt = 0; mt < 2; ++mt)
+                    for (int mt = 0; mt < kIgMT; ++mt)
 #pragma unroll
                         for (int nt = 0; nt < NT; ++nt)
                             acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(va[mt][j][cc], b4[nt][cc], acc[mt][nt],
@@ -198,35 +222,57 @@ __global__ __launch_bounds__(kIgThreads, 1) void conv_igemm_kernel(IgArgs a) {
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+            for (int mt = 0; mt < kIgMT; ++mt)
 #pragma unroll
-                for (int j = 0; j < CJ; ++j) va[mt][j] = vb[mt][j];
+                for (int j = 0; j < CJ; ++j) {
+                    va[mt][j] = vb[mt][j];
+                    asm volatile("" ::"v"(va[mt][j]));
+                }
         }
-        // C/D map: row = (r & 3) + 8 (r >> 2) + 4 h of the m-tile, column n = 32 nt + i
+        // C/D map: row = (r & 3) + 8 (r >> 2) + 4 h of the m-tile, column n = 32 nt + i.  Buffer stores (and, for the
+        // data gradient, loads of y_prev) with out-of-range offsets for ragged rows / padded columns: no branches, and
+        // the 16 y_prev loads of an n-tile are all in flight before the first is used
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
+        for (int mt = 0; mt < kIgMT; ++mt)
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
                 const int n = 32 * nt + i;
+                const int64_t m0 = blk * kIgRows + wave * 32 * kIgMT + mt * 32 + 4 * h;
+                auto offset = [&](int r) -> int {
+                    const int64_t m = m0 + (r & 3) + 8 * (r >> 2);
+                    return m < a.rows && n < a.COUT ? (int)(m * a.COUT + n) * 4 : INT32_MIN;
+                };
+                if (MODE == 0) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int64_t m = blk * kIgRows + wave * 64 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (m < a.rows && n < a.COUT) {
-                        const int64_t o = m * a.COUT + n;
-                        if (MODE == 0) {
-                            a.out[o] = ig_act<ACT>(acc[mt][nt][r] + bn[nt], a.slope);
-                        } else {
-                            float v = acc[mt][nt][r];
-                            if (ACT >= 0 && a.yprev) v = ig_grad<ACT>(v, a.yprev[o], a.slope);
-                            a.out[o] = v;
-                            bsum[nt] += v;
+                    for (int r = 0; r < 16; ++r)
+                        __builtin_amdgcn_raw_buffer_store_b32(
+                            __builtin_bit_cast(unsigned, ig_act<ACT>(acc[mt][nt][r] + bn[nt], a.slope)), rout,
+                            offset(r), 0, 0);
+                } else {
+#pragma unroll
+                    for (int r0 = 0; r0 < 16; r0 += 8) {   // 8 y_prev loads in flight at a time
+                        float yp[8];
+                        if (ACT >= 0) {
+#pragma unroll
+                            for (int r = 0; r < 8; ++r) {
+                                const int o = offset(r0 + r);
+                                yp[r] = a.yprev[o != INT32_MIN ? o / 4 : 0];   // dropped rows: any valid address
+                            }
+                        }
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) {
+                            const int o = offset(r0 + r);
+                            float v = acc[mt][nt][r0 + r];
+                            if (ACT >= 0) v = ig_grad<ACT>(v, yp[r], a.slope);
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rout, o, 0, 0);
+                            bsum[nt] += o != INT32_MIN ? v : 0.f;
                         }
                     }
                 }
             }
         if (more) {
-            cur[0] = nxt[0];
-            cur[1] = nxt[1];
+#pragma unroll
+            for (int mt = 0; mt < kIgMT; ++mt) cur[mt] = nxt[mt];
         }
     }
     if (MODE == 1 && a.bias_partial) {
@@ -247,32 +293,42 @@ __global__ __launch_bounds__(kIgThreads, 1) void conv_igemm_kernel(IgArgs a) {
 }
 
 // ---- K29: weight gradient ------------------------------------------------------------------------------------------
+// v_mfma_f32_16x16x4_f32 (k = 4 rows per instruction): lane (kk, i) supplies dz[row 4 s + kk][16 nt + i] (A) and
+// in[pixel(row 4 s + kk, tap_j), c_j] (B, column j = 16 ct + i of the wave's tiles).  A wave holds TN x TC 16 x 16 tiles
+// (TN = COUT / 16 row tiles, TC column tiles: 4 x 9 = 36 tiles = 144 accumulator registers at C3's conv3), so one load
+// feeds TC (A) or TN (B) MFMAs: TN + TC 4-B loads per 4 rows and TN TC MFMAs (13 loads per 36 MFMAs at conv3).
 constexpr int kWgGrid = 512;
-constexpr int kWgMaxWaves = 8;
+constexpr int kWgMaxWaves = 16;
 
 struct WgArgs {
     const float *g;      // NHWC [rows, COUT]: d loss / d output (after the activation when act < 0)
     const float *y;      // the block's forward output (act >= 0), NHWC like g
-    const float *in;     // NHWC [B, IH, IW, CIN]: the block's input
+    const float *in;     // NHWC [B, IH, IW, CIN]
+    int64_t in_bytes;    // < 2^31: the loads use 32-bit buffer offsets: the block's input
     float *partial;      // [gridDim.x][COUT][CIN][K][K]
     float *bias_partial; // [gridDim.x][COUT] (nullable; act >= 0)
     int64_t rows;
     int IH, IW, CIN, OH, OW, COUT, K, S, P, ncols;  // ncols = K K CIN
     float slope;
+    // the LDS-slab form (conv_wgrad_lds_kernel): R output rows of one image per slab, nsl slabs per image; the x slab
+    // [(R - 1) S + K][PW][CS] (zero-padded, CS = channel stride), then the dz slab [ceil4(R OW)][COUTS]
+    int R, nsl, PW, CS, COUTS, xs_floats;
+    int64_t nslabs;
 };
 
-template <int NTN, int CTW, int ACT>
-__global__ __launch_bounds__(64 * kWgMaxWaves) void conv_wgrad_kernel(WgArgs a) {
-    const int t = threadIdx.x, lane = t & 63, h = lane >> 5, i = lane & 31;
+template <int TN, int TC, int ACT>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgArgs a) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const int t = threadIdx.x, lane = t & 63, kk = lane >> 4, i = lane & 15;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int64_t pairs = (a.rows + 1) / 2;
-    const int64_t p0 = pairs * blockIdx.x / gridDim.x, p1 = pairs * (blockIdx.x + 1) / gridDim.x;
-    // this lane's columns: (tap, channel) of column 32 ct + i of the wave's tiles
-    int cky[CTW], ckx[CTW], cch[CTW];
-    bool cok[CTW];
+    const int64_t quads = (a.rows + 3) / 4;
+    const int64_t q0 = quads * blockIdx.x / gridDim.x, q1 = quads * (blockIdx.x + 1) / gridDim.x;
+    // this lane's columns: (tap, channel) of column 16 ct + i of the wave's tiles
+    int cky[TC], ckx[TC], cch[TC];
+    bool cok[TC];
 #pragma unroll
-    for (int j = 0; j < CTW; ++j) {
-        const int gc = (wave * CTW + j) * 32 + i;
+    for (int j = 0; j < TC; ++j) {
+        const int gc = (wave * TC + j) * 16 + i;
         cok[j] = gc < a.ncols;
         const int gcc = cok[j] ? gc : 0;
         const int tap = gcc / a.CIN;
@@ -280,48 +336,43 @@ __global__ __launch_bounds__(64 * kWgMaxWaves) void conv_wgrad_kernel(WgArgs a) 
         cky[j] = tap / a.K;
         ckx[j] = tap - cky[j] * a.K;
     }
-    f32x16 acc[NTN][CTW];
+    f4 acc[TN][TC];
 #pragma unroll
-    for (int nt = 0; nt < NTN; ++nt)
+    for (int nt = 0; nt < TN; ++nt)
 #pragma unroll
-        for (int j = 0; j < CTW; ++j)
+        for (int j = 0; j < TC; ++j) acc[nt][j] = f4{0.f, 0.f, 0.f, 0.f};
+    float bsum[TN];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[nt][j][r] = 0.f;
-    float bsum[NTN];
-#pragma unroll
-    for (int nt = 0; nt < NTN; ++nt) bsum[nt] = 0.f;
-    // this lane's row 2 p + h, tracked as (b, oy, ox)
-    int64_t m = 2 * p0 + h;
+    for (int nt = 0; nt < TN; ++nt) bsum[nt] = 0.f;
+    // this lane's row 4 q + kk, tracked as (b, oy, ox)
+    int64_t m = 4 * q0 + kk;
     const int64_t ohw = (int64_t)a.OH * a.OW;
     int64_t b = m / ohw;
     int rem = (int)(m - b * ohw);
     int oy = rem / a.OW, ox = rem - (rem / a.OW) * a.OW;
-    constexpr int U = 4;
-    float an[U][NTN], xn[U][CTW];
-    auto load_group = [&](int64_t pp) {
+    constexpr int U = 2;
+    float an[U][TN], xn[U][TC];
+    // range-checked buffer loads (offset past the record count -> 0): no select between a load and its MFMA, so the
+    // waits for group qq + U land after group qq's MFMAs; act'(0) x 0 = 0, so a dropped row contributes nothing
+    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.g), 0,
+                                                                        (int)(a.rows * a.COUT * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(ACT >= 0 ? a.y : a.g), 0,
+                                                                        (int)(a.rows * a.COUT * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.in), 0,
+                                                                        (int)a.in_bytes, 0x00020000);
+    float yn[U][TN];   // act >= 0: the block's output at the g rows, act' applied at use (not right after the load)
+    auto load_group = [&](int64_t qq) {
+        // the U rows' geometry first (the carry loop is control flow), then the loads as one straight-line run
+        int go[U], gy[U], gx[U], gp[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const bool mv = pp + u < p1 && m < a.rows;
-            const int64_t mc = mv ? m : 0;
-#pragma unroll
-            for (int nt = 0; nt < NTN; ++nt) {
-                const int n = 32 * nt + i;
-                const bool ok = mv && n < a.COUT;
-                const int64_t o = mc * a.COUT + (n < a.COUT ? n : 0);
-                float v = a.g[o];
-                if (ACT >= 0) v = ig_grad<ACT>(v, a.y[o], a.slope);
-                an[u][nt] = ok ? v : 0.f;
-            }
-            const int pixb = (int)((mv ? b : 0) * a.IH);
-#pragma unroll
-            for (int j = 0; j < CTW; ++j) {
-                const int iy = oy * a.S - a.P + cky[j], ix = ox * a.S - a.P + ckx[j];
-                const bool inb = mv && cok[j] && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
-                const float v = a.in[((int64_t)(pixb + (inb ? iy : 0)) * a.IW + (inb ? ix : 0)) * a.CIN + cch[j]];
-                xn[u][j] = inb ? v : 0.f;
-            }
-            m += 2;
-            ox += 2;
+            const bool mv = qq + u < q1 && m < a.rows;
+            go[u] = mv ? (int)m * a.COUT * 4 : INT32_MIN;
+            gy[u] = mv ? oy * a.S - a.P : INT32_MIN / 2;   // an out-of-range row for every tap
+            gx[u] = ox * a.S - a.P;
+            gp[u] = (int)b * a.IH;
+            m += 4;
+            ox += 4;
             while (ox >= a.OW) {
                 ox -= a.OW;
                 if (++oy >= a.OH) {
@@ -330,58 +381,262 @@ __global__ __launch_bounds__(64 * kWgMaxWaves) void conv_wgrad_kernel(WgArgs a) 
                 }
             }
         }
-    };
-    if (p0 < p1) load_group(p0);
-    for (int64_t pp = p0; pp < p1; pp += U) {
-        float av[U][NTN], xv[U][CTW];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
 #pragma unroll
-            for (int nt = 0; nt < NTN; ++nt) av[u][nt] = an[u][nt];
+            for (int nt = 0; nt < TN; ++nt) {
+                const int n = 16 * nt + i;
+                const int o = n < a.COUT ? go[u] + 4 * n : INT32_MIN;
+                an[u][nt] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, o, 0, 0));
+                if (ACT >= 0) yn[u][nt] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, o, 0, 0));
+            }
 #pragma unroll
-            for (int j = 0; j < CTW; ++j) xv[u][j] = xn[u][j];
+            for (int j = 0; j < TC; ++j) {
+                const int iy = gy[u] + cky[j], ix = gx[u] + ckx[j];
+                const bool inb = cok[j] && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
+                const int o = inb ? (((gp[u] + iy) * a.IW + ix) * a.CIN + cch[j]) * 4 : INT32_MIN;
+                xn[u][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, o, 0, 0));
+            }
         }
-        if (pp + U < p1) load_group(pp + U);
+    };
+    if (q0 < q1) load_group(q0);
+    for (int64_t qq = q0; qq < q1; qq += U) {
+        float av[U][TN], xv[U][TC];
+        // group qq's loads (issued one MFMA phase ago) are waited for HERE, before group qq + U's are issued: the
+        // empty asm pins the wait to the copy (left to itself the compiler waits at the first MFMA with vmcnt(0),
+        // draining the new group's loads too)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int nt = 0; nt < TN; ++nt) {
+                av[u][nt] = ACT >= 0 ? ig_grad<ACT>(an[u][nt], yn[u][nt], a.slope) : an[u][nt];
+                asm volatile("" ::"v"(av[u][nt]));
+            }
+#pragma unroll
+            for (int j = 0; j < TC; ++j) {
+                xv[u][j] = xn[u][j];
+                asm volatile("" ::"v"(xv[u][j]));
+            }
+        }
+        if (qq + U < q1) load_group(qq + U);
         if (ACT >= 0 && wave == 0) {
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int nt = 0; nt < NTN; ++nt) bsum[nt] += av[u][nt];
+                for (int nt = 0; nt < TN; ++nt) bsum[nt] += av[u][nt];
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int nt = 0; nt < NTN; ++nt)
+            for (int nt = 0; nt < TN; ++nt)
 #pragma unroll
-                for (int j = 0; j < CTW; ++j)
-                    acc[nt][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u][nt], xv[u][j], acc[nt][j], 0, 0, 0);
+                for (int j = 0; j < TC; ++j)
+                    acc[nt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][nt], xv[u][j], acc[nt][j], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
     }
-    // D of tile (nt, j): row n = 32 nt + (r & 3) + 8 (r >> 2) + 4 h, column = this wave's column 32 ct + i -> the
-    // weight layout [n][c][ky][kx]
+    // D of tile (nt, j): row n = 16 nt + 4 kk + r, column = this wave's column 16 ct + i -> weight layout [n][c][ky][kx]
     const int taps = a.K * a.K;
     float *pr = a.partial + (int64_t)blockIdx.x * a.COUT * a.ncols;
 #pragma unroll
-    for (int j = 0; j < CTW; ++j) {
+    for (int j = 0; j < TC; ++j) {
         if (!cok[j]) continue;
         const int col = cch[j] * taps + cky[j] * a.K + ckx[j];
 #pragma unroll
-        for (int nt = 0; nt < NTN; ++nt)
+        for (int nt = 0; nt < TN; ++nt)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int n = 32 * nt + (r & 3) + 8 * (r >> 2) + 4 * h;
+            for (int r = 0; r < 4; ++r) {
+                const int n = 16 * nt + 4 * kk + r;
                 if (n < a.COUT) pr[(int64_t)n * a.ncols + col] = acc[nt][j][r];
             }
     }
     if (ACT >= 0 && a.bias_partial && wave == 0) {
 #pragma unroll
-        for (int nt = 0; nt < NTN; ++nt) {
-            const float s = bsum[nt] + __shfl_xor(bsum[nt], 32, 64);
-            const int n = 32 * nt + i;
-            if (h == 0 && n < a.COUT) a.bias_partial[(int64_t)blockIdx.x * a.COUT + n] = s;
+        for (int nt = 0; nt < TN; ++nt) {
+            float s = bsum[nt];
+            s += __shfl_xor(s, 16, 64);
+            s += __shfl_xor(s, 32, 64);
+            const int n = 16 * nt + i;
+            if (kk == 0 && n < a.COUT) a.bias_partial[(int64_t)blockIdx.x * a.COUT + n] = s;
         }
     }
+}
+
+// K29 (LDS-slab form, the one every production shape takes): a block stages one slab — R output rows of one image —
+// at a time: the input rows it reads, zero-padded, as xs[pr][pc][CS] (so no tap needs a bounds check), and its dz rows
+// (act'(y) folded in, zero rows up to a multiple of 4) as dzs[p][COUTS].  CS and COUTS are padded so that the four
+// 16-lane groups of a ds_read_b32 (four consecutive pixels) fall in different 16-bank quarters.  Then every operand is one
+// ds_read_b32 at (pixel base + a per-lane column offset fixed for the whole kernel): per 4 pixels a wave issues TN + TC
+// LDS reads and one add per B read, against TN x TC MFMAs, where the streaming form spent ~10 VALU per global load.
+constexpr int kWsFloats = 19456;   // 76 KiB: two blocks per CU
+bool g_wgrad_stream_only = false;
+
+template <int TN, int TC, int ACT>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_lds_kernel(WgArgs a) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) float sm[kWsFloats];
+    float *xs = sm;
+    float *dzs = sm + a.xs_floats;
+    const int t = threadIdx.x, lane = t & 63, kk = lane >> 4, i = lane & 15;
+    const int nthr = blockDim.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    int coff[TC], cky[TC], ckx[TC], cch[TC];
+    bool cok[TC];
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+        const int gc = (wave * TC + j) * 16 + i;
+        cok[j] = gc < a.ncols;
+        const int gcc = cok[j] ? gc : 0;
+        const int tap = gcc / a.CIN;
+        cch[j] = gcc - tap * a.CIN;
+        cky[j] = tap / a.K;
+        ckx[j] = tap - cky[j] * a.K;
+        coff[j] = (cky[j] * a.PW + ckx[j]) * a.CS + cch[j];
+    }
+    f4 acc[TN][TC];
+#pragma unroll
+    for (int nt = 0; nt < TN; ++nt)
+#pragma unroll
+        for (int j = 0; j < TC; ++j) acc[nt][j] = f4{0.f, 0.f, 0.f, 0.f};
+    float bsum[TN];
+#pragma unroll
+    for (int nt = 0; nt < TN; ++nt) bsum[nt] = 0.f;
+    const int CQ = a.CIN / 4, NQ = a.COUT / 4;
+    const int64_t ohw = (int64_t)a.OH * a.OW;
+    for (int64_t z = blockIdx.x; z < a.nslabs; z += gridDim.x) {
+        const int64_t b = z / a.nsl;
+        const int oy0 = (int)(z - b * a.nsl) * a.R;
+        const int rh = a.OH - oy0 < a.R ? a.OH - oy0 : a.R;
+        const int np = rh * a.OW, np4 = (np + 3) & ~3;
+        const int prh = (rh - 1) * a.S + a.K;
+        __syncthreads();   // the previous slab's reads are done
+        // staging: each thread's loads of a batch are all issued before its LDS writes (a load-wait-write loop costs one
+        // memory latency per element, which at these slab sizes outweighs the slab's MFMAs)
+        constexpr int XB = 6, DB = ACT >= 0 ? 2 : 4;
+        const int nx = prh * a.PW * CQ;
+        const int iy0 = oy0 * a.S - a.P;
+        for (int e0 = t; e0 < nx; e0 += XB * nthr) {
+            f4 v[XB];
+#pragma unroll
+            for (int u = 0; u < XB; ++u) {
+                const int e = e0 + u * nthr;
+                const int c4 = e % CQ, pp = e / CQ, pc = pp % a.PW, pr = pp / a.PW;
+                const int iy = iy0 + pr, ix = pc - a.P;
+                v[u] = f4{0.f, 0.f, 0.f, 0.f};
+                if (e < nx && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW)
+                    v[u] = *reinterpret_cast<const f4 *>(a.in + ((b * a.IH + iy) * a.IW + ix) * a.CIN + 4 * c4);
+            }
+#pragma unroll
+            for (int u = 0; u < XB; ++u) {
+                const int e = e0 + u * nthr;
+                if (e < nx) *reinterpret_cast<f4 *>(xs + (e / CQ) * a.CS + 4 * (e % CQ)) = v[u];
+            }
+        }
+        const int nd = np4 * NQ;
+        const int64_t row0 = b * ohw + (int64_t)oy0 * a.OW;
+        for (int e0 = t; e0 < nd; e0 += DB * nthr) {
+            f4 v[DB], yy[DB];
+#pragma unroll
+            for (int u = 0; u < DB; ++u) {
+                const int e = e0 + u * nthr;
+                const int n4 = e % NQ, p = e / NQ;
+                v[u] = f4{0.f, 0.f, 0.f, 0.f};
+                yy[u] = v[u];
+                if (e < nd && p < np) {
+                    const int64_t o = (row0 + p) * a.COUT + 4 * n4;
+                    v[u] = *reinterpret_cast<const f4 *>(a.g + o);
+                    if (ACT >= 0) yy[u] = *reinterpret_cast<const f4 *>(a.y + o);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < DB; ++u) {
+                const int e = e0 + u * nthr;
+                f4 w = v[u];
+                if (ACT >= 0) {
+                    w.x = ig_grad<ACT>(w.x, yy[u].x, a.slope);
+                    w.y = ig_grad<ACT>(w.y, yy[u].y, a.slope);
+                    w.z = ig_grad<ACT>(w.z, yy[u].z, a.slope);
+                    w.w = ig_grad<ACT>(w.w, yy[u].w, a.slope);
+                }
+                if (e < nd) *reinterpret_cast<f4 *>(dzs + (e / NQ) * a.COUTS + 4 * (e % NQ)) = w;
+            }
+        }
+        __syncthreads();
+        // lane (kk, i) takes pixel 4 s + kk of the slab: (row oyr, column ox), advanced by 4 pixels per step
+        int oyr = kk / a.OW, ox = kk - (kk / a.OW) * a.OW;
+        float an[TN], xn[TC];
+        auto load_quad = [&](int s) {
+            const int p = 4 * s + kk;
+            const int base = p < np ? (oyr * a.S * a.PW + ox * a.S) * a.CS : 0;   // dz row p >= np is 0
+#pragma unroll
+            for (int nt = 0; nt < TN; ++nt) an[nt] = dzs[p * a.COUTS + 16 * nt + i];
+#pragma unroll
+            for (int j = 0; j < TC; ++j) xn[j] = xs[base + coff[j]];
+            ox += 4;
+            while (ox >= a.OW) {
+                ox -= a.OW;
+                ++oyr;
+            }
+        };
+        const int nq = np4 / 4;
+        load_quad(0);
+        for (int s = 0; s < nq; ++s) {
+            float av[TN], xv[TC];
+#pragma unroll
+            for (int nt = 0; nt < TN; ++nt) {
+                av[nt] = an[nt];
+                asm volatile("" ::"v"(av[nt]));
+            }
+#pragma unroll
+            for (int j = 0; j < TC; ++j) {
+                xv[j] = xn[j];
+                asm volatile("" ::"v"(xv[j]));
+            }
+            if (s + 1 < nq) load_quad(s + 1);
+            if (ACT >= 0 && wave == 0) {
+#pragma unroll
+                for (int nt = 0; nt < TN; ++nt) bsum[nt] += av[nt];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int nt = 0; nt < TN; ++nt)
+#pragma unroll
+                for (int j = 0; j < TC; ++j)
+                    acc[nt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[nt], xv[j], acc[nt][j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    const int taps = a.K * a.K;
+    float *pr = a.partial + (int64_t)blockIdx.x * a.COUT * a.ncols;
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+        if (!cok[j]) continue;
+        const int col = cch[j] * taps + cky[j] * a.K + ckx[j];
+#pragma unroll
+        for (int nt = 0; nt < TN; ++nt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = 16 * nt + 4 * kk + r;
+                if (n < a.COUT) pr[(int64_t)n * a.ncols + col] = acc[nt][j][r];
+            }
+    }
+    if (ACT >= 0 && a.bias_partial && wave == 0) {
+#pragma unroll
+        for (int nt = 0; nt < TN; ++nt) {
+            float sm4 = bsum[nt];
+            sm4 += __shfl_xor(sm4, 16, 64);
+            sm4 += __shfl_xor(sm4, 32, 64);
+            const int n = 16 * nt + i;
+            if (kk == 0 && n < a.COUT) a.bias_partial[(int64_t)blockIdx.x * a.COUT + n] = sm4;
+        }
+    }
+}
+
+// channel stride with (S x stride) mod 64 in {16, 48}: four consecutive pixels in four different 16-bank quarters
+int ws_pad(int need, int step) {
+    for (int c = need; c < need + 64; c += 4)
+        if ((step * c) % 64 == 16 || (step * c) % 64 == 48) return c;
+    return need;
 }
 
 template <int MODE, int ACT>
@@ -432,10 +687,10 @@ XPA_API int xpa_conv_fwd(int act, const float *x, int64_t batch, int64_t in_h, i
         !ig_shape(in_c, out_c, kernel, cinp, nt) || ((uintptr_t)x % 16))
         return (int)hipErrorInvalidValue;
     const int64_t OH = (in_h + 2 * pad - kernel) / stride + 1, OW = (in_w + 2 * pad - kernel) / stride + 1;
-    if (OH < 1 || OW < 1 || batch * in_h * in_w * in_c >= ((int64_t)1 << 31) || batch * OH * OW >= ((int64_t)1 << 31))
+    if (OH < 1 || OW < 1 || batch * in_h * in_w * in_c * 4 >= ((int64_t)1 << 31) || batch * OH * OW >= ((int64_t)1 << 31))
         return (int)hipErrorInvalidValue;
     IgArgs a{};
-    a.in = x; a.w = w; a.bias = bias; a.out = y;
+    a.in = x; a.in_bytes = batch * in_h * in_w * in_c * 4; a.w = w; a.bias = bias; a.out = y;
     a.rows = batch * OH * OW; a.nblk = (a.rows + kIgRows - 1) / kIgRows;
     a.IH = (int)in_h; a.IW = (int)in_w; a.CIN = (int)in_c; a.OH = (int)OH; a.OW = (int)OW; a.COUT = (int)out_c;
     a.K = (int)kernel; a.S = (int)stride; a.P = (int)pad; a.slope = slope;
@@ -460,10 +715,11 @@ XPA_API int xpa_conv_dgrad(const float *dy, int64_t batch, int64_t out_h, int64_
         !ig_shape(out_c, in_c, kernel, cinp, nt) || ((uintptr_t)dy % 16) ||
         out_h != (in_h + 2 * pad - kernel) / stride + 1 || out_w != (in_w + 2 * pad - kernel) / stride + 1 ||
         out_h < 1 || out_w < 1 || (act_prev >= 0 && !y_prev) ||
-        batch * in_h * in_w * in_c >= ((int64_t)1 << 31) || batch * out_h * out_w * out_c >= ((int64_t)1 << 31))
+        batch * in_h * in_w * in_c >= ((int64_t)1 << 31) || batch * out_h * out_w * out_c * 4 >= ((int64_t)1 << 31))
         return (int)hipErrorInvalidValue;
     IgArgs a{};
-    a.in = dy; a.w = w; a.yprev = act_prev >= 0 ? y_prev : nullptr; a.out = dx; a.bias_partial = bias_partial;
+    a.in = dy; a.in_bytes = batch * out_h * out_w * out_c * 4; a.w = w;
+    a.yprev = act_prev >= 0 ? y_prev : nullptr; a.out = dx; a.bias_partial = bias_partial;
     a.rows = batch * in_h * in_w; a.nblk = (a.rows + kIgRows - 1) / kIgRows;
     a.IH = (int)out_h; a.IW = (int)out_w; a.CIN = (int)out_c; a.OH = (int)in_h; a.OW = (int)in_w; a.COUT = (int)in_c;
     a.K = (int)kernel; a.S = (int)stride; a.P = (int)pad; a.slope = slope;
@@ -476,6 +732,9 @@ XPA_API int xpa_conv_dgrad(const float *dy, int64_t batch, int64_t out_h, int64_
 
 XPA_API int64_t xpa_conv_wgrad_num_partials(void) { return kWgGrid; }
 
+// diagnostics / tests: 1 = always take the streaming K29 form (no LDS slabs)
+XPA_API void xpa_conv_wgrad_force_stream(int on) { g_wgrad_stream_only = on != 0; }
+
 XPA_API int xpa_conv_wgrad(int act, const float *g, const float *y, float slope, const float *x, int64_t batch,
                            int64_t in_h, int64_t in_w, int64_t in_c, int64_t out_c, int64_t kernel, int64_t stride,
                            int64_t pad, float *partial, float *bias_partial, xpa_stream_t stream) {
@@ -484,32 +743,62 @@ XPA_API int xpa_conv_wgrad(int act, const float *g, const float *y, float slope,
         return (int)hipErrorInvalidValue;
     const int64_t OH = (in_h + 2 * pad - kernel) / stride + 1, OW = (in_w + 2 * pad - kernel) / stride + 1;
     const int64_t ncols = kernel * kernel * in_c;
-    const int ntn = out_c <= 32 ? 1 : 2;
-    // column tiles per wave: 3 when the tiles split evenly into <= 8 waves that way (conv3: 18 = 6 x 3), else 4
-    const int64_t nct = (ncols + 31) / 32;
-    const int ctw = (nct % 3 == 0 && nct / 3 <= kWgMaxWaves) ? 3 : 4;
-    const int64_t waves = (nct + ctw - 1) / ctw;
-    if (OH < 1 || OW < 1 || waves > kWgMaxWaves || batch * in_h * in_w * in_c >= ((int64_t)1 << 31) ||
-        batch * OH * OW * out_c >= ((int64_t)1 << 31))
+    const int tn = out_c <= 16 ? 1 : out_c <= 32 ? 2 : 4;
+    // 16-column tiles over 4 waves (more waves only past 4 x 9 tiles): TC = ceil(tiles / 4), rounded to 2 / 4 / 8 / 9
+    const int64_t nct = (ncols + 15) / 16;
+    int tc = (int)((nct + 3) / 4);
+    tc = tc <= 2 ? 2 : tc <= 4 ? 4 : tc <= 8 ? 8 : 9;
+    const int64_t waves = (nct + tc - 1) / tc;
+    if (OH < 1 || OW < 1 || waves > 4 || batch * in_h * in_w * in_c * 4 >= ((int64_t)1 << 31) ||
+        batch * OH * OW * out_c * 4 >= ((int64_t)1 << 31))
         return (int)hipErrorInvalidValue;
     WgArgs a{};
-    a.g = g; a.y = y; a.in = x; a.partial = partial; a.bias_partial = act >= 0 ? bias_partial : nullptr;
+    a.g = g; a.y = y; a.in = x; a.in_bytes = batch * in_h * in_w * in_c * 4;
+    a.partial = partial; a.bias_partial = act >= 0 ? bias_partial : nullptr;
     a.rows = batch * OH * OW;
     a.IH = (int)in_h; a.IW = (int)in_w; a.CIN = (int)in_c; a.OH = (int)OH; a.OW = (int)OW; a.COUT = (int)out_c;
     a.K = (int)kernel; a.S = (int)stride; a.P = (int)pad; a.ncols = (int)ncols; a.slope = slope;
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid(kWgGrid), block((unsigned)(64 * waves));
-#define XPA_WG(N_, C_, A_) hipLaunchKernelGGL((conv_wgrad_kernel<N_, C_, A_>), grid, block, 0, s, a)
+    // the LDS-slab form when a slab of at least one output row fits (and the f4 staging applies)
+    bool slab = !g_wgrad_stream_only && in_c % 4 == 0 && out_c % 4 == 0 && (uintptr_t)x % 16 == 0 &&
+                (uintptr_t)g % 16 == 0 && (act < 0 || (uintptr_t)y % 16 == 0);
+    if (slab) {
+        a.PW = (int)((OW - 1) * stride + kernel);
+        a.CS = ws_pad((int)in_c, (int)stride);
+        a.COUTS = ws_pad(16 * tn, 1);
+        auto floats = [&](int64_t r) {
+            const int64_t xs = (((r - 1) * stride + kernel) * a.PW * a.CS + 3) & ~(int64_t)3;
+            return xs + ((r * OW + 3) & ~(int64_t)3) * a.COUTS;
+        };
+        int64_t r = OH;
+        while (r >= 1 && floats(r) > kWsFloats) --r;
+        slab = r >= 1;
+        if (slab) {
+            const int64_t nsl = (OH + r - 1) / r;
+            a.R = (int)((OH + nsl - 1) / nsl);
+            a.nsl = (int)nsl;
+            a.nslabs = batch * nsl;
+            a.xs_floats = (int)(((a.R - 1) * stride + kernel) * a.PW * a.CS + 3) & ~3;
+        }
+    }
+#define XPA_WG(N_, C_, A_)                                                                           \
+    if (slab) hipLaunchKernelGGL((conv_wgrad_lds_kernel<N_, C_, A_>), grid, block, 0, s, a);       \
+    else hipLaunchKernelGGL((conv_wgrad_kernel<N_, C_, A_>), grid, block, 0, s, a)
 #define XPA_WG_A(N_, C_)                 \
     if (act < 0) XPA_WG(N_, C_, -1);      \
     else if (act == 0) XPA_WG(N_, C_, 0); \
     else if (act == 1) XPA_WG(N_, C_, 1); \
     else XPA_WG(N_, C_, 2);
-    if (ntn == 1) {
-        if (ctw == 3) { XPA_WG_A(1, 3) } else { XPA_WG_A(1, 4) }
-    } else {
-        if (ctw == 3) { XPA_WG_A(2, 3) } else { XPA_WG_A(2, 4) }
-    }
+#define XPA_WG_C(N_)                                  \
+    if (tc == 2) { XPA_WG_A(N_, 2) }                  \
+    else if (tc == 4) { XPA_WG_A(N_, 4) }             \
+    else if (tc == 8) { XPA_WG_A(N_, 8) }             \
+    else { XPA_WG_A(N_, 9) }
+    if (tn == 1) { XPA_WG_C(1) }
+    else if (tn == 2) { XPA_WG_C(2) }
+    else { XPA_WG_C(4) }
+#undef XPA_WG_C
 #undef XPA_WG_A
 #undef XPA_WG
     return xpa_launch_status();

@@ -242,7 +242,7 @@ class _Trunk:
             hs = [h]
             convs = self.convs
         for conv, code, slope in convs:
-            if self._igemm_ok(conv):   # K28: implicit GEMM on the fp32 matrix cores, bias + activation fused
+            if self._igemm_ok(conv, h.numel()):   # K28: implicit GEMM on the fp32 matrix cores, bias + activation fused
                 y = self._conv_fwd(conv, code, slope, h)
             else:
                 z = F.conv2d(h.permute(0, 3, 1, 2), conv.weight, None, conv.stride, conv.padding)
@@ -272,15 +272,16 @@ class _Trunk:
 
     use_igemm = True   # K28 / K29 for every conv they take (False: MIOpen, the r02 path)
 
-    def _igemm_ok(self, conv):
+    def _igemm_ok(self, conv, numel):
+        """numel: the largest operand K28 / K29 load (32-bit buffer offsets: under 2 GiB)."""
         k, st, pd = conv.kernel_size, conv.stride, conv.padding
-        return (self.use_igemm and k[0] == k[1] and st[0] == st[1] and pd[0] == pd[1] and conv.padding_mode == "zeros"
+        return (self.use_igemm and numel * 4 < 2 ** 31 and k[0] == k[1] and st[0] == st[1] and pd[0] == pd[1] and conv.padding_mode == "zeros"
                 and conv.in_channels % 4 == 0 and conv.weight.is_contiguous()
                 and bool(ops.lib().xpa_conv_igemm_ok(conv.in_channels, conv.out_channels, k[0])))
 
-    def _igemm_dgrad_ok(self, conv):
+    def _igemm_dgrad_ok(self, conv, numel):
         k, st = conv.kernel_size, conv.stride
-        return (self._igemm_ok(conv) and st[0] <= 2 and conv.out_channels % 4 == 0
+        return (self._igemm_ok(conv, numel) and st[0] <= 2 and conv.out_channels % 4 == 0
                 and bool(ops.lib().xpa_conv_igemm_ok(conv.out_channels, conv.in_channels, k[0])))
 
     @staticmethod
@@ -430,7 +431,8 @@ class _Trunk:
                 self._conv1_wgrad(conv, g, hs[0], act=None if g_dz else (code, slope, y))
                 break
             x_in = self.frames(hs[i]) if hs[i].dtype == torch.uint8 else hs[i]
-            ig = self._igemm_ok(conv)
+            numel = max(x_in.numel(), g.numel())
+            ig = self._igemm_ok(conv, numel)
             need_in = i > 0
             if not g_dz and (need_in or not ig):
                 # the data gradient (and the library weight gradient) read dz: K22 in place, + the bias gradient
@@ -438,7 +440,7 @@ class _Trunk:
                 g_dz = True
             if ig:   # K29 (with the activation backward + bias gradient folded in when g is not dz yet)
                 self._conv_wgrad(conv, g, -1 if g_dz else code, slope, y, x_in)
-            if not ig or (need_in and not self._dgrad_ok(conv) and not self._igemm_dgrad_ok(conv)):
+            if not ig or (need_in and not self._dgrad_ok(conv) and not self._igemm_dgrad_ok(conv, numel)):
                 k27 = need_in and self._dgrad_ok(conv)
                 gx, gw, _ = torch.ops.aten.convolution_backward(
                     g.permute(0, 3, 1, 2), x_in.permute(0, 3, 1, 2), conv.weight, None, list(conv.stride),
