@@ -24,3 +24,13 @@ def golden():
             cache[name] = dict(np.load(os.path.join(GOLDEN, name), allow_pickle=False))
         return cache[name]
     return load
+
+
+@pytest.fixture(params=["k28", "auto"])
+def conv_path(request, monkeypatch):
+    """The explicit CNN trunk's conv choice: "k28" forces K28 / K29 for every conv they take (the C3 update's path at
+    any batch); "auto" keeps the size rule (MIOpen below fused_cnn._Trunk.igemm_min_rows output pixels)."""
+    from xuanpolicy_amd import fused_cnn
+    if request.param == "k28":
+        monkeypatch.setattr(fused_cnn._Trunk, "igemm_min_rows", 0)
+    return request.param

@@ -110,11 +110,11 @@ def _check_sd1(pol, g, rtol, atol, env=None):
 
 
 @pytest.mark.parametrize("fixture", ["atari_a2c.npz", "atari_a2c_prod.npz"])
-def test_a2c_atari_replays_reference_agent(golden, fixture):
+def test_a2c_atari_replays_reference_agent(golden, fixture, conv_path):
     """G8: the reference's two recorded A2C_Agent iterations on Atari-shaped frames (a2c_agent.py:57-107,
     env_name "Atari": DummyOnPolicyBuffer_Atari memory_tools.py:526-560, AC_CNN_Atari cnn.py:45-93 +
     Categorical_AC_Policy, life losses keep the path open) replayed through the device buffer (uint8 frames,
-    K1 GAE with the Atari closures, K4 sample + adv-norm) and A2C_Learner (CNN on MIOpen/hipBLASLt, K2
+    K1 GAE with the Atari closures, K4 sample + adv-norm) and A2C_Learner (CNN on K25-K29 or MIOpen per conv_path, hipBLASLt, K2
     categorical loss, K9 clip + Adam): GAE, every update's info dict, the final parameters.  The frames are
     regenerated by stepping the oracle SynthAtari env with the recorded actions through the reference's
     DummyVecEnv / agent observation flow and checked against the recorded per-step frame sums.

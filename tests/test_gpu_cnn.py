@@ -81,7 +81,7 @@ def _c3_policy(K=6, seed=0):
 
 
 @pytest.mark.parametrize("B", [96, 257])
-def test_fused_cnn_matches_autograd(B):
+def test_fused_cnn_matches_autograd(B, conv_path):
     """FusedCNNActorCritic forward (logits, v) and every parameter gradient for given d logits / d v == autograd
     through the reference-layout modules (AC_CNN_Atari: uint8 / 255, NCHW convs with bias, ReLU, Flatten in
     (C, H, W) order, fc, heads)."""

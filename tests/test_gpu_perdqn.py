@@ -66,7 +66,7 @@ def _perdqn_batch(seed, k, B, A):
 
 
 @pytest.mark.parametrize("fixture", ["perdqn.npz", "perdqn_prod.npz"])
-def test_perdqn_learner_replays_reference(golden, fixture):
+def test_perdqn_learner_replays_reference(golden, fixture, conv_path):
     """G9 / G9P: the reference's PerDQN_Learner updates replayed.  perdqn_prod.npz is the production Basic_CNN
     ([32, 64, 64] / [8, 4, 3] / [4, 2, 1] + q 512) at the C5 batch of 2048: K25 conv1 from the uint8 frames, K23 / K24
     max pool, K26 / K27 in the backward, K19."""
@@ -110,7 +110,7 @@ def test_perdqn_learner_replays_reference(golden, fixture):
 
 
 @pytest.mark.parametrize("filters", [[8, 8], [32, 64]])
-def test_perdqn_agent_loop_on_device(filters):
+def test_perdqn_agent_loop_on_device(filters, conv_path):
     """[8, 8]: MIOpen's NHWC kernels for every conv (the r02 intermittent-fault configuration); [32, 64]: the production
     first two convs (K25 / K26 / K27 + MIOpen's conv2 weight gradient).  Every device error word stays 0."""
     from xuanpolicy_amd.runner import build_perdqn
@@ -133,7 +133,7 @@ def test_perdqn_agent_loop_on_device(filters):
     assert 0.4 < agent.PER_beta <= 1.0 and agent.egreedy < agent.start_greedy
 
 
-def test_perdqn_agent_train_replays_reference(golden):
+def test_perdqn_agent_train_replays_reference(golden, conv_path):
     """G10: the reference's PerDQN_Agent.train (perdqn_agent.py:56-95) replayed through the device agent — SynthAtari
     device envs (18 actions), the production Basic_CNN + q 512, PER buffer with K6 store / sample / priority update, K4
     frame gathers, PerDQN_Learner (K25 / K23 / K19 / K24 / K26 / K27 + MIOpen / hipBLASLt), target copies every 5

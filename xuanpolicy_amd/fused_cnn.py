@@ -242,7 +242,7 @@ class _Trunk:
             hs = [h]
             convs = self.convs
         for conv, code, slope in convs:
-            if self._igemm_ok(conv, h.numel()):   # K28: implicit GEMM on the fp32 matrix cores, bias + activation fused
+            if self._igemm_ok(conv, h.numel(), self._out_rows(conv, h.shape)):   # K28 (bias + activation fused)
                 y = self._conv_fwd(conv, code, slope, h)
             else:
                 z = F.conv2d(h.permute(0, 3, 1, 2), conv.weight, None, conv.stride, conv.padding)
@@ -270,19 +270,35 @@ class _Trunk:
             fouts.append(s)
         return s, (hs, None, flat, fouts)
 
-    use_igemm = True   # K28 / K29 for every conv they take (False: MIOpen, the r02 path)
+    use_igemm = True   # K28 / K29 for the convs they take (False: MIOpen for every conv, the r02 path)
+    # K28 / K29 hold one weight image per CU and tile the output rows 32 at a time per wave, so below ~1 M output rows
+    # a launch has too few tiles per CU to balance (C5's batch 2048 = 800 rows per CU = 25 tiles over 16 waves) and
+    # MIOpen's kernels measure faster there (tools/c5_ab.py: 2.26 vs 2.65 ms per C5 learner step; C3's rollout
+    # forwards at 1024 frames 71 vs 84-94 us).  Small-channel convs (< 16 in or out: the test nets, r02's fault
+    # suspect) always take K28 / K29.
+    igemm_min_rows = 1 << 20
 
-    def _igemm_ok(self, conv, numel):
-        """numel: the largest operand K28 / K29 load (32-bit buffer offsets: under 2 GiB)."""
+    def _igemm_ok(self, conv, numel, rows=None):
+        """numel: the largest operand K28 / K29 load (32-bit buffer offsets: under 2 GiB); rows: the conv's output
+        pixels B x OH x OW (None: no size preference)."""
         k, st, pd = conv.kernel_size, conv.stride, conv.padding
-        return (self.use_igemm and numel * 4 < 2 ** 31 and k[0] == k[1] and st[0] == st[1] and pd[0] == pd[1] and conv.padding_mode == "zeros"
+        small_c = min(conv.in_channels, conv.out_channels) < 16
+        return (self.use_igemm and numel * 4 < 2 ** 31 and k[0] == k[1] and st[0] == st[1] and pd[0] == pd[1]
+                and (rows is None or small_c or rows >= self.igemm_min_rows)
+                and conv.padding_mode == "zeros"
                 and conv.in_channels % 4 == 0 and conv.weight.is_contiguous()
                 and bool(ops.lib().xpa_conv_igemm_ok(conv.in_channels, conv.out_channels, k[0])))
 
-    def _igemm_dgrad_ok(self, conv, numel):
+    def _igemm_dgrad_ok(self, conv, numel, rows=None):
         k, st = conv.kernel_size, conv.stride
-        return (self._igemm_ok(conv, numel) and st[0] <= 2 and conv.out_channels % 4 == 0
+        return (self._igemm_ok(conv, numel, rows) and st[0] <= 2 and conv.out_channels % 4 == 0
                 and bool(ops.lib().xpa_conv_igemm_ok(conv.out_channels, conv.in_channels, k[0])))
+
+    @staticmethod
+    def _out_rows(conv, shape):
+        B, H, W = shape[0], shape[1], shape[2]
+        k, st, pd = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        return B * ((H + 2 * pd - k) // st + 1) * ((W + 2 * pd - k) // st + 1)
 
     @staticmethod
     def _conv_fwd(conv, code, slope, h):
@@ -432,7 +448,8 @@ class _Trunk:
                 break
             x_in = self.frames(hs[i]) if hs[i].dtype == torch.uint8 else hs[i]
             numel = max(x_in.numel(), g.numel())
-            ig = self._igemm_ok(conv, numel)
+            rows = y.shape[0] * y.shape[1] * y.shape[2]
+            ig = self._igemm_ok(conv, numel, rows)
             need_in = i > 0
             if not g_dz and (need_in or not ig):
                 # the data gradient (and the library weight gradient) read dz: K22 in place, + the bias gradient
@@ -440,7 +457,7 @@ class _Trunk:
                 g_dz = True
             if ig:   # K29 (with the activation backward + bias gradient folded in when g is not dz yet)
                 self._conv_wgrad(conv, g, -1 if g_dz else code, slope, y, x_in)
-            if not ig or (need_in and not self._dgrad_ok(conv) and not self._igemm_dgrad_ok(conv, numel)):
+            if not ig or (need_in and not self._dgrad_ok(conv) and not self._igemm_dgrad_ok(conv, numel, rows)):
                 k27 = need_in and self._dgrad_ok(conv)
                 gx, gw, _ = torch.ops.aten.convolution_backward(
                     g.permute(0, 3, 1, 2), x_in.permute(0, 3, 1, 2), conv.weight, None, list(conv.stride),
