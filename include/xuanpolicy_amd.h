@@ -267,6 +267,17 @@ int xpa_clip_adam_step(float *param, float *grad, float *exp_avg, float *exp_avg
 int xpa_clip_adam_step_partials(float *param, float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
                                 const double *sq_partials, int64_t n_sq, float max_norm, float lr, float beta1,
                                 float beta2, float eps, int64_t step, float *total_norm_out, xpa_stream_t stream);
+/* K9 with the learning rate and Adam step read from a device schedule, so that a captured update (forward + loss +
+ * backward + this) can be replayed for the next update: sched[2k] = lr_k / (1 - beta1^step_k), sched[2k + 1] =
+ * 1 / sqrt(1 - beta2^step_k) (xpa_adam_sched_entry computes an entry with xpa_clip_adam_step's arithmetic), k =
+ * cursor[0]; cursor is int32[3] = {update index, block ticket (0 between launches), overflow flag}.  The launch
+ * advances cursor[0] by one (its last block to finish reading); k >= n_sched is clamped to n_sched - 1 and sets
+ * cursor[2].  The host refills sched and resets cursor once per window of updates (flat.FusedClipAdam). */
+int xpa_clip_adam_step_sched(float *param, float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+                             double *norm_partials, float max_norm, float beta1, float beta2, float eps,
+                             const float *sched, int64_t n_sched, int32_t *cursor, float *total_norm_out,
+                             xpa_stream_t stream);
+void xpa_adam_sched_entry(float lr, float beta1, float beta2, int64_t step, float *out2);
 
 /* K10 — activation backward fused with bias-gradient column sums for one MLP layer (row-major
  * [rows, cols]).  Replaces the activation backward and the bias-gradient reduction torch autograd runs

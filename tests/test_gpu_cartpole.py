@@ -136,3 +136,32 @@ def test_graph_capture_failure_falls_back_to_eager():
         out.append([p.detach().cpu().numpy().copy() for p in agent.policy.parameters()])
     for a, b in zip(*out):
         np.testing.assert_allclose(b, a, rtol=1e-6, atol=1e-7)
+
+
+def test_graphed_k9_schedule_windows(monkeypatch):
+    """K9 captured in the slot graphs reads (lr, Adam step) from the device schedule (xpa_clip_adam_step_sched): with a
+    24-update window the table is refilled five times inside two iterations (128 updates) and the LinearLR decay is
+    live; the parameters, the Adam step count and the host learning rate equal the eager run's (host K9 arguments),
+    and no launch ran past its window."""
+    from xuanpolicy_amd import flat
+    from xuanpolicy_amd.runner import build_cartpole_ppo
+    monkeypatch.setattr(flat.FusedClipAdam, "SCHED_WINDOW", 24)
+    out, lrs, steps = [], [], []
+    for graphed in (False, True):
+        agent = build_cartpole_ppo(n_envs=8, n_steps=128, hidden=64, seed=5, device=DEV, graph_update=graphed)
+        for _ in range(2):
+            agent.train(128, log=False)
+        torch.cuda.synchronize()
+        fo = agent.learner.fused_opt
+        assert fo.sched_enabled == graphed
+        if graphed:
+            assert not fo.sched_overflow()
+            assert sum(isinstance(v, tuple) for v in agent.learner._slot_graphs.values()) == 8
+            assert len(agent.learner._epoch_graphs) == 1   # epochs 3-16 replay one whole-epoch graph
+        out.append([p.detach().cpu().numpy().copy() for p in agent.policy.parameters()])
+        lrs.append(agent.learner.optimizer.param_groups[0]["lr"])
+        steps.append(fo.step_count)
+    assert steps[0] == steps[1] == 128
+    assert lrs[0] == lrs[1] and lrs[0] < agent.config.learning_rate
+    for a, b in zip(*out):
+        np.testing.assert_allclose(b, a, rtol=1e-6, atol=1e-7)

@@ -106,6 +106,9 @@ SIGNATURES = {
                                                    c_p, c_p, c_p, c_p]),
     "xpa_clip_adam_step_partials": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_f32, c_f32, c_f32, c_f32,
                                                    c_f32, c_i64, c_p, c_p]),
+    "xpa_clip_adam_step_sched": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_p, c_f32, c_f32, c_f32, c_f32, c_p, c_i64,
+                                                c_p, c_p, c_p]),
+    "xpa_adam_sched_entry": (None, [c_f32, c_f32, c_f32, c_i64, c_p]),
     "xpa_colsum_finalize_batch": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p]),
     "xpa_per_store": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i64, c_i64, ctypes.c_double, c_p]),
     "xpa_per_update_priorities": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_i64, ctypes.c_double,

@@ -501,8 +501,13 @@ class _OnPolicyAgent:
         scalars = None
         fm = self._rollout_mlp() if not self.global_advnorm else None
         rows_path = fm is not None and self.fuse_gather and fm.rows_ok(obs_flat)
+        # graphed small-batch updates (C1): the epoch's minibatches go to the learner as one list, which replays them
+        # as one captured graph once every slot is captured (learners.update_epoch)
+        epoch_batches = (not rows_path and not self.global_advnorm and getattr(self.learner, "graph_updates", False)
+                         and hasattr(self.learner, "update_epoch"))
         for _ in range(self.n_epoch):
             perm = self.epoch_permutation(NT)
+            batches = []
             for start in range(0, NT, B):
                 idx = perm[start:start + B]
                 b = idx.shape[0]
@@ -528,9 +533,13 @@ class _OnPolicyAgent:
                             torch.empty((ops.gather_num_partials(b), 2), dtype=torch.float64, device=self.device))
                     mbs[(b, obs_flat.dtype, tuple(obs_flat.shape[1:]))] = bufs
                 self.obs_mb, self.adv_part = bufs
-                def gather(idx=idx):
+                def gather(idx=idx, obs_out=self.obs_mb, part=self.adv_part):
                     return ops.gather_minibatch(idx, obs_flat, adv=adv_flat if use_advnorm else None,
-                                                obs_out=self.obs_mb, adv_partials=self.adv_part if use_advnorm else None)
+                                                obs_out=obs_out, adv_partials=part if use_advnorm else None)
+                if epoch_batches:
+                    batches.append((self.obs_mb, idx, act_flat, adv_flat, ret_flat, logp_flat,
+                                    self.adv_part if use_advnorm else None, gather))
+                    continue
                 if not self.global_advnorm:
                     # the gather rides in the learner's slot graph when the update is graphed (writes obs_mb / adv_part)
                     scalars = self.learner.update_fused(self.obs_mb, idx, act_flat, adv_flat, ret_flat, logp_flat,
@@ -546,6 +555,11 @@ class _OnPolicyAgent:
                 scalars = self.learner.update_fused(obs_mb, idx, act_flat, adv_flat, ret_flat, logp_flat, part)
                 if self.update_log is not None:
                     self.update_log.append(scalars.clone())
+            if batches:
+                outs = self.learner.update_epoch(batches, keep_all=self.update_log is not None)
+                scalars = outs[-1]
+                if self.update_log is not None:
+                    self.update_log.extend(outs)
         self.last_info = scalars
         self.iterations += 1
         if self.defer_boot:

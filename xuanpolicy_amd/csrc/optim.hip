@@ -48,8 +48,10 @@ __global__ __launch_bounds__(kOptThreads) void clip_adam_kernel(float *__restric
                                                                 const double *__restrict__ partials, int n_partials,
                                                                 float max_norm, float b1, float b2, float step_size,
                                                                 float inv_bc2_sqrt, float eps,
-                                                                float *__restrict__ norm_out) {
-    __shared__ float s_coef;
+                                                                float *__restrict__ norm_out,
+                                                                const float *__restrict__ sched, int n_sched,
+                                                                int *__restrict__ cursor) {
+    __shared__ float s_coef, s_step, s_inv;
     if (threadIdx.x < 64) {
         double s = 0.0;
         for (int k = threadIdx.x; k < n_partials; k += 64) s += partials[k];
@@ -61,10 +63,33 @@ __global__ __launch_bounds__(kOptThreads) void clip_adam_kernel(float *__restric
             if (max_norm >= 0.f) coef = fminf(max_norm / (total + 1e-6f), 1.0f);
             s_coef = coef;
             if (blockIdx.x == 0 && norm_out) *norm_out = total;
+            s_step = step_size;
+            s_inv = inv_bc2_sqrt;
+            if (sched) {
+                // device schedule (step_size, 1/sqrt(bc2)) of update cursor[0]; an index past the table is clamped
+                // and flagged in cursor[2]
+                int k = __hip_atomic_load(cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (k >= n_sched) {
+                    if (blockIdx.x == 0) cursor[2] = 1;
+                    k = n_sched - 1;
+                }
+                s_step = sched[2 * k];
+                s_inv = sched[2 * k + 1];
+            }
         }
     }
     __syncthreads();
     const float coef = s_coef;
+    step_size = s_step;
+    inv_bc2_sqrt = s_inv;
+    if (sched && threadIdx.x == 0) {
+        // every block has read cursor[0]: the last one to take a ticket advances it for the next update's launch
+        const int t = __hip_atomic_fetch_add(cursor + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == (int)gridDim.x - 1) {
+            cursor[1] = 0;
+            __hip_atomic_fetch_add(cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     const int64_t n4 = n / 4;
     float4 *p4 = reinterpret_cast<float4 *>(p);
     float4 *g4 = reinterpret_cast<float4 *>(g);
@@ -117,7 +142,7 @@ XPA_API int xpa_clip_adam_step_partials(float *param, float *grad, float *exp_av
     if (ab > 2048) ab = 2048;
     hipLaunchKernelGGL(clip_adam_kernel, dim3((unsigned)ab), dim3(kOptThreads), 0, (hipStream_t)stream, param, grad,
                        exp_avg, exp_avg_sq, n, sq_partials, (int)n_sq, max_norm, beta1, beta2, step_size,
-                       inv_bc2_sqrt, eps, total_norm_out);
+                       inv_bc2_sqrt, eps, total_norm_out, nullptr, 0, nullptr);
     return xpa_launch_status();
 }
 
@@ -142,6 +167,41 @@ XPA_API int xpa_clip_adam_step(float *param, float *grad, float *exp_avg, float 
     if (ab > 2048) ab = 2048;
     hipLaunchKernelGGL(clip_adam_kernel, dim3((unsigned)ab), dim3(kOptThreads), 0, s, param, grad, exp_avg, exp_avg_sq,
                        n, norm_partials, (int)nb, max_norm, beta1, beta2, step_size, inv_bc2_sqrt, eps,
-                       total_norm_out);
+                       total_norm_out, nullptr, 0, nullptr);
     return xpa_launch_status();
+}
+
+// K9 with (step_size, 1/sqrt(bc2)) read from a device schedule: sched[2k], sched[2k + 1] for update k = cursor[0]
+// (cursor: int32[3] = {update index, block ticket, overflow flag}); the launch advances cursor[0] itself, so a
+// captured update (forward + loss + backward + this) replays with the next update's Adam step and learning rate.
+// The host fills the schedule once per window of updates (flat.FusedClipAdam.step_sched).
+XPA_API int xpa_clip_adam_step_sched(float *param, float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+                                     double *norm_partials, float max_norm, float beta1, float beta2, float eps,
+                                     const float *sched, int64_t n_sched, int32_t *cursor, float *total_norm_out,
+                                     xpa_stream_t stream) {
+    if (n <= 0 || !param || !grad || !exp_avg || !exp_avg_sq || !norm_partials || !sched || !cursor || n_sched <= 0 ||
+        n_sched > 0x7fffffff)
+        return (int)hipErrorInvalidValue;
+    if (((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16)
+        return (int)hipErrorInvalidValue;
+    const int64_t nb = norm_blocks(n);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(grad_sqnorm_kernel, dim3((unsigned)nb), dim3(kOptThreads), 0, s, grad, n, norm_partials);
+    const int st = xpa_launch_status();
+    if (st) return st;
+    int64_t ab = (n / 4 + kOptThreads - 1) / kOptThreads;
+    if (ab < 1) ab = 1;
+    if (ab > 2048) ab = 2048;
+    hipLaunchKernelGGL(clip_adam_kernel, dim3((unsigned)ab), dim3(kOptThreads), 0, s, param, grad, exp_avg, exp_avg_sq,
+                       n, norm_partials, (int)nb, max_norm, beta1, beta2, 0.f, 0.f, eps, total_norm_out, sched,
+                       (int)n_sched, cursor);
+    return xpa_launch_status();
+}
+
+// The host-side schedule entry of update `step` with learning rate lr (the arithmetic of xpa_clip_adam_step).
+XPA_API void xpa_adam_sched_entry(float lr, float beta1, float beta2, int64_t step, float *out2) {
+    const double bc1 = 1.0 - pow((double)beta1, (double)step);
+    const double bc2 = 1.0 - pow((double)beta2, (double)step);
+    out2[0] = (float)((double)lr / bc1);
+    out2[1] = (float)(1.0 / sqrt(bc2));
 }

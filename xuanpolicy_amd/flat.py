@@ -161,3 +161,94 @@ class FusedClipAdam:
             _lib.check(rc, "xpa_clip_adam_step")
         self._step_t.fill_(float(self.step_count))
         self.optimizer._opt_called = True  # the LR scheduler checks that an optimizer step happened
+
+    # ---- device schedule: (lr, Adam step) of the next updates in HBM, so K9 can sit inside a captured update ----
+    SCHED_WINDOW = 256
+    sched_enabled = False
+
+    def enable_sched(self, on=True):
+        """Route every step through xpa_clip_adam_step_sched (K9 reading its learning rate and Adam step from a device
+        table filled once per SCHED_WINDOW updates): the launch is then graph-capturable."""
+        self.sched_enabled = bool(on)
+        if on and getattr(self, "_sched", None) is None:
+            dev = self.fs.param.device
+            self._sched = torch.zeros(2 * self.SCHED_WINDOW, dtype=torch.float32, device=dev)
+            self._cursor = torch.zeros(4, dtype=torch.int32, device=dev)
+            self._sched_end = self.step_count        # step_count of the last update the table covers
+        return self
+
+    def _future_lrs(self, scheduler, count):
+        """The learning rates of the next `count` updates: the scheduler stepped ahead on a saved state, then
+        restored (its own arithmetic, whatever the schedule)."""
+        groups = self.optimizer.param_groups
+        g = groups[0]
+        if scheduler is None:
+            return [float(g["lr"])] * count
+        import warnings
+        saved_state = scheduler.state_dict()
+        saved_lrs = [gg["lr"] for gg in groups]
+        saved_called = getattr(self.optimizer, "_opt_called", None)
+        out = []
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            for _ in range(count):
+                lr = g["lr"]
+                out.append(float(lr) if not isinstance(lr, torch.Tensor) else float(lr.item()))
+                self.optimizer._opt_called = True
+                scheduler.step()
+        scheduler.load_state_dict(saved_state)
+        for gg, lr in zip(groups, saved_lrs):
+            gg["lr"] = lr
+        if saved_called is not None:
+            self.optimizer._opt_called = saved_called
+        return out
+
+    def ensure_window(self, scheduler, need=1):
+        """Before `need` updates that launch K9 from the schedule (outside any capture): refill the table and reset the
+        cursor unless the current window still covers them.  Stream-ordered H2D copy from a fresh pinned buffer."""
+        if need > self.SCHED_WINDOW:
+            raise ValueError("%d scheduled updates exceed the %d-entry window" % (need, self.SCHED_WINDOW))
+        if self.step_count + need <= self._sched_end:
+            return
+        import ctypes
+        import numpy as np
+        g = self.optimizer.param_groups[0]
+        b1, b2 = g["betas"]
+        W = self.SCHED_WINDOW
+        lrs = self._future_lrs(scheduler, W)
+        host = torch.zeros(2 * W, dtype=torch.float32).pin_memory()
+        out2 = (ctypes.c_float * 2)()
+        vals = np.empty(2 * W, dtype=np.float32)
+        for k in range(W):
+            ops.lib().xpa_adam_sched_entry(lrs[k], float(b1), float(b2), self.step_count + 1 + k,
+                                           ctypes.addressof(out2))
+            vals[2 * k], vals[2 * k + 1] = out2[0], out2[1]
+        host.copy_(torch.from_numpy(vals))
+        self._sched.copy_(host, non_blocking=True)
+        self._cursor.zero_()
+        self._sched_host = host                       # keep the pinned source alive until the copy has run
+        self._sched_end = self.step_count + W
+
+    def launch_sched(self, max_norm):
+        """The device part of a scheduled step (capturable): norm pass + clip + Adam, cursor advanced on device."""
+        if max_norm is not None and float(max_norm) < 0:
+            raise ValueError("max_norm must be >= 0 (None: no clipping)")
+        max_norm = -1.0 if max_norm is None else float(max_norm)
+        g = self.optimizer.param_groups[0]
+        b1, b2 = g["betas"]
+        rc = ops.lib().xpa_clip_adam_step_sched(ops._p(self.fs.param), ops._p(self.fs.flat), ops._p(self.exp_avg),
+                                                ops._p(self.exp_avg_sq), self.fs.numel, ops._p(self.partials),
+                                                max_norm, float(b1), float(b2), float(g["eps"]), ops._p(self._sched),
+                                                self.SCHED_WINDOW, ops._p(self._cursor), ops._p(self.total_norm),
+                                                ops._stream(self.fs.param.device))
+        _lib.check(rc, "xpa_clip_adam_step_sched")
+
+    def host_step(self):
+        """The host bookkeeping of a scheduled step (after its launch or its graph replay)."""
+        self.step_count += 1
+        self._step_t.fill_(float(self.step_count))
+        self.optimizer._opt_called = True
+
+    def sched_overflow(self):
+        """True if a scheduled launch ran past its window (host-synchronising read; tests / diagnostics)."""
+        return bool(int(self._cursor[2].item()))

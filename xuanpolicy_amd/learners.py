@@ -116,7 +116,11 @@ class _FusedPolicyGradient(Learner):
             self.grad_sync(self._params)
             sq = None
         fused = getattr(self, "fused_opt", None)
-        if fused is not None:
+        if fused is not None and fused.sched_enabled and self.grad_sync is None:
+            fused.ensure_window(self.scheduler)
+            fused.launch_sched(self._max_norm if self._use_clip else None)   # K9 from the device schedule
+            fused.host_step()
+        elif fused is not None:
             fused.step(self._max_norm if self._use_clip else None, sq=sq)  # xpa_clip_adam_step (K9)
         else:
             if self._use_clip:
@@ -167,6 +171,19 @@ class _FusedPolicyGradient(Learner):
             self._sync_clip_step()
             return scalars
         if fm is not None and self._graph_ok(obs):
+            fused = getattr(self, "fused_opt", None)
+            if fused is not None and getattr(self, "graph_k9", True):
+                # K9 inside the slot graph: it reads lr / Adam step from the device schedule and advances its cursor
+                if not fused.sched_enabled:
+                    fused.enable_sched()
+                fused.ensure_window(self.scheduler)
+                scalars = self._graphed_mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, pre,
+                                                   k9=lambda: fused.launch_sched(self._max_norm if self._use_clip
+                                                                                 else None))
+                fused.host_step()
+                if self.scheduler is not None:
+                    self.scheduler.step()
+                return scalars
             scalars = self._graphed_mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, pre)
             self._sync_clip_step()
             return scalars
@@ -186,9 +203,11 @@ class _FusedPolicyGradient(Learner):
     # ~15-20 us of host time apiece (profiles/r02f_c1_host_probe.txt).  The explicit forward + loss + backward of one
     # minibatch slot is therefore captured once into a hipGraph and replayed.  Every input is a fixed buffer: the rollout
     # columns, the persistent epoch permutation (idx is a slice of it) and the gathered obs rows.  The parameters are
-    # updated in place by K9.  K9 itself runs outside the graph, because lr and the Adam step count are kernel arguments
-    # that change every update.  Slot graphs are keyed by those pointers.  A slot's first update runs eagerly and warms
-    # up workspaces and BLAS handles; the second captures; later ones replay.
+    # updated in place by K9, which is captured too (r03): it reads the learning rate and the Adam step of the update
+    # from a device schedule (flat.FusedClipAdam.ensure_window fills it once per 256 updates by stepping the scheduler
+    # ahead on a saved state) at a device cursor it advances itself, so a replay is the next update's complete step.
+    # Slot graphs are keyed by those pointers.  A slot's first update runs eagerly and warms up workspaces and BLAS
+    # handles; the second captures; later ones replay.
     graph_max_rows = 8192
     graph_max_slots = 64   # captured slot graphs per learner; beyond it (e.g. unstable input pointers) stay eager
 
@@ -199,19 +218,27 @@ class _FusedPolicyGradient(Learner):
                 and not ops.TIMER.enabled
                 and len(self.__dict__.get("_slot_graphs", ())) < self.graph_max_slots)
 
-    def _graphed_mlp_update(self, fm, obs, idx, act, adv, ret, old_logp, adv_partials, pre=None):
+    def _slot_key(self, obs, idx, act, adv, ret, old_logp, adv_partials):
         ptr = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
         # the loss coefficients are kernel arguments baked into a capture: part of the key
-        key = (ptr(obs), tuple(obs.shape), ptr(idx), -1 if idx is None else idx.shape[0], ptr(act), ptr(adv), ptr(ret),
-               ptr(old_logp), ptr(adv_partials), float(self.clip_range), float(self.vf_coef), float(self.ent_coef)) \
-            + tuple(p.data_ptr() for p in self._params)
+        return (ptr(obs), tuple(obs.shape), ptr(idx), -1 if idx is None else idx.shape[0], ptr(act), ptr(adv),
+                ptr(ret), ptr(old_logp), ptr(adv_partials), float(self.clip_range), float(self.vf_coef),
+                float(self.ent_coef)) + tuple(p.data_ptr() for p in self._params)
+
+    def _graphed_mlp_update(self, fm, obs, idx, act, adv, ret, old_logp, adv_partials, pre=None, k9=None):
+        """k9: the device part of the clip + Adam step (xpa_clip_adam_step_sched), run after the backward and captured
+        with it; the caller does the host bookkeeping."""
+        key = self._slot_key(obs, idx, act, adv, ret, old_logp, adv_partials)
         graphs = self.__dict__.setdefault("_slot_graphs", {})
         ent = graphs.get(key)
         if ent is None:                     # first use of this slot: eager (warm-up)
             graphs[key] = "warm"
             if pre is not None:
                 pre()
-            return self._mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, step=False)
+            out = self._mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, step=False)
+            if k9 is not None:
+                k9()
+            return out
         if ent == "warm":
             if self.__dict__.get("_graph_pool") is None:
                 self._graph_pool = torch.cuda.graph_pool_handle()
@@ -223,6 +250,8 @@ class _FusedPolicyGradient(Learner):
                     if pre is not None:
                         pre()
                     out = self._mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, step=False)
+                    if k9 is not None:
+                        k9()
             except Exception:               # a launch that cannot be captured: stay eager from here on
                 self._graph_failed = True
                 torch.cuda.synchronize()
@@ -232,10 +261,70 @@ class _FusedPolicyGradient(Learner):
                 del graphs[key]
                 if pre is not None:
                     pre()
-                return self._mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, step=False)
+                out = self._mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, step=False)
+                if k9 is not None:
+                    k9()
+                return out
             graphs[key] = ent = (g, out, self._ws)   # the graph writes into this workspace: keep it alive
         ent[0].replay()
         return ent[1]
+
+    def update_epoch(self, batches, keep_all=False):
+        """One epoch of minibatch updates, batches = [(obs, idx, act, adv, ret, old_logp, adv_partials, pre), ...].
+        Once every minibatch slot of the epoch has its captured slot graph (K9 inside), the whole sequence is captured
+        once more as ONE graph keyed by the slots, and later epochs are one replay (the epoch's host work is then the
+        permutation launch before it and the per-update bookkeeping after it).  Otherwise the updates run one by one
+        through update_fused.  Returns the per-update loss-scalar tensors (keep_all False: only the last is guaranteed
+        to hold its own update's values — the eager updates share their workspace's scalars)."""
+        fm = self._fused_mlp()
+        fused = getattr(self, "fused_opt", None)
+        slots = self.__dict__.get("_slot_graphs", {})
+        keys = [self._slot_key(b[0], b[1], b[2], b[3], b[4], b[5], b[6]) for b in batches] \
+            if fm is not None and not fm.fused_heads else None
+        ready = (keys is not None and fused is not None and fused.sched_enabled and getattr(self, "graph_k9", True)
+                 and getattr(self, "graph_epochs", True) and all(self._graph_ok(b[0]) for b in batches)
+                 and all(isinstance(slots.get(k), tuple) for k in keys) and len(batches) <= fused.SCHED_WINDOW)
+        if not ready:
+            return self._eager_epoch(batches, keep_all)
+        epochs = self.__dict__.setdefault("_epoch_graphs", {})
+        ekey = tuple(keys)
+        fused.ensure_window(self.scheduler, need=len(batches))
+        ent = epochs.get(ekey)
+        if ent is None:
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g, pool=self._graph_pool):
+                    outs = []
+                    for (obs, idx, act, adv, ret, old_logp, adv_partials, pre) in batches:
+                        if pre is not None:
+                            pre()
+                        out = self._mlp_update(fm, obs, idx, act, adv, ret, old_logp, adv_partials, step=False)
+                        # every update of the epoch writes the same workspace: each one's scalars copied out in-graph
+                        outs.append(out.clone())
+                        fused.launch_sched(self._max_norm if self._use_clip else None)
+            except Exception:
+                # nothing of the aborted capture ran: stay with the slot graphs from here on
+                self.graph_epochs = False
+                torch.cuda.synchronize()
+                fm._cq.reset()
+                fm._cq_early.reset()
+                return self._eager_epoch(batches, keep_all)
+            epochs[ekey] = ent = (g, outs)
+        ent[0].replay()
+        for _ in batches:
+            self.iterations += 1
+            fused.host_step()
+            if self.scheduler is not None:
+                self.scheduler.step()
+        # the graph's scalar buffers are rewritten by the next replay: copies when every update's values are kept
+        return [o.clone() for o in ent[1]] if keep_all else list(ent[1])
+
+    def _eager_epoch(self, batches, keep_all):
+        outs = []
+        for b in batches:
+            out = self.update_fused(*b[:7], pre=b[7])
+            outs.append(out.clone() if keep_all else out)
+        return outs
 
     def _mlp_update(self, fm, obs, idx, act, adv, ret, old_logp, adv_partials, step):
         """Explicit forward (fused_mlp) + K2 loss + explicit backward into the flat gradient (+ K9 when step)."""
