@@ -279,6 +279,35 @@ int xpa_clip_adam_step_sched(float *param, float *grad, float *exp_avg, float *e
                              xpa_stream_t stream);
 void xpa_adam_sched_entry(float lr, float beta1, float beta2, int64_t step, float *out2);
 
+/* K30 — one whole PPO-Clip / A2C minibatch update of a small MLP actor-critic in ONE launch (one workgroup, every
+ * activation in LDS): representation Linear(d_in, h0) + act, actor Linear(h0, h1) + act -> Linear(h1, k) (Categorical
+ * logits), critic Linear(h0, h2) + act -> Linear(h2, 1).  Rows through idx from obs [n_rows, obs_ld] and the flat
+ * act / old_logp / adv / ret buffers (memory_tools.py:230-243, with the minibatch adv normalisation when
+ * use_advnorm), the forward, K2's categorical loss (the OUT_KEYS scalars into `scalars`), the backward (every
+ * gradient into its view of the flat gradient buffer), clip_grad_norm_(max_norm; < 0: none) and Adam over the flat
+ * buffers [0, n) with (lr, step) from the device schedule at cursor (xpa_clip_adam_step_sched's convention; the
+ * launch advances cursor[0]).  Replaces ~25 launches per update of the C1 configuration (ppoclip_learner.py:24-65).
+ * Limits: h0, h1, h2 multiples of 4 and <= 256, 2 <= k <= 16, xpa_small_mlp_lds_floats(...) <= 40704. */
+typedef struct XpaSmallMlpArgs {
+    int batch, d_in, h0, h1, h2, k, act_code, algo, use_advnorm, n_sched;
+    float slope, clip_range, vf_coef, ent_coef, max_norm, beta1, beta2, eps;
+    const float *obs;
+    int64_t obs_ld;
+    const int64_t *idx;
+    int64_t n_rows;
+    const float *actions, *old_logp, *adv, *ret;
+    const float *W0, *b0, *W1, *b1, *W2, *b2, *Wa, *ba, *Wc, *bc;
+    float *gW0, *gb0, *gW1, *gb1, *gW2, *gb2, *gWa, *gba, *gWc, *gbc;
+    float *param, *grad, *exp_avg, *exp_avg_sq;
+    int64_t n;
+    const float *sched;
+    int32_t *cursor;
+    float *scalars, *total_norm_out;
+    int64_t *stamps;   /* diagnostics (nullable): s_memtime at the kernel's phase boundaries, thread 0 */
+} XpaSmallMlpArgs;
+int64_t xpa_small_mlp_lds_floats(int64_t batch, int64_t d_in, int64_t h0, int64_t h1, int64_t h2, int64_t k);
+int xpa_small_mlp_update(const XpaSmallMlpArgs *args, xpa_stream_t stream);
+
 /* K10 — activation backward fused with bias-gradient column sums for one MLP layer (row-major
  * [rows, cols]).  Replaces the activation backward and the bias-gradient reduction torch autograd runs
  * per mlp_block (xuance/torch/utils/layers.py:8-24) inside loss.backward() (ppoclip_learner.py:46).

@@ -73,6 +73,7 @@ def test_graphed_updates_match_eager():
     out = []
     for graphed in (False, True):
         agent = build_cartpole_ppo(n_envs=8, n_steps=128, hidden=64, seed=4, device=DEV, graph_update=graphed)
+        agent.learner.small_updates = False   # the multi-kernel slot graphs (K30 has its own test)
         for _ in range(2):
             agent.train(128, log=False)
         torch.cuda.synchronize()
@@ -94,6 +95,7 @@ def test_graphed_updates_ragged_last_minibatch():
     for graphed in (False, True):
         agent = build_cartpole_ppo(n_envs=8, n_steps=100, hidden=64, seed=6, device=DEV, graph_update=graphed,
                                    n_minibatch=6, n_epoch=2)
+        agent.learner.small_updates = False
         assert agent.batch_size == 133
         for _ in range(3):
             agent.train(100, log=False)
@@ -115,6 +117,7 @@ def test_graph_capture_failure_falls_back_to_eager():
     out = []
     for inject in (False, True):
         agent = build_cartpole_ppo(n_envs=8, n_steps=128, hidden=64, seed=4, device=DEV, graph_update=inject)
+        agent.learner.small_updates = False
         if inject:
             fm = agent.learner._fused_mlp()
             real = ops.ColsumQueue.flush
@@ -149,6 +152,7 @@ def test_graphed_k9_schedule_windows(monkeypatch):
     out, lrs, steps = [], [], []
     for graphed in (False, True):
         agent = build_cartpole_ppo(n_envs=8, n_steps=128, hidden=64, seed=5, device=DEV, graph_update=graphed)
+        agent.learner.small_updates = False
         for _ in range(2):
             agent.train(128, log=False)
         torch.cuda.synchronize()
@@ -165,3 +169,48 @@ def test_graphed_k9_schedule_windows(monkeypatch):
     assert lrs[0] == lrs[1] and lrs[0] < agent.config.learning_rate
     for a, b in zip(*out):
         np.testing.assert_allclose(b, a, rtol=1e-6, atol=1e-7)
+
+
+def test_small_mlp_update_matches_multi_kernel_path():
+    """K30 (xpa_small_mlp_update: gather + forward + loss + backward + clip + Adam in one launch) against the
+    multi-kernel update (K13 / hipBLASLt / K2 / K10 / K9) from the same start: every update's loss scalars and the
+    parameters after one iteration (64 updates), within the f32 reassociation of the two paths."""
+    from xuanpolicy_amd.runner import build_cartpole_ppo
+    res = []
+    for small in (True, False):
+        agent = build_cartpole_ppo(n_envs=8, n_steps=128, hidden=64, seed=7, device=DEV)
+        agent.learner.small_updates = small
+        agent.update_log = []
+        agent.train(128, log=False)
+        torch.cuda.synchronize()
+        assert agent.learner.small_update_ok(agent.memory.observations.reshape(1024, -1), 128) == small
+        res.append(([u.cpu().numpy() for u in agent.update_log],
+                    [p.detach().cpu().numpy().copy() for p in agent.policy.parameters()]))
+    (log_s, par_s), (log_m, par_m) = res
+    assert len(log_s) == len(log_m) == 64
+    for u, (a, b) in enumerate(zip(log_s, log_m)):
+        np.testing.assert_allclose(a[:6], b[:6], rtol=1e-4, atol=1e-5, err_msg="update %d" % u)
+    for a, b in zip(par_s, par_m):
+        np.testing.assert_allclose(a, b, rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("n_steps,n_mb", [(128, 8), (100, 6)])
+def test_small_mlp_epoch_graphs_match_eager(n_steps, n_mb):
+    """K30 epochs captured as one graph (learners.small_epoch: eager the first epoch of a layout, captured the second,
+    replayed after) give the eager K30 run's parameters bit for bit — including a ragged last minibatch (800 rows in
+    minibatches of 133) — and the schedule cursor never runs past its window."""
+    from xuanpolicy_amd.runner import build_cartpole_ppo
+    out = []
+    for graphed in (False, True):
+        agent = build_cartpole_ppo(n_envs=8, n_steps=n_steps, hidden=64, seed=4, device=DEV, graph_update=graphed,
+                                   n_minibatch=n_mb, n_epoch=4)
+        for _ in range(3):
+            agent.train(n_steps, log=False)
+        torch.cuda.synchronize()
+        assert agent.learner.small_update_ok(agent.memory.observations.reshape(8 * n_steps, -1), agent.batch_size)
+        graphs = getattr(agent.learner, "_small_graphs", {})
+        assert sum(isinstance(v, tuple) for v in graphs.values()) == (1 if graphed else 0)
+        assert not agent.learner.fused_opt.sched_overflow()
+        out.append([p.detach().cpu().numpy().copy() for p in agent.policy.parameters()])
+    for a, b in zip(*out):
+        np.testing.assert_array_equal(b, a)

@@ -17,12 +17,28 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "libxuanpolicy_amd.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
 SOURCES = ["gae.hip", "loss.hip", "rollout.hip", "optim.hip", "mlp.hip", "head.hip", "thin.hip", "per.hip", "atari.hip",
-           "classic.hip", "dqn.hip", "conv.hip", "igemm.hip"]
+           "classic.hip", "dqn.hip", "conv.hip", "igemm.hip", "smallmlp.hip"]
 HEADER = os.path.join(REPO_DIR, "include", "xuanpolicy_amd.h")
 
 ABI_VERSION = 2
 
 c_i32, c_i64, c_u32, c_f32, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
+
+class XpaSmallMlpArgs(ctypes.Structure):
+    """include/xuanpolicy_amd.h XpaSmallMlpArgs (K30), field for field."""
+    _fields_ = ([(n, ctypes.c_int) for n in ("batch", "d_in", "h0", "h1", "h2", "k", "act_code", "algo", "use_advnorm",
+                                             "n_sched")]
+                + [(n, ctypes.c_float) for n in ("slope", "clip_range", "vf_coef", "ent_coef", "max_norm", "beta1",
+                                                 "beta2", "eps")]
+                + [("obs", ctypes.c_void_p), ("obs_ld", ctypes.c_int64), ("idx", ctypes.c_void_p),
+                   ("n_rows", ctypes.c_int64)]
+                + [(n, ctypes.c_void_p) for n in ("actions", "old_logp", "adv", "ret", "W0", "b0", "W1", "b1", "W2",
+                                                  "b2", "Wa", "ba", "Wc", "bc", "gW0", "gb0", "gW1", "gb1", "gW2",
+                                                  "gb2", "gWa", "gba", "gWc", "gbc", "param", "grad", "exp_avg",
+                                                  "exp_avg_sq")]
+                + [("n", ctypes.c_int64), ("sched", ctypes.c_void_p), ("cursor", ctypes.c_void_p),
+                   ("scalars", ctypes.c_void_p), ("total_norm_out", ctypes.c_void_p), ("stamps", ctypes.c_void_p)])
+
 
 # name -> (restype, argtypes); mirrors include/xuanpolicy_amd.h one-for-one.
 SIGNATURES = {
@@ -109,6 +125,8 @@ SIGNATURES = {
     "xpa_clip_adam_step_sched": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_p, c_f32, c_f32, c_f32, c_f32, c_p, c_i64,
                                                 c_p, c_p, c_p]),
     "xpa_adam_sched_entry": (None, [c_f32, c_f32, c_f32, c_i64, c_p]),
+    "xpa_small_mlp_lds_floats": (c_i64, [c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
+    "xpa_small_mlp_update": (ctypes.c_int, [c_p, c_p]),
     "xpa_colsum_finalize_batch": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p]),
     "xpa_per_store": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i64, c_i64, ctypes.c_double, c_p]),
     "xpa_per_update_priorities": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_i64, ctypes.c_double,

@@ -505,8 +505,19 @@ class _OnPolicyAgent:
         # as one captured graph once every slot is captured (learners.update_epoch)
         epoch_batches = (not rows_path and not self.global_advnorm and getattr(self.learner, "graph_updates", False)
                          and hasattr(self.learner, "update_epoch"))
+        # K30: the whole small-MLP update (gather + forward + loss + backward + clip + Adam) in one launch per
+        # minibatch, an epoch of them one captured graph (learners.small_epoch)
+        small = (not rows_path and not self.global_advnorm and hasattr(self.learner, "small_update_ok")
+                 and self.learner.small_update_ok(obs_flat, B))
         for _ in range(self.n_epoch):
             perm = self.epoch_permutation(NT)
+            if small:
+                batches = [(perm[s:s + B], act_flat, adv_flat, ret_flat, logp_flat) for s in range(0, NT, B)]
+                outs = self.learner.small_epoch(obs_flat, batches, use_advnorm, keep_all=self.update_log is not None)
+                scalars = outs[-1]
+                if self.update_log is not None:
+                    self.update_log.extend(outs)
+                continue
             batches = []
             for start in range(0, NT, B):
                 idx = perm[start:start + B]

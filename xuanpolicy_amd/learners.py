@@ -16,11 +16,12 @@ all-reduce when data-parallel] -> clip_grad_norm_ -> optimizer.step -> scheduler
     backward) and K9 — no autograd graph (DESIGN.md §3).  update() returns host floats like the reference (one sync);
 update_fused() keeps everything on device for the agent's hot loop.
 """
+import ctypes
 import os
 
 import torch
 
-from . import ops
+from . import _lib, ops
 from .policies import policy_heads
 
 
@@ -268,6 +269,127 @@ class _FusedPolicyGradient(Learner):
             graphs[key] = ent = (g, out, self._ws)   # the graph writes into this workspace: keep it alive
         ent[0].replay()
         return ent[1]
+
+    # ---- K30: the whole small-MLP update in one launch (C1) ----------------------------------------------------
+    def small_update_ok(self, obs_flat, batch):
+        """True when a minibatch of `batch` rows of obs_flat [n_rows, d] can take K30 (xpa_small_mlp_update): a
+        Categorical actor-critic of one representation layer and one hidden layer per head (all with the same
+        activation), flat parameters with the fused Adam, no data-parallel gradient sync, and the LDS budget."""
+        if not getattr(self, "small_updates", True) or self.grad_sync is not None or self.dist != "categorical":
+            return False
+        fm = self._fused_mlp()
+        fused = getattr(self, "fused_opt", None)
+        if fm is None or fused is None or len(fm.rep) != 1 or len(fm.actor) != 2 or len(fm.critic) != 2 \
+                or fused.fs.numel % 4:
+            return False
+        if not (isinstance(obs_flat, torch.Tensor) and obs_flat.is_cuda and obs_flat.dim() == 2
+                and obs_flat.dtype == torch.float32 and obs_flat.stride(1) == 1):
+            return False
+        (l0, c0, s0), (l1, c1, s1), (la, ca, _), (l2, c2, s2), (lc, cc, _) = (fm.rep[0], fm.actor[0], fm.actor[1],
+                                                                              fm.critic[0], fm.critic[1])
+        if not (c0 == c1 == c2 and s0 == s1 == s2 and ca == 0 and cc == 0 and lc.out_features == 1):
+            return False
+        h0, h1, h2, k = l0.out_features, l1.out_features, l2.out_features, la.out_features
+        if any(h % 4 or h > 256 for h in (h0, h1, h2)) or not 2 <= k <= 16 or l0.in_features != obs_flat.shape[1]:
+            return False
+        return int(ops.lib().xpa_small_mlp_lds_floats(batch, l0.in_features, h0, h1, h2, k)) <= 40704
+
+    def _small_launch(self, obs_flat, idx, act, adv, ret, old_logp, use_advnorm):
+        """One K30 launch (capturable): reads lr / Adam step at the schedule cursor and advances it."""
+        fm, fused = self._fused_mlp(), self.fused_opt
+        (l0, code, slope), (l1, _, _), (la, _, _), (l2, _, _), (lc, _, _) = (fm.rep[0], fm.actor[0], fm.actor[1],
+                                                                             fm.critic[0], fm.critic[1])
+        if getattr(self, "_small_scalars", None) is None:
+            self._small_scalars = torch.zeros(8, dtype=torch.float32, device=obs_flat.device)
+        g = self.optimizer.param_groups[0]
+        b1, b2 = g["betas"]
+        max_norm = float(self._max_norm) if self._use_clip else -1.0
+        a = _lib.XpaSmallMlpArgs()
+        a.batch, a.d_in, a.h0, a.h1, a.h2, a.k = (idx.shape[0], l0.in_features, l0.out_features, l1.out_features,
+                                                  l2.out_features, la.out_features)
+        a.act_code, a.algo, a.use_advnorm, a.n_sched = code, ops.ALGO[self.algo], int(bool(use_advnorm)), \
+            fused.SCHED_WINDOW
+        a.slope, a.clip_range, a.vf_coef, a.ent_coef = slope, float(self.clip_range), float(self.vf_coef), \
+            float(self.ent_coef)
+        a.max_norm, a.beta1, a.beta2, a.eps = max_norm, float(b1), float(b2), float(g["eps"])
+        a.obs, a.obs_ld, a.idx, a.n_rows = obs_flat.data_ptr(), obs_flat.stride(0), idx.data_ptr(), obs_flat.shape[0]
+        a.actions, a.adv, a.ret = act.data_ptr(), adv.data_ptr(), ret.data_ptr()
+        a.old_logp = old_logp.data_ptr() if old_logp is not None else None
+        a.W0, a.b0, a.W1, a.b1 = l0.weight.data_ptr(), l0.bias.data_ptr(), l1.weight.data_ptr(), l1.bias.data_ptr()
+        a.W2, a.b2, a.Wa, a.ba = l2.weight.data_ptr(), l2.bias.data_ptr(), la.weight.data_ptr(), la.bias.data_ptr()
+        a.Wc, a.bc = lc.weight.data_ptr(), lc.bias.data_ptr()
+        a.gW0, a.gb0, a.gW1, a.gb1 = (l0.weight.grad.data_ptr(), l0.bias.grad.data_ptr(), l1.weight.grad.data_ptr(),
+                                      l1.bias.grad.data_ptr())
+        a.gW2, a.gb2, a.gWa, a.gba = (l2.weight.grad.data_ptr(), l2.bias.grad.data_ptr(), la.weight.grad.data_ptr(),
+                                      la.bias.grad.data_ptr())
+        a.gWc, a.gbc = lc.weight.grad.data_ptr(), lc.bias.grad.data_ptr()
+        a.param, a.grad = fused.fs.param.data_ptr(), fused.fs.flat.data_ptr()
+        a.exp_avg, a.exp_avg_sq, a.n = fused.exp_avg.data_ptr(), fused.exp_avg_sq.data_ptr(), fused.fs.numel
+        a.sched, a.cursor = fused._sched.data_ptr(), fused._cursor.data_ptr()
+        a.scalars, a.total_norm_out = self._small_scalars.data_ptr(), fused.total_norm.data_ptr()
+        st = getattr(self, "small_stamps", None)   # diagnostics: int64 [16] of phase timestamps (tools/k30_stamps.py)
+        a.stamps = st.data_ptr() if st is not None else None
+        _lib.check(ops.lib().xpa_small_mlp_update(ctypes.byref(a), ops._stream(obs_flat.device)),
+                   "xpa_small_mlp_update")
+        return self._small_scalars
+
+    def small_update(self, obs_flat, idx, act, adv, ret, old_logp=None, use_advnorm=True):
+        """One minibatch update through K30 (eager): the device part, then the host bookkeeping of the step."""
+        fused = self.fused_opt
+        if not fused.sched_enabled:
+            fused.enable_sched()
+        fused.ensure_window(self.scheduler)
+        self.iterations += 1
+        out = self._small_launch(obs_flat, idx, act, adv, ret, old_logp, use_advnorm)
+        fused.host_step()
+        if self.scheduler is not None:
+            self.scheduler.step()
+        return out
+
+    def small_epoch(self, obs_flat, batches, use_advnorm, keep_all=False):
+        """An epoch of K30 updates, batches = [(idx, act, adv, ret, old_logp), ...]: eager the first time a batch
+        layout is seen, then captured once as one graph (the launches read the schedule at the device cursor) and
+        replayed.  Returns the per-update loss-scalar tensors (see update_epoch for keep_all)."""
+        fused = self.fused_opt
+        if not fused.sched_enabled:
+            fused.enable_sched()
+        ptr = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+        key = (ptr(obs_flat), tuple(obs_flat.shape), bool(use_advnorm), float(self.clip_range), float(self.vf_coef),
+               float(self.ent_coef)) + tuple((ptr(b[0]), b[0].shape[0], ptr(b[1]), ptr(b[2]), ptr(b[3]), ptr(b[4]))
+                                            for b in batches)
+        graphs = self.__dict__.setdefault("_small_graphs", {})
+        ent = graphs.get(key)
+        graphed = getattr(self, "graph_updates", False) and not getattr(self, "_graph_failed", False) \
+            and len(batches) <= fused.SCHED_WINDOW
+        if ent is None or not graphed:
+            outs = []
+            for b in batches:
+                out = self.small_update(obs_flat, *b, use_advnorm=use_advnorm)
+                outs.append(out.clone() if keep_all else out)
+            if graphed:
+                graphs[key] = "warm"
+            return outs
+        fused.ensure_window(self.scheduler, need=len(batches))
+        if ent == "warm":
+            if self.__dict__.get("_graph_pool") is None:
+                self._graph_pool = torch.cuda.graph_pool_handle()
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g, pool=self._graph_pool):
+                    outs = [self._small_launch(obs_flat, *b, use_advnorm=use_advnorm).clone() for b in batches]
+            except Exception:
+                self._graph_failed = True
+                torch.cuda.synchronize()
+                del graphs[key]
+                return self.small_epoch(obs_flat, batches, use_advnorm, keep_all)
+            graphs[key] = ent = (g, outs)
+        ent[0].replay()
+        for _ in batches:
+            self.iterations += 1
+            fused.host_step()
+            if self.scheduler is not None:
+                self.scheduler.step()
+        return [o.clone() for o in ent[1]] if keep_all else list(ent[1])
 
     def update_epoch(self, batches, keep_all=False):
         """One epoch of minibatch updates, batches = [(obs, idx, act, adv, ret, old_logp, adv_partials, pre), ...].
