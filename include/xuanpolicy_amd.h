@@ -287,7 +287,8 @@ void xpa_adam_sched_entry(float lr, float beta1, float beta2, int64_t step, floa
  * gradient into its view of the flat gradient buffer), clip_grad_norm_(max_norm; < 0: none) and Adam over the flat
  * buffers [0, n) with (lr, step) from the device schedule at cursor (xpa_clip_adam_step_sched's convention; the
  * launch advances cursor[0]).  Replaces ~25 launches per update of the C1 configuration (ppoclip_learner.py:24-65).
- * Limits: h0, h1, h2 multiples of 4 and <= 256, 2 <= k <= 16, xpa_small_mlp_lds_floats(...) <= 40704. */
+ * Limits: d_in <= 32, h0, h1, h2 multiples of 32 and <= 256, 2 <= k <= 16, xpa_small_mlp_lds_floats(...) <= 40704;
+ * the flat buffers 16-B aligned with n % 4 == 0.  The products run on v_mfma_f32_32x32x2_f32 (exact f32 fma chains). */
 typedef struct XpaSmallMlpArgs {
     int batch, d_in, h0, h1, h2, k, act_code, algo, use_advnorm, n_sched;
     float slope, clip_range, vf_coef, ent_coef, max_norm, beta1, beta2, eps;

@@ -11,12 +11,12 @@
 // ~25 launches it was bound by their latency (~105 us per update); here one workgroup of 512 threads keeps every
 // activation in LDS and the update takes one launch.
 //
-// Layout: activations transposed, [feature][batch] with row stride BPS = BP + 4 (BP = batch rounded up to 4; the
-// +4 puts consecutive feature rows 4 banks apart, so the 16 rows a wave reads in a tile step are conflict-free).
-// Forward tiles: a thread owns 4 output features x 4 rows and walks the input features (one ds_read_b128 of the
-// input rows, one of the transposed weights, 16 FMAs).  Weight gradients: a thread owns 4 x 4 (out, in) and walks
-// the rows 4 at a time (8 ds_read_b128, 64 FMAs).  In-place reuse: h1 / h2 become dh1 / dh2 once the output layers'
-// weight gradients are formed, h0 becomes dh0 once the hidden layers' weight gradients are formed.
+// Layout: activations transposed, [feature][batch] with row stride S = BP + 4 (BP = batch rounded up to 32).
+// Every product (the five forward layers, the five weight gradients, the two data gradients) is a set of 32 x 32
+// tiles on v_mfma_f32_32x32x2_f32 (exact f32 fma chains), one wave per tile, operands read straight from the LDS
+// images with per-operand strides (the first form, VALU 4 x 4 register tiles, was bound by its LDS round trips:
+// 95 us per update at C1, 222 k cycles of which 41 k in the output layers alone).  In-place reuse: h1 / h2 become
+// dh1 / dh2 once the output layers' weight gradients are formed, h0 becomes dh0 once the hidden ones' are.
 // Arithmetic of the loss and of the clip + Adam step: exactly K2's per-row formulas (loss.hip) and K9's (optim.hip).
 #include "xpa_common.h"
 
@@ -25,6 +25,7 @@ namespace {
 constexpr int kSmThreads = 512;
 constexpr int kSmWaves = kSmThreads / 64;
 constexpr int kSmLds = 40704;   // floats (159 KiB: the rest of the 160 KiB holds the reduction scratch)
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 template <int ACT>
 __device__ __forceinline__ float sm_act(float z, float slope) {
@@ -39,90 +40,38 @@ __device__ __forceinline__ float sm_grad(float y, float slope) {   // d act / d 
     return 1.f;
 }
 
-// outT[j][b] = act(bias[j] + sum_i inT[i][b] WT[i][j]),  j < HO, b < BP (row stride S, WT row stride HO)
-template <int ACT>
-__device__ void sm_fwd(const float *inT, int HI, const float *WT, const float *bias, int HO, float *outT, int BP,
-                       int S, float slope) {
-    const int tj = HO / 4, tb = BP / 4;
-    for (int t = threadIdx.x; t < tj * tb; t += kSmThreads) {
-        const int j0 = 4 * (t % tj), b0 = 4 * (t / tj);
-        float acc[4][4];
+// One 32 x 32 tile D[m][n] = sum_{k < kred} A(m, k) B(k, n) with A(m, k) = pa[k ak + m am], B(k, n) = pb[k bk + n bn]
+// (LDS), rows m >= mvalid / columns n >= nvalid of the operands read as 0.  Lane (i, h) feeds A(i, k + h) and
+// B(k + h, i); D element r of lane (i, h) is D[(r & 3) + 8 (r >> 2) + 4 h][i].
+__device__ __forceinline__ f32x16 sm_tile(const float *pa, int am, int ak, int mvalid, const float *pb, int bk, int bn,
+                                          int nvalid, int kred) {
+    const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
+    const bool av = i < mvalid, bv = i < nvalid;
+    const float *qa = pa + (av ? i : 0) * am + h * ak, *qb = pb + (bv ? i : 0) * bn + h * bk;
+    f32x16 acc;
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    // 8 k-steps per group: the 16 operand reads issued before the group's MFMAs (a plain loop ran load, wait,
+    // MFMA per k-step: one LDS round trip per MFMA)
+    int k = 0;
+    for (; k + 16 <= kred; k += 16) {
+        float x[8], y[8];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
-#pragma unroll 4
-        for (int i = 0; i < HI; ++i) {
-            const float4 x = *reinterpret_cast<const float4 *>(inT + i * S + b0);
-            const float4 w = *reinterpret_cast<const float4 *>(WT + i * HO + j0);
-            const float xv[4] = {x.x, x.y, x.z, x.w}, wv[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(xv[c], wv[r], acc[r][c]);
+        for (int u = 0; u < 8; ++u) {
+            x[u] = qa[(k + 2 * u) * ak];
+            y[u] = qb[(k + 2 * u) * bk];
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            float4 o;
-            o.x = sm_act<ACT>(acc[r][0] + bias[j0 + r], slope);
-            o.y = sm_act<ACT>(acc[r][1] + bias[j0 + r], slope);
-            o.z = sm_act<ACT>(acc[r][2] + bias[j0 + r], slope);
-            o.w = sm_act<ACT>(acc[r][3] + bias[j0 + r], slope);
-            *reinterpret_cast<float4 *>(outT + (j0 + r) * S + b0) = o;
-        }
+        for (int u = 0; u < 8; ++u)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av ? x[u] : 0.f, bv ? y[u] : 0.f, acc, 0, 0, 0);
     }
-}
-
-// gW[j][i] = sum_b dT[j][b] inT[i][b] (j < JO rows and i < IV columns written, JP / HI padded to 4), gb[j] =
-// sum_b dT[j][b]; b < BP (padding rows of dT are 0).  Written to global in torch's [out][in] layout ([JO][IV]);
-// squares summed into sq (per thread, f64).
-__device__ void sm_wgrad(const float *dT, int JO, int JP, const float *inT, int HI, int IV, int BP, int S, float *gW,
-                         float *gb, double &sq) {
-    const int tj = JP / 4, ti = HI / 4;
-    for (int t = threadIdx.x; t < tj * ti; t += kSmThreads) {
-        const int j0 = 4 * (t % tj), i0 = 4 * (t / tj);
-        float acc[4][4], bs[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
-#pragma unroll 2
-        for (int b = 0; b < BP; b += 4) {
-            float4 d[4], x[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) d[r] = *reinterpret_cast<const float4 *>(dT + (j0 + r) * S + b);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) x[c] = *reinterpret_cast<const float4 *>(inT + (i0 + c) * S + b);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    float a = acc[r][c];
-                    a = fmaf(d[r].x, x[c].x, a);
-                    a = fmaf(d[r].y, x[c].y, a);
-                    a = fmaf(d[r].z, x[c].z, a);
-                    a = fmaf(d[r].w, x[c].w, a);
-                    acc[r][c] = a;
-                }
-                if (i0 == 0) bs[r] += (d[r].x + d[r].y) + (d[r].z + d[r].w);
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            if (j0 + r >= JO) continue;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                if (i0 + c >= IV) continue;
-                gW[(j0 + r) * IV + i0 + c] = acc[r][c];
-                sq += (double)acc[r][c] * acc[r][c];
-            }
-            if (i0 == 0) {
-                gb[j0 + r] = bs[r];
-                sq += (double)bs[r] * bs[r];
-            }
-        }
+    for (; k < kred; k += 2) {
+        const float x = qa[k * ak], y = qb[k * bk];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av ? x : 0.f, bv ? y : 0.f, acc, 0, 0, 0);
     }
+    return acc;
 }
+__device__ __forceinline__ int sm_row(int r) { return (r & 3) + 8 * (r >> 2) + 4 * ((threadIdx.x & 63) >> 5); }
 
 #define XPA_SM_STAMP(i_)                                                                  \
     do {                                                                                  \
@@ -134,91 +83,197 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
     __shared__ __attribute__((aligned(16))) float lds[kSmLds];
     __shared__ double s_red[kSmWaves * 6];
     __shared__ float s_stat[4];
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int B = a.batch, BP = (B + 3) & ~3, S = BP + 4;
+    __shared__ float s_coef, s_step, s_inv;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, li = lane & 31;
+    const int B = a.batch, BP = (B + 31) & ~31, S = BP + 4;
     const int D = a.d_in, DP = (a.d_in + 3) & ~3, H0 = a.h0, H1 = a.h1, H2 = a.h2, K = a.k, KP = (a.k + 3) & ~3;
+    const int MB = BP / 32;
+    const float slope = a.slope;
     // ---- LDS carve (offsets multiples of 4 floats) ----
     float *xT = lds;                       // [DP][S]
     float *h0T = xT + DP * S;              // [H0][S]  -> dh0
     float *h1T = h0T + H0 * S;             // [H1][S]  -> dh1
     float *h2T = h1T + H1 * S;             // [H2][S]  -> dh2
     float *dlT = h2T + H2 * S;             // [KP][S]  d logits (rows >= K zero)
-    float *dvT = dlT + KP * S;             // [4][S]   d v in row 0, rows 1-3 zero
+    float *dvT = dlT + KP * S;             // [4][S]   d v in row 0
     float *W0T = dvT + 4 * S;              // [DP][H0]
-    float *W1T = W0T + DP * H0;            // [H0][H1]
-    float *W2T = W1T + H0 * H1;            // [H0][H2]
+    float *W1T = W0T + DP * H0;            // [H0][H1], after the forward W1 row-major [H1][H0]
+    float *W2T = W1T + H0 * H1;            // [H0][H2], after the forward W2 row-major [H2][H0]
     float *WaT = W2T + H0 * H2;            // [H1][KP]
-    float *WcT = WaT + H1 * KP;            // [H2][4]  (column 0)
-    float *bias = WcT + H2 * 4;            // b0 | b1 | b2 | ba (KP) | bc (4)
-    float *b0s = bias, *b1s = b0s + H0, *b2s = b1s + H1, *bas = b2s + H2, *bcs = bas + KP;
-    float *rowf = bcs + 4;                 // act, old_logp, adv, ret: [4][BP]
-    float *logit = rowf + 4 * BP;          // [BP][KP] (row-major, the loss reads its row)
+    float *Wcv = WaT + H1 * KP;            // [H2]
+    float *b0s = Wcv + H2, *b1s = b0s + H0, *b2s = b1s + H1, *bas = b2s + H2, *bcs = bas + KP;
+    float *rowf = bcs + 4;                 // action, old_logp, adv, ret: [4][BP]
+    float *logit = rowf + 4 * BP;          // [BP][KP]
     float *vrow = logit + BP * KP;         // [BP]
     XPA_SM_STAMP(0);
-    // ---- stage the weights (transposed), biases, the minibatch rows through idx ----
-    // coalesced reads of the row-major torch weights, 8 loads in flight per thread, scattered LDS writes (a
-    // load-wait-store loop costs one global latency per element: ~30 us of this kernel at C1 before)
-    auto stage_T = [&](const float *src, int rows, int cols, float *dst, int ldd, int col_limit) {
-        // dst[c * ldd + r] = src[r * cols + c] for r < rows, c < cols (c >= col_limit: 0)
-        const int n = rows * cols;
-        for (int e0 = t; e0 < n; e0 += 8 * kSmThreads) {
-            float v[8];
+    // ---- staging: two global round trips in all — the row indices with every weight load, then the rows ----
+    // (five dependent load / store rounds took ~21 k cycles before)
+    const int n0 = H0 * D, na = K * H1, nm = n0 + na + H2 + H0 + H1 + H2 + K + 1;   // W0 | Wa | Wc | biases
+    const int nw1 = H0 * H1, nw2 = H0 * H2;
+    const bool fast = nm <= 2 * kSmThreads && nw1 <= 8 * kSmThreads && nw2 <= 8 * kSmThreads && BP <= kSmThreads;
+    // element e of the small-tensor range: its source (loads) and LDS destination (stores)
+    auto msrc_of = [&](int e, int &off) -> const float * {
+        if (e < n0) { off = e; return a.W0; }
+        if ((e -= n0) < na) { off = e; return a.Wa; }
+        if ((e -= na) < H2) { off = e; return a.Wc; }
+        if ((e -= H2) < H0) { off = e; return a.b0; }
+        if ((e -= H0) < H1) { off = e; return a.b1; }
+        if ((e -= H1) < H2) { off = e; return a.b2; }
+        if ((e -= H2) < K) { off = e; return a.ba; }
+        off = 0;
+        return a.bc;
+    };
+    auto mdst_of = [&](int e) -> float * {
+        if (e < n0) return W0T + (e % D) * H0 + e / D;
+        if ((e -= n0) < na) return WaT + (e % H1) * KP + e / H1;
+        if ((e -= na) < H2) return Wcv + e;
+        if ((e -= H2) < H0) return b0s + e;
+        if ((e -= H0) < H1) return b1s + e;
+        if ((e -= H1) < H2) return b2s + e;
+        if ((e -= H2) < K) return bas + e;
+        return bcs;
+    };
+    if (fast) {
+        const bool rb = t < BP && t < B;
+        int64_t row = rb ? a.idx[t] : 0;
+        float vm[2], v1[8], v2[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int e = e0 + u * kSmThreads;
-                v[u] = e < n ? src[e] : 0.f;
+        for (int u = 0; u < 2; ++u) {
+            int off;
+            const float *src = msrc_of(t + u * kSmThreads, off);
+            vm[u] = t + u * kSmThreads < nm ? src[off] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {   // destination order (see stage_T below)
+            const int e1 = t + u * kSmThreads;
+            v1[u] = e1 < nw1 ? a.W1[(e1 % H1) * H0 + e1 / H1] : 0.f;
+            v2[u] = e1 < nw2 ? a.W2[(e1 % H2) * H0 + e1 / H2] : 0.f;
+        }
+        // the rows (second round trip)
+        const bool valid = rb && row >= 0 && row < a.n_rows;
+        const int64_t rc = valid ? row : 0;
+        float xo[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) xo[i] = i < D ? a.obs[rc * a.obs_ld + i] : 0.f;
+        const float act_v = a.actions[rc], lp_v = a.old_logp ? a.old_logp[rc] : 0.f, av = a.adv[rc], rt = a.ret[rc];
+        // LDS stores
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (t + u * kSmThreads < nm) *mdst_of(t + u * kSmThreads) = vm[u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e1 = t + u * kSmThreads;
+            if (e1 < nw1) W1T[e1] = v1[u];
+            if (e1 < nw2) W2T[e1] = v2[u];
+        }
+        if (t < BP) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i)
+                if (i < DP) xT[i * S + t] = valid ? xo[i] : 0.f;
+            rowf[0 * BP + t] = valid ? act_v : 0.f;
+            rowf[1 * BP + t] = valid ? lp_v : 0.f;
+            rowf[2 * BP + t] = valid ? av : 0.f;
+            rowf[3 * BP + t] = valid ? rt : 0.f;
+        }
+    } else {
+    {
+        // the small tensors as one virtual range: W0 [H0][D] | Wa [K][H1] | Wc [H2] | b0 | b1 | b2 | ba | bc
+        const int n0 = H0 * D, na = K * H1, nm = n0 + na + H2 + H0 + H1 + H2 + K + 1;
+        for (int e0 = t; e0 < nm; e0 += 4 * kSmThreads) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                int e = e0 + u * kSmThreads;
+                const float *src = a.bc;
+                int off = 0;
+                if (e < n0) { src = a.W0; off = e; }
+                else if ((e -= n0) < na) { src = a.Wa; off = e; }
+                else if ((e -= na) < H2) { src = a.Wc; off = e; }
+                else if ((e -= H2) < H0) { src = a.b0; off = e; }
+                else if ((e -= H0) < H1) { src = a.b1; off = e; }
+                else if ((e -= H1) < H2) { src = a.b2; off = e; }
+                else if ((e -= H2) < K) { src = a.ba; off = e; }
+                v[u] = e0 + u * kSmThreads < nm ? src[off] : 0.f;
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int e = e0 + u * kSmThreads;
-                if (e < n) {
-                    const int r = e / cols, c = e - (e / cols) * cols;
-                    dst[c * ldd + r] = c < col_limit ? v[u] : 0.f;
-                }
+            for (int u = 0; u < 4; ++u) {
+                int e = e0 + u * kSmThreads;
+                if (e >= nm) continue;
+                if (e < n0) { W0T[(e % D) * H0 + e / D] = v[u]; continue; }
+                if ((e -= n0) < na) { WaT[(e % H1) * KP + e / H1] = v[u]; continue; }
+                if ((e -= na) < H2) { Wcv[e] = v[u]; continue; }
+                if ((e -= H2) < H0) { b0s[e] = v[u]; continue; }
+                if ((e -= H0) < H1) { b1s[e] = v[u]; continue; }
+                if ((e -= H1) < H2) { b2s[e] = v[u]; continue; }
+                if ((e -= H2) < K) { bas[e] = v[u]; continue; }
+                bcs[0] = v[u];
             }
         }
-    };
-    stage_T(a.W0, H0, D, W0T, H0, D);               // W0 [H0][D] -> W0T [D][H0] (rows D .. DP zeroed below)
-    for (int e = t; e < (DP - D) * H0; e += kSmThreads) W0T[D * H0 + e] = 0.f;
-    stage_T(a.W1, H1, H0, W1T, H1, H0);             // W1 [H1][H0] -> W1T [H0][H1]
-    stage_T(a.W2, H2, H0, W2T, H2, H0);             // W2 [H2][H0] -> W2T [H0][H2]
-    for (int e = t; e < H1 * KP; e += kSmThreads) WaT[e] = 0.f;
-    for (int e = t; e < H2 * 4; e += kSmThreads) WcT[e] = 0.f;
-    __syncthreads();
-    stage_T(a.Wa, K, H1, WaT, KP, H1);              // Wa [K][H1] -> WaT [H1][KP]
-    stage_T(a.Wc, 1, H2, WcT, 4, H2);               // Wc [1][H2] -> WcT [H2][4] column 0
-    for (int e = t; e < H0; e += kSmThreads) b0s[e] = a.b0[e];
-    for (int e = t; e < H1; e += kSmThreads) b1s[e] = a.b1[e];
-    for (int e = t; e < H2; e += kSmThreads) b2s[e] = a.b2[e];
-    for (int e = t; e < KP; e += kSmThreads) bas[e] = e < K ? a.ba[e] : 0.f;
-    if (t < 4) bcs[t] = t == 0 ? a.bc[0] : 0.f;
-    double adv_s = 0.0, adv_q = 0.0;
+        // zero pads: W0T rows D .. DP, WaT columns K .. KP, ba K .. KP
+        for (int e = t; e < (DP - D) * H0; e += kSmThreads) W0T[D * H0 + e] = 0.f;
+        for (int e = t; e < H1 * (KP - K); e += kSmThreads) WaT[(e / (KP - K)) * KP + K + e % (KP - K)] = 0.f;
+        for (int e = K + t; e < KP; e += kSmThreads) bas[e] = 0.f;
+        // W1 [H1][H0] -> W1T [H0][H1], W2 likewise: 8 loads per thread in flight
+        // walked in destination order (dst[e], e = i rows + j, from src[j cols + i]): consecutive lanes write
+        // consecutive LDS words (source order made every lane of a wave hit one bank: a 64-way conflict per write)
+        auto stage_T = [&](const float *src, int rows, int cols, float *dst) {
+            const int n = rows * cols;
+            for (int e0 = t; e0 < n; e0 += 8 * kSmThreads) {
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int e = e0 + u * kSmThreads;
+                    v[u] = e < n ? src[(e % rows) * cols + e / rows] : 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (e0 + u * kSmThreads < n) dst[e0 + u * kSmThreads] = v[u];
+            }
+        };
+        stage_T(a.W1, H1, H0, W1T);
+        stage_T(a.W2, H2, H0, W2T);
+    }
+    double adv_s0 = 0.0, adv_q0 = 0.0;
     for (int b = t; b < BP; b += kSmThreads) {
         const bool ok = b < B;
         const int64_t row = ok ? a.idx[b] : 0;
         const bool valid = ok && row >= 0 && row < a.n_rows;
         const int64_t rc = valid ? row : 0;
-        for (int i = 0; i < DP; ++i) xT[i * S + b] = valid && i < D ? a.obs[rc * a.obs_ld + i] : 0.f;
-        const float av = valid ? a.adv[rc] : 0.f;
-        rowf[0 * BP + b] = valid ? a.actions[rc] : 0.f;
-        rowf[1 * BP + b] = valid && a.old_logp ? a.old_logp[rc] : 0.f;
-        rowf[2 * BP + b] = av;
-        rowf[3 * BP + b] = valid ? a.ret[rc] : 0.f;
-        if (ok) {   // the minibatch advantage moments (K4's (sum, sumsq) in f64), over the batch rows
-            adv_s += (double)av;
-            adv_q += (double)av * av;
+        float xo[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) xo[i] = i < D ? a.obs[rc * a.obs_ld + i] : 0.f;
+        const float act_v = a.actions[rc], lp_v = a.old_logp ? a.old_logp[rc] : 0.f, av = a.adv[rc], rt = a.ret[rc];
+#pragma unroll
+        for (int i = 0; i < 32; ++i)
+            if (i < DP) xT[i * S + b] = valid ? xo[i] : 0.f;
+        rowf[0 * BP + b] = valid ? act_v : 0.f;
+        rowf[1 * BP + b] = valid ? lp_v : 0.f;
+        rowf[2 * BP + b] = valid ? av : 0.f;
+        rowf[3 * BP + b] = valid ? rt : 0.f;
+        if (ok) {   // the minibatch advantage moments (K4's (sum, sumsq) in f64) over the batch rows
+            const double ad = valid ? (double)av : 0.0;
+            adv_s0 += ad;
+            adv_q0 += ad * ad;
         }
     }
-    // rows BP .. S of every [feature][S] array are never read; zero the padded dvT rows 1-3 and dlT rows >= K
+    }
+    for (int e = t; e < (DP - D) * H0; e += kSmThreads) W0T[D * H0 + e] = 0.f;
+    for (int e = t; e < H1 * (KP - K); e += kSmThreads) WaT[(e / (KP - K)) * KP + K + e % (KP - K)] = 0.f;
+    for (int e = K + t; e < KP; e += kSmThreads) bas[e] = 0.f;
+    __syncthreads();   // the rows' advantages are in LDS
+    double adv_s = 0.0, adv_q = 0.0;
+    for (int b = t; b < B; b += kSmThreads) {   // the minibatch advantage moments (K4's (sum, sumsq) in f64)
+        const double ad = (double)rowf[2 * BP + b];
+        adv_s += ad;
+        adv_q += ad * ad;
+    }
     for (int e = t; e < 4 * S; e += kSmThreads) dvT[e] = 0.f;
     for (int e = t; e < KP * S; e += kSmThreads) dlT[e] = 0.f;
-    {
-        adv_s = xpa_wave_sum(adv_s);
-        adv_q = xpa_wave_sum(adv_q);
-        if (lane == 0) {
-            s_red[w] = adv_s;
-            s_red[kSmWaves + w] = adv_q;
-        }
+    adv_s = xpa_wave_sum(adv_s);
+    adv_q = xpa_wave_sum(adv_q);
+    if (lane == 0) {
+        s_red[w] = adv_s;
+        s_red[kSmWaves + w] = adv_q;
     }
     __syncthreads();
     if (t == 0) {
@@ -238,30 +293,46 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
         }
     }
     XPA_SM_STAMP(1);
-    // ---- forward ----
-    sm_fwd<ACT>(xT, DP, W0T, b0s, H0, h0T, BP, S, a.slope);
+    // ---- forward: h0 = act(x W0^T + b0), then h1 / h2 from h0 ----
+    for (int tl = w; tl < MB * (H0 / 32); tl += kSmWaves) {
+        const int b0 = 32 * (tl % MB), j0 = 32 * (tl / MB);
+        const f32x16 acc = sm_tile(xT + b0, 1, S, 32, W0T + j0, H0, 1, 32, DP);
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            h0T[(j0 + li) * S + b0 + sm_row(r)] = sm_act<ACT>(acc[r] + b0s[j0 + li], slope);
+    }
     __syncthreads();
-    sm_fwd<ACT>(h0T, H0, W1T, b1s, H1, h1T, BP, S, a.slope);
-    sm_fwd<ACT>(h0T, H0, W2T, b2s, H2, h2T, BP, S, a.slope);
+    {
+        const int n1 = MB * (H1 / 32), n2 = MB * (H2 / 32);
+        for (int tl = w; tl < n1 + n2; tl += kSmWaves) {
+            const bool two = tl >= n1;
+            const int q = two ? tl - n1 : tl, b0 = 32 * (q % MB), j0 = 32 * (q / MB);
+            const int HO = two ? H2 : H1;
+            const float *WT = two ? W2T : W1T, *bb = two ? b2s : b1s;
+            float *outT = two ? h2T : h1T;
+            const f32x16 acc = sm_tile(h0T + b0, 1, S, 32, WT + j0, HO, 1, 32, H0);
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                outT[(j0 + li) * S + b0 + sm_row(r)] = sm_act<ACT>(acc[r] + bb[j0 + li], slope);
+        }
+    }
     __syncthreads();
     XPA_SM_STAMP(2);
-    // output layers: one thread per row (logits from h1, value from h2)
-    for (int b = t; b < BP; b += kSmThreads) {
-        float z[16];
+    // output layers: logits [BP][KP] from h1, v [BP] from h2
+    for (int tl = w; tl < 2 * MB; tl += kSmWaves) {
+        const bool val = tl >= MB;
+        const int b0 = 32 * (val ? tl - MB : tl);
+        const f32x16 acc = val ? sm_tile(h2T + b0, 1, S, 32, Wcv, 1, 0, 1, H2)
+                               : sm_tile(h1T + b0, 1, S, 32, WaT, KP, 1, KP, H1);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) z[k] = 0.f;
-        float vv = 0.f;
-        for (int j = 0; j < H1; ++j) {
-            const float h = h1T[j * S + b];
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if (k < KP) z[k] = fmaf(h, WaT[j * KP + k], z[k]);
+        for (int r = 0; r < 16; ++r) {
+            const int b = b0 + sm_row(r);
+            if (val) {
+                if (li == 0) vrow[b] = acc[r] + bcs[0];
+            } else if (li < KP) {
+                logit[b * KP + li] = acc[r] + bas[li];
+            }
         }
-        for (int j = 0; j < H2; ++j) vv = fmaf(h2T[j * S + b], WcT[j * 4], vv);
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if (k < KP) logit[b * KP + k] = z[k] + bas[k];
-        vrow[b] = vv + bcs[0];
     }
     __syncthreads();
     XPA_SM_STAMP(3);
@@ -344,92 +415,133 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
     XPA_SM_STAMP(4);
     // ---- backward ----
     double sq = 0.0;   // this thread's share of |grad|^2
-    sm_wgrad(dlT, K, KP, h1T, H1, H1, BP, S, a.gWa, a.gba, sq);   // output layers (they still read h1 / h2)
-    sm_wgrad(dvT, 1, 4, h2T, H2, H2, BP, S, a.gWc, a.gbc, sq);
+    // the hidden weights row-major ([j][i], over the transposed forward copies) for dh0: loads issued now, stored
+    // below (the forward is the last reader of the transposed images)
+    {
+        const int n1 = H1 * H0, n2 = H2 * H0;
+        for (int e0 = t; e0 < n1 + n2; e0 += 8 * kSmThreads) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = e0 + u * kSmThreads;
+                v[u] = e < n1 ? a.W1[e] : (e < n1 + n2 ? a.W2[e - n1] : 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = e0 + u * kSmThreads;
+                if (e < n1 + n2) W1T[e] = v[u];   // W2T == W1T + H0 H1: the W2 block follows contiguously
+            }
+        }
+    }
+    // output layers' weight gradients: gWa [K][H1] = dl^T h1, gWc [H2] = dv^T h2
+    for (int tl = w; tl < H1 / 32 + H2 / 32; tl += kSmWaves) {
+        const bool val = tl >= H1 / 32;
+        const int j0 = 32 * (val ? tl - H1 / 32 : tl);
+        const f32x16 acc = val ? sm_tile(dvT, S, 1, 1, h2T + j0 * S, 1, S, 32, BP)
+                               : sm_tile(dlT, S, 1, KP, h1T + j0 * S, 1, S, 32, BP);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = sm_row(r);
+            if (val ? m == 0 : m < K) {
+                const float g = acc[r];
+                if (val) a.gWc[j0 + li] = g;
+                else a.gWa[m * H1 + j0 + li] = g;
+                sq += (double)g * g;
+            }
+        }
+    }
     __syncthreads();
     XPA_SM_STAMP(5);
-    // dh1 = (dlogits Wa) act'(h1), dh2 = dv wc act'(h2): in place over h1 / h2
-    for (int e = t; e < H1 * BP; e += kSmThreads) {
-        const int j = e / BP, b = e % BP;
-        float g = 0.f;
-        for (int k = 0; k < K; ++k) g = fmaf(dlT[k * S + b], WaT[j * KP + k], g);
-        float *p = h1T + j * S + b;
-        *p = g * sm_grad<ACT>(*p, a.slope);
+    // dh1 = (dl Wa) act'(h1) on MFMA, dh2 = dv wc act'(h2) elementwise: in place over h1 / h2
+    for (int tl = w; tl < MB * (H1 / 32); tl += kSmWaves) {
+        const int b0 = 32 * (tl % MB), j0 = 32 * (tl / MB);
+        const f32x16 acc = sm_tile(dlT + b0, 1, S, 32, WaT + j0 * KP, 1, KP, 32, KP);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float *p = h1T + (j0 + li) * S + b0 + sm_row(r);
+            *p = acc[r] * sm_grad<ACT>(*p, slope);
+        }
     }
     for (int e = t; e < H2 * BP; e += kSmThreads) {
         const int j = e / BP, b = e % BP;
         float *p = h2T + j * S + b;
-        *p = dvT[b] * WcT[j * 4] * sm_grad<ACT>(*p, a.slope);
+        *p = dvT[b] * Wcv[j] * sm_grad<ACT>(*p, slope);
     }
     __syncthreads();
     XPA_SM_STAMP(6);
-    sm_wgrad(h1T, H1, H1, h0T, H0, H0, BP, S, a.gW1, a.gb1, sq);   // hidden layers (read h0)
-    sm_wgrad(h2T, H2, H2, h0T, H0, H0, BP, S, a.gW2, a.gb2, sq);
-    // the hidden weights row-major ([j][i], over the transposed forward copies) for dh0's 16-B weight reads
-    auto copy8 = [&](const float *src, float *dst, int n) {
-        for (int e0 = t; e0 < n; e0 += 8 * kSmThreads) {
-            float v[8];
+    // hidden layers' weight gradients: gW1 [H1][H0] = dh1^T h0, gW2 [H2][H0] = dh2^T h0
+    {
+        const int n1 = (H1 / 32) * (H0 / 32), n2 = (H2 / 32) * (H0 / 32);
+        for (int tl = w; tl < n1 + n2; tl += kSmWaves) {
+            const bool two = tl >= n1;
+            const int q = two ? tl - n1 : tl, j0 = 32 * (q % ((two ? H2 : H1) / 32)), i0 = 32 * (q / ((two ? H2 : H1) / 32));
+            const f32x16 acc = sm_tile((two ? h2T : h1T) + j0 * S, S, 1, 32, h0T + i0 * S, 1, S, 32, BP);
+            float *gW = two ? a.gW2 : a.gW1;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = e0 + u * kSmThreads < n ? src[e0 + u * kSmThreads] : 0.f;
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (e0 + u * kSmThreads < n) dst[e0 + u * kSmThreads] = v[u];
+            for (int r = 0; r < 16; ++r) {
+                const float g = acc[r];
+                gW[(j0 + sm_row(r)) * H0 + i0 + li] = g;
+                sq += (double)g * g;
+            }
         }
-    };
-    copy8(a.W1, W1T, H1 * H0);
-    copy8(a.W2, W2T, H2 * H0);
+    }
     __syncthreads();
     XPA_SM_STAMP(7);
-    // dh0 = (dh1 W1 + dh2 W2) act'(h0), in place over h0: thread tile 4 features x 4 rows
-    {
-        const int ti = H0 / 4, tb = BP / 4;
-        for (int q = t; q < ti * tb; q += kSmThreads) {
-            const int i0 = 4 * (q % ti), b0 = 4 * (q / ti);
-            float acc[4][4];
+    // dh0 = (dh1 W1 + dh2 W2) act'(h0), in place over h0
+    for (int tl = w; tl < MB * (H0 / 32); tl += kSmWaves) {
+        const int b0 = 32 * (tl % MB), i0 = 32 * (tl / MB);
+        f32x16 acc = sm_tile(h1T + b0, 1, S, 32, W1T + i0, H0, 1, 32, H1);
+        const f32x16 acc2 = sm_tile(h2T + b0, 1, S, 32, W1T + H1 * H0 + i0, H0, 1, 32, H2);
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
-            for (int j = 0; j < H1; ++j) {
-                const float4 d = *reinterpret_cast<const float4 *>(h1T + j * S + b0);
-                const float4 wq = *reinterpret_cast<const float4 *>(W1T + j * H0 + i0);   // W1[j][i0 .. i0 + 3]
-                const float dv[4] = {d.x, d.y, d.z, d.w}, wr[4] = {wq.x, wq.y, wq.z, wq.w};
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(dv[c], wr[r], acc[r][c]);
-            }
-            for (int j = 0; j < H2; ++j) {
-                const float4 d = *reinterpret_cast<const float4 *>(h2T + j * S + b0);
-                const float4 wq = *reinterpret_cast<const float4 *>(W2T + j * H0 + i0);   // W2[j][i0 .. i0 + 3]
-                const float dv[4] = {d.x, d.y, d.z, d.w}, wr[4] = {wq.x, wq.y, wq.z, wq.w};
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(dv[c], wr[r], acc[r][c]);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float4 *p = reinterpret_cast<float4 *>(h0T + (i0 + r) * S + b0);
-                float4 y = *p;
-                y.x = acc[r][0] * sm_grad<ACT>(y.x, a.slope);
-                y.y = acc[r][1] * sm_grad<ACT>(y.y, a.slope);
-                y.z = acc[r][2] * sm_grad<ACT>(y.z, a.slope);
-                y.w = acc[r][3] * sm_grad<ACT>(y.w, a.slope);
-                // padding rows b >= B: their dh1 / dh2 are 0 (dlT / dvT are 0 there), so dh0 is 0 too
-                *p = y;
-            }
+        for (int r = 0; r < 16; ++r) {
+            float *p = h0T + (i0 + li) * S + b0 + sm_row(r);
+            *p = (acc[r] + acc2[r]) * sm_grad<ACT>(*p, slope);
         }
     }
     __syncthreads();
     XPA_SM_STAMP(8);
-    sm_wgrad(h0T, H0, H0, xT, DP, D, BP, S, a.gW0, a.gb0, sq);   // first layer ([H0][D]: padding columns dropped)
+    // first layer's weight gradient gW0 [H0][D] = dh0^T x, and every bias gradient (row sums over the batch)
+    for (int tl = w; tl < H0 / 32; tl += kSmWaves) {
+        const int i0 = 32 * tl;
+        const f32x16 acc = sm_tile(h0T + i0 * S, S, 1, 32, xT, 1, S, DP, BP);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if (li < D) {
+                const float g = acc[r];
+                a.gW0[(i0 + sm_row(r)) * D + li] = g;
+                sq += (double)g * g;
+            }
+        }
+    }
+    {
+        // bias gradients: one thread per output feature, its row summed with 16-B reads (BP % 32 == 0)
+        const int nr = H0 + H1 + H2 + K + 1;
+        for (int f = t; f < nr; f += kSmThreads) {
+            const float *src;
+            float *dst;
+            if (f < H0) { src = h0T + f * S; dst = a.gb0 + f; }
+            else if (f < H0 + H1) { src = h1T + (f - H0) * S; dst = a.gb1 + f - H0; }
+            else if (f < H0 + H1 + H2) { src = h2T + (f - H0 - H1) * S; dst = a.gb2 + f - H0 - H1; }
+            else if (f < H0 + H1 + H2 + K) { src = dlT + (f - H0 - H1 - H2) * S; dst = a.gba + f - H0 - H1 - H2; }
+            else { src = dvT; dst = a.gbc; }
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+            for (int b = 0; b < BP; b += 4) {
+                const float4 v = *reinterpret_cast<const float4 *>(src + b);
+                s0 += v.x;
+                s1 += v.y;
+                s2 += v.z;
+                s3 += v.w;
+            }
+            const float s = (s0 + s1) + (s2 + s3);
+            *dst = s;
+            sq += (double)s * s;
+        }
+    }
     XPA_SM_STAMP(9);
     // ---- clip_grad_norm_ + Adam over the flat buffers (K9's arithmetic, schedule at the device cursor) ----
     sq = xpa_wave_sum(sq);
     if (lane == 0) s_red[w] = sq;
     __syncthreads();   // also orders every gradient store of the block before the flat-buffer reads below
-    __shared__ float s_coef, s_step, s_inv;
     if (t == 0) {
         double s = 0.0;
         for (int i = 0; i < kSmWaves; ++i) s += s_red[i];
@@ -494,16 +606,16 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
 }  // namespace
 
 XPA_API int64_t xpa_small_mlp_lds_floats(int64_t batch, int64_t d_in, int64_t h0, int64_t h1, int64_t h2, int64_t k) {
-    const int64_t BP = (batch + 3) & ~3, S = BP + 4, DP = (d_in + 3) & ~3, KP = (k + 3) & ~3;
-    return DP * S + (h0 + h1 + h2) * S + KP * S + 4 * S + DP * h0 + h0 * h1 + h0 * h2 + h1 * KP + h2 * 4 + h0 + h1 +
-           h2 + KP + 4 + 4 * BP + BP * KP + BP;
+    const int64_t BP = (batch + 31) & ~31, S = BP + 4, DP = (d_in + 3) & ~3, KP = (k + 3) & ~3;
+    return DP * S + (h0 + h1 + h2) * S + KP * S + 4 * S + DP * h0 + h0 * h1 + h0 * h2 + h1 * KP + h2 + h0 + h1 + h2 +
+           KP + 4 + 4 * BP + BP * KP + BP;
 }
 
 XPA_API int xpa_small_mlp_update(const XpaSmallMlpArgs *args, xpa_stream_t stream) {
     if (!args) return (int)hipErrorInvalidValue;
     const XpaSmallMlpArgs &a = *args;
-    if (a.batch < 1 || a.d_in < 1 || a.h0 < 4 || a.h1 < 4 || a.h2 < 4 || a.h0 % 4 || a.h1 % 4 || a.h2 % 4 ||
-        a.h0 > 256 || a.h1 > 256 || a.h2 > 256 || a.k < 2 || a.k > 16 || a.act_code < 0 || a.act_code > 2 ||
+    if (a.batch < 1 || a.d_in < 1 || a.d_in > 32 || a.h0 < 32 || a.h1 < 32 || a.h2 < 32 || a.h0 % 32 || a.h1 % 32 ||
+        a.h2 % 32 || a.h0 > 256 || a.h1 > 256 || a.h2 > 256 || a.k < 2 || a.k > 16 || a.act_code < 0 || a.act_code > 2 ||
         (a.algo != XPA_ALGO_PPO && a.algo != XPA_ALGO_A2C) || (a.algo == XPA_ALGO_PPO && !a.old_logp) || !a.obs ||
         !a.idx || !a.actions || !a.adv || !a.ret || !a.param || !a.grad || !a.exp_avg || !a.exp_avg_sq || !a.sched ||
         !a.cursor || a.n_sched < 1 || !a.scalars || a.n < 1 || !a.W0 || !a.b0 || !a.W1 || !a.b1 || !a.W2 || !a.b2 ||

@@ -290,7 +290,8 @@ class _FusedPolicyGradient(Learner):
         if not (c0 == c1 == c2 and s0 == s1 == s2 and ca == 0 and cc == 0 and lc.out_features == 1):
             return False
         h0, h1, h2, k = l0.out_features, l1.out_features, l2.out_features, la.out_features
-        if any(h % 4 or h > 256 for h in (h0, h1, h2)) or not 2 <= k <= 16 or l0.in_features != obs_flat.shape[1]:
+        if any(h % 32 or h > 256 for h in (h0, h1, h2)) or not 2 <= k <= 16 or l0.in_features != obs_flat.shape[1] \
+                or l0.in_features > 32:
             return False
         return int(ops.lib().xpa_small_mlp_lds_floats(batch, l0.in_features, h0, h1, h2, k)) <= 40704
 
