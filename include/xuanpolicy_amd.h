@@ -222,6 +222,52 @@ int xpa_cartpole_step(int64_t n_envs, const float *act_in, int64_t ld_act, doubl
                       int32_t *ep_step, uint32_t *ep_index, float *ep_score, float *ep_last_score,
                       int32_t *ep_last_len, uint32_t seed, int32_t max_episode_steps, xpa_stream_t stream);
 
+/* K32 — `steps` whole device env steps of a small-MLP Categorical PPO / A2C agent on CartPole in ONE launch (one
+ * workgroup; the step loop of ppoclip_agent.py:43-101 / a2c_agent.py:42-98 with DummyVecEnv_Gym's auto-reset):
+ * per step, obs_rms.update (xpa_rms_update's sums and merge, in its order), the normalisation into obs_norm and the
+ * buffer column (xpa_obs_normalize), the policy forward — representation Linear(d_in, h0) + act, actor Linear(h0,
+ * h1) + act -> Linear(h1, k), critic Linear(h0, h2) + act -> Linear(h2, 1) — K3's Categorical sample + stores
+ * (xpa_rollout_sample), K18's CartPole step (xpa_cartpole_step) and K8's deferred-bootstrap post step with the
+ * final-observation normalisation (xpa_rollout_post_deferred_norm); the cursor advances by `steps`.  Every stage
+ * but the forward is the multi-kernel path's arithmetic bit for bit (the forward's dot products are f32 fma chains
+ * in a fixed order).  Replaces ~10 launches per env step of the C1 configuration.  Limits: n_envs <= 256,
+ * d_in == 4 (CartPole), h0 in {32, 64}, h1, h2 in {32, 64}, k == 2, xpa_small_rollout_lds_floats(...) <= 16384.
+ * use_obsnorm = 0: the statistics are read, not updated (the agent's use_obsnorm False). */
+typedef struct XpaSmallRolloutArgs {
+    int n_envs, horizon, steps, d_in, h0, h1, h2, k, act_code, use_obsnorm, n_slots, mask_returns, use_rewnorm;
+    int max_episode_steps;
+    float slope, obs_clip, gamma, rew_range;
+    uint32_t seed, env_seed;
+    const float *W0, *b0, *W1, *b1, *W2, *b2, *Wa, *ba, *Wc, *bc;
+    float *obs_mean, *obs_var;
+    double *obs_count;
+    float *obs_norm;
+    int64_t ld_norm;
+    float *buf_obs, *buf_act, *buf_logp, *buf_val, *buf_rew, *buf_term;
+    uint8_t *buf_closed;
+    float *buf_boot;
+    float *act_in;
+    int64_t ld_act;
+    double *env_state;
+    float *env_obs;
+    int64_t ld_obs;
+    float *final_obs, *env_rew;
+    uint8_t *env_term, *env_trunc;
+    int32_t *ep_step;
+    uint32_t *ep_index;
+    float *ep_score, *ep_last_score;
+    int32_t *ep_last_len;
+    float *returns, *ret_mean, *ret_var;
+    double *ret_count;
+    float *slot_obs;
+    int32_t *slot_t, *overflow;
+    float *boot_norm;
+    int64_t ld_boot;
+    xpa_cursor_t *cursor;
+} XpaSmallRolloutArgs;
+int64_t xpa_small_rollout_lds_floats(int64_t n_envs, int64_t d_in, int64_t h0, int64_t h1, int64_t h2, int64_t k);
+int xpa_small_rollout_cartpole(const XpaSmallRolloutArgs *args, xpa_stream_t stream);
+
 /* K19 — PER-DQN TD target, loss, gradient and priorities (BASELINE.json configs[4]; replaces the tensor algebra
  * of PerDQN_Learner.update, xuance/torch/learners/qlearning_family/perdqn_learner.py:23-30, 48).
  * y = rew + (gamma * (1 - term)) * max_a targetQ[b, a]; p = evalQ[b, act[b]]; dQ[b, :] = one-hot(act[b]) * 2 (p - y) / B

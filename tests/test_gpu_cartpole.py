@@ -214,3 +214,38 @@ def test_small_mlp_epoch_graphs_match_eager(n_steps, n_mb):
         out.append([p.detach().cpu().numpy().copy() for p in agent.policy.parameters()])
     for a, b in zip(*out):
         np.testing.assert_array_equal(b, a)
+
+
+@pytest.mark.parametrize("agent_name", ["PPO_Clip", "A2C"])
+def test_fused_rollout_matches_multi_kernel_steps(agent_name):
+    """K32 (xpa_small_rollout_cartpole: obs RMS + normalise + MLP forward + sample + CartPole step + K8 post in one
+    launch) against the multi-kernel step (K5, obs_normalize, the torch forward, K3, K18, K8) from the same start:
+    iteration 1's 128 steps as ONE K32 launch, then an update, then 127 single-step launches (time limit 40: mid-buffer
+    truncations fill the deferred slots).  Everything but the forward is the same arithmetic, so the actions, buffer
+    observations, rewards / closures, slots, RMS statistics, returns and env state are bit-identical; the stored
+    values / log-probs agree within the f32 reassociation of the two forwards."""
+    from xuanpolicy_amd.runner import build_cartpole_ppo
+    res = []
+    for fused in (True, False):
+        agent = build_cartpole_ppo(n_envs=8, n_steps=128, hidden=64, seed=9, device=DEV, max_episode_steps=40,
+                                   agent=agent_name, fused_rollout=fused, clip_grad=0.5)
+        assert agent.defer_boot and agent.n_slots == 4
+        agent.train(128 + 127, log=False)
+        torch.cuda.synchronize()
+        assert (agent._small_rollout() is not None) == fused
+        mem, env = agent.memory, agent.envs
+        logp = mem.auxiliary_infos["old_logp"] if agent.algo == "ppo" else agent.logp_scratch
+        res.append({k: v.detach().cpu().numpy().copy() for k, v in dict(
+            obs=mem.observations, act=mem.actions, rew=mem.rewards, term=mem.terminals, closed=mem.closed,
+            boot=mem.boot, slot_t=agent.slot_t, slot_obs=agent.slot_obs, boot_obs=agent.boot_obs,
+            obs_mean=agent.obs_mean, obs_var=agent.obs_var, obs_count=agent.obs_count, ret_mean=agent.ret_mean,
+            ret_var=agent.ret_var, ret_count=agent.ret_count, returns=agent.returns, state=env.state,
+            ep_index=env.ep_index, ep_score=env.ep_score, cursor=agent.cursor, obs_norm=agent.obs_norm,
+            val=mem.values, logp=logp).items()})
+    f, m = res
+    assert (f["slot_t"] >= 0).sum() > 0 and f["closed"][:, :127].sum() > 8
+    for k in f:
+        if k in ("val", "logp"):
+            np.testing.assert_allclose(f[k][:, :127], m[k][:, :127], rtol=1e-4, atol=1e-5, err_msg=k)
+        else:
+            np.testing.assert_array_equal(f[k], m[k], err_msg=k)

@@ -40,6 +40,27 @@ class XpaSmallMlpArgs(ctypes.Structure):
                    ("scalars", ctypes.c_void_p), ("total_norm_out", ctypes.c_void_p), ("stamps", ctypes.c_void_p)])
 
 
+class XpaSmallRolloutArgs(ctypes.Structure):
+    """include/xuanpolicy_amd.h XpaSmallRolloutArgs (K32), field for field."""
+    _fields_ = ([(n, ctypes.c_int) for n in ("n_envs", "horizon", "steps", "d_in", "h0", "h1", "h2", "k", "act_code",
+                                             "use_obsnorm", "n_slots", "mask_returns", "use_rewnorm",
+                                             "max_episode_steps")]
+                + [(n, ctypes.c_float) for n in ("slope", "obs_clip", "gamma", "rew_range")]
+                + [("seed", ctypes.c_uint32), ("env_seed", ctypes.c_uint32)]
+                + [(n, ctypes.c_void_p) for n in ("W0", "b0", "W1", "b1", "W2", "b2", "Wa", "ba", "Wc", "bc",
+                                                  "obs_mean", "obs_var", "obs_count", "obs_norm")]
+                + [("ld_norm", ctypes.c_int64)]
+                + [(n, ctypes.c_void_p) for n in ("buf_obs", "buf_act", "buf_logp", "buf_val", "buf_rew", "buf_term",
+                                                  "buf_closed", "buf_boot", "act_in")]
+                + [("ld_act", ctypes.c_int64), ("env_state", ctypes.c_void_p), ("env_obs", ctypes.c_void_p),
+                   ("ld_obs", ctypes.c_int64)]
+                + [(n, ctypes.c_void_p) for n in ("final_obs", "env_rew", "env_term", "env_trunc", "ep_step",
+                                                  "ep_index", "ep_score", "ep_last_score", "ep_last_len", "returns",
+                                                  "ret_mean", "ret_var", "ret_count", "slot_obs", "slot_t", "overflow",
+                                                  "boot_norm")]
+                + [("ld_boot", ctypes.c_int64), ("cursor", ctypes.c_void_p)])
+
+
 # name -> (restype, argtypes); mirrors include/xuanpolicy_amd.h one-for-one.
 SIGNATURES = {
     "xpa_abi_version": (ctypes.c_int, []),
@@ -127,6 +148,8 @@ SIGNATURES = {
     "xpa_adam_sched_entry": (None, [c_f32, c_f32, c_f32, c_i64, c_p]),
     "xpa_small_mlp_lds_floats": (c_i64, [c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
     "xpa_small_mlp_update": (ctypes.c_int, [c_p, c_p]),
+    "xpa_small_rollout_lds_floats": (c_i64, [c_i64, c_i64, c_i64, c_i64, c_i64, c_i64]),
+    "xpa_small_rollout_cartpole": (ctypes.c_int, [c_p, c_p]),
     "xpa_colsum_finalize_batch": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p]),
     "xpa_per_store": (ctypes.c_int, [c_p, c_p, c_p, c_i64, c_i64, c_i64, ctypes.c_double, c_p]),
     "xpa_per_update_priorities": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_i64, ctypes.c_double,

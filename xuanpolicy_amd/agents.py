@@ -26,6 +26,7 @@ CPU generator; the truncation bootstrap value V(norm(final obs)) is computed for
 all finished envs of a step in one Chan update (mathematically equal to the reference's sequential
 single-value updates).
 """
+import ctypes
 import json
 import os
 import time
@@ -33,7 +34,7 @@ import time
 import numpy as np
 import torch
 
-from . import ops
+from . import _lib, ops
 from .buffer import DummyOnPolicyBuffer, DummyOnPolicyBuffer_Atari
 from .fused_mlp import Rows
 from .learners import A2C_Learner, PerDQN_Learner, PPOCLIP_Learner
@@ -112,6 +113,9 @@ class _OnPolicyAgent:
         self.fuse_env_step = True   # device SynthBox env stepped inside K14 when possible (_env_fused)
         self.fuse_value_gae = True  # deferred bootstraps' value head inside the GAE scan (xpa_gae_scan_value)
         self.fuse_gather = True     # minibatch gather + adv moments inside the update's K13 (fused_mlp.Rows)
+        # K32: whole device env steps (RMS, normalise, forward, sample, env, post) in one launch (_small_rollout)
+        self.fused_rollout = bool(_cfg(config, "fused_rollout", True))
+        self._k32 = self._k32_key = None
         self.current_step = 0
         self.current_episode = np.zeros((N,), np.int32)
         self.iterations = 0
@@ -302,8 +306,76 @@ class _OnPolicyAgent:
             ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count, partials=self.rms_part,
                            ticket=self._rms_ticket)
 
+    def _small_rollout(self):
+        """K32's argument block (xpa_small_rollout_cartpole) when whole device env steps run as one launch: a CartPole
+        device env with deferred bootstraps, no per-step collective, and the small_policy_layers policy shape; else
+        None.  Rebuilt when the parameters are re-homed (the block holds their pointers)."""
+        if not self.fused_rollout or not self.device_env or self.device.type != "cuda":
+            return None
+        key = tuple(p.data_ptr() for p in self.policy.parameters())
+        if self._k32_key != key:
+            self._k32_key, self._k32 = key, self._build_small_rollout()
+        return self._k32
+
+    def _build_small_rollout(self):
+        env = self.envs
+        get = getattr(self.learner, "small_policy_layers", None)
+        layers = get() if get is not None else None
+        if (layers is None or getattr(env, "kind", None) != "cartpole" or not self.defer_boot or self.raw_obs
+                or self.sync_obs_rms or self.algo not in ("ppo", "a2c") or self.obs_dim != 4):
+            return None
+        (l0, l1, la, l2, lc), code, slope = layers
+        N, T, D = self.n_envs, self.n_steps, self.obs_dim
+        h0, h1, h2, k = l0.out_features, l1.out_features, l2.out_features, la.out_features
+        if h0 not in (32, 64) or h1 not in (32, 64) or h2 not in (32, 64) or k != 2 or l0.in_features != D:
+            return None
+        lf = int(ops.lib().xpa_small_rollout_lds_floats(N, D, h0, h1, h2, k))
+        if not 0 < lf <= 16384:
+            return None
+        mem = self.memory
+        bufs = (mem.observations, mem.actions, mem.values, mem.rewards, mem.terminals, mem.boot)
+        if any(b.dtype != torch.float32 or not b.is_contiguous() for b in bufs) or not mem.closed.is_contiguous():
+            return None
+        a = _lib.XpaSmallRolloutArgs()
+        a.n_envs, a.horizon, a.steps, a.d_in, a.h0, a.h1, a.h2, a.k = N, T, 1, D, h0, h1, h2, k
+        a.act_code, a.use_obsnorm, a.n_slots = int(code), int(self.use_obsnorm), int(self.n_slots)
+        a.mask_returns, a.use_rewnorm, a.max_episode_steps = int(self.algo == "ppo"), int(self.use_rewnorm), \
+            int(env.max_episode_steps)
+        a.slope, a.obs_clip, a.gamma, a.rew_range = float(slope), float(self._obs_clip()), float(self.gamma), \
+            float(self.rewnorm_range)
+        a.seed, a.env_seed = int(self.seed) & 0xFFFFFFFF, int(env.noise_seed) & 0xFFFFFFFF
+        p = ops._p
+        a.W0, a.b0, a.W1, a.b1, a.W2, a.b2 = (p(l0.weight), p(l0.bias), p(l1.weight), p(l1.bias), p(l2.weight),
+                                              p(l2.bias))
+        a.Wa, a.ba, a.Wc, a.bc = p(la.weight), p(la.bias), p(lc.weight), p(lc.bias)
+        a.obs_mean, a.obs_var, a.obs_count = p(self.obs_mean), p(self.obs_var), p(self.obs_count)
+        a.obs_norm, a.ld_norm = p(self.obs_norm), self.obs_norm.stride(0)
+        logp_buf = mem.auxiliary_infos["old_logp"] if self.algo == "ppo" else self.logp_scratch
+        a.buf_obs, a.buf_act, a.buf_logp, a.buf_val = p(mem.observations), p(mem.actions), p(logp_buf), p(mem.values)
+        a.buf_rew, a.buf_term, a.buf_closed, a.buf_boot = p(mem.rewards), p(mem.terminals), p(mem.closed), p(mem.boot)
+        a.act_in, a.ld_act = p(env.act_in), env.act_in.stride(0)
+        a.env_state, a.env_obs, a.ld_obs = p(env.state), p(env.obs), env.obs.stride(0)
+        a.final_obs, a.env_rew, a.env_term, a.env_trunc = p(env.final_obs), p(env.rew), p(env.term), p(env.trunc)
+        a.ep_step, a.ep_index, a.ep_score = p(env.ep_step), p(env.ep_index), p(env.ep_score)
+        a.ep_last_score, a.ep_last_len = p(env.ep_last_score), p(env.ep_last_len)
+        a.returns, a.ret_mean, a.ret_var, a.ret_count = p(self.returns), p(self.ret_mean), p(self.ret_var), \
+            p(self.ret_count)
+        a.slot_obs, a.slot_t, a.overflow = p(self.slot_obs), p(self.slot_t), p(self.slot_overflow)
+        a.boot_norm, a.ld_boot = p(self.boot_obs), self.boot_obs.stride(0)
+        a.cursor = p(self.cursor)
+        return a
+
+    def _small_rollout_launch(self, a, steps):
+        a.steps = int(steps)
+        _lib.check(ops.lib().xpa_small_rollout_cartpole(ctypes.byref(a), ops._stream(self.device)),
+                   "xpa_small_rollout_cartpole")
+
     def _rollout_step_device(self):
         env = self.envs
+        k32 = self._small_rollout()
+        if k32 is not None:
+            self._small_rollout_launch(k32, 1)
+            return
         x = env.obs
         if self.raw_obs:
             ops.store_column(x, self.memory.observations, self.cursor)
@@ -329,6 +401,9 @@ class _OnPolicyAgent:
     def _rollout_step_graph(self):
         """The device env step captured once into a hipGraph and replayed: every per-step argument
         (buffer column, RNG step) lives in the device cursor, so the same graph serves all steps."""
+        if self._small_rollout() is not None:   # one launch per step: nothing to capture
+            self._rollout_step_device()
+            return
         key = tuple(p.data_ptr() for p in self.policy.parameters())
         if self._graph is not None and key != self._graph_key:
             self._graph = None  # parameters were re-homed (e.g. flat buffers attached): re-capture
@@ -350,6 +425,10 @@ class _OnPolicyAgent:
         """k consecutive device env steps captured into ONE hipGraph (k x 5 kernels) and replayed as a unit: a
         per-step replay leaves the GPU idle ~8 us between graphs while the host launches the next (r02 trace:
         127 such gaps = 1.0 ms of a 72 ms iteration).  Same replay invariance as _rollout_step_graph."""
+        k32 = self._small_rollout()
+        if k32 is not None:   # the k steps as one K32 launch
+            self._small_rollout_launch(k32, k)
+            return k
         key = (k,) + tuple(p.data_ptr() for p in self.policy.parameters())
         if self._chunk_graph is not None and key != self._chunk_key:
             self._chunk_graph = None

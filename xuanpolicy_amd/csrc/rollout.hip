@@ -6,7 +6,7 @@
 //   K8 xpa_rollout_post      reward norm, return tracker, ret_rms, path closures (ppoclip_agent.py:68-101)
 // All per-step kernels read the buffer column from a device cursor so a whole env step can be
 // captured once in a hipGraph and replayed.
-#include "xpa_common.h"
+#include "cartpole_body.h"
 
 namespace {
 
@@ -285,13 +285,11 @@ __device__ __forceinline__ void gauss_sample_store(int64_t n, int A, int64_t T, 
     buf_val[cell] = v;
 }
 
-__device__ __forceinline__ void cat_sample_store(int64_t n, int K, int64_t T, const float *z, float v,
-                                                 const xpa_cursor_t *__restrict__ cur, uint32_t seed,
-                                                 float *__restrict__ buf_act, float *__restrict__ buf_logp,
-                                                 float *__restrict__ buf_val, float *__restrict__ env_in,
-                                                 int64_t ld_env) {
-    const int64_t t = cur->ptr;
-    const uint32_t step = cur->step;
+// Returns the sampled action (K32 steps its env with it).
+__device__ __forceinline__ int cat_sample_store_at(int64_t n, int K, int64_t T, int32_t t, uint32_t step,
+                                                   const float *z, float v, uint32_t seed, float *__restrict__ buf_act,
+                                                   float *__restrict__ buf_logp, float *__restrict__ buf_val,
+                                                   float *__restrict__ env_in, int64_t ld_env) {
     const int64_t cell = n * T + t;
     float m = z[0];
     for (int k = 1; k < K; ++k) m = fmaxf(m, z[k]);
@@ -312,6 +310,15 @@ __device__ __forceinline__ void cat_sample_store(int64_t n, int K, int64_t T, co
     buf_logp[cell] = z[pick] - lse;
     buf_val[cell] = v;
     for (int k = 0; k < K; ++k) env_in[n * ld_env + k] = (k == pick) ? 1.f : 0.f;
+    return pick;
+}
+
+__device__ __forceinline__ void cat_sample_store(int64_t n, int K, int64_t T, const float *z, float v,
+                                                 const xpa_cursor_t *__restrict__ cur, uint32_t seed,
+                                                 float *__restrict__ buf_act, float *__restrict__ buf_logp,
+                                                 float *__restrict__ buf_val, float *__restrict__ env_in,
+                                                 int64_t ld_env) {
+    cat_sample_store_at(n, K, T, cur->ptr, cur->step, z, v, seed, buf_act, buf_logp, buf_val, env_in, ld_env);
 }
 
 __global__ __launch_bounds__(256) void rollout_sample_gauss_kernel(
@@ -548,6 +555,66 @@ __device__ __forceinline__ float obs_norm1(float x, float m, float v, float clip
     return fminf(fmaxf(y, -clip), clip);
 }
 
+// K8's per-env body (shared with K32): reward normalisation, buffer column t, closures / kept truncation rows,
+// the return tracker; (cnt, sum, sumsq) = the env's contribution to ret_rms's batch moments.
+template <bool DEFER, bool NORM>
+__device__ __forceinline__ void post_env(
+    int64_t n, int64_t n_envs, int64_t T, int32_t t, bool last, float rstd, float r, bool te, bool tr, float vb,
+    float *__restrict__ returns, float *__restrict__ buf_rew, float *__restrict__ buf_term,
+    uint8_t *__restrict__ buf_closed, float *__restrict__ buf_boot, float gamma, int mask_returns, int use_rewnorm,
+    float rew_range, int atari_lifeloss, const float *__restrict__ boot_obs, int64_t ld_boot, int64_t dim,
+    float *__restrict__ slot_obs, int *__restrict__ slot_t, int n_slots, int *__restrict__ overflow,
+    const float *__restrict__ obs_mean, const float *__restrict__ obs_var, float obs_clip,
+    float *__restrict__ boot_norm, int64_t ld_norm, double &cnt, double &sum, double &sumsq) {
+    const float R = returns[n];
+    const int64_t cell = n * T + t;
+    buf_rew[cell] = use_rewnorm ? fminf(fmaxf(r / rstd, -rew_range), rew_range) : r;
+    buf_term[cell] = te ? 1.f : 0.f;
+    const bool done = te || tr;
+    const bool close = last || (done && !(atari_lifeloss && !tr));
+    buf_closed[cell] = close ? 1 : 0;
+    buf_boot[cell] = close ? (te ? 0.f : vb) : 0.f;
+    if (DEFER && close && !te && !last) {  // mid-buffer truncation: keep the row for later
+        int k = 0;
+        while (k < n_slots && slot_t[(int64_t)k * n_envs + n] >= 0) ++k;
+        if (k == n_slots) {  // contract broken: counted (the agent raises), the last slot is reused
+            atomicAdd(overflow, 1);
+            k = n_slots - 1;
+        }
+        const int64_t sl = (int64_t)k * n_envs + n;
+        slot_t[sl] = (int)t;
+        for (int64_t d = 0; d < dim; ++d)
+            slot_obs[sl * dim + d] = NORM ? obs_norm1(boot_obs[n * ld_boot + d], obs_mean[d], obs_var[d], obs_clip)
+                                          : boot_obs[n * ld_boot + d];
+    }
+    if (NORM && last)
+        for (int64_t d = 0; d < dim; ++d)
+            boot_norm[n * ld_norm + d] = obs_norm1(boot_obs[n * ld_boot + d], obs_mean[d], obs_var[d], obs_clip);
+    float Rk = mask_returns ? (te ? 0.f : gamma * R) + r : gamma * R + r;
+    if (done) {
+        cnt = 1.0;
+        sum = (double)Rk;
+        sumsq = (double)Rk * (double)Rk;
+        Rk = 0.f;
+    }
+    returns[n] = Rk;
+}
+
+// ret_rms.update_from_moments (statistic_tools.py:86-112) from the summed (count, sum, sumsq) of the closed paths.
+__device__ __forceinline__ void ret_rms_merge(double c, double s1, double s2, float *ret_mean, float *ret_var,
+                                              double *ret_count) {
+    if (c > 0.0) {
+        const double bm = s1 / c;
+        const double bvar = fmax(s2 / c - bm * bm, 0.0);
+        const double c0 = *ret_count, m0 = (double)*ret_mean, v0 = (double)*ret_var;
+        const double tot = c0 + c;
+        const double delta = bm - m0;
+        *ret_mean = (float)(m0 + delta * c / tot);
+        *ret_var = (float)((v0 * c0 + bvar * c + delta * delta * c0 * c / tot) / tot);
+        *ret_count = tot;
+    }
+}
+
 template <bool DEFER, bool NORM = false>
 __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
     int64_t n_envs, int64_t T, const float *__restrict__ rew, const uint8_t *__restrict__ term,
@@ -568,43 +635,12 @@ __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
     const bool last = (t == (int32_t)(T - 1));
     double cnt = 0.0, sum = 0.0, sumsq = 0.0;
     const int64_t n = (int64_t)blockIdx.x * kPostThreads + threadIdx.x;
-    if (n < n_envs) {
-        const float r = rew[n];
-        const float vb = DEFER ? 0.f : v_boot[n];
-        const float R = returns[n];
-        const bool te = term[n] != 0, tr = trunc[n] != 0;
-        const int64_t cell = n * T + t;
-        buf_rew[cell] = use_rewnorm ? fminf(fmaxf(r / rstd, -rew_range), rew_range) : r;
-        buf_term[cell] = te ? 1.f : 0.f;
-        const bool done = te || tr;
-        const bool close = last || (done && !(atari_lifeloss && !tr));
-        buf_closed[cell] = close ? 1 : 0;
-        buf_boot[cell] = close ? (te ? 0.f : vb) : 0.f;
-        if (DEFER && close && !te && !last) {  // mid-buffer truncation: keep the row for later
-            int k = 0;
-            while (k < n_slots && slot_t[(int64_t)k * n_envs + n] >= 0) ++k;
-            if (k == n_slots) {  // contract broken: counted (the agent raises), the last slot is reused
-                atomicAdd(overflow, 1);
-                k = n_slots - 1;
-            }
-            const int64_t sl = (int64_t)k * n_envs + n;
-            slot_t[sl] = (int)t;
-            for (int64_t d = 0; d < dim; ++d)
-                slot_obs[sl * dim + d] = NORM ? obs_norm1(boot_obs[n * ld_boot + d], obs_mean[d], obs_var[d], obs_clip)
-                                              : boot_obs[n * ld_boot + d];
-        }
-        if (NORM && last)
-            for (int64_t d = 0; d < dim; ++d)
-                boot_norm[n * ld_norm + d] = obs_norm1(boot_obs[n * ld_boot + d], obs_mean[d], obs_var[d], obs_clip);
-        float Rk = mask_returns ? (te ? 0.f : gamma * R) + r : gamma * R + r;
-        if (done) {
-            cnt = 1.0;
-            sum = (double)Rk;
-            sumsq = (double)Rk * (double)Rk;
-            Rk = 0.f;
-        }
-        returns[n] = Rk;
-    }
+    if (n < n_envs)
+        post_env<DEFER, NORM>(n, n_envs, T, t, last, rstd, rew[n], term[n] != 0, trunc[n] != 0,
+                              DEFER ? 0.f : v_boot[n], returns, buf_rew, buf_term, buf_closed, buf_boot, gamma,
+                              mask_returns, use_rewnorm, rew_range, atari_lifeloss, boot_obs, ld_boot, dim, slot_obs,
+                              slot_t, n_slots, overflow, obs_mean, obs_var, obs_clip, boot_norm, ld_norm, cnt, sum,
+                              sumsq);
     constexpr int nw = kPostThreads / 64;
     cnt = xpa_block_sum(cnt, s_red, nw);
     sum = xpa_block_sum(sum, s_red, nw);
@@ -632,19 +668,221 @@ __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
         s1 += staged ? s_pp[3 * g + 1] : xpa_load_agent(partials + 3 * g + 1);
         s2 += staged ? s_pp[3 * g + 2] : xpa_load_agent(partials + 3 * g + 2);
     }
-    if (c > 0.0) {
-        const double bm = s1 / c;
-        const double bvar = fmax(s2 / c - bm * bm, 0.0);
-        const double c0 = *ret_count, m0 = (double)*ret_mean, v0 = (double)*ret_var;
-        const double tot = c0 + c;
-        const double delta = bm - m0;
-        *ret_mean = (float)(m0 + delta * c / tot);
-        *ret_var = (float)((v0 * c0 + bvar * c + delta * delta * c0 * c / tot) / tot);
-        *ret_count = tot;
-    }
+    ret_rms_merge(c, s1, s2, ret_mean, ret_var, ret_count);
     cur->ptr = (int32_t)((t + 1) % T);
     cur->step = cur->step + 1u;
     *ticket = 0u;
+}
+
+// ---------------------------------------------------------------------------------------------
+// K32 — `steps` device env steps of a small-MLP Categorical agent on CartPole in one launch (one workgroup):
+// obs RMS (K5) -> normalise (obs_normalize) -> MLP forward -> K3 sample/store -> K18 env step -> K8 (deferred,
+// NORM).  The RMS sums, the merge, the normalisation, the sampler, the env and the post step are the multi-kernel
+// path's own code or arithmetic (one RMS partial block: rows summed per (row group, column) and the groups in
+// order, as rms_partials_kernel<., 256> does for n <= 256); the weight rows the forward needs stay in VGPRs for
+// the whole launch.  C1: 8 envs, ~10 launches x 128 steps per rollout -> one launch.
+// ---------------------------------------------------------------------------------------------
+constexpr int kRoThreads = 256;
+constexpr int kRoLdsMax = 16384;  // floats of dynamic LDS (64 KiB: no attribute needed)
+
+__host__ __device__ constexpr int ro_r4(int x) { return (x + 3) & ~3; }
+
+struct RoLayout {
+    int sy, sh0, sh12, sz, swo, sbo, total;
+};
+__host__ __device__ inline RoLayout ro_layout(int N, int D, int H0, int H1, int H2, int K) {
+    RoLayout l;
+    const int K1 = K + 1;
+    l.sy = 0;
+    l.sh0 = ro_r4(N * D);
+    l.sh12 = l.sh0 + N * H0;
+    l.sz = l.sh12 + N * (H1 + H2);
+    l.swo = ro_r4(l.sz + N * K1);
+    l.sbo = l.swo + K1 * 64;
+    l.total = ro_r4(l.sbo + K1);
+    return l;
+}
+
+template <int ACT>
+__device__ __forceinline__ float ro_act(float z, float slope) {
+    if (ACT == 1) return z > 0.f ? z : z * slope;
+    if (ACT == 2) return tanhf(z);
+    return z;
+}
+
+template <int ACT, int H0>
+__global__ __launch_bounds__(kRoThreads) void small_rollout_cartpole_kernel(XpaSmallRolloutArgs a) {
+    extern __shared__ float lds[];
+    __shared__ double s_sum[kRoThreads], s_sq[kRoThreads];
+    __shared__ double s_red[kRoThreads / 64];
+    __shared__ float s_mean[32], s_var[32];
+    const int tid = threadIdx.x;
+    const int N = a.n_envs, D = a.d_in, H1 = a.h1, H2 = a.h2, K = a.k, K1 = a.k + 1, U = a.h1 + a.h2;
+    const int T = a.horizon;
+    const RoLayout L = ro_layout(N, D, H0, H1, H2, K);
+    float *sy = lds + L.sy, *sh0 = lds + L.sh0, *sh12 = lds + L.sh12, *sz = lds + L.sz, *swo = lds + L.swo,
+          *sbo = lds + L.sbo;
+    const XpaCartPoleEnv env{a.env_state,   a.env_obs,   a.ld_obs,     a.final_obs,  a.env_rew,
+                             a.env_term,    a.env_trunc, a.ep_step,    a.ep_index,   a.ep_score,
+                             a.ep_last_score, a.ep_last_len, a.env_seed, a.max_episode_steps,
+                             cartpole::kThetaThreshold};
+    // output layers into LDS (rows 0..K-1 actor, row K critic; 64-float rows)
+    for (int e = tid; e < K1 * 64; e += kRoThreads) {
+        const int c = e >> 6, j = e & 63;
+        float w = 0.f;
+        if (c < K && j < H1) w = a.Wa[c * H1 + j];
+        if (c == K && j < H2) w = a.Wc[j];
+        swo[e] = w;
+    }
+    if (tid < K1) sbo[tid] = tid < K ? a.ba[tid] : a.bc[0];
+    // layer 0: unit u0 = tid % H0 over row groups of G0 rows; its weight row in VGPRs
+    constexpr int G0 = kRoThreads / H0;
+    const int u0 = tid % H0, g0 = tid / H0;
+    float w0[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) w0[k] = k < D ? a.W0[u0 * D + k] : 0.f;
+    const float b0u = a.b0[u0];
+    // layers 1 | 2 side by side: unit u12 < H1 actor, else critic
+    const int G12 = kRoThreads / U;
+    const int u12 = tid % U, g12 = tid / U;
+    const bool on12 = g12 < G12;
+    const float *wr = u12 < H1 ? a.W1 + u12 * H0 : a.W2 + (u12 - H1) * H0;
+    float w1[H0];
+#pragma unroll
+    for (int k = 0; k < H0; ++k) w1[k] = on12 ? wr[k] : 0.f;
+    const float b12 = on12 ? (u12 < H1 ? a.b1[u12] : a.b2[u12 - H1]) : 0.f;
+
+    int32_t t = a.cursor->ptr;
+    uint32_t step = a.cursor->step;
+    for (int s = 0; s < a.steps; ++s) {
+        const bool last = t == T - 1;
+        // (a) obs_rms.update(obs): xpa_rms_update with one partial block
+        if (a.use_obsnorm) {
+            const int groups = kRoThreads / D;
+            const int c = tid % D, gsub = tid / D;
+            double sm = 0.0, q = 0.0;
+            if (gsub < groups) {
+                const float sh = a.obs_mean[c];
+                for (int r = gsub; r < N; r += groups) {
+                    const double v = (double)a.env_obs[r * a.ld_obs + c] - (double)sh;
+                    sm += v;
+                    q += v * v;
+                }
+            }
+            s_sum[tid] = sm;
+            s_sq[tid] = q;
+            __syncthreads();
+            const double c0 = *a.obs_count;
+            if (tid < D) {
+                double ts = 0.0, tq = 0.0;
+                for (int k = 0; k < groups; ++k) {
+                    ts += s_sum[k * D + tid];
+                    tq += s_sq[k * D + tid];
+                }
+                double s1 = 0.0, q1 = 0.0;  // rms_merge_body over the one partial
+                s1 += ts;
+                q1 += tq;
+                const double n = (double)N;
+                const double ms = s1 / n;
+                const double m0 = (double)a.obs_mean[tid], v0 = (double)a.obs_var[tid];
+                const double bm = m0 + ms;
+                const double bvar = fmax(q1 / n - ms * ms, 0.0);
+                const double tot = c0 + n;
+                const double delta = bm - m0;
+                const double new_mean = m0 + delta * n / tot;
+                const double m2 = v0 * c0 + bvar * n + delta * delta * c0 * n / tot;
+                const float fm = (float)new_mean, fv = (float)(m2 / tot);
+                a.obs_mean[tid] = fm;
+                a.obs_var[tid] = fv;
+                s_mean[tid] = fm;
+                s_var[tid] = fv;
+            }
+            __syncthreads();
+            if (tid == 0) *a.obs_count = c0 + (double)N;
+        } else {
+            if (tid < D) {
+                s_mean[tid] = a.obs_mean[tid];
+                s_var[tid] = a.obs_var[tid];
+            }
+            __syncthreads();
+        }
+        // (b) normalise into the policy input and buffer column t (obs_normalize_kernel's arithmetic)
+        for (int e = tid; e < N * D; e += kRoThreads) {
+            const int r = e / D, d = e - r * D;
+            const float y = obs_norm1(a.env_obs[r * a.ld_obs + d], s_mean[d], s_var[d], a.obs_clip);
+            sy[e] = y;
+            a.obs_norm[r * a.ld_norm + d] = y;
+            a.buf_obs[((int64_t)r * T + t) * D + d] = y;
+        }
+        __syncthreads();
+        // (c) representation layer
+        for (int r = g0; r < N; r += G0) {
+            float acc = b0u;
+#pragma unroll
+            for (int k = 0; k < 32; ++k)
+                if (k < D) acc = fmaf(w0[k], sy[r * D + k], acc);
+            sh0[r * H0 + u0] = ro_act<ACT>(acc, a.slope);
+        }
+        __syncthreads();
+        // (d) actor | critic hidden layers (the h0 row is a wave-uniform broadcast read)
+        if (on12)
+            for (int r = g12; r < N; r += G12) {
+                const float4 *hr = reinterpret_cast<const float4 *>(sh0 + r * H0);
+                float acc = b12;
+#pragma unroll
+                for (int i = 0; i < H0 / 4; ++i) {
+                    const float4 h = hr[i];
+                    acc = fmaf(w1[4 * i], h.x, acc);
+                    acc = fmaf(w1[4 * i + 1], h.y, acc);
+                    acc = fmaf(w1[4 * i + 2], h.z, acc);
+                    acc = fmaf(w1[4 * i + 3], h.w, acc);
+                }
+                sh12[r * U + u12] = ro_act<ACT>(acc, a.slope);
+            }
+        __syncthreads();
+        // (e) logits | value
+        for (int p = tid; p < N * K1; p += kRoThreads) {
+            const int r = p / K1, c = p - r * K1;
+            const float4 *h = reinterpret_cast<const float4 *>(sh12 + r * U + (c < K ? 0 : H1));
+            const float4 *w = reinterpret_cast<const float4 *>(swo + c * 64);
+            const int hx = (c < K ? H1 : H2) >> 2;
+            float acc = sbo[c];
+            for (int i = 0; i < hx; ++i) {
+                const float4 hv = h[i], wv = w[i];
+                acc = fmaf(wv.x, hv.x, acc);
+                acc = fmaf(wv.y, hv.y, acc);
+                acc = fmaf(wv.z, hv.z, acc);
+                acc = fmaf(wv.w, hv.w, acc);
+            }
+            sz[p] = acc;
+        }
+        __syncthreads();
+        // (f) sample + store, env step, post step (one thread per env)
+        const float rstd = fminf(fmaxf(sqrtf(*a.ret_var), 0.1f), 100.0f);
+        double cnt = 0.0, sum = 0.0, sumsq = 0.0;
+        if (tid < N) {
+            const float *z = sz + tid * K1;
+            const int pick = cat_sample_store_at(tid, K, T, t, step, z, z[K], a.seed, a.buf_act, a.buf_logp,
+                                                 a.buf_val, a.act_in, a.ld_act);
+            bool te, tr;
+            const float r = cartpole::step(env, tid, pick, &te, &tr);
+            post_env<true, true>(tid, N, T, t, last, rstd, r, te, tr, 0.f, a.returns, a.buf_rew, a.buf_term,
+                                 a.buf_closed, a.buf_boot, a.gamma, a.mask_returns, a.use_rewnorm, a.rew_range, 0,
+                                 a.final_obs, 4, D, a.slot_obs, a.slot_t, a.n_slots, a.overflow, a.obs_mean, a.obs_var,
+                                 a.obs_clip, a.boot_norm, a.ld_boot, cnt, sum, sumsq);
+        }
+        cnt = xpa_block_sum(cnt, s_red, kRoThreads / 64);
+        sum = xpa_block_sum(sum, s_red, kRoThreads / 64);
+        sumsq = xpa_block_sum(sumsq, s_red, kRoThreads / 64);
+        if (tid == 0) ret_rms_merge(cnt, sum, sumsq, a.ret_mean, a.ret_var, a.ret_count);
+        t = (t + 1) % T;
+        step += 1u;
+        __syncthreads();  // env obs, ret / obs statistics and count visible to the next step
+    }
+    if (tid == 0) {
+        a.cursor->ptr = t;
+        a.cursor->step = step;
+    }
 }
 
 }  // namespace
@@ -988,5 +1226,46 @@ XPA_API int xpa_rollout_policy_head_synthbox(int act, int64_t n_envs, int64_t ac
     else if (act == 1) XPA_K14E(1);
     else XPA_K14E(2);
 #undef XPA_K14E
+    return xpa_launch_status();
+}
+
+// ---- K32 -------------------------------------------------------------------------------------------
+XPA_API int64_t xpa_small_rollout_lds_floats(int64_t n_envs, int64_t d_in, int64_t h0, int64_t h1, int64_t h2,
+                                             int64_t k) {
+    if (n_envs <= 0 || n_envs > 256 || d_in <= 0 || d_in > 32 || h0 <= 0 || h0 > 64 || h1 <= 0 || h1 > 64 ||
+        h2 <= 0 || h2 > 64 || k <= 0 || k > 16)
+        return -1;
+    return ro_layout((int)n_envs, (int)d_in, (int)h0, (int)h1, (int)h2, (int)k).total;
+}
+
+XPA_API int xpa_small_rollout_cartpole(const XpaSmallRolloutArgs *a, xpa_stream_t stream) {
+    if (!a || a->n_envs <= 0 || a->n_envs > 256 || a->horizon <= 0 || a->steps <= 0 || a->d_in != 4 ||
+        (a->h0 != 32 && a->h0 != 64) || (a->h1 != 32 && a->h1 != 64) || (a->h2 != 32 && a->h2 != 64) || a->k != 2 ||
+        a->act_code < 0 || a->act_code > 2 || a->n_slots < 1 || a->n_slots > a->horizon || a->max_episode_steps <= 0 ||
+        a->ld_norm < a->d_in || a->ld_obs < 4 || a->ld_act < 2 || a->ld_boot < a->d_in)
+        return (int)hipErrorInvalidValue;
+    if (!a->W0 || !a->b0 || !a->W1 || !a->b1 || !a->W2 || !a->b2 || !a->Wa || !a->ba || !a->Wc || !a->bc ||
+        !a->obs_mean || !a->obs_var || !a->obs_count || !a->obs_norm || !a->buf_obs || !a->buf_act || !a->buf_logp ||
+        !a->buf_val || !a->buf_rew || !a->buf_term || !a->buf_closed || !a->buf_boot || !a->act_in || !a->env_state ||
+        !a->env_obs || !a->final_obs || !a->env_rew || !a->env_term || !a->env_trunc || !a->ep_step || !a->ep_index ||
+        !a->ep_score || !a->ep_last_score || !a->ep_last_len || !a->returns || !a->ret_mean || !a->ret_var ||
+        !a->ret_count || !a->slot_obs || !a->slot_t || !a->overflow || !a->boot_norm || !a->cursor)
+        return (int)hipErrorInvalidValue;
+    const int64_t lf = xpa_small_rollout_lds_floats(a->n_envs, a->d_in, a->h0, a->h1, a->h2, a->k);
+    if (lf < 0 || lf > kRoLdsMax) return (int)hipErrorInvalidValue;
+    const size_t bytes = (size_t)lf * sizeof(float);
+    hipStream_t s = (hipStream_t)stream;
+#define XPA_RO_LAUNCH(ACT, H0) \
+    hipLaunchKernelGGL((small_rollout_cartpole_kernel<ACT, H0>), dim3(1), dim3(kRoThreads), bytes, s, *a)
+    if (a->h0 == 64) {
+        if (a->act_code == 0) XPA_RO_LAUNCH(0, 64);
+        else if (a->act_code == 1) XPA_RO_LAUNCH(1, 64);
+        else XPA_RO_LAUNCH(2, 64);
+    } else {
+        if (a->act_code == 0) XPA_RO_LAUNCH(0, 32);
+        else if (a->act_code == 1) XPA_RO_LAUNCH(1, 32);
+        else XPA_RO_LAUNCH(2, 32);
+    }
+#undef XPA_RO_LAUNCH
     return xpa_launch_status();
 }

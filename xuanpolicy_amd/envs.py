@@ -298,6 +298,7 @@ class CartPoleVecEnv:
     input the rollout kernels write.  Same interface as SynthBoxVecEnv (obs, act_in, final_obs, rew / term /
     trunc, step_device(), host step() with DummyVecEnv_Gym's contract).  CPU checker:
     oracle/synth_env.CartPoleEnv."""
+    kind = "cartpole"   # agents._small_rollout: K32 steps this env inside the fused rollout step
 
     def __init__(self, n_envs, seed=1, max_episode_steps=500, device=None, shard=0):
         self.num_envs, self.seed, self.max_episode_steps = int(n_envs), int(seed), int(max_episode_steps)

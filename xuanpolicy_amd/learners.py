@@ -271,24 +271,35 @@ class _FusedPolicyGradient(Learner):
         return ent[1]
 
     # ---- K30: the whole small-MLP update in one launch (C1) ----------------------------------------------------
-    def small_update_ok(self, obs_flat, batch):
-        """True when a minibatch of `batch` rows of obs_flat [n_rows, d] can take K30 (xpa_small_mlp_update): a
-        Categorical actor-critic of one representation layer and one hidden layer per head (all with the same
-        activation), flat parameters with the fused Adam, no data-parallel gradient sync, and the LDS budget."""
-        if not getattr(self, "small_updates", True) or self.grad_sync is not None or self.dist != "categorical":
-            return False
+    def small_policy_layers(self):
+        """((l0, l1, la, l2, lc), code, slope) when the policy is a Categorical actor-critic of one representation
+        layer and one hidden layer per head, all with the same activation — the shape K30 (update) and K32 (rollout
+        step) take — else None."""
+        if self.dist != "categorical":
+            return None
         fm = self._fused_mlp()
+        if fm is None or len(fm.rep) != 1 or len(fm.actor) != 2 or len(fm.critic) != 2:
+            return None
+        (l0, c0, s0), (l1, c1, s1), (la, ca, _), (l2, c2, s2), (lc, cc, _) = (fm.rep[0], fm.actor[0], fm.actor[1],
+                                                                              fm.critic[0], fm.critic[1])
+        if not (c0 == c1 == c2 and s0 == s1 == s2 and ca == 0 and cc == 0 and lc.out_features == 1):
+            return None
+        return (l0, l1, la, l2, lc), c0, s0
+
+    def small_update_ok(self, obs_flat, batch):
+        """True when a minibatch of `batch` rows of obs_flat [n_rows, d] can take K30 (xpa_small_mlp_update): the
+        small_policy_layers shape, flat parameters with the fused Adam, no data-parallel gradient sync, and the LDS
+        budget."""
+        if not getattr(self, "small_updates", True) or self.grad_sync is not None:
+            return False
         fused = getattr(self, "fused_opt", None)
-        if fm is None or fused is None or len(fm.rep) != 1 or len(fm.actor) != 2 or len(fm.critic) != 2 \
-                or fused.fs.numel % 4:
+        layers = self.small_policy_layers()
+        if layers is None or fused is None or fused.fs.numel % 4:
             return False
         if not (isinstance(obs_flat, torch.Tensor) and obs_flat.is_cuda and obs_flat.dim() == 2
                 and obs_flat.dtype == torch.float32 and obs_flat.stride(1) == 1):
             return False
-        (l0, c0, s0), (l1, c1, s1), (la, ca, _), (l2, c2, s2), (lc, cc, _) = (fm.rep[0], fm.actor[0], fm.actor[1],
-                                                                              fm.critic[0], fm.critic[1])
-        if not (c0 == c1 == c2 and s0 == s1 == s2 and ca == 0 and cc == 0 and lc.out_features == 1):
-            return False
+        (l0, l1, la, l2, lc), _, _ = layers
         h0, h1, h2, k = l0.out_features, l1.out_features, l2.out_features, la.out_features
         if any(h % 32 or h > 256 for h in (h0, h1, h2)) or not 2 <= k <= 16 or l0.in_features != obs_flat.shape[1] \
                 or l0.in_features > 32:
