@@ -264,6 +264,7 @@ typedef struct XpaSmallRolloutArgs {
     float *boot_norm;
     int64_t ld_boot;
     xpa_cursor_t *cursor;
+    int64_t *stamps; /* diagnostics (nullable): s_memtime cycles per phase summed over the steps, [9] */
 } XpaSmallRolloutArgs;
 int64_t xpa_small_rollout_lds_floats(int64_t n_envs, int64_t d_in, int64_t h0, int64_t h1, int64_t h2, int64_t k);
 int xpa_small_rollout_cartpole(const XpaSmallRolloutArgs *args, xpa_stream_t stream);

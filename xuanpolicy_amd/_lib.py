@@ -58,7 +58,7 @@ class XpaSmallRolloutArgs(ctypes.Structure):
                                                   "ep_index", "ep_score", "ep_last_score", "ep_last_len", "returns",
                                                   "ret_mean", "ret_var", "ret_count", "slot_obs", "slot_t", "overflow",
                                                   "boot_norm")]
-                + [("ld_boot", ctypes.c_int64), ("cursor", ctypes.c_void_p)])
+                + [("ld_boot", ctypes.c_int64), ("cursor", ctypes.c_void_p), ("stamps", ctypes.c_void_p)])
 
 
 # name -> (restype, argtypes); mirrors include/xuanpolicy_amd.h one-for-one.

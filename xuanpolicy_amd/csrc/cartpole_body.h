@@ -29,11 +29,38 @@ __device__ __forceinline__ double reset_dim(uint32_t seed, uint32_t env, uint32_
     return (double)xpa_u01(xpa_hash4(seed ^ kSaltCartPole, env, ep, d)) * 0.1 - 0.05;
 }
 
-// One env's step with action a (0 / 1).  Returns the reward; *te / *tr the flags; final_obs / obs / state written.
-__device__ __forceinline__ float step(const XpaCartPoleEnv &e, int64_t n, int a, bool *te_out, bool *tr_out) {
-#pragma clang fp contract(off)  // gym's Python arithmetic: every product and sum rounded on its own (no fma)
+// One env's mutable state, held in registers by the caller (K18 loads and stores it around one step; K32 keeps it
+// for a whole launch of steps).
+struct Local {
+    double x, x_dot, theta, theta_dot;
+    int ep_step;
+    uint32_t ep_index;
+    float ep_score;
+};
+
+__device__ __forceinline__ Local load(const XpaCartPoleEnv &e, int64_t n) {
+    const double *st = e.state + 4 * n;
+    return Local{st[0], st[1], st[2], st[3], e.ep_step[n], e.ep_index[n], e.ep_score[n]};
+}
+
+__device__ __forceinline__ void store(const XpaCartPoleEnv &e, int64_t n, const Local &s) {
     double *st = e.state + 4 * n;
-    double x = st[0], x_dot = st[1], theta = st[2], theta_dot = st[3];
+    st[0] = s.x;
+    st[1] = s.x_dot;
+    st[2] = s.theta;
+    st[3] = s.theta_dot;
+    e.ep_step[n] = s.ep_step;
+    e.ep_index[n] = s.ep_index;
+    e.ep_score[n] = s.ep_score;
+}
+
+// One env's step with action a (0 / 1) on the register state s: writes final_obs / obs / rew / term / trunc (and
+// the finished episode's score / length); returns the reward, *te / *tr the flags, obs_out[0..3] the next
+// observation (the reset state after a done).
+__device__ __forceinline__ float step(const XpaCartPoleEnv &e, int64_t n, int a, Local &s, bool *te_out,
+                                      bool *tr_out, float *obs_out) {
+#pragma clang fp contract(off)  // gym's Python arithmetic: every product and sum rounded on its own (no fma)
+    double x = s.x, x_dot = s.x_dot, theta = s.theta, theta_dot = s.theta_dot;
     const double force = a == 1 ? kForce : -kForce;
     const double costheta = cos(theta), sintheta = sin(theta);
     const double temp = (force + kPoleMassLength * (theta_dot * theta_dot) * sintheta) / kTotalMass;
@@ -46,9 +73,9 @@ __device__ __forceinline__ float step(const XpaCartPoleEnv &e, int64_t n, int a,
     theta_dot = theta_dot + kTau * thetaacc;
     const double th = e.theta_threshold;
     const bool te = x < -kXThreshold || x > kXThreshold || theta < -th || theta > th;
-    const int steps = e.ep_step[n] + 1;
+    const int steps = s.ep_step + 1;
     const bool tr = steps >= e.max_episode_steps;  // gym TimeLimit: independent of terminated
-    const float score = e.ep_score[n] + 1.0f;
+    const float score = s.ep_score + 1.0f;
     float *fo = e.final_obs + 4 * n;
     fo[0] = (float)x;
     fo[1] = (float)x_dot;
@@ -58,29 +85,33 @@ __device__ __forceinline__ float step(const XpaCartPoleEnv &e, int64_t n, int a,
     e.term[n] = te ? 1 : 0;
     e.trunc[n] = tr ? 1 : 0;
     if (te || tr) {
-        const uint32_t ep = e.ep_index[n] + 1u;
-        e.ep_index[n] = ep;
+        const uint32_t ep = s.ep_index + 1u;
+        s.ep_index = ep;
         e.ep_last_score[n] = score;
         e.ep_last_len[n] = steps;
-        e.ep_step[n] = 0;
-        e.ep_score[n] = 0.f;
+        s.ep_step = 0;
+        s.ep_score = 0.f;
         x = reset_dim(e.seed, (uint32_t)n, ep, 0);
         x_dot = reset_dim(e.seed, (uint32_t)n, ep, 1);
         theta = reset_dim(e.seed, (uint32_t)n, ep, 2);
         theta_dot = reset_dim(e.seed, (uint32_t)n, ep, 3);
     } else {
-        e.ep_step[n] = steps;
-        e.ep_score[n] = score;
+        s.ep_step = steps;
+        s.ep_score = score;
     }
-    st[0] = x;
-    st[1] = x_dot;
-    st[2] = theta;
-    st[3] = theta_dot;
+    s.x = x;
+    s.x_dot = x_dot;
+    s.theta = theta;
+    s.theta_dot = theta_dot;
+    obs_out[0] = (float)x;
+    obs_out[1] = (float)x_dot;
+    obs_out[2] = (float)theta;
+    obs_out[3] = (float)theta_dot;
     float *o = e.obs + n * e.ld_obs;
-    o[0] = (float)x;
-    o[1] = (float)x_dot;
-    o[2] = (float)theta;
-    o[3] = (float)theta_dot;
+    o[0] = obs_out[0];
+    o[1] = obs_out[1];
+    o[2] = obs_out[2];
+    o[3] = obs_out[3];
     *te_out = te;
     *tr_out = tr;
     return 1.0f;

@@ -14,8 +14,11 @@ __global__ __launch_bounds__(256) void cartpole_step_kernel(int64_t n_envs, cons
                                                             int64_t ld_act, XpaCartPoleEnv e) {
     const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (n >= n_envs) return;
+    cartpole::Local s = cartpole::load(e, n);
     bool te, tr;
-    cartpole::step(e, n, act_in[n * ld_act + 1] > 0.5f ? 1 : 0, &te, &tr);
+    float o[4];
+    cartpole::step(e, n, act_in[n * ld_act + 1] > 0.5f ? 1 : 0, s, &te, &tr, o);
+    cartpole::store(e, n, s);
 }
 }  // namespace
 

@@ -556,17 +556,17 @@ __device__ __forceinline__ float obs_norm1(float x, float m, float v, float clip
 }
 
 // K8's per-env body (shared with K32): reward normalisation, buffer column t, closures / kept truncation rows,
-// the return tracker; (cnt, sum, sumsq) = the env's contribution to ret_rms's batch moments.
+// the return tracker (R in, the new running return out); (cnt, sum, sumsq) = the env's contribution to ret_rms's
+// batch moments.
 template <bool DEFER, bool NORM>
-__device__ __forceinline__ void post_env(
+__device__ __forceinline__ float post_env(
     int64_t n, int64_t n_envs, int64_t T, int32_t t, bool last, float rstd, float r, bool te, bool tr, float vb,
-    float *__restrict__ returns, float *__restrict__ buf_rew, float *__restrict__ buf_term,
+    float R, float *__restrict__ buf_rew, float *__restrict__ buf_term,
     uint8_t *__restrict__ buf_closed, float *__restrict__ buf_boot, float gamma, int mask_returns, int use_rewnorm,
     float rew_range, int atari_lifeloss, const float *__restrict__ boot_obs, int64_t ld_boot, int64_t dim,
     float *__restrict__ slot_obs, int *__restrict__ slot_t, int n_slots, int *__restrict__ overflow,
     const float *__restrict__ obs_mean, const float *__restrict__ obs_var, float obs_clip,
     float *__restrict__ boot_norm, int64_t ld_norm, double &cnt, double &sum, double &sumsq) {
-    const float R = returns[n];
     const int64_t cell = n * T + t;
     buf_rew[cell] = use_rewnorm ? fminf(fmaxf(r / rstd, -rew_range), rew_range) : r;
     buf_term[cell] = te ? 1.f : 0.f;
@@ -597,21 +597,32 @@ __device__ __forceinline__ void post_env(
         sumsq = (double)Rk * (double)Rk;
         Rk = 0.f;
     }
-    returns[n] = Rk;
+    return Rk;  // the env's running return
 }
 
 // ret_rms.update_from_moments (statistic_tools.py:86-112) from the summed (count, sum, sumsq) of the closed paths.
-__device__ __forceinline__ void ret_rms_merge(double c, double s1, double s2, float *ret_mean, float *ret_var,
-                                              double *ret_count) {
+__device__ __forceinline__ void ret_rms_merge_local(double c, double s1, double s2, float &m, float &v, double &cnt) {
     if (c > 0.0) {
         const double bm = s1 / c;
         const double bvar = fmax(s2 / c - bm * bm, 0.0);
-        const double c0 = *ret_count, m0 = (double)*ret_mean, v0 = (double)*ret_var;
+        const double c0 = cnt, m0 = (double)m, v0 = (double)v;
         const double tot = c0 + c;
         const double delta = bm - m0;
-        *ret_mean = (float)(m0 + delta * c / tot);
-        *ret_var = (float)((v0 * c0 + bvar * c + delta * delta * c0 * c / tot) / tot);
-        *ret_count = tot;
+        m = (float)(m0 + delta * c / tot);
+        v = (float)((v0 * c0 + bvar * c + delta * delta * c0 * c / tot) / tot);
+        cnt = tot;
+    }
+}
+
+__device__ __forceinline__ void ret_rms_merge(double c, double s1, double s2, float *ret_mean, float *ret_var,
+                                              double *ret_count) {
+    if (c > 0.0) {
+        float m = *ret_mean, v = *ret_var;
+        double cnt = *ret_count;
+        ret_rms_merge_local(c, s1, s2, m, v, cnt);
+        *ret_mean = m;
+        *ret_var = v;
+        *ret_count = cnt;
     }
 }
 
@@ -636,8 +647,8 @@ __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
     double cnt = 0.0, sum = 0.0, sumsq = 0.0;
     const int64_t n = (int64_t)blockIdx.x * kPostThreads + threadIdx.x;
     if (n < n_envs)
-        post_env<DEFER, NORM>(n, n_envs, T, t, last, rstd, rew[n], term[n] != 0, trunc[n] != 0,
-                              DEFER ? 0.f : v_boot[n], returns, buf_rew, buf_term, buf_closed, buf_boot, gamma,
+        returns[n] = post_env<DEFER, NORM>(n, n_envs, T, t, last, rstd, rew[n], term[n] != 0, trunc[n] != 0,
+                              DEFER ? 0.f : v_boot[n], returns[n], buf_rew, buf_term, buf_closed, buf_boot, gamma,
                               mask_returns, use_rewnorm, rew_range, atari_lifeloss, boot_obs, ld_boot, dim, slot_obs,
                               slot_t, n_slots, overflow, obs_mean, obs_var, obs_clip, boot_norm, ld_norm, cnt, sum,
                               sumsq);
@@ -688,19 +699,43 @@ constexpr int kRoLdsMax = 16384;  // floats of dynamic LDS (64 KiB: no attribute
 __host__ __device__ constexpr int ro_r4(int x) { return (x + 3) & ~3; }
 
 struct RoLayout {
-    int sy, sh0, sh12, sz, swo, sbo, total;
+    int sy, sz, sbo, total;
 };
+// sy: the normalised observations [N][4]; sz: the output layers' partial sums [unit wave][N][K + 1]; sbo: biases
 __host__ __device__ inline RoLayout ro_layout(int N, int D, int H0, int H1, int H2, int K) {
     RoLayout l;
-    const int K1 = K + 1;
+    const int K1 = K + 1, WU = (H1 + H2 + 63) / 64;
+    (void)H0;
     l.sy = 0;
-    l.sh0 = ro_r4(N * D);
-    l.sh12 = l.sh0 + N * H0;
-    l.sz = l.sh12 + N * (H1 + H2);
-    l.swo = ro_r4(l.sz + N * K1);
-    l.sbo = l.swo + K1 * 64;
+    l.sz = ro_r4(N * D);
+    l.sbo = ro_r4(l.sz + WU * N * K1);
     l.total = ro_r4(l.sbo + K1);
     return l;
+}
+
+// Sum over the wave's 64 lanes on DPP lane moves (no LDS round trip); the total lands in lane 63.  Lanes a move
+// leaves out (row_mask) add 0.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float ro_dpp(float src) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, src), CTRL, ROW_MASK, 0xf,
+                                                                 false));
+}
+__device__ __forceinline__ float ro_wave_sum63(float v) {
+    v += ro_dpp<0xB1>(v);        // quad_perm [1, 0, 3, 2]
+    v += ro_dpp<0x4E>(v);        // quad_perm [2, 3, 0, 1]
+    v += ro_dpp<0x141>(v);       // row_half_mirror: sums of 8
+    v += ro_dpp<0x140>(v);       // row_mirror: sums of 16
+    v += ro_dpp<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3
+    v += ro_dpp<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
+    return v;
+}
+
+// K8's f64 wave butterfly (xpa_wave_sum) when only lanes [0, n) hold values (the rest +0): the steps whose partner
+// lanes are all empty add +0 and are skipped.
+__device__ __forceinline__ double ro_wave_sum_first(double v, int n) {
+    for (int o = 32; o > 0; o >>= 1)
+        if (o < n) v += __shfl_xor(v, o, 64);
+    return v;
 }
 
 template <int ACT>
@@ -715,76 +750,125 @@ __global__ __launch_bounds__(kRoThreads) void small_rollout_cartpole_kernel(XpaS
     extern __shared__ float lds[];
     __shared__ double s_sum[kRoThreads], s_sq[kRoThreads];
     __shared__ double s_red[kRoThreads / 64];
-    __shared__ float s_mean[32], s_var[32];
+    __shared__ float s_mean[4], s_var[4];
+    __shared__ float s_obs[256 * 4];  // the raw observations of the step
+    __shared__ float s_rstd;
+    constexpr int D = 4;  // CartPole
     const int tid = threadIdx.x;
-    const int N = a.n_envs, D = a.d_in, H1 = a.h1, H2 = a.h2, K = a.k, K1 = a.k + 1, U = a.h1 + a.h2;
+    const int N = a.n_envs, H1 = a.h1, H2 = a.h2, K = a.k, K1 = a.k + 1, U = a.h1 + a.h2;
     const int T = a.horizon;
     const RoLayout L = ro_layout(N, D, H0, H1, H2, K);
-    float *sy = lds + L.sy, *sh0 = lds + L.sh0, *sh12 = lds + L.sh12, *sz = lds + L.sz, *swo = lds + L.swo,
-          *sbo = lds + L.sbo;
+    float *sy = lds + L.sy, *sz = lds + L.sz, *sbo = lds + L.sbo;
     const XpaCartPoleEnv env{a.env_state,   a.env_obs,   a.ld_obs,     a.final_obs,  a.env_rew,
                              a.env_term,    a.env_trunc, a.ep_step,    a.ep_index,   a.ep_score,
                              a.ep_last_score, a.ep_last_len, a.env_seed, a.max_episode_steps,
                              cartpole::kThetaThreshold};
-    // output layers into LDS (rows 0..K-1 actor, row K critic; 64-float rows)
-    for (int e = tid; e < K1 * 64; e += kRoThreads) {
-        const int c = e >> 6, j = e & 63;
-        float w = 0.f;
-        if (c < K && j < H1) w = a.Wa[c * H1 + j];
-        if (c == K && j < H2) w = a.Wc[j];
-        swo[e] = w;
-    }
     if (tid < K1) sbo[tid] = tid < K ? a.ba[tid] : a.bc[0];
-    // layer 0: unit u0 = tid % H0 over row groups of G0 rows; its weight row in VGPRs
-    constexpr int G0 = kRoThreads / H0;
-    const int u0 = tid % H0, g0 = tid / H0;
-    float w0[32];
-#pragma unroll
-    for (int k = 0; k < 32; ++k) w0[k] = k < D ? a.W0[u0 * D + k] : 0.f;
-    const float b0u = a.b0[u0];
-    // layers 1 | 2 side by side: unit u12 < H1 actor, else critic
-    const int G12 = kRoThreads / U;
-    const int u12 = tid % U, g12 = tid / U;
-    const bool on12 = g12 < G12;
-    const float *wr = u12 < H1 ? a.W1 + u12 * H0 : a.W2 + (u12 - H1) * H0;
+    // The forward runs inside each wave with no LDS round trip: a wave owns 64 consecutive units of the actor |
+    // critic hidden layers (unit wave wu) for every RG-th row; lane k first forms h0[r][k] itself (the
+    // representation layer, recomputed by the WU waves sharing a row), then the hidden layer reads h0 through
+    // v_readlane (an SGPR broadcast) against the lane's weight row in VGPRs, and the output layers are wave sums.
+    const int wave = tid >> 6, lane = tid & 63;
+    const int WU = (U + 63) >> 6, RG = 4 / WU;
+    const int wu = wave % WU, rg = wave / WU;
+    const int u = wu * 64 + lane;
+    const bool uok = u < U && rg < RG;
+    const bool actor = u < H1;
+    const int l0 = lane < H0 ? lane : 0;
+    const float4 w0 = make_float4(a.W0[l0 * D], a.W0[l0 * D + 1], a.W0[l0 * D + 2], a.W0[l0 * D + 3]);
+    const float b0u = a.b0[l0];
+    const int uc = uok ? u : 0;
+    const float *wr = actor ? a.W1 + uc * H0 : a.W2 + (uc - H1) * H0;
     float w1[H0];
 #pragma unroll
-    for (int k = 0; k < H0; ++k) w1[k] = on12 ? wr[k] : 0.f;
-    const float b12 = on12 ? (u12 < H1 ? a.b1[u12] : a.b2[u12 - H1]) : 0.f;
+    for (int k = 0; k < H0; ++k) w1[k] = uok ? wr[k] : 0.f;
+    const float b12 = uok ? (actor ? a.b1[uc] : a.b2[uc - H1]) : 0.f;
+    // this lane's output-layer weights: wo[o] for the K logits (actor units) or the value (critic units)
+    float wo[3];
+#pragma unroll
+    for (int o = 0; o < 3; ++o)
+        wo[o] = !uok || o >= K1 ? 0.f : (o < K ? (actor ? a.Wa[o * H1 + uc] : 0.f) : (actor ? 0.f : a.Wc[uc - H1]));
 
+    // state that lives across the steps of the launch: each env's CartPole state and running return (thread n),
+    // the raw observations and obs statistics (LDS), the obs count (every thread), the return statistics (thread 0)
+    cartpole::Local es{};
+    float R = 0.f;
+    if (tid < N) {
+        es = cartpole::load(env, tid);
+        R = a.returns[tid];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) s_obs[tid * 4 + d] = a.env_obs[tid * a.ld_obs + d];
+    }
+    if (tid < D) {
+        s_mean[tid] = a.obs_mean[tid];
+        s_var[tid] = a.obs_var[tid];
+    }
+    double ocount = *a.obs_count;
+    float rmean = 0.f, rvar = 0.f;
+    double rcount = 0.0;
+    if (tid == 0) {
+        rmean = *a.ret_mean;
+        rvar = *a.ret_var;
+        rcount = *a.ret_count;
+        s_rstd = fminf(fmaxf(sqrtf(rvar), 0.1f), 100.0f);
+    }
     int32_t t = a.cursor->ptr;
     uint32_t step = a.cursor->step;
+    int64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0, st_t0 = 0;
+#define XPA_RO_STAMP(i_)                                                    \
+    do {                                                                    \
+        if (a.stamps && tid == 0) {                                         \
+            const int64_t now_ = (int64_t)__builtin_amdgcn_s_memtime();     \
+            st_acc[i_] += now_ - st_prev;                                   \
+            st_prev = now_;                                                 \
+        }                                                                   \
+    } while (0)
+    __syncthreads();
+    if (a.stamps && tid == 0) st_prev = st_t0 = (int64_t)__builtin_amdgcn_s_memtime();
+    constexpr int kGroups = kRoThreads / D;  // rms_partials_kernel<., 256>'s row groups at dim 4
     for (int s = 0; s < a.steps; ++s) {
         const bool last = t == T - 1;
         // (a) obs_rms.update(obs): xpa_rms_update with one partial block
         if (a.use_obsnorm) {
-            const int groups = kRoThreads / D;
-            const int c = tid % D, gsub = tid / D;
-            double sm = 0.0, q = 0.0;
-            if (gsub < groups) {
-                const float sh = a.obs_mean[c];
-                for (int r = gsub; r < N; r += groups) {
-                    const double v = (double)a.env_obs[r * a.ld_obs + c] - (double)sh;
+            double ts = 0.0, tq = 0.0;
+            if (N <= kGroups) {
+                // one row per row group: the group-ordered sums are the row sums in row order (every group sum is
+                // 0 + v or 0 + v * v, rounded once; the empty groups add +0)
+                if (tid < D) {
+#pragma clang fp contract(off)
+                    const float sh = s_mean[tid];
+                    for (int r = 0; r < N; ++r) {
+                        const double v = (double)s_obs[r * 4 + tid] - (double)sh;
+                        const double vv = v * v;
+                        ts = ts + v;
+                        tq = tq + vv;
+                    }
+                }
+            } else {
+                const int c = tid % D, gsub = tid / D;
+                double sm = 0.0, q = 0.0;
+                const float sh = s_mean[c];
+                for (int r = gsub; r < N; r += kGroups) {
+                    const double v = (double)s_obs[r * 4 + c] - (double)sh;
                     sm += v;
                     q += v * v;
                 }
+                s_sum[tid] = sm;
+                s_sq[tid] = q;
+                __syncthreads();
+                if (tid < D)
+                    for (int k = 0; k < kGroups; ++k) {
+                        ts += s_sum[k * D + tid];
+                        tq += s_sq[k * D + tid];
+                    }
             }
-            s_sum[tid] = sm;
-            s_sq[tid] = q;
-            __syncthreads();
-            const double c0 = *a.obs_count;
             if (tid < D) {
-                double ts = 0.0, tq = 0.0;
-                for (int k = 0; k < groups; ++k) {
-                    ts += s_sum[k * D + tid];
-                    tq += s_sq[k * D + tid];
-                }
                 double s1 = 0.0, q1 = 0.0;  // rms_merge_body over the one partial
                 s1 += ts;
                 q1 += tq;
-                const double n = (double)N;
+                const double n = (double)N, c0 = ocount;
                 const double ms = s1 / n;
-                const double m0 = (double)a.obs_mean[tid], v0 = (double)a.obs_var[tid];
+                const double m0 = (double)s_mean[tid], v0 = (double)s_var[tid];
                 const double bm = m0 + ms;
                 const double bvar = fmax(q1 / n - ms * ms, 0.0);
                 const double tot = c0 + n;
@@ -797,88 +881,120 @@ __global__ __launch_bounds__(kRoThreads) void small_rollout_cartpole_kernel(XpaS
                 s_mean[tid] = fm;
                 s_var[tid] = fv;
             }
-            __syncthreads();
-            if (tid == 0) *a.obs_count = c0 + (double)N;
-        } else {
-            if (tid < D) {
-                s_mean[tid] = a.obs_mean[tid];
-                s_var[tid] = a.obs_var[tid];
-            }
+            ocount = ocount + (double)N;
+            if (tid == 0) *a.obs_count = ocount;
             __syncthreads();
         }
+        XPA_RO_STAMP(0);
         // (b) normalise into the policy input and buffer column t (obs_normalize_kernel's arithmetic)
         for (int e = tid; e < N * D; e += kRoThreads) {
-            const int r = e / D, d = e - r * D;
-            const float y = obs_norm1(a.env_obs[r * a.ld_obs + d], s_mean[d], s_var[d], a.obs_clip);
+            const int r = e >> 2, d = e & 3;
+            const float y = obs_norm1(s_obs[e], s_mean[d], s_var[d], a.obs_clip);
             sy[e] = y;
             a.obs_norm[r * a.ld_norm + d] = y;
             a.buf_obs[((int64_t)r * T + t) * D + d] = y;
         }
         __syncthreads();
-        // (c) representation layer
-        for (int r = g0; r < N; r += G0) {
-            float acc = b0u;
+        XPA_RO_STAMP(1);
+        // (c)-(e) the forward, four rows per pass
+        for (int r0 = rg; r0 < N && rg < RG; r0 += 4 * RG) {
+            float h0[4], acc[4];
 #pragma unroll
-            for (int k = 0; k < 32; ++k)
-                if (k < D) acc = fmaf(w0[k], sy[r * D + k], acc);
-            sh0[r * H0 + u0] = ro_act<ACT>(acc, a.slope);
-        }
-        __syncthreads();
-        // (d) actor | critic hidden layers (the h0 row is a wave-uniform broadcast read)
-        if (on12)
-            for (int r = g12; r < N; r += G12) {
-                const float4 *hr = reinterpret_cast<const float4 *>(sh0 + r * H0);
-                float acc = b12;
+            for (int j = 0; j < 4; ++j) {
+                const int r = r0 + j * RG;
+                const float4 y = *reinterpret_cast<const float4 *>(sy + (r < N ? r : r0) * D);
+                float z = b0u;
+                z = fmaf(w0.x, y.x, z);
+                z = fmaf(w0.y, y.y, z);
+                z = fmaf(w0.z, y.z, z);
+                z = fmaf(w0.w, y.w, z);
+                h0[j] = ro_act<ACT>(z, a.slope);
+                acc[j] = b12;
+            }
 #pragma unroll
-                for (int i = 0; i < H0 / 4; ++i) {
-                    const float4 h = hr[i];
-                    acc = fmaf(w1[4 * i], h.x, acc);
-                    acc = fmaf(w1[4 * i + 1], h.y, acc);
-                    acc = fmaf(w1[4 * i + 2], h.z, acc);
-                    acc = fmaf(w1[4 * i + 3], h.w, acc);
+            for (int k = 0; k < H0; ++k)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float hk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, h0[j]), k));
+                    acc[j] = fmaf(w1[k], hk, acc[j]);
                 }
-                sh12[r * U + u12] = ro_act<ACT>(acc, a.slope);
+            float part[4][3];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float h = ro_act<ACT>(acc[j], a.slope);
+#pragma unroll
+                for (int o = 0; o < 3; ++o) part[j][o] = wo[o] * h;
             }
-        __syncthreads();
-        // (e) logits | value
-        for (int p = tid; p < N * K1; p += kRoThreads) {
-            const int r = p / K1, c = p - r * K1;
-            const float4 *h = reinterpret_cast<const float4 *>(sh12 + r * U + (c < K ? 0 : H1));
-            const float4 *w = reinterpret_cast<const float4 *>(swo + c * 64);
-            const int hx = (c < K ? H1 : H2) >> 2;
-            float acc = sbo[c];
-            for (int i = 0; i < hx; ++i) {
-                const float4 hv = h[i], wv = w[i];
-                acc = fmaf(wv.x, hv.x, acc);
-                acc = fmaf(wv.y, hv.y, acc);
-                acc = fmaf(wv.z, hv.z, acc);
-                acc = fmaf(wv.w, hv.w, acc);
-            }
-            sz[p] = acc;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int o = 0; o < 3; ++o) part[j][o] = ro_wave_sum63(part[j][o]);
+            if (lane == 63)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int r = r0 + j * RG;
+                    if (r < N)
+                        for (int o = 0; o < K1; ++o) sz[(wu * N + r) * K1 + o] = part[j][o];
+                }
         }
         __syncthreads();
+        XPA_RO_STAMP(4);
         // (f) sample + store, env step, post step (one thread per env)
-        const float rstd = fminf(fmaxf(sqrtf(*a.ret_var), 0.1f), 100.0f);
         double cnt = 0.0, sum = 0.0, sumsq = 0.0;
         if (tid < N) {
-            const float *z = sz + tid * K1;
+            float z[3];
+            for (int o = 0; o < K1; ++o) {
+                float v = sbo[o];
+                for (int w = 0; w < WU; ++w) v += sz[(w * N + tid) * K1 + o];
+                z[o] = v;
+            }
             const int pick = cat_sample_store_at(tid, K, T, t, step, z, z[K], a.seed, a.buf_act, a.buf_logp,
                                                  a.buf_val, a.act_in, a.ld_act);
             bool te, tr;
-            const float r = cartpole::step(env, tid, pick, &te, &tr);
-            post_env<true, true>(tid, N, T, t, last, rstd, r, te, tr, 0.f, a.returns, a.buf_rew, a.buf_term,
-                                 a.buf_closed, a.buf_boot, a.gamma, a.mask_returns, a.use_rewnorm, a.rew_range, 0,
-                                 a.final_obs, 4, D, a.slot_obs, a.slot_t, a.n_slots, a.overflow, a.obs_mean, a.obs_var,
-                                 a.obs_clip, a.boot_norm, a.ld_boot, cnt, sum, sumsq);
+            float o[4];
+            const float r = cartpole::step(env, tid, pick, es, &te, &tr, o);
+#pragma unroll
+            for (int d = 0; d < 4; ++d) s_obs[tid * 4 + d] = o[d];
+            R = post_env<true, true>(tid, N, T, t, last, s_rstd, r, te, tr, 0.f, R, a.buf_rew, a.buf_term,
+                                     a.buf_closed, a.buf_boot, a.gamma, a.mask_returns, a.use_rewnorm, a.rew_range,
+                                     0, a.final_obs, 4, D, a.slot_obs, a.slot_t, a.n_slots, a.overflow, s_mean, s_var,
+                                     a.obs_clip, a.boot_norm, a.ld_boot, cnt, sum, sumsq);
+            a.returns[tid] = R;
         }
-        cnt = xpa_block_sum(cnt, s_red, kRoThreads / 64);
-        sum = xpa_block_sum(sum, s_red, kRoThreads / 64);
-        sumsq = xpa_block_sum(sumsq, s_red, kRoThreads / 64);
-        if (tid == 0) ret_rms_merge(cnt, sum, sumsq, a.ret_mean, a.ret_var, a.ret_count);
+        XPA_RO_STAMP(5);
+        // (g) ret_rms over the closed paths: K8's block sums (all envs in wave 0 when N <= 64: the other waves'
+        // sums are +0), then its merge
+        if (N <= 64) {
+            if (tid < 64) {
+                const int np2 = N <= 1 ? 1 : 1 << (32 - __builtin_clz(N - 1));  // lanes [0, np2) may hold values
+                cnt = 0.0 + ro_wave_sum_first(cnt, np2);
+                sum = 0.0 + ro_wave_sum_first(sum, np2);
+                sumsq = 0.0 + ro_wave_sum_first(sumsq, np2);
+            }
+        } else {
+            cnt = xpa_block_sum(cnt, s_red, kRoThreads / 64);
+            sum = xpa_block_sum(sum, s_red, kRoThreads / 64);
+            sumsq = xpa_block_sum(sumsq, s_red, kRoThreads / 64);
+        }
+        if (tid == 0 && cnt > 0.0) {
+            ret_rms_merge_local(cnt, sum, sumsq, rmean, rvar, rcount);
+            *a.ret_mean = rmean;
+            *a.ret_var = rvar;
+            *a.ret_count = rcount;
+            s_rstd = fminf(fmaxf(sqrtf(rvar), 0.1f), 100.0f);
+        }
+        XPA_RO_STAMP(6);
         t = (t + 1) % T;
         step += 1u;
-        __syncthreads();  // env obs, ret / obs statistics and count visible to the next step
+        __syncthreads();  // next observations, statistics and rstd visible to the next step
+        XPA_RO_STAMP(7);
     }
+#undef XPA_RO_STAMP
+    if (a.stamps && tid == 0) {
+        for (int i = 0; i < 8; ++i) a.stamps[i] = st_acc[i];
+        a.stamps[8] = (int64_t)__builtin_amdgcn_s_memtime() - st_t0;
+    }
+    if (tid < N) cartpole::store(env, tid, es);
     if (tid == 0) {
         a.cursor->ptr = t;
         a.cursor->step = step;

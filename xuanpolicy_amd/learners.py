@@ -306,8 +306,9 @@ class _FusedPolicyGradient(Learner):
             return False
         return int(ops.lib().xpa_small_mlp_lds_floats(batch, l0.in_features, h0, h1, h2, k)) <= 40704
 
-    def _small_launch(self, obs_flat, idx, act, adv, ret, old_logp, use_advnorm):
-        """One K30 launch (capturable): reads lr / Adam step at the schedule cursor and advances it."""
+    def _small_launch(self, obs_flat, idx, act, adv, ret, old_logp, use_advnorm, scalars=None):
+        """One K30 launch (capturable): reads lr / Adam step at the schedule cursor and advances it.  scalars: the
+        8-float destination of the loss scalars (default: the learner's shared one)."""
         fm, fused = self._fused_mlp(), self.fused_opt
         (l0, code, slope), (l1, _, _), (la, _, _), (l2, _, _), (lc, _, _) = (fm.rep[0], fm.actor[0], fm.actor[1],
                                                                              fm.critic[0], fm.critic[1])
@@ -338,12 +339,13 @@ class _FusedPolicyGradient(Learner):
         a.param, a.grad = fused.fs.param.data_ptr(), fused.fs.flat.data_ptr()
         a.exp_avg, a.exp_avg_sq, a.n = fused.exp_avg.data_ptr(), fused.exp_avg_sq.data_ptr(), fused.fs.numel
         a.sched, a.cursor = fused._sched.data_ptr(), fused._cursor.data_ptr()
-        a.scalars, a.total_norm_out = self._small_scalars.data_ptr(), fused.total_norm.data_ptr()
+        out = self._small_scalars if scalars is None else scalars
+        a.scalars, a.total_norm_out = out.data_ptr(), fused.total_norm.data_ptr()
         st = getattr(self, "small_stamps", None)   # diagnostics: int64 [16] of phase timestamps (tools/k30_stamps.py)
         a.stamps = st.data_ptr() if st is not None else None
         _lib.check(ops.lib().xpa_small_mlp_update(ctypes.byref(a), ops._stream(obs_flat.device)),
                    "xpa_small_mlp_update")
-        return self._small_scalars
+        return out
 
     def small_update(self, obs_flat, idx, act, adv, ret, old_logp=None, use_advnorm=True):
         """One minibatch update through K30 (eager): the device part, then the host bookkeeping of the step."""
@@ -386,9 +388,12 @@ class _FusedPolicyGradient(Learner):
             if self.__dict__.get("_graph_pool") is None:
                 self._graph_pool = torch.cuda.graph_pool_handle()
             g = torch.cuda.CUDAGraph()
+            # every update writes its loss scalars into its own row (no per-update copy inside the graph)
+            rows = torch.zeros((len(batches), 8), dtype=torch.float32, device=obs_flat.device)
             try:
                 with torch.cuda.graph(g, pool=self._graph_pool):
-                    outs = [self._small_launch(obs_flat, *b, use_advnorm=use_advnorm).clone() for b in batches]
+                    outs = [self._small_launch(obs_flat, *b, use_advnorm=use_advnorm, scalars=rows[i])
+                            for i, b in enumerate(batches)]
             except Exception:
                 self._graph_failed = True
                 torch.cuda.synchronize()
