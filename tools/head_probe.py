@@ -17,6 +17,10 @@ the DMAs 68-74 (so the loop itself reaches ~80 % of the floor and the DMAs add ~
 had been one branch + load + wait per output).  Rejected: per-wave private operand rings (each wave
 DMAs its own A copy + its B rows, no k-loop barrier): GEMM 100 / 92, worse — the 4x A re-reads cost more
 than the barriers (MFMA stream alone only 70 / 66 without them).
+r03: fragment prefetch (chunk c + 1's ds_reads in flight during chunk c's MFMAs, DMAs two chunks ahead,
+measured as an A/B variant and dropped): GEMM alone 88.5 / 88.2 vs 89.0 / 86.1, full 115.9 / 97.3 vs 113.8 / 98.0
+— the fragment reads' latency was not what bounds the loop.  hipBLASLt's own F.linear of the same
+[65 536 x 256] x [256 x 256] shape: 82.6 us (0.66 of the floor) — K16's GEMM is within 7 % of it.
 Shape: the C2
 minibatch (65 536 rows, hidden 256, Gaussian actor K = 6, PPO); per-launch device time from events
 around `reps` back-to-back launches."""
@@ -32,6 +36,10 @@ OUT = os.path.join(HERE, "_probe")
 VARIANTS = {0: "full", 1: "gemm only", 2: "epilogue only", 3: "staging only", 4: "epilogue without dz stores",
             5: "epilogue without phase 2", 6: "gemm without operand DMAs"}
 FLAGS = {}   # variant -> hipcc defines, when not just -DXPA_HEAD_PROBE=<variant>
+# variant subset: XPA_PROBE_VARIANTS=0,1,7 (default all)
+_sel = os.environ.get("XPA_PROBE_VARIANTS")
+if _sel:
+    VARIANTS = {int(v): VARIANTS[int(v)] for v in _sel.split(",")}
 
 
 def build():
@@ -39,7 +47,7 @@ def build():
     os.makedirs(OUT, exist_ok=True)
     procs = []
     for v in VARIANTS:
-        cmd = ([os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")] + _lib.HIPCC_FLAGS + FLAGS.get(v, ["-DXPA_HEAD_PROBE=%d" % v]) + ["-o",
+        cmd = ([os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")] + _lib.HIPCC_FLAGS + ["-shared"] + FLAGS.get(v, ["-DXPA_HEAD_PROBE=%d" % v]) + ["-o",
                os.path.join(OUT, "libxpa_probe%d.so" % v)] + [os.path.join(_lib.CSRC, s) for s in _lib.SOURCES])
         procs.append(subprocess.Popen(cmd))
     for p in procs:
