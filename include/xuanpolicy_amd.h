@@ -352,6 +352,13 @@ typedef struct XpaSmallMlpArgs {
     int32_t *cursor;
     float *scalars, *total_norm_out;
     int64_t *stamps;   /* diagnostics (nullable): s_memtime at the kernel's phase boundaries, thread 0 */
+    /* split form (n_groups = ceil(batch / 32) in [2, 16]; 0 or 1: one workgroup): workgroup g forms the forward /
+     * backward of minibatch rows [32 g, 32 g + 32) and writes its partial gradients into grad_part[g * n ...] (at the
+     * flat buffer's offsets; zero-initialised once, 16-B aligned) and its loss sums into loss_part[8 g ...]; a second
+     * launch sums them in g order, clips and steps Adam. */
+    int n_groups;
+    float *grad_part;
+    double *loss_part;
 } XpaSmallMlpArgs;
 int64_t xpa_small_mlp_lds_floats(int64_t batch, int64_t d_in, int64_t h0, int64_t h1, int64_t h2, int64_t k);
 int xpa_small_mlp_update(const XpaSmallMlpArgs *args, xpa_stream_t stream);

@@ -249,3 +249,28 @@ def test_fused_rollout_matches_multi_kernel_steps(agent_name):
             np.testing.assert_allclose(f[k][:, :127], m[k][:, :127], rtol=1e-4, atol=1e-5, err_msg=k)
         else:
             np.testing.assert_array_equal(f[k], m[k], err_msg=k)
+
+
+@pytest.mark.parametrize("n_steps,n_mb", [(128, 8), (100, 7)])
+def test_small_mlp_split_matches_one_workgroup(n_steps, n_mb):
+    """K30's split form (one workgroup per 32 minibatch rows writing partial gradients + a finalize launch that sums
+    them in workgroup order, clips and steps Adam) against the one-workgroup form from the same start: every update's
+    loss scalars and the parameters after two iterations, within the f32 reassociation of the row sums (128-row and
+    ragged 114-row minibatches: 4 workgroups, the last with 18 rows)."""
+    from xuanpolicy_amd.runner import build_cartpole_ppo
+    res = []
+    for split in (True, False):
+        agent = build_cartpole_ppo(n_envs=8, n_steps=n_steps, hidden=64, seed=8, device=DEV, n_minibatch=n_mb)
+        agent.learner.small_split = split
+        agent.update_log = []
+        for _ in range(2):
+            agent.train(n_steps, log=False)
+        torch.cuda.synchronize()
+        res.append(([u.cpu().numpy() for u in agent.update_log],
+                    [p.detach().cpu().numpy().copy() for p in agent.policy.parameters()]))
+    (log_s, par_s), (log_o, par_o) = res
+    assert len(log_s) == len(log_o) > 0
+    for u, (a, b) in enumerate(zip(log_s, log_o)):
+        np.testing.assert_allclose(a[:6], b[:6], rtol=1e-4, atol=1e-5, err_msg="update %d" % u)
+    for a, b in zip(par_s, par_o):
+        np.testing.assert_allclose(a, b, rtol=1e-3, atol=1e-5)

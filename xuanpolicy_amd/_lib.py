@@ -37,7 +37,8 @@ class XpaSmallMlpArgs(ctypes.Structure):
                                                   "gb2", "gWa", "gba", "gWc", "gbc", "param", "grad", "exp_avg",
                                                   "exp_avg_sq")]
                 + [("n", ctypes.c_int64), ("sched", ctypes.c_void_p), ("cursor", ctypes.c_void_p),
-                   ("scalars", ctypes.c_void_p), ("total_norm_out", ctypes.c_void_p), ("stamps", ctypes.c_void_p)])
+                   ("scalars", ctypes.c_void_p), ("total_norm_out", ctypes.c_void_p), ("stamps", ctypes.c_void_p),
+                   ("n_groups", ctypes.c_int), ("grad_part", ctypes.c_void_p), ("loss_part", ctypes.c_void_p)])
 
 
 class XpaSmallRolloutArgs(ctypes.Structure):

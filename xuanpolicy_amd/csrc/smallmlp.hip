@@ -73,9 +73,9 @@ __device__ __forceinline__ f32x16 sm_tile(const float *pa, int am, int ak, int m
 }
 __device__ __forceinline__ int sm_row(int r) { return (r & 3) + 8 * (r >> 2) + 4 * ((threadIdx.x & 63) >> 5); }
 
-#define XPA_SM_STAMP(i_)                                                                  \
-    do {                                                                                  \
-        if (a.stamps && t == 0) a.stamps[i_] = (int64_t)__builtin_amdgcn_s_memtime();     \
+#define XPA_SM_STAMP(i_)                                                                                  \
+    do {                                                                                                  \
+        if (a.stamps && t == 0 && blockIdx.x == 0) a.stamps[i_] = (int64_t)__builtin_amdgcn_s_memtime(); \
     } while (0)
 
 template <int ACT, int ALGO>
@@ -85,7 +85,17 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
     __shared__ float s_stat[4];
     __shared__ float s_coef, s_step, s_inv;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, li = lane & 31;
-    const int B = a.batch, BP = (B + 31) & ~31, S = BP + 4;
+    // Split form (G = gridDim.x > 1): workgroup g takes minibatch rows [32 g, 32 g + 32) and writes its partial
+    // weight / bias gradients (sums over its rows) into grad_part[g] at the flat buffer's offsets and its loss sums
+    // into loss_part[g]; small_mlp_finalize_kernel then sums the partials in g order, clips and steps Adam.  The
+    // advantage moments are over the whole minibatch in every workgroup.
+    const int G = gridDim.x, gi = blockIdx.x;
+    const int Btot = a.batch;
+    const int r0 = G > 1 ? 32 * gi : 0;
+    const int B = G > 1 ? min(32, Btot - r0) : Btot;   // this workgroup's rows
+    const int64_t *idx = a.idx + r0;
+    auto gp = [&](float *p) -> float * { return G > 1 ? a.grad_part + (int64_t)gi * a.n + (p - a.grad) : p; };
+    const int BP = (B + 31) & ~31, S = BP + 4;
     const int D = a.d_in, DP = (a.d_in + 3) & ~3, H0 = a.h0, H1 = a.h1, H2 = a.h2, K = a.k, KP = (a.k + 3) & ~3;
     const int MB = BP / 32;
     const float slope = a.slope;
@@ -97,9 +107,11 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
     float *dlT = h2T + H2 * S;             // [KP][S]  d logits (rows >= K zero)
     float *dvT = dlT + KP * S;             // [4][S]   d v in row 0
     float *W0T = dvT + 4 * S;              // [DP][H0]
-    float *W1T = W0T + DP * H0;            // [H0][H1], after the forward W1 row-major [H1][H0]
-    float *W2T = W1T + H0 * H1;            // [H0][H2], after the forward W2 row-major [H2][H0]
-    float *WaT = W2T + H0 * H2;            // [H1][KP]
+    // W1T / W2T: row stride H1 + 1 / H2 + 1, so that the coalesced (source-order) staging writes are conflict-free
+    const int H1P = H1 + 1, H2P = H2 + 1;
+    float *W1T = W0T + DP * H0;            // [H0][H1P], after the forward W1 row-major [H1][H0]
+    float *W2T = W1T + H0 * H1P;           // [H0][H2P], after the forward W2 row-major [H2][H0] (at W1T + H1 H0)
+    float *WaT = W2T + H0 * H2P;           // [H1][KP]
     float *Wcv = WaT + H1 * KP;            // [H2]
     float *b0s = Wcv + H2, *b1s = b0s + H0, *b2s = b1s + H1, *bas = b2s + H2, *bcs = bas + KP;
     float *rowf = bcs + 4;                 // action, old_logp, adv, ret: [4][BP]
@@ -110,7 +122,9 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
     // (five dependent load / store rounds took ~21 k cycles before)
     const int n0 = H0 * D, na = K * H1, nm = n0 + na + H2 + H0 + H1 + H2 + K + 1;   // W0 | Wa | Wc | biases
     const int nw1 = H0 * H1, nw2 = H0 * H2;
-    const bool fast = nm <= 2 * kSmThreads && nw1 <= 8 * kSmThreads && nw2 <= 8 * kSmThreads && BP <= kSmThreads;
+    const bool fast = nm <= 2 * kSmThreads && nw1 <= 8 * kSmThreads && nw2 <= 8 * kSmThreads && BP <= kSmThreads &&
+                      Btot <= kSmThreads;
+    float adv_all = 0.f;   // split form: the advantage of minibatch row t (the moments are over every row)
     // element e of the small-tensor range: its source (loads) and LDS destination (stores)
     auto msrc_of = [&](int e, int &off) -> const float * {
         if (e < n0) { off = e; return a.W0; }
@@ -135,7 +149,9 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
     };
     if (fast) {
         const bool rb = t < BP && t < B;
-        int64_t row = rb ? a.idx[t] : 0;
+        int64_t row = rb ? idx[t] : 0;
+        const bool ra = G > 1 && t < Btot;
+        const int64_t rowa = ra ? a.idx[t] : 0;
         float vm[2], v1[8], v2[8];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -144,10 +160,10 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
             vm[u] = t + u * kSmThreads < nm ? src[off] : 0.f;
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {   // destination order (see stage_T below)
+        for (int u = 0; u < 8; ++u) {   // source order: coalesced loads (see stage_T below)
             const int e1 = t + u * kSmThreads;
-            v1[u] = e1 < nw1 ? a.W1[(e1 % H1) * H0 + e1 / H1] : 0.f;
-            v2[u] = e1 < nw2 ? a.W2[(e1 % H2) * H0 + e1 / H2] : 0.f;
+            v1[u] = e1 < nw1 ? a.W1[e1] : 0.f;
+            v2[u] = e1 < nw2 ? a.W2[e1] : 0.f;
         }
         // the rows (second round trip)
         const bool valid = rb && row >= 0 && row < a.n_rows;
@@ -156,6 +172,7 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
 #pragma unroll
         for (int i = 0; i < 32; ++i) xo[i] = i < D ? a.obs[rc * a.obs_ld + i] : 0.f;
         const float act_v = a.actions[rc], lp_v = a.old_logp ? a.old_logp[rc] : 0.f, av = a.adv[rc], rt = a.ret[rc];
+        if (ra && rowa >= 0 && rowa < a.n_rows) adv_all = a.adv[rowa];
         // LDS stores
 #pragma unroll
         for (int u = 0; u < 2; ++u)
@@ -163,8 +180,8 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int e1 = t + u * kSmThreads;
-            if (e1 < nw1) W1T[e1] = v1[u];
-            if (e1 < nw2) W2T[e1] = v2[u];
+            if (e1 < nw1) W1T[(e1 % H0) * H1P + e1 / H0] = v1[u];
+            if (e1 < nw2) W2T[(e1 % H0) * H2P + e1 / H0] = v2[u];
         }
         if (t < BP) {
 #pragma unroll
@@ -213,30 +230,32 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
         for (int e = t; e < (DP - D) * H0; e += kSmThreads) W0T[D * H0 + e] = 0.f;
         for (int e = t; e < H1 * (KP - K); e += kSmThreads) WaT[(e / (KP - K)) * KP + K + e % (KP - K)] = 0.f;
         for (int e = K + t; e < KP; e += kSmThreads) bas[e] = 0.f;
-        // W1 [H1][H0] -> W1T [H0][H1], W2 likewise: 8 loads per thread in flight
-        // walked in destination order (dst[e], e = i rows + j, from src[j cols + i]): consecutive lanes write
-        // consecutive LDS words (source order made every lane of a wave hit one bank: a 64-way conflict per write)
-        auto stage_T = [&](const float *src, int rows, int cols, float *dst) {
+        // W1 [H1][H0] -> W1T [H0][H1P], W2 likewise: 8 loads per thread in flight, walked in source order (coalesced:
+        // a destination-order gather made every lane of a wave touch its own cache line) and written with the odd
+        // row stride H1P (consecutive lanes -> consecutive banks; with stride H1 every lane hit one bank)
+        auto stage_T = [&](const float *src, int rows, int cols, float *dst, int ldd) {
             const int n = rows * cols;
             for (int e0 = t; e0 < n; e0 += 8 * kSmThreads) {
                 float v[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const int e = e0 + u * kSmThreads;
-                    v[u] = e < n ? src[(e % rows) * cols + e / rows] : 0.f;
+                    v[u] = e < n ? src[e] : 0.f;
                 }
 #pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (e0 + u * kSmThreads < n) dst[e0 + u * kSmThreads] = v[u];
+                for (int u = 0; u < 8; ++u) {
+                    const int e = e0 + u * kSmThreads;
+                    if (e < n) dst[(e % cols) * ldd + e / cols] = v[u];
+                }
             }
         };
-        stage_T(a.W1, H1, H0, W1T);
-        stage_T(a.W2, H2, H0, W2T);
+        stage_T(a.W1, H1, H0, W1T, H1P);
+        stage_T(a.W2, H2, H0, W2T, H2P);
     }
     double adv_s0 = 0.0, adv_q0 = 0.0;
     for (int b = t; b < BP; b += kSmThreads) {
         const bool ok = b < B;
-        const int64_t row = ok ? a.idx[b] : 0;
+        const int64_t row = ok ? idx[b] : 0;
         const bool valid = ok && row >= 0 && row < a.n_rows;
         const int64_t rc = valid ? row : 0;
         float xo[32];
@@ -262,10 +281,25 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
     for (int e = K + t; e < KP; e += kSmThreads) bas[e] = 0.f;
     __syncthreads();   // the rows' advantages are in LDS
     double adv_s = 0.0, adv_q = 0.0;
-    for (int b = t; b < B; b += kSmThreads) {   // the minibatch advantage moments (K4's (sum, sumsq) in f64)
-        const double ad = (double)rowf[2 * BP + b];
-        adv_s += ad;
-        adv_q += ad * ad;
+    if (G == 1) {
+        for (int b = t; b < B; b += kSmThreads) {   // the minibatch advantage moments (K4's (sum, sumsq) in f64)
+            const double ad = (double)rowf[2 * BP + b];
+            adv_s += ad;
+            adv_q += ad * ad;
+        }
+    } else if (fast) {
+        if (t < Btot) {   // the same per-row terms, from the rows' advantages loaded with the staging
+            const double ad = (double)adv_all;
+            adv_s += ad;
+            adv_q += ad * ad;
+        }
+    } else {
+        for (int b = t; b < Btot; b += kSmThreads) {
+            const int64_t row = a.idx[b];
+            const double ad = (row >= 0 && row < a.n_rows) ? (double)a.adv[row] : 0.0;
+            adv_s += ad;
+            adv_q += ad * ad;
+        }
     }
     for (int e = t; e < 4 * S; e += kSmThreads) dvT[e] = 0.f;
     for (int e = t; e < KP * S; e += kSmThreads) dlT[e] = 0.f;
@@ -283,8 +317,8 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
             q += s_red[kSmWaves + i];
         }
         if (a.use_advnorm) {   // memory_tools.py:241-242, the arithmetic of loss.hip adv_moments
-            const double mean = s / (double)B;
-            const double var = fmax(q / (double)B - mean * mean, 0.0);
+            const double mean = s / (double)Btot;
+            const double var = fmax(q / (double)Btot - mean * mean, 0.0);
             s_stat[0] = (float)mean;
             s_stat[1] = (float)(1.0 / ((double)(float)sqrt(var) + 1e-8));
         } else {
@@ -307,10 +341,10 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
         for (int tl = w; tl < n1 + n2; tl += kSmWaves) {
             const bool two = tl >= n1;
             const int q = two ? tl - n1 : tl, b0 = 32 * (q % MB), j0 = 32 * (q / MB);
-            const int HO = two ? H2 : H1;
+            const int HOP = two ? H2P : H1P;
             const float *WT = two ? W2T : W1T, *bb = two ? b2s : b1s;
             float *outT = two ? h2T : h1T;
-            const f32x16 acc = sm_tile(h0T + b0, 1, S, 32, WT + j0, HO, 1, 32, H0);
+            const f32x16 acc = sm_tile(h0T + b0, 1, S, 32, WT + j0, HOP, 1, 32, H0);
 #pragma unroll
             for (int r = 0; r < 16; ++r)
                 outT[(j0 + li) * S + b0 + sm_row(r)] = sm_act<ACT>(acc[r] + bb[j0 + li], slope);
@@ -337,11 +371,11 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
     __syncthreads();
     XPA_SM_STAMP(3);
     // ---- loss, one thread per row (K2's categorical arithmetic) ----
-    const float inv_b = 1.0f / (float)B;
+    const float inv_b = 1.0f / (float)Btot;
     float surr = 0.f, sqe = 0.f, ent = 0.f, clipc = 0.f, vsum = 0.f;
     const float mean_a = s_stat[0], inv_a = s_stat[1];
     for (int b = t; b < B; b += kSmThreads) {
-        const int64_t row = a.idx[b];
+        const int64_t row = idx[b];
         if (!(row >= 0 && row < a.n_rows)) continue;   // out-of-range index: zero gradient (dlT / dvT stay 0)
         const float *zr = logit + b * KP;
         const float A_n = (rowf[2 * BP + b] - mean_a) * inv_a;
@@ -397,7 +431,14 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
         }
     }
     __syncthreads();
-    if (t == 0) {
+    if (t == 0 && G > 1) {   // split form: this workgroup's loss sums (finalized by small_mlp_finalize_kernel)
+        for (int q = 0; q < 5; ++q) {
+            double tq = 0.0;
+            for (int i = 0; i < kSmWaves; ++i) tq += s_red[q * kSmWaves + i];
+            a.loss_part[gi * 8 + q] = tq;
+        }
+    }
+    if (t == 0 && G == 1) {
         double tot[5];
         for (int q = 0; q < 5; ++q) {
             tot[q] = 0.0;
@@ -444,8 +485,8 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
             const int m = sm_row(r);
             if (val ? m == 0 : m < K) {
                 const float g = acc[r];
-                if (val) a.gWc[j0 + li] = g;
-                else a.gWa[m * H1 + j0 + li] = g;
+                if (val) gp(a.gWc)[j0 + li] = g;
+                else gp(a.gWa)[m * H1 + j0 + li] = g;
                 sq += (double)g * g;
             }
         }
@@ -476,7 +517,7 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
             const bool two = tl >= n1;
             const int q = two ? tl - n1 : tl, j0 = 32 * (q % ((two ? H2 : H1) / 32)), i0 = 32 * (q / ((two ? H2 : H1) / 32));
             const f32x16 acc = sm_tile((two ? h2T : h1T) + j0 * S, S, 1, 32, h0T + i0 * S, 1, S, 32, BP);
-            float *gW = two ? a.gW2 : a.gW1;
+            float *gW = gp(two ? a.gW2 : a.gW1);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const float g = acc[r];
@@ -508,7 +549,7 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
         for (int r = 0; r < 16; ++r) {
             if (li < D) {
                 const float g = acc[r];
-                a.gW0[(i0 + sm_row(r)) * D + li] = g;
+                gp(a.gW0)[(i0 + sm_row(r)) * D + li] = g;
                 sq += (double)g * g;
             }
         }
@@ -519,11 +560,11 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
         for (int f = t; f < nr; f += kSmThreads) {
             const float *src;
             float *dst;
-            if (f < H0) { src = h0T + f * S; dst = a.gb0 + f; }
-            else if (f < H0 + H1) { src = h1T + (f - H0) * S; dst = a.gb1 + f - H0; }
-            else if (f < H0 + H1 + H2) { src = h2T + (f - H0 - H1) * S; dst = a.gb2 + f - H0 - H1; }
-            else if (f < H0 + H1 + H2 + K) { src = dlT + (f - H0 - H1 - H2) * S; dst = a.gba + f - H0 - H1 - H2; }
-            else { src = dvT; dst = a.gbc; }
+            if (f < H0) { src = h0T + f * S; dst = gp(a.gb0) + f; }
+            else if (f < H0 + H1) { src = h1T + (f - H0) * S; dst = gp(a.gb1) + f - H0; }
+            else if (f < H0 + H1 + H2) { src = h2T + (f - H0 - H1) * S; dst = gp(a.gb2) + f - H0 - H1; }
+            else if (f < H0 + H1 + H2 + K) { src = dlT + (f - H0 - H1 - H2) * S; dst = gp(a.gba) + f - H0 - H1 - H2; }
+            else { src = dvT; dst = gp(a.gbc); }
             float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
             for (int b = 0; b < BP; b += 4) {
                 const float4 v = *reinterpret_cast<const float4 *>(src + b);
@@ -538,6 +579,7 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
         }
     }
     XPA_SM_STAMP(9);
+    if (G > 1) return;   // the split form's partials are done: small_mlp_finalize_kernel sums, clips and steps
     // ---- clip_grad_norm_ + Adam over the flat buffers (K9's arithmetic, schedule at the device cursor) ----
     sq = xpa_wave_sum(sq);
     if (lane == 0) s_red[w] = sq;
@@ -603,11 +645,128 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_update_kernel(XpaSmal
     if (t == 0) a.cursor[0] = a.cursor[0] + 1;
 }
 
+// Split form's second launch: the loss scalars from the workgroups' loss sums, the gradient as the sum of the
+// workgroups' partials in workgroup order (written to the flat gradient buffer), clip_grad_norm_ and Adam — K30's
+// tail arithmetic.
+template <int ALGO>
+__global__ __launch_bounds__(kSmThreads, 1) void small_mlp_finalize_kernel(XpaSmallMlpArgs a) {
+    __shared__ double s_red[kSmWaves];
+    __shared__ float s_coef, s_step, s_inv;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int G = a.n_groups;
+    if (t == 0) {
+        double tot[5];
+        for (int q = 0; q < 5; ++q) {
+            tot[q] = 0.0;
+            for (int g = 0; g < G; ++g) tot[q] += a.loss_part[g * 8 + q];
+        }
+        const double Bd = (double)a.batch;
+        const double actor = -tot[0] / Bd, critic = tot[1] / Bd, entropy = tot[2] / Bd;
+        a.scalars[XPA_OUT_ACTOR_LOSS] = (float)actor;
+        a.scalars[XPA_OUT_CRITIC_LOSS] = (float)critic;
+        a.scalars[XPA_OUT_ENTROPY] = (float)entropy;
+        a.scalars[XPA_OUT_LOSS] = (float)(actor - (double)a.ent_coef * entropy + (double)a.vf_coef * critic);
+        a.scalars[XPA_OUT_CLIP_RATIO] = ALGO == XPA_ALGO_PPO ? (float)(tot[3] / Bd) : 0.f;
+        a.scalars[XPA_OUT_VALUE_MEAN] = (float)(tot[4] / Bd);
+    }
+    const int64_t n4 = a.n / 4;
+    const float4 *part4 = reinterpret_cast<const float4 *>(a.grad_part);
+    float4 *p4 = reinterpret_cast<float4 *>(a.param), *g4 = reinterpret_cast<float4 *>(a.grad);
+    float4 *m4 = reinterpret_cast<float4 *>(a.exp_avg), *v4 = reinterpret_cast<float4 *>(a.exp_avg_sq);
+    double sq = 0.0;
+    for (int64_t i0 = t; i0 < n4; i0 += 2 * kSmThreads) {
+        float4 P[2][16];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int64_t i = i0 + u * kSmThreads < n4 ? i0 + u * kSmThreads : n4 - 1;
+#pragma unroll
+            for (int g = 0; g < 16; ++g)
+                if (g < G) P[u][g] = part4[(int64_t)g * n4 + i];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            float4 s = P[u][0];
+#pragma unroll
+            for (int g = 1; g < 16; ++g)
+                if (g < G) {
+                    s.x += P[u][g].x;
+                    s.y += P[u][g].y;
+                    s.z += P[u][g].z;
+                    s.w += P[u][g].w;
+                }
+            if (i0 + u * kSmThreads < n4) {
+                g4[i0 + u * kSmThreads] = s;
+                sq += (double)s.x * s.x;
+                sq += (double)s.y * s.y;
+                sq += (double)s.z * s.z;
+                sq += (double)s.w * s.w;
+            }
+        }
+    }
+    sq = xpa_wave_sum(sq);
+    if (lane == 0) s_red[w] = sq;
+    __syncthreads();   // also orders the gradient stores before the Adam pass's reads
+    if (t == 0) {
+        double s = 0.0;
+        for (int i = 0; i < kSmWaves; ++i) s += s_red[i];
+        const float total = (float)sqrt(s);
+        float coef = 1.0f;
+        if (a.max_norm >= 0.f) coef = fminf(a.max_norm / (total + 1e-6f), 1.0f);
+        s_coef = coef;
+        if (a.total_norm_out) *a.total_norm_out = total;
+        int k = a.cursor[0];
+        if (k >= a.n_sched) {
+            a.cursor[2] = 1;
+            k = a.n_sched - 1;
+        }
+        s_step = a.sched[2 * k];
+        s_inv = a.sched[2 * k + 1];
+    }
+    __syncthreads();
+    const float coef = s_coef, step_size = s_step, inv_bc2_sqrt = s_inv;
+    const float b1 = a.beta1, b2 = a.beta2, eps = a.eps;
+    for (int64_t i0 = t; i0 < n4; i0 += 4 * kSmThreads) {
+        float4 P[4], Gr[4], M[4], V[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = i0 + u * kSmThreads < n4 ? i0 + u * kSmThreads : n4 - 1;
+            P[u] = p4[i];
+            Gr[u] = g4[i];
+            M[u] = m4[i];
+            V[u] = v4[i];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float *pp = &P[u].x, *gg = &Gr[u].x, *mm = &M[u].x, *vv = &V[u].x;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                float g = gg[c] * coef, m = mm[c], v = vv[c];
+                m = m + (1.0f - b1) * (g - m);
+                v = b2 * v + (1.0f - b2) * g * g;
+                const float denom = sqrtf(v) * inv_bc2_sqrt + eps;
+                pp[c] = pp[c] - step_size * (m / denom);
+                gg[c] = g;
+                mm[c] = m;
+                vv[c] = v;
+            }
+            if (i0 + u * kSmThreads < n4) {
+                const int64_t i = i0 + u * kSmThreads;
+                p4[i] = P[u];
+                g4[i] = Gr[u];
+                m4[i] = M[u];
+                v4[i] = V[u];
+            }
+        }
+    }
+    if (t == 0) a.cursor[0] = a.cursor[0] + 1;
+}
+
 }  // namespace
 
 XPA_API int64_t xpa_small_mlp_lds_floats(int64_t batch, int64_t d_in, int64_t h0, int64_t h1, int64_t h2, int64_t k) {
     const int64_t BP = (batch + 31) & ~31, S = BP + 4, DP = (d_in + 3) & ~3, KP = (k + 3) & ~3;
-    return DP * S + (h0 + h1 + h2) * S + KP * S + 4 * S + DP * h0 + h0 * h1 + h0 * h2 + h1 * KP + h2 + h0 + h1 + h2 +
+    return DP * S + (h0 + h1 + h2) * S + KP * S + 4 * S + DP * h0 + h0 * (h1 + 1) + h0 * (h2 + 1) + h1 * KP + h2 + h0 +
+           h1 + h2 +
            KP + 4 + 4 * BP + BP * KP + BP;
 }
 
@@ -623,9 +782,13 @@ XPA_API int xpa_small_mlp_update(const XpaSmallMlpArgs *args, xpa_stream_t strea
         !a.gba || !a.gWc || !a.gbc || a.n % 4 ||
         ((uintptr_t)a.param | (uintptr_t)a.grad | (uintptr_t)a.exp_avg | (uintptr_t)a.exp_avg_sq) % 16)
         return (int)hipErrorInvalidValue;
-    if (xpa_small_mlp_lds_floats(a.batch, a.d_in, a.h0, a.h1, a.h2, a.k) > kSmLds) return (int)hipErrorInvalidValue;
+    const int G = a.n_groups < 1 ? 1 : a.n_groups;
+    if (G > 1 && (G > 16 || G != (a.batch + 31) / 32 || !a.grad_part || !a.loss_part || (uintptr_t)a.grad_part % 16))
+        return (int)hipErrorInvalidValue;
+    if (xpa_small_mlp_lds_floats(G > 1 ? 32 : a.batch, a.d_in, a.h0, a.h1, a.h2, a.k) > kSmLds)
+        return (int)hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
-#define XPA_SM(A_, G_) hipLaunchKernelGGL((small_mlp_update_kernel<A_, G_>), dim3(1), dim3(kSmThreads), 0, s, a)
+#define XPA_SM(A_, G_) hipLaunchKernelGGL((small_mlp_update_kernel<A_, G_>), dim3(G), dim3(kSmThreads), 0, s, a)
     if (a.algo == XPA_ALGO_PPO) {
         if (a.act_code == 0) XPA_SM(0, XPA_ALGO_PPO);
         else if (a.act_code == 1) XPA_SM(1, XPA_ALGO_PPO);
@@ -636,5 +799,11 @@ XPA_API int xpa_small_mlp_update(const XpaSmallMlpArgs *args, xpa_stream_t strea
         else XPA_SM(2, XPA_ALGO_A2C);
     }
 #undef XPA_SM
+    if (G > 1) {
+        if (a.algo == XPA_ALGO_PPO)
+            hipLaunchKernelGGL((small_mlp_finalize_kernel<XPA_ALGO_PPO>), dim3(1), dim3(kSmThreads), 0, s, a);
+        else
+            hipLaunchKernelGGL((small_mlp_finalize_kernel<XPA_ALGO_A2C>), dim3(1), dim3(kSmThreads), 0, s, a);
+    }
     return xpa_launch_status();
 }

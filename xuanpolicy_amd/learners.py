@@ -304,7 +304,8 @@ class _FusedPolicyGradient(Learner):
         if any(h % 32 or h > 256 for h in (h0, h1, h2)) or not 2 <= k <= 16 or l0.in_features != obs_flat.shape[1] \
                 or l0.in_features > 32:
             return False
-        return int(ops.lib().xpa_small_mlp_lds_floats(batch, l0.in_features, h0, h1, h2, k)) <= 40704
+        rows = 32 if getattr(self, "small_split", True) and 32 < batch <= 512 else batch   # per workgroup
+        return int(ops.lib().xpa_small_mlp_lds_floats(rows, l0.in_features, h0, h1, h2, k)) <= 40704
 
     def _small_launch(self, obs_flat, idx, act, adv, ret, old_logp, use_advnorm, scalars=None):
         """One K30 launch (capturable): reads lr / Adam step at the schedule cursor and advances it.  scalars: the
@@ -343,6 +344,16 @@ class _FusedPolicyGradient(Learner):
         a.scalars, a.total_norm_out = out.data_ptr(), fused.total_norm.data_ptr()
         st = getattr(self, "small_stamps", None)   # diagnostics: int64 [16] of phase timestamps (tools/k30_stamps.py)
         a.stamps = st.data_ptr() if st is not None else None
+        # split form: one workgroup per 32 minibatch rows + a finalize launch (small_split = False: one workgroup)
+        B = idx.shape[0]
+        G = (B + 31) // 32 if getattr(self, "small_split", True) and 32 < B <= 512 else 1
+        a.n_groups = G
+        if G > 1:
+            ws = self.__dict__.setdefault("_small_split_ws", {})
+            if G not in ws:   # zero-filled once: elements no gradient view covers stay 0
+                ws[G] = (torch.zeros((G, fused.fs.numel), dtype=torch.float32, device=obs_flat.device),
+                         torch.zeros((G, 8), dtype=torch.float64, device=obs_flat.device))
+            a.grad_part, a.loss_part = ws[G][0].data_ptr(), ws[G][1].data_ptr()
         _lib.check(ops.lib().xpa_small_mlp_update(ctypes.byref(a), ops._stream(obs_flat.device)),
                    "xpa_small_mlp_update")
         return out
