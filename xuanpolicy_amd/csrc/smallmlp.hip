@@ -673,39 +673,94 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_finalize_kernel(XpaSm
     const float4 *part4 = reinterpret_cast<const float4 *>(a.grad_part);
     float4 *p4 = reinterpret_cast<float4 *>(a.param), *g4 = reinterpret_cast<float4 *>(a.grad);
     float4 *m4 = reinterpret_cast<float4 *>(a.exp_avg), *v4 = reinterpret_cast<float4 *>(a.exp_avg_sq);
+    const float b1 = a.beta1, b2 = a.beta2, eps = a.eps;
+    // Adam's element update (K9's arithmetic): gg is the unclipped gradient in, the clipped one out
+    auto adam4 = [&](float4 &P, float4 &Gr, float4 &M, float4 &V, float coef, float step_size, float inv_bc2_sqrt) {
+        float *pp = &P.x, *gg = &Gr.x, *mm = &M.x, *vv = &V.x;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = gg[c] * coef, m = mm[c], v = vv[c];
+            m = m + (1.0f - b1) * (g - m);
+            v = b2 * v + (1.0f - b2) * g * g;
+            const float denom = sqrtf(v) * inv_bc2_sqrt + eps;
+            pp[c] = pp[c] - step_size * (m / denom);
+            gg[c] = g;
+            mm[c] = m;
+            vv[c] = v;
+        }
+    };
+    // Every element's partials, parameter and moments loaded in ONE round trip before the norm (the norm only scales
+    // the gradient): up to kFinJ float4 elements per thread held in registers.
+    constexpr int kFinJ = 6;
+    const bool regs = n4 <= (int64_t)kFinJ * kSmThreads && G <= 4;
     double sq = 0.0;
-    for (int64_t i0 = t; i0 < n4; i0 += 2 * kSmThreads) {
-        float4 P[2][16];
+    float4 Sg[kFinJ], Pp[kFinJ], Mm[kFinJ], Vv[kFinJ];
+    if (regs) {
+        float4 Q[kFinJ][4];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int64_t i = i0 + u * kSmThreads < n4 ? i0 + u * kSmThreads : n4 - 1;
+        for (int j = 0; j < kFinJ; ++j) {
+            const int64_t i0 = t + (int64_t)j * kSmThreads;
+            const int64_t i = i0 < n4 ? i0 : n4 - 1;
 #pragma unroll
-            for (int g = 0; g < 16; ++g)
-                if (g < G) P[u][g] = part4[(int64_t)g * n4 + i];
+            for (int g = 0; g < 4; ++g)
+                if (g < G) Q[j][g] = part4[(int64_t)g * n4 + i];
+            Pp[j] = p4[i];
+            Mm[j] = m4[i];
+            Vv[j] = v4[i];
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            float4 s = P[u][0];
+        for (int j = 0; j < kFinJ; ++j) {
+            float4 sg = Q[j][0];
 #pragma unroll
-            for (int g = 1; g < 16; ++g)
+            for (int g = 1; g < 4; ++g)
                 if (g < G) {
-                    s.x += P[u][g].x;
-                    s.y += P[u][g].y;
-                    s.z += P[u][g].z;
-                    s.w += P[u][g].w;
+                    sg.x += Q[j][g].x;
+                    sg.y += Q[j][g].y;
+                    sg.z += Q[j][g].z;
+                    sg.w += Q[j][g].w;
                 }
-            if (i0 + u * kSmThreads < n4) {
-                g4[i0 + u * kSmThreads] = s;
-                sq += (double)s.x * s.x;
-                sq += (double)s.y * s.y;
-                sq += (double)s.z * s.z;
-                sq += (double)s.w * s.w;
+            Sg[j] = sg;
+            if (t + (int64_t)j * kSmThreads < n4) {
+                sq += (double)sg.x * sg.x;
+                sq += (double)sg.y * sg.y;
+                sq += (double)sg.z * sg.z;
+                sq += (double)sg.w * sg.w;
+            }
+        }
+    } else {
+        for (int64_t i0 = t; i0 < n4; i0 += 2 * kSmThreads) {
+            float4 P[2][16];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int64_t i = i0 + u * kSmThreads < n4 ? i0 + u * kSmThreads : n4 - 1;
+#pragma unroll
+                for (int g = 0; g < 16; ++g)
+                    if (g < G) P[u][g] = part4[(int64_t)g * n4 + i];
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                float4 sg = P[u][0];
+#pragma unroll
+                for (int g = 1; g < 16; ++g)
+                    if (g < G) {
+                        sg.x += P[u][g].x;
+                        sg.y += P[u][g].y;
+                        sg.z += P[u][g].z;
+                        sg.w += P[u][g].w;
+                    }
+                if (i0 + u * kSmThreads < n4) {
+                    g4[i0 + u * kSmThreads] = sg;
+                    sq += (double)sg.x * sg.x;
+                    sq += (double)sg.y * sg.y;
+                    sq += (double)sg.z * sg.z;
+                    sq += (double)sg.w * sg.w;
+                }
             }
         }
     }
     sq = xpa_wave_sum(sq);
     if (lane == 0) s_red[w] = sq;
-    __syncthreads();   // also orders the gradient stores before the Adam pass's reads
+    __syncthreads();   // also orders the two-pass form's gradient stores before its Adam pass's reads
     if (t == 0) {
         double s = 0.0;
         for (int i = 0; i < kSmWaves; ++i) s += s_red[i];
@@ -724,37 +779,39 @@ __global__ __launch_bounds__(kSmThreads, 1) void small_mlp_finalize_kernel(XpaSm
     }
     __syncthreads();
     const float coef = s_coef, step_size = s_step, inv_bc2_sqrt = s_inv;
-    const float b1 = a.beta1, b2 = a.beta2, eps = a.eps;
-    for (int64_t i0 = t; i0 < n4; i0 += 4 * kSmThreads) {
-        float4 P[4], Gr[4], M[4], V[4];
+    if (regs) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int64_t i = i0 + u * kSmThreads < n4 ? i0 + u * kSmThreads : n4 - 1;
-            P[u] = p4[i];
-            Gr[u] = g4[i];
-            M[u] = m4[i];
-            V[u] = v4[i];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            float *pp = &P[u].x, *gg = &Gr[u].x, *mm = &M[u].x, *vv = &V[u].x;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                float g = gg[c] * coef, m = mm[c], v = vv[c];
-                m = m + (1.0f - b1) * (g - m);
-                v = b2 * v + (1.0f - b2) * g * g;
-                const float denom = sqrtf(v) * inv_bc2_sqrt + eps;
-                pp[c] = pp[c] - step_size * (m / denom);
-                gg[c] = g;
-                mm[c] = m;
-                vv[c] = v;
+        for (int j = 0; j < kFinJ; ++j) {
+            const int64_t i = t + (int64_t)j * kSmThreads;
+            adam4(Pp[j], Sg[j], Mm[j], Vv[j], coef, step_size, inv_bc2_sqrt);
+            if (i < n4) {
+                p4[i] = Pp[j];
+                g4[i] = Sg[j];
+                m4[i] = Mm[j];
+                v4[i] = Vv[j];
             }
-            if (i0 + u * kSmThreads < n4) {
-                const int64_t i = i0 + u * kSmThreads;
-                p4[i] = P[u];
-                g4[i] = Gr[u];
-                m4[i] = M[u];
-                v4[i] = V[u];
+        }
+    } else {
+        for (int64_t i0 = t; i0 < n4; i0 += 4 * kSmThreads) {
+            float4 P[4], Gr[4], M[4], V[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t i = i0 + u * kSmThreads < n4 ? i0 + u * kSmThreads : n4 - 1;
+                P[u] = p4[i];
+                Gr[u] = g4[i];
+                M[u] = m4[i];
+                V[u] = v4[i];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                adam4(P[u], Gr[u], M[u], V[u], coef, step_size, inv_bc2_sqrt);
+                if (i0 + u * kSmThreads < n4) {
+                    const int64_t i = i0 + u * kSmThreads;
+                    p4[i] = P[u];
+                    g4[i] = Gr[u];
+                    m4[i] = M[u];
+                    v4[i] = V[u];
+                }
             }
         }
     }
