@@ -216,8 +216,9 @@ def test_small_mlp_epoch_graphs_match_eager(n_steps, n_mb):
         np.testing.assert_array_equal(b, a)
 
 
-@pytest.mark.parametrize("agent_name", ["PPO_Clip", "A2C"])
-def test_fused_rollout_matches_multi_kernel_steps(agent_name):
+@pytest.mark.parametrize("agent_name,hidden,obsnorm", [("PPO_Clip", 64, True), ("A2C", 64, True), ("PPO_Clip", 32, True),
+                                                       ("PPO_Clip", 64, False)])
+def test_fused_rollout_matches_multi_kernel_steps(agent_name, hidden, obsnorm):
     """K32 (xpa_small_rollout_cartpole: obs RMS + normalise + MLP forward + sample + CartPole step + K8 post in one
     launch) against the multi-kernel step (K5, obs_normalize, the torch forward, K3, K18, K8) from the same start:
     iteration 1's 128 steps as ONE K32 launch, then an update, then 127 single-step launches (time limit 40: mid-buffer
@@ -227,8 +228,8 @@ def test_fused_rollout_matches_multi_kernel_steps(agent_name):
     from xuanpolicy_amd.runner import build_cartpole_ppo
     res = []
     for fused in (True, False):
-        agent = build_cartpole_ppo(n_envs=8, n_steps=128, hidden=64, seed=9, device=DEV, max_episode_steps=40,
-                                   agent=agent_name, fused_rollout=fused, clip_grad=0.5)
+        agent = build_cartpole_ppo(n_envs=8, n_steps=128, hidden=hidden, seed=9, device=DEV, max_episode_steps=40,
+                                   agent=agent_name, fused_rollout=fused, clip_grad=0.5, use_obsnorm=obsnorm)
         assert agent.defer_boot and agent.n_slots == 4
         agent.train(128 + 127, log=False)
         torch.cuda.synchronize()
