@@ -312,7 +312,8 @@ class _OnPolicyAgent:
         None.  Rebuilt when the parameters are re-homed (the block holds their pointers)."""
         if not self.fused_rollout or not self.device_env or self.device.type != "cuda":
             return None
-        key = tuple(p.data_ptr() for p in self.policy.parameters())
+        key = tuple(p.data_ptr() for p in self.policy.parameters()) + (self.memory.observations.data_ptr(),
+                                                                      self.memory.actions.data_ptr())
         if self._k32_key != key:
             self._k32_key, self._k32 = key, self._build_small_rollout()
         return self._k32
