@@ -162,11 +162,22 @@ __global__ __launch_bounds__(kRmsThreads) void rms_partials_kernel(const float *
         double s = 0.0, q = 0.0;
         if (gsub < groups) {
             const float sh = shift ? shift[c0 + c] : 0.f;
-#pragma unroll 4
-            for (int64_t r = r0 + gsub; r < r1; r += groups) {
-                const double v = (double)x[r * ld + c0 + c] - (double)sh;
-                s += v;
-                q += v * v;
+            // 16 rows' loads issued before their (in-order) accumulation: one memory round trip per 16 rows (the
+            // unroll-4 loop waited once per 4 rows: ~5 serial HBM round trips per thread at C2's 17 columns)
+            for (int64_t rb = r0 + gsub; rb < r1; rb += 16 * (int64_t)groups) {
+                float xv[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int64_t r = rb + (int64_t)u * groups;
+                    xv[u] = x[(r < r1 ? r : rb) * ld + c0 + c];
+                }
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (rb + (int64_t)u * groups < r1) {
+                        const double v = (double)xv[u] - (double)sh;
+                        s += v;
+                        q += v * v;
+                    }
             }
         }
         s_sum[threadIdx.x] = s;

@@ -142,11 +142,17 @@ __global__ __launch_bounds__(256) void thin_fwd_norm_kernel(const float *__restr
         const int64_t r0 = tile * TILE;
         __syncthreads();
         for (int i = t; i < TILE * DMAX; i += 256) {
+            // loads unconditional from clamped addresses (under the validity branch hipcc waited for them at the
+            // join, after the weight loads: two serial round trips per tile)
             const int r = i / DMAX, k = i - r * DMAX;
+            const bool ok = k < din && r0 + r < rows;
+            const int kc = k < din ? k : 0;
+            const int64_t rc = r0 + r < rows ? r0 + r : r0;
+            const float xv = x[rc * ldx + kc], mv = mean[kc], vv = var[kc];
             float y = 0.f;
-            if (k < din && r0 + r < rows) {
-                const float sd = sqrtf(var[k]);
-                y = (x[(r0 + r) * ldx + k] - mean[k]) / (sd + 1e-8f);
+            if (ok) {
+                const float sd = sqrtf(vv);
+                y = (xv - mv) / (sd + 1e-8f);
                 y = fminf(fmaxf(y, -clip), clip);
                 xn[(r0 + r) * ldn + k] = y;
                 if (col) col[(r0 + r) * col_ld + coff + k] = y;
