@@ -712,14 +712,16 @@ __host__ __device__ constexpr int ro_r4(int x) { return (x + 3) & ~3; }
 struct RoLayout {
     int sy, sz, sbo, total;
 };
-// sy: the normalised observations [N][4]; sz: the output layers' partial sums [unit wave][N][K + 1]; sbo: biases
+// sy: the normalised observations [N][4]; sz: the output layers' partial sums [wave][N][K + 1]; sbo: biases
 __host__ __device__ inline RoLayout ro_layout(int N, int D, int H0, int H1, int H2, int K) {
     RoLayout l;
-    const int K1 = K + 1, WU = (H1 + H2 + 63) / 64;
+    const int K1 = K + 1;
     (void)H0;
+    (void)H1;
+    (void)H2;
     l.sy = 0;
     l.sz = ro_r4(N * D);
-    l.sbo = ro_r4(l.sz + WU * N * K1);
+    l.sbo = ro_r4(l.sz + 4 * N * K1);
     l.total = ro_r4(l.sbo + K1);
     return l;
 }
@@ -740,6 +742,16 @@ __device__ __forceinline__ float ro_wave_sum63(float v) {
     v += ro_dpp<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3
     return v;
 }
+
+// Sum over the 16 lanes of each DPP row (every lane gets its row's sum).
+__device__ __forceinline__ float ro_row_sum16(float v) {
+    v += ro_dpp<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+    v += ro_dpp<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+    v += ro_dpp<0x141>(v);  // row_half_mirror: sums of 8
+    v += ro_dpp<0x140>(v);  // row_mirror: sums of 16
+    return v;
+}
+typedef float ro_f32x4 __attribute__((ext_vector_type(4)));
 
 // K8's f64 wave butterfly (xpa_wave_sum) when only lanes [0, n) hold values (the rest +0): the steps whose partner
 // lanes are all empty add +0 and are skipped.
@@ -775,30 +787,38 @@ __global__ __launch_bounds__(kRoThreads) void small_rollout_cartpole_kernel(XpaS
                              a.ep_last_score, a.ep_last_len, a.env_seed, a.max_episode_steps,
                              cartpole::kThetaThreshold};
     if (tid < K1) sbo[tid] = tid < K ? a.ba[tid] : a.bc[0];
-    // The forward runs inside each wave with no LDS round trip: a wave owns 64 consecutive units of the actor |
-    // critic hidden layers (unit wave wu) for every RG-th row; lane k first forms h0[r][k] itself (the
-    // representation layer, recomputed by the WU waves sharing a row), then the hidden layer reads h0 through
-    // v_readlane (an SGPR broadcast) against the lane's weight row in VGPRs, and the output layers are wave sums.
+    // The forward on v_mfma_f32_16x16x4_f32: [16-row tile of envs] x [actor | critic hidden units], K = h0.  Wave w
+    // owns the unit tiles w and w + 4 (16 units each) with their weight rows in VGPRs (B operand, loaded once per
+    // launch); lane (q, i) forms the A operand itself — h0[row i][4 kk + q] of the representation layer, from the
+    // normalised row in LDS — so h0 never goes through LDS; the output layers are per-lane partial dot products over
+    // the lane's units, summed over the 16 lanes of a DPP row and then over the waves (LDS, fixed order).
     const int wave = tid >> 6, lane = tid & 63;
-    const int WU = (U + 63) >> 6, RG = 4 / WU;
-    const int wu = wave % WU, rg = wave / WU;
-    const int u = wu * 64 + lane;
-    const bool uok = u < U && rg < RG;
-    const bool actor = u < H1;
-    const int l0 = lane < H0 ? lane : 0;
-    const float4 w0 = make_float4(a.W0[l0 * D], a.W0[l0 * D + 1], a.W0[l0 * D + 2], a.W0[l0 * D + 3]);
-    const float b0u = a.b0[l0];
-    const int uc = uok ? u : 0;
-    const float *wr = actor ? a.W1 + uc * H0 : a.W2 + (uc - H1) * H0;
-    float w1[H0];
+    const int li = lane & 15, lq = lane >> 4;
+    constexpr int KK = H0 / 4;
+    const int UT = U >> 4;   // unit tiles (4, 6 or 8)
+    float4 w0k[KK];
+    float b0k[KK];
 #pragma unroll
-    for (int k = 0; k < H0; ++k) w1[k] = uok ? wr[k] : 0.f;
-    const float b12 = uok ? (actor ? a.b1[uc] : a.b2[uc - H1]) : 0.f;
-    // this lane's output-layer weights: wo[o] for the K logits (actor units) or the value (critic units)
-    float wo[3];
+    for (int kk = 0; kk < KK; ++kk) {
+        const int k = 4 * kk + lq;
+        w0k[kk] = make_float4(a.W0[k * D], a.W0[k * D + 1], a.W0[k * D + 2], a.W0[k * D + 3]);
+        b0k[kk] = a.b0[k];
+    }
+    float bw[2][KK], b12[2], wo[2][3];
 #pragma unroll
-    for (int o = 0; o < 3; ++o)
-        wo[o] = !uok || o >= K1 ? 0.f : (o < K ? (actor ? a.Wa[o * H1 + uc] : 0.f) : (actor ? 0.f : a.Wc[uc - H1]));
+    for (int j = 0; j < 2; ++j) {
+        const int tile = wave + 4 * j;
+        const bool tok = tile < UT;
+        const int u = tok ? 16 * tile + li : 0;
+        const bool actor = u < H1;
+        const float *wr = actor ? a.W1 + u * H0 : a.W2 + (u - H1) * H0;
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) bw[j][kk] = tok ? wr[4 * kk + lq] : 0.f;
+        b12[j] = tok ? (actor ? a.b1[u] : a.b2[u - H1]) : 0.f;
+#pragma unroll
+        for (int o = 0; o < 3; ++o)
+            wo[j][o] = !tok || o >= K1 ? 0.f : (o < K ? (actor ? a.Wa[o * H1 + u] : 0.f) : (actor ? 0.f : a.Wc[u - H1]));
+    }
 
     // state that lives across the steps of the launch: each env's CartPole state and running return (thread n),
     // the raw observations and obs statistics (LDS), the obs count (every thread), the return statistics (thread 0)
@@ -907,45 +927,44 @@ __global__ __launch_bounds__(kRoThreads) void small_rollout_cartpole_kernel(XpaS
         }
         __syncthreads();
         XPA_RO_STAMP(1);
-        // (c)-(e) the forward, four rows per pass
-        for (int r0 = rg; r0 < N && rg < RG; r0 += 4 * RG) {
-            float h0[4], acc[4];
+        // (c)-(e) the forward, one 16-row tile of envs at a time
+        for (int r0 = 0; r0 < N; r0 += 16) {
+            const int ra = r0 + li < N ? r0 + li : N - 1;   // this lane's A row (rows past N: results unused)
+            const float4 y = *reinterpret_cast<const float4 *>(sy + ra * D);
+            float av[KK];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int r = r0 + j * RG;
-                const float4 y = *reinterpret_cast<const float4 *>(sy + (r < N ? r : r0) * D);
-                float z = b0u;
-                z = fmaf(w0.x, y.x, z);
-                z = fmaf(w0.y, y.y, z);
-                z = fmaf(w0.z, y.z, z);
-                z = fmaf(w0.w, y.w, z);
-                h0[j] = ro_act<ACT>(z, a.slope);
-                acc[j] = b12;
+            for (int kk = 0; kk < KK; ++kk) {
+                float z = b0k[kk];
+                z = fmaf(w0k[kk].x, y.x, z);
+                z = fmaf(w0k[kk].y, y.y, z);
+                z = fmaf(w0k[kk].z, y.z, z);
+                z = fmaf(w0k[kk].w, y.w, z);
+                av[kk] = ro_act<ACT>(z, a.slope);
             }
+            ro_f32x4 acc[2];
 #pragma unroll
-            for (int k = 0; k < H0; ++k)
+            for (int j = 0; j < 2; ++j) acc[j] = ro_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float hk = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, h0[j]), k));
-                    acc[j] = fmaf(w1[k], hk, acc[j]);
-                }
+            for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], bw[j][kk], acc[j], 0, 0, 0);
+            // D element r of lane (q, i): row r0 + 4 q + r, unit 16 tile + i
             float part[4][3];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float h = ro_act<ACT>(acc[j], a.slope);
+            for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int o = 0; o < 3; ++o) part[j][o] = wo[o] * h;
-            }
+                for (int o = 0; o < 3; ++o) {
+                    float pv = 0.f;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+                    for (int j = 0; j < 2; ++j) pv = fmaf(wo[j][o], ro_act<ACT>(acc[j][r] + b12[j], a.slope), pv);
+                    part[r][o] = ro_row_sum16(pv);
+                }
+            if (li == 0)
 #pragma unroll
-                for (int o = 0; o < 3; ++o) part[j][o] = ro_wave_sum63(part[j][o]);
-            if (lane == 63)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int r = r0 + j * RG;
-                    if (r < N)
-                        for (int o = 0; o < K1; ++o) sz[(wu * N + r) * K1 + o] = part[j][o];
+                for (int r = 0; r < 4; ++r) {
+                    const int m = r0 + 4 * lq + r;
+                    if (m < N)
+                        for (int o = 0; o < K1; ++o) sz[(wave * N + m) * K1 + o] = part[r][o];
                 }
         }
         __syncthreads();
@@ -956,7 +975,7 @@ __global__ __launch_bounds__(kRoThreads) void small_rollout_cartpole_kernel(XpaS
             float z[3];
             for (int o = 0; o < K1; ++o) {
                 float v = sbo[o];
-                for (int w = 0; w < WU; ++w) v += sz[(w * N + tid) * K1 + o];
+                for (int w = 0; w < 4; ++w) v += sz[(w * N + tid) * K1 + o];
                 z[o] = v;
             }
             const int pick = cat_sample_store_at(tid, K, T, t, step, z, z[K], a.seed, a.buf_act, a.buf_logp,
