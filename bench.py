@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--gae-form", choices=("value", "split"), default="value",
                    help="value: the deferred bootstraps' value head fused into the GAE scan (K1V, one launch); "
                         "split: value head (K14) then the compact GAE scan (K1)")
+    p.add_argument("--trunk-heads", choices=("on", "off"), default="on",
+                   help="K16X (trunk layer inside the head GEMM launches) or r03's K13 forward + K16 (A/B)")
     p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc HBM-traffic passes")
     p.add_argument("--no-rocprof", action="store_true",
                    help="skip the child rocprofv3 --kernel-trace run that times the in-loop GAE launches")
@@ -787,6 +789,9 @@ def main():
                                shard=rank)
     agent.learner.enable_fast_path()  # flat params/grads, fused clip+Adam, RCCL hook when world > 1
     agent.fuse_value_gae = args.gae_form == "value"
+    fm0 = agent.learner._fused_mlp()
+    if fm0 is not None:
+        fm0.use_trunk_heads = args.trunk_heads == "on"
     if world > 1:
         broadcast_parameters(agent.policy)
 
@@ -906,9 +911,14 @@ def main():
         update_kernels = {}
         if heads_ms and getattr(agent.learner._fused_mlp(), "gemm_heads", False):
             fl = pair_gemm_flops(B, args.hidden, args.hidden)
+            fmh = agent.learner._fused_mlp()
+            trunk = fmh.trunk_heads and fmh.use_trunk_heads
             update_kernels["heads"] = {
-                "kernel": "xpa_head_gemm_actor + xpa_head_gemm_critic (K16: hidden-layer GEMM on fp32 MFMA "
-                          "+ fused head epilogue, per minibatch)", "bound": "mfma",
+                "kernel": ("xpa_head_gemm_trunk_actor + xpa_head_gemm_trunk_critic (K16X: trunk layer + hidden-layer "
+                           "GEMM on fp32 MFMA + fused head epilogue, per minibatch; FLOP counted: the hidden GEMMs)"
+                           if trunk else
+                           "xpa_head_gemm_actor + xpa_head_gemm_critic (K16: hidden-layer GEMM on fp32 MFMA "
+                           "+ fused head epilogue, per minibatch)"), "bound": "mfma",
                 "avg_us": round(heads_ms * 1e3, 3), "flops": fl, "achieved": round(fl / heads_ms / 1e9, 1),
                 "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(fl / heads_ms / 1e9 / FP32_MFMA_PEAK_TFLOPS, 4), "launches": ops.TIMER.count("heads"),

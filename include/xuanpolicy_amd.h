@@ -489,6 +489,26 @@ int xpa_head_gemm_critic(int act, int64_t batch, int64_t hidden, const float *x,
                          float *partial_dw, float *partial_db_hidden, float *partial_db_out, float *loss_partials,
                          int64_t loss_width, xpa_stream_t stream);
 
+/* K16X — K16 with the representation's first layer Linear(d_in <= 20, 256) + activation `act` (K13's, bit for bit)
+ * in the prologue: the h tile is formed in LDS from the minibatch's gathered observation rows x_rows [batch, d_in]
+ * (row stride ld_rows; e.g. xpa_thin_linear_act_fwd_gather with h = NULL), w_in [256, d_in], b_in [256], and
+ * feeds the hidden GEMM straight from LDS.  h_out (may be NULL; row stride ld_h) receives h for the backward (the
+ * actor writes it, the critic recomputes it).  Otherwise exactly K16 (act_dim <= 8). */
+int xpa_head_gemm_trunk_actor(int algo, int dist, int act, int64_t batch, int64_t act_dim, int64_t hidden,
+                              const float *x_rows, int64_t ld_rows, int64_t d_in, const float *w_in, const float *b_in,
+                              float slope_in, float *h_out, int64_t ld_h, const float *w_hidden, const float *b_hidden,
+                              int64_t ld_dz, const float *w, const float *b, float slope, const float *logstd,
+                              const int64_t *idx, int64_t n_rows, const float *act_buf, const float *old_logp,
+                              const float *adv, const double *adv_partials, int64_t n_adv_partials, float clip_range,
+                              float ent_coef, float *dz, float *partial_dw, float *partial_db_hidden,
+                              float *partial_db_out, float *loss_partials, int64_t loss_width, xpa_stream_t stream);
+int xpa_head_gemm_trunk_critic(int act, int64_t batch, int64_t hidden, const float *x_rows, int64_t ld_rows,
+                               int64_t d_in, const float *w_in, const float *b_in, float slope_in, float *h_out,
+                               int64_t ld_h, const float *w_hidden, const float *b_hidden, int64_t ld_dz, const float *w,
+                               const float *b, float slope, const int64_t *idx, int64_t n_rows, const float *ret,
+                               float vf_coef, float *dz, float *partial_dw, float *partial_db_hidden,
+                               float *partial_db_out, float *loss_partials, int64_t loss_width, xpa_stream_t stream);
+
 /* K6 — prioritized replay (PerOffPolicyBuffer, memory_tools.py:369-492; Sum/MinSegmentTree,
  * segtree_tool.py:4-86) with f64 trees on device: one [n_envs, 2*capacity] array per tree (node 1 =
  * root, leaf i at capacity + i; neutral 0 / +inf), capacity = next power of two >= n_size.

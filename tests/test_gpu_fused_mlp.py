@@ -574,3 +574,94 @@ def test_thin_gather_forms_equal_k4_then_k13(rows, n_rows, din):
     _lib.check(L.xpa_thin_linear_act_bwd_gather(1, ops._p(gr), 256, ops._p(h), 256, rows, ops._p(flat), din, n_rows,
                                                 ops._p(idx), din, 256, 0.01, ops._p(pw2), ops._p(pb2), st), "bwd_gather")
     assert torch.equal(pw, pw2) and torch.equal(pb, pb2)
+
+
+@pytest.mark.parametrize("algo,dist,K,B,code,din", [
+    ("ppo", "gaussian", 6, 4133, 1, 17),    # the C2 head and trunk widths, ragged tail (4133 = 64 * 64 + 37)
+    ("a2c", "categorical", 4, 777, 0, 4),
+    ("ppo", "categorical", 8, 193, 2, 20),
+    ("a2c", "gaussian", 6, 64, 1, 17),
+])
+def test_head_gemm_trunk_kernels_equal_k13_then_k16(algo, dist, K, B, code, din):
+    """K16X (xpa_head_gemm_trunk_actor / _critic: the trunk layer Linear(d_in, 256) + act formed in the prologue)
+    against K13 (xpa_thin_linear_act_fwd) followed by K16 on the same inputs: the h the actor writes is K13's bit for
+    bit (same fmaf chain); dz, every per-block partial and the loss partials equal K16's up to the hidden GEMM's
+    summation order (the MFMA k order differs: rel 2e-5, the K16-vs-fp64 tolerance); canaries around h, dz and the
+    partials.  Rows whose hidden pre-activation sits within rounding of an activation kink are masked (either
+    branch is right there)."""
+    from xuanpolicy_amd import ops
+    L, s = ops.lib(), ops._stream()
+    g = torch.Generator(device=DEV).manual_seed(B + K + din)
+    H, R = 256, B + 300
+    slope = 0.01
+    xr = torch.randn(B, din, device=DEV, generator=g)
+    w0 = torch.randn(H, din, device=DEV, generator=g) / 4
+    b0 = torch.randn(H, device=DEV, generator=g) * 0.1
+    wh_a, wh_c = (torch.randn(H, H, device=DEV, generator=g) / 16 for _ in range(2))
+    bh_a, bh_c = (torch.randn(H, device=DEV, generator=g) * 0.1 for _ in range(2))
+    w_a = torch.randn(K, H, device=DEV, generator=g) / 16
+    b_a = torch.randn(K, device=DEV, generator=g) * 0.1
+    w_c = torch.randn(1, H, device=DEV, generator=g) / 16
+    b_c = torch.randn(1, device=DEV, generator=g) * 0.1
+    logstd = (-1 + 0.1 * torch.randn(K, device=DEV, generator=g)) if dist == "gaussian" else None
+    idx = torch.randperm(R, device=DEV, generator=g)[:B].contiguous()
+    idx[B // 2] = -1
+    adv = torch.randn(R, device=DEV, generator=g)
+    ret = torch.randn(R, device=DEV, generator=g)
+    act = (torch.randn(R, K, device=DEV, generator=g) * 0.5 if dist == "gaussian"
+           else torch.randint(0, K, (R,), device=DEV, generator=g).float())
+    old = -1.5 + 0.3 * torch.randn(R, device=DEV, generator=g) if algo == "ppo" else None
+    h_ref = torch.empty(B, H, device=DEV)
+    assert L.xpa_thin_linear_act_fwd(code, ops._p(xr), din, B, din, H, ops._p(w0), ops._p(b0), slope, ops._p(h_ref), H,
+                                     s) == 0
+    if code != 2:
+        with torch.no_grad():
+            near = ((h_ref @ wh_a.t() + bh_a).abs() < 1e-4).any(1) | ((h_ref @ wh_c.t() + bh_c).abs() < 1e-4).any(1)
+        idx[near] = -1
+    G = int(L.xpa_head_fused_num_partials(B))
+    W = int(L.xpa_loss_partial_width(K))
+    pad = 64
+    algo_c, dist_c = ops.ALGO[algo], ops.DIST[dist]
+    ent, clip, vf = 0.01, 0.2, 0.25
+
+    def run(trunk):
+        cz = lambda n, v=555.0: torch.full((n + 2 * pad,), v, device=DEV)   # noqa: E731
+        out = dict(dz=cz(B * 2 * H, 777.0), h=cz(B * H, 333.0), p_dw_a=cz(G * K * H), p_dbh_a=cz(G * H),
+                   p_dbo_a=cz(G * K), p_dw_c=cz(G * H), p_dbh_c=cz(G * H), p_dbo_c=cz(G), lp=cz(G * W))
+        out["lp"][pad:-pad] = 0.0
+        v = lambda k: ops._p(out[k][pad:])   # noqa: E731
+        dz = out["dz"][pad:pad + B * 2 * H].view(B, 2 * H)
+        p_ls = ops._p(logstd) if logstd is not None else None
+        p_old = ops._p(old) if old is not None else None
+        if trunk:
+            assert L.xpa_head_gemm_trunk_actor(
+                algo_c, dist_c, code, B, K, H, ops._p(xr), din, din, ops._p(w0), ops._p(b0), slope, v("h"), H,
+                ops._p(wh_a), ops._p(bh_a), 2 * H, ops._p(w_a), ops._p(b_a), slope, p_ls, ops._p(idx), R, ops._p(act),
+                p_old, ops._p(adv), None, 0, clip, ent, ops._p(dz), v("p_dw_a"), v("p_dbh_a"), v("p_dbo_a"), v("lp"),
+                W, s) == 0
+            assert L.xpa_head_gemm_trunk_critic(
+                code, B, H, ops._p(xr), din, din, ops._p(w0), ops._p(b0), slope, None, H, ops._p(wh_c), ops._p(bh_c),
+                2 * H, ops._p(w_c), ops._p(b_c), slope, ops._p(idx), R, ops._p(ret), vf, ops._p(dz[:, H:]),
+                v("p_dw_c"), v("p_dbh_c"), v("p_dbo_c"), v("lp"), W, s) == 0
+        else:
+            assert L.xpa_head_gemm_actor(algo_c, dist_c, code, B, K, H, ops._p(h_ref), H, ops._p(wh_a), ops._p(bh_a),
+                                         2 * H, ops._p(w_a), ops._p(b_a), slope, p_ls, ops._p(idx), R, ops._p(act),
+                                         p_old, ops._p(adv), None, 0, clip, ent, ops._p(dz), v("p_dw_a"), v("p_dbh_a"),
+                                         v("p_dbo_a"), v("lp"), W, s) == 0
+            assert L.xpa_head_gemm_critic(code, B, H, ops._p(h_ref), H, ops._p(wh_c), ops._p(bh_c), 2 * H,
+                                          ops._p(w_c), ops._p(b_c), slope, ops._p(idx), R, ops._p(ret), vf,
+                                          ops._p(dz[:, H:]), v("p_dw_c"), v("p_dbh_c"), v("p_dbo_c"), v("lp"), W,
+                                          s) == 0
+        torch.cuda.synchronize()
+        for k, t in out.items():
+            fill = {"dz": 777.0, "h": 333.0}.get(k, 555.0)
+            assert bool((t[:pad] == fill).all()) and bool((t[-pad:] == fill).all()), k + " written out of bounds"
+        return {k: t[pad:-pad] for k, t in out.items()}
+
+    ref, got = run(False), run(True)
+    assert torch.equal(got["h"].view(B, H), h_ref), "h differs from K13's"
+    for k in ("dz", "p_dw_a", "p_dbh_a", "p_dbo_a", "p_dw_c", "p_dbh_c", "p_dbo_c", "lp"):
+        a, b = got[k].double(), ref[k].double()
+        scale = b.abs().max().item() + 1e-12
+        err = (a - b).abs().max().item()
+        assert err <= 2e-5 * scale + 1e-9, (k, err, scale)

@@ -196,6 +196,13 @@ SIGNATURES = {
                                            c_f32, c_p, c_p, c_p, c_p, c_p, c_i64, c_p]),
     "xpa_head_gemm_critic": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_f32, c_p,
                                             c_i64, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64, c_p]),
+    "xpa_head_gemm_trunk_actor": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_i64,
+                                                 c_i64, c_p, c_p, c_f32, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_f32, c_p,
+                                                 c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_f32, c_f32, c_p, c_p, c_p, c_p,
+                                                 c_p, c_i64, c_p]),
+    "xpa_head_gemm_trunk_critic": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p, c_f32, c_p,
+                                                  c_i64, c_p, c_p, c_i64, c_p, c_p, c_f32, c_p, c_i64, c_p, c_f32, c_p,
+                                                  c_p, c_p, c_p, c_p, c_i64, c_p]),
     "xpa_grad_norm_num_partials": (c_i64, [c_i64]),
     "xpa_clip_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_p, c_f32, c_f32, c_f32, c_f32, c_f32, c_i64, c_p,
                                           c_p]),

@@ -119,6 +119,12 @@ struct HeadArgs {
     float clip_range, ent_coef, vf_coef;
     float *dz, *p_dw, *p_dbh, *p_dbo, *p_loss;
     int loss_width;
+    // K16X: the trunk's first layer (gathered rows [batch, din] at ldxr, W0 [256, din], b0) and the h output
+    const float *xr, *W0, *b0;
+    int64_t ldxr, ldh;
+    int din;
+    float slope0;
+    float *hout;
 };
 
 __device__ __forceinline__ void load_tile(float4 (&zq)[16], const float *__restrict__ z, int64_t ld, int64_t tile,
@@ -719,6 +725,148 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
     epi.finish(p_dw, p_dbh, p_dbo, p_loss, loss_width);
 }
 
+// K16X (r03): K16 with the representation's first layer (K13's Linear(d_in <= 20, 256) + activation) in its
+// prologue, so the trunk output h is formed in LDS from the minibatch's gathered observation rows and never
+// read back from HBM (the actor launch writes it once, for the hidden layers' dW GEMM and K13's backward; the
+// critic launch recomputes it).  The A operand of the hidden GEMM is then the whole [64 x 256] h tile resident in
+// LDS (row stride kS, the epilogue tile's image), and each wave's B operand — its own 64 rows of Wh, which no
+// other wave of the block reads — goes global (L2) -> VGPRs directly: no operand DMAs, no barrier in the k loop.
+// k loop: 16 chunks of 16 k; lane (i, hh) holds k = k0 + 8 hh + 4 q + s (q < 2, s < 4) of its A row / B row, fed as
+// the MFMA's k = hh at step (q, s) (any k order is exact as long as A and B agree); chunk c + 1's B registers
+// load during chunk c's 32 MFMAs.  h arithmetic: K13's fmaf chain over the zero-padded DMAX inputs, so h is
+// bit for bit thin_fwd_kernel's.
+constexpr int kKC2 = 16;
+constexpr int kChunks2 = kKin / kKC2;
+constexpr int kTrunkDMax = 20;
+
+// lane (i, hh): k = k0 + 8 hh + 4 q + s (q < 2, s < 4) of B rows i (ct = 0) and 32 + i (ct = 1) of the wave's 64
+__device__ __forceinline__ void trunk_load_b(f4v (&b)[2][2], const float *__restrict__ wb, int k0) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) b[ct][q] = *reinterpret_cast<const f4v *>(wb + ct * 32 * kKin + k0 + 4 * q);
+}
+
+__device__ __forceinline__ void trunk_chunk(const float *s_a, int k0, const f4v (&b)[2][2], f32x16 (&acc)[2][2], int i,
+                                            int hh) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        f4v a[2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) a[rt] = *reinterpret_cast<const f4v *>(s_a + (rt * 32 + i) * kS + k0 + 8 * hh + 4 * q);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct)
+                    acc[rt][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[rt][s], b[ct][q][s], acc[rt][ct], 0, 0, 0);
+    }
+}
+
+template <int MODE, int ALGO, int ACT, int KMAX>
+__global__ __launch_bounds__(256, 2) void head_gemm_trunk_kernel(XPA_HEAD_KERNEL_PARAMS, const float *__restrict__ xr,
+                                                                 int64_t ldxr, int din, const float *__restrict__ W0,
+                                                                 const float *__restrict__ b0, float slope0,
+                                                                 float *__restrict__ hout, int64_t ldh) {
+    using Epi = HeadEpi<MODE, ALGO, ACT, KMAX>;
+    constexpr int DMAX = kTrunkDMax;
+    constexpr int kPartOff = kTile * kS;
+    constexpr int kPartSz = kWaves * kTile * Epi::PH > kTile * DMAX ? kWaves * kTile * Epi::PH : kTile * DMAX;
+    constexpr int kDhOff = kPartOff + kPartSz;
+    constexpr int kStatsOff = kDhOff + kTile * Epi::KP;
+    static_assert((kStatsOff + 4) * 4 <= 81920, "2 blocks per CU");
+    __shared__ __attribute__((aligned(16))) float lds[kStatsOff + 4];
+    float *s_a = lds;             // the h tile (A operand over all 256 k), then the epilogue's act(z) tile
+    float *s_x = lds + kPartOff;  // the x tile [64][DMAX] (prologue only; the epilogue's partials reuse it)
+    auto s_part = reinterpret_cast<float(*)[kTile][Epi::PH]>(lds + kPartOff);
+    auto s_dh = reinterpret_cast<float(*)[Epi::KP]>(lds + kDhOff);
+    float *s_stats = lds + kStatsOff;
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int i = lane & 31, hh = lane >> 5;
+    const int64_t ntiles = (batch + kTile - 1) / kTile;
+    if ((int64_t)blockIdx.x >= head_partials(batch)) return;  // no partial row of its own (see kGridMax)
+    Epi epi;
+    epi.init(K_in, W, logstd, adv_partials, n_adv_partials, batch, clip_range, slope, s_stats);
+    const float bh0 = bh[wave * 64 + i], bh1 = bh[wave * 64 + 32 + i];
+    const float *wb = Wh + (int64_t)(wave * 64 + i) * kKin + 8 * hh;  // lane's B row (ct = 0; ct = 1 at + 32 rows)
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t r0 = tile * kTile;
+        const RowIn<KMAX> in = epi.rows(tile, batch, idx, n_rows, act, old_logp, adv, ret);
+        f4v b[2][2][2];
+        trunk_load_b(b[0], wb, 0);  // independent of the tile: in flight across the prologue
+        // thread t's row of W0 (L2), loaded per tile so it is not live across the GEMM and the epilogue
+        float w0[DMAX];
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) w0[k] = W0[t * din + (k < din ? k : 0)];
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) w0[k] = k < din ? w0[k] : 0.f;
+        const float b0c = b0[t];
+        __syncthreads();            // the previous tile's epilogue is done with the LDS
+        for (int e = t; e < kTile * DMAX; e += 256) {
+            const int r = e / DMAX, k = e - r * DMAX;
+            const int64_t row = r0 + r < batch ? r0 + r : batch - 1;
+            const float v = xr[row * ldxr + (k < din ? k : 0)];
+            s_x[e] = (k < din && r0 + r < batch) ? v : 0.f;
+        }
+        __syncthreads();
+        // h tile: thread t = column t (K13's arithmetic); rows past the batch see zero inputs (never used)
+#pragma unroll 4
+        for (int r = 0; r < kTile; ++r) {
+            const float *xrow = s_x + r * DMAX;
+            float a0 = 0.f;
+#pragma unroll
+            for (int k = 0; k < DMAX; k += 4) {
+                const float4 xv = *reinterpret_cast<const float4 *>(xrow + k);
+                a0 = fmaf(xv.x, w0[k], a0);
+                a0 = fmaf(xv.y, w0[k + 1], a0);
+                a0 = fmaf(xv.z, w0[k + 2], a0);
+                a0 = fmaf(xv.w, w0[k + 3], a0);
+            }
+            const float hv = act_f<ACT>(a0 + b0c, slope0);
+            s_a[r * kS + t] = hv;
+            // the actor launch: h to HBM (a wave writes 256 contiguous bytes of the row)
+            if (hout && r0 + r < batch) __builtin_nontemporal_store(hv, hout + (r0 + r) * ldh + t);
+        }
+        __syncthreads();
+        f32x16 acc[2][2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[rt][ct][r] = 0.f;
+#pragma unroll 1
+        for (int c = 0; c < kChunks2; c += 2) {  // two chunks per trip: the ring slots stay static
+            trunk_load_b(b[1], wb, (c + 1) * kKC2);
+            __builtin_amdgcn_sched_barrier(0);
+            trunk_chunk(s_a, c * kKC2, b[0], acc, i, hh);
+            __builtin_amdgcn_sched_barrier(0);
+            // unconditional (the last trip re-reads chunk 15, unused): under a branch the join's wait drained it
+            trunk_load_b(b[0], wb, (c + 2 < kChunks2 ? c + 2 : kChunks2 - 1) * kKC2);
+            __builtin_amdgcn_sched_barrier(0);
+            trunk_chunk(s_a, (c + 1) * kKC2, b[1], acc, i, hh);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();  // every wave done with the h tile before act(z) overwrites it
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                const int col = wave * 64 + ct * 32 + i;
+                const float bc = ct ? bh1 : bh0;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                    s_a[row * kS + col] = act_f<ACT>(acc[rt][ct][r] + bc, slope);
+                }
+            }
+        epi.tile(s_a, s_part, s_dh, in, tile, batch, W, bias, dz, ld, ent_coef, vf_coef);
+    }
+    epi.finish(p_dw, p_dbh, p_dbo, p_loss, loss_width);
+}
+
 }  // namespace
 
 #ifndef XPA_HEAD_KERNELS_ONLY  // tools/_probe: include the kernels alone and instantiate one
@@ -728,40 +876,44 @@ XPA_API int64_t xpa_head_fused_num_partials(int64_t batch) {
 
 namespace {
 #define XPA_HEAD_ARGS(a) a.batch, a.K, a.ld, a.z, a.ldx, a.Wh, a.bh, a.W, a.bias, a.slope, a.logstd, a.idx, a.n_rows, a.act, a.old_logp, a.adv, a.ret, a.adv_partials, a.n_adv_partials, a.clip_range, a.ent_coef, a.vf_coef, a.dz, a.p_dw, a.p_dbh, a.p_dbo, a.p_loss, a.loss_width
-template <bool GEMM, int MODE, int ALGO, int ACT, int KMAX>
+// KIND: 0 K12 (z from HBM), 1 K16 (hidden GEMM inside), 2 K16X (trunk layer + hidden GEMM inside)
+template <int KIND, int MODE, int ALGO, int ACT, int KMAX>
 void launch_one(const HeadArgs &a, hipStream_t s) {
     const dim3 grid((unsigned)xpa_head_fused_num_partials(a.batch)), block(256);
-    if constexpr (GEMM)
+    if constexpr (KIND == 2)
+        hipLaunchKernelGGL((head_gemm_trunk_kernel<MODE, ALGO, ACT, KMAX>), grid, block, 0, s, XPA_HEAD_ARGS(a), a.xr,
+                           a.ldxr, a.din, a.W0, a.b0, a.slope0, a.hout, a.ldh);
+    else if constexpr (KIND == 1)
         hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX>), grid, block, 0, s, XPA_HEAD_ARGS(a));
     else
         hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, ACT, KMAX>), grid, block, 0, s, XPA_HEAD_ARGS(a));
 }
 
-template <bool GEMM, int MODE, int ALGO, int KMAX>
+template <int KIND, int MODE, int ALGO, int KMAX>
 void launch_act(const HeadArgs &a, int act_code, hipStream_t s) {
-    if (act_code == 0) launch_one<GEMM, MODE, ALGO, 0, KMAX>(a, s);
-    else if (act_code == 1) launch_one<GEMM, MODE, ALGO, 1, KMAX>(a, s);
-    else launch_one<GEMM, MODE, ALGO, 2, KMAX>(a, s);
+    if (act_code == 0) launch_one<KIND, MODE, ALGO, 0, KMAX>(a, s);
+    else if (act_code == 1) launch_one<KIND, MODE, ALGO, 1, KMAX>(a, s);
+    else launch_one<KIND, MODE, ALGO, 2, KMAX>(a, s);
 }
 
-template <bool GEMM, int MODE, int ALGO>
+template <int KIND, int MODE, int ALGO>
 void launch_head(const HeadArgs &a, int act_code, hipStream_t s) {
-    if constexpr (MODE == 2) launch_act<GEMM, MODE, ALGO, 1>(a, act_code, s);
-    else if (a.K <= 4) launch_act<GEMM, MODE, ALGO, 4>(a, act_code, s);  // KMAX = smallest of 4 / 6 / 8 >= K
-    else if (a.K <= 6) launch_act<GEMM, MODE, ALGO, 6>(a, act_code, s);
-    else if (a.K <= 8) launch_act<GEMM, MODE, ALGO, 8>(a, act_code, s);
-    else launch_act<GEMM, MODE, ALGO, 18>(a, act_code, s);  // C4 (A = 17), 18-way categorical
+    if constexpr (MODE == 2) launch_act<KIND, MODE, ALGO, 1>(a, act_code, s);
+    else if (a.K <= 4) launch_act<KIND, MODE, ALGO, 4>(a, act_code, s);  // KMAX = smallest of 4 / 6 / 8 >= K
+    else if (a.K <= 6) launch_act<KIND, MODE, ALGO, 6>(a, act_code, s);
+    else if (a.K <= 8) launch_act<KIND, MODE, ALGO, 8>(a, act_code, s);
+    else if constexpr (KIND != 2) launch_act<KIND, MODE, ALGO, 18>(a, act_code, s);  // C4 (A = 17), 18-way categorical
 }
 #undef XPA_HEAD_ARGS
 
-template <bool GEMM>
+template <int KIND>
 int actor_entry(int algo, int dist, int act_code, HeadArgs &a, hipStream_t s) {
     if (dist == XPA_DIST_GAUSSIAN) {
-        if (algo == XPA_ALGO_PPO) launch_head<GEMM, 0, 0>(a, act_code, s);
-        else launch_head<GEMM, 0, 1>(a, act_code, s);
+        if (algo == XPA_ALGO_PPO) launch_head<KIND, 0, 0>(a, act_code, s);
+        else launch_head<KIND, 0, 1>(a, act_code, s);
     } else {
-        if (algo == XPA_ALGO_PPO) launch_head<GEMM, 1, 0>(a, act_code, s);
-        else launch_head<GEMM, 1, 1>(a, act_code, s);
+        if (algo == XPA_ALGO_PPO) launch_head<KIND, 1, 0>(a, act_code, s);
+        else launch_head<KIND, 1, 1>(a, act_code, s);
     }
     return xpa_launch_status();
 }
@@ -802,7 +954,7 @@ XPA_API int xpa_head_fused_actor(int algo, int dist, int act_code, int64_t batch
     a.ret = nullptr; a.adv_partials = adv_partials; a.n_adv_partials = n_adv_partials; a.clip_range = clip_range;
     a.ent_coef = ent_coef; a.vf_coef = 0.f; a.dz = dz; a.p_dw = partial_dw; a.p_dbh = partial_db_hidden;
     a.p_dbo = partial_db_out; a.p_loss = loss_partials; a.loss_width = (int)loss_width;
-    return actor_entry<false>(algo, dist, act_code, a, (hipStream_t)stream);
+    return actor_entry<0>(algo, dist, act_code, a, (hipStream_t)stream);
 }
 
 XPA_API int xpa_head_fused_critic(int act_code, int64_t batch, int64_t hidden, int64_t ld, const float *z, const float *w,
@@ -819,7 +971,7 @@ XPA_API int xpa_head_fused_critic(int act_code, int64_t batch, int64_t hidden, i
     a.batch = batch; a.K = 1; a.ld = ld; a.z = z; a.ldx = ld; a.W = w; a.bias = b; a.slope = slope; a.idx = idx;
     a.n_rows = n_rows; a.ret = ret; a.vf_coef = vf_coef; a.dz = dz; a.p_dw = partial_dw; a.p_dbh = partial_db_hidden;
     a.p_dbo = partial_db_out; a.p_loss = loss_partials; a.loss_width = (int)loss_width;
-    launch_head<false, 2, 0>(a, act_code, (hipStream_t)stream);
+    launch_head<0, 2, 0>(a, act_code, (hipStream_t)stream);
     return xpa_launch_status();
 }
 
@@ -843,7 +995,7 @@ XPA_API int xpa_head_gemm_actor(int algo, int dist, int act_code, int64_t batch,
     a.n_adv_partials = n_adv_partials; a.clip_range = clip_range; a.ent_coef = ent_coef; a.vf_coef = 0.f; a.dz = dz;
     a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
     a.loss_width = (int)loss_width;
-    return actor_entry<true>(algo, dist, act_code, a, (hipStream_t)stream);
+    return actor_entry<1>(algo, dist, act_code, a, (hipStream_t)stream);
 }
 
 XPA_API int xpa_head_gemm_critic(int act_code, int64_t batch, int64_t hidden, const float *x, int64_t ldx,
@@ -862,7 +1014,71 @@ XPA_API int xpa_head_gemm_critic(int act_code, int64_t batch, int64_t hidden, co
     a.bias = b; a.slope = slope; a.idx = idx; a.n_rows = n_rows; a.ret = ret; a.vf_coef = vf_coef; a.dz = dz;
     a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
     a.loss_width = (int)loss_width;
-    launch_head<true, 2, 0>(a, act_code, (hipStream_t)stream);
+    launch_head<1, 2, 0>(a, act_code, (hipStream_t)stream);
+    return xpa_launch_status();
+}
+
+namespace {
+int check_trunk(int64_t d_in, const float *x_rows, int64_t ld_rows, const float *w_in, const float *b_in,
+                const float *w_hidden, const float *b_hidden, int64_t ld_dz) {
+    if (d_in < 1 || d_in > kTrunkDMax || !x_rows || ld_rows < d_in || !w_in || !b_in || !w_hidden || !b_hidden ||
+        (uintptr_t)w_hidden % 16 || ld_dz < kH)
+        return (int)hipErrorInvalidValue;
+    return 0;
+}
+}  // namespace
+
+XPA_API int xpa_head_gemm_trunk_actor(int algo, int dist, int act_code, int64_t batch, int64_t act_dim, int64_t hidden,
+                                      const float *x_rows, int64_t ld_rows, int64_t d_in, const float *w_in,
+                                      const float *b_in, float slope_in, float *h_out, int64_t ld_h,
+                                      const float *w_hidden, const float *b_hidden, int64_t ld_dz, const float *w,
+                                      const float *b, float slope, const float *logstd, const int64_t *idx,
+                                      int64_t n_rows, const float *act, const float *old_logp, const float *adv,
+                                      const double *adv_partials, int64_t n_adv_partials, float clip_range,
+                                      float ent_coef, float *dz, float *partial_dw, float *partial_db_hidden,
+                                      float *partial_db_out, float *loss_partials, int64_t loss_width,
+                                      xpa_stream_t stream) {
+    int rc = check_actor(algo, dist, act_code, batch, act_dim, hidden, w, b, logstd, n_rows, idx, act, old_logp, adv, dz,
+                         partial_dw, partial_db_hidden, partial_db_out, loss_partials, loss_width);
+    if (rc) return rc;
+    rc = check_trunk(d_in, x_rows, ld_rows, w_in, b_in, w_hidden, b_hidden, ld_dz);
+    if (rc) return rc;
+    if (act_dim > 8 || (h_out && ((uintptr_t)h_out % 16 || ld_h < kH || ld_h % 4))) return (int)hipErrorInvalidValue;
+    HeadArgs a{};
+    a.batch = batch; a.K = (int)act_dim; a.ld = ld_dz; a.z = nullptr; a.ldx = kKin; a.Wh = w_hidden; a.bh = b_hidden;
+    a.W = w; a.bias = b; a.slope = slope; a.logstd = logstd; a.idx = idx; a.n_rows = n_rows; a.act = act;
+    a.old_logp = old_logp; a.adv = adv; a.ret = nullptr; a.adv_partials = adv_partials;
+    a.n_adv_partials = n_adv_partials; a.clip_range = clip_range; a.ent_coef = ent_coef; a.vf_coef = 0.f; a.dz = dz;
+    a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
+    a.loss_width = (int)loss_width;
+    a.xr = x_rows; a.ldxr = ld_rows; a.din = (int)d_in; a.W0 = w_in; a.b0 = b_in; a.slope0 = slope_in;
+    a.hout = h_out; a.ldh = ld_h;
+    return actor_entry<2>(algo, dist, act_code, a, (hipStream_t)stream);
+}
+
+XPA_API int xpa_head_gemm_trunk_critic(int act_code, int64_t batch, int64_t hidden, const float *x_rows,
+                                       int64_t ld_rows, int64_t d_in, const float *w_in, const float *b_in,
+                                       float slope_in, float *h_out, int64_t ld_h, const float *w_hidden,
+                                       const float *b_hidden, int64_t ld_dz, const float *w, const float *b,
+                                       float slope, const int64_t *idx, int64_t n_rows, const float *ret,
+                                       float vf_coef, float *dz, float *partial_dw, float *partial_db_hidden,
+                                       float *partial_db_out, float *loss_partials, int64_t loss_width,
+                                       xpa_stream_t stream) {
+    if (batch <= 0 || hidden != kH || act_code < 0 || act_code > 2 || !w || !b || !ret || !dz || !partial_dw ||
+        !partial_db_hidden || !partial_db_out || !loss_partials || loss_width < kPartBase || n_rows <= 0 ||
+        (!idx && n_rows < batch) || (uintptr_t)w % 16)
+        return (int)hipErrorInvalidValue;
+    int rc = check_trunk(d_in, x_rows, ld_rows, w_in, b_in, w_hidden, b_hidden, ld_dz);
+    if (rc) return rc;
+    if (h_out && ((uintptr_t)h_out % 16 || ld_h < kH || ld_h % 4)) return (int)hipErrorInvalidValue;
+    HeadArgs a{};
+    a.batch = batch; a.K = 1; a.ld = ld_dz; a.z = nullptr; a.ldx = kKin; a.Wh = w_hidden; a.bh = b_hidden; a.W = w;
+    a.bias = b; a.slope = slope; a.idx = idx; a.n_rows = n_rows; a.ret = ret; a.vf_coef = vf_coef; a.dz = dz;
+    a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
+    a.loss_width = (int)loss_width;
+    a.xr = x_rows; a.ldxr = ld_rows; a.din = (int)d_in; a.W0 = w_in; a.b0 = b_in; a.slope0 = slope_in;
+    a.hout = h_out; a.ldh = ld_h;
+    launch_head<2, 2, 0>(a, act_code, (hipStream_t)stream);
     return xpa_launch_status();
 }
 #endif  // XPA_HEAD_KERNELS_ONLY

@@ -96,6 +96,7 @@ __global__ __launch_bounds__(256) void thin_fwd_kernel(const float *__restrict__
                 adv_partials[2 * tile + 1] = q;
             }
         }
+        if (IDX && !h) continue;  // gather-only form (K16X forms h itself): the rows and the moments
         __syncthreads();
         const int nr = (int)min((int64_t)TILE, rows - r0);
         for (int r = 0; r < nr; ++r) {
@@ -382,7 +383,7 @@ XPA_API int xpa_thin_linear_act_fwd_gather(int act, const float *x, int64_t ldx,
                                            float slope, float *h, int64_t ldh, const float *adv, double *adv_partials,
                                            float *x_out, xpa_stream_t stream) {
     if (rows <= 0 || n_rows <= 0 || d_in < 1 || d_in > kMaxIn || d_out != kCols || act < 0 || act > 2 || !x || !idx ||
-        !w || !b || !h || ldx < d_in || ldh < d_out || (adv_partials && !adv))
+        !w || !b || (!h && !x_out) || ldx < d_in || (h && ldh < d_out) || (adv_partials && !adv))
         return (int)hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
     const int64_t tiles = (rows + kTile - 1) / kTile;

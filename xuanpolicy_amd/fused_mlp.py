@@ -82,6 +82,7 @@ class Rows:
     def __init__(self, flat, idx):
         self.flat, self.idx = flat, idx
         self.gathered = None   # set by the gather forward: the rows as a contiguous [B, d] copy
+        self.trunk = None      # K16X: (gathered rows, W0, b0, slope, h out) when the head launches form h
         self.shape = (idx.shape[0], flat.shape[1])
         self.device = flat.device
         self.dtype = flat.dtype
@@ -124,6 +125,13 @@ class FusedActorCritic:
         # K16: the paired hidden layers' forward GEMM inside the head kernels (fp32 MFMA), when their
         # input is 256 wide; z is then never materialised.
         self.gemm_heads = self.pair is not None and self.actor[0][0].in_features == ops.HEAD_HIDDEN
+        # K16X: the trunk (one thin layer, d_in <= 20, the heads' activation) inside the K16 launches as well, so the
+        # update's trunk output h is formed in LDS and written once (by the actor launch) instead of K13's write + two
+        # K16 reads; minibatch rows from Rows only (the gather-only K13 form supplies the rows and the adv moments)
+        self.trunk_heads = (self.gemm_heads and self.thin0 and len(self.rep) == 1
+                            and self.rep[0][0].in_features <= ops.TRUNK_DMAX and k <= 8
+                            and self.rep[0][1:] == self.actor[-2][1:] == self.critic[-2][1:])
+        self.use_trunk_heads = True
         n_params = sum(1 for _ in policy.parameters())
         n_cov = 2 * (len(self.rep) + len(self.actor) + len(self.critic)) + (0 if self.discrete else 1)
         if n_params != n_cov:
@@ -170,9 +178,14 @@ class FusedActorCritic:
             # the gathered rows are written beside h (4 B x d_in per row) so the backward reads them contiguously
             # (reading them through idx again cost K13's backward 3.3 us per update)
             x.gathered = torch.empty((B, lin.in_features), dtype=torch.float32, device=x.device)
+            # K16X: gather-only (h = NULL); the actor head launch forms h and writes it here
+            deferred = self.trunk_heads and self.use_trunk_heads and len(self.rep) == 1
+            if deferred:
+                x.trunk = (x.gathered, lin.weight, lin.bias, slope, h)
             _lib.check(ops.lib().xpa_thin_linear_act_fwd_gather(
                 code, ops._p(x.flat), x.flat.stride(0), x.flat.shape[0], ops._p(x.idx), B, lin.in_features,
-                lin.out_features, ops._p(lin.weight), ops._p(lin.bias), slope, ops._p(h), h.stride(0),
+                lin.out_features, ops._p(lin.weight), ops._p(lin.bias), slope, None if deferred else ops._p(h),
+                h.stride(0),
                 ops._p(adv) if adv_partials is not None else None,
                 ops._p(adv_partials) if adv_partials is not None else None, ops._p(x.gathered),
                 ops._stream(x.device)), "xpa_thin_linear_act_fwd_gather")
@@ -336,7 +349,8 @@ class FusedActorCritic:
                                               adv, ret, old_logp=old_logp, idx=idx, adv_partials=adv_partials,
                                               clip_range=clip_range, vf_coef=vf_coef, ent_coef=ent_coef, grads=grads,
                                               colsum_queue=self._cq, gemm=gemm, sq_logstd=self._sq.data_ptr(),
-                                              defer_loss=True)
+                                              defer_loss=True,
+                                              trunk=x.trunk if gemm is not None and isinstance(x, Rows) else None)
         have_rep = len(self.rep) > 0
         if paired:   # dW of both hidden layers and dX (K = 512, no accumulate pass) as single GEMMs
             dz = self._hws.dz_pair

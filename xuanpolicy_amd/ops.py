@@ -389,6 +389,7 @@ def policy_loss(algo, dist, head, logstd, v, act, adv, ret, old_logp=None, idx=N
 # ------------------------------------------------------------------------------------------------
 HEAD_HIDDEN = 256  # hidden width K12 handles (64 lanes x 4 columns)
 HEAD_KMAX = 18   # widest head of the fused head kernels K12 / K16 (and K14's rollout head)
+TRUNK_DMAX = 20  # widest trunk input K16X forms in its prologue (xpa_head_gemm_trunk_*)
 
 
 class HeadWorkspace:
@@ -511,13 +512,16 @@ class ColsumQueue:
 
 def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, w_critic, b_critic, act_critic,
                 logstd, act, adv, ret, old_logp=None, idx=None, adv_partials=None, clip_range=0.2, vf_coef=0.25,
-                ent_coef=0.0, grads=None, colsum_queue=None, gemm=None, sq_logstd=None, defer_loss=False):
+                ent_coef=0.0, grads=None, colsum_queue=None, gemm=None, sq_logstd=None, defer_loss=False, trunk=None):
     """K12 actor + critic heads, loss finalize and the column-sum finalizes.
 
     z_*: hidden pre-activations [B, 256] (unit column stride; row stride = the workspace dz row stride,
     e.g. the halves of a [B, 512] actor|critic pre-activation with a paired workspace); w_*/b_*: output layer
     gemm = (x [B, 256], (w_h_actor, b_h_actor), (w_h_critic, b_h_critic)): K16 — the hidden layers' GEMMs
-    run inside the head kernels on the matrix cores and z_actor / z_critic are not used (pass None). (K x 256 / 1 x 256); act_*: (code, slope)
+    run inside the head kernels on the matrix cores and z_actor / z_critic are not used (pass None).
+    trunk = (x_rows [B, d_in], w_in [256, d_in], b_in, slope_in, h_out) with gemm: K16X — the trunk layer
+    Linear(d_in <= TRUNK_DMAX, 256) + the heads' activation is formed inside the launches too; gemm's x must be h_out,
+    which the actor launch writes. (K x 256 / 1 x 256); act_*: (code, slope)
     of the hidden activation.  colsum_queue: an ops.ColsumQueue to defer the column-sum finalizes into
     (flushed by the caller), else they run here.  grads: dict with the gradient views to write — 'w_actor', 'b_actor',
     'bh_actor', 'w_critic', 'b_critic', 'bh_critic', 'logstd' (gaussian).  Returns (scalars, dz_actor,
@@ -564,7 +568,28 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
     n_adv = adv_partials.shape[0] if adv_partials is not None else 0
     p_logstd = _p(logstd) if dist == "gaussian" else None
     p_old = _p(old_logp) if algo == "ppo" else None
-    if gemm is not None:
+    if trunk is not None:
+        if gemm is None or trunk[4] is not x:
+            raise ValueError("trunk needs gemm with x = the trunk's h output")
+        xr, w0, b0, slope0, h_out = trunk
+        _req(xr, "x_rows", torch.float32)
+        din = xr.shape[1]
+        if xr.dim() != 2 or xr.shape[0] != B or din > TRUNK_DMAX or tuple(w0.shape) != (H, din):
+            raise ValueError("trunk rows must be [%d, <= %d] with w_in [%d, d_in]" % (B, TRUNK_DMAX, H))
+        _lib.check(L.xpa_head_gemm_trunk_actor(ALGO[algo], DIST[dist], act_actor[0], B, K, H, _p(xr), xr.stride(0), din,
+                                               _p(w0), _p(b0), float(slope0), _p(h_out), h_out.stride(0), _p(wha),
+                                               _p(bha), ld, _p(w_actor), _p(b_actor), float(act_actor[1]), p_logstd,
+                                               _p(idx), rows, _p(act), p_old, _p(adv), _p(adv_partials), n_adv,
+                                               float(clip_range), float(ent_coef), _p(ws.dz_actor), _p(ws.p_dw_actor),
+                                               _p(ws.p_dbh_actor), _p(ws.p_dbo_actor), _p(ws.loss_partials), W, s),
+                   "xpa_head_gemm_trunk_actor")
+        _lib.check(L.xpa_head_gemm_trunk_critic(act_critic[0], B, H, _p(xr), xr.stride(0), din, _p(w0), _p(b0),
+                                                float(slope0), None, H, _p(whc), _p(bhc), ld, _p(w_critic),
+                                                _p(b_critic), float(act_critic[1]), _p(idx), rows, _p(ret),
+                                                float(vf_coef), _p(ws.dz_critic), _p(ws.p_dw_critic),
+                                                _p(ws.p_dbh_critic), _p(ws.p_dbo_critic), _p(ws.loss_partials), W, s),
+                   "xpa_head_gemm_trunk_critic")
+    elif gemm is not None:
         _lib.check(L.xpa_head_gemm_actor(ALGO[algo], DIST[dist], act_actor[0], B, K, H, _p(x), x.stride(0), _p(wha),
                                          _p(bha), ld, _p(w_actor), _p(b_actor), float(act_actor[1]), p_logstd, _p(idx),
                                          rows, _p(act), p_old, _p(adv), _p(adv_partials), n_adv, float(clip_range),
