@@ -49,7 +49,7 @@ def parse():
     p.add_argument("--gae-form", choices=("value", "split"), default="value",
                    help="value: the deferred bootstraps' value head fused into the GAE scan (K1V, one launch); "
                         "split: value head (K14) then the compact GAE scan (K1)")
-    p.add_argument("--trunk-heads", choices=("on", "off"), default="on",
+    p.add_argument("--trunk-heads", choices=("on", "off"), default="off",
                    help="K16X (trunk layer inside the head GEMM launches) or r03's K13 forward + K16 (A/B)")
     p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc HBM-traffic passes")
     p.add_argument("--no-rocprof", action="store_true",

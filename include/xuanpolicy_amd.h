@@ -490,10 +490,10 @@ int xpa_head_gemm_critic(int act, int64_t batch, int64_t hidden, const float *x,
                          int64_t loss_width, xpa_stream_t stream);
 
 /* K16X — K16 with the representation's first layer Linear(d_in <= 20, 256) + activation `act` (K13's, bit for bit)
- * in the prologue: the h tile is formed in LDS from the minibatch's gathered observation rows x_rows [batch, d_in]
- * (row stride ld_rows; e.g. xpa_thin_linear_act_fwd_gather with h = NULL), w_in [256, d_in], b_in [256], and
- * feeds the hidden GEMM straight from LDS.  h_out (may be NULL; row stride ld_h) receives h for the backward (the
- * actor writes it, the critic recomputes it).  Otherwise exactly K16 (act_dim <= 8). */
+ * in the prologue: each block forms its tile's h rows from the minibatch's gathered observation rows x_rows
+ * [batch, d_in] (row stride ld_rows; e.g. xpa_thin_linear_act_fwd_gather with h = NULL), w_in [256, d_in], b_in [256],
+ * writes them to h_out (required; row stride ld_h: the backward's copy) and runs K16's k loop on them (A operand read
+ * back from L2).  Otherwise exactly K16 (act_dim <= 8).  The learner's critic then runs plain K16 on h_out. */
 int xpa_head_gemm_trunk_actor(int algo, int dist, int act, int64_t batch, int64_t act_dim, int64_t hidden,
                               const float *x_rows, int64_t ld_rows, int64_t d_in, const float *w_in, const float *b_in,
                               float slope_in, float *h_out, int64_t ld_h, const float *w_hidden, const float *b_hidden,

@@ -652,8 +652,58 @@ __device__ __forceinline__ void gemm_chunk(const float *st, f32x16 (&acc)[2][2],
     }
 }
 
-template <int MODE, int ALGO, int ACT, int KMAX>
-__global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAMS) {
+// K16X prologue (r03): the representation's first layer (K13's Linear(d_in <= 20, 256) + activation, bit for bit
+// its fmaf chain over the zero-padded inputs) for the tile's rows, from the minibatch's gathered observation rows;
+// thread t = column t; h goes to HBM (the backward's copy) with plain stores, so the k loop's A-operand DMAs right
+// after read it from L2.  s_x: [64][DMAX] floats of LDS (the operand ring's space, free until the first DMA).
+// Ends with every store drained and a block barrier.
+constexpr int kTrunkDMax = 20;
+template <int ACT>
+__device__ __forceinline__ void trunk_prologue(float *s_x, const float *__restrict__ xr, int64_t ldxr, int din,
+                                               const float *__restrict__ W0, const float *__restrict__ b0,
+                                               float slope0, float *__restrict__ hout, int64_t ldh, int64_t r0,
+                                               int64_t batch) {
+    constexpr int DMAX = kTrunkDMax;
+    const int t = threadIdx.x;
+    float w0[DMAX];
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) w0[k] = W0[t * din + (k < din ? k : 0)];
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) w0[k] = k < din ? w0[k] : 0.f;
+    const float b0c = b0[t];
+    for (int e = t; e < kTile * DMAX; e += 256) {
+        const int r = e / DMAX, k = e - r * DMAX;
+        const int64_t row = r0 + r < batch ? r0 + r : batch - 1;
+        const float v = xr[row * ldxr + (k < din ? k : 0)];
+        s_x[e] = (k < din && r0 + r < batch) ? v : 0.f;
+    }
+    __syncthreads();
+    const int nr = (int)min((int64_t)kTile, batch - r0);
+    for (int r = 0; r < nr; ++r) {
+        const float *xrow = s_x + r * DMAX;
+        float a0 = 0.f;
+#pragma unroll
+        for (int k = 0; k < DMAX; k += 4) {
+            const float4 xv = *reinterpret_cast<const float4 *>(xrow + k);
+            a0 = fmaf(xv.x, w0[k], a0);
+            a0 = fmaf(xv.y, w0[k + 1], a0);
+            a0 = fmaf(xv.z, w0[k + 2], a0);
+            a0 = fmaf(xv.w, w0[k + 3], a0);
+        }
+        hout[(r0 + r) * ldh + t] = act_f<ACT>(a0 + b0c, slope0);
+    }
+    xpa_drain();      // this block's h rows are in L2 before any wave's DMA reads them
+    __syncthreads();  // (and every wave is done with s_x before the ring overwrites it)
+}
+
+// TRUNK (K16X, r03): the prologue above forms the tile's A rows (h) first; z / ldx are then ignored and the k loop
+// reads A from hout / ldh.
+template <int MODE, int ALGO, int ACT, int KMAX, bool TRUNK = false>
+__global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAMS, const float *__restrict__ xr = nullptr,
+                                                           int64_t ldxr = 0, int din = 0,
+                                                           const float *__restrict__ W0 = nullptr,
+                                                           const float *__restrict__ b0 = nullptr, float slope0 = 0.f,
+                                                           float *__restrict__ hout = nullptr, int64_t ldh = 0) {
     using Epi = HeadEpi<MODE, ALGO, ACT, KMAX>;
     // ONE LDS array (a second __shared__ object beside the DMA target can make hipcc wait vmcnt(0) before
     // every chunk's ds_reads): operand stages / h tile, then the epilogue's partials, d head and stats.
@@ -684,9 +734,16 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[rt][ct][r] = 0.f;
         __syncthreads();  // the previous tile's epilogue is done with smem
+        const float *xa = z;
+        int64_t lda = ldx;
+        if constexpr (TRUNK) {
+            trunk_prologue<ACT>(smem, xr, ldxr, din, W0, b0, slope0, hout, ldh, r0, batch);
+            xa = hout;
+            lda = ldh;
+        }
 #if XPA_HEAD_PROBE != 2 && XPA_HEAD_PROBE != 4 && XPA_HEAD_PROBE != 5  // tools/head_probe.py: 2 = epilogue alone (4, 5: parts of it)
-        gemm_issue(lds_base, z, ldx, Wh, r0, batch, 0, lane, wave);
-        gemm_issue(lds_base + kStage * 4, z, ldx, Wh, r0, batch, kKC, lane, wave);
+        gemm_issue(lds_base, xa, lda, Wh, r0, batch, 0, lane, wave);
+        gemm_issue(lds_base + kStage * 4, xa, lda, Wh, r0, batch, kKC, lane, wave);
 #pragma unroll 1
         for (int c = 0; c < kChunks; ++c) {
             // own DMAs of chunk c landed (chunk c + 1's may still fly), then every wave's: chunk c is in
@@ -694,7 +751,7 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
             if (c + 1 < kChunks) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kDmaPerChunk) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
             if (c + 2 < kChunks)
-                gemm_issue(lds_base + ((c + 2) % kStages) * kStage * 4, z, ldx, Wh, r0, batch, (c + 2) * kKC, lane,
+                gemm_issue(lds_base + ((c + 2) % kStages) * kStage * 4, xa, lda, Wh, r0, batch, (c + 2) * kKC, lane,
                            wave);
 #if XPA_HEAD_PROBE != 3  // 3 = operand staging alone
             gemm_chunk(smem + (c % kStages) * kStage, acc, lane, wave);
@@ -725,148 +782,6 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
     epi.finish(p_dw, p_dbh, p_dbo, p_loss, loss_width);
 }
 
-// K16X (r03): K16 with the representation's first layer (K13's Linear(d_in <= 20, 256) + activation) in its
-// prologue, so the trunk output h is formed in LDS from the minibatch's gathered observation rows and never
-// read back from HBM (the actor launch writes it once, for the hidden layers' dW GEMM and K13's backward; the
-// critic launch recomputes it).  The A operand of the hidden GEMM is then the whole [64 x 256] h tile resident in
-// LDS (row stride kS, the epilogue tile's image), and each wave's B operand — its own 64 rows of Wh, which no
-// other wave of the block reads — goes global (L2) -> VGPRs directly: no operand DMAs, no barrier in the k loop.
-// k loop: 16 chunks of 16 k; lane (i, hh) holds k = k0 + 8 hh + 4 q + s (q < 2, s < 4) of its A row / B row, fed as
-// the MFMA's k = hh at step (q, s) (any k order is exact as long as A and B agree); chunk c + 1's B registers
-// load during chunk c's 32 MFMAs.  h arithmetic: K13's fmaf chain over the zero-padded DMAX inputs, so h is
-// bit for bit thin_fwd_kernel's.
-constexpr int kKC2 = 16;
-constexpr int kChunks2 = kKin / kKC2;
-constexpr int kTrunkDMax = 20;
-
-// lane (i, hh): k = k0 + 8 hh + 4 q + s (q < 2, s < 4) of B rows i (ct = 0) and 32 + i (ct = 1) of the wave's 64
-__device__ __forceinline__ void trunk_load_b(f4v (&b)[2][2], const float *__restrict__ wb, int k0) {
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) b[ct][q] = *reinterpret_cast<const f4v *>(wb + ct * 32 * kKin + k0 + 4 * q);
-}
-
-__device__ __forceinline__ void trunk_chunk(const float *s_a, int k0, const f4v (&b)[2][2], f32x16 (&acc)[2][2], int i,
-                                            int hh) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        f4v a[2];
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt) a[rt] = *reinterpret_cast<const f4v *>(s_a + (rt * 32 + i) * kS + k0 + 8 * hh + 4 * q);
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-                for (int ct = 0; ct < 2; ++ct)
-                    acc[rt][ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[rt][s], b[ct][q][s], acc[rt][ct], 0, 0, 0);
-    }
-}
-
-template <int MODE, int ALGO, int ACT, int KMAX>
-__global__ __launch_bounds__(256, 2) void head_gemm_trunk_kernel(XPA_HEAD_KERNEL_PARAMS, const float *__restrict__ xr,
-                                                                 int64_t ldxr, int din, const float *__restrict__ W0,
-                                                                 const float *__restrict__ b0, float slope0,
-                                                                 float *__restrict__ hout, int64_t ldh) {
-    using Epi = HeadEpi<MODE, ALGO, ACT, KMAX>;
-    constexpr int DMAX = kTrunkDMax;
-    constexpr int kPartOff = kTile * kS;
-    constexpr int kPartSz = kWaves * kTile * Epi::PH > kTile * DMAX ? kWaves * kTile * Epi::PH : kTile * DMAX;
-    constexpr int kDhOff = kPartOff + kPartSz;
-    constexpr int kStatsOff = kDhOff + kTile * Epi::KP;
-    static_assert((kStatsOff + 4) * 4 <= 81920, "2 blocks per CU");
-    __shared__ __attribute__((aligned(16))) float lds[kStatsOff + 4];
-    float *s_a = lds;             // the h tile (A operand over all 256 k), then the epilogue's act(z) tile
-    float *s_x = lds + kPartOff;  // the x tile [64][DMAX] (prologue only; the epilogue's partials reuse it)
-    auto s_part = reinterpret_cast<float(*)[kTile][Epi::PH]>(lds + kPartOff);
-    auto s_dh = reinterpret_cast<float(*)[Epi::KP]>(lds + kDhOff);
-    float *s_stats = lds + kStatsOff;
-    const int t = threadIdx.x, lane = t & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int i = lane & 31, hh = lane >> 5;
-    const int64_t ntiles = (batch + kTile - 1) / kTile;
-    if ((int64_t)blockIdx.x >= head_partials(batch)) return;  // no partial row of its own (see kGridMax)
-    Epi epi;
-    epi.init(K_in, W, logstd, adv_partials, n_adv_partials, batch, clip_range, slope, s_stats);
-    const float bh0 = bh[wave * 64 + i], bh1 = bh[wave * 64 + 32 + i];
-    const float *wb = Wh + (int64_t)(wave * 64 + i) * kKin + 8 * hh;  // lane's B row (ct = 0; ct = 1 at + 32 rows)
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t r0 = tile * kTile;
-        const RowIn<KMAX> in = epi.rows(tile, batch, idx, n_rows, act, old_logp, adv, ret);
-        f4v b[2][2][2];
-        trunk_load_b(b[0], wb, 0);  // independent of the tile: in flight across the prologue
-        // thread t's row of W0 (L2), loaded per tile so it is not live across the GEMM and the epilogue
-        float w0[DMAX];
-#pragma unroll
-        for (int k = 0; k < DMAX; ++k) w0[k] = W0[t * din + (k < din ? k : 0)];
-#pragma unroll
-        for (int k = 0; k < DMAX; ++k) w0[k] = k < din ? w0[k] : 0.f;
-        const float b0c = b0[t];
-        __syncthreads();            // the previous tile's epilogue is done with the LDS
-        for (int e = t; e < kTile * DMAX; e += 256) {
-            const int r = e / DMAX, k = e - r * DMAX;
-            const int64_t row = r0 + r < batch ? r0 + r : batch - 1;
-            const float v = xr[row * ldxr + (k < din ? k : 0)];
-            s_x[e] = (k < din && r0 + r < batch) ? v : 0.f;
-        }
-        __syncthreads();
-        // h tile: thread t = column t (K13's arithmetic); rows past the batch see zero inputs (never used)
-#pragma unroll 4
-        for (int r = 0; r < kTile; ++r) {
-            const float *xrow = s_x + r * DMAX;
-            float a0 = 0.f;
-#pragma unroll
-            for (int k = 0; k < DMAX; k += 4) {
-                const float4 xv = *reinterpret_cast<const float4 *>(xrow + k);
-                a0 = fmaf(xv.x, w0[k], a0);
-                a0 = fmaf(xv.y, w0[k + 1], a0);
-                a0 = fmaf(xv.z, w0[k + 2], a0);
-                a0 = fmaf(xv.w, w0[k + 3], a0);
-            }
-            const float hv = act_f<ACT>(a0 + b0c, slope0);
-            s_a[r * kS + t] = hv;
-            // the actor launch: h to HBM (a wave writes 256 contiguous bytes of the row)
-            if (hout && r0 + r < batch) __builtin_nontemporal_store(hv, hout + (r0 + r) * ldh + t);
-        }
-        __syncthreads();
-        f32x16 acc[2][2];
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[rt][ct][r] = 0.f;
-#pragma unroll 1
-        for (int c = 0; c < kChunks2; c += 2) {  // two chunks per trip: the ring slots stay static
-            trunk_load_b(b[1], wb, (c + 1) * kKC2);
-            __builtin_amdgcn_sched_barrier(0);
-            trunk_chunk(s_a, c * kKC2, b[0], acc, i, hh);
-            __builtin_amdgcn_sched_barrier(0);
-            // unconditional (the last trip re-reads chunk 15, unused): under a branch the join's wait drained it
-            trunk_load_b(b[0], wb, (c + 2 < kChunks2 ? c + 2 : kChunks2 - 1) * kKC2);
-            __builtin_amdgcn_sched_barrier(0);
-            trunk_chunk(s_a, (c + 1) * kKC2, b[1], acc, i, hh);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        __syncthreads();  // every wave done with the h tile before act(z) overwrites it
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct) {
-                const int col = wave * 64 + ct * 32 + i;
-                const float bc = ct ? bh1 : bh0;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-                    s_a[row * kS + col] = act_f<ACT>(acc[rt][ct][r] + bc, slope);
-                }
-            }
-        epi.tile(s_a, s_part, s_dh, in, tile, batch, W, bias, dz, ld, ent_coef, vf_coef);
-    }
-    epi.finish(p_dw, p_dbh, p_dbo, p_loss, loss_width);
-}
-
 }  // namespace
 
 #ifndef XPA_HEAD_KERNELS_ONLY  // tools/_probe: include the kernels alone and instantiate one
@@ -881,10 +796,11 @@ template <int KIND, int MODE, int ALGO, int ACT, int KMAX>
 void launch_one(const HeadArgs &a, hipStream_t s) {
     const dim3 grid((unsigned)xpa_head_fused_num_partials(a.batch)), block(256);
     if constexpr (KIND == 2)
-        hipLaunchKernelGGL((head_gemm_trunk_kernel<MODE, ALGO, ACT, KMAX>), grid, block, 0, s, XPA_HEAD_ARGS(a), a.xr,
+        hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, true>), grid, block, 0, s, XPA_HEAD_ARGS(a), a.xr,
                            a.ldxr, a.din, a.W0, a.b0, a.slope0, a.hout, a.ldh);
     else if constexpr (KIND == 1)
-        hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX>), grid, block, 0, s, XPA_HEAD_ARGS(a));
+        hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, false>), grid, block, 0, s, XPA_HEAD_ARGS(a),
+                           nullptr, (int64_t)0, 0, nullptr, nullptr, 0.f, nullptr, (int64_t)0);
     else
         hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, ACT, KMAX>), grid, block, 0, s, XPA_HEAD_ARGS(a));
 }
@@ -1043,7 +959,7 @@ XPA_API int xpa_head_gemm_trunk_actor(int algo, int dist, int act_code, int64_t 
     if (rc) return rc;
     rc = check_trunk(d_in, x_rows, ld_rows, w_in, b_in, w_hidden, b_hidden, ld_dz);
     if (rc) return rc;
-    if (act_dim > 8 || (h_out && ((uintptr_t)h_out % 16 || ld_h < kH || ld_h % 4))) return (int)hipErrorInvalidValue;
+    if (act_dim > 8 || !h_out || (uintptr_t)h_out % 16 || ld_h < kH || ld_h % 4) return (int)hipErrorInvalidValue;
     HeadArgs a{};
     a.batch = batch; a.K = (int)act_dim; a.ld = ld_dz; a.z = nullptr; a.ldx = kKin; a.Wh = w_hidden; a.bh = b_hidden;
     a.W = w; a.bias = b; a.slope = slope; a.logstd = logstd; a.idx = idx; a.n_rows = n_rows; a.act = act;
@@ -1070,7 +986,7 @@ XPA_API int xpa_head_gemm_trunk_critic(int act_code, int64_t batch, int64_t hidd
         return (int)hipErrorInvalidValue;
     int rc = check_trunk(d_in, x_rows, ld_rows, w_in, b_in, w_hidden, b_hidden, ld_dz);
     if (rc) return rc;
-    if (h_out && ((uintptr_t)h_out % 16 || ld_h < kH || ld_h % 4)) return (int)hipErrorInvalidValue;
+    if (!h_out || (uintptr_t)h_out % 16 || ld_h < kH || ld_h % 4) return (int)hipErrorInvalidValue;
     HeadArgs a{};
     a.batch = batch; a.K = 1; a.ld = ld_dz; a.z = nullptr; a.ldx = kKin; a.Wh = w_hidden; a.bh = b_hidden; a.W = w;
     a.bias = b; a.slope = slope; a.idx = idx; a.n_rows = n_rows; a.ret = ret; a.vf_coef = vf_coef; a.dz = dz;

@@ -70,22 +70,45 @@ __global__ __launch_bounds__(256) void thin_fwd_kernel(const float *__restrict__
             __syncthreads();
         }
         // zero-padded columns din..DMAX-1 stay 0 from this loop's (r, k < DMAX) writes
-        for (int i = t; i < TILE * DMAX; i += 256) {
-            const int r = i / DMAX, k = i - r * DMAX;
-            if (IDX) {
+        float av = 0.f;
+        if constexpr (IDX) {
+            // every load of the tile issued before the first use (clamped addresses, validity by select; r02: the
+            // loads under the validity branch each waited at the join — one round trip per element and one for adv)
+            constexpr int kPer = (TILE * DMAX + 255) / 256;
+            float v[kPer];
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                const int i = t + 256 * u;
+                const int r = i < TILE * DMAX ? i / DMAX : 0, k = i - (i / DMAX) * DMAX;
                 const int64_t sr = s_src[r];
-                const float v = (k < din && sr >= 0) ? x[sr * ldx + k] : 0.f;
-                s_x[r * kPad + k] = v;
-                if (x_out && k < din && r0 + r < rows) x_out[(r0 + r) * din + k] = v;  // the gathered rows, for the backward
-            } else {
+                const bool ok = i < TILE * DMAX && k < din && sr >= 0;
+                v[u] = x[ok ? sr * ldx + k : 0];
+                v[u] = ok ? v[u] : 0.f;
+            }
+            const int64_t sa = t < TILE ? s_src[t] : -1;
+            if (adv_partials) {
+                av = adv[sa >= 0 ? sa : 0];
+                av = sa >= 0 ? av : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                const int i = t + 256 * u;
+                if (i < TILE * DMAX) {
+                    const int r = i / DMAX, k = i - r * DMAX;
+                    s_x[r * kPad + k] = v[u];
+                    if (x_out && k < din && r0 + r < rows) x_out[(r0 + r) * din + k] = v[u];  // the gathered rows
+                }
+            }
+        } else {
+            for (int i = t; i < TILE * DMAX; i += 256) {
+                const int r = i / DMAX, k = i - r * DMAX;
                 s_x[r * kPad + k] = (k < din && r0 + r < rows) ? x[(r0 + r) * ldx + k] : 0.f;
             }
         }
         if (IDX && adv_partials) {  // K4's moments of this tile (thread t <-> row t)
             double sm = 0.0, q = 0.0;
-            const int64_t sr = t < TILE ? s_src[t] : -1;
-            if (sr >= 0) {
-                const double a = (double)adv[sr];
+            {
+                const double a = (double)av;   // 0 for an invalid row: adds nothing, as before
                 sm = a;
                 q = a * a;
             }

@@ -131,7 +131,8 @@ class FusedActorCritic:
         self.trunk_heads = (self.gemm_heads and self.thin0 and len(self.rep) == 1
                             and self.rep[0][0].in_features <= ops.TRUNK_DMAX and k <= 8
                             and self.rep[0][1:] == self.actor[-2][1:] == self.critic[-2][1:])
-        self.use_trunk_heads = True
+        # measured slower at C2 (r03): off unless asked for (bench.py --trunk-heads on)
+        self.use_trunk_heads = False
         n_params = sum(1 for _ in policy.parameters())
         n_cov = 2 * (len(self.rep) + len(self.actor) + len(self.critic)) + (0 if self.discrete else 1)
         if n_params != n_cov:

@@ -583,12 +583,11 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
                                                float(clip_range), float(ent_coef), _p(ws.dz_actor), _p(ws.p_dw_actor),
                                                _p(ws.p_dbh_actor), _p(ws.p_dbo_actor), _p(ws.loss_partials), W, s),
                    "xpa_head_gemm_trunk_actor")
-        _lib.check(L.xpa_head_gemm_trunk_critic(act_critic[0], B, H, _p(xr), xr.stride(0), din, _p(w0), _p(b0),
-                                                float(slope0), None, H, _p(whc), _p(bhc), ld, _p(w_critic),
-                                                _p(b_critic), float(act_critic[1]), _p(idx), rows, _p(ret),
-                                                float(vf_coef), _p(ws.dz_critic), _p(ws.p_dw_critic),
-                                                _p(ws.p_dbh_critic), _p(ws.p_dbo_critic), _p(ws.loss_partials), W, s),
-                   "xpa_head_gemm_trunk_critic")
+        # the critic reads the h the actor launch wrote (plain K16)
+        _lib.check(L.xpa_head_gemm_critic(act_critic[0], B, H, _p(h_out), h_out.stride(0), _p(whc), _p(bhc), ld,
+                                          _p(w_critic), _p(b_critic), float(act_critic[1]), _p(idx), rows, _p(ret),
+                                          float(vf_coef), _p(ws.dz_critic), _p(ws.p_dw_critic), _p(ws.p_dbh_critic),
+                                          _p(ws.p_dbo_critic), _p(ws.loss_partials), W, s), "xpa_head_gemm_critic")
     elif gemm is not None:
         _lib.check(L.xpa_head_gemm_actor(ALGO[algo], DIST[dist], act_actor[0], B, K, H, _p(x), x.stride(0), _p(wha),
                                          _p(bha), ld, _p(w_actor), _p(b_actor), float(act_actor[1]), p_logstd, _p(idx),
