@@ -10,9 +10,9 @@ Q="--no-cpu-baseline --no-sweep --no-per --no-c1 --no-c3 --no-c4 --no-pmc --no-r
 timeout -k 10 300 python -u bench.py --steps 6 --warmup 2 $Q --out $O/${T}_bench.json > $O/${T}_bench.log 2>&1 || { tail -5 $O/${T}_bench.log; exit 5; }
 python -c "import json;d=json.load(open('$O/${T}_bench.json'));print(d['value'], d['ms_per_step'], d['update_kernels']['heads']['avg_us'], d['phase_split_ms'])"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_prof -o run -- python -u bench.py --steps 3 --warmup 2 $Q --no-kernel-timing --out $O/${T}_prof.json > $O/${T}_prof.log 2>&1 || { tail -5 $O/${T}_prof.log; exit 6; }
-python - <<'PY'
-import csv,glob
-f=glob.glob('gpurun_out/${T}_prof/**/run_kernel_stats.csv',recursive=True)[0]
+T=$T python - <<'PY'
+import csv,glob,os
+f=glob.glob('gpurun_out/%s_prof/**/run_kernel_stats.csv' % os.environ['T'],recursive=True)[0]
 for r in sorted(csv.DictReader(open(f)),key=lambda r:-float(r['TotalDurationNs']))[:12]:
     print(r['Name'][:70], r['Calls'], round(float(r['AverageNs'])/1e3,1))
 PY
