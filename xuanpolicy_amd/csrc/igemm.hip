@@ -515,42 +515,50 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_lds_kernel(WgArgs a) {
         constexpr int XB = 6, DB = ACT >= 0 ? 2 : 4;
         const int nx = prh * a.PW * CQ;
         const int iy0 = oy0 * a.S - a.P;
+        // (r03) every load unconditional from a clamped address, validity applied by select: under the bounds
+        // branches hipcc waited vmcnt(0) at the joins — two or three serial round trips per batch instead of one
         for (int e0 = t; e0 < nx; e0 += XB * nthr) {
             f4 v[XB];
+            bool ok[XB];
 #pragma unroll
             for (int u = 0; u < XB; ++u) {
                 const int e = e0 + u * nthr;
                 const int c4 = e % CQ, pp = e / CQ, pc = pp % a.PW, pr = pp / a.PW;
                 const int iy = iy0 + pr, ix = pc - a.P;
-                v[u] = f4{0.f, 0.f, 0.f, 0.f};
-                if (e < nx && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW)
-                    v[u] = *reinterpret_cast<const f4 *>(a.in + ((b * a.IH + iy) * a.IW + ix) * a.CIN + 4 * c4);
+                ok[u] = e < nx && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
+                const int64_t off = ok[u] ? ((b * a.IH + iy) * a.IW + ix) * a.CIN + 4 * c4 : 0;
+                v[u] = *reinterpret_cast<const f4 *>(a.in + off);
             }
 #pragma unroll
             for (int u = 0; u < XB; ++u) {
                 const int e = e0 + u * nthr;
-                if (e < nx) *reinterpret_cast<f4 *>(xs + (e / CQ) * a.CS + 4 * (e % CQ)) = v[u];
+                const f4 zero = {0.f, 0.f, 0.f, 0.f};
+                if (e < nx) *reinterpret_cast<f4 *>(xs + (e / CQ) * a.CS + 4 * (e % CQ)) = ok[u] ? v[u] : zero;
             }
         }
         const int nd = np4 * NQ;
         const int64_t row0 = b * ohw + (int64_t)oy0 * a.OW;
         for (int e0 = t; e0 < nd; e0 += DB * nthr) {
             f4 v[DB], yy[DB];
+            bool ok[DB];
 #pragma unroll
             for (int u = 0; u < DB; ++u) {
                 const int e = e0 + u * nthr;
                 const int n4 = e % NQ, p = e / NQ;
-                v[u] = f4{0.f, 0.f, 0.f, 0.f};
-                yy[u] = v[u];
-                if (e < nd && p < np) {
-                    const int64_t o = (row0 + p) * a.COUT + 4 * n4;
-                    v[u] = *reinterpret_cast<const f4 *>(a.g + o);
-                    if (ACT >= 0) yy[u] = *reinterpret_cast<const f4 *>(a.y + o);
-                }
+                ok[u] = e < nd && p < np;
+                const int64_t o = ok[u] ? (row0 + p) * a.COUT + 4 * n4 : 0;
+                v[u] = *reinterpret_cast<const f4 *>(a.g + o);
+                yy[u] = f4{0.f, 0.f, 0.f, 0.f};
+                if (ACT >= 0) yy[u] = *reinterpret_cast<const f4 *>(a.y + o);
             }
 #pragma unroll
             for (int u = 0; u < DB; ++u) {
                 const int e = e0 + u * nthr;
+                const f4 zero = {0.f, 0.f, 0.f, 0.f};
+                if (!ok[u]) {
+                    v[u] = zero;
+                    yy[u] = zero;
+                }
                 f4 w = v[u];
                 if (ACT >= 0) {
                     w.x = ig_grad<ACT>(w.x, yy[u].x, a.slope);
