@@ -170,7 +170,7 @@ class FusedActorCritic:
         return (self.fused_heads and self.thin0 and flat.dim() == 2 and flat.dtype == torch.float32
                 and flat.stride(1) == 1 and flat.is_cuda)
 
-    def _rep_forward(self, x, norm=None, adv=None, adv_partials=None):
+    def _rep_forward(self, x, norm=None, adv=None, adv_partials=None, defer_trunk=False):
         if isinstance(x, Rows):
             # K4's gather folded into K13's x staging (+ the advantage moments when adv_partials is given)
             lin, code, slope = self.rep[0]
@@ -180,7 +180,8 @@ class FusedActorCritic:
             # (reading them through idx again cost K13's backward 3.3 us per update)
             x.gathered = torch.empty((B, lin.in_features), dtype=torch.float32, device=x.device)
             # K16X: gather-only (h = NULL); the actor head launch forms h and writes it here
-            deferred = self.trunk_heads and self.use_trunk_heads and len(self.rep) == 1
+            # (only for forward_hidden -> loss_backward, where the K16X launches consume x.trunk; h is unwritten until then)
+            deferred = defer_trunk and self.trunk_heads and self.use_trunk_heads and len(self.rep) == 1
             if deferred:
                 x.trunk = (x.gathered, lin.weight, lin.bias, slope, h)
             _lib.check(ops.lib().xpa_thin_linear_act_fwd_gather(
@@ -302,7 +303,8 @@ class FusedActorCritic:
     def forward_hidden(self, x, adv=None, adv_partials=None):
         """Forward up to the heads' last hidden pre-activations (K12 does the rest).  x may be Rows(flat, idx); then
         adv_partials (if given) receives the minibatch's advantage moments of adv[idx] (K4's partials)."""
-        rep_outs = self._rep_forward(x, adv=adv, adv_partials=adv_partials)
+        rep_outs = self._rep_forward(x, adv=adv, adv_partials=adv_partials,
+                                     defer_trunk=self.pair is not None and self.gemm_heads)
         s = rep_outs[-1] if rep_outs else x
         if self.pair is not None and self.gemm_heads:   # K16 forms z inside the head kernels
             return (x, rep_outs, s, (([], s, None), ([], s, None)))
