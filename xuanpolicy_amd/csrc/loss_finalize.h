@@ -18,14 +18,17 @@ struct XpaLossFinalizeArgs {
 constexpr int kXpaLossPartBase = 5;
 constexpr int kXpaLossMaxAct = 64;
 
-// Every thread of the block calls it (threads >= 256 only join the barrier).  sq_out (nullable): sum of
-// d_logstd^2, written through (sc1) for a ticketed hand-off in the same launch.  s_tot / s_dls: LDS.
+// Every thread of the block calls it (blockDim.x a multiple of 64).  sq_out (nullable): sum of d_logstd^2, written
+// through (sc1) for a ticketed hand-off in the same launch.  s_tot / s_dls: LDS.
 __device__ inline void xpa_loss_finalize_body(const XpaLossFinalizeArgs &a, double *sq_out, double *s_tot,
                                               float *s_dls) {
     const int ncols = kXpaLossPartBase + (a.dist == XPA_DIST_GAUSSIAN ? a.A : 0);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (threadIdx.x < 256) {
-        for (int j = w; j < ncols; j += 4) {  // one wave per column, fixed lane order -> deterministic
+    // every wave of the block takes columns (r03: the batched finalize's 16-wave block sums C2's 11 columns in one
+    // pass — one memory round trip — instead of three passes of 4 waves)
+    const int nw = (int)(blockDim.x >> 6);
+    {
+        for (int j = w; j < ncols; j += nw) {  // one wave per column, fixed lane order -> deterministic
             double s = 0.0;
             int64_t k = lane;
             for (; k + 7 * 64 < a.n_partials; k += 8 * 64) {  // 8 loads in flight, added in k order
