@@ -56,6 +56,22 @@ def test_invalid_arguments_rejected_before_launch(lib):
                                        None, None, None, None) == 1
     assert lib.xpa_gather_minibatch(None, 8, 8, None, 4, None, None, None, None, None) == 1
     assert lib.xpa_rms_merge(None, 3, 100, 4, None, None, None, None) == 1
+    # K16X: the trunk width (d_in <= 20), the head width (<= 8) and h_out's alignment are checked before any launch
+    # (fake, 16-B aligned non-null pointers elsewhere, so only the checked argument can fail)
+    import ctypes
+    P = ctypes.c_void_p(256)
+
+    def trunk_actor(act_dim=6, d_in=17, h_out=P):
+        return lib.xpa_head_gemm_trunk_actor(0, 0, 1, 64, act_dim, 256, P, d_in, d_in, P, P, 0.01, h_out, 256, P, P,
+                                             512, P, P, 0.01, P, P, 100, P, P, P, P, 1, 0.2, 0.0, P, P, P, P, P, 16, None)
+    assert trunk_actor(d_in=21) == 1
+    assert trunk_actor(act_dim=9) == 1
+    assert trunk_actor(h_out=ctypes.c_void_p(260)) == 1
+    assert lib.xpa_head_gemm_trunk_critic(1, 64, 256, P, 21, 21, P, P, 0.01, None, 256, P, P, 512, P, P, 0.01, P, 100,
+                                          P, 0.25, P, P, P, P, P, 16, None) == 1
+    # the gather-only K13 form needs the rows output when h is NULL
+    assert lib.xpa_thin_linear_act_fwd_gather(1, P, 17, 100, P, 64, 17, 256, P, P, 0.01, None, 256, P, P, None,
+                                              None) == 1
 
 
 def test_ops_refuse_cpu_tensors():
