@@ -30,7 +30,12 @@ typedef struct ihipStream_t *xpa_stream_t; /* == hipStream_t */
  * word `err` added to xpa_per_sample / xpa_gather_minibatch / xpa_synthatari_step / xpa_maxpool_act_bwd_bias; max_norm of
  * xpa_clip_adam_step[_partials]: < 0 disables clipping, 0 zeroes the gradient (ABI 1 callers passing 0 to mean "no
  * clipping" must pass -1). */
-#define XPA_ABI_VERSION 2
+/* ABI 3 (round 4): xpa_rollout_post_deferred_norm takes (slot_src, ld_slot) after ld_final — the rows a kept
+ * truncation's bootstrap is formed from when they are not the final observations (A2C: the next, reset, observation;
+ * NULL: final_obs as before); XpaSmallRolloutArgs gains slot_reset_obs (the same choice for K32); xpa_rollout_post
+ * takes v_boot_mid after v_boot (nullable: the bootstrap values of closures before the rollout's last step, A2C's
+ * V(norm(reset_obs)); the last step's closures use v_boot). */
+#define XPA_ABI_VERSION 3
 
 /* Device-resident rollout cursor read by the per-step kernels, so a captured step replays
  * without host-side arguments changing: ptr = buffer column being written (DummyOnPolicyBuffer.ptr,
@@ -236,6 +241,7 @@ int xpa_cartpole_step(int64_t n_envs, const float *act_in, int64_t ld_act, doubl
 typedef struct XpaSmallRolloutArgs {
     int n_envs, horizon, steps, d_in, h0, h1, h2, k, act_code, use_obsnorm, n_slots, mask_returns, use_rewnorm;
     int max_episode_steps;
+    int slot_reset_obs; /* 1: a kept truncation row is the env's next (reset) observation (A2C, a2c_agent.py:88-95) */
     float slope, obs_clip, gamma, rew_range;
     uint32_t seed, env_seed;
     const float *W0, *b0, *W1, *b1, *W2, *b2, *Wa, *ba, *Wc, *bc;
@@ -289,7 +295,8 @@ int xpa_dqn_td_loss(int64_t batch, int64_t n_actions, const float *evalQ, int64_
  * 0 before the first call (the kernel leaves it at 0). */
 int64_t xpa_rollout_post_num_blocks(int64_t n_envs);
 int xpa_rollout_post(int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term,
-                     const uint8_t *trunc, const float *v_boot, xpa_cursor_t *cursor, float *ret_mean,
+                     const uint8_t *trunc, const float *v_boot, const float *v_boot_mid, xpa_cursor_t *cursor,
+                     float *ret_mean,
                      float *ret_var, double *ret_count, float *returns, float *buf_rew, float *buf_term,
                      uint8_t *buf_closed, float *buf_boot, float gamma, int mask_returns, int use_rewnorm,
                      float rew_range, int atari_lifeloss, double *partials, uint32_t *ticket,
@@ -582,9 +589,13 @@ int xpa_rollout_post_deferred(int64_t n_envs, int64_t horizon, const float *rew,
 /* xpa_rollout_post_deferred with the normalisation of the final observations folded in: final_obs holds
  * the RAW observations; a kept truncation row is normalised with obs_mean / obs_var (clip obs_clip,
  * xpa_obs_normalize's arithmetic) into slot_obs, and at the rollout's last step every env's normalised
- * final observation is written into boot_norm [n_envs, ld_norm] (the input of the deferred critic pass). */
+ * final observation is written into boot_norm [n_envs, ld_norm] (the input of the deferred critic pass).
+ * slot_src [n_envs, ld_slot] (nullable, RAW): the rows kept truncations are formed from instead of final_obs — the
+ * env's next (reset) observations for A2C, whose critic call sees obs[i] = reset_obs (a2c_agent.py:88-95); the
+ * last step's boot_norm rows are final_obs either way (the full-buffer closures, a2c_agent.py:67-72). */
 int xpa_rollout_post_deferred_norm(int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term,
-                                   const uint8_t *trunc, const float *final_obs, int64_t ld_final, int64_t obs_dim,
+                                   const uint8_t *trunc, const float *final_obs, int64_t ld_final,
+                                   const float *slot_src, int64_t ld_slot, int64_t obs_dim,
                                    const float *obs_mean, const float *obs_var, float obs_clip, float *boot_norm,
                                    int64_t ld_norm, float *slot_obs, int32_t *slot_t, int64_t n_slots,
                                    int32_t *overflow, xpa_cursor_t *cursor, float *ret_mean, float *ret_var,

@@ -624,6 +624,8 @@ class AgentLoopRef:
                 if terms[i] or truncs[i]:
                     self.ret_rms.update(self.returns[i:i + 1])
                     self.returns[i] = 0.0
+                    if self.algo == "a2c":   # a2c_agent.py:88-95: reset_obs replaces the row before the critic call
+                        obs[i] = infos[i]["reset_obs"]
                     if terms[i]:
                         self.memory.finish_path(0.0, i)
                     else:
@@ -631,6 +633,110 @@ class AgentLoopRef:
                         self.memory.finish_path(bv[i], i)
                     obs[i] = infos[i]["reset_obs"]
         self.obs = obs
+
+
+class VecAgentRef:
+    """The reference's on-policy train() loop over a host VecEnv, step for step: ppoclip_agent.py:59-111 (algo "ppo")
+    and a2c_agent.py:57-107 (algo "a2c") with agent.py:104-123's observation / reward processing — the loop a user of
+    the reference runs over DummyVecEnv_Gym / SubprocVecEnv_Gym (envs: buf_obs + step(acts) -> (obs, rew, term, trunc,
+    infos with reset_obs), e.g. synth_env.DummyVecEnvRef).
+
+    Two hooks replace what a replay cannot reproduce: action_source(obs) -> the actions to take (the device agent's
+    recorded draws; the reference samples torch's CPU generator), and on_full(self) runs where the reference runs
+    its n_epoch x n_minibatch updates (after the full-buffer finish_path calls, before memory.clear(); the tests
+    snapshot the buffer there and replay the updates with the device permutations).  The policy computes values and
+    the log-probabilities of the given actions (`heads(obs)` / `dist(head, logstd)`, f64 in the tests).
+
+    The loop's quirks are kept, since a drop-in must reproduce them:
+      * every train() call restarts from envs.buf_obs (ppoclip_agent.py:60): rows of envs that ended on the previous
+        call's last step still hold their final observation there;
+      * without obs-norm, `obs` is envs.buf_obs itself on a call's first step, and the store runs after envs.step,
+        so a vec env that writes buf_obs in place (DummyVecEnv) has that column hold the post-step observations;
+      * A2C replaces obs[i] (= next_obs[i]) by reset_obs BEFORE the critic call of a mid-rollout truncation, so the
+        bootstrap is V(norm(reset_obs)) (a2c_agent.py:88-95); PPO calls the critic first: V(norm(final obs))
+        (ppoclip_agent.py:95-101); the full-buffer closures use V(norm(next_obs)) before either (:69-75);
+      * Atari (env_name "Atari"): a terminal without truncation (a life loss) keeps the path open and the obs
+        (ppoclip_agent.py:93-94); ret_rms / the return tracker still see it;
+      * returns: PPO masks with (1 - terminal) (ppoclip_agent.py:87), A2C does not (a2c_agent.py:82)."""
+
+    def __init__(self, envs, policy, algo, n_steps, action_source, on_full=None, gamma=0.99, gae_lambda=0.95,
+                 use_gae=True, use_advnorm=True, use_obsnorm=True, use_rewnorm=True, obsnorm_range=5.0,
+                 rewnorm_range=5.0, atari=False, discrete=False):
+        self.envs, self.policy, self.algo = envs, policy, algo
+        self.action_source, self.on_full = action_source, on_full
+        self.n_envs, self.n_steps = envs.num_envs, n_steps
+        self.gamma, self.atari, self.discrete = gamma, atari, discrete
+        self.use_obsnorm, self.use_rewnorm = use_obsnorm, use_rewnorm
+        self.obsnorm_range, self.rewnorm_range = obsnorm_range, rewnorm_range
+        obs_shape = tuple(envs.observation_space.shape)
+        act_shape = () if discrete else tuple(envs.action_space.shape)
+        aux = {"old_logp": ()} if algo == "ppo" else {}
+        self.memory = BufferRef(obs_shape, act_shape, aux, self.n_envs, n_steps, use_gae, use_advnorm, gamma, gae_lambda,
+                                obs_dtype=np.uint8 if atari else np.float32)
+        self.obs_rms = RunningMeanStdRef(obs_shape)
+        self.ret_rms = RunningMeanStdRef(())
+        self.returns = np.zeros((self.n_envs,), np.float32)
+        self.current_step = 0
+
+    def _proc_obs(self, obs):
+        return process_observation(obs, self.obs_rms, self.obsnorm_range) if self.use_obsnorm else obs
+
+    def _proc_rew(self, rew):
+        return process_reward(rew, self.ret_rms, self.rewnorm_range) if self.use_rewnorm else rew
+
+    def _eval(self, obs, acts=None):
+        """(values, log-probs of acts or None) — the critic / distribution part of _action (ppoclip_agent.py:50-57)."""
+        torch = _torch()
+        dt = next(self.policy.parameters()).dtype
+        x = obs if (isinstance(obs, np.ndarray) and obs.dtype == np.uint8) else torch.as_tensor(np.asarray(obs), dtype=dt)
+        with torch.no_grad():
+            head, logstd, v = self.policy.heads(x)
+            lp = None
+            if acts is not None:
+                d = self.policy.dist(head, logstd)
+                a = torch.as_tensor(np.asarray(acts))
+                lp = d.log_prob(a.long()) if self.discrete else d.log_prob(a.to(dt)).sum(-1)
+                lp = lp.numpy()
+        return v.numpy(), lp
+
+    def train(self, train_steps):
+        obs = self.envs.buf_obs
+        for _ in range(train_steps):
+            if self.use_obsnorm:   # RunningMeanStd.update only matters with obs-norm (its statistics are unused else)
+                self.obs_rms.update(obs)
+            obs = self._proc_obs(obs)
+            acts = self.action_source(obs)
+            value, logps = self._eval(obs, acts)
+            next_obs, rewards, terminals, truncs, infos = self.envs.step(acts)
+            aux = {"old_logp": logps} if self.algo == "ppo" else None
+            self.memory.store(obs, acts, self._proc_rew(rewards), value, terminals, aux)
+            if self.memory.full:
+                vals, _ = self._eval(self._proc_obs(next_obs))
+                for i in range(self.n_envs):
+                    self.memory.finish_path(0.0 if terminals[i] else vals[i], i)
+                if self.on_full is not None:
+                    self.on_full(self)
+                self.memory.clear()
+            if self.algo == "ppo":
+                self.returns = (1 - terminals) * self.gamma * self.returns + rewards
+            else:
+                self.returns = self.gamma * self.returns + rewards
+            obs = next_obs
+            for i in range(self.n_envs):
+                if terminals[i] or truncs[i]:
+                    self.ret_rms.update(self.returns[i:i + 1])
+                    self.returns[i] = 0.0
+                    if self.atari and not truncs[i]:
+                        continue
+                    if self.algo == "a2c":
+                        obs[i] = infos[i]["reset_obs"]
+                    if terminals[i]:
+                        self.memory.finish_path(0.0, i)
+                    else:
+                        vals, _ = self._eval(self._proc_obs(next_obs))
+                        self.memory.finish_path(vals[i], i)
+                    obs[i] = infos[i]["reset_obs"]
+            self.current_step += self.n_envs
 
 
 # ---------------------------------------------------------------------------------------------------------------

@@ -173,6 +173,56 @@ class SynthBoxEnv:
         return s.copy(), r, term, trunc, info
 
 
+class DummyVecEnvRef:
+    """DummyVecEnv_Gym / DummyVecEnv_Atari (xuance/environment/gym/gym_vec_env.py:148-231) restated over a list of
+    env objects with the step contract above: the host VecEnv a reference user hands the agent.
+
+      reset()      every env, rows saved into buf_obs (gym_vec_env.py:177-182)
+      step(acts)   env e steps with acts[e]; a done env (terminated or truncated) is reset and its first observation
+                   goes to infos[e]["reset_obs"]; buf_obs[e] = the step's observation (the final one of a done env)
+                   is written IN PLACE; copies of buf_obs / rewards / flags / infos are returned (:201-212)
+
+    buf_obs is one array for the object's life (float32, uint8 with atari=True), so an agent that keeps a reference
+    to it across envs.step (ppoclip_agent.py:60 `obs = self.envs.buf_obs`) sees the step's writes — the reference's
+    first-store alias.  record: every action array passed to step() is appended to .actions (the tests hand the
+    device agent's draws to the oracle loop)."""
+
+    def __init__(self, envs, observation_space=None, action_space=None, atari=False):
+        self.envs = list(envs)
+        self.num_envs = len(self.envs)
+        e0 = self.envs[0]
+        self.observation_space = observation_space if observation_space is not None else e0.observation_space
+        self.action_space = action_space if action_space is not None else e0.action_space
+        self.obs_shape = tuple(self.observation_space.shape)
+        self.buf_obs = np.zeros((self.num_envs,) + self.obs_shape, np.uint8 if atari else np.float32)
+        self.buf_dones = np.zeros((self.num_envs,), bool)
+        self.buf_trunctions = np.zeros((self.num_envs,), bool)
+        self.buf_rews = np.zeros((self.num_envs,), np.float32)
+        self.buf_infos = [{} for _ in range(self.num_envs)]
+        self.max_episode_length = getattr(e0, "max_episode_steps", 1000)
+        self.actions = []
+
+    def reset(self):
+        for e, env in enumerate(self.envs):
+            obs, info = env.reset()
+            self.buf_obs[e] = obs
+            self.buf_infos[e] = info
+        return self.buf_obs.copy(), list(self.buf_infos)
+
+    def step(self, actions):
+        self.actions.append(np.array(actions, copy=True))
+        for e, env in enumerate(self.envs):
+            obs, self.buf_rews[e], self.buf_dones[e], self.buf_trunctions[e], self.buf_infos[e] = env.step(actions[e])
+            if self.buf_dones[e] or self.buf_trunctions[e]:
+                self.buf_infos[e]["reset_obs"], _ = env.reset()
+            self.buf_obs[e] = obs
+        return (self.buf_obs.copy(), self.buf_rews.copy(), self.buf_dones.copy(), self.buf_trunctions.copy(),
+                list(self.buf_infos))
+
+    def close(self):
+        pass
+
+
 class SynthBoxVec:
     """numpy-vectorised variant of the same env ('second CPU variant with the env
     vectorised in numpy').  Same semantics as N SynthBoxEnv instances in a DummyVecEnv."""

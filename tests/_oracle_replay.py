@@ -18,17 +18,36 @@ import torch
 from oracle import cpu_ref
 
 
-def replay_last_step_iteration(agent, D, A, hidden, discrete, algo, ent, n_epoch, n_mb, expect_mid_truncations=False):
+def _load_by_order(pol, agent):
+    """The agent's parameters into the oracle policy in state_dict order (the CNN oracle names its critic head
+    differently from the reference; the order is the reference's)."""
+    src = [v.detach().cpu() for v in agent.policy.state_dict().values()]
+    keys = list(pol.state_dict().keys())
+    assert len(src) == len(keys)
+    pol.load_state_dict(dict(zip(keys, src)))
+
+
+def _obs_input(obs):
+    """Buffer observations as the oracle policy takes them: uint8 frames as numpy (the policy scales them), else f64."""
+    return obs if obs.dtype == np.uint8 else torch.as_tensor(obs.astype(np.float64))
+
+
+def replay_last_step_iteration(agent, D, A, hidden, discrete, algo, ent, n_epoch, n_mb, expect_mid_truncations=False,
+                               pol=None):
+    """pol: the oracle policy to replay with (default: the MLP actor-critic of `hidden`); it is loaded with the agent's
+    weights here.  The deferred-bootstrap checks run when the agent defers them (device envs); a host VecEnv's
+    per-step bootstraps are checked against the reference loop by tests/test_gpu_hostenv.py."""
     N, T = agent.n_envs, agent.n_steps
     cfg = agent.config
-    pol = cpu_ref.build_actor_critic_ref(D, A, hidden, hidden, hidden, discrete=discrete,
-                                         activation=getattr(cfg, "activation", "LeakyReLU"))
-    pol.load_state_dict({k: v.detach().cpu() for k, v in agent.policy.state_dict().items()})
+    if pol is None:
+        pol = cpu_ref.build_actor_critic_ref(D, A, hidden, hidden, hidden, discrete=discrete,
+                                             activation=getattr(cfg, "activation", "LeakyReLU"))
+    _load_by_order(pol, agent)
     pol.double()
     # the optimizer / schedule state the updates of this iteration start from (Adam moments + step, LinearLR)
-    opt_state = {n: {k: (v.detach().cpu().clone() if isinstance(v, torch.Tensor) else v)
-                     for k, v in agent.learner.optimizer.state[p].items()}
-                 for n, p in agent.policy.named_parameters()}
+    opt_state = [{k: (v.detach().cpu().clone() if isinstance(v, torch.Tensor) else v)
+                  for k, v in agent.learner.optimizer.state[p].items()}
+                 for p in agent.policy.parameters()]   # in parameter order (= the oracle's)
     lr0 = agent.learner.optimizer.param_groups[0]["lr"]
     sched_epoch = agent.learner.scheduler.last_epoch
     perm_counter = agent._perm_counter
@@ -39,10 +58,11 @@ def replay_last_step_iteration(agent, D, A, hidden, discrete, algo, ent, n_epoch
     gamma, lam = float(mem.gamma), float(mem.gae_lam)
 
     # ---- rollout: values and old log-probs at the iteration's weights (f64 oracle) ----
-    obs = mem.observations.cpu().numpy().astype(np.float64)
+    obs_np = mem.observations.cpu().numpy()
+    obs_shape = tuple(obs_np.shape[2:])
     act = mem.actions.cpu().numpy().astype(np.float64)
     with torch.no_grad():
-        head, logstd, v = pol.heads(torch.as_tensor(obs.reshape(N * T, D)))
+        head, logstd, v = pol.heads(_obs_input(obs_np.reshape((N * T,) + obs_shape)))
         d = pol.dist(head, logstd)
         if discrete:
             lp = d.log_prob(torch.as_tensor(act.reshape(N * T)).long())
@@ -57,6 +77,19 @@ def replay_last_step_iteration(agent, D, A, hidden, discrete, algo, ent, n_epoch
     term = mem.terminals.cpu().numpy()
     closed = mem.closed.cpu().numpy().astype(bool)
     boot = mem.boot.cpu().numpy()
+    if agent.defer_boot:
+        _check_deferred(agent, pol, N, T, term, closed, boot, expect_mid_truncations)
+
+    # ---- GAE (north_star: 1e-5 on advantages / returns) ----
+    adv, ret = cpu_ref.gae_rows(mem.rewards.cpu().numpy(), mem.values.cpu().numpy(), term, closed.astype(np.uint8),
+                                boot, gamma, lam)
+    np.testing.assert_allclose(mem.advantages.cpu().numpy(), adv, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(mem.returns.cpu().numpy(), ret, rtol=1e-5, atol=1e-5)
+    replay_updates(agent, pol, opt_state, lr0, sched_epoch, perm_counter, adv, ret, discrete, A, algo, ent, n_epoch,
+                   n_mb)
+
+
+def _check_deferred(agent, pol, N, T, term, closed, boot, expect_mid_truncations):
     with torch.no_grad():
         v_last = pol.heads(torch.as_tensor(agent.boot_obs.cpu().numpy().astype(np.float64)))[2].numpy()
         v_slot = pol.heads(torch.as_tensor(agent.slot_obs.cpu().numpy().astype(np.float64)))[2].numpy()
@@ -73,29 +106,32 @@ def replay_last_step_iteration(agent, D, A, hidden, discrete, algo, ent, n_epoch
     assert (k_of < S).all(), "more mid-buffer truncations than deferred slots"
     np.testing.assert_allclose(boot[rows, cols], v_slot[k_of * N + rows], rtol=1e-4, atol=1e-4)
 
-    # ---- GAE (north_star: 1e-5 on advantages / returns) ----
-    adv, ret = cpu_ref.gae_rows(mem.rewards.cpu().numpy(), mem.values.cpu().numpy(), term, closed.astype(np.uint8),
-                                boot, gamma, lam)
-    np.testing.assert_allclose(mem.advantages.cpu().numpy(), adv, rtol=1e-5, atol=1e-5)
-    np.testing.assert_allclose(mem.returns.cpu().numpy(), ret, rtol=1e-5, atol=1e-5)
 
-    # ---- updates: the oracle learner replays the buffer with the device permutations ----
+def replay_updates(agent, pol, opt_state, lr0, sched_epoch, perm_counter, adv, ret, discrete, A, algo, ent, n_epoch,
+                   n_mb):
+    """The oracle learner replays the agent's buffer (with adv / ret given) using the device permutations, from the
+    Adam / LinearLR state the iteration's updates started from: every update's loss scalars and the final weights."""
+    N, T = agent.n_envs, agent.n_steps
+    cfg, mem = agent.config, agent.memory
     pol.float()
     opt = torch.optim.Adam(pol.parameters(), cfg.learning_rate, eps=1e-5)
     sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.0, total_iters=cfg.running_steps)
     # continue from the agent's Adam moments and LinearLR position (it steps once per update,
     # ppoclip_learner.py:50-51)
-    named = dict(pol.named_parameters())
-    for n, st in opt_state.items():
+    params = list(pol.parameters())
+    assert len(params) == len(opt_state)
+    for p, st in zip(params, opt_state):
         if st:
-            opt.state[named[n]] = {"step": torch.tensor(float(st["step"])), "exp_avg": st["exp_avg"].float().clone(),
+            opt.state[p] = {"step": torch.tensor(float(st["step"])), "exp_avg": st["exp_avg"].float().clone(),
                                    "exp_avg_sq": st["exp_avg_sq"].float().clone()}
     opt.param_groups[0]["lr"] = lr0
     sch.last_epoch = sched_epoch
     clip = cfg.clip_grad_norm if algo == "ppo" else cfg.clip_grad
     lrn = cpu_ref.LearnerRef(pol, opt, sch, algo, cfg.vf_coef, ent, getattr(cfg, "clip_range", 0.2), clip, True)
-    buf = cpu_ref.BufferRef((D,), () if discrete else (A,), {"old_logp": ()} if algo == "ppo" else {}, N, T)
-    buf.observations[:] = mem.observations.cpu().numpy()
+    obs_np = mem.observations.cpu().numpy()
+    buf = cpu_ref.BufferRef(obs_np.shape[2:], () if discrete else (A,), {"old_logp": ()} if algo == "ppo" else {}, N, T,
+                            obs_dtype=obs_np.dtype)
+    buf.observations[:] = obs_np
     buf.actions[:] = mem.actions.cpu().numpy()
     buf.values[:] = mem.values.cpu().numpy()
     buf.returns[:], buf.advantages[:] = ret, adv
@@ -119,6 +155,5 @@ def replay_last_step_iteration(agent, D, A, hidden, discrete, algo, ent, n_epoch
             if algo == "ppo":
                 assert abs(got[4] - info["clip_ratio"]) <= 2.0 / B + 1e-7, ("clip_ratio", u, got[4], info["clip_ratio"])
             u += 1
-    for k, val in agent.policy.state_dict().items():
-        np.testing.assert_allclose(val.detach().cpu().numpy(), pol.state_dict()[k].numpy(), rtol=1e-3, atol=1e-4,
-                                   err_msg=k)
+    for (k, val), ref in zip(agent.policy.state_dict().items(), pol.state_dict().values()):
+        np.testing.assert_allclose(val.detach().cpu().numpy(), ref.numpy(), rtol=1e-3, atol=1e-4, err_msg=k)

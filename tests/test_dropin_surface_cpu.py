@@ -79,3 +79,78 @@ def test_jsonl_logger(tmp_path):
     rec = json.loads(open(tmp_path / "log" / "scalars.jsonl").read().strip())
     assert rec == {"step": 7, "a": 1.5, "Episode-Steps/env-0": 3.0}
     assert _make_writer("none", str(tmp_path)) is None
+
+
+def _layer_sig(layers):
+    return [(lin.in_features, lin.out_features, code, slope) for lin, code, slope in layers]
+
+
+@pytest.mark.parametrize("discrete", [False, True])
+def test_reference_policy_objects_take_the_fast_path_plan(discrete):
+    """examples/ppo/ppo_mujoco.py:43-58 builds the policy from the REFERENCE's classes (xuance.torch.representations
+    .Basic_MLP + xuance.torch.policies.Gaussian_AC_Policy / Categorical_AC_Policy, which carry no `discrete`
+    attribute).  The fast-path planner recognises networks by structure, so those objects get the same layer parse,
+    the same fused-head / K13 / paired-hidden-layer plan and the same flat-buffer placement as the mirror classes —
+    the device agent's fused update, not the generic fallback.  Imports the reference in this container only."""
+    if not os.path.isdir("/root/reference"):
+        pytest.skip("reference not mounted")
+    import torch
+    from tests.golden.ref_loader import import_reference
+    import_reference()
+    import gym
+    from xuance.torch.policies import Categorical_AC_Policy as RefCat, Gaussian_AC_Policy as RefGauss
+    from xuance.torch.representations import Basic_MLP as RefMLP
+    from xuance.torch.utils import ActivationFunctions as RefAct
+    from xuanpolicy_amd.fused_mlp import FusedActorCritic, head_placement
+    from xuanpolicy_amd.policies import (ActivationFunctions, Basic_MLP, Categorical_AC_Policy, Gaussian_AC_Policy,
+                                         policy_discrete)
+    space = gym.spaces.Discrete(4) if discrete else gym.spaces.Box(-1, 1, (6,))
+    init = torch.nn.init.orthogonal_
+
+    def build(mlp, pol_cls, acts):
+        rep = mlp(input_shape=(17,), hidden_sizes=[256], normalize=None, initialize=init, activation=acts["LeakyReLU"],
+                  device="cpu")
+        return pol_cls(action_space=space, representation=rep, actor_hidden_size=[256], critic_hidden_size=[256],
+                       normalize=None, initialize=init, activation=acts["LeakyReLU"], device="cpu")
+    ref = build(RefMLP, RefCat if discrete else RefGauss, RefAct)
+    ours = build(Basic_MLP, Categorical_AC_Policy if discrete else Gaussian_AC_Policy, ActivationFunctions)
+    assert not hasattr(ref, "discrete") and policy_discrete(ref) == policy_discrete(ours) == discrete
+    assert list(ref.state_dict().keys()) == list(ours.state_dict().keys())
+    fr, fo = FusedActorCritic(ref), FusedActorCritic(ours)
+    for part in ("rep", "actor", "critic"):
+        assert _layer_sig(getattr(fr, part)) == _layer_sig(getattr(fo, part)), part
+    for flag in ("discrete", "fused_heads", "thin0", "trunk_heads"):
+        assert getattr(fr, flag) == getattr(fo, flag), flag
+    assert fr.fused_heads and fr.thin0   # the C2 plan: K13 trunk + fused heads (K16 once the flat buffers pair them)
+    hr, ho = head_placement(ref), head_placement(ours)
+    assert len(hr) == len(ho) == 2
+    assert [[tuple(t.shape) for t in g] for g in hr] == [[tuple(t.shape) for t in g] for g in ho]
+    assert hr[0][0] is ref.actor.model[0].weight if discrete else hr[0][0] is ref.actor.mu[0].weight
+    assert hr[0][1] is ref.critic.model[0].weight
+
+
+def test_integration_patch_rebinds_the_example_imports():
+    """INTEGRATION.md's patch for xuance/torch/agents/__init__.py rebinds the module attributes the example imports
+    (`from xuance.torch.agents import PPOCLIP_Agent, get_total_iters`, ppo_mujoco.py:61) besides REGISTRY, so the
+    unmodified example reaches the device agent.  Applied here to the imported reference module (this container)."""
+    if not os.path.isdir("/root/reference"):
+        pytest.skip("reference not mounted")
+    from tests.golden.ref_loader import import_reference
+    import_reference()
+    import xuance.torch.agents as ref_agents
+    import xuanpolicy_amd.agents as amd
+    src = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    block = src.split("```python\n# xuance/torch/agents/__init__.py", 1)[1].split("```", 1)[0].split("\n", 1)[1]
+    saved = {k: getattr(ref_agents, k) for k in ("PPOCLIP_Agent", "A2C_Agent", "get_total_iters")}
+    saved_reg = dict(ref_agents.REGISTRY)
+    try:
+        exec(compile(block, "INTEGRATION.md", "exec"), ref_agents.__dict__)
+        from xuance.torch.agents import A2C_Agent, PPOCLIP_Agent, get_total_iters   # the example's import line
+        assert PPOCLIP_Agent is amd.PPOCLIP_Agent and A2C_Agent is amd.A2C_Agent
+        assert get_total_iters is amd.get_total_iters
+        assert ref_agents.REGISTRY["PPO_Clip"] is amd.PPOCLIP_Agent and ref_agents.REGISTRY["A2C"] is amd.A2C_Agent
+    finally:
+        for k, v in saved.items():
+            setattr(ref_agents, k, v)
+        ref_agents.REGISTRY.clear()
+        ref_agents.REGISTRY.update(saved_reg)

@@ -141,6 +141,43 @@ def test_graph_capture_failure_falls_back_to_eager():
         np.testing.assert_allclose(b, a, rtol=1e-6, atol=1e-7)
 
 
+def test_epoch_graph_capture_failure_falls_back_to_slot_graphs():
+    """a failure inside the whole-epoch capture (learners.update_epoch, after every slot graph exists)
+    restores the learner's workspace / partial buffers and continues on the slot graphs — the parameters equal a run
+    that never tried the epoch graph."""
+    from xuanpolicy_amd import ops
+    from xuanpolicy_amd.runner import build_cartpole_ppo
+    out = []
+    for inject in (False, True):
+        agent = build_cartpole_ppo(n_envs=8, n_steps=100, hidden=64, seed=4, device=DEV, n_minibatch=6, n_epoch=4)
+        agent.learner.small_updates = False
+        fm = agent.learner._fused_mlp()
+        state = {"raised": 0}
+        if inject:
+            real = ops.ColsumQueue.flush
+
+            def flaky(self, *a, **k):
+                slots = agent.learner.__dict__.get("_slot_graphs", {})
+                if (torch.cuda.is_current_stream_capturing() and not state["raised"]
+                        and sum(isinstance(v, tuple) for v in slots.values()) == 7):
+                    state["raised"] = 1
+                    raise RuntimeError("injected epoch-capture failure")
+                return real(self, *a, **k)
+            fm._cq.flush = flaky.__get__(fm._cq)
+        else:
+            agent.learner.graph_epochs = False
+        for _ in range(2):
+            agent.train(100, log=False)
+        torch.cuda.synchronize()
+        assert not agent.learner.graph_epochs
+        assert not agent.learner.__dict__.get("_epoch_graphs")
+        if inject:
+            assert state["raised"] == 1 and not getattr(agent.learner, "_graph_failed", False)
+        out.append([p.detach().cpu().numpy().copy() for p in agent.policy.parameters()])
+    for a, b in zip(*out):
+        np.testing.assert_allclose(b, a, rtol=1e-6, atol=1e-7)
+
+
 def test_graphed_k9_schedule_windows(monkeypatch):
     """K9 captured in the slot graphs reads (lr, Adam step) from the device schedule (xpa_clip_adam_step_sched): with a
     24-update window the table is refilled five times inside two iterations (128 updates) and the LinearLR decay is
@@ -216,19 +253,22 @@ def test_small_mlp_epoch_graphs_match_eager(n_steps, n_mb):
         np.testing.assert_array_equal(b, a)
 
 
-@pytest.mark.parametrize("agent_name,hidden,obsnorm", [("PPO_Clip", 64, True), ("A2C", 64, True), ("PPO_Clip", 32, True),
-                                                       ("PPO_Clip", 64, False)])
-def test_fused_rollout_matches_multi_kernel_steps(agent_name, hidden, obsnorm):
+@pytest.mark.parametrize("agent_name,hidden,obsnorm,n_envs", [("PPO_Clip", 64, True, 8), ("A2C", 64, True, 8),
+                                                               ("PPO_Clip", 32, True, 8), ("PPO_Clip", 64, False, 8),
+                                                               ("PPO_Clip", 64, True, 100), ("A2C", 64, True, 256)])
+def test_fused_rollout_matches_multi_kernel_steps(agent_name, hidden, obsnorm, n_envs):
     """K32 (xpa_small_rollout_cartpole: obs RMS + normalise + MLP forward + sample + CartPole step + K8 post in one
     launch) against the multi-kernel step (K5, obs_normalize, the torch forward, K3, K18, K8) from the same start:
     iteration 1's 128 steps as ONE K32 launch, then an update, then 127 single-step launches (time limit 40: mid-buffer
-    truncations fill the deferred slots).  Everything but the forward is the same arithmetic, so the actions, buffer
+    truncations fill the deferred slots).  n_envs 100 / 256 run K32's N > 64 branches (the row-group obs-RMS sums and
+    the block-sum ret_rms merge); A2C keeps the reset observations in its slots (a2c_agent.py:88-95) on both paths.
+    Everything but the forward is the same arithmetic, so the actions, buffer
     observations, rewards / closures, slots, RMS statistics, returns and env state are bit-identical; the stored
     values / log-probs agree within the f32 reassociation of the two forwards."""
     from xuanpolicy_amd.runner import build_cartpole_ppo
     res = []
     for fused in (True, False):
-        agent = build_cartpole_ppo(n_envs=8, n_steps=128, hidden=hidden, seed=9, device=DEV, max_episode_steps=40,
+        agent = build_cartpole_ppo(n_envs=n_envs, n_steps=128, hidden=hidden, seed=9, device=DEV, max_episode_steps=40,
                                    agent=agent_name, fused_rollout=fused, clip_grad=0.5, use_obsnorm=obsnorm)
         assert agent.defer_boot and agent.n_slots == 4
         agent.train(128 + 127, log=False)
@@ -244,7 +284,7 @@ def test_fused_rollout_matches_multi_kernel_steps(agent_name, hidden, obsnorm):
             ep_index=env.ep_index, ep_score=env.ep_score, cursor=agent.cursor, obs_norm=agent.obs_norm,
             val=mem.values, logp=logp).items()})
     f, m = res
-    assert (f["slot_t"] >= 0).sum() > 0 and f["closed"][:, :127].sum() > 8
+    assert (f["slot_t"] >= 0).sum() > 0 and f["closed"][:, :127].sum() > n_envs
     for k in f:
         if k in ("val", "logp"):
             np.testing.assert_allclose(f[k][:, :127], m[k][:, :127], rtol=1e-4, atol=1e-5, err_msg=k)
@@ -275,3 +315,38 @@ def test_small_mlp_split_matches_one_workgroup(n_steps, n_mb):
         np.testing.assert_allclose(a[:6], b[:6], rtol=1e-4, atol=1e-5, err_msg="update %d" % u)
     for a, b in zip(par_s, par_o):
         np.testing.assert_allclose(a, b, rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("small", [True, False])
+def test_graphed_k9_follows_lr_changes_outside_the_scheduler(small):
+    """the device (lr, Adam step) table read by the captured K9 (and by K30, eager or captured) is refilled
+    when the learning rate changes outside scheduler.step() inside a live window — here an edited param_groups lr and
+    a replaced scheduler after the first iteration.  Reference: the eager multi-kernel update, whose K9 takes the host
+    lr every step.  The captured multi-kernel path must match it to rounding; K30 (other arithmetic) to 1e-2 — a stale
+    table (the old, decayed lr for 64 updates) moves the weights by ~1e-2 absolute."""
+    from xuanpolicy_amd.runner import build_cartpole_ppo
+    out = []
+    for sm, graphed in ((False, False), (small, True)):
+        agent = build_cartpole_ppo(n_envs=8, n_steps=128, hidden=64, seed=5, device=DEV, graph_update=graphed)
+        agent.learner.small_updates = sm
+        agent.train(128, log=False)
+        opt = agent.learner.optimizer
+        for g in opt.param_groups:
+            g["lr"] = 1e-3
+        agent.learner.scheduler = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.25,
+                                                                    total_iters=300)
+        agent.train(128, log=False)
+        torch.cuda.synchronize()
+        fo = agent.learner.fused_opt
+        if fo.sched_enabled:
+            assert not fo.sched_overflow()
+            assert fo._sched_lrs[fo.step_count - fo._sched_start] == opt.param_groups[0]["lr"]
+        out.append(([p.detach().cpu().numpy().copy() for p in agent.policy.parameters()],
+                    opt.param_groups[0]["lr"]))
+    (pa, la), (pb, lb) = out
+    assert la == lb and la < 1e-3
+    for a, b in zip(pa, pb):
+        if small:
+            np.testing.assert_allclose(b, a, rtol=1e-2, atol=1e-3)
+        else:
+            np.testing.assert_allclose(b, a, rtol=1e-6, atol=1e-7)

@@ -111,8 +111,10 @@ def test_perdqn_learner_replays_reference(golden, fixture, conv_path):
 
 @pytest.mark.parametrize("filters", [[8, 8], [32, 64]])
 def test_perdqn_agent_loop_on_device(filters, conv_path):
-    """[8, 8]: MIOpen's NHWC kernels for every conv (the r02 intermittent-fault configuration); [32, 64]: the production
-    first two convs (K25 / K26 / K27 + MIOpen's conv2 weight gradient).  Every device error word stays 0."""
+    """[8, 8]: the r02 intermittent-fault configuration (4 / 8-channel convs), which since r03 runs K28 / K29 for every
+    conv — the small-channel MIOpen route it faulted on is refused (fused_cnn._library_conv_guard, tested below);
+    [32, 64]: the production first two convs (K25 / K26 / K27; conv2's weight gradient on K29 or MIOpen per
+    conv_path).  Every device error word stays 0."""
     from xuanpolicy_amd.runner import build_perdqn
     agent = build_perdqn(n_envs=4, n_size=256, batch_size=64, device=DEV, start_training=64, sync_frequency=20,
                          filters=filters, kernels=[8, 4], strides=[4, 2], q_hidden_size=[32], max_episode_steps=40)
@@ -206,3 +208,21 @@ def test_perdqn_agent_train_replays_reference(golden, conv_path):
     np.testing.assert_allclose(mem.max_priority.cpu().numpy(), g["max_priority"], rtol=1e-4)
     for key, v in agent.policy.state_dict().items():
         np.testing.assert_allclose(v.cpu().numpy(), g["sd1/" + key], rtol=1e-3, atol=5e-5, err_msg=key)
+
+
+def test_small_channel_library_conv_is_refused():
+    """use_igemm off on a net with 8-channel convs: the explicit CNN path raises instead of calling MIOpen's NHWC kernels
+    for those shapes (the r02 fault suspect)."""
+    from xuanpolicy_amd import fused_cnn
+    from xuanpolicy_amd.runner import build_perdqn
+    agent = build_perdqn(n_envs=2, n_size=64, batch_size=16, device=DEV, start_training=16, filters=[8, 8],
+                         kernels=[8, 4], strides=[4, 2], q_hidden_size=[32], max_episode_steps=40)
+    fq = agent.learner._fused_q()
+    assert fq is not None
+    old = fused_cnn._Trunk.use_igemm
+    fused_cnn._Trunk.use_igemm = False
+    try:
+        with pytest.raises(RuntimeError, match="small-channel MIOpen route"):
+            agent.learner.q_values(agent.envs.obs)
+    finally:
+        fused_cnn._Trunk.use_igemm = old

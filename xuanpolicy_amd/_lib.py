@@ -20,7 +20,7 @@ SOURCES = ["gae.hip", "loss.hip", "rollout.hip", "optim.hip", "mlp.hip", "head.h
            "classic.hip", "dqn.hip", "conv.hip", "igemm.hip", "smallmlp.hip"]
 HEADER = os.path.join(REPO_DIR, "include", "xuanpolicy_amd.h")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 c_i32, c_i64, c_u32, c_f32, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
 
@@ -45,7 +45,7 @@ class XpaSmallRolloutArgs(ctypes.Structure):
     """include/xuanpolicy_amd.h XpaSmallRolloutArgs (K32), field for field."""
     _fields_ = ([(n, ctypes.c_int) for n in ("n_envs", "horizon", "steps", "d_in", "h0", "h1", "h2", "k", "act_code",
                                              "use_obsnorm", "n_slots", "mask_returns", "use_rewnorm",
-                                             "max_episode_steps")]
+                                             "max_episode_steps", "slot_reset_obs")]
                 + [(n, ctypes.c_float) for n in ("slope", "obs_clip", "gamma", "rew_range")]
                 + [("seed", ctypes.c_uint32), ("env_seed", ctypes.c_uint32)]
                 + [(n, ctypes.c_void_p) for n in ("W0", "b0", "W1", "b1", "W2", "b2", "Wa", "ba", "Wc", "bc",
@@ -97,7 +97,7 @@ SIGNATURES = {
     "xpa_dqn_td_loss": (ctypes.c_int, [c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_f32, c_p, c_i64, c_p, c_p,
                                        c_p, c_p]),
     "xpa_rollout_post_num_blocks": (c_i64, [c_i64]),
-    "xpa_rollout_post": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+    "xpa_rollout_post": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                                         c_f32, ctypes.c_int, ctypes.c_int, c_f32, ctypes.c_int, c_p, c_p, c_p]),
     "xpa_act_bwd_num_partials": (c_i64, [c_i64]),
     "xpa_act_bwd_colsum": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_i64, c_i64, c_f32, c_p, c_p, c_p]),
@@ -161,7 +161,8 @@ SIGNATURES = {
     "xpa_synthatari_step": (ctypes.c_int, [c_i64, c_i64, c_p, c_i64, c_u32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                                            c_p, c_p, c_p, c_p, c_p, c_p]),
     "xpa_synthatari_reset": (ctypes.c_int, [c_i64, c_u32, c_p, c_p, c_p]),
-    "xpa_rollout_post_deferred_norm": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_f32,
+    "xpa_rollout_post_deferred_norm": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i64, c_p,
+                                                      c_p, c_f32,
                                                       c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                                                       c_p, c_p, c_p, c_f32, ctypes.c_int, ctypes.c_int, c_f32,
                                                       ctypes.c_int, c_p, c_p, c_p]),

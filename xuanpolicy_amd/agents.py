@@ -38,7 +38,7 @@ from . import _lib, ops
 from .buffer import DummyOnPolicyBuffer, DummyOnPolicyBuffer_Atari
 from .fused_mlp import Rows
 from .learners import A2C_Learner, PerDQN_Learner, PPOCLIP_Learner
-from .policies import policy_heads, space_shape
+from .policies import policy_discrete, policy_heads, space_shape
 
 FLOAT_MAX = 3.0e38
 
@@ -65,7 +65,7 @@ class _OnPolicyAgent:
         self.observation_space = envs.observation_space
         self.action_space = envs.action_space
         self.device = next(policy.parameters()).device
-        self.discrete = bool(getattr(policy, "discrete", not hasattr(policy.actor, "logstd")))
+        self.discrete = policy_discrete(policy)
         self.dist = "categorical" if self.discrete else "gaussian"
         self.auxiliary_info_shape = {"old_logp": ()} if self.algo == "ppo" else {}
         Buffer = DummyOnPolicyBuffer_Atari if self.atari else DummyOnPolicyBuffer
@@ -75,6 +75,10 @@ class _OnPolicyAgent:
                              self.n_steps, _cfg(config, "use_gae", True), _cfg(config, "use_advnorm", True),
                              self.gamma, self.gae_lam, device=self.device)
         self.learner = self._make_learner(config, policy, optimizer, scheduler)
+        # A2C bootstraps a mid-rollout truncation with V(norm(reset_obs)): a2c_agent.py:88-95 writes obs[i] =
+        # reset_obs into next_obs before its critic call (PPO calls the critic first, ppoclip_agent.py:95-101, and
+        # both use the final observations for the full-buffer closures).  False: the final observation for A2C too.
+        self.boot_from_reset = self.algo == "a2c" and bool(_cfg(config, "a2c_reset_bootstrap", True))
         self.use_obsnorm = bool(_cfg(config, "use_obsnorm", False))
         self.use_rewnorm = bool(_cfg(config, "use_rewnorm", False))
         self.obsnorm_range = float(_cfg(config, "obsnorm_range", 5))
@@ -265,9 +269,13 @@ class _OnPolicyAgent:
 
     def _post(self, rew, term, trunc, final_obs):
         mem = self.memory
+        # A2C over a device env stepped per step (replayed graphs: the host does not know which column is the last):
+        # both bootstrap values, K8 takes V(next obs) for closures before the last step (boot_from_reset)
+        mid = self.boot_from_reset and self.device_env
         if self.raw_obs:
             v_boot = self._zero_vboot if self.raw_defer else self._heads(final_obs)[2]
-            self._post_kernel(rew, term, trunc, v_boot)
+            v_mid = self._heads(self.envs.obs)[2] if (mid and not self.raw_defer) else None
+            self._post_kernel(rew, term, trunc, v_boot, v_mid)
             return
         if self.defer_boot:
             # final-obs normalisation folded into K8: kept truncation rows and, at the last step, every env's
@@ -278,24 +286,34 @@ class _OnPolicyAgent:
                              mask_returns=(self.algo == "ppo"), use_rewnorm=self.use_rewnorm,
                              rew_range=self.rewnorm_range, atari_lifeloss=self.atari,
                              deferred=(final_obs, self.slot_obs, self.slot_t, self.slot_overflow, self.obs_mean,
-                                       self.obs_var, self._obs_clip(), self.boot_obs),
+                                       self.obs_var, self._obs_clip(), self.boot_obs)
+                             + ((self.envs.obs,) if self.boot_from_reset else ()),
                              workspace=self.post_ws)
             return
         self._normalize_into(final_obs, self.boot_obs, False)
+        v_boot = self._boot_values(self.boot_obs)
+        v_mid = None
+        if mid:
+            if getattr(self, "_mid_obs", None) is None:
+                self._mid_obs = torch.empty_like(self.boot_obs)
+            self._normalize_into(self.envs.obs, self._mid_obs, False)
+            v_mid = self._boot_values(self._mid_obs)
+        self._post_kernel(rew, term, trunc, v_boot, v_mid)
+
+    def _boot_values(self, x):
         fm = self._rollout_mlp()
         if fm is not None:
-            v_boot = fm.rollout_value(self.boot_obs)
-        else:
-            with torch.no_grad():
-                v_boot = policy_heads(self.policy, self.boot_obs)[2]
-        self._post_kernel(rew, term, trunc, v_boot)
+            return fm.rollout_value(x)
+        with torch.no_grad():
+            return policy_heads(self.policy, x)[2]
 
-    def _post_kernel(self, rew, term, trunc, v_boot):
+    def _post_kernel(self, rew, term, trunc, v_boot, v_mid=None):
         mem = self.memory
         ops.rollout_post(rew, term, trunc, v_boot.contiguous(), self.cursor, self.ret_mean, self.ret_var,
                          self.ret_count, self.returns, mem.rewards, mem.terminals, mem.closed, mem.boot, self.gamma,
                          mask_returns=(self.algo == "ppo"), use_rewnorm=self.use_rewnorm,
-                         rew_range=self.rewnorm_range, atari_lifeloss=self.atari, workspace=self.post_ws)
+                         rew_range=self.rewnorm_range, atari_lifeloss=self.atari, workspace=self.post_ws,
+                         v_boot_mid=v_mid.contiguous() if v_mid is not None else None)
 
     def _rms_update(self, x):
         if self.sync_obs_rms:
@@ -342,6 +360,7 @@ class _OnPolicyAgent:
         a.act_code, a.use_obsnorm, a.n_slots = int(code), int(self.use_obsnorm), int(self.n_slots)
         a.mask_returns, a.use_rewnorm, a.max_episode_steps = int(self.algo == "ppo"), int(self.use_rewnorm), \
             int(env.max_episode_steps)
+        a.slot_reset_obs = int(self.boot_from_reset)
         a.slope, a.obs_clip, a.gamma, a.rew_range = float(slope), float(self._obs_clip()), float(self.gamma), \
             float(self.rewnorm_range)
         a.seed, a.env_seed = int(self.seed) & 0xFFFFFFFF, int(env.noise_seed) & 0xFFFFFFFF
@@ -447,12 +466,26 @@ class _OnPolicyAgent:
         return k
 
     def _rollout_step_host(self):
-        """Same kernels around a host VecEnv (numpy in/out, reset_obs in infos)."""
+        """One step of ppoclip_agent.py:59-111 / a2c_agent.py:57-107 over a host VecEnv (numpy in / out, reset_obs
+        in infos; gym_vec_env.py:148-231): the same kernels with per-step H2D / D2H copies, and the loop's host
+        semantics kept as they are (checked step for step against oracle.cpu_ref.VecAgentRef,
+        tests/test_gpu_hostenv.py):
+          * a train() call starts from envs.buf_obs (ppoclip_agent.py:60): a row whose env ended on the previous
+            call's last step still holds its final observation there;
+          * without obs-norm the reference stores `obs` after envs.step, and on a call's first step that is
+            envs.buf_obs itself: the column holds what that array holds after the step (DummyVecEnv writes it in
+            place, SubprocVecEnv rebinds it — the object kept here is read either way);
+          * done envs continue from infos[i]["reset_obs"]; with env_name "Atari" a life loss (terminal, not
+            truncated) keeps the path and the observation (ppoclip_agent.py:93-94);
+          * A2C's mid-rollout truncation bootstraps are V(norm(reset_obs)) (a2c_agent.py:88-95, boot_from_reset)."""
         env, dev = self.envs, self.device
         dt = np.uint8 if self.raw_obs else np.float32
         shape = (self.n_envs,) + (tuple(self.obs_shape) if self.raw_obs else (-1,))
+        alias = None
         if self._host_obs is None:
-            self._host_obs = np.asarray(env.buf_obs, dt).reshape(shape)
+            self._host_obs = np.array(env.buf_obs, dt, copy=True).reshape(shape)
+            if not self.use_obsnorm:
+                alias = env.buf_obs
         x = torch.as_tensor(self._host_obs, device=dev)
         if self.raw_obs:
             ops.store_column(x.contiguous(), self.memory.observations, self.cursor)
@@ -467,10 +500,10 @@ class _OnPolicyAgent:
         if self.discrete:
             acts = acts.astype(np.int64)
         next_obs, rews, terms, truncs, infos = env.step(acts)
+        if alias is not None:   # the stored column is what the vec env's buf_obs holds now
+            col = self.memory.observations[:, t]
+            col.copy_(torch.as_tensor(np.asarray(alias, dt).reshape(col.shape), device=dev))
         next_obs = np.asarray(next_obs, dt).reshape(shape)
-        self._post(torch.as_tensor(np.asarray(rews, np.float32), device=dev),
-                   torch.as_tensor(np.asarray(terms, np.uint8), device=dev),
-                   torch.as_tensor(np.asarray(truncs, np.uint8), device=dev), torch.as_tensor(next_obs, device=dev))
         obs = next_obs.copy()
         for i in range(self.n_envs):
             if terms[i] or truncs[i]:
@@ -478,6 +511,12 @@ class _OnPolicyAgent:
                     continue
                 obs[i] = np.asarray(infos[i]["reset_obs"], dt).reshape(obs[i].shape)
                 self.current_episode[i] += 1
+        # K8 reads the bootstrap rows where a path closes: the final observations, except A2C's mid-rollout
+        # truncations (reset_obs); the last step's closures use the final observations for every algorithm
+        boot_src = obs if (self.boot_from_reset and t < self.n_steps - 1) else next_obs
+        self._post(torch.as_tensor(np.asarray(rews, np.float32), device=dev),
+                   torch.as_tensor(np.asarray(terms, np.uint8), device=dev),
+                   torch.as_tensor(np.asarray(truncs, np.uint8), device=dev), torch.as_tensor(boot_src, device=dev))
         self._host_obs = obs
 
     # ---- buffer-full phase ------------------------------------------------------------------------------
@@ -676,6 +715,7 @@ class _OnPolicyAgent:
     def train(self, train_steps, log=True):
         if not self.device_env:
             step_fn = self._rollout_step_host
+            self._host_obs = None   # every call starts from envs.buf_obs (ppoclip_agent.py:60)
         else:
             step_fn = self._rollout_step_graph if self.use_graph else self._rollout_step_device
         chunk = self.graph_chunk if (self.device_env and self.use_graph) else 1
@@ -837,9 +877,12 @@ class PerDQN_Agent:
         self.current_step = 0
         self.current_episode = np.zeros(self.n_envs, np.int32)
         self.infos = []
-        # perdqn_agent.py:57-66: train() starts from `obs = self.envs.buf_obs`, which aliases the vec env's buffer
-        # (no obsnorm copy), so the first store of every train() call holds the frames envs.step just wrote.
-        # Reproduced by default (a drop-in stores what the reference stores); False stores the pre-step frames.
+        # perdqn_agent.py:57-66: train() starts from `obs = self.envs.buf_obs` and stores `obs` after envs.step, so the
+        # first store of every train() call holds whatever that array holds after the step: the step's frames for a
+        # vec env that writes buf_obs in place (DummyVecEnv, gym_vec_env.py:228), the pre-step ones for one that
+        # rebinds it (SubprocVecEnv, gym_vec_env.py:101).  A host vec env is handled by keeping that object and
+        # storing its contents; the device envs model the in-place DummyVecEnv (their final_obs).  Reproduced by
+        # default (a drop-in stores what the reference stores); False stores the pre-step frames.
         self.alias_first_obs = bool(_cfg(config, "alias_first_obs", True))
         # optional callable() -> uniforms [n_envs, batch / n_envs] for the next PER sample (e.g. the reference's
         # recorded random.random() draws, memory_tools.py:415); None: the buffer's counter-hash uniforms
@@ -872,15 +915,21 @@ class PerDQN_Agent:
         return nxt, rew, term, trunc
 
     def train(self, train_steps, sync_info=False):
-        """perdqn_agent.py:56-95."""
+        """perdqn_agent.py:56-95.  A host vec env: every call starts from envs.buf_obs (perdqn_agent.py:57), whose rows
+        of envs that ended on the previous call's last step still hold their final frames."""
         env = self.envs
-        if not self.device_env and not hasattr(self, "_host_obs"):
-            self._host_obs = np.array(env.buf_obs, copy=True)
+        buf0 = None
+        if not self.device_env:
+            buf0 = env.buf_obs
+            self._host_obs = np.array(buf0, copy=True)
         for k in range(train_steps):
             obs = env.obs.clone() if self.device_env else self._host_obs
             acts = self._action(obs, self.egreedy)
             nxt, rew, term, trunc = self._env_step(acts)
-            self.memory.store(nxt if (k == 0 and self.alias_first_obs) else obs, acts, rew, term, nxt)
+            first = obs
+            if k == 0 and self.alias_first_obs:
+                first = nxt if self.device_env else np.array(buf0, copy=True)
+            self.memory.store(first, acts, rew, term, nxt)
             if self.current_step > self.start_training and self.current_step % self.train_frequency == 0:
                 u = self.uniform_source() if self.uniform_source is not None else None
                 o, a, r, d, n, w, idxes = self.memory.sample(self.PER_beta, uniforms=u)

@@ -577,7 +577,8 @@ __device__ __forceinline__ float post_env(
     float rew_range, int atari_lifeloss, const float *__restrict__ boot_obs, int64_t ld_boot, int64_t dim,
     float *__restrict__ slot_obs, int *__restrict__ slot_t, int n_slots, int *__restrict__ overflow,
     const float *__restrict__ obs_mean, const float *__restrict__ obs_var, float obs_clip,
-    float *__restrict__ boot_norm, int64_t ld_norm, double &cnt, double &sum, double &sumsq) {
+    float *__restrict__ boot_norm, int64_t ld_norm, double &cnt, double &sum, double &sumsq,
+    const float *__restrict__ slot_src = nullptr, int64_t ld_slot = 0) {
     const int64_t cell = n * T + t;
     buf_rew[cell] = use_rewnorm ? fminf(fmaxf(r / rstd, -rew_range), rew_range) : r;
     buf_term[cell] = te ? 1.f : 0.f;
@@ -594,9 +595,11 @@ __device__ __forceinline__ float post_env(
         }
         const int64_t sl = (int64_t)k * n_envs + n;
         slot_t[sl] = (int)t;
+        // the row the bootstrap is formed from: the final observation (PPO), or with slot_src the env's next
+        // (reset) observation — A2C's critic call sees obs[i] = reset_obs (a2c_agent.py:88-95)
+        const float *src = slot_src ? slot_src + n * ld_slot : boot_obs + n * ld_boot;
         for (int64_t d = 0; d < dim; ++d)
-            slot_obs[sl * dim + d] = NORM ? obs_norm1(boot_obs[n * ld_boot + d], obs_mean[d], obs_var[d], obs_clip)
-                                          : boot_obs[n * ld_boot + d];
+            slot_obs[sl * dim + d] = NORM ? obs_norm1(src[d], obs_mean[d], obs_var[d], obs_clip) : src[d];
     }
     if (NORM && last)
         for (int64_t d = 0; d < dim; ++d)
@@ -649,7 +652,8 @@ __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
     double *__restrict__ partials,
     unsigned int *__restrict__ ticket, const float *__restrict__ obs_mean = nullptr,
     const float *__restrict__ obs_var = nullptr, float obs_clip = 0.f, float *__restrict__ boot_norm = nullptr,
-    int64_t ld_norm = 0) {
+    int64_t ld_norm = 0, const float *__restrict__ slot_src = nullptr, int64_t ld_slot = 0,
+    const float *__restrict__ v_boot_mid = nullptr) {
     __shared__ double s_red[kPostThreads / 64];
     __shared__ bool s_last;
     const int32_t t = cur->ptr;
@@ -659,10 +663,10 @@ __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
     const int64_t n = (int64_t)blockIdx.x * kPostThreads + threadIdx.x;
     if (n < n_envs)
         returns[n] = post_env<DEFER, NORM>(n, n_envs, T, t, last, rstd, rew[n], term[n] != 0, trunc[n] != 0,
-                              DEFER ? 0.f : v_boot[n], returns[n], buf_rew, buf_term, buf_closed, buf_boot, gamma,
+                              DEFER ? 0.f : (v_boot_mid && !last ? v_boot_mid[n] : v_boot[n]), returns[n], buf_rew, buf_term, buf_closed, buf_boot, gamma,
                               mask_returns, use_rewnorm, rew_range, atari_lifeloss, boot_obs, ld_boot, dim, slot_obs,
                               slot_t, n_slots, overflow, obs_mean, obs_var, obs_clip, boot_norm, ld_norm, cnt, sum,
-                              sumsq);
+                              sumsq, slot_src, ld_slot);
     constexpr int nw = kPostThreads / 64;
     cnt = xpa_block_sum(cnt, s_red, nw);
     sum = xpa_block_sum(sum, s_red, nw);
@@ -988,7 +992,8 @@ __global__ __launch_bounds__(kRoThreads) void small_rollout_cartpole_kernel(XpaS
             R = post_env<true, true>(tid, N, T, t, last, s_rstd, r, te, tr, 0.f, R, a.buf_rew, a.buf_term,
                                      a.buf_closed, a.buf_boot, a.gamma, a.mask_returns, a.use_rewnorm, a.rew_range,
                                      0, a.final_obs, 4, D, a.slot_obs, a.slot_t, a.n_slots, a.overflow, s_mean, s_var,
-                                     a.obs_clip, a.boot_norm, a.ld_boot, cnt, sum, sumsq);
+                                     a.obs_clip, a.boot_norm, a.ld_boot, cnt, sum, sumsq,
+                                     a.slot_reset_obs ? a.env_obs : nullptr, a.ld_obs);
             a.returns[tid] = R;
         }
         XPA_RO_STAMP(5);
@@ -1167,7 +1172,8 @@ XPA_API int64_t xpa_rollout_post_num_blocks(int64_t n_envs) {
 }
 
 XPA_API int xpa_rollout_post(int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term,
-                             const uint8_t *trunc, const float *v_boot, xpa_cursor_t *cursor, float *ret_mean,
+                             const uint8_t *trunc, const float *v_boot, const float *v_boot_mid,
+                             xpa_cursor_t *cursor, float *ret_mean,
                              float *ret_var, double *ret_count, float *returns, float *buf_rew, float *buf_term,
                              uint8_t *buf_closed, float *buf_boot, float gamma, int mask_returns, int use_rewnorm,
                              float rew_range, int atari_lifeloss, double *partials, uint32_t *ticket,
@@ -1181,7 +1187,8 @@ XPA_API int xpa_rollout_post(int64_t n_envs, int64_t horizon, const float *rew, 
                        ret_mean, ret_var, ret_count, returns, buf_rew, buf_term, buf_closed, buf_boot, gamma,
                        mask_returns, use_rewnorm, rew_range, atari_lifeloss, (const float *)nullptr, (int64_t)0,
                        (int64_t)0, (float *)nullptr, (int *)nullptr, 0, (int *)nullptr, partials, (unsigned *)ticket,
-                       (const float *)nullptr, (const float *)nullptr, 0.f, (float *)nullptr, (int64_t)0);
+                       (const float *)nullptr, (const float *)nullptr, 0.f, (float *)nullptr, (int64_t)0,
+                       (const float *)nullptr, (int64_t)0, v_boot_mid);
     return xpa_launch_status();
 }
 
@@ -1209,7 +1216,7 @@ XPA_API int xpa_rollout_post_deferred(int64_t n_envs, int64_t horizon, const flo
 
 XPA_API int xpa_rollout_post_deferred_norm(int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term,
                                            const uint8_t *trunc, const float *final_obs, int64_t ld_final,
-                                           int64_t obs_dim, const float *obs_mean, const float *obs_var,
+                                           const float *slot_src, int64_t ld_slot, int64_t obs_dim, const float *obs_mean, const float *obs_var,
                                            float obs_clip, float *boot_norm, int64_t ld_norm, float *slot_obs,
                                            int32_t *slot_t, int64_t n_slots, int32_t *overflow,
                                            xpa_cursor_t *cursor, float *ret_mean,
@@ -1218,7 +1225,7 @@ XPA_API int xpa_rollout_post_deferred_norm(int64_t n_envs, int64_t horizon, cons
                                            int mask_returns, int use_rewnorm, float rew_range, int atari_lifeloss,
                                            double *partials, uint32_t *ticket, xpa_stream_t stream) {
     if (n_envs <= 0 || horizon <= 0 || obs_dim <= 0 || ld_final < obs_dim || ld_norm < obs_dim || n_slots < 1 ||
-        n_slots > horizon || !rew || !term ||
+        n_slots > horizon || (slot_src && ld_slot < obs_dim) || !rew || !term ||
         !trunc || !final_obs || !obs_mean || !obs_var || !boot_norm || !slot_obs || !slot_t || !overflow || !cursor ||
         !ret_mean || !ret_var || !ret_count || !returns || !buf_rew || !buf_term || !buf_closed || !buf_boot ||
         !partials || !ticket || xpa_rollout_post_num_blocks(n_envs) > 0x7fffffff)
@@ -1228,8 +1235,7 @@ XPA_API int xpa_rollout_post_deferred_norm(int64_t n_envs, int64_t horizon, cons
                        (const float *)nullptr, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term,
                        buf_closed, buf_boot, gamma, mask_returns, use_rewnorm, rew_range, atari_lifeloss, final_obs,
                        ld_final, obs_dim, slot_obs, slot_t, (int)n_slots, overflow, partials, (unsigned *)ticket,
-                       obs_mean, obs_var,
-                       obs_clip, boot_norm, ld_norm);
+                       obs_mean, obs_var, obs_clip, boot_norm, ld_norm, slot_src, ld_slot);
     return xpa_launch_status();
 }
 

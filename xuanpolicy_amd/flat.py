@@ -208,14 +208,18 @@ class FusedClipAdam:
         cursor unless the current window still covers them.  Stream-ordered H2D copy from a fresh pinned buffer."""
         if need > self.SCHED_WINDOW:
             raise ValueError("%d scheduled updates exceed the %d-entry window" % (need, self.SCHED_WINDOW))
-        if self.step_count + need <= self._sched_end:
+        g = self.optimizer.param_groups[0]
+        b1, b2 = g["betas"]
+        if self.step_count + need <= self._sched_end and self._window_valid(scheduler, g):
             return
         import ctypes
         import numpy as np
-        g = self.optimizer.param_groups[0]
-        b1, b2 = g["betas"]
         W = self.SCHED_WINDOW
         lrs = self._future_lrs(scheduler, W)
+        # what the table was built from: refilled when any of it changes outside scheduler.step() (a replaced
+        # scheduler, an edited param_groups lr, loaded optimizer / scheduler state, other betas)
+        self._sched_lrs, self._sched_start = lrs, self.step_count
+        self._sched_from = (scheduler, float(b1), float(b2))
         host = torch.zeros(2 * W, dtype=torch.float32).pin_memory()
         out2 = (ctypes.c_float * 2)()
         vals = np.empty(2 * W, dtype=np.float32)
@@ -228,6 +232,17 @@ class FusedClipAdam:
         self._cursor.zero_()
         self._sched_host = host                       # keep the pinned source alive until the copy has run
         self._sched_end = self.step_count + W
+
+    def _window_valid(self, scheduler, g):
+        lrs = getattr(self, "_sched_lrs", None)
+        if lrs is None:
+            return False
+        sch, b1, b2 = self._sched_from
+        j = self.step_count - self._sched_start
+        lr = g["lr"]
+        lr = float(lr) if not isinstance(lr, torch.Tensor) else float(lr.item())
+        return (sch is scheduler and (b1, b2) == tuple(float(b) for b in g["betas"]) and 0 <= j < len(lrs)
+                and lrs[j] == lr)
 
     def launch_sched(self, max_norm):
         """The device part of a scheduled step (capturable): norm pass + clip + Adam, cursor advanced on device."""

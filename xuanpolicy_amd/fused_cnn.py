@@ -33,7 +33,7 @@ import torch.nn.functional as F
 
 from . import _lib, ops
 from .fused_mlp import _act_code, _parse
-from .policies import AC_CNN_Atari, Basic_CNN
+from .policies import AC_CNN_Atari, Basic_CNN, policy_discrete
 
 
 def _conv_layers(model):
@@ -144,6 +144,19 @@ def _chain_backward(parts, layers, inputs, outs, g, acc=None, need_dx=True):
     return g
 
 
+def _library_conv_guard(conv):
+    """The explicit CNN path refuses MIOpen for convolutions with fewer than 16 input or output channels.  The r02
+    intermittent hipErrorIllegalAddress of the PER-DQN agent loop (2 of 9 runs, 8-channel test net)
+    surfaced at the first host sync after one agent step whose only library convolutions were MIOpen's NHWC kernels
+    for 4 / 8-channel shapes; every hand-written kernel of that step carries a device error word since r03 and
+    reported 0 in every later run.  K28 / K29 take every such conv, so reaching MIOpen here means use_igemm was turned
+    off (or a shape K28 / K29 reject): an error instead of the unproven route."""
+    if min(conv.in_channels, conv.out_channels) < 16:
+        raise RuntimeError("conv %d -> %d channels: the small-channel MIOpen route is refused (r02 fault suspect); "
+                           "keep use_igemm on (K28 / K29 take convs with in_channels %% 4 == 0, <= 64 channels)"
+                           % (conv.in_channels, conv.out_channels))
+
+
 def _ensure_grads(params):
     for p in params:
         if p.grad is None:
@@ -154,7 +167,11 @@ class _Trunk:
     """The explicit forward / backward of one AC_CNN_Atari or Basic_CNN representation."""
 
     def __init__(self, rep, parts):
-        if not isinstance(rep, (AC_CNN_Atari, Basic_CNN)):
+        # structural, not nominal: the reference's own AC_CNN_Atari / Basic_CNN (cnn.py:5-93: a `.model` nn.Sequential
+        # of conv blocks [+ max pool] + Flatten [+ fc blocks], input_shape (C, H, W), observations / 255 in forward)
+        # take this path as ours do; _conv_layers raises ValueError on anything else
+        if not (isinstance(rep, (AC_CNN_Atari, Basic_CNN)) or (isinstance(getattr(rep, "model", None), nn.Sequential)
+                                                                and len(getattr(rep, "input_shape", ())) == 3)):
             raise ValueError("representation %r has no explicit CNN path" % type(rep).__name__)
         self.rep = rep
         self.convs, self.tail, self.fc = _conv_layers(rep.model)
@@ -245,6 +262,7 @@ class _Trunk:
             if self._igemm_ok(conv, h.numel(), self._out_rows(conv, h.shape)):   # K28 (bias + activation fused)
                 y = self._conv_fwd(conv, code, slope, h)
             else:
+                _library_conv_guard(conv)
                 z = F.conv2d(h.permute(0, 3, 1, 2), conv.weight, None, conv.stride, conv.padding)
                 y = z.permute(0, 2, 3, 1)
                 if not y.is_contiguous():
@@ -459,6 +477,7 @@ class _Trunk:
                 self._conv_wgrad(conv, g, -1 if g_dz else code, slope, y, x_in)
             if not ig or (need_in and not self._dgrad_ok(conv) and not self._igemm_dgrad_ok(conv, numel, rows)):
                 k27 = need_in and self._dgrad_ok(conv)
+                _library_conv_guard(conv)
                 gx, gw, _ = torch.ops.aten.convolution_backward(
                     g.permute(0, 3, 1, 2), x_in.permute(0, 3, 1, 2), conv.weight, None, list(conv.stride),
                     list(conv.padding), [1, 1], False, [0, 0], 1, [need_in and not k27, not ig, False])
@@ -486,7 +505,7 @@ class FusedCNNActorCritic:
         self.trunk_ = _Trunk(policy.representation, self.parts)
         if self.trunk_.tail != "flatten":
             raise ValueError("the actor-critic path expects AC_CNN_Atari")
-        self.discrete = bool(getattr(policy, "discrete", False))
+        self.discrete = policy_discrete(policy)
         self.actor = _parse(policy.actor.model if self.discrete else policy.actor.mu)
         self.critic = _parse(policy.critic.model)
         self.logstd = None if self.discrete else policy.actor.logstd

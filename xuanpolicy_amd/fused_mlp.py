@@ -22,7 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib, ops
-from .policies import Basic_Identical, Basic_MLP, _splitk_splits
+from .policies import Basic_Identical, _splitk_splits, policy_discrete
 
 
 def _act_code(m):
@@ -54,8 +54,21 @@ def _parse(seq):
     return layers
 
 
+def _rep_layers(rep):
+    """The representation's Linear(+activation) chain, recognised by structure rather than class, so the reference's
+    own Basic_MLP / Basic_Identical (xuance/torch/representations/mlp.py:5-51: a `.model` nn.Sequential of mlp_block
+    Linear + activation pairs, empty for the identity) take the same path as ours; anything else (convolutions,
+    normalisation layers) raises ValueError and the learner keeps the generic path."""
+    model = getattr(rep, "model", None)
+    if isinstance(model, nn.Sequential):
+        return _parse(model)
+    if isinstance(rep, Basic_Identical):
+        return []
+    raise ValueError("representation %r has no explicit backward" % type(rep).__name__)
+
+
 def _head_layers(policy):
-    discrete = bool(getattr(policy, "discrete", False))
+    discrete = policy_discrete(policy)
     actor = [m for m in (policy.actor.model if discrete else policy.actor.mu) if isinstance(m, nn.Linear)]
     critic = [m for m in policy.critic.model if isinstance(m, nn.Linear)]
     return actor, critic
@@ -93,14 +106,8 @@ class FusedActorCritic:
     (pass it as `flat` to use the paired actor|critic hidden layer when head_placement applied)."""
 
     def __init__(self, policy, flat=None):
-        rep = policy.representation
-        if isinstance(rep, Basic_MLP):
-            self.rep = _parse(rep.model)
-        elif isinstance(rep, Basic_Identical):
-            self.rep = []
-        else:
-            raise ValueError("representation %r has no explicit backward" % type(rep).__name__)
-        self.discrete = bool(getattr(policy, "discrete", False))
+        self.rep = _rep_layers(policy.representation)
+        self.discrete = policy_discrete(policy)
         self.actor = _parse(policy.actor.model if self.discrete else policy.actor.mu)
         self.critic = _parse(policy.critic.model)
         self.logstd = None if self.discrete else policy.actor.logstd

@@ -22,7 +22,7 @@ import os
 import torch
 
 from . import _lib, ops
-from .policies import policy_heads
+from .policies import policy_discrete, policy_heads
 
 
 class Learner:
@@ -56,7 +56,7 @@ class Learner:
 
 
 def _dist_of(policy):
-    return "categorical" if getattr(policy, "discrete", not hasattr(policy.actor, "logstd")) else "gaussian"
+    return "categorical" if policy_discrete(policy) else "gaussian"
 
 
 class _FusedPolicyGradient(Learner):
@@ -219,12 +219,30 @@ class _FusedPolicyGradient(Learner):
                 and not ops.TIMER.enabled
                 and len(self.__dict__.get("_slot_graphs", ())) < self.graph_max_slots)
 
+    def _step_key(self):
+        """What a captured update bakes in besides its inputs: the parameter / gradient pointers, the fused optimizer's
+        buffers (flat params and grads, Adam moments, schedule table + cursor, norm output) and the K9 constants
+        (max_norm, clipping, betas, eps).  Re-homed parameters or a changed hyper-parameter give a new key, so a stale
+        graph is never replayed against freed memory or old constants."""
+        ptr = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+        fused = getattr(self, "fused_opt", None)
+        fk = ()
+        if fused is not None:
+            fk = (ptr(fused.fs.param), ptr(fused.fs.flat), ptr(fused.exp_avg), ptr(fused.exp_avg_sq),
+                  ptr(getattr(fused, "_sched", None)), ptr(getattr(fused, "_cursor", None)),
+                  ptr(getattr(fused, "total_norm", None)))
+        g = self.optimizer.param_groups[0]
+        b1, b2 = g.get("betas", (0.9, 0.999))
+        return (tuple(p.data_ptr() for p in self._params) + tuple(ptr(p.grad) for p in self._params) + fk
+                + (float(self._max_norm) if self._max_norm is not None else None, bool(self._use_clip), float(b1),
+                   float(b2), float(g.get("eps", 0.0))))
+
     def _slot_key(self, obs, idx, act, adv, ret, old_logp, adv_partials):
         ptr = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
         # the loss coefficients are kernel arguments baked into a capture: part of the key
         return (ptr(obs), tuple(obs.shape), ptr(idx), -1 if idx is None else idx.shape[0], ptr(act), ptr(adv),
                 ptr(ret), ptr(old_logp), ptr(adv_partials), float(self.clip_range), float(self.vf_coef),
-                float(self.ent_coef)) + tuple(p.data_ptr() for p in self._params)
+                float(self.ent_coef)) + self._step_key()
 
     def _graphed_mlp_update(self, fm, obs, idx, act, adv, ret, old_logp, adv_partials, pre=None, k9=None):
         """k9: the device part of the clip + Adam step (xpa_clip_adam_step_sched), run after the backward and captured
@@ -380,12 +398,14 @@ class _FusedPolicyGradient(Learner):
             fused.enable_sched()
         ptr = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
         key = (ptr(obs_flat), tuple(obs_flat.shape), bool(use_advnorm), float(self.clip_range), float(self.vf_coef),
-               float(self.ent_coef)) + tuple((ptr(b[0]), b[0].shape[0], ptr(b[1]), ptr(b[2]), ptr(b[3]), ptr(b[4]))
-                                            for b in batches)
+               float(self.ent_coef), bool(getattr(self, "small_split", True))) + \
+            tuple((ptr(b[0]), b[0].shape[0], ptr(b[1]), ptr(b[2]), ptr(b[3]), ptr(b[4])) for b in batches) + \
+            self._step_key()
         graphs = self.__dict__.setdefault("_small_graphs", {})
         ent = graphs.get(key)
+        # bounded like the slot graphs: a caller whose pointers never repeat stays eager instead of growing the cache
         graphed = getattr(self, "graph_updates", False) and not getattr(self, "_graph_failed", False) \
-            and len(batches) <= fused.SCHED_WINDOW
+            and len(batches) <= fused.SCHED_WINDOW and (ent is not None or len(graphs) < self.graph_max_slots)
         if ent is None or not graphed:
             outs = []
             for b in batches:
@@ -442,6 +462,9 @@ class _FusedPolicyGradient(Learner):
         ent = epochs.get(ekey)
         if ent is None:
             g = torch.cuda.CUDAGraph()
+            # host-side state a failed capture could leave pointing into the aborted capture's pool (a ragged last
+            # minibatch reallocates the workspace inside it): restored before the eager fallback
+            saved = (self._ws, dict(fm._partials), fm._hws)
             try:
                 with torch.cuda.graph(g, pool=self._graph_pool):
                     outs = []
@@ -456,6 +479,7 @@ class _FusedPolicyGradient(Learner):
                 # nothing of the aborted capture ran: stay with the slot graphs from here on
                 self.graph_epochs = False
                 torch.cuda.synchronize()
+                self._ws, fm._partials, fm._hws = saved
                 fm._cq.reset()
                 fm._cq_early.reset()
                 return self._eager_epoch(batches, keep_all)

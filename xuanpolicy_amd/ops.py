@@ -809,12 +809,14 @@ def post_workspace(n_envs, device):
 
 def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term,
                  buf_closed, buf_boot, gamma, mask_returns=True, use_rewnorm=True, rew_range=5.0, atari_lifeloss=False,
-                 deferred=None, workspace=None):
+                 deferred=None, workspace=None, v_boot_mid=None):
     """K8: reward normalisation, return tracker + ret_rms, rewards/terminals/closures into the buffer
     column cursor.ptr, then cursor.ptr = (ptr + 1) % horizon, cursor.step += 1.
     deferred = (boot_obs [N, D] (row stride may exceed D), slot_obs [S N, D], slot_t int32 [S N], overflow
     int32 [1]): no v_boot; truncation rows are kept (up to S per env) for bootstrap_fixup after the rollout.
-    workspace = post_workspace(N) (kept by the caller across steps; allocated here when None)."""
+    workspace = post_workspace(N) (kept by the caller across steps; allocated here when None).
+    v_boot_mid [N] (not deferred): the bootstrap values of closures before the rollout's last step (A2C's
+    V(norm(reset_obs)), a2c_agent.py:88-95); v_boot is used at the last step (and everywhere when None)."""
     N = rew.shape[0]
     _req(rew, "rew", torch.float32, (N,))
     _req(term, "term", torch.uint8, (N,))
@@ -831,20 +833,24 @@ def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count,
         _req(t, name, torch.float32, (N, T))
     _req(buf_closed, "buf_closed", torch.uint8, (N, T))
     part, ticket = workspace if workspace is not None else post_workspace(N, rew.device)
-    if deferred is not None and len(deferred) == 8:
-        # (final_obs RAW, slot_obs, slot_t, overflow, obs_mean, obs_var, obs_clip, boot_norm): normalisation
-        # of the final observations folded into K8 (xpa_rollout_post_deferred_norm)
-        final_obs, slot_obs, slot_t, overflow, obs_mean, obs_var, obs_clip, boot_norm = deferred
+    if deferred is not None and len(deferred) in (8, 9):
+        # (final_obs RAW, slot_obs, slot_t, overflow, obs_mean, obs_var, obs_clip, boot_norm[, slot_src RAW]):
+        # normalisation of the final observations folded into K8 (xpa_rollout_post_deferred_norm); slot_src (A2C:
+        # the env's next observations) replaces final_obs as the source of kept truncation rows
+        final_obs, slot_obs, slot_t, overflow, obs_mean, obs_var, obs_clip, boot_norm = deferred[:8]
+        slot_src = deferred[8] if len(deferred) == 9 else None
         D = slot_obs.shape[1]
         S = _n_slots(slot_t, N)
         ldf = _row_stride(final_obs, "final_obs", D)
         ldn = _row_stride(boot_norm, "boot_norm", D)
+        lds = _row_stride(slot_src, "slot_src", D) if slot_src is not None else 0
         _req(slot_obs, "slot_obs", torch.float32, (S * N, D))
         _req(overflow, "overflow", torch.int32, (1,))
         _req(obs_mean, "obs_mean", torch.float32, (D,))
         _req(obs_var, "obs_var", torch.float32, (D,))
         rc = lib().xpa_rollout_post_deferred_norm(
-            N, T, _p(rew), _p(term), _p(trunc), _p(final_obs), ldf, D, _p(obs_mean), _p(obs_var), float(obs_clip),
+            N, T, _p(rew), _p(term), _p(trunc), _p(final_obs), ldf, _p(slot_src), lds,
+            D, _p(obs_mean), _p(obs_var), float(obs_clip),
             _p(boot_norm), ldn, _p(slot_obs), _p(slot_t), S, _p(overflow), _p(cursor), _p(ret_mean), _p(ret_var),
             _p(ret_count), _p(returns), _p(buf_rew), _p(buf_term), _p(buf_closed), _p(buf_boot), float(gamma),
             int(bool(mask_returns)), int(bool(use_rewnorm)), float(rew_range), int(bool(atari_lifeloss)), _p(part),
@@ -866,7 +872,10 @@ def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count,
                                              _p(part), _p(ticket), _stream(rew.device))
         _lib.check(rc, "xpa_rollout_post_deferred")
         return
-    rc = lib().xpa_rollout_post(N, T, _p(rew), _p(term), _p(trunc), _p(v_boot), _p(cursor), _p(ret_mean), _p(ret_var),
+    if v_boot_mid is not None:
+        _req(v_boot_mid, "v_boot_mid", torch.float32, (N,))
+    rc = lib().xpa_rollout_post(N, T, _p(rew), _p(term), _p(trunc), _p(v_boot), _p(v_boot_mid), _p(cursor),
+                                _p(ret_mean), _p(ret_var),
                                 _p(ret_count), _p(returns), _p(buf_rew), _p(buf_term), _p(buf_closed), _p(buf_boot),
                                 float(gamma), int(bool(mask_returns)), int(bool(use_rewnorm)), float(rew_range),
                                 int(bool(atari_lifeloss)), _p(part), _p(ticket), _stream(rew.device))

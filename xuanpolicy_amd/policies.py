@@ -423,6 +423,13 @@ REGISTRY_Representation = {"Basic_Identical": Basic_Identical, "Basic_MLP": Basi
                            "Basic_CNN": Basic_CNN}
 
 
+def policy_discrete(policy):
+    """Categorical when the actor has no logstd: categorical.py's ActorNet holds .model, gaussian.py's .mu + .logstd
+    (the reference's classes carry no `discrete` attribute; ours do, with the same meaning)."""
+    d = getattr(policy, "discrete", None)
+    return bool(d) if d is not None else not hasattr(policy.actor, "logstd")
+
+
 def policy_heads(policy, x):
     """(head, logstd, v) for our policies or the reference's classes (same attribute layout)."""
     if hasattr(policy, "heads"):
