@@ -412,15 +412,23 @@ def test_colsum_queue_deferred_loss_finalize(nseg, dist):
         assert total is None
 
 
-@pytest.mark.parametrize("algo,dist,K,B,code", [
-    ("a2c", "categorical", 18, 777, 0),    # the r01 aperture-violation configuration
-    ("ppo", "gaussian", 17, 4133, 1),      # C4 head width, ragged tail (4133 = 64 * 64 + 37)
-    ("ppo", "categorical", 18, 193, 2),
-    ("a2c", "gaussian", 6, 65, 1),
-    ("ppo", "gaussian", 6, 64, 0),
+@pytest.mark.parametrize("algo,dist,K,B,code,ws", [
+    ("a2c", "categorical", 18, 777, 0, False),    # the r01 aperture-violation configuration
+    ("ppo", "gaussian", 17, 4133, 1, False),      # C4 head width, ragged tail (4133 = 64 * 64 + 37)
+    ("ppo", "categorical", 18, 193, 2, False),
+    ("a2c", "gaussian", 6, 65, 1, False),
+    ("ppo", "gaussian", 6, 64, 0, False),
+    # K16W: ragged tails, one tile, a grid below the tile count (20037 rows = 314 tiles on 256 blocks: partial rows
+    # 256..313 written as zeros), 8-wide heads
+    ("ppo", "gaussian", 6, 4133, 1, True),
+    ("a2c", "categorical", 8, 777, 0, True),
+    ("ppo", "categorical", 4, 64, 2, True),
+    ("ppo", "gaussian", 6, 20037, 1, True),
+    ("a2c", "gaussian", 8, 33, 1, True),
 ])
-def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code):
-    """K16 (xpa_head_gemm_actor / _critic) through the C ABI against float64 autograd of the same head:
+def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code, ws):
+    """K16 (xpa_head_gemm_actor / _critic) or K16W (xpa_head_gemm_ws_*) through the C ABI against float64 autograd
+    of the same head:
     z = x Wh^T + bh, h = act(z), head = h W^T + b, the PPO-Clip / A2C loss with Gaussian / Categorical
     log-prob + entropy (ppoclip_learner.py:32-44, a2c_learner.py:24-31) and the critic's value loss.
     Checked: dz (d loss / d z), the summed per-block partials (dW_out, db_out, db_hidden, loss sums) and
@@ -468,13 +476,15 @@ def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code):
     v = lambda t: ops._p(t[pad:])   # noqa: E731
     algo_c, dist_c = ops.ALGO[algo], ops.DIST[dist]
     ent, clip, vf = 0.01, 0.2, 0.25
-    assert L.xpa_head_gemm_actor(algo_c, dist_c, code, B, K, H, ops._p(x), H, ops._p(wh_a), ops._p(bh_a), 2 * H,
-                                 ops._p(w_a), ops._p(b_a), slope, ops._p(logstd) if logstd is not None else None,
-                                 ops._p(idx), R, ops._p(act), ops._p(old) if old is not None else None, ops._p(adv),
-                                 None, 0, clip, ent, ops._p(dz), v(p_dw_a), v(p_dbh_a), v(p_dbo_a), v(lp), W, s) == 0
-    assert L.xpa_head_gemm_critic(code, B, H, ops._p(x), H, ops._p(wh_c), ops._p(bh_c), 2 * H, ops._p(w_c),
-                                  ops._p(b_c), slope, ops._p(idx), R, ops._p(ret), vf, ops._p(dz[:, H:]), v(p_dw_c),
-                                  v(p_dbh_c), v(p_dbo_c), v(lp), W, s) == 0
+    fa = L.xpa_head_gemm_ws_actor if ws else L.xpa_head_gemm_actor
+    fc = L.xpa_head_gemm_ws_critic if ws else L.xpa_head_gemm_critic
+    assert fa(algo_c, dist_c, code, B, K, H, ops._p(x), H, ops._p(wh_a), ops._p(bh_a), 2 * H,
+              ops._p(w_a), ops._p(b_a), slope, ops._p(logstd) if logstd is not None else None,
+              ops._p(idx), R, ops._p(act), ops._p(old) if old is not None else None, ops._p(adv),
+              None, 0, clip, ent, ops._p(dz), v(p_dw_a), v(p_dbh_a), v(p_dbo_a), v(lp), W, s) == 0
+    assert fc(code, B, H, ops._p(x), H, ops._p(wh_c), ops._p(bh_c), 2 * H, ops._p(w_c),
+              ops._p(b_c), slope, ops._p(idx), R, ops._p(ret), vf, ops._p(dz[:, H:]), v(p_dw_c),
+              v(p_dbh_c), v(p_dbo_c), v(lp), W, s) == 0
     torch.cuda.synchronize()
     for t in (p_dw_a, p_dbh_a, p_dbo_a, p_dw_c, p_dbh_c, p_dbo_c):
         assert bool((t[:pad] == 555.0).all()) and bool((t[-pad:] == 555.0).all()), "partials written out of bounds"
@@ -535,6 +545,55 @@ def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code):
     assert abs(got[2] - entropy.item()) < 1e-5 and abs(got[3] - total.item()) < 1e-5
     if ls is not None:
         close(dls, ls.grad, "d logstd", rel=1e-5)
+
+
+@pytest.mark.parametrize("algo,dist,K,B", [("ppo", "gaussian", 6, 65536), ("a2c", "categorical", 4, 20037),
+                                          ("ppo", "gaussian", 6, 3000), ("ppo", "categorical", 8, 130)])
+def test_head_gemm_ws_equals_k16(algo, dist, K, B):
+    """K16W (wave-specialised) against K16 on the same inputs: dz bit for bit (the same GEMM k order, the same epilogue
+    chains, only the thread running each changes) and the per-block partials summed over their rows to f32 rounding
+    (the two grids group the tiles into blocks differently); every partial row K16W's grid does not own is 0."""
+    from xuanpolicy_amd import ops
+    L, s = ops.lib(), ops._stream()
+    g = torch.Generator(device=DEV).manual_seed(B * 3 + K)
+    H, R = 256, B + 100
+    x = torch.randn(B, H, device=DEV, generator=g)
+    wh_a, wh_c = (torch.randn(H, H, device=DEV, generator=g) / 16 for _ in range(2))
+    bh_a, bh_c = (torch.randn(H, device=DEV, generator=g) * 0.1 for _ in range(2))
+    w_a, b_a = torch.randn(K, H, device=DEV, generator=g) / 16, torch.randn(K, device=DEV, generator=g) * 0.1
+    w_c, b_c = torch.randn(1, H, device=DEV, generator=g) / 16, torch.randn(1, device=DEV, generator=g) * 0.1
+    logstd = (-1 + 0.1 * torch.randn(K, device=DEV, generator=g)) if dist == "gaussian" else None
+    idx = torch.randperm(R, device=DEV, generator=g)[:B].contiguous()
+    adv, ret = torch.randn(R, device=DEV, generator=g), torch.randn(R, device=DEV, generator=g)
+    act = (torch.randn(R, K, device=DEV, generator=g) * 0.5 if dist == "gaussian"
+           else torch.randint(0, K, (R,), device=DEV, generator=g).float())
+    old = -1.5 + 0.3 * torch.randn(R, device=DEV, generator=g) if algo == "ppo" else None
+    G = int(L.xpa_head_fused_num_partials(B))
+    Wd = int(L.xpa_loss_partial_width(K))
+    outs = []
+    for ws in (False, True):
+        dz = torch.full((B, 2 * H), 123.0, device=DEV)
+        parts = [torch.full((G, n), 9.0, device=DEV) for n in (K * H, H, K, H, H, 1)]
+        lp = torch.zeros(G, Wd, device=DEV)
+        fa = L.xpa_head_gemm_ws_actor if ws else L.xpa_head_gemm_actor
+        fc = L.xpa_head_gemm_ws_critic if ws else L.xpa_head_gemm_critic
+        assert fa(ops.ALGO[algo], ops.DIST[dist], 1, B, K, H, ops._p(x), H, ops._p(wh_a), ops._p(bh_a), 2 * H,
+                  ops._p(w_a), ops._p(b_a), 0.01, ops._p(logstd), ops._p(idx), R, ops._p(act), ops._p(old),
+                  ops._p(adv), None, 0, 0.2, 0.01, ops._p(dz), ops._p(parts[0]), ops._p(parts[1]), ops._p(parts[2]),
+                  ops._p(lp), Wd, s) == 0
+        assert fc(1, B, H, ops._p(x), H, ops._p(wh_c), ops._p(bh_c), 2 * H, ops._p(w_c), ops._p(b_c), 0.01,
+                  ops._p(idx), R, ops._p(ret), 0.25, ops._p(dz[:, H:]), ops._p(parts[3]), ops._p(parts[4]),
+                  ops._p(parts[5]), ops._p(lp), Wd, s) == 0
+        torch.cuda.synchronize()
+        outs.append((dz, parts, lp))
+    (dz0, p0, l0), (dz1, p1, l1) = outs
+    assert torch.equal(dz0, dz1), "dz differs from K16"
+    gw = int(L.xpa_head_gemm_ws_grid(B))
+    assert gw == min(G, 256)
+    for a, b in zip(p0 + [l0], p1 + [l1]):
+        if G > gw:
+            assert bool((b[gw:] == 0).all()), "rows beyond K16W's grid must be zero"
+        torch.testing.assert_close(b.double().sum(0), a.double().sum(0), rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("rows,n_rows,din", [(65536, 524288, 17), (1000, 5000, 4), (77, 300, 17)])

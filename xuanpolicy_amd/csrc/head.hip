@@ -144,58 +144,77 @@ __device__ __forceinline__ void load_tile(float4 (&zq)[16], const float *__restr
 
 // ---- shared epilogue: everything after h = act(z) of a 64-row tile is in LDS ----------------------
 // MODE: 0 Gaussian actor, 1 Categorical actor, 2 critic.  ALGO: 0 PPO, 1 A2C (actor only).
+// NW: the waves running it (4: K12 / K16, all of the block; 2: K16W's epilogue waves).  Epilogue thread e (0 .. 64 NW)
+// owns columns e + 64 NW j (j < CPT = 4 / NW) in phase 2; in phase 1 wave w owns the row quarters w 4/NW + i.  The
+// arithmetic of every output is the same whichever NW runs it (each quarter / column is one sequential chain in the
+// same order), so K16W reproduces K16 bit for bit.
+// The steps have no barriers of their own: a kernel runs them in order with a block barrier between consecutive steps
+// (the K12 / K16 wrapper `tile` does exactly that; K16W places them between its k-chunk barriers).
 typedef float f2v __attribute__((ext_vector_type(2)));
 template <int KMAX>
-struct RowIn {  // wave 0, lane = row of the tile
+struct RowIn {  // epilogue wave 0, lane = row of the tile
     bool valid;
     bool masked;  // a batch row whose index is out of range (contributes nothing)
     float x, old, act[KMAX];
 };
 
-template <int MODE, int ALGO, int ACT, int KMAX>
+template <int MODE, int ALGO, int ACT, int KMAX, int NW = 4>
 struct HeadEpi {
     static constexpr int KP = (KMAX + 3) & ~3;  // 16-B aligned d-head rows
     // phase-1 partials per pass: heads wider than 8 (C4's 17 / 18) go through s_part in two halves, so the K16 block
     // fits 80 KiB of LDS (2 blocks per CU; 90 KiB with all 18 at once)
     static constexpr int PH = KMAX > 8 ? (KMAX + 1) / 2 : KMAX;
+    static constexpr int NPASS = (KMAX + PH - 1) / PH;
+    static constexpr int NT = 64 * NW;      // epilogue threads
+    static constexpr int CPT = 4 / NW;      // phase-2 columns per thread
+    static constexpr int QPW = 4 / NW;      // phase-1 row quarters per wave
     // phase 2 (column t); dW_out accumulated in output pairs (v_pk_fma_f32: the same fused multiply-add per output,
     // half the VALU issues)
     static constexpr bool kPk = KMAX <= 8;  // the wide heads (C4) keep scalar accumulators (packed pairs spill there)
     static constexpr int KH2 = (KMAX + 1) / 2;
-    float wc[KMAX], acc_dw[kPk ? 1 : KMAX], acc_dbh;
-    f2v acc_dw2[kPk ? KH2 : 1];
+    float wc[CPT][KMAX], acc_dw[CPT][kPk ? 1 : KMAX], acc_dbh[CPT];
+    f2v acc_dw2[CPT][kPk ? KH2 : 1];
     float acc_dbo[KMAX], acc_dls[KMAX], var_[KMAX], logsc[KMAX];
     float sum0, sum1, sum2, ent_const, inv_b, lo, hi, a_mean, a_inv, slope;
-    int K;
+    float hd[KMAX];  // epilogue wave 0: the row's head outputs between the phase-1 passes and the loss
+    int K, e;        // e: epilogue thread index
 
-    // W: output layer [K, 256]; s_stats: 2 floats of LDS.  Ends with a block barrier.
-    __device__ __forceinline__ void init(int K_in, const float *__restrict__ W, const float *__restrict__ logstd,
-                                         const double *__restrict__ adv_partials, int64_t n_adv_partials,
-                                         int64_t batch, float clip_range, float slope_, float *s_stats) {
-        const int t = threadIdx.x;
+    // W: output layer [K, 256]; s_stats: 2 floats of LDS.  init_a, a block barrier, then init_b.
+    __device__ __forceinline__ void init_a(int e_, int K_in, const float *__restrict__ W,
+                                           const float *__restrict__ logstd, const double *__restrict__ adv_partials,
+                                           int64_t n_adv_partials, int64_t batch, float clip_range, float slope_,
+                                           float *s_stats) {
+        e = e_;
         K = MODE == 2 ? 1 : K_in;
         slope = slope_;
         if (MODE != 2 && adv_partials) {
-            adv_stats(adv_partials, n_adv_partials, batch, s_stats, s_stats + 1);
-        } else if (t == 0) {
+            if (e < 64) adv_stats(adv_partials, n_adv_partials, batch, s_stats, s_stats + 1);
+        } else if (e == 0) {
             s_stats[0] = 0.f;
             s_stats[1] = 1.f;
         }
 #pragma unroll
+        for (int j = 0; j < CPT; ++j)
+#pragma unroll
+            for (int o = 0; o < KMAX; ++o) wc[j][o] = o < K ? W[o * kH + e + NT * j] : 0.f;
+#pragma unroll
         for (int o = 0; o < KMAX; ++o) {
-            wc[o] = o < K ? W[o * kH + t] : 0.f;
             acc_dbo[o] = acc_dls[o] = 0.f;
             var_[o] = 1.f;
             logsc[o] = 0.f;
+            hd[o] = 0.f;
         }
-        if constexpr (kPk) {
 #pragma unroll
-            for (int o2 = 0; o2 < KH2; ++o2) acc_dw2[o2] = f2v{0.f, 0.f};
-        } else {
+        for (int j = 0; j < CPT; ++j) {
+            if constexpr (kPk) {
 #pragma unroll
-            for (int o = 0; o < KMAX; ++o) acc_dw[o] = 0.f;
+                for (int o2 = 0; o2 < KH2; ++o2) acc_dw2[j][o2] = f2v{0.f, 0.f};
+            } else {
+#pragma unroll
+                for (int o = 0; o < KMAX; ++o) acc_dw[j][o] = 0.f;
+            }
+            acc_dbh[j] = 0.f;
         }
-        acc_dbh = 0.f;
         sum0 = sum1 = sum2 = ent_const = 0.f;
         if (MODE == 0) {
 #pragma unroll
@@ -209,7 +228,8 @@ struct HeadEpi {
         inv_b = 1.0f / (float)batch;
         lo = 1.0f - clip_range;
         hi = 1.0f + clip_range;
-        __syncthreads();
+    }
+    __device__ __forceinline__ void init_b(const float *s_stats) {
         a_mean = s_stats[0];
         a_inv = s_stats[1];
     }
@@ -224,8 +244,8 @@ struct HeadEpi {
         in.x = in.old = 0.f;
 #pragma unroll
         for (int o = 0; o < KMAX; ++o) in.act[o] = 0.f;
-        const int lane = threadIdx.x & 63;
-        if ((threadIdx.x >> 6) == 0) {
+        const int lane = e & 63;
+        if (e < 64) {
             const int64_t b = tile * kTile + lane;
             if (b < batch) {
                 const int64_t row = idx ? idx[b] : b;
@@ -251,169 +271,169 @@ struct HeadEpi {
         return in;
     }
 
-    // s_h holds h = act(z) of rows [tile*64, tile*64 + 64) (row stride kS).  Starts with a barrier
-    // (s_h complete), ends with one (s_h / s_dh free for the next tile).
-    __device__ __forceinline__ void tile(const float *s_h, float (*s_part)[kTile][PH], float (*s_dh)[KP],
-                                         const RowIn<KMAX> &in, int64_t tile, int64_t batch,
-                                         const float *__restrict__ W, const float *__restrict__ bias,
-                                         float *__restrict__ dz, int64_t ld, float ent_coef, float vf_coef) {
-        const int t = threadIdx.x, lane = t & 63;
-        const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-        __syncthreads();
-        // ---- phase 1: partial dot products, row = lane, quarter = wave ----
-        // Outputs [o0, o0 + PH) per pass; wide heads take two passes (re-reading the row quarter from LDS) so that
-        // s_part and the live partials stay half-sized.
-#pragma unroll 1
-        for (int o0 = 0; o0 < KMAX; o0 += PH) {
-            if (o0 > 0) __syncthreads();  // wave 0 has read the previous pass
+    // ---- phase 1, pass `pass`: partial dot products of outputs [pass PH, pass PH + PH), row = lane, quarter of
+    // wave w's set.  Reads s_h (h of the tile, row stride kS), writes s_part.  Unconditional loads (rows o >= K re-read
+    // row 0; their sums are never used): the scalar loads of a step issue together.  One fmaf chain per output and
+    // quarter over its 64 columns in order.
+    __device__ __forceinline__ void p1(int pass, const float *s_h, float (*s_part)[kTile][PH],
+                                       const float *__restrict__ W) const {
+        const int lane = e & 63;
+        const int wave = __builtin_amdgcn_readfirstlane(e >> 6);
+        const int o0 = pass * PH;
+#pragma unroll
+        for (int qi = 0; qi < QPW; ++qi) {
+            const int quarter = wave * QPW + qi;
             float p[PH];
 #pragma unroll
             for (int o = 0; o < PH; ++o) p[o] = 0.f;
-            const float *hrow = s_h + lane * kS + wave * 64;
-            const float *wq = W + wave * 64;
+            const float *hrow = s_h + lane * kS + quarter * 64;
+            const float *wq = W + quarter * 64;
 #pragma unroll 4
             for (int j = 0; j < 16; ++j) {
                 const float4 hv = *reinterpret_cast<const float4 *>(hrow + 4 * j);
-                // unconditional (rows o >= K re-read row 0; their sums are never used): the scalar loads of a
-                // step issue together instead of one branch + load + wait per output
 #pragma unroll
                 for (int o = 0; o < PH; ++o) {
                     const int oo = o0 + o;
                     const float4 w4 = *reinterpret_cast<const float4 *>(wq + (oo < K ? oo : 0) * kH + 4 * j);
-                    p[o] += hv.x * w4.x + hv.y * w4.y + hv.z * w4.z + hv.w * w4.w;
+                    p[o] = fmaf(hv.x, w4.x, p[o]);
+                    p[o] = fmaf(hv.y, w4.y, p[o]);
+                    p[o] = fmaf(hv.z, w4.z, p[o]);
+                    p[o] = fmaf(hv.w, w4.w, p[o]);
                 }
             }
 #pragma unroll
-            for (int o = 0; o < PH; ++o) s_part[wave][lane][o] = p[o];
-            __syncthreads();
-            // the head outputs of wave 0's row: the 4 quarters summed in a fixed order, + bias, parked in the row's
-            // s_dh slots (free until the loss below overwrites them with d-head) so nothing stays live across passes
-            if (wave == 0) {
-#pragma unroll
-                for (int o = 0; o < PH; ++o)
-                    if (o0 + o < KMAX)
-                        s_dh[lane][o0 + o] =
-                            o0 + o < K ? ((s_part[0][lane][o] + s_part[1][lane][o]) +
-                                          (s_part[2][lane][o] + s_part[3][lane][o])) +
-                                             bias[o0 + o]
-                                       : 0.f;
-            }
+            for (int o = 0; o < PH; ++o) s_part[quarter][lane][o] = p[o];
         }
-        float hd[KMAX];
-        if (wave == 0) {
+    }
+    // epilogue wave 0 after a phase-1 pass: the head outputs of its row (the 4 quarters summed in a fixed order + bias)
+    __device__ __forceinline__ void p1_sum(int pass, float (*s_part)[kTile][PH], const float *__restrict__ bias) {
+        if (e >= 64) return;
+        const int lane = e;
+        const int o0 = pass * PH;
 #pragma unroll
-            for (int o = 0; o < KMAX; ++o) hd[o] = s_dh[lane][o];
-        }
-        // ---- loss: wave 0, one lane per row ----
-        if (wave == 0) {
-            float dh_[KMAX];
+        for (int o = 0; o < PH; ++o)
+            if (o0 + o < KMAX)
+                hd[o0 + o] = o0 + o < K ? ((s_part[0][lane][o] + s_part[1][lane][o]) +
+                                           (s_part[2][lane][o] + s_part[3][lane][o])) +
+                                              bias[o0 + o]
+                                        : 0.f;
+    }
+
+    // ---- loss: epilogue wave 0, one lane per row (after the last p1_sum); d head -> s_dh ----
+    __device__ __forceinline__ void loss(float (*s_dh)[KP], const RowIn<KMAX> &in, float ent_coef, float vf_coef) {
+        if (e >= 64) return;
+        const int lane = e;
+        float dh_[KMAX];
 #pragma unroll
-            for (int o = 0; o < KMAX; ++o) dh_[o] = 0.f;
-            if (in.valid) {
-                if (MODE == 2) {
-                    const float diffv = hd[0] - in.x;
-                    sum0 += diffv * diffv;
-                    sum1 += hd[0];
-                    dh_[0] = vf_coef * 2.0f * diffv * inv_b;
-                    acc_dbo[0] += dh_[0];
+        for (int o = 0; o < KMAX; ++o) dh_[o] = 0.f;
+        if (in.valid) {
+            if (MODE == 2) {
+                const float diffv = hd[0] - in.x;
+                sum0 += diffv * diffv;
+                sum1 += hd[0];
+                dh_[0] = vf_coef * 2.0f * diffv * inv_b;
+                acc_dbo[0] += dh_[0];
+            } else {
+                const float A_n = (in.x - a_mean) * a_inv;
+                float logp = 0.f, ent = 0.f, lse = 0.f;
+                int ai = 0;
+                float diff[KMAX];
+                if (MODE == 0) {
+#pragma unroll
+                    for (int o = 0; o < KMAX; ++o) {
+                        diff[o] = 0.f;
+                        if (o < K) {
+                            diff[o] = in.act[o] - hd[o];
+                            logp += -(diff[o] * diff[o]) / (2.0f * var_[o]) - logsc[o] - kLogSqrt2Pi;
+                        }
+                    }
+                    ent = ent_const;
                 } else {
-                    const float A_n = (in.x - a_mean) * a_inv;
-                    float logp = 0.f, ent = 0.f, lse = 0.f;
-                    int ai = 0;
-                    float diff[KMAX];
-                    if (MODE == 0) {
+                    float m = hd[0];
 #pragma unroll
-                        for (int o = 0; o < KMAX; ++o) {
-                            diff[o] = 0.f;
-                            if (o < K) {
-                                diff[o] = in.act[o] - hd[o];
-                                logp += -(diff[o] * diff[o]) / (2.0f * var_[o]) - logsc[o] - kLogSqrt2Pi;
-                            }
-                        }
-                        ent = ent_const;
-                    } else {
-                        float m = hd[0];
+                    for (int o = 1; o < KMAX; ++o)
+                        if (o < K) m = fmaxf(m, hd[o]);
+                    float se = 0.f;
 #pragma unroll
-                        for (int o = 1; o < KMAX; ++o)
-                            if (o < K) m = fmaxf(m, hd[o]);
-                        float se = 0.f;
-#pragma unroll
-                        for (int o = 0; o < KMAX; ++o)
-                            if (o < K) se += expf(hd[o] - m);
-                        lse = m + logf(se);
-                        ai = (int)in.act[0];
-                        ai = ai < 0 ? 0 : (ai >= K ? K - 1 : ai);
-#pragma unroll
-                        for (int o = 0; o < KMAX; ++o) {
-                            if (o < K) {
-                                const float ln = hd[o] - lse;
-                                ent -= expf(ln) * ln;
-                                if (o == ai) logp = ln;
-                            }
-                        }
-                    }
-                    float dlogp;
-                    if (ALGO == 0) {
-                        const float ratio = expf(logp - in.old);
-                        const float cr = fminf(fmaxf(ratio, lo), hi);
-                        const float s1 = cr * A_n, s2 = A_n * ratio;
-                        sum0 += fminf(s1, s2);
-                        const bool inr = (ratio >= lo) && (ratio <= hi);
-                        const float g1 = inr ? A_n : 0.f;
-                        const float w1 = (s1 < s2) ? 1.f : ((s1 == s2) ? 0.5f : 0.f);
-                        const float w2 = (s2 < s1) ? 1.f : ((s1 == s2) ? 0.5f : 0.f);
-                        dlogp = -inv_b * (w1 * g1 + w2 * A_n) * ratio;
-                        sum2 += ((ratio < lo) || (ratio > hi)) ? 1.f : 0.f;
-                    } else {
-                        sum0 += A_n * logp;
-                        dlogp = -A_n * inv_b;
-                    }
-                    sum1 += ent;
-                    const float ec = ent_coef * inv_b;
+                    for (int o = 0; o < KMAX; ++o)
+                        if (o < K) se += expf(hd[o] - m);
+                    lse = m + logf(se);
+                    ai = (int)in.act[0];
+                    ai = ai < 0 ? 0 : (ai >= K ? K - 1 : ai);
 #pragma unroll
                     for (int o = 0; o < KMAX; ++o) {
                         if (o < K) {
-                            if (MODE == 0) {
-                                dh_[o] = dlogp * diff[o] / var_[o];
-                                acc_dls[o] += dlogp * (diff[o] * diff[o] / var_[o] - 1.0f);
-                            } else {
-                                const float ln = hd[o] - lse;
-                                const float p = expf(ln);
-                                dh_[o] = dlogp * ((o == ai ? 1.f : 0.f) - p) + ec * p * (ln + ent);
-                            }
-                            acc_dbo[o] += dh_[o];
+                            const float ln = hd[o] - lse;
+                            ent -= expf(ln) * ln;
+                            if (o == ai) logp = ln;
                         }
                     }
                 }
-            }
-            if (MODE == 0 && in.masked) {  // hand back the ent_coef / B the finalize subtracts for every row
+                float dlogp;
+                if (ALGO == 0) {
+                    const float ratio = expf(logp - in.old);
+                    const float cr = fminf(fmaxf(ratio, lo), hi);
+                    const float s1 = cr * A_n, s2 = A_n * ratio;
+                    sum0 += fminf(s1, s2);
+                    const bool inr = (ratio >= lo) && (ratio <= hi);
+                    const float g1 = inr ? A_n : 0.f;
+                    const float w1 = (s1 < s2) ? 1.f : ((s1 == s2) ? 0.5f : 0.f);
+                    const float w2 = (s2 < s1) ? 1.f : ((s1 == s2) ? 0.5f : 0.f);
+                    dlogp = -inv_b * (w1 * g1 + w2 * A_n) * ratio;
+                    sum2 += ((ratio < lo) || (ratio > hi)) ? 1.f : 0.f;
+                } else {
+                    sum0 += A_n * logp;
+                    dlogp = -A_n * inv_b;
+                }
+                sum1 += ent;
+                const float ec = ent_coef * inv_b;
 #pragma unroll
-                for (int o = 0; o < KMAX; ++o)
-                    if (o < K) acc_dls[o] += ent_coef * inv_b;
+                for (int o = 0; o < KMAX; ++o) {
+                    if (o < K) {
+                        if (MODE == 0) {
+                            dh_[o] = dlogp * diff[o] / var_[o];
+                            acc_dls[o] += dlogp * (diff[o] * diff[o] / var_[o] - 1.0f);
+                        } else {
+                            const float ln = hd[o] - lse;
+                            const float p = expf(ln);
+                            dh_[o] = dlogp * ((o == ai ? 1.f : 0.f) - p) + ec * p * (ln + ent);
+                        }
+                        acc_dbo[o] += dh_[o];
+                    }
+                }
             }
-#pragma unroll
-            for (int o = 0; o < KMAX; ++o) s_dh[lane][o] = dh_[o];
         }
-        __syncthreads();
-        // ---- phase 2: column owner t ----
-#if XPA_HEAD_PROBE == 5  // 5 = epilogue alone without phase 2
-        const int nr = 0;
-#else
-        const int nr = (int)min((int64_t)kTile, batch - tile * kTile);
-#endif
-        float *dzt = dz + tile * kTile * ld + t;
-        f2v wc2[KH2];
+        if (MODE == 0 && in.masked) {  // hand back the ent_coef / B the finalize subtracts for every row
 #pragma unroll
-        for (int o2 = 0; o2 < KH2; ++o2) wc2[o2] = f2v{wc[2 * o2], 2 * o2 + 1 < KMAX ? wc[2 * o2 + 1] : 0.f};
-        // rows in groups of 4: every LDS read of the group (h, and the d-head rows as 16-B broadcasts)
-        // issued before the arithmetic, which keeps the row order of the accumulations (bitwise the
-        // same sums as one row at a time)
-        int r = 0;
+            for (int o = 0; o < KMAX; ++o)
+                if (o < K) acc_dls[o] += ent_coef * inv_b;
+        }
+#pragma unroll
+        for (int o = 0; o < KMAX; ++o) s_dh[lane][o] = dh_[o];
+    }
+
+    // ---- phase 2, rows [r0, r1) of the tile: column owner.  dz[r, c] = (d head[r] . w[:, c]) * act'(h[r, c]), dW_out
+    // and db_hidden accumulated in registers; rows in groups of 4 (every LDS read of the group issued before the
+    // arithmetic, the row order of the accumulations kept: bitwise the same sums as one row at a time).
+    __device__ __forceinline__ void p2(const float *s_h, float (*s_dh)[KP], int64_t tile, int64_t batch, int r0, int r1,
+                                       float *__restrict__ dz, int64_t ld) {
+#if XPA_HEAD_PROBE == 5  // 5 = epilogue alone without phase 2
+        r1 = r0;
+#endif
+        const int nr = (int)min((int64_t)r1, batch - tile * kTile);
+        f2v wc2[CPT][KH2];
+#pragma unroll
+        for (int j = 0; j < CPT; ++j)
+#pragma unroll
+            for (int o2 = 0; o2 < KH2; ++o2)
+                wc2[j][o2] = f2v{wc[j][2 * o2], 2 * o2 + 1 < KMAX ? wc[j][2 * o2 + 1] : 0.f};
+        int r = r0;
         for (; r + 4 <= nr; r += 4) {
-            float hv[4], gq[4][KP];
+            float hv[CPT][4], gq[4][KP];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                hv[u] = s_h[(r + u) * kS + t];
+#pragma unroll
+                for (int j = 0; j < CPT; ++j) hv[j][u] = s_h[(r + u) * kS + e + NT * j];
 #pragma unroll
                 for (int q = 0; q < KP; q += 4) {
                     const float4 g4 = *reinterpret_cast<const float4 *>(&s_dh[r + u][q]);
@@ -424,73 +444,84 @@ struct HeadEpi {
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                float d = 0.f;
-                if constexpr (kPk) {
-                    // d head . w over the even and the odd outputs as one packed chain, then their sum (o >= K:
-                    // s_dh and wc are 0)
-                    f2v d2 = {0.f, 0.f};
+            for (int u = 0; u < 4; ++u)
 #pragma unroll
-                    for (int o2 = 0; o2 < KH2; ++o2)
-                        d2 = __builtin_elementwise_fma(f2v{gq[u][2 * o2], gq[u][2 * o2 + 1]}, wc2[o2], d2);
-                    d = d2.x + d2.y;
-                    const f2v hh = {hv[u], hv[u]};
-#pragma unroll
-                    for (int o2 = 0; o2 < KH2; ++o2)  // KP >= 2 KH2: the pad slots of s_dh are 0
-                        acc_dw2[o2] = __builtin_elementwise_fma(f2v{gq[u][2 * o2], gq[u][2 * o2 + 1]}, hh, acc_dw2[o2]);
-                } else {
-#pragma unroll
-                    for (int o = 0; o < KMAX; ++o) {
-                        d += gq[u][o] * wc[o];
-                        acc_dw[o] += gq[u][o] * hv[u];
-                    }
-                }
-                d *= act_g<ACT>(hv[u], slope);
-#if XPA_HEAD_PROBE != 4  // 4 = epilogue alone without the dz stores
-                __builtin_nontemporal_store(d, dzt + (r + u) * ld);
-#endif
-                acc_dbh += d;
-            }
+                for (int j = 0; j < CPT; ++j) col_row(j, hv[j][u], gq[u], wc2[j], dz + (tile * kTile + r + u) * ld);
         }
         for (; r < nr; ++r) {
-            const float h = s_h[r * kS + t];
-            float d = 0.f;
-            if constexpr (kPk) {
-                f2v d2 = {0.f, 0.f};
+            float gq[KP];
 #pragma unroll
-                for (int o2 = 0; o2 < KH2; ++o2)
-                    d2 = __builtin_elementwise_fma(f2v{s_dh[r][2 * o2], s_dh[r][2 * o2 + 1]}, wc2[o2], d2);
-                d = d2.x + d2.y;
-                const f2v hh = {h, h};
+            for (int q = 0; q < KP; ++q) gq[q] = s_dh[r][q];
 #pragma unroll
-                for (int o2 = 0; o2 < KH2; ++o2)
-                    acc_dw2[o2] = __builtin_elementwise_fma(f2v{s_dh[r][2 * o2], s_dh[r][2 * o2 + 1]}, hh, acc_dw2[o2]);
-            } else {
-#pragma unroll
-                for (int o = 0; o < KMAX; ++o) {
-                    const float g = s_dh[r][o];
-                    d += g * wc[o];
-                    acc_dw[o] += g * h;
-                }
-            }
-            d *= act_g<ACT>(h, slope);
-#if XPA_HEAD_PROBE != 4
-            __builtin_nontemporal_store(d, dzt + r * ld);
-#endif
-            acc_dbh += d;
+            for (int j = 0; j < CPT; ++j) col_row(j, s_h[r * kS + e + NT * j], gq, wc2[j], dz + (tile * kTile + r) * ld);
         }
+    }
+    __device__ __forceinline__ void col_row(int j, float h, const float (&g)[KP], const f2v (&wc2)[KH2],
+                                            float *__restrict__ dzrow) {
+        float d = 0.f;
+        if constexpr (kPk) {
+            // d head . w over the even and the odd outputs as one packed chain, then their sum (o >= K: s_dh and wc
+            // are 0)
+            f2v d2 = {0.f, 0.f};
+#pragma unroll
+            for (int o2 = 0; o2 < KH2; ++o2) d2 = __builtin_elementwise_fma(f2v{g[2 * o2], g[2 * o2 + 1]}, wc2[o2], d2);
+            d = d2.x + d2.y;
+            const f2v hh = {h, h};
+#pragma unroll
+            for (int o2 = 0; o2 < KH2; ++o2)  // KP >= 2 KH2: the pad slots of s_dh are 0
+                acc_dw2[j][o2] = __builtin_elementwise_fma(f2v{g[2 * o2], g[2 * o2 + 1]}, hh, acc_dw2[j][o2]);
+        } else {
+#pragma unroll
+            for (int o = 0; o < KMAX; ++o) {
+                d += g[o] * wc[j][o];
+                acc_dw[j][o] += g[o] * h;
+            }
+        }
+        d *= act_g<ACT>(h, slope);
+#if XPA_HEAD_PROBE != 4  // 4 = epilogue alone without the dz stores
+        __builtin_nontemporal_store(d, dzrow + e + NT * j);
+#endif
+        acc_dbh[j] += d;
+    }
+
+    // K12 / K16 (NW = 4, the whole block): phase 1 -> loss -> phase 2 with the block barriers between.  Starts with a
+    // barrier (s_h complete), ends with one (s_h / s_dh free for the next tile).
+    __device__ __forceinline__ void tile(const float *s_h, float (*s_part)[kTile][PH], float (*s_dh)[KP],
+                                         const RowIn<KMAX> &in, int64_t tile, int64_t batch,
+                                         const float *__restrict__ W, const float *__restrict__ bias,
+                                         float *__restrict__ dz, int64_t ld, float ent_coef, float vf_coef) {
+        __syncthreads();
+#pragma unroll 1
+        for (int pass = 0; pass < NPASS; ++pass) {
+            if (pass > 0) __syncthreads();  // wave 0 has read the previous pass
+            p1(pass, s_h, s_part, W);
+            __syncthreads();
+            p1_sum(pass, s_part, bias);
+        }
+        loss(s_dh, in, ent_coef, vf_coef);
+        __syncthreads();
+        p2(s_h, s_dh, tile, batch, 0, kTile, dz, ld);
         __syncthreads();  // s_h / s_dh reused by the next tile
     }
 
+    // Per-block partial row `blk`; with `zero_blk` >= 0 also a row of zeros (K16W: rows its grid does not own).
     __device__ __forceinline__ void finish(float *__restrict__ p_dw, float *__restrict__ p_dbh,
-                                           float *__restrict__ p_dbo, float *__restrict__ p_loss, int loss_width) {
-        const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-        const int64_t blk = blockIdx.x;
+                                           float *__restrict__ p_dbo, float *__restrict__ p_loss, int loss_width,
+                                           int64_t blk, int64_t zero_blk = -1) {
+        const int lane = e & 63;
 #pragma unroll
-        for (int o = 0; o < KMAX; ++o)
-            if (o < K) p_dw[(blk * K + o) * kH + t] = kPk ? acc_dw2[o >> 1][o & 1] : acc_dw[kPk ? 0 : o];
-        p_dbh[blk * kH + t] = acc_dbh;
-        if (wave == 0) {
+        for (int j = 0; j < CPT; ++j) {
+            const int c = e + NT * j;
+#pragma unroll
+            for (int o = 0; o < KMAX; ++o)
+                if (o < K) {
+                    p_dw[(blk * K + o) * kH + c] = kPk ? acc_dw2[j][o >> 1][o & 1] : acc_dw[j][kPk ? 0 : o];
+                    if (zero_blk >= 0) p_dw[(zero_blk * K + o) * kH + c] = 0.f;
+                }
+            p_dbh[blk * kH + c] = acc_dbh[j];
+            if (zero_blk >= 0) p_dbh[zero_blk * kH + c] = 0.f;
+        }
+        if (e < 64) {
             sum0 = xpa_wave_sum(sum0);
             sum1 = xpa_wave_sum(sum1);
             sum2 = xpa_wave_sum(sum2);
@@ -511,11 +542,24 @@ struct HeadEpi {
                     prow[2] = sum1;
                     prow[3] = sum2;
                 }
+                float *zrow = zero_blk >= 0 ? p_loss + zero_blk * loss_width : nullptr;
+                if (zrow) {
+                    if (MODE == 2) {
+                        zrow[1] = 0.f;
+                        zrow[4] = 0.f;
+                    } else {
+                        zrow[0] = zrow[2] = zrow[3] = 0.f;
+                    }
+                }
 #pragma unroll
                 for (int o = 0; o < KMAX; ++o) {
                     if (o < K) {
                         p_dbo[blk * K + o] = acc_dbo[o];
                         if (MODE == 0) prow[kPartBase + o] = acc_dls[o];
+                        if (zrow) {
+                            p_dbo[zero_blk * K + o] = 0.f;
+                            if (MODE == 0) zrow[kPartBase + o] = 0.f;
+                        }
                     }
                 }
             }
@@ -547,7 +591,9 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(XPA_HEAD_KERNEL_PARAM
     float4 zq[16];
     load_tile(zq, z, ldx, tile, batch);
     Epi epi;
-    epi.init(K_in, W, logstd, adv_partials, n_adv_partials, batch, clip_range, slope, s_stats);
+    epi.init_a(t, K_in, W, logstd, adv_partials, n_adv_partials, batch, clip_range, slope, s_stats);
+    __syncthreads();
+    epi.init_b(s_stats);
     for (; tile < ntiles; tile += gridDim.x) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {  // stage h = act(z)
@@ -562,7 +608,7 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(XPA_HEAD_KERNEL_PARAM
         if (next < ntiles) load_tile(zq, z, ldx, next, batch);  // in flight during the epilogue
         epi.tile(s_h, s_part, s_dh, in, tile, batch, W, bias, dz, ld, ent_coef, vf_coef);
     }
-    epi.finish(p_dw, p_dbh, p_dbo, p_loss, loss_width);
+    epi.finish(p_dw, p_dbh, p_dbo, p_loss, loss_width, blockIdx.x);
 }
 
 // K16: the hidden layer's GEMM itself on the fp32 matrix cores, z = x Wh^T + bh for a [64 x 256] tile
@@ -721,7 +767,9 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
     const int64_t ntiles = (batch + kTile - 1) / kTile;
     if ((int64_t)blockIdx.x >= head_partials(batch)) return;  // no partial row of its own (see kGridMax)
     Epi epi;
-    epi.init(K_in, W, logstd, adv_partials, n_adv_partials, batch, clip_range, slope, s_stats);
+    epi.init_a(t, K_in, W, logstd, adv_partials, n_adv_partials, batch, clip_range, slope, s_stats);
+    __syncthreads();
+    epi.init_b(s_stats);
     const float bh0 = bh[wave * 64 + (lane & 31)], bh1 = bh[wave * 64 + 32 + (lane & 31)];
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t r0 = tile * kTile;
@@ -779,7 +827,158 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
         epi.tile(smem, s_part, s_dh, in, tile, batch, W, bias, dz, ld, ent_coef, vf_coef);
 #endif
     }
-    epi.finish(p_dw, p_dbh, p_dbo, p_loss, loss_width);
+    epi.finish(p_dw, p_dbh, p_dbo, p_loss, loss_width, blockIdx.x);
+}
+
+// K16W (r04): K16 with its waves specialised, one 512-thread block per CU persistent over 64-row tiles, so that the
+// K12 epilogue of tile n runs on other waves WHILE the matrix cores compute tile n + 1 (K16 runs them one after the
+// other inside a block; its two co-resident blocks overlap them only by chance).
+//   waves 0-3 (G): tile n + 1's hidden GEMM exactly as K16 (wave g: columns 64g .. 64g + 63 as 2 x 2 32x32 tiles,
+//                  v_mfma_f32_32x32x2_f32, the same k order), then h = act(z + bh) into the h tile;
+//   waves 4-5 (E): the K12 epilogue of tile n on the h tile, split into barrier-separated steps (phase-1 passes, their
+//                  sums + the loss, phase 2 in 8-row slices) that fit between the GEMM's k-chunk barriers;
+//   waves 6-7 (D): only the operand DMAs of the 3-stage ring (chunk q + 2 right after the barrier of chunk q, 10
+//                  global_load_lds_dwordx4 per wave and chunk), so their hand-counted vmcnt sees no other memory op.
+// One block barrier per k chunk (the D waves' vmcnt for chunk q before it), two per tile for the h hand-off.  The
+// chunk sequence runs on across a block's tiles, so the next tile's first chunks are in flight during the last ones.
+// Every output is K16's arithmetic (shared gemm_chunk and HeadEpi; NW = 2 only changes which thread runs a chain):
+// bit for bit K16's dz and partials (tests/test_gpu_fused_mlp.py).  KMAX <= 8 (the E waves' state beside G's
+// accumulators must fit 256 VGPRs); wider heads (C4's A = 17) keep K16.
+constexpr int kWsGridMax = 256;  // one block per CU
+constexpr int kWsP2Split = 8;    // phase-2 slices per tile (8 rows each)
+__host__ __device__ constexpr int64_t head_ws_grid(int64_t batch) {
+    return (batch + kTile - 1) / kTile < kWsGridMax ? (batch + kTile - 1) / kTile : kWsGridMax;
+}
+
+template <int MODE, int ALGO, int ACT, int KMAX>
+__global__ __launch_bounds__(512, 1) void head_gemm_ws_kernel(XPA_HEAD_KERNEL_PARAMS) {
+    static_assert(KMAX <= 8, "K16W: heads up to 8 wide");
+    using Epi = HeadEpi<MODE, ALGO, ACT, KMAX, 2>;
+    constexpr int kHOff = kStages * kStage;  // the ring, then the h tile (both live at once here)
+    constexpr int kPartOff = kHOff + kTile * kS;
+    constexpr int kDhOff = kPartOff + kWaves * kTile * Epi::PH;
+    constexpr int kStatsOff = kDhOff + kTile * Epi::KP;
+    static_assert((kStatsOff + 4) * 4 <= 160 * 1024, "K16W: one block per CU");
+    constexpr int kSteps = 2 * Epi::NPASS + kWsP2Split;  // E's steps per tile
+    static_assert(kSteps <= kChunks, "the epilogue steps fit between the GEMM's chunk barriers");
+    __shared__ __attribute__((aligned(16))) float lds[kStatsOff + 4];
+    float *smem = lds;
+    float *s_h = lds + kHOff;
+    auto s_part = reinterpret_cast<float(*)[kTile][Epi::PH]>(lds + kPartOff);
+    auto s_dh = reinterpret_cast<float(*)[Epi::KP]>(lds + kDhOff);
+    float *s_stats = lds + kStatsOff;
+    const unsigned lds_base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const bool is_g = wave < 4, is_e = wave == 4 || wave == 5, is_d = wave >= 6;
+    const int64_t ntiles = (batch + kTile - 1) / kTile;
+    const int64_t G = gridDim.x, blk = blockIdx.x;
+    if (blk >= ntiles) return;  // the grid is at most the tile count (head_ws_grid): never taken
+    const int64_t my_tiles = (ntiles - 1 - blk) / G + 1;
+    const int64_t nchunks = my_tiles * kChunks;
+    // Each role runs its own copy of the period / chunk loop (so the allocator sees G's accumulators and E's epilogue
+    // state in disjoint branches); every copy executes the same barrier sequence: per period, one per chunk (or per
+    // epilogue step in the last period) and the two of the h hand-off.
+    Epi epi;
+    if (is_e) epi.init_a(t - 256, K_in, W, logstd, adv_partials, n_adv_partials, batch, clip_range, slope, s_stats);
+    __syncthreads();  // s_stats; no DMA in flight yet
+    if (is_g) {
+        const float bh0 = bh[wave * 64 + (lane & 31)], bh1 = bh[wave * 64 + 32 + (lane & 31)];
+#pragma unroll 1
+        for (int64_t i = 0; i <= my_tiles; ++i) {
+            const bool gemm = i < my_tiles;
+            f32x16 acc[2][2];
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[rt][ct][r] = 0.f;
+            const int nph = gemm ? kChunks : kSteps;
+#pragma unroll 1
+            for (int c = 0; c < nph; ++c) {
+                asm volatile("s_barrier" ::: "memory");
+                if (gemm) gemm_chunk(smem + ((i * kChunks + c) % kStages) * kStage, acc, lane, wave);
+            }
+            asm volatile("s_barrier" ::: "memory");  // X: the E waves are done with the h tile of tile i - 1
+            if (gemm) {
+                // h = act(z + bh) into the h tile: C/D map row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col = lane & 31
+#pragma unroll
+                for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                    for (int ct = 0; ct < 2; ++ct) {
+                        const int col = wave * 64 + ct * 32 + (lane & 31);
+                        const float bc = ct ? bh1 : bh0;
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                            s_h[row * kS + col] = act_f<ACT>(acc[rt][ct][r] + bc, slope);
+                        }
+                    }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+            asm volatile("s_barrier" ::: "memory");  // Y: the h tile of tile i is complete
+        }
+    } else if (is_e) {
+        epi.init_b(s_stats);
+        RowIn<KMAX> in_cur = {}, in_nxt = {};
+#pragma unroll 1
+        for (int64_t i = 0; i <= my_tiles; ++i) {  // period i: the epilogue of the block's tile i - 1
+            const bool gemm = i < my_tiles, epil = i > 0;
+            const int64_t tile_e = blk + (i - 1) * G;
+            if (gemm) in_nxt = epi.rows(blk + i * G, batch, idx, n_rows, act, old_logp, adv, ret);  // used next period
+            const int nph = gemm ? kChunks : kSteps;
+#pragma unroll 1
+            for (int c = 0; c < nph; ++c) {
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the previous step's LDS writes done
+                if (!epil || c >= kSteps) continue;
+                if (c < 2 * Epi::NPASS) {
+                    const int pass = c >> 1;
+                    if ((c & 1) == 0) {
+                        epi.p1(pass, s_h, s_part, W);
+                    } else {
+                        epi.p1_sum(pass, s_part, bias);
+                        if (pass == Epi::NPASS - 1) epi.loss(s_dh, in_cur, ent_coef, vf_coef);
+                    }
+                } else {
+                    const int sl = c - 2 * Epi::NPASS;
+                    epi.p2(s_h, s_dh, tile_e, batch, sl * (kTile / kWsP2Split), (sl + 1) * (kTile / kWsP2Split), dz,
+                           ld);
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // X
+            asm volatile("s_barrier" ::: "memory");                           // Y
+            in_cur = in_nxt;
+        }
+        const int64_t np = head_partials(batch);
+        epi.finish(p_dw, p_dbh, p_dbo, p_loss, loss_width, blk, blk + G < np ? blk + G : -1);
+    } else {  // D: wave d issues the A / B rows K16's waves 2d and 2d + 1 would
+        const int d = wave - 6;
+        auto issue = [&](int64_t q) {
+            const int64_t tile = blk + (q / kChunks) * G;
+            const unsigned st = lds_base + (unsigned)((q % kStages) * kStage * 4);
+            gemm_issue(st, z, ldx, Wh, tile * kTile, batch, (int)(q % kChunks) * kKC, lane, 2 * d);
+            gemm_issue(st, z, ldx, Wh, tile * kTile, batch, (int)(q % kChunks) * kKC, lane, 2 * d + 1);
+        };
+        issue(0);
+        if (nchunks > 1) issue(1);
+#pragma unroll 1
+        for (int64_t i = 0; i <= my_tiles; ++i) {
+            const bool gemm = i < my_tiles;
+            const int nph = gemm ? kChunks : kSteps;
+#pragma unroll 1
+            for (int c = 0; c < nph; ++c) {
+                const int64_t q = i * kChunks + c;
+                // own DMAs of chunk q landed (chunk q + 1's may still fly), then the barrier: chunk q is in LDS for
+                // every wave and stage (q + 2) % 3 — chunk q - 1's — has been read
+                if (gemm && q + 1 < nchunks) asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+                if (gemm && q + 2 < nchunks) issue(q + 2);
+            }
+            asm volatile("s_barrier" ::: "memory");  // X
+            asm volatile("s_barrier" ::: "memory");  // Y
+        }
+    }
 }
 
 }  // namespace
@@ -795,7 +994,11 @@ namespace {
 template <int KIND, int MODE, int ALGO, int ACT, int KMAX>
 void launch_one(const HeadArgs &a, hipStream_t s) {
     const dim3 grid((unsigned)xpa_head_fused_num_partials(a.batch)), block(256);
-    if constexpr (KIND == 2)
+    if constexpr (KIND == 3) {
+        if constexpr (KMAX <= 8)
+            hipLaunchKernelGGL((head_gemm_ws_kernel<MODE, ALGO, ACT, KMAX>), dim3((unsigned)head_ws_grid(a.batch)),
+                               dim3(512), 0, s, XPA_HEAD_ARGS(a));
+    } else if constexpr (KIND == 2)
         hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, true>), grid, block, 0, s, XPA_HEAD_ARGS(a), a.xr,
                            a.ldxr, a.din, a.W0, a.b0, a.slope0, a.hout, a.ldh);
     else if constexpr (KIND == 1)
@@ -818,7 +1021,7 @@ void launch_head(const HeadArgs &a, int act_code, hipStream_t s) {
     else if (a.K <= 4) launch_act<KIND, MODE, ALGO, 4>(a, act_code, s);  // KMAX = smallest of 4 / 6 / 8 >= K
     else if (a.K <= 6) launch_act<KIND, MODE, ALGO, 6>(a, act_code, s);
     else if (a.K <= 8) launch_act<KIND, MODE, ALGO, 8>(a, act_code, s);
-    else if constexpr (KIND != 2) launch_act<KIND, MODE, ALGO, 18>(a, act_code, s);  // C4 (A = 17), 18-way categorical
+    else if constexpr (KIND != 2 && KIND != 3) launch_act<KIND, MODE, ALGO, 18>(a, act_code, s);  // C4 (A = 17), 18-way
 }
 #undef XPA_HEAD_ARGS
 
@@ -931,6 +1134,57 @@ XPA_API int xpa_head_gemm_critic(int act_code, int64_t batch, int64_t hidden, co
     a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
     a.loss_width = (int)loss_width;
     launch_head<1, 2, 0>(a, act_code, (hipStream_t)stream);
+    return xpa_launch_status();
+}
+
+// K16W entries: xpa_head_gemm_actor / _critic's arguments and outputs (the same partial-row count, rows the grid does
+// not own written as zeros); act_dim <= 8.
+XPA_API int64_t xpa_head_gemm_ws_grid(int64_t batch) {
+    return head_ws_grid(batch);
+}
+
+XPA_API int xpa_head_gemm_ws_actor(int algo, int dist, int act_code, int64_t batch, int64_t act_dim, int64_t hidden,
+                                   const float *x, int64_t ldx, const float *w_hidden, const float *b_hidden,
+                                   int64_t ld_dz, const float *w, const float *b, float slope, const float *logstd,
+                                   const int64_t *idx, int64_t n_rows, const float *act, const float *old_logp,
+                                   const float *adv, const double *adv_partials, int64_t n_adv_partials,
+                                   float clip_range, float ent_coef, float *dz, float *partial_dw,
+                                   float *partial_db_hidden, float *partial_db_out, float *loss_partials,
+                                   int64_t loss_width, xpa_stream_t stream) {
+    int rc = check_actor(algo, dist, act_code, batch, act_dim, hidden, w, b, logstd, n_rows, idx, act, old_logp, adv, dz,
+                         partial_dw, partial_db_hidden, partial_db_out, loss_partials, loss_width);
+    if (rc) return rc;
+    if (act_dim > 8 || !x || !w_hidden || !b_hidden || ((uintptr_t)x | (uintptr_t)w_hidden) % 16 || ldx < kKin ||
+        ldx % 4 || ld_dz < kH)
+        return (int)hipErrorInvalidValue;
+    HeadArgs a{};
+    a.batch = batch; a.K = (int)act_dim; a.ld = ld_dz; a.z = x; a.ldx = ldx; a.Wh = w_hidden; a.bh = b_hidden;
+    a.W = w; a.bias = b; a.slope = slope; a.logstd = logstd; a.idx = idx; a.n_rows = n_rows; a.act = act;
+    a.old_logp = old_logp; a.adv = adv; a.ret = nullptr; a.adv_partials = adv_partials;
+    a.n_adv_partials = n_adv_partials; a.clip_range = clip_range; a.ent_coef = ent_coef; a.vf_coef = 0.f; a.dz = dz;
+    a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
+    a.loss_width = (int)loss_width;
+    return actor_entry<3>(algo, dist, act_code, a, (hipStream_t)stream);
+}
+
+XPA_API int xpa_head_gemm_ws_critic(int act_code, int64_t batch, int64_t hidden, const float *x, int64_t ldx,
+                                    const float *w_hidden, const float *b_hidden, int64_t ld_dz, const float *w,
+                                    const float *b, float slope, const int64_t *idx, int64_t n_rows, const float *ret,
+                                    float vf_coef, float *dz, float *partial_dw, float *partial_db_hidden,
+                                    float *partial_db_out, float *loss_partials, int64_t loss_width,
+                                    xpa_stream_t stream) {
+    if (batch <= 0 || hidden != kH || act_code < 0 || act_code > 2 || !x || !w_hidden || !b_hidden || !w || !b ||
+        !ret || !dz || !partial_dw || !partial_db_hidden || !partial_db_out || !loss_partials ||
+        loss_width < kPartBase || n_rows <= 0 || (!idx && n_rows < batch))
+        return (int)hipErrorInvalidValue;
+    if (((uintptr_t)x | (uintptr_t)w_hidden | (uintptr_t)w) % 16 || ldx < kKin || ldx % 4 || ld_dz < kH)
+        return (int)hipErrorInvalidValue;
+    HeadArgs a{};
+    a.batch = batch; a.K = 1; a.ld = ld_dz; a.z = x; a.ldx = ldx; a.Wh = w_hidden; a.bh = b_hidden; a.W = w;
+    a.bias = b; a.slope = slope; a.idx = idx; a.n_rows = n_rows; a.ret = ret; a.vf_coef = vf_coef; a.dz = dz;
+    a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
+    a.loss_width = (int)loss_width;
+    launch_head<3, 2, 0>(a, act_code, (hipStream_t)stream);
     return xpa_launch_status();
 }
 

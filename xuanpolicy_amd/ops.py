@@ -510,6 +510,9 @@ class ColsumQueue:
         return total, written
 
 
+K16W_ENABLED = True   # fused_heads' gemm form: K16W (xpa_head_gemm_ws_*) where it applies, else K16
+
+
 def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, w_critic, b_critic, act_critic,
                 logstd, act, adv, ret, old_logp=None, idx=None, adv_partials=None, clip_range=0.2, vf_coef=0.25,
                 ent_coef=0.0, grads=None, colsum_queue=None, gemm=None, sq_logstd=None, defer_loss=False, trunk=None):
@@ -589,15 +592,19 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
                                           float(vf_coef), _p(ws.dz_critic), _p(ws.p_dw_critic), _p(ws.p_dbh_critic),
                                           _p(ws.p_dbo_critic), _p(ws.loss_partials), W, s), "xpa_head_gemm_critic")
     elif gemm is not None:
-        _lib.check(L.xpa_head_gemm_actor(ALGO[algo], DIST[dist], act_actor[0], B, K, H, _p(x), x.stride(0), _p(wha),
-                                         _p(bha), ld, _p(w_actor), _p(b_actor), float(act_actor[1]), p_logstd, _p(idx),
-                                         rows, _p(act), p_old, _p(adv), _p(adv_partials), n_adv, float(clip_range),
-                                         float(ent_coef), _p(ws.dz_actor), _p(ws.p_dw_actor), _p(ws.p_dbh_actor),
-                                         _p(ws.p_dbo_actor), _p(ws.loss_partials), W, s), "xpa_head_gemm_actor")
-        _lib.check(L.xpa_head_gemm_critic(act_critic[0], B, H, _p(x), x.stride(0), _p(whc), _p(bhc), ld, _p(w_critic),
-                                          _p(b_critic), float(act_critic[1]), _p(idx), rows, _p(ret), float(vf_coef),
-                                          _p(ws.dz_critic), _p(ws.p_dw_critic), _p(ws.p_dbh_critic),
-                                          _p(ws.p_dbo_critic), _p(ws.loss_partials), W, s), "xpa_head_gemm_critic")
+        # K16W (wave-specialised, the epilogue overlapped with the GEMM) for heads up to 8 wide; K16 otherwise
+        wsa = K16W_ENABLED and K <= 8
+        fa = L.xpa_head_gemm_ws_actor if wsa else L.xpa_head_gemm_actor
+        fc = L.xpa_head_gemm_ws_critic if K16W_ENABLED else L.xpa_head_gemm_critic
+        _lib.check(fa(ALGO[algo], DIST[dist], act_actor[0], B, K, H, _p(x), x.stride(0), _p(wha),
+                      _p(bha), ld, _p(w_actor), _p(b_actor), float(act_actor[1]), p_logstd, _p(idx),
+                      rows, _p(act), p_old, _p(adv), _p(adv_partials), n_adv, float(clip_range),
+                      float(ent_coef), _p(ws.dz_actor), _p(ws.p_dw_actor), _p(ws.p_dbh_actor),
+                      _p(ws.p_dbo_actor), _p(ws.loss_partials), W, s), "xpa_head_gemm_actor")
+        _lib.check(fc(act_critic[0], B, H, _p(x), x.stride(0), _p(whc), _p(bhc), ld, _p(w_critic),
+                      _p(b_critic), float(act_critic[1]), _p(idx), rows, _p(ret), float(vf_coef),
+                      _p(ws.dz_critic), _p(ws.p_dw_critic), _p(ws.p_dbh_critic),
+                      _p(ws.p_dbo_critic), _p(ws.loss_partials), W, s), "xpa_head_gemm_critic")
     else:
         _lib.check(L.xpa_head_fused_actor(ALGO[algo], DIST[dist], act_actor[0], B, K, H, ld, _p(z_actor), _p(w_actor),
                                           _p(b_actor), float(act_actor[1]), p_logstd, _p(idx), rows, _p(act), p_old,
