@@ -85,6 +85,34 @@ def finish_path_py(rew, val, term, start, end, bootstrap, gamma, lam, use_gae, a
             adv[t] = float(rew[t]) + gamma * vnext - float(val[t])
 
 
+def finish_path_np(rew, val, term, start, end, bootstrap, gamma, lam, use_gae, adv, ret):
+    """memory_tools.py:206-229 restated with its own data flow (np.append of the bootstrap, a reversed Python loop over
+    NumPy scalars): the CPU baseline's GAE, so the baseline pays what the reference pays for it (the C restatement in
+    gae_ref.c is ~8x faster; tools/cpu_calibrate.py)."""
+    path = np.arange(start, end).astype(np.int32)
+    vs = np.append(np.array(val[path]), [bootstrap], axis=0)
+    if use_gae:
+        rewards = np.array(rew[path])
+        advantages = np.zeros_like(rewards)
+        dones = np.array(term[path])
+        last = 0
+        for t in reversed(range(len(path))):
+            delta = rewards[t] + (1 - dones[t]) * gamma * vs[t + 1] - vs[t]
+            advantages[t] = last = delta + (1 - dones[t]) * gamma * lam * last
+        returns = advantages + vs[:-1]
+    else:
+        rewards = np.append(np.array(rew[path]), [bootstrap], axis=0)
+        returns = np.zeros_like(rewards)
+        run = 0.0
+        for t in reversed(range(len(rewards))):
+            run = rewards[t] + gamma * run
+            returns[t] = run
+        returns = returns[:-1]
+        advantages = rewards[:-1] + gamma * vs[1:] - vs[:-1]
+    ret[path] = returns
+    adv[path] = advantages
+
+
 def gae_rows(rew, val, term, closed, boot, gamma, lam, use_gae=True, adv=None, ret=None):
     """GAE over a full [N, T] buffer cut into paths by closure flags (see gae_ref.c)."""
     rew = np.ascontiguousarray(rew, np.float32)
@@ -118,13 +146,14 @@ class BufferRef:
     (memory_tools.py:526-560).  Records closures so tests can hand them to the GPU kernel."""
 
     def __init__(self, obs_shape, act_shape, aux_shape, n_envs, n_size, use_gae=True, use_advnorm=True,
-                 gamma=0.99, gae_lam=0.95, obs_dtype=np.float32):
+                 gamma=0.99, gae_lam=0.95, obs_dtype=np.float32, gae_impl="c"):
         self.obs_shape, self.act_shape, self.aux_shape = tuple(obs_shape), tuple(act_shape), dict(aux_shape or {})
         self.n_envs, self.n_size = n_envs, n_size
         self.buffer_size = n_envs * n_size
         self.use_gae, self.use_advnorm = use_gae, use_advnorm
         self.gamma, self.gae_lam = gamma, gae_lam
         self.obs_dtype = obs_dtype
+        self.gae_impl = gae_impl   # "c": gae_ref.c (checker); "np": the reference's own data flow (CPU baseline)
         self.start_ids = np.zeros(n_envs, np.int64)
         self.clear()
 
@@ -165,8 +194,11 @@ class BufferRef:
         if end > start:
             self.closed[i, end - 1] = 1
             self.boot[i, end - 1] = val
-            lib = _lib()
-            if lib is not None:
+            lib = _lib() if self.gae_impl == "c" else None
+            if self.gae_impl == "np":
+                finish_path_np(self.rewards[i], self.values[i], self.terminals[i], start, end, float(val),
+                               self.gamma, self.gae_lam, self.use_gae, self.advantages[i], self.returns[i])
+            elif lib is not None:
                 lib.oracle_finish_path(self.rewards[i], self.values[i], self.terminals[i], start, end, float(val),
                                        float(self.gamma), float(self.gae_lam), int(self.use_gae),
                                        self.advantages[i], self.returns[i])
@@ -507,7 +539,7 @@ class AgentLoopRef:
 
     def __init__(self, envs, policy, learner, n_steps, n_epoch, n_minibatch, gamma=0.99, gae_lambda=0.95,
                  algo="ppo", use_gae=True, use_advnorm=True, use_obsnorm=True, use_rewnorm=True,
-                 obsnorm_range=5.0, rewnorm_range=5.0, vectorized_env=None):
+                 obsnorm_range=5.0, rewnorm_range=5.0, vectorized_env=None, gae_impl="np"):
         self.envs = envs                          # list of per-env objects (Dummy) or None
         self.venv = vectorized_env                # SynthBoxVec (numpy-vectorised variant) or None
         self.n_envs = len(envs) if envs is not None else vectorized_env.num_envs
@@ -522,7 +554,8 @@ class AgentLoopRef:
         self.discrete = first.discrete if first is not None else vectorized_env.discrete
         act_shape = () if self.discrete else (A,)
         aux = {"old_logp": ()} if algo == "ppo" else {}
-        self.memory = BufferRef((D,), act_shape, aux, self.n_envs, n_steps, use_gae, use_advnorm, gamma, gae_lambda)
+        self.memory = BufferRef((D,), act_shape, aux, self.n_envs, n_steps, use_gae, use_advnorm, gamma, gae_lambda,
+                                gae_impl=gae_impl)
         self.obs_rms = RunningMeanStdRef((D,))
         self.ret_rms = RunningMeanStdRef(())
         self.returns = np.zeros(self.n_envs, np.float32)
