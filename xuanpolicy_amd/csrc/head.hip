@@ -321,6 +321,7 @@ struct HeadEpi {
 
     // ---- loss: epilogue wave 0, one lane per row (after the last p1_sum); d head -> s_dh ----
     __device__ __forceinline__ void loss(float (*s_dh)[KP], const RowIn<KMAX> &in, float ent_coef, float vf_coef) {
+#pragma clang fp contract(off)  // every product and sum rounded on its own: the same bits in every kernel inlining it
         if (e >= 64) return;
         const int lane = e;
         float dh_[KMAX];
@@ -458,6 +459,7 @@ struct HeadEpi {
     }
     __device__ __forceinline__ void col_row(int j, float h, const float (&g)[KP], const f2v (&wc2)[KH2],
                                             float *__restrict__ dzrow) {
+#pragma clang fp contract(off)
         float d = 0.f;
         if constexpr (kPk) {
             // d head . w over the even and the odd outputs as one packed chain, then their sum (o >= K: s_dh and wc
