@@ -62,6 +62,26 @@ def test_fast_path_iteration_matches_oracle(agent_name, discrete, A, ent):
     replay_last_step_iteration(agent, D, A, [H], discrete, algo, ent, n_epoch, n_mb, expect_mid_truncations=not discrete)
 
 
+@pytest.mark.parametrize("agent_name,discrete,A", [("PPO_Clip", False, 6), ("A2C", True, 8)])
+def test_fast_path_iteration_with_k16w_matches_oracle(agent_name, discrete, A, monkeypatch):
+    """The same end-to-end replay with the heads on K16W (xpa_head_gemm_ws_*: wave-specialised, the epilogue of one
+    tile overlapped with the next tile's GEMM) instead of K16 — the adv moments, the loss finalize, the partial rows
+    beyond its grid."""
+    from xuanpolicy_amd import ops
+    from xuanpolicy_amd.runner import build_synthbox_ppo
+    monkeypatch.setattr(ops, "K16W_ENABLED", True)
+    N, T, D, H = 512, 64, 17, 256
+    agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=D, act_dim=A, hidden=H, n_epoch=2, n_minibatch=4,
+                               seed=21, device=DEV, agent=agent_name, discrete=discrete, ent_coef=0.01,
+                               max_episode_steps=T + 17)
+    fm = agent.learner._fused_mlp()
+    assert fm is not None and fm.gemm_heads
+    agent.train(T, log=False)
+    agent.train(T - 1, log=False)
+    replay_last_step_iteration(agent, D, A, [H], discrete, "ppo" if agent_name == "PPO_Clip" else "a2c", 0.01, 2, 4,
+                               expect_mid_truncations=not discrete)
+
+
 def test_c4_shape_iteration_matches_oracle():
     """C4's per-shard shapes (BASELINE.json configs[3]: SynthBox(obs=376, act=17), ppo/mujoco.yaml, [256] nets) at a
     reduced N x T: the 376-wide trunk (no K13: the first layer is a library GEMM), the non-K14E rollout (K14 policy

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--probe", action="store_true", help="also time K16W with parts switched off")
     a = ap.parse_args()
     import torch
     from xuanpolicy_amd import ops
@@ -70,6 +71,20 @@ def main():
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) * 1e3 / a.reps
                 res.setdefault("%s_%s" % ("k16w" if ws else "k16", name), []).append(round(us, 2))
+    if a.probe:   # K16W with parts switched off (xpa_head_gemm_ws_probe): 1 no epilogue, 2 no MFMA, 4 no DMA
+        for mask in (1, 2, 4, 5, 3, 6, 7):
+            assert L.xpa_head_gemm_ws_probe(mask) == 0
+            for name, fn in (("actor", actor), ("critic", critic)):
+                fn(True)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.reps):
+                    fn(True)
+                e1.record()
+                torch.cuda.synchronize()
+                res["k16w_%s_probe%d" % (name, mask)] = [round(e0.elapsed_time(e1) * 1e3 / a.reps, 2)]
+        assert L.xpa_head_gemm_ws_probe(0) == 0
     floor = 2.0 * B * H * H / 157.3e12 * 1e6
     out = {"batch": B, "floor_us_per_head": round(floor, 2), "us_per_launch": res,
            "frac_of_fp32_mfma_peak": {k: round(floor / min(v), 3) for k, v in res.items()}}

@@ -42,12 +42,13 @@ __device__ __forceinline__ float act_g(float h, float slope) {  // d act / d z a
     return 1.f;
 }
 
-__device__ __forceinline__ void adv_stats(const double *partials, int64_t n, int64_t batch, float *mean, float *inv) {
-    if (threadIdx.x < 64) {
+__device__ __forceinline__ void adv_stats(const double *partials, int64_t n, int64_t batch, float *mean, float *inv,
+                                          int tid) {
+    if (tid < 64) {  // tid: the calling group's thread index (K16W's epilogue waves are not threads 0..63)
         // eight 16-B loads in flight per lane (n = 1024 partials at C2: 2 round trips instead of 16 at the start of
         // every block); each lane still adds its k = lane, lane + 64, ... in order
         double s = 0.0, q = 0.0;
-        int64_t k = threadIdx.x;
+        int64_t k = tid;
         for (; k + 7 * 64 < n; k += 8 * 64) {
             double2 v[8];
 #pragma unroll
@@ -64,7 +65,7 @@ __device__ __forceinline__ void adv_stats(const double *partials, int64_t n, int
         }
         s = xpa_wave_sum(s);
         q = xpa_wave_sum(q);
-        if (threadIdx.x == 0) {
+        if (tid == 0) {
             const double m = s / (double)batch;
             const double var = fmax(q / (double)batch - m * m, 0.0);
             *mean = (float)m;
@@ -188,7 +189,7 @@ struct HeadEpi {
         K = MODE == 2 ? 1 : K_in;
         slope = slope_;
         if (MODE != 2 && adv_partials) {
-            if (e < 64) adv_stats(adv_partials, n_adv_partials, batch, s_stats, s_stats + 1);
+            adv_stats(adv_partials, n_adv_partials, batch, s_stats, s_stats + 1, e);
         } else if (e == 0) {
             s_stats[0] = 0.f;
             s_stats[1] = 1.f;
@@ -848,6 +849,11 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
 // accumulators must fit 256 VGPRs); wider heads (C4's A = 17) keep K16.
 constexpr int kWsGridMax = 256;  // one block per CU
 constexpr int kWsP2Split = 8;    // phase-2 slices per tile (8 rows each)
+constexpr int kWsStages = 4;     // operand ring: chunk q + 3 is issued during chunk q (3 chunks of DMA flight time)
+constexpr int kWsDma = 10;       // DMAs per D wave and chunk
+// diagnostics (tools/k16w_ab.py --probe): bit 0 the E waves skip the epilogue steps, bit 1 the G waves skip their MFMAs
+// (and the h write), bit 2 the D waves issue no DMAs; every barrier stays.  0 in production.
+__device__ int g_ws_probe = 0;
 __host__ __device__ constexpr int64_t head_ws_grid(int64_t batch) {
     return (batch + kTile - 1) / kTile < kWsGridMax ? (batch + kTile - 1) / kTile : kWsGridMax;
 }
@@ -856,7 +862,7 @@ template <int MODE, int ALGO, int ACT, int KMAX>
 __global__ __launch_bounds__(512, 1) void head_gemm_ws_kernel(XPA_HEAD_KERNEL_PARAMS) {
     static_assert(KMAX <= 8, "K16W: heads up to 8 wide");
     using Epi = HeadEpi<MODE, ALGO, ACT, KMAX, 2>;
-    constexpr int kHOff = kStages * kStage;  // the ring, then the h tile (both live at once here)
+    constexpr int kHOff = kWsStages * kStage;  // the ring, then the h tile (both live at once here)
     constexpr int kPartOff = kHOff + kTile * kS;
     constexpr int kDhOff = kPartOff + kWaves * kTile * Epi::PH;
     constexpr int kStatsOff = kDhOff + kTile * Epi::KP;
@@ -878,6 +884,7 @@ __global__ __launch_bounds__(512, 1) void head_gemm_ws_kernel(XPA_HEAD_KERNEL_PA
     if (blk >= ntiles) return;  // the grid is at most the tile count (head_ws_grid): never taken
     const int64_t my_tiles = (ntiles - 1 - blk) / G + 1;
     const int64_t nchunks = my_tiles * kChunks;
+    const int probe = __builtin_amdgcn_readfirstlane(g_ws_probe);
     // Each role runs its own copy of the period / chunk loop (so the allocator sees G's accumulators and E's epilogue
     // state in disjoint branches); every copy executes the same barrier sequence: per period, one per chunk (or per
     // epilogue step in the last period) and the two of the h hand-off.
@@ -900,10 +907,10 @@ __global__ __launch_bounds__(512, 1) void head_gemm_ws_kernel(XPA_HEAD_KERNEL_PA
 #pragma unroll 1
             for (int c = 0; c < nph; ++c) {
                 asm volatile("s_barrier" ::: "memory");
-                if (gemm) gemm_chunk(smem + ((i * kChunks + c) % kStages) * kStage, acc, lane, wave);
+                if (gemm && !(probe & 2)) gemm_chunk(smem + ((i * kChunks + c) % kWsStages) * kStage, acc, lane, wave);
             }
             asm volatile("s_barrier" ::: "memory");  // X: the E waves are done with the h tile of tile i - 1
-            if (gemm) {
+            if (gemm && !(probe & 2)) {
                 // h = act(z + bh) into the h tile: C/D map row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col = lane & 31
 #pragma unroll
                 for (int rt = 0; rt < 2; ++rt)
@@ -933,7 +940,7 @@ __global__ __launch_bounds__(512, 1) void head_gemm_ws_kernel(XPA_HEAD_KERNEL_PA
 #pragma unroll 1
             for (int c = 0; c < nph; ++c) {
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the previous step's LDS writes done
-                if (!epil || c >= kSteps) continue;
+                if (!epil || c >= kSteps || (probe & 1)) continue;
                 if (c < 2 * Epi::NPASS) {
                     const int pass = c >> 1;
                     if ((c & 1) == 0) {
@@ -956,14 +963,16 @@ __global__ __launch_bounds__(512, 1) void head_gemm_ws_kernel(XPA_HEAD_KERNEL_PA
         epi.finish(p_dw, p_dbh, p_dbo, p_loss, loss_width, blk, blk + G < np ? blk + G : -1);
     } else {  // D: wave d issues the A / B rows K16's waves 2d and 2d + 1 would
         const int d = wave - 6;
+        const bool dma = !(probe & 4);
         auto issue = [&](int64_t q) {
+            if (!dma) return;
             const int64_t tile = blk + (q / kChunks) * G;
-            const unsigned st = lds_base + (unsigned)((q % kStages) * kStage * 4);
+            const unsigned st = lds_base + (unsigned)((q % kWsStages) * kStage * 4);
             gemm_issue(st, z, ldx, Wh, tile * kTile, batch, (int)(q % kChunks) * kKC, lane, 2 * d);
             gemm_issue(st, z, ldx, Wh, tile * kTile, batch, (int)(q % kChunks) * kKC, lane, 2 * d + 1);
         };
-        issue(0);
-        if (nchunks > 1) issue(1);
+        constexpr int L = kWsStages - 1;  // chunks in flight ahead of the one being consumed
+        for (int64_t q = 0; q < L && q < nchunks; ++q) issue(q);
 #pragma unroll 1
         for (int64_t i = 0; i <= my_tiles; ++i) {
             const bool gemm = i < my_tiles;
@@ -971,11 +980,13 @@ __global__ __launch_bounds__(512, 1) void head_gemm_ws_kernel(XPA_HEAD_KERNEL_PA
 #pragma unroll 1
             for (int c = 0; c < nph; ++c) {
                 const int64_t q = i * kChunks + c;
-                // own DMAs of chunk q landed (chunk q + 1's may still fly), then the barrier: chunk q is in LDS for
-                // every wave and stage (q + 2) % 3 — chunk q - 1's — has been read
-                if (gemm && q + 1 < nchunks) asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
+                // own DMAs of chunk q landed (the up to L - 1 chunks issued after it may still fly), then the barrier:
+                // chunk q is in LDS for every wave and stage (q + L) % kWsStages — chunk q - 1's — has been read
+                const int64_t after = gemm ? (q + L - 1 < nchunks ? L - 1 : nchunks - 1 - q) : 0;
+                if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * kWsDma) : "memory");
+                else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kWsDma) : "memory");
                 else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-                if (gemm && q + 2 < nchunks) issue(q + 2);
+                if (gemm && q + L < nchunks) issue(q + L);
             }
             asm volatile("s_barrier" ::: "memory");  // X
             asm volatile("s_barrier" ::: "memory");  // Y
@@ -1143,6 +1154,11 @@ XPA_API int xpa_head_gemm_critic(int act_code, int64_t batch, int64_t hidden, co
 // not own written as zeros); act_dim <= 8.
 XPA_API int64_t xpa_head_gemm_ws_grid(int64_t batch) {
     return head_ws_grid(batch);
+}
+
+// diagnostics only (tools/k16w_ab.py --probe): see g_ws_probe
+XPA_API int xpa_head_gemm_ws_probe(int mask) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ws_probe), &mask, sizeof(int));
 }
 
 XPA_API int xpa_head_gemm_ws_actor(int algo, int dist, int act_code, int64_t batch, int64_t act_dim, int64_t hidden,

@@ -510,7 +510,7 @@ class ColsumQueue:
         return total, written
 
 
-K16W_ENABLED = True   # fused_heads' gemm form: K16W (xpa_head_gemm_ws_*) where it applies, else K16
+K16W_ENABLED = False  # fused_heads' gemm form: K16W (xpa_head_gemm_ws_*) where it applies, else K16
 
 
 def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, w_critic, b_critic, act_critic,
