@@ -528,6 +528,9 @@ class LearnerRef:
         if self.algo == "ppo":
             lo, hi = 1 - self.clip_range, 1 + self.clip_range
             info["clip_ratio"] = float(((ratio < lo).sum() + (ratio > hi).sum()) / ratio.shape[0])
+            # rows whose ratio sits within f32 rounding of a clip bound: their side of it is not decided by the math
+            r = ratio.detach().double()
+            info["clip_boundary_rows"] = int(((r - lo).abs() < 1e-5).sum() + ((r - hi).abs() < 1e-5).sum())
         return info
 
 

@@ -153,7 +153,9 @@ def replay_updates(agent, pol, opt_state, lr0, sched_epoch, perm_counter, adv, r
                 assert abs(got[j] - info[k]) < 1e-4 * max(1.0, abs(info[k])), (k, u, got[j], info[k])
             assert abs(got[5] - info["predict_value"]) < 1e-4 * max(1.0, abs(info["predict_value"]))
             if algo == "ppo":
-                assert abs(got[4] - info["clip_ratio"]) <= 2.0 / B + 1e-7, ("clip_ratio", u, got[4], info["clip_ratio"])
+                # rows within f32 rounding of a clip bound may land on either side (counted by the oracle)
+                tol = (2.0 + info["clip_boundary_rows"]) / B + 1e-7
+                assert abs(got[4] - info["clip_ratio"]) <= tol, ("clip_ratio", u, got[4], info["clip_ratio"], tol)
             u += 1
     for (k, val), ref in zip(agent.policy.state_dict().items(), pol.state_dict().values()):
         np.testing.assert_allclose(val.detach().cpu().numpy(), ref.numpy(), rtol=1e-3, atol=1e-4, err_msg=k)
