@@ -536,6 +536,18 @@ int xpa_head_gemm_trunk_critic(int act, int64_t batch, int64_t hidden, const flo
                                float vf_coef, float *dz, float *partial_dw, float *partial_db_hidden,
                                float *partial_db_out, float *loss_partials, int64_t loss_width, xpa_stream_t stream);
 
+/* K40 — f32 GEMM on the bf16 matrix cores by a three-way split of each f32 operand into bf16 (hi + mid + lo, exact)
+ * and the six products above 2^-24 relative (csrc/sgemm3.hip): the f32 GEMM's accuracy at 2.67x the f32 MFMA rate.
+ * Replaces the hidden-layer matmuls of loss.backward() in PPOCLIP_Learner.update (ppoclip_learner.py:40-46) /
+ * A2C_Learner.update (a2c_learner.py:33-39) — here dX of the paired hidden layer, dz_pair [B, 512] . Wh_pair [512, 256].
+ * xpa_s3_split_b: B [k, n] with element (i, j) at b[i * sk + j * sn] -> out (xpa_s3_split_bytes(k, n) bytes, 16-B
+ *   aligned), the three bf16 planes in the GEMM's operand order; k % 16 == 0, n == 256.
+ * xpa_s3_gemm: c [m, 256] (row stride ldc) = a [m, k] (f32, row stride lda, 16-B aligned rows) . B, from B's split. */
+int64_t xpa_s3_split_bytes(int64_t k, int64_t n);
+int xpa_s3_split_b(const float *b, int64_t k, int64_t n, int64_t sk, int64_t sn, void *out, xpa_stream_t stream);
+int xpa_s3_gemm(const float *a, int64_t lda, const void *b_split, float *c, int64_t ldc, int64_t m, int64_t k, int64_t n,
+                xpa_stream_t stream);
+
 /* K6 — prioritized replay (PerOffPolicyBuffer, memory_tools.py:369-492; Sum/MinSegmentTree,
  * segtree_tool.py:4-86) with f64 trees on device: one [n_envs, 2*capacity] array per tree (node 1 =
  * root, leaf i at capacity + i; neutral 0 / +inf), capacity = next power of two >= n_size.

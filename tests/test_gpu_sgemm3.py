@@ -1,0 +1,90 @@
+"""GPU: K40, the f32 GEMM on the bf16 matrix cores by a three-way operand split (csrc/sgemm3.hip).
+
+The split must be exact (hi + mid + lo == x for every f32 operand element), and the GEMM must carry the f32 GEMM's
+own error: against an f64 product of the same f32 operands, K40's max abs error stays within 2x (+ a 2^-24-relative
+floor) of torch's f32 GEMM on the same device (hipBLASLt on the f32 matrix cores), on operands whose magnitudes
+span ~8 decades (exp of a normal), so every split plane is exercised."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _setup():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _wide(shape, g, scale=1.0):
+    return (torch.randn(shape, device=DEV, generator=g) * torch.exp(2 * torch.randn(shape, device=DEV, generator=g))
+            * scale)
+
+
+def _planes(split, k):
+    """Decode xpa_s3_split_b's layout back to three [k, 256] f64 planes (for the exactness check)."""
+    raw = split.view(torch.int16).cpu().numpy().astype(np.uint16).astype(np.uint32) << 16
+    v = raw.view(np.float32).astype(np.float64).reshape(k // 16, 3, 8, 2, 32, 8)
+    out = np.zeros((3, k, 256))
+    for h in range(2):
+        for j in range(8):
+            kk = 4 * h + j + (4 if j >= 4 else 0)
+            for cb in range(8):
+                out[:, kk::16, cb * 32:(cb + 1) * 32] = v[:, :, cb, h, :, j].transpose(1, 0, 2)
+    return out
+
+
+@pytest.mark.parametrize("k,transposed", [(512, False), (256, True), (16, False)])
+def test_split_is_exact(k, transposed):
+    from xuanpolicy_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(k)
+    src = _wide((256, k) if transposed else (k, 256), g)
+    b = src.t() if transposed else src
+    sp = ops.s3_split(b)
+    torch.cuda.synchronize()
+    pl = _planes(sp, k)
+    want = b.double().cpu().numpy()
+    assert np.array_equal(pl.sum(0), want)
+    # each plane is the round-to-nearest bf16 of what the previous ones leave
+    hi = b.to(torch.bfloat16).double().cpu().numpy()
+    assert np.array_equal(pl[0], hi)
+
+
+@pytest.mark.parametrize("m,k,lda_pad,t_b", [(65536, 512, 0, False), (1000, 512, 0, False), (4097, 256, 8, True),
+                                             (300, 256, 0, True), (1, 16, 0, False), (257, 32, 4, False)])
+def test_gemm_matches_f32_gemm_error(m, k, lda_pad, t_b):
+    from xuanpolicy_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(m + k)
+    abuf = _wide((m, k + lda_pad), g)
+    a = abuf[:, :k]
+    w = torch.randn(256, k, device=DEV, generator=g) / 16 if t_b else torch.randn(k, 256, device=DEV, generator=g) / 16
+    b = w.t() if t_b else w
+    out = torch.full((m, 256), float("nan"), device=DEV)
+    ops.s3_gemm(a, ops.s3_split(b), k, out=out)
+    native = torch.mm(a, b)
+    torch.cuda.synchronize()
+    ref = a.double() @ b.double()
+    scale = ref.abs().max().item()
+    err = (out.double() - ref).abs().max().item()
+    err_f32 = (native.double() - ref).abs().max().item()
+    assert torch.isfinite(out).all()
+    assert err <= 2 * err_f32 + 2 ** -24 * scale, (err, err_f32, scale)
+    # rms error: no systematic bias from the dropped terms
+    rms = (out.double() - ref).pow(2).mean().sqrt().item()
+    rms_f32 = (native.double() - ref).pow(2).mean().sqrt().item()
+    assert rms <= 2 * rms_f32 + 1e-30
+
+
+def test_gemm_rejects_bad_shapes():
+    from xuanpolicy_amd import _lib, ops
+    a = torch.randn(64, 24, device=DEV)
+    with pytest.raises(_lib.XpaError):
+        ops.s3_split(torch.randn(24, 256, device=DEV))          # k % 16
+    with pytest.raises(_lib.XpaError):
+        ops.s3_split(torch.randn(32, 128, device=DEV))          # n != 256
+    sp = ops.s3_split(torch.randn(32, 256, device=DEV))
+    with pytest.raises(_lib.XpaError):
+        ops.s3_gemm(a, sp, 24)
+    torch.cuda.synchronize()

@@ -17,7 +17,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "libxuanpolicy_amd.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
 SOURCES = ["gae.hip", "loss.hip", "rollout.hip", "optim.hip", "mlp.hip", "head.hip", "thin.hip", "per.hip", "atari.hip",
-           "classic.hip", "dqn.hip", "conv.hip", "igemm.hip", "smallmlp.hip"]
+           "classic.hip", "dqn.hip", "conv.hip", "igemm.hip", "smallmlp.hip", "sgemm3.hip"]
 HEADER = os.path.join(REPO_DIR, "include", "xuanpolicy_amd.h")
 
 ABI_VERSION = 3
@@ -211,6 +211,9 @@ SIGNATURES = {
     "xpa_head_gemm_trunk_critic": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p, c_f32, c_p,
                                                   c_i64, c_p, c_p, c_i64, c_p, c_p, c_f32, c_p, c_i64, c_p, c_f32, c_p,
                                                   c_p, c_p, c_p, c_p, c_i64, c_p]),
+    "xpa_s3_split_bytes": (c_i64, [c_i64, c_i64]),
+    "xpa_s3_split_b": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
+    "xpa_s3_gemm": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
     "xpa_grad_norm_num_partials": (c_i64, [c_i64]),
     "xpa_clip_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_p, c_f32, c_f32, c_f32, c_f32, c_f32, c_i64, c_p,
                                           c_p]),

@@ -1,0 +1,206 @@
+// K40 — the update's f32 GEMMs on the bf16 matrix cores by a three-way split (gfx950).
+//
+// gfx950 has no xf32 MFMA: f32 operands run on v_mfma_f32_32x32x2_f32 at 64 FLOP/clk/SIMD (157.3 TF), 1/16 of the
+// bf16 rate.  An f32 value splits EXACTLY into three bf16 values, x = hi + mid + lo (each the round-to-nearest bf16
+// of what the previous ones leave; 3 x 8 significant bits = the f32 significand), so
+//     a b = ah bh + (ah bm + am bh) + (am bm + ah bl + al bh) + [am bl + al bm + al bl]
+// where the bracketed terms are below 2^-24 relative and are dropped.  Every kept product of two bf16 values is
+// exact in f32 and v_mfma_f32_32x32x16_bf16 accumulates in f32, so a GEMM of the six products into one f32
+// accumulator carries the f32 GEMM's error (one rounding of the running sum per 16-k group of each product, where the
+// f32 MFMA rounds once per 2 k) at 6 x 16 / 16 = 6/16 of the f32 MFMA's cycles: 2.67x its arithmetic rate.
+// tests/test_gpu_sgemm3.py holds it to the f32 MFMA GEMM's own error against an f64 product.
+//
+// Reference: the hidden layers' matmuls inside loss.backward() of PPOCLIP_Learner.update / A2C_Learner.update
+// (ppoclip_learner.py:40-46, a2c_learner.py:33-39; torch f32 on the CPU): here the dX GEMM of the paired hidden layer,
+// g = dz_pair [B, 512] . Wh_pair [512, 256] (fused_mlp.FusedActorCritic.loss_backward).
+//
+//   xpa_s3_split_b : B [K, N] (any strides) -> its three bf16 planes, laid out as the k loop's LDS image
+//   xpa_s3_gemm    : C [M, 256] = A [M, K] (f32, row-major) . B (split), K % 16 == 0
+//
+// Mapping: 512 threads (8 waves), 256 rows per block, wave w owns rows [32 w, 32 w + 32) x all 256 columns (8
+// accumulators of 32 x 32).  Per 16-k chunk a stage holds the A image (256 rows x 64 B of f32, K16's XOR-swizzled
+// 16-B slots, DMA'd by each wave for its own rows) and the B image (3 planes x 256 columns x 32 B, one contiguous
+// 24 KiB run of the split buffer); both arrive by LDS-DMA (global_load_lds_dwordx4) through a 3-stage ring with the
+// counted vmcnt + one barrier per chunk of K16.  Each wave splits its A fragment (8 f32 per lane) in VALU and runs
+// 8 x 6 MFMAs per chunk.  The k order inside a chunk is permuted (lane half h takes the quads h and h + 2 of its row,
+// as K16) and the split kernel writes B's planes in that same order: any k order is exact as long as A and B agree.
+#include "xpa_common.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) char lds_char_t;
+
+constexpr int kN = 256;                     // output columns (all of them per block)
+constexpr int kWaves = 8;
+constexpr int kRows = 32 * kWaves;          // rows per block
+constexpr int kKC = 16;                     // k per chunk (one bf16 MFMA k step)
+constexpr int kAImg = kRows * kKC * 4;      // bytes, 16 KiB
+constexpr int kBImg = 3 * kN * kKC * 2;     // bytes, 24 KiB
+constexpr int kStage = kAImg + kBImg;       // 40 KiB
+constexpr int kStages = 3;
+constexpr int kDma = 2 + kBImg / 1024 / kWaves;  // per wave and chunk: 2 A + 3 B (the vmcnt of one chunk in flight)
+static_assert(kBImg % (1024 * kWaves) == 0, "B image splits evenly over the waves");
+
+__device__ __forceinline__ void glds16(const void *g, unsigned lds_wave_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds_wave_base)
+                 : "memory", "m0");
+}
+
+// the k of element j of lane half h inside a 16-k chunk (quads h and h + 2)
+__device__ __forceinline__ int kmap(int h, int j) { return 4 * h + j + (j >= 4 ? 4 : 0); }
+
+// x = hi + mid + lo exactly (round-to-nearest-even bf16 at each step; the residuals are exact in f32)
+__device__ __forceinline__ void split3(float x, __bf16 &hi, __bf16 &mid, __bf16 &lo) {
+    hi = (__bf16)x;
+    const float r1 = x - (float)hi;
+    mid = (__bf16)r1;
+    const float r2 = r1 - (float)mid;
+    lo = (__bf16)r2;
+}
+
+// ---- B -> three planes -------------------------------------------------------------------------------------
+// out (bf16): [K / 16 chunks][3 planes][8 column blocks][2 halves][32 columns][8]; element j of (chunk c, plane p,
+// block cb, half h, column r) is plane p of B[16 c + kmap(h, j)][32 cb + r].  One thread per (c, n, h).
+__global__ __launch_bounds__(256) void split_b_kernel(const float *__restrict__ b, int64_t K, int64_t sk, int64_t sn,
+                                                      __bf16 *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t total = (K / kKC) * kN * 2;
+    if (t >= total) return;
+    const int h = (int)(t & 1);
+    const int n = (int)((t >> 1) % kN);
+    const int64_t c = (t >> 1) / kN;
+    bf16x8 ph, pm, pl;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float x = b[(c * kKC + kmap(h, j)) * sk + (int64_t)n * sn];
+        __bf16 a0, a1, a2;
+        split3(x, a0, a1, a2);
+        ph[j] = a0;
+        pm[j] = a1;
+        pl[j] = a2;
+    }
+    const int cb = n >> 5, r = n & 31;
+    bf16x8 *o = reinterpret_cast<bf16x8 *>(out) + c * (3 * 8 * 64) + cb * 64 + h * 32 + r;
+    o[0] = ph;
+    o[8 * 64] = pm;
+    o[16 * 64] = pl;
+}
+
+// ---- the GEMM ---------------------------------------------------------------------------------------------
+// chunk c's DMAs of wave w into the stage at LDS byte address st: A rows r0 + 32 w .. + 31 (two 16-row
+// instructions, lane = (row, 16-B slot), slot p of row r holding k quad p ^ ((r >> 2) & 3)), then B's 1-KiB pieces
+// 3 w .. 3 w + 2 of the chunk's 24 KiB.  Rows past M re-read row M - 1 (never stored).
+__device__ __forceinline__ void issue(unsigned st, const float *__restrict__ a, int64_t lda,
+                                      const __bf16 *__restrict__ bs, int64_t r0, int64_t M, int c, int lane,
+                                      int wave) {
+    const int rr = lane >> 2, p = lane & 3;
+    const int q = p ^ ((rr >> 2) & 3);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        int64_t row = r0 + wave * 32 + i * 16 + rr;
+        row = row < M ? row : M - 1;
+        glds16(a + row * lda + c * kKC + 4 * q, st + (unsigned)((wave * 32 + i * 16) * kKC * 4));
+    }
+    const char *bsrc = reinterpret_cast<const char *>(bs) + (int64_t)c * kBImg;
+    constexpr int kPer = kBImg / 1024 / kWaves;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int piece = wave * kPer + j;
+        glds16(bsrc + piece * 1024 + lane * 16, st + (unsigned)(kAImg + piece * 1024));
+    }
+}
+
+__device__ __forceinline__ void chunk(const char *st, f32x16 (&acc)[8], int lane, int wave) {
+    const int h = lane >> 5, i = lane & 31;
+    const int sw = (i >> 2) & 3;
+    const float *arow = reinterpret_cast<const float *>(st) + (wave * 32 + i) * kKC;
+    const float4 alo = *reinterpret_cast<const float4 *>(arow + 4 * (h ^ sw));
+    const float4 ahi = *reinterpret_cast<const float4 *>(arow + 4 * ((h + 2) ^ sw));
+    const float av[8] = {alo.x, alo.y, alo.z, alo.w, ahi.x, ahi.y, ahi.z, ahi.w};
+    bf16x8 ah, am, al;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        __bf16 x0, x1, x2;
+        split3(av[j], x0, x1, x2);
+        ah[j] = x0;
+        am[j] = x1;
+        al[j] = x2;
+    }
+    const bf16x8 *bimg = reinterpret_cast<const bf16x8 *>(st + kAImg) + lane;
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) {
+        const bf16x8 bh = bimg[cb * 64], bm = bimg[(8 + cb) * 64], bl = bimg[(16 + cb) * 64];
+        // smallest terms first into the running sum
+        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc[cb], 0, 0, 0);
+        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[cb], 0, 0, 0);
+        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[cb], 0, 0, 0);
+        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc[cb], 0, 0, 0);
+        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc[cb], 0, 0, 0);
+        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[cb], 0, 0, 0);
+    }
+}
+
+__global__ __launch_bounds__(512, 1) void s3_gemm_kernel(const float *__restrict__ a, int64_t lda,
+                                                         const __bf16 *__restrict__ bs, float *__restrict__ c,
+                                                         int64_t ldc, int64_t M, int nchunks) {
+    // ONE LDS array (the DMA target; see head.hip)
+    __shared__ __attribute__((aligned(16))) char lds[kStages * kStage];
+    const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int64_t r0 = (int64_t)blockIdx.x * kRows;
+    f32x16 acc[8];
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[cb][r] = 0.f;
+    issue(base, a, lda, bs, r0, M, 0, lane, wave);
+    if (nchunks > 1) issue(base + kStage, a, lda, bs, r0, M, 1, lane, wave);
+#pragma unroll 1
+    for (int ch = 0; ch < nchunks; ++ch) {
+        // own DMAs of chunk ch landed (ch + 1's may still fly), then every wave's: the stage ch + 2 refills was
+        // read by every wave in chunk ch - 1
+        if (ch + 1 < nchunks) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kDma) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (ch + 2 < nchunks) issue(base + ((ch + 2) % kStages) * kStage, a, lda, bs, r0, M, ch + 2, lane, wave);
+        chunk(lds + (ch % kStages) * kStage, acc, lane, wave);
+    }
+    // C/D map of 32x32 MFMA: row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col = lane & 31
+    const int h = lane >> 5, col = lane & 31;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t row = r0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < M) {
+            float *crow = c + row * ldc + col;
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb) crow[cb * 32] = acc[cb][r];
+        }
+    }
+}
+
+}  // namespace
+
+XPA_API int64_t xpa_s3_split_bytes(int64_t k, int64_t n) {
+    return k * n * 3 * 2;
+}
+
+XPA_API int xpa_s3_split_b(const float *b, int64_t k, int64_t n, int64_t sk, int64_t sn, void *out,
+                           xpa_stream_t stream) {
+    if (!b || !out || k <= 0 || k % kKC != 0 || n != kN) return (int)hipErrorInvalidValue;
+    const int64_t total = (k / kKC) * kN * 2;
+    split_b_kernel<<<dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream>>>(b, k, sk, sn,
+                                                                                    static_cast<__bf16 *>(out));
+    return xpa_launch_status();
+}
+
+XPA_API int xpa_s3_gemm(const float *a, int64_t lda, const void *b_split, float *c, int64_t ldc, int64_t m, int64_t k,
+                        int64_t n, xpa_stream_t stream) {
+    if (!a || !b_split || !c || m <= 0 || k <= 0 || k % kKC != 0 || n != kN || lda < k || ldc < n ||
+        (reinterpret_cast<uintptr_t>(a) & 15) || (lda & 3) || k / kKC > (1 << 20))
+        return (int)hipErrorInvalidValue;
+    s3_gemm_kernel<<<dim3((unsigned)((m + kRows - 1) / kRows)), dim3(512), 0, stream>>>(
+        a, lda, static_cast<const __bf16 *>(b_split), c, ldc, m, (int)(k / kKC));
+    return xpa_launch_status();
+}

@@ -146,6 +146,35 @@ def _row_stride(t, name, cols):
 
 
 # ------------------------------------------------------------------------------------------------
+def s3_split(b, out=None):
+    """K40: the three bf16 planes of the f32 GEMM operand b [k, 256] (any strides; e.g. W.t() for x W^T), in the
+    layout xpa_s3_gemm reads.  Returns a uint8 device tensor of xpa_s3_split_bytes(k, 256) bytes."""
+    _req(b, "b", torch.float32, contiguous=False)
+    k, n = b.shape
+    nbytes = int(lib().xpa_s3_split_bytes(k, n))
+    if out is None:
+        out = torch.empty(nbytes, dtype=torch.uint8, device=b.device)
+    _req(out, "out", torch.uint8, (nbytes,))
+    _lib.check(lib().xpa_s3_split_b(_p(b), k, n, b.stride(0), b.stride(1), _p(out), _stream(b.device)),
+               "xpa_s3_split_b")
+    return out
+
+
+def s3_gemm(a, b_split, k, out=None):
+    """K40: out [m, 256] = a [m, k] . B for B split by s3_split (f32 accuracy on the bf16 matrix cores)."""
+    _req(a, "a", torch.float32, contiguous=False)
+    lda = _row_stride(a, "a", k)
+    m = a.shape[0]
+    if out is None:
+        out = torch.empty(m, 256, dtype=torch.float32, device=a.device)
+    ldc = _row_stride(out, "out", 256)
+    if out.shape[0] != m:
+        raise ValueError("out must have %d rows" % m)
+    _lib.check(lib().xpa_s3_gemm(_p(a), lda, _p(b_split), _p(out), ldc, m, k, 256, _stream(a.device)), "xpa_s3_gemm")
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
 def gae_scan(rew, val, term, closed, boot, gamma, gae_lambda, use_gae=True, adv=None, ret=None):
     """K1.  All [n_envs, horizon]; closed uint8, the rest float32.  Returns (adv, ret)."""
     N, T = rew.shape
