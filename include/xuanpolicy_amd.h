@@ -516,6 +516,22 @@ int xpa_head_gemm_ws_critic(int act, int64_t batch, int64_t hidden, const float 
                             float *partial_dw, float *partial_db_hidden, float *partial_db_out, float *loss_partials,
                             int64_t loss_width, xpa_stream_t stream);
 
+/* K16S — K16 with the hidden GEMM on the bf16 matrix cores by the three-way split of K40 (xpa_s3_gemm): the same
+ * arguments, outputs and epilogue as xpa_head_gemm_actor / _critic; the GEMM carries the f32 GEMM's error (not K16's
+ * bits) at 6/16 of its matrix-core cycles. */
+int xpa_head_gemm_s3_actor(int algo, int dist, int act, int64_t batch, int64_t act_dim, int64_t hidden, const float *x,
+                           int64_t ldx, const float *w_hidden, const float *b_hidden, int64_t ld_dz, const float *w,
+                           const float *b, float slope, const float *logstd, const int64_t *idx, int64_t n_rows,
+                           const float *act_buf, const float *old_logp, const float *adv, const double *adv_partials,
+                           int64_t n_adv_partials, float clip_range, float ent_coef, float *dz, float *partial_dw,
+                           float *partial_db_hidden, float *partial_db_out, float *loss_partials, int64_t loss_width,
+                           xpa_stream_t stream);
+int xpa_head_gemm_s3_critic(int act, int64_t batch, int64_t hidden, const float *x, int64_t ldx,
+                            const float *w_hidden, const float *b_hidden, int64_t ld_dz, const float *w, const float *b,
+                            float slope, const int64_t *idx, int64_t n_rows, const float *ret, float vf_coef, float *dz,
+                            float *partial_dw, float *partial_db_hidden, float *partial_db_out, float *loss_partials,
+                            int64_t loss_width, xpa_stream_t stream);
+
 /* K16X — K16 with the representation's first layer Linear(d_in <= 20, 256) + activation `act` (K13's, bit for bit)
  * in the prologue: each block forms its tile's h rows from the minibatch's gathered observation rows x_rows
  * [batch, d_in] (row stride ld_rows; e.g. xpa_thin_linear_act_fwd_gather with h = NULL), w_in [256, d_in], b_in [256],

@@ -412,22 +412,28 @@ def test_colsum_queue_deferred_loss_finalize(nseg, dist):
         assert total is None
 
 
-@pytest.mark.parametrize("algo,dist,K,B,code,ws", [
-    ("a2c", "categorical", 18, 777, 0, False),    # the r01 aperture-violation configuration
-    ("ppo", "gaussian", 17, 4133, 1, False),      # C4 head width, ragged tail (4133 = 64 * 64 + 37)
-    ("ppo", "categorical", 18, 193, 2, False),
-    ("a2c", "gaussian", 6, 65, 1, False),
-    ("ppo", "gaussian", 6, 64, 0, False),
+@pytest.mark.parametrize("algo,dist,K,B,code,form", [
+    ("a2c", "categorical", 18, 777, 0, "k16"),    # the r01 aperture-violation configuration
+    ("ppo", "gaussian", 17, 4133, 1, "k16"),      # C4 head width, ragged tail (4133 = 64 * 64 + 37)
+    ("ppo", "categorical", 18, 193, 2, "k16"),
+    ("a2c", "gaussian", 6, 65, 1, "k16"),
+    ("ppo", "gaussian", 6, 64, 0, "k16"),
     # K16W: ragged tails, one tile, a grid below the tile count (20037 rows = 314 tiles on 256 blocks: partial rows
     # 256..313 written as zeros), 8-wide heads
-    ("ppo", "gaussian", 6, 4133, 1, True),
-    ("a2c", "categorical", 8, 777, 0, True),
-    ("ppo", "categorical", 4, 64, 2, True),
-    ("ppo", "gaussian", 6, 20037, 1, True),
-    ("a2c", "gaussian", 8, 33, 1, True),
+    ("ppo", "gaussian", 6, 4133, 1, "ws"),
+    ("a2c", "categorical", 8, 777, 0, "ws"),
+    ("ppo", "categorical", 4, 64, 2, "ws"),
+    ("ppo", "gaussian", 6, 20037, 1, "ws"),
+    ("a2c", "gaussian", 8, 33, 1, "ws"),
+    # K16S (the GEMM by the bf16 three-way split): the K16 case matrix's shapes
+    ("a2c", "categorical", 18, 777, 0, "s3"),
+    ("ppo", "gaussian", 17, 4133, 1, "s3"),
+    ("ppo", "categorical", 18, 193, 2, "s3"),
+    ("ppo", "gaussian", 6, 20037, 1, "s3"),
+    ("a2c", "gaussian", 6, 65, 1, "s3"),
 ])
-def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code, ws):
-    """K16 (xpa_head_gemm_actor / _critic) or K16W (xpa_head_gemm_ws_*) through the C ABI against float64 autograd
+def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code, form):
+    """K16 (xpa_head_gemm_actor / _critic), K16W (xpa_head_gemm_ws_*) or K16S (xpa_head_gemm_s3_*) through the C ABI against float64 autograd
     of the same head:
     z = x Wh^T + bh, h = act(z), head = h W^T + b, the PPO-Clip / A2C loss with Gaussian / Categorical
     log-prob + entropy (ppoclip_learner.py:32-44, a2c_learner.py:24-31) and the critic's value loss.
@@ -476,8 +482,8 @@ def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code, ws):
     v = lambda t: ops._p(t[pad:])   # noqa: E731
     algo_c, dist_c = ops.ALGO[algo], ops.DIST[dist]
     ent, clip, vf = 0.01, 0.2, 0.25
-    fa = L.xpa_head_gemm_ws_actor if ws else L.xpa_head_gemm_actor
-    fc = L.xpa_head_gemm_ws_critic if ws else L.xpa_head_gemm_critic
+    pre = {"k16": "xpa_head_gemm_", "ws": "xpa_head_gemm_ws_", "s3": "xpa_head_gemm_s3_"}[form]
+    fa, fc = getattr(L, pre + "actor"), getattr(L, pre + "critic")
     assert fa(algo_c, dist_c, code, B, K, H, ops._p(x), H, ops._p(wh_a), ops._p(bh_a), 2 * H,
               ops._p(w_a), ops._p(b_a), slope, ops._p(logstd) if logstd is not None else None,
               ops._p(idx), R, ops._p(act), ops._p(old) if old is not None else None, ops._p(adv),

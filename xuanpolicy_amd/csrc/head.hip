@@ -14,6 +14,7 @@
 // columns, the critic launch the critic columns of the same partials array.
 // HBM: reads z (4 B/elem), writes dz (4 B/elem): 2 KiB per row at H = 256, plus the per-row inputs.
 #include "xpa_common.h"
+#include "s3_split.h"
 
 #ifndef XPA_HEAD_PROBE  // tools/head_probe.py builds variants with parts compiled out
 #define XPA_HEAD_PROBE 0
@@ -701,6 +702,35 @@ __device__ __forceinline__ void gemm_chunk(const float *st, f32x16 (&acc)[2][2],
     }
 }
 
+// K16S (r04): gemm_chunk's k step on the bf16 matrix cores by the three-way split (s3_split.h): the same LDS images
+// and fragment reads, each wave splits its two A and two B fragments (8 f32 per lane each) in VALU and runs 4 x 6
+// v_mfma_f32_32x32x16_bf16 (the element order j of a fragment is gemm_chunk's k order s2 — quads h, h + 2 — for A and
+// B alike).  2.67x fewer matrix-core cycles per chunk than the 32 f32 MFMAs; the f32 GEMM's accuracy, not its bits.
+__device__ __forceinline__ void gemm_chunk_s3(const float *st, f32x16 (&acc)[2][2], int lane, int wave) {
+    const float *A = st, *B = st + kAImg;
+    const int h = lane >> 5, i = lane & 31;
+    const int sw = (i >> 2) & 3;
+    const int olo = 4 * (h ^ sw), ohi = 4 * ((h + 2) ^ sw);
+    xpa_bf16x8 ah[2], am[2], al[2], bh[2], bm[2], bl[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+        const float *pa = A + (rt * 32 + i) * kKC;
+        xpa_split8(*reinterpret_cast<const float4 *>(pa + olo), *reinterpret_cast<const float4 *>(pa + ohi), ah[rt],
+                   am[rt], al[rt]);
+    }
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+        const float *pb = B + (wave * 64 + ct * 32 + i) * kKC;
+        xpa_split8(*reinterpret_cast<const float4 *>(pb + olo), *reinterpret_cast<const float4 *>(pb + ohi), bh[ct],
+                   bm[ct], bl[ct]);
+    }
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+            acc[rt][ct] = xpa_mfma_s3(ah[rt], am[rt], al[rt], bh[ct], bm[ct], bl[ct], acc[rt][ct]);
+}
+
 // K16X prologue (r03): the representation's first layer (K13's Linear(d_in <= 20, 256) + activation, bit for bit
 // its fmaf chain over the zero-padded inputs) for the tile's rows, from the minibatch's gathered observation rows;
 // thread t = column t; h goes to HBM (the backward's copy) with plain stores, so the k loop's A-operand DMAs right
@@ -747,7 +777,7 @@ __device__ __forceinline__ void trunk_prologue(float *s_x, const float *__restri
 
 // TRUNK (K16X, r03): the prologue above forms the tile's A rows (h) first; z / ldx are then ignored and the k loop
 // reads A from hout / ldh.
-template <int MODE, int ALGO, int ACT, int KMAX, bool TRUNK = false>
+template <int MODE, int ALGO, int ACT, int KMAX, bool TRUNK = false, bool S3 = false>
 __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAMS, const float *__restrict__ xr = nullptr,
                                                            int64_t ldxr = 0, int din = 0,
                                                            const float *__restrict__ W0 = nullptr,
@@ -805,7 +835,8 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
                 gemm_issue(lds_base + ((c + 2) % kStages) * kStage * 4, xa, lda, Wh, r0, batch, (c + 2) * kKC, lane,
                            wave);
 #if XPA_HEAD_PROBE != 3  // 3 = operand staging alone
-            gemm_chunk(smem + (c % kStages) * kStage, acc, lane, wave);
+            if constexpr (S3) gemm_chunk_s3(smem + (c % kStages) * kStage, acc, lane, wave);
+            else gemm_chunk(smem + (c % kStages) * kStage, acc, lane, wave);
 #endif
         }
         __syncthreads();  // every wave done with the stages before the h tile overwrites them
@@ -1003,7 +1034,8 @@ XPA_API int64_t xpa_head_fused_num_partials(int64_t batch) {
 
 namespace {
 #define XPA_HEAD_ARGS(a) a.batch, a.K, a.ld, a.z, a.ldx, a.Wh, a.bh, a.W, a.bias, a.slope, a.logstd, a.idx, a.n_rows, a.act, a.old_logp, a.adv, a.ret, a.adv_partials, a.n_adv_partials, a.clip_range, a.ent_coef, a.vf_coef, a.dz, a.p_dw, a.p_dbh, a.p_dbo, a.p_loss, a.loss_width
-// KIND: 0 K12 (z from HBM), 1 K16 (hidden GEMM inside), 2 K16X (trunk layer + hidden GEMM inside)
+// KIND: 0 K12 (z from HBM), 1 K16 (hidden GEMM inside), 2 K16X (trunk layer + hidden GEMM inside), 3 K16W,
+// 4 K16S (K16 with the hidden GEMM on the bf16 matrix cores by the three-way split)
 template <int KIND, int MODE, int ALGO, int ACT, int KMAX>
 void launch_one(const HeadArgs &a, hipStream_t s) {
     const dim3 grid((unsigned)xpa_head_fused_num_partials(a.batch)), block(256);
@@ -1011,7 +1043,10 @@ void launch_one(const HeadArgs &a, hipStream_t s) {
         if constexpr (KMAX <= 8)
             hipLaunchKernelGGL((head_gemm_ws_kernel<MODE, ALGO, ACT, KMAX>), dim3((unsigned)head_ws_grid(a.batch)),
                                dim3(512), 0, s, XPA_HEAD_ARGS(a));
-    } else if constexpr (KIND == 2)
+    } else if constexpr (KIND == 4)
+        hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, false, true>), grid, block, 0, s, XPA_HEAD_ARGS(a),
+                           nullptr, (int64_t)0, 0, nullptr, nullptr, 0.f, nullptr, (int64_t)0);
+    else if constexpr (KIND == 2)
         hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, true>), grid, block, 0, s, XPA_HEAD_ARGS(a), a.xr,
                            a.ldxr, a.din, a.W0, a.b0, a.slope0, a.hout, a.ldh);
     else if constexpr (KIND == 1)
@@ -1107,18 +1142,35 @@ XPA_API int xpa_head_fused_critic(int act_code, int64_t batch, int64_t hidden, i
     return xpa_launch_status();
 }
 
-XPA_API int xpa_head_gemm_actor(int algo, int dist, int act_code, int64_t batch, int64_t act_dim, int64_t hidden,
-                                const float *x, int64_t ldx, const float *w_hidden, const float *b_hidden, int64_t ld_dz,
-                                const float *w, const float *b, float slope, const float *logstd, const int64_t *idx,
-                                int64_t n_rows, const float *act, const float *old_logp, const float *adv,
-                                const double *adv_partials, int64_t n_adv_partials, float clip_range, float ent_coef,
-                                float *dz, float *partial_dw, float *partial_db_hidden, float *partial_db_out,
-                                float *loss_partials, int64_t loss_width, xpa_stream_t stream) {
+namespace {
+#define XPA_GEMM_ACTOR_PARAMS                                                                                          \
+    int algo, int dist, int act_code, int64_t batch, int64_t act_dim, int64_t hidden, const float *x, int64_t ldx,  \
+        const float *w_hidden, const float *b_hidden, int64_t ld_dz, const float *w, const float *b, float slope,   \
+        const float *logstd, const int64_t *idx, int64_t n_rows, const float *act, const float *old_logp,           \
+        const float *adv, const double *adv_partials, int64_t n_adv_partials, float clip_range, float ent_coef,     \
+        float *dz, float *partial_dw, float *partial_db_hidden, float *partial_db_out, float *loss_partials,        \
+        int64_t loss_width, xpa_stream_t stream
+#define XPA_GEMM_ACTOR_ARGS                                                                                            \
+    algo, dist, act_code, batch, act_dim, hidden, x, ldx, w_hidden, b_hidden, ld_dz, w, b, slope, logstd, idx, n_rows, \
+        act, old_logp, adv, adv_partials, n_adv_partials, clip_range, ent_coef, dz, partial_dw, partial_db_hidden,   \
+        partial_db_out, loss_partials, loss_width, stream
+#define XPA_GEMM_CRITIC_PARAMS                                                                                         \
+    int act_code, int64_t batch, int64_t hidden, const float *x, int64_t ldx, const float *w_hidden,                \
+        const float *b_hidden, int64_t ld_dz, const float *w, const float *b, float slope, const int64_t *idx,      \
+        int64_t n_rows, const float *ret, float vf_coef, float *dz, float *partial_dw, float *partial_db_hidden,     \
+        float *partial_db_out, float *loss_partials, int64_t loss_width, xpa_stream_t stream
+#define XPA_GEMM_CRITIC_ARGS                                                                                           \
+    act_code, batch, hidden, x, ldx, w_hidden, b_hidden, ld_dz, w, b, slope, idx, n_rows, ret, vf_coef, dz,         \
+        partial_dw, partial_db_hidden, partial_db_out, loss_partials, loss_width, stream
+
+// the hidden-GEMM head kernels' entries (KIND 1 K16, 3 K16W, 4 K16S): same arguments, same outputs
+template <int KIND>
+int gemm_actor_entry(XPA_GEMM_ACTOR_PARAMS) {
     int rc = check_actor(algo, dist, act_code, batch, act_dim, hidden, w, b, logstd, n_rows, idx, act, old_logp, adv, dz,
                          partial_dw, partial_db_hidden, partial_db_out, loss_partials, loss_width);
     if (rc) return rc;
-    if (!x || !w_hidden || !b_hidden || ((uintptr_t)x | (uintptr_t)w_hidden) % 16 || ldx < kKin || ldx % 4 ||
-        ld_dz < kH)
+    if ((KIND == 3 && act_dim > 8) || !x || !w_hidden || !b_hidden || ((uintptr_t)x | (uintptr_t)w_hidden) % 16 ||
+        ldx < kKin || ldx % 4 || ld_dz < kH)
         return (int)hipErrorInvalidValue;
     HeadArgs a{};
     a.batch = batch; a.K = (int)act_dim; a.ld = ld_dz; a.z = x; a.ldx = ldx; a.Wh = w_hidden; a.bh = b_hidden;
@@ -1127,14 +1179,11 @@ XPA_API int xpa_head_gemm_actor(int algo, int dist, int act_code, int64_t batch,
     a.n_adv_partials = n_adv_partials; a.clip_range = clip_range; a.ent_coef = ent_coef; a.vf_coef = 0.f; a.dz = dz;
     a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
     a.loss_width = (int)loss_width;
-    return actor_entry<1>(algo, dist, act_code, a, (hipStream_t)stream);
+    return actor_entry<KIND>(algo, dist, act_code, a, (hipStream_t)stream);
 }
 
-XPA_API int xpa_head_gemm_critic(int act_code, int64_t batch, int64_t hidden, const float *x, int64_t ldx,
-                                 const float *w_hidden, const float *b_hidden, int64_t ld_dz, const float *w,
-                                 const float *b, float slope, const int64_t *idx, int64_t n_rows, const float *ret,
-                                 float vf_coef, float *dz, float *partial_dw, float *partial_db_hidden,
-                                 float *partial_db_out, float *loss_partials, int64_t loss_width, xpa_stream_t stream) {
+template <int KIND>
+int gemm_critic_entry(XPA_GEMM_CRITIC_PARAMS) {
     if (batch <= 0 || hidden != kH || act_code < 0 || act_code > 2 || !x || !w_hidden || !b_hidden || !w || !b ||
         !ret || !dz || !partial_dw || !partial_db_hidden || !partial_db_out || !loss_partials ||
         loss_width < kPartBase || n_rows <= 0 || (!idx && n_rows < batch))
@@ -1146,9 +1195,16 @@ XPA_API int xpa_head_gemm_critic(int act_code, int64_t batch, int64_t hidden, co
     a.bias = b; a.slope = slope; a.idx = idx; a.n_rows = n_rows; a.ret = ret; a.vf_coef = vf_coef; a.dz = dz;
     a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
     a.loss_width = (int)loss_width;
-    launch_head<1, 2, 0>(a, act_code, (hipStream_t)stream);
+    launch_head<KIND, 2, 0>(a, act_code, (hipStream_t)stream);
     return xpa_launch_status();
 }
+}  // namespace
+
+XPA_API int xpa_head_gemm_actor(XPA_GEMM_ACTOR_PARAMS) { return gemm_actor_entry<1>(XPA_GEMM_ACTOR_ARGS); }
+XPA_API int xpa_head_gemm_critic(XPA_GEMM_CRITIC_PARAMS) { return gemm_critic_entry<1>(XPA_GEMM_CRITIC_ARGS); }
+// K16S: the same arguments and outputs; the hidden GEMM at the f32 GEMM's accuracy, not K16's bits
+XPA_API int xpa_head_gemm_s3_actor(XPA_GEMM_ACTOR_PARAMS) { return gemm_actor_entry<4>(XPA_GEMM_ACTOR_ARGS); }
+XPA_API int xpa_head_gemm_s3_critic(XPA_GEMM_CRITIC_PARAMS) { return gemm_critic_entry<4>(XPA_GEMM_CRITIC_ARGS); }
 
 // K16W entries: xpa_head_gemm_actor / _critic's arguments and outputs (the same partial-row count, rows the grid does
 // not own written as zeros); act_dim <= 8.
@@ -1161,50 +1217,12 @@ XPA_API int xpa_head_gemm_ws_probe(int mask) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ws_probe), &mask, sizeof(int));
 }
 
-XPA_API int xpa_head_gemm_ws_actor(int algo, int dist, int act_code, int64_t batch, int64_t act_dim, int64_t hidden,
-                                   const float *x, int64_t ldx, const float *w_hidden, const float *b_hidden,
-                                   int64_t ld_dz, const float *w, const float *b, float slope, const float *logstd,
-                                   const int64_t *idx, int64_t n_rows, const float *act, const float *old_logp,
-                                   const float *adv, const double *adv_partials, int64_t n_adv_partials,
-                                   float clip_range, float ent_coef, float *dz, float *partial_dw,
-                                   float *partial_db_hidden, float *partial_db_out, float *loss_partials,
-                                   int64_t loss_width, xpa_stream_t stream) {
-    int rc = check_actor(algo, dist, act_code, batch, act_dim, hidden, w, b, logstd, n_rows, idx, act, old_logp, adv, dz,
-                         partial_dw, partial_db_hidden, partial_db_out, loss_partials, loss_width);
-    if (rc) return rc;
-    if (act_dim > 8 || !x || !w_hidden || !b_hidden || ((uintptr_t)x | (uintptr_t)w_hidden) % 16 || ldx < kKin ||
-        ldx % 4 || ld_dz < kH)
-        return (int)hipErrorInvalidValue;
-    HeadArgs a{};
-    a.batch = batch; a.K = (int)act_dim; a.ld = ld_dz; a.z = x; a.ldx = ldx; a.Wh = w_hidden; a.bh = b_hidden;
-    a.W = w; a.bias = b; a.slope = slope; a.logstd = logstd; a.idx = idx; a.n_rows = n_rows; a.act = act;
-    a.old_logp = old_logp; a.adv = adv; a.ret = nullptr; a.adv_partials = adv_partials;
-    a.n_adv_partials = n_adv_partials; a.clip_range = clip_range; a.ent_coef = ent_coef; a.vf_coef = 0.f; a.dz = dz;
-    a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
-    a.loss_width = (int)loss_width;
-    return actor_entry<3>(algo, dist, act_code, a, (hipStream_t)stream);
-}
-
-XPA_API int xpa_head_gemm_ws_critic(int act_code, int64_t batch, int64_t hidden, const float *x, int64_t ldx,
-                                    const float *w_hidden, const float *b_hidden, int64_t ld_dz, const float *w,
-                                    const float *b, float slope, const int64_t *idx, int64_t n_rows, const float *ret,
-                                    float vf_coef, float *dz, float *partial_dw, float *partial_db_hidden,
-                                    float *partial_db_out, float *loss_partials, int64_t loss_width,
-                                    xpa_stream_t stream) {
-    if (batch <= 0 || hidden != kH || act_code < 0 || act_code > 2 || !x || !w_hidden || !b_hidden || !w || !b ||
-        !ret || !dz || !partial_dw || !partial_db_hidden || !partial_db_out || !loss_partials ||
-        loss_width < kPartBase || n_rows <= 0 || (!idx && n_rows < batch))
-        return (int)hipErrorInvalidValue;
-    if (((uintptr_t)x | (uintptr_t)w_hidden | (uintptr_t)w) % 16 || ldx < kKin || ldx % 4 || ld_dz < kH)
-        return (int)hipErrorInvalidValue;
-    HeadArgs a{};
-    a.batch = batch; a.K = 1; a.ld = ld_dz; a.z = x; a.ldx = ldx; a.Wh = w_hidden; a.bh = b_hidden; a.W = w;
-    a.bias = b; a.slope = slope; a.idx = idx; a.n_rows = n_rows; a.ret = ret; a.vf_coef = vf_coef; a.dz = dz;
-    a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
-    a.loss_width = (int)loss_width;
-    launch_head<3, 2, 0>(a, act_code, (hipStream_t)stream);
-    return xpa_launch_status();
-}
+XPA_API int xpa_head_gemm_ws_actor(XPA_GEMM_ACTOR_PARAMS) { return gemm_actor_entry<3>(XPA_GEMM_ACTOR_ARGS); }
+XPA_API int xpa_head_gemm_ws_critic(XPA_GEMM_CRITIC_PARAMS) { return gemm_critic_entry<3>(XPA_GEMM_CRITIC_ARGS); }
+#undef XPA_GEMM_ACTOR_PARAMS
+#undef XPA_GEMM_ACTOR_ARGS
+#undef XPA_GEMM_CRITIC_PARAMS
+#undef XPA_GEMM_CRITIC_ARGS
 
 namespace {
 int check_trunk(int64_t d_in, const float *x_rows, int64_t ld_rows, const float *w_in, const float *b_in,

@@ -25,11 +25,12 @@
 // 8 x 6 MFMAs per chunk.  The k order inside a chunk is permuted (lane half h takes the quads h and h + 2 of its row,
 // as K16) and the split kernel writes B's planes in that same order: any k order is exact as long as A and B agree.
 #include "xpa_common.h"
+#include "s3_split.h"
 
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef xpa_f32x16 f32x16;
+typedef xpa_bf16x8 bf16x8;
 typedef __attribute__((address_space(3))) char lds_char_t;
 
 constexpr int kN = 256;                     // output columns (all of them per block)
@@ -51,15 +52,6 @@ __device__ __forceinline__ void glds16(const void *g, unsigned lds_wave_base) {
 // the k of element j of lane half h inside a 16-k chunk (quads h and h + 2)
 __device__ __forceinline__ int kmap(int h, int j) { return 4 * h + j + (j >= 4 ? 4 : 0); }
 
-// x = hi + mid + lo exactly (round-to-nearest-even bf16 at each step; the residuals are exact in f32)
-__device__ __forceinline__ void split3(float x, __bf16 &hi, __bf16 &mid, __bf16 &lo) {
-    hi = (__bf16)x;
-    const float r1 = x - (float)hi;
-    mid = (__bf16)r1;
-    const float r2 = r1 - (float)mid;
-    lo = (__bf16)r2;
-}
-
 // ---- B -> three planes -------------------------------------------------------------------------------------
 // out (bf16): [K / 16 chunks][3 planes][8 column blocks][2 halves][32 columns][8]; element j of (chunk c, plane p,
 // block cb, half h, column r) is plane p of B[16 c + kmap(h, j)][32 cb + r].  One thread per (c, n, h).
@@ -76,7 +68,7 @@ __global__ __launch_bounds__(256) void split_b_kernel(const float *__restrict__ 
     for (int j = 0; j < 8; ++j) {
         const float x = b[(c * kKC + kmap(h, j)) * sk + (int64_t)n * sn];
         __bf16 a0, a1, a2;
-        split3(x, a0, a1, a2);
+        xpa_split3(x, a0, a1, a2);
         ph[j] = a0;
         pm[j] = a1;
         pl[j] = a2;
@@ -118,28 +110,12 @@ __device__ __forceinline__ void chunk(const char *st, f32x16 (&acc)[8], int lane
     const float *arow = reinterpret_cast<const float *>(st) + (wave * 32 + i) * kKC;
     const float4 alo = *reinterpret_cast<const float4 *>(arow + 4 * (h ^ sw));
     const float4 ahi = *reinterpret_cast<const float4 *>(arow + 4 * ((h + 2) ^ sw));
-    const float av[8] = {alo.x, alo.y, alo.z, alo.w, ahi.x, ahi.y, ahi.z, ahi.w};
     bf16x8 ah, am, al;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        __bf16 x0, x1, x2;
-        split3(av[j], x0, x1, x2);
-        ah[j] = x0;
-        am[j] = x1;
-        al[j] = x2;
-    }
+    xpa_split8(alo, ahi, ah, am, al);
     const bf16x8 *bimg = reinterpret_cast<const bf16x8 *>(st + kAImg) + lane;
 #pragma unroll
-    for (int cb = 0; cb < 8; ++cb) {
-        const bf16x8 bh = bimg[cb * 64], bm = bimg[(8 + cb) * 64], bl = bimg[(16 + cb) * 64];
-        // smallest terms first into the running sum
-        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc[cb], 0, 0, 0);
-        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[cb], 0, 0, 0);
-        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[cb], 0, 0, 0);
-        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc[cb], 0, 0, 0);
-        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc[cb], 0, 0, 0);
-        acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[cb], 0, 0, 0);
-    }
+    for (int cb = 0; cb < 8; ++cb)
+        acc[cb] = xpa_mfma_s3(ah, am, al, bimg[cb * 64], bimg[(8 + cb) * 64], bimg[(16 + cb) * 64], acc[cb]);
 }
 
 __global__ __launch_bounds__(512, 1) void s3_gemm_kernel(const float *__restrict__ a, int64_t lda,
