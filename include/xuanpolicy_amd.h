@@ -563,6 +563,13 @@ int64_t xpa_s3_split_bytes(int64_t k, int64_t n);
 int xpa_s3_split_b(const float *b, int64_t k, int64_t n, int64_t sk, int64_t sn, void *out, xpa_stream_t stream);
 int xpa_s3_gemm(const float *a, int64_t lda, const void *b_split, float *c, int64_t ldc, int64_t m, int64_t k, int64_t n,
                 xpa_stream_t stream);
+/* K41 — the weight gradient dW = a^T b over the batch on the same split (a [rows, m] = dz, row stride lda; b [rows, 256]
+ * = the layer input, row stride ldb; m % 128 == 0), split-K: out [slices, m, 256] holds one partial per slice of
+ * ceil(rows / slices) rows (rounded up to 32), summed by the caller — the learner's fixed-order f64 finalize, as for
+ * the batched f32 GEMM it replaces.  xpa_s3_wgrad_num_slices: the slice count that fills the chip (0: bad shape). */
+int64_t xpa_s3_wgrad_num_slices(int64_t rows, int64_t m);
+int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ldb, int64_t rows, int64_t m, int64_t n,
+                 int64_t slices, float *out, xpa_stream_t stream);
 
 /* K6 — prioritized replay (PerOffPolicyBuffer, memory_tools.py:369-492; Sum/MinSegmentTree,
  * segtree_tool.py:4-86) with f64 trees on device: one [n_envs, 2*capacity] array per tree (node 1 =

@@ -88,3 +88,26 @@ def test_gemm_rejects_bad_shapes():
     with pytest.raises(_lib.XpaError):
         ops.s3_gemm(a, sp, 24)
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("rows,m,lda_pad,slices", [(65536, 512, 0, None), (65536, 256, 0, None), (4133, 512, 8, None),
+                                                   (100, 128, 0, 1), (1000, 256, 4, 7), (33, 128, 0, 2)])
+def test_wgrad_matches_f32_gemm_error(rows, m, lda_pad, slices):
+    """K41: the slices' sum of dz^T x against an f64 product, within the f32 GEMM's own error (torch's dz^T x on the
+    device); ragged slices (rows not a multiple of the slice count or of 32) and strided rows."""
+    from xuanpolicy_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(rows + m)
+    a = _wide((rows, m + lda_pad), g)[:, :m]
+    b = torch.randn(rows, 256, device=DEV, generator=g)
+    part = ops.s3_wgrad(a, b, slices=slices)
+    S = part.shape[0]
+    assert S == (slices or ops.s3_wgrad_slices(rows, m))
+    got = part.double().sum(0)
+    native = torch.mm(a.t(), b)
+    torch.cuda.synchronize()
+    ref = a.double().t() @ b.double()
+    scale = ref.abs().max().item()
+    err = (got - ref).abs().max().item()
+    err_f32 = (native.double() - ref).abs().max().item()
+    assert torch.isfinite(part).all()
+    assert err <= 2 * err_f32 + 2 ** -24 * scale, (err, err_f32, scale)

@@ -55,6 +55,22 @@ def main():
         r["bf16x6_floor_us"] = round(6 * flop / 2.5e15 * 1e6, 2)
         r["s3_frac_of_f32_floor"] = round(r["f32_floor_us"] / min(r["s3_us"]), 3)
         r["torch_frac_of_f32_floor"] = round(r["f32_floor_us"] / min(r["torch_us"]), 3)
+    # K41: dW = dz^T x (the paired hidden layer's weight gradient) vs the learner's split-K batched f32 GEMM (8 slices)
+    B = 65536
+    dz = torch.randn(B, 512, device=dev, generator=g)
+    x = torch.randn(B, 256, device=dev, generator=g)
+    S = ops.s3_wgrad_slices(B, 512)
+    part = torch.empty(S, 512, 256, device=dev)
+    ws8 = torch.empty(8, 512, 256, device=dev)
+    r = res.setdefault("wgrad_B%d_M512" % B, {"s3_us": [], "torch_bmm8_us": [], "slices": S})
+    for _ in range(a.rounds):
+        r["s3_us"].append(round(_time(lambda: ops.s3_wgrad(dz, x, out=part), a.reps), 2))
+        r["torch_bmm8_us"].append(round(_time(lambda: torch.bmm(dz.view(8, B // 8, 512).transpose(1, 2),
+                                                                  x.view(8, B // 8, 256), out=ws8), a.reps), 2))
+    flop = 2.0 * B * 512 * 256
+    r["f32_floor_us"] = round(flop / 157.3e12 * 1e6, 2)
+    r["s3_frac_of_f32_floor"] = round(r["f32_floor_us"] / min(r["s3_us"]), 3)
+    r["torch_frac_of_f32_floor"] = round(r["f32_floor_us"] / min(r["torch_bmm8_us"]), 3)
     print(json.dumps(res))
     if a.out:
         with open(a.out, "w") as f:

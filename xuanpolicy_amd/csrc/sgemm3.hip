@@ -156,7 +156,156 @@ __global__ __launch_bounds__(512, 1) void s3_gemm_kernel(const float *__restrict
     }
 }
 
+// ---- K41: weight gradients dW = A^T B over the batch (K = rows), split-K -----------------------------------
+// out[s] [M, 256] = A[rows of slice s]^T . B[rows of slice s], A [rows, M] (dz), B [rows, 256] (the layer input);
+// the slices are summed by the caller (the learner's fixed-order f64 column-sum finalize), as the batched f32 GEMM
+// it replaces.  Both operands are k-major (k = batch row), so they are staged through registers: per 32-row chunk a
+// thread loads 8 k-strided values of one column for each of its 3 units (one A, two B: 512 + 1024 units of (column,
+// k step, lane half) per chunk), splits them and writes the three bf16 fragments (16 B each) straight into the
+// MFMA-ready LDS image [plane][column block][k step][64 lanes][16 B] — conflict-free ds_write_b128 / ds_read_b128.
+// Block: 512 threads, a 128 x 256 tile of out[s]; wave w owns rows 64 (w & 1) .. + 63 x columns 64 (w >> 1) .. + 63
+// (2 x 2 accumulators).  Two stages (72 KiB each): chunk c + 1's loads land in registers while chunk c's 48 MFMAs
+// per wave run, one raw barrier per chunk (a __syncthreads would also wait for those loads: vmcnt counts both).
+// Blocks of one slice sit on one XCD (blockIdx % 8 is the XCD), so the M / 128 tiles re-read B's rows from one L2.
+constexpr int kWgM = 128;
+constexpr int kWgKC = 32;
+constexpr int kWgAImg = 3 * 4 * 2 * 1024;  // bytes: [3 planes][4 row blocks][2 k steps][64 lanes][16 B]
+constexpr int kWgBImg = 3 * 8 * 2 * 1024;  // [3][8 column blocks][2][64][16 B]
+constexpr int kWgStage = kWgAImg + kWgBImg;  // 72 KiB
+
+struct WgUnits {
+    float a[8], b0[8], b1[8];
+};
+
+// chunk at k0 (rows < kend): A unit (column ma, k step sa, half ha), B units (column nb, k step sb, halves 0 / 1)
+__device__ __forceinline__ void wg_load(WgUnits &u, const float *__restrict__ A, int64_t lda, const float *__restrict__ B,
+                                        int64_t ldb, int64_t k0, int64_t kend, int ma, int sa, int ha, int nb, int sb) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int64_t ra = k0 + 16 * sa + kmap(ha, j);
+        const int64_t rb0 = k0 + 16 * sb + kmap(0, j), rb1 = k0 + 16 * sb + kmap(1, j);
+        // rows past the slice re-read its last row (branch-free loads), then count as 0
+        const float va = A[min(ra, kend - 1) * lda + ma];
+        const float v0 = B[min(rb0, kend - 1) * ldb + nb], v1 = B[min(rb1, kend - 1) * ldb + nb];
+        u.a[j] = ra < kend ? va : 0.f;
+        u.b0[j] = rb0 < kend ? v0 : 0.f;
+        u.b1[j] = rb1 < kend ? v1 : 0.f;
+    }
+}
+
+__device__ __forceinline__ void wg_put(char *st, const float (&v)[8], int off) {
+    bf16x8 h, m, l;
+    xpa_split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), h, m, l);
+    *reinterpret_cast<bf16x8 *>(st + off) = h;
+    *reinterpret_cast<bf16x8 *>(st + off + 8 * 1024 * ((off < kWgAImg) ? 1 : 2)) = m;  // plane stride
+    *reinterpret_cast<bf16x8 *>(st + off + 16 * 1024 * ((off < kWgAImg) ? 1 : 2)) = l;
+}
+
+__device__ __forceinline__ void wg_store(char *st, const WgUnits &u, int ml, int sa, int ha, int nb, int sb) {
+    // A image: plane stride 8 KiB ([4][2][64][16]), B image: 16 KiB ([8][2][64][16])
+    wg_put(st, u.a, (((ml >> 5) * 2 + sa) * 64 + ha * 32 + (ml & 31)) * 16);
+    wg_put(st, u.b0, kWgAImg + (((nb >> 5) * 2 + sb) * 64 + (nb & 31)) * 16);
+    wg_put(st, u.b1, kWgAImg + (((nb >> 5) * 2 + sb) * 64 + 32 + (nb & 31)) * 16);
+}
+
+__device__ __forceinline__ void wg_chunk(const char *st, f32x16 (&acc)[2][2], int lane, int wm, int wn) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        bf16x8 ah[2], am[2], al[2], bh[2], bm[2], bl[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const bf16x8 *pa = reinterpret_cast<const bf16x8 *>(st) + ((2 * wm + i) * 2 + s) * 64 + lane;
+            ah[i] = pa[0];
+            am[i] = pa[8 * 64];
+            al[i] = pa[16 * 64];
+            const bf16x8 *pb = reinterpret_cast<const bf16x8 *>(st + kWgAImg) + ((2 * wn + i) * 2 + s) * 64 + lane;
+            bh[i] = pb[0];
+            bm[i] = pb[16 * 64];
+            bl[i] = pb[32 * 64];
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = xpa_mfma_s3(ah[i], am[i], al[i], bh[j], bm[j], bl[j], acc[i][j]);
+    }
+}
+
+__global__ __launch_bounds__(512, 1) void s3_wgrad_kernel(const float *__restrict__ A, int64_t lda,
+                                                          const float *__restrict__ B, int64_t ldb, int64_t rows,
+                                                          int64_t M, int slices, int64_t slice_rows,
+                                                          float *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * kWgStage];
+    const int mtiles = (int)(M / kWgM);
+    const int nblk = slices * mtiles;
+    int L = blockIdx.x;
+    if (nblk % 8 == 0) L = (blockIdx.x & 7) * (nblk >> 3) + (blockIdx.x >> 3);  // one slice's tiles on one XCD
+    const int slice = L / mtiles, mt = L - slice * mtiles;
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wm = wave & 1, wn = wave >> 1;
+    const int ml = t & 127, sa = (t >> 7) & 1, ha = t >> 8, nb = t & 255, sb = t >> 8;
+    const float *Am = A + (int64_t)mt * kWgM;
+    const int64_t k0 = (int64_t)slice * slice_rows;
+    const int64_t kend = min(rows, k0 + slice_rows);
+    const int nch = kend > k0 ? (int)((kend - k0 + kWgKC - 1) / kWgKC) : 0;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    WgUnits u;
+    if (nch > 0) {
+        wg_load(u, Am, lda, B, ldb, k0, kend, ml, sa, ha, nb, sb);
+        wg_store(lds, u, ml, sa, ha, nb, sb);
+        if (nch > 1) wg_load(u, Am, lda, B, ldb, k0 + kWgKC, kend, ml, sa, ha, nb, sb);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+        wg_chunk(lds + (c & 1) * kWgStage, acc, lane, wm, wn);
+        if (c + 1 < nch) {
+            // stage (c + 1) & 1 was last read in chunk c - 1, before the previous barrier
+            wg_store(lds + ((c + 1) & 1) * kWgStage, u, ml, sa, ha, nb, sb);
+            if (c + 2 < nch) wg_load(u, Am, lda, B, ldb, k0 + (int64_t)(c + 2) * kWgKC, kend, ml, sa, ha, nb, sb);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    float *o = out + ((int64_t)slice * M + (int64_t)mt * kWgM) * kN;
+    const int h = lane >> 5, col = lane & 31;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = 64 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) o[(int64_t)row * kN + 64 * wn + 32 * j + col] = acc[i][j][r];
+        }
+}
+
 }  // namespace
+
+// the split-K slice count of xpa_s3_wgrad for this shape (the caller's workspace: slices x m x 256 floats)
+XPA_API int64_t xpa_s3_wgrad_num_slices(int64_t rows, int64_t m) {
+    if (rows <= 0 || m <= 0 || m % kWgM) return 0;
+    int64_t s = 256 / (m / kWgM);
+    s = s < 1 ? 1 : (s > 64 ? 64 : s);
+    while (s > 1 && rows / s < 4 * kWgKC) s >>= 1;
+    return s;
+}
+
+XPA_API int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ldb, int64_t rows, int64_t m, int64_t n,
+                         int64_t slices, float *out, xpa_stream_t stream) {
+    if (!a || !b || !out || rows <= 0 || m <= 0 || m % kWgM || n != kN || lda < m || ldb < n || slices < 1 ||
+        slices > 4096)
+        return (int)hipErrorInvalidValue;
+    int64_t per = (rows + slices - 1) / slices;
+    per = (per + kWgKC - 1) / kWgKC * kWgKC;
+    s3_wgrad_kernel<<<dim3((unsigned)(slices * (m / kWgM))), dim3(512), 0, stream>>>(a, lda, b, ldb, rows, m,
+                                                                                     (int)slices, per, out);
+    return xpa_launch_status();
+}
 
 XPA_API int64_t xpa_s3_split_bytes(int64_t k, int64_t n) {
     return k * n * 3 * 2;

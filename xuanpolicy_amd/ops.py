@@ -174,6 +174,27 @@ def s3_gemm(a, b_split, k, out=None):
     return out
 
 
+def s3_wgrad_slices(rows, m):
+    return int(lib().xpa_s3_wgrad_num_slices(rows, m))
+
+
+def s3_wgrad(a, b, out=None, slices=None):
+    """K41: per-slice partials out [S, m, 256] of a^T b over the rows (a [rows, m] = dz, b [rows, 256] = the layer
+    input; unit column strides), on the bf16 matrix cores by the three-way split.  The caller sums the S slices."""
+    _req(a, "a", torch.float32, contiguous=False)
+    _req(b, "b", torch.float32, contiguous=False)
+    rows, m = a.shape
+    lda, ldb = _row_stride(a, "a", m), _row_stride(b, "b", 256)
+    if b.shape[0] != rows:
+        raise ValueError("a and b must have the same rows")
+    S = slices or s3_wgrad_slices(rows, m)
+    if out is None:
+        out = torch.empty(S, m, 256, dtype=torch.float32, device=a.device)
+    _req(out, "out", torch.float32, (S, m, 256))
+    _lib.check(lib().xpa_s3_wgrad(_p(a), lda, _p(b), ldb, rows, m, 256, S, _p(out), _stream(a.device)), "xpa_s3_wgrad")
+    return out
+
+
 # ------------------------------------------------------------------------------------------------
 def gae_scan(rew, val, term, closed, boot, gamma, gae_lambda, use_gae=True, adv=None, ret=None):
     """K1.  All [n_envs, horizon]; closed uint8, the rest float32.  Returns (adv, ret)."""
