@@ -51,6 +51,9 @@ def parse():
                         "split: value head (K14) then the compact GAE scan (K1)")
     p.add_argument("--trunk-heads", choices=("on", "off"), default="off",
                    help="K16X (trunk layer inside the head GEMM launches) or r03's K13 forward + K16 (A/B)")
+    p.add_argument("--gemm", choices=("f32", "split3"), default="f32",
+                   help="the update's hidden-layer GEMMs: f32 MFMA (K16 + hipBLASLt) or the bf16 three-way split "
+                        "(K16S + K40 + K41, the f32 GEMM's accuracy on the bf16 matrix cores)")
     p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc HBM-traffic passes")
     p.add_argument("--no-rocprof", action="store_true",
                    help="skip the child rocprofv3 --kernel-trace run that times the in-loop GAE launches")
@@ -810,6 +813,7 @@ def main():
     from xuanpolicy_amd.distributed import broadcast_parameters, init_from_env, local_device
     from xuanpolicy_amd.runner import build_synthbox_ppo
 
+    ops.S3_GEMMS = args.gemm == "split3"
     rank, local, world = init_from_env()
     device = local_device(local)
     torch.cuda.set_device(device)
@@ -1024,6 +1028,8 @@ def main():
                                    "(n_epoch %d, n_minibatch %d, nets [%d] LeakyReLU)" %
                                    (N, T, args.n_epoch, args.n_minibatch, args.hidden),
                        "num_envs_per_gpu": N, "horizon": T, "global_envs": N * world, "minibatch": B,
+                       "update_gemms": ("bf16 three-way split (K16S heads, K40 dX, K41 dW; f32 accuracy)"
+                                        if ops.S3_GEMMS else "f32 MFMA (K16 heads, hipBLASLt dX / dW)"),
                        "updates_per_step": args.n_epoch * args.n_minibatch,
                        "parallelism": ("dp1 (one env shard, no collective)" if world == 1 else
                                        "dp%d (env shards; ONE all-reduce of the flat gradient per minibatch over "

@@ -82,6 +82,28 @@ def test_fast_path_iteration_with_k16w_matches_oracle(agent_name, discrete, A, m
                                expect_mid_truncations=not discrete)
 
 
+@pytest.mark.parametrize("agent_name,discrete,A", [("PPO_Clip", False, 6), ("A2C", True, 18)])
+def test_fast_path_iteration_with_split_gemms_matches_oracle(agent_name, discrete, A, monkeypatch):
+    """The same end-to-end replay with the update's hidden-layer GEMMs on the bf16 matrix cores by the three-way
+    split (ops.S3_GEMMS: K16S heads, K40 dX, K41 dW slices into the f64 finalize): every update's loss within 1e-4
+    and the final weights, as for the f32 MFMA path."""
+    from xuanpolicy_amd import ops
+    from xuanpolicy_amd.runner import build_synthbox_ppo
+    monkeypatch.setattr(ops, "S3_GEMMS", True)
+    N, T, D, H = 512, 64, 17, 256
+    agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=D, act_dim=A, hidden=H, n_epoch=2, n_minibatch=4,
+                               seed=23, device=DEV, agent=agent_name, discrete=discrete, ent_coef=0.01,
+                               max_episode_steps=T + 17)
+    fm = agent.learner._fused_mlp()
+    assert fm is not None and fm.gemm_heads and fm.pair is not None
+    agent.train(T, log=False)
+    agent.train(T - 1, log=False)
+    assert any(k[0] == "s3wgrad" for k in fm._partials if isinstance(k, tuple)), "K41 not used"
+    assert any(k[0] == "s3split" for k in fm._partials if isinstance(k, tuple)), "K40 not used"
+    replay_last_step_iteration(agent, D, A, [H], discrete, "ppo" if agent_name == "PPO_Clip" else "a2c", 0.01, 2, 4,
+                               expect_mid_truncations=not discrete)
+
+
 def test_c4_shape_iteration_matches_oracle():
     """C4's per-shard shapes (BASELINE.json configs[3]: SynthBox(obs=376, act=17), ppo/mujoco.yaml, [256] nets) at a
     reduced N x T: the 376-wide trunk (no K13: the first layer is a library GEMM), the non-K14E rollout (K14 policy

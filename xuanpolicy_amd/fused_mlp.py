@@ -373,7 +373,7 @@ class FusedActorCritic:
             else:
                 self._weight_grad(dz, s, self.pair[2], queue=self._cq)
             if have_rep:
-                self._chain_backward(self.rep, [x] + rep_outs[:-1], rep_outs, torch.mm(dz, self.pair[0]),
+                self._chain_backward(self.rep, [x] + rep_outs[:-1], rep_outs, self._dx(dz, self.pair[0]),
                                      need_dx=False, thin_first=self.thin0)
             self._flush_with_norm(s.device)   # every deferred column-sum finalize in one launch
             return scalars
@@ -426,12 +426,37 @@ class FusedActorCritic:
                                         ops._p(g) if code else None, ops._p(part), s), "xpa_act_bwd_colsum")
         _lib.check(L.xpa_colsum_finalize(ops._p(part), part.shape[0], cols, ops._p(out), s), "xpa_colsum_finalize")
 
+    def _dx(self, dz, w):
+        """dX = dz w (w [k, n_in]): K40 on the bf16 matrix cores by the three-way split when ops.S3_GEMMS and the shape
+        fits (n_in = 256, k % 16 == 0), else the f32 GEMM."""
+        k, n_in = w.shape
+        if not (ops.S3_GEMMS and n_in == 256 and k % 16 == 0 and dz.stride(1) == 1):
+            return torch.mm(dz, w)
+        key = ("s3split", k)
+        buf = self._partials.get(key)
+        if buf is None:
+            buf = torch.empty(int(ops.lib().xpa_s3_split_bytes(k, n_in)), dtype=torch.uint8, device=dz.device)
+            self._partials[key] = buf
+        return ops.s3_gemm(dz, ops.s3_split(w, out=buf), k)
+
     def _weight_grad(self, dz, x, out, queue=None):
         """dW = dz^T x.  Split-K (a batched GEMM over slices of the batch) when the GEMM alone would not
         fill the chip; with `queue` the slice sum is one more segment of the batched column-sum finalize
-        (f64, fixed order) instead of its own reduction launch."""
+        (f64, fixed order) instead of its own reduction launch.  With ops.S3_GEMMS and a fitting shape (n_in = 256,
+        n_out % 128 == 0) the slices come from K41 on the bf16 matrix cores by the three-way split."""
         B, n_out = dz.shape
         n_in = x.shape[1]
+        if (queue is not None and ops.S3_GEMMS and n_in == 256 and n_out % 128 == 0 and isinstance(x, torch.Tensor)
+                and x.stride(1) == 1 and dz.stride(1) == 1):
+            S = ops.s3_wgrad_slices(B, n_out)
+            key = ("s3wgrad", S, n_out)
+            ws = self._partials.get(key)
+            if ws is None:
+                ws = torch.empty((S, n_out, n_in), dtype=torch.float32, device=dz.device)
+                self._partials[key] = ws
+            ops.s3_wgrad(dz, x, out=ws)
+            queue.add(ws.view(S, n_out * n_in), out.view(-1))
+            return
         s = _splitk_splits(B, n_out, n_in)
         if queue is not None:   # (s == 1: the finalize only copies, so every gradient still passes through it)
             key = ("splitk", s, n_out, n_in)

@@ -561,6 +561,9 @@ class ColsumQueue:
 
 
 K16W_ENABLED = False  # fused_heads' gemm form: K16W (xpa_head_gemm_ws_*) where it applies, else K16
+# The update's hidden-layer GEMMs on the bf16 matrix cores by the three-way split (K16S heads, K40 dX, K41 dW):
+# the f32 GEMM's accuracy, not the f32 MFMA's bits.  Read when a learner's update is built / captured.
+S3_GEMMS = False
 
 
 def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, w_critic, b_critic, act_critic,
@@ -644,8 +647,9 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
     elif gemm is not None:
         # K16W (wave-specialised, the epilogue overlapped with the GEMM) for heads up to 8 wide; K16 otherwise
         wsa = K16W_ENABLED and K <= 8
-        fa = L.xpa_head_gemm_ws_actor if wsa else L.xpa_head_gemm_actor
-        fc = L.xpa_head_gemm_ws_critic if K16W_ENABLED else L.xpa_head_gemm_critic
+        fa = L.xpa_head_gemm_ws_actor if wsa else L.xpa_head_gemm_s3_actor if S3_GEMMS else L.xpa_head_gemm_actor
+        fc = (L.xpa_head_gemm_ws_critic if K16W_ENABLED else L.xpa_head_gemm_s3_critic if S3_GEMMS
+              else L.xpa_head_gemm_critic)
         _lib.check(fa(ALGO[algo], DIST[dist], act_actor[0], B, K, H, _p(x), x.stride(0), _p(wha),
                       _p(bha), ld, _p(w_actor), _p(b_actor), float(act_actor[1]), p_logstd, _p(idx),
                       rows, _p(act), p_old, _p(adv), _p(adv_partials), n_adv, float(clip_range),
