@@ -913,7 +913,7 @@ def main():
             # a plain copy of the launch's own bytes (3 reads + 2 writes of 16 B per 4 elements) on the event clock
             launch_copy_us = None
             if not args.no_kernel_timing:
-                nl = int(gb) // 20
+                nl = int(gb) // 20 // 4 * 4   # the copy kernel moves float4s
                 bufs = [torch.empty(nl, device=device) for _ in range(3)]
                 launch_copy_us = ops.stream_copy_us(*bufs)
                 del bufs

@@ -560,6 +560,7 @@ int xpa_head_gemm_trunk_critic(int act, int64_t batch, int64_t hidden, const flo
  *   aligned), the three bf16 planes in the GEMM's operand order; k % 16 == 0, n == 256.
  * xpa_s3_gemm: c [m, 256] (row stride ldc) = a [m, k] (f32, row stride lda, 16-B aligned rows) . B, from B's split. */
 int64_t xpa_s3_split_bytes(int64_t k, int64_t n);
+int xpa_s3_probe(int mask); /* diagnostics: parts of K40 / K41 switched off (tools/s3_ab.py --probe); 0 = production */
 int xpa_s3_split_b(const float *b, int64_t k, int64_t n, int64_t sk, int64_t sn, void *out, xpa_stream_t stream);
 int xpa_s3_gemm(const float *a, int64_t lda, const void *b_split, float *c, int64_t ldc, int64_t m, int64_t k, int64_t n,
                 xpa_stream_t stream);

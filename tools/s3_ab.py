@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--probe", action="store_true", help="also time K40 / K41 with parts switched off (xpa_s3_probe)")
     a = ap.parse_args()
     import torch
     from xuanpolicy_amd import ops
@@ -58,7 +59,8 @@ def main():
     # K41: dW = dz^T x (the paired hidden layer's weight gradient) vs the learner's split-K batched f32 GEMM (8 slices)
     B = 65536
     dz = torch.randn(B, 512, device=dev, generator=g)
-    x = torch.randn(B, 256, device=dev, generator=g)
+    x_in = torch.randn(B, 256, device=dev, generator=g)
+    x = x_in
     S = ops.s3_wgrad_slices(B, 512)
     part = torch.empty(S, 512, 256, device=dev)
     ws8 = torch.empty(8, 512, 256, device=dev)
@@ -71,6 +73,18 @@ def main():
     r["f32_floor_us"] = round(flop / 157.3e12 * 1e6, 2)
     r["s3_frac_of_f32_floor"] = round(r["f32_floor_us"] / min(r["s3_us"]), 3)
     r["torch_frac_of_f32_floor"] = round(r["f32_floor_us"] / min(r["torch_bmm8_us"]), 3)
+    if a.probe:   # 1 no MFMA, 2 no operand loads, 4 one MFMA instead of six
+        L = ops.lib()
+        M, K = 65536, 512
+        x = torch.randn(M, K, device=dev, generator=g)
+        sp = ops.s3_split(torch.randn(K, 256, device=dev, generator=g) / 16)
+        out = torch.empty(M, 256, device=dev)
+        pr = res.setdefault("probe_us", {})
+        for mask in (0, 1, 2, 3, 4, 6):
+            assert L.xpa_s3_probe(mask) == 0
+            pr["k40_%d" % mask] = round(_time(lambda: ops.s3_gemm(x, sp, K, out=out), a.reps), 2)
+            pr["k41_%d" % mask] = round(_time(lambda: ops.s3_wgrad(dz, x_in, out=part), a.reps), 2)
+        assert L.xpa_s3_probe(0) == 0
     print(json.dumps(res))
     if a.out:
         with open(a.out, "w") as f:

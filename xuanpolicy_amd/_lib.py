@@ -216,6 +216,7 @@ SIGNATURES = {
     "xpa_head_gemm_trunk_critic": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p, c_f32, c_p,
                                                   c_i64, c_p, c_p, c_i64, c_p, c_p, c_f32, c_p, c_i64, c_p, c_f32, c_p,
                                                   c_p, c_p, c_p, c_p, c_i64, c_p]),
+    "xpa_s3_probe": (ctypes.c_int, [ctypes.c_int]),
     "xpa_s3_split_bytes": (c_i64, [c_i64, c_i64]),
     "xpa_s3_split_b": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
     "xpa_s3_gemm": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),

@@ -49,6 +49,11 @@ __device__ __forceinline__ void glds16(const void *g, unsigned lds_wave_base) {
                  : "memory", "m0");
 }
 
+// diagnostics only (tools/s3_ab.py --probe, xpa_s3_probe): 1 = no MFMAs (fragments still read / split), 2 = no operand
+// loads (K40: no DMAs after the first two chunks; K41: no global loads — stale registers), 4 = one MFMA (hi x hi) per
+// tile and k step instead of the six.  0 in production.
+int g_s3_probe = 0;  // host side: selects the kernel instantiation
+
 // the k of element j of lane half h inside a 16-k chunk (quads h and h + 2)
 __device__ __forceinline__ int kmap(int h, int j) { return 4 * h + j + (j >= 4 ? 4 : 0); }
 
@@ -104,6 +109,7 @@ __device__ __forceinline__ void issue(unsigned st, const float *__restrict__ a, 
     }
 }
 
+template <int PROBE>
 __device__ __forceinline__ void chunk(const char *st, f32x16 (&acc)[8], int lane, int wave) {
     const int h = lane >> 5, i = lane & 31;
     const int sw = (i >> 2) & 3;
@@ -113,11 +119,22 @@ __device__ __forceinline__ void chunk(const char *st, f32x16 (&acc)[8], int lane
     bf16x8 ah, am, al;
     xpa_split8(alo, ahi, ah, am, al);
     const bf16x8 *bimg = reinterpret_cast<const bf16x8 *>(st + kAImg) + lane;
+    if constexpr ((PROBE & 5) != 0) {
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb) {
+            const bf16x8 bh = bimg[cb * 64], bm = bimg[(8 + cb) * 64], bl = bimg[(16 + cb) * 64];
+            if constexpr ((PROBE & 1) != 0) asm volatile("" ::"v"(ah), "v"(am), "v"(al), "v"(bh), "v"(bm), "v"(bl));
+            else acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[cb], 0, 0, 0);
+            if constexpr ((PROBE & 1) == 0) asm volatile("" ::"v"(am), "v"(al), "v"(bm), "v"(bl));
+        }
+        return;
+    }
 #pragma unroll
     for (int cb = 0; cb < 8; ++cb)
         acc[cb] = xpa_mfma_s3(ah, am, al, bimg[cb * 64], bimg[(8 + cb) * 64], bimg[(16 + cb) * 64], acc[cb]);
 }
 
+template <int PROBE>
 __global__ __launch_bounds__(512, 1) void s3_gemm_kernel(const float *__restrict__ a, int64_t lda,
                                                          const __bf16 *__restrict__ bs, float *__restrict__ c,
                                                          int64_t ldc, int64_t M, int nchunks) {
@@ -140,8 +157,9 @@ __global__ __launch_bounds__(512, 1) void s3_gemm_kernel(const float *__restrict
         // read by every wave in chunk ch - 1
         if (ch + 1 < nchunks) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kDma) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        if (ch + 2 < nchunks) issue(base + ((ch + 2) % kStages) * kStage, a, lda, bs, r0, M, ch + 2, lane, wave);
-        chunk(lds + (ch % kStages) * kStage, acc, lane, wave);
+        if (ch + 2 < nchunks && (PROBE & 2) == 0)
+            issue(base + ((ch + 2) % kStages) * kStage, a, lda, bs, r0, M, ch + 2, lane, wave);
+        chunk<PROBE>(lds + (ch % kStages) * kStage, acc, lane, wave);
     }
     // C/D map of 32x32 MFMA: row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col = lane & 31
     const int h = lane >> 5, col = lane & 31;
@@ -208,6 +226,7 @@ __device__ __forceinline__ void wg_store(char *st, const WgUnits &u, int ml, int
     wg_put(st, u.b1, kWgAImg + (((nb >> 5) * 2 + sb) * 64 + 32 + (nb & 31)) * 16);
 }
 
+template <int PROBE>
 __device__ __forceinline__ void wg_chunk(const char *st, f32x16 (&acc)[2][2], int lane, int wm, int wn) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -223,6 +242,18 @@ __device__ __forceinline__ void wg_chunk(const char *st, f32x16 (&acc)[2][2], in
             bm[i] = pb[16 * 64];
             bl[i] = pb[32 * 64];
         }
+        if constexpr ((PROBE & 5) != 0) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if constexpr ((PROBE & 1) != 0)
+                        asm volatile("" ::"v"(ah[i]), "v"(am[i]), "v"(al[i]), "v"(bh[j]), "v"(bm[j]), "v"(bl[j]));
+                    else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                    if constexpr ((PROBE & 1) == 0) asm volatile("" ::"v"(am[i]), "v"(al[i]), "v"(bm[j]), "v"(bl[j]));
+                }
+            continue;
+        }
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -230,6 +261,7 @@ __device__ __forceinline__ void wg_chunk(const char *st, f32x16 (&acc)[2][2], in
     }
 }
 
+template <int PROBE>
 __global__ __launch_bounds__(512, 1) void s3_wgrad_kernel(const float *__restrict__ A, int64_t lda,
                                                           const float *__restrict__ B, int64_t ldb, int64_t rows,
                                                           int64_t M, int slices, int64_t slice_rows,
@@ -264,11 +296,12 @@ __global__ __launch_bounds__(512, 1) void s3_wgrad_kernel(const float *__restric
     }
 #pragma unroll 1
     for (int c = 0; c < nch; ++c) {
-        wg_chunk(lds + (c & 1) * kWgStage, acc, lane, wm, wn);
+        wg_chunk<PROBE>(lds + (c & 1) * kWgStage, acc, lane, wm, wn);
         if (c + 1 < nch) {
             // stage (c + 1) & 1 was last read in chunk c - 1, before the previous barrier
             wg_store(lds + ((c + 1) & 1) * kWgStage, u, ml, sa, ha, nb, sb);
-            if (c + 2 < nch) wg_load(u, Am, lda, B, ldb, k0 + (int64_t)(c + 2) * kWgKC, kend, ml, sa, ha, nb, sb);
+            if (c + 2 < nch && (PROBE & 2) == 0)
+                wg_load(u, Am, lda, B, ldb, k0 + (int64_t)(c + 2) * kWgKC, kend, ml, sa, ha, nb, sb);
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
@@ -302,9 +335,19 @@ XPA_API int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ld
         return (int)hipErrorInvalidValue;
     int64_t per = (rows + slices - 1) / slices;
     per = (per + kWgKC - 1) / kWgKC * kWgKC;
-    s3_wgrad_kernel<<<dim3((unsigned)(slices * (m / kWgM))), dim3(512), 0, stream>>>(a, lda, b, ldb, rows, m,
-                                                                                     (int)slices, per, out);
+    const dim3 grid((unsigned)(slices * (m / kWgM))), block(512);
+    switch (g_s3_probe) {
+#define XPA_WG(P) case P: s3_wgrad_kernel<P><<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out); break;
+        XPA_WG(1) XPA_WG(2) XPA_WG(3) XPA_WG(4) XPA_WG(6)
+#undef XPA_WG
+        default: s3_wgrad_kernel<0><<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out);
+    }
     return xpa_launch_status();
+}
+
+XPA_API int xpa_s3_probe(int mask) {
+    g_s3_probe = mask;
+    return 0;
 }
 
 XPA_API int64_t xpa_s3_split_bytes(int64_t k, int64_t n) {
@@ -325,7 +368,13 @@ XPA_API int xpa_s3_gemm(const float *a, int64_t lda, const void *b_split, float 
     if (!a || !b_split || !c || m <= 0 || k <= 0 || k % kKC != 0 || n != kN || lda < k || ldc < n ||
         (reinterpret_cast<uintptr_t>(a) & 15) || (lda & 3) || k / kKC > (1 << 20))
         return (int)hipErrorInvalidValue;
-    s3_gemm_kernel<<<dim3((unsigned)((m + kRows - 1) / kRows)), dim3(512), 0, stream>>>(
-        a, lda, static_cast<const __bf16 *>(b_split), c, ldc, m, (int)(k / kKC));
+    const dim3 grid((unsigned)((m + kRows - 1) / kRows)), block(512);
+    const __bf16 *bs = static_cast<const __bf16 *>(b_split);
+    switch (g_s3_probe) {
+#define XPA_GM(P) case P: s3_gemm_kernel<P><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, (int)(k / kKC)); break;
+        XPA_GM(1) XPA_GM(2) XPA_GM(3) XPA_GM(4) XPA_GM(6)
+#undef XPA_GM
+        default: s3_gemm_kernel<0><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, (int)(k / kKC));
+    }
     return xpa_launch_status();
 }
