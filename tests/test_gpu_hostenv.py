@@ -103,8 +103,10 @@ def _run(agent, host, ref_env, pol, algo, discrete, A, ent, n_epoch, n_mb, atari
     pol.double()
     agent.train(T - 1, log=False)
     ref.train(T - 1)
+    # without obs-norm the first store of each train() call (columns 0 and T - 1 here) aliases the post-step buf_obs
+    alias = (0, T - 1) if not agent.use_obsnorm else ()
     replay_last_step_iteration(agent, None, A, None, discrete, algo, ent, n_epoch, n_mb,
-                               pol=_fresh_like(pol))
+                               pol=_fresh_like(pol), alias_cols=alias)
     ref.train(1)
     assert len(snaps) == 2 and feed["k"] == 2 * T
     _check_rollout(agent, ref, snaps[1], 1)

@@ -52,9 +52,21 @@ def test_split_is_exact(k, transposed):
     assert np.array_equal(pl[0], hi)
 
 
+@pytest.mark.parametrize("form", [0, 8])
 @pytest.mark.parametrize("m,k,lda_pad,t_b", [(65536, 512, 0, False), (1000, 512, 0, False), (4097, 256, 8, True),
                                              (300, 256, 0, True), (1, 16, 0, False), (257, 32, 4, False)])
-def test_gemm_matches_f32_gemm_error(m, k, lda_pad, t_b):
+def test_gemm_matches_f32_gemm_error(m, k, lda_pad, t_b, form):
+    """form 0: one 8-wave block per CU, 3-stage ring; form 8: two 4-wave blocks per CU, 2 stages (xpa_s3_probe)."""
+    from xuanpolicy_amd import ops
+    L = ops.lib()
+    assert L.xpa_s3_probe(form) == 0
+    try:
+        _gemm_case(m, k, lda_pad, t_b)
+    finally:
+        L.xpa_s3_probe(0)
+
+
+def _gemm_case(m, k, lda_pad, t_b):
     from xuanpolicy_amd import ops
     g = torch.Generator(device=DEV).manual_seed(m + k)
     abuf = _wide((m, k + lda_pad), g)

@@ -34,15 +34,18 @@ typedef xpa_bf16x8 bf16x8;
 typedef __attribute__((address_space(3))) char lds_char_t;
 
 constexpr int kN = 256;                     // output columns (all of them per block)
-constexpr int kWaves = 8;
-constexpr int kRows = 32 * kWaves;          // rows per block
 constexpr int kKC = 16;                     // k per chunk (one bf16 MFMA k step)
-constexpr int kAImg = kRows * kKC * 4;      // bytes, 16 KiB
 constexpr int kBImg = 3 * kN * kKC * 2;     // bytes, 24 KiB
-constexpr int kStage = kAImg + kBImg;       // 40 KiB
-constexpr int kStages = 3;
-constexpr int kDma = 2 + kBImg / 1024 / kWaves;  // per wave and chunk: 2 A + 3 B (the vmcnt of one chunk in flight)
-static_assert(kBImg % (1024 * kWaves) == 0, "B image splits evenly over the waves");
+// K40 geometry: W waves of 32 rows (a block = 32 W rows x 256 columns), S ring stages (prefetch depth S - 1)
+template <int W>
+struct S3Geom {
+    static constexpr int kRows = 32 * W;
+    static constexpr int kAImg = kRows * kKC * 4;       // bytes: 16 KiB at W = 8
+    static constexpr int kStage = kAImg + kBImg;
+    static constexpr int kPer = kBImg / 1024 / W;       // B pieces per wave and chunk
+    static constexpr int kDma = 2 + kPer;               // the vmcnt of one chunk in flight
+    static_assert(kBImg % (1024 * W) == 0, "B image splits evenly over the waves");
+};
 
 __device__ __forceinline__ void glds16(const void *g, unsigned lds_wave_base) {
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds_wave_base)
@@ -89,9 +92,11 @@ __global__ __launch_bounds__(256) void split_b_kernel(const float *__restrict__ 
 // chunk c's DMAs of wave w into the stage at LDS byte address st: A rows r0 + 32 w .. + 31 (two 16-row
 // instructions, lane = (row, 16-B slot), slot p of row r holding k quad p ^ ((r >> 2) & 3)), then B's 1-KiB pieces
 // 3 w .. 3 w + 2 of the chunk's 24 KiB.  Rows past M re-read row M - 1 (never stored).
+template <int W>
 __device__ __forceinline__ void issue(unsigned st, const float *__restrict__ a, int64_t lda,
                                       const __bf16 *__restrict__ bs, int64_t r0, int64_t M, int c, int lane,
                                       int wave) {
+    using G = S3Geom<W>;
     const int rr = lane >> 2, p = lane & 3;
     const int q = p ^ ((rr >> 2) & 3);
 #pragma unroll
@@ -101,16 +106,16 @@ __device__ __forceinline__ void issue(unsigned st, const float *__restrict__ a, 
         glds16(a + row * lda + c * kKC + 4 * q, st + (unsigned)((wave * 32 + i * 16) * kKC * 4));
     }
     const char *bsrc = reinterpret_cast<const char *>(bs) + (int64_t)c * kBImg;
-    constexpr int kPer = kBImg / 1024 / kWaves;
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        const int piece = wave * kPer + j;
-        glds16(bsrc + piece * 1024 + lane * 16, st + (unsigned)(kAImg + piece * 1024));
+    for (int j = 0; j < G::kPer; ++j) {
+        const int piece = wave * G::kPer + j;
+        glds16(bsrc + piece * 1024 + lane * 16, st + (unsigned)(G::kAImg + piece * 1024));
     }
 }
 
-template <int PROBE>
+template <int W, int PROBE>
 __device__ __forceinline__ void chunk(const char *st, f32x16 (&acc)[8], int lane, int wave) {
+    constexpr int kAImg = S3Geom<W>::kAImg;
     const int h = lane >> 5, i = lane & 31;
     const int sw = (i >> 2) & 3;
     const float *arow = reinterpret_cast<const float *>(st) + (wave * 32 + i) * kKC;
@@ -134,32 +139,34 @@ __device__ __forceinline__ void chunk(const char *st, f32x16 (&acc)[8], int lane
         acc[cb] = xpa_mfma_s3(ah, am, al, bimg[cb * 64], bimg[(8 + cb) * 64], bimg[(16 + cb) * 64], acc[cb]);
 }
 
-template <int PROBE>
-__global__ __launch_bounds__(512, 1) void s3_gemm_kernel(const float *__restrict__ a, int64_t lda,
-                                                         const __bf16 *__restrict__ bs, float *__restrict__ c,
-                                                         int64_t ldc, int64_t M, int nchunks) {
+template <int W, int S, int PROBE>
+__global__ __launch_bounds__(64 * W, 8 / W) void s3_gemm_kernel(const float *__restrict__ a, int64_t lda,
+                                                               const __bf16 *__restrict__ bs, float *__restrict__ c,
+                                                               int64_t ldc, int64_t M, int nchunks) {
+    using G = S3Geom<W>;
     // ONE LDS array (the DMA target; see head.hip)
-    __shared__ __attribute__((aligned(16))) char lds[kStages * kStage];
+    __shared__ __attribute__((aligned(16))) char lds[S * G::kStage];
     const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int64_t r0 = (int64_t)blockIdx.x * kRows;
+    const int64_t r0 = (int64_t)blockIdx.x * G::kRows;
     f32x16 acc[8];
 #pragma unroll
     for (int cb = 0; cb < 8; ++cb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[cb][r] = 0.f;
-    issue(base, a, lda, bs, r0, M, 0, lane, wave);
-    if (nchunks > 1) issue(base + kStage, a, lda, bs, r0, M, 1, lane, wave);
+#pragma unroll
+    for (int d = 0; d < S - 1; ++d)
+        if (d < nchunks) issue<W>(base + d * G::kStage, a, lda, bs, r0, M, d, lane, wave);
 #pragma unroll 1
     for (int ch = 0; ch < nchunks; ++ch) {
-        // own DMAs of chunk ch landed (ch + 1's may still fly), then every wave's: the stage ch + 2 refills was
-        // read by every wave in chunk ch - 1
-        if (ch + 1 < nchunks) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kDma) : "memory");
+        // own DMAs of chunk ch landed (with 3 stages chunk ch + 1's may still fly), then every wave's: the stage
+        // chunk ch + S - 1 refills was read by every wave in chunk ch - 1
+        if (S == 3 && ch + 1 < nchunks) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G::kDma) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        if (ch + 2 < nchunks && (PROBE & 2) == 0)
-            issue(base + ((ch + 2) % kStages) * kStage, a, lda, bs, r0, M, ch + 2, lane, wave);
-        chunk<PROBE>(lds + (ch % kStages) * kStage, acc, lane, wave);
+        if (ch + S - 1 < nchunks && (PROBE & 2) == 0)
+            issue<W>(base + ((ch + S - 1) % S) * G::kStage, a, lda, bs, r0, M, ch + S - 1, lane, wave);
+        chunk<W, PROBE>(lds + (ch % S) * G::kStage, acc, lane, wave);
     }
     // C/D map of 32x32 MFMA: row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col = lane & 31
     const int h = lane >> 5, col = lane & 31;
@@ -336,7 +343,7 @@ XPA_API int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ld
     int64_t per = (rows + slices - 1) / slices;
     per = (per + kWgKC - 1) / kWgKC * kWgKC;
     const dim3 grid((unsigned)(slices * (m / kWgM))), block(512);
-    switch (g_s3_probe) {
+    switch (g_s3_probe & 7) {
 #define XPA_WG(P) case P: s3_wgrad_kernel<P><<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out); break;
         XPA_WG(1) XPA_WG(2) XPA_WG(3) XPA_WG(4) XPA_WG(6)
 #undef XPA_WG
@@ -368,13 +375,25 @@ XPA_API int xpa_s3_gemm(const float *a, int64_t lda, const void *b_split, float 
     if (!a || !b_split || !c || m <= 0 || k <= 0 || k % kKC != 0 || n != kN || lda < k || ldc < n ||
         (reinterpret_cast<uintptr_t>(a) & 15) || (lda & 3) || k / kKC > (1 << 20))
         return (int)hipErrorInvalidValue;
-    const dim3 grid((unsigned)((m + kRows - 1) / kRows)), block(512);
     const __bf16 *bs = static_cast<const __bf16 *>(b_split);
-    switch (g_s3_probe) {
-#define XPA_GM(P) case P: s3_gemm_kernel<P><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, (int)(k / kKC)); break;
+    const int nch = (int)(k / kKC);
+    // form (probe bit 8): 0 = one 8-wave block per CU with a 3-stage ring, 8 = two 4-wave blocks per CU, 2 stages
+    if (g_s3_probe & 8) {
+        const dim3 grid((unsigned)((m + 127) / 128)), block(256);
+        switch (g_s3_probe & 7) {
+#define XPA_GM(P) case P: s3_gemm_kernel<4, 2, P><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, nch); break;
+            XPA_GM(1) XPA_GM(2) XPA_GM(3) XPA_GM(4) XPA_GM(6)
+#undef XPA_GM
+            default: s3_gemm_kernel<4, 2, 0><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, nch);
+        }
+        return xpa_launch_status();
+    }
+    const dim3 grid((unsigned)((m + 255) / 256)), block(512);
+    switch (g_s3_probe & 7) {
+#define XPA_GM(P) case P: s3_gemm_kernel<8, 3, P><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, nch); break;
         XPA_GM(1) XPA_GM(2) XPA_GM(3) XPA_GM(4) XPA_GM(6)
 #undef XPA_GM
-        default: s3_gemm_kernel<0><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, (int)(k / kKC));
+        default: s3_gemm_kernel<8, 3, 0><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, nch);
     }
     return xpa_launch_status();
 }
