@@ -123,3 +123,22 @@ def test_wgrad_matches_f32_gemm_error(rows, m, lda_pad, slices):
     err_f32 = (native.double() - ref).abs().max().item()
     assert torch.isfinite(part).all()
     assert err <= 2 * err_f32 + 2 ** -24 * scale, (err, err_f32, scale)
+
+
+@pytest.mark.parametrize("rows,m,slices", [(65536, 512, None), (4133, 256, 5), (100, 128, 1)])
+def test_wgrad_wave_specialised_equals_k41(rows, m, slices):
+    """K41W (producer / consumer waves, xpa_s3_probe form bit 8) writes K41's partials bit for bit: the same LDS image,
+    products and k order per accumulator."""
+    from xuanpolicy_amd import ops
+    L = ops.lib()
+    g = torch.Generator(device=DEV).manual_seed(rows * 3 + m)
+    a = _wide((rows, m), g)
+    b = torch.randn(rows, 256, device=DEV, generator=g)
+    p0 = ops.s3_wgrad(a, b, slices=slices)
+    assert L.xpa_s3_probe(8) == 0
+    try:
+        p1 = ops.s3_wgrad(a, b, slices=slices)
+        torch.cuda.synchronize()
+    finally:
+        L.xpa_s3_probe(0)
+    assert torch.equal(p0, p1)

@@ -324,6 +324,128 @@ __global__ __launch_bounds__(512, 1) void s3_wgrad_kernel(const float *__restric
         }
 }
 
+// K41W: the same product with the roles split over the waves of the block, so the staging and the MFMAs overlap by
+// construction instead of alternating in every wave between the chunk barriers: waves 4-7 (producers) load chunk
+// c + 2 into registers and split / write chunk c + 1 into the other stage while waves 0-3 (consumers, one per SIMD)
+// run chunk c's MFMAs; one barrier per chunk hands the stage over.  Consumer w owns rows 64 (w & 1) .. + 63 x
+// columns 128 (w >> 1) .. + 127 (2 x 4 accumulators).  A producer thread p stages 6 units per chunk: A (column
+// p & 127, k step p >> 7, halves 0 / 1) and B (column p, k steps 0 / 1, halves 0 / 1).  Same LDS image, same products
+// and k order per accumulator as K41: the outputs are K41's bit for bit.
+__device__ __forceinline__ void wgw_load(float (&v)[6][8], const float *__restrict__ A, int64_t lda,
+                                         const float *__restrict__ B, int64_t ldb, int64_t k0, int64_t kend, int p) {
+    const int ma = p & 127, sa = p >> 7;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t ra = k0 + 16 * sa + kmap(h, j);
+            const float va = A[min(ra, kend - 1) * lda + ma];
+            v[h][j] = ra < kend ? va : 0.f;
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int64_t rb = k0 + 16 * s + kmap(h, j);
+                const float vb = B[min(rb, kend - 1) * ldb + p];
+                v[2 + 2 * s + h][j] = rb < kend ? vb : 0.f;
+            }
+    }
+}
+
+__device__ __forceinline__ void wgw_store(char *st, const float (&v)[6][8], int p) {
+    const int ma = p & 127, sa = p >> 7;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) wg_put(st, v[h], (((ma >> 5) * 2 + sa) * 64 + h * 32 + (ma & 31)) * 16);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            wg_put(st, v[2 + 2 * s + h], kWgAImg + (((p >> 5) * 2 + s) * 64 + h * 32 + (p & 31)) * 16);
+}
+
+__device__ __forceinline__ void wgw_chunk(const char *st, f32x16 (&acc)[2][4], int lane, int wm, int wn) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        bf16x8 ah[2], am[2], al[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const bf16x8 *pa = reinterpret_cast<const bf16x8 *>(st) + ((2 * wm + i) * 2 + s) * 64 + lane;
+            ah[i] = pa[0];
+            am[i] = pa[8 * 64];
+            al[i] = pa[16 * 64];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bf16x8 *pb = reinterpret_cast<const bf16x8 *>(st + kWgAImg) + ((4 * wn + j) * 2 + s) * 64 + lane;
+            const bf16x8 bh = pb[0], bm = pb[16 * 64], bl = pb[32 * 64];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) acc[i][j] = xpa_mfma_s3(ah[i], am[i], al[i], bh, bm, bl, acc[i][j]);
+        }
+    }
+}
+
+__global__ __launch_bounds__(512, 1) void s3_wgrad_ws_kernel(const float *__restrict__ A, int64_t lda,
+                                                             const float *__restrict__ B, int64_t ldb, int64_t rows,
+                                                             int64_t M, int slices, int64_t slice_rows,
+                                                             float *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * kWgStage];
+    const int mtiles = (int)(M / kWgM);
+    const int nblk = slices * mtiles;
+    int L = blockIdx.x;
+    if (nblk % 8 == 0) L = (blockIdx.x & 7) * (nblk >> 3) + (blockIdx.x >> 3);  // one slice's tiles on one XCD
+    const int slice = L / mtiles, mt = L - slice * mtiles;
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const float *Am = A + (int64_t)mt * kWgM;
+    const int64_t k0 = (int64_t)slice * slice_rows;
+    const int64_t kend = min(rows, k0 + slice_rows);
+    const int nch = kend > k0 ? (int)((kend - k0 + kWgKC - 1) / kWgKC) : 0;
+    if (wave >= 4) {   // producers: the same barrier sequence as the consumers (1 + nch barriers)
+        const int p = t - 256;
+        float v[6][8];
+        if (nch > 0) {
+            wgw_load(v, Am, lda, B, ldb, k0, kend, p);
+            wgw_store(lds, v, p);
+            if (nch > 1) wgw_load(v, Am, lda, B, ldb, k0 + kWgKC, kend, p);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll 1
+        for (int c = 0; c < nch; ++c) {
+            if (c + 1 < nch) {
+                wgw_store(lds + ((c + 1) & 1) * kWgStage, v, p);
+                if (c + 2 < nch) wgw_load(v, Am, lda, B, ldb, k0 + (int64_t)(c + 2) * kWgKC, kend, p);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        return;
+    }
+    const int wm = wave & 1, wn = wave >> 1;
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    asm volatile("s_barrier" ::: "memory");
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+        wgw_chunk(lds + (c & 1) * kWgStage, acc, lane, wm, wn);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // done reading stage c & 1
+    }
+    float *o = out + ((int64_t)slice * M + (int64_t)mt * kWgM) * kN;
+    const int h = lane >> 5, col = lane & 31;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = 64 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[(int64_t)row * kN + 128 * wn + 32 * j + col] = acc[i][j][r];
+        }
+}
+
 }  // namespace
 
 // the split-K slice count of xpa_s3_wgrad for this shape (the caller's workspace: slices x m x 256 floats)
@@ -343,6 +465,10 @@ XPA_API int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ld
     int64_t per = (rows + slices - 1) / slices;
     per = (per + kWgKC - 1) / kWgKC * kWgKC;
     const dim3 grid((unsigned)(slices * (m / kWgM))), block(512);
+    if (g_s3_probe & 8) {   // the wave-specialised form (K41W)
+        s3_wgrad_ws_kernel<<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out);
+        return xpa_launch_status();
+    }
     switch (g_s3_probe & 7) {
 #define XPA_WG(P) case P: s3_wgrad_kernel<P><<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out); break;
         XPA_WG(1) XPA_WG(2) XPA_WG(3) XPA_WG(4) XPA_WG(6)
