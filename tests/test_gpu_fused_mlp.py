@@ -431,6 +431,10 @@ def test_colsum_queue_deferred_loss_finalize(nseg, dist):
     ("ppo", "categorical", 18, 193, 2, "s3"),
     ("ppo", "gaussian", 6, 20037, 1, "s3"),
     ("a2c", "gaussian", 6, 65, 1, "s3"),
+    # K16P (Wh's planes split once, DMA'd)
+    ("ppo", "gaussian", 6, 4133, 1, "s3p"),
+    ("a2c", "categorical", 18, 777, 0, "s3p"),
+    ("ppo", "categorical", 8, 193, 2, "s3p"),
 ])
 def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code, form):
     """K16 (xpa_head_gemm_actor / _critic), K16W (xpa_head_gemm_ws_*) or K16S (xpa_head_gemm_s3_*) through the C ABI against float64 autograd
@@ -482,13 +486,17 @@ def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code, form):
     v = lambda t: ops._p(t[pad:])   # noqa: E731
     algo_c, dist_c = ops.ALGO[algo], ops.DIST[dist]
     ent, clip, vf = 0.01, 0.2, 0.25
-    pre = {"k16": "xpa_head_gemm_", "ws": "xpa_head_gemm_ws_", "s3": "xpa_head_gemm_s3_"}[form]
+    pre = {"k16": "xpa_head_gemm_", "ws": "xpa_head_gemm_ws_", "s3": "xpa_head_gemm_s3_", "s3p": "xpa_head_gemm_s3p_"}[form]
     fa, fc = getattr(L, pre + "actor"), getattr(L, pre + "critic")
-    assert fa(algo_c, dist_c, code, B, K, H, ops._p(x), H, ops._p(wh_a), ops._p(bh_a), 2 * H,
+    if form == "s3p":   # the hidden weights as Wh^T's three bf16 planes
+        wh_a_arg, wh_c_arg = ops.s3_split(wh_a.t()), ops.s3_split(wh_c.t())
+    else:
+        wh_a_arg, wh_c_arg = wh_a, wh_c
+    assert fa(algo_c, dist_c, code, B, K, H, ops._p(x), H, ops._p(wh_a_arg), ops._p(bh_a), 2 * H,
               ops._p(w_a), ops._p(b_a), slope, ops._p(logstd) if logstd is not None else None,
               ops._p(idx), R, ops._p(act), ops._p(old) if old is not None else None, ops._p(adv),
               None, 0, clip, ent, ops._p(dz), v(p_dw_a), v(p_dbh_a), v(p_dbo_a), v(lp), W, s) == 0
-    assert fc(code, B, H, ops._p(x), H, ops._p(wh_c), ops._p(bh_c), 2 * H, ops._p(w_c),
+    assert fc(code, B, H, ops._p(x), H, ops._p(wh_c_arg), ops._p(bh_c), 2 * H, ops._p(w_c),
               ops._p(b_c), slope, ops._p(idx), R, ops._p(ret), vf, ops._p(dz[:, H:]), v(p_dw_c),
               v(p_dbh_c), v(p_dbo_c), v(lp), W, s) == 0
     torch.cuda.synchronize()

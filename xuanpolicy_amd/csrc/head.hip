@@ -731,6 +731,53 @@ __device__ __forceinline__ void gemm_chunk_s3(const float *st, f32x16 (&acc)[2][
             acc[rt][ct] = xpa_mfma_s3(ah[rt], am[rt], al[rt], bh[ct], bm[ct], bl[ct], acc[rt][ct]);
 }
 
+// K16P (r04): K16S with Wh's three bf16 planes split once per update (xpa_s3_split_b of Wh^T, K40's layout: per 16-k
+// chunk 24 KiB = [plane][column block][lane][16 B]) and DMA'd as they are, so the waves split only their A fragments.
+// A chunk's stage is 4 KiB of A + 24 KiB of planes; two stages (56 KiB) fit the epilogue tile, so the ring is one
+// chunk deep: chunk c + 1 is issued right after chunk c's barrier.
+constexpr int kPStageB = 4096 + 24576;  // bytes
+static_assert(2 * kPStageB <= kTile * kS * 4, "two K16P stages share the epilogue tile");
+__device__ __forceinline__ void gemm_issue_p(unsigned st, const float *__restrict__ x, int64_t ldx,
+                                             const char *__restrict__ wsp, int64_t r0, int64_t batch, int c, int lane,
+                                             int wave) {
+    const int rr = lane >> 2, p = lane & 3;
+    const int q = p ^ ((rr >> 2) & 3);
+    int64_t grow = r0 + wave * 16 + rr;
+    grow = grow < batch ? grow : batch - 1;
+    glds16(x + grow * ldx + c * kKC + 4 * q, st + (unsigned)(wave * 16 * kKC * 4));
+    const char *src = wsp + (int64_t)c * 24576;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const int piece = wave * 6 + j;
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src + piece * 1024 + lane * 16),
+                     "s"(st + (unsigned)(4096 + piece * 1024))
+                     : "memory", "m0");
+    }
+}
+constexpr int kPDmaPerChunk = 7;
+
+__device__ __forceinline__ void gemm_chunk_s3p(const char *st, f32x16 (&acc)[2][2], int lane, int wave) {
+    const float *A = reinterpret_cast<const float *>(st);
+    const int h = lane >> 5, i = lane & 31;
+    const int sw = (i >> 2) & 3;
+    const int olo = 4 * (h ^ sw), ohi = 4 * ((h + 2) ^ sw);
+    xpa_bf16x8 ah[2], am[2], al[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+        const float *pa = A + (rt * 32 + i) * kKC;
+        xpa_split8(*reinterpret_cast<const float4 *>(pa + olo), *reinterpret_cast<const float4 *>(pa + ohi), ah[rt],
+                   am[rt], al[rt]);
+    }
+    const xpa_bf16x8 *bimg = reinterpret_cast<const xpa_bf16x8 *>(st + 4096) + lane;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+        const int cb = 2 * wave + ct;
+        const xpa_bf16x8 bh = bimg[cb * 64], bm = bimg[(8 + cb) * 64], bl = bimg[(16 + cb) * 64];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) acc[rt][ct] = xpa_mfma_s3(ah[rt], am[rt], al[rt], bh, bm, bl, acc[rt][ct]);
+    }
+}
+
 // K16X prologue (r03): the representation's first layer (K13's Linear(d_in <= 20, 256) + activation, bit for bit
 // its fmaf chain over the zero-padded inputs) for the tile's rows, from the minibatch's gathered observation rows;
 // thread t = column t; h goes to HBM (the backward's copy) with plain stores, so the k loop's A-operand DMAs right
@@ -777,7 +824,7 @@ __device__ __forceinline__ void trunk_prologue(float *s_x, const float *__restri
 
 // TRUNK (K16X, r03): the prologue above forms the tile's A rows (h) first; z / ldx are then ignored and the k loop
 // reads A from hout / ldh.
-template <int MODE, int ALGO, int ACT, int KMAX, bool TRUNK = false, bool S3 = false>
+template <int MODE, int ALGO, int ACT, int KMAX, bool TRUNK = false, int S3 = 0>
 __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAMS, const float *__restrict__ xr = nullptr,
                                                            int64_t ldxr = 0, int din = 0,
                                                            const float *__restrict__ W0 = nullptr,
@@ -823,6 +870,18 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
             lda = ldh;
         }
 #if XPA_HEAD_PROBE != 2 && XPA_HEAD_PROBE != 4 && XPA_HEAD_PROBE != 5  // tools/head_probe.py: 2 = epilogue alone (4, 5: parts of it)
+        if constexpr (S3 == 2) {   // K16P: Wh arrives as its three bf16 planes (the pointer is the split buffer)
+            const char *wsp = reinterpret_cast<const char *>(Wh);
+            gemm_issue_p(lds_base, xa, lda, wsp, r0, batch, 0, lane, wave);
+#pragma unroll 1
+            for (int c = 0; c < kChunks; ++c) {
+                // own chunk-c DMAs landed, then every wave's; chunk c - 1's stage (the one c + 1 refills) was read
+                asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+                if (c + 1 < kChunks)
+                    gemm_issue_p(lds_base + ((c + 1) & 1) * kPStageB, xa, lda, wsp, r0, batch, c + 1, lane, wave);
+                gemm_chunk_s3p(reinterpret_cast<const char *>(smem) + (c & 1) * kPStageB, acc, lane, wave);
+            }
+        } else {
         gemm_issue(lds_base, xa, lda, Wh, r0, batch, 0, lane, wave);
         gemm_issue(lds_base + kStage * 4, xa, lda, Wh, r0, batch, kKC, lane, wave);
 #pragma unroll 1
@@ -835,9 +894,10 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
                 gemm_issue(lds_base + ((c + 2) % kStages) * kStage * 4, xa, lda, Wh, r0, batch, (c + 2) * kKC, lane,
                            wave);
 #if XPA_HEAD_PROBE != 3  // 3 = operand staging alone
-            if constexpr (S3) gemm_chunk_s3(smem + (c % kStages) * kStage, acc, lane, wave);
+            if constexpr (S3 == 1) gemm_chunk_s3(smem + (c % kStages) * kStage, acc, lane, wave);
             else gemm_chunk(smem + (c % kStages) * kStage, acc, lane, wave);
 #endif
+        }
         }
         __syncthreads();  // every wave done with the stages before the h tile overwrites them
 #endif
@@ -1035,7 +1095,7 @@ XPA_API int64_t xpa_head_fused_num_partials(int64_t batch) {
 namespace {
 #define XPA_HEAD_ARGS(a) a.batch, a.K, a.ld, a.z, a.ldx, a.Wh, a.bh, a.W, a.bias, a.slope, a.logstd, a.idx, a.n_rows, a.act, a.old_logp, a.adv, a.ret, a.adv_partials, a.n_adv_partials, a.clip_range, a.ent_coef, a.vf_coef, a.dz, a.p_dw, a.p_dbh, a.p_dbo, a.p_loss, a.loss_width
 // KIND: 0 K12 (z from HBM), 1 K16 (hidden GEMM inside), 2 K16X (trunk layer + hidden GEMM inside), 3 K16W,
-// 4 K16S (K16 with the hidden GEMM on the bf16 matrix cores by the three-way split)
+// 4 K16S (K16 with the hidden GEMM on the bf16 matrix cores by the three-way split), 5 K16P (K16S with Wh pre-split)
 template <int KIND, int MODE, int ALGO, int ACT, int KMAX>
 void launch_one(const HeadArgs &a, hipStream_t s) {
     const dim3 grid((unsigned)xpa_head_fused_num_partials(a.batch)), block(256);
@@ -1044,7 +1104,10 @@ void launch_one(const HeadArgs &a, hipStream_t s) {
             hipLaunchKernelGGL((head_gemm_ws_kernel<MODE, ALGO, ACT, KMAX>), dim3((unsigned)head_ws_grid(a.batch)),
                                dim3(512), 0, s, XPA_HEAD_ARGS(a));
     } else if constexpr (KIND == 4)
-        hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, false, true>), grid, block, 0, s, XPA_HEAD_ARGS(a),
+        hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, false, 1>), grid, block, 0, s, XPA_HEAD_ARGS(a),
+                           nullptr, (int64_t)0, 0, nullptr, nullptr, 0.f, nullptr, (int64_t)0);
+    else if constexpr (KIND == 5)
+        hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, false, 2>), grid, block, 0, s, XPA_HEAD_ARGS(a),
                            nullptr, (int64_t)0, 0, nullptr, nullptr, 0.f, nullptr, (int64_t)0);
     else if constexpr (KIND == 2)
         hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, true>), grid, block, 0, s, XPA_HEAD_ARGS(a), a.xr,
@@ -1205,6 +1268,9 @@ XPA_API int xpa_head_gemm_critic(XPA_GEMM_CRITIC_PARAMS) { return gemm_critic_en
 // K16S: the same arguments and outputs; the hidden GEMM at the f32 GEMM's accuracy, not K16's bits
 XPA_API int xpa_head_gemm_s3_actor(XPA_GEMM_ACTOR_PARAMS) { return gemm_actor_entry<4>(XPA_GEMM_ACTOR_ARGS); }
 XPA_API int xpa_head_gemm_s3_critic(XPA_GEMM_CRITIC_PARAMS) { return gemm_critic_entry<4>(XPA_GEMM_CRITIC_ARGS); }
+// K16P: as K16S with w_hidden = the split buffer of Wh^T (xpa_s3_split_b(Wh, 256, 256, 1, 256, ...))
+XPA_API int xpa_head_gemm_s3p_actor(XPA_GEMM_ACTOR_PARAMS) { return gemm_actor_entry<5>(XPA_GEMM_ACTOR_ARGS); }
+XPA_API int xpa_head_gemm_s3p_critic(XPA_GEMM_CRITIC_PARAMS) { return gemm_critic_entry<5>(XPA_GEMM_CRITIC_ARGS); }
 
 // K16W entries: xpa_head_gemm_actor / _critic's arguments and outputs (the same partial-row count, rows the grid does
 // not own written as zeros); act_dim <= 8.
