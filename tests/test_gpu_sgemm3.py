@@ -142,3 +142,23 @@ def test_wgrad_wave_specialised_equals_k41(rows, m, slices):
     finally:
         L.xpa_s3_probe(0)
     assert torch.equal(p0, p1)
+
+
+@pytest.mark.parametrize("m,k", [(65536, 512), (4133, 256), (100, 32)])
+def test_gemm_wave_specialised_equals_k40(m, k):
+    """K40W (producer / consumer waves, form bit 16) and K40's two-block form (bit 8) write K40's output bit for bit:
+    the same split, the same six products in the same order per accumulator, the same k order."""
+    from xuanpolicy_amd import ops
+    L = ops.lib()
+    g = torch.Generator(device=DEV).manual_seed(m + 7 * k)
+    a = _wide((m, k), g)
+    sp = ops.s3_split(torch.randn(k, 256, device=DEV, generator=g) / 16)
+    ref = ops.s3_gemm(a, sp, k)
+    try:
+        for form in (8, 16):
+            assert L.xpa_s3_probe(form) == 0
+            out = ops.s3_gemm(a, sp, k)
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref), form
+    finally:
+        L.xpa_s3_probe(0)

@@ -181,6 +181,117 @@ __global__ __launch_bounds__(64 * W, 8 / W) void s3_gemm_kernel(const float *__r
     }
 }
 
+// K40W: K40 with the roles split over the waves (as K41W): waves 4-7 (producers) DMA the operands of chunk c + 2 (their
+// own 32 A rows each + B's planes) and split chunk c + 1's A rows (own DMAs, so a vmcnt wait suffices) into the bf16
+// planes of the stage, while waves 0-3 (consumers, one per SIMD, 32 rows x 256 columns each) read ready planes and run
+// chunk c's 48 MFMAs; one barrier per chunk.  Stage: A planes [3][4 row blocks][64 lanes][16 B] (12 KiB), B planes
+// (24 KiB), the raw A rows (8 KiB, K16's swizzled image); 3 stages, one 512-thread block per CU, persistent over
+// 128-row tiles.  Products, their order and the k order are K40's: the output is K40's bit for bit.
+constexpr int kWRows = 128;
+constexpr int kWAPl = 3 * 4 * 1024;                 // A planes, bytes
+constexpr int kWRaw = kWRows * kKC * 4;             // raw A rows, bytes
+constexpr int kWStage = kWAPl + kBImg + kWRaw;      // 44 KiB
+constexpr int kWDma = 2 + kBImg / 1024 / 4;         // per producer wave and chunk: 2 A rows + 6 B pieces
+
+__device__ __forceinline__ void w_issue(unsigned st, const float *__restrict__ a, int64_t lda,
+                                        const __bf16 *__restrict__ bs, int64_t r0, int64_t M, int c, int lane, int pw) {
+    const int rr = lane >> 2, p = lane & 3;
+    const int q = p ^ ((rr >> 2) & 3);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        int64_t row = r0 + pw * 32 + i * 16 + rr;
+        row = row < M ? row : M - 1;
+        glds16(a + row * lda + c * kKC + 4 * q, st + (unsigned)(kWAPl + kBImg + (pw * 32 + i * 16) * kKC * 4));
+    }
+    const char *bsrc = reinterpret_cast<const char *>(bs) + (int64_t)c * kBImg;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const int piece = pw * 6 + j;
+        glds16(bsrc + piece * 1024 + lane * 16, st + (unsigned)(kWAPl + piece * 1024));
+    }
+}
+
+// producer wave pw: split its 32 raw rows (lane (i, h): row 32 pw + i, quads h and h + 2) into the A planes
+__device__ __forceinline__ void w_split(char *st, int lane, int pw) {
+    const int h = lane >> 5, i = lane & 31;
+    const int sw = (i >> 2) & 3;
+    const float *arow = reinterpret_cast<const float *>(st + kWAPl + kBImg) + (pw * 32 + i) * kKC;
+    bf16x8 ah, am, al;
+    xpa_split8(*reinterpret_cast<const float4 *>(arow + 4 * (h ^ sw)),
+               *reinterpret_cast<const float4 *>(arow + 4 * ((h + 2) ^ sw)), ah, am, al);
+    bf16x8 *pl = reinterpret_cast<bf16x8 *>(st) + pw * 64 + lane;
+    pl[0] = ah;
+    pl[4 * 64] = am;
+    pl[8 * 64] = al;
+}
+
+__device__ __forceinline__ void w_chunk(const char *st, f32x16 (&acc)[8], int lane, int cw) {
+    const bf16x8 *pa = reinterpret_cast<const bf16x8 *>(st) + cw * 64 + lane;
+    const bf16x8 ah = pa[0], am = pa[4 * 64], al = pa[8 * 64];
+    const bf16x8 *bimg = reinterpret_cast<const bf16x8 *>(st + kWAPl) + lane;
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb)
+        acc[cb] = xpa_mfma_s3(ah, am, al, bimg[cb * 64], bimg[(8 + cb) * 64], bimg[(16 + cb) * 64], acc[cb]);
+}
+
+__global__ __launch_bounds__(512, 1) void s3_gemm_ws_kernel(const float *__restrict__ a, int64_t lda,
+                                                            const __bf16 *__restrict__ bs, float *__restrict__ c,
+                                                            int64_t ldc, int64_t M, int nchunks) {
+    __shared__ __attribute__((aligned(16))) char lds[3 * kWStage];
+    const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int64_t ntiles = (M + kWRows - 1) / kWRows;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t r0 = tile * kWRows;
+        if (wave >= 4) {   // producers: 1 + nchunks barriers per tile, as the consumers
+            const int pw = wave - 4;
+            w_issue(base, a, lda, bs, r0, M, 0, lane, pw);
+            if (nchunks > 1) {
+                w_issue(base + kWStage, a, lda, bs, r0, M, 1, lane, pw);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWDma) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            w_split(lds, lane, pw);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll 1
+            for (int ch = 0; ch < nchunks; ++ch) {
+                if (ch + 2 < nchunks) {
+                    w_issue(base + ((ch + 2) % 3) * kWStage, a, lda, bs, r0, M, ch + 2, lane, pw);
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWDma) : "memory");   // chunk ch + 1 landed
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                if (ch + 1 < nchunks) w_split(lds + ((ch + 1) % 3) * kWStage, lane, pw);
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            }
+            continue;
+        }
+        f32x16 acc[8];
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[cb][r] = 0.f;
+        asm volatile("s_barrier" ::: "memory");
+#pragma unroll 1
+        for (int ch = 0; ch < nchunks; ++ch) {
+            w_chunk(lds + (ch % 3) * kWStage, acc, lane, wave);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        const int h = lane >> 5, col = lane & 31;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t row = r0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (row < M) {
+                float *crow = c + row * ldc + col;
+#pragma unroll
+                for (int cb = 0; cb < 8; ++cb) crow[cb * 32] = acc[cb][r];
+            }
+        }
+    }
+}
+
 // ---- K41: weight gradients dW = A^T B over the batch (K = rows), split-K -----------------------------------
 // out[s] [M, 256] = A[rows of slice s]^T . B[rows of slice s], A [rows, M] (dz), B [rows, 256] (the layer input);
 // the slices are summed by the caller (the learner's fixed-order f64 column-sum finalize), as the batched f32 GEMM
@@ -503,7 +614,13 @@ XPA_API int xpa_s3_gemm(const float *a, int64_t lda, const void *b_split, float 
         return (int)hipErrorInvalidValue;
     const __bf16 *bs = static_cast<const __bf16 *>(b_split);
     const int nch = (int)(k / kKC);
-    // form (probe bit 8): 0 = one 8-wave block per CU with a 3-stage ring, 8 = two 4-wave blocks per CU, 2 stages
+    // form (probe bits 8 / 16): 0 = one 8-wave block per CU with a 3-stage ring, 8 = two 4-wave blocks per CU, 2 stages,
+    // 16 = the wave-specialised K40W
+    if (g_s3_probe & 16) {
+        const int64_t nt = (m + kWRows - 1) / kWRows;
+        s3_gemm_ws_kernel<<<dim3((unsigned)(nt < 256 ? nt : 256)), dim3(512), 0, stream>>>(a, lda, bs, c, ldc, m, nch);
+        return xpa_launch_status();
+    }
     if (g_s3_probe & 8) {
         const dim3 grid((unsigned)((m + 127) / 128)), block(256);
         switch (g_s3_probe & 7) {
