@@ -146,7 +146,8 @@ def test_wgrad_wave_specialised_equals_k41(rows, m, slices):
 
 @pytest.mark.parametrize("m,k", [(65536, 512), (4133, 256), (100, 32)])
 def test_gemm_wave_specialised_equals_k40(m, k):
-    """K40W (producer / consumer waves, form bit 16) and K40's two-block form (bit 8) write K40's output bit for bit:
+    """K40W (producer / consumer waves, form bit 16), K40's two-block form (bit 8) and its 64 x 128 wave tile (bit 32)
+    write K40's output bit for bit:
     the same split, the same six products in the same order per accumulator, the same k order."""
     from xuanpolicy_amd import ops
     L = ops.lib()
@@ -155,7 +156,7 @@ def test_gemm_wave_specialised_equals_k40(m, k):
     sp = ops.s3_split(torch.randn(k, 256, device=DEV, generator=g) / 16)
     ref = ops.s3_gemm(a, sp, k)
     try:
-        for form in (8, 16):
+        for form in (8, 16, 32):
             assert L.xpa_s3_probe(form) == 0
             out = ops.s3_gemm(a, sp, k)
             torch.cuda.synchronize()

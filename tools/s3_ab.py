@@ -80,7 +80,7 @@ def main():
         sp = ops.s3_split(torch.randn(K, 256, device=dev, generator=g) / 16)
         out = torch.empty(M, 256, device=dev)
         pr = res.setdefault("probe_us", {})
-        for mask in (0, 1, 2, 3, 4, 6, 8, 9, 10, 11, 12, 16):
+        for mask in (0, 1, 2, 3, 4, 6, 8, 9, 10, 11, 12, 16, 32):
             assert L.xpa_s3_probe(mask) == 0
             pr["k40_%d" % mask] = round(_time(lambda: ops.s3_gemm(x, sp, K, out=out), a.reps), 2)
             if mask < 8 or mask == 8:

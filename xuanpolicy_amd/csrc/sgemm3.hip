@@ -139,7 +139,32 @@ __device__ __forceinline__ void chunk(const char *st, f32x16 (&acc)[8], int lane
         acc[cb] = xpa_mfma_s3(ah, am, al, bimg[cb * 64], bimg[(8 + cb) * 64], bimg[(16 + cb) * 64], acc[cb]);
 }
 
-template <int W, int S, int PROBE>
+// the 64 x 128 wave tile (W = 8 only): wave (wr = w & 3, wc = w >> 2) owns rows 64 wr .. + 63 x columns 128 wc ..
+// + 127 (2 x 4 accumulators): per chunk 4 A + 12 B fragment reads per wave instead of 2 + 24 (the LDS reads of the
+// 32 x 256 tile were one B image per wave)
+__device__ __forceinline__ void chunk64(const char *st, f32x16 (&acc)[8], int lane, int wave) {
+    constexpr int kAImg = S3Geom<8>::kAImg;
+    const int h = lane >> 5, i = lane & 31;
+    const int sw = (i >> 2) & 3;
+    const int wr = wave & 3, wc = wave >> 2;
+    bf16x8 ah[2], am[2], al[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+        const float *arow = reinterpret_cast<const float *>(st) + (wr * 64 + rt * 32 + i) * kKC;
+        xpa_split8(*reinterpret_cast<const float4 *>(arow + 4 * (h ^ sw)),
+                   *reinterpret_cast<const float4 *>(arow + 4 * ((h + 2) ^ sw)), ah[rt], am[rt], al[rt]);
+    }
+    const bf16x8 *bimg = reinterpret_cast<const bf16x8 *>(st + kAImg) + lane;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int cb = 4 * wc + j;
+        const bf16x8 bh = bimg[cb * 64], bm = bimg[(8 + cb) * 64], bl = bimg[(16 + cb) * 64];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) acc[rt * 4 + j] = xpa_mfma_s3(ah[rt], am[rt], al[rt], bh, bm, bl, acc[rt * 4 + j]);
+    }
+}
+
+template <int W, int S, int PROBE, int T64 = 0>
 __global__ __launch_bounds__(64 * W, 8 / W) void s3_gemm_kernel(const float *__restrict__ a, int64_t lda,
                                                                const __bf16 *__restrict__ bs, float *__restrict__ c,
                                                                int64_t ldc, int64_t M, int nchunks) {
@@ -166,10 +191,26 @@ __global__ __launch_bounds__(64 * W, 8 / W) void s3_gemm_kernel(const float *__r
         else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         if (ch + S - 1 < nchunks && (PROBE & 2) == 0)
             issue<W>(base + ((ch + S - 1) % S) * G::kStage, a, lda, bs, r0, M, ch + S - 1, lane, wave);
-        chunk<W, PROBE>(lds + (ch % S) * G::kStage, acc, lane, wave);
+        if constexpr (T64 != 0) chunk64(lds + (ch % S) * G::kStage, acc, lane, wave);
+        else chunk<W, PROBE>(lds + (ch % S) * G::kStage, acc, lane, wave);
     }
     // C/D map of 32x32 MFMA: row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col = lane & 31
     const int h = lane >> 5, col = lane & 31;
+    if constexpr (T64 != 0) {
+        const int wr = wave & 3, wc = wave >> 2;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t row = r0 + wr * 64 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (row < M) {
+                    float *crow = c + row * ldc + 128 * wc + col;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) crow[j * 32] = acc[rt * 4 + j][r];
+                }
+            }
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int64_t row = r0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -616,6 +657,11 @@ XPA_API int xpa_s3_gemm(const float *a, int64_t lda, const void *b_split, float 
     const int nch = (int)(k / kKC);
     // form (probe bits 8 / 16): 0 = one 8-wave block per CU with a 3-stage ring, 8 = two 4-wave blocks per CU, 2 stages,
     // 16 = the wave-specialised K40W
+    if (g_s3_probe & 32) {   // the 64 x 128 wave tile
+        s3_gemm_kernel<8, 3, 0, 1><<<dim3((unsigned)((m + 255) / 256)), dim3(512), 0, stream>>>(a, lda, bs, c, ldc, m,
+                                                                                              nch);
+        return xpa_launch_status();
+    }
     if (g_s3_probe & 16) {
         const int64_t nt = (m + kWRows - 1) / kWRows;
         s3_gemm_ws_kernel<<<dim3((unsigned)(nt < 256 ? nt : 256)), dim3(512), 0, stream>>>(a, lda, bs, c, ldc, m, nch);
