@@ -163,3 +163,29 @@ def test_gemm_wave_specialised_equals_k40(m, k):
             assert torch.equal(out, ref), form
     finally:
         L.xpa_s3_probe(0)
+
+
+@pytest.mark.parametrize("rows,m,lda_pad,slices", [(65536, 512, 0, None), (4133, 256, 8, 5), (100, 128, 0, 1),
+                                                   (33, 128, 4, 2)])
+def test_wgrad_vector_staged_matches_f32_gemm_error(rows, m, lda_pad, slices):
+    """K41V (form bit 16: float4 staging, k-major planes read back with ds_read_b64_tr_b16): the slices' sum within
+    the f32 GEMM's own error against an f64 product, like K41 (a different k order inside a step, so not K41's bits)."""
+    from xuanpolicy_amd import ops
+    L = ops.lib()
+    g = torch.Generator(device=DEV).manual_seed(rows + 5 * m)
+    a = _wide((rows, m + lda_pad), g)[:, :m]
+    b = torch.randn(rows, 256, device=DEV, generator=g)
+    assert L.xpa_s3_probe(16) == 0
+    try:
+        part = ops.s3_wgrad(a, b, slices=slices)
+        torch.cuda.synchronize()
+    finally:
+        L.xpa_s3_probe(0)
+    got = part.double().sum(0)
+    native = torch.mm(a.t(), b)
+    ref = a.double().t() @ b.double()
+    scale = ref.abs().max().item()
+    assert torch.isfinite(part).all()
+    err = (got - ref).abs().max().item()
+    err_f32 = (native.double() - ref).abs().max().item()
+    assert err <= 2 * err_f32 + 2 ** -24 * scale, (err, err_f32, scale)

@@ -598,6 +598,165 @@ __global__ __launch_bounds__(512, 1) void s3_wgrad_ws_kernel(const float *__rest
         }
 }
 
+// K41V: K41 with vector staging and transposed fragment reads.  Each thread loads whole float4s of a row (k) of
+// dz / x (6 dwordx4 per chunk instead of 24 k-strided dwords), splits them and writes the three bf16 planes k-major —
+// [32 k rows][128 columns] tiles, 256-B rows XOR-swizzled by 16-B chunk (cdna_hip_programming.md T10 layout (b)) — with
+// ds_write_b64; the MFMA fragments (8 consecutive k of one column) come back with ds_read_b64_tr_b16 (two per plane).
+// Natural k order inside a step (lane half h: k 8h .. 8h + 7); the outputs carry K41's accuracy, not its bits.
+constexpr int kVPlane = 32 * 128 * 2;                  // bytes of one [32][128] bf16 tile
+constexpr int kVStage = 3 * kVPlane + 3 * 2 * kVPlane;  // A: 3 planes x 1 tile; B: 3 planes x 2 tiles = 72 KiB
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+__device__ __forceinline__ int v_off(int row, int col) {   // byte offset of (row, col .. col + 3) in a [32][128] tile
+    const int ch = col >> 3;
+    return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) + 2 * (col & 7);
+}
+
+struct VUnits {
+    float4 a[2], b[4];
+};
+
+__device__ __forceinline__ float4 v_zero_if(float4 v, bool keep) {
+    return make_float4(keep ? v.x : 0.f, keep ? v.y : 0.f, keep ? v.z : 0.f, keep ? v.w : 0.f);
+}
+
+__device__ __forceinline__ void v_load(VUnits &u, const float *__restrict__ A, int64_t lda, const float *__restrict__ B,
+                                       int64_t ldb, int64_t k0, int64_t kend, int t) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int idx = t + 512 * j, k = idx >> 5, cq = idx & 31;
+        const int64_t r = k0 + k;
+        const float4 v = *reinterpret_cast<const float4 *>(A + min(r, kend - 1) * lda + 4 * cq);
+        u.a[j] = v_zero_if(v, r < kend);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int idx = t + 512 * j, k = idx >> 6, nq = idx & 63;
+        const int64_t r = k0 + k;
+        const float4 v = *reinterpret_cast<const float4 *>(B + min(r, kend - 1) * ldb + 4 * nq);
+        u.b[j] = v_zero_if(v, r < kend);
+    }
+}
+
+// the three planes of 4 consecutive columns, each packed as 4 bf16 (8 B)
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void v_put(char *plane0, int plane_stride, int off, float4 v) {
+    const float e[4] = {v.x, v.y, v.z, v.w};
+    bf16x4 h, m, l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        __bf16 a0, a1, a2;
+        xpa_split3(e[j], a0, a1, a2);
+        h[j] = a0;
+        m[j] = a1;
+        l[j] = a2;
+    }
+    *reinterpret_cast<bf16x4 *>(plane0 + off) = h;
+    *reinterpret_cast<bf16x4 *>(plane0 + plane_stride + off) = m;
+    *reinterpret_cast<bf16x4 *>(plane0 + 2 * plane_stride + off) = l;
+}
+
+__device__ __forceinline__ void v_store(char *st, const VUnits &u, int t) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int idx = t + 512 * j, k = idx >> 5, cq = idx & 31;
+        v_put(st, kVPlane, v_off(k, 4 * cq), u.a[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int idx = t + 512 * j, k = idx >> 6, n = 4 * (idx & 63);
+        v_put(st + 3 * kVPlane, 2 * kVPlane, (n >> 7) * kVPlane + v_off(k, n & 127), u.b[j]);
+    }
+}
+
+__device__ __forceinline__ bf16x8 v_frag(const char *tile, int row0, int col) {
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)(tile + v_off(row0, col)));
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s *)(tile + v_off(row0 + 4, col)));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+__device__ __forceinline__ void v_chunk(const char *st, f32x16 (&acc)[2][2], int lane, int wm, int wn) {
+    // lane 4q + p of 16-lane group g supplies row 8h + 4jj + q (h = g >> 1) and columns 16 (g & 1) + 4p .. + 3 of its
+    // 32-column block; it receives column 16 (g & 1) + (lane & 15): the MFMA's lane map (row / column lane & 31, k 8h + j)
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3, h = lane >> 5;
+    const int cofs = 16 * (g & 1) + 4 * p;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int row0 = 16 * s + 8 * h + q;
+        bf16x8 ah[2], am[2], al[2], bh[2], bm[2], bl[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int col = 32 * (2 * wm + i) + cofs;
+            ah[i] = v_frag(st, row0, col);
+            am[i] = v_frag(st + kVPlane, row0, col);
+            al[i] = v_frag(st + 2 * kVPlane, row0, col);
+            const int n = 32 * (2 * wn + i) + cofs;
+            const char *bt = st + 3 * kVPlane + (n >> 7) * kVPlane;
+            bh[i] = v_frag(bt, row0, n & 127);
+            bm[i] = v_frag(bt + 2 * kVPlane, row0, n & 127);
+            bl[i] = v_frag(bt + 4 * kVPlane, row0, n & 127);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = xpa_mfma_s3(ah[i], am[i], al[i], bh[j], bm[j], bl[j], acc[i][j]);
+    }
+}
+
+__global__ __launch_bounds__(512, 1) void s3_wgrad_v_kernel(const float *__restrict__ A, int64_t lda,
+                                                            const float *__restrict__ B, int64_t ldb, int64_t rows,
+                                                            int64_t M, int slices, int64_t slice_rows,
+                                                            float *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * kVStage];
+    const int mtiles = (int)(M / kWgM);
+    const int nblk = slices * mtiles;
+    int L = blockIdx.x;
+    if (nblk % 8 == 0) L = (blockIdx.x & 7) * (nblk >> 3) + (blockIdx.x >> 3);  // one slice's tiles on one XCD
+    const int slice = L / mtiles, mt = L - slice * mtiles;
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wm = wave & 1, wn = wave >> 1;
+    const float *Am = A + (int64_t)mt * kWgM;
+    const int64_t k0 = (int64_t)slice * slice_rows;
+    const int64_t kend = min(rows, k0 + slice_rows);
+    const int nch = kend > k0 ? (int)((kend - k0 + kWgKC - 1) / kWgKC) : 0;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    VUnits u;
+    if (nch > 0) {
+        v_load(u, Am, lda, B, ldb, k0, kend, t);
+        v_store(lds, u, t);
+        if (nch > 1) v_load(u, Am, lda, B, ldb, k0 + kWgKC, kend, t);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+#pragma unroll 1
+    for (int c = 0; c < nch; ++c) {
+        v_chunk(lds + (c & 1) * kVStage, acc, lane, wm, wn);
+        if (c + 1 < nch) {
+            v_store(lds + ((c + 1) & 1) * kVStage, u, t);
+            if (c + 2 < nch) v_load(u, Am, lda, B, ldb, k0 + (int64_t)(c + 2) * kWgKC, kend, t);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    float *o = out + ((int64_t)slice * M + (int64_t)mt * kWgM) * kN;
+    const int h = lane >> 5, col = lane & 31;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = 64 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) o[(int64_t)row * kN + 64 * wn + 32 * j + col] = acc[i][j][r];
+        }
+}
+
 }  // namespace
 
 // the split-K slice count of xpa_s3_wgrad for this shape (the caller's workspace: slices x m x 256 floats)
@@ -617,6 +776,11 @@ XPA_API int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ld
     int64_t per = (rows + slices - 1) / slices;
     per = (per + kWgKC - 1) / kWgKC * kWgKC;
     const dim3 grid((unsigned)(slices * (m / kWgM))), block(512);
+    if ((g_s3_probe & 16) && lda % 4 == 0 && ldb % 4 == 0 && ((reinterpret_cast<uintptr_t>(a) |
+                                                                 reinterpret_cast<uintptr_t>(b)) & 15) == 0) {
+        s3_wgrad_v_kernel<<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out);   // K41V
+        return xpa_launch_status();
+    }
     if (g_s3_probe & 8) {   // the wave-specialised form (K41W)
         s3_wgrad_ws_kernel<<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out);
         return xpa_launch_status();
