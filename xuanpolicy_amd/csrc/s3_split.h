@@ -1,7 +1,8 @@
 // The three-way bf16 split of f32 operands for the bf16 matrix cores (K40 sgemm3.hip, K16S head.hip).
 //
 // x = hi + mid + lo EXACTLY: hi = bf16_rn(x), mid = bf16_rn(x - hi), lo = bf16_rn(x - hi - mid); both residuals are
-// exact in f32 and 3 x 8 significant bits cover the f32 significand (lo is exact for |x| above ~2^-110).  A product
+// exact in f32 and 3 x 8 significant bits cover the f32 significand: exact for 2^-100 <= |x| < 3.39e38 (bf16's largest
+// finite value; below 2^-100 lo drops bits under 2^-24 of x, tests/test_split_model_cpu.py).  A product
 // a b keeps the six terms above 2^-24 relative, summed smallest first into one f32 accumulator:
 //     am bm + ah bl + al bh + ah bm + am bh + ah bh
 // (dropped: am bl, al bm, al bl <= 2^-25 relative).  Each bf16 x bf16 product is exact in f32.  An infinite or NaN
