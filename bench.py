@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--gemm", choices=("f32", "split3"), default="f32",
                    help="the update's hidden-layer GEMMs: f32 MFMA (K16 + hipBLASLt) or the bf16 three-way split "
                         "(K16S + K40 + K41, the f32 GEMM's accuracy on the bf16 matrix cores)")
+    p.add_argument("--s3-heads", choices=("s3", "s3p"), default="s3",
+                   help="with --gemm split3: K16S (both fragments split in the k loop) or K16P (Wh's planes split once)")
     p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc HBM-traffic passes")
     p.add_argument("--no-rocprof", action="store_true",
                    help="skip the child rocprofv3 --kernel-trace run that times the in-loop GAE launches")
@@ -814,6 +816,7 @@ def main():
     from xuanpolicy_amd.runner import build_synthbox_ppo
 
     ops.S3_GEMMS = args.gemm == "split3"
+    ops.S3_HEADS = args.s3_heads
     rank, local, world = init_from_env()
     device = local_device(local)
     torch.cuda.set_device(device)

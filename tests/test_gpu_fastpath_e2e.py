@@ -82,14 +82,16 @@ def test_fast_path_iteration_with_k16w_matches_oracle(agent_name, discrete, A, m
                                expect_mid_truncations=not discrete)
 
 
-@pytest.mark.parametrize("agent_name,discrete,A", [("PPO_Clip", False, 6), ("A2C", True, 18)])
-def test_fast_path_iteration_with_split_gemms_matches_oracle(agent_name, discrete, A, monkeypatch):
+@pytest.mark.parametrize("agent_name,discrete,A,heads", [("PPO_Clip", False, 6, "s3"), ("A2C", True, 18, "s3"),
+                                                         ("PPO_Clip", False, 6, "s3p")])
+def test_fast_path_iteration_with_split_gemms_matches_oracle(agent_name, discrete, A, heads, monkeypatch):
     """The same end-to-end replay with the update's hidden-layer GEMMs on the bf16 matrix cores by the three-way
     split (ops.S3_GEMMS: K16S heads, K40 dX, K41 dW slices into the f64 finalize): every update's loss within 1e-4
     and the final weights, as for the f32 MFMA path."""
     from xuanpolicy_amd import ops
     from xuanpolicy_amd.runner import build_synthbox_ppo
     monkeypatch.setattr(ops, "S3_GEMMS", True)
+    monkeypatch.setattr(ops, "S3_HEADS", heads)
     N, T, D, H = 512, 64, 17, 256
     agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=D, act_dim=A, hidden=H, n_epoch=2, n_minibatch=4,
                                seed=21, device=DEV, agent=agent_name, discrete=discrete, ent_coef=0.01,
@@ -100,6 +102,8 @@ def test_fast_path_iteration_with_split_gemms_matches_oracle(agent_name, discret
     agent.train(T - 1, log=False)
     assert any(k[0] == "s3wgrad" for k in fm._partials if isinstance(k, tuple)), "K41 not used"
     assert any(k[0] == "s3split" for k in fm._partials if isinstance(k, tuple)), "K40 not used"
+    if heads == "s3p":
+        assert any(k[:2] == ("s3split", "s3p_a") for k in fm._partials if isinstance(k, tuple)), "K16P not used"
     replay_last_step_iteration(agent, D, A, [H], discrete, "ppo" if agent_name == "PPO_Clip" else "a2c", 0.01, 2, 4,
                                expect_mid_truncations=not discrete)
 

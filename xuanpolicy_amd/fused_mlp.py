@@ -344,9 +344,11 @@ class FusedActorCritic:
         paired = self.pair is not None
         if self._hws is None or self._hws.batch != B:
             self._hws = ops.HeadWorkspace(B, K, s.device, paired=paired)
-        gemm = None
+        gemm = wh_split = None
         if z_a is None:   # K16
             gemm = (s, (lin_ah.weight, lin_ah.bias), (lin_ch.weight, lin_ch.bias))
+            if ops.S3_GEMMS and ops.S3_HEADS == "s3p" and not ops.K16W_ENABLED:   # K16P: Wh^T's planes, once per update
+                wh_split = (self._split(lin_ah.weight.t(), "s3p_a"), self._split(lin_ch.weight.t(), "s3p_c"))
         grads = {"w_actor": lin_ao.weight.grad, "b_actor": lin_ao.bias.grad, "bh_actor": lin_ah.bias.grad,
                  "w_critic": lin_co.weight.grad, "b_critic": lin_co.bias.grad, "bh_critic": lin_ch.bias.grad}
         if self.logstd is not None:
@@ -359,6 +361,7 @@ class FusedActorCritic:
                                               adv, ret, old_logp=old_logp, idx=idx, adv_partials=adv_partials,
                                               clip_range=clip_range, vf_coef=vf_coef, ent_coef=ent_coef, grads=grads,
                                               colsum_queue=self._cq, gemm=gemm, sq_logstd=self._sq.data_ptr(),
+                                              wh_split=wh_split,
                                               defer_loss=True,
                                               trunk=x.trunk if gemm is not None and isinstance(x, Rows) else None)
         have_rep = len(self.rep) > 0
@@ -426,18 +429,23 @@ class FusedActorCritic:
                                         ops._p(g) if code else None, ops._p(part), s), "xpa_act_bwd_colsum")
         _lib.check(L.xpa_colsum_finalize(ops._p(part), part.shape[0], cols, ops._p(out), s), "xpa_colsum_finalize")
 
+    def _split(self, b, name):
+        """s3_split of b [k, 256] into a buffer kept per name (graph-capture safe: allocated on first use)."""
+        k = b.shape[0]
+        key = ("s3split", name, k)
+        buf = self._partials.get(key)
+        if buf is None:
+            buf = torch.empty(int(ops.lib().xpa_s3_split_bytes(k, 256)), dtype=torch.uint8, device=b.device)
+            self._partials[key] = buf
+        return ops.s3_split(b, out=buf)
+
     def _dx(self, dz, w):
         """dX = dz w (w [k, n_in]): K40 on the bf16 matrix cores by the three-way split when ops.S3_GEMMS and the shape
         fits (n_in = 256, k % 16 == 0), else the f32 GEMM."""
         k, n_in = w.shape
         if not (ops.S3_GEMMS and n_in == 256 and k % 16 == 0 and dz.stride(1) == 1):
             return torch.mm(dz, w)
-        key = ("s3split", k)
-        buf = self._partials.get(key)
-        if buf is None:
-            buf = torch.empty(int(ops.lib().xpa_s3_split_bytes(k, n_in)), dtype=torch.uint8, device=dz.device)
-            self._partials[key] = buf
-        return ops.s3_gemm(dz, ops.s3_split(w, out=buf), k)
+        return ops.s3_gemm(dz, self._split(w, "dx"), k)
 
     def _weight_grad(self, dz, x, out, queue=None):
         """dW = dz^T x.  Split-K (a batched GEMM over slices of the batch) when the GEMM alone would not

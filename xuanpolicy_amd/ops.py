@@ -564,11 +564,13 @@ K16W_ENABLED = False  # fused_heads' gemm form: K16W (xpa_head_gemm_ws_*) where 
 # The update's hidden-layer GEMMs on the bf16 matrix cores by the three-way split (K16S heads, K40 dX, K41 dW):
 # the f32 GEMM's accuracy, not the f32 MFMA's bits.  Read when a learner's update is built / captured.
 S3_GEMMS = False
+S3_HEADS = "s3"   # with S3_GEMMS: "s3" K16S (both fragments split in the k loop), "s3p" K16P (Wh's planes split once)
 
 
 def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, w_critic, b_critic, act_critic,
                 logstd, act, adv, ret, old_logp=None, idx=None, adv_partials=None, clip_range=0.2, vf_coef=0.25,
-                ent_coef=0.0, grads=None, colsum_queue=None, gemm=None, sq_logstd=None, defer_loss=False, trunk=None):
+                ent_coef=0.0, grads=None, colsum_queue=None, gemm=None, sq_logstd=None, defer_loss=False, trunk=None,
+                wh_split=None):
     """K12 actor + critic heads, loss finalize and the column-sum finalizes.
 
     z_*: hidden pre-activations [B, 256] (unit column stride; row stride = the workspace dz row stride,
@@ -577,7 +579,8 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
     run inside the head kernels on the matrix cores and z_actor / z_critic are not used (pass None).
     trunk = (x_rows [B, d_in], w_in [256, d_in], b_in, slope_in, h_out) with gemm: K16X — the trunk layer
     Linear(d_in <= TRUNK_DMAX, 256) + the heads' activation is formed inside the launches too; gemm's x must be h_out,
-    which the actor launch writes. (K x 256 / 1 x 256); act_*: (code, slope)
+    which the actor launch writes.  wh_split = (planes of w_h_actor^T, planes of w_h_critic^T) (s3_split): K16P.
+    (K x 256 / 1 x 256); act_*: (code, slope)
     of the hidden activation.  colsum_queue: an ops.ColsumQueue to defer the column-sum finalizes into
     (flushed by the caller), else they run here.  grads: dict with the gradient views to write — 'w_actor', 'b_actor',
     'bh_actor', 'w_critic', 'b_critic', 'bh_critic', 'logstd' (gaussian).  Returns (scalars, dz_actor,
@@ -650,6 +653,9 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
         fa = L.xpa_head_gemm_ws_actor if wsa else L.xpa_head_gemm_s3_actor if S3_GEMMS else L.xpa_head_gemm_actor
         fc = (L.xpa_head_gemm_ws_critic if K16W_ENABLED else L.xpa_head_gemm_s3_critic if S3_GEMMS
               else L.xpa_head_gemm_critic)
+        if wh_split is not None and not wsa and not K16W_ENABLED:   # K16P: the hidden weights as their bf16 planes
+            fa, fc = L.xpa_head_gemm_s3p_actor, L.xpa_head_gemm_s3p_critic
+            wha, whc = wh_split
         _lib.check(fa(ALGO[algo], DIST[dist], act_actor[0], B, K, H, _p(x), x.stride(0), _p(wha),
                       _p(bha), ld, _p(w_actor), _p(b_actor), float(act_actor[1]), p_logstd, _p(idx),
                       rows, _p(act), p_old, _p(adv), _p(adv_partials), n_adv, float(clip_range),
