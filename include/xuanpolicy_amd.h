@@ -503,6 +503,9 @@ int xpa_head_gemm_critic(int act, int64_t batch, int64_t hidden, const float *x,
  * bit for bit; act_dim <= 8. */
 int64_t xpa_head_gemm_ws_grid(int64_t batch);
 int xpa_head_gemm_ws_probe(int mask); /* diagnostics: parts of K16W switched off (tools/k16w_ab.py); 0 = production */
+/* test support: fill every CU's LDS with NaN bit patterns, so a following kernel that reads LDS it did not write
+ * produces NaN (tests/test_gpu_fused_mlp.py) */
+int xpa_lds_poison(xpa_stream_t stream);
 int xpa_head_gemm_ws_actor(int algo, int dist, int act, int64_t batch, int64_t act_dim, int64_t hidden, const float *x,
                            int64_t ldx, const float *w_hidden, const float *b_hidden, int64_t ld_dz, const float *w,
                            const float *b, float slope, const float *logstd, const int64_t *idx, int64_t n_rows,

@@ -436,13 +436,16 @@ def test_colsum_queue_deferred_loss_finalize(nseg, dist):
     ("a2c", "categorical", 18, 777, 0, "s3p"),
     ("ppo", "categorical", 8, 193, 2, "s3p"),
 ])
-def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code, form):
+@pytest.mark.parametrize("poison", [False, True])
+def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code, form, poison):
     """K16 (xpa_head_gemm_actor / _critic), K16W (xpa_head_gemm_ws_*) or K16S (xpa_head_gemm_s3_*) through the C ABI against float64 autograd
     of the same head:
     z = x Wh^T + bh, h = act(z), head = h W^T + b, the PPO-Clip / A2C loss with Gaussian / Categorical
     log-prob + entropy (ppoclip_learner.py:32-44, a2c_learner.py:24-31) and the critic's value loss.
     Checked: dz (d loss / d z), the summed per-block partials (dW_out, db_out, db_hidden, loss sums) and
-    untouched memory around every output (canaries on both sides of dz and the partials)."""
+    untouched memory around every output (canaries on both sides of dz and the partials).  poison: every CU's LDS
+    filled with NaN bit patterns first (xpa_lds_poison) — a kernel reading LDS it did not write shows it (r04: the
+    critic's phase 2 read the unwritten pad slot of d head)."""
     from xuanpolicy_amd import ops
     L, s = ops.lib(), ops._stream()
     g = torch.Generator(device=DEV).manual_seed(B + K)
@@ -488,6 +491,9 @@ def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code, form):
     ent, clip, vf = 0.01, 0.2, 0.25
     pre = {"k16": "xpa_head_gemm_", "ws": "xpa_head_gemm_ws_", "s3": "xpa_head_gemm_s3_", "s3p": "xpa_head_gemm_s3p_"}[form]
     fa, fc = getattr(L, pre + "actor"), getattr(L, pre + "critic")
+    if poison:
+        torch.cuda.synchronize()
+        assert L.xpa_lds_poison(s) == 0
     if form == "s3p":   # the hidden weights as Wh^T's three bf16 planes
         wh_a_arg, wh_c_arg = ops.s3_split(wh_a.t()), ops.s3_split(wh_c.t())
     else:
@@ -496,6 +502,8 @@ def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code, form):
               ops._p(w_a), ops._p(b_a), slope, ops._p(logstd) if logstd is not None else None,
               ops._p(idx), R, ops._p(act), ops._p(old) if old is not None else None, ops._p(adv),
               None, 0, clip, ent, ops._p(dz), v(p_dw_a), v(p_dbh_a), v(p_dbo_a), v(lp), W, s) == 0
+    if poison:   # the critic launch behind fresh poison too (else it sees the actor's leftovers)
+        assert L.xpa_lds_poison(s) == 0
     assert fc(code, B, H, ops._p(x), H, ops._p(wh_c_arg), ops._p(bh_c), 2 * H, ops._p(w_c),
               ops._p(b_c), slope, ops._p(idx), R, ops._p(ret), vf, ops._p(dz[:, H:]), v(p_dw_c),
               v(p_dbh_c), v(p_dbo_c), v(lp), W, s) == 0

@@ -199,6 +199,7 @@ SIGNATURES = {
                                             c_i64, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64, c_p]),
     "xpa_head_gemm_ws_grid": (c_i64, [c_i64]),
     "xpa_head_gemm_ws_probe": (ctypes.c_int, [ctypes.c_int]),
+    "xpa_lds_poison": (ctypes.c_int, [c_p]),
     "xpa_head_gemm_ws_actor": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_i64,
                                               c_p, c_p, c_i64, c_p, c_p, c_f32, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64,
                                               c_f32, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64, c_p]),

@@ -411,8 +411,11 @@ struct HeadEpi {
             for (int o = 0; o < KMAX; ++o)
                 if (o < K) acc_dls[o] += ent_coef * inv_b;
         }
+        // the pad slots [KMAX, KP) too: phase 2 reads d head in float4s and, for KMAX = 1 (the critic), pairs slot 1
+        // with a zero weight — LDS left over from an earlier kernel there (an Inf / NaN bit pattern) made 0 x NaN
+        // dz rows (r04; tests/test_gpu_fused_mlp.py::test_head_gemm_kernels_vs_fp64_autograd after other kernels)
 #pragma unroll
-        for (int o = 0; o < KMAX; ++o) s_dh[lane][o] = dh_[o];
+        for (int o = 0; o < KP; ++o) s_dh[lane][o] = o < KMAX ? dh_[o] : 0.f;
     }
 
     // ---- phase 2, rows [r0, r1) of the tile: column owner.  dz[r, c] = (d head[r] . w[:, c]) * act'(h[r, c]), dW_out
@@ -1276,6 +1279,20 @@ XPA_API int xpa_head_gemm_s3p_critic(XPA_GEMM_CRITIC_PARAMS) { return gemm_criti
 // not own written as zeros); act_dim <= 8.
 XPA_API int64_t xpa_head_gemm_ws_grid(int64_t batch) {
     return head_ws_grid(batch);
+}
+
+// Test support: fill every CU's LDS with NaN bit patterns (one 160 KiB block per CU, twice over), so that a kernel
+// launched next that reads LDS it did not write sees a NaN instead of whatever the previous kernel left (usually
+// finite).  tests/test_gpu_fused_mlp.py runs the head kernels behind it.
+__global__ __launch_bounds__(1024) void lds_poison_kernel() {
+    __shared__ unsigned lds[40960];
+    for (int i = threadIdx.x; i < 40960; i += 1024) lds[i] = 0xFFFFFFFFu;
+    __syncthreads();
+    if (lds[(threadIdx.x * 37) % 40960] == 0u) lds[0] = 1u;  // keep the stores
+}
+XPA_API int xpa_lds_poison(xpa_stream_t stream) {
+    lds_poison_kernel<<<dim3(512), dim3(1024), 0, (hipStream_t)stream>>>();
+    return xpa_launch_status();
 }
 
 // diagnostics only (tools/k16w_ab.py --probe): see g_ws_probe
