@@ -51,10 +51,10 @@ def parse():
                         "split: value head (K14) then the compact GAE scan (K1)")
     p.add_argument("--trunk-heads", choices=("on", "off"), default="off",
                    help="K16X (trunk layer inside the head GEMM launches) or r03's K13 forward + K16 (A/B)")
-    p.add_argument("--gemm", choices=("f32", "split3"), default="f32",
+    p.add_argument("--gemm", choices=("f32", "split3"), default="split3",
                    help="the update's hidden-layer GEMMs: f32 MFMA (K16 + hipBLASLt) or the bf16 three-way split "
                         "(K16S + K40 + K41, the f32 GEMM's accuracy on the bf16 matrix cores)")
-    p.add_argument("--s3-heads", choices=("s3", "s3p"), default="s3",
+    p.add_argument("--s3-heads", choices=("s3", "s3p"), default="s3p",
                    help="with --gemm split3: K16S (both fragments split in the k loop) or K16P (Wh's planes split once)")
     p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc HBM-traffic passes")
     p.add_argument("--no-rocprof", action="store_true",
@@ -1031,7 +1031,9 @@ def main():
                                    "(n_epoch %d, n_minibatch %d, nets [%d] LeakyReLU)" %
                                    (N, T, args.n_epoch, args.n_minibatch, args.hidden),
                        "num_envs_per_gpu": N, "horizon": T, "global_envs": N * world, "minibatch": B,
-                       "update_gemms": ("bf16 three-way split (K16S heads, K40 dX, K41 dW; f32 accuracy)"
+                       "update_gemms": ("f32 GEMMs as exact three-way bf16 splits on the bf16 matrix cores (%s heads, "
+                                        "K40 dX, K41V dW; error <= 2x the f32 GEMM's vs f64: tests/test_gpu_sgemm3.py)"
+                                        % ("K16P" if ops.S3_HEADS == "s3p" else "K16S")
                                         if ops.S3_GEMMS else "f32 MFMA (K16 heads, hipBLASLt dX / dW)"),
                        "updates_per_step": args.n_epoch * args.n_minibatch,
                        "parallelism": ("dp1 (one env shard, no collective)" if world == 1 else

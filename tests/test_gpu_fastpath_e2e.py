@@ -146,11 +146,34 @@ def test_deferred_bootstraps_with_several_truncations_per_rollout():
     assert int(agent.slot_overflow) == 0 and int(agent.slot_t.max()) == -1
 
 
-def test_trunk_heads_iteration_equals_k13_k16():
+@pytest.mark.parametrize("agent_name,discrete,A", [("PPO_Clip", False, 6), ("A2C", True, 18)])
+def test_fast_path_iteration_with_f32_gemms_matches_oracle(agent_name, discrete, A, monkeypatch):
+    """The r03 update path (ops.S3_GEMMS off: K16 heads on the f32 MFMA, hipBLASLt dX and split-K dW) replayed the same
+    way — the A/B partner of the default split GEMMs (bench.py --gemm f32)."""
+    from xuanpolicy_amd import ops
+    from xuanpolicy_amd.runner import build_synthbox_ppo
+    monkeypatch.setattr(ops, "S3_GEMMS", False)
+    N, T, D, H = 512, 64, 17, 256
+    agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=D, act_dim=A, hidden=H, n_epoch=2, n_minibatch=4,
+                               seed=21, device=DEV, agent=agent_name, discrete=discrete, ent_coef=0.01,
+                               max_episode_steps=T + 17)
+    fm = agent.learner._fused_mlp()
+    assert fm is not None and fm.gemm_heads and fm.pair is not None
+    agent.train(T, log=False)
+    agent.train(T - 1, log=False)
+    assert not any(isinstance(k, tuple) and k[0] in ("s3split", "s3wgrad") for k in fm._partials)
+    replay_last_step_iteration(agent, D, A, [H], discrete, "ppo" if agent_name == "PPO_Clip" else "a2c", 0.01, 2, 4,
+                               expect_mid_truncations=not discrete)
+
+
+def test_trunk_heads_iteration_equals_k13_k16(monkeypatch):
     """The K16X learner wiring (fused_mlp.use_trunk_heads: the gather-only K13 form, xpa_head_gemm_trunk_actor writing
     h, plain K16 critic on that h, dW GEMM and K13 backward on it) against the default K13 forward + K16: one whole C2
-    fast-path iteration from the same seed, every parameter and every update's loss scalars bit for bit."""
+    fast-path iteration from the same seed, every parameter and every update's loss scalars bit for bit.  K16X exists on
+    the f32 MFMA only: both runs take the f32 GEMMs (ops.S3_GEMMS off)."""
+    from xuanpolicy_amd import ops
     from xuanpolicy_amd.runner import build_synthbox_ppo
+    monkeypatch.setattr(ops, "S3_GEMMS", False)
     runs = []
     for on in (False, True):
         agent = build_synthbox_ppo(n_envs=256, n_steps=32, obs_dim=17, act_dim=6, hidden=256, n_epoch=2,

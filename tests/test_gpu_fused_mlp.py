@@ -435,6 +435,7 @@ def test_colsum_queue_deferred_loss_finalize(nseg, dist):
     ("ppo", "gaussian", 6, 4133, 1, "s3p"),
     ("a2c", "categorical", 18, 777, 0, "s3p"),
     ("ppo", "categorical", 8, 193, 2, "s3p"),
+    ("ppo", "gaussian", 17, 4133, 1, "s3p"),   # C4's head on the production split form
 ])
 @pytest.mark.parametrize("poison", [False, True])
 def test_head_gemm_kernels_vs_fp64_autograd(algo, dist, K, B, code, form, poison):

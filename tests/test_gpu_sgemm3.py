@@ -102,16 +102,24 @@ def test_gemm_rejects_bad_shapes():
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("form", [0, 32])
 @pytest.mark.parametrize("rows,m,lda_pad,slices", [(65536, 512, 0, None), (65536, 256, 0, None), (4133, 512, 8, None),
-                                                   (100, 128, 0, 1), (1000, 256, 4, 7), (33, 128, 0, 2)])
-def test_wgrad_matches_f32_gemm_error(rows, m, lda_pad, slices):
-    """K41: the slices' sum of dz^T x against an f64 product, within the f32 GEMM's own error (torch's dz^T x on the
-    device); ragged slices (rows not a multiple of the slice count or of 32) and strided rows."""
+                                                   (100, 128, 0, 1), (1000, 256, 4, 7), (33, 128, 0, 2), (77, 128, 3, 2)])
+def test_wgrad_matches_f32_gemm_error(rows, m, lda_pad, slices, form):
+    """K41V (form 0, production) / the register-staged K41 (32): the slices' sum of dz^T x against an f64 product,
+    within the f32 GEMM's own error (torch's dz^T x on the device); ragged slices (rows not a multiple of the slice count
+    or of 32), strided rows, and an odd row stride (lda = m + 3: K41V's float4 staging does not apply, K41 runs)."""
     from xuanpolicy_amd import ops
+    L = ops.lib()
     g = torch.Generator(device=DEV).manual_seed(rows + m)
     a = _wide((rows, m + lda_pad), g)[:, :m]
     b = torch.randn(rows, 256, device=DEV, generator=g)
-    part = ops.s3_wgrad(a, b, slices=slices)
+    assert L.xpa_s3_probe(form) == 0
+    try:
+        part = ops.s3_wgrad(a, b, slices=slices)
+        torch.cuda.synchronize()
+    finally:
+        L.xpa_s3_probe(0)
     S = part.shape[0]
     assert S == (slices or ops.s3_wgrad_slices(rows, m))
     got = part.double().sum(0)
@@ -127,16 +135,17 @@ def test_wgrad_matches_f32_gemm_error(rows, m, lda_pad, slices):
 
 @pytest.mark.parametrize("rows,m,slices", [(65536, 512, None), (4133, 256, 5), (100, 128, 1)])
 def test_wgrad_wave_specialised_equals_k41(rows, m, slices):
-    """K41W (producer / consumer waves, xpa_s3_probe form bit 8) writes K41's partials bit for bit: the same LDS image,
-    products and k order per accumulator."""
+    """K41W (producer / consumer waves, xpa_s3_probe form bit 8) writes the register-staged K41's partials (bit 32) bit
+    for bit: the same LDS image, products and k order per accumulator."""
     from xuanpolicy_amd import ops
     L = ops.lib()
     g = torch.Generator(device=DEV).manual_seed(rows * 3 + m)
     a = _wide((rows, m), g)
     b = torch.randn(rows, 256, device=DEV, generator=g)
-    p0 = ops.s3_wgrad(a, b, slices=slices)
-    assert L.xpa_s3_probe(8) == 0
     try:
+        assert L.xpa_s3_probe(32) == 0
+        p0 = ops.s3_wgrad(a, b, slices=slices)
+        assert L.xpa_s3_probe(8) == 0
         p1 = ops.s3_wgrad(a, b, slices=slices)
         torch.cuda.synchronize()
     finally:

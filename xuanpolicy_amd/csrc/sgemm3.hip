@@ -776,8 +776,11 @@ XPA_API int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ld
     int64_t per = (rows + slices - 1) / slices;
     per = (per + kWgKC - 1) / kWgKC * kWgKC;
     const dim3 grid((unsigned)(slices * (m / kWgM))), block(512);
-    if ((g_s3_probe & 16) && lda % 4 == 0 && ldb % 4 == 0 && ((reinterpret_cast<uintptr_t>(a) |
-                                                                 reinterpret_cast<uintptr_t>(b)) & 15) == 0) {
+    // the production form is K41V (float4 staging; rows 16-B aligned); probe bits select the others: 8 K41W,
+    // 32 or any of 1 / 2 / 4 the register-staged K41 (and its probes)
+    const bool vec_ok = lda % 4 == 0 && ldb % 4 == 0 &&
+                        ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
+    if (vec_ok && (g_s3_probe & (1 | 2 | 4 | 8 | 32)) == 0) {
         s3_wgrad_v_kernel<<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out);   // K41V
         return xpa_launch_status();
     }

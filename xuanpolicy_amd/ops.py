@@ -563,8 +563,8 @@ class ColsumQueue:
 K16W_ENABLED = False  # fused_heads' gemm form: K16W (xpa_head_gemm_ws_*) where it applies, else K16
 # The update's hidden-layer GEMMs on the bf16 matrix cores by the three-way split (K16S heads, K40 dX, K41 dW):
 # the f32 GEMM's accuracy, not the f32 MFMA's bits.  Read when a learner's update is built / captured.
-S3_GEMMS = False
-S3_HEADS = "s3"   # with S3_GEMMS: "s3" K16S (both fragments split in the k loop), "s3p" K16P (Wh's planes split once)
+S3_GEMMS = True
+S3_HEADS = "s3p"   # with S3_GEMMS: "s3" K16S (both fragments split in the k loop), "s3p" K16P (Wh's planes split once)
 
 
 def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, w_critic, b_critic, act_critic,
