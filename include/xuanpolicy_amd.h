@@ -580,6 +580,9 @@ int xpa_head_gemm_trunk_critic(int act, int64_t batch, int64_t hidden, const flo
 int64_t xpa_s3_split_bytes(int64_t k, int64_t n);
 int xpa_s3_probe(int mask); /* diagnostics: parts of K40 / K41 switched off (tools/s3_ab.py --probe); 0 = production */
 int xpa_s3_split_b(const float *b, int64_t k, int64_t n, int64_t sk, int64_t sn, void *out, xpa_stream_t stream);
+/* n_mat <= 4 splits (n = 256 each) in one launch: the arrays hold each matrix's pointer, k, strides and output */
+int xpa_s3_split_batch(int n_mat, const float *const *b, const int64_t *k, const int64_t *sk, const int64_t *sn,
+                       void *const *out, xpa_stream_t stream);
 int xpa_s3_gemm(const float *a, int64_t lda, const void *b_split, float *c, int64_t ldc, int64_t m, int64_t k, int64_t n,
                 xpa_stream_t stream);
 /* K41 — the weight gradient dW = a^T b over the batch on the same split (a [rows, m] = dz, row stride lda; b [rows, 256]

@@ -198,3 +198,17 @@ def test_wgrad_vector_staged_matches_f32_gemm_error(rows, m, lda_pad, slices):
     err = (got - ref).abs().max().item()
     err_f32 = (native.double() - ref).abs().max().item()
     assert err <= 2 * err_f32 + 2 ** -24 * scale, (err, err_f32, scale)
+
+
+def test_split_batch_equals_single_splits():
+    """xpa_s3_split_batch (the update's one split launch: Wh_pair, Wh_actor^T, Wh_critic^T) == xpa_s3_split_b each."""
+    from xuanpolicy_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(3)
+    mats = [torch.randn(512, 256, device=DEV, generator=g), torch.randn(256, 256, device=DEV, generator=g).t(),
+            _wide((256, 256), g).t(), torch.randn(32, 256, device=DEV, generator=g)]
+    outs = [torch.empty(int(ops.lib().xpa_s3_split_bytes(m.shape[0], 256)), dtype=torch.uint8, device=DEV)
+            for m in mats]
+    ops.s3_split_batch(list(zip(mats, outs)))
+    torch.cuda.synchronize()
+    for m, o in zip(mats, outs):
+        assert torch.equal(o, ops.s3_split(m))

@@ -225,6 +225,7 @@ SIGNATURES = {
     "xpa_s3_probe": (ctypes.c_int, [ctypes.c_int]),
     "xpa_s3_split_bytes": (c_i64, [c_i64, c_i64]),
     "xpa_s3_split_b": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
+    "xpa_s3_split_batch": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p, c_p]),
     "xpa_s3_gemm": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
     "xpa_s3_wgrad_num_slices": (c_i64, [c_i64, c_i64]),
     "xpa_s3_wgrad": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),

@@ -88,6 +88,38 @@ __global__ __launch_bounds__(256) void split_b_kernel(const float *__restrict__ 
     o[16 * 64] = pl;
 }
 
+// up to 4 matrices split in one launch (the update's three per step: Wh_pair for dX, Wh_actor^T and Wh_critic^T for
+// K16P): block y = matrix
+struct SplitBatch {
+    const float *b[4];
+    int64_t k[4], sk[4], sn[4];
+    __bf16 *out[4];
+};
+__global__ __launch_bounds__(256) void split_batch_kernel(SplitBatch sb) {
+    const int i = blockIdx.y;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t K = sb.k[i];
+    if (t >= (K / kKC) * kN * 2) return;
+    const float *b = sb.b[i];
+    const int64_t sk = sb.sk[i], sn = sb.sn[i];
+    const int h = (int)(t & 1);
+    const int n = (int)((t >> 1) % kN);
+    const int64_t c = (t >> 1) / kN;
+    bf16x8 ph, pm, pl;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        __bf16 a0, a1, a2;
+        xpa_split3(b[(c * kKC + kmap(h, j)) * sk + (int64_t)n * sn], a0, a1, a2);
+        ph[j] = a0;
+        pm[j] = a1;
+        pl[j] = a2;
+    }
+    bf16x8 *o = reinterpret_cast<bf16x8 *>(sb.out[i]) + c * (3 * 8 * 64) + (n >> 5) * 64 + h * 32 + (n & 31);
+    o[0] = ph;
+    o[8 * 64] = pm;
+    o[16 * 64] = pl;
+}
+
 // ---- the GEMM ---------------------------------------------------------------------------------------------
 // chunk c's DMAs of wave w into the stage at LDS byte address st: A rows r0 + 32 w .. + 31 (two 16-row
 // instructions, lane = (row, 16-B slot), slot p of row r holding k quad p ^ ((r >> 2) & 3)), then B's 1-KiB pieces
@@ -804,6 +836,26 @@ XPA_API int xpa_s3_probe(int mask) {
 
 XPA_API int64_t xpa_s3_split_bytes(int64_t k, int64_t n) {
     return k * n * 3 * 2;
+}
+
+// n_mat <= 4 matrices B_i [k_i, 256] (element (r, c) at b_i[r sk_i + c sn_i]) split into out_i in one launch
+XPA_API int xpa_s3_split_batch(int n_mat, const float *const *b, const int64_t *k, const int64_t *sk, const int64_t *sn,
+                               void *const *out, xpa_stream_t stream) {
+    if (n_mat < 1 || n_mat > 4 || !b || !k || !sk || !sn || !out) return (int)hipErrorInvalidValue;
+    SplitBatch sb{};
+    int64_t kmax = 0;
+    for (int i = 0; i < n_mat; ++i) {
+        if (!b[i] || !out[i] || k[i] <= 0 || k[i] % kKC) return (int)hipErrorInvalidValue;
+        sb.b[i] = b[i];
+        sb.k[i] = k[i];
+        sb.sk[i] = sk[i];
+        sb.sn[i] = sn[i];
+        sb.out[i] = static_cast<__bf16 *>(out[i]);
+        kmax = k[i] > kmax ? k[i] : kmax;
+    }
+    const int64_t total = (kmax / kKC) * kN * 2;
+    split_batch_kernel<<<dim3((unsigned)((total + 255) / 256), (unsigned)n_mat), dim3(256), 0, stream>>>(sb);
+    return xpa_launch_status();
 }
 
 XPA_API int xpa_s3_split_b(const float *b, int64_t k, int64_t n, int64_t sk, int64_t sn, void *out,

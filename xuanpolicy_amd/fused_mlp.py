@@ -345,10 +345,17 @@ class FusedActorCritic:
         if self._hws is None or self._hws.batch != B:
             self._hws = ops.HeadWorkspace(B, K, s.device, paired=paired)
         gemm = wh_split = None
+        splits = []   # (matrix, name): every split this update needs, one launch (xpa_s3_split_batch)
         if z_a is None:   # K16
             gemm = (s, (lin_ah.weight, lin_ah.bias), (lin_ch.weight, lin_ch.bias))
             if ops.S3_GEMMS and ops.S3_HEADS == "s3p" and not ops.K16W_ENABLED:   # K16P: Wh^T's planes, once per update
-                wh_split = (self._split(lin_ah.weight.t(), "s3p_a"), self._split(lin_ch.weight.t(), "s3p_c"))
+                splits += [(lin_ah.weight.t(), "s3p_a"), (lin_ch.weight.t(), "s3p_c")]
+        if paired and len(self.rep) > 0 and self._dx_split_ok(self.pair[0]):
+            splits.append((self.pair[0], "dx"))
+        if splits:
+            bufs = self._split_many(splits)
+            if splits[0][1] == "s3p_a":
+                wh_split = (bufs[0], bufs[1])
         grads = {"w_actor": lin_ao.weight.grad, "b_actor": lin_ao.bias.grad, "bh_actor": lin_ah.bias.grad,
                  "w_critic": lin_co.weight.grad, "b_critic": lin_co.bias.grad, "bh_critic": lin_ch.bias.grad}
         if self.logstd is not None:
@@ -429,23 +436,31 @@ class FusedActorCritic:
                                         ops._p(g) if code else None, ops._p(part), s), "xpa_act_bwd_colsum")
         _lib.check(L.xpa_colsum_finalize(ops._p(part), part.shape[0], cols, ops._p(out), s), "xpa_colsum_finalize")
 
-    def _split(self, b, name):
-        """s3_split of b [k, 256] into a buffer kept per name (graph-capture safe: allocated on first use)."""
-        k = b.shape[0]
+    def _split_buf(self, k, name, device):
         key = ("s3split", name, k)
         buf = self._partials.get(key)
-        if buf is None:
-            buf = torch.empty(int(ops.lib().xpa_s3_split_bytes(k, 256)), dtype=torch.uint8, device=b.device)
+        if buf is None:   # graph-capture safe: allocated on first (eager) use
+            buf = torch.empty(int(ops.lib().xpa_s3_split_bytes(k, 256)), dtype=torch.uint8, device=device)
             self._partials[key] = buf
-        return ops.s3_split(b, out=buf)
+        return buf
+
+    def _split_many(self, items):
+        """The bf16 planes of every (matrix [k, 256], name) in one launch, into buffers kept per name."""
+        bufs = [self._split_buf(b.shape[0], name, b.device) for b, name in items]
+        ops.s3_split_batch([(b, o) for (b, _), o in zip(items, bufs)])
+        return bufs
+
+    @staticmethod
+    def _dx_split_ok(w):
+        return ops.S3_GEMMS and w.shape[1] == 256 and w.shape[0] % 16 == 0
 
     def _dx(self, dz, w):
         """dX = dz w (w [k, n_in]): K40 on the bf16 matrix cores by the three-way split when ops.S3_GEMMS and the shape
-        fits (n_in = 256, k % 16 == 0), else the f32 GEMM."""
+        fits (n_in = 256, k % 16 == 0; w's planes were written by this update's split launch), else the f32 GEMM."""
         k, n_in = w.shape
-        if not (ops.S3_GEMMS and n_in == 256 and k % 16 == 0 and dz.stride(1) == 1):
+        if not (self._dx_split_ok(w) and dz.stride(1) == 1):
             return torch.mm(dz, w)
-        return ops.s3_gemm(dz, self._split(w, "dx"), k)
+        return ops.s3_gemm(dz, self._split_buf(k, "dx", dz.device), k)
 
     def _weight_grad(self, dz, x, out, queue=None):
         """dW = dz^T x.  Split-K (a batched GEMM over slices of the batch) when the GEMM alone would not

@@ -160,6 +160,31 @@ def s3_split(b, out=None):
     return out
 
 
+_SPLIT_PLANS = {}
+
+
+def s3_split_batch(pairs):
+    """K40's split of up to 4 matrices in one launch: pairs = [(b [k, 256] any strides, out uint8 buffer), ...]."""
+    L = lib()
+    key = tuple((b.data_ptr(), b.shape[0], b.stride(0), b.stride(1), o.data_ptr()) for b, o in pairs)
+    plan = _SPLIT_PLANS.get(key)
+    if plan is None:
+        for b, o in pairs:
+            _req(b, "b", torch.float32, contiguous=False)
+            if b.shape[1] != 256:
+                raise ValueError("s3_split_batch: b must be [k, 256]")
+            _req(o, "out", torch.uint8, (int(L.xpa_s3_split_bytes(b.shape[0], 256)),))
+        n = len(pairs)
+        arrs = ((ctypes.c_void_p * n)(*[k[0] for k in key]), (ctypes.c_int64 * n)(*[k[1] for k in key]),
+                (ctypes.c_int64 * n)(*[k[2] for k in key]), (ctypes.c_int64 * n)(*[k[3] for k in key]),
+                (ctypes.c_void_p * n)(*[k[4] for k in key]))
+        if len(_SPLIT_PLANS) > 256:
+            _SPLIT_PLANS.clear()
+        plan = _SPLIT_PLANS[key] = (n, arrs, [ctypes.cast(a, ctypes.c_void_p) for a in arrs])
+    n, _keep, args = plan
+    _lib.check(L.xpa_s3_split_batch(n, *args, _stream(pairs[0][0].device)), "xpa_s3_split_batch")
+
+
 def s3_gemm(a, b_split, k, out=None):
     """K40: out [m, 256] = a [m, k] . B for B split by s3_split (f32 accuracy on the bf16 matrix cores)."""
     _req(a, "a", torch.float32, contiguous=False)
