@@ -299,8 +299,14 @@ constexpr int kMaxSegs = 16;
 constexpr int kWideTile = kColTile * kColGroups;
 constexpr int kWideMaxG = 32;
 
+// Segments with 32 < G <= 256 (K41's 64 weight-gradient slices over C = 131 072): 256-column tiles, 4 row groups of
+// 256 threads (rows grp, grp + 4, ...; 16 loads in flight), the groups added in order in f64 — r04: the 64-column
+// tiles of colsum_tile took 32 us for K41's 32 MiB.
+constexpr int kMidTile = 256;
+constexpr int kMidMaxG = 256;
 __host__ __device__ inline int64_t seg_tiles(int64_t G, int64_t C) {
-    return G <= kWideMaxG ? (C + kWideTile - 1) / kWideTile : (C + kColTile - 1) / kColTile;
+    return G <= kWideMaxG ? (C + kWideTile - 1) / kWideTile
+                          : G <= kMidMaxG ? (C + kMidTile - 1) / kMidTile : (C + kColTile - 1) / kColTile;
 }
 
 struct ColsumBatch {
@@ -355,6 +361,40 @@ __device__ __forceinline__ void colsum_batch_tile(const ColsumBatch &b, int tile
                 for (int w = 0; w < kWideTile / 64; ++w) t += s_red[0][w];
                 xpa_store_agent(sq, t);
             }
+        }
+    } else if (b.G[sg] <= kMidMaxG) {
+        static_assert(kColGroups * kColTile == 4 * kMidTile, "the mid path reuses s_red as [4][256]");
+        auto s4 = reinterpret_cast<double(*)[kMidTile]>(s_red);
+        const int64_t G = b.G[sg];
+        const int C = b.C[sg];
+        const int grp = threadIdx.x >> 8, lc = threadIdx.x & (kMidTile - 1);
+        const int c = (tile - b.tile0[sg]) * kMidTile + lc;
+        const float *part = b.part[sg];
+        double acc = 0.0;
+        if (c < C) {
+            int64_t k = grp;
+            for (; k + 15 * 4 < G; k += 16 * 4) {  // 16 loads in flight, added in row order
+                float a[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) a[u] = part[(k + 4 * u) * C + c];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) acc += (double)a[u];
+            }
+            for (; k < G; k += 4) acc += (double)part[k * C + c];
+        }
+        s4[grp][lc] = acc;
+        __syncthreads();
+        float o = 0.f;
+        if (grp == 0 && c < C) {
+            o = (float)(((s4[0][lc] + s4[1][lc]) + s4[2][lc]) + s4[3][lc]);
+            b.out[sg][c] = o;
+        }
+        if (sq) {
+            __syncthreads();   // s4 read by group 0: its slots reused for the wave sums
+            const double q = xpa_wave_sum((double)o * (double)o);
+            if ((threadIdx.x & 63) == 0 && grp == 0) s4[1][threadIdx.x >> 6] = q;
+            __syncthreads();
+            if (threadIdx.x == 0) xpa_store_agent(sq, ((s4[1][0] + s4[1][1]) + s4[1][2]) + s4[1][3]);
         }
     } else {
         colsum_tile(b.part[sg], b.G[sg], b.C[sg], (tile - b.tile0[sg]) * kColTile, b.out[sg], s_red, sq);
