@@ -590,6 +590,14 @@ int xpa_s3_gemm(const float *a, int64_t lda, const void *b_split, float *c, int6
  * ceil(rows / slices) rows (rounded up to 32), summed by the caller — the learner's fixed-order f64 finalize, as for
  * the batched f32 GEMM it replaces.  xpa_s3_wgrad_num_slices: the slice count that fills the chip (0: bad shape). */
 int64_t xpa_s3_wgrad_num_slices(int64_t rows, int64_t m);
+/* K42 — xpa_s3_gemm's g = dz . B kept in registers and the first representation layer's backward (K13's,
+ * xpa_thin_linear_act_bwd) done on it: dz1 = g * act'(h) (h [rows, 256] = the layer's output, act as K13), per-block
+ * partials of db1 [G, 256] and dW1 [G, 256 * d_in] (x [rows, d_in] = the layer's input rows, d_in <= 32);
+ * G = xpa_s3_gemm_trunk_bwd_num_partials(rows).  g itself is never written. */
+int64_t xpa_s3_gemm_trunk_bwd_num_partials(int64_t rows);
+int xpa_s3_gemm_trunk_bwd(const float *dz, int64_t ldz, const void *b_split, int64_t k, const float *h, int64_t ldh,
+                          const float *x, int64_t ldx, int64_t rows, int64_t d_in, int act, float slope,
+                          float *partial_dw, float *partial_db, xpa_stream_t stream);
 int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ldb, int64_t rows, int64_t m, int64_t n,
                  int64_t slices, float *out, xpa_stream_t stream);
 

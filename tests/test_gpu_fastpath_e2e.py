@@ -104,6 +104,7 @@ def test_fast_path_iteration_with_split_gemms_matches_oracle(agent_name, discret
     assert any(k[0] == "s3split" for k in fm._partials if isinstance(k, tuple)), "K40 not used"
     if heads == "s3p":
         assert any(k[:2] == ("s3split", "s3p_a") for k in fm._partials if isinstance(k, tuple)), "K16P not used"
+    assert any(k[0] == "k42" for k in fm._partials if isinstance(k, tuple)), "K42 not used"
     replay_last_step_iteration(agent, D, A, [H], discrete, "ppo" if agent_name == "PPO_Clip" else "a2c", 0.01, 2, 4,
                                expect_mid_truncations=not discrete)
 

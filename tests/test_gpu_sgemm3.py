@@ -212,3 +212,36 @@ def test_split_batch_equals_single_splits():
     torch.cuda.synchronize()
     for m, o in zip(mats, outs):
         assert torch.equal(o, ops.s3_split(m))
+
+
+@pytest.mark.parametrize("rows,din,act", [(65536, 17, 1), (4133, 17, 2), (300, 5, 0), (77, 32, 1)])
+def test_gemm_trunk_bwd_matches_f64(rows, din, act):
+    """K42 (the dX GEMM with the first layer's backward in its epilogue) against an f64 restatement of K40 + K13's
+    backward: g = dz W, dz1 = g act'(h) (LeakyReLU 0.01 / tanh / identity on the layer's output h), dW1 = dz1^T x,
+    db1 = sum dz1 — the partial rows summed, within 2e-5 of the output scale (f32 GEMM + f32 partial sums)."""
+    from xuanpolicy_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(rows + din)
+    K = 512
+    dz = torch.randn(rows, K, device=DEV, generator=g) * 1e-3
+    w = torch.randn(K, 256, device=DEV, generator=g) / 16
+    x = torch.randn(rows, din, device=DEV, generator=g)
+    pre = torch.randn(rows, 256, device=DEV, generator=g)
+    slope = 0.01
+    h = {0: pre, 1: torch.nn.functional.leaky_relu(pre, slope), 2: torch.tanh(pre)}[act]
+    h = h.clone()
+    h[::7, ::5] = 0.0   # exact zeros: the LeakyReLU branch h > 0 is false there
+    pdw, pdb = ops.s3_gemm_trunk_bwd(dz, ops.s3_split(w), K, h, x, act, slope)
+    torch.cuda.synchronize()
+    d = lambda t: t.double()   # noqa: E731
+    gg = d(dz) @ d(w)
+    gp = {0: lambda hh: torch.ones_like(hh), 1: lambda hh: torch.where(hh > 0, 1.0, slope),
+          2: lambda hh: 1.0 - hh * hh}[act](d(h))
+    dz1 = gg * gp
+    ref_dw = (dz1.t() @ d(x)).reshape(-1)
+    ref_db = dz1.sum(0)
+    got_dw, got_db = pdw.double().sum(0), pdb.double().sum(0)
+    assert torch.isfinite(pdw).all() and torch.isfinite(pdb).all()
+    for got, ref, what in ((got_dw, ref_dw, "dW1"), (got_db, ref_db, "db1")):
+        scale = ref.abs().max().item()
+        err = (got - ref).abs().max().item()
+        assert err <= 2e-5 * scale, (what, err, scale)

@@ -228,6 +228,9 @@ SIGNATURES = {
     "xpa_s3_split_batch": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p, c_p]),
     "xpa_s3_gemm": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
     "xpa_s3_wgrad_num_slices": (c_i64, [c_i64, c_i64]),
+    "xpa_s3_gemm_trunk_bwd_num_partials": (c_i64, [c_i64]),
+    "xpa_s3_gemm_trunk_bwd": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64, ctypes.c_int,
+                                             c_f32, c_p, c_p, c_p]),
     "xpa_s3_wgrad": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
     "xpa_grad_norm_num_partials": (c_i64, [c_i64]),
     "xpa_clip_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_p, c_f32, c_f32, c_f32, c_f32, c_f32, c_i64, c_p,

@@ -365,6 +365,126 @@ __global__ __launch_bounds__(512, 1) void s3_gemm_ws_kernel(const float *__restr
     }
 }
 
+// ---- K42: K40's dX GEMM with the representation's first layer backward in its epilogue ---------------------------
+// g = dz . Wh_pair stays in the accumulators: dz1 = g * act'(h) (h = the layer's output, K13's act_g), db1 = the column
+// sums of dz1 and dW1 = dz1^T x (x = the layer's input rows, d_in <= 32) per block, as K13's backward (thin.hip) does
+// from a g in HBM — g is never stored (64 MiB less written and read per C2 update) and K13's backward launch is gone.
+// dW1's product runs on the same split: the accumulator tile of a wave (column on the lane, rows in the registers) is
+// the B operand of Y = x^T dz1 as it is (registers 8s .. 8s + 7 = the 8 k of k step s, cdna_hip_programming.md §3),
+// x^T's fragment holds the same rows.  Per column block the 8 waves' Y [d_in x 32] meet in LDS and are added in wave
+// order; one partial row per block (xpa_s3_gemm_trunk_bwd_num_partials), finalized by the caller's f64 column sums.
+template <int ACT>
+__device__ __forceinline__ float tb_act_g(float h, float slope) {  // thin.hip act_g
+    if (ACT == 1) return h > 0.f ? 1.f : slope;
+    if (ACT == 2) return 1.0f - h * h;
+    return 1.f;
+}
+
+template <int ACT>
+__global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *__restrict__ a, int64_t lda,
+                                                                   const __bf16 *__restrict__ bs, int64_t M,
+                                                                   int nchunks, const float *__restrict__ hmat,
+                                                                   int64_t ldh, const float *__restrict__ x,
+                                                                   int64_t ldx, int din, float slope,
+                                                                   float *__restrict__ p_dw, float *__restrict__ p_db) {
+    using G = S3Geom<8>;
+    __shared__ __attribute__((aligned(16))) char lds[3 * G::kStage];
+    const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int64_t r0 = (int64_t)blockIdx.x * G::kRows;
+    f32x16 acc[8];
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[cb][r] = 0.f;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+        if (d < nchunks) issue<8>(base + d * G::kStage, a, lda, bs, r0, M, d, lane, wave);
+#pragma unroll 1
+    for (int ch = 0; ch < nchunks; ++ch) {
+        if (ch + 1 < nchunks) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G::kDma) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (ch + 2 < nchunks) issue<8>(base + ((ch + 2) % 3) * G::kStage, a, lda, bs, r0, M, ch + 2, lane, wave);
+        chunk<8, 0>(lds + (ch % 3) * G::kStage, acc, lane, wave);
+    }
+    __syncthreads();   // every wave done with the ring: the epilogue reuses its LDS
+    // ---- dz1 = g * act'(h) in place (rows past M: 0)
+    const int hh = lane >> 5, col = lane & 31;
+    const int64_t wrow = r0 + wave * 32;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t row = wrow + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const bool ok = row < M;
+        const float *hrow = hmat + (ok ? row : 0) * ldh + col;
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb) {
+            const float hv = hrow[cb * 32];
+            acc[cb][r] = ok ? acc[cb][r] * tb_act_g<ACT>(hv, slope) : 0.f;
+        }
+    }
+    // ---- x^T's fragments for the wave's 32 rows: lane (feature i, half hh), k step s element j = row rho(8 s + j, hh)
+    bf16x8 xh[2], xm[2], xl[2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int r = 8 * st + j;
+            const int64_t row = wrow + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const bool ok = row < M && col < din;
+            const float xv = x[(row < M ? row : 0) * ldx + (col < din ? col : 0)];
+            v[j] = ok ? xv : 0.f;
+        }
+        xpa_split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), xh[st], xm[st], xl[st]);
+    }
+    float *s_y = reinterpret_cast<float *>(lds);                 // [8 waves][32 features][32 columns]
+    float *s_db = reinterpret_cast<float *>(lds) + 8 * 32 * 32;  // [8 waves][256]
+#pragma unroll 1
+    for (int cb = 0; cb < 8; ++cb) {
+        // db1: the wave's 32 rows of this column block (16 per lane half, then the two halves)
+        float cs = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cs += acc[cb][r];
+        cs += __shfl_xor(cs, 32, 64);
+        if (hh == 0) s_db[wave * 256 + cb * 32 + col] = cs;
+        // Y = x^T dz1 over the wave's rows: two k steps of 16 rows
+        f32x16 y;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) y[r] = 0.f;
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = acc[cb][8 * st + j];
+            bf16x8 gh, gm, gl;
+            xpa_split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), gh, gm, gl);
+            y = xpa_mfma_s3(xh[st], xm[st], xl[st], gh, gm, gl, y);
+        }
+        // Y's rows are the features: lane (column, hh) holds features rho(r, hh)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int f = (r & 3) + 8 * (r >> 2) + 4 * hh;
+            s_y[(wave * 32 + f) * 32 + col] = y[r];
+        }
+        __syncthreads();
+        for (int e = t; e < din * 32; e += 512) {   // (feature, column) pairs: the 8 waves in order
+            const int f = e >> 5, c = e & 31;
+            float sum = s_y[f * 32 + c];
+#pragma unroll
+            for (int w = 1; w < 8; ++w) sum += s_y[(w * 32 + f) * 32 + c];
+            p_dw[(int64_t)blockIdx.x * (256 * din) + (cb * 32 + c) * din + f] = sum;
+        }
+        __syncthreads();   // s_y reused by the next column block
+    }
+    if (t < 256) {
+        float sum = s_db[t];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) sum += s_db[w * 256 + t];
+        p_db[(int64_t)blockIdx.x * 256 + t] = sum;
+    }
+}
+
 // ---- K41: weight gradients dW = A^T B over the batch (K = rows), split-K -----------------------------------
 // out[s] [M, 256] = A[rows of slice s]^T . B[rows of slice s], A [rows, M] (dz), B [rows, 256] (the layer input);
 // the slices are summed by the caller (the learner's fixed-order f64 column-sum finalize), as the batched f32 GEMM
@@ -864,6 +984,31 @@ XPA_API int xpa_s3_split_b(const float *b, int64_t k, int64_t n, int64_t sk, int
     const int64_t total = (k / kKC) * kN * 2;
     split_b_kernel<<<dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream>>>(b, k, sk, sn,
                                                                                     static_cast<__bf16 *>(out));
+    return xpa_launch_status();
+}
+
+XPA_API int64_t xpa_s3_gemm_trunk_bwd_num_partials(int64_t rows) {
+    return rows > 0 ? (rows + 255) / 256 : 0;
+}
+
+// K42: the dX GEMM g = dz . B (B split, k % 16 == 0, n = 256) and the first representation layer's backward on it:
+// partial_dw [G, 256 * d_in] (W1's layout [256][d_in]) and partial_db [G, 256], G = xpa_s3_gemm_trunk_bwd_num_partials
+XPA_API int xpa_s3_gemm_trunk_bwd(const float *dz, int64_t ldz, const void *b_split, int64_t k, const float *h,
+                                  int64_t ldh, const float *x, int64_t ldx, int64_t rows, int64_t d_in, int act,
+                                  float slope, float *partial_dw, float *partial_db, xpa_stream_t stream) {
+    if (!dz || !b_split || !h || !x || !partial_dw || !partial_db || rows <= 0 || k <= 0 || k % kKC != 0 ||
+        ldz < k || (ldz & 3) || (reinterpret_cast<uintptr_t>(dz) & 15) || ldh < kN || d_in < 1 || d_in > 32 ||
+        ldx < d_in || act < 0 || act > 2 || k / kKC > (1 << 20))
+        return (int)hipErrorInvalidValue;
+    const dim3 grid((unsigned)xpa_s3_gemm_trunk_bwd_num_partials(rows)), block(512);
+    const __bf16 *bs = static_cast<const __bf16 *>(b_split);
+    const int nch = (int)(k / kKC);
+#define XPA_TB(A_) s3_gemm_trunk_bwd_kernel<A_><<<grid, block, 0, stream>>>(dz, ldz, bs, rows, nch, h, ldh, x, ldx, \
+                                                                          (int)d_in, slope, partial_dw, partial_db)
+    if (act == 0) XPA_TB(0);
+    else if (act == 1) XPA_TB(1);
+    else XPA_TB(2);
+#undef XPA_TB
     return xpa_launch_status();
 }
 

@@ -382,7 +382,7 @@ class FusedActorCritic:
                 self.early_grad_sync(self.pair[2])
             else:
                 self._weight_grad(dz, s, self.pair[2], queue=self._cq)
-            if have_rep:
+            if have_rep and not self._trunk_bwd_fused(dz, x, rep_outs):
                 self._chain_backward(self.rep, [x] + rep_outs[:-1], rep_outs, self._dx(dz, self.pair[0]),
                                      need_dx=False, thin_first=self.thin0)
             self._flush_with_norm(s.device)   # every deferred column-sum finalize in one launch
@@ -449,6 +449,35 @@ class FusedActorCritic:
         bufs = [self._split_buf(b.shape[0], name, b.device) for b, name in items]
         ops.s3_split_batch([(b, o) for (b, _), o in zip(items, bufs)])
         return bufs
+
+    FUSE_TRUNK_BWD = True   # K42 where it applies (ops.S3_GEMMS, one thin representation layer)
+
+    def _trunk_bwd_fused(self, dz, x, rep_outs):
+        """K42: the dX GEMM and the one representation layer's backward (K13's) in one launch, g never stored.  Returns
+        False (nothing done) when it does not apply: not the split GEMMs, more than one representation layer, no K13
+        first layer, d_in > 32, or rows not given as the gathered minibatch."""
+        if not (self.FUSE_TRUNK_BWD and self._dx_split_ok(self.pair[0]) and len(self.rep) == 1 and self.thin0
+                and dz.stride(1) == 1):
+            return False
+        lin, code, slope = self.rep[0]
+        xr = x.gathered if isinstance(x, Rows) else x
+        if not isinstance(xr, torch.Tensor) or xr.dim() != 2 or xr.stride(1) != 1 or lin.in_features > 32:
+            return False
+        h = rep_outs[0]
+        if not isinstance(h, torch.Tensor) or h.stride(1) != 1 or h.shape[1] != 256:
+            return False
+        rows = dz.shape[0]
+        key = ("k42", rows, lin.in_features)
+        ws = self._partials.get(key)
+        if ws is None:
+            G = int(ops.lib().xpa_s3_gemm_trunk_bwd_num_partials(rows))
+            ws = (torch.empty((G, 256 * lin.in_features), device=dz.device), torch.empty((G, 256), device=dz.device))
+            self._partials[key] = ws
+        k = self.pair[0].shape[0]
+        ops.s3_gemm_trunk_bwd(dz, self._split_buf(k, "dx", dz.device), k, h, xr, code, slope, ws[0], ws[1])
+        self._cq.add(ws[0], lin.weight.grad)
+        self._cq.add(ws[1], lin.bias.grad)
+        return True
 
     @staticmethod
     def _dx_split_ok(w):

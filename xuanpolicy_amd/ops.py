@@ -199,6 +199,29 @@ def s3_gemm(a, b_split, k, out=None):
     return out
 
 
+def s3_gemm_trunk_bwd(dz, b_split, k, h, x, act, slope, partial_dw=None, partial_db=None):
+    """K42: g = dz [rows, k] . B (split) kept in registers; the first representation layer's backward on it (dz1 =
+    g * act'(h), its bias / weight gradients) as per-block partials ([G, 256 * d_in], [G, 256]); g is not stored."""
+    L = lib()
+    _req(dz, "dz", torch.float32, contiguous=False)
+    ldz = _row_stride(dz, "dz", k)
+    rows = dz.shape[0]
+    ldh = _row_stride(h, "h", 256)
+    d_in = x.shape[1]
+    ldx = _row_stride(x, "x", d_in)
+    G = int(L.xpa_s3_gemm_trunk_bwd_num_partials(rows))
+    if partial_dw is None:
+        partial_dw = torch.empty(G, 256 * d_in, dtype=torch.float32, device=dz.device)
+    if partial_db is None:
+        partial_db = torch.empty(G, 256, dtype=torch.float32, device=dz.device)
+    _req(partial_dw, "partial_dw", torch.float32, (G, 256 * d_in))
+    _req(partial_db, "partial_db", torch.float32, (G, 256))
+    _lib.check(L.xpa_s3_gemm_trunk_bwd(_p(dz), ldz, _p(b_split), k, _p(h), ldh, _p(x), ldx, rows, d_in, int(act),
+                                       float(slope), _p(partial_dw), _p(partial_db), _stream(dz.device)),
+               "xpa_s3_gemm_trunk_bwd")
+    return partial_dw, partial_db
+
+
 def s3_wgrad_slices(rows, m):
     return int(lib().xpa_s3_wgrad_num_slices(rows, m))
 
