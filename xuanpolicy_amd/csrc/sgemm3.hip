@@ -440,7 +440,7 @@ __global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *
     }
     float *s_y = reinterpret_cast<float *>(lds);                 // [8 waves][32 features][32 columns]
     float *s_db = reinterpret_cast<float *>(lds) + 8 * 32 * 32;  // [8 waves][256]
-#pragma unroll 1
+#pragma unroll   // unrolled: acc[cb] with a run-time cb put the accumulators in scratch (576 B, 2x the launch)
     for (int cb = 0; cb < 8; ++cb) {
         // db1: the wave's 32 rows of this column block (16 per lane half, then the two halves)
         float cs = 0.f;
