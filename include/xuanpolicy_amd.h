@@ -600,6 +600,33 @@ int xpa_s3_gemm_trunk_bwd(const float *dz, int64_t ldz, const void *b_split, int
                           float *partial_dw, float *partial_db, xpa_stream_t stream);
 int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ldb, int64_t rows, int64_t m, int64_t n,
                  int64_t slices, float *out, xpa_stream_t stream);
+/* K42S (r04): xpa_s3_gemm_trunk_bwd with act' taken from h's sign bits (h_sign: 32 bytes per row, byte b bit j =
+ * h[row, 32 j + b] > 0, as xpa_head_gemm_s3r_actor writes them) instead of h; act 0 (identity) or 1 (LeakyReLU /
+ * ReLU).  The same outputs bit for bit; 32 B instead of 1 KiB read per row. */
+int xpa_s3_gemm_trunk_bwd_sign(const float *dz, int64_t ldz, const void *b_split, int64_t k, const unsigned *h_sign,
+                               const float *x, int64_t ldx, int64_t rows, int64_t d_in, int act, float slope,
+                               float *partial_dw, float *partial_db, xpa_stream_t stream);
+/* K16R (r04): xpa_head_gemm_s3p_actor / _critic (w_hidden = the split buffer of Wh^T) with the heads' input h formed
+ * inside from the gathered minibatch rows (the representation's one thin layer: x_rows [batch, d_in <= 20], w_in
+ * [256, d_in], b_in, the heads' activation at slope_in) — xpa_thin_linear_act_fwd's h bit for bit, so the update
+ * reads no h for the heads (ppoclip_learner.py:31-33 policy(obs) forward, layers.py:8-24 mlp_block).  The actor
+ * writes h (h_out, for the weight gradient) and, when h_sign is given, its sign bits (xpa_s3_gemm_trunk_bwd_sign).
+ * act_dim <= 8. */
+int xpa_head_gemm_s3r_actor(int algo, int dist, int act, int64_t batch, int64_t act_dim, int64_t hidden,
+                            const float *x_rows, int64_t ld_rows, int64_t d_in, const float *w_in, const float *b_in,
+                            float slope_in, float *h_out, int64_t ld_h, unsigned *h_sign, const void *w_hidden,
+                            const float *b_hidden, int64_t ld_dz, const float *w, const float *b, float slope,
+                            const float *logstd, const int64_t *idx, int64_t n_rows, const float *act_buf,
+                            const float *old_logp, const float *adv, const double *adv_partials,
+                            int64_t n_adv_partials, float clip_range, float ent_coef, float *dz, float *partial_dw,
+                            float *partial_db_hidden, float *partial_db_out, float *loss_partials, int64_t loss_width,
+                            xpa_stream_t stream);
+int xpa_head_gemm_s3r_critic(int act, int64_t batch, int64_t hidden, const float *x_rows, int64_t ld_rows,
+                             int64_t d_in, const float *w_in, const float *b_in, float slope_in, const void *w_hidden,
+                             const float *b_hidden, int64_t ld_dz, const float *w, const float *b, float slope,
+                             const int64_t *idx, int64_t n_rows, const float *ret, float vf_coef, float *dz,
+                             float *partial_dw, float *partial_db_hidden, float *partial_db_out, float *loss_partials,
+                             int64_t loss_width, xpa_stream_t stream);
 
 /* K6 — prioritized replay (PerOffPolicyBuffer, memory_tools.py:369-492; Sum/MinSegmentTree,
  * segtree_tool.py:4-86) with f64 trees on device: one [n_envs, 2*capacity] array per tree (node 1 =

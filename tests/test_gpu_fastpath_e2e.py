@@ -104,6 +104,7 @@ def test_fast_path_iteration_with_split_gemms_matches_oracle(agent_name, discret
     assert any(k[0] == "s3split" for k in fm._partials if isinstance(k, tuple)), "K40 not used"
     if heads == "s3p":
         assert any(k[:2] == ("s3split", "s3p_a") for k in fm._partials if isinstance(k, tuple)), "K16P not used"
+        assert any(k[0] == "hsign" for k in fm._partials if isinstance(k, tuple)), "K16R / K42S not used"
     assert any(k[0] == "k42" for k in fm._partials if isinstance(k, tuple)), "K42 not used"
     replay_last_step_iteration(agent, D, A, [H], discrete, "ppo" if agent_name == "PPO_Clip" else "a2c", 0.01, 2, 4,
                                expect_mid_truncations=not discrete)
@@ -184,6 +185,32 @@ def test_trunk_heads_iteration_equals_k13_k16(monkeypatch):
         fm.use_trunk_heads = on
         agent.train(32)
         torch.cuda.synchronize()
+        runs.append(([p.detach().clone() for p in agent.policy.parameters()], [dict(i) for i in agent.infos]))
+    (p0, i0), (p1, i1) = runs
+    assert len(p0) == len(p1) and all(torch.equal(a, b) for a, b in zip(p0, p1))
+    assert i0 == i1
+
+
+def test_s3r_trunk_iteration_equals_k13_k16p(monkeypatch):
+    """The K16R learner wiring (fused_mlp.TRUNK_S3R: the gather-only K13 form; h formed inside both split-GEMM head
+    launches, the actor writing h and its sign bits; K41 on that h; K42S's act' from the bits) against K13's forward +
+    K16P + K42 on h: one whole C2 fast-path iteration from the same seed, every parameter and every update's loss
+    scalars bit for bit."""
+    from xuanpolicy_amd import ops
+    from xuanpolicy_amd.fused_mlp import FusedActorCritic
+    from xuanpolicy_amd.runner import build_synthbox_ppo
+    monkeypatch.setattr(ops, "S3_GEMMS", True)
+    monkeypatch.setattr(ops, "S3_HEADS", "s3p")
+    runs = []
+    for on in (False, True):
+        monkeypatch.setattr(FusedActorCritic, "TRUNK_S3R", on)
+        agent = build_synthbox_ppo(n_envs=256, n_steps=32, obs_dim=17, act_dim=6, hidden=256, n_epoch=2,
+                                   n_minibatch=4, seed=3, device="cuda:0")
+        fm = agent.learner._fused_mlp()
+        assert fm is not None and fm.trunk_heads and fm._s3r_on() == on
+        agent.train(32)
+        torch.cuda.synchronize()
+        assert any(isinstance(k, tuple) and k[0] == "hsign" for k in fm._partials) == on
         runs.append(([p.detach().clone() for p in agent.policy.parameters()], [dict(i) for i in agent.infos]))
     (p0, i0), (p1, i1) = runs
     assert len(p0) == len(p1) and all(torch.equal(a, b) for a, b in zip(p0, p1))

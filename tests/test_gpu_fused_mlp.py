@@ -739,3 +739,115 @@ def test_head_gemm_trunk_kernels_equal_k13_then_k16(algo, dist, K, B, code, din)
     assert torch.equal(got["h"].view(B, H), h_ref), "h differs from K13's"
     for k in ("dz", "p_dw_a", "p_dbh_a", "p_dbo_a", "p_dw_c", "p_dbh_c", "p_dbo_c", "lp"):
         assert torch.equal(got[k], ref[k]), k   # same h, same k loop and epilogue: bit for bit
+
+
+@pytest.mark.parametrize("algo,dist,K,B,code,din", [
+    ("ppo", "gaussian", 6, 4133, 1, 17),    # the C2 head and trunk widths, ragged tail (4133 = 64 * 64 + 37)
+    ("a2c", "categorical", 4, 777, 0, 4),
+    ("ppo", "categorical", 8, 193, 2, 20),   # tanh: h written, no sign bits
+    ("a2c", "gaussian", 6, 64, 1, 17),
+    ("ppo", "gaussian", 6, 20037, 1, 17),
+])
+def test_head_gemm_s3r_equals_k13_then_k16p(algo, dist, K, B, code, din):
+    """K16R (xpa_head_gemm_s3r_*: h formed from the gathered rows in the k loop of the split-GEMM heads) against K13
+    (xpa_thin_linear_act_fwd) followed by K16P on the same inputs, bit for bit: the h the actor writes (K13's fmaf
+    chain), its sign bits, dz, every partial and the loss partials; canaries around every output."""
+    from xuanpolicy_amd import ops
+    L, s = ops.lib(), ops._stream()
+    g = torch.Generator(device=DEV).manual_seed(B + K + din + 1)
+    H, R = 256, B + 300
+    slope = 0.01
+    xr = torch.randn(B, din, device=DEV, generator=g)
+    w0 = torch.randn(H, din, device=DEV, generator=g) / 4
+    b0 = torch.randn(H, device=DEV, generator=g) * 0.1
+    wh_a, wh_c = (torch.randn(H, H, device=DEV, generator=g) / 16 for _ in range(2))
+    bh_a, bh_c = (torch.randn(H, device=DEV, generator=g) * 0.1 for _ in range(2))
+    w_a = torch.randn(K, H, device=DEV, generator=g) / 16
+    b_a = torch.randn(K, device=DEV, generator=g) * 0.1
+    w_c = torch.randn(1, H, device=DEV, generator=g) / 16
+    b_c = torch.randn(1, device=DEV, generator=g) * 0.1
+    logstd = (-1 + 0.1 * torch.randn(K, device=DEV, generator=g)) if dist == "gaussian" else None
+    idx = torch.randperm(R, device=DEV, generator=g)[:B].contiguous()
+    idx[B // 2] = -1
+    adv = torch.randn(R, device=DEV, generator=g)
+    ret = torch.randn(R, device=DEV, generator=g)
+    act = (torch.randn(R, K, device=DEV, generator=g) * 0.5 if dist == "gaussian"
+           else torch.randint(0, K, (R,), device=DEV, generator=g).float())
+    old = -1.5 + 0.3 * torch.randn(R, device=DEV, generator=g) if algo == "ppo" else None
+    h_ref = torch.empty(B, H, device=DEV)
+    assert L.xpa_thin_linear_act_fwd(code, ops._p(xr), din, B, din, H, ops._p(w0), ops._p(b0), slope, ops._p(h_ref), H,
+                                     s) == 0
+    wsa, wsc = ops.s3_split(wh_a.t()), ops.s3_split(wh_c.t())
+    G = int(L.xpa_head_fused_num_partials(B))
+    W = int(L.xpa_loss_partial_width(K))
+    pad = 64
+    algo_c, dist_c = ops.ALGO[algo], ops.DIST[dist]
+    ent, clip, vf = 0.01, 0.2, 0.25
+    use_sign = code in (0, 1)
+
+    def run(trunk):
+        assert L.xpa_lds_poison(s) == 0
+        cz = lambda n, v=555.0: torch.full((n + 2 * pad,), v, device=DEV)   # noqa: E731
+        out = dict(dz=cz(B * 2 * H, 777.0), h=cz(B * H, 333.0), sg=cz(B * 8, 0.5), p_dw_a=cz(G * K * H),
+                   p_dbh_a=cz(G * H), p_dbo_a=cz(G * K), p_dw_c=cz(G * H), p_dbh_c=cz(G * H), p_dbo_c=cz(G),
+                   lp=cz(G * W))
+        out["lp"][pad:-pad] = 0.0
+        v = lambda k: ops._p(out[k][pad:])   # noqa: E731
+        dz = out["dz"][pad:pad + B * 2 * H].view(B, 2 * H)
+        p_ls = ops._p(logstd) if logstd is not None else None
+        p_old = ops._p(old) if old is not None else None
+        if trunk:
+            assert L.xpa_head_gemm_s3r_actor(
+                algo_c, dist_c, code, B, K, H, ops._p(xr), din, din, ops._p(w0), ops._p(b0), slope, v("h"), H,
+                v("sg") if use_sign else None, ops._p(wsa), ops._p(bh_a), 2 * H, ops._p(w_a), ops._p(b_a), slope, p_ls,
+                ops._p(idx), R, ops._p(act), p_old, ops._p(adv), None, 0, clip, ent, ops._p(dz), v("p_dw_a"),
+                v("p_dbh_a"), v("p_dbo_a"), v("lp"), W, s) == 0
+            assert L.xpa_head_gemm_s3r_critic(
+                code, B, H, ops._p(xr), din, din, ops._p(w0), ops._p(b0), slope, ops._p(wsc), ops._p(bh_c), 2 * H,
+                ops._p(w_c), ops._p(b_c), slope, ops._p(idx), R, ops._p(ret), vf, ops._p(dz[:, H:]), v("p_dw_c"),
+                v("p_dbh_c"), v("p_dbo_c"), v("lp"), W, s) == 0
+        else:
+            assert L.xpa_head_gemm_s3p_actor(algo_c, dist_c, code, B, K, H, ops._p(h_ref), H, ops._p(wsa),
+                                             ops._p(bh_a), 2 * H, ops._p(w_a), ops._p(b_a), slope, p_ls, ops._p(idx),
+                                             R, ops._p(act), p_old, ops._p(adv), None, 0, clip, ent, ops._p(dz),
+                                             v("p_dw_a"), v("p_dbh_a"), v("p_dbo_a"), v("lp"), W, s) == 0
+            assert L.xpa_head_gemm_s3p_critic(code, B, H, ops._p(h_ref), H, ops._p(wsc), ops._p(bh_c), 2 * H,
+                                              ops._p(w_c), ops._p(b_c), slope, ops._p(idx), R, ops._p(ret), vf,
+                                              ops._p(dz[:, H:]), v("p_dw_c"), v("p_dbh_c"), v("p_dbo_c"), v("lp"), W,
+                                              s) == 0
+        torch.cuda.synchronize()
+        for k, t in out.items():
+            fill = {"dz": 777.0, "h": 333.0, "sg": 0.5}.get(k, 555.0)
+            assert bool((t[:pad] == fill).all()) and bool((t[-pad:] == fill).all()), k + " written out of bounds"
+        return {k: t[pad:-pad] for k, t in out.items()}
+
+    ref, got = run(False), run(True)
+    assert torch.equal(got["h"].view(B, H), h_ref), "h differs from K13's"
+    if use_sign:
+        bits = (h_ref > 0).view(B, 8, 32).to(torch.int32)                      # [row, j, byte b]
+        want = (bits << torch.arange(8, device=DEV, dtype=torch.int32).view(1, 8, 1)).sum(1).to(torch.uint8)
+        assert torch.equal(got["sg"].view(torch.uint8).view(B, 32), want), "sign bits"
+    for k in ("dz", "p_dw_a", "p_dbh_a", "p_dbo_a", "p_dw_c", "p_dbh_c", "p_dbo_c", "lp"):
+        assert torch.equal(got[k], ref[k]), k   # same h, same k loop and epilogue: bit for bit
+
+
+@pytest.mark.parametrize("rows,din,code", [(4133, 17, 1), (65536, 17, 1), (777, 4, 0), (300, 20, 1)])
+def test_trunk_bwd_sign_equals_h_form(rows, din, code):
+    """K42S (act' from K16R's sign bits) == K42 (act' from h) bit for bit: the same factor per element."""
+    from xuanpolicy_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(rows + din)
+    xr = torch.randn(rows, din, device=DEV, generator=g)
+    h = torch.randn(rows, 256, device=DEV, generator=g)
+    if code == 1:
+        h = torch.where(h > 0, h, 0.01 * h)
+    h[5, 7] = 0.0   # a zero activation takes the slope branch in both forms
+    dz = torch.randn(rows, 512, device=DEV, generator=g)
+    w = torch.randn(512, 256, device=DEV, generator=g) / 16
+    bs = ops.s3_split(w)
+    bits = (h > 0).view(rows, 8, 32).to(torch.int32)
+    sign = (bits << torch.arange(8, device=DEV, dtype=torch.int32).view(1, 8, 1)).sum(1).to(torch.uint8)
+    sign = sign.contiguous().view(torch.int32).view(rows, 8)
+    ref = ops.s3_gemm_trunk_bwd(dz, bs, 512, h, xr, code, 0.01)
+    got = ops.s3_gemm_trunk_bwd(dz, bs, 512, None, xr, code, 0.01, h_sign=sign)
+    torch.cuda.synchronize()
+    assert torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1])

@@ -34,7 +34,9 @@ REPO = os.path.dirname(HERE)
 sys.path.insert(0, REPO)
 OUT = os.path.join(HERE, "_probe")
 VARIANTS = {0: "full", 1: "gemm only", 2: "epilogue only", 3: "staging only", 4: "epilogue without dz stores",
-            5: "epilogue without phase 2", 6: "gemm without operand DMAs"}
+            5: "epilogue without phase 2", 6: "gemm without operand DMAs", 7: "K16P without its B-plane DMAs"}
+# XPA_PROBE_FORM=s3p times the K16P entries (Wh as its bf16 planes, r04) instead of the f32 K16 ones
+FORM = os.environ.get("XPA_PROBE_FORM", "k16")
 FLAGS = {}   # variant -> hipcc defines, when not just -DXPA_HEAD_PROBE=<variant>
 # variant subset: XPA_PROBE_VARIANTS=0,1,7 (default all)
 _sel = os.environ.get("XPA_PROBE_VARIANTS")
@@ -77,22 +79,27 @@ def child(v, reps=30):
     L, s = _lib.load(), ops._stream(dev)
     W = ws.loss_partials.shape[1]
 
+    pre = "xpa_head_gemm_s3p_" if FORM == "s3p" else "xpa_head_gemm_"
+    fa, fc = getattr(L, pre + "actor"), getattr(L, pre + "critic")
+    if FORM == "s3p":
+        wha, whc = ops.s3_split(wha.t()), ops.s3_split(whc.t())
+
     def actor():
-        _lib.check(L.xpa_head_gemm_actor(0, 0, 1, B, K, H, ops._p(x), H, ops._p(wha), ops._p(bha), 2 * H, ops._p(wa),
+        _lib.check(fa(0, 0, 1, B, K, H, ops._p(x), H, ops._p(wha), ops._p(bha), 2 * H, ops._p(wa),
                                          ops._p(ba), 0.01, ops._p(logstd), ops._p(idx), R, ops._p(act), ops._p(old),
                                          ops._p(adv), ops._p(part), part.shape[0], 0.2, 0.0, ops._p(ws.dz_actor),
                                          ops._p(ws.p_dw_actor), ops._p(ws.p_dbh_actor), ops._p(ws.p_dbo_actor),
                                          ops._p(ws.loss_partials), W, s), "actor")
 
     def critic():
-        _lib.check(L.xpa_head_gemm_critic(1, B, H, ops._p(x), H, ops._p(whc), ops._p(bhc), 2 * H, ops._p(wc),
+        _lib.check(fc(1, B, H, ops._p(x), H, ops._p(whc), ops._p(bhc), 2 * H, ops._p(wc),
                                           ops._p(bc), 0.01, ops._p(idx), R, ops._p(ret), 0.25, ops._p(ws.dz_critic),
                                           ops._p(ws.p_dw_critic), ops._p(ws.p_dbh_critic), ops._p(ws.p_dbo_critic),
                                           ops._p(ws.loss_partials), W, s), "critic")
 
     res = {}
     fns = [("actor", actor), ("critic", critic)]
-    if v == 0:   # the library GEMM of the same shape, for reference
+    if v == 0 and FORM != "s3p":   # the library GEMM of the same shape, for reference
         import torch.nn.functional as F
         fns.append(("hipblaslt_linear_256x256", lambda: F.linear(x, wha, bha)))
     for name, fn in fns:
@@ -108,7 +115,7 @@ def child(v, reps=30):
         res[name] = round(e0.elapsed_time(e1) / reps * 1e3, 2)
     flops = 2.0 * B * H * H
     res["gemm_floor_us_at_peak"] = round(flops / 157.3e6, 2)
-    print(json.dumps({"variant": VARIANTS[v], **res}), flush=True)
+    print(json.dumps({"variant": VARIANTS[v], "form": FORM, **res}), flush=True)
 
 
 def run():

@@ -222,6 +222,15 @@ SIGNATURES = {
     "xpa_head_gemm_trunk_critic": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p, c_f32, c_p,
                                                   c_i64, c_p, c_p, c_i64, c_p, c_p, c_f32, c_p, c_i64, c_p, c_f32, c_p,
                                                   c_p, c_p, c_p, c_p, c_i64, c_p]),
+    "xpa_head_gemm_s3r_actor": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_i64,
+                                               c_i64, c_p, c_p, c_f32, c_p, c_i64, c_p, c_p, c_p, c_i64, c_p, c_p, c_f32,
+                                               c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_f32, c_f32, c_p, c_p, c_p,
+                                               c_p, c_p, c_i64, c_p]),
+    "xpa_head_gemm_s3r_critic": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p, c_f32, c_p, c_p,
+                                                c_i64, c_p, c_p, c_f32, c_p, c_i64, c_p, c_f32, c_p, c_p, c_p, c_p, c_p,
+                                                c_i64, c_p]),
+    "xpa_s3_gemm_trunk_bwd_sign": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, ctypes.c_int,
+                                                  c_f32, c_p, c_p, c_p]),
     "xpa_s3_probe": (ctypes.c_int, [ctypes.c_int]),
     "xpa_s3_split_bytes": (c_i64, [c_i64, c_i64]),
     "xpa_s3_split_b": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),

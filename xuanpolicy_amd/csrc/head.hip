@@ -127,6 +127,7 @@ struct HeadArgs {
     int din;
     float slope0;
     float *hout;
+    unsigned *hmask;  // K16R: the trunk activations' sign bits [batch, 8 words] (actor; may be null)
 };
 
 __device__ __forceinline__ void load_tile(float4 (&zq)[16], const float *__restrict__ z, int64_t ld, int64_t tile,
@@ -748,13 +749,14 @@ __device__ __forceinline__ void gemm_issue_p(unsigned st, const float *__restric
     int64_t grow = r0 + wave * 16 + rr;
     grow = grow < batch ? grow : batch - 1;
     glds16(x + grow * ldx + c * kKC + 4 * q, st + (unsigned)(wave * 16 * kKC * 4));
+#if XPA_HEAD_PROBE == 7  // 7 = K16P without its B-plane DMAs (A rows still staged)
+    return;
+#endif
     const char *src = wsp + (int64_t)c * 24576;
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
         const int piece = wave * 6 + j;
-        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src + piece * 1024 + lane * 16),
-                     "s"(st + (unsigned)(4096 + piece * 1024))
-                     : "memory", "m0");
+        glds16(reinterpret_cast<const float *>(src + piece * 1024 + lane * 16), st + (unsigned)(4096 + piece * 1024));
     }
 }
 constexpr int kPDmaPerChunk = 7;
@@ -779,6 +781,67 @@ __device__ __forceinline__ void gemm_chunk_s3p(const char *st, f32x16 (&acc)[2][
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) acc[rt][ct] = xpa_mfma_s3(ah[rt], am[rt], al[rt], bh, bm, bl, acc[rt][ct]);
     }
+}
+
+// K16R (r04): K16P with the A operand (the trunk activations h) formed in the k loop instead of read from HBM:
+// h = act(x W0^T + b0) for the tile's 64 rows, the representation's one thin layer (K13's Linear(d_in <= 20, 256) +
+// activation, its fmaf chain over the zero-padded inputs: the same bits as K13's h).  Thread t owns row t >> 2 of
+// the tile and slot p = t & 3 of the chunk's swizzled A image (k quad q = p ^ ((row >> 2) & 3), gemm_issue_p's
+// layout), so per 16-k chunk it forms 4 values (80 FMAs from its x row in registers and 4 W0 rows in LDS) and writes
+// them with one ds_write_b128 where the DMA would have landed them.  W0 / b0 are staged per tile beside the two
+// operand stages (the epilogue reuses that LDS).  The actor launch also writes h (K41's operand) and its sign bits
+// (K42's act' for LeakyReLU / identity); K13 only gathers the minibatch rows (64 MiB of h writes and 192 MiB of h
+// reads fewer per C2 update).
+constexpr int kRW = 20;                                   // W0 row stride in LDS (= kTrunkDMax, zero padded)
+constexpr int kROff = 2 * kPStageB;                       // bytes: W0 then b0 after the two stages
+constexpr int kREnd = kROff + (kH * kRW + kH) * 4;       // 78848 B
+__device__ __forceinline__ void gemm_issue_b(unsigned st, const char *__restrict__ wsp, int c, int lane, int wave) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const int piece = wave * 6 + j;
+        glds16(reinterpret_cast<const float *>(wsp + (int64_t)c * 24576 + piece * 1024 + lane * 16),
+               st + (unsigned)(4096 + piece * 1024));
+    }
+}
+
+// lane p of a row's 4 lanes (a DPP quad) holds x[4 i + p] in xq[i]: x[k] = quad broadcast of xq[k >> 2] from lane
+// k & 3 (folded into the FMAs as DPP operands), 5 VGPRs instead of 20 for the row
+__device__ __forceinline__ float quad_bcast(float v, int j) {
+    const int ctrl = j * 0x55;   // quad_perm [j, j, j, j]
+    int r;
+    switch (j) {
+        case 0: r = __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x00, 0xF, 0xF, false); break;
+        case 1: r = __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x55, 0xF, 0xF, false); break;
+        case 2: r = __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xAA, 0xF, 0xF, false); break;
+        default: r = __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xFF, 0xF, 0xF, false); break;
+    }
+    (void)ctrl;
+    return __builtin_bit_cast(float, r);
+}
+
+template <int ACT>
+__device__ __forceinline__ void trunk_chunk(char *st, const float *s_w0, const float (&xq)[kRW / 4], int c, int q,
+                                            float slope0, float4 &hq) {
+    const int k0 = 16 * c + 4 * q;
+    const float4 bq = *reinterpret_cast<const float4 *>(s_w0 + kH * kRW + k0);
+    float hv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float *wr = s_w0 + (k0 + j) * kRW;
+        float a0 = 0.f;
+#pragma unroll
+        for (int i = 0; i < kRW / 4; ++i) {
+            const float4 w4 = *reinterpret_cast<const float4 *>(wr + 4 * i);
+            a0 = fmaf(quad_bcast(xq[i], 0), w4.x, a0);
+            a0 = fmaf(quad_bcast(xq[i], 1), w4.y, a0);
+            a0 = fmaf(quad_bcast(xq[i], 2), w4.z, a0);
+            a0 = fmaf(quad_bcast(xq[i], 3), w4.w, a0);
+        }
+        const float b = j == 0 ? bq.x : j == 1 ? bq.y : j == 2 ? bq.z : bq.w;
+        hv[j] = act_f<ACT>(a0 + b, slope0);
+    }
+    hq = make_float4(hv[0], hv[1], hv[2], hv[3]);
+    *reinterpret_cast<float4 *>(st + 16 * threadIdx.x) = hq;
 }
 
 // K16X prologue (r03): the representation's first layer (K13's Linear(d_in <= 20, 256) + activation, bit for bit
@@ -832,14 +895,17 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
                                                            int64_t ldxr = 0, int din = 0,
                                                            const float *__restrict__ W0 = nullptr,
                                                            const float *__restrict__ b0 = nullptr, float slope0 = 0.f,
-                                                           float *__restrict__ hout = nullptr, int64_t ldh = 0) {
+                                                           float *__restrict__ hout = nullptr, int64_t ldh = 0,
+                                                           unsigned *__restrict__ hmask = nullptr) {
     using Epi = HeadEpi<MODE, ALGO, ACT, KMAX>;
     // ONE LDS array (a second __shared__ object beside the DMA target can make hipcc wait vmcnt(0) before
     // every chunk's ds_reads): operand stages / h tile, then the epilogue's partials, d head and stats.
     constexpr int kPartOff = kTile * kS, kDhOff = kPartOff + kWaves * kTile * Epi::PH;
     constexpr int kStatsOff = kDhOff + kTile * Epi::KP;
     static_assert(KMAX <= 8 || (kStatsOff + 4) * 4 <= 81920, "wide heads: 2 blocks per CU");
-    __shared__ __attribute__((aligned(16))) float lds[kStatsOff + 4];
+    constexpr int kLdsFloats = S3 == 3 && kREnd / 4 > kStatsOff + 4 ? kREnd / 4 : kStatsOff + 4;
+    static_assert(kLdsFloats * 4 <= 81920, "K16R: 2 blocks per CU");
+    __shared__ __attribute__((aligned(16))) float lds[kLdsFloats];
     float *smem = lds;
     auto s_part = reinterpret_cast<float(*)[kTile][Epi::PH]>(lds + kPartOff);
     auto s_dh = reinterpret_cast<float(*)[Epi::KP]>(lds + kDhOff);
@@ -873,7 +939,61 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
             lda = ldh;
         }
 #if XPA_HEAD_PROBE != 2 && XPA_HEAD_PROBE != 4 && XPA_HEAD_PROBE != 5  // tools/head_probe.py: 2 = epilogue alone (4, 5: parts of it)
-        if constexpr (S3 == 2) {   // K16P: Wh arrives as its three bf16 planes (the pointer is the split buffer)
+        if constexpr (S3 == 3) {   // K16R: B as K16P, A formed from the gathered rows (see trunk_chunk)
+            const char *wsp = reinterpret_cast<const char *>(Wh);
+            float *s_w0 = reinterpret_cast<float *>(reinterpret_cast<char *>(smem) + kROff);
+            gemm_issue_b(lds_base, wsp, 0, lane, wave);
+            for (int e = t; e < kH * kRW; e += 256) {
+                const int cc = e / kRW, k = e - cc * kRW;
+                s_w0[e] = k < din ? W0[cc * din + k] : 0.f;
+            }
+            s_w0[kH * kRW + t] = b0[t];
+            // rows past the batch form (and the actor writes) row batch - 1's values again: the same bits, so the
+            // stores need no predicate and every wave issues the same count (the counted waits below)
+            const int rr = t >> 2, q = (t & 3) ^ ((rr >> 2) & 3);
+            const int64_t xrow = r0 + rr < batch ? r0 + rr : batch - 1;
+            float xv[kRW / 4];
+#pragma unroll
+            for (int i = 0; i < kRW / 4; ++i) {
+                const int k = 4 * i + (t & 3);
+                const float v = xr[xrow * ldxr + (k < din ? k : 0)];
+                xv[i] = k < din ? v : 0.f;
+            }
+            __syncthreads();   // W0 / b0 staged (and chunk 0's planes landed)
+            float *hrow = hout != nullptr ? hout + xrow * ldh + 4 * q : nullptr;
+            // sign bits, K42S's lane order: byte b of a row's 32 bytes holds bit j = h[row, 32 j + b] > 0, so this
+            // thread's 4 columns 16 c + 4 q + i (i < 4) of every chunk of parity P land in bytes 16 P + 4 q + i, bit c / 2
+            unsigned sgn[2] = {0u, 0u};
+            auto form = [&](int c) {
+                float4 hq;
+                trunk_chunk<ACT>(reinterpret_cast<char *>(smem) + (c & 1) * kPStageB, s_w0, xv, c, q, slope0, hq);
+                if (hrow != nullptr) {
+                    *reinterpret_cast<float4 *>(hrow + 16 * c) = hq;
+                    const unsigned sh = (unsigned)(c >> 1);
+                    const unsigned add = ((hq.x > 0.f ? 1u : 0u) << sh) | ((hq.y > 0.f ? 1u : 0u) << (8 + sh)) |
+                                         ((hq.z > 0.f ? 1u : 0u) << (16 + sh)) | ((hq.w > 0.f ? 1u : 0u) << (24 + sh));
+                    if (c & 1) sgn[1] |= add;
+                    else sgn[0] |= add;
+                }
+            };
+            form(0);
+#pragma unroll 1
+            for (int c = 0; c < kChunks; ++c) {
+                // chunk c's planes landed (the store of chunk c's h, issued after them, may still fly) and every
+                // wave wrote its A image; chunk c - 1's stage is free
+                if (hrow != nullptr) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                if (c + 1 < kChunks) gemm_issue_b(lds_base + ((c + 1) & 1) * kPStageB, wsp, c + 1, lane, wave);
+#if XPA_HEAD_PROBE != 3
+                gemm_chunk_s3p(reinterpret_cast<const char *>(smem) + (c & 1) * kPStageB, acc, lane, wave);
+#endif
+                if (c + 1 < kChunks) form(c + 1);
+            }
+            if (hrow != nullptr && hmask != nullptr) {
+                hmask[xrow * 8 + q] = sgn[0];
+                hmask[xrow * 8 + 4 + q] = sgn[1];
+            }
+        } else if constexpr (S3 == 2) {   // K16P: Wh arrives as its three bf16 planes (the pointer is the split buffer)
             const char *wsp = reinterpret_cast<const char *>(Wh);
             gemm_issue_p(lds_base, xa, lda, wsp, r0, batch, 0, lane, wave);
 #pragma unroll 1
@@ -882,7 +1002,9 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
                 asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
                 if (c + 1 < kChunks)
                     gemm_issue_p(lds_base + ((c + 1) & 1) * kPStageB, xa, lda, wsp, r0, batch, c + 1, lane, wave);
+#if XPA_HEAD_PROBE != 3
                 gemm_chunk_s3p(reinterpret_cast<const char *>(smem) + (c & 1) * kPStageB, acc, lane, wave);
+#endif
             }
         } else {
         gemm_issue(lds_base, xa, lda, Wh, r0, batch, 0, lane, wave);
@@ -1098,7 +1220,8 @@ XPA_API int64_t xpa_head_fused_num_partials(int64_t batch) {
 namespace {
 #define XPA_HEAD_ARGS(a) a.batch, a.K, a.ld, a.z, a.ldx, a.Wh, a.bh, a.W, a.bias, a.slope, a.logstd, a.idx, a.n_rows, a.act, a.old_logp, a.adv, a.ret, a.adv_partials, a.n_adv_partials, a.clip_range, a.ent_coef, a.vf_coef, a.dz, a.p_dw, a.p_dbh, a.p_dbo, a.p_loss, a.loss_width
 // KIND: 0 K12 (z from HBM), 1 K16 (hidden GEMM inside), 2 K16X (trunk layer + hidden GEMM inside), 3 K16W,
-// 4 K16S (K16 with the hidden GEMM on the bf16 matrix cores by the three-way split), 5 K16P (K16S with Wh pre-split)
+// 4 K16S (K16 with the hidden GEMM on the bf16 matrix cores by the three-way split), 5 K16P (K16S with Wh pre-split),
+// 6 K16R (K16P with h formed from the gathered rows in the k loop)
 template <int KIND, int MODE, int ALGO, int ACT, int KMAX>
 void launch_one(const HeadArgs &a, hipStream_t s) {
     const dim3 grid((unsigned)xpa_head_fused_num_partials(a.batch)), block(256);
@@ -1108,16 +1231,19 @@ void launch_one(const HeadArgs &a, hipStream_t s) {
                                dim3(512), 0, s, XPA_HEAD_ARGS(a));
     } else if constexpr (KIND == 4)
         hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, false, 1>), grid, block, 0, s, XPA_HEAD_ARGS(a),
-                           nullptr, (int64_t)0, 0, nullptr, nullptr, 0.f, nullptr, (int64_t)0);
+                           nullptr, (int64_t)0, 0, nullptr, nullptr, 0.f, nullptr, (int64_t)0, nullptr);
     else if constexpr (KIND == 5)
         hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, false, 2>), grid, block, 0, s, XPA_HEAD_ARGS(a),
-                           nullptr, (int64_t)0, 0, nullptr, nullptr, 0.f, nullptr, (int64_t)0);
+                           nullptr, (int64_t)0, 0, nullptr, nullptr, 0.f, nullptr, (int64_t)0, nullptr);
     else if constexpr (KIND == 2)
         hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, true>), grid, block, 0, s, XPA_HEAD_ARGS(a), a.xr,
-                           a.ldxr, a.din, a.W0, a.b0, a.slope0, a.hout, a.ldh);
+                           a.ldxr, a.din, a.W0, a.b0, a.slope0, a.hout, a.ldh, nullptr);
+    else if constexpr (KIND == 6)
+        hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, false, 3>), grid, block, 0, s, XPA_HEAD_ARGS(a),
+                           a.xr, a.ldxr, a.din, a.W0, a.b0, a.slope0, a.hout, a.ldh, a.hmask);
     else if constexpr (KIND == 1)
         hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, false>), grid, block, 0, s, XPA_HEAD_ARGS(a),
-                           nullptr, (int64_t)0, 0, nullptr, nullptr, 0.f, nullptr, (int64_t)0);
+                           nullptr, (int64_t)0, 0, nullptr, nullptr, 0.f, nullptr, (int64_t)0, nullptr);
     else
         hipLaunchKernelGGL((head_tile_kernel<MODE, ALGO, ACT, KMAX>), grid, block, 0, s, XPA_HEAD_ARGS(a));
 }
@@ -1135,7 +1261,8 @@ void launch_head(const HeadArgs &a, int act_code, hipStream_t s) {
     else if (a.K <= 4) launch_act<KIND, MODE, ALGO, 4>(a, act_code, s);  // KMAX = smallest of 4 / 6 / 8 >= K
     else if (a.K <= 6) launch_act<KIND, MODE, ALGO, 6>(a, act_code, s);
     else if (a.K <= 8) launch_act<KIND, MODE, ALGO, 8>(a, act_code, s);
-    else if constexpr (KIND != 2 && KIND != 3) launch_act<KIND, MODE, ALGO, 18>(a, act_code, s);  // C4 (A = 17), 18-way
+    else if constexpr (KIND != 2 && KIND != 3 && KIND != 6)
+        launch_act<KIND, MODE, ALGO, 18>(a, act_code, s);  // C4 (A = 17), 18-way
 }
 #undef XPA_HEAD_ARGS
 
@@ -1368,6 +1495,64 @@ XPA_API int xpa_head_gemm_trunk_critic(int act_code, int64_t batch, int64_t hidd
     a.xr = x_rows; a.ldxr = ld_rows; a.din = (int)d_in; a.W0 = w_in; a.b0 = b_in; a.slope0 = slope_in;
     a.hout = h_out; a.ldh = ld_h;
     launch_head<2, 2, 0>(a, act_code, (hipStream_t)stream);
+    return xpa_launch_status();
+}
+// K16R entries: xpa_head_gemm_s3p_*'s outputs (w_hidden = the split buffer of Wh^T) with the hidden layer's input h
+// formed inside from the gathered minibatch rows x_rows [batch, d_in <= 20] (the representation's one thin layer:
+// w_in [256, d_in], b_in, the heads' activation with slope_in) — K13's h bit for bit.  The actor also writes h
+// (h_out [batch, >= 256] at ld_h) and, when h_sign is given, its sign bits: byte b of row r's 32 bytes (h_sign + 8 r)
+// bit j = h[r, 32 j + b] > 0 (xpa_s3_gemm_trunk_bwd_sign's act', one byte per lane there).  act_dim <= 8.
+XPA_API int xpa_head_gemm_s3r_actor(int algo, int dist, int act_code, int64_t batch, int64_t act_dim, int64_t hidden,
+                                    const float *x_rows, int64_t ld_rows, int64_t d_in, const float *w_in,
+                                    const float *b_in, float slope_in, float *h_out, int64_t ld_h, unsigned *h_sign,
+                                    const void *w_hidden, const float *b_hidden, int64_t ld_dz, const float *w,
+                                    const float *b, float slope, const float *logstd, const int64_t *idx,
+                                    int64_t n_rows, const float *act, const float *old_logp, const float *adv,
+                                    const double *adv_partials, int64_t n_adv_partials, float clip_range,
+                                    float ent_coef, float *dz, float *partial_dw, float *partial_db_hidden,
+                                    float *partial_db_out, float *loss_partials, int64_t loss_width,
+                                    xpa_stream_t stream) {
+    int rc = check_actor(algo, dist, act_code, batch, act_dim, hidden, w, b, logstd, n_rows, idx, act, old_logp, adv, dz,
+                         partial_dw, partial_db_hidden, partial_db_out, loss_partials, loss_width);
+    if (rc) return rc;
+    const float *whp = static_cast<const float *>(w_hidden);
+    rc = check_trunk(d_in, x_rows, ld_rows, w_in, b_in, whp, b_hidden, ld_dz);
+    if (rc) return rc;
+    if (act_dim > 8 || !h_out || (uintptr_t)h_out % 16 || ld_h < kH || ld_h % 4) return (int)hipErrorInvalidValue;
+    HeadArgs a{};
+    a.batch = batch; a.K = (int)act_dim; a.ld = ld_dz; a.z = nullptr; a.ldx = kKin; a.Wh = whp; a.bh = b_hidden;
+    a.W = w; a.bias = b; a.slope = slope; a.logstd = logstd; a.idx = idx; a.n_rows = n_rows; a.act = act;
+    a.old_logp = old_logp; a.adv = adv; a.ret = nullptr; a.adv_partials = adv_partials;
+    a.n_adv_partials = n_adv_partials; a.clip_range = clip_range; a.ent_coef = ent_coef; a.vf_coef = 0.f; a.dz = dz;
+    a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
+    a.loss_width = (int)loss_width;
+    a.xr = x_rows; a.ldxr = ld_rows; a.din = (int)d_in; a.W0 = w_in; a.b0 = b_in; a.slope0 = slope_in;
+    a.hout = h_out; a.ldh = ld_h; a.hmask = h_sign;
+    return actor_entry<6>(algo, dist, act_code, a, (hipStream_t)stream);
+}
+
+XPA_API int xpa_head_gemm_s3r_critic(int act_code, int64_t batch, int64_t hidden, const float *x_rows,
+                                     int64_t ld_rows, int64_t d_in, const float *w_in, const float *b_in,
+                                     float slope_in, const void *w_hidden, const float *b_hidden, int64_t ld_dz,
+                                     const float *w, const float *b, float slope, const int64_t *idx, int64_t n_rows,
+                                     const float *ret, float vf_coef, float *dz, float *partial_dw,
+                                     float *partial_db_hidden, float *partial_db_out, float *loss_partials,
+                                     int64_t loss_width, xpa_stream_t stream) {
+    if (batch <= 0 || hidden != kH || act_code < 0 || act_code > 2 || !w || !b || !ret || !dz || !partial_dw ||
+        !partial_db_hidden || !partial_db_out || !loss_partials || loss_width < kPartBase || n_rows <= 0 ||
+        (!idx && n_rows < batch) || (uintptr_t)w % 16)
+        return (int)hipErrorInvalidValue;
+    const float *whp = static_cast<const float *>(w_hidden);
+    int rc = check_trunk(d_in, x_rows, ld_rows, w_in, b_in, whp, b_hidden, ld_dz);
+    if (rc) return rc;
+    HeadArgs a{};
+    a.batch = batch; a.K = 1; a.ld = ld_dz; a.z = nullptr; a.ldx = kKin; a.Wh = whp; a.bh = b_hidden; a.W = w;
+    a.bias = b; a.slope = slope; a.idx = idx; a.n_rows = n_rows; a.ret = ret; a.vf_coef = vf_coef; a.dz = dz;
+    a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
+    a.loss_width = (int)loss_width;
+    a.xr = x_rows; a.ldxr = ld_rows; a.din = (int)d_in; a.W0 = w_in; a.b0 = b_in; a.slope0 = slope_in;
+    a.hout = nullptr; a.ldh = 0; a.hmask = nullptr;
+    launch_head<6, 2, 0>(a, act_code, (hipStream_t)stream);
     return xpa_launch_status();
 }
 #endif  // XPA_HEAD_KERNELS_ONLY

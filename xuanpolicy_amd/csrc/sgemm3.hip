@@ -380,13 +380,17 @@ __device__ __forceinline__ float tb_act_g(float h, float slope) {  // thin.hip a
     return 1.f;
 }
 
-template <int ACT>
+// SIGN (r04, K42S): act' from the sign bits K16R's actor launch wrote (byte col of the row's 32: bit cb = h[row, 32 cb +
+// col] > 0; LeakyReLU / identity only) instead of the 1 KiB h row — the same factor, 64 MiB less read per C2 update.
+template <int ACT, bool SIGN = false>
 __global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *__restrict__ a, int64_t lda,
                                                                    const __bf16 *__restrict__ bs, int64_t M,
                                                                    int nchunks, const float *__restrict__ hmat,
                                                                    int64_t ldh, const float *__restrict__ x,
                                                                    int64_t ldx, int din, float slope,
-                                                                   float *__restrict__ p_dw, float *__restrict__ p_db) {
+                                                                   float *__restrict__ p_dw, float *__restrict__ p_db,
+                                                                   const unsigned *__restrict__ hsign = nullptr) {
+    static_assert(!SIGN || ACT != 2, "sign bits carry act' of LeakyReLU / identity only");
     using G = S3Geom<8>;
     __shared__ __attribute__((aligned(16))) char lds[3 * G::kStage];
     const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
@@ -416,11 +420,20 @@ __global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *
     for (int r = 0; r < 16; ++r) {
         const int64_t row = wrow + (r & 3) + 8 * (r >> 2) + 4 * hh;
         const bool ok = row < M;
-        const float *hrow = hmat + (ok ? row : 0) * ldh + col;
+        if constexpr (SIGN) {   // byte col of the row: bit cb = h[row, 32 cb + col] > 0
+            const unsigned bits = reinterpret_cast<const unsigned char *>(hsign + (ok ? row : 0) * 8)[col];
 #pragma unroll
-        for (int cb = 0; cb < 8; ++cb) {
-            const float hv = hrow[cb * 32];
-            acc[cb][r] = ok ? acc[cb][r] * tb_act_g<ACT>(hv, slope) : 0.f;
+            for (int cb = 0; cb < 8; ++cb) {
+                const float g = ACT == 1 ? (((bits >> cb) & 1u) ? 1.f : slope) : 1.f;
+                acc[cb][r] = ok ? acc[cb][r] * g : 0.f;
+            }
+        } else {
+            const float *hrow = hmat + (ok ? row : 0) * ldh + col;
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb) {
+                const float hv = hrow[cb * 32];
+                acc[cb][r] = ok ? acc[cb][r] * tb_act_g<ACT>(hv, slope) : 0.f;
+            }
         }
     }
     // ---- x^T's fragments for the wave's 32 rows: lane (feature i, half hh), k step s element j = row rho(8 s + j, hh)
@@ -1009,6 +1022,28 @@ XPA_API int xpa_s3_gemm_trunk_bwd(const float *dz, int64_t ldz, const void *b_sp
     else if (act == 1) XPA_TB(1);
     else XPA_TB(2);
 #undef XPA_TB
+    return xpa_launch_status();
+}
+
+// K42S: xpa_s3_gemm_trunk_bwd with act' from h's sign bits (xpa_head_gemm_s3r_actor's h_sign: 32 bytes per row, byte
+// b bit j = h[row, 32 j + b] > 0) instead of h; act 0 (identity) or 1 (LeakyReLU / ReLU).  The same outputs bit for bit.
+XPA_API int xpa_s3_gemm_trunk_bwd_sign(const float *dz, int64_t ldz, const void *b_split, int64_t k,
+                                       const unsigned *h_sign, const float *x, int64_t ldx, int64_t rows,
+                                       int64_t d_in, int act, float slope, float *partial_dw, float *partial_db,
+                                       xpa_stream_t stream) {
+    if (!dz || !b_split || !h_sign || !x || !partial_dw || !partial_db || rows <= 0 || k <= 0 || k % kKC != 0 ||
+        ldz < k || (ldz & 3) || (reinterpret_cast<uintptr_t>(dz) & 15) || (reinterpret_cast<uintptr_t>(h_sign) & 15) ||
+        d_in < 1 || d_in > 32 || ldx < d_in || act < 0 || act > 1 || k / kKC > (1 << 20))
+        return (int)hipErrorInvalidValue;
+    const dim3 grid((unsigned)xpa_s3_gemm_trunk_bwd_num_partials(rows)), block(512);
+    const __bf16 *bs = static_cast<const __bf16 *>(b_split);
+    const int nch = (int)(k / kKC);
+    if (act == 0)
+        s3_gemm_trunk_bwd_kernel<0, true><<<grid, block, 0, stream>>>(dz, ldz, bs, rows, nch, nullptr, 0, x, ldx,
+                                                                       (int)d_in, slope, partial_dw, partial_db, h_sign);
+    else
+        s3_gemm_trunk_bwd_kernel<1, true><<<grid, block, 0, stream>>>(dz, ldz, bs, rows, nch, nullptr, 0, x, ldx,
+                                                                       (int)d_in, slope, partial_dw, partial_db, h_sign);
     return xpa_launch_status();
 }
 

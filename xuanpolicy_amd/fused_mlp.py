@@ -188,9 +188,16 @@ class FusedActorCritic:
             x.gathered = torch.empty((B, lin.in_features), dtype=torch.float32, device=x.device)
             # K16X: gather-only (h = NULL); the actor head launch forms h and writes it here
             # (only for forward_hidden -> loss_backward, where the K16X launches consume x.trunk; h is unwritten until then)
-            deferred = defer_trunk and self.trunk_heads and self.use_trunk_heads and len(self.rep) == 1
+            deferred = defer_trunk and self.trunk_heads and (self.use_trunk_heads or self._s3r_on()) and len(self.rep) == 1
             if deferred:
                 x.trunk = (x.gathered, lin.weight, lin.bias, slope, h)
+                if self._s3r_on() and code in (0, 1):   # K16R's sign bits of h for K42S (act' without reading h)
+                    key = ("hsign", B)
+                    sign = self._partials.get(key)
+                    if sign is None:
+                        sign = torch.empty((B, 8), dtype=torch.int32, device=x.device)
+                        self._partials[key] = sign
+                    x.trunk = x.trunk + (sign,)
             _lib.check(ops.lib().xpa_thin_linear_act_fwd_gather(
                 code, ops._p(x.flat), x.flat.stride(0), x.flat.shape[0], ops._p(x.idx), B, lin.in_features,
                 lin.out_features, ops._p(lin.weight), ops._p(lin.bias), slope, None if deferred else ops._p(h),
@@ -451,6 +458,13 @@ class FusedActorCritic:
         return bufs
 
     FUSE_TRUNK_BWD = True   # K42 where it applies (ops.S3_GEMMS, one thin representation layer)
+    # K16R where it applies (the split heads, one thin representation layer with the heads' activation): h formed
+    # inside both head launches from the gathered rows (K13 only gathers), the actor writes h and its sign bits
+    TRUNK_S3R = True
+
+    def _s3r_on(self):
+        return (self.TRUNK_S3R and self.trunk_heads and ops.S3_GEMMS and ops.S3_HEADS == "s3p"
+                and not ops.K16W_ENABLED)
 
     def _trunk_bwd_fused(self, dz, x, rep_outs):
         """K42: the dX GEMM and the one representation layer's backward (K13's) in one launch, g never stored.  Returns
@@ -474,7 +488,10 @@ class FusedActorCritic:
             ws = (torch.empty((G, 256 * lin.in_features), device=dz.device), torch.empty((G, 256), device=dz.device))
             self._partials[key] = ws
         k = self.pair[0].shape[0]
-        ops.s3_gemm_trunk_bwd(dz, self._split_buf(k, "dx", dz.device), k, h, xr, code, slope, ws[0], ws[1])
+        trunk = getattr(x, "trunk", None) if isinstance(x, Rows) else None
+        sign = trunk[5] if trunk is not None and len(trunk) > 5 else None   # K42S: act' from K16R's sign bits
+        ops.s3_gemm_trunk_bwd(dz, self._split_buf(k, "dx", dz.device), k, h, xr, code, slope, ws[0], ws[1],
+                              h_sign=sign)
         self._cq.add(ws[0], lin.weight.grad)
         self._cq.add(ws[1], lin.bias.grad)
         return True

@@ -199,14 +199,15 @@ def s3_gemm(a, b_split, k, out=None):
     return out
 
 
-def s3_gemm_trunk_bwd(dz, b_split, k, h, x, act, slope, partial_dw=None, partial_db=None):
+def s3_gemm_trunk_bwd(dz, b_split, k, h, x, act, slope, partial_dw=None, partial_db=None, h_sign=None):
     """K42: g = dz [rows, k] . B (split) kept in registers; the first representation layer's backward on it (dz1 =
-    g * act'(h), its bias / weight gradients) as per-block partials ([G, 256 * d_in], [G, 256]); g is not stored."""
+    g * act'(h), its bias / weight gradients) as per-block partials ([G, 256 * d_in], [G, 256]); g is not stored.
+    h_sign (int32 [rows, 8], K16R's sign bits; act 0 / 1): K42S, act' from the bits (h is not read, may be None)."""
     L = lib()
     _req(dz, "dz", torch.float32, contiguous=False)
     ldz = _row_stride(dz, "dz", k)
     rows = dz.shape[0]
-    ldh = _row_stride(h, "h", 256)
+    ldh = _row_stride(h, "h", 256) if h_sign is None else 0
     d_in = x.shape[1]
     ldx = _row_stride(x, "x", d_in)
     G = int(L.xpa_s3_gemm_trunk_bwd_num_partials(rows))
@@ -216,6 +217,12 @@ def s3_gemm_trunk_bwd(dz, b_split, k, h, x, act, slope, partial_dw=None, partial
         partial_db = torch.empty(G, 256, dtype=torch.float32, device=dz.device)
     _req(partial_dw, "partial_dw", torch.float32, (G, 256 * d_in))
     _req(partial_db, "partial_db", torch.float32, (G, 256))
+    if h_sign is not None:
+        _req(h_sign, "h_sign", torch.int32, (rows, 8))
+        _lib.check(L.xpa_s3_gemm_trunk_bwd_sign(_p(dz), ldz, _p(b_split), k, _p(h_sign), _p(x), ldx, rows, d_in,
+                                                int(act), float(slope), _p(partial_dw), _p(partial_db),
+                                                _stream(dz.device)), "xpa_s3_gemm_trunk_bwd_sign")
+        return partial_dw, partial_db
     _lib.check(L.xpa_s3_gemm_trunk_bwd(_p(dz), ldz, _p(b_split), k, _p(h), ldh, _p(x), ldx, rows, d_in, int(act),
                                        float(slope), _p(partial_dw), _p(partial_db), _stream(dz.device)),
                "xpa_s3_gemm_trunk_bwd")
@@ -625,9 +632,11 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
     e.g. the halves of a [B, 512] actor|critic pre-activation with a paired workspace); w_*/b_*: output layer
     gemm = (x [B, 256], (w_h_actor, b_h_actor), (w_h_critic, b_h_critic)): K16 — the hidden layers' GEMMs
     run inside the head kernels on the matrix cores and z_actor / z_critic are not used (pass None).
-    trunk = (x_rows [B, d_in], w_in [256, d_in], b_in, slope_in, h_out) with gemm: K16X — the trunk layer
+    trunk = (x_rows [B, d_in], w_in [256, d_in], b_in, slope_in, h_out[, h_sign]) with gemm: K16X — the trunk layer
     Linear(d_in <= TRUNK_DMAX, 256) + the heads' activation is formed inside the launches too; gemm's x must be h_out,
-    which the actor launch writes.  wh_split = (planes of w_h_actor^T, planes of w_h_critic^T) (s3_split): K16P.
+    which the actor launch writes.  wh_split = (planes of w_h_actor^T, planes of w_h_critic^T) (s3_split): K16P; with
+    trunk as well K16R (h formed in both launches' k loops, the actor writes h and, given h_sign int32 [B, 8], its
+    sign bits for K42S).
     (K x 256 / 1 x 256); act_*: (code, slope)
     of the hidden activation.  colsum_queue: an ops.ColsumQueue to defer the column-sum finalizes into
     (flushed by the caller), else they run here.  grads: dict with the gradient views to write — 'w_actor', 'b_actor',
@@ -678,11 +687,32 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
     if trunk is not None:
         if gemm is None or trunk[4] is not x:
             raise ValueError("trunk needs gemm with x = the trunk's h output")
-        xr, w0, b0, slope0, h_out = trunk
+        xr, w0, b0, slope0, h_out = trunk[:5]
+        h_sign = trunk[5] if len(trunk) > 5 else None
         _req(xr, "x_rows", torch.float32)
         din = xr.shape[1]
         if xr.dim() != 2 or xr.shape[0] != B or din > TRUNK_DMAX or tuple(w0.shape) != (H, din):
             raise ValueError("trunk rows must be [%d, <= %d] with w_in [%d, d_in]" % (B, TRUNK_DMAX, H))
+    if trunk is not None and wh_split is not None:
+        # K16R: h formed from the gathered rows inside both launches (Wh as its bf16 planes); the actor writes h
+        # and its sign bits
+        if h_sign is not None:
+            _req(h_sign, "h_sign", torch.int32, (B, 8))
+        wsa, wsc = wh_split
+        _lib.check(L.xpa_head_gemm_s3r_actor(ALGO[algo], DIST[dist], act_actor[0], B, K, H, _p(xr), xr.stride(0), din,
+                                             _p(w0), _p(b0), float(slope0), _p(h_out), h_out.stride(0),
+                                             _p(h_sign) if h_sign is not None else None, _p(wsa), _p(bha), ld,
+                                             _p(w_actor), _p(b_actor), float(act_actor[1]), p_logstd, _p(idx), rows,
+                                             _p(act), p_old, _p(adv), _p(adv_partials), n_adv, float(clip_range),
+                                             float(ent_coef), _p(ws.dz_actor), _p(ws.p_dw_actor), _p(ws.p_dbh_actor),
+                                             _p(ws.p_dbo_actor), _p(ws.loss_partials), W, s), "xpa_head_gemm_s3r_actor")
+        _lib.check(L.xpa_head_gemm_s3r_critic(act_critic[0], B, H, _p(xr), xr.stride(0), din, _p(w0), _p(b0),
+                                              float(slope0), _p(wsc), _p(bhc), ld, _p(w_critic), _p(b_critic),
+                                              float(act_critic[1]), _p(idx), rows, _p(ret), float(vf_coef),
+                                              _p(ws.dz_critic), _p(ws.p_dw_critic), _p(ws.p_dbh_critic),
+                                              _p(ws.p_dbo_critic), _p(ws.loss_partials), W, s),
+                   "xpa_head_gemm_s3r_critic")
+    elif trunk is not None:
         _lib.check(L.xpa_head_gemm_trunk_actor(ALGO[algo], DIST[dist], act_actor[0], B, K, H, _p(xr), xr.stride(0), din,
                                                _p(w0), _p(b0), float(slope0), _p(h_out), h_out.stride(0), _p(wha),
                                                _p(bha), ld, _p(w_actor), _p(b_actor), float(act_actor[1]), p_logstd,
