@@ -192,26 +192,28 @@ def test_trunk_heads_iteration_equals_k13_k16(monkeypatch):
 
 
 def test_s3r_trunk_iteration_equals_k13_k16p(monkeypatch):
-    """The K16R learner wiring (fused_mlp.TRUNK_S3R: the gather-only K13 form; h formed inside both split-GEMM head
-    launches, the actor writing h and its sign bits; K41 on that h; K42S's act' from the bits) against K13's forward +
-    K16P + K42 on h: one whole C2 fast-path iteration from the same seed, every parameter and every update's loss
-    scalars bit for bit."""
+    """The trunk's h and act' three ways, one whole C2 fast-path iteration each from the same seed: K13's forward +
+    K16P + K42 on h (reference), K13 writing h's sign bits + K16P + K42S (the default, fused_mlp.SIGN_BITS), and the
+    K16R wiring (fused_mlp.TRUNK_S3R: the gather-only K13 form; h formed inside both split-GEMM head launches, the actor
+    writing h and its sign bits; K41 on that h; K42S) — every parameter and every update's loss scalars bit for bit."""
     from xuanpolicy_amd import ops
     from xuanpolicy_amd.fused_mlp import FusedActorCritic
     from xuanpolicy_amd.runner import build_synthbox_ppo
     monkeypatch.setattr(ops, "S3_GEMMS", True)
     monkeypatch.setattr(ops, "S3_HEADS", "s3p")
     runs = []
-    for on in (False, True):
-        monkeypatch.setattr(FusedActorCritic, "TRUNK_S3R", on)
+    for s3r, sign in ((False, False), (False, True), (True, True)):
+        monkeypatch.setattr(FusedActorCritic, "TRUNK_S3R", s3r)
+        monkeypatch.setattr(FusedActorCritic, "SIGN_BITS", sign)
         agent = build_synthbox_ppo(n_envs=256, n_steps=32, obs_dim=17, act_dim=6, hidden=256, n_epoch=2,
                                    n_minibatch=4, seed=3, device="cuda:0")
         fm = agent.learner._fused_mlp()
-        assert fm is not None and fm.trunk_heads and fm._s3r_on() == on
+        assert fm is not None and fm.trunk_heads and fm._s3r_on() == s3r
         agent.train(32)
         torch.cuda.synchronize()
-        assert any(isinstance(k, tuple) and k[0] == "hsign" for k in fm._partials) == on
+        assert any(isinstance(k, tuple) and k[0] == "hsign" for k in fm._partials) == (s3r or sign)
         runs.append(([p.detach().clone() for p in agent.policy.parameters()], [dict(i) for i in agent.infos]))
-    (p0, i0), (p1, i1) = runs
-    assert len(p0) == len(p1) and all(torch.equal(a, b) for a, b in zip(p0, p1))
-    assert i0 == i1
+    p0, i0 = runs[0]
+    for p1, i1 in runs[1:]:
+        assert len(p0) == len(p1) and all(torch.equal(a, b) for a, b in zip(p0, p1))
+        assert i0 == i1

@@ -851,3 +851,40 @@ def test_trunk_bwd_sign_equals_h_form(rows, din, code):
     got = ops.s3_gemm_trunk_bwd(dz, bs, 512, None, xr, code, 0.01, h_sign=sign)
     torch.cuda.synchronize()
     assert torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1])
+
+
+@pytest.mark.parametrize("rows,n_rows,din,code", [(4133, 5000, 17, 1), (65536, 70000, 17, 1), (200, 300, 4, 0)])
+def test_thin_gather_sign_form(rows, n_rows, din, code):
+    """xpa_thin_linear_act_fwd_gather_sign: h, the gathered rows and the adv moments bit for bit the gather form's,
+    plus h's sign bits in K42S's byte layout (byte b of a row, bit j = h[row, 32 j + b] > 0)."""
+    from xuanpolicy_amd import ops
+    L, st = ops.lib(), ops._stream()
+    g = torch.Generator(device=DEV).manual_seed(rows + din)
+    flat = torch.randn(n_rows, din, device=DEV, generator=g)
+    idx = torch.randperm(n_rows, device=DEV, generator=g)[:rows].contiguous()
+    idx[rows // 3] = -1
+    w = torch.randn(256, din, device=DEV, generator=g) / 4
+    b = torch.randn(256, device=DEV, generator=g) * 0.1
+    b[3] = -1e9   # a column that is never positive
+    adv = torch.randn(n_rows, device=DEV, generator=g)
+    tiles = (rows + 63) // 64
+    outs = []
+    for sign in (False, True):
+        h = torch.full((rows, 256), 7.0, device=DEV)
+        xo = torch.full((rows, din), 7.0, device=DEV)
+        ap = torch.zeros(2 * tiles, dtype=torch.float64, device=DEV)
+        sg = torch.full((rows + 2, 8), 12345, dtype=torch.int32, device=DEV)
+        args = [code, ops._p(flat), din, n_rows, ops._p(idx), rows, din, 256, ops._p(w), ops._p(b), 0.01, ops._p(h), 256,
+                ops._p(adv), ops._p(ap), ops._p(xo)]
+        if sign:
+            assert L.xpa_thin_linear_act_fwd_gather_sign(*args, ops._p(sg), st) == 0
+        else:
+            assert L.xpa_thin_linear_act_fwd_gather(*args, st) == 0
+        torch.cuda.synchronize()
+        outs.append((h, xo, ap, sg))
+    (h0, x0, a0, _), (h1, x1, a1, sg) = outs
+    assert torch.equal(h0, h1) and torch.equal(x0, x1) and torch.equal(a0, a1)
+    bits = (h1 > 0).view(rows, 8, 32).to(torch.int32)
+    want = (bits << torch.arange(8, device=DEV, dtype=torch.int32).view(1, 8, 1)).sum(1).to(torch.uint8)
+    assert torch.equal(sg[:rows].contiguous().view(torch.uint8).view(rows, 32), want)
+    assert bool((sg[rows:] == 12345).all()), "sign rows past the batch written"

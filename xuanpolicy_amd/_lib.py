@@ -231,6 +231,8 @@ SIGNATURES = {
                                                 c_i64, c_p]),
     "xpa_s3_gemm_trunk_bwd_sign": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, ctypes.c_int,
                                                   c_f32, c_p, c_p, c_p]),
+    "xpa_thin_linear_act_fwd_gather_sign": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_p,
+                                                           c_p, c_f32, c_p, c_i64, c_p, c_p, c_p, c_p, c_p]),
     "xpa_s3_probe": (ctypes.c_int, [ctypes.c_int]),
     "xpa_s3_split_bytes": (c_i64, [c_i64, c_i64]),
     "xpa_s3_split_b": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),

@@ -48,9 +48,11 @@ __global__ __launch_bounds__(256) void thin_fwd_kernel(const float *__restrict__
                                                        const int64_t *__restrict__ idx = nullptr, int64_t n_rows = 0,
                                                        const float *__restrict__ adv = nullptr,
                                                        double *__restrict__ adv_partials = nullptr,
-                                                       float *__restrict__ x_out = nullptr) {
+                                                       float *__restrict__ x_out = nullptr,
+                                                       unsigned *__restrict__ hsign = nullptr) {
     constexpr int kPad = DMAX + 4;  // row stride of the staged x tile (16-B aligned rows)
     __shared__ __attribute__((aligned(16))) float s_x[TILE * kPad];
+    __shared__ unsigned long long s_ball[IDX ? TILE * 4 : 1];   // hsign: each wave's h > 0 ballot per row
     __shared__ int64_t s_src[IDX ? TILE : 1];
     __shared__ double s_red[4];
     const int t = threadIdx.x;
@@ -133,7 +135,31 @@ __global__ __launch_bounds__(256) void thin_fwd_kernel(const float *__restrict__
                 acc = fmaf(xv.z, w[k + 2], acc);
                 acc = fmaf(xv.w, w[k + 3], acc);
             }
-            __builtin_nontemporal_store(act_f<ACT>(acc + bc, slope), h + (r0 + r) * ldh + t);
+            const float hv = act_f<ACT>(acc + bc, slope);
+            __builtin_nontemporal_store(hv, h + (r0 + r) * ldh + t);
+            if (IDX && hsign != nullptr) {
+                const unsigned long long bl = __ballot(hv > 0.f);
+                if ((t & 63) == 0) s_ball[r * 4 + (t >> 6)] = bl;
+            }
+        }
+        if (IDX && hsign != nullptr) {
+            // the sign bits in K42S's lane order: byte b of a row's 32 bytes, bit j = h[row, 32 j + b] > 0 (column
+            // 32 j + b is lane 32 (j & 1) + b of wave j >> 1); thread t writes words 2 (t & 3), + 1 of row t >> 2
+            __syncthreads();
+            const int r = t >> 2;
+            if (r < nr) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int d = 2 * (t & 3) + u;   // bytes 4 d .. 4 d + 3
+                    unsigned word = 0u;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const unsigned v = (unsigned)(s_ball[r * 4 + (j >> 1)] >> (32 * (j & 1) + 4 * d)) & 0xFu;
+                        word |= ((v & 1u) | ((v & 2u) << 7) | ((v & 4u) << 14) | ((v & 8u) << 21)) << j;
+                    }
+                    hsign[(r0 + r) * 8 + d] = word;
+                }
+            }
         }
     }
 }
@@ -423,6 +449,35 @@ XPA_API int xpa_thin_linear_act_fwd_gather(int act, const float *x, int64_t ldx,
     if (act == 0) { XPA_FWDG_D(0) }
     else if (act == 1) { XPA_FWDG_D(1) }
     else { XPA_FWDG_D(2) }
+#undef XPA_FWDG_D
+#undef XPA_FWDG
+    return xpa_launch_status();
+}
+
+// the gather form writing h and its sign bits (h_sign: 32 bytes per row, byte b bit j = h[row, 32 j + b] > 0, the
+// layout xpa_s3_gemm_trunk_bwd_sign reads); h and h_sign required, act 0 / 1 (the bits carry LeakyReLU's act')
+XPA_API int xpa_thin_linear_act_fwd_gather_sign(int act, const float *x, int64_t ldx, int64_t n_rows,
+                                                const int64_t *idx, int64_t rows, int64_t d_in, int64_t d_out,
+                                                const float *w, const float *b, float slope, float *h, int64_t ldh,
+                                                const float *adv, double *adv_partials, float *x_out,
+                                                unsigned *h_sign, xpa_stream_t stream) {
+    if (rows <= 0 || n_rows <= 0 || d_in < 1 || d_in > kMaxIn || d_out != kCols || act < 0 || act > 1 || !x || !idx ||
+        !w || !b || !h || !h_sign || ldx < d_in || ldh < d_out || (adv_partials && !adv))
+        return (int)hipErrorInvalidValue;
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t tiles = (rows + kTile - 1) / kTile;
+    const dim3 grid((unsigned)(tiles < kFwdGrid ? tiles : kFwdGrid));
+    const int dm = dmax_for((int)d_in);
+#define XPA_FWDG(A_, D_)                                                                                             \
+    hipLaunchKernelGGL((thin_fwd_kernel<A_, D_, kTile, true>), grid, dim3(256), 0, s, x, ldx, rows, (int)d_in, w, b,   \
+                       slope, h, ldh, idx, n_rows, adv, adv_partials, x_out, h_sign)
+#define XPA_FWDG_D(A_)                 \
+    if (dm == 8) XPA_FWDG(A_, 8);      \
+    else if (dm == 20) XPA_FWDG(A_, 20); \
+    else if (dm == 32) XPA_FWDG(A_, 32); \
+    else XPA_FWDG(A_, 64);
+    if (act == 0) { XPA_FWDG_D(0) }
+    else { XPA_FWDG_D(1) }
 #undef XPA_FWDG_D
 #undef XPA_FWDG
     return xpa_launch_status();

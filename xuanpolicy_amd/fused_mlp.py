@@ -96,6 +96,7 @@ class Rows:
         self.flat, self.idx = flat, idx
         self.gathered = None   # set by the gather forward: the rows as a contiguous [B, d] copy
         self.trunk = None      # K16X: (gathered rows, W0, b0, slope, h out) when the head launches form h
+        self.hsign = None      # K13's sign bits of h (int32 [B, 8]) for K42S
         self.shape = (idx.shape[0], flat.shape[1])
         self.device = flat.device
         self.dtype = flat.dtype
@@ -192,12 +193,18 @@ class FusedActorCritic:
             if deferred:
                 x.trunk = (x.gathered, lin.weight, lin.bias, slope, h)
                 if self._s3r_on() and code in (0, 1):   # K16R's sign bits of h for K42S (act' without reading h)
-                    key = ("hsign", B)
-                    sign = self._partials.get(key)
-                    if sign is None:
-                        sign = torch.empty((B, 8), dtype=torch.int32, device=x.device)
-                        self._partials[key] = sign
-                    x.trunk = x.trunk + (sign,)
+                    x.trunk = x.trunk + (self._sign_buf(B, x.device),)
+            x.hsign = None
+            if not deferred and defer_trunk and self._sign_on(code):
+                # K13 writes h's sign bits beside h: K42S's act' (32 B per row read instead of h's 1 KiB)
+                x.hsign = self._sign_buf(B, x.device)
+                _lib.check(ops.lib().xpa_thin_linear_act_fwd_gather_sign(
+                    code, ops._p(x.flat), x.flat.stride(0), x.flat.shape[0], ops._p(x.idx), B, lin.in_features,
+                    lin.out_features, ops._p(lin.weight), ops._p(lin.bias), slope, ops._p(h), h.stride(0),
+                    ops._p(adv) if adv_partials is not None else None,
+                    ops._p(adv_partials) if adv_partials is not None else None, ops._p(x.gathered),
+                    ops._p(x.hsign), ops._stream(x.device)), "xpa_thin_linear_act_fwd_gather_sign")
+                return [h] + self._chain_forward(self.rep[1:], h)
             _lib.check(ops.lib().xpa_thin_linear_act_fwd_gather(
                 code, ops._p(x.flat), x.flat.stride(0), x.flat.shape[0], ops._p(x.idx), B, lin.in_features,
                 lin.out_features, ops._p(lin.weight), ops._p(lin.bias), slope, None if deferred else ops._p(h),
@@ -460,11 +467,27 @@ class FusedActorCritic:
     FUSE_TRUNK_BWD = True   # K42 where it applies (ops.S3_GEMMS, one thin representation layer)
     # K16R where it applies (the split heads, one thin representation layer with the heads' activation): h formed
     # inside both head launches from the gathered rows (K13 only gathers), the actor writes h and its sign bits
-    TRUNK_S3R = True
+    # (r04n: K16R measured slower at C2 — actor 132 / critic 108 us vs K16P's 80 / 63 on h from HBM: the in-loop trunk
+    # FMAs are not hidden behind the MFMAs — so it is an opt-in)
+    TRUNK_S3R = False
+    # K42S by default: K13's gather form writes h's sign bits beside h and K42 reads them instead of h
+    SIGN_BITS = True
 
     def _s3r_on(self):
         return (self.TRUNK_S3R and self.trunk_heads and ops.S3_GEMMS and ops.S3_HEADS == "s3p"
                 and not ops.K16W_ENABLED)
+
+    def _sign_on(self, code):
+        return (self.SIGN_BITS and self.FUSE_TRUNK_BWD and code in (0, 1) and len(self.rep) == 1 and self.pair is not None
+                and self._dx_split_ok(self.pair[0]) and self.rep[0][0].in_features <= 32)
+
+    def _sign_buf(self, B, device):
+        key = ("hsign", B)
+        sign = self._partials.get(key)
+        if sign is None:   # graph-capture safe: allocated on first (eager) use
+            sign = torch.empty((B, 8), dtype=torch.int32, device=device)
+            self._partials[key] = sign
+        return sign
 
     def _trunk_bwd_fused(self, dz, x, rep_outs):
         """K42: the dX GEMM and the one representation layer's backward (K13's) in one launch, g never stored.  Returns
@@ -490,6 +513,8 @@ class FusedActorCritic:
         k = self.pair[0].shape[0]
         trunk = getattr(x, "trunk", None) if isinstance(x, Rows) else None
         sign = trunk[5] if trunk is not None and len(trunk) > 5 else None   # K42S: act' from K16R's sign bits
+        if sign is None and isinstance(x, Rows):
+            sign = getattr(x, "hsign", None)   # or from K13's
         ops.s3_gemm_trunk_bwd(dz, self._split_buf(k, "dx", dz.device), k, h, xr, code, slope, ws[0], ws[1],
                               h_sign=sign)
         self._cq.add(ws[0], lin.weight.grad)
