@@ -646,7 +646,7 @@ typedef __attribute__((address_space(3))) char lds_char_t;
 // DMA — i.e. before each chunk's fragment reads, draining the ring; here the waits are the counted ones
 // of the k-loop (and its last chunk waits vmcnt(0), so no compiler-counted wait after the loop is short).
 __device__ __forceinline__ void glds16(const float *g, unsigned lds_wave_base) {
-#if XPA_HEAD_PROBE == 6  // 6 = the GEMM without its operand DMAs (MFMA stream on stale LDS)
+#if XPA_HEAD_PROBE == 6 || XPA_HEAD_PROBE == 9  // 6 = the GEMM without its operand DMAs (MFMA stream on stale LDS)
     asm volatile("" ::"v"(g), "s"(lds_wave_base) : "memory");
     return;
 #endif
@@ -770,8 +770,15 @@ __device__ __forceinline__ void gemm_chunk_s3p(const char *st, f32x16 (&acc)[2][
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
         const float *pa = A + (rt * 32 + i) * kKC;
+#if XPA_HEAD_PROBE == 8 || XPA_HEAD_PROBE == 9  // 8 = K16P without the A split (f32 bits fed as bf16); 9 = also no DMAs
+        const float4 lo = *reinterpret_cast<const float4 *>(pa + olo), hi = *reinterpret_cast<const float4 *>(pa + ohi);
+        ah[rt] = __builtin_bit_cast(xpa_bf16x8, lo);
+        am[rt] = __builtin_bit_cast(xpa_bf16x8, hi);
+        al[rt] = __builtin_bit_cast(xpa_bf16x8, lo);
+#else
         xpa_split8(*reinterpret_cast<const float4 *>(pa + olo), *reinterpret_cast<const float4 *>(pa + ohi), ah[rt],
                    am[rt], al[rt]);
+#endif
     }
     const xpa_bf16x8 *bimg = reinterpret_cast<const xpa_bf16x8 *>(st + 4096) + lane;
 #pragma unroll
