@@ -54,7 +54,7 @@ def parse():
     p.add_argument("--gemm", choices=("f32", "split3"), default="split3",
                    help="the update's hidden-layer GEMMs: f32 MFMA (K16 + hipBLASLt) or the bf16 three-way split "
                         "(K16S + K40 + K41, the f32 GEMM's accuracy on the bf16 matrix cores)")
-    p.add_argument("--s3-heads", choices=("s3", "s3p"), default="s3p",
+    p.add_argument("--s3-heads", choices=("s3", "s3p", "s3q"), default="s3p",
                    help="with --gemm split3: K16S (both fragments split in the k loop) or K16P (Wh's planes split once)")
     p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc HBM-traffic passes")
     p.add_argument("--no-rocprof", action="store_true",
@@ -1033,7 +1033,7 @@ def main():
                        "num_envs_per_gpu": N, "horizon": T, "global_envs": N * world, "minibatch": B,
                        "update_gemms": ("f32 GEMMs as exact three-way bf16 splits on the bf16 matrix cores (%s heads, "
                                         "K40 dX, K41V dW; error <= 2x the f32 GEMM's vs f64: tests/test_gpu_sgemm3.py)"
-                                        % ("K16P" if ops.S3_HEADS == "s3p" else "K16S")
+                                        % {"s3p": "K16P", "s3q": "K16Q"}.get(ops.S3_HEADS, "K16S")
                                         if ops.S3_GEMMS else "f32 MFMA (K16 heads, hipBLASLt dX / dW)"),
                        "updates_per_step": args.n_epoch * args.n_minibatch,
                        "parallelism": ("dp1 (one env shard, no collective)" if world == 1 else

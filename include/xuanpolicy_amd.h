@@ -549,6 +549,20 @@ int xpa_head_gemm_s3p_critic(int act, int64_t batch, int64_t hidden, const float
                              const float *b, float slope, const int64_t *idx, int64_t n_rows, const float *ret,
                              float vf_coef, float *dz, float *partial_dw, float *partial_db_hidden,
                              float *partial_db_out, float *loss_partials, int64_t loss_width, xpa_stream_t stream);
+/* K16Q (r04) — K16P's arguments and outputs bit for bit with the waves tiled 32 rows x 128 columns (one A fragment
+ * split per wave and chunk instead of two). */
+int xpa_head_gemm_s3q_actor(int algo, int dist, int act, int64_t batch, int64_t act_dim, int64_t hidden, const float *x,
+                            int64_t ldx, const float *w_hidden_split, const float *b_hidden, int64_t ld_dz,
+                            const float *w, const float *b, float slope, const float *logstd, const int64_t *idx,
+                            int64_t n_rows, const float *act_buf, const float *old_logp, const float *adv,
+                            const double *adv_partials, int64_t n_adv_partials, float clip_range, float ent_coef,
+                            float *dz, float *partial_dw, float *partial_db_hidden, float *partial_db_out,
+                            float *loss_partials, int64_t loss_width, xpa_stream_t stream);
+int xpa_head_gemm_s3q_critic(int act, int64_t batch, int64_t hidden, const float *x, int64_t ldx,
+                             const float *w_hidden_split, const float *b_hidden, int64_t ld_dz, const float *w,
+                             const float *b, float slope, const int64_t *idx, int64_t n_rows, const float *ret,
+                             float vf_coef, float *dz, float *partial_dw, float *partial_db_hidden,
+                             float *partial_db_out, float *loss_partials, int64_t loss_width, xpa_stream_t stream);
 
 /* K16X — K16 with the representation's first layer Linear(d_in <= 20, 256) + activation `act` (K13's, bit for bit)
  * in the prologue: each block forms its tile's h rows from the minibatch's gathered observation rows x_rows

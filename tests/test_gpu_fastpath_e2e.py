@@ -83,7 +83,7 @@ def test_fast_path_iteration_with_k16w_matches_oracle(agent_name, discrete, A, m
 
 
 @pytest.mark.parametrize("agent_name,discrete,A,heads", [("PPO_Clip", False, 6, "s3"), ("A2C", True, 18, "s3"),
-                                                         ("PPO_Clip", False, 6, "s3p")])
+                                                         ("PPO_Clip", False, 6, "s3p"), ("A2C", True, 8, "s3q")])
 def test_fast_path_iteration_with_split_gemms_matches_oracle(agent_name, discrete, A, heads, monkeypatch):
     """The same end-to-end replay with the update's hidden-layer GEMMs on the bf16 matrix cores by the three-way
     split (ops.S3_GEMMS: K16S heads, K40 dX, K41 dW slices into the f64 finalize): every update's loss within 1e-4
@@ -102,7 +102,7 @@ def test_fast_path_iteration_with_split_gemms_matches_oracle(agent_name, discret
     agent.train(T - 1, log=False)
     assert any(k[0] == "s3wgrad" for k in fm._partials if isinstance(k, tuple)), "K41 not used"
     assert any(k[0] == "s3split" for k in fm._partials if isinstance(k, tuple)), "K40 not used"
-    if heads == "s3p":
+    if heads in ("s3p", "s3q"):
         assert any(k[:2] == ("s3split", "s3p_a") for k in fm._partials if isinstance(k, tuple)), "K16P not used"
         assert any(k[0] == "hsign" for k in fm._partials if isinstance(k, tuple)), "K16R / K42S not used"
     assert any(k[0] == "k42" for k in fm._partials if isinstance(k, tuple)), "K42 not used"

@@ -888,3 +888,50 @@ def test_thin_gather_sign_form(rows, n_rows, din, code):
     want = (bits << torch.arange(8, device=DEV, dtype=torch.int32).view(1, 8, 1)).sum(1).to(torch.uint8)
     assert torch.equal(sg[:rows].contiguous().view(torch.uint8).view(rows, 32), want)
     assert bool((sg[rows:] == 12345).all()), "sign rows past the batch written"
+
+
+@pytest.mark.parametrize("algo,dist,K,B,code", [("ppo", "gaussian", 6, 4133, 1), ("a2c", "categorical", 8, 777, 0),
+                                                ("ppo", "gaussian", 6, 65536, 1), ("ppo", "categorical", 4, 193, 2)])
+def test_head_gemm_s3q_equals_s3p(algo, dist, K, B, code):
+    """K16Q (32 x 128 wave tiles) == K16P bit for bit: dz and every partial (each output's accumulation chain and the
+    epilogue are the same, only which wave computes it differs)."""
+    from xuanpolicy_amd import ops
+    L, s = ops.lib(), ops._stream()
+    g = torch.Generator(device=DEV).manual_seed(B + K + 7)
+    H, R = 256, B + 300
+    x = torch.randn(B, H, device=DEV, generator=g)
+    wh_a, wh_c = (torch.randn(H, H, device=DEV, generator=g) / 16 for _ in range(2))
+    bh_a, bh_c = (torch.randn(H, device=DEV, generator=g) * 0.1 for _ in range(2))
+    w_a = torch.randn(K, H, device=DEV, generator=g) / 16
+    b_a = torch.randn(K, device=DEV, generator=g) * 0.1
+    w_c = torch.randn(1, H, device=DEV, generator=g) / 16
+    b_c = torch.randn(1, device=DEV, generator=g) * 0.1
+    logstd = (-1 + 0.1 * torch.randn(K, device=DEV, generator=g)) if dist == "gaussian" else None
+    idx = torch.randperm(R, device=DEV, generator=g)[:B].contiguous()
+    idx[B // 2] = -1
+    adv, ret = torch.randn(R, device=DEV, generator=g), torch.randn(R, device=DEV, generator=g)
+    act = (torch.randn(R, K, device=DEV, generator=g) * 0.5 if dist == "gaussian"
+           else torch.randint(0, K, (R,), device=DEV, generator=g).float())
+    old = -1.5 + 0.3 * torch.randn(R, device=DEV, generator=g) if algo == "ppo" else None
+    wsa, wsc = ops.s3_split(wh_a.t()), ops.s3_split(wh_c.t())
+    G = int(L.xpa_head_fused_num_partials(B))
+    W = int(L.xpa_loss_partial_width(K))
+    p = ops._p
+
+    def run(form):
+        assert L.xpa_lds_poison(s) == 0
+        dz = torch.full((B, 2 * H), 777.0, device=DEV)
+        parts = [torch.full((G, n), 555.0, device=DEV) for n in (K * H, H, K, H, H, 1)]
+        lp = torch.zeros(G, W, device=DEV)
+        fa, fc = getattr(L, "xpa_head_gemm_%s_actor" % form), getattr(L, "xpa_head_gemm_%s_critic" % form)
+        assert fa(ops.ALGO[algo], ops.DIST[dist], code, B, K, H, p(x), H, p(wsa), p(bh_a), 2 * H, p(w_a), p(b_a), 0.01,
+                  p(logstd) if logstd is not None else None, p(idx), R, p(act), p(old) if old is not None else None,
+                  p(adv), None, 0, 0.2, 0.01, p(dz), p(parts[0]), p(parts[1]), p(parts[2]), p(lp), W, s) == 0
+        assert fc(code, B, H, p(x), H, p(wsc), p(bh_c), 2 * H, p(w_c), p(b_c), 0.01, p(idx), R, p(ret), 0.25,
+                  p(dz[:, H:]), p(parts[3]), p(parts[4]), p(parts[5]), p(lp), W, s) == 0
+        torch.cuda.synchronize()
+        return [dz] + parts + [lp]
+
+    ref, got = run("s3p"), run("s3q")
+    for i, (a_, b_) in enumerate(zip(ref, got)):
+        assert torch.equal(a_, b_), i

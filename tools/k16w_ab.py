@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--out", default=None)
     ap.add_argument("--probe", action="store_true", help="also time K16W with parts switched off")
+    ap.add_argument("--forms", default="k16,k16w,k16s,k16p,k16q")
     a = ap.parse_args()
     import torch
     from xuanpolicy_amd import ops
@@ -47,22 +48,23 @@ def main():
     lp = torch.zeros(G, Wd, device=dev)
     p = ops._p
 
-    pre = {False: "xpa_head_gemm_", True: "xpa_head_gemm_ws_", "s3": "xpa_head_gemm_s3_", "s3p": "xpa_head_gemm_s3p_"}
+    pre = {False: "xpa_head_gemm_", True: "xpa_head_gemm_ws_", "s3": "xpa_head_gemm_s3_", "s3p": "xpa_head_gemm_s3p_", "s3q": "xpa_head_gemm_s3q_"}
     sp_a, sp_c = ops.s3_split(wh_a.t()), ops.s3_split(wh_c.t())   # K16P: Wh^T's planes
 
     def actor(ws):
         f = getattr(L, pre[ws] + "actor")
-        return f(0, 0, 1, B, K, H, p(x), H, p(sp_a) if ws == "s3p" else p(wh_a), p(bh_a), 2 * H, p(w_a), p(b_a), 0.01, p(logstd), p(idx), R,
+        return f(0, 0, 1, B, K, H, p(x), H, p(sp_a) if ws in ("s3p", "s3q") else p(wh_a), p(bh_a), 2 * H, p(w_a), p(b_a), 0.01, p(logstd), p(idx), R,
                  p(act), p(old), p(adv), None, 0, 0.2, 0.0, p(dz), p(parts[0]), p(parts[1]), p(parts[2]), p(lp), Wd, s)
 
     def critic(ws):
         f = getattr(L, pre[ws] + "critic")
-        return f(1, B, H, p(x), H, p(sp_c) if ws == "s3p" else p(wh_c), p(bh_c), 2 * H, p(w_c), p(b_c), 0.01, p(idx), R, p(ret), 0.25,
+        return f(1, B, H, p(x), H, p(sp_c) if ws in ("s3p", "s3q") else p(wh_c), p(bh_c), 2 * H, p(w_c), p(b_c), 0.01, p(idx), R, p(ret), 0.25,
                  p(dz[:, H:]), p(parts[3]), p(parts[4]), p(parts[5]), p(lp), Wd, s)
 
     res = {}
     for _ in range(a.rounds):
-        for ws in (False, True, "s3", "s3p"):
+        fmap = {"k16": False, "k16w": True, "k16s": "s3", "k16p": "s3p", "k16q": "s3q"}
+        for ws in [fmap[f] for f in a.forms.split(",")]:
             for name, fn in (("actor", actor), ("critic", critic)):
                 assert fn(ws) == 0
                 torch.cuda.synchronize()
@@ -73,7 +75,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) * 1e3 / a.reps
-                res.setdefault("%s_%s" % ({False: "k16", True: "k16w", "s3": "k16s", "s3p": "k16p"}[ws], name), []).append(round(us, 2))
+                res.setdefault("%s_%s" % ({False: "k16", True: "k16w", "s3": "k16s", "s3p": "k16p", "s3q": "k16q"}[ws], name), []).append(round(us, 2))
     if a.probe:   # K16W with parts switched off (xpa_head_gemm_ws_probe): 1 no epilogue, 2 no MFMA, 4 no DMA
         for mask in (1, 2, 4, 5, 3, 6, 7):
             assert L.xpa_head_gemm_ws_probe(mask) == 0

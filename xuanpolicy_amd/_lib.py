@@ -215,6 +215,11 @@ SIGNATURES = {
                                               c_f32, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64, c_p]),
     "xpa_head_gemm_s3p_critic": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_f32,
                                                c_p, c_i64, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64, c_p]),
+    "xpa_head_gemm_s3q_actor": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_i64,
+                                              c_p, c_p, c_i64, c_p, c_p, c_f32, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64,
+                                              c_f32, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64, c_p]),
+    "xpa_head_gemm_s3q_critic": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_f32,
+                                               c_p, c_i64, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64, c_p]),
     "xpa_head_gemm_trunk_actor": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_i64, c_i64, c_i64, c_p, c_i64,
                                                  c_i64, c_p, c_p, c_f32, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_f32, c_p,
                                                  c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_f32, c_f32, c_p, c_p, c_p, c_p,

@@ -790,6 +790,27 @@ __device__ __forceinline__ void gemm_chunk_s3p(const char *st, f32x16 (&acc)[2][
     }
 }
 
+// K16Q (r04): K16P's operands with the waves tiled 2 x 2 over the [64 x 256] tile as 32 rows x 128 columns each
+// (row tile wave & 1, column blocks 4 (wave >> 1) .. + 3) instead of 64 rows x 64 columns: each wave splits ONE A
+// fragment per chunk (K16P: both row tiles, so every A value was split by all 4 waves) and reads 4 B column blocks'
+// planes (ds_read_b128, no VALU).  Every output's accumulation chain is K16P's: bit for bit the same dz / partials.
+__device__ __forceinline__ void gemm_chunk_s3q(const char *st, f32x16 (&acc)[2][2], int lane, int wave) {
+    const float *A = reinterpret_cast<const float *>(st);
+    const int h = lane >> 5, i = lane & 31;
+    const int sw = (i >> 2) & 3;
+    const float *pa = A + ((wave & 1) * 32 + i) * kKC;
+    xpa_bf16x8 ah, am, al;
+    xpa_split8(*reinterpret_cast<const float4 *>(pa + 4 * (h ^ sw)),
+               *reinterpret_cast<const float4 *>(pa + 4 * ((h + 2) ^ sw)), ah, am, al);
+    const xpa_bf16x8 *bimg = reinterpret_cast<const xpa_bf16x8 *>(st + 4096) + lane;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int cb = 4 * (wave >> 1) + j;
+        acc[j >> 1][j & 1] = xpa_mfma_s3(ah, am, al, bimg[cb * 64], bimg[(8 + cb) * 64], bimg[(16 + cb) * 64],
+                                         acc[j >> 1][j & 1]);
+    }
+}
+
 // K16R (r04): K16P with the A operand (the trunk activations h) formed in the k loop instead of read from HBM:
 // h = act(x W0^T + b0) for the tile's 64 rows, the representation's one thin layer (K13's Linear(d_in <= 20, 256) +
 // activation, its fmaf chain over the zero-padded inputs: the same bits as K13's h).  Thread t owns row t >> 2 of
@@ -1000,7 +1021,7 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
                 hmask[xrow * 8 + q] = sgn[0];
                 hmask[xrow * 8 + 4 + q] = sgn[1];
             }
-        } else if constexpr (S3 == 2) {   // K16P: Wh arrives as its three bf16 planes (the pointer is the split buffer)
+        } else if constexpr (S3 == 2 || S3 == 4) {   // K16P / K16Q: Wh arrives as its three bf16 planes (the split buffer)
             const char *wsp = reinterpret_cast<const char *>(Wh);
             gemm_issue_p(lds_base, xa, lda, wsp, r0, batch, 0, lane, wave);
 #pragma unroll 1
@@ -1010,7 +1031,8 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
                 if (c + 1 < kChunks)
                     gemm_issue_p(lds_base + ((c + 1) & 1) * kPStageB, xa, lda, wsp, r0, batch, c + 1, lane, wave);
 #if XPA_HEAD_PROBE != 3
-                gemm_chunk_s3p(reinterpret_cast<const char *>(smem) + (c & 1) * kPStageB, acc, lane, wave);
+                if constexpr (S3 == 4) gemm_chunk_s3q(reinterpret_cast<const char *>(smem) + (c & 1) * kPStageB, acc, lane, wave);
+                else gemm_chunk_s3p(reinterpret_cast<const char *>(smem) + (c & 1) * kPStageB, acc, lane, wave);
 #endif
             }
         } else {
@@ -1038,11 +1060,14 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
         for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct) {
-                const int col = wave * 64 + ct * 32 + (lane & 31);
-                const float bc = ct ? bh1 : bh0;
+                // K16Q: acc[a][b] is column block 2 a + b of the wave's 128 columns, rows of row tile wave & 1
+                const int col = S3 == 4 ? (wave >> 1) * 128 + (2 * rt + ct) * 32 + (lane & 31)
+                                        : wave * 64 + ct * 32 + (lane & 31);
+                const float bc = S3 == 4 ? bh[col] : ct ? bh1 : bh0;
+                const int row0 = S3 == 4 ? (wave & 1) * 32 : rt * 32;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                    const int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                     smem[row * kS + col] = act_f<ACT>(acc[rt][ct][r] + bc, slope);
                 }
             }
@@ -1228,7 +1253,7 @@ namespace {
 #define XPA_HEAD_ARGS(a) a.batch, a.K, a.ld, a.z, a.ldx, a.Wh, a.bh, a.W, a.bias, a.slope, a.logstd, a.idx, a.n_rows, a.act, a.old_logp, a.adv, a.ret, a.adv_partials, a.n_adv_partials, a.clip_range, a.ent_coef, a.vf_coef, a.dz, a.p_dw, a.p_dbh, a.p_dbo, a.p_loss, a.loss_width
 // KIND: 0 K12 (z from HBM), 1 K16 (hidden GEMM inside), 2 K16X (trunk layer + hidden GEMM inside), 3 K16W,
 // 4 K16S (K16 with the hidden GEMM on the bf16 matrix cores by the three-way split), 5 K16P (K16S with Wh pre-split),
-// 6 K16R (K16P with h formed from the gathered rows in the k loop)
+// 6 K16R (K16P with h formed from the gathered rows in the k loop), 7 K16Q (K16P with 32 x 128 wave tiles)
 template <int KIND, int MODE, int ALGO, int ACT, int KMAX>
 void launch_one(const HeadArgs &a, hipStream_t s) {
     const dim3 grid((unsigned)xpa_head_fused_num_partials(a.batch)), block(256);
@@ -1245,6 +1270,9 @@ void launch_one(const HeadArgs &a, hipStream_t s) {
     else if constexpr (KIND == 2)
         hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, true>), grid, block, 0, s, XPA_HEAD_ARGS(a), a.xr,
                            a.ldxr, a.din, a.W0, a.b0, a.slope0, a.hout, a.ldh, nullptr);
+    else if constexpr (KIND == 7)
+        hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, false, 4>), grid, block, 0, s, XPA_HEAD_ARGS(a),
+                           nullptr, (int64_t)0, 0, nullptr, nullptr, 0.f, nullptr, (int64_t)0, nullptr);
     else if constexpr (KIND == 6)
         hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, false, 3>), grid, block, 0, s, XPA_HEAD_ARGS(a),
                            a.xr, a.ldxr, a.din, a.W0, a.b0, a.slope0, a.hout, a.ldh, a.hmask);
@@ -1408,6 +1436,9 @@ XPA_API int xpa_head_gemm_s3_critic(XPA_GEMM_CRITIC_PARAMS) { return gemm_critic
 // K16P: as K16S with w_hidden = the split buffer of Wh^T (xpa_s3_split_b(Wh, 256, 256, 1, 256, ...))
 XPA_API int xpa_head_gemm_s3p_actor(XPA_GEMM_ACTOR_PARAMS) { return gemm_actor_entry<5>(XPA_GEMM_ACTOR_ARGS); }
 XPA_API int xpa_head_gemm_s3p_critic(XPA_GEMM_CRITIC_PARAMS) { return gemm_critic_entry<5>(XPA_GEMM_CRITIC_ARGS); }
+// K16Q: K16P's arguments and outputs bit for bit, the waves tiled 32 x 128 (one A fragment split per wave and chunk)
+XPA_API int xpa_head_gemm_s3q_actor(XPA_GEMM_ACTOR_PARAMS) { return gemm_actor_entry<7>(XPA_GEMM_ACTOR_ARGS); }
+XPA_API int xpa_head_gemm_s3q_critic(XPA_GEMM_CRITIC_PARAMS) { return gemm_critic_entry<7>(XPA_GEMM_CRITIC_ARGS); }
 
 // K16W entries: xpa_head_gemm_actor / _critic's arguments and outputs (the same partial-row count, rows the grid does
 // not own written as zeros); act_dim <= 8.

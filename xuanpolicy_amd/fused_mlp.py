@@ -362,7 +362,7 @@ class FusedActorCritic:
         splits = []   # (matrix, name): every split this update needs, one launch (xpa_s3_split_batch)
         if z_a is None:   # K16
             gemm = (s, (lin_ah.weight, lin_ah.bias), (lin_ch.weight, lin_ch.bias))
-            if ops.S3_GEMMS and ops.S3_HEADS == "s3p" and not ops.K16W_ENABLED:   # K16P: Wh^T's planes, once per update
+            if ops.S3_GEMMS and ops.S3_HEADS in ("s3p", "s3q") and not ops.K16W_ENABLED:   # K16P / K16Q: Wh^T's planes
                 splits += [(lin_ah.weight.t(), "s3p_a"), (lin_ch.weight.t(), "s3p_c")]
         if paired and len(self.rep) > 0 and self._dx_split_ok(self.pair[0]):
             splits.append((self.pair[0], "dx"))
@@ -474,7 +474,7 @@ class FusedActorCritic:
     SIGN_BITS = True
 
     def _s3r_on(self):
-        return (self.TRUNK_S3R and self.trunk_heads and ops.S3_GEMMS and ops.S3_HEADS == "s3p"
+        return (self.TRUNK_S3R and self.trunk_heads and ops.S3_GEMMS and ops.S3_HEADS in ("s3p", "s3q")
                 and not ops.K16W_ENABLED)
 
     def _sign_on(self, code):

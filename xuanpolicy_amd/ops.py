@@ -619,7 +619,8 @@ K16W_ENABLED = False  # fused_heads' gemm form: K16W (xpa_head_gemm_ws_*) where 
 # The update's hidden-layer GEMMs on the bf16 matrix cores by the three-way split (K16S heads, K40 dX, K41 dW):
 # the f32 GEMM's accuracy, not the f32 MFMA's bits.  Read when a learner's update is built / captured.
 S3_GEMMS = True
-S3_HEADS = "s3p"   # with S3_GEMMS: "s3" K16S (both fragments split in the k loop), "s3p" K16P (Wh's planes split once)
+S3_HEADS = "s3p"   # with S3_GEMMS: "s3" K16S (both fragments split in the k loop), "s3p" K16P (Wh's planes split once),
+                   # "s3q" K16Q (K16P's bits, 32 x 128 wave tiles)
 
 
 def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, w_critic, b_critic, act_critic,
@@ -731,8 +732,11 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
         fa = L.xpa_head_gemm_ws_actor if wsa else L.xpa_head_gemm_s3_actor if S3_GEMMS else L.xpa_head_gemm_actor
         fc = (L.xpa_head_gemm_ws_critic if K16W_ENABLED else L.xpa_head_gemm_s3_critic if S3_GEMMS
               else L.xpa_head_gemm_critic)
-        if wh_split is not None and not wsa and not K16W_ENABLED:   # K16P: the hidden weights as their bf16 planes
-            fa, fc = L.xpa_head_gemm_s3p_actor, L.xpa_head_gemm_s3p_critic
+        if wh_split is not None and not wsa and not K16W_ENABLED:   # K16P / K16Q: the hidden weights as bf16 planes
+            if S3_HEADS == "s3q":
+                fa, fc = L.xpa_head_gemm_s3q_actor, L.xpa_head_gemm_s3q_critic
+            else:
+                fa, fc = L.xpa_head_gemm_s3p_actor, L.xpa_head_gemm_s3p_critic
             wha, whc = wh_split
         _lib.check(fa(ALGO[algo], DIST[dist], act_actor[0], B, K, H, _p(x), x.stride(0), _p(wha),
                       _p(bha), ld, _p(w_actor), _p(b_actor), float(act_actor[1]), p_logstd, _p(idx),
