@@ -299,10 +299,11 @@ constexpr int kMaxSegs = 16;
 constexpr int kWideTile = kColTile * kColGroups;
 constexpr int kWideMaxG = 32;
 
-// Segments with 32 < G <= 256 (K41's 64 weight-gradient slices over C = 131 072): 256-column tiles, 4 row groups of
-// 256 threads (rows grp, grp + 4, ...; 16 loads in flight), the groups added in order in f64 — r04: the 64-column
-// tiles of colsum_tile took 32 us for K41's 32 MiB.
-constexpr int kMidTile = 256;
+// Segments with 32 < G <= 256 (K41's 64 weight-gradient slices over C = 131 072): 512-column tiles, 4 row groups of
+// 256 threads (rows grp, grp + 4, ...; 2 columns c, c + 256 per thread, 16 loads in flight each), the groups added in
+// order in f64 — r04: the 64-column tiles of colsum_tile took 32 us for K41's 32 MiB; 256-column tiles (one column per
+// thread) 20 us, their 512 blocks + the other segments' spilling into a second round of blocks (2 per CU).
+constexpr int kMidTile = 512;
 constexpr int kMidMaxG = 256;
 __host__ __device__ inline int64_t seg_tiles(int64_t G, int64_t C) {
     return G <= kWideMaxG ? (C + kWideTile - 1) / kWideTile
@@ -363,35 +364,49 @@ __device__ __forceinline__ void colsum_batch_tile(const ColsumBatch &b, int tile
             }
         }
     } else if (b.G[sg] <= kMidMaxG) {
-        static_assert(kColGroups * kColTile == 4 * kMidTile, "the mid path reuses s_red as [4][256]");
-        auto s4 = reinterpret_cast<double(*)[kMidTile]>(s_red);
+        static_assert(kColGroups * kColTile == 4 * 256, "the mid path reuses s_red as [4][256]");
+        auto s4 = reinterpret_cast<double(*)[256]>(s_red);
         const int64_t G = b.G[sg];
         const int C = b.C[sg];
-        const int grp = threadIdx.x >> 8, lc = threadIdx.x & (kMidTile - 1);
-        const int c = (tile - b.tile0[sg]) * kMidTile + lc;
+        const int grp = threadIdx.x >> 8, lc = threadIdx.x & 255;
+        const int c0 = (tile - b.tile0[sg]) * kMidTile + lc;
         const float *part = b.part[sg];
-        double acc = 0.0;
-        if (c < C) {
+        double acc[2] = {0.0, 0.0};
+        {
             int64_t k = grp;
-            for (; k + 15 * 4 < G; k += 16 * 4) {  // 16 loads in flight, added in row order
-                float a[16];
+            for (; k + 15 * 4 < G; k += 16 * 4) {  // 2 x 16 loads in flight, each column added in row order
+                float a[2][16];
 #pragma unroll
-                for (int u = 0; u < 16; ++u) a[u] = part[(k + 4 * u) * C + c];
+                for (int h = 0; h < 2; ++h) {
+                    const int c = min(c0 + 256 * h, C - 1);
 #pragma unroll
-                for (int u = 0; u < 16; ++u) acc += (double)a[u];
+                    for (int u = 0; u < 16; ++u) a[h][u] = part[(k + 4 * u) * C + c];
+                }
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) acc[h] += (double)a[h][u];
             }
-            for (; k < G; k += 4) acc += (double)part[k * C + c];
+            for (; k < G; k += 4) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) acc[h] += (double)part[k * C + min(c0 + 256 * h, C - 1)];
+            }
         }
-        s4[grp][lc] = acc;
-        __syncthreads();
-        float o = 0.f;
-        if (grp == 0 && c < C) {
-            o = (float)(((s4[0][lc] + s4[1][lc]) + s4[2][lc]) + s4[3][lc]);
-            b.out[sg][c] = o;
+        float o[2] = {0.f, 0.f};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {   // the 4 groups of column set h, added in order
+            if (h) __syncthreads();       // set 0's s4 reads done
+            s4[grp][lc] = acc[h];
+            __syncthreads();
+            const int c = c0 + 256 * h;
+            if (grp == 0 && c < C) {
+                o[h] = (float)(((s4[0][lc] + s4[1][lc]) + s4[2][lc]) + s4[3][lc]);
+                b.out[sg][c] = o[h];
+            }
         }
         if (sq) {
             __syncthreads();   // s4 read by group 0: its slots reused for the wave sums
-            const double q = xpa_wave_sum((double)o * (double)o);
+            const double q = xpa_wave_sum((double)o[0] * (double)o[0] + (double)o[1] * (double)o[1]);
             if ((threadIdx.x & 63) == 0 && grp == 0) s4[1][threadIdx.x >> 6] = q;
             __syncthreads();
             if (threadIdx.x == 0) xpa_store_agent(sq, ((s4[1][0] + s4[1][1]) + s4[1][2]) + s4[1][3]);
