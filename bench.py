@@ -54,8 +54,9 @@ def parse():
     p.add_argument("--gemm", choices=("f32", "split3"), default="split3",
                    help="the update's hidden-layer GEMMs: f32 MFMA (K16 + hipBLASLt) or the bf16 three-way split "
                         "(K16S + K40 + K41, the f32 GEMM's accuracy on the bf16 matrix cores)")
-    p.add_argument("--s3-heads", choices=("s3", "s3p", "s3q"), default="s3p",
-                   help="with --gemm split3: K16S (both fragments split in the k loop) or K16P (Wh's planes split once)")
+    p.add_argument("--s3-heads", choices=("s3", "s3p", "s3q"), default="s3q",
+                   help="with --gemm split3: K16S (both fragments split in the k loop), K16P (Wh's planes split once) or "
+                        "K16Q (K16P with 32 x 128 wave tiles, bit-identical)")
     p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc HBM-traffic passes")
     p.add_argument("--no-rocprof", action="store_true",
                    help="skip the child rocprofv3 --kernel-trace run that times the in-loop GAE launches")
@@ -1001,12 +1002,21 @@ def main():
                 "kernel": ("xpa_head_gemm_trunk_actor + xpa_head_gemm_trunk_critic (K16X: trunk layer + hidden-layer "
                            "GEMM on fp32 MFMA + fused head epilogue, per minibatch; FLOP counted: the hidden GEMMs)"
                            if trunk else
-                           "xpa_head_gemm_actor + xpa_head_gemm_critic (K16: hidden-layer GEMM on fp32 MFMA "
-                           "+ fused head epilogue, per minibatch)"), "bound": "mfma",
+                           ("xpa_head_gemm_%s_actor + _critic (%s: the hidden-layer f32 GEMM as an exact three-way bf16 "
+                            "split on the bf16 matrix cores, 6 bf16 products per f32 product, + fused head epilogue, "
+                            "per minibatch; achieved / frac: f32-GEMM FLOP against the fp32 MFMA peak)"
+                            % (ops.S3_HEADS, {"s3p": "K16P", "s3q": "K16Q"}.get(ops.S3_HEADS, "K16S"))
+                            if ops.S3_GEMMS else
+                            "xpa_head_gemm_actor + xpa_head_gemm_critic (K16: hidden-layer GEMM on fp32 MFMA "
+                            "+ fused head epilogue, per minibatch)")), "bound": "mfma",
                 "avg_us": round(heads_ms * 1e3, 3), "flops": fl, "achieved": round(fl / heads_ms / 1e9, 1),
                 "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(fl / heads_ms / 1e9 / FP32_MFMA_PEAK_TFLOPS, 4), "launches": ops.TIMER.count("heads"),
                 "timing": "event pairs on the launch stream in one extra iteration after the timed region"}
+            if ops.S3_GEMMS and not trunk:   # the matrix cores' own work: 6 bf16 products per f32 product
+                update_kernels["heads"].update({
+                    "bf16_mfma_flops": 6 * fl, "bf16_achieved": round(6 * fl / heads_ms / 1e9, 1),
+                    "bf16_peak": 2500.0, "bf16_frac": round(6 * fl / heads_ms / 1e9 / 2500.0, 4)})
         elif heads_ms:
             hb = heads_bytes(B, args.act_dim, args.hidden)
             update_kernels["heads"] = {

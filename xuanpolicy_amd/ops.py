@@ -619,7 +619,7 @@ K16W_ENABLED = False  # fused_heads' gemm form: K16W (xpa_head_gemm_ws_*) where 
 # The update's hidden-layer GEMMs on the bf16 matrix cores by the three-way split (K16S heads, K40 dX, K41 dW):
 # the f32 GEMM's accuracy, not the f32 MFMA's bits.  Read when a learner's update is built / captured.
 S3_GEMMS = True
-S3_HEADS = "s3p"   # with S3_GEMMS: "s3" K16S (both fragments split in the k loop), "s3p" K16P (Wh's planes split once),
+S3_HEADS = "s3q"   # with S3_GEMMS: "s3" K16S (both fragments split in the k loop), "s3p" K16P (Wh's planes split once),
                    # "s3q" K16Q (K16P's bits, 32 x 128 wave tiles)
 
 
