@@ -1042,7 +1042,7 @@ def main():
                                    (N, T, args.n_epoch, args.n_minibatch, args.hidden),
                        "num_envs_per_gpu": N, "horizon": T, "global_envs": N * world, "minibatch": B,
                        "update_gemms": ("f32 GEMMs as exact three-way bf16 splits on the bf16 matrix cores (%s heads, "
-                                        "K40 dX, K41V dW; error <= 2x the f32 GEMM's vs f64: tests/test_gpu_sgemm3.py)"
+                                        "K42S dX + trunk backward, K41V dW; error <= 2x the f32 GEMM's vs f64: tests/test_gpu_sgemm3.py)"
                                         % {"s3p": "K16P", "s3q": "K16Q"}.get(ops.S3_HEADS, "K16S")
                                         if ops.S3_GEMMS else "f32 MFMA (K16 heads, hipBLASLt dX / dW)"),
                        "updates_per_step": args.n_epoch * args.n_minibatch,

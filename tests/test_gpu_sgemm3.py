@@ -200,6 +200,26 @@ def test_wgrad_vector_staged_matches_f32_gemm_error(rows, m, lda_pad, slices):
     assert err <= 2 * err_f32 + 2 ** -24 * scale, (err, err_f32, scale)
 
 
+@pytest.mark.parametrize("rows,m,lda_pad,slices", [(65536, 512, 0, None), (4133, 256, 8, 5), (33, 128, 4, 2)])
+def test_wgrad_interleaved_schedule_equals_k41v(rows, m, lda_pad, slices):
+    """K41V's interleaved schedule (xpa_s3_probe bit 64: the next stage's split placed between the MFMA blocks, the
+    last chunks' staging unconditional) writes K41V's partials bit for bit: the same products per accumulator in the
+    same order."""
+    from xuanpolicy_amd import ops
+    L = ops.lib()
+    g = torch.Generator(device=DEV).manual_seed(rows + 11 * m)
+    a = _wide((rows, m + lda_pad), g)[:, :m]
+    b = torch.randn(rows, 256, device=DEV, generator=g)
+    ref = ops.s3_wgrad(a, b, slices=slices)
+    try:
+        assert L.xpa_s3_probe(64) == 0
+        got = ops.s3_wgrad(a, b, slices=slices)
+        torch.cuda.synchronize()
+    finally:
+        L.xpa_s3_probe(0)
+    assert torch.equal(ref, got)
+
+
 def test_split_batch_equals_single_splits():
     """xpa_s3_split_batch (the update's one split launch: Wh_pair, Wh_actor^T, Wh_critic^T) == xpa_s3_split_b each."""
     from xuanpolicy_amd import ops

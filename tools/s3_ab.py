@@ -73,17 +73,18 @@ def main():
     r["f32_floor_us"] = round(flop / 157.3e12 * 1e6, 2)
     r["s3_frac_of_f32_floor"] = round(r["f32_floor_us"] / min(r["s3_us"]), 3)
     r["torch_frac_of_f32_floor"] = round(r["f32_floor_us"] / min(r["torch_bmm8_us"]), 3)
-    if a.probe:   # 1 no MFMA, 2 no operand loads, 4 one MFMA instead of six; + 8: K40's two-block form / K41W; 16: K40W
+    if a.probe:   # 1 no MFMA, 2 no operand loads, 4 one MFMA instead of six; + 8: K40's two-block form / K41W; 16: K40W;
+        # 64: K41V's interleaved schedule
         L = ops.lib()
         M, K = 65536, 512
         x = torch.randn(M, K, device=dev, generator=g)
         sp = ops.s3_split(torch.randn(K, 256, device=dev, generator=g) / 16)
         out = torch.empty(M, 256, device=dev)
         pr = res.setdefault("probe_us", {})
-        for mask in (0, 1, 2, 3, 4, 6, 8, 9, 10, 11, 12, 16, 32):
+        for mask in (0, 1, 2, 3, 4, 6, 8, 9, 10, 11, 12, 16, 32, 64):
             assert L.xpa_s3_probe(mask) == 0
             pr["k40_%d" % mask] = round(_time(lambda: ops.s3_gemm(x, sp, K, out=out), a.reps), 2)
-            if mask < 8 or mask in (8, 16):
+            if mask < 8 or mask in (8, 16, 64):
                 pr["k41_%d" % mask] = round(_time(lambda: ops.s3_wgrad(dz, x_in, out=part), a.reps), 2)
         assert L.xpa_s3_probe(0) == 0
     print(json.dumps(res))

@@ -870,6 +870,58 @@ __device__ __forceinline__ void v_chunk(const char *st, f32x16 (&acc)[2][2], int
     }
 }
 
+// SCHED (r04 probe bit 64): the loop body as ONE scheduling region (the next stage's split / stores and the chunk-after's
+// loads unconditional: past the last chunk they rewrite the idle stage / re-read clamped rows) with
+// sched_group_barrier placing ~5 VALU after each MFMA, so the split of chunk c + 1 issues inside chunk c's MFMA gaps
+// (hipcc's own order: all 48 MFMAs, then ~250 VALU and the stores, with the matrix pipe idle — both waves of a SIMD
+// reach that phase together after the chunk barrier).
+// v_chunk with v_store's six float4 splits (each 3 ds_write_b64) placed one after each 6-MFMA accumulator block, in
+// segments the scheduler may not merge (sched_barrier), and the second k step's fragment reads one segment in
+__device__ __forceinline__ void v_frags(const char *st, int s, int lane, int wm, int wn, bf16x8 (&ah)[2],
+                                        bf16x8 (&am)[2], bf16x8 (&al)[2], bf16x8 (&bh)[2], bf16x8 (&bm)[2],
+                                        bf16x8 (&bl)[2]) {
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3, h = lane >> 5;
+    const int cofs = 16 * (g & 1) + 4 * p;
+    const int row0 = 16 * s + 8 * h + q;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int col = 32 * (2 * wm + i) + cofs;
+        ah[i] = v_frag(st, row0, col);
+        am[i] = v_frag(st + kVPlane, row0, col);
+        al[i] = v_frag(st + 2 * kVPlane, row0, col);
+        const int n = 32 * (2 * wn + i) + cofs;
+        const char *bt = st + 3 * kVPlane + (n >> 7) * kVPlane;
+        bh[i] = v_frag(bt, row0, n & 127);
+        bm[i] = v_frag(bt + 2 * kVPlane, row0, n & 127);
+        bl[i] = v_frag(bt + 4 * kVPlane, row0, n & 127);
+    }
+}
+
+__device__ __forceinline__ void v_put_unit(char *nx, const VUnits &u, int t, int unit) {
+    if (unit < 2) {
+        const int idx = t + 512 * unit, k = idx >> 5, cq = idx & 31;
+        v_put(nx, kVPlane, v_off(k, 4 * cq), u.a[unit]);
+    } else {
+        const int j = unit - 2, idx = t + 512 * j, k = idx >> 6, n = 4 * (idx & 63);
+        v_put(nx + 3 * kVPlane, 2 * kVPlane, (n >> 7) * kVPlane + v_off(k, n & 127), u.b[j]);
+    }
+}
+
+__device__ __forceinline__ void v_chunk_il(const char *st, char *nx, const VUnits &u, f32x16 (&acc)[2][2], int lane,
+                                           int wm, int wn, int t) {
+    bf16x8 ah[2][2], am[2][2], al[2][2], bh[2][2], bm[2][2], bl[2][2];
+    v_frags(st, 0, lane, wm, wn, ah[0], am[0], al[0], bh[0], bm[0], bl[0]);
+#pragma unroll
+    for (int seg = 0; seg < 8; ++seg) {
+        const int s = seg >> 2, i = (seg >> 1) & 1, j = seg & 1;
+        acc[i][j] = xpa_mfma_s3(ah[s][i], am[s][i], al[s][i], bh[s][j], bm[s][j], bl[s][j], acc[i][j]);
+        if (seg < 6) v_put_unit(nx, u, t, seg);
+        if (seg == 1) v_frags(st, 1, lane, wm, wn, ah[1], am[1], al[1], bh[1], bm[1], bl[1]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int SCHED = 0>
 __global__ __launch_bounds__(512, 1) void s3_wgrad_v_kernel(const float *__restrict__ A, int64_t lda,
                                                             const float *__restrict__ B, int64_t ldb, int64_t rows,
                                                             int64_t M, int slices, int64_t slice_rows,
@@ -903,8 +955,11 @@ __global__ __launch_bounds__(512, 1) void s3_wgrad_v_kernel(const float *__restr
     }
 #pragma unroll 1
     for (int c = 0; c < nch; ++c) {
-        v_chunk(lds + (c & 1) * kVStage, acc, lane, wm, wn);
-        if (c + 1 < nch) {
+        if constexpr (!SCHED) v_chunk(lds + (c & 1) * kVStage, acc, lane, wm, wn);
+        if constexpr (SCHED) {
+            v_chunk_il(lds + (c & 1) * kVStage, lds + ((c + 1) & 1) * kVStage, u, acc, lane, wm, wn, t);
+            v_load(u, Am, lda, B, ldb, k0 + (int64_t)(c + 2) * kWgKC, kend, t);
+        } else if (c + 1 < nch) {
             v_store(lds + ((c + 1) & 1) * kVStage, u, t);
             if (c + 2 < nch) v_load(u, Am, lda, B, ldb, k0 + (int64_t)(c + 2) * kWgKC, kend, t);
         }
@@ -945,8 +1000,11 @@ XPA_API int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ld
     // 32 or any of 1 / 2 / 4 the register-staged K41 (and its probes)
     const bool vec_ok = lda % 4 == 0 && ldb % 4 == 0 &&
                         ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
-    if (vec_ok && (g_s3_probe & (1 | 2 | 4 | 8 | 32)) == 0) {
-        s3_wgrad_v_kernel<<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out);   // K41V
+    if (vec_ok && (g_s3_probe & (1 | 2 | 4 | 8 | 32)) == 0) {   // K41V (bit 64: its interleaved schedule)
+        if (g_s3_probe & 64)
+            s3_wgrad_v_kernel<1><<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out);
+        else
+            s3_wgrad_v_kernel<0><<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out);
         return xpa_launch_status();
     }
     if (g_s3_probe & 8) {   // the wave-specialised form (K41W)
