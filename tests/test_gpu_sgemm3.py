@@ -202,9 +202,9 @@ def test_wgrad_vector_staged_matches_f32_gemm_error(rows, m, lda_pad, slices):
 
 @pytest.mark.parametrize("rows,m,lda_pad,slices", [(65536, 512, 0, None), (4133, 256, 8, 5), (33, 128, 4, 2)])
 def test_wgrad_interleaved_schedule_equals_k41v(rows, m, lda_pad, slices):
-    """K41V's interleaved schedule (xpa_s3_probe bit 64: the next stage's split placed between the MFMA blocks, the
-    last chunks' staging unconditional) writes K41V's partials bit for bit: the same products per accumulator in the
-    same order."""
+    """K41V's interleaved schedule (the default: the next stage's split placed between the MFMA blocks, the last
+    chunks' staging unconditional) writes the partials of hipcc's own schedule (xpa_s3_probe bit 64) bit for bit: the
+    same products per accumulator in the same order."""
     from xuanpolicy_amd import ops
     L = ops.lib()
     g = torch.Generator(device=DEV).manual_seed(rows + 11 * m)

@@ -781,6 +781,8 @@ __device__ __forceinline__ int v_off(int row, int col) {   // byte offset of (ro
 
 struct VUnits {
     float4 a[2], b[4];
+    unsigned ok;   // bit u: unit u's row is inside the slice (a[0..1] = bits 0..1, b[0..3] = bits 2..5); applied at the
+                   // split, not after the load, so no wait for the load sits in the loop body
 };
 
 __device__ __forceinline__ float4 v_zero_if(float4 v, bool keep) {
@@ -789,20 +791,22 @@ __device__ __forceinline__ float4 v_zero_if(float4 v, bool keep) {
 
 __device__ __forceinline__ void v_load(VUnits &u, const float *__restrict__ A, int64_t lda, const float *__restrict__ B,
                                        int64_t ldb, int64_t k0, int64_t kend, int t) {
+    unsigned ok = 0u;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int idx = t + 512 * j, k = idx >> 5, cq = idx & 31;
         const int64_t r = k0 + k;
-        const float4 v = *reinterpret_cast<const float4 *>(A + min(r, kend - 1) * lda + 4 * cq);
-        u.a[j] = v_zero_if(v, r < kend);
+        u.a[j] = *reinterpret_cast<const float4 *>(A + min(r, kend - 1) * lda + 4 * cq);
+        ok |= (r < kend ? 1u : 0u) << j;
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int idx = t + 512 * j, k = idx >> 6, nq = idx & 63;
         const int64_t r = k0 + k;
-        const float4 v = *reinterpret_cast<const float4 *>(B + min(r, kend - 1) * ldb + 4 * nq);
-        u.b[j] = v_zero_if(v, r < kend);
+        u.b[j] = *reinterpret_cast<const float4 *>(B + min(r, kend - 1) * ldb + 4 * nq);
+        ok |= (r < kend ? 1u : 0u) << (2 + j);
     }
+    u.ok = ok;
 }
 
 // the three planes of 4 consecutive columns, each packed as 4 bf16 (8 B)
@@ -827,12 +831,13 @@ __device__ __forceinline__ void v_store(char *st, const VUnits &u, int t) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int idx = t + 512 * j, k = idx >> 5, cq = idx & 31;
-        v_put(st, kVPlane, v_off(k, 4 * cq), u.a[j]);
+        v_put(st, kVPlane, v_off(k, 4 * cq), v_zero_if(u.a[j], (u.ok >> j) & 1u));
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int idx = t + 512 * j, k = idx >> 6, n = 4 * (idx & 63);
-        v_put(st + 3 * kVPlane, 2 * kVPlane, (n >> 7) * kVPlane + v_off(k, n & 127), u.b[j]);
+        v_put(st + 3 * kVPlane, 2 * kVPlane, (n >> 7) * kVPlane + v_off(k, n & 127),
+              v_zero_if(u.b[j], (u.ok >> (2 + j)) & 1u));
     }
 }
 
@@ -870,7 +875,7 @@ __device__ __forceinline__ void v_chunk(const char *st, f32x16 (&acc)[2][2], int
     }
 }
 
-// SCHED (r04 probe bit 64): the loop body as ONE scheduling region (the next stage's split / stores and the chunk-after's
+// SCHED (r04, the default; probe bit 64 selects SCHED = 0): the loop body as ONE scheduling region (the next stage's split / stores and the chunk-after's
 // loads unconditional: past the last chunk they rewrite the idle stage / re-read clamped rows) with
 // sched_group_barrier placing ~5 VALU after each MFMA, so the split of chunk c + 1 issues inside chunk c's MFMA gaps
 // (hipcc's own order: all 48 MFMAs, then ~250 VALU and the stores, with the matrix pipe idle — both waves of a SIMD
@@ -898,17 +903,21 @@ __device__ __forceinline__ void v_frags(const char *st, int s, int lane, int wm,
 }
 
 __device__ __forceinline__ void v_put_unit(char *nx, const VUnits &u, int t, int unit) {
+    const bool keep = (u.ok >> unit) & 1u;
     if (unit < 2) {
         const int idx = t + 512 * unit, k = idx >> 5, cq = idx & 31;
-        v_put(nx, kVPlane, v_off(k, 4 * cq), u.a[unit]);
+        v_put(nx, kVPlane, v_off(k, 4 * cq), v_zero_if(u.a[unit], keep));
     } else {
         const int j = unit - 2, idx = t + 512 * j, k = idx >> 6, n = 4 * (idx & 63);
-        v_put(nx + 3 * kVPlane, 2 * kVPlane, (n >> 7) * kVPlane + v_off(k, n & 127), u.b[j]);
+        v_put(nx + 3 * kVPlane, 2 * kVPlane, (n >> 7) * kVPlane + v_off(k, n & 127), v_zero_if(u.b[j], keep));
     }
 }
 
-__device__ __forceinline__ void v_chunk_il(const char *st, char *nx, const VUnits &u, f32x16 (&acc)[2][2], int lane,
-                                           int wm, int wn, int t) {
+// (and the loads of the chunk after next issued in segment 6, once the six units are split, so they fly during the
+// last two MFMA blocks)
+__device__ __forceinline__ void v_chunk_il(const char *st, char *nx, VUnits &u, f32x16 (&acc)[2][2], int lane, int wm,
+                                           int wn, int t, const float *__restrict__ A, int64_t lda,
+                                           const float *__restrict__ B, int64_t ldb, int64_t k_next, int64_t kend) {
     bf16x8 ah[2][2], am[2][2], al[2][2], bh[2][2], bm[2][2], bl[2][2];
     v_frags(st, 0, lane, wm, wn, ah[0], am[0], al[0], bh[0], bm[0], bl[0]);
 #pragma unroll
@@ -917,6 +926,7 @@ __device__ __forceinline__ void v_chunk_il(const char *st, char *nx, const VUnit
         acc[i][j] = xpa_mfma_s3(ah[s][i], am[s][i], al[s][i], bh[s][j], bm[s][j], bl[s][j], acc[i][j]);
         if (seg < 6) v_put_unit(nx, u, t, seg);
         if (seg == 1) v_frags(st, 1, lane, wm, wn, ah[1], am[1], al[1], bh[1], bm[1], bl[1]);
+        if (seg == 6) v_load(u, A, lda, B, ldb, k_next, kend, t);
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -957,8 +967,8 @@ __global__ __launch_bounds__(512, 1) void s3_wgrad_v_kernel(const float *__restr
     for (int c = 0; c < nch; ++c) {
         if constexpr (!SCHED) v_chunk(lds + (c & 1) * kVStage, acc, lane, wm, wn);
         if constexpr (SCHED) {
-            v_chunk_il(lds + (c & 1) * kVStage, lds + ((c + 1) & 1) * kVStage, u, acc, lane, wm, wn, t);
-            v_load(u, Am, lda, B, ldb, k0 + (int64_t)(c + 2) * kWgKC, kend, t);
+            v_chunk_il(lds + (c & 1) * kVStage, lds + ((c + 1) & 1) * kVStage, u, acc, lane, wm, wn, t, Am, lda, B, ldb,
+                       k0 + (int64_t)(c + 2) * kWgKC, kend);
         } else if (c + 1 < nch) {
             v_store(lds + ((c + 1) & 1) * kVStage, u, t);
             if (c + 2 < nch) v_load(u, Am, lda, B, ldb, k0 + (int64_t)(c + 2) * kWgKC, kend, t);
@@ -1000,11 +1010,11 @@ XPA_API int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ld
     // 32 or any of 1 / 2 / 4 the register-staged K41 (and its probes)
     const bool vec_ok = lda % 4 == 0 && ldb % 4 == 0 &&
                         ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
-    if (vec_ok && (g_s3_probe & (1 | 2 | 4 | 8 | 32)) == 0) {   // K41V (bit 64: its interleaved schedule)
-        if (g_s3_probe & 64)
-            s3_wgrad_v_kernel<1><<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out);
-        else
+    if (vec_ok && (g_s3_probe & (1 | 2 | 4 | 8 | 32)) == 0) {   // K41V (bit 64: without its interleaved schedule)
+        if (g_s3_probe & 64)   // hipcc's own schedule (r04p: 115 us vs 104 interleaved at C2)
             s3_wgrad_v_kernel<0><<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out);
+        else
+            s3_wgrad_v_kernel<1><<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out);
         return xpa_launch_status();
     }
     if (g_s3_probe & 8) {   // the wave-specialised form (K41W)
