@@ -37,6 +37,8 @@ __device__ __forceinline__ float act_g(float h, float slope) {
     return 1.f;
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 // IDX: the rows are x[idx[r]] of the full rollout buffer (n_rows rows; an index outside [0, n_rows) gives a zero row
 // and adds nothing to the moments), i.e. K4's minibatch gather folded into the staging of the x tile, and with
 // adv_partials the K4 advantage moments of each 64-row tile (f64 (sum, sum of squares), thread t <-> row t and
@@ -50,8 +52,12 @@ __global__ __launch_bounds__(256) void thin_fwd_kernel(const float *__restrict__
                                                        double *__restrict__ adv_partials = nullptr,
                                                        float *__restrict__ x_out = nullptr,
                                                        unsigned *__restrict__ hsign = nullptr) {
-    constexpr int kPad = DMAX + 4;  // row stride of the staged x tile (16-B aligned rows)
-    __shared__ __attribute__((aligned(16))) float s_x[TILE * kPad];
+    // the staged x tile as row pairs: element (r, k) at ((r >> 1) DMAX + k) 2 + (r & 1), so one float4 broadcast
+    // read holds features k, k + 1 of rows r, r + 1 and each v_pk_fma_f32 runs the two rows' chains (r04: one
+    // fmaf chain per row — 45 instructions per row and wave — kept the kernel VALU-issue bound); every chain is
+    // still the same k-ascending fmaf sequence, so h is bit for bit the one-row form's
+    static_assert(TILE % 2 == 0 && DMAX % 2 == 0, "row pairs, feature pairs");
+    __shared__ __attribute__((aligned(16))) float s_x[TILE * DMAX];
     __shared__ unsigned long long s_ball[IDX ? TILE * 4 : 1];   // hsign: each wave's h > 0 ballot per row
     __shared__ int64_t s_src[IDX ? TILE : 1];
     __shared__ double s_red[4];
@@ -97,14 +103,14 @@ __global__ __launch_bounds__(256) void thin_fwd_kernel(const float *__restrict__
                 const int i = t + 256 * u;
                 if (i < TILE * DMAX) {
                     const int r = i / DMAX, k = i - r * DMAX;
-                    s_x[r * kPad + k] = v[u];
+                    s_x[((r >> 1) * DMAX + k) * 2 + (r & 1)] = v[u];
                     if (x_out && k < din && r0 + r < rows) x_out[(r0 + r) * din + k] = v[u];  // the gathered rows
                 }
             }
         } else {
             for (int i = t; i < TILE * DMAX; i += 256) {
                 const int r = i / DMAX, k = i - r * DMAX;
-                s_x[r * kPad + k] = (k < din && r0 + r < rows) ? x[(r0 + r) * ldx + k] : 0.f;
+                s_x[((r >> 1) * DMAX + k) * 2 + (r & 1)] = (k < din && r0 + r < rows) ? x[(r0 + r) * ldx + k] : 0.f;
             }
         }
         if (IDX && adv_partials) {  // K4's moments of this tile (thread t <-> row t)
@@ -124,22 +130,24 @@ __global__ __launch_bounds__(256) void thin_fwd_kernel(const float *__restrict__
         if (IDX && !h) continue;  // gather-only form (K16X forms h itself): the rows and the moments
         __syncthreads();
         const int nr = (int)min((int64_t)TILE, rows - r0);
-        for (int r = 0; r < nr; ++r) {
-            const float *xr = s_x + r * kPad;
-            float acc = 0.f;
+        for (int r = 0; r < nr; r += 2) {   // rows r, r + 1 (a row past the tile's end is staged as zeros)
+            const float4 *xp = reinterpret_cast<const float4 *>(s_x + (r >> 1) * DMAX * 2);
+            f2 acc = {0.f, 0.f};
 #pragma unroll
-            for (int k = 0; k < DMAX; k += 4) {
-                const float4 xv = *reinterpret_cast<const float4 *>(xr + k);
-                acc = fmaf(xv.x, w[k], acc);
-                acc = fmaf(xv.y, w[k + 1], acc);
-                acc = fmaf(xv.z, w[k + 2], acc);
-                acc = fmaf(xv.w, w[k + 3], acc);
+            for (int k = 0; k < DMAX; k += 2) {
+                const float4 xv = xp[k >> 1];   // (x[r][k], x[r + 1][k], x[r][k + 1], x[r + 1][k + 1])
+                acc = __builtin_elementwise_fma(f2{xv.x, xv.y}, f2{w[k], w[k]}, acc);
+                acc = __builtin_elementwise_fma(f2{xv.z, xv.w}, f2{w[k + 1], w[k + 1]}, acc);
             }
-            const float hv = act_f<ACT>(acc + bc, slope);
-            __builtin_nontemporal_store(hv, h + (r0 + r) * ldh + t);
-            if (IDX && hsign != nullptr) {
-                const unsigned long long bl = __ballot(hv > 0.f);
-                if ((t & 63) == 0) s_ball[r * 4 + (t >> 6)] = bl;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                if (e == 1 && r + 1 >= nr) break;
+                const float hv = act_f<ACT>(acc[e] + bc, slope);
+                __builtin_nontemporal_store(hv, h + (r0 + r + e) * ldh + t);
+                if (IDX && hsign != nullptr) {
+                    const unsigned long long bl = __ballot(hv > 0.f);
+                    if ((t & 63) == 0) s_ball[(r + e) * 4 + (t >> 6)] = bl;
+                }
             }
         }
         if (IDX && hsign != nullptr) {
@@ -260,7 +268,7 @@ __global__ __launch_bounds__(1024) void thin_bwd_kernel(const float *__restrict_
                     const int64_t sr = r0 + r < rows ? idx[r0 + r] : -1;
                     s_x[r * kPad + k] = (k < din && sr >= 0 && sr < n_rows) ? x[sr * ldx + k] : 0.f;
                 } else {
-                    s_x[r * kPad + k] = (k < din && r0 + r < rows) ? x[(r0 + r) * ldx + k] : 0.f;
+                    s_x[((r >> 1) * DMAX + k) * 2 + (r & 1)] = (k < din && r0 + r < rows) ? x[(r0 + r) * ldx + k] : 0.f;
                 }
             }
         }
