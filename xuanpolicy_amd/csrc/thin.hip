@@ -268,7 +268,7 @@ __global__ __launch_bounds__(1024) void thin_bwd_kernel(const float *__restrict_
                     const int64_t sr = r0 + r < rows ? idx[r0 + r] : -1;
                     s_x[r * kPad + k] = (k < din && sr >= 0 && sr < n_rows) ? x[sr * ldx + k] : 0.f;
                 } else {
-                    s_x[((r >> 1) * DMAX + k) * 2 + (r & 1)] = (k < din && r0 + r < rows) ? x[(r0 + r) * ldx + k] : 0.f;
+                    s_x[r * kPad + k] = (k < din && r0 + r < rows) ? x[(r0 + r) * ldx + k] : 0.f;
                 }
             }
         }
