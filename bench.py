@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--s3-heads", choices=("s3", "s3p", "s3q"), default="s3q",
                    help="with --gemm split3: K16S (both fragments split in the k loop), K16P (Wh's planes split once) or "
                         "K16Q (K16P with 32 x 128 wave tiles, bit-identical)")
+    p.add_argument("--thin-store", choices=("nt", "plain"), default="nt",
+                   help="K13's h stores: non-temporal (default) or plain (A/B; xpa_thin_probe)")
     p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc HBM-traffic passes")
     p.add_argument("--no-rocprof", action="store_true",
                    help="skip the child rocprofv3 --kernel-trace run that times the in-loop GAE launches")
@@ -818,6 +820,8 @@ def main():
 
     ops.S3_GEMMS = args.gemm == "split3"
     ops.S3_HEADS = args.s3_heads
+    if args.thin_store == "plain":
+        ops.lib().xpa_thin_probe(1)
     rank, local, world = init_from_env()
     device = local_device(local)
     torch.cuda.set_device(device)

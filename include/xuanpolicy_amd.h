@@ -752,6 +752,8 @@ int xpa_thin_linear_act_fwd_gather(int act, const float *x, int64_t ldx, int64_t
                                    int64_t rows, int64_t d_in, int64_t d_out, const float *w, const float *b,
                                    float slope, float *h, int64_t ldh, const float *adv, double *adv_partials,
                                    float *x_out, xpa_stream_t stream);
+/* Diagnostics: bit 1 makes xpa_thin_linear_act_fwd_gather_sign store h with plain stores (default non-temporal). */
+int xpa_thin_probe(int mask);
 /* The gather form writing h and its sign bits as well (r04; h_sign: 32 bytes per row, byte b bit j = h[row, 32 j + b]
  * > 0, the layout xpa_s3_gemm_trunk_bwd_sign reads); act 0 / 1. */
 int xpa_thin_linear_act_fwd_gather_sign(int act, const float *x, int64_t ldx, int64_t n_rows, const int64_t *idx,

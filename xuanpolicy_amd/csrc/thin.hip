@@ -43,7 +43,9 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // and adds nothing to the moments), i.e. K4's minibatch gather folded into the staging of the x tile, and with
 // adv_partials the K4 advantage moments of each 64-row tile (f64 (sum, sum of squares), thread t <-> row t and
 // xpa_block_sum: K4's partials bit for bit).  Only the 64-row tile form takes IDX.
-template <int ACT, int DMAX, int TILE, bool IDX = false>
+// NT: h stored non-temporally (the default); false (xpa_thin_probe bit 1, r04 A/B): plain stores, so the update's h
+// may stay in the caches for the head launches and K41 that read it next
+template <int ACT, int DMAX, int TILE, bool IDX = false, bool NT = true>
 __global__ __launch_bounds__(256) void thin_fwd_kernel(const float *__restrict__ x, int64_t ldx, int64_t rows, int din,
                                                        const float *__restrict__ W, const float *__restrict__ bias,
                                                        float slope, float *__restrict__ h, int64_t ldh,
@@ -143,7 +145,8 @@ __global__ __launch_bounds__(256) void thin_fwd_kernel(const float *__restrict__
             for (int e = 0; e < 2; ++e) {
                 if (e == 1 && r + 1 >= nr) break;
                 const float hv = act_f<ACT>(acc[e] + bc, slope);
-                __builtin_nontemporal_store(hv, h + (r0 + r + e) * ldh + t);
+                if constexpr (NT) __builtin_nontemporal_store(hv, h + (r0 + r + e) * ldh + t);
+                else h[(r0 + r + e) * ldh + t] = hv;
                 if (IDX && hsign != nullptr) {
                     const unsigned long long bl = __ballot(hv > 0.f);
                     if ((t & 63) == 0) s_ball[(r + e) * 4 + (t >> 6)] = bl;
@@ -373,6 +376,13 @@ int dmax_for(int din) { return din <= 8 ? 8 : din <= 20 ? 20 : din <= 32 ? 32 : 
 
 }  // namespace
 
+// diagnostics / A-B (tools): bit 1 = the sign gather form with plain (not non-temporal) h stores
+static int g_thin_probe = 0;
+XPA_API int xpa_thin_probe(int mask) {
+    g_thin_probe = mask;
+    return 0;
+}
+
 XPA_API int64_t xpa_thin_bwd_num_partials(int64_t rows) {
     const int64_t blocks = ((rows + kTile - 1) / kTile + 3) / 4;  // 4 tiles per block-iteration
     return blocks < kBwdGrid ? (blocks > 0 ? blocks : 1) : kBwdGrid;
@@ -477,8 +487,12 @@ XPA_API int xpa_thin_linear_act_fwd_gather_sign(int act, const float *x, int64_t
     const dim3 grid((unsigned)(tiles < kFwdGrid ? tiles : kFwdGrid));
     const int dm = dmax_for((int)d_in);
 #define XPA_FWDG(A_, D_)                                                                                             \
-    hipLaunchKernelGGL((thin_fwd_kernel<A_, D_, kTile, true>), grid, dim3(256), 0, s, x, ldx, rows, (int)d_in, w, b,   \
-                       slope, h, ldh, idx, n_rows, adv, adv_partials, x_out, h_sign)
+    if (g_thin_probe & 1)                                                                                            \
+        hipLaunchKernelGGL((thin_fwd_kernel<A_, D_, kTile, true, false>), grid, dim3(256), 0, s, x, ldx, rows,        \
+                           (int)d_in, w, b, slope, h, ldh, idx, n_rows, adv, adv_partials, x_out, h_sign);           \
+    else                                                                                                             \
+        hipLaunchKernelGGL((thin_fwd_kernel<A_, D_, kTile, true>), grid, dim3(256), 0, s, x, ldx, rows, (int)d_in, w, \
+                           b, slope, h, ldh, idx, n_rows, adv, adv_partials, x_out, h_sign)
 #define XPA_FWDG_D(A_)                 \
     if (dm == 8) XPA_FWDG(A_, 8);      \
     else if (dm == 20) XPA_FWDG(A_, 20); \
