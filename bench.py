@@ -59,6 +59,8 @@ def parse():
                         "K16Q (K16P with 32 x 128 wave tiles, bit-identical)")
     p.add_argument("--thin-store", choices=("nt", "plain"), default="nt",
                    help="K13's h stores: non-temporal (default) or plain (A/B; xpa_thin_probe)")
+    p.add_argument("--dz-store", choices=("nt", "plain"), default="nt",
+                   help="the head kernels' dz stores: non-temporal (default) or plain (A/B; xpa_head_store_probe)")
     p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc HBM-traffic passes")
     p.add_argument("--no-rocprof", action="store_true",
                    help="skip the child rocprofv3 --kernel-trace run that times the in-loop GAE launches")
@@ -825,6 +827,8 @@ def main():
     rank, local, world = init_from_env()
     device = local_device(local)
     torch.cuda.set_device(device)
+    if args.dz_store == "plain":
+        assert ops.lib().xpa_head_store_probe(1) == 0
     N, T = args.n_envs, args.horizon
     agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=args.obs_dim, act_dim=args.act_dim, hidden=args.hidden,
                                n_epoch=args.n_epoch, n_minibatch=args.n_minibatch, seed=1, device=device,

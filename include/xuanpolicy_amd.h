@@ -754,6 +754,8 @@ int xpa_thin_linear_act_fwd_gather(int act, const float *x, int64_t ldx, int64_t
                                    float *x_out, xpa_stream_t stream);
 /* Diagnostics: bit 1 makes xpa_thin_linear_act_fwd_gather_sign store h with plain stores (default non-temporal). */
 int xpa_thin_probe(int mask);
+/* Diagnostics: 1 makes the head kernels store dz with plain (not non-temporal) stores. */
+int xpa_head_store_probe(int plain);
 /* The gather form writing h and its sign bits as well (r04; h_sign: 32 bytes per row, byte b bit j = h[row, 32 j + b]
  * > 0, the layout xpa_s3_gemm_trunk_bwd_sign reads); act 0 / 1. */
 int xpa_thin_linear_act_fwd_gather_sign(int act, const float *x, int64_t ldx, int64_t n_rows, const int64_t *idx,

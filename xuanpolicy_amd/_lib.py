@@ -239,6 +239,7 @@ SIGNATURES = {
     "xpa_thin_linear_act_fwd_gather_sign": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_p,
                                                            c_p, c_f32, c_p, c_i64, c_p, c_p, c_p, c_p, c_p]),
     "xpa_thin_probe": (ctypes.c_int, [ctypes.c_int]),
+    "xpa_head_store_probe": (ctypes.c_int, [ctypes.c_int]),
     "xpa_s3_probe": (ctypes.c_int, [ctypes.c_int]),
     "xpa_s3_split_bytes": (c_i64, [c_i64, c_i64]),
     "xpa_s3_split_b": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),

@@ -145,6 +145,10 @@ __device__ __forceinline__ void load_tile(float4 (&zq)[16], const float *__restr
     }
 }
 
+// dz stores: non-temporal (0, the default) or plain (1: xpa_head_store_probe, r04 A/B — the update's dz is read next by
+// K41 and K42, and the 128 MiB of both halves fit the MALL)
+__device__ int g_head_dz_plain = 0;
+
 // ---- shared epilogue: everything after h = act(z) of a 64-row tile is in LDS ----------------------
 // MODE: 0 Gaussian actor, 1 Categorical actor, 2 critic.  ALGO: 0 PPO, 1 A2C (actor only).
 // NW: the waves running it (4: K12 / K16, all of the block; 2: K16W's epilogue waves).  Epilogue thread e (0 .. 64 NW)
@@ -487,7 +491,8 @@ struct HeadEpi {
         }
         d *= act_g<ACT>(h, slope);
 #if XPA_HEAD_PROBE != 4  // 4 = epilogue alone without the dz stores
-        __builtin_nontemporal_store(d, dzrow + e + NT * j);
+        if (g_head_dz_plain) dzrow[e + NT * j] = d;   // A/B (xpa_head_store_probe): dz kept in the caches for K41 / K42
+        else __builtin_nontemporal_store(d, dzrow + e + NT * j);
 #endif
         acc_dbh[j] += d;
     }
@@ -1458,6 +1463,10 @@ __global__ __launch_bounds__(1024) void lds_poison_kernel() {
 XPA_API int xpa_lds_poison(xpa_stream_t stream) {
     lds_poison_kernel<<<dim3(512), dim3(1024), 0, (hipStream_t)stream>>>();
     return xpa_launch_status();
+}
+
+XPA_API int xpa_head_store_probe(int plain) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_head_dz_plain), &plain, sizeof(int));
 }
 
 // diagnostics only (tools/k16w_ab.py --probe): see g_ws_probe
