@@ -61,6 +61,7 @@ def parse():
                    help="K13's h stores: non-temporal (default) or plain (A/B; xpa_thin_probe)")
     p.add_argument("--dz-store", choices=("nt", "plain"), default="nt",
                    help="the head kernels' dz stores: non-temporal (default) or plain (A/B; xpa_head_store_probe)")
+    p.add_argument("--s3-probe", type=int, default=0, help="xpa_s3_probe mask for A/B runs (0: the production forms)")
     p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc HBM-traffic passes")
     p.add_argument("--no-rocprof", action="store_true",
                    help="skip the child rocprofv3 --kernel-trace run that times the in-loop GAE launches")
@@ -824,6 +825,8 @@ def main():
     ops.S3_HEADS = args.s3_heads
     if args.thin_store == "plain":
         ops.lib().xpa_thin_probe(1)
+    if args.s3_probe:
+        ops.lib().xpa_s3_probe(args.s3_probe)
     rank, local, world = init_from_env()
     device = local_device(local)
     torch.cuda.set_device(device)

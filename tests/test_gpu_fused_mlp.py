@@ -935,3 +935,29 @@ def test_head_gemm_s3q_equals_s3p(algo, dist, K, B, code):
     ref, got = run("s3p"), run("s3q")
     for i, (a_, b_) in enumerate(zip(ref, got)):
         assert torch.equal(a_, b_), i
+
+
+@pytest.mark.parametrize("rows,din,code", [(65536, 17, 1), (4133, 17, 1), (300, 4, 0), (20, 17, 1)])
+def test_trunk_bwd_sign_lookahead_equals_default(rows, din, code):
+    """K42S's lookahead form (xpa_s3_probe bit 128: 4-stage ring, chunk c + 1's A split between chunk c's MFMA blocks)
+    == the default form bit for bit (same products, same order per accumulator), including 1- and 2-chunk tails."""
+    from xuanpolicy_amd import ops
+    L = ops.lib()
+    g = torch.Generator(device=DEV).manual_seed(rows + 3 * din)
+    xr = torch.randn(rows, din, device=DEV, generator=g)
+    h = torch.randn(rows, 256, device=DEV, generator=g)
+    for k in (512, 32, 16):
+        dz = torch.randn(rows, k, device=DEV, generator=g)
+        w = torch.randn(k, 256, device=DEV, generator=g) / 16
+        bs = ops.s3_split(w)
+        bits = (h > 0).view(rows, 8, 32).to(torch.int32)
+        sign = (bits << torch.arange(8, device=DEV, dtype=torch.int32).view(1, 8, 1)).sum(1).to(torch.uint8)
+        sign = sign.contiguous().view(torch.int32).view(rows, 8)
+        ref = ops.s3_gemm_trunk_bwd(dz, bs, k, None, xr, code, 0.01, h_sign=sign)
+        try:
+            assert L.xpa_s3_probe(128) == 0
+            got = ops.s3_gemm_trunk_bwd(dz, bs, k, None, xr, code, 0.01, h_sign=sign)
+            torch.cuda.synchronize()
+        finally:
+            L.xpa_s3_probe(0)
+        assert torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1]), k

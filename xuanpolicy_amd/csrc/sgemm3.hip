@@ -373,6 +373,32 @@ __global__ __launch_bounds__(512, 1) void s3_gemm_ws_kernel(const float *__restr
 // the B operand of Y = x^T dz1 as it is (registers 8s .. 8s + 7 = the 8 k of k step s, cdna_hip_programming.md §3),
 // x^T's fragment holds the same rows.  Per column block the 8 waves' Y [d_in x 32] meet in LDS and are added in wave
 // order; one partial row per block (xpa_s3_gemm_trunk_bwd_num_partials), finalized by the caller's f64 column sums.
+// K42S lookahead form (r04, xpa_s3_probe bit 128): a 4-stage ring, each wave splitting chunk c + 1's A fragment
+// between chunk c's MFMA blocks (K41V's interleave), so the split no longer precedes the MFMAs of its own chunk
+__device__ __forceinline__ void a_split(const char *st, int lane, int wave, bf16x8 &ah, bf16x8 &am, bf16x8 &al) {
+    const int h = lane >> 5, i = lane & 31;
+    const int sw = (i >> 2) & 3;
+    const float *arow = reinterpret_cast<const float *>(st) + (wave * 32 + i) * kKC;
+    xpa_split8(*reinterpret_cast<const float4 *>(arow + 4 * (h ^ sw)),
+               *reinterpret_cast<const float4 *>(arow + 4 * ((h + 2) ^ sw)), ah, am, al);
+}
+
+__device__ __forceinline__ void chunk_la(const char *st, const char *st_next, f32x16 (&acc)[8], int lane, int wave,
+                                         bf16x8 &ah, bf16x8 &am, bf16x8 &al) {
+    constexpr int kAImg = S3Geom<8>::kAImg;
+    const bf16x8 *bimg = reinterpret_cast<const bf16x8 *>(st + kAImg) + lane;
+    bf16x8 nh, nm, nl;
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) {
+        acc[cb] = xpa_mfma_s3(ah, am, al, bimg[cb * 64], bimg[(8 + cb) * 64], bimg[(16 + cb) * 64], acc[cb]);
+        if (cb == 1) a_split(st_next, lane, wave, nh, nm, nl);   // past the last chunk: a stale stage, unused
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    ah = nh;
+    am = nm;
+    al = nl;
+}
+
 template <int ACT>
 __device__ __forceinline__ float tb_act_g(float h, float slope) {  // thin.hip act_g
     if (ACT == 1) return h > 0.f ? 1.f : slope;
@@ -382,7 +408,7 @@ __device__ __forceinline__ float tb_act_g(float h, float slope) {  // thin.hip a
 
 // SIGN (r04, K42S): act' from the sign bits K16R's actor launch wrote (byte col of the row's 32: bit cb = h[row, 32 cb +
 // col] > 0; LeakyReLU / identity only) instead of the 1 KiB h row — the same factor, 64 MiB less read per C2 update.
-template <int ACT, bool SIGN = false>
+template <int ACT, bool SIGN = false, int LA = 0>
 __global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *__restrict__ a, int64_t lda,
                                                                    const __bf16 *__restrict__ bs, int64_t M,
                                                                    int nchunks, const float *__restrict__ hmat,
@@ -392,7 +418,8 @@ __global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *
                                                                    const unsigned *__restrict__ hsign = nullptr) {
     static_assert(!SIGN || ACT != 2, "sign bits carry act' of LeakyReLU / identity only");
     using G = S3Geom<8>;
-    __shared__ __attribute__((aligned(16))) char lds[3 * G::kStage];
+    constexpr int kS = LA ? 4 : 3;   // ring stages (4 x 40 KiB = the whole 160 KiB with the lookahead)
+    __shared__ __attribute__((aligned(16))) char lds[kS * G::kStage];
     const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -402,6 +429,26 @@ __global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *
     for (int cb = 0; cb < 8; ++cb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[cb][r] = 0.f;
+    if constexpr (LA) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+            if (d < nchunks) issue<8>(base + d * G::kStage, a, lda, bs, r0, M, d, lane, wave);
+        // chunk 0 landed (chunks 1, 2 may fly), everyone's; then its A fragment split
+        if (nchunks >= 3) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * G::kDma) : "memory");
+        else if (nchunks == 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G::kDma) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        bf16x8 ah, am, al;
+        a_split(lds, lane, wave, ah, am, al);
+#pragma unroll 1
+        for (int ch = 0; ch < nchunks; ++ch) {
+            // chunk ch + 1 landed (ch + 2 may fly), everyone's; the stage chunk ch + 3 refills held chunk ch - 1,
+            // whose B fragments every wave read in iteration ch - 1 (its A in ch - 2)
+            if (ch + 2 < nchunks) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G::kDma) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            if (ch + 3 < nchunks) issue<8>(base + ((ch + 3) & 3) * G::kStage, a, lda, bs, r0, M, ch + 3, lane, wave);
+            chunk_la(lds + (ch & 3) * G::kStage, lds + ((ch + 1) & 3) * G::kStage, acc, lane, wave, ah, am, al);
+        }
+    } else {
 #pragma unroll
     for (int d = 0; d < 2; ++d)
         if (d < nchunks) issue<8>(base + d * G::kStage, a, lda, bs, r0, M, d, lane, wave);
@@ -411,6 +458,7 @@ __global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *
         else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         if (ch + 2 < nchunks) issue<8>(base + ((ch + 2) % 3) * G::kStage, a, lda, bs, r0, M, ch + 2, lane, wave);
         chunk<8, 0>(lds + (ch % 3) * G::kStage, acc, lane, wave);
+    }
     }
     __syncthreads();   // every wave done with the ring: the epilogue reuses its LDS
     // ---- dz1 = g * act'(h) in place (rows past M: 0)
@@ -1106,9 +1154,18 @@ XPA_API int xpa_s3_gemm_trunk_bwd_sign(const float *dz, int64_t ldz, const void 
     const dim3 grid((unsigned)xpa_s3_gemm_trunk_bwd_num_partials(rows)), block(512);
     const __bf16 *bs = static_cast<const __bf16 *>(b_split);
     const int nch = (int)(k / kKC);
-    if (act == 0)
+    const bool la = (g_s3_probe & 128) != 0;   // the lookahead form (A/B)
+    if (act == 0 && la)
+        s3_gemm_trunk_bwd_kernel<0, true, 1><<<grid, block, 0, stream>>>(dz, ldz, bs, rows, nch, nullptr, 0, x, ldx,
+                                                                          (int)d_in, slope, partial_dw, partial_db,
+                                                                          h_sign);
+    else if (act == 0)
         s3_gemm_trunk_bwd_kernel<0, true><<<grid, block, 0, stream>>>(dz, ldz, bs, rows, nch, nullptr, 0, x, ldx,
                                                                        (int)d_in, slope, partial_dw, partial_db, h_sign);
+    else if (la)
+        s3_gemm_trunk_bwd_kernel<1, true, 1><<<grid, block, 0, stream>>>(dz, ldz, bs, rows, nch, nullptr, 0, x, ldx,
+                                                                          (int)d_in, slope, partial_dw, partial_db,
+                                                                          h_sign);
     else
         s3_gemm_trunk_bwd_kernel<1, true><<<grid, block, 0, stream>>>(dz, ldz, bs, rows, nch, nullptr, 0, x, ldx,
                                                                        (int)d_in, slope, partial_dw, partial_db, h_sign);
