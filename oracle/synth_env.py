@@ -185,9 +185,15 @@ class DummyVecEnvRef:
     buf_obs is one array for the object's life (float32, uint8 with atari=True), so an agent that keeps a reference
     to it across envs.step (ppoclip_agent.py:60 `obs = self.envs.buf_obs`) sees the step's writes — the reference's
     first-store alias.  record: every action array passed to step() is appended to .actions (the tests hand the
-    device agent's draws to the oracle loop)."""
+    device agent's draws to the oracle loop).
 
-    def __init__(self, envs, observation_space=None, action_space=None, atari=False):
+    rebind=True restates SubprocVecEnv_Gym's contract instead (gym_vec_env.py:89-121): reset() and step() bind a NEW
+    buf_obs array (np.array of the workers' observations) rather than writing the old one, so an agent's reference
+    taken before envs.step keeps the pre-step observations (no first-store alias), and a done env's reset_obs is
+    np.array of the worker's one-element result tuple: shape (1,) + obs_shape."""
+
+    def __init__(self, envs, observation_space=None, action_space=None, atari=False, rebind=False):
+        self.rebind = bool(rebind)
         self.envs = list(envs)
         self.num_envs = len(self.envs)
         e0 = self.envs[0]
@@ -203,6 +209,11 @@ class DummyVecEnvRef:
         self.actions = []
 
     def reset(self):
+        if self.rebind:
+            res = [env.reset() for env in self.envs]
+            self.buf_obs = np.array([o for o, _ in res])
+            self.buf_infos = [i for _, i in res]
+            return self.buf_obs.copy(), list(self.buf_infos)
         for e, env in enumerate(self.envs):
             obs, info = env.reset()
             self.buf_obs[e] = obs
@@ -211,11 +222,23 @@ class DummyVecEnvRef:
 
     def step(self, actions):
         self.actions.append(np.array(actions, copy=True))
-        for e, env in enumerate(self.envs):
-            obs, self.buf_rews[e], self.buf_dones[e], self.buf_trunctions[e], self.buf_infos[e] = env.step(actions[e])
-            if self.buf_dones[e] or self.buf_trunctions[e]:
-                self.buf_infos[e]["reset_obs"], _ = env.reset()
-            self.buf_obs[e] = obs
+        if self.rebind:
+            res = [env.step(actions[e]) for e, env in enumerate(self.envs)]
+            self.buf_obs = np.array([r[0] for r in res])
+            self.buf_rews = np.array([r[1] for r in res])
+            self.buf_dones = np.array([r[2] for r in res])
+            self.buf_trunctions = np.array([r[3] for r in res])
+            self.buf_infos = [r[4] for r in res]
+            for e, env in enumerate(self.envs):
+                if self.buf_dones[e] or self.buf_trunctions[e]:
+                    self.buf_infos[e]["reset_obs"] = np.array((env.reset()[0],))
+        else:
+            for e, env in enumerate(self.envs):
+                obs, self.buf_rews[e], self.buf_dones[e], self.buf_trunctions[e], self.buf_infos[e] = \
+                    env.step(actions[e])
+                if self.buf_dones[e] or self.buf_trunctions[e]:
+                    self.buf_infos[e]["reset_obs"], _ = env.reset()
+                self.buf_obs[e] = obs
         return (self.buf_obs.copy(), self.buf_rews.copy(), self.buf_dones.copy(), self.buf_trunctions.copy(),
                 list(self.buf_infos))
 

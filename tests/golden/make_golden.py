@@ -645,6 +645,144 @@ def capture_perdqn_agent(N=4, n_size=128, batch=64, A=18, steps=48, seed=13, max
     print(fname, len(out), "updates", n_up)
 
 
+# ----------------------------------------------------------------------------------------------
+# G11: the reference's own train() loop over its own host VecEnvs (round 5).  PPOCLIP_Agent.train / A2C_Agent.train
+# (ppoclip_agent.py:59-111, a2c_agent.py:57-107) over DummyVecEnv_Gym / DummyVecEnv_Atari / SubprocVecEnv_Gym
+# (gym_vec_env.py:40-231) of SynthBox / SynthAtari thunks, split into several train() calls whose boundaries fall on
+# done steps.  Recorded: every action handed to envs.step (the oracle loop is fed them: the reference samples torch's
+# CPU generator), and at every full-buffer point (mem.clear, after the learner's updates) the whole buffer, every
+# closure and bootstrap, the obs / return RunningMeanStd state, the return tracker, and the post-update weights
+# (the oracle loads them there, so the fixture pins the LOOP; the learner is pinned by G3-G5).  At the end: the RMS
+# state and tracker again.
+VEC_CASES = {
+    # name: (algo, discrete, D / K, A, N, T, max_ep, obsnorm, calls, vec)
+    "ppo_gauss_norm": ("ppo", False, 5, 3, 8, 16, 5, True, (5, 5, 6, 16), "dummy"),
+    "ppo_gauss_raw": ("ppo", False, 5, 3, 8, 16, 5, False, (5, 5, 6, 16), "dummy"),
+    "a2c_cat_norm": ("a2c", True, 5, 4, 8, 16, 5, True, (5, 5, 6, 16), "dummy"),
+    "ppo_gauss_raw_subproc": ("ppo", False, 5, 3, 8, 16, 5, False, (5, 5, 6, 16), "subproc"),
+    "atari_a2c": ("a2c", True, None, 6, 8, 32, 40, False, (17, 15, 32), "atari"),
+}
+VEC_ATARI_NET = dict(filters=[8, 8], kernels=[8, 4], strides=[4, 2], fc_hidden_sizes=[16])
+
+
+class _VecBox(SynthBoxEnv):
+    """SynthBoxEnv with the reference's env contract (spaces set by the ctor; close()); module level so that
+    SubprocVecEnv_Gym's spawned workers can unpickle the thunks."""
+
+    def close(self):
+        pass
+
+
+def _vec_box_thunk(D, A, seed, i, discrete, max_ep):
+    spaces = (gym.spaces.Box(-1, 1, (D,)), gym.spaces.Discrete(A) if discrete else gym.spaces.Box(-1, 1, (A,)))
+    return _VecBox(D, A, seed=seed, env_index=i, discrete=discrete, max_episode_steps=max_ep, spaces=spaces)
+
+
+def capture_vecloop(name, seed=11):
+    import functools
+    algo, discrete, D, A, N, T, max_ep, obsnorm, calls, vec = VEC_CASES[name]
+    atari = vec == "atari"
+    cfg = types.SimpleNamespace(render=False, n_steps=T, n_minibatch=4, n_epoch=2, gamma=0.99, gae_lambda=0.95,
+                                env_name="Atari" if atari else "SynthBox", use_gae=True, use_advnorm=True, device="cpu",
+                                model_dir="./models/", log_dir="./logs/", vf_coef=0.25, ent_coef=0.01, clip_range=0.2,
+                                clip_grad_norm=0.5, use_grad_clip=True, clip_grad=0.5, use_obsnorm=obsnorm,
+                                use_rewnorm=obsnorm, obsnorm_range=5, rewnorm_range=5, seed=seed, logger="tensorboard",
+                                test_mode=False)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    if atari:
+        obs_space, act_space = gym.spaces.Box(0, 255, (84, 84, 4)), gym.spaces.Discrete(A)
+
+        class _Env(SynthAtariEnv):
+            observation_space, action_space = obs_space, act_space
+
+            def close(self):
+                pass
+        envs = DummyVecEnv_Atari([(lambda i=i: _Env(i, seed=seed, n_actions=A, max_episode_steps=max_ep))
+                                  for i in range(N)])
+        net = VEC_ATARI_NET
+        rep = AC_CNN_Atari((84, 84, 4), net["kernels"], net["strides"], net["filters"], None,
+                           torch.nn.init.orthogonal_, torch.nn.ReLU, "cpu", net["fc_hidden_sizes"])
+        policy = Categorical_AC_Policy(act_space, rep, [], [], None, torch.nn.init.orthogonal_, torch.nn.ReLU, "cpu")
+    else:
+        thunks = [functools.partial(_vec_box_thunk, D, A, seed, i, discrete, max_ep) for i in range(N)]
+        if vec == "subproc":
+            from xuance.environment.gym.gym_vec_env import SubprocVecEnv_Gym
+            envs = SubprocVecEnv_Gym(thunks)
+        else:
+            envs = DummyVecEnv_Gym(thunks)
+        policy = _policy(D, A, discrete, seed=seed)
+    out = {}
+    _sd("sd0/", policy, out)
+    opt = torch.optim.Adam(policy.parameters(), 4e-4, eps=1e-5)
+    sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.0, total_iters=10000)
+    agent = (PPOCLIP_Agent if algo == "ppo" else A2C_Agent)(cfg, envs, policy, opt, sch, "cpu")
+    envs.reset()
+    iters = sum(calls) // T
+    rec = {"closed": np.zeros((iters, N, T), np.uint8), "boot": np.zeros((iters, N, T), np.float32)}
+    snaps, env_acts = [], []
+    mem = agent.memory
+    it = {"k": 0}
+    orig_fp, orig_clear, orig_step = mem.finish_path, mem.clear, envs.step
+
+    def rms_state():
+        return {"obs_mean": np.array(agent.obs_rms.mean, np.float64, copy=True),
+                "obs_var": np.array(agent.obs_rms.var, np.float64, copy=True),
+                "obs_count": np.asarray(agent.obs_rms.count, np.float64),
+                "ret_mean": np.asarray(agent.ret_rms.mean, np.float64), "ret_var": np.asarray(agent.ret_rms.var, np.float64),
+                "ret_count": np.asarray(agent.ret_rms.count, np.float64),
+                "returns": np.array(agent.returns, np.float32, copy=True)}
+
+    def finish_path(val, i):
+        end = mem.n_size if mem.full else mem.ptr
+        if end > mem.start_ids[i] and it["k"] < iters:
+            rec["closed"][it["k"], i, end - 1] = 1
+            rec["boot"][it["k"], i, end - 1] = val
+        return orig_fp(val, i)
+
+    def clear():
+        s_ = {"act": mem.actions.copy(), "rew": mem.rewards.copy(), "val": mem.values.copy(),
+              "term": mem.terminals.copy(), "ret": mem.returns.copy(), "adv": mem.advantages.copy(),
+              "logp": mem.auxiliary_infos["old_logp"].copy() if algo == "ppo" else np.zeros((N, T), np.float32)}
+        if atari:
+            s_["frame_sum"] = mem.observations.reshape(N, T, -1).astype(np.int64).sum(-1)
+        else:
+            s_["obs"] = mem.observations.copy()
+        s_.update(rms_state())
+        for k_, v_ in policy.state_dict().items():
+            s_["sd/" + k_] = v_.detach().cpu().numpy().copy()
+        snaps.append(s_)
+        it["k"] += 1
+        return orig_clear()
+
+    def step(acts):
+        env_acts.append(np.asarray(acts).copy())
+        return orig_step(acts)
+
+    mem.finish_path, mem.clear, envs.step = finish_path, clear, step
+    try:
+        for k_ in calls:
+            agent.train(k_)
+    finally:
+        if vec == "subproc":
+            envs.close()
+    assert len(snaps) == iters
+    for k_ in snaps[0]:
+        out["it/" + k_] = np.stack([s_[k_] for s_ in snaps])
+    for k_, v_ in rms_state().items():
+        out["end/" + k_] = v_
+    out["closed"], out["boot"] = rec["closed"], rec["boot"]
+    out["env_actions"] = np.stack(env_acts)
+    out["calls"] = np.asarray(calls, np.int64)
+    out["config"] = np.asarray([N, T, D or 0, A, max_ep, int(obsnorm), int(discrete), seed, cfg.n_epoch,
+                                cfg.n_minibatch], np.int64)
+    fname = "vecloop_%s.npz" % name
+    np.savez_compressed(os.path.join(HERE, fname), **out)
+    mid = (out["closed"][:, :, :T - 1] != 0) & (out["it/term"][:, :, :T - 1] == 0)
+    print(fname, len(out), "closures", int(out["closed"].sum()), "mid truncations", int(mid.sum()),
+          "terminals", int(out["it/term"].sum()))
+
+
 if __name__ == "__main__":
     os.makedirs("/tmp/xref_run", exist_ok=True)
     os.chdir("/tmp/xref_run")
@@ -665,3 +803,6 @@ if __name__ == "__main__":
         capture_perdqn(B=2048, n_updates=3, seed=23, sync=2, net=PERDQN_PROD_NET, fname="perdqn_prod.npz",
                        every_sd=False)
         capture_perdqn_agent()
+    if "vecloop" in which:   # round 5: G11
+        for name in VEC_CASES:
+            capture_vecloop(name)

@@ -215,3 +215,39 @@ def test_atari_deferred_last_bootstrap_matches_per_step():
     assert int(bufs[0][1].sum()) > 48        # game overs inside the rollout as well as the last column
     for a, b in zip(*bufs):
         assert torch.equal(a, b)
+
+
+def test_a2c_raw_mid_bootstrap_from_next_values_matches_per_step():
+    """A2C over raw frames whose truncations are NOT terminal (gym's TimeLimit contract instead of the Atari flag rule):
+    a close at step t < T - 1 bootstraps with V(reset frames) (a2c_agent.py:88-95).  raw_mid_next reads it from the
+    rollout's own value column t + 1 after the rollout; the per-step form (defer_bootstrap=False) runs a second critic
+    forward over every env at every step.  The buffers must be identical."""
+    from xuanpolicy_amd.envs import SynthAtariVecEnv
+    from xuanpolicy_amd.runner import build_agent, get_arguments
+
+    class TruncOnlyAtari(SynthAtariVecEnv):
+        def __init__(self, *a, **kw):
+            super().__init__(*a, **kw)
+            self.truncation_implies_terminal = False
+
+        def step_device(self):
+            super().step_device()
+            self.term.mul_((self.trunc == 0).to(torch.uint8))   # game overs / the step limit: truncated only
+
+    bufs = []
+    for defer in (True, False):
+        cfg = get_arguments("a2c", "atari", "SynthAtari-v0")
+        cfg.parallels, cfg.n_steps, cfg.seed, cfg.n_epoch, cfg.n_minibatch = 48, 32, 5, 1, 4
+        cfg.max_episode_steps, cfg.defer_bootstrap = 9, defer
+        torch.manual_seed(5)
+        envs = TruncOnlyAtari(48, 6, seed=5, max_episode_steps=9, device=DEV)
+        agent = build_agent(cfg, DEV, envs=envs)
+        assert not agent.raw_defer and agent.raw_mid_next == defer
+        agent.train(32)
+        torch.cuda.synchronize()
+        m = agent.memory
+        bufs.append([t.clone() for t in (m.values, m.boot, m.closed, m.terminals, m.advantages, m.returns)])
+    closed, term = bufs[0][2][:, :-1] != 0, bufs[0][3][:, :-1] != 0
+    assert int((closed & ~term).sum()) > 48     # non-terminal closes inside the rollout
+    for a, b in zip(*bufs):
+        assert torch.equal(a, b)

@@ -169,6 +169,12 @@ class _OnPolicyAgent:
         self.raw_defer = (self.raw_obs and self.device_env and bool(_cfg(config, "defer_bootstrap", True))
                           and bool(getattr(envs, "truncation_implies_terminal", False)))
         self._zero_vboot = torch.zeros((N,), **f32) if self.raw_defer else None
+        # A2C over raw-frame device envs without that contract: a truncation at step t < T - 1 bootstraps with
+        # V(reset frames) = V(obs of step t + 1), which is exactly the value the rollout stores in column t + 1 (the
+        # same frames through the same critic forward, weights unchanged inside a rollout), so it is read from there
+        # after the rollout (_raw_mid_from_next) instead of a second critic forward over every env at every step
+        self.raw_mid_next = (self.raw_obs and self.device_env and self.boot_from_reset and not self.raw_defer
+                             and bool(_cfg(config, "defer_bootstrap", True)))
         self._graph = None
         self._graph_pool = None
         # device env steps per replayed graph (train() falls back to single-step replays at chunk boundaries it
@@ -274,7 +280,8 @@ class _OnPolicyAgent:
         mid = self.boot_from_reset and self.device_env
         if self.raw_obs:
             v_boot = self._zero_vboot if self.raw_defer else self._heads(final_obs)[2]
-            v_mid = self._heads(self.envs.obs)[2] if (mid and not self.raw_defer) else None
+            v_mid = (self._heads(self.envs.obs)[2] if (mid and not self.raw_defer and not self.raw_mid_next)
+                     else None)
             self._post_kernel(rew, term, trunc, v_boot, v_mid)
             return
         if self.defer_boot:
@@ -564,6 +571,18 @@ class _OnPolicyAgent:
         self._raw_vb[N:].copy_(self._heads(self.envs.final_obs)[2])
         ops.bootstrap_fixup(self._raw_vb, self._raw_slots, mem.terminals, mem.boot)
 
+    def _raw_mid_from_next(self):
+        """raw_mid_next: the bootstrap of every non-terminal close before the last step is V(reset frames) =
+        values[:, t + 1] (a2c_agent.py:88-95: obs[i] = reset_obs, then the critic on next_obs); K8 wrote V(final
+        frames) there, which only the last column keeps."""
+        mem = self.memory
+        T = self.n_steps
+        if T < 2:
+            return
+        mid = (mem.closed[:, :T - 1] != 0) & (mem.terminals[:, :T - 1] == 0)
+        b = mem.boot[:, :T - 1]
+        b.copy_(torch.where(mid, mem.values[:, 1:T], b))
+
     def _check_overflow(self):
         # More truncations per env than slots cannot happen for the device envs (their one truncation source is the
         # time limit, and __init__ sizes n_slots from it), so this guard of the env contract is checked without a
@@ -582,6 +601,8 @@ class _OnPolicyAgent:
         mem.size = self.n_steps
         if self.raw_defer:
             self._raw_last_bootstraps()
+        elif self.raw_mid_next:
+            self._raw_mid_from_next()
         zc = None
         one_slot = self.defer_boot and self.n_slots == 1   # the fused scans take one deferred truncation per env
         if (one_slot and not self.atari and not mem._pending and self.fuse_value_gae

@@ -198,6 +198,18 @@ class _Trunk:
         self.u8_conv1 = (C == 4 and c0.in_channels == 4 and c0.out_channels == 32 and tuple(c0.kernel_size) == (8, 8)
                          and c0.stride[0] == c0.stride[1] and c0.padding[0] == c0.padding[1]
                          and c0.padding_mode == "zeros")
+        # a small-channel conv (< 16 in or out) must run on K28 / K29 (forward, weight gradient and, past the first
+        # block, the data gradient): MIOpen's small-channel route is refused (_library_conv_guard).  A net with such
+        # a conv that K28 / K29 cannot take (e.g. a 3-channel RGB first conv, in_channels % 4 != 0) gets no explicit
+        # path: ValueError here sends the learner to the generic autograd path instead of failing mid-update.
+        for i, (conv, _, _) in enumerate(self.convs):
+            if min(conv.in_channels, conv.out_channels) >= 16 or (i == 0 and self.u8_conv1):
+                continue
+            if not self._igemm_shape_ok(conv) or (i > 0 and not self._dgrad_ok(conv)
+                                                  and not self._igemm_dgrad_shape_ok(conv)):
+                raise ValueError("conv %d -> %d channels (kernel %s): no K28 / K29 form and the small-channel "
+                                 "library route is refused" % (conv.in_channels, conv.out_channels,
+                                                              tuple(conv.kernel_size)))
 
     def params(self):
         out = []
@@ -296,21 +308,29 @@ class _Trunk:
     # suspect) always take K28 / K29.
     igemm_min_rows = 1 << 20
 
-    def _igemm_ok(self, conv, numel, rows=None):
-        """numel: the largest operand K28 / K29 load (32-bit buffer offsets: under 2 GiB); rows: the conv's output
-        pixels B x OH x OW (None: no size preference)."""
+    @staticmethod
+    def _igemm_shape_ok(conv):
+        """The shape part of K28 / K29's conditions (no size preference, no 2 GiB operand check)."""
         k, st, pd = conv.kernel_size, conv.stride, conv.padding
-        small_c = min(conv.in_channels, conv.out_channels) < 16
-        return (self.use_igemm and numel * 4 < 2 ** 31 and k[0] == k[1] and st[0] == st[1] and pd[0] == pd[1]
-                and (rows is None or small_c or rows >= self.igemm_min_rows)
-                and conv.padding_mode == "zeros"
+        return (k[0] == k[1] and st[0] == st[1] and pd[0] == pd[1] and conv.padding_mode == "zeros"
                 and conv.in_channels % 4 == 0 and conv.weight.is_contiguous()
                 and bool(ops.lib().xpa_conv_igemm_ok(conv.in_channels, conv.out_channels, k[0])))
 
-    def _igemm_dgrad_ok(self, conv, numel, rows=None):
+    @classmethod
+    def _igemm_dgrad_shape_ok(cls, conv):
         k, st = conv.kernel_size, conv.stride
-        return (self._igemm_ok(conv, numel, rows) and st[0] <= 2 and conv.out_channels % 4 == 0
+        return (cls._igemm_shape_ok(conv) and st[0] <= 2 and conv.out_channels % 4 == 0
                 and bool(ops.lib().xpa_conv_igemm_ok(conv.out_channels, conv.in_channels, k[0])))
+
+    def _igemm_ok(self, conv, numel, rows=None):
+        """numel: the largest operand K28 / K29 load (32-bit buffer offsets: under 2 GiB); rows: the conv's output
+        pixels B x OH x OW (None: no size preference)."""
+        small_c = min(conv.in_channels, conv.out_channels) < 16
+        return (self.use_igemm and numel * 4 < 2 ** 31 and (rows is None or small_c or rows >= self.igemm_min_rows)
+                and self._igemm_shape_ok(conv))
+
+    def _igemm_dgrad_ok(self, conv, numel, rows=None):
+        return self._igemm_ok(conv, numel, rows) and self._igemm_dgrad_shape_ok(conv)
 
     @staticmethod
     def _out_rows(conv, shape):

@@ -102,6 +102,12 @@ class Rows:
         self.dtype = flat.dtype
 
 
+def _vec4_rows(t):
+    """The split GEMMs (K40 / K41 / K42) read operands as 16-B vectors: unit column stride, a row stride that is a
+    multiple of 4 floats and a 16-B aligned base.  Anything else takes the f32 library / chain path."""
+    return t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
+
+
 class FusedActorCritic:
     """Built from a Gaussian/Categorical actor-critic policy whose parameters live in a FlatState
     (pass it as `flat` to use the paired actor|critic hidden layer when head_placement applied)."""
@@ -359,10 +365,14 @@ class FusedActorCritic:
         if self._hws is None or self._hws.batch != B:
             self._hws = ops.HeadWorkspace(B, K, s.device, paired=paired)
         gemm = wh_split = None
+        trunk = x.trunk if z_a is None and isinstance(x, Rows) else None
         splits = []   # (matrix, name): every split this update needs, one launch (xpa_s3_split_batch)
         if z_a is None:   # K16
             gemm = (s, (lin_ah.weight, lin_ah.bias), (lin_ch.weight, lin_ch.bias))
-            if ops.S3_GEMMS and ops.S3_HEADS in ("s3p", "s3q") and not ops.K16W_ENABLED:   # K16P / K16Q: Wh^T's planes
+            # K16P / K16Q: Wh^T's planes.  With a deferred trunk the planes select K16R, which runs only behind
+            # TRUNK_S3R; the use_trunk_heads opt-in (K16X) takes Wh in f32
+            if (ops.S3_GEMMS and ops.S3_HEADS in ("s3p", "s3q") and not ops.K16W_ENABLED
+                    and (trunk is None or self._s3r_on())):
                 splits += [(lin_ah.weight.t(), "s3p_a"), (lin_ch.weight.t(), "s3p_c")]
         if paired and len(self.rep) > 0 and self._dx_split_ok(self.pair[0]):
             splits.append((self.pair[0], "dx"))
@@ -384,7 +394,7 @@ class FusedActorCritic:
                                               colsum_queue=self._cq, gemm=gemm, sq_logstd=self._sq.data_ptr(),
                                               wh_split=wh_split,
                                               defer_loss=True,
-                                              trunk=x.trunk if gemm is not None and isinstance(x, Rows) else None)
+                                              trunk=trunk)
         have_rep = len(self.rep) > 0
         if paired:   # dW of both hidden layers and dX (K = 512, no accumulate pass) as single GEMMs
             dz = self._hws.dz_pair
@@ -494,7 +504,7 @@ class FusedActorCritic:
         False (nothing done) when it does not apply: not the split GEMMs, more than one representation layer, no K13
         first layer, d_in > 32, or rows not given as the gathered minibatch."""
         if not (self.FUSE_TRUNK_BWD and self._dx_split_ok(self.pair[0]) and len(self.rep) == 1 and self.thin0
-                and dz.stride(1) == 1):
+                and _vec4_rows(dz)):
             return False
         lin, code, slope = self.rep[0]
         xr = x.gathered if isinstance(x, Rows) else x
@@ -529,7 +539,7 @@ class FusedActorCritic:
         """dX = dz w (w [k, n_in]): K40 on the bf16 matrix cores by the three-way split when ops.S3_GEMMS and the shape
         fits (n_in = 256, k % 16 == 0; w's planes were written by this update's split launch), else the f32 GEMM."""
         k, n_in = w.shape
-        if not (self._dx_split_ok(w) and dz.stride(1) == 1):
+        if not (self._dx_split_ok(w) and _vec4_rows(dz)):
             return torch.mm(dz, w)
         return ops.s3_gemm(dz, self._split_buf(k, "dx", dz.device), k)
 
@@ -541,7 +551,7 @@ class FusedActorCritic:
         B, n_out = dz.shape
         n_in = x.shape[1]
         if (queue is not None and ops.S3_GEMMS and n_in == 256 and n_out % 128 == 0 and isinstance(x, torch.Tensor)
-                and x.stride(1) == 1 and dz.stride(1) == 1):
+                and _vec4_rows(x) and _vec4_rows(dz)):
             S = ops.s3_wgrad_slices(B, n_out)
             key = ("s3wgrad", S, n_out)
             ws = self._partials.get(key)
