@@ -940,7 +940,7 @@ def test_head_gemm_s3q_equals_s3p(algo, dist, K, B, code):
 @pytest.mark.parametrize("rows,din,code", [(65536, 17, 1), (4133, 17, 1), (300, 4, 0), (20, 17, 1)])
 def test_trunk_bwd_sign_lookahead_equals_default(rows, din, code):
     """K42S's lookahead form (xpa_s3_probe bit 128: 4-stage ring, chunk c + 1's A split between chunk c's MFMA blocks)
-    == the default form bit for bit (same products, same order per accumulator), including 1- and 2-chunk tails."""
+    and its ping-pong form (bit 256: the two waves of a SIMD one phase apart) == the default form bit for bit (same products, same order per accumulator), including 1- and 2-chunk tails."""
     from xuanpolicy_amd import ops
     L = ops.lib()
     g = torch.Generator(device=DEV).manual_seed(rows + 3 * din)
@@ -954,10 +954,11 @@ def test_trunk_bwd_sign_lookahead_equals_default(rows, din, code):
         sign = (bits << torch.arange(8, device=DEV, dtype=torch.int32).view(1, 8, 1)).sum(1).to(torch.uint8)
         sign = sign.contiguous().view(torch.int32).view(rows, 8)
         ref = ops.s3_gemm_trunk_bwd(dz, bs, k, None, xr, code, 0.01, h_sign=sign)
-        try:
-            assert L.xpa_s3_probe(128) == 0
-            got = ops.s3_gemm_trunk_bwd(dz, bs, k, None, xr, code, 0.01, h_sign=sign)
-            torch.cuda.synchronize()
-        finally:
-            L.xpa_s3_probe(0)
-        assert torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1]), k
+        for form in (128, 256):   # 256: the ping-pong k loop (r05)
+            try:
+                assert L.xpa_s3_probe(form) == 0
+                got = ops.s3_gemm_trunk_bwd(dz, bs, k, None, xr, code, 0.01, h_sign=sign)
+                torch.cuda.synchronize()
+            finally:
+                L.xpa_s3_probe(0)
+            assert torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1]), (k, form)

@@ -155,8 +155,8 @@ def test_wgrad_wave_specialised_equals_k41(rows, m, slices):
 
 @pytest.mark.parametrize("m,k", [(65536, 512), (4133, 256), (100, 32)])
 def test_gemm_wave_specialised_equals_k40(m, k):
-    """K40W (producer / consumer waves, form bit 16), K40's two-block form (bit 8) and its 64 x 128 wave tile (bit 32)
-    write K40's output bit for bit:
+    """K40W (producer / consumer waves, form bit 16), K40's two-block form (bit 8), its 64 x 128 wave tile (bit 32) and
+    its ping-pong k loop (bit 256, r05) write K40's output bit for bit:
     the same split, the same six products in the same order per accumulator, the same k order."""
     from xuanpolicy_amd import ops
     L = ops.lib()
@@ -165,7 +165,7 @@ def test_gemm_wave_specialised_equals_k40(m, k):
     sp = ops.s3_split(torch.randn(k, 256, device=DEV, generator=g) / 16)
     ref = ops.s3_gemm(a, sp, k)
     try:
-        for form in (8, 16, 32):
+        for form in (8, 16, 32, 256):
             assert L.xpa_s3_probe(form) == 0
             out = ops.s3_gemm(a, sp, k)
             torch.cuda.synchronize()
@@ -204,20 +204,21 @@ def test_wgrad_vector_staged_matches_f32_gemm_error(rows, m, lda_pad, slices):
 def test_wgrad_interleaved_schedule_equals_k41v(rows, m, lda_pad, slices):
     """K41V's interleaved schedule (the default: the next stage's split placed between the MFMA blocks, the last
     chunks' staging unconditional) writes the partials of hipcc's own schedule (xpa_s3_probe bit 64) bit for bit: the
-    same products per accumulator in the same order."""
+    same products per accumulator in the same order; so does the ping-pong form (bit 256, r05)."""
     from xuanpolicy_amd import ops
     L = ops.lib()
     g = torch.Generator(device=DEV).manual_seed(rows + 11 * m)
     a = _wide((rows, m + lda_pad), g)[:, :m]
     b = torch.randn(rows, 256, device=DEV, generator=g)
     ref = ops.s3_wgrad(a, b, slices=slices)
-    try:
-        assert L.xpa_s3_probe(64) == 0
-        got = ops.s3_wgrad(a, b, slices=slices)
-        torch.cuda.synchronize()
-    finally:
-        L.xpa_s3_probe(0)
-    assert torch.equal(ref, got)
+    for form in (64, 256):   # 256: the ping-pong form (r05)
+        try:
+            assert L.xpa_s3_probe(form) == 0
+            got = ops.s3_wgrad(a, b, slices=slices)
+            torch.cuda.synchronize()
+        finally:
+            L.xpa_s3_probe(0)
+        assert torch.equal(ref, got), form
 
 
 def test_split_batch_equals_single_splits():

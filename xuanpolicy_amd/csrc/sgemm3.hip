@@ -399,6 +399,128 @@ __device__ __forceinline__ void chunk_la(const char *st, const char *st_next, f3
     al = nl;
 }
 
+// ---- PP (r05): the k loop as a ping-pong between the two waves of each SIMD ------------------------------------------
+// K40 / K42 as written run both waves of a SIMD (w and w + 4) through the same chunk in lockstep: after each chunk
+// barrier both split their A fragment and read their B fragments, then both issue their 48 MFMAs, so the matrix pipe
+// idles through the first part and the VALU / LDS through the second (r04q probes: 84 us with no operand loads at all
+// against ~45 us of MFMA time; the non-MFMA part alone 42 us — nothing overlapped).  Here the k loop is a sequence of
+// phases, one block barrier each, and the halves (half = w >> 2) run one phase apart:
+//     phase p, half h, q = p - h:  q even -> prep chunk q / 2 (its A fragment: 2 ds_read_b128 + the split in VALU)
+//                                  q odd  -> compute chunk (q - 1) / 2 (48 MFMAs, B fragments read from the stage)
+// so in every phase one wave of each SIMD issues MFMAs while its partner preps.  Chunk c's stage is read in phases 2c
+// .. 2c + 2; chunk c + 3 refills it, issued at the start of phase 2c + 3 (each wave its own DMAs, as K40) and waited
+// for (counted vmcnt + the barrier) at the end of phase 2c + 5, the phase before half 0 preps it.  Same products, same
+// k order per accumulator as K40: the outputs are K40's bit for bit.
+// the B fragments of column block cb + 1 are read while cb's six MFMAs run (one block ahead, sched_barrier-pinned:
+// hipcc otherwise hoists all 24 reads, 96 VGPRs beside the 128 accumulators)
+__device__ __forceinline__ void pp_compute(const char *st, f32x16 (&acc)[8], int lane, const bf16x8 &ah,
+                                           const bf16x8 &am, const bf16x8 &al) {
+    const bf16x8 *bimg = reinterpret_cast<const bf16x8 *>(st + S3Geom<8>::kAImg) + lane;
+    bf16x8 bh = bimg[0], bm = bimg[8 * 64], bl = bimg[16 * 64];
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) {
+        bf16x8 nh, nm, nl;
+        if (cb + 1 < 8) {
+            nh = bimg[(cb + 1) * 64];
+            nm = bimg[(9 + cb) * 64];
+            nl = bimg[(17 + cb) * 64];
+        }
+        acc[cb] = xpa_mfma_s3(ah, am, al, bh, bm, bl, acc[cb]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (cb + 1 < 8) {
+            bh = nh;
+            bm = nm;
+            bl = nl;
+        }
+    }
+}
+
+__device__ __forceinline__ void pp_loop(unsigned base, const char *lds, const float *__restrict__ a, int64_t lda,
+                                        const __bf16 *__restrict__ bs, int64_t r0, int64_t M, int nchunks, int lane,
+                                        int wave, f32x16 (&acc)[8]) {
+    using G = S3Geom<8>;
+    const int N = nchunks;
+    issue<8>(base, a, lda, bs, r0, M, 0, lane, wave);
+    if (N > 1) {
+        issue<8>(base + G::kStage, a, lda, bs, r0, M, 1, lane, wave);
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G::kDma) : "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    // phase ends: even phases a bare barrier; odd phase 2m + 1 starts by issuing chunk m + 2 and ends once every
+    // wave's chunk m + 1 landed.  Each half runs its own straight-line loop (no branch around the MFMAs: hipcc copied
+    // and spilled the accumulators at the joins of a phase-indexed loop)
+    auto end_even = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto start_odd = [&](int m) {
+        if (m + 2 < N) issue<8>(base + ((m + 2) % 3) * G::kStage, a, lda, bs, r0, M, m + 2, lane, wave);
+    };
+    auto end_odd = [&](int m) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (m + 2 < N) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G::kDma) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    bf16x8 ah, am, al;
+    if (wave < 4) {   // half 0: phase 2c preps chunk c, phase 2c + 1 computes it
+#pragma unroll 1
+        for (int c = 0; c < N; ++c) {
+            a_split(lds + (c % 3) * G::kStage, lane, wave, ah, am, al);
+            end_even();
+            start_odd(c);
+            pp_compute(lds + (c % 3) * G::kStage, acc, lane, ah, am, al);
+            end_odd(c);
+        }
+        end_even();
+    } else {          // half 1: one phase behind
+        end_even();
+        start_odd(0);
+        a_split(lds, lane, wave, ah, am, al);
+        end_odd(0);
+#pragma unroll 1
+        for (int c = 1; c < N; ++c) {
+            pp_compute(lds + ((c - 1) % 3) * G::kStage, acc, lane, ah, am, al);
+            end_even();
+            start_odd(c);
+            a_split(lds + (c % 3) * G::kStage, lane, wave, ah, am, al);
+            end_odd(c);
+        }
+        pp_compute(lds + ((N - 1) % 3) * G::kStage, acc, lane, ah, am, al);
+        end_even();
+    }
+}
+
+// K40 with the ping-pong k loop (one 8-wave block per 256 rows, the 3-stage ring)
+__global__ __launch_bounds__(512, 1) void s3_gemm_pp_kernel(const float *__restrict__ a, int64_t lda,
+                                                            const __bf16 *__restrict__ bs, float *__restrict__ c,
+                                                            int64_t ldc, int64_t M, int nchunks) {
+    using G = S3Geom<8>;
+    __shared__ __attribute__((aligned(16))) char lds[3 * G::kStage];
+    const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int64_t r0 = (int64_t)blockIdx.x * G::kRows;
+    f32x16 acc[8];
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[cb][r] = 0.f;
+    pp_loop(base, lds, a, lda, bs, r0, M, nchunks, lane, wave, acc);
+    const int h = lane >> 5, col = lane & 31;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t row = r0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < M) {
+            float *crow = c + row * ldc + col;
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb) crow[cb * 32] = acc[cb][r];
+        }
+    }
+}
+
 template <int ACT>
 __device__ __forceinline__ float tb_act_g(float h, float slope) {  // thin.hip act_g
     if (ACT == 1) return h > 0.f ? 1.f : slope;
@@ -418,7 +540,7 @@ __global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *
                                                                    const unsigned *__restrict__ hsign = nullptr) {
     static_assert(!SIGN || ACT != 2, "sign bits carry act' of LeakyReLU / identity only");
     using G = S3Geom<8>;
-    constexpr int kS = LA ? 4 : 3;   // ring stages (4 x 40 KiB = the whole 160 KiB with the lookahead)
+    constexpr int kS = LA == 1 ? 4 : 3;   // ring stages (4 x 40 KiB = the whole 160 KiB with the lookahead)
     __shared__ __attribute__((aligned(16))) char lds[kS * G::kStage];
     const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
     const int t = threadIdx.x, lane = t & 63;
@@ -429,7 +551,9 @@ __global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *
     for (int cb = 0; cb < 8; ++cb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[cb][r] = 0.f;
-    if constexpr (LA) {
+    if constexpr (LA == 2) {
+        pp_loop(base, lds, a, lda, bs, r0, M, nchunks, lane, wave, acc);
+    } else if constexpr (LA == 1) {
 #pragma unroll
         for (int d = 0; d < 3; ++d)
             if (d < nchunks) issue<8>(base + d * G::kStage, a, lda, bs, r0, M, d, lane, wave);
@@ -1035,6 +1159,84 @@ __global__ __launch_bounds__(512, 1) void s3_wgrad_v_kernel(const float *__restr
         }
 }
 
+// K41V-PP (r05): K41V's staging and fragments with the two waves of each SIMD one phase apart (K40 / K42's ping-pong):
+// half 0 (waves 0-3) runs chunk c's MFMAs in phase 2c and stages its share of chunk c + 1 (its float4 units: the same
+// thread-to-unit map as K41V, so each half writes half of the chunk's k rows) in phase 2c + 1; half 1 stages in 2c and
+// computes in 2c + 1.  Chunk c + 1 is complete after phase 2c + 1; it reuses chunk c - 1's stage, which half 1 read
+// last in phase 2c - 1.  One raw barrier per phase (lgkmcnt(0) first: the stage writes landed); each thread's global
+// loads of chunk c + 2 are issued right after it stored its share of c + 1, two phases before their use.  Same
+// fragments, products and order per accumulator as K41V's plain schedule: the same outputs bit for bit.
+__global__ __launch_bounds__(512, 1) void s3_wgrad_pp_kernel(const float *__restrict__ A, int64_t lda,
+                                                             const float *__restrict__ B, int64_t ldb, int64_t rows,
+                                                             int64_t M, int slices, int64_t slice_rows,
+                                                             float *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * kVStage];
+    const int mtiles = (int)(M / kWgM);
+    const int nblk = slices * mtiles;
+    int L = blockIdx.x;
+    if (nblk % 8 == 0) L = (blockIdx.x & 7) * (nblk >> 3) + (blockIdx.x >> 3);  // one slice's tiles on one XCD
+    const int slice = L / mtiles, mt = L - slice * mtiles;
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wm = wave & 1, wn = wave >> 1;
+    const float *Am = A + (int64_t)mt * kWgM;
+    const int64_t k0 = (int64_t)slice * slice_rows;
+    const int64_t kend = min(rows, k0 + slice_rows);
+    const int nch = kend > k0 ? (int)((kend - k0 + kWgKC - 1) / kWgKC) : 0;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    VUnits u;
+    if (nch > 0) {
+        v_load(u, Am, lda, B, ldb, k0, kend, t);
+        v_store(lds, u, t);
+        if (nch > 1) v_load(u, Am, lda, B, ldb, k0 + kWgKC, kend, t);
+        bar();
+        if (wave < 4) {
+#pragma unroll 1
+            for (int c = 0; c < nch; ++c) {
+                v_chunk(lds + (c & 1) * kVStage, acc, lane, wm, wn);
+                bar();
+                if (c + 1 < nch) {
+                    v_store(lds + ((c + 1) & 1) * kVStage, u, t);
+                    if (c + 2 < nch) v_load(u, Am, lda, B, ldb, k0 + (int64_t)(c + 2) * kWgKC, kend, t);
+                }
+                bar();
+            }
+        } else {
+#pragma unroll 1
+            for (int c = 0; c < nch; ++c) {
+                if (c + 1 < nch) {
+                    v_store(lds + ((c + 1) & 1) * kVStage, u, t);
+                    if (c + 2 < nch) v_load(u, Am, lda, B, ldb, k0 + (int64_t)(c + 2) * kWgKC, kend, t);
+                }
+                bar();
+                v_chunk(lds + (c & 1) * kVStage, acc, lane, wm, wn);
+                bar();
+            }
+        }
+    }
+    float *o = out + ((int64_t)slice * M + (int64_t)mt * kWgM) * kN;
+    const int h = lane >> 5, col = lane & 31;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = 64 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) o[(int64_t)row * kN + 64 * wn + 32 * j + col] = acc[i][j][r];
+        }
+}
+
 }  // namespace
 
 // the split-K slice count of xpa_s3_wgrad for this shape (the caller's workspace: slices x m x 256 floats)
@@ -1059,7 +1261,9 @@ XPA_API int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ld
     const bool vec_ok = lda % 4 == 0 && ldb % 4 == 0 &&
                         ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
     if (vec_ok && (g_s3_probe & (1 | 2 | 4 | 8 | 32)) == 0) {   // K41V (bit 64: without its interleaved schedule)
-        if (g_s3_probe & 64)   // hipcc's own schedule (r04p: 115 us vs 104 interleaved at C2)
+        if (g_s3_probe & 256)   // the ping-pong form (r05)
+            s3_wgrad_pp_kernel<<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out);
+        else if (g_s3_probe & 64)   // hipcc's own schedule (r04p: 115 us vs 104 interleaved at C2)
             s3_wgrad_v_kernel<0><<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out);
         else
             s3_wgrad_v_kernel<1><<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out);
@@ -1155,7 +1359,16 @@ XPA_API int xpa_s3_gemm_trunk_bwd_sign(const float *dz, int64_t ldz, const void 
     const __bf16 *bs = static_cast<const __bf16 *>(b_split);
     const int nch = (int)(k / kKC);
     const bool la = (g_s3_probe & 128) != 0;   // the lookahead form (A/B)
-    if (act == 0 && la)
+    const bool pp = (g_s3_probe & 256) != 0;   // the ping-pong k loop (A/B)
+    if (pp && act == 0)
+        s3_gemm_trunk_bwd_kernel<0, true, 2><<<grid, block, 0, stream>>>(dz, ldz, bs, rows, nch, nullptr, 0, x, ldx,
+                                                                          (int)d_in, slope, partial_dw, partial_db,
+                                                                          h_sign);
+    else if (pp)
+        s3_gemm_trunk_bwd_kernel<1, true, 2><<<grid, block, 0, stream>>>(dz, ldz, bs, rows, nch, nullptr, 0, x, ldx,
+                                                                          (int)d_in, slope, partial_dw, partial_db,
+                                                                          h_sign);
+    else if (act == 0 && la)
         s3_gemm_trunk_bwd_kernel<0, true, 1><<<grid, block, 0, stream>>>(dz, ldz, bs, rows, nch, nullptr, 0, x, ldx,
                                                                           (int)d_in, slope, partial_dw, partial_db,
                                                                           h_sign);
@@ -1181,6 +1394,10 @@ XPA_API int xpa_s3_gemm(const float *a, int64_t lda, const void *b_split, float 
     const int nch = (int)(k / kKC);
     // form (probe bits 8 / 16): 0 = one 8-wave block per CU with a 3-stage ring, 8 = two 4-wave blocks per CU, 2 stages,
     // 16 = the wave-specialised K40W
+    if (g_s3_probe & 256) {   // the ping-pong k loop
+        s3_gemm_pp_kernel<<<dim3((unsigned)((m + 255) / 256)), dim3(512), 0, stream>>>(a, lda, bs, c, ldc, m, nch);
+        return xpa_launch_status();
+    }
     if (g_s3_probe & 32) {   // the 64 x 128 wave tile
         s3_gemm_kernel<8, 3, 0, 1><<<dim3((unsigned)((m + 255) / 256)), dim3(512), 0, stream>>>(a, lda, bs, c, ldc, m,
                                                                                               nch);
