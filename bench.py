@@ -62,6 +62,9 @@ def parse():
     p.add_argument("--dz-store", choices=("nt", "plain"), default="nt",
                    help="the head kernels' dz stores: non-temporal (default) or plain (A/B; xpa_head_store_probe)")
     p.add_argument("--s3-probe", type=int, default=0, help="xpa_s3_probe mask for A/B runs (0: the production forms)")
+    p.add_argument("--pair-sa", type=int, default=0, help="K41P's actor share of 128 slices (0: the default)")
+    p.add_argument("--crit-factored", choices=("on", "off"), default="on",
+                   help="the critic's factored backward (K41P / K42C, r05) or its dz_critic through K41V / K42S")
     p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc HBM-traffic passes")
     p.add_argument("--no-rocprof", action="store_true",
                    help="skip the child rocprofv3 --kernel-trace run that times the in-loop GAE launches")
@@ -823,6 +826,10 @@ def main():
 
     ops.S3_GEMMS = args.gemm == "split3"
     ops.S3_HEADS = args.s3_heads
+    from xuanpolicy_amd.fused_mlp import FusedActorCritic
+    FusedActorCritic.CRIT_FACTORED = args.crit_factored == "on"
+    if args.pair_sa:
+        ops.lib().xpa_s3_wgrad_pair_tune(args.pair_sa)
     if args.thin_store == "plain":
         ops.lib().xpa_thin_probe(1)
     if args.s3_probe:

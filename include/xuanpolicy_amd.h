@@ -620,6 +620,40 @@ int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ldb, int64
 int xpa_s3_gemm_trunk_bwd_sign(const float *dz, int64_t ldz, const void *b_split, int64_t k, const unsigned *h_sign,
                                const float *x, int64_t ldx, int64_t rows, int64_t d_in, int act, float slope,
                                float *partial_dw, float *partial_db, xpa_stream_t stream);
+/* r05 — the critic's factored backward (LeakyReLU / ReLU hidden layer, one output unit: dz_c[r, c] = dv[r] wc[c]
+ * (slope + (1 - slope) m[r, c]), m = [h_c > 0]), replacing the critic's half of the paired hidden layer's dX and dW
+ * inside loss.backward() of PPOCLIP_Learner.update / A2C_Learner.update (ppoclip_learner.py:40-46, a2c_learner.py:33-39)
+ * by masked GEMMs whose mask operand is exact in bf16 (three split products instead of six) and never storing dz_c.
+ * xpa_head_gemm_s3q_critic_mask: xpa_head_gemm_s3q_critic that also writes the hidden activations' sign bits
+ *   (mask [batch][8] u32, bit c & 31 of word c >> 5 = h[row, c] > 0) and d loss / d v per row (dv [batch]); dz may be
+ *   NULL (not stored).
+ * xpa_s3_split_batch_scaled: xpa_s3_split_batch with matrix i's rows k >= rs_from[i] scaled by rs_a[i] *
+ *   rs_w[i][k - rs_from[i]] before the split (rs_w[i] NULL: none), and with cs_out, cs_out[j] = cs_slope * sum_c
+ *   rs_w[c] B[rs_from + c][j] for the first scaled matrix.
+ * xpa_s3_gemm_trunk_bwd_crit: K42S with the critic's half of g = dz_pair . Wh_pair as dv[r] (m . V + cs), V = (1 -
+ *   slope) diag(wc) Wh_c and cs = slope wc . Wh_c (b_split = the scaled split of [Wh_a; Wh_c], k_a + k_c rows).
+ * xpa_s3_wgrad_pair: the paired layer's weight-gradient slices, out_a [sa, 256, 256] of dz_a^T h and out_c
+ *   [sc, 256, 256] of wc[c] ((1 - slope) m^T Y + slope colsum(Y)), Y = dv (.) h; slice counts and rows per slice from
+ *   xpa_s3_wgrad_pair_slices. */
+int xpa_head_gemm_s3q_critic_mask(int act, int64_t batch, int64_t hidden, const float *x, int64_t ldx,
+                                  const float *w_hidden_split, const float *b_hidden, int64_t ld_dz, const float *w,
+                                  const float *b, float slope, const int64_t *idx, int64_t n_rows, const float *ret,
+                                  float vf_coef, float *dz, float *partial_dw, float *partial_db_hidden,
+                                  float *partial_db_out, float *loss_partials, int64_t loss_width, xpa_stream_t stream,
+                                  unsigned *mask, float *dv);
+int xpa_s3_split_batch_scaled(int n_mat, const float *const *b, const int64_t *k, const int64_t *sk, const int64_t *sn,
+                              void *const *out, const float *const *rs_w, const float *rs_a, const int64_t *rs_from,
+                              float *cs_out, float cs_slope, xpa_stream_t stream);
+int xpa_s3_gemm_trunk_bwd_crit(const float *dz_a, int64_t ldz, const void *b_split, int64_t k_a, int64_t k_c,
+                               const unsigned *crit_mask, const float *crit_dv, const float *crit_cs,
+                               const unsigned *h_sign, const float *x, int64_t ldx, int64_t rows, int64_t d_in, int act,
+                               float slope, float *partial_dw, float *partial_db, xpa_stream_t stream);
+int xpa_s3_wgrad_pair_slices(int64_t rows, int64_t *sa, int64_t *sc, int64_t *per_a, int64_t *per_c);
+int xpa_s3_wgrad_pair_tune(int sa_target); /* the actor's share of 128 slices (default 68) */
+int xpa_s3_wgrad_pair(const float *dz_a, int64_t lda, const float *h, int64_t ldb, int64_t rows,
+                      const unsigned *crit_mask, const float *crit_dv, const float *crit_wc, float crit_slope,
+                      int64_t sa, int64_t per_a, int64_t sc, int64_t per_c, float *out_a, float *out_c,
+                      xpa_stream_t stream);
 /* K16R (r04): xpa_head_gemm_s3p_actor / _critic (w_hidden = the split buffer of Wh^T) with the heads' input h formed
  * inside from the gathered minibatch rows (the representation's one thin layer: x_rows [batch, d_in <= 20], w_in
  * [256, d_in], b_in, the heads' activation at slope_in) — xpa_thin_linear_act_fwd's h bit for bit, so the update

@@ -241,6 +241,17 @@ SIGNATURES = {
     "xpa_thin_probe": (ctypes.c_int, [ctypes.c_int]),
     "xpa_head_store_probe": (ctypes.c_int, [ctypes.c_int]),
     "xpa_s3_probe": (ctypes.c_int, [ctypes.c_int]),
+    "xpa_head_gemm_s3q_critic_mask": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p,
+                                                     c_f32, c_p, c_i64, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64, c_p,
+                                                     c_p, c_p]),
+    "xpa_s3_split_batch_scaled": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32,
+                                                 c_p]),
+    "xpa_s3_gemm_trunk_bwd_crit": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64,
+                                                  c_i64, ctypes.c_int, c_f32, c_p, c_p, c_p]),
+    "xpa_s3_wgrad_pair_slices": (ctypes.c_int, [c_i64, c_p, c_p, c_p, c_p]),
+    "xpa_s3_wgrad_pair_tune": (ctypes.c_int, [ctypes.c_int]),
+    "xpa_s3_wgrad_pair": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i64, c_p, c_p, c_p, c_f32, c_i64, c_i64, c_i64,
+                                         c_i64, c_p, c_p, c_p]),
     "xpa_s3_split_bytes": (c_i64, [c_i64, c_i64]),
     "xpa_s3_split_b": (ctypes.c_int, [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
     "xpa_s3_split_batch": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p, c_p]),

@@ -128,6 +128,8 @@ struct HeadArgs {
     float slope0;
     float *hout;
     unsigned *hmask;  // K16R: the trunk activations' sign bits [batch, 8 words] (actor; may be null)
+    unsigned *cmask;  // r05: the critic's hidden sign bits [batch, 8 words] (HeadEpi::mask_out; may be null)
+    float *cdv;       // r05: the critic's d loss / d v [batch] (may be null)
 };
 
 __device__ __forceinline__ void load_tile(float4 (&zq)[16], const float *__restrict__ z, int64_t ld, int64_t tile,
@@ -185,6 +187,12 @@ struct HeadEpi {
     float sum0, sum1, sum2, ent_const, inv_b, lo, hi, a_mean, a_inv, slope;
     float hd[KMAX];  // epilogue wave 0: the row's head outputs between the phase-1 passes and the loss
     int K, e;        // e: epilogue thread index
+    // r05, the critic's factored backward (K16Q critic, xpa_head_gemm_s3q_critic_mask): mask_out (nullable) gets the
+    // sign bits of the hidden activations, [batch][8] words, bit c & 31 of word c >> 5 = h[row, c] > 0; dv_out
+    // (nullable) d loss / d v per row; dz_on = false skips the dz stores (db_hidden / dW_out are still accumulated)
+    unsigned *mask_out = nullptr;
+    float *dv_out = nullptr;
+    bool dz_on = true;
 
     // W: output layer [K, 256]; s_stats: 2 floats of LDS.  init_a, a block barrier, then init_b.
     __device__ __forceinline__ void init_a(int e_, int K_in, const float *__restrict__ W,
@@ -432,6 +440,18 @@ struct HeadEpi {
         r1 = r0;
 #endif
         const int nr = (int)min((int64_t)r1, batch - tile * kTile);
+        unsigned mlo = 0u, mhi = 0u;   // mask_out: lane r of each wave ends with row r's two words of its 64 columns
+        auto ballot_row = [&](int rr, float h) {
+            if constexpr (CPT == 1) {
+                if (mask_out != nullptr) {
+                    const unsigned long long bl = __ballot(h > 0.f);
+                    if ((e & 63) == rr) {
+                        mlo = (unsigned)bl;
+                        mhi = (unsigned)(bl >> 32);
+                    }
+                }
+            }
+        };
         f2v wc2[CPT][KH2];
 #pragma unroll
         for (int j = 0; j < CPT; ++j)
@@ -455,9 +475,11 @@ struct HeadEpi {
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < 4; ++u) {
 #pragma unroll
                 for (int j = 0; j < CPT; ++j) col_row(j, hv[j][u], gq[u], wc2[j], dz + (tile * kTile + r + u) * ld);
+                ballot_row(r + u, hv[0][u]);
+            }
         }
         for (; r < nr; ++r) {
             float gq[KP];
@@ -465,6 +487,16 @@ struct HeadEpi {
             for (int q = 0; q < KP; ++q) gq[q] = s_dh[r][q];
 #pragma unroll
             for (int j = 0; j < CPT; ++j) col_row(j, s_h[r * kS + e + NT * j], gq, wc2[j], dz + (tile * kTile + r) * ld);
+            ballot_row(r, s_h[r * kS + e]);
+        }
+        if constexpr (CPT == 1) {
+            // rows r0 .. nr of this call: lane r's words (rows past the batch: not stored)
+            const int lr = e & 63;
+            if (mask_out != nullptr && lr >= r0 && lr < nr) {
+                unsigned *mrow = mask_out + (tile * kTile + lr) * 8 + 2 * (e >> 6);
+                mrow[0] = mlo;
+                mrow[1] = mhi;
+            }
         }
     }
     __device__ __forceinline__ void col_row(int j, float h, const float (&g)[KP], const f2v (&wc2)[KH2],
@@ -491,8 +523,10 @@ struct HeadEpi {
         }
         d *= act_g<ACT>(h, slope);
 #if XPA_HEAD_PROBE != 4  // 4 = epilogue alone without the dz stores
-        if (g_head_dz_plain) dzrow[e + NT * j] = d;   // A/B (xpa_head_store_probe): dz kept in the caches for K41 / K42
-        else __builtin_nontemporal_store(d, dzrow + e + NT * j);
+        if (dz_on) {
+            if (g_head_dz_plain) dzrow[e + NT * j] = d;   // A/B (xpa_head_store_probe): dz kept in the caches for K41 / K42
+            else __builtin_nontemporal_store(d, dzrow + e + NT * j);
+        }
 #endif
         acc_dbh[j] += d;
     }
@@ -513,6 +547,7 @@ struct HeadEpi {
         }
         loss(s_dh, in, ent_coef, vf_coef);
         __syncthreads();
+        if (MODE == 2 && dv_out != nullptr && e < 64 && tile * kTile + e < batch) dv_out[tile * kTile + e] = s_dh[e][0];
         p2(s_h, s_dh, tile, batch, 0, kTile, dz, ld);
         __syncthreads();  // s_h / s_dh reused by the next tile
     }
@@ -929,7 +964,9 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
                                                            const float *__restrict__ W0 = nullptr,
                                                            const float *__restrict__ b0 = nullptr, float slope0 = 0.f,
                                                            float *__restrict__ hout = nullptr, int64_t ldh = 0,
-                                                           unsigned *__restrict__ hmask = nullptr) {
+                                                           unsigned *__restrict__ hmask = nullptr,
+                                                           unsigned *__restrict__ cmask = nullptr,
+                                                           float *__restrict__ cdv = nullptr) {
     using Epi = HeadEpi<MODE, ALGO, ACT, KMAX>;
     // ONE LDS array (a second __shared__ object beside the DMA target can make hipcc wait vmcnt(0) before
     // every chunk's ds_reads): operand stages / h tile, then the epilogue's partials, d head and stats.
@@ -950,6 +987,9 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
     if ((int64_t)blockIdx.x >= head_partials(batch)) return;  // no partial row of its own (see kGridMax)
     Epi epi;
     epi.init_a(t, K_in, W, logstd, adv_partials, n_adv_partials, batch, clip_range, slope, s_stats);
+    epi.mask_out = cmask;
+    epi.dv_out = cdv;
+    epi.dz_on = dz != nullptr;
     __syncthreads();
     epi.init_b(s_stats);
     const float bh0 = bh[wave * 64 + (lane & 31)], bh1 = bh[wave * 64 + 32 + (lane & 31)];
@@ -1277,7 +1317,7 @@ void launch_one(const HeadArgs &a, hipStream_t s) {
                            a.ldxr, a.din, a.W0, a.b0, a.slope0, a.hout, a.ldh, nullptr);
     else if constexpr (KIND == 7)
         hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, false, 4>), grid, block, 0, s, XPA_HEAD_ARGS(a),
-                           nullptr, (int64_t)0, 0, nullptr, nullptr, 0.f, nullptr, (int64_t)0, nullptr);
+                           nullptr, (int64_t)0, 0, nullptr, nullptr, 0.f, nullptr, (int64_t)0, nullptr, a.cmask, a.cdv);
     else if constexpr (KIND == 6)
         hipLaunchKernelGGL((head_gemm_kernel<MODE, ALGO, ACT, KMAX, false, 3>), grid, block, 0, s, XPA_HEAD_ARGS(a),
                            a.xr, a.ldxr, a.din, a.W0, a.b0, a.slope0, a.hout, a.ldh, a.hmask);
@@ -1416,11 +1456,12 @@ int gemm_actor_entry(XPA_GEMM_ACTOR_PARAMS) {
 }
 
 template <int KIND>
-int gemm_critic_entry(XPA_GEMM_CRITIC_PARAMS) {
+int gemm_critic_entry(XPA_GEMM_CRITIC_PARAMS, unsigned *cmask = nullptr, float *cdv = nullptr) {
     if (batch <= 0 || hidden != kH || act_code < 0 || act_code > 2 || !x || !w_hidden || !b_hidden || !w || !b ||
-        !ret || !dz || !partial_dw || !partial_db_hidden || !partial_db_out || !loss_partials ||
+        !ret || (!dz && !(cmask && cdv)) || !partial_dw || !partial_db_hidden || !partial_db_out || !loss_partials ||
         loss_width < kPartBase || n_rows <= 0 || (!idx && n_rows < batch))
         return (int)hipErrorInvalidValue;
+    if ((cmask || cdv) && (KIND != 7 || (uintptr_t)cmask % 8)) return (int)hipErrorInvalidValue;
     if (((uintptr_t)x | (uintptr_t)w_hidden | (uintptr_t)w) % 16 || ldx < kKin || ldx % 4 || ld_dz < kH)
         return (int)hipErrorInvalidValue;
     HeadArgs a{};
@@ -1428,6 +1469,7 @@ int gemm_critic_entry(XPA_GEMM_CRITIC_PARAMS) {
     a.bias = b; a.slope = slope; a.idx = idx; a.n_rows = n_rows; a.ret = ret; a.vf_coef = vf_coef; a.dz = dz;
     a.p_dw = partial_dw; a.p_dbh = partial_db_hidden; a.p_dbo = partial_db_out; a.p_loss = loss_partials;
     a.loss_width = (int)loss_width;
+    a.cmask = cmask; a.cdv = cdv;
     launch_head<KIND, 2, 0>(a, act_code, (hipStream_t)stream);
     return xpa_launch_status();
 }
@@ -1444,6 +1486,13 @@ XPA_API int xpa_head_gemm_s3p_critic(XPA_GEMM_CRITIC_PARAMS) { return gemm_criti
 // K16Q: K16P's arguments and outputs bit for bit, the waves tiled 32 x 128 (one A fragment split per wave and chunk)
 XPA_API int xpa_head_gemm_s3q_actor(XPA_GEMM_ACTOR_PARAMS) { return gemm_actor_entry<7>(XPA_GEMM_ACTOR_ARGS); }
 XPA_API int xpa_head_gemm_s3q_critic(XPA_GEMM_CRITIC_PARAMS) { return gemm_critic_entry<7>(XPA_GEMM_CRITIC_ARGS); }
+// r05: K16Q critic for the factored critic backward: also writes the hidden activations' sign bits (mask [batch][8]
+// u32, bit c & 31 of word c >> 5 = h[row, c] > 0) and d loss / d v per row (dv [batch]); dz may be null (not stored:
+// K41V / K42S then take the critic's half from mask, dv and the output weights)
+XPA_API int xpa_head_gemm_s3q_critic_mask(XPA_GEMM_CRITIC_PARAMS, unsigned *mask, float *dv) {
+    if (!mask || !dv) return (int)hipErrorInvalidValue;
+    return gemm_critic_entry<7>(XPA_GEMM_CRITIC_ARGS, mask, dv);
+}
 
 // K16W entries: xpa_head_gemm_actor / _critic's arguments and outputs (the same partial-row count, rows the grid does
 // not own written as zeros); act_dim <= 8.

@@ -56,6 +56,7 @@ __device__ __forceinline__ void glds16(const void *g, unsigned lds_wave_base) {
 // loads (K40: no DMAs after the first two chunks; K41: no global loads — stale registers), 4 = one MFMA (hi x hi) per
 // tile and k step instead of the six.  0 in production.
 int g_s3_probe = 0;  // host side: selects the kernel instantiation
+int g_pair_sa = 68;  // K41P: the actor's share of 128 slices (xpa_s3_wgrad_pair_tune)
 
 // the k of element j of lane half h inside a 16-k chunk (quads h and h + 2)
 __device__ __forceinline__ int kmap(int h, int j) { return 4 * h + j + (j >= 4 ? 4 : 0); }
@@ -90,13 +91,55 @@ __global__ __launch_bounds__(256) void split_b_kernel(const float *__restrict__ 
 
 // up to 4 matrices split in one launch (the update's three per step: Wh_pair for dX, Wh_actor^T and Wh_critic^T for
 // K16P): block y = matrix
+// r05 (K42C): rows k >= rs_from[i] of matrix i scaled by rs_a[i] * rs_w[i][k - rs_from[i]] before the split (V =
+// (1 - slope) diag(wc) Wh_c; rs_w null: no scale), and with cs_out the extra block row y = n_mat writes cs_out[j] =
+// cs_slope * sum_c rs_w[c] B_i[rs_from + c][j] (f32 fma chain in c order) for the first scaled matrix i
 struct SplitBatch {
     const float *b[4];
     int64_t k[4], sk[4], sn[4];
     __bf16 *out[4];
+    const float *rs_w[4];
+    float rs_a[4];
+    int64_t rs_from[4];
+    int n;
+    float *cs_out;
+    float cs_slope;
 };
 __global__ __launch_bounds__(256) void split_batch_kernel(SplitBatch sb) {
     const int i = blockIdx.y;
+    if (i == sb.n) {   // cs: block b (< 8) owns columns 32 b .. + 31; 8 row groups of 32 threads, then the groups in order
+        if (blockIdx.x >= 8) return;
+        __shared__ float s_p[8][32];
+        int m = 0;
+        while (m < sb.n && sb.rs_w[m] == nullptr) ++m;
+        const int col = 32 * (int)blockIdx.x + (threadIdx.x & 31), grp = threadIdx.x >> 5;
+        const float *b = sb.b[m] + sb.rs_from[m] * sb.sk[m] + (int64_t)col * sb.sn[m];
+        const float *w = sb.rs_w[m];
+        const int64_t kc = sb.k[m] - sb.rs_from[m], sk = sb.sk[m];
+        const int64_t c0 = grp * kc / 8, c1 = (grp + 1) * kc / 8;
+        float acc = 0.f;
+        int64_t c = c0;
+        for (; c + 16 <= c1; c += 16) {   // 16 loads in flight, fma in row order
+            float v[16], wv[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                v[u] = b[(c + u) * sk];
+                wv[u] = w[c + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) acc = fmaf(wv[u], v[u], acc);
+        }
+        for (; c < c1; ++c) acc = fmaf(w[c], b[c * sk], acc);
+        s_p[grp][threadIdx.x & 31] = acc;
+        __syncthreads();
+        if (grp == 0) {
+            float sum = s_p[0][threadIdx.x];
+#pragma unroll
+            for (int g = 1; g < 8; ++g) sum += s_p[g][threadIdx.x];
+            sb.cs_out[col] = sb.cs_slope * sum;
+        }
+        return;
+    }
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t K = sb.k[i];
     if (t >= (K / kKC) * kN * 2) return;
@@ -105,11 +148,15 @@ __global__ __launch_bounds__(256) void split_batch_kernel(SplitBatch sb) {
     const int h = (int)(t & 1);
     const int n = (int)((t >> 1) % kN);
     const int64_t c = (t >> 1) / kN;
+    const float *rw = sb.rs_w[i];
     bf16x8 ph, pm, pl;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         __bf16 a0, a1, a2;
-        xpa_split3(b[(c * kKC + kmap(h, j)) * sk + (int64_t)n * sn], a0, a1, a2);
+        const int64_t kk = c * kKC + kmap(h, j);
+        float v = b[kk * sk + (int64_t)n * sn];
+        if (rw != nullptr && kk >= sb.rs_from[i]) v *= sb.rs_a[i] * rw[kk - sb.rs_from[i]];
+        xpa_split3(v, a0, a1, a2);
         ph[j] = a0;
         pm[j] = a1;
         pl[j] = a2;
@@ -528,63 +575,14 @@ __device__ __forceinline__ float tb_act_g(float h, float slope) {  // thin.hip a
     return 1.f;
 }
 
-// SIGN (r04, K42S): act' from the sign bits K16R's actor launch wrote (byte col of the row's 32: bit cb = h[row, 32 cb +
-// col] > 0; LeakyReLU / identity only) instead of the 1 KiB h row — the same factor, 64 MiB less read per C2 update.
-template <int ACT, bool SIGN = false, int LA = 0>
-__global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *__restrict__ a, int64_t lda,
-                                                                   const __bf16 *__restrict__ bs, int64_t M,
-                                                                   int nchunks, const float *__restrict__ hmat,
-                                                                   int64_t ldh, const float *__restrict__ x,
-                                                                   int64_t ldx, int din, float slope,
-                                                                   float *__restrict__ p_dw, float *__restrict__ p_db,
-                                                                   const unsigned *__restrict__ hsign = nullptr) {
-    static_assert(!SIGN || ACT != 2, "sign bits carry act' of LeakyReLU / identity only");
-    using G = S3Geom<8>;
-    constexpr int kS = LA == 1 ? 4 : 3;   // ring stages (4 x 40 KiB = the whole 160 KiB with the lookahead)
-    __shared__ __attribute__((aligned(16))) char lds[kS * G::kStage];
-    const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
-    const int t = threadIdx.x, lane = t & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int64_t r0 = (int64_t)blockIdx.x * G::kRows;
-    f32x16 acc[8];
-#pragma unroll
-    for (int cb = 0; cb < 8; ++cb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[cb][r] = 0.f;
-    if constexpr (LA == 2) {
-        pp_loop(base, lds, a, lda, bs, r0, M, nchunks, lane, wave, acc);
-    } else if constexpr (LA == 1) {
-#pragma unroll
-        for (int d = 0; d < 3; ++d)
-            if (d < nchunks) issue<8>(base + d * G::kStage, a, lda, bs, r0, M, d, lane, wave);
-        // chunk 0 landed (chunks 1, 2 may fly), everyone's; then its A fragment split
-        if (nchunks >= 3) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * G::kDma) : "memory");
-        else if (nchunks == 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G::kDma) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        bf16x8 ah, am, al;
-        a_split(lds, lane, wave, ah, am, al);
-#pragma unroll 1
-        for (int ch = 0; ch < nchunks; ++ch) {
-            // chunk ch + 1 landed (ch + 2 may fly), everyone's; the stage chunk ch + 3 refills held chunk ch - 1,
-            // whose B fragments every wave read in iteration ch - 1 (its A in ch - 2)
-            if (ch + 2 < nchunks) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G::kDma) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-            if (ch + 3 < nchunks) issue<8>(base + ((ch + 3) & 3) * G::kStage, a, lda, bs, r0, M, ch + 3, lane, wave);
-            chunk_la(lds + (ch & 3) * G::kStage, lds + ((ch + 1) & 3) * G::kStage, acc, lane, wave, ah, am, al);
-        }
-    } else {
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-        if (d < nchunks) issue<8>(base + d * G::kStage, a, lda, bs, r0, M, d, lane, wave);
-#pragma unroll 1
-    for (int ch = 0; ch < nchunks; ++ch) {
-        if (ch + 1 < nchunks) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G::kDma) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        if (ch + 2 < nchunks) issue<8>(base + ((ch + 2) % 3) * G::kStage, a, lda, bs, r0, M, ch + 2, lane, wave);
-        chunk<8, 0>(lds + (ch % 3) * G::kStage, acc, lane, wave);
-    }
-    }
-    __syncthreads();   // every wave done with the ring: the epilogue reuses its LDS
+// K42's epilogue (after the k loop, every wave done with the ring): dz1 = g * act'(h) in the accumulators, db1 and dW1
+// partials of the block (row block blockIdx.x); lds: the ring's LDS, reused
+template <int ACT, bool SIGN>
+__device__ __forceinline__ void tb_epilogue(f32x16 (&acc)[8], char *lds, int64_t r0, int64_t M, int t, int lane,
+                                            int wave, const float *__restrict__ hmat, int64_t ldh,
+                                            const float *__restrict__ x, int64_t ldx, int din, float slope,
+                                            float *__restrict__ p_dw, float *__restrict__ p_db,
+                                            const unsigned *__restrict__ hsign) {
     // ---- dz1 = g * act'(h) in place (rows past M: 0)
     const int hh = lane >> 5, col = lane & 31;
     const int64_t wrow = r0 + wave * 32;
@@ -668,6 +666,187 @@ __global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *
         for (int w = 1; w < 8; ++w) sum += s_db[w * 256 + t];
         p_db[(int64_t)blockIdx.x * 256 + t] = sum;
     }
+}
+
+// SIGN (r04, K42S): act' from the sign bits K16R's actor launch wrote (byte col of the row's 32: bit cb = h[row, 32 cb +
+// col] > 0; LeakyReLU / identity only) instead of the 1 KiB h row — the same factor, 64 MiB less read per C2 update.
+template <int ACT, bool SIGN = false, int LA = 0>
+__global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *__restrict__ a, int64_t lda,
+                                                                   const __bf16 *__restrict__ bs, int64_t M,
+                                                                   int nchunks, const float *__restrict__ hmat,
+                                                                   int64_t ldh, const float *__restrict__ x,
+                                                                   int64_t ldx, int din, float slope,
+                                                                   float *__restrict__ p_dw, float *__restrict__ p_db,
+                                                                   const unsigned *__restrict__ hsign = nullptr) {
+    static_assert(!SIGN || ACT != 2, "sign bits carry act' of LeakyReLU / identity only");
+    using G = S3Geom<8>;
+    constexpr int kS = LA == 1 ? 4 : 3;   // ring stages (4 x 40 KiB = the whole 160 KiB with the lookahead)
+    __shared__ __attribute__((aligned(16))) char lds[kS * G::kStage];
+    const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int64_t r0 = (int64_t)blockIdx.x * G::kRows;
+    f32x16 acc[8];
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[cb][r] = 0.f;
+    if constexpr (LA == 2) {
+        pp_loop(base, lds, a, lda, bs, r0, M, nchunks, lane, wave, acc);
+    } else if constexpr (LA == 1) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+            if (d < nchunks) issue<8>(base + d * G::kStage, a, lda, bs, r0, M, d, lane, wave);
+        // chunk 0 landed (chunks 1, 2 may fly), everyone's; then its A fragment split
+        if (nchunks >= 3) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * G::kDma) : "memory");
+        else if (nchunks == 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G::kDma) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        bf16x8 ah, am, al;
+        a_split(lds, lane, wave, ah, am, al);
+#pragma unroll 1
+        for (int ch = 0; ch < nchunks; ++ch) {
+            // chunk ch + 1 landed (ch + 2 may fly), everyone's; the stage chunk ch + 3 refills held chunk ch - 1,
+            // whose B fragments every wave read in iteration ch - 1 (its A in ch - 2)
+            if (ch + 2 < nchunks) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G::kDma) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            if (ch + 3 < nchunks) issue<8>(base + ((ch + 3) & 3) * G::kStage, a, lda, bs, r0, M, ch + 3, lane, wave);
+            chunk_la(lds + (ch & 3) * G::kStage, lds + ((ch + 1) & 3) * G::kStage, acc, lane, wave, ah, am, al);
+        }
+    } else {
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+        if (d < nchunks) issue<8>(base + d * G::kStage, a, lda, bs, r0, M, d, lane, wave);
+#pragma unroll 1
+    for (int ch = 0; ch < nchunks; ++ch) {
+        if (ch + 1 < nchunks) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G::kDma) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (ch + 2 < nchunks) issue<8>(base + ((ch + 2) % 3) * G::kStage, a, lda, bs, r0, M, ch + 2, lane, wave);
+        chunk<8, 0>(lds + (ch % 3) * G::kStage, acc, lane, wave);
+    }
+    }
+    __syncthreads();   // every wave done with the ring: the epilogue reuses its LDS
+    tb_epilogue<ACT, SIGN>(acc, lds, r0, M, t, lane, wave, hmat, ldh, x, ldx, din, slope, p_dw, p_db, hsign);
+}
+
+// ---- K42C (r05): K42S with the critic's half of dX factored -------------------------------------------------------
+// The paired dX GEMM g = dz_pair . Wh_pair splits into the actor's half (dz_a . Wh_a: dz_a an f32 operand, six products)
+// and the critic's: with the critic's hidden activation LeakyReLU (act' = slope + (1 - slope) m, m = [h_c > 0]) and its
+// one output unit, dz_c[r, c] = dv[r] wc[c] act'(h_c[r, c]), so
+//     (dz_c . Wh_c)[r, j] = dv[r] (sum_c m[r, c] V[c, j] + cs[j]),  V = (1 - slope) diag(wc) Wh_c,  cs = slope wc . Wh_c
+// where m is exact in bf16 (0 / 1): the masked product takes THREE bf16 products (m V_lo, m V_mid, m V_hi; every one
+// exact in f32, f32 accumulation), not six, and dz_c is never stored or read (the critic head writes the 32 B of
+// sign bits and dv per row instead: xpa_head_gemm_s3q_critic_mask).  The k loop runs the critic's chunks first (split
+// buffer chunks nca .. nca + ncc - 1: V's planes; A = the row's mask bits from LDS, no A DMA), scales the accumulators
+// by dv[row] after adding cs, then the actor's chunks exactly as K42S (A = dz_a rows by LDS-DMA + the split).  The
+// epilogue (the trunk layer's backward) is K42S's.
+constexpr int kCMaskStride = 9;   // words per row of the LDS mask image (8 + 1: the 32 rows of a read hit 32 banks)
+template <int ACT>
+__global__ __launch_bounds__(512, 1) void s3_trunk_bwd_crit_kernel(
+    const float *__restrict__ a, int64_t lda, const __bf16 *__restrict__ bs, int64_t M, int nca, int ncc,
+    const unsigned *__restrict__ cmask, const float *__restrict__ cdv, const float *__restrict__ ccs,
+    const float *__restrict__ x, int64_t ldx, int din, float slope, float *__restrict__ p_dw, float *__restrict__ p_db,
+    const unsigned *__restrict__ hsign) {
+    using G = S3Geom<8>;
+    constexpr int kRing = 3 * G::kStage;
+    constexpr int kMaskOff = kRing, kDvOff = kMaskOff + 256 * kCMaskStride * 4, kCsOff = kDvOff + 256 * 4;
+    __shared__ __attribute__((aligned(16))) char lds[kCsOff + 256 * 4];
+    const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int64_t r0 = (int64_t)blockIdx.x * G::kRows;
+    unsigned *s_mask = reinterpret_cast<unsigned *>(lds + kMaskOff);
+    float *s_dv = reinterpret_cast<float *>(lds + kDvOff);
+    float *s_cs = reinterpret_cast<float *>(lds + kCsOff);
+    {   // the block's 256 mask rows (one uint4 per thread), dv rows and cs (rows past M: zeros)
+        const int rr = t >> 1, q = t & 1;
+        const int64_t row = r0 + rr;
+        uint4 w = make_uint4(0u, 0u, 0u, 0u);
+        if (row < M) w = *reinterpret_cast<const uint4 *>(cmask + row * 8 + 4 * q);
+        unsigned *d = s_mask + rr * kCMaskStride + 4 * q;
+        d[0] = w.x; d[1] = w.y; d[2] = w.z; d[3] = w.w;
+        if (t < 256) {
+            s_dv[t] = r0 + t < M ? cdv[r0 + t] : 0.f;
+            s_cs[t] = ccs[t];
+        }
+    }
+    __syncthreads();
+    f32x16 acc[8];
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[cb][r] = 0.f;
+    const int N = nca + ncc;
+    // processing index i -> split chunk: the critic's first
+    auto chunk_of = [&](int i) { return i < ncc ? nca + i : i - ncc; };
+    auto issue_i = [&](int i) {
+        const unsigned st = base + (i % 3) * G::kStage;
+        const int c = chunk_of(i);
+        const int rr = lane >> 2, p = lane & 3;
+        if (i >= ncc) {   // actor chunk: A rows by DMA (K40's swizzled image)
+            const int q = p ^ ((rr >> 2) & 3);
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                int64_t row = r0 + wave * 32 + k * 16 + rr;
+                row = row < M ? row : M - 1;
+                glds16(a + row * lda + c * kKC + 4 * q, st + (unsigned)((wave * 32 + k * 16) * kKC * 4));
+            }
+        }
+        const char *bsrc = reinterpret_cast<const char *>(bs) + (int64_t)c * kBImg;
+#pragma unroll
+        for (int j = 0; j < G::kPer; ++j) {
+            const int piece = wave * G::kPer + j;
+            glds16(bsrc + piece * 1024 + lane * 16, st + (unsigned)(G::kAImg + piece * 1024));
+        }
+    };
+    // wait for every wave's DMAs of processing index i (i + 1's may still fly), then the barrier
+    auto wait_i = [&](int i) {
+        if (i + 1 >= N) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        else if (i + 1 >= ncc) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G::kDma) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G::kPer) : "memory");
+    };
+    issue_i(0);
+    if (N > 1) issue_i(1);
+    const int hh = lane >> 5, i32 = lane & 31;
+    const unsigned *mrow = s_mask + (wave * 32 + i32) * kCMaskStride;
+#pragma unroll 1
+    for (int i = 0; i < ncc; ++i) {
+        wait_i(i);
+        if (i + 2 < N) issue_i(i + 2);
+        // A = the 8 mask bits of the lane's row at k = 16 i + kmap(hh, j) (the split's k order), as bf16 0 / 1
+        const unsigned wbits = mrow[i >> 1] >> (16 * (i & 1) + 4 * hh);
+        unsigned pk[4];
+#pragma unroll
+        for (int pj = 0; pj < 4; ++pj) {
+            const int j0 = 2 * pj, j1 = 2 * pj + 1;
+            const int b0 = j0 < 4 ? j0 : j0 + 4, b1 = j1 < 4 ? j1 : j1 + 4;
+            pk[pj] = (((wbits >> b0) & 1u) * 0x3F80u) | ((((wbits >> b1) & 1u) * 0x3F80u) << 16);
+        }
+        const bf16x8 am = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+        const bf16x8 *bimg = reinterpret_cast<const bf16x8 *>(lds + (i % 3) * G::kStage + G::kAImg) + lane;
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb) {
+            acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bimg[(16 + cb) * 64], acc[cb], 0, 0, 0);
+            acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bimg[(8 + cb) * 64], acc[cb], 0, 0, 0);
+            acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bimg[cb * 64], acc[cb], 0, 0, 0);
+        }
+    }
+    {   // acc = dv[row] (acc + cs[col]): the critic's half of g
+        const int col = lane & 31;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float dvr = s_dv[wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh];
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb) acc[cb][r] = dvr * (acc[cb][r] + s_cs[cb * 32 + col]);
+        }
+    }
+#pragma unroll 1
+    for (int i = ncc; i < N; ++i) {
+        wait_i(i);
+        if (i + 2 < N) issue_i(i + 2);
+        chunk<8, 0>(lds + (i % 3) * G::kStage, acc, lane, wave);
+    }
+    __syncthreads();   // every wave done with the ring: the epilogue reuses its LDS
+    tb_epilogue<ACT, true>(acc, lds, r0, M, t, lane, wave, nullptr, 0, x, ldx, din, slope, p_dw, p_db, hsign);
 }
 
 // ---- K41: weight gradients dW = A^T B over the batch (K = rows), split-K -----------------------------------
@@ -1237,6 +1416,196 @@ __global__ __launch_bounds__(512, 1) void s3_wgrad_pp_kernel(const float *__rest
         }
 }
 
+// ---- K41P (r05): the paired hidden layer's weight gradient with the critic's half factored --------------------------
+// dW_pair = dz_pair^T h splits into the actor's [256, 256] (dz_a^T h, K41V's six-product split, interleaved schedule) and
+// the critic's: with dz_c[r, c] = dv[r] wc[c] (slope + (1 - slope) m[r, c]) (the critic head's one output unit,
+// LeakyReLU hidden layer, m = [h_c > 0] from its sign bits),
+//     dW_c[c, j] = wc[c] ((1 - slope) sum_r m[r, c] Y[r, j] + slope sum_r Y[r, j]),  Y = dv (.) h   (one f32 rounding)
+// where m^T Y takes THREE bf16 products (m exact in bf16: m Y_lo, m Y_mid, m Y_hi) instead of six and dz_c is never
+// read.  One launch: blocks [0, 2 sa) are the actor's (2 column tiles of 128 x sa slices), blocks [2 sa, 2 sa + 2 sc)
+// the critic's (sc slices, ~2x the rows per slice: the same MFMA work per block); each critic block also forms its
+// slice's column sums of Y (per-thread float4 over its staged rows, then the 8 waves in order) and writes its partial
+// already as wc[c] ((1 - slope) P + slope colsum), so the caller's fixed-order slice sum gives dW_c.
+struct CUnits {   // the critic's staging units: A = 4 mask bits per unit, B = Y rows (h float4 times dv of the row)
+    unsigned abits[2];
+    float4 b[4];
+    float bdv[4];
+    unsigned ok;
+};
+
+__device__ __forceinline__ void c_load(CUnits &u, const unsigned *__restrict__ cmask, const float *__restrict__ cdv,
+                                       int mt, const float *__restrict__ B, int64_t ldb, int64_t k0, int64_t kend,
+                                       int t) {
+    unsigned ok = 0u;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int idx = t + 512 * j, k = idx >> 5, cq = idx & 31;
+        const int64_t r = k0 + k;
+        const int c = mt * kWgM + 4 * cq;
+        u.abits[j] = cmask[min(r, kend - 1) * 8 + (c >> 5)] >> (c & 31);
+        ok |= (r < kend ? 1u : 0u) << j;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int idx = t + 512 * j, k = idx >> 6, nq = idx & 63;
+        const int64_t r = k0 + k;
+        const int64_t rc = min(r, kend - 1);
+        u.b[j] = *reinterpret_cast<const float4 *>(B + rc * ldb + 4 * nq);
+        u.bdv[j] = cdv[rc];
+        ok |= (r < kend ? 1u : 0u) << (2 + j);
+    }
+    u.ok = ok;
+}
+
+// unit `unit` of the critic's staging into stage nx (A: the hi plane only — m is 0 / 1 — B: the three planes of Y);
+// ysum accumulates the thread's Y columns 4 (t & 63) .. + 3 over its rows
+__device__ __forceinline__ void c_put_unit(char *nx, const CUnits &u, int t, int unit, float4 &ysum) {
+    const bool keep = (u.ok >> unit) & 1u;
+    if (unit < 2) {
+        const int idx = t + 512 * unit, k = idx >> 5, cq = idx & 31;
+        const unsigned bits = keep ? u.abits[unit] : 0u;
+        const unsigned lo = ((bits & 1u) * 0x3F80u) | (((bits >> 1) & 1u) * 0x3F800000u);
+        const unsigned hi = (((bits >> 2) & 1u) * 0x3F80u) | (((bits >> 3) & 1u) * 0x3F800000u);
+        *reinterpret_cast<uint2 *>(nx + v_off(k, 4 * cq)) = make_uint2(lo, hi);
+    } else {
+        const int j = unit - 2, idx = t + 512 * j, k = idx >> 6, n = 4 * (idx & 63);
+        const float d = u.bdv[j];
+        float4 y = make_float4(d * u.b[j].x, d * u.b[j].y, d * u.b[j].z, d * u.b[j].w);
+        y = v_zero_if(y, keep);
+        ysum.x += y.x;
+        ysum.y += y.y;
+        ysum.z += y.z;
+        ysum.w += y.w;
+        v_put(nx + 3 * kVPlane, 2 * kVPlane, (n >> 7) * kVPlane + v_off(k, n & 127), y);
+    }
+}
+
+// K41V's interleaved chunk for the critic: 8 segments of (3 MFMAs of one accumulator: m Y_lo, m Y_mid, m Y_hi) + one
+// staging unit of the next stage; the second k step's fragments read in segment 1, the loads of the chunk after next
+// in segment 6
+__device__ __forceinline__ void c_chunk_il(const char *st, char *nx, CUnits &u, f32x16 (&acc)[2][2], int lane, int wm,
+                                           int wn, int t, const unsigned *__restrict__ cmask,
+                                           const float *__restrict__ cdv, int mt, const float *__restrict__ B,
+                                           int64_t ldb, int64_t k_next, int64_t kend, float4 &ysum) {
+    bf16x8 ah[2][2], am[2][2], al[2][2], bh[2][2], bm[2][2], bl[2][2];
+    v_frags(st, 0, lane, wm, wn, ah[0], am[0], al[0], bh[0], bm[0], bl[0]);
+#pragma unroll
+    for (int seg = 0; seg < 8; ++seg) {
+        const int s = seg >> 2, i = (seg >> 1) & 1, j = seg & 1;
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s][i], bl[s][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s][i], bm[s][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s][i], bh[s][j], acc[i][j], 0, 0, 0);
+        if (seg < 6) c_put_unit(nx, u, t, seg, ysum);
+        if (seg == 1) v_frags(st, 1, lane, wm, wn, ah[1], am[1], al[1], bh[1], bm[1], bl[1]);
+        if (seg == 6) c_load(u, cmask, cdv, mt, B, ldb, k_next, kend, t);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+__global__ __launch_bounds__(512, 1) void s3_wgrad_pair_kernel(const float *__restrict__ A, int64_t lda,
+                                                               const float *__restrict__ B, int64_t ldb, int64_t rows,
+                                                               int sa, int64_t per_a, int sc, int64_t per_c,
+                                                               const unsigned *__restrict__ cmask,
+                                                               const float *__restrict__ cdv,
+                                                               const float *__restrict__ cwc, float cslope,
+                                                               float *__restrict__ out_a, float *__restrict__ out_c) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * kVStage];
+    const int nblk = 2 * (sa + sc);
+    int L = blockIdx.x;
+    if (nblk % 8 == 0) L = (blockIdx.x & 7) * (nblk >> 3) + (blockIdx.x >> 3);   // a slice's 2 tiles on one XCD
+    const bool crit = L >= 2 * sa;
+    const int Lr = crit ? L - 2 * sa : L;
+    const int slice = Lr >> 1, mt = Lr & 1;
+    const int64_t per = crit ? per_c : per_a;
+    const int t = threadIdx.x, lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wm = wave & 1, wn = wave >> 1;
+    const int64_t k0 = (int64_t)slice * per;
+    const int64_t kend = min(rows, k0 + per);
+    const int nch = kend > k0 ? (int)((kend - k0 + kWgKC - 1) / kWgKC) : 0;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    float4 ysum = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (!crit) {   // K41V (interleaved schedule) on the actor's columns
+        const float *Am = A + (int64_t)mt * kWgM;
+        VUnits u;
+        if (nch > 0) {
+            v_load(u, Am, lda, B, ldb, k0, kend, t);
+            v_store(lds, u, t);
+            if (nch > 1) v_load(u, Am, lda, B, ldb, k0 + kWgKC, kend, t);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+#pragma unroll 1
+        for (int c = 0; c < nch; ++c) {
+            v_chunk_il(lds + (c & 1) * kVStage, lds + ((c + 1) & 1) * kVStage, u, acc, lane, wm, wn, t, Am, lda, B, ldb,
+                       k0 + (int64_t)(c + 2) * kWgKC, kend);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+    } else {
+        CUnits u;
+        if (nch > 0) {
+            c_load(u, cmask, cdv, mt, B, ldb, k0, kend, t);
+#pragma unroll
+            for (int unit = 0; unit < 6; ++unit) c_put_unit(lds, u, t, unit, ysum);
+            if (nch > 1) c_load(u, cmask, cdv, mt, B, ldb, k0 + kWgKC, kend, t);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+#pragma unroll 1
+        for (int c = 0; c < nch; ++c) {
+            // past the last chunk the staging rewrites the idle stage from rows >= kend: zeros (ok bits), so the
+            // column sums are unaffected
+            c_chunk_il(lds + (c & 1) * kVStage, lds + ((c + 1) & 1) * kVStage, u, acc, lane, wm, wn, t, cmask, cdv, mt,
+                       B, ldb, k0 + (int64_t)(c + 2) * kWgKC, kend, ysum);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+    }
+    const int h = lane >> 5, col = lane & 31;
+    if (!crit) {
+        float *o = out_a + ((int64_t)slice * 256 + (int64_t)mt * kWgM) * kN;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = 64 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) o[(int64_t)row * kN + 64 * wn + 32 * j + col] = acc[i][j][r];
+            }
+        return;
+    }
+    // the slice's column sums of Y: thread t holds columns 4 (t & 63) .. + 3 over the rows of its units; the 8 threads
+    // of a column quad (t >> 6 = 0 .. 7) added in order
+    float *s_ys = reinterpret_cast<float *>(lds);   // [8][256], the ring is free (every wave passed the last barrier)
+    *reinterpret_cast<float4 *>(s_ys + (t >> 6) * 256 + 4 * (t & 63)) = ysum;
+    __syncthreads();
+    float *s_cs = s_ys + 8 * 256;   // [256]
+    if (t < 256) {
+        float sum = s_ys[t];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) sum += s_ys[w * 256 + t];
+        s_cs[t] = sum;
+    }
+    __syncthreads();
+    float *o = out_c + ((int64_t)slice * 256 + (int64_t)mt * kWgM) * kN;
+    const float a1 = 1.0f - cslope;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = 64 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const float w = cwc[mt * kWgM + row];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int n = 64 * wn + 32 * j + col;
+                o[(int64_t)row * kN + n] = w * (a1 * acc[i][j][r] + cslope * s_cs[n]);
+            }
+        }
+}
+
 }  // namespace
 
 // the split-K slice count of xpa_s3_wgrad for this shape (the caller's workspace: slices x m x 256 floats)
@@ -1282,6 +1651,48 @@ XPA_API int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ld
     return xpa_launch_status();
 }
 
+// K41P (r05): slice counts of xpa_s3_wgrad_pair for `rows` (sa actor, sc critic slices; their rows per slice in
+// per_a / per_c, multiples of 32): 2 (sa + sc) <= 256 blocks with ~2x the critic's rows per slice (3 products vs 6)
+XPA_API int xpa_s3_wgrad_pair_slices(int64_t rows, int64_t *sa, int64_t *sc, int64_t *per_a, int64_t *per_c) {
+    if (rows <= 0 || !sa || !sc || !per_a || !per_c) return (int)hipErrorInvalidValue;
+    auto fit = [&](int64_t want, int64_t *s, int64_t *per) {
+        int64_t n = want < 1 ? 1 : want;
+        while (n > 1 && rows / n < 4 * kWgKC) n >>= 1;
+        int64_t p = (rows + n - 1) / n;
+        p = (p + kWgKC - 1) / kWgKC * kWgKC;
+        *per = p;
+        *s = (rows + p - 1) / p;
+    };
+    fit(g_pair_sa, sa, per_a);
+    fit(128 - g_pair_sa, sc, per_c);
+    return 0;
+}
+
+// the actor's share of K41P's 128 slice pairs (tuning: a critic chunk stages as many units as an actor chunk but runs
+// half the MFMAs, so the balance sits between the MFMA ratio 85 / 43 and equal rows)
+XPA_API int xpa_s3_wgrad_pair_tune(int sa_target) {
+    if (sa_target < 8 || sa_target > 120) return (int)hipErrorInvalidValue;
+    g_pair_sa = sa_target;
+    return 0;
+}
+
+// dz_a [rows, 256] (row stride lda, the actor's half), h [rows, 256] (ldb), crit_mask [rows, 8] + crit_dv [rows]
+// (xpa_head_gemm_s3q_critic_mask), crit_wc [256] (the critic's output weights), crit_slope (its hidden activation's):
+// out_a [sa, 256, 256] (slices of dz_a^T h), out_c [sc, 256, 256] (slices of dW_c, wc and the slope term applied)
+XPA_API int xpa_s3_wgrad_pair(const float *dz_a, int64_t lda, const float *h, int64_t ldb, int64_t rows,
+                              const unsigned *crit_mask, const float *crit_dv, const float *crit_wc, float crit_slope,
+                              int64_t sa, int64_t per_a, int64_t sc, int64_t per_c, float *out_a, float *out_c,
+                              xpa_stream_t stream) {
+    if (!dz_a || !h || !crit_mask || !crit_dv || !crit_wc || !out_a || !out_c || rows <= 0 || lda < 256 || ldb < 256 ||
+        (lda & 3) || (ldb & 3) || ((reinterpret_cast<uintptr_t>(dz_a) | reinterpret_cast<uintptr_t>(h)) & 15) ||
+        sa < 1 || sc < 1 || per_a % kWgKC || per_c % kWgKC || sa * per_a < rows || sc * per_c < rows ||
+        2 * (sa + sc) > 4096)
+        return (int)hipErrorInvalidValue;
+    s3_wgrad_pair_kernel<<<dim3((unsigned)(2 * (sa + sc))), dim3(512), 0, stream>>>(
+        dz_a, lda, h, ldb, rows, (int)sa, per_a, (int)sc, per_c, crit_mask, crit_dv, crit_wc, crit_slope, out_a, out_c);
+    return xpa_launch_status();
+}
+
 XPA_API int xpa_s3_probe(int mask) {
     g_s3_probe = mask;
     return 0;
@@ -1291,11 +1702,36 @@ XPA_API int64_t xpa_s3_split_bytes(int64_t k, int64_t n) {
     return k * n * 3 * 2;
 }
 
+XPA_API int xpa_s3_split_batch_scaled(int n_mat, const float *const *b, const int64_t *k, const int64_t *sk,
+                                      const int64_t *sn, void *const *out, const float *const *rs_w, const float *rs_a,
+                                      const int64_t *rs_from, float *cs_out, float cs_slope, xpa_stream_t stream);
 // n_mat <= 4 matrices B_i [k_i, 256] (element (r, c) at b_i[r sk_i + c sn_i]) split into out_i in one launch
 XPA_API int xpa_s3_split_batch(int n_mat, const float *const *b, const int64_t *k, const int64_t *sk, const int64_t *sn,
                                void *const *out, xpa_stream_t stream) {
+    return xpa_s3_split_batch_scaled(n_mat, b, k, sk, sn, out, nullptr, nullptr, nullptr, nullptr, 0.f, stream);
+}
+
+// xpa_s3_split_batch with per-matrix row scales (rs_w[i] nullable: rows k >= rs_from[i] times rs_a[i] * rs_w[i][k -
+// rs_from[i]]) and, with cs_out, cs_out[j] = cs_slope * sum_c rs_w[c] B[rs_from + c][j] of the first scaled matrix
+XPA_API int xpa_s3_split_batch_scaled(int n_mat, const float *const *b, const int64_t *k, const int64_t *sk,
+                                      const int64_t *sn, void *const *out, const float *const *rs_w, const float *rs_a,
+                                      const int64_t *rs_from, float *cs_out, float cs_slope, xpa_stream_t stream) {
     if (n_mat < 1 || n_mat > 4 || !b || !k || !sk || !sn || !out) return (int)hipErrorInvalidValue;
     SplitBatch sb{};
+    sb.n = n_mat;
+    sb.cs_out = cs_out;
+    sb.cs_slope = cs_slope;
+    bool any_rs = false;
+    for (int i = 0; i < n_mat; ++i) {
+        sb.rs_w[i] = rs_w ? rs_w[i] : nullptr;
+        sb.rs_a[i] = rs_w && rs_w[i] ? rs_a[i] : 1.f;
+        sb.rs_from[i] = rs_w && rs_w[i] ? rs_from[i] : 0;
+        if (sb.rs_w[i]) {
+            if (sb.rs_from[i] < 0 || sb.rs_from[i] >= k[i]) return (int)hipErrorInvalidValue;
+            any_rs = true;
+        }
+    }
+    if (cs_out && !any_rs) return (int)hipErrorInvalidValue;
     int64_t kmax = 0;
     for (int i = 0; i < n_mat; ++i) {
         if (!b[i] || !out[i] || k[i] <= 0 || k[i] % kKC) return (int)hipErrorInvalidValue;
@@ -1307,7 +1743,9 @@ XPA_API int xpa_s3_split_batch(int n_mat, const float *const *b, const int64_t *
         kmax = k[i] > kmax ? k[i] : kmax;
     }
     const int64_t total = (kmax / kKC) * kN * 2;
-    split_batch_kernel<<<dim3((unsigned)((total + 255) / 256), (unsigned)n_mat), dim3(256), 0, stream>>>(sb);
+    int64_t gx = (total + 255) / 256;
+    if (cs_out && gx < 8) gx = 8;   // the cs row uses 8 blocks
+    split_batch_kernel<<<dim3((unsigned)gx, (unsigned)(n_mat + (cs_out ? 1 : 0))), dim3(256), 0, stream>>>(sb);
     return xpa_launch_status();
 }
 
@@ -1382,6 +1820,34 @@ XPA_API int xpa_s3_gemm_trunk_bwd_sign(const float *dz, int64_t ldz, const void 
     else
         s3_gemm_trunk_bwd_kernel<1, true><<<grid, block, 0, stream>>>(dz, ldz, bs, rows, nch, nullptr, 0, x, ldx,
                                                                        (int)d_in, slope, partial_dw, partial_db, h_sign);
+    return xpa_launch_status();
+}
+
+// K42C (r05): xpa_s3_gemm_trunk_bwd_sign with the critic's half of the paired dX factored (see s3_trunk_bwd_crit_kernel):
+// dz_a [rows, k_a] (row stride ldz; the actor's half only), b_split = the split of [Wh_a; V] (k_a + k_c rows, V =
+// (1 - slope_c) diag(wc) Wh_c: xpa_s3_split_batch with a row scale), crit_mask [rows, 8] u32 + crit_dv [rows] from
+// xpa_head_gemm_s3q_critic_mask, crit_cs [256] = slope_c wc . Wh_c.  act 0 / 1 (the trunk layer's, from h_sign).
+XPA_API int xpa_s3_gemm_trunk_bwd_crit(const float *dz_a, int64_t ldz, const void *b_split, int64_t k_a, int64_t k_c,
+                                       const unsigned *crit_mask, const float *crit_dv, const float *crit_cs,
+                                       const unsigned *h_sign, const float *x, int64_t ldx, int64_t rows, int64_t d_in,
+                                       int act, float slope, float *partial_dw, float *partial_db, xpa_stream_t stream) {
+    if (!dz_a || !b_split || !crit_mask || !crit_dv || !crit_cs || !h_sign || !x || !partial_dw || !partial_db ||
+        rows <= 0 || k_a <= 0 || k_c <= 0 || k_a % kKC != 0 || k_c % kKC != 0 || k_c > 256 || ldz < k_a || (ldz & 3) ||
+        (reinterpret_cast<uintptr_t>(dz_a) & 15) || (reinterpret_cast<uintptr_t>(h_sign) & 15) ||
+        (reinterpret_cast<uintptr_t>(crit_mask) & 15) || d_in < 1 || d_in > 32 || ldx < d_in || act < 0 || act > 1 ||
+        (k_a + k_c) / kKC > (1 << 20))
+        return (int)hipErrorInvalidValue;
+    const dim3 grid((unsigned)xpa_s3_gemm_trunk_bwd_num_partials(rows)), block(512);
+    const __bf16 *bs = static_cast<const __bf16 *>(b_split);
+    const int nca = (int)(k_a / kKC), ncc = (int)(k_c / kKC);
+    if (act == 0)
+        s3_trunk_bwd_crit_kernel<0><<<grid, block, 0, stream>>>(dz_a, ldz, bs, rows, nca, ncc, crit_mask, crit_dv,
+                                                                 crit_cs, x, ldx, (int)d_in, slope, partial_dw,
+                                                                 partial_db, h_sign);
+    else
+        s3_trunk_bwd_crit_kernel<1><<<grid, block, 0, stream>>>(dz_a, ldz, bs, rows, nca, ncc, crit_mask, crit_dv,
+                                                                 crit_cs, x, ldx, (int)d_in, slope, partial_dw,
+                                                                 partial_db, h_sign);
     return xpa_launch_status();
 }
 

@@ -374,10 +374,17 @@ class FusedActorCritic:
             if (ops.S3_GEMMS and ops.S3_HEADS in ("s3p", "s3q") and not ops.K16W_ENABLED
                     and (trunk is None or self._s3r_on())):
                 splits += [(lin_ah.weight.t(), "s3p_a"), (lin_ch.weight.t(), "s3p_c")]
+        crit = (self._crit_plan(x, rep_outs, c_code, B, s.device)
+                if paired and z_a is None and trunk is None and wh_split is None and splits else None)
+        scales = cs = None
         if paired and len(self.rep) > 0 and self._dx_split_ok(self.pair[0]):
             splits.append((self.pair[0], "dx"))
+            if crit is not None:   # K42C: the critic's rows of the dX split scaled by (1 - slope) wc, + cs
+                H = ops.HEAD_HIDDEN
+                scales = [None] * (len(splits) - 1) + [(lin_co.weight.view(-1), 1.0 - float(c_slope), H)]
+                cs = (crit[2], float(c_slope))
         if splits:
-            bufs = self._split_many(splits)
+            bufs = self._split_many(splits, scales, cs)
             if splits[0][1] == "s3p_a":
                 wh_split = (bufs[0], bufs[1])
         grads = {"w_actor": lin_ao.weight.grad, "b_actor": lin_ao.bias.grad, "bh_actor": lin_ah.bias.grad,
@@ -394,8 +401,18 @@ class FusedActorCritic:
                                               colsum_queue=self._cq, gemm=gemm, sq_logstd=self._sq.data_ptr(),
                                               wh_split=wh_split,
                                               defer_loss=True,
-                                              trunk=trunk)
+                                              trunk=trunk,
+                                              crit_mask=crit[:2] if crit is not None else None)
         have_rep = len(self.rep) > 0
+        if paired and crit is not None:   # r05: K41P + K42C, the critic's half factored (dz_critic never written)
+            q = self._cq_early if self.early_grad_sync is not None else self._cq
+            self._weight_grad_pair(s, crit, lin_co, c_slope, q)
+            if self.early_grad_sync is not None:
+                self._cq_early.flush(s.device)
+                self.early_grad_sync(self.pair[2])
+            assert self._trunk_bwd_fused(self._hws.dz_actor, x, rep_outs, crit=crit)
+            self._flush_with_norm(s.device)
+            return scalars
         if paired:   # dW of both hidden layers and dX (K = 512, no accumulate pass) as single GEMMs
             dz = self._hws.dz_pair
             if self.early_grad_sync is not None:
@@ -468,11 +485,58 @@ class FusedActorCritic:
             self._partials[key] = buf
         return buf
 
-    def _split_many(self, items):
-        """The bf16 planes of every (matrix [k, 256], name) in one launch, into buffers kept per name."""
-        bufs = [self._split_buf(b.shape[0], name, b.device) for b, name in items]
-        ops.s3_split_batch([(b, o) for (b, _), o in zip(items, bufs)])
+    def _split_many(self, items, scales=None, cs=None):
+        """The bf16 planes of every (matrix [k, 256], name) in one launch, into buffers kept per name (scales / cs:
+        ops.s3_split_batch's, for K42C)."""
+        bufs = [self._split_buf(b.shape[0], name + ("_crit" if scales and sc else ""), b.device)
+                for (b, name), sc in zip(items, scales or [None] * len(items))]
+        ops.s3_split_batch([(b, o) for (b, _), o in zip(items, bufs)], scales, cs)
         return bufs
+
+    # r05: the critic's half of the paired hidden layer's dX and dW factored (K42C / K41P: masked GEMMs on exact 0 / 1
+    # operands, three split products instead of six; dz_critic never stored) where it applies: the K16Q heads, a
+    # LeakyReLU / ReLU critic hidden layer and K42S's trunk backward
+    CRIT_FACTORED = True
+
+    def _crit_plan(self, x, rep_outs, c_code, B, device):
+        """(mask int32 [B, 8], dv [B], cs [256]) buffers when the factored critic backward applies, else None."""
+        if not (self.CRIT_FACTORED and ops.S3_GEMMS and ops.S3_HEADS == "s3q" and not ops.K16W_ENABLED and c_code == 1
+                and self.critic[-1][0].out_features == 1 and self.pair is not None and len(self.rep) == 1):
+            return None
+        lin, code, _ = self.rep[0]
+        if not (self.FUSE_TRUNK_BWD and self._dx_split_ok(self.pair[0]) and self.thin0 and code in (0, 1)
+                and isinstance(x, Rows) and getattr(x, "hsign", None) is not None and lin.in_features <= 32):
+            return None
+        xr = x.gathered
+        h = rep_outs[0] if rep_outs else None
+        if not (isinstance(xr, torch.Tensor) and xr.dim() == 2 and xr.stride(1) == 1 and isinstance(h, torch.Tensor)
+                and h.shape[1] == 256 and _vec4_rows(h)):
+            return None
+        if self._hws is None or not _vec4_rows(self._hws.dz_actor):
+            return None
+        key = ("crit", B)
+        bufs = self._partials.get(key)
+        if bufs is None:   # graph-capture safe: allocated on first (eager) use
+            bufs = (torch.empty((B, 8), dtype=torch.int32, device=device), torch.empty((B,), dtype=torch.float32,
+                                                                                       device=device),
+                    torch.empty((256,), dtype=torch.float32, device=device))
+            self._partials[key] = bufs
+        return bufs
+
+    def _weight_grad_pair(self, s, crit, lin_co, c_slope, queue):
+        """K41P: the paired hidden layer's dW slices (actor: dz_a^T h; critic: factored), two finalize segments."""
+        B = s.shape[0]
+        sa, per_a, sc, per_c = ops.s3_wgrad_pair_slices(B)
+        key = ("wgrad_pair", sa, sc)
+        ws = self._partials.get(key)
+        if ws is None:
+            ws = (torch.empty((sa, 256, 256), dtype=torch.float32, device=s.device),
+                  torch.empty((sc, 256, 256), dtype=torch.float32, device=s.device))
+            self._partials[key] = ws
+        ops.s3_wgrad_pair(self._hws.dz_actor, s, crit[0], crit[1], lin_co.weight.view(-1), c_slope, ws[0], ws[1])
+        g = self.pair[2]
+        queue.add(ws[0].view(sa, -1), g[:256].reshape(-1))
+        queue.add(ws[1].view(sc, -1), g[256:].reshape(-1))
 
     FUSE_TRUNK_BWD = True   # K42 where it applies (ops.S3_GEMMS, one thin representation layer)
     # K16R where it applies (the split heads, one thin representation layer with the heads' activation): h formed
@@ -499,7 +563,7 @@ class FusedActorCritic:
             self._partials[key] = sign
         return sign
 
-    def _trunk_bwd_fused(self, dz, x, rep_outs):
+    def _trunk_bwd_fused(self, dz, x, rep_outs, crit=None):
         """K42: the dX GEMM and the one representation layer's backward (K13's) in one launch, g never stored.  Returns
         False (nothing done) when it does not apply: not the split GEMMs, more than one representation layer, no K13
         first layer, d_in > 32, or rows not given as the gathered minibatch."""
@@ -525,8 +589,13 @@ class FusedActorCritic:
         sign = trunk[5] if trunk is not None and len(trunk) > 5 else None   # K42S: act' from K16R's sign bits
         if sign is None and isinstance(x, Rows):
             sign = getattr(x, "hsign", None)   # or from K13's
-        ops.s3_gemm_trunk_bwd(dz, self._split_buf(k, "dx", dz.device), k, h, xr, code, slope, ws[0], ws[1],
-                              h_sign=sign)
+        if crit is not None:   # K42C: dz = the actor's half only
+            H = ops.HEAD_HIDDEN
+            ops.s3_gemm_trunk_bwd_crit(dz, self._split_buf(k, "dx_crit", dz.device), H, k - H, crit[0], crit[1],
+                                       crit[2], sign, xr, code, slope, ws[0], ws[1])
+        else:
+            ops.s3_gemm_trunk_bwd(dz, self._split_buf(k, "dx", dz.device), k, h, xr, code, slope, ws[0], ws[1],
+                                  h_sign=sign)
         self._cq.add(ws[0], lin.weight.grad)
         self._cq.add(ws[1], lin.bias.grad)
         return True

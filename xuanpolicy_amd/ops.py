@@ -163,8 +163,13 @@ def s3_split(b, out=None):
 _SPLIT_PLANS = {}
 
 
-def s3_split_batch(pairs):
-    """K40's split of up to 4 matrices in one launch: pairs = [(b [k, 256] any strides, out uint8 buffer), ...]."""
+def s3_split_batch(pairs, scales=None, cs=None):
+    """K40's split of up to 4 matrices in one launch: pairs = [(b [k, 256] any strides, out uint8 buffer), ...].
+    scales (r05, K42C): per pair None or (w f32 [k - start], a, start): rows k >= start scaled by a * w[k - start]
+    before the split; cs = (out f32 [256], slope): out[j] = slope * sum_c w[c] b[start + c, j] of the first scaled
+    pair."""
+    if scales is not None or cs is not None:
+        return _s3_split_batch_scaled(pairs, scales, cs)
     L = lib()
     key = tuple((b.data_ptr(), b.shape[0], b.stride(0), b.stride(1), o.data_ptr()) for b, o in pairs)
     plan = _SPLIT_PLANS.get(key)
@@ -183,6 +188,103 @@ def s3_split_batch(pairs):
         plan = _SPLIT_PLANS[key] = (n, arrs, [ctypes.cast(a, ctypes.c_void_p) for a in arrs])
     n, _keep, args = plan
     _lib.check(L.xpa_s3_split_batch(n, *args, _stream(pairs[0][0].device)), "xpa_s3_split_batch")
+
+
+def _s3_split_batch_scaled(pairs, scales, cs):
+    L = lib()
+    scales = scales or [None] * len(pairs)
+    key = ("scaled",) + tuple((b.data_ptr(), b.shape[0], b.stride(0), b.stride(1), o.data_ptr(),
+                               sc[0].data_ptr() if sc else 0, float(sc[1]) if sc else 1.0, int(sc[2]) if sc else 0)
+                              for (b, o), sc in zip(pairs, scales)) + ((cs[0].data_ptr(), float(cs[1])) if cs else (0,))
+    plan = _SPLIT_PLANS.get(key)
+    if plan is None:
+        for (b, o), sc in zip(pairs, scales):
+            _req(b, "b", torch.float32, contiguous=False)
+            if b.shape[1] != 256:
+                raise ValueError("s3_split_batch: b must be [k, 256]")
+            _req(o, "out", torch.uint8, (int(L.xpa_s3_split_bytes(b.shape[0], 256)),))
+            if sc is not None:
+                _req(sc[0], "scale", torch.float32, (b.shape[0] - int(sc[2]),))
+        if cs is not None:
+            _req(cs[0], "cs", torch.float32, (256,))
+            if not any(sc is not None for sc in scales):
+                raise ValueError("s3_split_batch: cs needs a scaled matrix")
+        n = len(pairs)
+        rows = [k[:5] for k in key[1:1 + n]]
+        arrs = ((ctypes.c_void_p * n)(*[r[0] for r in rows]), (ctypes.c_int64 * n)(*[r[1] for r in rows]),
+                (ctypes.c_int64 * n)(*[r[2] for r in rows]), (ctypes.c_int64 * n)(*[r[3] for r in rows]),
+                (ctypes.c_void_p * n)(*[r[4] for r in rows]),
+                (ctypes.c_void_p * n)(*[sc[0].data_ptr() if sc else None for sc in scales]),
+                (ctypes.c_float * n)(*[float(sc[1]) if sc else 1.0 for sc in scales]),
+                (ctypes.c_int64 * n)(*[int(sc[2]) if sc else 0 for sc in scales]))
+        if len(_SPLIT_PLANS) > 256:
+            _SPLIT_PLANS.clear()
+        plan = _SPLIT_PLANS[key] = (n, arrs, [ctypes.cast(a, ctypes.c_void_p) for a in arrs])
+    n, _keep, args = plan
+    _lib.check(L.xpa_s3_split_batch_scaled(n, *args, _p(cs[0]) if cs else None, float(cs[1]) if cs else 0.0,
+                                           _stream(pairs[0][0].device)), "xpa_s3_split_batch_scaled")
+
+
+def s3_gemm_trunk_bwd_crit(dz_a, b_split, k_a, k_c, mask, dv, cs, h_sign, x, act, slope, partial_dw=None,
+                           partial_db=None):
+    """K42C (r05): K42S with the critic's half of g = dz_pair . Wh_pair factored (csrc/sgemm3.hip): dz_a [rows, k_a]
+    (the actor's half), b_split = s3_split_batch of [Wh_a; Wh_c] with the critic rows scaled by (1 - slope_c) wc,
+    mask int32 [rows, 8] / dv [rows] from the critic head (fused_heads crit_mask), cs [256] = slope_c wc . Wh_c."""
+    L = lib()
+    _req(dz_a, "dz_a", torch.float32, contiguous=False)
+    ldz = _row_stride(dz_a, "dz_a", k_a)
+    rows = dz_a.shape[0]
+    d_in = x.shape[1]
+    ldx = _row_stride(x, "x", d_in)
+    _req(mask, "mask", torch.int32, (rows, 8))
+    _req(dv, "dv", torch.float32, (rows,))
+    _req(cs, "cs", torch.float32, (256,))
+    _req(h_sign, "h_sign", torch.int32, (rows, 8))
+    G = int(L.xpa_s3_gemm_trunk_bwd_num_partials(rows))
+    if partial_dw is None:
+        partial_dw = torch.empty(G, 256 * d_in, dtype=torch.float32, device=dz_a.device)
+    if partial_db is None:
+        partial_db = torch.empty(G, 256, dtype=torch.float32, device=dz_a.device)
+    _req(partial_dw, "partial_dw", torch.float32, (G, 256 * d_in))
+    _req(partial_db, "partial_db", torch.float32, (G, 256))
+    _lib.check(L.xpa_s3_gemm_trunk_bwd_crit(_p(dz_a), ldz, _p(b_split), k_a, k_c, _p(mask), _p(dv), _p(cs), _p(h_sign),
+                                            _p(x), ldx, rows, d_in, int(act), float(slope), _p(partial_dw),
+                                            _p(partial_db), _stream(dz_a.device)), "xpa_s3_gemm_trunk_bwd_crit")
+    return partial_dw, partial_db
+
+
+def s3_wgrad_pair_slices(rows):
+    """(sa, per_a, sc, per_c) of K41P for `rows`."""
+    v = [ctypes.c_int64() for _ in range(4)]
+    _lib.check(lib().xpa_s3_wgrad_pair_slices(rows, *[ctypes.byref(x) for x in v]), "xpa_s3_wgrad_pair_slices")
+    sa, sc, per_a, per_c = (x.value for x in v)
+    return sa, per_a, sc, per_c
+
+
+def s3_wgrad_pair(dz_a, h, mask, dv, wc, slope, out_a=None, out_c=None):
+    """K41P (r05): the paired hidden layer's weight-gradient slices — out_a [sa, 256, 256] of dz_a^T h (six-product
+    split) and out_c [sc, 256, 256] of the critic's wc[c] ((1 - slope) m^T Y + slope colsum(Y)), Y = dv (.) h (three
+    products: m exact in bf16).  The caller sums the slices (f64, fixed order)."""
+    _req(dz_a, "dz_a", torch.float32, contiguous=False)
+    _req(h, "h", torch.float32, contiguous=False)
+    rows = dz_a.shape[0]
+    lda, ldb = _row_stride(dz_a, "dz_a", 256), _row_stride(h, "h", 256)
+    if h.shape[0] != rows:
+        raise ValueError("dz_a and h must have the same rows")
+    _req(mask, "mask", torch.int32, (rows, 8))
+    _req(dv, "dv", torch.float32, (rows,))
+    _req(wc, "wc", torch.float32, (256,))
+    sa, per_a, sc, per_c = s3_wgrad_pair_slices(rows)
+    if out_a is None:
+        out_a = torch.empty(sa, 256, 256, dtype=torch.float32, device=dz_a.device)
+    if out_c is None:
+        out_c = torch.empty(sc, 256, 256, dtype=torch.float32, device=dz_a.device)
+    _req(out_a, "out_a", torch.float32, (sa, 256, 256))
+    _req(out_c, "out_c", torch.float32, (sc, 256, 256))
+    _lib.check(lib().xpa_s3_wgrad_pair(_p(dz_a), lda, _p(h), ldb, rows, _p(mask), _p(dv), _p(wc), float(slope), sa,
+                                       per_a, sc, per_c, _p(out_a), _p(out_c), _stream(dz_a.device)),
+               "xpa_s3_wgrad_pair")
+    return out_a, out_c
 
 
 def s3_gemm(a, b_split, k, out=None):
@@ -626,7 +728,7 @@ S3_HEADS = "s3q"   # with S3_GEMMS: "s3" K16S (both fragments split in the k loo
 def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, w_critic, b_critic, act_critic,
                 logstd, act, adv, ret, old_logp=None, idx=None, adv_partials=None, clip_range=0.2, vf_coef=0.25,
                 ent_coef=0.0, grads=None, colsum_queue=None, gemm=None, sq_logstd=None, defer_loss=False, trunk=None,
-                wh_split=None):
+                wh_split=None, crit_mask=None):
     """K12 actor + critic heads, loss finalize and the column-sum finalizes.
 
     z_*: hidden pre-activations [B, 256] (unit column stride; row stride = the workspace dz row stride,
@@ -637,7 +739,8 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
     Linear(d_in <= TRUNK_DMAX, 256) + the heads' activation is formed inside the launches too; gemm's x must be h_out,
     which the actor launch writes.  wh_split = (planes of w_h_actor^T, planes of w_h_critic^T) (s3_split): K16P; with
     trunk as well K16R (h formed in both launches' k loops, the actor writes h and, given h_sign int32 [B, 8], its
-    sign bits for K42S).
+    sign bits for K42S).  crit_mask = (mask int32 [B, 8], dv f32 [B]) with the K16Q heads (r05): the critic writes its
+    hidden activations' sign bits and d loss / d v per row instead of dz_critic (K41P / K42C's factored critic).
     (K x 256 / 1 x 256); act_*: (code, slope)
     of the hidden activation.  colsum_queue: an ops.ColsumQueue to defer the column-sum finalizes into
     (flushed by the caller), else they run here.  grads: dict with the gradient views to write — 'w_actor', 'b_actor',
@@ -743,10 +846,22 @@ def fused_heads(algo, dist, ws, z_actor, w_actor, b_actor, act_actor, z_critic, 
                       rows, _p(act), p_old, _p(adv), _p(adv_partials), n_adv, float(clip_range),
                       float(ent_coef), _p(ws.dz_actor), _p(ws.p_dw_actor), _p(ws.p_dbh_actor),
                       _p(ws.p_dbo_actor), _p(ws.loss_partials), W, s), "xpa_head_gemm_actor")
-        _lib.check(fc(act_critic[0], B, H, _p(x), x.stride(0), _p(whc), _p(bhc), ld, _p(w_critic),
-                      _p(b_critic), float(act_critic[1]), _p(idx), rows, _p(ret), float(vf_coef),
-                      _p(ws.dz_critic), _p(ws.p_dw_critic), _p(ws.p_dbh_critic),
-                      _p(ws.p_dbo_critic), _p(ws.loss_partials), W, s), "xpa_head_gemm_critic")
+        if crit_mask is not None:
+            if not (wh_split is not None and S3_HEADS == "s3q" and not K16W_ENABLED):
+                raise ValueError("crit_mask needs the K16Q heads")
+            cm, cdv = crit_mask
+            _req(cm, "crit mask", torch.int32, (B, 8))
+            _req(cdv, "crit dv", torch.float32, (B,))
+            _lib.check(L.xpa_head_gemm_s3q_critic_mask(act_critic[0], B, H, _p(x), x.stride(0), _p(whc), _p(bhc), ld,
+                                                       _p(w_critic), _p(b_critic), float(act_critic[1]), _p(idx), rows,
+                                                       _p(ret), float(vf_coef), None, _p(ws.p_dw_critic),
+                                                       _p(ws.p_dbh_critic), _p(ws.p_dbo_critic), _p(ws.loss_partials),
+                                                       W, s, _p(cm), _p(cdv)), "xpa_head_gemm_s3q_critic_mask")
+        else:
+            _lib.check(fc(act_critic[0], B, H, _p(x), x.stride(0), _p(whc), _p(bhc), ld, _p(w_critic),
+                          _p(b_critic), float(act_critic[1]), _p(idx), rows, _p(ret), float(vf_coef),
+                          _p(ws.dz_critic), _p(ws.p_dw_critic), _p(ws.p_dbh_critic),
+                          _p(ws.p_dbo_critic), _p(ws.loss_partials), W, s), "xpa_head_gemm_critic")
     else:
         _lib.check(L.xpa_head_fused_actor(ALGO[algo], DIST[dist], act_actor[0], B, K, H, ld, _p(z_actor), _p(w_actor),
                                           _p(b_actor), float(act_actor[1]), p_logstd, _p(idx), rows, _p(act), p_old,
