@@ -82,16 +82,23 @@ def test_fast_path_iteration_with_k16w_matches_oracle(agent_name, discrete, A, m
                                expect_mid_truncations=not discrete)
 
 
-@pytest.mark.parametrize("agent_name,discrete,A,heads", [("PPO_Clip", False, 6, "s3"), ("A2C", True, 18, "s3"),
-                                                         ("PPO_Clip", False, 6, "s3p"), ("A2C", True, 8, "s3q")])
-def test_fast_path_iteration_with_split_gemms_matches_oracle(agent_name, discrete, A, heads, monkeypatch):
+@pytest.mark.parametrize("agent_name,discrete,A,heads,crit", [("PPO_Clip", False, 6, "s3", False),
+                                                              ("A2C", True, 18, "s3", False),
+                                                              ("PPO_Clip", False, 6, "s3p", False),
+                                                              ("A2C", True, 8, "s3q", False),
+                                                              ("A2C", True, 8, "s3q", True),
+                                                              ("PPO_Clip", False, 6, "s3q", True)])
+def test_fast_path_iteration_with_split_gemms_matches_oracle(agent_name, discrete, A, heads, crit, monkeypatch):
     """The same end-to-end replay with the update's hidden-layer GEMMs on the bf16 matrix cores by the three-way
     split (ops.S3_GEMMS: K16S heads, K40 dX, K41 dW slices into the f64 finalize): every update's loss within 1e-4
-    and the final weights, as for the f32 MFMA path."""
+    and the final weights, as for the f32 MFMA path.  crit: the factored critic backward (r05, the default with the
+    K16Q heads: K41P / K42C, dz_critic never stored) instead of K41V / K42S on the whole dz_pair."""
     from xuanpolicy_amd import ops
+    from xuanpolicy_amd.fused_mlp import FusedActorCritic
     from xuanpolicy_amd.runner import build_synthbox_ppo
     monkeypatch.setattr(ops, "S3_GEMMS", True)
     monkeypatch.setattr(ops, "S3_HEADS", heads)
+    monkeypatch.setattr(FusedActorCritic, "CRIT_FACTORED", crit)
     N, T, D, H = 512, 64, 17, 256
     agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=D, act_dim=A, hidden=H, n_epoch=2, n_minibatch=4,
                                seed=21, device=DEV, agent=agent_name, discrete=discrete, ent_coef=0.01,
@@ -100,7 +107,11 @@ def test_fast_path_iteration_with_split_gemms_matches_oracle(agent_name, discret
     assert fm is not None and fm.gemm_heads and fm.pair is not None
     agent.train(T, log=False)
     agent.train(T - 1, log=False)
-    assert any(k[0] == "s3wgrad" for k in fm._partials if isinstance(k, tuple)), "K41 not used"
+    if crit:
+        assert any(k[0] == "wgrad_pair" for k in fm._partials if isinstance(k, tuple)), "K41P not used"
+        assert any(k[0] == "crit" for k in fm._partials if isinstance(k, tuple)), "the factored critic not used"
+    else:
+        assert any(k[0] == "s3wgrad" for k in fm._partials if isinstance(k, tuple)), "K41 not used"
     assert any(k[0] == "s3split" for k in fm._partials if isinstance(k, tuple)), "K40 not used"
     if heads in ("s3p", "s3q"):
         assert any(k[:2] == ("s3split", "s3p_a") for k in fm._partials if isinstance(k, tuple)), "K16P not used"

@@ -80,9 +80,9 @@ def child(v, reps=30):
     L, s = _lib.load(), ops._stream(dev)
     W = ws.loss_partials.shape[1]
 
-    pre = "xpa_head_gemm_s3p_" if FORM == "s3p" else "xpa_head_gemm_"
+    pre = "xpa_head_gemm_%s_" % FORM if FORM in ("s3p", "s3q") else "xpa_head_gemm_"
     fa, fc = getattr(L, pre + "actor"), getattr(L, pre + "critic")
-    if FORM == "s3p":
+    if FORM in ("s3p", "s3q"):
         wha, whc = ops.s3_split(wha.t()), ops.s3_split(whc.t())
 
     def actor():
@@ -100,7 +100,7 @@ def child(v, reps=30):
 
     res = {}
     fns = [("actor", actor), ("critic", critic)]
-    if v == 0 and FORM != "s3p":   # the library GEMM of the same shape, for reference
+    if v == 0 and FORM not in ("s3p", "s3q"):   # the library GEMM of the same shape, for reference
         import torch.nn.functional as F
         fns.append(("hipblaslt_linear_256x256", lambda: F.linear(x, wha, bha)))
     for name, fn in fns:
