@@ -654,6 +654,37 @@ int xpa_s3_wgrad_pair(const float *dz_a, int64_t lda, const float *h, int64_t ld
                       const unsigned *crit_mask, const float *crit_dv, const float *crit_wc, float crit_slope,
                       int64_t sa, int64_t per_a, int64_t sc, int64_t per_c, float *out_a, float *out_c,
                       xpa_stream_t stream);
+/* r05 — a wide representation layer (C4: Linear(376, 256) + LeakyReLU, mlp_block of layers.py:8-24 inside
+ * ppoclip_learner.py:31-33's policy(obs) and its loss.backward()) on the split GEMMs instead of the f32 library GEMMs:
+ * xpa_gather_minibatch_pitched: K4 into rows of pitch out_row_bytes (the pitch's tail untouched: a zero pad stays zero).
+ * xpa_s3_split_batch_padded: xpa_s3_split_batch where matrix i holds kv[i] <= k[i] rows, rows kv .. k - 1 split as 0.
+ * xpa_s3_gemm_bias_act (K40F): C = act(A . B + bias), act 0 identity / 1 LeakyReLU / 2 tanh, with sign_out (act 0 / 1,
+ *   nullable) the output's sign bits (the h_sign layout of xpa_s3_gemm_trunk_bwd_sign).
+ * xpa_s3_gemm_trunk_bwd_dz (K42W) / xpa_s3_gemm_trunk_bwd_crit_dz: K42S / K42C whose epilogue stores dz1 = g act'(h)
+ *   [rows, 256] (ld_out) and the db1 partials [G, 256] instead of the thin layer's dW (that comes from xpa_s3_wgrad on
+ *   the padded rows and dz1, i.e. dW^T slices [S, k_pad, 256]).
+ * xpa_colsum_finalize_batch_map: xpa_colsum_finalize_batch(_sq(_loss)) with per-segment output maps tmap [n][3] =
+ *   (inner, valid, ld): inner 0 = identity, else partial column r inner + i -> out[i ld + r] for r < valid (dropped
+ *   otherwise) — K41V's dW^T slices finalized straight into W [256][376]; loss_partials NULL: no loss block. */
+int xpa_gather_minibatch_pitched(const int64_t *idx, int64_t batch, int64_t n_rows, const void *obs,
+                                 int64_t obs_row_bytes, void *obs_out, int64_t out_row_bytes, const float *adv,
+                                 double *adv_partials, int32_t *err, xpa_stream_t stream);
+int xpa_s3_split_batch_padded(int n_mat, const float *const *b, const int64_t *k, const int64_t *kv, const int64_t *sk,
+                              const int64_t *sn, void *const *out, xpa_stream_t stream);
+int xpa_s3_gemm_bias_act(const float *a, int64_t lda, const void *b_split, float *c, int64_t ldc, int64_t m, int64_t k,
+                         const float *bias, int act, float slope, unsigned *sign_out, xpa_stream_t stream);
+int xpa_s3_gemm_trunk_bwd_dz(const float *dz, int64_t ldz, const void *b_split, int64_t k, const unsigned *h_sign,
+                             int64_t rows, int act, float slope, float *dz_out, int64_t ld_out, float *partial_db,
+                             xpa_stream_t stream);
+int xpa_s3_gemm_trunk_bwd_crit_dz(const float *dz_a, int64_t ldz, const void *b_split, int64_t k_a, int64_t k_c,
+                                  const unsigned *crit_mask, const float *crit_dv, const float *crit_cs,
+                                  const unsigned *h_sign, int64_t rows, int act, float slope, float *dz_out,
+                                  int64_t ld_out, float *partial_db, xpa_stream_t stream);
+int xpa_colsum_finalize_batch_map(int n_segs, const float *const *partials, const int64_t *n_partials,
+                                  const int64_t *cols, float *const *outs, const int64_t *tmap, double *sq,
+                                  int32_t *ticket, int algo, int dist, int64_t batch, int64_t act_dim,
+                                  const float *loss_partials, int64_t n_loss_partials, float vf_coef, float ent_coef,
+                                  float *scalars, float *d_logstd, xpa_stream_t stream);
 /* K16R (r04): xpa_head_gemm_s3p_actor / _critic (w_hidden = the split buffer of Wh^T) with the heads' input h formed
  * inside from the gathered minibatch rows (the representation's one thin layer: x_rows [batch, d_in <= 20], w_in
  * [256, d_in], b_in, the heads' activation at slope_in) — xpa_thin_linear_act_fwd's h bit for bit, so the update

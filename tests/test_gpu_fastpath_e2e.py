@@ -121,13 +121,18 @@ def test_fast_path_iteration_with_split_gemms_matches_oracle(agent_name, discret
                                expect_mid_truncations=not discrete)
 
 
-def test_c4_shape_iteration_matches_oracle():
+@pytest.mark.parametrize("wide", [True, False])
+def test_c4_shape_iteration_matches_oracle(wide, monkeypatch):
     """C4's per-shard shapes (BASELINE.json configs[3]: SynthBox(obs=376, act=17), ppo/mujoco.yaml, [256] nets) at a
     reduced N x T: the 376-wide trunk (no K13: the first layer is a library GEMM), the non-K14E rollout (K14 policy
     head + the separate env GEMM + K7), the 1024-thread K5 for wide observations, the KMAX-18 K16 bucket (A = 17)
     and the K9 step — one whole iteration replayed against the oracle (values, old log-probs, bootstraps, GAE,
     every update's loss scalars, final weights)."""
+    from xuanpolicy_amd.fused_mlp import FusedActorCritic
     from xuanpolicy_amd.runner import build_synthbox_ppo
+    # r05: the wide trunk layer on K40F / K42W (or K42C's dz form) / K41V with the transposed finalize; off = the
+    # library GEMM trunk of r04
+    monkeypatch.setattr(FusedActorCritic, "WIDE_TRUNK", wide)
     N, T, D, A, H = 512, 64, 376, 17, 256
     n_epoch, n_mb = 2, 4
     agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=D, act_dim=A, hidden=H, n_epoch=n_epoch,
@@ -138,6 +143,9 @@ def test_c4_shape_iteration_matches_oracle():
     agent.train(T, log=False)
     agent.train(T - 1, log=False)
     replay_last_step_iteration(agent, D, A, [H], False, "ppo", 0.0, n_epoch, n_mb, expect_mid_truncations=True)
+    assert fm._wide_on() == wide
+    keys = {k[0] for k in fm._partials if isinstance(k, tuple)}
+    assert (("wide_bwd" in keys) and ("wide_x" in keys)) == wide, keys
 
 
 def test_deferred_bootstraps_with_several_truncations_per_rollout():

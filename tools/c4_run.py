@@ -9,4 +9,7 @@ import bench  # noqa: E402
 if __name__ == "__main__":
     import torch
     it = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 2
+    if "wide-off" in sys.argv:   # the r04 trunk (library GEMMs) for A/B
+        from xuanpolicy_amd.fused_mlp import FusedActorCritic
+        FusedActorCritic.WIDE_TRUNK = False
     print(json.dumps(bench.c4_bench(torch.device("cuda:0"), 0, 1, steps=it, warmup=1)))

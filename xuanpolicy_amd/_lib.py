@@ -248,6 +248,17 @@ SIGNATURES = {
                                                  c_p]),
     "xpa_s3_gemm_trunk_bwd_crit": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64,
                                                   c_i64, ctypes.c_int, c_f32, c_p, c_p, c_p]),
+    "xpa_s3_split_batch_padded": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "xpa_s3_gemm_bias_act": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_p, ctypes.c_int, c_f32, c_p,
+                                            c_p]),
+    "xpa_s3_gemm_trunk_bwd_dz": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_p, c_i64, ctypes.c_int, c_f32, c_p, c_i64,
+                                                c_p, c_p]),
+    "xpa_s3_gemm_trunk_bwd_crit_dz": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64,
+                                                     ctypes.c_int, c_f32, c_p, c_i64, c_p, c_p]),
+    "xpa_gather_minibatch_pitched": (ctypes.c_int, [c_p, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p]),
+    "xpa_colsum_finalize_batch_map": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, ctypes.c_int,
+                                                     ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_f32, c_f32, c_p, c_p,
+                                                     c_p]),
     "xpa_s3_wgrad_pair_slices": (ctypes.c_int, [c_i64, c_p, c_p, c_p, c_p]),
     "xpa_s3_wgrad_pair_tune": (ctypes.c_int, [ctypes.c_int]),
     "xpa_s3_wgrad_pair": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i64, c_p, c_p, c_p, c_f32, c_i64, c_i64, c_i64,

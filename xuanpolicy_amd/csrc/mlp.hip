@@ -243,9 +243,25 @@ constexpr int kColGroups = 16;
 
 // sq != nullptr: also the tile's sum of squared outputs (f64, wave 0) into *sq — the gradient-norm
 // partial the clip + Adam step reads (xpa_clip_adam_step_partials), in place of a separate norm pass.
+// Output map (r05; tm_inner = 0: out[c]): column c = r tm_inner + i of the partials goes to out[i tm_ld + r] when
+// r < tm_valid and is dropped otherwise — a transposed, row-trimmed store (K41V's x^T dz slices of the C4 trunk layer,
+// [384 padded inputs][256] -> dW [256][376])
+__device__ __forceinline__ bool colsum_put(float *__restrict__ out, int c, float o, int tm_inner, int tm_valid,
+                                           int64_t tm_ld) {
+    if (tm_inner == 0) {
+        out[c] = o;
+        return true;
+    }
+    const int r = c / tm_inner, i = c - r * tm_inner;
+    if (r >= tm_valid) return false;
+    out[(int64_t)i * tm_ld + r] = o;
+    return true;
+}
+
 __device__ __forceinline__ void colsum_tile(const float *__restrict__ part, int64_t G, int C, int c0,
                                             float *__restrict__ out, double (*s_red)[kColTile],
-                                            double *__restrict__ sq = nullptr) {
+                                            double *__restrict__ sq = nullptr, int tm_inner = 0, int tm_valid = 0,
+                                            int64_t tm_ld = 0) {
     const int lane = threadIdx.x & (kColTile - 1), grp = threadIdx.x / kColTile;
     const int c = c0 + lane;
     double s = 0.0;
@@ -276,7 +292,7 @@ __device__ __forceinline__ void colsum_tile(const float *__restrict__ part, int6
             double t = s_red[0][lane];
             for (int g = 1; g < kColGroups; ++g) t += s_red[g][lane];
             o = (float)t;
-            out[c] = o;
+            if (!colsum_put(out, c, o, tm_inner, tm_valid, tm_ld)) o = 0.f;
         }
         if (sq) {  // grp 0 is wave 0 (kColTile == 64)
             const double q = xpa_wave_sum((double)o * (double)o);
@@ -316,6 +332,8 @@ struct ColsumBatch {
     int64_t G[kMaxSegs];
     int C[kMaxSegs];
     int tile0[kMaxSegs + 1];  // first column tile of each segment
+    int tm_inner[kMaxSegs], tm_valid[kMaxSegs];   // output maps (colsum_put; 0 = identity)
+    int64_t tm_ld[kMaxSegs];
     int n;
     // nullable: clip-norm partials.  sq[0] = a share written beforehand (d logstd, loss finalize),
     // sq[1 + tile] = each tile's sum of squared outputs, and the last block to finish (ticket) writes
@@ -351,7 +369,7 @@ __device__ __forceinline__ void colsum_batch_tile(const ColsumBatch &b, int tile
             }
             for (; k < G; ++k) acc += (double)part[k * C + c];
             o = (float)acc;
-            b.out[sg][c] = o;
+            if (!colsum_put(b.out[sg], c, o, b.tm_inner[sg], b.tm_valid[sg], b.tm_ld[sg])) o = 0.f;
         }
         if (sq) {
             const double q = xpa_wave_sum((double)o * (double)o);
@@ -401,7 +419,7 @@ __device__ __forceinline__ void colsum_batch_tile(const ColsumBatch &b, int tile
             const int c = c0 + 256 * h;
             if (grp == 0 && c < C) {
                 o[h] = (float)(((s4[0][lc] + s4[1][lc]) + s4[2][lc]) + s4[3][lc]);
-                b.out[sg][c] = o[h];
+                if (!colsum_put(b.out[sg], c, o[h], b.tm_inner[sg], b.tm_valid[sg], b.tm_ld[sg])) o[h] = 0.f;
             }
         }
         if (sq) {
@@ -412,7 +430,8 @@ __device__ __forceinline__ void colsum_batch_tile(const ColsumBatch &b, int tile
             if (threadIdx.x == 0) xpa_store_agent(sq, ((s4[1][0] + s4[1][1]) + s4[1][2]) + s4[1][3]);
         }
     } else {
-        colsum_tile(b.part[sg], b.G[sg], b.C[sg], (tile - b.tile0[sg]) * kColTile, b.out[sg], s_red, sq);
+        colsum_tile(b.part[sg], b.G[sg], b.C[sg], (tile - b.tile0[sg]) * kColTile, b.out[sg], s_red, sq,
+                    b.tm_inner[sg], b.tm_valid[sg], b.tm_ld[sg]);
     }
 }
 
@@ -551,7 +570,7 @@ XPA_API int64_t xpa_colsum_batch_tiles(int n_segs, const int64_t *n_partials, co
 namespace {
 int colsum_batch_launch(int n_segs, const float *const *partials, const int64_t *n_partials, const int64_t *cols,
                         float *const *outs, double *sq, int32_t *ticket, const XpaLossFinalizeArgs *loss,
-                        xpa_stream_t stream) {
+                        xpa_stream_t stream, const int64_t *tmap = nullptr) {
     if (n_segs <= 0 || n_segs > kMaxSegs || !partials || !n_partials || !cols || !outs) return (int)hipErrorInvalidValue;
     if (sq && !ticket) return (int)hipErrorInvalidValue;
     ColsumBatch b{};
@@ -570,6 +589,13 @@ int colsum_batch_launch(int n_segs, const float *const *partials, const int64_t 
         b.out[i] = outs[i];
         b.G[i] = n_partials[i];
         b.C[i] = (int)cols[i];
+        if (tmap && tmap[3 * i] != 0) {   // (inner, valid, ld): C = rows x inner, valid <= rows, ld >= valid
+            const int64_t in = tmap[3 * i], va = tmap[3 * i + 1], ld = tmap[3 * i + 2];
+            if (in < 1 || cols[i] % in != 0 || va < 1 || va > cols[i] / in || ld < va) return (int)hipErrorInvalidValue;
+            b.tm_inner[i] = (int)in;
+            b.tm_valid[i] = (int)va;
+            b.tm_ld[i] = ld;
+        }
         b.tile0[i] = (int)tiles;
         tiles += seg_tiles(n_partials[i], cols[i]);
     }
@@ -598,6 +624,25 @@ XPA_API int xpa_colsum_finalize_batch_sq_loss(int n_segs, const float *const *pa
     const XpaLossFinalizeArgs loss{algo, dist, batch, (int)act_dim, loss_partials, n_loss_partials,
                                    (int)xpa_loss_partial_width(act_dim), vf_coef, ent_coef, scalars, d_logstd};
     return colsum_batch_launch(n_segs, partials, n_partials, cols, outs, sq, ticket, &loss, stream);
+}
+
+// r05: the batched finalizes with per-segment output maps tmap [n_segs][3] = (inner, valid, ld) (inner 0: identity;
+// else column r inner + i -> out[i ld + r] for r < valid, dropped otherwise); sq / ticket nullable as a pair; with
+// loss_partials the loss finalize block as in xpa_colsum_finalize_batch_sq_loss (algo .. d_logstd ignored otherwise)
+XPA_API int xpa_colsum_finalize_batch_map(int n_segs, const float *const *partials, const int64_t *n_partials,
+                                          const int64_t *cols, float *const *outs, const int64_t *tmap, double *sq,
+                                          int32_t *ticket, int algo, int dist, int64_t batch, int64_t act_dim,
+                                          const float *loss_partials, int64_t n_loss_partials, float vf_coef,
+                                          float ent_coef, float *scalars, float *d_logstd, xpa_stream_t stream) {
+    if (!tmap) return (int)hipErrorInvalidValue;
+    if (!loss_partials) return colsum_batch_launch(n_segs, partials, n_partials, cols, outs, sq, ticket, nullptr, stream,
+                                                   tmap);
+    if (!sq || !ticket || batch <= 0 || act_dim <= 0 || act_dim > kXpaLossMaxAct || n_loss_partials <= 0 || !scalars ||
+        (dist == XPA_DIST_GAUSSIAN && !d_logstd))
+        return (int)hipErrorInvalidValue;
+    const XpaLossFinalizeArgs loss{algo, dist, batch, (int)act_dim, loss_partials, n_loss_partials,
+                                   (int)xpa_loss_partial_width(act_dim), vf_coef, ent_coef, scalars, d_logstd};
+    return colsum_batch_launch(n_segs, partials, n_partials, cols, outs, sq, ticket, &loss, stream, tmap);
 }
 
 XPA_API int xpa_colsum_finalize_batch(int n_segs, const float *const *partials, const int64_t *n_partials,

@@ -26,7 +26,8 @@ template <typename V>
 __global__ __launch_bounds__(256) void gather_rows_kernel(const int64_t *__restrict__ idx, int64_t batch,
                                                           int64_t n_rows, const V *__restrict__ src, int64_t row_vecs,
                                                           V *__restrict__ dst, const float *__restrict__ adv,
-                                                          double *__restrict__ adv_partials, int *__restrict__ err) {
+                                                          double *__restrict__ adv_partials, int *__restrict__ err,
+                                                          int64_t out_vecs = -1) {
     __shared__ double s_red[4];
     __shared__ int64_t s_src[kGatherRows];
     const int64_t r0 = (int64_t)blockIdx.x * kGatherRows;
@@ -40,14 +41,16 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const int64_t *__restr
     __syncthreads();
     // Consecutive lanes copy consecutive vectors of a row (32-bit index math; the row's source offset
     // comes from LDS), so each row is one contiguous burst.
+    // out_vecs (r05): the output row pitch in vectors (-1: packed rows); the pitch's tail of each row is not written
     const uint32_t rv = (uint32_t)row_vecs;
     const uint32_t n = (uint32_t)nr * rv;
-    V *out = dst + r0 * row_vecs;
+    const int64_t op = out_vecs < 0 ? row_vecs : out_vecs;
+    V *out = dst + r0 * op;
     for (uint32_t e = threadIdx.x; e < n; e += 256) {
         const uint32_t r = e / rv;
         const uint32_t c = e - r * rv;
         const int64_t sr = s_src[r];
-        out[e] = (sr >= 0 && sr < n_rows) ? src[sr * row_vecs + c] : V{};
+        out[(int64_t)r * op + c] = (sr >= 0 && sr < n_rows) ? src[sr * row_vecs + c] : V{};
     }
     if (adv_partials) {
         double s = 0.0, q = 0.0;
@@ -1069,6 +1072,23 @@ XPA_API int xpa_gather_minibatch(const int64_t *idx, int64_t batch, int64_t n_ro
     else
         hipLaunchKernelGGL(gather_rows_kernel<uint8_t>, dim3((unsigned)blocks), dim3(256), 0, s, idx, batch,
                            n_rows, (const uint8_t *)obs, obs_row_bytes, (uint8_t *)obs_out, adv, adv_partials, err);
+    return xpa_launch_status();
+}
+
+// r05: K4 into rows of pitch out_row_bytes >= obs_row_bytes (the bytes past each row's obs_row_bytes untouched: the
+// C4 trunk's zero-padded K40F operand, 376 -> 384 floats); 16-B vectors only
+XPA_API int xpa_gather_minibatch_pitched(const int64_t *idx, int64_t batch, int64_t n_rows, const void *obs,
+                                         int64_t obs_row_bytes, void *obs_out, int64_t out_row_bytes,
+                                         const float *adv, double *adv_partials, int32_t *err, xpa_stream_t stream) {
+    if (batch <= 0 || n_rows <= 0 || obs_row_bytes <= 0 || !idx || !obs || !obs_out || out_row_bytes < obs_row_bytes ||
+        obs_row_bytes % 16 || out_row_bytes % 16 || (((uintptr_t)obs | (uintptr_t)obs_out) % 16) ||
+        (adv_partials && !adv))
+        return (int)hipErrorInvalidValue;
+    const int64_t blocks = xpa_gather_num_partials(batch);
+    if ((int64_t)kGatherRows * (obs_row_bytes / 16) > 0xffffffffLL) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(gather_rows_kernel<uint4>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, idx, batch,
+                       n_rows, (const uint4 *)obs, obs_row_bytes / 16, (uint4 *)obs_out, adv, adv_partials, err,
+                       out_row_bytes / 16);
     return xpa_launch_status();
 }
 

@@ -101,6 +101,7 @@ struct SplitBatch {
     const float *rs_w[4];
     float rs_a[4];
     int64_t rs_from[4];
+    int64_t kv[4];   // rows k >= kv[i] are zero (r05: W0^T [376, 256] split as k = 384 for the C4 trunk forward)
     int n;
     float *cs_out;
     float cs_slope;
@@ -154,7 +155,7 @@ __global__ __launch_bounds__(256) void split_batch_kernel(SplitBatch sb) {
     for (int j = 0; j < 8; ++j) {
         __bf16 a0, a1, a2;
         const int64_t kk = c * kKC + kmap(h, j);
-        float v = b[kk * sk + (int64_t)n * sn];
+        float v = kk < sb.kv[i] ? b[kk * sk + (int64_t)n * sn] : 0.f;
         if (rw != nullptr && kk >= sb.rs_from[i]) v *= sb.rs_a[i] * rw[kk - sb.rs_from[i]];
         xpa_split3(v, a0, a1, a2);
         ph[j] = a0;
@@ -243,10 +244,16 @@ __device__ __forceinline__ void chunk64(const char *st, f32x16 (&acc)[8], int la
     }
 }
 
-template <int W, int S, int PROBE, int T64 = 0>
+// EPI (r05, K40F: the C4 trunk layer's forward): 0 = C = A B; 1 / 2 / 3 = C = act(A B + bias) with act identity /
+// LeakyReLU (slope) / tanh, and with `sign` (EPI 1 / 2) the output's sign bits beside it (32 bytes per row, byte col bit
+// cb = C[row, 32 cb + col] > 0: K42S's act' source, the layout xpa_thin_linear_act_fwd_gather_sign writes)
+template <int W, int S, int PROBE, int T64 = 0, int EPI = 0>
 __global__ __launch_bounds__(64 * W, 8 / W) void s3_gemm_kernel(const float *__restrict__ a, int64_t lda,
                                                                const __bf16 *__restrict__ bs, float *__restrict__ c,
-                                                               int64_t ldc, int64_t M, int nchunks) {
+                                                               int64_t ldc, int64_t M, int nchunks,
+                                                               const float *__restrict__ bias = nullptr,
+                                                               float slope = 0.f,
+                                                               unsigned char *__restrict__ sign = nullptr) {
     using G = S3Geom<W>;
     // ONE LDS array (the DMA target; see head.hip)
     __shared__ __attribute__((aligned(16))) char lds[S * G::kStage];
@@ -288,6 +295,29 @@ __global__ __launch_bounds__(64 * W, 8 / W) void s3_gemm_kernel(const float *__r
                     for (int j = 0; j < 4; ++j) crow[j * 32] = acc[rt * 4 + j][r];
                 }
             }
+        return;
+    }
+    if constexpr (EPI != 0) {
+        float bv[8];
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb) bv[cb] = bias[cb * 32 + col];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t row = r0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (row < M) {
+                float *crow = c + row * ldc + col;
+                unsigned bits = 0u;
+#pragma unroll
+                for (int cb = 0; cb < 8; ++cb) {
+                    float v = acc[cb][r] + bv[cb];
+                    if constexpr (EPI == 2) v = v > 0.f ? v : v * slope;
+                    if constexpr (EPI == 3) v = tanhf(v);
+                    crow[cb * 32] = v;
+                    bits |= (v > 0.f ? 1u : 0u) << cb;
+                }
+                if (EPI != 3 && sign != nullptr) sign[row * 32 + col] = (unsigned char)bits;
+            }
+        }
         return;
     }
 #pragma unroll
@@ -577,12 +607,13 @@ __device__ __forceinline__ float tb_act_g(float h, float slope) {  // thin.hip a
 
 // K42's epilogue (after the k loop, every wave done with the ring): dz1 = g * act'(h) in the accumulators, db1 and dW1
 // partials of the block (row block blockIdx.x); lds: the ring's LDS, reused
-template <int ACT, bool SIGN>
+template <int ACT, bool SIGN, bool DZ = false>
 __device__ __forceinline__ void tb_epilogue(f32x16 (&acc)[8], char *lds, int64_t r0, int64_t M, int t, int lane,
                                             int wave, const float *__restrict__ hmat, int64_t ldh,
                                             const float *__restrict__ x, int64_t ldx, int din, float slope,
                                             float *__restrict__ p_dw, float *__restrict__ p_db,
-                                            const unsigned *__restrict__ hsign) {
+                                            const unsigned *__restrict__ hsign, float *__restrict__ dz_out = nullptr,
+                                            int64_t ld_out = 0) {
     // ---- dz1 = g * act'(h) in place (rows past M: 0)
     const int hh = lane >> 5, col = lane & 31;
     const int64_t wrow = r0 + wave * 32;
@@ -605,6 +636,34 @@ __device__ __forceinline__ void tb_epilogue(f32x16 (&acc)[8], char *lds, int64_t
                 acc[cb][r] = ok ? acc[cb][r] * tb_act_g<ACT>(hv, slope) : 0.f;
             }
         }
+    }
+    if constexpr (DZ) {   // r05 (K42W, a wide trunk layer): dz1 stored for K41V's dW, db1 partials; no thin dW
+        float *s_db = reinterpret_cast<float *>(lds);   // [8 waves][256]
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t row = wrow + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (row < M) {
+                float *drow = dz_out + row * ld_out + col;
+#pragma unroll
+                for (int cb = 0; cb < 8; ++cb) drow[cb * 32] = acc[cb][r];
+            }
+        }
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb) {
+            float cs = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cs += acc[cb][r];
+            cs += __shfl_xor(cs, 32, 64);
+            if (hh == 0) s_db[wave * 256 + cb * 32 + col] = cs;
+        }
+        __syncthreads();
+        if (t < 256) {
+            float sum = s_db[t];
+#pragma unroll
+            for (int w = 1; w < 8; ++w) sum += s_db[w * 256 + t];
+            p_db[(int64_t)blockIdx.x * 256 + t] = sum;
+        }
+        return;
     }
     // ---- x^T's fragments for the wave's 32 rows: lane (feature i, half hh), k step s element j = row rho(8 s + j, hh)
     bf16x8 xh[2], xm[2], xl[2];
@@ -670,14 +729,16 @@ __device__ __forceinline__ void tb_epilogue(f32x16 (&acc)[8], char *lds, int64_t
 
 // SIGN (r04, K42S): act' from the sign bits K16R's actor launch wrote (byte col of the row's 32: bit cb = h[row, 32 cb +
 // col] > 0; LeakyReLU / identity only) instead of the 1 KiB h row — the same factor, 64 MiB less read per C2 update.
-template <int ACT, bool SIGN = false, int LA = 0>
+template <int ACT, bool SIGN = false, int LA = 0, bool DZ = false>
 __global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *__restrict__ a, int64_t lda,
                                                                    const __bf16 *__restrict__ bs, int64_t M,
                                                                    int nchunks, const float *__restrict__ hmat,
                                                                    int64_t ldh, const float *__restrict__ x,
                                                                    int64_t ldx, int din, float slope,
                                                                    float *__restrict__ p_dw, float *__restrict__ p_db,
-                                                                   const unsigned *__restrict__ hsign = nullptr) {
+                                                                   const unsigned *__restrict__ hsign = nullptr,
+                                                                   float *__restrict__ dz_out = nullptr,
+                                                                   int64_t ld_out = 0) {
     static_assert(!SIGN || ACT != 2, "sign bits carry act' of LeakyReLU / identity only");
     using G = S3Geom<8>;
     constexpr int kS = LA == 1 ? 4 : 3;   // ring stages (4 x 40 KiB = the whole 160 KiB with the lookahead)
@@ -725,7 +786,8 @@ __global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *
     }
     }
     __syncthreads();   // every wave done with the ring: the epilogue reuses its LDS
-    tb_epilogue<ACT, SIGN>(acc, lds, r0, M, t, lane, wave, hmat, ldh, x, ldx, din, slope, p_dw, p_db, hsign);
+    tb_epilogue<ACT, SIGN, DZ>(acc, lds, r0, M, t, lane, wave, hmat, ldh, x, ldx, din, slope, p_dw, p_db, hsign,
+                               dz_out, ld_out);
 }
 
 // ---- K42C (r05): K42S with the critic's half of dX factored -------------------------------------------------------
@@ -740,12 +802,12 @@ __global__ __launch_bounds__(512, 1) void s3_gemm_trunk_bwd_kernel(const float *
 // by dv[row] after adding cs, then the actor's chunks exactly as K42S (A = dz_a rows by LDS-DMA + the split).  The
 // epilogue (the trunk layer's backward) is K42S's.
 constexpr int kCMaskStride = 9;   // words per row of the LDS mask image (8 + 1: the 32 rows of a read hit 32 banks)
-template <int ACT>
+template <int ACT, bool DZ = false>
 __global__ __launch_bounds__(512, 1) void s3_trunk_bwd_crit_kernel(
     const float *__restrict__ a, int64_t lda, const __bf16 *__restrict__ bs, int64_t M, int nca, int ncc,
     const unsigned *__restrict__ cmask, const float *__restrict__ cdv, const float *__restrict__ ccs,
     const float *__restrict__ x, int64_t ldx, int din, float slope, float *__restrict__ p_dw, float *__restrict__ p_db,
-    const unsigned *__restrict__ hsign) {
+    const unsigned *__restrict__ hsign, float *__restrict__ dz_out = nullptr, int64_t ld_out = 0) {
     using G = S3Geom<8>;
     constexpr int kRing = 3 * G::kStage;
     constexpr int kMaskOff = kRing, kDvOff = kMaskOff + 256 * kCMaskStride * 4, kCsOff = kDvOff + 256 * 4;
@@ -846,7 +908,8 @@ __global__ __launch_bounds__(512, 1) void s3_trunk_bwd_crit_kernel(
         chunk<8, 0>(lds + (i % 3) * G::kStage, acc, lane, wave);
     }
     __syncthreads();   // every wave done with the ring: the epilogue reuses its LDS
-    tb_epilogue<ACT, true>(acc, lds, r0, M, t, lane, wave, nullptr, 0, x, ldx, din, slope, p_dw, p_db, hsign);
+    tb_epilogue<ACT, true, DZ>(acc, lds, r0, M, t, lane, wave, nullptr, 0, x, ldx, din, slope, p_dw, p_db, hsign,
+                               dz_out, ld_out);
 }
 
 // ---- K41: weight gradients dW = A^T B over the batch (K = rows), split-K -----------------------------------
@@ -1713,9 +1776,10 @@ XPA_API int xpa_s3_split_batch(int n_mat, const float *const *b, const int64_t *
 
 // xpa_s3_split_batch with per-matrix row scales (rs_w[i] nullable: rows k >= rs_from[i] times rs_a[i] * rs_w[i][k -
 // rs_from[i]]) and, with cs_out, cs_out[j] = cs_slope * sum_c rs_w[c] B[rs_from + c][j] of the first scaled matrix
-XPA_API int xpa_s3_split_batch_scaled(int n_mat, const float *const *b, const int64_t *k, const int64_t *sk,
-                                      const int64_t *sn, void *const *out, const float *const *rs_w, const float *rs_a,
-                                      const int64_t *rs_from, float *cs_out, float cs_slope, xpa_stream_t stream) {
+namespace {
+int split_batch_impl(int n_mat, const float *const *b, const int64_t *k, const int64_t *kv, const int64_t *sk,
+                     const int64_t *sn, void *const *out, const float *const *rs_w, const float *rs_a,
+                     const int64_t *rs_from, float *cs_out, float cs_slope, xpa_stream_t stream) {
     if (n_mat < 1 || n_mat > 4 || !b || !k || !sk || !sn || !out) return (int)hipErrorInvalidValue;
     SplitBatch sb{};
     sb.n = n_mat;
@@ -1739,6 +1803,8 @@ XPA_API int xpa_s3_split_batch_scaled(int n_mat, const float *const *b, const in
         sb.k[i] = k[i];
         sb.sk[i] = sk[i];
         sb.sn[i] = sn[i];
+        sb.kv[i] = kv ? kv[i] : k[i];
+        if (sb.kv[i] < 1 || sb.kv[i] > k[i] || (sb.rs_w[i] && sb.kv[i] != k[i])) return (int)hipErrorInvalidValue;
         sb.out[i] = static_cast<__bf16 *>(out[i]);
         kmax = k[i] > kmax ? k[i] : kmax;
     }
@@ -1747,6 +1813,21 @@ XPA_API int xpa_s3_split_batch_scaled(int n_mat, const float *const *b, const in
     if (cs_out && gx < 8) gx = 8;   // the cs row uses 8 blocks
     split_batch_kernel<<<dim3((unsigned)gx, (unsigned)(n_mat + (cs_out ? 1 : 0))), dim3(256), 0, stream>>>(sb);
     return xpa_launch_status();
+}
+}  // namespace
+
+XPA_API int xpa_s3_split_batch_scaled(int n_mat, const float *const *b, const int64_t *k, const int64_t *sk,
+                                      const int64_t *sn, void *const *out, const float *const *rs_w, const float *rs_a,
+                                      const int64_t *rs_from, float *cs_out, float cs_slope, xpa_stream_t stream) {
+    return split_batch_impl(n_mat, b, k, nullptr, sk, sn, out, rs_w, rs_a, rs_from, cs_out, cs_slope, stream);
+}
+
+// r05 (C4 trunk): xpa_s3_split_batch where matrix i holds kv[i] <= k[i] rows (element (r, c) at b_i[r sk_i + c sn_i],
+// r < kv_i) and its planes cover k_i rows, rows kv_i .. k_i - 1 zero (a K that is not a multiple of 16 padded up)
+XPA_API int xpa_s3_split_batch_padded(int n_mat, const float *const *b, const int64_t *k, const int64_t *kv,
+                                      const int64_t *sk, const int64_t *sn, void *const *out, xpa_stream_t stream) {
+    if (!kv) return (int)hipErrorInvalidValue;
+    return split_batch_impl(n_mat, b, k, kv, sk, sn, out, nullptr, nullptr, nullptr, nullptr, 0.f, stream);
 }
 
 XPA_API int xpa_s3_split_b(const float *b, int64_t k, int64_t n, int64_t sk, int64_t sn, void *out,
@@ -1848,6 +1929,80 @@ XPA_API int xpa_s3_gemm_trunk_bwd_crit(const float *dz_a, int64_t ldz, const voi
         s3_trunk_bwd_crit_kernel<1><<<grid, block, 0, stream>>>(dz_a, ldz, bs, rows, nca, ncc, crit_mask, crit_dv,
                                                                  crit_cs, x, ldx, (int)d_in, slope, partial_dw,
                                                                  partial_db, h_sign);
+    return xpa_launch_status();
+}
+
+// K42W (r05, the C4 trunk layer): xpa_s3_gemm_trunk_bwd_sign for a representation layer too wide for the fused thin dW:
+// dz_out [rows, 256] (row stride ld_out) = g . act'(h) from h's sign bits, and the db partials [G, 256]; the layer's
+// dW comes from xpa_s3_wgrad on (x, dz_out)
+XPA_API int xpa_s3_gemm_trunk_bwd_dz(const float *dz, int64_t ldz, const void *b_split, int64_t k,
+                                     const unsigned *h_sign, int64_t rows, int act, float slope, float *dz_out,
+                                     int64_t ld_out, float *partial_db, xpa_stream_t stream) {
+    if (!dz || !b_split || !h_sign || !dz_out || !partial_db || rows <= 0 || k <= 0 || k % kKC != 0 || ldz < k ||
+        (ldz & 3) || (reinterpret_cast<uintptr_t>(dz) & 15) || (reinterpret_cast<uintptr_t>(h_sign) & 15) ||
+        ld_out < kN || act < 0 || act > 1 || k / kKC > (1 << 20))
+        return (int)hipErrorInvalidValue;
+    const dim3 grid((unsigned)xpa_s3_gemm_trunk_bwd_num_partials(rows)), block(512);
+    const __bf16 *bs = static_cast<const __bf16 *>(b_split);
+    const int nch = (int)(k / kKC);
+    if (act == 0)
+        s3_gemm_trunk_bwd_kernel<0, true, 0, true><<<grid, block, 0, stream>>>(dz, ldz, bs, rows, nch, nullptr, 0,
+                                                                                nullptr, 0, 0, slope, nullptr,
+                                                                                partial_db, h_sign, dz_out, ld_out);
+    else
+        s3_gemm_trunk_bwd_kernel<1, true, 0, true><<<grid, block, 0, stream>>>(dz, ldz, bs, rows, nch, nullptr, 0,
+                                                                                nullptr, 0, 0, slope, nullptr,
+                                                                                partial_db, h_sign, dz_out, ld_out);
+    return xpa_launch_status();
+}
+
+// K42C's dz form (r05, the C4 trunk layer with the factored critic): xpa_s3_gemm_trunk_bwd_crit, its epilogue K42W's
+XPA_API int xpa_s3_gemm_trunk_bwd_crit_dz(const float *dz_a, int64_t ldz, const void *b_split, int64_t k_a,
+                                          int64_t k_c, const unsigned *crit_mask, const float *crit_dv,
+                                          const float *crit_cs, const unsigned *h_sign, int64_t rows, int act,
+                                          float slope, float *dz_out, int64_t ld_out, float *partial_db,
+                                          xpa_stream_t stream) {
+    if (!dz_a || !b_split || !crit_mask || !crit_dv || !crit_cs || !h_sign || !dz_out || !partial_db || rows <= 0 ||
+        k_a <= 0 || k_c <= 0 || k_a % kKC != 0 || k_c % kKC != 0 || k_c > 256 || ldz < k_a || (ldz & 3) ||
+        (reinterpret_cast<uintptr_t>(dz_a) & 15) || (reinterpret_cast<uintptr_t>(h_sign) & 15) ||
+        (reinterpret_cast<uintptr_t>(crit_mask) & 15) || ld_out < kN || act < 0 || act > 1 ||
+        (k_a + k_c) / kKC > (1 << 20))
+        return (int)hipErrorInvalidValue;
+    const dim3 grid((unsigned)xpa_s3_gemm_trunk_bwd_num_partials(rows)), block(512);
+    const __bf16 *bs = static_cast<const __bf16 *>(b_split);
+    const int nca = (int)(k_a / kKC), ncc = (int)(k_c / kKC);
+    if (act == 0)
+        s3_trunk_bwd_crit_kernel<0, true><<<grid, block, 0, stream>>>(dz_a, ldz, bs, rows, nca, ncc, crit_mask,
+                                                                       crit_dv, crit_cs, nullptr, 0, 0, slope, nullptr,
+                                                                       partial_db, h_sign, dz_out, ld_out);
+    else
+        s3_trunk_bwd_crit_kernel<1, true><<<grid, block, 0, stream>>>(dz_a, ldz, bs, rows, nca, ncc, crit_mask,
+                                                                       crit_dv, crit_cs, nullptr, 0, 0, slope, nullptr,
+                                                                       partial_db, h_sign, dz_out, ld_out);
+    return xpa_launch_status();
+}
+
+// K40F (r05, the C4 trunk layer's forward): C [m, 256] = act(A [m, k] . B + bias), B split (k % 16 == 0; a layer
+// width that is not a multiple of 16 goes in zero-padded: A's row pitch >= k with zero columns, B's planes from
+// xpa_s3_split_batch_padded).  act 0 identity / 1 LeakyReLU (slope) / 2 tanh; sign_out (nullable, act 0 / 1): the
+// output's sign bits, 32 bytes per row (K42W's act').
+XPA_API int xpa_s3_gemm_bias_act(const float *a, int64_t lda, const void *b_split, float *c, int64_t ldc, int64_t m,
+                                 int64_t k, const float *bias, int act, float slope, unsigned *sign_out,
+                                 xpa_stream_t stream) {
+    if (!a || !b_split || !c || !bias || m <= 0 || k <= 0 || k % kKC != 0 || lda < k || ldc < kN ||
+        (reinterpret_cast<uintptr_t>(a) & 15) || (lda & 3) || act < 0 || act > 2 || (sign_out && act == 2) ||
+        (reinterpret_cast<uintptr_t>(sign_out) & 15) || k / kKC > (1 << 20))
+        return (int)hipErrorInvalidValue;
+    const __bf16 *bs = static_cast<const __bf16 *>(b_split);
+    const int nch = (int)(k / kKC);
+    const dim3 grid((unsigned)((m + 255) / 256)), block(512);
+    unsigned char *sg = reinterpret_cast<unsigned char *>(sign_out);
+    if (act == 0)
+        s3_gemm_kernel<8, 3, 0, 0, 1><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, nch, bias, slope, sg);
+    else if (act == 1)
+        s3_gemm_kernel<8, 3, 0, 0, 2><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, nch, bias, slope, sg);
+    else
+        s3_gemm_kernel<8, 3, 0, 0, 3><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, nch, bias, slope, nullptr);
     return xpa_launch_status();
 }
 

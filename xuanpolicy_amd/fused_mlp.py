@@ -127,6 +127,12 @@ class FusedActorCritic:
         # K13 for the first representation layer when its input is narrow (observation width <= 64)
         self.thin0 = (len(self.rep) > 0 and self.rep[0][0].in_features <= 64
                       and self.rep[0][0].out_features == ops.HEAD_HIDDEN)
+        # r05 (C4): one WIDE representation layer (d_in > 64, d_in % 4 == 0, identity / LeakyReLU) on the split GEMMs —
+        # K40F forward from the zero-padded gathered rows (+ h's sign bits), K42W / K42C-dz backward to dz1, K41V dW^T
+        # slices finalized transposed into W0's gradient (_wide_on)
+        self.wide0 = (len(self.rep) == 1 and not self.thin0 and self.rep[0][0].out_features == ops.HEAD_HIDDEN
+                      and self.rep[0][0].in_features % 4 == 0 and self.rep[0][0].in_features <= 4096
+                      and self.rep[0][1] in (0, 1))
         self.pair = None
         if self.fused_heads and flat is not None and len(self.actor) == 2 and len(self.critic) == 2:
             la, lc = self.actor[0][0], self.critic[0][0]
@@ -180,11 +186,73 @@ class FusedActorCritic:
         return outs
 
     def rows_ok(self, flat):
-        """True when the update can take Rows(flat, idx) (K13 with the gather folded in)."""
-        return (self.fused_heads and self.thin0 and flat.dim() == 2 and flat.dtype == torch.float32
-                and flat.stride(1) == 1 and flat.is_cuda)
+        """True when the update can take Rows(flat, idx) (K13 with the gather folded in, or the wide trunk's pitched
+        gather)."""
+        return (self.fused_heads and (self.thin0 or self._wide_on()) and flat.dim() == 2
+                and flat.dtype == torch.float32 and flat.stride(1) == 1 and flat.is_cuda
+                and (self.thin0 or flat.is_contiguous()))
+
+    WIDE_TRUNK = True   # r05: the wide trunk layer on K40F / K42W / K41V where it applies (bench.py --wide-trunk off: A/B)
+
+    def _wide_on(self):
+        return (self.WIDE_TRUNK and self.wide0 and self.fused_heads and ops.S3_GEMMS and self.pair is not None
+                and self._dx_split_ok(self.pair[0]))
+
+    def _wide_forward(self, x, adv, adv_partials):
+        """The wide trunk layer's forward on the minibatch rows x = Rows(flat, idx): the pitched gather into a
+        zero-padded [B, d_pad] buffer (+ the advantage moments), W0^T's split (zero rows to d_pad), K40F (bias,
+        activation and h's sign bits in the epilogue)."""
+        lin, code, slope = self.rep[0]
+        B, d = x.idx.shape[0], lin.in_features
+        kp = (d + 15) // 16 * 16
+        key = ("wide_x", B, kp)
+        xp = self._partials.get(key)
+        if xp is None:   # graph-capture safe: allocated (and its pad zeroed) on first (eager) use
+            xp = torch.zeros((B, kp), dtype=torch.float32, device=x.device)
+            self._partials[key] = xp
+        ops.gather_minibatch_pitched(x.idx, x.flat, xp, adv=adv if adv_partials is not None else None,
+                                     adv_partials=adv_partials)
+        x.gathered = xp
+        x.hsign = self._sign_buf(B, x.device)
+        wsplit = self._split_buf(kp, "w0t", x.device)
+        ops.s3_split_padded(lin.weight.t(), kp, out=wsplit)
+        h = torch.empty((B, lin.out_features), dtype=torch.float32, device=x.device)
+        ops.s3_gemm_bias_act(xp, wsplit, kp, lin.bias, code, slope, out=h, sign=x.hsign)
+        return [h]
+
+    def _wide_bwd(self, dz, x, crit):
+        """K42W (or K42C's dz form with the factored critic): dz1 = (dz . Wh_pair) act'(h) and db0's partials; K41V's
+        slices of x_pad^T dz1, finalized transposed (and trimmed to d_in) into W0's gradient."""
+        lin, code, slope = self.rep[0]
+        B, d = dz.shape[0], lin.in_features
+        xp = x.gathered
+        kp = xp.shape[1]
+        S = max(1, 256 // (kp // 128))
+        key = ("wide_bwd", B, kp, S)
+        ws = self._partials.get(key)
+        if ws is None:
+            G = int(ops.lib().xpa_s3_gemm_trunk_bwd_num_partials(B))
+            ws = (torch.empty((B, 256), device=dz.device), torch.empty((G, 256), device=dz.device),
+                  torch.empty((S, kp, 256), device=dz.device))
+            self._partials[key] = ws
+        dz1, pdb, pdw = ws
+        k = self.pair[0].shape[0]
+        if crit is not None:
+            H = ops.HEAD_HIDDEN
+            ops.s3_gemm_trunk_bwd_dz(dz, self._split_buf(k, "dx_crit", dz.device), k, x.hsign, code, slope, dz1, pdb,
+                                     crit=(H, k - H, crit[0], crit[1], crit[2]))
+        else:
+            ops.s3_gemm_trunk_bwd_dz(dz, self._split_buf(k, "dx", dz.device), k, x.hsign, code, slope, dz1, pdb)
+        ops.s3_wgrad(xp, dz1, out=pdw, slices=S)
+        self._cq.add(pdw.view(S, -1), lin.weight.grad, tmap=(256, d, d))
+        self._cq.add(pdb, lin.bias.grad)
+        return True
 
     def _rep_forward(self, x, norm=None, adv=None, adv_partials=None, defer_trunk=False):
+        if isinstance(x, Rows) and not self.thin0:
+            if not self._wide_on():
+                raise ValueError("Rows input needs the thin (K13) or the wide (K40F) trunk layer")
+            return self._wide_forward(x, adv, adv_partials)
         if isinstance(x, Rows):
             # K4's gather folded into K13's x staging (+ the advantage moments when adv_partials is given)
             lin, code, slope = self.rep[0]
@@ -504,8 +572,9 @@ class FusedActorCritic:
                 and self.critic[-1][0].out_features == 1 and self.pair is not None and len(self.rep) == 1):
             return None
         lin, code, _ = self.rep[0]
-        if not (self.FUSE_TRUNK_BWD and self._dx_split_ok(self.pair[0]) and self.thin0 and code in (0, 1)
-                and isinstance(x, Rows) and getattr(x, "hsign", None) is not None and lin.in_features <= 32):
+        if not (self.FUSE_TRUNK_BWD and self._dx_split_ok(self.pair[0]) and code in (0, 1)
+                and ((self.thin0 and lin.in_features <= 32) or self._wide_on())
+                and isinstance(x, Rows) and getattr(x, "hsign", None) is not None):
             return None
         xr = x.gathered
         h = rep_outs[0] if rep_outs else None
@@ -566,7 +635,10 @@ class FusedActorCritic:
     def _trunk_bwd_fused(self, dz, x, rep_outs, crit=None):
         """K42: the dX GEMM and the one representation layer's backward (K13's) in one launch, g never stored.  Returns
         False (nothing done) when it does not apply: not the split GEMMs, more than one representation layer, no K13
-        first layer, d_in > 32, or rows not given as the gathered minibatch."""
+        first layer, d_in > 32, or rows not given as the gathered minibatch.  The wide trunk layer: _wide_bwd."""
+        if (self._wide_on() and isinstance(x, Rows) and getattr(x, "hsign", None) is not None
+                and isinstance(x.gathered, torch.Tensor) and _vec4_rows(dz)):
+            return self._wide_bwd(dz, x, crit)
         if not (self.FUSE_TRUNK_BWD and self._dx_split_ok(self.pair[0]) and len(self.rep) == 1 and self.thin0
                 and _vec4_rows(dz)):
             return False

@@ -331,6 +331,97 @@ def s3_gemm_trunk_bwd(dz, b_split, k, h, x, act, slope, partial_dw=None, partial
     return partial_dw, partial_db
 
 
+def s3_split_padded(b, k_pad, out=None):
+    """The split of b [kv, 256] (any strides) padded with zero rows to k_pad (a multiple of 16): K40F's operand for a
+    layer width that is not a multiple of 16 (xpa_s3_split_batch_padded)."""
+    _req(b, "b", torch.float32, contiguous=False)
+    kv, n = b.shape
+    if n != 256 or k_pad % 16 or k_pad < kv:
+        raise ValueError("s3_split_padded: b must be [kv, 256], kv <= k_pad, k_pad % 16 == 0")
+    L = lib()
+    nbytes = int(L.xpa_s3_split_bytes(k_pad, 256))
+    if out is None:
+        out = torch.empty(nbytes, dtype=torch.uint8, device=b.device)
+    _req(out, "out", torch.uint8, (nbytes,))
+    arr = lambda t, v: (t * 1)(v)   # noqa: E731
+    _lib.check(L.xpa_s3_split_batch_padded(1, arr(ctypes.c_void_p, b.data_ptr()), arr(ctypes.c_int64, k_pad),
+                                           arr(ctypes.c_int64, kv), arr(ctypes.c_int64, b.stride(0)),
+                                           arr(ctypes.c_int64, b.stride(1)), arr(ctypes.c_void_p, out.data_ptr()),
+                                           _stream(b.device)), "xpa_s3_split_batch_padded")
+    return out
+
+
+def s3_gemm_bias_act(a, b_split, k, bias, act, slope, out=None, sign=None):
+    """K40F (r05): out [m, 256] = act(a [m, k] . B + bias) (act 0 identity / 1 LeakyReLU / 2 tanh); sign (int32 [m, 8],
+    act 0 / 1): the output's sign bits for K42W.  a's columns past the layer width must be zero (padded rows)."""
+    _req(a, "a", torch.float32, contiguous=False)
+    lda = _row_stride(a, "a", k)
+    m = a.shape[0]
+    _req(bias, "bias", torch.float32, (256,))
+    if out is None:
+        out = torch.empty(m, 256, dtype=torch.float32, device=a.device)
+    ldc = _row_stride(out, "out", 256)
+    if out.shape[0] != m:
+        raise ValueError("out must have %d rows" % m)
+    if sign is not None:
+        _req(sign, "sign", torch.int32, (m, 8))
+    _lib.check(lib().xpa_s3_gemm_bias_act(_p(a), lda, _p(b_split), _p(out), ldc, m, k, _p(bias), int(act),
+                                          float(slope), _p(sign) if sign is not None else None, _stream(a.device)),
+               "xpa_s3_gemm_bias_act")
+    return out
+
+
+def s3_gemm_trunk_bwd_dz(dz, b_split, k, h_sign, act, slope, dz_out, partial_db, crit=None):
+    """K42W (r05): g = dz [rows, k] . B (split); dz_out [rows, 256] = g act'(h) from h's sign bits, partial_db [G, 256]
+    (the wide trunk layer's; its dW from s3_wgrad on the layer input and dz_out).  crit = (k_a, k_c, mask, dv, cs):
+    K42C's factored critic half (dz = the actor's half, [rows, k_a])."""
+    L = lib()
+    _req(dz, "dz", torch.float32, contiguous=False)
+    rows = dz.shape[0]
+    ld_out = _row_stride(dz_out, "dz_out", 256)
+    _req(h_sign, "h_sign", torch.int32, (rows, 8))
+    G = int(L.xpa_s3_gemm_trunk_bwd_num_partials(rows))
+    _req(partial_db, "partial_db", torch.float32, (G, 256))
+    if dz_out.shape[0] != rows:
+        raise ValueError("dz_out must have %d rows" % rows)
+    if crit is not None:
+        k_a, k_c, mask, dv, cs = crit
+        ldz = _row_stride(dz, "dz_a", k_a)
+        _req(mask, "mask", torch.int32, (rows, 8))
+        _req(dv, "dv", torch.float32, (rows,))
+        _req(cs, "cs", torch.float32, (256,))
+        _lib.check(L.xpa_s3_gemm_trunk_bwd_crit_dz(_p(dz), ldz, _p(b_split), k_a, k_c, _p(mask), _p(dv), _p(cs),
+                                                   _p(h_sign), rows, int(act), float(slope), _p(dz_out), ld_out,
+                                                   _p(partial_db), _stream(dz.device)), "xpa_s3_gemm_trunk_bwd_crit_dz")
+        return dz_out, partial_db
+    ldz = _row_stride(dz, "dz", k)
+    _lib.check(L.xpa_s3_gemm_trunk_bwd_dz(_p(dz), ldz, _p(b_split), k, _p(h_sign), rows, int(act), float(slope),
+                                          _p(dz_out), ld_out, _p(partial_db), _stream(dz.device)),
+               "xpa_s3_gemm_trunk_bwd_dz")
+    return dz_out, partial_db
+
+
+def gather_minibatch_pitched(idx, obs, obs_out, adv=None, adv_partials=None):
+    """K4 into rows of obs_out [B, pitch] (pitch >= the row width; columns past it untouched, so a zero pad stays
+    zero): the wide trunk's K40F operand.  obs [n_rows, d] f32 contiguous, d % 4 == 0."""
+    _req(idx, "idx", torch.int64)
+    B = idx.shape[0]
+    if obs.dim() != 2 or not obs.is_contiguous():
+        raise ValueError("obs must be a contiguous [n_rows, d] tensor")
+    _req(obs_out, "obs_out", torch.float32, contiguous=False)
+    d = obs.shape[1]
+    if obs_out.dim() != 2 or obs_out.shape[0] != B or obs_out.stride(1) != 1 or obs_out.stride(0) < d:
+        raise ValueError("obs_out must be [B, >= %d] with unit column stride" % d)
+    if adv is not None:
+        _req(adv, "adv", torch.float32)
+        _req(adv_partials, "adv_partials", torch.float64, (gather_num_partials(B), 2))
+    _lib.check(lib().xpa_gather_minibatch_pitched(_p(idx), B, obs.shape[0], _p(obs), d * 4, _p(obs_out),
+                                                  obs_out.stride(0) * 4, _p(adv) if adv is not None else None,
+                                                  _p(adv_partials) if adv is not None else None, None,
+                                                  _stream(obs.device)), "xpa_gather_minibatch_pitched")
+    return obs_out
+
+
 def s3_wgrad_slices(rows, m):
     return int(lib().xpa_s3_wgrad_num_slices(rows, m))
 
@@ -651,12 +742,21 @@ class ColsumQueue:
         self.loss = (int(algo), int(dist), int(batch), int(act_dim), loss_partials, float(vf_coef), float(ent_coef),
                      scalars, d_logstd)
 
-    def add(self, part, out):
+    def add(self, part, out, tmap=None):
+        """tmap (r05) = (inner, valid, ld): column r inner + i of the partials goes to out[i ld + r] for r < valid
+        (xpa_colsum_finalize_batch_map; e.g. K41V's padded dW^T slices into W [256, d_in]); out then holds
+        inner * valid elements."""
         _req(part, "partials", torch.float32)
         _req(out, "out", torch.float32)
-        if part.dim() != 2 or out.numel() != part.shape[1]:
-            raise ValueError("partials must be [G, C] and out must have C elements")
-        self.items.append((part, out))
+        if tmap is None:
+            if part.dim() != 2 or out.numel() != part.shape[1]:
+                raise ValueError("partials must be [G, C] and out must have C elements")
+        else:
+            inner, valid, ld = (int(v) for v in tmap)
+            if (part.dim() != 2 or part.shape[1] % inner or valid > part.shape[1] // inner or out.numel() != inner * valid
+                    or not out.is_contiguous() or ld != valid):
+                raise ValueError("tmap: partials [G, rows * inner], out contiguous [inner, valid], ld == valid")
+        self.items.append((part, out, tmap))
 
     def flush(self, device=None, sq=None):
         """Launch the queued finalizes.  sq (float64 tensor, >= tiles + 2 entries, sq[0] written beforehand):
@@ -671,7 +771,7 @@ class ColsumQueue:
                                                              _p(sq) if sq is not None else None, _stream(dev)),
                            "xpa_policy_loss_finalize")
             return None, 0
-        key = tuple((p.data_ptr(), p.shape[0], p.shape[1], o.data_ptr()) for p, o in self.items)
+        key = tuple((p.data_ptr(), p.shape[0], p.shape[1], o.data_ptr(), tm) for p, o, tm in self.items)
         plan = self._plans.get(key)
         if plan is None:
             plan = []
@@ -682,7 +782,10 @@ class ColsumQueue:
                         (ctypes.c_int64 * n)(*[c[2] for c in chunk]), (ctypes.c_void_p * n)(*[c[3] for c in chunk]))
                 tiles = int(lib().xpa_colsum_batch_tiles(n, ctypes.cast(arrs[1], ctypes.c_void_p),
                                                          ctypes.cast(arrs[2], ctypes.c_void_p)))
-                plan.append((n, arrs, [ctypes.cast(a, ctypes.c_void_p) for a in arrs], tiles))
+                tmap = None
+                if any(c[4] is not None for c in chunk):   # the map entry (r05): (inner, valid, ld) per segment
+                    tmap = (ctypes.c_int64 * (3 * n))(*[v for c in chunk for v in (c[4] or (0, 0, 0))])
+                plan.append((n, arrs, [ctypes.cast(a, ctypes.c_void_p) for a in arrs], tiles, tmap))
             self._plans[key] = plan
         dev = device if device is not None else self.items[0][0].device
         s = _stream(dev)
@@ -699,8 +802,18 @@ class ColsumQueue:
         if one:
             if self._ticket is None:
                 self._ticket = torch.zeros((1,), dtype=torch.int32, device=dev)
-            n, _keep, args, tiles = plan[0]
-            if loss is not None:   # one launch: the column tiles + the loss finalize block
+            n, _keep, args, tiles, tmap = plan[0]
+            if tmap is not None:
+                la = loss if loss is not None else (0, 0, 0, 0, None, 0.0, 0.0, None, None)
+                a, d, B, K, lp, vf, ent, sc, dls = la
+                _lib.check(L.xpa_colsum_finalize_batch_map(n, *args, ctypes.cast(tmap, ctypes.c_void_p), _p(sq),
+                                                           _p(self._ticket), a, d, B, K,
+                                                           _p(lp) if lp is not None else None,
+                                                           lp.shape[0] if lp is not None else 0, vf, ent,
+                                                           _p(sc) if sc is not None else None,
+                                                           _p(dls) if dls is not None else None, s),
+                           "xpa_colsum_finalize_batch_map")
+            elif loss is not None:   # one launch: the column tiles + the loss finalize block
                 a, d, B, K, lp, vf, ent, sc, dls = loss
                 _lib.check(L.xpa_colsum_finalize_batch_sq_loss(n, *args, _p(sq), _p(self._ticket), a, d, B, K, _p(lp),
                                                                lp.shape[0], vf, ent, _p(sc), _p(dls), s),
@@ -710,9 +823,14 @@ class ColsumQueue:
                            "xpa_colsum_finalize_batch_sq")
             total = sq[1 + tiles:2 + tiles]
         else:
-            for n, _keep, args, _tiles in plan:
-                _lib.check(L.xpa_colsum_finalize_batch(n, *args, s), "xpa_colsum_finalize_batch")
-        written = sum(o.numel() for _, o in self.items)
+            for n, _keep, args, _tiles, tmap in plan:
+                if tmap is not None:
+                    _lib.check(L.xpa_colsum_finalize_batch_map(n, *args, ctypes.cast(tmap, ctypes.c_void_p), None, None,
+                                                               0, 0, 0, 0, None, 0, 0.0, 0.0, None, None, s),
+                               "xpa_colsum_finalize_batch_map")
+                else:
+                    _lib.check(L.xpa_colsum_finalize_batch(n, *args, s), "xpa_colsum_finalize_batch")
+        written = sum(o.numel() for _, o, _ in self.items)
         self.items = []
         return total, written
 
