@@ -275,7 +275,7 @@ def test_colsum_finalize_batch_matches_single():
         outs.append(out)
         refs.append(ref)
     q.flush()
-    q.items = [(torch.zeros(2, 2, device=DEV), torch.zeros(2, device=DEV))]
+    q.add(torch.zeros(2, 2, device=DEV), torch.zeros(2, device=DEV))
     q.flush()                      # a second plan
     for o, r in zip(outs, refs):
         assert torch.equal(o, r)

@@ -183,7 +183,12 @@ struct HeadEpi {
     static constexpr int KH2 = (KMAX + 1) / 2;
     float wc[CPT][KMAX], acc_dw[CPT][kPk ? 1 : KMAX], acc_dbh[CPT];
     f2v acc_dw2[CPT][kPk ? KH2 : 1];
-    float acc_dbo[KMAX], acc_dls[KMAX], var_[KMAX], logsc[KMAX];
+    // the wide heads (C4) keep the Gaussian's per-output variance / log-scale in LDS (s_stats[2 ..], written by
+    // init_a): 36 registers fewer where the kernel sits at the 256-register cap of 2 blocks per CU
+    static constexpr bool kLdsVar = KMAX > 8;
+    static constexpr int kStatN = kLdsVar ? 2 + 2 * KMAX : 2;   // floats of s_stats
+    float acc_dbo[KMAX], acc_dls[KMAX], var_[kLdsVar ? 1 : KMAX], logsc[kLdsVar ? 1 : KMAX];
+    const float *s_var = nullptr;   // kLdsVar: var at s_var[o], log-scale at s_var[KMAX + o]
     float sum0, sum1, sum2, ent_const, inv_b, lo, hi, a_mean, a_inv, slope;
     float hd[KMAX];  // epilogue wave 0: the row's head outputs between the phase-1 passes and the loss
     int K, e;        // e: epilogue thread index
@@ -215,9 +220,16 @@ struct HeadEpi {
 #pragma unroll
         for (int o = 0; o < KMAX; ++o) {
             acc_dbo[o] = acc_dls[o] = 0.f;
+            hd[o] = 0.f;
+        }
+#pragma unroll
+        for (int o = 0; o < (kLdsVar ? 1 : KMAX); ++o) {
             var_[o] = 1.f;
             logsc[o] = 0.f;
-            hd[o] = 0.f;
+        }
+        if (kLdsVar && e < KMAX) {
+            s_stats[2 + e] = 1.f;
+            s_stats[2 + KMAX + e] = 0.f;
         }
 #pragma unroll
         for (int j = 0; j < CPT; ++j) {
@@ -235,9 +247,17 @@ struct HeadEpi {
 #pragma unroll
             for (int o = 0; o < KMAX; ++o) {
                 const float sc = o < K ? expf(logstd[o]) : 1.f;
-                var_[o] = sc * sc;
-                logsc[o] = logf(sc);
-                if (o < K) ent_const += kHalfLog2PiPlusHalf + logsc[o];
+                const float ls = logf(sc);
+                if constexpr (kLdsVar) {
+                    if (e == o) {
+                        s_stats[2 + o] = sc * sc;
+                        s_stats[2 + KMAX + o] = ls;
+                    }
+                } else {
+                    var_[o] = sc * sc;
+                    logsc[o] = ls;
+                }
+                if (o < K) ent_const += kHalfLog2PiPlusHalf + ls;
             }
         }
         inv_b = 1.0f / (float)batch;
@@ -247,7 +267,10 @@ struct HeadEpi {
     __device__ __forceinline__ void init_b(const float *s_stats) {
         a_mean = s_stats[0];
         a_inv = s_stats[1];
+        s_var = s_stats + 2;
     }
+    __device__ __forceinline__ float var_at(int o) const { return kLdsVar ? s_var[o] : var_[o]; }
+    __device__ __forceinline__ float logsc_at(int o) const { return kLdsVar ? s_var[KMAX + o] : logsc[o]; }
 
     __device__ __forceinline__ RowIn<KMAX> rows(int64_t tile, int64_t batch, const int64_t *__restrict__ idx,
                                                 int64_t n_rows, const float *__restrict__ act,
@@ -360,7 +383,7 @@ struct HeadEpi {
                         diff[o] = 0.f;
                         if (o < K) {
                             diff[o] = in.act[o] - hd[o];
-                            logp += -(diff[o] * diff[o]) / (2.0f * var_[o]) - logsc[o] - kLogSqrt2Pi;
+                            logp += -(diff[o] * diff[o]) / (2.0f * var_at(o)) - logsc_at(o) - kLogSqrt2Pi;
                         }
                     }
                     ent = ent_const;
@@ -407,8 +430,8 @@ struct HeadEpi {
                 for (int o = 0; o < KMAX; ++o) {
                     if (o < K) {
                         if (MODE == 0) {
-                            dh_[o] = dlogp * diff[o] / var_[o];
-                            acc_dls[o] += dlogp * (diff[o] * diff[o] / var_[o] - 1.0f);
+                            dh_[o] = dlogp * diff[o] / var_at(o);
+                            acc_dls[o] += dlogp * (diff[o] * diff[o] / var_at(o) - 1.0f);
                         } else {
                             const float ln = hd[o] - lse;
                             const float p = expf(ln);
@@ -459,10 +482,12 @@ struct HeadEpi {
             for (int o2 = 0; o2 < KH2; ++o2)
                 wc2[j][o2] = f2v{wc[j][2 * o2], 2 * o2 + 1 < KMAX ? wc[j][2 * o2 + 1] : 0.f};
         int r = r0;
-        for (; r + 4 <= nr; r += 4) {
-            float hv[CPT][4], gq[4][KP];
+        // the wide heads (C4's 17 / 18) batch 2 rows: 4 rows' d head (4 x 20 registers) beside wc / acc_dw spilled
+        constexpr int RG = KMAX > 8 ? 1 : 4;
+        for (; r + RG <= nr; r += RG) {
+            float hv[CPT][RG], gq[RG][KP];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < RG; ++u) {
 #pragma unroll
                 for (int j = 0; j < CPT; ++j) hv[j][u] = s_h[(r + u) * kS + e + NT * j];
 #pragma unroll
@@ -475,7 +500,7 @@ struct HeadEpi {
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < RG; ++u) {
 #pragma unroll
                 for (int j = 0; j < CPT; ++j) col_row(j, hv[j][u], gq[u], wc2[j], dz + (tile * kTile + r + u) * ld);
                 ballot_row(r + u, hv[0][u]);
@@ -538,7 +563,9 @@ struct HeadEpi {
                                          const float *__restrict__ W, const float *__restrict__ bias,
                                          float *__restrict__ dz, int64_t ld, float ent_coef, float vf_coef) {
         __syncthreads();
-#pragma unroll 1
+        // unrolled: with a run-time pass (NPASS = 2, the wide heads) hd[pass PH + o] is a dynamic index and the whole
+        // epilogue state went to scratch (r05: 600 B per lane, C4's actor head 196 us)
+#pragma unroll
         for (int pass = 0; pass < NPASS; ++pass) {
             if (pass > 0) __syncthreads();  // wave 0 has read the previous pass
             p1(pass, s_h, s_part, W);
@@ -631,7 +658,7 @@ __global__ __launch_bounds__(256, 2) void head_tile_kernel(XPA_HEAD_KERNEL_PARAM
     __shared__ __attribute__((aligned(16))) float s_h[kTile * kS];
     __shared__ __attribute__((aligned(16))) float s_part[kWaves][kTile][Epi::PH];
     __shared__ __attribute__((aligned(16))) float s_dh[kTile][Epi::KP];
-    __shared__ float s_stats[2];
+    __shared__ float s_stats[Epi::kStatN];
     const int t = threadIdx.x;
     const int64_t ntiles = (batch + kTile - 1) / kTile;
     if ((int64_t)blockIdx.x >= head_partials(batch)) return;  // no partial row of its own (see kGridMax)
@@ -972,8 +999,9 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
     // every chunk's ds_reads): operand stages / h tile, then the epilogue's partials, d head and stats.
     constexpr int kPartOff = kTile * kS, kDhOff = kPartOff + kWaves * kTile * Epi::PH;
     constexpr int kStatsOff = kDhOff + kTile * Epi::KP;
-    static_assert(KMAX <= 8 || (kStatsOff + 4) * 4 <= 81920, "wide heads: 2 blocks per CU");
-    constexpr int kLdsFloats = S3 == 3 && kREnd / 4 > kStatsOff + 4 ? kREnd / 4 : kStatsOff + 4;
+    constexpr int kStatsEnd = kStatsOff + (Epi::kStatN > 4 ? Epi::kStatN : 4);
+    static_assert(KMAX <= 8 || kStatsEnd * 4 <= 81920, "wide heads: 2 blocks per CU");
+    constexpr int kLdsFloats = S3 == 3 && kREnd / 4 > kStatsEnd ? kREnd / 4 : kStatsEnd;
     static_assert(kLdsFloats * 4 <= 81920, "K16R: 2 blocks per CU");
     __shared__ __attribute__((aligned(16))) float lds[kLdsFloats];
     float *smem = lds;
@@ -995,7 +1023,10 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
     const float bh0 = bh[wave * 64 + (lane & 31)], bh1 = bh[wave * 64 + 32 + (lane & 31)];
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t r0 = tile * kTile;
-        const RowIn<KMAX> in = epi.rows(tile, batch, idx, n_rows, act, old_logp, adv, ret);
+        // the rows' inputs load before the k loop (their latency hidden behind it) — for the wide heads (C4) after it:
+        // act[18] live across the k loop pushed the kernel past 256 registers (r05: 608 B of scratch per lane)
+        RowIn<KMAX> in;
+        if constexpr (KMAX <= 8) in = epi.rows(tile, batch, idx, n_rows, act, old_logp, adv, ret);
         f32x16 acc[2][2];
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
@@ -1120,6 +1151,7 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
         __syncthreads();
         if (r0 + (t >> 2) < batch) dz[(r0 + (t >> 2)) * ld + (t & 3)] = smem[(t >> 2) * kS + (t & 3)];
 #else
+        if constexpr (KMAX > 8) in = epi.rows(tile, batch, idx, n_rows, act, old_logp, adv, ret);
         epi.tile(smem, s_part, s_dh, in, tile, batch, W, bias, dz, ld, ent_coef, vf_coef);
 #endif
     }
