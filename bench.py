@@ -22,6 +22,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md; the 2:1-sparsity figure is not used)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # dense f32-input MFMA (= f32 vector rate; no xf32 on gfx950), same table
 
 
@@ -189,8 +190,8 @@ def live_gae_traffic(form, timeout_s=150):
 
 def live_gae_rocprof(args, timeout_s=300, form=None):
     """The in-loop GAE launch timed by the profiler: a child `rocprofv3 --kernel-trace` run of this bench (same
-    workload and GAE form, 2 warmup + 3 timed iterations, no side measurements); the average kernel-trace duration of
-    the 3 timed in-loop GAE launches.  Returns (avg us, [us, ...], note) or (None, None, note)."""
+    workload and GAE form, 2 warmup + 8 timed iterations, no side measurements); the average kernel-trace duration of
+    the 8 timed in-loop GAE launches (r05: 8, from 3).  Returns (avg us, [us, ...], note) or (None, None, note)."""
     import csv
     import glob
     import shutil
@@ -201,7 +202,7 @@ def live_gae_rocprof(args, timeout_s=300, form=None):
         return None, None, "rocprofv3 not found"
     tmp = tempfile.mkdtemp(prefix="xpa_kt_")
     cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--kernel-trace", "--output-format", "csv", "-d", tmp, "-o",
-           "run", "--", sys.executable, os.path.abspath(__file__), "--steps", "3", "--warmup", "2", "--gae-form",
+           "run", "--", sys.executable, os.path.abspath(__file__), "--steps", "8", "--warmup", "2", "--gae-form",
            form or args.gae_form, "--n-envs", str(args.n_envs), "--horizon", str(args.horizon), "--obs-dim", str(args.obs_dim),
            "--act-dim", str(args.act_dim), "--hidden", str(args.hidden), "--n-epoch", str(args.n_epoch),
            "--n-minibatch", str(args.n_minibatch), "--no-pmc", "--no-rocprof", "--no-cpu-baseline", "--no-sweep",
@@ -216,13 +217,13 @@ def live_gae_rocprof(args, timeout_s=300, form=None):
         return None, None, "rocprofv3 child run exited %d: %s" % (r.returncode, r.stderr[-300:])
     rows = [x for x in csv.DictReader(open(files[0])) if "gae_dpp_kernel" in x["Kernel_Name"]]
     rows.sort(key=lambda x: int(x["Start_Timestamp"]))
-    dur = [(int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e3 for x in rows[:5]]
-    if len(dur) < 5:
-        return None, None, "expected 5 in-loop GAE launches in the trace, found %d" % len(dur)
-    timed = dur[2:5]
-    return sum(timed) / 3, [round(d, 3) for d in timed], (
-        "rocprofv3 --kernel-trace of a child run of this bench (same workload, --gae-form %s; 2 warmup + 3 timed "
-        "iterations): the 3 timed in-loop GAE launches" % (form or args.gae_form))
+    dur = [(int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e3 for x in rows[:10]]
+    if len(dur) < 10:
+        return None, None, "expected 10 in-loop GAE launches in the trace, found %d" % len(dur)
+    timed = dur[2:10]
+    return sum(timed) / len(timed), [round(d, 3) for d in timed], (
+        "rocprofv3 --kernel-trace of a child run of this bench (same workload, --gae-form %s; 2 warmup + 8 timed "
+        "iterations): the 8 timed in-loop GAE launches" % (form or args.gae_form))
 
 
 def cache_flush(flush, mode):
@@ -1034,10 +1035,16 @@ def main():
                 "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(fl / heads_ms / 1e9 / FP32_MFMA_PEAK_TFLOPS, 4), "launches": ops.TIMER.count("heads"),
                 "timing": "event pairs on the launch stream in one extra iteration after the timed region"}
-            if ops.S3_GEMMS and not trunk:   # the matrix cores' own work: 6 bf16 products per f32 product
-                update_kernels["heads"].update({
-                    "bf16_mfma_flops": 6 * fl, "bf16_achieved": round(6 * fl / heads_ms / 1e9, 1),
-                    "bf16_peak": 2500.0, "bf16_frac": round(6 * fl / heads_ms / 1e9 / 2500.0, 4)})
+            if ops.S3_GEMMS and not trunk:
+                # r05: the roofline of the launches is the bf16 matrix cores they run on (6 bf16 products per f32
+                # product); the f32-equivalent rate against the fp32 MFMA peak stays beside it
+                h = update_kernels["heads"]
+                h["kernel"] = h["kernel"].replace("achieved / frac: f32-GEMM FLOP against the fp32 MFMA peak",
+                                                  "achieved / frac: the bf16 MFMA FLOP against the dense bf16 peak")
+                h["f32_equivalent"] = {"flops": fl, "achieved": h["achieved"], "peak": FP32_MFMA_PEAK_TFLOPS,
+                                       "unit": "TFLOP/s", "frac": h["frac"]}
+                h.update({"flops": 6 * fl, "achieved": round(6 * fl / heads_ms / 1e9, 1), "peak": BF16_MFMA_PEAK_TFLOPS,
+                          "frac": round(6 * fl / heads_ms / 1e9 / BF16_MFMA_PEAK_TFLOPS, 4)})
         elif heads_ms:
             hb = heads_bytes(B, args.act_dim, args.hidden)
             update_kernels["heads"] = {
@@ -1046,6 +1053,20 @@ def main():
                 "achieved": round(hb / heads_ms / 1e6, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(hb / heads_ms / 1e6 / HBM_PEAK_GBS, 4), "launches": ops.TIMER.count("heads"),
                 "timing": "event pairs on the launch stream in one extra iteration after the timed region"}
+        fmu = agent.learner._fused_mlp()
+        if ops.S3_GEMMS and phase_ms and getattr(fmu, "gemm_heads", False):
+            # r05: the update's three paired-layer products on the split (heads' forward 6 products; dX / dW 6 for the
+            # actor half and 3 for the critic half when factored) against the dense bf16 peak, and the measured update
+            fl = pair_gemm_flops(B, args.hidden, args.hidden)
+            per_bwd = 4.5 if FusedActorCritic.CRIT_FACTORED else 6.0
+            bf = (6.0 + 2 * per_bwd) * fl
+            upd_us = phase_ms["update_incl_gae"] * 1e3 / (args.n_epoch * args.n_minibatch)
+            update_kernels["update_floor"] = {
+                "what": "one minibatch update: its paired-layer products as bf16 MFMA FLOP (heads 6 products, dX / dW %s) "
+                        "at the dense bf16 peak, vs the measured update (phase events incl. the iteration's one GAE "
+                        "launch, / updates per iteration)" % ("6 actor + 3 critic" if per_bwd < 6 else "6"),
+                "bf16_mfma_gflop": round(bf / 1e9, 2), "floor_us": round(bf / BF16_MFMA_PEAK_TFLOPS / 1e6, 2),
+                "measured_us": round(upd_us, 2), "frac": round(bf / BF16_MFMA_PEAK_TFLOPS / 1e6 / upd_us, 4)}
         if gemm_ms:
             fl = pair_gemm_flops(B, args.hidden, args.hidden)
             update_kernels["gemm_pair"] = {
@@ -1062,9 +1083,12 @@ def main():
                                    "(n_epoch %d, n_minibatch %d, nets [%d] LeakyReLU)" %
                                    (N, T, args.n_epoch, args.n_minibatch, args.hidden),
                        "num_envs_per_gpu": N, "horizon": T, "global_envs": N * world, "minibatch": B,
-                       "update_gemms": ("f32 GEMMs as exact three-way bf16 splits on the bf16 matrix cores (%s heads, "
-                                        "K42S dX + trunk backward, K41V dW; error <= 2x the f32 GEMM's vs f64: tests/test_gpu_sgemm3.py)"
-                                        % {"s3p": "K16P", "s3q": "K16Q"}.get(ops.S3_HEADS, "K16S")
+                       "update_gemms": ("f32 GEMMs as exact three-way bf16 splits on the bf16 matrix cores (%s heads, %s; "
+                                        "error <= 2x the f32 GEMM's vs f64: tests/test_gpu_sgemm3.py)"
+                                        % ({"s3p": "K16P", "s3q": "K16Q"}.get(ops.S3_HEADS, "K16S"),
+                                           "K42C dX + trunk backward and K41P dW with the critic's half factored "
+                                           "(masked GEMMs, 3 products)" if FusedActorCritic.CRIT_FACTORED else
+                                           "K42S dX + trunk backward, K41V dW")
                                         if ops.S3_GEMMS else "f32 MFMA (K16 heads, hipBLASLt dX / dW)"),
                        "updates_per_step": args.n_epoch * args.n_minibatch,
                        "parallelism": ("dp1 (one env shard, no collective)" if world == 1 else

@@ -63,7 +63,7 @@ def child(v, reps=30):
     from xuanpolicy_amd import _lib, ops
     _lib.load(os.path.join(OUT, "libxpa_probe%d.so" % v))
     dev = torch.device("cuda:0")
-    B, H, K = 65536, 256, 6
+    B, H, K = 65536, 256, int(os.environ.get("XPA_PROBE_K", "6"))   # XPA_PROBE_K=17: C4's actor head
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.randn(B, H, device=dev, generator=g)
     wha, whc = (torch.randn(H, H, device=dev, generator=g) * 0.06 for _ in range(2))
@@ -116,7 +116,7 @@ def child(v, reps=30):
         res[name] = round(e0.elapsed_time(e1) / reps * 1e3, 2)
     flops = 2.0 * B * H * H
     res["gemm_floor_us_at_peak"] = round(flops / 157.3e6, 2)
-    print(json.dumps({"variant": VARIANTS[v], "form": FORM, **res}), flush=True)
+    print(json.dumps({"variant": VARIANTS[v], "form": FORM, "K": K, **res}), flush=True)
 
 
 def run():
