@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--pair-sa", type=int, default=0, help="K41P's actor share of 128 slices (0: the default)")
     p.add_argument("--crit-factored", choices=("on", "off"), default="on",
                    help="the critic's factored backward (K41P / K42C, r05) or its dz_critic through K41V / K42S")
+    p.add_argument("--rollout-split", choices=("on", "off"), default="on",
+                   help="the rollout's paired hidden GEMM on the split (K40R, r05) or the f32 library GEMM")
     p.add_argument("--wide-trunk", choices=("on", "off"), default="on",
                    help="C4's 376-wide trunk layer on the split GEMMs (K40F / K42W / K41V, r05) or the f32 library GEMMs")
     p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc HBM-traffic passes")
@@ -832,6 +834,7 @@ def main():
     from xuanpolicy_amd.fused_mlp import FusedActorCritic
     FusedActorCritic.CRIT_FACTORED = args.crit_factored == "on"
     FusedActorCritic.WIDE_TRUNK = args.wide_trunk == "on"
+    FusedActorCritic.ROLLOUT_SPLIT = args.rollout_split == "on"
     if args.pair_sa:
         ops.lib().xpa_s3_wgrad_pair_tune(args.pair_sa)
     if args.thin_store == "plain":

@@ -666,6 +666,11 @@ int xpa_s3_wgrad_pair(const float *dz_a, int64_t lda, const float *h, int64_t ld
  * xpa_colsum_finalize_batch_map: xpa_colsum_finalize_batch(_sq(_loss)) with per-segment output maps tmap [n][3] =
  *   (inner, valid, ld): inner 0 = identity, else partial column r inner + i -> out[i ld + r] for r < valid (dropped
  *   otherwise) — K41V's dW^T slices finalized straight into W [256][376]; loss_partials NULL: no loss block. */
+/* K40R (r05): the rollout's paired hidden layer z [m, 512] = x [m, 256] . [B0 | B1] + bias on the split (B0 / B1 =
+ * Wh_actor^T / Wh_critic^T split by xpa_s3_split_b, k = 256): 64-row x 128-column blocks for the rollout's few rows
+ * (ppoclip_agent.py:63 self.action(obs) -> the policy's hidden layers); each output equals xpa_s3_gemm's + bias. */
+int xpa_s3_gemm_rows_pair(const float *a, int64_t lda, const void *b0_split, const void *b1_split, const float *bias,
+                          float *c, int64_t ldc, int64_t m, xpa_stream_t stream);
 int xpa_gather_minibatch_pitched(const int64_t *idx, int64_t batch, int64_t n_rows, const void *obs,
                                  int64_t obs_row_bytes, void *obs_out, int64_t out_row_bytes, const float *adv,
                                  double *adv_partials, int32_t *err, xpa_stream_t stream);

@@ -33,7 +33,8 @@ def _obs_input(obs):
 
 
 def replay_last_step_iteration(agent, D, A, hidden, discrete, algo, ent, n_epoch, n_mb, expect_mid_truncations=False,
-                               pol=None, alias_cols=()):
+                               pol=None, alias_cols=(), report=None, loss_tol=1e-4, w_atol=1e-4,
+                               clip_tol=None):
     """pol: the oracle policy to replay with (default: the MLP actor-critic of `hidden`); it is loaded with the agent's
     weights here.  The deferred-bootstrap checks run when the agent defers them (device envs); a host VecEnv's
     per-step bootstraps are checked against the reference loop by tests/test_gpu_hostenv.py.  alias_cols: buffer
@@ -92,7 +93,7 @@ def replay_last_step_iteration(agent, D, A, hidden, discrete, algo, ent, n_epoch
     np.testing.assert_allclose(mem.advantages.cpu().numpy(), adv, rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(mem.returns.cpu().numpy(), ret, rtol=1e-5, atol=1e-5)
     replay_updates(agent, pol, opt_state, lr0, sched_epoch, perm_counter, adv, ret, discrete, A, algo, ent, n_epoch,
-                   n_mb)
+                   n_mb, report=report, loss_tol=loss_tol, w_atol=w_atol, clip_tol=clip_tol)
 
 
 def _check_deferred(agent, pol, N, T, term, closed, boot, expect_mid_truncations):
@@ -114,7 +115,7 @@ def _check_deferred(agent, pol, N, T, term, closed, boot, expect_mid_truncations
 
 
 def replay_updates(agent, pol, opt_state, lr0, sched_epoch, perm_counter, adv, ret, discrete, A, algo, ent, n_epoch,
-                   n_mb):
+                   n_mb, report=None, loss_tol=1e-4, w_atol=1e-4, clip_tol=None):
     """The oracle learner replays the agent's buffer (with adv / ret given) using the device permutations, from the
     Adam / LinearLR state the iteration's updates started from: every update's loss scalars and the final weights."""
     N, T = agent.n_envs, agent.n_steps
@@ -154,14 +155,27 @@ def replay_updates(agent, pol, opt_state, lr0, sched_epoch, perm_counter, adv, r
             info = lrn.update(o, a, r, ad, ax.get("old_logp"))
             got = agent.update_log[u].cpu().numpy()   # ops.OUT_KEYS order
             ref_loss = info["actor-loss"] - ent * info["entropy"] + cfg.vf_coef * info["critic-loss"]
-            assert abs(got[3] - ref_loss) < 1e-4, ("loss", u, got[3], ref_loss)
+            if report is not None:   # diagnostics (tools/c4_drift.py): record instead of asserting
+                report.append(("update", u, [float(got[j]) for j in range(6)],
+                               [float(info[k]) for k in ("actor-loss", "critic-loss", "entropy")] + [float(ref_loss)]))
+                u += 1
+                continue
+            # relative above 1, as its components below (C4's critic loss reaches ~35: 1e-4 absolute there is 3e-6
+            # relative, inside the two f32 paths' summation-order noise)
+            assert abs(got[3] - ref_loss) < loss_tol * max(1.0, abs(ref_loss)), ("loss", u, got[3], ref_loss)
             for j, k in enumerate(("actor-loss", "critic-loss", "entropy")):
-                assert abs(got[j] - info[k]) < 1e-4 * max(1.0, abs(info[k])), (k, u, got[j], info[k])
+                assert abs(got[j] - info[k]) < loss_tol * max(1.0, abs(info[k])), (k, u, got[j], info[k])
             assert abs(got[5] - info["predict_value"]) < 1e-4 * max(1.0, abs(info["predict_value"]))
             if algo == "ppo":
                 # rows within f32 rounding of a clip bound may land on either side (counted by the oracle)
                 tol = (2.0 + info["clip_boundary_rows"]) / B + 1e-7
+                if clip_tol is not None:   # a drifting replay (see the C4 test): rows near a bound beyond f32 rounding
+                    tol = max(tol, clip_tol)
                 assert abs(got[4] - info["clip_ratio"]) <= tol, ("clip_ratio", u, got[4], info["clip_ratio"], tol)
             u += 1
     for (k, val), ref in zip(agent.policy.state_dict().items(), pol.state_dict().values()):
-        np.testing.assert_allclose(val.detach().cpu().numpy(), ref.numpy(), rtol=1e-3, atol=1e-4, err_msg=k)
+        if report is not None:
+            a, b = val.detach().cpu().double().numpy(), ref.double().numpy()
+            report.append(("weight", k, float(np.abs(a - b).max()), float(np.abs(b).max())))
+            continue
+        np.testing.assert_allclose(val.detach().cpu().numpy(), ref.numpy(), rtol=1e-3, atol=w_atol, err_msg=k)

@@ -142,7 +142,14 @@ def test_c4_shape_iteration_matches_oracle(wide, monkeypatch):
     assert agent.defer_boot and agent.n_slots == 1 and not agent._env_fused(fm)
     agent.train(T, log=False)
     agent.train(T - 1, log=False)
-    replay_last_step_iteration(agent, D, A, [H], False, "ppo", 0.0, n_epoch, n_mb, expect_mid_truncations=True)
+    # tolerances (r05): over the iteration's 8 updates the f32 device path and the f64 oracle drift apart through Adam
+    # (near-zero gradients of the 376-wide layer normalised to +-lr steps), and the PPO actor loss is a cancellation
+    # (|mean| ~0.02 of O(1) terms): profiles/r05/c4_drift.jsonl shows the r04 library-GEMM path at 2.1e-4 on the actor
+    # loss and 2.4e-4 on weights for seed 18, the split path at 0 there and the reverse for seed 17 — 5e-4 / 5e-4 is
+    # ~2x the largest drift of the six runs (every trunk / rollout GEMM form); the drifted ratios move rows across the
+    # clip bounds (19 of 8192 at update 5 of one run), so the clip fraction is held to 5e-3 (41 rows)
+    replay_last_step_iteration(agent, D, A, [H], False, "ppo", 0.0, n_epoch, n_mb, expect_mid_truncations=True,
+                               loss_tol=5e-4, w_atol=5e-4, clip_tol=5e-3)
     assert fm._wide_on() == wide
     keys = {k[0] for k in fm._partials if isinstance(k, tuple)}
     assert (("wide_bwd" in keys) and ("wide_x" in keys)) == wide, keys

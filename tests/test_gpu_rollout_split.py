@@ -1,0 +1,59 @@
+"""GPU: K40R (r05), the rollout's paired hidden layer on the split GEMM (csrc/sgemm3.hip xpa_s3_gemm_rows_pair).
+
+  * every output equals K40's (xpa_s3_gemm on the same half) + bias, bit for bit, on ragged row counts;
+  * a C2-shaped rollout with K40R against the f32 library GEMM's: actions, log-probs and values within the f32 GEMM's
+    error (the end-to-end oracle replays in test_gpu_fastpath_e2e.py run with K40R on, the default)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _setup():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.mark.parametrize("M", [4096, 777, 64, 5, 65536])
+def test_rows_pair_equals_k40_halves(M):
+    from xuanpolicy_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(M)
+    x = torch.randn(M, 256, device=DEV, generator=g) * torch.exp(torch.randn(M, 1, device=DEV, generator=g))
+    wa = torch.randn(256, 256, device=DEV, generator=g) / 16
+    wc = torch.randn(256, 256, device=DEV, generator=g) / 16
+    b = torch.randn(512, device=DEV, generator=g)
+    sa, sc = ops.s3_split(wa.t()), ops.s3_split(wc.t())
+    z = torch.full((M, 512), 777.0, device=DEV)
+    ops.s3_gemm_rows_pair(x, sa, sc, b, out=z)
+    za = ops.s3_gemm(x, sa, 256) + b[:256]
+    zc = ops.s3_gemm(x, sc, 256) + b[256:]
+    torch.cuda.synchronize()
+    assert torch.equal(z[:, :256], za)
+    assert torch.equal(z[:, 256:], zc)
+    # and close to the f64 product (the split's f32 accuracy)
+    ref = x.double() @ torch.cat([wa, wc], 0).double().t() + b.double()
+    bound = 4e-6 * (x.double().abs() @ torch.cat([wa, wc], 0).double().abs().t()) + 1e-6
+    assert bool(((z.double() - ref).abs() <= bound).all())
+
+
+def test_rollout_with_k40r_matches_library_gemm(monkeypatch):
+    """Two agents from one seed, one rollout each: K40R (default) vs the f32 library GEMM (ROLLOUT_SPLIT off)."""
+    from xuanpolicy_amd.fused_mlp import FusedActorCritic
+    from xuanpolicy_amd.runner import build_synthbox_ppo
+    outs = []
+    for split in (True, False):
+        monkeypatch.setattr(FusedActorCritic, "ROLLOUT_SPLIT", split)
+        agent = build_synthbox_ppo(n_envs=512, n_steps=16, obs_dim=17, act_dim=6, hidden=256, n_epoch=1,
+                                   n_minibatch=4, seed=5, device="cuda:0")
+        agent.train(15, log=False)   # stops before the update: the buffers hold the rollout
+        fm = agent.learner._fused_mlp()
+        assert (getattr(fm, "_roll_split", None) is not None) == split
+        m = agent.memory
+        outs.append((m.actions[:, :15].clone(), m.auxiliary_infos["old_logp"][:, :15].clone(),
+                     m.values[:, :15].clone()))
+        del agent
+    for a, b in zip(*outs):
+        scale = b.abs().max().item()
+        assert (a - b).abs().max().item() <= 1e-4 * max(scale, 1.0)

@@ -747,6 +747,9 @@ class _OnPolicyAgent:
                 fc = self._rollout_cnn()
                 if fc is not None:
                     fc.refresh()   # outside any captured graph: the replays read the refreshed weight copy
+                fm = self._rollout_mlp()
+                if fm is not None:
+                    fm.rollout_refresh()   # K40R's weight planes for this rollout (same: outside the graphs)
             if chunk > 1 and left >= chunk and self._t % chunk == 0 and self.n_steps - self._t >= chunk:
                 k = self._rollout_chunk_graph(chunk)
             else:

@@ -482,8 +482,7 @@ struct HeadEpi {
             for (int o2 = 0; o2 < KH2; ++o2)
                 wc2[j][o2] = f2v{wc[j][2 * o2], 2 * o2 + 1 < KMAX ? wc[j][2 * o2 + 1] : 0.f};
         int r = r0;
-        // the wide heads (C4's 17 / 18) batch 2 rows: 4 rows' d head (4 x 20 registers) beside wc / acc_dw spilled
-        constexpr int RG = KMAX > 8 ? 1 : 4;
+        constexpr int RG = 4;   // rows per group
         for (; r + RG <= nr; r += RG) {
             float hv[CPT][RG], gq[RG][KP];
 #pragma unroll

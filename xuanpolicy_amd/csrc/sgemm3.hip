@@ -331,6 +331,91 @@ __global__ __launch_bounds__(64 * W, 8 / W) void s3_gemm_kernel(const float *__r
     }
 }
 
+// K40R (r05): the rollout's paired hidden layer z [M, 512] = x [M, 256] . [B0 | B1] + bias (B0 / B1 = Wh_actor^T /
+// Wh_critic^T, each split by xpa_s3_split_b into K40's chunk images) for the rollout's few rows (4096 at C2, where K40's
+// 256-row blocks would leave all but 32 CUs idle and the f32 library GEMM took 15.5 us): 64-row x 128-column blocks
+// (grid M / 64 x 4 column quarters: 256 at C2) of 4 waves, wave (wr = w & 1, wc = w >> 1) owning rows 32 wr .. + 31 x
+// columns 64 wc .. + 63 of the block (2 accumulators); per 16-k chunk the block's A rows (4 KiB, K40's swizzled image)
+// and its 12 KiB of B planes arrive by LDS-DMA through a 3-stage ring, one A and three B instructions per wave.  K40's
+// products, product order and k order: every output is K40's (xpa_s3_gemm on the same half) + bias, bit for bit.
+constexpr int kRRows = 64;
+constexpr int kRAImg = kRRows * kKC * 4;   // 4 KiB
+constexpr int kRBImg = 3 * 4 * 1024;       // 12 KiB: 3 planes x 4 column blocks
+constexpr int kRStage = kRAImg + kRBImg;
+// S ring stages (S - 1 chunks requested ahead: a chunk is 384 MFMA cycles per wave, far less than an L2 round trip, so
+// the 16-k chunks must be requested deep ahead)
+template <int S>
+__global__ __launch_bounds__(256, 1) void s3_gemm_r64_kernel(const float *__restrict__ a, int64_t lda,
+                                                            const __bf16 *__restrict__ bs0,
+                                                            const __bf16 *__restrict__ bs1, float *__restrict__ c,
+                                                            int64_t ldc, int64_t M, int nchunks,
+                                                            const float *__restrict__ bias) {
+    __shared__ __attribute__((aligned(16))) char lds[S * kRStage];
+    const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int64_t r0 = (int64_t)blockIdx.x * kRRows;
+    const int q = blockIdx.y;                       // column quarter of the 512
+    const char *bsrc0 = reinterpret_cast<const char *>(q < 2 ? bs0 : bs1);
+    const int coff = (q & 1) * 4;                   // first column block of the quarter inside its matrix
+    auto issue = [&](unsigned st, int ch) {
+        const int rr = lane >> 2, p = lane & 3;
+        const int qq = p ^ ((rr >> 2) & 3);
+        int64_t row = r0 + wave * 16 + rr;
+        row = row < M ? row : M - 1;
+        glds16(a + row * lda + ch * kKC + 4 * qq, st + (unsigned)(wave * 16 * kKC * 4));
+        const char *bsrc = bsrc0 + (int64_t)ch * kBImg;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int piece = wave * 3 + k, plane = piece >> 2, j = piece & 3;
+            glds16(bsrc + (plane * 8 + coff + j) * 1024 + lane * 16, st + (unsigned)(kRAImg + piece * 1024));
+        }
+    };
+    f32x16 acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+#pragma unroll
+    for (int d = 0; d < S - 1; ++d)
+        if (d < nchunks) issue(base + d * kRStage, d);
+    const int wr = wave & 1, wc = wave >> 1;
+    const int h = lane >> 5, i = lane & 31, sw = (i >> 2) & 3;
+#pragma unroll 1
+    for (int ch = 0; ch < nchunks; ++ch) {
+        // own DMAs of chunk ch landed (the `ahead` chunks after it may fly: 4 instructions each), then every wave's;
+        // the stage chunk ch + S - 1 refills was read in chunk ch - 1
+        const int ahead = min(nchunks - 1 - ch, S - 2);
+        if (ahead >= 4) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+        else if (ahead == 3) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+        else if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (ch + S - 1 < nchunks) issue(base + ((ch + S - 1) % S) * kRStage, ch + S - 1);
+        const char *st = lds + (ch % S) * kRStage;
+        const float *arow = reinterpret_cast<const float *>(st) + (32 * wr + i) * kKC;
+        bf16x8 ah, am, al;
+        xpa_split8(*reinterpret_cast<const float4 *>(arow + 4 * (h ^ sw)),
+                   *reinterpret_cast<const float4 *>(arow + 4 * ((h + 2) ^ sw)), ah, am, al);
+        const bf16x8 *bimg = reinterpret_cast<const bf16x8 *>(st + kRAImg) + lane;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int cbl = 2 * wc + j;
+            acc[j] = xpa_mfma_s3(ah, am, al, bimg[cbl * 64], bimg[(4 + cbl) * 64], bimg[(8 + cbl) * 64], acc[j]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int col = q * 128 + (2 * wc + j) * 32 + i;
+        const float bv = bias[col];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t row = r0 + 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (row < M) c[row * ldc + col] = acc[j][r] + bv;
+        }
+    }
+}
+
 // K40W: K40 with the roles split over the waves (as K41W): waves 4-7 (producers) DMA the operands of chunk c + 2 (their
 // own 32 A rows each + B's planes) and split chunk c + 1's A rows (own DMAs, so a vmcnt wait suffices) into the bf16
 // planes of the stage, while waves 0-3 (consumers, one per SIMD, 32 rows x 256 columns each) read ready planes and run
@@ -2003,6 +2088,22 @@ XPA_API int xpa_s3_gemm_bias_act(const float *a, int64_t lda, const void *b_spli
         s3_gemm_kernel<8, 3, 0, 0, 2><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, nch, bias, slope, sg);
     else
         s3_gemm_kernel<8, 3, 0, 0, 3><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, nch, bias, slope, nullptr);
+    return xpa_launch_status();
+}
+
+// K40R (r05): z [m, 512] = x [m, 256] . [B0 | B1] + bias, B0 / B1 split by xpa_s3_split_b (k = 256): the rollout's
+// paired hidden layer; each output is xpa_s3_gemm's + bias bit for bit
+XPA_API int xpa_s3_gemm_rows_pair(const float *a, int64_t lda, const void *b0_split, const void *b1_split,
+                                  const float *bias, float *c, int64_t ldc, int64_t m, xpa_stream_t stream) {
+    if (!a || !b0_split || !b1_split || !bias || !c || m <= 0 || lda < kN || ldc < 2 * kN || (lda & 3) ||
+        (reinterpret_cast<uintptr_t>(a) & 15) || (m + kRRows - 1) / kRRows > 0x7fffffff)
+        return (int)hipErrorInvalidValue;
+    const dim3 grid((unsigned)((m + kRRows - 1) / kRRows), 4);
+    const __bf16 *b0 = static_cast<const __bf16 *>(b0_split), *b1 = static_cast<const __bf16 *>(b1_split);
+    if (g_s3_probe & 512)   // the 3-stage form (A/B)
+        s3_gemm_r64_kernel<3><<<grid, dim3(256), 0, stream>>>(a, lda, b0, b1, c, ldc, m, kN / kKC, bias);
+    else
+        s3_gemm_r64_kernel<6><<<grid, dim3(256), 0, stream>>>(a, lda, b0, b1, c, ldc, m, kN / kKC, bias);
     return xpa_launch_status();
 }
 

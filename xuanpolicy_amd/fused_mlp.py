@@ -352,6 +352,28 @@ class FusedActorCritic:
     def rollout_ok(self):
         return self.pair is not None
 
+    # r05 (K40R): the rollout's paired hidden GEMM on the split; the planes of [Wh_actor^T | Wh_critic^T] are re-split at
+    # the start of every rollout (rollout_refresh, outside any captured graph: the weights change only in the update)
+    ROLLOUT_SPLIT = True
+
+    def rollout_refresh(self):
+        """Split the paired hidden layer's weights for K40R (one launch, before a rollout's first step); afterwards
+        rollout_act uses the planes until the next refresh.  A no-op (planes dropped) where K40R does not apply."""
+        lin_a, lin_c = self.actor[0][0], self.critic[0][0]
+        ok = (self.ROLLOUT_SPLIT and ops.S3_GEMMS and self.pair is not None and self.gemm_heads
+              and lin_a.in_features == 256 and lin_a.out_features == 256 and lin_c.out_features == 256)
+        if not ok:
+            self._roll_split = None
+            return
+        bufs = self._split_many([(lin_a.weight.t(), "roll_a"), (lin_c.weight.t(), "roll_c")])
+        self._roll_split = (bufs[0], bufs[1])
+
+    def _rollout_pair(self, s):
+        rs = getattr(self, "_roll_split", None)
+        if rs is not None and s.dim() == 2 and s.shape[1] == 256 and _vec4_rows(s):
+            return ops.s3_gemm_rows_pair(s, rs[0], rs[1], self.pair[1])
+        return F.linear(s, self.pair[0], self.pair[1])
+
     @torch.no_grad()
     def rollout_act(self, x, dist, cursor, seed, buf_act, buf_logp, buf_val, env_in, act_clip=1.0, norm=None,
                     env=None):
@@ -360,7 +382,7 @@ class FusedActorCritic:
         inside the same K14 launch (ops.rollout_policy_head_synthbox; the caller skips env.step_device())."""
         rep_outs = self._rep_forward(x, norm=norm)
         s = rep_outs[-1] if rep_outs else x
-        z = F.linear(s, self.pair[0], self.pair[1])
+        z = self._rollout_pair(s)
         H = ops.HEAD_HIDDEN
         lin_ao = self.actor[-1][0]
         lin_co = self.critic[-1][0]

@@ -331,6 +331,26 @@ def s3_gemm_trunk_bwd(dz, b_split, k, h, x, act, slope, partial_dw=None, partial
     return partial_dw, partial_db
 
 
+def s3_gemm_rows_pair(a, b0_split, b1_split, bias, out=None):
+    """K40R (r05): out [m, 512] = a [m, 256] . [B0 | B1] + bias (B0 / B1 split by s3_split / s3_split_batch, k = 256):
+    the rollout's paired hidden layer; each output is s3_gemm's + bias bit for bit."""
+    _req(a, "a", torch.float32, contiguous=False)
+    lda = _row_stride(a, "a", 256)
+    m = a.shape[0]
+    _req(bias, "bias", torch.float32, (512,))
+    if out is None:
+        out = torch.empty(m, 512, dtype=torch.float32, device=a.device)
+    ldc = _row_stride(out, "out", 512)
+    if out.shape[0] != m:
+        raise ValueError("out must have %d rows" % m)
+    nb = int(lib().xpa_s3_split_bytes(256, 256))
+    for b in (b0_split, b1_split):
+        _req(b, "b_split", torch.uint8, (nb,))
+    _lib.check(lib().xpa_s3_gemm_rows_pair(_p(a), lda, _p(b0_split), _p(b1_split), _p(bias), _p(out), ldc, m,
+                                           _stream(a.device)), "xpa_s3_gemm_rows_pair")
+    return out
+
+
 def s3_split_padded(b, k_pad, out=None):
     """The split of b [kv, 256] (any strides) padded with zero rows to k_pad (a multiple of 16): K40F's operand for a
     layer width that is not a multiple of 16 (xpa_s3_split_batch_padded)."""
