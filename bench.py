@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--pair-sa", type=int, default=0, help="K41P's actor share of 128 slices (0: the default)")
     p.add_argument("--crit-factored", choices=("on", "off"), default="on",
                    help="the critic's factored backward (K41P / K42C, r05) or its dz_critic through K41V / K42S")
+    p.add_argument("--rollout-h-store", choices=("plain", "nt"), default="nt",
+                   help="the rollout trunk's h stores: non-temporal (default) or plain (A/B; xpa_thin_probe bit 2)")
     p.add_argument("--rollout-split", choices=("on", "off"), default="on",
                    help="the rollout's paired hidden GEMM on the split (K40R, r05) or the f32 library GEMM")
     p.add_argument("--wide-trunk", choices=("on", "off"), default="on",
@@ -837,8 +839,9 @@ def main():
     FusedActorCritic.ROLLOUT_SPLIT = args.rollout_split == "on"
     if args.pair_sa:
         ops.lib().xpa_s3_wgrad_pair_tune(args.pair_sa)
-    if args.thin_store == "plain":
-        ops.lib().xpa_thin_probe(1)
+    thin_probe = (1 if args.thin_store == "plain" else 0) | (2 if args.rollout_h_store == "plain" else 0)
+    if thin_probe:
+        ops.lib().xpa_thin_probe(thin_probe)
     if args.s3_probe:
         ops.lib().xpa_s3_probe(args.s3_probe)
     rank, local, world = init_from_env()

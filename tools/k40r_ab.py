@@ -1,5 +1,5 @@
-"""A/B of the rollout's paired hidden GEMM at C2's rollout shape ([4096, 256] x [256, 512]): K40R 6-stage (default),
-K40R 3-stage (xpa_s3_probe bit 512) and the f32 library GEMM (F.linear), alternating in one process, event-timed."""
+"""A/B of the rollout's paired hidden GEMM at C2's rollout shape ([4096, 256] x [256, 512]): K40R 2 stages x 4 chunks (default),
+3 x 1 (xpa_s3_probe bit 512), 3 x 2 (bit 1024) and the f32 library GEMM (F.linear), alternating in one process, event-timed."""
 import json
 import os
 import sys
@@ -32,12 +32,11 @@ def main():
         torch.cuda.synchronize()
         return round(e0.elapsed_time(e1) * 1e3 / reps, 2)
 
-    res = {"k40r_s6": [], "k40r_s3": [], "f_linear": []}
+    res = {"k40r_2x4": [], "k40r_3x1": [], "k40r_3x2": [], "f_linear": []}
     for _ in range(5):
-        L.xpa_s3_probe(0)
-        res["k40r_s6"].append(t(lambda: ops.s3_gemm_rows_pair(x, sa, sc, b, out=out)))
-        L.xpa_s3_probe(512)
-        res["k40r_s3"].append(t(lambda: ops.s3_gemm_rows_pair(x, sa, sc, b, out=out)))
+        for name, pr in (("k40r_2x4", 0), ("k40r_3x1", 512), ("k40r_3x2", 1024)):
+            L.xpa_s3_probe(pr)
+            res[name].append(t(lambda: ops.s3_gemm_rows_pair(x, sa, sc, b, out=out)))
         L.xpa_s3_probe(0)
         res["f_linear"].append(t(lambda: F.linear(x, w, b)))
     print(json.dumps({"M": M, **res}))

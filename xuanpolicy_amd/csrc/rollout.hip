@@ -440,6 +440,16 @@ constexpr int kRolloutKMax = 32;  // head width limit of K14 (lanes < K draw the
 // ENV (Gaussian only): the SynthBox env step of the same env fused after the sample — pre = [W | U] (s | clip(a))
 // from the state row and the lanes' clipped actions (fixed k order), then K7's body: no env GEMM and no K7
 // launch.  Needs D <= 64 (one state dim per lane).
+// r05: with n_envs % 64 == 0, K14E's block b (on XCD b % 8) takes the 8-env granule G = 8 (m >> 1) + (b & 7), m = b >> 3,
+// half m & 1: granule G lies on XCD G % 8 — where the rollout trunk's 8-row tile G was written (thin_fwd_norm: block = tile)
+// and K40R's XCD-mapped row tiles read and write it — so the z rows and the next step's observation rows stay in one
+// XCD's L2 from producer to consumer.  Any env order gives the same per-env results.
+__device__ __forceinline__ int64_t xcd_env(int64_t b, int wave, int64_t n_envs) {
+    if ((n_envs & 63) != 0) return b * 4 + wave;
+    const int64_t m = b >> 3, G = 8 * (m >> 1) + (b & 7);
+    return 8 * G + 4 * (m & 1) + wave;
+}
+
 template <int MODE, int ACT, bool ENV = false>
 __global__ __launch_bounds__(256) void rollout_policy_head_kernel(
     int64_t n_envs, int K, int64_t T, const float *__restrict__ za, const float *__restrict__ zc, int64_t ld,
@@ -450,7 +460,7 @@ __global__ __launch_bounds__(256) void rollout_policy_head_kernel(
     SynthEnvArgs env) {
     __shared__ float s_head[4][kRolloutKMax];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t n = (int64_t)blockIdx.x * 4 + wave;
+    const int64_t n = ENV ? xcd_env(blockIdx.x, wave, n_envs) : (int64_t)blockIdx.x * 4 + wave;
     if (n >= n_envs) return;  // wave-uniform
     // ENV: the env's state row, counters and the first kPreW rows of [W | U]^T are loaded first, so their
     // latency hides under the head arithmetic

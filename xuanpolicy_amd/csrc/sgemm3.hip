@@ -342,33 +342,49 @@ constexpr int kRRows = 64;
 constexpr int kRAImg = kRRows * kKC * 4;   // 4 KiB
 constexpr int kRBImg = 3 * 4 * 1024;       // 12 KiB: 3 planes x 4 column blocks
 constexpr int kRStage = kRAImg + kRBImg;
-// S ring stages (S - 1 chunks requested ahead: a chunk is 384 MFMA cycles per wave, far less than an L2 round trip, so
-// the 16-k chunks must be requested deep ahead)
-template <int S>
+// S ring stages of CPS 16-k chunks each (S - 1 stages requested ahead): one barrier per stage.  A chunk is only 384
+// MFMA cycles per wave here (12 MFMAs), far less than an L2 round trip + a barrier, so several chunks ride one stage.
+template <int S, int CPS>
 __global__ __launch_bounds__(256, 1) void s3_gemm_r64_kernel(const float *__restrict__ a, int64_t lda,
                                                             const __bf16 *__restrict__ bs0,
                                                             const __bf16 *__restrict__ bs1, float *__restrict__ c,
                                                             int64_t ldc, int64_t M, int nchunks,
                                                             const float *__restrict__ bias) {
-    __shared__ __attribute__((aligned(16))) char lds[S * kRStage];
+    constexpr int kSt = CPS * kRStage;
+    __shared__ __attribute__((aligned(16))) char lds[S * kSt];
     const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int64_t r0 = (int64_t)blockIdx.x * kRRows;
+    // XCD-aware rows (r05, M % 512 == 0): block bx (on XCD bx % 8, as gridDim.x is a multiple of 8) takes the 8-row
+    // groups t = x + 8 (8 k + g), x = bx & 7, k = bx >> 3, g < 8 — the trunk launch wrote group t on XCD t % 8 = x, and
+    // K14E reads it there (xcd_env); image row R = 8 g + j holds global row 8 t + j
+    const bool xr = (M & 511) == 0;
+    auto grow = [&](int R) -> int64_t {
+        if (!xr) return r0 + R;
+        const int64_t t = (int64_t)(blockIdx.x & 7) + 8 * (8 * (int64_t)(blockIdx.x >> 3) + (R >> 3));
+        return 8 * t + (R & 7);
+    };
     const int q = blockIdx.y;                       // column quarter of the 512
     const char *bsrc0 = reinterpret_cast<const char *>(q < 2 ? bs0 : bs1);
     const int coff = (q & 1) * 4;                   // first column block of the quarter inside its matrix
-    auto issue = [&](unsigned st, int ch) {
-        const int rr = lane >> 2, p = lane & 3;
-        const int qq = p ^ ((rr >> 2) & 3);
-        int64_t row = r0 + wave * 16 + rr;
-        row = row < M ? row : M - 1;
-        glds16(a + row * lda + ch * kKC + 4 * qq, st + (unsigned)(wave * 16 * kKC * 4));
-        const char *bsrc = bsrc0 + (int64_t)ch * kBImg;
+    const int nst = nchunks / CPS;                  // the caller checks nchunks % CPS == 0
+    auto issue = [&](unsigned st, int stage) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int piece = wave * 3 + k, plane = piece >> 2, j = piece & 3;
-            glds16(bsrc + (plane * 8 + coff + j) * 1024 + lane * 16, st + (unsigned)(kRAImg + piece * 1024));
+        for (int u = 0; u < CPS; ++u) {
+            const int ch = stage * CPS + u;
+            const unsigned sc = st + (unsigned)(u * kRStage);
+            const int rr = lane >> 2, p = lane & 3;
+            const int qq = p ^ ((rr >> 2) & 3);
+            int64_t row = grow(wave * 16 + rr);
+            row = row < M ? row : M - 1;
+            glds16(a + row * lda + ch * kKC + 4 * qq, sc + (unsigned)(wave * 16 * kKC * 4));
+            const char *bsrc = bsrc0 + (int64_t)ch * kBImg;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const int piece = wave * 3 + k, plane = piece >> 2, j = piece & 3;
+                glds16(bsrc + (plane * 8 + coff + j) * 1024 + lane * 16, sc + (unsigned)(kRAImg + piece * 1024));
+            }
         }
     };
     f32x16 acc[2];
@@ -378,30 +394,32 @@ __global__ __launch_bounds__(256, 1) void s3_gemm_r64_kernel(const float *__rest
         for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 #pragma unroll
     for (int d = 0; d < S - 1; ++d)
-        if (d < nchunks) issue(base + d * kRStage, d);
+        if (d < nst) issue(base + d * kSt, d);
     const int wr = wave & 1, wc = wave >> 1;
     const int h = lane >> 5, i = lane & 31, sw = (i >> 2) & 3;
+    constexpr int kPerSt = 4 * CPS;   // DMA instructions per wave and stage
 #pragma unroll 1
-    for (int ch = 0; ch < nchunks; ++ch) {
-        // own DMAs of chunk ch landed (the `ahead` chunks after it may fly: 4 instructions each), then every wave's;
-        // the stage chunk ch + S - 1 refills was read in chunk ch - 1
-        const int ahead = min(nchunks - 1 - ch, S - 2);
-        if (ahead >= 4) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
-        else if (ahead == 3) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
-        else if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    for (int sg = 0; sg < nst; ++sg) {
+        // own DMAs of stage sg landed (the `ahead` stages after it may fly), then every wave's; the slot stage
+        // sg + S - 1 refills was read in stage sg - 1
+        const int ahead = min(nst - 1 - sg, S - 2);
+        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * kPerSt) : "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(kPerSt) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        if (ch + S - 1 < nchunks) issue(base + ((ch + S - 1) % S) * kRStage, ch + S - 1);
-        const char *st = lds + (ch % S) * kRStage;
-        const float *arow = reinterpret_cast<const float *>(st) + (32 * wr + i) * kKC;
-        bf16x8 ah, am, al;
-        xpa_split8(*reinterpret_cast<const float4 *>(arow + 4 * (h ^ sw)),
-                   *reinterpret_cast<const float4 *>(arow + 4 * ((h + 2) ^ sw)), ah, am, al);
-        const bf16x8 *bimg = reinterpret_cast<const bf16x8 *>(st + kRAImg) + lane;
+        if (sg + S - 1 < nst) issue(base + ((sg + S - 1) % S) * kSt, sg + S - 1);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int cbl = 2 * wc + j;
-            acc[j] = xpa_mfma_s3(ah, am, al, bimg[cbl * 64], bimg[(4 + cbl) * 64], bimg[(8 + cbl) * 64], acc[j]);
+        for (int u = 0; u < CPS; ++u) {
+            const char *st = lds + (sg % S) * kSt + u * kRStage;
+            const float *arow = reinterpret_cast<const float *>(st) + (32 * wr + i) * kKC;
+            bf16x8 ah, am, al;
+            xpa_split8(*reinterpret_cast<const float4 *>(arow + 4 * (h ^ sw)),
+                       *reinterpret_cast<const float4 *>(arow + 4 * ((h + 2) ^ sw)), ah, am, al);
+            const bf16x8 *bimg = reinterpret_cast<const bf16x8 *>(st + kRAImg) + lane;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int cbl = 2 * wc + j;
+                acc[j] = xpa_mfma_s3(ah, am, al, bimg[cbl * 64], bimg[(4 + cbl) * 64], bimg[(8 + cbl) * 64], acc[j]);
+            }
         }
     }
 #pragma unroll
@@ -410,7 +428,7 @@ __global__ __launch_bounds__(256, 1) void s3_gemm_r64_kernel(const float *__rest
         const float bv = bias[col];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int64_t row = r0 + 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int64_t row = grow(32 * wr + (r & 3) + 8 * (r >> 2) + 4 * h);
             if (row < M) c[row * ldc + col] = acc[j][r] + bv;
         }
     }
@@ -2100,10 +2118,13 @@ XPA_API int xpa_s3_gemm_rows_pair(const float *a, int64_t lda, const void *b0_sp
         return (int)hipErrorInvalidValue;
     const dim3 grid((unsigned)((m + kRRows - 1) / kRRows), 4);
     const __bf16 *b0 = static_cast<const __bf16 *>(b0_split), *b1 = static_cast<const __bf16 *>(b1_split);
-    if (g_s3_probe & 512)   // the 3-stage form (A/B)
-        s3_gemm_r64_kernel<3><<<grid, dim3(256), 0, stream>>>(a, lda, b0, b1, c, ldc, m, kN / kKC, bias);
+    // forms (xpa_s3_probe, A/B): default 2 stages x 4 chunks; 512: 3 x 1 (a barrier per chunk); 1024: 3 x 2
+    if (g_s3_probe & 512)
+        s3_gemm_r64_kernel<3, 1><<<grid, dim3(256), 0, stream>>>(a, lda, b0, b1, c, ldc, m, kN / kKC, bias);
+    else if (g_s3_probe & 1024)
+        s3_gemm_r64_kernel<3, 2><<<grid, dim3(256), 0, stream>>>(a, lda, b0, b1, c, ldc, m, kN / kKC, bias);
     else
-        s3_gemm_r64_kernel<6><<<grid, dim3(256), 0, stream>>>(a, lda, b0, b1, c, ldc, m, kN / kKC, bias);
+        s3_gemm_r64_kernel<2, 4><<<grid, dim3(256), 0, stream>>>(a, lda, b0, b1, c, ldc, m, kN / kKC, bias);
     return xpa_launch_status();
 }
 

@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void thin_fwd_norm_kernel(const float *__restr
                                                             const float *__restrict__ var, float clip,
                                                             float *__restrict__ xn, int64_t ldn,
                                                             float *__restrict__ col, int64_t col_ld,
-                                                            const xpa_cursor_t *__restrict__ cursor) {
+                                                            const xpa_cursor_t *__restrict__ cursor, int h_nt) {
     constexpr int TILE = 8;
     constexpr int kPad = DMAX + 4;
     __shared__ __attribute__((aligned(16))) float s_x[TILE * kPad];
@@ -233,7 +233,11 @@ __global__ __launch_bounds__(256) void thin_fwd_norm_kernel(const float *__restr
                 acc = fmaf(xv.z, w[k + 2], acc);
                 acc = fmaf(xv.w, w[k + 3], acc);
             }
-            __builtin_nontemporal_store(act_f<ACT>(acc + bc, slope), h + (r0 + r) * ldh + t);
+            // non-temporal by default; xpa_thin_probe bit 2 (r05 A/B): plain stores, so the paired hidden GEMM (K40R,
+            // XCD-mapped rows) might read h from L2 — measured no faster (profiles/r05/r05r2_*: 5.77 vs 5.61 ms rollout)
+            const float hv = act_f<ACT>(acc + bc, slope);
+            if (h_nt) __builtin_nontemporal_store(hv, h + (r0 + r) * ldh + t);
+            else h[(r0 + r) * ldh + t] = hv;
         }
     }
 }
@@ -431,7 +435,7 @@ XPA_API int xpa_thin_linear_act_fwd_norm(int act, const float *x, int64_t ldx, i
     const int dm = dmax_for((int)d_in);
 #define XPA_FWDN(A_, D_)                                                                                            \
     hipLaunchKernelGGL((thin_fwd_norm_kernel<A_, D_>), grid, dim3(256), 0, s, x, ldx, rows, (int)d_in, w, b, slope, h, \
-                       ldh, mean, var, clip, xn, ldn, col, col_ld, cursor)
+                       ldh, mean, var, clip, xn, ldn, col, col_ld, cursor, (g_thin_probe & 2) != 0 ? 0 : 1)
 #define XPA_FWDN_D(A_)              \
     if (dm == 8) XPA_FWDN(A_, 8);   \
     else if (dm == 20) XPA_FWDN(A_, 20); \
