@@ -666,6 +666,19 @@ int xpa_s3_wgrad_pair(const float *dz_a, int64_t lda, const float *h, int64_t ld
  * xpa_colsum_finalize_batch_map: xpa_colsum_finalize_batch(_sq(_loss)) with per-segment output maps tmap [n][3] =
  *   (inner, valid, ld): inner 0 = identity, else partial column r inner + i -> out[i ld + r] for r < valid (dropped
  *   otherwise) — K41V's dW^T slices finalized straight into W [256][376]; loss_partials NULL: no loss block. */
+/* r05: xpa_rollout_post_deferred_norm with the NEXT step's obs_rms.update folded in (ppoclip_agent.py:62-63: the
+ * reference updates obs_rms with each observation before acting on it): rms_x [n_envs, obs_dim] (row stride rms_ld) =
+ * the observation the env step just produced; rms_part f64 [2 * xpa_rollout_post_num_blocks(n_envs), obs_dim];
+ * obs_mean / obs_var / obs_count updated in place by the last block after every block normalised with the old
+ * statistics.  obs_dim <= 64.  The next step then normalises without an rms launch of its own. */
+int xpa_rollout_post_deferred_norm_rms(
+    int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term, const uint8_t *trunc, const float *final_obs,
+    int64_t ld_final, const float *slot_src, int64_t ld_slot, int64_t obs_dim, float *obs_mean, float *obs_var,
+    double *obs_count, float obs_clip, float *boot_norm, int64_t ld_norm, float *slot_obs, int32_t *slot_t,
+    int64_t n_slots, int32_t *overflow, xpa_cursor_t *cursor, float *ret_mean, float *ret_var, double *ret_count,
+    float *returns, float *buf_rew, float *buf_term, uint8_t *buf_closed, float *buf_boot, float gamma,
+    int mask_returns, int use_rewnorm, float rew_range, int atari_lifeloss, double *partials, uint32_t *ticket,
+    const float *rms_x, int64_t rms_ld, double *rms_part, xpa_stream_t stream);
 /* K40R (r05): the rollout's paired hidden layer z [m, 512] = x [m, 256] . [B0 | B1] + bias on the split (B0 / B1 =
  * Wh_actor^T / Wh_critic^T split by xpa_s3_split_b, k = 256): 64-row x 128-column blocks for the rollout's few rows
  * (ppoclip_agent.py:63 self.action(obs) -> the policy's hidden layers); each output equals xpa_s3_gemm's + bias. */

@@ -57,3 +57,29 @@ def test_rollout_with_k40r_matches_library_gemm(monkeypatch):
     for a, b in zip(*outs):
         scale = b.abs().max().item()
         assert (a - b).abs().max().item() <= 1e-4 * max(scale, 1.0)
+
+
+def test_fold_rms_matches_standalone_update(monkeypatch):
+    """r05: the next step's obs_rms.update folded into K8 (xpa_rollout_post_deferred_norm_rms) against the standalone
+    per-step update (xpa_rms_update): the running statistics and the stored normalised observations after a rollout
+    and a half (the fold's block partials sum the same rows in another fixed order: f64 rounding only)."""
+    import xuanpolicy_amd.agents as ag
+    from xuanpolicy_amd.runner import build_synthbox_ppo
+    outs = []
+    for fold in (True, False):
+        monkeypatch.setattr(ag, "FOLD_RMS", fold)
+        agent = build_synthbox_ppo(n_envs=1000, n_steps=16, obs_dim=17, act_dim=6, hidden=256, n_epoch=1,
+                                   n_minibatch=4, seed=9, device="cuda:0", max_episode_steps=7)
+        assert agent._rms_fold_ok() == fold
+        agent.train(16 + 7, log=False)   # one rollout + update, then 7 steps of the next
+        stored = (agent.memory.observations[:, :7].clone(), agent.memory.values[:, :7].clone())
+        if not fold:   # the fold has merged the observation the last step produced already; the standalone path
+            agent._rms_update(agent.envs.obs)   # merges it at the next step: catch up before comparing
+        torch.cuda.synchronize()
+        outs.append((agent.obs_mean.clone(), agent.obs_var.clone(), agent.obs_count.clone()) + stored)
+        del agent
+    (m1, v1, c1, o1, val1), (m0, v0, c0, o0, val0) = outs
+    assert torch.equal(c1, c0)
+    assert torch.allclose(m1, m0, rtol=1e-6, atol=1e-7) and torch.allclose(v1, v0, rtol=1e-6, atol=1e-7)
+    assert torch.allclose(o1, o0, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(val1, val0, rtol=1e-4, atol=1e-5)

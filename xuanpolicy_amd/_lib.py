@@ -248,6 +248,11 @@ SIGNATURES = {
                                                  c_p]),
     "xpa_s3_gemm_trunk_bwd_crit": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64,
                                                   c_i64, ctypes.c_int, c_f32, c_p, c_p, c_p]),
+    "xpa_rollout_post_deferred_norm_rms": (ctypes.c_int, [c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i64,
+                                                          c_p, c_p, c_p, c_f32, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p,
+                                                          c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, ctypes.c_int,
+                                                          ctypes.c_int, c_f32, ctypes.c_int, c_p, c_p, c_p, c_i64, c_p,
+                                                          c_p]),
     "xpa_s3_gemm_rows_pair": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p]),
     "xpa_s3_split_batch_padded": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "xpa_s3_gemm_bias_act": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_p, ctypes.c_int, c_f32, c_p,

@@ -47,6 +47,12 @@ def _cfg(config, name, default):
     return getattr(config, name, default)
 
 
+# r05: fold the next step's obs_rms.update into K8 on the device-env path (xpa_rollout_post_deferred_norm_rms).
+# Measured neutral at C2 (profiles/r05/r05fold: rollout 5.70 / 5.68 ms on vs 5.68 / 5.69 off — the merge chain moves
+# into K8, 6.5 + 7.7 -> 15.0 us), so it is an opt-in (bench.py --fold-rms on); off keeps the reference's update order
+# exactly, also around test() calls (which update obs_rms with the test observations, ppoclip_agent.py:125)
+FOLD_RMS = False
+
 class _OnPolicyAgent:
     algo = "ppo"
 
@@ -117,6 +123,12 @@ class _OnPolicyAgent:
         self.fuse_env_step = True   # device SynthBox env stepped inside K14 when possible (_env_fused)
         self.fuse_value_gae = True  # deferred bootstraps' value head inside the GAE scan (xpa_gae_scan_value)
         self.fuse_gather = True     # minibatch gather + adv moments inside the update's K13 (fused_mlp.Rows)
+        # r05: the next step's obs_rms.update folded into K8 (xpa_rollout_post_deferred_norm_rms) on the device-env
+        # path; _rms_pending: the current observation's statistics are not merged yet (the first step, or after
+        # anything but a folded step produced env.obs), so that step runs the standalone update first
+        self.fold_rms = FOLD_RMS
+        self._rms_pending = True
+        self._rms_fold_part = None
         # K32: whole device env steps (RMS, normalise, forward, sample, env, post) in one launch (_small_rollout)
         self.fused_rollout = bool(_cfg(config, "fused_rollout", True))
         self._k32 = self._k32_key = None
@@ -286,8 +298,15 @@ class _OnPolicyAgent:
             return
         if self.defer_boot:
             # final-obs normalisation folded into K8: kept truncation rows and, at the last step, every env's
-            # normalised final observation (boot_obs) — no separate normalise launch per step
+            # normalised final observation (boot_obs) — no separate normalise launch per step; with fold_rms also the
+            # next step's obs_rms.update (its statistics then merged once this step's normalisations are done)
             mem = self.memory
+            rms = None
+            if self._rms_fold_ok():
+                if self._rms_fold_part is None:
+                    self._rms_fold_part = torch.empty((2 * int(ops.lib().xpa_rollout_post_num_blocks(self.n_envs)),
+                                                       self.obs_dim), dtype=torch.float64, device=self.device)
+                rms = (self.envs.obs, self.obs_count, self._rms_fold_part)
             ops.rollout_post(rew, term, trunc, None, self.cursor, self.ret_mean, self.ret_var, self.ret_count,
                              self.returns, mem.rewards, mem.terminals, mem.closed, mem.boot, self.gamma,
                              mask_returns=(self.algo == "ppo"), use_rewnorm=self.use_rewnorm,
@@ -295,7 +314,7 @@ class _OnPolicyAgent:
                              deferred=(final_obs, self.slot_obs, self.slot_t, self.slot_overflow, self.obs_mean,
                                        self.obs_var, self._obs_clip(), self.boot_obs)
                              + ((self.envs.obs,) if self.boot_from_reset else ()),
-                             workspace=self.post_ws)
+                             workspace=self.post_ws, rms=rms)
             return
         self._normalize_into(final_obs, self.boot_obs, False)
         v_boot = self._boot_values(self.boot_obs)
@@ -321,6 +340,12 @@ class _OnPolicyAgent:
                          mask_returns=(self.algo == "ppo"), use_rewnorm=self.use_rewnorm,
                          rew_range=self.rewnorm_range, atari_lifeloss=self.atari, workspace=self.post_ws,
                          v_boot_mid=v_mid.contiguous() if v_mid is not None else None)
+
+    def _rms_fold_ok(self):
+        """The next step's obs_rms.update rides in K8 (device env, per-rank statistics, deferred bootstraps, D <= 64)."""
+        return (self.fold_rms and self.device_env and self.use_obsnorm and not self.sync_obs_rms and self.defer_boot
+                and not self.raw_obs and self.obs_dim <= 64 and self.envs.obs.dim() == 2
+                and self.envs.obs.stride(1) == 1)
 
     def _rms_update(self, x):
         if self.sync_obs_rms:
@@ -408,8 +433,9 @@ class _OnPolicyAgent:
             ops.store_column(x, self.memory.observations, self.cursor)
             self._policy_in = x
         else:
-            if self.use_obsnorm:
+            if self.use_obsnorm and (self._rms_pending or not self._rms_fold_ok()):
                 self._rms_update(x)
+                self._rms_pending = False
             fm = self._rollout_mlp()
             if fm is not None and fm.thin0 and x.stride(1) == 1:
                 fuse = self._env_fused(fm)

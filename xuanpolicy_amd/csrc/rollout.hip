@@ -653,7 +653,13 @@ __device__ __forceinline__ void ret_rms_merge(double c, double s1, double s2, fl
     }
 }
 
-template <bool DEFER, bool NORM = false>
+// RMS (r05): the NEXT step's obs_rms.update folded in — each block also sums (x - mean) and its square over its envs'
+// rows of the observation the env step just produced (f64; the block's 4 waves' sums in order), in
+// rms_partials_kernel's partial layout, and the last block runs rms_merge_body after the ret_rms merge.  The next
+// step then normalises with the merged statistics and needs no rms launch of its own (the reference updates obs_rms with
+// the observation before acting on it: ppoclip_agent.py:62-63, statistic_tools.py:86-112).  obs_dim <= 64.
+constexpr int kPostRmsMax = 64;
+template <bool DEFER, bool NORM = false, bool RMS = false>
 __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
     int64_t n_envs, int64_t T, const float *__restrict__ rew, const uint8_t *__restrict__ term,
     const uint8_t *__restrict__ trunc, const float *__restrict__ v_boot, xpa_cursor_t *__restrict__ cur,
@@ -666,7 +672,9 @@ __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
     unsigned int *__restrict__ ticket, const float *__restrict__ obs_mean = nullptr,
     const float *__restrict__ obs_var = nullptr, float obs_clip = 0.f, float *__restrict__ boot_norm = nullptr,
     int64_t ld_norm = 0, const float *__restrict__ slot_src = nullptr, int64_t ld_slot = 0,
-    const float *__restrict__ v_boot_mid = nullptr) {
+    const float *__restrict__ v_boot_mid = nullptr, const float *__restrict__ rms_x = nullptr, int64_t rms_ld = 0,
+    int rms_dim = 0, double *__restrict__ rms_part = nullptr, float *rms_mean = nullptr,
+    float *__restrict__ rms_var = nullptr, double *__restrict__ rms_count = nullptr) {
     __shared__ double s_red[kPostThreads / 64];
     __shared__ bool s_last;
     const int32_t t = cur->ptr;
@@ -681,9 +689,54 @@ __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
                               slot_t, n_slots, overflow, obs_mean, obs_var, obs_clip, boot_norm, ld_norm, cnt, sum,
                               sumsq, slot_src, ld_slot);
     constexpr int nw = kPostThreads / 64;
+    if constexpr (RMS) {   // this block's partial of the next observation's moments around the running mean
+        // 16 columns at a time: the block's rows staged in LDS, then thread (g, j) sums rows g, g + 16, ... of column j
+        // in f64 (x - mean exact in f64) and the 16 row groups are added in order
+        __shared__ float s_x[kPostThreads][17];
+        __shared__ double s_p[16][16], s_q[16][16];
+        const int j = threadIdx.x & 15, g = threadIdx.x >> 4;
+        for (int c0 = 0; c0 < rms_dim; c0 += 16) {
+            const int nc = rms_dim - c0 < 16 ? rms_dim - c0 : 16;
+            const int64_t nr = n < n_envs ? n : 0;
+            float v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = rms_x[nr * rms_ld + c0 + (u < nc ? u : 0)];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) s_x[threadIdx.x][u] = v[u];
+            __syncthreads();
+            double sp = 0.0, sq = 0.0;
+            if (j < nc) {
+                const double mu = (double)rms_mean[c0 + j];
+                for (int r = g; r < kPostThreads; r += 16) {
+                    if ((int64_t)blockIdx.x * kPostThreads + r >= n_envs) break;
+                    const double d = (double)s_x[r][j] - mu;
+                    sp += d;
+                    sq += d * d;
+                }
+            }
+            s_p[g][j] = sp;
+            s_q[g][j] = sq;
+            __syncthreads();
+            if ((int)threadIdx.x < nc) {
+                double a = s_p[0][threadIdx.x], b = s_q[0][threadIdx.x];
+#pragma unroll
+                for (int w = 1; w < 16; ++w) {
+                    a += s_p[w][threadIdx.x];
+                    b += s_q[w][threadIdx.x];
+                }
+                xpa_store_agent(rms_part + (int64_t)blockIdx.x * rms_dim + c0 + threadIdx.x, a);
+                xpa_store_agent(rms_part + ((int64_t)gridDim.x + blockIdx.x) * rms_dim + c0 + threadIdx.x, b);
+            }
+            __syncthreads();   // s_x / s_p reused by the next 16 columns
+        }
+    }
     cnt = xpa_block_sum(cnt, s_red, nw);
     sum = xpa_block_sum(sum, s_red, nw);
     sumsq = xpa_block_sum(sumsq, s_red, nw);
+    if (RMS) {
+        xpa_drain();        // every thread's rms partial stores complete before thread 0's ticket
+        __syncthreads();
+    }
     if (threadIdx.x == 0) {  // sc1 stores, drained before the ticket (no L2 write-back fence)
         xpa_store_agent(partials + 3 * blockIdx.x, cnt);
         xpa_store_agent(partials + 3 * blockIdx.x + 1, sum);
@@ -693,6 +746,10 @@ __global__ __launch_bounds__(kPostThreads) void rollout_post_kernel(
     }
     __syncthreads();
     if (!s_last) return;
+    if constexpr (RMS) {   // the next observation's obs_rms merge (all of the last block's threads), then ret_rms
+        rms_merge_body(rms_part, gridDim.x, n_envs, rms_dim, rms_mean, rms_var, rms_count);
+        __syncthreads();
+    }
     // all of the last block's threads load the partials at once (one round trip), thread 0 sums them in
     // block order (deterministic)
     __shared__ double s_pp[3 * 1024];
@@ -1266,6 +1323,35 @@ XPA_API int xpa_rollout_post_deferred_norm(int64_t n_envs, int64_t horizon, cons
                        buf_closed, buf_boot, gamma, mask_returns, use_rewnorm, rew_range, atari_lifeloss, final_obs,
                        ld_final, obs_dim, slot_obs, slot_t, (int)n_slots, overflow, partials, (unsigned *)ticket,
                        obs_mean, obs_var, obs_clip, boot_norm, ld_norm, slot_src, ld_slot);
+    return xpa_launch_status();
+}
+
+// r05: xpa_rollout_post_deferred_norm with the NEXT step's obs_rms.update folded in (rms_x [n_envs, rms_dim], row
+// stride rms_ld: the observation the env step just produced; rms_part f64 [2 * xpa_rollout_post_num_blocks(n_envs),
+// rms_dim]; obs_mean / obs_var / obs_count updated in place by the last block, after every block normalised with the
+// old statistics).  obs_dim <= 64.
+XPA_API int xpa_rollout_post_deferred_norm_rms(
+    int64_t n_envs, int64_t horizon, const float *rew, const uint8_t *term, const uint8_t *trunc, const float *final_obs,
+    int64_t ld_final, const float *slot_src, int64_t ld_slot, int64_t obs_dim, float *obs_mean, float *obs_var,
+    double *obs_count, float obs_clip, float *boot_norm, int64_t ld_norm, float *slot_obs, int32_t *slot_t,
+    int64_t n_slots, int32_t *overflow, xpa_cursor_t *cursor, float *ret_mean, float *ret_var, double *ret_count,
+    float *returns, float *buf_rew, float *buf_term, uint8_t *buf_closed, float *buf_boot, float gamma,
+    int mask_returns, int use_rewnorm, float rew_range, int atari_lifeloss, double *partials, uint32_t *ticket,
+    const float *rms_x, int64_t rms_ld, double *rms_part, xpa_stream_t stream) {
+    if (n_envs <= 0 || horizon <= 0 || obs_dim <= 0 || obs_dim > kPostRmsMax || ld_final < obs_dim ||
+        ld_norm < obs_dim || n_slots < 1 || n_slots > horizon || (slot_src && ld_slot < obs_dim) || !rew || !term ||
+        !trunc || !final_obs || !obs_mean || !obs_var || !obs_count || !boot_norm || !slot_obs || !slot_t ||
+        !overflow || !cursor || !ret_mean || !ret_var || !ret_count || !returns || !buf_rew || !buf_term ||
+        !buf_closed || !buf_boot || !partials || !ticket || !rms_x || rms_ld < obs_dim || !rms_part ||
+        xpa_rollout_post_num_blocks(n_envs) > 0x7fffffff)
+        return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((rollout_post_kernel<true, true, true>), dim3((unsigned)xpa_rollout_post_num_blocks(n_envs)),
+                       dim3(kPostThreads), 0, (hipStream_t)stream, n_envs, horizon, rew, term, trunc,
+                       (const float *)nullptr, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term,
+                       buf_closed, buf_boot, gamma, mask_returns, use_rewnorm, rew_range, atari_lifeloss, final_obs,
+                       ld_final, obs_dim, slot_obs, slot_t, (int)n_slots, overflow, partials, (unsigned *)ticket,
+                       obs_mean, obs_var, obs_clip, boot_norm, ld_norm, slot_src, ld_slot, (const float *)nullptr,
+                       rms_x, rms_ld, (int)obs_dim, rms_part, obs_mean, obs_var, obs_count);
     return xpa_launch_status();
 }
 

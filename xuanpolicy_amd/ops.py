@@ -1211,14 +1211,17 @@ def post_workspace(n_envs, device):
 
 def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term,
                  buf_closed, buf_boot, gamma, mask_returns=True, use_rewnorm=True, rew_range=5.0, atari_lifeloss=False,
-                 deferred=None, workspace=None, v_boot_mid=None):
+                 deferred=None, workspace=None, v_boot_mid=None, rms=None):
     """K8: reward normalisation, return tracker + ret_rms, rewards/terminals/closures into the buffer
     column cursor.ptr, then cursor.ptr = (ptr + 1) % horizon, cursor.step += 1.
     deferred = (boot_obs [N, D] (row stride may exceed D), slot_obs [S N, D], slot_t int32 [S N], overflow
     int32 [1]): no v_boot; truncation rows are kept (up to S per env) for bootstrap_fixup after the rollout.
     workspace = post_workspace(N) (kept by the caller across steps; allocated here when None).
     v_boot_mid [N] (not deferred): the bootstrap values of closures before the rollout's last step (A2C's
-    V(norm(reset_obs)), a2c_agent.py:88-95); v_boot is used at the last step (and everywhere when None)."""
+    V(norm(reset_obs)), a2c_agent.py:88-95); v_boot is used at the last step (and everywhere when None).
+    rms = (x [N, D] the observation the env step produced, obs_count f64 [1], rms_part f64 [2 * blocks, D]) with the
+    8 / 9-element deferred form (r05, D <= 64): the next step's obs_rms.update folded in (obs_mean / obs_var of
+    `deferred` and obs_count updated in place after the normalisation used the old statistics)."""
     N = rew.shape[0]
     _req(rew, "rew", torch.float32, (N,))
     _req(term, "term", torch.uint8, (N,))
@@ -1250,6 +1253,22 @@ def rollout_post(rew, term, trunc, v_boot, cursor, ret_mean, ret_var, ret_count,
         _req(overflow, "overflow", torch.int32, (1,))
         _req(obs_mean, "obs_mean", torch.float32, (D,))
         _req(obs_var, "obs_var", torch.float32, (D,))
+        if rms is not None:
+            rx, rcount, rpart = rms
+            rld = _row_stride(rx, "rms_x", D)
+            if rx.shape[0] != N:
+                raise ValueError("rms_x must have one row per env")
+            _req(rcount, "obs_count", torch.float64, (1,))
+            _req(rpart, "rms_part", torch.float64, (2 * int(lib().xpa_rollout_post_num_blocks(N)), D))
+            rc = lib().xpa_rollout_post_deferred_norm_rms(
+                N, T, _p(rew), _p(term), _p(trunc), _p(final_obs), ldf, _p(slot_src), lds, D, _p(obs_mean),
+                _p(obs_var), _p(rcount), float(obs_clip), _p(boot_norm), ldn, _p(slot_obs), _p(slot_t), S,
+                _p(overflow), _p(cursor), _p(ret_mean), _p(ret_var), _p(ret_count), _p(returns), _p(buf_rew),
+                _p(buf_term), _p(buf_closed), _p(buf_boot), float(gamma), int(bool(mask_returns)),
+                int(bool(use_rewnorm)), float(rew_range), int(bool(atari_lifeloss)), _p(part), _p(ticket), _p(rx), rld,
+                _p(rpart), _stream(rew.device))
+            _lib.check(rc, "xpa_rollout_post_deferred_norm_rms")
+            return
         rc = lib().xpa_rollout_post_deferred_norm(
             N, T, _p(rew), _p(term), _p(trunc), _p(final_obs), ldf, _p(slot_src), lds,
             D, _p(obs_mean), _p(obs_var), float(obs_clip),
