@@ -679,6 +679,14 @@ int xpa_rollout_post_deferred_norm_rms(
     float *returns, float *buf_rew, float *buf_term, uint8_t *buf_closed, float *buf_boot, float gamma,
     int mask_returns, int use_rewnorm, float rew_range, int atari_lifeloss, double *partials, uint32_t *ticket,
     const float *rms_x, int64_t rms_ld, double *rms_part, xpa_stream_t stream);
+/* r05, the row-index forms of K40F / K41V (C4's wide trunk straight from the rollout buffer, no gathered copy): A's
+ * row r is row idx[r] of a; k (K40F) / m (K41V) may exceed a's row width (a zero-padded B, or output rows the caller
+ * drops) when the buffer has readable, finite slack after its last row.  K41V: rows per slice <= 1536. */
+int xpa_s3_gemm_bias_act_rows(const float *a, int64_t lda, const int64_t *ridx, const void *b_split, float *c,
+                              int64_t ldc, int64_t m, int64_t k, const float *bias, int act, float slope,
+                              unsigned *sign_out, xpa_stream_t stream);
+int xpa_s3_wgrad_rows(const float *a, int64_t lda, const int64_t *aidx, const float *b, int64_t ldb, int64_t rows,
+                      int64_t m, int64_t n, int64_t slices, float *out, xpa_stream_t stream);
 /* K40R (r05): the rollout's paired hidden layer z [m, 512] = x [m, 256] . [B0 | B1] + bias on the split (B0 / B1 =
  * Wh_actor^T / Wh_critic^T split by xpa_s3_split_b, k = 256): 64-row x 128-column blocks for the rollout's few rows
  * (ppoclip_agent.py:63 self.action(obs) -> the policy's hidden layers); each output equals xpa_s3_gemm's + bias. */

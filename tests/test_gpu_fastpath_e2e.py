@@ -121,8 +121,8 @@ def test_fast_path_iteration_with_split_gemms_matches_oracle(agent_name, discret
                                expect_mid_truncations=not discrete)
 
 
-@pytest.mark.parametrize("wide", [True, False])
-def test_c4_shape_iteration_matches_oracle(wide, monkeypatch):
+@pytest.mark.parametrize("mode", ["direct", "gather", "off"])
+def test_c4_shape_iteration_matches_oracle(mode, monkeypatch):
     """C4's per-shard shapes (BASELINE.json configs[3]: SynthBox(obs=376, act=17), ppo/mujoco.yaml, [256] nets) at a
     reduced N x T: the 376-wide trunk (no K13: the first layer is a library GEMM), the non-K14E rollout (K14 policy
     head + the separate env GEMM + K7), the 1024-thread K5 for wide observations, the KMAX-18 K16 bucket (A = 17)
@@ -132,7 +132,9 @@ def test_c4_shape_iteration_matches_oracle(wide, monkeypatch):
     from xuanpolicy_amd.runner import build_synthbox_ppo
     # r05: the wide trunk layer on K40F / K42W (or K42C's dz form) / K41V with the transposed finalize; off = the
     # library GEMM trunk of r04
+    wide = mode != "off"
     monkeypatch.setattr(FusedActorCritic, "WIDE_TRUNK", wide)
+    monkeypatch.setattr(FusedActorCritic, "WIDE_DIRECT", mode == "direct")   # rows through idx, or the pitched gather
     N, T, D, A, H = 512, 64, 376, 17, 256
     n_epoch, n_mb = 2, 4
     agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=D, act_dim=A, hidden=H, n_epoch=n_epoch,
@@ -152,7 +154,7 @@ def test_c4_shape_iteration_matches_oracle(wide, monkeypatch):
                                loss_tol=5e-4, w_atol=5e-4, clip_tol=5e-3)
     assert fm._wide_on() == wide
     keys = {k[0] for k in fm._partials if isinstance(k, tuple)}
-    assert (("wide_bwd" in keys) and ("wide_x" in keys)) == wide, keys
+    assert ("wide_bwd" in keys) == wide and ("wide_x" in keys) == (mode == "gather"), keys
 
 
 def test_deferred_bootstraps_with_several_truncations_per_rollout():

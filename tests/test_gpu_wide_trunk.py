@@ -152,3 +152,31 @@ def test_finalize_output_map(S, kp, d):
     assert ((o2.double() - other.double().sum(0)).abs() <= 1e-6 * other.double().sum(0).abs() + 1e-6).all()
     want = (w.double() ** 2).sum() + (o2.double() ** 2).sum()
     assert abs(total.item() - want.item()) <= 1e-9 * want.item()
+
+
+@pytest.mark.parametrize("M,n_rows,d", [(65536, 70000, 376), (777, 5000, 376), (300, 400, 100)])
+def test_row_index_forms_equal_gathered(M, n_rows, d):
+    """r05: K40F and K41V reading the minibatch rows through idx from a buffer with zeroed slack equal their forms on
+    the gathered, zero-padded rows bit for bit (K41V: the rows below the layer width, the rest is dropped)."""
+    from xuanpolicy_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(M + d + 1)
+    kp, mp = (d + 15) // 16 * 16, (d + 127) // 128 * 128
+    store = torch.zeros(n_rows * d + 128, device=DEV)
+    flat = store[:n_rows * d].view(n_rows, d)
+    flat.copy_(torch.randn(n_rows, d, device=DEV, generator=g))
+    idx = torch.randint(0, n_rows, (M,), device=DEV, generator=g)
+    xp = torch.zeros(M, mp, device=DEV)
+    xp[:, :d] = flat[idx]
+    w = torch.randn(256, d, device=DEV, generator=g) / d ** 0.5
+    b = torch.randn(256, device=DEV, generator=g) * 0.1
+    ws = ops.s3_split_padded(w.t(), kp)
+    s1, s2 = torch.empty((M, 8), dtype=torch.int32, device=DEV), torch.empty((M, 8), dtype=torch.int32, device=DEV)
+    h1 = ops.s3_gemm_bias_act(flat, ws, kp, b, 1, 0.01, sign=s1, ridx=idx)
+    h2 = ops.s3_gemm_bias_act(xp[:, :kp].contiguous(), ws, kp, b, 1, 0.01, sign=s2)
+    dz = torch.randn(M, 256, device=DEV, generator=g)
+    S = max(1, 256 // (mp // 128))
+    p1 = ops.s3_wgrad(flat, dz, slices=S, aidx=idx, m=mp)
+    p2 = ops.s3_wgrad(xp, dz, slices=S)
+    torch.cuda.synchronize()
+    assert torch.equal(h1, h2) and torch.equal(s1, s2)
+    assert torch.equal(p1[:, :d], p2[:, :d])

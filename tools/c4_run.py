@@ -12,4 +12,7 @@ if __name__ == "__main__":
     if "wide-off" in sys.argv:   # the r04 trunk (library GEMMs) for A/B
         from xuanpolicy_amd.fused_mlp import FusedActorCritic
         FusedActorCritic.WIDE_TRUNK = False
+    if "gather" in sys.argv:     # the wide trunk on the pitched gather (no row-index forms) for A/B
+        from xuanpolicy_amd.fused_mlp import FusedActorCritic
+        FusedActorCritic.WIDE_DIRECT = False
     print(json.dumps(bench.c4_bench(torch.device("cuda:0"), 0, 1, steps=it, warmup=1)))

@@ -253,6 +253,9 @@ SIGNATURES = {
                                                           c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, ctypes.c_int,
                                                           ctypes.c_int, c_f32, ctypes.c_int, c_p, c_p, c_p, c_i64, c_p,
                                                           c_p]),
+    "xpa_s3_gemm_bias_act_rows": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, ctypes.c_int,
+                                                 c_f32, c_p, c_p]),
+    "xpa_s3_wgrad_rows": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
     "xpa_s3_gemm_rows_pair": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p]),
     "xpa_s3_split_batch_padded": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "xpa_s3_gemm_bias_act": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_p, ctypes.c_int, c_f32, c_p,

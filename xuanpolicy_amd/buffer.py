@@ -29,6 +29,8 @@ def _dev(device):
     return torch.device(device)
 
 
+OBS_SLACK = 128   # elements of zeroed slack after the observation buffer (see DummyOnPolicyBuffer.__init__)
+
 class DummyOnPolicyBuffer:
     obs_dtype = torch.float32
 
@@ -46,7 +48,11 @@ class DummyOnPolicyBuffer:
         self.start_ids = np.zeros(self.n_envs, np.int64)
         N, T, dev = self.n_envs, self.n_size, self.device
         f32 = dict(dtype=torch.float32, device=dev)
-        self.observations = torch.zeros((N, T) + self.obs_shape, dtype=self.obs_dtype, device=dev)
+        # r05: OBS_SLACK zeroed elements after the last row (same allocation): the update's split GEMMs may read a row
+        # tile past a row's end (C4's 376-wide trunk read through the minibatch index, fused_mlp._wide_forward)
+        n_obs = N * T * int(np.prod(self.obs_shape, dtype=np.int64))
+        self.observations = torch.zeros(n_obs + OBS_SLACK, dtype=self.obs_dtype, device=dev)[:n_obs].view(
+            (N, T) + self.obs_shape)
         self.actions = torch.zeros((N, T) + self.act_shape, **f32)
         self.rewards = torch.zeros((N, T), **f32)
         self._returns = torch.zeros((N, T), **f32)

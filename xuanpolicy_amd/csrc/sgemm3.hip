@@ -193,6 +193,22 @@ __device__ __forceinline__ void issue(unsigned st, const float *__restrict__ a, 
     }
 }
 
+// issue<W> with the lane's two A row pointers precomputed (r05, K40F: rows possibly through an index, ar_i = the row's
+// base + 4 q, so no index load or address arithmetic sits in front of each chunk's DMAs)
+template <int W>
+__device__ __forceinline__ void issue_rows(unsigned st, const float *ar0, const float *ar1,
+                                           const __bf16 *__restrict__ bs, int c, int lane, int wave) {
+    using G = S3Geom<W>;
+    glds16(ar0 + c * kKC, st + (unsigned)((wave * 32) * kKC * 4));
+    glds16(ar1 + c * kKC, st + (unsigned)((wave * 32 + 16) * kKC * 4));
+    const char *bsrc = reinterpret_cast<const char *>(bs) + (int64_t)c * kBImg;
+#pragma unroll
+    for (int j = 0; j < G::kPer; ++j) {
+        const int piece = wave * G::kPer + j;
+        glds16(bsrc + piece * 1024 + lane * 16, st + (unsigned)(G::kAImg + piece * 1024));
+    }
+}
+
 template <int W, int PROBE>
 __device__ __forceinline__ void chunk(const char *st, f32x16 (&acc)[8], int lane, int wave) {
     constexpr int kAImg = S3Geom<W>::kAImg;
@@ -253,7 +269,8 @@ __global__ __launch_bounds__(64 * W, 8 / W) void s3_gemm_kernel(const float *__r
                                                                int64_t ldc, int64_t M, int nchunks,
                                                                const float *__restrict__ bias = nullptr,
                                                                float slope = 0.f,
-                                                               unsigned char *__restrict__ sign = nullptr) {
+                                                               unsigned char *__restrict__ sign = nullptr,
+                                                               const int64_t *__restrict__ ridx = nullptr) {
     using G = S3Geom<W>;
     // ONE LDS array (the DMA target; see head.hip)
     __shared__ __attribute__((aligned(16))) char lds[S * G::kStage];
@@ -266,9 +283,27 @@ __global__ __launch_bounds__(64 * W, 8 / W) void s3_gemm_kernel(const float *__r
     for (int cb = 0; cb < 8; ++cb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[cb][r] = 0.f;
+    // K40F (EPI != 0): the lane's two A rows resolved once (through ridx when given: the minibatch rows of the rollout
+    // buffer, r05), rows past M re-reading row M - 1 as issue<W> does
+    const float *ar[2] = {a, a};
+    if constexpr (EPI != 0) {
+        const int rr = lane >> 2, p = lane & 3;
+        const int q = p ^ ((rr >> 2) & 3);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            int64_t row = r0 + wave * 32 + i * 16 + rr;
+            row = row < M ? row : M - 1;
+            if (ridx != nullptr) row = ridx[row];
+            ar[i] = a + row * lda + 4 * q;
+        }
+    }
+    auto issue_any = [&](unsigned st, int c) {
+        if constexpr (EPI != 0) issue_rows<W>(st, ar[0], ar[1], bs, c, lane, wave);
+        else issue<W>(st, a, lda, bs, r0, M, c, lane, wave);
+    };
 #pragma unroll
     for (int d = 0; d < S - 1; ++d)
-        if (d < nchunks) issue<W>(base + d * G::kStage, a, lda, bs, r0, M, d, lane, wave);
+        if (d < nchunks) issue_any(base + d * G::kStage, d);
 #pragma unroll 1
     for (int ch = 0; ch < nchunks; ++ch) {
         // own DMAs of chunk ch landed (with 3 stages chunk ch + 1's may still fly), then every wave's: the stage
@@ -276,7 +311,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void s3_gemm_kernel(const float *__r
         if (S == 3 && ch + 1 < nchunks) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(G::kDma) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
         if (ch + S - 1 < nchunks && (PROBE & 2) == 0)
-            issue<W>(base + ((ch + S - 1) % S) * G::kStage, a, lda, bs, r0, M, ch + S - 1, lane, wave);
+            issue_any(base + ((ch + S - 1) % S) * G::kStage, ch + S - 1);
         if constexpr (T64 != 0) chunk64(lds + (ch % S) * G::kStage, acc, lane, wave);
         else chunk<W, PROBE>(lds + (ch % S) * G::kStage, acc, lane, wave);
     }
@@ -1306,14 +1341,18 @@ __device__ __forceinline__ float4 v_zero_if(float4 v, bool keep) {
     return make_float4(keep ? v.x : 0.f, keep ? v.y : 0.f, keep ? v.z : 0.f, keep ? v.w : 0.f);
 }
 
+// s_idx (r05, K41V's row-index form): A's row r is row s_idx[r] of A (the slice's indices staged in LDS; B's rows
+// are read directly)
 __device__ __forceinline__ void v_load(VUnits &u, const float *__restrict__ A, int64_t lda, const float *__restrict__ B,
-                                       int64_t ldb, int64_t k0, int64_t kend, int t) {
+                                       int64_t ldb, int64_t k0, int64_t kend, int t,
+                                       const int64_t *s_idx = nullptr) {
     unsigned ok = 0u;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int idx = t + 512 * j, k = idx >> 5, cq = idx & 31;
         const int64_t r = k0 + k;
-        u.a[j] = *reinterpret_cast<const float4 *>(A + min(r, kend - 1) * lda + 4 * cq);
+        const int64_t rc = min(r, kend - 1);
+        u.a[j] = *reinterpret_cast<const float4 *>(A + (s_idx != nullptr ? s_idx[rc] : rc) * lda + 4 * cq);
         ok |= (r < kend ? 1u : 0u) << j;
     }
 #pragma unroll
@@ -1434,7 +1473,8 @@ __device__ __forceinline__ void v_put_unit(char *nx, const VUnits &u, int t, int
 // last two MFMA blocks)
 __device__ __forceinline__ void v_chunk_il(const char *st, char *nx, VUnits &u, f32x16 (&acc)[2][2], int lane, int wm,
                                            int wn, int t, const float *__restrict__ A, int64_t lda,
-                                           const float *__restrict__ B, int64_t ldb, int64_t k_next, int64_t kend) {
+                                           const float *__restrict__ B, int64_t ldb, int64_t k_next, int64_t kend,
+                                           const int64_t *s_idx = nullptr) {
     bf16x8 ah[2][2], am[2][2], al[2][2], bh[2][2], bm[2][2], bl[2][2];
     v_frags(st, 0, lane, wm, wn, ah[0], am[0], al[0], bh[0], bm[0], bl[0]);
 #pragma unroll
@@ -1443,17 +1483,21 @@ __device__ __forceinline__ void v_chunk_il(const char *st, char *nx, VUnits &u, 
         acc[i][j] = xpa_mfma_s3(ah[s][i], am[s][i], al[s][i], bh[s][j], bm[s][j], bl[s][j], acc[i][j]);
         if (seg < 6) v_put_unit(nx, u, t, seg);
         if (seg == 1) v_frags(st, 1, lane, wm, wn, ah[1], am[1], al[1], bh[1], bm[1], bl[1]);
-        if (seg == 6) v_load(u, A, lda, B, ldb, k_next, kend, t);
+        if (seg == 6) v_load(u, A, lda, B, ldb, k_next, kend, t, s_idx);
         __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-template <int SCHED = 0>
+// IDX (r05): A's rows through aidx (the minibatch rows of the rollout buffer: C4's wide trunk dW without a gathered
+// copy); the slice's indices are staged in LDS once (slice_rows <= kVIdxMax)
+constexpr int kVIdxMax = 1536;   // 12 KiB beside the 144 KiB of stages
+template <int SCHED = 0, bool IDX = false>
 __global__ __launch_bounds__(512, 1) void s3_wgrad_v_kernel(const float *__restrict__ A, int64_t lda,
                                                             const float *__restrict__ B, int64_t ldb, int64_t rows,
                                                             int64_t M, int slices, int64_t slice_rows,
-                                                            float *__restrict__ out) {
-    __shared__ __attribute__((aligned(16))) char lds[2 * kVStage];
+                                                            float *__restrict__ out,
+                                                            const int64_t *__restrict__ aidx = nullptr) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * kVStage + (IDX ? kVIdxMax * 8 : 0)];
     const int mtiles = (int)(M / kWgM);
     const int nblk = slices * mtiles;
     int L = blockIdx.x;
@@ -1466,6 +1510,13 @@ __global__ __launch_bounds__(512, 1) void s3_wgrad_v_kernel(const float *__restr
     const int64_t k0 = (int64_t)slice * slice_rows;
     const int64_t kend = min(rows, k0 + slice_rows);
     const int nch = kend > k0 ? (int)((kend - k0 + kWgKC - 1) / kWgKC) : 0;
+    const int64_t *s_idx = nullptr;   // IDX: s_idx[r] (r in [k0, kend)) = aidx[r], from LDS
+    if constexpr (IDX) {
+        int64_t *si = reinterpret_cast<int64_t *>(lds + 2 * kVStage);
+        for (int64_t r = k0 + t; r < kend; r += 512) si[r - k0] = aidx[r];
+        __syncthreads();
+        s_idx = si - k0;
+    }
     f32x16 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -1475,9 +1526,9 @@ __global__ __launch_bounds__(512, 1) void s3_wgrad_v_kernel(const float *__restr
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     VUnits u;
     if (nch > 0) {
-        v_load(u, Am, lda, B, ldb, k0, kend, t);
+        v_load(u, Am, lda, B, ldb, k0, kend, t, s_idx);
         v_store(lds, u, t);
-        if (nch > 1) v_load(u, Am, lda, B, ldb, k0 + kWgKC, kend, t);
+        if (nch > 1) v_load(u, Am, lda, B, ldb, k0 + kWgKC, kend, t, s_idx);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
 #pragma unroll 1
@@ -1485,10 +1536,10 @@ __global__ __launch_bounds__(512, 1) void s3_wgrad_v_kernel(const float *__restr
         if constexpr (!SCHED) v_chunk(lds + (c & 1) * kVStage, acc, lane, wm, wn);
         if constexpr (SCHED) {
             v_chunk_il(lds + (c & 1) * kVStage, lds + ((c + 1) & 1) * kVStage, u, acc, lane, wm, wn, t, Am, lda, B, ldb,
-                       k0 + (int64_t)(c + 2) * kWgKC, kend);
+                       k0 + (int64_t)(c + 2) * kWgKC, kend, s_idx);
         } else if (c + 1 < nch) {
             v_store(lds + ((c + 1) & 1) * kVStage, u, t);
-            if (c + 2 < nch) v_load(u, Am, lda, B, ldb, k0 + (int64_t)(c + 2) * kWgKC, kend, t);
+            if (c + 2 < nch) v_load(u, Am, lda, B, ldb, k0 + (int64_t)(c + 2) * kWgKC, kend, t, s_idx);
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
@@ -1817,6 +1868,23 @@ XPA_API int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ld
     return xpa_launch_status();
 }
 
+// K41V's row-index form (r05): A's row r is row aidx[r] of a (C4's trunk dW straight from the rollout buffer); m may
+// exceed a's row width by < 128 (the last row tile reads past each row: the caller guarantees readable slack after the
+// buffer's last row; those output rows are garbage and dropped by the caller's finalize map); rows per slice <= 1536
+XPA_API int xpa_s3_wgrad_rows(const float *a, int64_t lda, const int64_t *aidx, const float *b, int64_t ldb,
+                              int64_t rows, int64_t m, int64_t n, int64_t slices, float *out, xpa_stream_t stream) {
+    if (!a || !aidx || !b || !out || rows <= 0 || m <= 0 || m % kWgM || n != kN || lda < 4 || m > lda + kWgM ||
+        ldb < n || slices < 1 || slices > 4096 || (lda & 3) || (ldb & 3) ||
+        ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15))
+        return (int)hipErrorInvalidValue;
+    int64_t per = (rows + slices - 1) / slices;
+    per = (per + kWgKC - 1) / kWgKC * kWgKC;
+    if (per > kVIdxMax) return (int)hipErrorInvalidValue;
+    const dim3 grid((unsigned)(slices * (m / kWgM))), block(512);
+    s3_wgrad_v_kernel<1, true><<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out, aidx);
+    return xpa_launch_status();
+}
+
 // K41P (r05): slice counts of xpa_s3_wgrad_pair for `rows` (sa actor, sc critic slices; their rows per slice in
 // per_a / per_c, multiples of 32): 2 (sa + sc) <= 256 blocks with ~2x the critic's rows per slice (3 products vs 6)
 XPA_API int xpa_s3_wgrad_pair_slices(int64_t rows, int64_t *sa, int64_t *sc, int64_t *per_a, int64_t *per_c) {
@@ -2089,10 +2157,35 @@ XPA_API int xpa_s3_gemm_trunk_bwd_crit_dz(const float *dz_a, int64_t ldz, const 
 // width that is not a multiple of 16 goes in zero-padded: A's row pitch >= k with zero columns, B's planes from
 // xpa_s3_split_batch_padded).  act 0 identity / 1 LeakyReLU (slope) / 2 tanh; sign_out (nullable, act 0 / 1): the
 // output's sign bits, 32 bytes per row (K42W's act').
+namespace {
+int gemm_bias_act_impl(const float *a, int64_t lda, const int64_t *ridx, const void *b_split, float *c, int64_t ldc,
+                       int64_t m, int64_t k, const float *bias, int act, float slope, unsigned *sign_out,
+                       xpa_stream_t stream);
+}
+
 XPA_API int xpa_s3_gemm_bias_act(const float *a, int64_t lda, const void *b_split, float *c, int64_t ldc, int64_t m,
                                  int64_t k, const float *bias, int act, float slope, unsigned *sign_out,
                                  xpa_stream_t stream) {
-    if (!a || !b_split || !c || !bias || m <= 0 || k <= 0 || k % kKC != 0 || lda < k || ldc < kN ||
+    if (lda < k) return (int)hipErrorInvalidValue;
+    return gemm_bias_act_impl(a, lda, nullptr, b_split, c, ldc, m, k, bias, act, slope, sign_out, stream);
+}
+
+// K40F's row-index form (r05): A's row r is row ridx[r] of a (the minibatch rows of the rollout buffer, no gathered
+// copy).  k may exceed the row width (a zero-padded B: split with xpa_s3_split_batch_padded): the columns past the
+// width then read the next row's first values (finite observations) or, for the buffer's last row, its allocation's
+// zeroed tail, and meet zero rows of B — the caller guarantees k - width floats of readable, finite slack.
+XPA_API int xpa_s3_gemm_bias_act_rows(const float *a, int64_t lda, const int64_t *ridx, const void *b_split, float *c,
+                                      int64_t ldc, int64_t m, int64_t k, const float *bias, int act, float slope,
+                                      unsigned *sign_out, xpa_stream_t stream) {
+    if (!ridx || lda < 4 || k > lda + kKC) return (int)hipErrorInvalidValue;
+    return gemm_bias_act_impl(a, lda, ridx, b_split, c, ldc, m, k, bias, act, slope, sign_out, stream);
+}
+
+namespace {
+int gemm_bias_act_impl(const float *a, int64_t lda, const int64_t *ridx, const void *b_split, float *c, int64_t ldc,
+                       int64_t m, int64_t k, const float *bias, int act, float slope, unsigned *sign_out,
+                       xpa_stream_t stream) {
+    if (!a || !b_split || !c || !bias || m <= 0 || k <= 0 || k % kKC != 0 || ldc < kN ||
         (reinterpret_cast<uintptr_t>(a) & 15) || (lda & 3) || act < 0 || act > 2 || (sign_out && act == 2) ||
         (reinterpret_cast<uintptr_t>(sign_out) & 15) || k / kKC > (1 << 20))
         return (int)hipErrorInvalidValue;
@@ -2101,13 +2194,15 @@ XPA_API int xpa_s3_gemm_bias_act(const float *a, int64_t lda, const void *b_spli
     const dim3 grid((unsigned)((m + 255) / 256)), block(512);
     unsigned char *sg = reinterpret_cast<unsigned char *>(sign_out);
     if (act == 0)
-        s3_gemm_kernel<8, 3, 0, 0, 1><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, nch, bias, slope, sg);
+        s3_gemm_kernel<8, 3, 0, 0, 1><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, nch, bias, slope, sg, ridx);
     else if (act == 1)
-        s3_gemm_kernel<8, 3, 0, 0, 2><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, nch, bias, slope, sg);
+        s3_gemm_kernel<8, 3, 0, 0, 2><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, nch, bias, slope, sg, ridx);
     else
-        s3_gemm_kernel<8, 3, 0, 0, 3><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, nch, bias, slope, nullptr);
+        s3_gemm_kernel<8, 3, 0, 0, 3><<<grid, block, 0, stream>>>(a, lda, bs, c, ldc, m, nch, bias, slope, nullptr,
+                                                                  ridx);
     return xpa_launch_status();
 }
+}  // namespace
 
 // K40R (r05): z [m, 512] = x [m, 256] . [B0 | B1] + bias, B0 / B1 split by xpa_s3_split_b (k = 256): the rollout's
 // paired hidden layer; each output is xpa_s3_gemm's + bias bit for bit

@@ -97,6 +97,7 @@ class Rows:
         self.gathered = None   # set by the gather forward: the rows as a contiguous [B, d] copy
         self.trunk = None      # K16X: (gathered rows, W0, b0, slope, h out) when the head launches form h
         self.hsign = None      # K13's sign bits of h (int32 [B, 8]) for K42S
+        self.wide_direct = False   # r05: the wide trunk read these rows through idx (no gathered copy)
         self.shape = (idx.shape[0], flat.shape[1])
         self.device = flat.device
         self.dtype = flat.dtype
@@ -198,13 +199,41 @@ class FusedActorCritic:
         return (self.WIDE_TRUNK and self.wide0 and self.fused_heads and ops.S3_GEMMS and self.pair is not None
                 and self._dx_split_ok(self.pair[0]))
 
+    WIDE_DIRECT = True   # r05: K40F / K41V read the minibatch rows through idx from the rollout buffer (no gather)
+
+    @staticmethod
+    def _wide_mpad(d):
+        return (d + 127) // 128 * 128   # K41V's row tiles over the layer's inputs
+
+    def _wide_direct_ok(self, x, d):
+        """The row-index forms apply: the flat buffer's rows are the layer width and readable, finite (zeroed) slack
+        follows its last row for the padded columns (buffer.OBS_SLACK)."""
+        f = x.flat
+        need = max((d + 15) // 16 * 16, self._wide_mpad(d)) - d
+        return (self.WIDE_DIRECT and f.dim() == 2 and f.is_contiguous() and f.shape[1] == d and d % 4 == 0
+                and f.data_ptr() % 16 == 0
+                and f.untyped_storage().nbytes() // 4 >= f.storage_offset() + f.numel() + need)
+
     def _wide_forward(self, x, adv, adv_partials):
-        """The wide trunk layer's forward on the minibatch rows x = Rows(flat, idx): the pitched gather into a
-        zero-padded [B, d_pad] buffer (+ the advantage moments), W0^T's split (zero rows to d_pad), K40F (bias,
-        activation and h's sign bits in the epilogue)."""
+        """The wide trunk layer's forward on the minibatch rows x = Rows(flat, idx): W0^T's split (zero rows to d_pad),
+        then K40F (bias, activation and h's sign bits in the epilogue) reading the rows through idx straight from the
+        rollout buffer (+ the advantage moments from a row-less K4); or, where the buffer has no slack, the pitched
+        gather into a zero-padded [B, d_pad] buffer first."""
         lin, code, slope = self.rep[0]
         B, d = x.idx.shape[0], lin.in_features
         kp = (d + 15) // 16 * 16
+        if self._wide_direct_ok(x, d):
+            if adv_partials is not None:   # K4's advantage moments alone (zero-width rows)
+                ops.gather_minibatch(x.idx, x.flat[:, :0], adv=adv, adv_partials=adv_partials,
+                                     obs_out=x.flat.new_empty((B, 0)))
+            x.gathered = None
+            x.wide_direct = True
+            x.hsign = self._sign_buf(B, x.device)
+            wsplit = self._split_buf(kp, "w0t", x.device)
+            ops.s3_split_padded(lin.weight.t(), kp, out=wsplit)
+            h = torch.empty((B, lin.out_features), dtype=torch.float32, device=x.device)
+            ops.s3_gemm_bias_act(x.flat, wsplit, kp, lin.bias, code, slope, out=h, sign=x.hsign, ridx=x.idx)
+            return [h]
         key = ("wide_x", B, kp)
         xp = self._partials.get(key)
         if xp is None:   # graph-capture safe: allocated (and its pad zeroed) on first (eager) use
@@ -225,8 +254,9 @@ class FusedActorCritic:
         slices of x_pad^T dz1, finalized transposed (and trimmed to d_in) into W0's gradient."""
         lin, code, slope = self.rep[0]
         B, d = dz.shape[0], lin.in_features
+        direct = getattr(x, "wide_direct", False)
         xp = x.gathered
-        kp = xp.shape[1]
+        kp = self._wide_mpad(d) if direct else xp.shape[1]
         S = max(1, 256 // (kp // 128))
         key = ("wide_bwd", B, kp, S)
         ws = self._partials.get(key)
@@ -243,7 +273,10 @@ class FusedActorCritic:
                                      crit=(H, k - H, crit[0], crit[1], crit[2]))
         else:
             ops.s3_gemm_trunk_bwd_dz(dz, self._split_buf(k, "dx", dz.device), k, x.hsign, code, slope, dz1, pdb)
-        ops.s3_wgrad(xp, dz1, out=pdw, slices=S)
+        if direct:   # K41V through idx from the rollout buffer (rows d .. kp - 1 of the slices: garbage, dropped)
+            ops.s3_wgrad(x.flat, dz1, out=pdw, slices=S, aidx=x.idx, m=kp)
+        else:
+            ops.s3_wgrad(xp, dz1, out=pdw, slices=S)
         self._cq.add(pdw.view(S, -1), lin.weight.grad, tmap=(256, d, d))
         self._cq.add(pdb, lin.bias.grad)
         return True
@@ -600,8 +633,8 @@ class FusedActorCritic:
             return None
         xr = x.gathered
         h = rep_outs[0] if rep_outs else None
-        if not (isinstance(xr, torch.Tensor) and xr.dim() == 2 and xr.stride(1) == 1 and isinstance(h, torch.Tensor)
-                and h.shape[1] == 256 and _vec4_rows(h)):
+        x_ok = self._wide_on() or (isinstance(xr, torch.Tensor) and xr.dim() == 2 and xr.stride(1) == 1)
+        if not (x_ok and isinstance(h, torch.Tensor) and h.shape[1] == 256 and _vec4_rows(h)):
             return None
         if self._hws is None or not _vec4_rows(self._hws.dz_actor):
             return None
@@ -659,7 +692,7 @@ class FusedActorCritic:
         False (nothing done) when it does not apply: not the split GEMMs, more than one representation layer, no K13
         first layer, d_in > 32, or rows not given as the gathered minibatch.  The wide trunk layer: _wide_bwd."""
         if (self._wide_on() and isinstance(x, Rows) and getattr(x, "hsign", None) is not None
-                and isinstance(x.gathered, torch.Tensor) and _vec4_rows(dz)):
+                and (isinstance(x.gathered, torch.Tensor) or getattr(x, "wide_direct", False)) and _vec4_rows(dz)):
             return self._wide_bwd(dz, x, crit)
         if not (self.FUSE_TRUNK_BWD and self._dx_split_ok(self.pair[0]) and len(self.rep) == 1 and self.thin0
                 and _vec4_rows(dz)):

@@ -371,10 +371,28 @@ def s3_split_padded(b, k_pad, out=None):
     return out
 
 
-def s3_gemm_bias_act(a, b_split, k, bias, act, slope, out=None, sign=None):
+def s3_gemm_bias_act(a, b_split, k, bias, act, slope, out=None, sign=None, ridx=None):
     """K40F (r05): out [m, 256] = act(a [m, k] . B + bias) (act 0 identity / 1 LeakyReLU / 2 tanh); sign (int32 [m, 8],
-    act 0 / 1): the output's sign bits for K42W.  a's columns past the layer width must be zero (padded rows)."""
+    act 0 / 1): the output's sign bits for K42W.  a's columns past the layer width must be zero (padded rows).
+    ridx (int64 [m]): the row-index form — row r is a[ridx[r]] of a [n_rows, width], k <= width + 16 with readable,
+    finite slack after a's last row (xpa_s3_gemm_bias_act_rows)."""
     _req(a, "a", torch.float32, contiguous=False)
+    if ridx is not None:
+        _req(ridx, "ridx", torch.int64)
+        if a.dim() != 2 or a.stride(1) != 1 or k > a.stride(0) + 16:
+            raise ValueError("a must be [n_rows, width] with unit column stride and k <= width + 16")
+        m = ridx.shape[0]
+        _req(bias, "bias", torch.float32, (256,))
+        if out is None:
+            out = torch.empty(m, 256, dtype=torch.float32, device=a.device)
+        ldc = _row_stride(out, "out", 256)
+        if sign is not None:
+            _req(sign, "sign", torch.int32, (m, 8))
+        _lib.check(lib().xpa_s3_gemm_bias_act_rows(_p(a), a.stride(0), _p(ridx), _p(b_split), _p(out), ldc, m, k,
+                                                   _p(bias), int(act), float(slope),
+                                                   _p(sign) if sign is not None else None, _stream(a.device)),
+                   "xpa_s3_gemm_bias_act_rows")
+        return out
     lda = _row_stride(a, "a", k)
     m = a.shape[0]
     _req(bias, "bias", torch.float32, (256,))
@@ -446,9 +464,26 @@ def s3_wgrad_slices(rows, m):
     return int(lib().xpa_s3_wgrad_num_slices(rows, m))
 
 
-def s3_wgrad(a, b, out=None, slices=None):
+def s3_wgrad(a, b, out=None, slices=None, aidx=None, m=None):
     """K41: per-slice partials out [S, m, 256] of a^T b over the rows (a [rows, m] = dz, b [rows, 256] = the layer
-    input; unit column strides), on the bf16 matrix cores by the three-way split.  The caller sums the S slices."""
+    input; unit column strides), on the bf16 matrix cores by the three-way split.  The caller sums the S slices.
+    aidx (int64 [rows], r05): a's row r is a[aidx[r]] of a [n_rows, width] (m given, m <= width + 127: output rows past
+    the width are garbage for the caller to drop; a needs readable slack after its last row; xpa_s3_wgrad_rows)."""
+    if aidx is not None:
+        _req(a, "a", torch.float32, contiguous=False)
+        _req(b, "b", torch.float32, contiguous=False)
+        _req(aidx, "aidx", torch.int64)
+        rows = aidx.shape[0]
+        ldb = _row_stride(b, "b", 256)
+        if b.shape[0] != rows or a.dim() != 2 or a.stride(1) != 1 or m is None:
+            raise ValueError("aidx form: b [rows, 256], a [n_rows, width], m given")
+        S = slices or s3_wgrad_slices(rows, m)
+        if out is None:
+            out = torch.empty(S, m, 256, dtype=torch.float32, device=a.device)
+        _req(out, "out", torch.float32, (S, m, 256))
+        _lib.check(lib().xpa_s3_wgrad_rows(_p(a), a.stride(0), _p(aidx), _p(b), ldb, rows, m, 256, S, _p(out),
+                                           _stream(a.device)), "xpa_s3_wgrad_rows")
+        return out
     _req(a, "a", torch.float32, contiguous=False)
     _req(b, "b", torch.float32, contiguous=False)
     rows, m = a.shape
