@@ -208,6 +208,66 @@ __global__ __launch_bounds__(kRmsThreads) void rms_partials_kernel(const float *
     }
 }
 
+// r05, wide observations (dim > kRmsWideDim, C4's 376): the same partials from a 2-D grid — block (g, cb) takes row
+// block g (kRmsRows rows) x columns 64 cb .. + 63, thread (group j, column c) sums rows j, j + 16, ... (16 loads in
+// flight) and the 16 groups are added in order — so np x ceil(dim / 64) blocks share the chip (the 1-D form ran the
+// 16 row blocks of a 4096-env step on 16 CUs: 21.5 us); the last of all the blocks merges (rms_merge_body, np = gridDim.x)
+template <bool MERGE>
+__global__ __launch_bounds__(1024) void rms_partials_cols_kernel(const float *__restrict__ x, int64_t n, int64_t dim,
+                                                                  int64_t ld, const float *shift,
+                                                                  double *__restrict__ part, float *mean,
+                                                                  float *__restrict__ var, double *__restrict__ count,
+                                                                  unsigned int *__restrict__ ticket) {
+    __shared__ double s_sum[16][64], s_sq[16][64];
+    __shared__ bool s_last;
+    const int64_t r0 = (int64_t)blockIdx.x * kRmsRows;
+    const int64_t r1 = r0 + kRmsRows < n ? r0 + kRmsRows : n;
+    const int64_t np = gridDim.x;
+    const int64_t c0 = (int64_t)blockIdx.y * 64;
+    const int c = threadIdx.x & 63, j = threadIdx.x >> 6;
+    double s = 0.0, q = 0.0;
+    if (c0 + c < dim) {
+        const float sh = shift ? shift[c0 + c] : 0.f;
+        for (int64_t rb = r0 + j; rb < r1; rb += 16 * 16) {
+            float xv[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int64_t r = rb + (int64_t)u * 16;
+                xv[u] = x[(r < r1 ? r : rb) * ld + c0 + c];
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (rb + (int64_t)u * 16 < r1) {
+                    const double v = (double)xv[u] - (double)sh;
+                    s += v;
+                    q += v * v;
+                }
+        }
+    }
+    s_sum[j][c] = s;
+    s_sq[j][c] = q;
+    __syncthreads();
+    if (threadIdx.x < 64 && c0 + threadIdx.x < dim) {
+        double ts = s_sum[0][threadIdx.x], tq = s_sq[0][threadIdx.x];
+#pragma unroll
+        for (int k = 1; k < 16; ++k) {
+            ts += s_sum[k][threadIdx.x];
+            tq += s_sq[k][threadIdx.x];
+        }
+        xpa_store_agent(part + (int64_t)blockIdx.x * dim + c0 + threadIdx.x, ts);
+        xpa_store_agent(part + (np + blockIdx.x) * dim + c0 + threadIdx.x, tq);
+    }
+    if (MERGE) {
+        xpa_drain();
+        __syncthreads();
+        if (threadIdx.x == 0) s_last = xpa_ticket(ticket) == (unsigned)(gridDim.x * gridDim.y - 1);
+        __syncthreads();
+        if (!s_last) return;
+        rms_merge_body(part, np, n, dim, mean, var, count);
+        if (threadIdx.x == 0) *ticket = 0u;
+    }
+}
+
 // Sum of the partials (fixed order) -> batch mean/var, then update_from_moments
 // (statistic_tools.py:86-112) into mean/var (f32) and count (f64).  mean doubles as the shift the
 // partials were taken around.
@@ -1167,9 +1227,9 @@ XPA_API int xpa_rms_partials(const float *x, int64_t n, int64_t dim, int64_t ld,
     if (n <= 0 || dim <= 0 || ld < dim || !x || !partials) return (int)hipErrorInvalidValue;
     const int64_t np = xpa_rms_num_partials(n);
     if (dim > kRmsWideDim)
-        hipLaunchKernelGGL((rms_partials_kernel<false, 1024>), dim3((unsigned)np), dim3(1024), 0, (hipStream_t)stream, x,
-                           n, dim, ld, shift, partials, (float *)nullptr, (float *)nullptr, (double *)nullptr,
-                           (unsigned int *)nullptr);
+        hipLaunchKernelGGL((rms_partials_cols_kernel<false>), dim3((unsigned)np, (unsigned)((dim + 63) / 64)), dim3(1024),
+                           0, (hipStream_t)stream, x, n, dim, ld, shift, partials, (float *)nullptr, (float *)nullptr,
+                           (double *)nullptr, (unsigned int *)nullptr);
     else
         hipLaunchKernelGGL((rms_partials_kernel<false, 256>), dim3((unsigned)np), dim3(256), 0, (hipStream_t)stream, x,
                            n, dim, ld, shift, partials, (float *)nullptr, (float *)nullptr, (double *)nullptr,
@@ -1183,8 +1243,9 @@ XPA_API int xpa_rms_update(const float *x, int64_t n, int64_t dim, int64_t ld, f
         return (int)hipErrorInvalidValue;
     const int64_t np = xpa_rms_num_partials(n);
     if (dim > kRmsWideDim)
-        hipLaunchKernelGGL((rms_partials_kernel<true, 1024>), dim3((unsigned)np), dim3(1024), 0, (hipStream_t)stream, x,
-                           n, dim, ld, (const float *)mean, partials, mean, var, count, (unsigned int *)ticket);
+        hipLaunchKernelGGL((rms_partials_cols_kernel<true>), dim3((unsigned)np, (unsigned)((dim + 63) / 64)), dim3(1024),
+                           0, (hipStream_t)stream, x, n, dim, ld, (const float *)mean, partials, mean, var, count,
+                           (unsigned int *)ticket);
     else
         hipLaunchKernelGGL((rms_partials_kernel<true, 256>), dim3((unsigned)np), dim3(256), 0, (hipStream_t)stream, x,
                            n, dim, ld, (const float *)mean, partials, mean, var, count, (unsigned int *)ticket);
