@@ -662,10 +662,17 @@ def c3_kernels(device, batch=16384):
             ts.append(e0.elapsed_time(e1) * 1e3)
         ts.sort()
         return ts[len(ts) // 2]
-    f_us = timed(lambda: _lib.check(L.xpa_conv1_u8_fwd(1, ops._p(x), batch, 84, 84, 4, 8, 4, 2, ops._p(w1), ops._p(b1),
-                                                       32, 0.0, ops._p(y1), st), "conv1_u8_fwd"))
-    w_us = timed(lambda: _lib.check(L.xpa_conv1_u8_wgrad(ops._p(g), ops._p(x), batch, 84, 84, 4, 8, 4, 2, 32,
-                                                         ops._p(wpart), st), "conv1_u8_wgrad"))
+    form0 = int(L.xpa_conv1_form(-1))
+    f_us, w_us = {}, {}
+    try:
+        for bit, tag in ((1, "bf16"), (0, "f32")):   # r05: K25B / K26B (bf16 matrix cores) and the fp32-MFMA forms
+            L.xpa_conv1_form(3 if bit else 0)
+            f_us[tag] = timed(lambda: _lib.check(L.xpa_conv1_u8_fwd(1, ops._p(x), batch, 84, 84, 4, 8, 4, 2, ops._p(w1),
+                                                                    ops._p(b1), 32, 0.0, ops._p(y1), st), "conv1_u8_fwd"))
+            w_us[tag] = timed(lambda: _lib.check(L.xpa_conv1_u8_wgrad(ops._p(g), ops._p(x), batch, 84, 84, 4, 8, 4, 2, 32,
+                                                                      ops._p(wpart), st), "conv1_u8_wgrad"))
+    finally:
+        L.xpa_conv1_form(form0)
     d_us = timed(lambda: _lib.check(L.xpa_conv_dgrad_s2k(ops._p(dy2), batch, 10, 10, 64, ops._p(w2), 32, 4, 2, 1, 21,
                                                          21, ops._p(dx2), st), "conv_dgrad_s2k"))
     b_us = timed(lambda: _lib.check(L.xpa_act_bwd_bias(1, ops._p(g), ops._p(h), rows, C, 0.0, ops._p(g), ops._p(part),
@@ -678,10 +685,22 @@ def c3_kernels(device, batch=16384):
         return {"kernel": name, "bound": "mfma", "avg_launch_us": round(us, 2), "flops_per_launch": flops,
                 "achieved": round(flops / us / 1e6, 1), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(flops / us / 1e6 / FP32_MFMA_PEAK_TFLOPS, 4), "shape": shape}
-    return {"conv1_u8_fwd": mfma("xpa_conv1_u8_fwd (K25)", f_us, c1_flops,
-                                 "%d frames 84x84x4 uint8 -> [B, 21, 21, 32] (8x8 s4 p2, bias + ReLU)" % batch),
-            "conv1_u8_wgrad": mfma("xpa_conv1_u8_wgrad (K26, partials; + f64 finalize)", w_us, c1_flops,
-                                   "dW [32, 4, 8, 8] over %d x 441 rows" % batch),
+    def bf16(name, us, flops, shape, planes=3):
+        # the frames are exact in bf16: `planes` bf16 products per f32 product, priced on the bf16 matrix peak
+        r = {"kernel": name, "bound": "mfma", "avg_launch_us": round(us, 2), "flops_per_launch": flops * planes,
+             "achieved": round(flops * planes / us / 1e6, 1), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+             "frac": round(flops * planes / us / 1e6 / BF16_MFMA_PEAK_TFLOPS, 4), "shape": shape,
+             "f32_equivalent_tflops": round(flops / us / 1e6, 1)}
+        return r
+
+    c1s = "%d frames 84x84x4 uint8 -> [B, 21, 21, 32] (8x8 s4 p2, bias + ReLU)" % batch
+    c1w = "dW [32, 4, 8, 8] over %d x 441 rows" % batch
+    return {"conv1_u8_fwd": bf16("xpa_conv1_u8_fwd (K25B: 3 bf16 products, the weight split)", f_us["bf16"],
+                                 c1_flops, c1s),
+            "conv1_u8_fwd_f32": mfma("xpa_conv1_u8_fwd (K25, fp32 MFMA form)", f_us["f32"], c1_flops, c1s),
+            "conv1_u8_wgrad": bf16("xpa_conv1_u8_wgrad (K26B: 3 bf16 products, the dz split; partials + f64 "
+                                   "finalize)", w_us["bf16"], c1_flops, c1w),
+            "conv1_u8_wgrad_f32": mfma("xpa_conv1_u8_wgrad (K26, fp32 MFMA form)", w_us["f32"], c1_flops, c1w),
             "conv_dgrad_s2k": mfma("xpa_conv_dgrad_s2k (K27)", d_us, c2_flops,
                                    "dX [B, 21, 21, 32] from dY [B, 10, 10, 64], 4x4 s2 p1"),
             "act_bwd_bias": {"kernel": "xpa_act_bwd_bias (K22, ReLU)", "bound": "hbm", "avg_launch_us": round(b_us, 2),

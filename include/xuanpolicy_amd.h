@@ -874,12 +874,18 @@ int xpa_thin_linear_act_bwd(int act, const float *g, int64_t ldg, const float *h
  * K20: dst[i] = float32(src[i] / 255.0) with the reference's arithmetic (NumPy float64 division, then the
  * float32 cast; cnn.py:89-92), bit for bit; n bytes in, n floats out (16-B aligned buffers take the vector path). */
 int xpa_frames_to_f32(const uint8_t *src, int64_t n, float *dst, xpa_stream_t stream);
+/* r05: the conv1 kernels' arithmetic — bit 0: K25B (forward), bit 1: K26B (weight gradient) on the bf16 matrix cores
+ * with the frames exact and the f32 operand split three ways; a cleared bit selects the fp32-MFMA form (K25 / K26).
+ * mask < 0 only reads.  Returns the previous mask (default 3). */
+int xpa_conv1_form(int mask);
 /* K25 — the first conv block straight from the uint8 frames (C3 AC_CNN_Atari / C5 Basic_CNN: cnn_block
  * xuance/torch/utils/layers.py:36-57 on observations / 255.0, cnn.py:89-92): y = act(conv2d(x / 255, w, stride, pad)
  * + bias) with x uint8 NHWC [batch, height, width, 4] (4-B aligned), w [32, 4, 8, 8] (torch's Conv2d layout), y f32
  * NHWC [batch, OH, OW, 32], OH = (height + 2 pad - 8) / stride + 1 (zero padding).  Computed as sum x (w / 255) on
  * fp32 MFMA (exact f32 fma chains; the 1/255 rounds once on the weight instead of once on the frame value).  act as xpa_bias_act.  channels must be 4,
- * kernel 8 and out_channels 32 (else hipErrorInvalidValue). */
+ * kernel 8 and out_channels 32 (else hipErrorInvalidValue).  r05 default (K25B, xpa_conv1_form bit 0): the same sum
+ * on the bf16 matrix cores — the bytes are exact in bf16 and w / 255 is cut into its exact three-way bf16 split, so
+ * each term is x (w / 255) rounded once as on fp32 MFMA; only the order of the f32 sum over taps differs. */
 int xpa_conv1_u8_fwd(int act, const uint8_t *x, int64_t batch, int64_t height, int64_t width, int64_t channels,
                      int64_t kernel, int64_t stride, int64_t pad, const float *w, const float *bias,
                      int64_t out_channels, float slope, float *y, xpa_stream_t stream);

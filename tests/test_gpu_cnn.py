@@ -225,9 +225,21 @@ def test_fused_qnetwork_matches_autograd(B):
     assert not bad, bad
 
 
+@pytest.fixture(params=[1, 0], ids=["k25b", "k25"])
+def conv1_form(request):
+    """r05: the conv1 forward on the bf16 matrix cores (K25B, the default) and on fp32 MFMA (K25)."""
+    _l, ops = _lib()
+    L = ops.lib()
+    prev = L.xpa_conv1_form(-1)
+    L.xpa_conv1_form((prev & ~1) | request.param)
+    yield request.param
+    L.xpa_conv1_form(prev)
+
+
 @pytest.mark.parametrize("B,act,slope,H,s,p", [(3, 1, 0.0, 84, 4, 2), (17, 0, 0.0, 84, 4, 2), (64, 1, 0.01, 84, 4, 2),
-                                             (5, 2, 0.0, 84, 4, 2), (4, 1, 0.0, 85, 3, 1), (3, 0, 0.0, 86, 4, 1)])
-def test_conv1_u8_matches_conv2d(B, act, slope, H, s, p):
+                                             (5, 2, 0.0, 84, 4, 2), (4, 1, 0.0, 85, 3, 1), (3, 0, 0.0, 86, 4, 1),
+                                             (1, 0, 0.0, 84, 4, 2), (2, 1, 0.0, 83, 4, 2)])
+def test_conv1_u8_matches_conv2d(B, act, slope, H, s, p, conv1_form):
     """K25 (the first conv block straight from uint8 frames on fp32 MFMA) == conv2d(K20 frames) + bias + act within
     fp32 summation-order rounding, at the AC_CNN_Atari / Basic_CNN shape (84 x 84 x 4, 8 x 8 stride 4 pad 2 -> 32)."""
     _l, ops = _lib()
@@ -245,10 +257,11 @@ def test_conv1_u8_matches_conv2d(B, act, slope, H, s, p):
     torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=2e-5)
 
 
-def test_conv1_u8_scale_within_one_rounding():
+def test_conv1_u8_scale_within_one_rounding(conv1_form):
     """K25 scales by 1/255 on the weight side (sum x (w / 255)): with one-hot weights (output n reads tap
     (c, ky, kx) = (n % 4, 2 + n // 8, 2 + n % 8 // 4 * 3) with weight 1) every output is x * float32(1 / 255), within
-    one f32 rounding of the reference's float32(x / 255.0) (K20), for all 256 byte values."""
+    one f32 rounding of the reference's float32(x / 255.0) (K20), for all 256 byte values.  K25B (bf16 matrix cores,
+    w / 255 split three ways): within one ulp of x * float32(1 / 255)."""
     _l, ops = _lib()
     B = 8
     x = (torch.arange(B * 84 * 84 * 4, dtype=torch.int64) * 2654435761 % 256).to(torch.uint8).reshape(B, 84, 84, 4)
@@ -268,9 +281,44 @@ def test_conv1_u8_scale_within_one_rounding():
         iy = torch.arange(21) * 4 - 2 + ky   # taps chosen inside the frame for every output position
         ix = torch.arange(21) * 4 - 2 + kx
         xs = xc[:, iy][:, :, ix][..., c].float()
-        assert torch.equal(yc[..., n], xs * torch.tensor(1.0 / 255.0, dtype=torch.float32)), n
-        torch.testing.assert_close(yc[..., n], fc[:, iy][:, :, ix][..., c], rtol=1.2e-7, atol=0)
+        ref = xs * torch.tensor(1.0 / 255.0, dtype=torch.float32)
+        if conv1_form == 0:
+            assert torch.equal(yc[..., n], ref), n
+            torch.testing.assert_close(yc[..., n], fc[:, iy][:, :, ix][..., c], rtol=1.2e-7, atol=0)
+        else:   # K25B: x lo + x mid is exact, the add of x hi rounds in the bf16 MFMA's accumulator (not RNE on
+            # every input): within one ulp of the correctly rounded product
+            ulp = (yc[..., n].view(torch.int32) - ref.view(torch.int32)).abs().max().item()
+            assert ulp <= 1, (n, ulp)
+            torch.testing.assert_close(yc[..., n], fc[:, iy][:, :, ix][..., c], rtol=2.4e-7, atol=0)
     assert len(torch.unique(xc)) == 256
+
+
+def test_conv1_u8_bf16_form_error_vs_fp32_form():
+    """K25B against K25 at the C3 update's row count scale (B = 1024 frames): both within f32 summation-order
+    rounding of the f64 conv, and K25B's error no larger than 2x K25's (the split keeps every term to one rounding)."""
+    _l, ops = _lib()
+    L = ops.lib()
+    B = 1024
+    g = torch.Generator(device="cpu").manual_seed(11)
+    x = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.int32).to(torch.uint8).to(DEV)
+    w = (torch.randn(32, 4, 8, 8, generator=g) * 0.05).to(DEV)
+    b = (torch.randn(32, generator=g) * 0.1).to(DEV)
+    prev = L.xpa_conv1_form(-1)
+    ys = []
+    try:
+        for form in (1, 0):
+            L.xpa_conv1_form((prev & ~1) | form)
+            y = torch.full((B, 21, 21, 32), float("nan"), device=DEV)
+            _l.check(L.xpa_conv1_u8_fwd(0, ops._p(x), B, 84, 84, 4, 8, 4, 2, ops._p(w), ops._p(b), 32, 0.0, ops._p(y),
+                                        ops._stream(DEV)), "conv1_u8")
+            ys.append(y.double())
+    finally:
+        L.xpa_conv1_form(prev)
+    ref = torch.nn.functional.conv2d((x.double() / 255.0).permute(0, 3, 1, 2), w.double(), b.double(), 4,
+                                     2).permute(0, 2, 3, 1)
+    e_b, e_f = (ys[0] - ref).abs().max().item(), (ys[1] - ref).abs().max().item()
+    assert e_b <= 2 * e_f + 1e-7, (e_b, e_f)
+    assert e_b <= 1e-5
 
 
 @pytest.mark.parametrize("B,H,k,s,p", [(7, 21, 4, 2, 1), (64, 21, 4, 2, 1), (3, 20, 4, 2, 0), (5, 19, 4, 2, 3),
@@ -290,8 +338,19 @@ def test_conv_dgrad_s2k_matches_conv2d_input(B, H, k, s, p):
     torch.testing.assert_close(dx.double(), ref.permute(0, 2, 3, 1), rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("B,H,s,p", [(1, 84, 4, 2), (6, 84, 4, 2), (33, 84, 4, 2), (5, 85, 3, 1)])
-def test_conv1_u8_wgrad_matches_conv2d_weight(B, H, s, p):
+@pytest.fixture(params=[2, 0], ids=["k26b", "k26"])
+def conv1_wform(request):
+    """r05: the conv1 weight gradient on the bf16 matrix cores (K26B, the default) and on fp32 MFMA (K26)."""
+    _l, ops = _lib()
+    L = ops.lib()
+    prev = L.xpa_conv1_form(-1)
+    L.xpa_conv1_form((prev & ~2) | request.param)
+    yield request.param
+    L.xpa_conv1_form(prev)
+
+
+@pytest.mark.parametrize("B,H,s,p", [(1, 84, 4, 2), (6, 84, 4, 2), (33, 84, 4, 2), (5, 85, 3, 1), (2, 83, 4, 2)])
+def test_conv1_u8_wgrad_matches_conv2d_weight(B, H, s, p, conv1_wform):
     """K26 partials + the f64 column-sum finalize == torch.nn.grad.conv2d_weight on (x / 255) in float64 (odd row
     counts: the last row pair half empty)."""
     _l, ops = _lib()
@@ -310,7 +369,7 @@ def test_conv1_u8_wgrad_matches_conv2d_weight(B, H, s, p):
 
 
 @pytest.mark.parametrize("act,slope", [(1, 0.0), (1, 0.01), (2, 0.0), (0, 0.0)])
-def test_conv1_u8_wgrad_act_matches_k22_then_k26(act, slope):
+def test_conv1_u8_wgrad_act_matches_k22_then_k26(act, slope, conv1_wform):
     """xpa_conv1_u8_wgrad_act (K26 with the activation backward + bias gradient folded in) == K22 on the conv's output
     then K26: the same weight gradient (bitwise: the same dz values in the same order) and the bias gradient within
     f32 summation-order rounding."""
@@ -341,3 +400,32 @@ def test_conv1_u8_wgrad_act_matches_k22_then_k26(act, slope):
     _l.check(L.xpa_colsum_finalize(ops._p(pw2), G, 8192, ops._p(dw_ref), st), "f")
     assert torch.equal(dw, dw_ref)
     torch.testing.assert_close(db, db_ref, rtol=1e-5, atol=1e-4)
+
+
+def test_conv1_u8_wgrad_bf16_form_error_vs_fp32_form():
+    """K26B against K26 at B = 1024 frames (451 584 rows): both against the f64 weight gradient, K26B's error no larger
+    than 2x K26's (dz split three ways, the frames exact: every product exact in f32)."""
+    _l, ops = _lib()
+    L, st = ops.lib(), ops._stream(DEV)
+    B = 1024
+    g = torch.Generator(device="cpu").manual_seed(12)
+    x = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.int32).to(torch.uint8).to(DEV)
+    dz = torch.randn(B, 21, 21, 32, generator=g).to(DEV)
+    G = int(L.xpa_conv1_u8_wgrad_num_partials())
+    prev = L.xpa_conv1_form(-1)
+    outs = []
+    try:
+        for form in (2, 0):
+            L.xpa_conv1_form((prev & ~2) | form)
+            part = torch.full((G, 8192), float("nan"), device=DEV)
+            _l.check(L.xpa_conv1_u8_wgrad(ops._p(dz), ops._p(x), B, 84, 84, 4, 8, 4, 2, 32, ops._p(part), st), "wgrad")
+            dw = torch.empty(32, 4, 8, 8, device=DEV)
+            _l.check(L.xpa_colsum_finalize(ops._p(part), G, 8192, ops._p(dw), st), "finalize")
+            outs.append(dw.double())
+    finally:
+        L.xpa_conv1_form(prev)
+    ref = torch.nn.grad.conv2d_weight((x.double() / 255.0).permute(0, 3, 1, 2), (32, 4, 8, 8),
+                                      dz.double().permute(0, 3, 1, 2), 4, 2)
+    e_b, e_f = (outs[0] - ref).abs().max().item(), (outs[1] - ref).abs().max().item()
+    assert e_b <= 2 * e_f + 1e-9, (e_b, e_f)
+    assert e_b <= 1e-5 * ref.abs().max().item() + 1e-4

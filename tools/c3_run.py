@@ -11,4 +11,11 @@ if __name__ == "__main__":
     import torch
     it = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 1
     full = "--full" in sys.argv
+    for a in sys.argv[1:]:   # r05 A/B: conv1-form=<mask> (xpa_conv1_form: bit 0 K25B, bit 1 K26B)
+        if a.startswith("conv1-form="):
+            from xuanpolicy_amd import ops
+            ops.lib().xpa_conv1_form(int(a.split("=")[1]))
+    if "--kernels" in sys.argv:
+        print(json.dumps(bench.c3_kernels(torch.device("cuda:0"))))
+        sys.exit(0)
     print(json.dumps(bench.c3_bench(torch.device("cuda:0"), steps=it, warmup=1, cpu=full, kernels=full)))

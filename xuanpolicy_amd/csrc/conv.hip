@@ -14,6 +14,7 @@
 //                            reduction of the conv / fc layers; a fixed grid (<= 2048 blocks) so the f64 finalize
 //                            (xpa_colsum_finalize) reads few partials.  K10's form for conv-sized row counts.
 #include "xpa_common.h"
+#include "s3_split.h"
 
 namespace {
 
@@ -371,6 +372,168 @@ __global__ __launch_bounds__(256, 4) void conv1_u8_fwd_kernel(const unsigned *__
     }
 }
 
+// ---- K25B: K25 on the bf16 matrix cores (r05) ---------------------------------------------------------------------
+// A byte is exact in bf16 (8 significant bits), so the frames need no split: only the weight side w / 255 (f32) is cut
+// into its exact three-way bf16 split (s3_split.h) and a 16-k step is 3 v_mfma_f32_32x32x16_bf16 (lo, mid, hi:
+// smallest first) instead of 8 v_mfma_f32_32x32x2_f32 — 96 against 512 MFMA cycles per 16 k.  Each product
+// x (w / 255)_plane is exact in f32 and x (mid + lo) has at most 24 significant bits, so a single tap's term reaches the
+// accumulator as x (w / 255) rounded once, as in K25; the sum over taps rounds in another (fixed) order.
+// k order: step s (16 k) = pixels 4 s .. 4 s + 3 (kernel row s / 2); lane half h feeds pixels 4 s + 2 h and 4 s + 2 h + 1
+// (a horizontally adjacent pair: one 8-B load in the X2 form) x 4 channels = its 8 k, the byte order of the two
+// dwords.  B image in LDS: [step 16][plane 3][lane 64] x 8 bf16 = 48 KiB, one ds_read_b128 per plane per step shared
+// by the wave's two row tiles.  Block = 8 waves x 64 rows, 2 blocks per CU, grid-stride over row blocks with K25's
+// register ring (chunk = 4 steps = 2 kernel rows).
+constexpr int kC1BRows = 512;
+
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+
+// 8 bytes -> 8 bf16 (each byte's f32 is exact; its bf16 is the f32's top half): v_cvt_f32_ubyte<c> + v_perm_b32
+__device__ __forceinline__ xpa_bf16x8 c1b_bytes(unsigned d0, unsigned d1) {
+    u32x4v r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const unsigned d = q < 2 ? d0 : d1, c = 16 * (q & 1);
+        const unsigned f0 = __float_as_uint((float)((d >> c) & 0xffu));
+        const unsigned f1 = __float_as_uint((float)((d >> (c + 8)) & 0xffu));
+        r[q] = __builtin_amdgcn_perm(f1, f0, 0x07060302u);
+    }
+    return __builtin_bit_cast(xpa_bf16x8, r);
+}
+
+template <bool X2>
+__device__ __forceinline__ void c1b_load_chunk(uint2 (&v)[2][4], const unsigned *const (&xr)[2], const int (&by)[2],
+                                               const int (&bx)[2], int H, int W, int chunk, int h) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int s = 4 * chunk + j, ky = s >> 1, kx = 4 * (s & 1) + 2 * h;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+            const int iy = by[rt] + ky, ix = bx[rt] + kx;
+            const bool yin = (unsigned)iy < (unsigned)H;
+            if (X2) {  // ix even, W even: both pixels in or both out
+                const bool inb = yin && (unsigned)ix < (unsigned)W;
+                const uint2 d = *reinterpret_cast<const uint2 *>(xr[rt] + (inb ? iy * W + ix : 0));
+                v[rt][j].x = inb ? d.x : 0u;
+                v[rt][j].y = inb ? d.y : 0u;
+            } else {
+                const bool in0 = yin && (unsigned)ix < (unsigned)W, in1 = yin && (unsigned)(ix + 1) < (unsigned)W;
+                const unsigned d0 = xr[rt][in0 ? iy * W + ix : 0], d1 = xr[rt][in1 ? iy * W + ix + 1 : 0];
+                v[rt][j].x = in0 ? d0 : 0u;
+                v[rt][j].y = in1 ? d1 : 0u;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void c1b_mfma_chunk(f32x16 (&acc)[2], const uint2 (&v)[2][4], const xpa_bf16x8 *sB,
+                                               int chunk, int lane) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const xpa_bf16x8 *b = sB + (4 * chunk + j) * 3 * 64 + lane;
+        const xpa_bf16x8 bh = b[0], bm = b[64], bl = b[128];
+        xpa_bf16x8 a[2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) a[rt] = c1b_bytes(v[rt][j].x, v[rt][j].y);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rt], bl, acc[rt], 0, 0, 0);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rt], bm, acc[rt], 0, 0, 0);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[rt], bh, acc[rt], 0, 0, 0);
+    }
+}
+
+template <int ACT, bool X2>
+__global__ __launch_bounds__(512, 2) void conv1_u8_fwd_bf16_kernel(const unsigned *__restrict__ x, int64_t rows, int H,
+                                                                   int W, int OH, int OW, int S, int P,
+                                                                   const float *__restrict__ w,
+                                                                   const float *__restrict__ bias, float slope,
+                                                                   float *__restrict__ y) {
+    __shared__ xpa_bf16x8 sB[16 * 3 * 64];  // [step][plane hi, mid, lo][lane]
+    const int t = threadIdx.x;
+    for (int e = t; e < 16 * 64; e += 512) {
+        const int s = e >> 6, l = e & 63, n = l & 31, hh = l >> 5;
+        xpa_bf16x8 ph, pm, pl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int p = 4 * s + 2 * hh + (j >> 2), c = j & 3;
+            __bf16 a, b, cc;
+            xpa_split3(w[((n * 4 + c) * 8 + (p >> 3)) * 8 + (p & 7)] / 255.0f, a, b, cc);
+            ph[j] = a;
+            pm[j] = b;
+            pl[j] = cc;
+        }
+        sB[(s * 3 + 0) * 64 + l] = ph;
+        sB[(s * 3 + 1) * 64 + l] = pm;
+        sB[(s * 3 + 2) * 64 + l] = pl;
+    }
+    __syncthreads();
+    const int lane = t & 63, h = lane >> 5, i = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const float bc = bias[i];
+    const int64_t ohw = (int64_t)OH * OW;
+    auto geometry = [&](int64_t blk, int (&by)[2], int (&bx)[2], const unsigned *(&xr)[2]) {
+        const int64_t r0 = blk * kC1BRows + wave * 64;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+            const int64_t m = r0 + rt * 32 + i;
+            const int64_t mc = m < rows ? m : rows - 1;
+            const int64_t b = mc / ohw;
+            const int rem = (int)(mc - b * ohw);
+            const int oy = rem / OW, ox = rem - (rem / OW) * OW;
+            by[rt] = oy * S - P;
+            bx[rt] = ox * S - P;
+            xr[rt] = x + b * H * W;
+        }
+    };
+    int64_t blk = blockIdx.x;
+    if (blk * kC1BRows >= rows) return;
+    int by[2], bx[2];
+    const unsigned *xr[2];
+    geometry(blk, by, bx, xr);
+    uint2 va[2][4], vb[2][4];
+    c1b_load_chunk<X2>(va, xr, by, bx, H, W, 0, h);
+    c1b_load_chunk<X2>(vb, xr, by, bx, H, W, 1, h);
+    for (;;) {
+        f32x16 acc[2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[rt][r] = 0.f;
+        __builtin_amdgcn_sched_barrier(0);
+        c1b_mfma_chunk(acc, va, sB, 0, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        c1b_load_chunk<X2>(va, xr, by, bx, H, W, 2, h);
+        __builtin_amdgcn_sched_barrier(0);
+        c1b_mfma_chunk(acc, vb, sB, 1, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        c1b_load_chunk<X2>(vb, xr, by, bx, H, W, 3, h);
+        __builtin_amdgcn_sched_barrier(0);
+        c1b_mfma_chunk(acc, va, sB, 2, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        const int64_t r0 = blk * kC1BRows + wave * 64;
+        const int64_t nblk = blk + gridDim.x;
+        const bool more = nblk * kC1BRows < rows;  // block-uniform
+        if (more) {
+            geometry(nblk, by, bx, xr);
+            c1b_load_chunk<X2>(va, xr, by, bx, H, W, 0, h);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        c1b_mfma_chunk(acc, vb, sB, 3, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) c1b_load_chunk<X2>(vb, xr, by, bx, H, W, 1, h);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t m = r0 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m < rows) y[m * 32 + i] = act_fwd<ACT>(acc[rt][r] + bc, slope);
+            }
+        if (!more) break;
+        blk = nblk;
+    }
+}
+
 // ---- K27: data gradient of a stride-s, 2s x 2s conv (the Nature CNN's second conv: 4 x 4 stride 2, 32 -> 64) ------
 // dX[b, iy, ix, n] = sum_{ky, kx, co} dY[b, oy, ox, co] W[co, n, ky, kx] over iy = oy s - P + ky, ix likewise.  With a
 // 2s kernel every input pixel takes exactly the taps (oy0 - dy, ky0 + dy s) x (ox0 - dx, kx0 + dx s), dy, dx in
@@ -678,6 +841,164 @@ __global__ __launch_bounds__(256, 2) void conv1_u8_wgrad_kernel(const float *__r
                 pr[(n * 4 + c) * 64 + (X2 ? 2 * j + g : 32 * g + j)] = acc[4 * g + c][r] / 255.0f;
             }
 }
+
+// ---- K26B: K26 on the bf16 matrix cores (r05) -------------------------------------------------------------------
+// The same [32 n] x [256 taps] product over rows with the MFMA's k = 16 rows (v_mfma_f32_32x32x16_bf16): lane (h, j)
+// owns rows 16 s + 8 h + u (u < 8) of step s — A = dz^T (dz[row][n = j], cut into its exact three-way bf16 split:
+// 3 products), B = the frames (byte c of the pixel dwords of those 8 rows, exact in bf16) — so a step is 8 tiles x 3
+// MFMAs against K26's 8 row pairs x 8 tiles of v_mfma_f32_32x32x2_f32 (768 against 4096 MFMA cycles per 16 rows).
+// Each product is exact in f32; the sum over rows rounds in another fixed order than K26's.  The accumulator layout,
+// the in-order wave reduction, the bias partials and the partial layout are K26's.
+template <bool X2, int ACT>
+__global__ __launch_bounds__(256, 2) void conv1_u8_wgrad_bf16_kernel(const float *__restrict__ dz,
+                                                                     const unsigned *__restrict__ x, int64_t rows, int H,
+                                                                     int W, int OH, int OW, int S, int P,
+                                                                     float *__restrict__ partial,
+                                                                     const float *__restrict__ y, float slope,
+                                                                     float *__restrict__ bias_partial) {
+    __shared__ __attribute__((aligned(16))) float s_red[64 * 16 * 8];
+    float bsum = 0.f;
+    const int t = threadIdx.x, lane = t & 63, h = lane >> 5, j = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int64_t steps = (rows + 15) / 16, nw = (int64_t)gridDim.x * 4, gw = (int64_t)blockIdx.x * 4 + wave;
+    const int64_t s0 = steps * gw / nw, s1 = steps * (gw + 1) / nw;
+    f32x16 acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+    int64_t m = 16 * s0 + 8 * h;
+    const int64_t ohw = (int64_t)OH * OW;
+    const int64_t mc0 = m < rows ? m : 0;
+    int64_t b = mc0 / ohw;
+    int rem = (int)(mc0 - b * ohw);
+    int oy = rem / OW, ox = rem - (rem / OW) * OW;
+    const int ky0 = X2 ? (j >> 2) : (j >> 3), kx = X2 ? 2 * (j & 3) : (j & 7);
+    auto advance = [&](int n) {
+        m += n;
+        ox += n;
+        while (ox >= OW) {
+            ox -= OW;
+            if (++oy >= OH) {
+                oy = 0;
+                ++b;
+            }
+        }
+    };
+    float an[8];
+    uint2 dn[8];
+    auto load_step = [&]() {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const bool mv = m < rows;
+            float a = dz[(mv ? m : 0) * 32 + j];
+            if (ACT >= 0) a = act_grad<ACT>(a, y[(mv ? m : 0) * 32 + j], slope);
+            if (X2) {
+                const int iy = oy * S - P + ky0, ix = ox * S - P + kx;
+                const bool inb = mv && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+                const uint2 v = *reinterpret_cast<const uint2 *>(x + ((mv ? b : 0) * H + (inb ? iy : 0)) * W +
+                                                                 (inb ? ix : 0));
+                dn[u].x = inb ? v.x : 0u;
+                dn[u].y = inb ? v.y : 0u;
+            } else {
+                unsigned v2[2];
+#pragma unroll
+                for (int g = 0; g < 2; ++g) {
+                    const int iy = oy * S - P + 4 * g + ky0, ix = ox * S - P + kx;
+                    const bool inb = mv && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+                    const unsigned v = x[((mv ? b : 0) * H + (inb ? iy : 0)) * W + (inb ? ix : 0)];
+                    v2[g] = inb ? v : 0u;
+                }
+                dn[u].x = v2[0];
+                dn[u].y = v2[1];
+            }
+            an[u] = mv ? a : 0.f;
+            advance(1);
+        }
+        advance(8);  // the other half's 8 rows
+    };
+    if (s0 < s1) load_step();
+    for (int64_t st = s0; st < s1; ++st) {
+        float a[8];
+        uint2 d[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            a[u] = an[u];
+            d[u] = dn[u];
+        }
+        if (st + 1 < s1) load_step();
+        if (ACT >= 0) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) bsum += a[u];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        xpa_bf16x8 ah, am, al;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            __bf16 p, q, r;
+            xpa_split3(a[u], p, q, r);
+            ah[u] = p;
+            am[u] = q;
+            al[u] = r;
+        }
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                u32x4v bb;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const unsigned d0 = g ? d[2 * q].y : d[2 * q].x, d1 = g ? d[2 * q + 1].y : d[2 * q + 1].x;
+                    const unsigned f0 = __float_as_uint((float)((d0 >> (8 * c)) & 0xffu));
+                    const unsigned f1 = __float_as_uint((float)((d1 >> (8 * c)) & 0xffu));
+                    bb[q] = __builtin_amdgcn_perm(f1, f0, 0x07060302u);
+                }
+                const xpa_bf16x8 bv = __builtin_bit_cast(xpa_bf16x8, bb);
+                f32x16 &ac = acc[4 * g + c];
+                ac = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bv, ac, 0, 0, 0);
+                ac = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bv, ac, 0, 0, 0);
+                ac = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bv, ac, 0, 0, 0);
+            }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (ACT >= 0) {
+        __shared__ float s_b[4][64];
+        s_b[wave][lane] = bsum;
+        __syncthreads();
+        if (t < 32) {
+            float tb = 0.f;
+            for (int w = 0; w < 4; ++w) tb += s_b[w][t] + s_b[w][t + 32];
+            bias_partial[(int64_t)blockIdx.x * 32 + t] = tb;
+        }
+    }
+    for (int src = 1; src < 4; ++src) {
+        __syncthreads();
+        if (wave == src) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) s_red[(q * 16 + r) * 64 + lane] = acc[q][r];
+        }
+        __syncthreads();
+        if (wave == 0) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[q][r] += s_red[(q * 16 + r) * 64 + lane];
+        }
+    }
+    if (wave != 0) return;
+    float *pr = partial + (int64_t)blockIdx.x * 8192;
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = (r & 3) + 8 * (r >> 2) + 4 * h;
+                pr[(n * 4 + c) * 64 + (X2 ? 2 * j + g : 32 * g + j)] = acc[4 * g + c][r] / 255.0f;
+            }
+}
 }  // namespace
 
 XPA_API int xpa_frames_to_f32(const uint8_t *src, int64_t n, float *dst, xpa_stream_t stream) {
@@ -778,6 +1099,15 @@ XPA_API int xpa_maxpool_act_bwd_bias(int act, const float *dout, const int32_t *
     return xpa_launch_status();
 }
 
+// r05: bit 0 = K25B (the conv1 forward on the bf16 matrix cores), bit 1 = K26B (its weight gradient likewise); a
+// cleared bit selects the fp32-MFMA form.  Returns the previous mask.
+static int g_conv1_bf16 = 3;
+XPA_API int xpa_conv1_form(int mask) {
+    const int prev = g_conv1_bf16;
+    if (mask >= 0) g_conv1_bf16 = mask;
+    return prev;
+}
+
 XPA_API int xpa_conv1_u8_fwd(int act, const uint8_t *x, int64_t batch, int64_t height, int64_t width, int64_t channels,
                              int64_t kernel, int64_t stride, int64_t pad, const float *w, const float *bias,
                              int64_t out_channels, float slope, float *y, xpa_stream_t stream) {
@@ -787,10 +1117,26 @@ XPA_API int xpa_conv1_u8_fwd(int act, const uint8_t *x, int64_t batch, int64_t h
         return (int)hipErrorInvalidValue;
     const int64_t OH = (height + 2 * pad - kernel) / stride + 1, OW = (width + 2 * pad - kernel) / stride + 1;
     const int64_t rows = batch * OH * OW;
-    const int64_t blocks = (rows + kC1Rows - 1) / kC1Rows;
-    const dim3 grid((unsigned)(blocks < 1024 ? blocks : 1024)), block(256);
     hipStream_t s = (hipStream_t)stream;
     const bool x2 = width % 2 == 0 && stride % 2 == 0 && pad % 2 == 0 && (uintptr_t)x % 8 == 0;
+    if (g_conv1_bf16 & 1) {  // K25B
+        const int64_t blocks = (rows + kC1BRows - 1) / kC1BRows;
+        const dim3 grid((unsigned)(blocks < 512 ? blocks : 512)), block(512);
+#define XPA_C1B(A_)                                                                                                  \
+    if (x2)                                                                                                          \
+        hipLaunchKernelGGL((conv1_u8_fwd_bf16_kernel<A_, true>), grid, block, 0, s, (const unsigned *)x, rows,        \
+                           (int)height, (int)width, (int)OH, (int)OW, (int)stride, (int)pad, w, bias, slope, y);     \
+    else                                                                                                             \
+        hipLaunchKernelGGL((conv1_u8_fwd_bf16_kernel<A_, false>), grid, block, 0, s, (const unsigned *)x, rows,       \
+                           (int)height, (int)width, (int)OH, (int)OW, (int)stride, (int)pad, w, bias, slope, y)
+        if (act == 0) XPA_C1B(0);
+        else if (act == 1) XPA_C1B(1);
+        else XPA_C1B(2);
+#undef XPA_C1B
+        return xpa_launch_status();
+    }
+    const int64_t blocks = (rows + kC1Rows - 1) / kC1Rows;
+    const dim3 grid((unsigned)(blocks < 1024 ? blocks : 1024)), block(256);
 #define XPA_C1(A_)                                                                                                   \
     if (x2)                                                                                                          \
         hipLaunchKernelGGL((conv1_u8_fwd_kernel<A_, true>), grid, block, 0, s, (const unsigned *)x, rows,             \
@@ -848,10 +1194,16 @@ XPA_API int xpa_conv1_u8_wgrad_act(int act, const float *dz, const float *y, flo
     const int64_t OH = (height + 2 * pad - kernel) / stride + 1, OW = (width + 2 * pad - kernel) / stride + 1;
     const bool x2 = width % 2 == 0 && stride % 2 == 0 && pad % 2 == 0 && (uintptr_t)x % 8 == 0;
     hipStream_t s = (hipStream_t)stream;
+    const bool bf = (g_conv1_bf16 & 2) != 0;  // K26B
 #define XPA_WG(X_, A_)                                                                                             \
-    hipLaunchKernelGGL((conv1_u8_wgrad_kernel<X_, A_>), dim3(kWgBlocks), dim3(256), 0, s, dz, (const unsigned *)x, \
-                       batch * OH * OW, (int)height, (int)width, (int)OH, (int)OW, (int)stride, (int)pad, partial, y, \
-                       slope, bias_partial)
+    if (bf)                                                                                                        \
+        hipLaunchKernelGGL((conv1_u8_wgrad_bf16_kernel<X_, A_>), dim3(kWgBlocks), dim3(256), 0, s, dz,             \
+                           (const unsigned *)x, batch * OH * OW, (int)height, (int)width, (int)OH, (int)OW,         \
+                           (int)stride, (int)pad, partial, y, slope, bias_partial);                                 \
+    else                                                                                                           \
+        hipLaunchKernelGGL((conv1_u8_wgrad_kernel<X_, A_>), dim3(kWgBlocks), dim3(256), 0, s, dz,                  \
+                           (const unsigned *)x, batch * OH * OW, (int)height, (int)width, (int)OH, (int)OW,         \
+                           (int)stride, (int)pad, partial, y, slope, bias_partial)
 #define XPA_WG_A(X_)                \
     if (act < 0) XPA_WG(X_, -1);    \
     else if (act == 0) XPA_WG(X_, 0); \
