@@ -666,15 +666,21 @@ def c3_kernels(device, batch=16384):
     f_us, w_us = {}, {}
     try:
         for bit, tag in ((1, "bf16"), (0, "f32")):   # r05: K25B / K26B (bf16 matrix cores) and the fp32-MFMA forms
-            L.xpa_conv1_form(3 if bit else 0)
+            L.xpa_conv1_form((form0 & ~3) | (3 if bit else 0))
             f_us[tag] = timed(lambda: _lib.check(L.xpa_conv1_u8_fwd(1, ops._p(x), batch, 84, 84, 4, 8, 4, 2, ops._p(w1),
                                                                     ops._p(b1), 32, 0.0, ops._p(y1), st), "conv1_u8_fwd"))
             w_us[tag] = timed(lambda: _lib.check(L.xpa_conv1_u8_wgrad(ops._p(g), ops._p(x), batch, 84, 84, 4, 8, 4, 2, 32,
                                                                       ops._p(wpart), st), "conv1_u8_wgrad"))
     finally:
         L.xpa_conv1_form(form0)
-    d_us = timed(lambda: _lib.check(L.xpa_conv_dgrad_s2k(ops._p(dy2), batch, 10, 10, 64, ops._p(w2), 32, 4, 2, 1, 21,
-                                                         21, ops._p(dx2), st), "conv_dgrad_s2k"))
+    d_us = {}
+    try:
+        for bit, tag in ((4, "bf16"), (0, "f32")):   # r05: K27B and the fp32-MFMA K27
+            L.xpa_conv1_form((form0 & ~4) | bit)
+            d_us[tag] = timed(lambda: _lib.check(L.xpa_conv_dgrad_s2k(ops._p(dy2), batch, 10, 10, 64, ops._p(w2), 32, 4,
+                                                                      2, 1, 21, 21, ops._p(dx2), st), "conv_dgrad_s2k"))
+    finally:
+        L.xpa_conv1_form(form0)
     b_us = timed(lambda: _lib.check(L.xpa_act_bwd_bias(1, ops._p(g), ops._p(h), rows, C, 0.0, ops._p(g), ops._p(part),
                                                        st), "act_bwd_bias"))
     c1_flops = 2.0 * rows * 256 * 32            # [rows, 8*8*4] x [256, 32]
@@ -686,7 +692,8 @@ def c3_kernels(device, batch=16384):
                 "achieved": round(flops / us / 1e6, 1), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(flops / us / 1e6 / FP32_MFMA_PEAK_TFLOPS, 4), "shape": shape}
     def bf16(name, us, flops, shape, planes=3):
-        # the frames are exact in bf16: `planes` bf16 products per f32 product, priced on the bf16 matrix peak
+        # `planes` bf16 products per f32 product (3: the frames are exact in bf16; 6: both operands split), priced on
+        # the bf16 matrix peak
         r = {"kernel": name, "bound": "mfma", "avg_launch_us": round(us, 2), "flops_per_launch": flops * planes,
              "achieved": round(flops * planes / us / 1e6, 1), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
              "frac": round(flops * planes / us / 1e6 / BF16_MFMA_PEAK_TFLOPS, 4), "shape": shape,
@@ -701,8 +708,10 @@ def c3_kernels(device, batch=16384):
             "conv1_u8_wgrad": bf16("xpa_conv1_u8_wgrad (K26B: 3 bf16 products, the dz split; partials + f64 "
                                    "finalize)", w_us["bf16"], c1_flops, c1w),
             "conv1_u8_wgrad_f32": mfma("xpa_conv1_u8_wgrad (K26, fp32 MFMA form)", w_us["f32"], c1_flops, c1w),
-            "conv_dgrad_s2k": mfma("xpa_conv_dgrad_s2k (K27)", d_us, c2_flops,
-                                   "dX [B, 21, 21, 32] from dY [B, 10, 10, 64], 4x4 s2 p1"),
+            "conv_dgrad_s2k": bf16("xpa_conv_dgrad_s2k (K27B: 6 bf16 products, both operands split)", d_us["bf16"],
+                                   c2_flops, "dX [B, 21, 21, 32] from dY [B, 10, 10, 64], 4x4 s2 p1", planes=6),
+            "conv_dgrad_s2k_f32": mfma("xpa_conv_dgrad_s2k (K27, fp32 MFMA form)", d_us["f32"], c2_flops,
+                                       "dX [B, 21, 21, 32] from dY [B, 10, 10, 64], 4x4 s2 p1"),
             "act_bwd_bias": {"kernel": "xpa_act_bwd_bias (K22, ReLU)", "bound": "hbm", "avg_launch_us": round(b_us, 2),
                              "algorithmic_bytes_per_launch": int(bb), "achieved": round(bb / b_us / 1e3, 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(bb / b_us / 1e3 / HBM_PEAK_GBS, 4),

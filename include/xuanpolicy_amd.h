@@ -874,9 +874,11 @@ int xpa_thin_linear_act_bwd(int act, const float *g, int64_t ldg, const float *h
  * K20: dst[i] = float32(src[i] / 255.0) with the reference's arithmetic (NumPy float64 division, then the
  * float32 cast; cnn.py:89-92), bit for bit; n bytes in, n floats out (16-B aligned buffers take the vector path). */
 int xpa_frames_to_f32(const uint8_t *src, int64_t n, float *dst, xpa_stream_t stream);
-/* r05: the conv1 kernels' arithmetic — bit 0: K25B (forward), bit 1: K26B (weight gradient) on the bf16 matrix cores
- * with the frames exact and the f32 operand split three ways; a cleared bit selects the fp32-MFMA form (K25 / K26).
- * mask < 0 only reads.  Returns the previous mask (default 3). */
+/* r05: the conv kernels' arithmetic — bit 0: K25B (conv1 forward), bit 1: K26B (conv1 weight gradient) on the bf16
+ * matrix cores with the frames exact and the f32 operand split three ways; bit 2: K27B (xpa_conv_dgrad_s2k) with both
+ * operands split three ways (six products, f32-GEMM accuracy).  A cleared bit selects the fp32-MFMA form (K25 / K26 /
+ * K27); so does an operand of 2^31 bytes or more (the bf16 forms read through one buffer record).  mask < 0 only
+ * reads.  Returns the previous mask (default 7). */
 int xpa_conv1_form(int mask);
 /* K25 — the first conv block straight from the uint8 frames (C3 AC_CNN_Atari / C5 Basic_CNN: cnn_block
  * xuance/torch/utils/layers.py:36-57 on observations / 255.0, cnn.py:89-92): y = act(conv2d(x / 255, w, stride, pad)

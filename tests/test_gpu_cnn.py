@@ -321,9 +321,20 @@ def test_conv1_u8_bf16_form_error_vs_fp32_form():
     assert e_b <= 1e-5
 
 
+@pytest.fixture(params=[4, 0], ids=["k27b", "k27"])
+def dgrad_form(request):
+    """r05: the conv2 data gradient on the bf16 matrix cores (K27B, the default) and on fp32 MFMA (K27)."""
+    _l, ops = _lib()
+    L = ops.lib()
+    prev = L.xpa_conv1_form(-1)
+    L.xpa_conv1_form((prev & ~4) | request.param)
+    yield request.param
+    L.xpa_conv1_form(prev)
+
+
 @pytest.mark.parametrize("B,H,k,s,p", [(7, 21, 4, 2, 1), (64, 21, 4, 2, 1), (3, 20, 4, 2, 0), (5, 19, 4, 2, 3),
-                                       (2, 9, 2, 1, 0), (4, 11, 2, 1, 1)])
-def test_conv_dgrad_s2k_matches_conv2d_input(B, H, k, s, p):
+                                       (2, 9, 2, 1, 0), (4, 11, 2, 1, 1), (1, 21, 4, 2, 1)])
+def test_conv_dgrad_s2k_matches_conv2d_input(B, H, k, s, p, dgrad_form):
     """K27 (data gradient of a 2s x 2s stride-s conv, 32 -> 64 channels, one implicit GEMM per residue class) ==
     torch.nn.grad.conv2d_input in float64, odd / even sizes, padding 0 .. 3 and stride 1 included."""
     _l, ops = _lib()
@@ -429,3 +440,30 @@ def test_conv1_u8_wgrad_bf16_form_error_vs_fp32_form():
     e_b, e_f = (outs[0] - ref).abs().max().item(), (outs[1] - ref).abs().max().item()
     assert e_b <= 2 * e_f + 1e-9, (e_b, e_f)
     assert e_b <= 1e-5 * ref.abs().max().item() + 1e-4
+
+
+def test_conv_dgrad_s2k_bf16_form_error_vs_fp32_form():
+    """K27B against K27 at B = 2048 (the C3 conv2 shape): both against the f64 data gradient, K27B's error no larger
+    than 2x K27's (the six-product split: f32-GEMM accuracy)."""
+    _l, ops = _lib()
+    L = ops.lib()
+    B = 2048
+    g = torch.Generator(device="cpu").manual_seed(13)
+    dy = torch.randn(B, 10, 10, 64, generator=g).to(DEV)
+    w = (torch.randn(64, 32, 4, 4, generator=g) * 0.1).to(DEV)
+    prev = L.xpa_conv1_form(-1)
+    outs = []
+    try:
+        for form in (4, 0):
+            L.xpa_conv1_form((prev & ~4) | form)
+            dx = torch.full((B, 21, 21, 32), float("nan"), device=DEV)
+            _l.check(L.xpa_conv_dgrad_s2k(ops._p(dy), B, 10, 10, 64, ops._p(w), 32, 4, 2, 1, 21, 21, ops._p(dx),
+                                          ops._stream(DEV)), "dgrad")
+            outs.append(dx.double())
+    finally:
+        L.xpa_conv1_form(prev)
+    ref = torch.nn.grad.conv2d_input((B, 32, 21, 21), w.double(), dy.double().permute(0, 3, 1, 2), 2, 1)
+    ref = ref.permute(0, 2, 3, 1)
+    e_b, e_f = (outs[0] - ref).abs().max().item(), (outs[1] - ref).abs().max().item()
+    assert e_b <= 2 * e_f + 1e-9, (e_b, e_f)
+    assert e_b <= 1e-5

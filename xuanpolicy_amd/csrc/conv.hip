@@ -82,6 +82,7 @@ __global__ __launch_bounds__(256) void bias_act_kernel(f4v *__restrict__ y, int6
 
 template <int ACT>
 __device__ __forceinline__ float act_grad(float dh, float h, float slope) {
+#pragma clang fp contract(off)  // no product here fuses into its consumer (K26B's split): one value per input everywhere
     if (ACT == 1) return h > 0.f ? dh : dh * slope;  // mask from the OUTPUT: h > 0 <=> z > 0 for slope >= 0
     if (ACT == 2) return dh * (1.0f - h * h);
     return dh;
@@ -400,9 +401,11 @@ __device__ __forceinline__ xpa_bf16x8 c1b_bytes(unsigned d0, unsigned d1) {
     return __builtin_bit_cast(xpa_bf16x8, r);
 }
 
+// Range-checked buffer loads (a tap outside the frame gets an offset past the record count: the hardware returns
+// zeros), so no select consumes a load and the wait for chunk c + 1 lands after chunk c's MFMAs.
 template <bool X2>
-__device__ __forceinline__ void c1b_load_chunk(uint2 (&v)[2][4], const unsigned *const (&xr)[2], const int (&by)[2],
-                                               const int (&bx)[2], int H, int W, int chunk, int h) {
+__device__ __forceinline__ void c1b_load_chunk(uint2 (&v)[2][4], __amdgpu_buffer_rsrc_t rx, const int (&xo)[2],
+                                               const int (&by)[2], const int (&bx)[2], int H, int W, int chunk, int h) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int s = 4 * chunk + j, ky = s >> 1, kx = 4 * (s & 1) + 2 * h;
@@ -410,16 +413,14 @@ __device__ __forceinline__ void c1b_load_chunk(uint2 (&v)[2][4], const unsigned 
         for (int rt = 0; rt < 2; ++rt) {
             const int iy = by[rt] + ky, ix = bx[rt] + kx;
             const bool yin = (unsigned)iy < (unsigned)H;
+            const int o = xo[rt] + (iy * W + ix) * 4;
             if (X2) {  // ix even, W even: both pixels in or both out
                 const bool inb = yin && (unsigned)ix < (unsigned)W;
-                const uint2 d = *reinterpret_cast<const uint2 *>(xr[rt] + (inb ? iy * W + ix : 0));
-                v[rt][j].x = inb ? d.x : 0u;
-                v[rt][j].y = inb ? d.y : 0u;
+                v[rt][j] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rx, inb ? o : INT32_MIN, 0, 0));
             } else {
                 const bool in0 = yin && (unsigned)ix < (unsigned)W, in1 = yin && (unsigned)(ix + 1) < (unsigned)W;
-                const unsigned d0 = xr[rt][in0 ? iy * W + ix : 0], d1 = xr[rt][in1 ? iy * W + ix + 1 : 0];
-                v[rt][j].x = in0 ? d0 : 0u;
-                v[rt][j].y = in1 ? d1 : 0u;
+                v[rt][j].x = __builtin_amdgcn_raw_buffer_load_b32(rx, in0 ? o : INT32_MIN, 0, 0);
+                v[rt][j].y = __builtin_amdgcn_raw_buffer_load_b32(rx, in1 ? o + 4 : INT32_MIN, 0, 0);
             }
         }
     }
@@ -472,7 +473,10 @@ __global__ __launch_bounds__(512, 2) void conv1_u8_fwd_bf16_kernel(const unsigne
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const float bc = bias[i];
     const int64_t ohw = (int64_t)OH * OW;
-    auto geometry = [&](int64_t blk, int (&by)[2], int (&bx)[2], const unsigned *(&xr)[2]) {
+    // the frames as one buffer record (the entry guarantees < 2^31 bytes)
+    const int nb = (int)(((rows - 1) / ohw + 1) * H * W * 4);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned *>(x), 0, nb, 0x00020000);
+    auto geometry = [&](int64_t blk, int (&by)[2], int (&bx)[2], int (&xr)[2]) {
         const int64_t r0 = blk * kC1BRows + wave * 64;
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
@@ -483,17 +487,16 @@ __global__ __launch_bounds__(512, 2) void conv1_u8_fwd_bf16_kernel(const unsigne
             const int oy = rem / OW, ox = rem - (rem / OW) * OW;
             by[rt] = oy * S - P;
             bx[rt] = ox * S - P;
-            xr[rt] = x + b * H * W;
+            xr[rt] = (int)(b * H * W * 4);
         }
     };
     int64_t blk = blockIdx.x;
     if (blk * kC1BRows >= rows) return;
-    int by[2], bx[2];
-    const unsigned *xr[2];
+    int by[2], bx[2], xr[2];
     geometry(blk, by, bx, xr);
     uint2 va[2][4], vb[2][4];
-    c1b_load_chunk<X2>(va, xr, by, bx, H, W, 0, h);
-    c1b_load_chunk<X2>(vb, xr, by, bx, H, W, 1, h);
+    c1b_load_chunk<X2>(va, rx, xr, by, bx, H, W, 0, h);
+    c1b_load_chunk<X2>(vb, rx, xr, by, bx, H, W, 1, h);
     for (;;) {
         f32x16 acc[2];
 #pragma unroll
@@ -503,11 +506,11 @@ __global__ __launch_bounds__(512, 2) void conv1_u8_fwd_bf16_kernel(const unsigne
         __builtin_amdgcn_sched_barrier(0);
         c1b_mfma_chunk(acc, va, sB, 0, lane);
         __builtin_amdgcn_sched_barrier(0);
-        c1b_load_chunk<X2>(va, xr, by, bx, H, W, 2, h);
+        c1b_load_chunk<X2>(va, rx, xr, by, bx, H, W, 2, h);
         __builtin_amdgcn_sched_barrier(0);
         c1b_mfma_chunk(acc, vb, sB, 1, lane);
         __builtin_amdgcn_sched_barrier(0);
-        c1b_load_chunk<X2>(vb, xr, by, bx, H, W, 3, h);
+        c1b_load_chunk<X2>(vb, rx, xr, by, bx, H, W, 3, h);
         __builtin_amdgcn_sched_barrier(0);
         c1b_mfma_chunk(acc, va, sB, 2, lane);
         __builtin_amdgcn_sched_barrier(0);
@@ -516,12 +519,12 @@ __global__ __launch_bounds__(512, 2) void conv1_u8_fwd_bf16_kernel(const unsigne
         const bool more = nblk * kC1BRows < rows;  // block-uniform
         if (more) {
             geometry(nblk, by, bx, xr);
-            c1b_load_chunk<X2>(va, xr, by, bx, H, W, 0, h);
+            c1b_load_chunk<X2>(va, rx, xr, by, bx, H, W, 0, h);
         }
         __builtin_amdgcn_sched_barrier(0);
         c1b_mfma_chunk(acc, vb, sB, 3, lane);
         __builtin_amdgcn_sched_barrier(0);
-        if (more) c1b_load_chunk<X2>(vb, xr, by, bx, H, W, 1, h);
+        if (more) c1b_load_chunk<X2>(vb, rx, xr, by, bx, H, W, 1, h);
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
@@ -682,6 +685,125 @@ __global__ __launch_bounds__(256, 2) void conv_dgrad_s2k_kernel(const float *__r
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
             // every lane learns the output offsets of its 16 rows from the row owners (lane i, h = 0)
+            __builtin_amdgcn_wave_barrier();
+            if (h == 0) s_orow[wave][i] = cur.orow[rt];
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int64_t o = s_orow[wave][row];
+                if (o >= 0) dx[o * 32 + i] = acc[rt][r];
+            }
+        }
+        if (more) cur = nxt;
+    }
+}
+
+// ---- K27B: K27 on the bf16 matrix cores (r05) -------------------------------------------------------------------
+// The same residue-class implicit GEMMs with both operands f32: dY split three ways in registers, the class's weight
+// operand split three ways into an LDS image [step 16][plane 3][lane 64] x 8 bf16 (48 KiB), six products per 16-k
+// step (s3_split.h: f32-GEMM accuracy).  Step s = (tap s / 4, channels 16 (s % 4) .. + 15); lane half h feeds channels
+// 16 (s % 4) + 8 h .. + 7 — two adjacent dY quads (32 B).  A chunk (tap, half of its 64 channels) is 2 steps; K27's
+// ring, persistent tile ranges and output scatter are unchanged.  4 x 6 MFMAs of 32 cycles per (tap, half) and row tile
+// against K27's 16 x 64.
+// dY through a range-checked buffer record (a tap outside the map reads zeros: no select consumes a load)
+__device__ __forceinline__ void dgrad_b_load_chunk(f4v (&v)[2][4], __amdgpu_buffer_rsrc_t rdy, const DgradRows &q,
+                                                   int tap, int half, int h) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c4 = 4 * (2 * half + (j >> 1)) + 2 * h + (j & 1);  // channel quad
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+            const int o = q.ok[rt][tap] ? 4 * (q.off[rt][tap] + 4 * c4) : INT32_MIN;
+            v[rt][j] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rdy, o, 0, 0));
+        }
+    }
+}
+
+__device__ __forceinline__ void dgrad_b_mfma_chunk(f32x16 (&acc)[2], const f4v (&v)[2][4], const xpa_bf16x8 *sB,
+                                                   int tap, int half, int lane) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const xpa_bf16x8 *b = sB + (4 * tap + 2 * half + k) * 3 * 64 + lane;
+        const xpa_bf16x8 bh = b[0], bm = b[64], bl = b[128];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+            xpa_bf16x8 ah, am, al;
+            const f4v q0 = v[rt][2 * k], q1 = v[rt][2 * k + 1];
+            xpa_split8(float4{q0[0], q0[1], q0[2], q0[3]}, float4{q1[0], q1[1], q1[2], q1[3]}, ah, am, al);
+            acc[rt] = xpa_mfma_s3(ah, am, al, bh, bm, bl, acc[rt]);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256, 2) void conv_dgrad_s2k_bf16_kernel(const float *__restrict__ dy,
+                                                                     const float *__restrict__ w, DgradGeom g,
+                                                                     float *__restrict__ dx) {
+    __shared__ xpa_bf16x8 sB[16 * 3 * 64];  // [step][plane hi, mid, lo][lane]
+    __shared__ int64_t s_orow[4][32];
+    const int t = threadIdx.x;
+    const int lane = t & 63, h = lane >> 5, i = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int64_t T = g.tiles[3];
+    const int64_t t0 = T * blockIdx.x / gridDim.x, t1 = T * (blockIdx.x + 1) / gridDim.x;
+    if (t0 >= t1) return;
+    const int K = 2 * g.S;
+    int staged = -1;
+    const __amdgpu_buffer_rsrc_t rdy = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(dy), 0, (int)(g.B * g.OH * g.OW * 256), 0x00020000);  // the entry: < 2^31 bytes
+    DgradRows cur, nxt;
+    dgrad_rows(g, t0, wave, i, cur);
+    f4v va[2][4], vb[2][4];
+    dgrad_b_load_chunk(va, rdy, cur, 0, 0, h);
+    for (int64_t tile = t0; tile < t1; ++tile) {
+        const int cls = dgrad_class(g, tile);
+        if (cls != staged) {  // block-uniform
+            const int ry = cls >> 1, rx = cls & 1;
+            __syncthreads();
+            for (int e = t; e < 16 * 64; e += 256) {  // W [64 co][32 n][K][K] -> B[k = (tap, co)][n]
+                const int s = e >> 6, l = e & 63, n = l & 31, hh = l >> 5, tap = s >> 2;
+                const int ky = ry + (tap >> 1) * g.S, kx = rx + (tap & 1) * g.S;
+                xpa_bf16x8 ph, pm, pl;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int co = 16 * (s & 3) + 8 * hh + u;
+                    __bf16 a, b, c;
+                    xpa_split3(w[((co * 32 + n) * K + ky) * K + kx], a, b, c);
+                    ph[u] = a;
+                    pm[u] = b;
+                    pl[u] = c;
+                }
+                sB[(s * 3 + 0) * 64 + l] = ph;
+                sB[(s * 3 + 1) * 64 + l] = pm;
+                sB[(s * 3 + 2) * 64 + l] = pl;
+            }
+            __syncthreads();
+            staged = cls;
+        }
+        const bool more = tile + 1 < t1;
+        f32x16 acc[2];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[rt][r] = 0.f;
+#pragma unroll
+        for (int tap = 0; tap < 4; ++tap) {
+            dgrad_b_load_chunk(vb, rdy, cur, tap, 1, h);
+            __builtin_amdgcn_sched_barrier(0);
+            dgrad_b_mfma_chunk(acc, va, sB, tap, 0, lane);
+            __builtin_amdgcn_sched_barrier(0);
+            if (tap + 1 < 4) {
+                dgrad_b_load_chunk(va, rdy, cur, tap + 1, 0, h);
+            } else if (more) {
+                dgrad_rows(g, tile + 1, wave, i, nxt);
+                dgrad_b_load_chunk(va, rdy, nxt, 0, 0, h);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            dgrad_b_mfma_chunk(acc, vb, sB, tap, 1, lane);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
             __builtin_amdgcn_wave_barrier();
             if (h == 0) s_orow[wave][i] = cur.orow[rt];
             __builtin_amdgcn_wave_barrier();
@@ -885,34 +1007,40 @@ __global__ __launch_bounds__(256, 2) void conv1_u8_wgrad_bf16_kernel(const float
             }
         }
     };
-    float an[8];
+    // range-checked buffer loads (rows past the end and taps outside the frame read zeros; the entry guarantees
+    // < 2^31 bytes per record), raw dz / y kept in the ring: no VALU op consumes a load before the next step's MFMAs
+    const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(dz), 0,
+                                                                        (int)(rows * 128), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ryy = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(ACT >= 0 ? y : dz), 0,
+                                                                         (int)(rows * 128), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned *>(x), 0, (int)(((rows - 1) / ohw + 1) * H * W * 4), 0x00020000);
+    float an[8], yn[8];
     uint2 dn[8];
     auto load_step = [&]() {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const bool mv = m < rows;
-            float a = dz[(mv ? m : 0) * 32 + j];
-            if (ACT >= 0) a = act_grad<ACT>(a, y[(mv ? m : 0) * 32 + j], slope);
+            const int oz = mv ? (int)(m * 128) + 4 * j : INT32_MIN;
+            an[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rz, oz, 0, 0));
+            if (ACT >= 0) yn[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ryy, oz, 0, 0));
+            const int xb = (int)(b * H * W * 4);
             if (X2) {
                 const int iy = oy * S - P + ky0, ix = ox * S - P + kx;
                 const bool inb = mv && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-                const uint2 v = *reinterpret_cast<const uint2 *>(x + ((mv ? b : 0) * H + (inb ? iy : 0)) * W +
-                                                                 (inb ? ix : 0));
-                dn[u].x = inb ? v.x : 0u;
-                dn[u].y = inb ? v.y : 0u;
+                dn[u] = __builtin_bit_cast(
+                    uint2, __builtin_amdgcn_raw_buffer_load_b64(rx, inb ? xb + (iy * W + ix) * 4 : INT32_MIN, 0, 0));
             } else {
-                unsigned v2[2];
 #pragma unroll
                 for (int g = 0; g < 2; ++g) {
                     const int iy = oy * S - P + 4 * g + ky0, ix = ox * S - P + kx;
                     const bool inb = mv && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-                    const unsigned v = x[((mv ? b : 0) * H + (inb ? iy : 0)) * W + (inb ? ix : 0)];
-                    v2[g] = inb ? v : 0u;
+                    const unsigned v =
+                        __builtin_amdgcn_raw_buffer_load_b32(rx, inb ? xb + (iy * W + ix) * 4 : INT32_MIN, 0, 0);
+                    if (g) dn[u].y = v;
+                    else dn[u].x = v;
                 }
-                dn[u].x = v2[0];
-                dn[u].y = v2[1];
             }
-            an[u] = mv ? a : 0.f;
             advance(1);
         }
         advance(8);  // the other half's 8 rows
@@ -923,7 +1051,7 @@ __global__ __launch_bounds__(256, 2) void conv1_u8_wgrad_bf16_kernel(const float
         uint2 d[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            a[u] = an[u];
+            a[u] = ACT >= 0 ? act_grad<ACT>(an[u], yn[u], slope) : an[u];  // a row past the end: 0 act'(0) = 0
             d[u] = dn[u];
         }
         if (st + 1 < s1) load_step();
@@ -1099,9 +1227,9 @@ XPA_API int xpa_maxpool_act_bwd_bias(int act, const float *dout, const int32_t *
     return xpa_launch_status();
 }
 
-// r05: bit 0 = K25B (the conv1 forward on the bf16 matrix cores), bit 1 = K26B (its weight gradient likewise); a
-// cleared bit selects the fp32-MFMA form.  Returns the previous mask.
-static int g_conv1_bf16 = 3;
+// r05: bit 0 = K25B (the conv1 forward on the bf16 matrix cores), bit 1 = K26B (its weight gradient likewise), bit 2 =
+// K27B (the conv2 data gradient likewise); a cleared bit selects the fp32-MFMA form.  Returns the previous mask.
+static int g_conv1_bf16 = 7;
 XPA_API int xpa_conv1_form(int mask) {
     const int prev = g_conv1_bf16;
     if (mask >= 0) g_conv1_bf16 = mask;
@@ -1119,7 +1247,7 @@ XPA_API int xpa_conv1_u8_fwd(int act, const uint8_t *x, int64_t batch, int64_t h
     const int64_t rows = batch * OH * OW;
     hipStream_t s = (hipStream_t)stream;
     const bool x2 = width % 2 == 0 && stride % 2 == 0 && pad % 2 == 0 && (uintptr_t)x % 8 == 0;
-    if (g_conv1_bf16 & 1) {  // K25B
+    if ((g_conv1_bf16 & 1) && batch * height * width * 4 < ((int64_t)1 << 31)) {  // K25B (one buffer record)
         const int64_t blocks = (rows + kC1BRows - 1) / kC1BRows;
         const dim3 grid((unsigned)(blocks < 512 ? blocks : 512)), block(512);
 #define XPA_C1B(A_)                                                                                                  \
@@ -1177,7 +1305,10 @@ XPA_API int xpa_conv_dgrad_s2k(const float *dy, int64_t batch, int64_t out_h, in
     }
     if (acc <= 0 || batch * out_h * out_w * 64 >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;  // int offsets
     const unsigned grid = (unsigned)(acc < kDgGrid ? acc : kDgGrid);
-    hipLaunchKernelGGL(conv_dgrad_s2k_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, dy, w, g, dx);
+    if ((g_conv1_bf16 & 4) && batch * out_h * out_w * 256 < ((int64_t)1 << 31))  // K27B (one buffer record for dY)
+        hipLaunchKernelGGL(conv_dgrad_s2k_bf16_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, dy, w, g, dx);
+    else
+        hipLaunchKernelGGL(conv_dgrad_s2k_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, dy, w, g, dx);
     return xpa_launch_status();
 }
 
@@ -1194,7 +1325,8 @@ XPA_API int xpa_conv1_u8_wgrad_act(int act, const float *dz, const float *y, flo
     const int64_t OH = (height + 2 * pad - kernel) / stride + 1, OW = (width + 2 * pad - kernel) / stride + 1;
     const bool x2 = width % 2 == 0 && stride % 2 == 0 && pad % 2 == 0 && (uintptr_t)x % 8 == 0;
     hipStream_t s = (hipStream_t)stream;
-    const bool bf = (g_conv1_bf16 & 2) != 0;  // K26B
+    const bool bf = (g_conv1_bf16 & 2) && batch * OH * OW * 128 < ((int64_t)1 << 31) &&
+                    batch * height * width * 4 < ((int64_t)1 << 31);  // K26B (one buffer record per operand)
 #define XPA_WG(X_, A_)                                                                                             \
     if (bf)                                                                                                        \
         hipLaunchKernelGGL((conv1_u8_wgrad_bf16_kernel<X_, A_>), dim3(kWgBlocks), dim3(256), 0, s, dz,             \

@@ -48,6 +48,7 @@ __device__ __forceinline__ float ig_act(float z, float slope) {
 
 template <int ACT>
 __device__ __forceinline__ float ig_grad(float d, float y, float slope) {  // d act / d z from the OUTPUT y
+#pragma clang fp contract(off)  // as conv.hip's act_grad (K22): the same value whichever kernel forms it
     if (ACT == 1) return y > 0.f ? d : d * slope;
     if (ACT == 2) return d * (1.0f - y * y);
     return d;
