@@ -599,6 +599,12 @@ int xpa_s3_split_batch(int n_mat, const float *const *b, const int64_t *k, const
                        void *const *out, xpa_stream_t stream);
 int xpa_s3_gemm(const float *a, int64_t lda, const void *b_split, float *c, int64_t ldc, int64_t m, int64_t k, int64_t n,
                 xpa_stream_t stream);
+/* K40G (r05): n <= 32 problems c[p] [m, 256] (row stride ldc) = a[p] [m, k] (row stride lda, 16-B aligned) . B[p]
+ * (xpa_s3_split_b planes) of one shape in ONE launch (grid (m / 256) x n): the column blocks and k parts of a GEMM wider
+ * than 256 columns (C3's fc layer).  Host arrays of device pointers; each problem's output is xpa_s3_gemm's bit for
+ * bit. */
+int xpa_s3_gemm_group(int n, const float *const *a, const void *const *b_split, float *const *c, int64_t lda,
+                      int64_t ldc, int64_t m, int64_t k, xpa_stream_t stream);
 /* K41 — the weight gradient dW = a^T b over the batch on the same split (a [rows, m] = dz, row stride lda; b [rows, 256]
  * = the layer input, row stride ldb; m % 128 == 0), split-K: out [slices, m, 256] holds one partial per slice of
  * ceil(rows / slices) rows (rounded up to 32), summed by the caller — the learner's fixed-order f64 finalize, as for

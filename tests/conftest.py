@@ -28,9 +28,11 @@ def golden():
 
 @pytest.fixture(params=["k28", "auto"])
 def conv_path(request, monkeypatch):
-    """The explicit CNN trunk's conv choice: "k28" forces K28 / K29 for every conv they take (the C3 update's path at
-    any batch); "auto" keeps the size rule (MIOpen below fused_cnn._Trunk.igemm_min_rows output pixels)."""
+    """The explicit CNN trunk's conv choice: "k28" forces K28 / K29 for every conv they take and the first fc layer's
+    split GEMMs (K40G, r05) — the C3 update's path at any batch; "auto" keeps the size rules (MIOpen below
+    fused_cnn._Trunk.igemm_min_rows output pixels, hipBLASLt for the fc layer below fc_split_min_rows)."""
     from xuanpolicy_amd import fused_cnn
     if request.param == "k28":
         monkeypatch.setattr(fused_cnn._Trunk, "igemm_min_rows", 0)
+        monkeypatch.setattr(fused_cnn._Trunk, "fc_split_min_rows", 0)
     return request.param

@@ -174,6 +174,37 @@ def test_gemm_wave_specialised_equals_k40(m, k):
         L.xpa_s3_probe(0)
 
 
+@pytest.mark.parametrize("m,in_f,out_f", [(16384, 6400, 512), (777, 512, 256), (3, 544, 256)])
+def test_gemm_group_equals_k40(m, in_f, out_f):
+    """K40G (r05): one launch of the fc layer's problems — forward k halves x 256-column blocks and data-gradient
+    column blocks (the last aligned to the end, overlapping its neighbour) — each output equal to its own K40 launch
+    bit for bit; the overlapped columns come out identical from both blocks."""
+    from xuanpolicy_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(m + in_f)
+    x = _wide((m, in_f), g)
+    w = torch.randn(out_f, in_f, device=DEV, generator=g) / 16
+    kh = in_f // 2
+    part = torch.full((2, m, out_f), float("nan"), device=DEV)
+    fwd = []
+    for j in range(out_f // 256):
+        for p in range(2):
+            fwd.append((x[:, p * kh:(p + 1) * kh], ops.s3_split(w[j * 256:(j + 1) * 256, p * kh:(p + 1) * kh].t()),
+                        part[p, :, j * 256:(j + 1) * 256]))
+    ops.s3_gemm_group(fwd, kh)
+    for a, b, c in fwd:
+        assert torch.equal(c, ops.s3_gemm(a, b, kh))
+    gz = _wide((m, out_f), g)
+    dx = torch.full((m, in_f), float("nan"), device=DEV)
+    c0s = [min(c, in_f - 256) for c in range(0, in_f, 256)]
+    dgr = [(gz, ops.s3_split(w[:, c0:c0 + 256]), dx[:, c0:c0 + 256]) for c0 in c0s]
+    ops.s3_gemm_group(dgr, out_f)
+    ref = gz.double() @ w.double()
+    for (a, b, _), c0 in zip(dgr, c0s):
+        assert torch.equal(dx[:, c0:c0 + 256], ops.s3_gemm(a, b, out_f))
+    bound = 4e-6 * (gz.double().abs() @ w.double().abs()) + 1e-6
+    assert bool(((dx.double() - ref).abs() <= bound).all())
+
+
 @pytest.mark.parametrize("rows,m,lda_pad,slices", [(65536, 512, 0, None), (4133, 256, 8, 5), (100, 128, 0, 1),
                                                    (33, 128, 4, 2)])
 def test_wgrad_vector_staged_matches_f32_gemm_error(rows, m, lda_pad, slices):

@@ -736,7 +736,8 @@ __device__ __forceinline__ void dgrad_b_mfma_chunk(f32x16 (&acc)[2], const f4v (
     }
 }
 
-__global__ __launch_bounds__(256, 2) void conv_dgrad_s2k_bf16_kernel(const float *__restrict__ dy,
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void conv_dgrad_s2k_bf16_kernel(const float *__restrict__ dy,
                                                                      const float *__restrict__ w, DgradGeom g,
                                                                      float *__restrict__ dx) {
     __shared__ xpa_bf16x8 sB[16 * 3 * 64];  // [step][plane hi, mid, lo][lane]
@@ -1305,9 +1306,15 @@ XPA_API int xpa_conv_dgrad_s2k(const float *dy, int64_t batch, int64_t out_h, in
     }
     if (acc <= 0 || batch * out_h * out_w * 64 >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;  // int offsets
     const unsigned grid = (unsigned)(acc < kDgGrid ? acc : kDgGrid);
-    if ((g_conv1_bf16 & 4) && batch * out_h * out_w * 256 < ((int64_t)1 << 31))  // K27B (one buffer record for dY)
-        hipLaunchKernelGGL(conv_dgrad_s2k_bf16_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, dy, w, g, dx);
-    else
+    if ((g_conv1_bf16 & 4) && batch * out_h * out_w * 256 < ((int64_t)1 << 31)) {  // K27B (one buffer record for dY)
+        if (g_conv1_bf16 & 8) {  // probe: 3 blocks per CU (<= 168 VGPRs)
+            const unsigned g3 = (unsigned)(acc < 768 ? acc : 768);
+            hipLaunchKernelGGL(conv_dgrad_s2k_bf16_kernel<3>, dim3(g3), dim3(256), 0, (hipStream_t)stream, dy, w, g, dx);
+        } else {
+            hipLaunchKernelGGL(conv_dgrad_s2k_bf16_kernel<2>, dim3(grid), dim3(256), 0, (hipStream_t)stream, dy, w, g,
+                               dx);
+        }
+    } else
         hipLaunchKernelGGL(conv_dgrad_s2k_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, dy, w, g, dx);
     return xpa_launch_status();
 }

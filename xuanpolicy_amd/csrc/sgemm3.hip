@@ -263,21 +263,21 @@ __device__ __forceinline__ void chunk64(const char *st, f32x16 (&acc)[8], int la
 // EPI (r05, K40F: the C4 trunk layer's forward): 0 = C = A B; 1 / 2 / 3 = C = act(A B + bias) with act identity /
 // LeakyReLU (slope) / tanh, and with `sign` (EPI 1 / 2) the output's sign bits beside it (32 bytes per row, byte col bit
 // cb = C[row, 32 cb + col] > 0: K42S's act' source, the layout xpa_thin_linear_act_fwd_gather_sign writes)
-template <int W, int S, int PROBE, int T64 = 0, int EPI = 0>
-__global__ __launch_bounds__(64 * W, 8 / W) void s3_gemm_kernel(const float *__restrict__ a, int64_t lda,
-                                                               const __bf16 *__restrict__ bs, float *__restrict__ c,
-                                                               int64_t ldc, int64_t M, int nchunks,
-                                                               const float *__restrict__ bias = nullptr,
-                                                               float slope = 0.f,
-                                                               unsigned char *__restrict__ sign = nullptr,
-                                                               const int64_t *__restrict__ ridx = nullptr) {
+// the body of K40 for row block blk (s3_gemm_kernel: blk = blockIdx.x; s3_gemm_group_kernel: one of several
+// problems per blockIdx.y)
+template <int W, int S, int PROBE, int T64, int EPI>
+__device__ __forceinline__ void s3_gemm_body(const float *__restrict__ a, int64_t lda, const __bf16 *__restrict__ bs,
+                                             float *__restrict__ c, int64_t ldc, int64_t M, int nchunks,
+                                             const float *__restrict__ bias, float slope,
+                                             unsigned char *__restrict__ sign, const int64_t *__restrict__ ridx,
+                                             int64_t blk) {
     using G = S3Geom<W>;
     // ONE LDS array (the DMA target; see head.hip)
     __shared__ __attribute__((aligned(16))) char lds[S * G::kStage];
     const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds);
     const int t = threadIdx.x, lane = t & 63;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int64_t r0 = (int64_t)blockIdx.x * G::kRows;
+    const int64_t r0 = blk * G::kRows;
     f32x16 acc[8];
 #pragma unroll
     for (int cb = 0; cb < 8; ++cb)
@@ -364,6 +364,35 @@ __global__ __launch_bounds__(64 * W, 8 / W) void s3_gemm_kernel(const float *__r
             for (int cb = 0; cb < 8; ++cb) crow[cb * 32] = acc[cb][r];
         }
     }
+}
+
+template <int W, int S, int PROBE, int T64 = 0, int EPI = 0>
+__global__ __launch_bounds__(64 * W, 8 / W) void s3_gemm_kernel(const float *__restrict__ a, int64_t lda,
+                                                               const __bf16 *__restrict__ bs, float *__restrict__ c,
+                                                               int64_t ldc, int64_t M, int nchunks,
+                                                               const float *__restrict__ bias = nullptr,
+                                                               float slope = 0.f,
+                                                               unsigned char *__restrict__ sign = nullptr,
+                                                               const int64_t *__restrict__ ridx = nullptr) {
+    s3_gemm_body<W, S, PROBE, T64, EPI>(a, lda, bs, c, ldc, M, nchunks, bias, slope, sign, ridx, blockIdx.x);
+}
+
+// K40G (r05): up to kS3Groups independent K40 problems of one shape in one launch (blockIdx.y = the problem): the
+// column blocks and k parts of a GEMM wider than 256 columns (C3's fc layer: [16384, 3136] x [3136, 512] forward in
+// 2 column halves x 2 k halves, its data gradient in 13 column blocks) fill the chip where one K40 launch of M / 256
+// blocks would not (64 blocks at 16 384 rows).
+constexpr int kS3Groups = 32;
+struct S3Group {
+    const float *a[kS3Groups];
+    const __bf16 *b[kS3Groups];
+    float *c[kS3Groups];
+};
+
+__global__ __launch_bounds__(512, 1) void s3_gemm_group_kernel(S3Group g, int64_t lda, int64_t ldc, int64_t M,
+                                                               int nchunks) {
+    const int p = blockIdx.y;
+    s3_gemm_body<8, 3, 0, 0, 0>(g.a[p], lda, g.b[p], g.c[p], ldc, M, nchunks, nullptr, 0.f, nullptr, nullptr,
+                                blockIdx.x);
 }
 
 // K40R (r05): the rollout's paired hidden layer z [M, 512] = x [M, 256] . [B0 | B1] + bias (B0 / B1 = Wh_actor^T /
@@ -2220,6 +2249,25 @@ XPA_API int xpa_s3_gemm_rows_pair(const float *a, int64_t lda, const void *b0_sp
         s3_gemm_r64_kernel<3, 2><<<grid, dim3(256), 0, stream>>>(a, lda, b0, b1, c, ldc, m, kN / kKC, bias);
     else
         s3_gemm_r64_kernel<2, 4><<<grid, dim3(256), 0, stream>>>(a, lda, b0, b1, c, ldc, m, kN / kKC, bias);
+    return xpa_launch_status();
+}
+
+// K40G (r05): n (<= 32) problems c[p] [m, 256] = a[p] [m, k] . B[p] (split by xpa_s3_split_b), one lda / ldc / m / k,
+// one launch (host pointer arrays)
+XPA_API int xpa_s3_gemm_group(int n, const float *const *a, const void *const *b_split, float *const *c, int64_t lda,
+                              int64_t ldc, int64_t m, int64_t k, xpa_stream_t stream) {
+    if (n < 1 || n > kS3Groups || !a || !b_split || !c || m <= 0 || k <= 0 || k % kKC != 0 || lda < k || ldc < kN ||
+        (lda & 3) || k / kKC > (1 << 20) || (m + 255) / 256 > 0x7fffffff)
+        return (int)hipErrorInvalidValue;
+    S3Group g{};
+    for (int p = 0; p < n; ++p) {
+        if (!a[p] || !b_split[p] || !c[p] || (reinterpret_cast<uintptr_t>(a[p]) & 15)) return (int)hipErrorInvalidValue;
+        g.a[p] = a[p];
+        g.b[p] = static_cast<const __bf16 *>(b_split[p]);
+        g.c[p] = c[p];
+    }
+    s3_gemm_group_kernel<<<dim3((unsigned)((m + 255) / 256), (unsigned)n), dim3(512), 0, stream>>>(g, lda, ldc, m,
+                                                                                                    (int)(k / kKC));
     return xpa_launch_status();
 }
 

@@ -188,6 +188,8 @@ class _Trunk:
         if self.tail == "flatten" and self.fc[0][0].in_features != shape[0] * shape[1] * shape[2]:
             raise ValueError("fc input width does not match the conv output")
         self._w_hwc = None      # the first fc weight with (H, W, C)-ordered columns, refreshed after each update
+        self._w_ver = 0         # bumped whenever _w_hwc is re-derived (the fc split planes follow it)
+        self._fcs = None        # K40G planes of _w_hwc (forward k halves, data-gradient column blocks) + their version
         self.stale = True
         self._dw_tmp = None
         self.parts = parts
@@ -232,7 +234,67 @@ class _Trunk:
                 self._w_hwc = torch.empty_like(w)
             self._w_hwc.view(w.shape[0], Hl, Wl, Cl).copy_(w.view(w.shape[0], Cl, Hl, Wl).permute(0, 2, 3, 1))
             self.stale = False
+            self._w_ver += 1
         return self._w_hwc
+
+    # r05: the first fc layer of the update's minibatches (C3: [16384, 3136] x [3136, 512]) on the bf16 matrix cores by
+    # the three-way split (K40G: one launch per GEMM; forward in 2 k halves x 256-column blocks, summed in a fixed
+    # order; the data gradient in 256-column blocks, the last one aligned to the end so no block is padded — the
+    # columns it shares with its neighbour come out bit-identical from both).  The rollout's 1024-frame forwards stay
+    # on hipBLASLt (fc_split_min_rows).  The weight gradient stays on hipBLASLt.
+    fc_split = True
+    fc_split_min_rows = 8192
+
+    def _fc_split_ok(self, rows):
+        if not (self.fc_split and ops.S3_GEMMS and self.tail == "flatten" and rows >= self.fc_split_min_rows):
+            return False
+        lin = self.fc[0][0]
+        return lin.out_features % 256 == 0 and lin.in_features % 32 == 0 and lin.in_features >= 512 and \
+            lin.out_features // 256 * 2 <= 32 and (lin.in_features + 255) // 256 <= 32
+
+    def _fc_planes(self):
+        """The split planes of the current _w_hwc: forward (column block j, k half p) and data-gradient column
+        blocks, re-split (4 matrices per launch) whenever _w_hwc was re-derived."""
+        w = self._fc0_weight()
+        if self._fcs is not None and self._fcs[0] == self._w_ver:
+            return self._fcs
+        out_f, in_f = w.shape
+        kh = in_f // 2
+        fwd = [w[j * 256:(j + 1) * 256, p * kh:(p + 1) * kh].t() for j in range(out_f // 256) for p in range(2)]
+        c0s = [min(c, in_f - 256) for c in range(0, in_f, 256)]
+        dgr = [w[:, c0:c0 + 256] for c0 in c0s]
+        old = self._fcs
+        if old is None:
+            nb_f, nb_d = int(ops.lib().xpa_s3_split_bytes(kh, 256)), int(ops.lib().xpa_s3_split_bytes(out_f, 256))
+            bufs_f = [torch.empty(nb_f, dtype=torch.uint8, device=w.device) for _ in fwd]
+            bufs_d = [torch.empty(nb_d, dtype=torch.uint8, device=w.device) for _ in dgr]
+        else:
+            bufs_f, bufs_d = old[1], old[2]
+        pairs = list(zip(fwd, bufs_f)) + list(zip(dgr, bufs_d))
+        for i in range(0, len(pairs), 4):
+            ops.s3_split_batch(pairs[i:i + 4])
+        self._fcs = (self._w_ver, bufs_f, bufs_d, c0s)
+        return self._fcs
+
+    def _fc0_forward_split(self, flat, lin, code, slope):
+        rows, in_f = flat.shape
+        out_f, kh = lin.out_features, in_f // 2
+        _, bf, _, _ = self._fc_planes()
+        part = self.parts.buf(("fcs", rows, out_f), (2, rows, out_f), flat.device)
+        probs = [(flat[:, p * kh:(p + 1) * kh], bf[j * 2 + p], part[p, :, j * 256:(j + 1) * 256])
+                 for j in range(out_f // 256) for p in range(2)]
+        ops.s3_gemm_group(probs, kh)
+        s = torch.add(part[0], part[1])
+        _bias_act(code, s, lin.bias, slope)
+        return s
+
+    def _fc0_dgrad_split(self, g):
+        rows = g.shape[0]
+        _, _, bd, c0s = self._fc_planes()
+        in_f = self.fc[0][0].in_features
+        dx = torch.empty((rows, in_f), dtype=torch.float32, device=g.device)
+        ops.s3_gemm_group([(g, b, dx[:, c0:c0 + 256]) for b, c0 in zip(bd, c0s)], g.shape[1])
+        return dx
 
     @staticmethod
     def frames(x):
@@ -293,10 +355,13 @@ class _Trunk:
         fouts = []
         s = flat
         for j, (lin, code, slope) in enumerate(self.fc):
-            w = self._fc0_weight() if j == 0 else lin.weight
-            s = F.linear(s, w, lin.bias)
-            if code:
-                _bias_act(code, s, None, slope)
+            if j == 0 and self._fc_split_ok(B) and flat.is_contiguous():
+                s = self._fc0_forward_split(flat, lin, code, slope)
+            else:
+                w = self._fc0_weight() if j == 0 else lin.weight
+                s = F.linear(s, w, lin.bias)
+                if code:
+                    _bias_act(code, s, None, slope)
             fouts.append(s)
         return s, (hs, None, flat, fouts)
 
@@ -451,7 +516,10 @@ class _Trunk:
                     Cl, Hl, Wl = self._chw
                     lin.weight.grad.view(lin.out_features, Cl, Hl, Wl).copy_(
                         self._dw_tmp.view(lin.out_features, Hl, Wl, Cl).permute(0, 3, 1, 2))
-                    g = torch.mm(g, self._fc0_weight())
+                    if self._fc_split_ok(g.shape[0]):
+                        g = self._fc0_dgrad_split(g)
+                    else:
+                        g = torch.mm(g, self._fc0_weight())
                 else:
                     torch.mm(g.t(), x_in, out=lin.weight.grad)
                     g = torch.mm(g, lin.weight)

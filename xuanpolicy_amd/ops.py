@@ -301,6 +301,36 @@ def s3_gemm(a, b_split, k, out=None):
     return out
 
 
+_GROUP_ARGS = {}
+
+
+def s3_gemm_group(problems, k):
+    """K40G (r05): [(a [m, k] view, b_split, out [m, 256] view), ...] (<= 32, one m / lda / ldc) in one launch; each
+    out is s3_gemm(a, b_split, k)'s bit for bit."""
+    n = len(problems)
+    if not 1 <= n <= 32:
+        raise ValueError("1..32 problems")
+    a0, _, c0 = problems[0]
+    m = a0.shape[0]
+    lda, ldc = _row_stride(a0, "a", k), _row_stride(c0, "out", 256)
+    key = tuple((a.data_ptr(), b.data_ptr(), c.data_ptr()) for a, b, c in problems) + (lda, ldc, m, k)
+    arrs = _GROUP_ARGS.get(key)
+    if arrs is None:
+        for a, b, c in problems:
+            _req(a, "a", torch.float32, contiguous=False)
+            _req(c, "out", torch.float32, contiguous=False)
+            if a.shape[0] != m or c.shape[0] != m or a.stride(0) != lda or c.stride(0) != ldc or a.shape[1] != k:
+                raise ValueError("s3_gemm_group: every problem needs the same m / lda / ldc")
+        arrs = ((ctypes.c_void_p * n)(*[a.data_ptr() for a, _, _ in problems]),
+                (ctypes.c_void_p * n)(*[b.data_ptr() for _, b, _ in problems]),
+                (ctypes.c_void_p * n)(*[c.data_ptr() for _, _, c in problems]))
+        if len(_GROUP_ARGS) > 64:
+            _GROUP_ARGS.clear()
+        _GROUP_ARGS[key] = arrs
+    _lib.check(lib().xpa_s3_gemm_group(n, arrs[0], arrs[1], arrs[2], lda, ldc, m, k, _stream(a0.device)),
+               "xpa_s3_gemm_group")
+
+
 def s3_gemm_trunk_bwd(dz, b_split, k, h, x, act, slope, partial_dw=None, partial_db=None, h_sign=None):
     """K42: g = dz [rows, k] . B (split) kept in registers; the first representation layer's backward on it (dz1 =
     g * act'(h), its bias / weight gradients) as per-block partials ([G, 256 * d_in], [G, 256]); g is not stored.
