@@ -883,8 +883,8 @@ int xpa_frames_to_f32(const uint8_t *src, int64_t n, float *dst, xpa_stream_t st
 /* r05: the conv kernels' arithmetic — bit 0: K25B (conv1 forward), bit 1: K26B (conv1 weight gradient) on the bf16
  * matrix cores with the frames exact and the f32 operand split three ways; bit 2: K27B (xpa_conv_dgrad_s2k) with both
  * operands split three ways (six products, f32-GEMM accuracy).  A cleared bit selects the fp32-MFMA form (K25 / K26 /
- * K27); so does an operand of 2^31 bytes or more (the bf16 forms read through one buffer record).  mask < 0 only
- * reads.  Returns the previous mask (default 7). */
+ * K27); so does an operand of 2^31 bytes or more (the bf16 forms read through one buffer record).  Bit 3: K27B at 3
+ * blocks per CU (an A/B probe; measured slower).  mask < 0 only reads.  Returns the previous mask (default 7). */
 int xpa_conv1_form(int mask);
 /* K25 — the first conv block straight from the uint8 frames (C3 AC_CNN_Atari / C5 Basic_CNN: cnn_block
  * xuance/torch/utils/layers.py:36-57 on observations / 255.0, cnn.py:89-92): y = act(conv2d(x / 255, w, stride, pad)
