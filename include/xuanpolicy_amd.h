@@ -886,6 +886,11 @@ int xpa_frames_to_f32(const uint8_t *src, int64_t n, float *dst, xpa_stream_t st
  * K27); so does an operand of 2^31 bytes or more (the bf16 forms read through one buffer record).  Bit 3: K27B at 3
  * blocks per CU (an A/B probe; measured slower).  mask < 0 only reads.  Returns the previous mask (default 7). */
 int xpa_conv1_form(int mask);
+/* r05: K28's arithmetic (xpa_conv_fwd / xpa_conv_dgrad) — bit 0: K28B, the implicit GEMM on the bf16 matrix cores with
+ * both f32 operands split three ways (six products, f32-GEMM accuracy), taken where the GEMM's input channels are a
+ * multiple of 16; bit 1: K28B with 3 row tiles per wave (A/B, forward only); 0 = the fp32-MFMA K28 (the default: K28B
+ * measured no faster inside the C3 update).  mask < 0 only reads.  Returns the previous mask. */
+int xpa_conv_igemm_form(int mask);
 /* K25 — the first conv block straight from the uint8 frames (C3 AC_CNN_Atari / C5 Basic_CNN: cnn_block
  * xuance/torch/utils/layers.py:36-57 on observations / 255.0, cnn.py:89-92): y = act(conv2d(x / 255, w, stride, pad)
  * + bias) with x uint8 NHWC [batch, height, width, 4] (4-B aligned), w [32, 4, 8, 8] (torch's Conv2d layout), y f32

@@ -23,6 +23,18 @@ def _setup():
         pytest.skip("no GPU")
 
 
+@pytest.fixture(params=[1, 3, 0], ids=["k28b", "k28b_mt3", "k28"])
+def ig_form(request):
+    """r05: K28 on the bf16 matrix cores (K28B, opt-in, where the GEMM's input channels are a multiple of 16; mt3: its
+    3-tile waves, forward only) and the fp32-MFMA K28 (the default)."""
+    from xuanpolicy_amd import ops
+    L = ops.lib()
+    prev = L.xpa_conv_igemm_form(-1)
+    L.xpa_conv_igemm_form(request.param)
+    yield request.param
+    L.xpa_conv_igemm_form(prev)
+
+
 def _data(B, H, W, Cin, Cout, k, s, seed):
     g = torch.Generator().manual_seed(seed)
     x = torch.rand(B, H, W, Cin, generator=g)
@@ -32,7 +44,7 @@ def _data(B, H, W, Cin, Cout, k, s, seed):
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-def test_conv_fwd_matches_f64(shape):
+def test_conv_fwd_matches_f64(shape, ig_form):
     from xuanpolicy_amd import _lib, ops
     B, H, W, Cin, Cout, k, s = shape
     p = (k - s) // 2
@@ -49,7 +61,7 @@ def test_conv_fwd_matches_f64(shape):
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-def test_conv_dgrad_matches_f64(shape):
+def test_conv_dgrad_matches_f64(shape, ig_form):
     """dX of the conv from dZ, times act'(y_prev) of the previous block (ReLU from its output), and that block's bias
     gradient (the column sums of the result)."""
     from xuanpolicy_amd import _lib, ops
@@ -130,3 +142,28 @@ def test_conv_igemm_rejects_bad_shapes():
     assert not L.xpa_conv_igemm_ok(64, 64, 5)     # weight image over 160 KiB
     assert not L.xpa_conv_igemm_ok(128, 64, 3)
     assert L.xpa_conv_fwd(1, None, 1, 10, 10, 64, None, None, 64, 3, 1, 1, 0.0, None, None) == 1
+
+
+@pytest.mark.parametrize("shape", [(2048, 21, 21, 32, 64, 4, 2), (2048, 10, 10, 64, 64, 3, 1)])
+def test_conv_fwd_bf16_form_error_vs_fp32_form(shape):
+    """K28B against K28 at C3's conv2 / conv3 shapes: both against the f64 conv, K28B's error no larger than 2x K28's."""
+    from xuanpolicy_amd import _lib, ops
+    L = ops.lib()
+    B, H, W, Cin, Cout, k, s = shape
+    p = (k - s) // 2
+    x, w, b = _data(*shape, seed=4)
+    ref = F.conv2d(x.double().permute(0, 3, 1, 2), w.double(), b.double(), s, p).permute(0, 2, 3, 1)
+    OH, OW = ref.shape[1], ref.shape[2]
+    xd, wd, bd = x.to(DEV), w.to(DEV), b.to(DEV)
+    prev = L.xpa_conv_igemm_form(-1)
+    errs = []
+    try:
+        for form in (1, 0):
+            L.xpa_conv_igemm_form(form)
+            y = torch.full((B, OH, OW, Cout), float("nan"), device=DEV)
+            _lib.check(L.xpa_conv_fwd(0, ops._p(xd), B, H, W, Cin, ops._p(wd), ops._p(bd), Cout, k, s, p, 0.0, ops._p(y),
+                                      ops._stream(DEV)), "xpa_conv_fwd")
+            errs.append(float((y.cpu().double() - ref).abs().max()))
+    finally:
+        L.xpa_conv_igemm_form(prev)
+    assert errs[0] <= 2 * errs[1] + 1e-9, errs

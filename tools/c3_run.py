@@ -15,6 +15,9 @@ if __name__ == "__main__":
         if a.startswith("conv1-form="):
             from xuanpolicy_amd import ops
             ops.lib().xpa_conv1_form(int(a.split("=")[1]))
+        if a.startswith("igemm-form="):   # r05 A/B: xpa_conv_igemm_form (bit 0 K28B)
+            from xuanpolicy_amd import ops
+            ops.lib().xpa_conv_igemm_form(int(a.split("=")[1]))
         if a.startswith("fc-split="):   # r05 A/B: the first fc layer on K40G (1) or hipBLASLt (0)
             from xuanpolicy_amd import fused_cnn
             fused_cnn._Trunk.fc_split = bool(int(a.split("=")[1]))

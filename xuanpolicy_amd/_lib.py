@@ -110,6 +110,7 @@ SIGNATURES = {
                                                c_i64, c_i64, c_p, c_p, c_p]),
     "xpa_conv1_u8_wgrad": (ctypes.c_int, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
     "xpa_conv1_form": (ctypes.c_int, [ctypes.c_int]),
+    "xpa_conv_igemm_form": (ctypes.c_int, [ctypes.c_int]),
     "xpa_conv1_u8_fwd": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p,
                                          c_i64, c_f32, c_p, c_p]),
     "xpa_bias_act": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_p, c_f32, c_p]),

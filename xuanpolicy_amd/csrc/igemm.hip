@@ -27,6 +27,7 @@
 //   With act >= 0 the operand is g * act'(y) (the block's own activation backward folded in: K22 is not run) and wave 0
 //   also writes the bias-gradient partials.
 #include "xpa_common.h"
+#include "s3_split.h"
 
 namespace {
 
@@ -648,8 +649,226 @@ int ws_pad(int need, int step) {
     return need;
 }
 
+// ---- K28B (r05): K28 on the bf16 matrix cores ----------------------------------------------------------------------
+// The same implicit GEMM (forward and data gradient, the same pixel maps, epilogues and buffer-record zero fill) with
+// both f32 operands cut into their exact three-way bf16 split (s3_split.h) and six v_mfma_f32_32x32x16_bf16 products per
+// 16-k step instead of eight v_mfma_f32_32x32x2_f32 — 192 against 512 matrix-core cycles per 16 k and 32 x 32 tile (K28
+// measured 0.85 MFMA-busy: matrix-core bound).  k order: step s = (tap s / (CIN / 16), channels 16 (s % (CIN / 16)) ..
+// + 15); lane half h feeds channels + 8 h .. + 7 (two adjacent 16-B quads of its row's pixel).  The weight image stays
+// f32 in LDS as [tap][channel octet][n][8] (the three planes would not fit: 221 KiB at C3's conv3); each wave splits
+// its B fragments per step (shared by its MT row tiles) and its A fragments per row tile.  Block = 8 waves (2 per SIMD,
+// up to 256 VGPRs), one per CU, wave = MT x 32 rows x COUTP.  CIN must be a multiple of 16 (no channel padding).
+template <int CIN, int NT, int MODE, int ACT, int MT>
+__global__ __launch_bounds__(512, 1) void conv_igemm_bf16_kernel(IgArgs a) {
+    constexpr int C8 = CIN / 8;
+    constexpr int SPT = CIN / 16;
+    constexpr int COUTP = 32 * NT;
+    constexpr int kRowsB = 8 * 32 * MT;
+    __shared__ __attribute__((aligned(16))) float sB[kIgLdsFloats];
+    const int t = threadIdx.x, lane = t & 63, h = lane >> 5, i = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int taps = a.K * a.K;
+    const int nst = taps * SPT;
+    // ---- the weight image [tap][c8][n][8] (f32) ----
+    const int img = taps * CIN * COUTP;
+    for (int e0 = t; e0 < img; e0 += 8 * 512) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = e0 + u * 512;
+            const int cc = e & 7, n = (e >> 3) % COUTP, c8 = ((e >> 3) / COUTP) % C8, tap = e / (8 * COUTP * C8);
+            const int c = 8 * c8 + cc, ky = tap / a.K, kx = tap - (tap / a.K) * a.K;
+            v[u] = 0.f;
+            if (e < img && n < a.COUT)
+                v[u] = MODE == 0 ? a.w[((n * CIN + c) * a.K + ky) * a.K + kx]
+                                 : a.w[((c * a.COUT + n) * a.K + ky) * a.K + kx];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (e0 + u * 512 < img) sB[e0 + u * 512] = v[u];
+    }
+    __syncthreads();
+    const int64_t nb = (a.rows + kRowsB - 1) / kRowsB;
+    const int64_t g0 = nb * blockIdx.x / gridDim.x, g1 = nb * (blockIdx.x + 1) / gridDim.x;
+    float bn[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) bn[nt] = 0.f;
+    if (MODE == 0 && a.bias) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) bn[nt] = 32 * nt + i < a.COUT ? a.bias[32 * nt + i] : 0.f;
+    }
+    float bsum[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) bsum[nt] = 0.f;
+    const int64_t ohw = (int64_t)a.OH * a.OW;
+    auto geometry = [&](int64_t blk, IgRow (&rr)[MT]) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const int64_t m = blk * kRowsB + wave * 32 * MT + mt * 32 + i;
+            const bool ok = m < a.rows;
+            const int64_t mc = ok ? m : 0;
+            const int64_t b = mc / ohw;
+            const int rem = (int)(mc - b * ohw);
+            rr[mt].oy = rem / a.OW;
+            rr[mt].ox = rem - rr[mt].oy * a.OW;
+            rr[mt].base = (int)(b * a.IH * a.IW);
+            rr[mt].ok = ok;
+        }
+    };
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(a.in), 0, (int)a.in_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, (int)(a.rows * a.COUT * 4),
+                                                                          0x00020000);
+    auto load_step = [&](f4v (&v)[MT][2], const IgRow (&rr)[MT], int s) {
+        const int tap = s / SPT, j = s - tap * SPT;
+        const int ky = tap / a.K, kx = tap - (tap / a.K) * a.K;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            bool valid;
+            const int pix = ig_pixel<MODE>(a, rr[mt], ky, kx, valid);
+            const int off = valid ? (pix * CIN + 16 * j + 8 * h) * 4 : INT32_MIN;
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                v[mt][q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rsrc, valid ? off + 16 * q
+                                                                                               : INT32_MIN, 0, 0));
+        }
+    };
+    if (g0 >= g1) return;
+    IgRow cur[MT], nxt[MT];
+    geometry(g0, cur);
+    f4v va[MT][2], vb[MT][2];
+    load_step(va, cur, 0);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) asm volatile("" ::"v"(va[mt][q]));
+    for (int64_t blk = g0; blk < g1; ++blk) {
+        const bool more = blk + 1 < g1;
+        f32x16 acc[MT][NT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.f;
+#pragma unroll 1
+        for (int s = 0; s < nst; ++s) {
+            if (s + 1 < nst) {
+                load_step(vb, cur, s + 1);
+            } else if (more) {
+                geometry(blk + 1, nxt);
+                load_step(vb, nxt, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            const int tap = s / SPT, j = s - tap * SPT;
+            xpa_bf16x8 bh[NT], bm[NT], bl[NT];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const f4v *bp = reinterpret_cast<const f4v *>(sB + ((tap * C8 + 2 * j + h) * COUTP + 32 * nt + i) * 8);
+                const f4v b0 = bp[0], b1 = bp[1];
+                xpa_split8(float4{b0[0], b0[1], b0[2], b0[3]}, float4{b1[0], b1[1], b1[2], b1[3]}, bh[nt], bm[nt],
+                           bl[nt]);
+            }
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                xpa_bf16x8 ah, am, al;
+                xpa_split8(float4{va[mt][0][0], va[mt][0][1], va[mt][0][2], va[mt][0][3]},
+                           float4{va[mt][1][0], va[mt][1][1], va[mt][1][2], va[mt][1][3]}, ah, am, al);
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = xpa_mfma_s3(ah, am, al, bh[nt], bm[nt], bl[nt], acc[mt][nt]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    va[mt][q] = vb[mt][q];
+                    asm volatile("" ::"v"(va[mt][q]));
+                }
+        }
+        // K28's epilogue per m-tile (C/D map: row = (r & 3) + 8 (r >> 2) + 4 h, column n = 32 nt + i)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const int n = 32 * nt + i;
+                const int64_t m0 = blk * kRowsB + wave * 32 * MT + mt * 32 + 4 * h;
+                auto offset = [&](int r) -> int {
+                    const int64_t m = m0 + (r & 3) + 8 * (r >> 2);
+                    return m < a.rows && n < a.COUT ? (int)(m * a.COUT + n) * 4 : INT32_MIN;
+                };
+                if (MODE == 0) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        __builtin_amdgcn_raw_buffer_store_b32(
+                            __builtin_bit_cast(unsigned, ig_act<ACT>(acc[mt][nt][r] + bn[nt], a.slope)), rout,
+                            offset(r), 0, 0);
+                } else {
+#pragma unroll
+                    for (int r0 = 0; r0 < 16; r0 += 8) {
+                        float yp[8];
+                        if (ACT >= 0) {
+#pragma unroll
+                            for (int r = 0; r < 8; ++r) {
+                                const int o = offset(r0 + r);
+                                yp[r] = a.yprev[o != INT32_MIN ? o / 4 : 0];
+                            }
+                        }
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) {
+                            const int o = offset(r0 + r);
+                            float v = acc[mt][nt][r0 + r];
+                            if (ACT >= 0) v = ig_grad<ACT>(v, yp[r], a.slope);
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rout, o, 0, 0);
+                            bsum[nt] += o != INT32_MIN ? v : 0.f;
+                        }
+                    }
+                }
+            }
+        if (more) {
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) cur[mt] = nxt[mt];
+        }
+    }
+    if (MODE == 1 && a.bias_partial) {
+        __syncthreads();
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const float s = bsum[nt] + __shfl_xor(bsum[nt], 32, 64);
+            if (h == 0) sB[wave * COUTP + 32 * nt + i] = s;
+        }
+        __syncthreads();
+        if (t < a.COUT) {
+            float s = 0.f;
+            for (int w = 0; w < 8; ++w) s += sB[w * COUTP + t];
+            a.bias_partial[(int64_t)blockIdx.x * a.COUT + t] = s;
+        }
+    }
+}
+
+// r05: bit 0 = K28B (the bf16 matrix-core form where CIN is a multiple of 16), bit 1 = its 3-tile waves.  Off by
+// default: 17-23 % faster per launch, but the C3 update's total GPU time came out unchanged (the kernels after it ran
+// ~6 % slower: profiles/r05/r05k28b/)
+int g_ig_form = 0;
+
 template <int MODE, int ACT>
 int ig_dispatch(const IgArgs &args, int cinp, int nt, hipStream_t s) {
+    if ((g_ig_form & 1) && args.CIN % 16 == 0 && args.CIN == cinp) {   // K28B
+        // MT = 2: 512-row block steps, so the data gradient's bias partials are K28's xpa_conv_dgrad_num_partials rows
+        const int mt = (g_ig_form & 2) && MODE == 0 ? 3 : 2;
+        const int64_t nb = (args.rows + 8 * 32 * mt - 1) / (8 * 32 * mt);
+        const unsigned g = (unsigned)(nb < kIgGrid ? nb : kIgGrid);
+#define XPA_IGB(C_, N_, M_) hipLaunchKernelGGL((conv_igemm_bf16_kernel<C_, N_, MODE, ACT, M_>), dim3(g), dim3(512), 0, s, args)
+#define XPA_IGB_M(C_, N_) if (mt == 3) XPA_IGB(C_, N_, 3); else XPA_IGB(C_, N_, 2)
+        if (nt == 1) {
+            if (cinp == 16) { XPA_IGB_M(16, 1); } else if (cinp == 32) { XPA_IGB_M(32, 1); } else { XPA_IGB_M(64, 1); }
+        } else {
+            if (cinp == 16) { XPA_IGB_M(16, 2); } else if (cinp == 32) { XPA_IGB_M(32, 2); } else { XPA_IGB_M(64, 2); }
+        }
+#undef XPA_IGB_M
+#undef XPA_IGB
+        return xpa_launch_status();
+    }
     const unsigned grid = (unsigned)(args.nblk < kIgGrid ? args.nblk : kIgGrid);
 #define XPA_IG(C_, N_) hipLaunchKernelGGL((conv_igemm_kernel<C_, N_, MODE, ACT>), dim3(grid), dim3(kIgThreads), 0, s, args)
     if (nt == 1) {
@@ -686,6 +905,14 @@ bool ig_shape(int64_t cin, int64_t cout, int64_t k, int &cinp, int &nt) {
 XPA_API int xpa_conv_igemm_ok(int64_t in_channels, int64_t out_channels, int64_t kernel) {
     int cinp, nt;
     return ig_shape(in_channels, out_channels, kernel, cinp, nt) ? 1 : 0;
+}
+
+// r05: K28's arithmetic — bit 0: K28B (bf16 matrix cores, six split products; taken where the GEMM's input channels
+// are a multiple of 16), bit 1: K28B with 3 row tiles per wave (A/B); 0 = the fp32-MFMA K28.  mask < 0 only reads.
+XPA_API int xpa_conv_igemm_form(int mask) {
+    const int prev = g_ig_form;
+    if (mask >= 0) g_ig_form = mask;
+    return prev;
 }
 
 XPA_API int xpa_conv_fwd(int act, const float *x, int64_t batch, int64_t in_h, int64_t in_w, int64_t in_c,
