@@ -605,6 +605,15 @@ int xpa_s3_gemm(const float *a, int64_t lda, const void *b_split, float *c, int6
  * bit. */
 int xpa_s3_gemm_group(int n, const float *const *a, const void *const *b_split, float *const *c, int64_t lda,
                       int64_t ldc, int64_t m, int64_t k, xpa_stream_t stream);
+/* K40G with the previous block's activation backward (r05, C3's fc data gradient into conv3): c[p] = (a[p] . B[p]) x
+ * act'(y[p]) (act 0 identity / 1 LeakyReLU(slope) from the output y / 2 tanh; y[p] at c[p]'s offsets, row stride
+ * ldc), equal to xpa_act_bwd_bias's dz bit for bit, and per (problem, 256-row block) the column sums of c[p] per
+ * channel (column mod channels; channels 32 or 64, every c[p] starting at a multiple of channels columns) in
+ * bias_partial [xpa_s3_gemm_group_act_num_partials(n, m)][channels] for xpa_colsum_finalize.  K22 folded in. */
+int64_t xpa_s3_gemm_group_act_num_partials(int n, int64_t m);
+int xpa_s3_gemm_group_act(int n, const float *const *a, const void *const *b_split, float *const *c,
+                          const float *const *y, int64_t lda, int64_t ldc, int64_t m, int64_t k, int act, float slope,
+                          int64_t channels, float *bias_partial, xpa_stream_t stream);
 /* K41 — the weight gradient dW = a^T b over the batch on the same split (a [rows, m] = dz, row stride lda; b [rows, 256]
  * = the layer input, row stride ldb; m % 128 == 0), split-K: out [slices, m, 256] holds one partial per slice of
  * ceil(rows / slices) rows (rounded up to 32), summed by the caller — the learner's fixed-order f64 finalize, as for

@@ -467,3 +467,43 @@ def test_conv_dgrad_s2k_bf16_form_error_vs_fp32_form():
     e_b, e_f = (outs[0] - ref).abs().max().item(), (outs[1] - ref).abs().max().item()
     assert e_b <= 2 * e_f + 1e-9, (e_b, e_f)
     assert e_b <= 1e-5
+
+
+def test_fc_act_fused_backward_equals_k22_path(monkeypatch):
+    """r05: the fc data gradient with the last conv block's activation backward + bias partials in its epilogue
+    (xpa_s3_gemm_group_act) against the K40G data gradient + K22: every gradient bit for bit except that block's bias
+    (the same values summed in another order: f32 rounding)."""
+    from xuanpolicy_amd import fused_cnn
+    from xuanpolicy_amd.fused_cnn import FusedCNNActorCritic
+    monkeypatch.setattr(fused_cnn._Trunk, "igemm_min_rows", 0)
+    monkeypatch.setattr(fused_cnn._Trunk, "fc_split_min_rows", 0)
+    B = 300
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.int32).to(torch.uint8).to(DEV)
+    d_head = (torch.randn(B, 6, generator=g) / B).to(DEV)
+    d_v = (torch.randn(B, generator=g) / B).to(DEV)
+    grads = []
+    for fuse in (True, False):
+        monkeypatch.setattr(fused_cnn._Trunk, "fc_fuse_act", fuse)
+        pol = _c3_policy()
+        with torch.no_grad():
+            for n, p in pol.named_parameters():
+                if n.endswith("bias"):
+                    p.normal_(0, 0.1, generator=torch.Generator(device=p.device).manual_seed(len(n)))
+        fc = FusedCNNActorCritic(pol)
+        for p in pol.parameters():
+            p.grad = torch.full_like(p, float("nan"))
+        assert fc.trunk_._fc_fuse_ok(B) == fuse
+        _, _, _, ctx = fc.forward(x)
+        fc.backward(ctx, d_head, d_v)
+        torch.cuda.synchronize()
+        grads.append({n: p.grad.clone() for n, p in pol.named_parameters()})
+        last = [n for n, p in pol.named_parameters() if p is fc.trunk_.convs[-1][0].bias]
+    assert len(last) == 1
+    for n in grads[0]:
+        a, b = grads[0][n], grads[1][n]
+        assert torch.isfinite(a).all(), n
+        if n == last[0]:
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6 * float(b.abs().max()) + 1e-9, msg=n)
+        else:
+            assert torch.equal(a, b), n

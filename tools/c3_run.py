@@ -18,6 +18,9 @@ if __name__ == "__main__":
         if a.startswith("igemm-form="):   # r05 A/B: xpa_conv_igemm_form (bit 0 K28B)
             from xuanpolicy_amd import ops
             ops.lib().xpa_conv_igemm_form(int(a.split("=")[1]))
+        if a.startswith("fc-act="):   # r05 A/B: the last conv's activation backward in the fc epilogue (1) or K22 (0)
+            from xuanpolicy_amd import fused_cnn
+            fused_cnn._Trunk.fc_fuse_act = bool(int(a.split("=")[1]))
         if a.startswith("fc-split="):   # r05 A/B: the first fc layer on K40G (1) or hipBLASLt (0)
             from xuanpolicy_amd import fused_cnn
             fused_cnn._Trunk.fc_split = bool(int(a.split("=")[1]))

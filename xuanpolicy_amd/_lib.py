@@ -279,6 +279,9 @@ SIGNATURES = {
     "xpa_s3_split_batch": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_p, c_p]),
     "xpa_s3_gemm": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
     "xpa_s3_gemm_group": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
+    "xpa_s3_gemm_group_act_num_partials": (c_i64, [ctypes.c_int, c_i64]),
+    "xpa_s3_gemm_group_act": (ctypes.c_int, [ctypes.c_int, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, ctypes.c_int,
+                                             c_f32, c_i64, c_p, c_p]),
     "xpa_s3_wgrad_num_slices": (c_i64, [c_i64, c_i64]),
     "xpa_s3_gemm_trunk_bwd_num_partials": (c_i64, [c_i64]),
     "xpa_s3_gemm_trunk_bwd": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64, ctypes.c_int,

@@ -263,14 +263,34 @@ __device__ __forceinline__ void chunk64(const char *st, f32x16 (&acc)[8], int la
 // EPI (r05, K40F: the C4 trunk layer's forward): 0 = C = A B; 1 / 2 / 3 = C = act(A B + bias) with act identity /
 // LeakyReLU (slope) / tanh, and with `sign` (EPI 1 / 2) the output's sign bits beside it (32 bytes per row, byte col bit
 // cb = C[row, 32 cb + col] > 0: K42S's act' source, the layout xpa_thin_linear_act_fwd_gather_sign writes)
+// K40G's activation-backward epilogue (r05, C3's fc data gradient = d conv3 output): the stored value is
+// g act'(y) with y read at the output's own (row, column) (the previous block's output, same layout and row stride),
+// and the block's column sums of it per channel (column mod C, C = 32 / 64) go to bpart[(problem x gridDim.x + row
+// block) x C + channel] — K22 folded in
+struct S3ActBwd {
+    int act = -1;   // -1: none (a plain store)
+    float slope = 0.f;
+    int C = 64;
+    float *bpart = nullptr;
+};
+
+template <int ACT>
+__device__ __forceinline__ float s3_act_grad(float d, float y, float slope) {
+#pragma clang fp contract(off)  // conv.hip's act_grad / igemm.hip's ig_grad: the same value as K22 writes
+    if (ACT == 1) return y > 0.f ? d : d * slope;
+    if (ACT == 2) return d * (1.0f - y * y);
+    return d;
+}
+
 // the body of K40 for row block blk (s3_gemm_kernel: blk = blockIdx.x; s3_gemm_group_kernel: one of several
-// problems per blockIdx.y)
-template <int W, int S, int PROBE, int T64, int EPI>
+// problems per blockIdx.y).  AB >= 0 (EPI 0 only): the activation-backward epilogue above, y at the output's offsets
+template <int W, int S, int PROBE, int T64, int EPI, int AB = -1>
 __device__ __forceinline__ void s3_gemm_body(const float *__restrict__ a, int64_t lda, const __bf16 *__restrict__ bs,
                                              float *__restrict__ c, int64_t ldc, int64_t M, int nchunks,
                                              const float *__restrict__ bias, float slope,
                                              unsigned char *__restrict__ sign, const int64_t *__restrict__ ridx,
-                                             int64_t blk) {
+                                             int64_t blk, const float *__restrict__ yab = nullptr,
+                                             const S3ActBwd *abp = nullptr) {
     using G = S3Geom<W>;
     // ONE LDS array (the DMA target; see head.hip)
     __shared__ __attribute__((aligned(16))) char lds[S * G::kStage];
@@ -355,6 +375,45 @@ __device__ __forceinline__ void s3_gemm_body(const float *__restrict__ a, int64_
         }
         return;
     }
+    if constexpr (AB >= 0) {
+        float s0 = 0.f, s1 = 0.f;   // channel col (even column blocks), 32 + col (odd; C = 32: both col)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t row = r0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (row < M) {
+                float *crow = c + row * ldc + col;
+                const float *yrow = yab + row * ldc + col;
+                float yv[8];
+#pragma unroll
+                for (int cb = 0; cb < 8; ++cb) yv[cb] = yrow[cb * 32];
+#pragma unroll
+                for (int cb = 0; cb < 8; ++cb) {
+                    const float v = s3_act_grad<AB>(acc[cb][r], yv[cb], abp->slope);
+                    crow[cb * 32] = v;
+                    if (cb & 1) s1 += v;
+                    else s0 += v;
+                }
+            }
+        }
+        s0 += __shfl_xor(s0, 32, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        __syncthreads();   // every wave is past the k loop: the LDS ring is free
+        float *red = reinterpret_cast<float *>(lds);
+        if (h == 0) {
+            red[wave * 64 + col] = s0;
+            red[wave * 64 + 32 + col] = s1;
+        }
+        __syncthreads();
+        const int t = threadIdx.x;
+        const int C = abp->C;
+        if (t < C) {
+            float tot = 0.f;
+            for (int w = 0; w < W; ++w)
+                tot += C == 64 ? red[w * 64 + t] : red[w * 64 + t] + red[w * 64 + 32 + t];
+            abp->bpart[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * C + t] = tot;
+        }
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int64_t row = r0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -386,13 +445,15 @@ struct S3Group {
     const float *a[kS3Groups];
     const __bf16 *b[kS3Groups];
     float *c[kS3Groups];
+    const float *y[kS3Groups];   // AB >= 0: the previous block's output at c[p]'s offsets
 };
 
+template <int AB>
 __global__ __launch_bounds__(512, 1) void s3_gemm_group_kernel(S3Group g, int64_t lda, int64_t ldc, int64_t M,
-                                                               int nchunks) {
+                                                               int nchunks, S3ActBwd ab) {
     const int p = blockIdx.y;
-    s3_gemm_body<8, 3, 0, 0, 0>(g.a[p], lda, g.b[p], g.c[p], ldc, M, nchunks, nullptr, 0.f, nullptr, nullptr,
-                                blockIdx.x);
+    s3_gemm_body<8, 3, 0, 0, 0, AB>(g.a[p], lda, g.b[p], g.c[p], ldc, M, nchunks, nullptr, 0.f, nullptr, nullptr,
+                                    blockIdx.x, g.y[p], &ab);
 }
 
 // K40R (r05): the rollout's paired hidden layer z [M, 512] = x [M, 256] . [B0 | B1] + bias (B0 / B1 = Wh_actor^T /
@@ -2266,8 +2327,43 @@ XPA_API int xpa_s3_gemm_group(int n, const float *const *a, const void *const *b
         g.b[p] = static_cast<const __bf16 *>(b_split[p]);
         g.c[p] = c[p];
     }
-    s3_gemm_group_kernel<<<dim3((unsigned)((m + 255) / 256), (unsigned)n), dim3(512), 0, stream>>>(g, lda, ldc, m,
-                                                                                                    (int)(k / kKC));
+    s3_gemm_group_kernel<-1><<<dim3((unsigned)((m + 255) / 256), (unsigned)n), dim3(512), 0, stream>>>(
+        g, lda, ldc, m, (int)(k / kKC), S3ActBwd{});
+    return xpa_launch_status();
+}
+
+// K40G with the previous block's activation backward in the epilogue (r05): c[p] = (a[p] . B[p]) act'(y[p]) (act 0
+// identity / 1 LeakyReLU(slope) from the output y / 2 tanh), and per (problem, row block) the column sums of c[p] per
+// channel (column mod channels, channels 32 or 64; each c[p] must start at a multiple of `channels` columns of the
+// layer) into bias_partial [n x ceil(m / 256)][channels] (xpa_s3_gemm_group_act_num_partials).  K22's output and
+// bias partials in one launch; the stored values equal xpa_act_bwd_bias's dz bit for bit.
+XPA_API int64_t xpa_s3_gemm_group_act_num_partials(int n, int64_t m) { return (int64_t)n * ((m + 255) / 256); }
+
+XPA_API int xpa_s3_gemm_group_act(int n, const float *const *a, const void *const *b_split, float *const *c,
+                                  const float *const *y, int64_t lda, int64_t ldc, int64_t m, int64_t k, int act,
+                                  float slope, int64_t channels, float *bias_partial, xpa_stream_t stream) {
+    if (n < 1 || n > kS3Groups || !a || !b_split || !c || !y || !bias_partial || m <= 0 || k <= 0 || k % kKC != 0 ||
+        lda < k || ldc < kN || (lda & 3) || k / kKC > (1 << 20) || (m + 255) / 256 > 0x7fffffff || act < 0 || act > 2 ||
+        (channels != 32 && channels != 64))
+        return (int)hipErrorInvalidValue;
+    S3Group g{};
+    for (int p = 0; p < n; ++p) {
+        if (!a[p] || !b_split[p] || !c[p] || !y[p] || (reinterpret_cast<uintptr_t>(a[p]) & 15))
+            return (int)hipErrorInvalidValue;
+        g.a[p] = a[p];
+        g.b[p] = static_cast<const __bf16 *>(b_split[p]);
+        g.c[p] = c[p];
+        g.y[p] = y[p];
+    }
+    S3ActBwd ab;
+    ab.act = act;
+    ab.slope = slope;
+    ab.C = (int)channels;
+    ab.bpart = bias_partial;
+    const dim3 grid((unsigned)((m + 255) / 256), (unsigned)n);
+    if (act == 0) s3_gemm_group_kernel<0><<<grid, dim3(512), 0, stream>>>(g, lda, ldc, m, (int)(k / kKC), ab);
+    else if (act == 1) s3_gemm_group_kernel<1><<<grid, dim3(512), 0, stream>>>(g, lda, ldc, m, (int)(k / kKC), ab);
+    else s3_gemm_group_kernel<2><<<grid, dim3(512), 0, stream>>>(g, lda, ldc, m, (int)(k / kKC), ab);
     return xpa_launch_status();
 }
 

@@ -288,6 +288,32 @@ class _Trunk:
         _bias_act(code, s, lin.bias, slope)
         return s
 
+    # r05: with the fc split, the data gradient's epilogue also applies the last conv block's activation backward and
+    # writes its bias-gradient partials (xpa_s3_gemm_group_act): that block's K22 pass over [B x H x W, C] is gone
+    fc_fuse_act = True
+
+    def _fc_fuse_ok(self, rows):
+        conv, code, _ = self.convs[-1]
+        in_f = self.fc[0][0].in_features
+        return (self.fc_fuse_act and self._fc_split_ok(rows) and in_f % 256 == 0 and conv.out_channels in (32, 64)
+                and code in (0, 1, 2))
+
+    def _fc0_dgrad_split_act(self, g, y_flat):
+        """dz of the last conv block (its output gradient x act'(its output)) from the fc's K40G data gradient, and
+        that block's bias gradient (f64 finalize of the per-block partials)."""
+        rows = g.shape[0]
+        _, _, bd, c0s = self._fc_planes()
+        conv, code, slope = self.convs[-1]
+        C = conv.out_channels
+        dz = torch.empty((rows, self.fc[0][0].in_features), dtype=torch.float32, device=g.device)
+        G = int(ops.lib().xpa_s3_gemm_group_act_num_partials(len(c0s), rows))
+        part = self.parts.buf(("fcab", rows, C), (G, C), g.device)
+        ops.s3_gemm_group_act([(g, b, dz[:, c0:c0 + 256]) for b, c0 in zip(bd, c0s)], g.shape[1],
+                              [y_flat[:, c0:c0 + 256] for c0 in c0s], code, slope, C, part)
+        _lib.check(ops.lib().xpa_colsum_finalize(ops._p(part), G, C, ops._p(conv.bias.grad), ops._stream(g.device)),
+                   "colsum db (fc act)")
+        return dz
+
     def _fc0_dgrad_split(self, g):
         rows = g.shape[0]
         _, _, bd, c0s = self._fc_planes()
@@ -503,6 +529,7 @@ class _Trunk:
         B = hs[0].shape[0]
         parts = self.parts
         g = ds
+        fused_dz = False   # g leaves the fc part as the last conv block's dz (its K22 done in the fc epilogue)
         if self.tail == "flatten":
             for j in range(len(self.fc) - 1, -1, -1):
                 lin, code, slope = self.fc[j]
@@ -516,7 +543,10 @@ class _Trunk:
                     Cl, Hl, Wl = self._chw
                     lin.weight.grad.view(lin.out_features, Cl, Hl, Wl).copy_(
                         self._dw_tmp.view(lin.out_features, Hl, Wl, Cl).permute(0, 3, 1, 2))
-                    if self._fc_split_ok(g.shape[0]):
+                    if self._fc_fuse_ok(g.shape[0]) and flat.is_contiguous():
+                        g = self._fc0_dgrad_split_act(g, flat)
+                        fused_dz = True
+                    elif self._fc_split_ok(g.shape[0]):
                         g = self._fc0_dgrad_split(g)
                     else:
                         g = torch.mm(g, self._fc0_weight())
@@ -526,7 +556,7 @@ class _Trunk:
         # conv blocks, last to first.  g is the NHWC gradient of the block's output (after its activation), or — once
         # a fused step has applied the activation backward (K24 for the max-pool tail, K28's data gradient epilogue) —
         # its pre-activation gradient dz (g_dz), with that block's bias gradient already written.
-        g_dz = False
+        g_dz = fused_dz
         for i in range(len(self.convs) - 1, -1, -1):
             conv, code, slope = self.convs[i]
             y = hs[i + 1]

@@ -331,6 +331,30 @@ def s3_gemm_group(problems, k):
                "xpa_s3_gemm_group")
 
 
+def s3_gemm_group_act(problems, k, ys, act, slope, channels, bias_partial):
+    """K40G with the previous block's activation backward (r05): problems as s3_gemm_group, ys the previous block's
+    output at each out's offsets (same row stride); bias_partial [xpa_s3_gemm_group_act_num_partials, channels]."""
+    n = len(problems)
+    if not 1 <= n <= 32 or len(ys) != n:
+        raise ValueError("1..32 problems, one y each")
+    a0, _, c0 = problems[0]
+    m = a0.shape[0]
+    lda, ldc = _row_stride(a0, "a", k), _row_stride(c0, "out", 256)
+    for (a, _, c), y in zip(problems, ys):
+        _req(a, "a", torch.float32, contiguous=False)
+        _req(c, "out", torch.float32, contiguous=False)
+        _req(y, "y", torch.float32, contiguous=False)
+        if a.shape[0] != m or c.shape[0] != m or a.stride(0) != lda or c.stride(0) != ldc or a.shape[1] != k or \
+                y.shape != c.shape or y.stride() != c.stride():
+            raise ValueError("s3_gemm_group_act: one m / lda / ldc, y shaped and strided as out")
+    G = int(lib().xpa_s3_gemm_group_act_num_partials(n, m))
+    _req(bias_partial, "bias_partial", torch.float32, (G, channels))
+    arr = lambda ts: (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])   # noqa: E731
+    _lib.check(lib().xpa_s3_gemm_group_act(n, arr([p[0] for p in problems]), arr([p[1] for p in problems]),
+                                           arr([p[2] for p in problems]), arr(ys), lda, ldc, m, k, act, float(slope),
+                                           channels, _p(bias_partial), _stream(a0.device)), "xpa_s3_gemm_group_act")
+
+
 def s3_gemm_trunk_bwd(dz, b_split, k, h, x, act, slope, partial_dw=None, partial_db=None, h_sign=None):
     """K42: g = dz [rows, k] . B (split) kept in registers; the first representation layer's backward on it (dz1 =
     g * act'(h), its bias / weight gradients) as per-block partials ([G, 256 * d_in], [G, 256]); g is not stored.
