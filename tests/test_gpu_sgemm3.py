@@ -297,3 +297,37 @@ def test_gemm_trunk_bwd_matches_f64(rows, din, act):
         scale = ref.abs().max().item()
         err = (got - ref).abs().max().item()
         assert err <= 2e-5 * scale, (what, err, scale)
+
+
+@pytest.mark.parametrize("act,slope,channels,m", [(1, 0.0, 64, 16384), (1, 0.01, 32, 777), (2, 0.0, 64, 300),
+                                                  (0, 0.0, 32, 5)])
+def test_gemm_group_act_equals_group_then_k22(act, slope, channels, m):
+    """xpa_s3_gemm_group_act (r05): the stored values equal K40G's output passed through K22 (xpa_act_bwd_bias) bit
+    for bit, and its per-channel bias partials sum (f64 finalize) to K22's bias gradient within f32 order rounding."""
+    from xuanpolicy_amd import _lib, ops
+    L, st = ops.lib(), ops._stream(DEV)
+    g = torch.Generator(device=DEV).manual_seed(m + 3 * act)
+    in_f, out_f = 1024, 512
+    gz = _wide((m, out_f), g, 1e-2)
+    w = torch.randn(out_f, in_f, device=DEV, generator=g) / 16
+    y = torch.randn(m, in_f, device=DEV, generator=g)
+    y = torch.tanh(y) if act == 2 else (torch.where(y > 0, y, y * slope) if act == 1 else y)
+    c0s = list(range(0, in_f, 256))
+    planes = [ops.s3_split(w[:, c0:c0 + 256]) for c0 in c0s]
+    dz = torch.full((m, in_f), float("nan"), device=DEV)
+    G = int(L.xpa_s3_gemm_group_act_num_partials(len(c0s), m))
+    part = torch.full((G, channels), float("nan"), device=DEV)
+    ops.s3_gemm_group_act([(gz, p, dz[:, c0:c0 + 256]) for p, c0 in zip(planes, c0s)], out_f,
+                          [y[:, c0:c0 + 256] for c0 in c0s], act, slope, channels, part)
+    db = torch.empty(channels, device=DEV)
+    _lib.check(L.xpa_colsum_finalize(ops._p(part), G, channels, ops._p(db), st), "finalize")
+    dx = torch.full((m, in_f), float("nan"), device=DEV)
+    ops.s3_gemm_group([(gz, p, dx[:, c0:c0 + 256]) for p, c0 in zip(planes, c0s)], out_f)
+    rows = m * in_f // channels
+    kp = torch.empty(int(L.xpa_act_bwd_bias_num_partials(rows, channels)), channels, device=DEV)
+    _lib.check(L.xpa_act_bwd_bias(act, ops._p(dx), ops._p(y), rows, channels, slope, ops._p(dx), ops._p(kp), st), "k22")
+    db_ref = torch.empty(channels, device=DEV)
+    _lib.check(L.xpa_colsum_finalize(ops._p(kp), kp.shape[0], channels, ops._p(db_ref), st), "finalize")
+    torch.cuda.synchronize()
+    assert torch.equal(dz, dx)
+    torch.testing.assert_close(db, db_ref, rtol=1e-5, atol=1e-5 * float(dx.abs().sum(0).max()) + 1e-9)
