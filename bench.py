@@ -74,6 +74,9 @@ def parse():
                    help="the rollout's paired hidden GEMM on the split (K40R, r05) or the f32 library GEMM")
     p.add_argument("--wide-trunk", choices=("on", "off"), default="on",
                    help="C4's 376-wide trunk layer on the split GEMMs (K40F / K42W / K41V, r05) or the f32 library GEMMs")
+    p.add_argument("--dp-path", choices=("on", "off"), default="on",
+                   help="at world 1: also time C2 with the data-parallel update path attached (distributed.LocalGradSync: "
+                        "its own clip-norm pass, eager K9; no collective) -> dp_update_path")
     p.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc HBM-traffic passes")
     p.add_argument("--no-rocprof", action="store_true",
                    help="skip the child rocprofv3 --kernel-trace run that times the in-loop GAE launches")
@@ -735,6 +738,8 @@ def c4_bench(device, rank, world, n_envs=4096, n_steps=128, steps=2, warmup=1):
     for _ in range(warmup):
         agent.train(n_steps)
     torch.cuda.synchronize()
+    gs = agent.learner.grad_sync
+    c0 = gs.collectives if gs is not None else 0
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -744,6 +749,7 @@ def c4_bench(device, rank, world, n_envs=4096, n_steps=128, steps=2, warmup=1):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    n_upd = steps * agent.n_epoch * agent.n_minibatch
     if world > 1:
         e = torch.tensor([el], dtype=torch.float64, device=device)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -752,7 +758,39 @@ def c4_bench(device, rank, world, n_envs=4096, n_steps=128, steps=2, warmup=1):
                        "nets [256] LeakyReLU" % (n_envs, world, n_steps),
            "metric": "env-steps/s", "value": round(world * n_envs * n_steps * steps / el, 1),
            "ms_per_iteration": round(el / steps * 1e3, 2), "iterations": steps, "n_gpus": world,
-           "fused_heads": bool(getattr(agent.learner._fused_mlp(), "fused_heads", False))}
+           "fused_heads": bool(getattr(agent.learner._fused_mlp(), "fused_heads", False)),
+           "collectives_per_minibatch": (gs.collectives - c0) / n_upd if gs is not None else 0}
+    del agent
+    torch.cuda.empty_cache()
+    return res
+
+
+def dp_path_bench(device, args, steps=3, warmup=1):
+    """C2 on one GPU with the data-parallel update path attached (distributed.LocalGradSync in place of the
+    all-reduce): the per-rank cost of world > 1 apart from the collective itself — the clip norm from its own pass
+    (the producers' partials are not the averaged gradient's), K9 launched eagerly per minibatch."""
+    import torch
+    from xuanpolicy_amd.distributed import LocalGradSync
+    from xuanpolicy_amd.runner import build_synthbox_ppo
+    N, T = args.n_envs, args.horizon
+    agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=args.obs_dim, act_dim=args.act_dim, hidden=args.hidden,
+                               n_epoch=args.n_epoch, n_minibatch=args.n_minibatch, seed=1, device=device)
+    agent.learner.enable_fast_path()
+    agent.fuse_value_gae = args.gae_form == "value"
+    hook = agent.learner.grad_sync = LocalGradSync(agent.learner.flat_grads)
+    for _ in range(warmup):
+        agent.train(T)
+    torch.cuda.synchronize()
+    c0 = hook.calls
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        agent.train(T)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    res = {"what": "C2 with the world > 1 update path on one GPU (grad_sync hook without a collective: own clip-norm "
+                   "pass, eager K9 per minibatch)", "value": round(N * T * steps / el, 1), "unit": "env-steps/s",
+           "ms_per_iteration": round(el / steps * 1e3, 3), "iterations": steps,
+           "hook_calls_per_minibatch": (hook.calls - c0) / (steps * args.n_epoch * args.n_minibatch)}
     del agent
     torch.cuda.empty_cache()
     return res
@@ -853,8 +891,88 @@ def cpu_baseline(args, cores):
     return res
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(gpus, argv, port):
+    """The child command of a self-launched multi-rank run: torch.distributed.run, one process per GPU of this node,
+    rendezvous on 127.0.0.1, this script with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def check_world(gpus, env=None):
+    """--gpus N is the number of ranks: under a launcher (WORLD_SIZE in the environment) it must equal WORLD_SIZE.
+    Returns the launcher's world size, or None when no launcher started this process."""
+    env = os.environ if env is None else env
+    if "WORLD_SIZE" not in env:
+        return None
+    world = int(env["WORLD_SIZE"])
+    if world != gpus:
+        raise SystemExit("bench.py: --gpus %d but the launcher started WORLD_SIZE=%d ranks; they must agree"
+                         % (gpus, world))
+    return world
+
+
+def self_launch(args, argv):
+    """`python bench.py --gpus N` (N > 1) with no launcher environment: start the N ranks as children through
+    torch.distributed.run — before this process touches torch.cuda or HIP, and as a child process, never an exec —
+    relay their output (stderr and every non-JSON stdout line to stderr, as it arrives), print rank 0's JSON line
+    and exit with the launcher's status.  Every rank then asserts WORLD_SIZE == --gpus (check_world)."""
+    import subprocess
+    cmd = launch_cmd(args.gpus, argv, _free_port())
+    print("bench.py: launching %d ranks: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, cwd=REPO)
+    line = None
+    for ln in p.stdout:
+        if ln.startswith("{") and '"metric"' in ln:
+            line = ln.strip()
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = p.wait()
+    if line is not None:
+        print(line, flush=True)
+    if rc == 0 and line is None:
+        print("bench.py: the ranks exited 0 without a JSON line", file=sys.stderr)
+        rc = 1
+    return rc
+
+
+def allreduce_probe(learner, device, reps=20):
+    """world > 1: one all-reduce of a buffer of the flat gradient's size (not the gradient itself) on this process
+    group, timed over `reps` back-to-back calls (host clock, synchronised): the per-minibatch collective's cost."""
+    import torch
+    import torch.distributed as dist
+    gs = getattr(learner, "grad_sync", None)
+    if gs is None:
+        return None
+    buf = torch.zeros_like(gs.fg.flat)
+    op = dist.ReduceOp.AVG if gs.avg else dist.ReduceOp.SUM
+    for _ in range(3):
+        dist.all_reduce(buf, op=op)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.all_reduce(buf, op=op)
+    torch.cuda.synchronize()
+    us = (time.perf_counter() - t0) / reps * 1e6
+    t = torch.tensor([us], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return {"bytes": int(buf.numel() * buf.element_size()), "avg_us": round(float(t), 2), "reps": reps,
+            "backend": dist.get_backend()}
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and check_world(args.gpus) is None:
+        sys.exit(self_launch(args, sys.argv[1:]))
+    check_world(args.gpus)
     import torch
     import torch.distributed as dist
     from xuanpolicy_amd import ops
@@ -901,6 +1019,8 @@ def main():
     ops.TIMER.enabled = not args.no_kernel_timing
     ops.TIMER.only = {"gae"}
     ops.TIMER.reset()
+    gs = agent.learner.grad_sync
+    coll0 = gs.collectives if gs is not None else 0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -915,6 +1035,17 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e)
+    n_updates = args.steps * args.n_epoch * args.n_minibatch
+    dp = None
+    if world > 1:
+        probe = allreduce_probe(agent.learner, device)
+        ms_step = elapsed / args.steps * 1e3
+        dp = {"collectives_per_minibatch": (gs.collectives - coll0) / n_updates if gs is not None else None,
+              "allreduce": probe,
+              "allreduce_time_share": (round(probe["avg_us"] * 1e-3 * args.n_epoch * args.n_minibatch / ms_step, 4)
+                                       if probe else None),
+              "note": "allreduce: one all-reduce of a buffer of the flat gradient's size, timed alone after the timed "
+                      "region (max over ranks); time share = its time x updates per iteration / ms_per_step"}
     gae_ms_timed = ops.TIMER.mean_ms("gae")
     gae_launches = ops.TIMER.count("gae")
     # One more (untimed) iteration with event pairs around the K12 launches and the paired GEMM, and
@@ -1140,6 +1271,8 @@ def main():
         }
         if c4 is not None:
             result["c4_box376"] = c4
+        if dp is not None:
+            result["data_parallel"] = dp
         if not args.no_sweep and world == 1:
             result["gae_sweep_flushed"] = gae_sweep(device, horizon=T)
             ls = loss_sweep(device, act_dim=args.act_dim)
@@ -1153,6 +1286,8 @@ def main():
                     "unit": "GB/s", "frac": k2["frac"], "algorithmic_bytes_per_launch": k2["algorithmic_bytes"],
                     "timing": "host-recorded events around one launch after a 512 MiB cache-flush read (median of 7); "
                               "see loss_sweep_flushed for larger batches"}
+        if args.dp_path == "on" and world == 1:
+            result["dp_update_path"] = dp_path_bench(device, args)
         if not args.no_c1 and world == 1:
             result["c1_cartpole"] = c1_bench(device)
         if not args.no_c3 and world == 1:

@@ -496,7 +496,8 @@ class LearnerRef:
         torch = _torch()
         self.iterations += 1
         if not (isinstance(obs, np.ndarray) and obs.dtype == np.uint8):   # raw frames: the policy scales them
-            obs = torch.as_tensor(obs, dtype=torch.float32)
+            # f32 observations; an f64 replay (precision envelopes) takes them exactly in its parameters' dtype
+            obs = torch.as_tensor(obs, dtype=torch.float32).to(next(self.policy.parameters()).dtype)
         act = torch.as_tensor(act)
         head, logstd, v = self.policy.heads(obs)
         ret = torch.as_tensor(ret).to(v.dtype)   # (the parameters' dtype: f32, or f64 for precision envelopes)

@@ -72,19 +72,26 @@ def envelope_atari(name="atari_a2c_prod.npz"):
     nl = (len(net) - 1) // 3
     filters, kernels, strides, fc = net[:nl], net[nl:2 * nl], net[2 * nl:3 * nl], net[3 * nl:]
     pol = cpu_ref.build_atari_ac_ref(K, filters, kernels, strides, fc)
-    ref_keys = [k[len("sd0sum/"):] for k in g if k.startswith("sd0sum/")]
+    small = "init_seed" not in g   # the small-net fixtures store their starting weights (sd0/)
+    pre = "sd0/" if small else "sd0sum/"
+    ref_keys = [k[len(pre):] for k in g if k.startswith(pre)]
     mine = list(pol.state_dict().keys())
     assert len(mine) == len(ref_keys)
     # the reference's state_dict order (representation, actor, critic) == the oracle's (critic_head last)
     order = [k for k in ref_keys if k.startswith("representation")] + [k for k in ref_keys if k.startswith("actor")] \
         + [k for k in ref_keys if k.startswith("critic")]
     shapes = [(k, pol.state_dict()[m].shape) for k, m in zip(order, mine)]
-    vals = uniform_state(shapes, int(g["init_seed"]))
+    vals = {k: g["sd0/" + k] for k, _ in shapes} if small else uniform_state(shapes, int(g["init_seed"]))
     pol.load_state_dict({m: torch.as_tensor(vals[k]) for k, m in zip(order, mine)})
     pol.double()
-    opt = torch.optim.Adam(pol.parameters(), 7e-4, eps=1e-5)
+    ppo = int(g.get("algo", 0)) == 1   # G12P: PPOCLIP_Agent (ppo/atari.yaml coefficients, make_golden.capture_atari)
+    if ppo:
+        lr, vf, ent, clip, gn = (float(x) for x in g["hyper"])
+    else:
+        lr, vf, ent, clip, gn = 7e-4, 0.25, 0.01, 0.0, 0.2
+    opt = torch.optim.Adam(pol.parameters(), lr, eps=1e-5)
     sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.0, total_iters=10000)
-    lrn = cpu_ref.LearnerRef(pol, opt, sch, "a2c", 0.25, 0.01, 0.0, 0.2, True)
+    lrn = cpu_ref.LearnerRef(pol, opt, sch, "ppo" if ppo else "a2c", vf, ent, clip, gn, True)
     envs = [SynthAtariEnv(i, seed=seed, n_actions=K, max_episode_steps=max_ep) for i in range(N)]
     obs = np.stack([e.reset()[0] for e in envs])
     B = N * T // n_mb
@@ -112,9 +119,10 @@ def envelope_atari(name="atari_a2c_prod.npz"):
                 idx = perm[s:s + B]
                 a = adv[idx]
                 a = (a - a.mean()) / (a.std() + 1e-8)    # memory_tools.py:241-242 (sample's adv-norm)
-                info = lrn.update(fl[idx], act[idx].astype(np.int64), ret[idx], a.astype(np.float32))
+                info = lrn.update(fl[idx], act[idx].astype(np.int64), ret[idx], a.astype(np.float32),
+                                  old_logp=g["old_logp"][it].reshape(-1)[idx] if ppo else None)
                 got = [info["actor-loss"], info["critic-loss"], info["entropy"], info["learning_rate"],
-                       info["predict_value"]]
+                       info["predict_value"]] + ([info["clip_ratio"]] if ppo else [])
                 infos.append(np.abs(np.asarray(got) - g["infos"][u]))
                 u += 1
     res = {"info": np.stack(infos)}
@@ -135,3 +143,5 @@ if __name__ == "__main__":
     torch.set_num_threads(8)
     envelope_perdqn()
     envelope_atari()
+    envelope_atari("atari_ppo_prod.npz")
+    envelope_atari("atari_ppo.npz")

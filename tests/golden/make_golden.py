@@ -398,12 +398,16 @@ def _uniform_init(policy, seed, out):
 
 
 def capture_atari(N=4, T=16, iters=2, max_ep=20, n_actions=6, seed=5, net=ATARI_NET, n_minibatch=2, n_epoch=2,
-                  fname="atari_a2c.npz", init_seed=None):
+                  fname="atari_a2c.npz", init_seed=None, algo="a2c"):
+    """G8 / G8P (algo "a2c": a2c/atari.yaml's coefficients) and G12 / G12P (algo "ppo": PPOCLIP_Agent with env_name
+    "Atari" and ppo/atari.yaml's lr 2.5e-4, clip_range 0.2, clip_grad_norm 0.5, vf 0.25, ent 0.01 —
+    examples/ppo/ppo_atari.py's agent; the buffer's old_logp column and the clip_ratio info are recorded too)."""
     cfg = types.SimpleNamespace(render=False, n_steps=T, n_minibatch=n_minibatch, n_epoch=n_epoch, gamma=0.99,
                                 gae_lambda=0.95, env_name="Atari", use_gae=True, use_advnorm=True, device="cpu", model_dir="./models/",
                                 log_dir="./logs/", vf_coef=0.25, ent_coef=0.01, clip_grad=0.2, use_obsnorm=False,
                                 use_rewnorm=False, obsnorm_range=5, rewnorm_range=5, seed=seed, logger="tensorboard",
-                                test_mode=False)
+                                test_mode=False, clip_range=0.2, clip_grad_norm=0.5, use_grad_clip=True)
+    lr = 7e-4 if algo == "a2c" else 2.5e-4
     np.random.seed(seed)
     torch.manual_seed(seed)
     obs_space, act_space = gym.spaces.Box(0, 255, (84, 84, 4)), gym.spaces.Discrete(n_actions)
@@ -425,9 +429,9 @@ def capture_atari(N=4, T=16, iters=2, max_ep=20, n_actions=6, seed=5, net=ATARI_
         _sd("sd0/", policy, out)
     else:
         _uniform_init(policy, init_seed, out)
-    opt = torch.optim.Adam(policy.parameters(), 7e-4, eps=1e-5)
+    opt = torch.optim.Adam(policy.parameters(), lr, eps=1e-5)
     sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.0, total_iters=10000)
-    agent = A2C_Agent(cfg, envs, policy, opt, sch, "cpu")
+    agent = (A2C_Agent if algo == "a2c" else PPOCLIP_Agent)(cfg, envs, policy, opt, sch, "cpu")
     envs.reset()
     rec = {"closed": np.zeros((iters, N, T), np.uint8), "boot": np.zeros((iters, N, T), np.float32)}
     snaps, perms, infos, env_acts = [], [], [], []
@@ -447,14 +451,15 @@ def capture_atari(N=4, T=16, iters=2, max_ep=20, n_actions=6, seed=5, net=ATARI_
         snaps.append({"act": mem.actions.copy(), "rew": mem.rewards.copy(), "val": mem.values.copy(),
                       "term": mem.terminals.copy(), "ret": mem.returns.copy(), "adv": mem.advantages.copy(),
                       "frame_sum": mem.observations.reshape(N, T, -1).astype(np.int64).sum(-1),
-                      "obs_dtype_u8": np.asarray(mem.observations.dtype == np.uint8)})
+                      "obs_dtype_u8": np.asarray(mem.observations.dtype == np.uint8),
+                      "old_logp": (mem.auxiliary_infos["old_logp"].copy() if algo == "ppo" else np.zeros(0))})
         it["k"] += 1
         return orig_clear()
 
     def update(*a):
         info = orig_update(*a)
         infos.append([float(info[k]) for k in ("actor-loss", "critic-loss", "entropy", "learning_rate",
-                                                "predict_value")])
+                                                "predict_value") + (("clip_ratio",) if algo == "ppo" else ())])
         return info
 
     def shuffle(x):
@@ -471,8 +476,10 @@ def capture_atari(N=4, T=16, iters=2, max_ep=20, n_actions=6, seed=5, net=ATARI_
         agent.train(iters * T)
     finally:
         np.random.shuffle = orig_shuffle
-    for k in ("act", "rew", "val", "term", "ret", "adv", "frame_sum"):
+    for k in ("act", "rew", "val", "term", "ret", "adv", "frame_sum") + (("old_logp",) if algo == "ppo" else ()):
         out[k] = np.stack([s_[k] for s_ in snaps])
+    out["algo"] = np.asarray(0 if algo == "a2c" else 1, np.int64)
+    out["hyper"] = np.asarray([lr, cfg.vf_coef, cfg.ent_coef, cfg.clip_range, cfg.clip_grad_norm], np.float64)
     assert all(bool(s_["obs_dtype_u8"]) for s_ in snaps)
     out["closed"], out["boot"] = rec["closed"], rec["boot"]
     out["env_actions"] = np.stack(env_acts).astype(np.int64)
@@ -803,6 +810,11 @@ if __name__ == "__main__":
         capture_perdqn(B=2048, n_updates=3, seed=23, sync=2, net=PERDQN_PROD_NET, fname="perdqn_prod.npz",
                        every_sd=False)
         capture_perdqn_agent()
+    if "ppo_atari" in which:   # round 6: G12 / G12P, examples/ppo/ppo_atari.py's PPOCLIP_Agent on Atari frames
+        torch.set_num_threads(8)
+        capture_atari(N=4, T=16, iters=2, max_ep=20, n_minibatch=4, n_epoch=4, fname="atari_ppo.npz", algo="ppo")
+        capture_atari(N=8, T=64, iters=2, max_ep=40, net=ATARI_PROD_NET, n_minibatch=4, n_epoch=4,
+                      fname="atari_ppo_prod.npz", init_seed=27, algo="ppo")
     if "vecloop" in which:   # round 5: G11
         for name in VEC_CASES:
             capture_vecloop(name)

@@ -111,34 +111,26 @@ def _check_sd1(pol, g, rtol, atol, env=None, efac=3):
         np.testing.assert_allclose(rs, g["sd1/" + key + "::rowsum"], rtol=rtol, atol=tol, err_msg=key + " row sums")
 
 
-@pytest.mark.parametrize("fixture", ["atari_a2c.npz", "atari_a2c_prod.npz"])
-def test_a2c_atari_replays_reference_agent(golden, fixture, conv_path):
-    """G8: the reference's two recorded A2C_Agent iterations on Atari-shaped frames (a2c_agent.py:57-107,
-    env_name "Atari": DummyOnPolicyBuffer_Atari memory_tools.py:526-560, AC_CNN_Atari cnn.py:45-93 +
-    Categorical_AC_Policy, life losses keep the path open) replayed through the device buffer (uint8 frames,
-    K1 GAE with the Atari closures, K4 sample + adv-norm) and A2C_Learner (CNN on K25-K29 or MIOpen per conv_path, hipBLASLt, K2
-    categorical loss, K9 clip + Adam): GAE, every update's info dict, the final parameters.  The frames are
-    regenerated by stepping the oracle SynthAtari env with the recorded actions through the reference's
-    DummyVecEnv / agent observation flow and checked against the recorded per-step frame sums.
-    atari_a2c_prod.npz (G8P) is the production net (filters [32, 64, 64], kernels [8, 4, 3], strides [4, 2, 1], fc
-    512; 8 envs x 64 steps, minibatches of 256): the fused path of the C3 bench — K25 conv1 from the uint8 frames,
-    MIOpen conv2 / conv3, the (H, W, C)-permuted fc0 weight, K2, K26 conv1 weight gradient with the folded ReLU
-    backward + bias, K27 stride-2 data gradient — replayed update by update.  A few Adam steps of an f32 net are
-    chaotic in the last bits (tests/golden/make_envelopes.py): the prod fixture carries, per update and per tensor, how
-    far the exact f64 replay lands from the reference, and the tolerances are max(base, 3 x that envelope) — update 0
-    (identical starting weights) is held to the base tolerances."""
+def _gae_close(got, ref):
+    """north_star's 1e-5 (absolute, plus 1e-5 relative), widened by 2^-20 of the row's largest |value| (the scan's f32
+    rounding is relative to the row's largest partial sum; tests/test_gpu_kernels.py::_gae_close)."""
+    got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+    row = np.abs(ref).max(axis=-1, keepdims=True)
+    tol = 1e-5 + 1e-5 * np.abs(ref) + 2.0 ** -20 * row
+    bad = np.abs(got - ref) > tol
+    assert not bad.any(), ("GAE mismatch", int(bad.sum()), float(np.abs(got - ref)[bad].max()))
+
+
+def _replay_atari(g, env, conv_path, efac=3, rtol=1e-4, base_atol=1e-5):
+    """Replay a G8 / G12 fixture (make_golden.capture_atari) through the device buffer and the learner the agent uses:
+    A2C_Learner (algo 0) or PPOCLIP_Learner (algo 1, old_logp from the buffer's aux column, clip_ratio checked).
+    Loss scalars: rtol 1e-4 + max(base_atol, efac x the fixture's f64 envelope) — update 0 (identical starting weights)
+    at the base tolerance; GAE at 1e-5 (_gae_close)."""
     from oracle.synth_env import SynthAtariEnv
     from xuanpolicy_amd.buffer import DummyOnPolicyBuffer_Atari
-    from xuanpolicy_amd.learners import A2C_Learner
+    from xuanpolicy_amd.learners import A2C_Learner, PPOCLIP_Learner
     from xuanpolicy_amd.policies import AC_CNN_Atari, Categorical_AC_Policy
-    g = golden(fixture)
-    env = golden(fixture.replace(".npz", "_env.npz")) if "init_seed" in g else None
-    # r05: with the first fc layer on the split GEMMs (K40G, forced at every batch by conv_path "k28") the update
-    # chain takes another f32 rounding path through Adam: measured up to 3.4x the envelope on one info entry
-    # (predict_value, update 6 of 8; single-step gradients stay at 2e-5 of scale: test_fused_cnn_matches_autograd),
-    # so that path is held to 4x the envelope instead of 3x
-    from xuanpolicy_amd import fused_cnn
-    efac = 4 if (conv_path == "k28" and fused_cnn._Trunk.fc_split) else 3
+    ppo = int(g["algo"]) == 1 if "algo" in g else False
     N, T, K, n_epoch, n_mb, max_ep, seed = (int(x) for x in g["config"])
     net = [int(x) for x in g["net"]]
     nl = (len(net) - 1) // 3
@@ -153,19 +145,26 @@ def test_a2c_atari_replays_reference_agent(golden, fixture, conv_path):
                        fc)
     pol = Categorical_AC_Policy(_Disc(), rep, [], [], None, torch.nn.init.orthogonal_, torch.nn.ReLU, DEV)
     _load_sd0(pol, g)
-    opt = torch.optim.Adam(pol.parameters(), 7e-4, eps=1e-5)
+    if ppo:
+        lr, vf, ent, clip, gn = (float(x) for x in g["hyper"])
+    else:
+        lr, vf, ent, clip, gn = 7e-4, 0.25, 0.01, 0.0, 0.2
+    opt = torch.optim.Adam(pol.parameters(), lr, eps=1e-5)
     sch = torch.optim.lr_scheduler.LinearLR(opt, start_factor=1.0, end_factor=0.0, total_iters=10000)
-    lrn = A2C_Learner(pol, opt, sch, DEV, "./", 0.25, 0.01, 0.2)
-    fc = lrn._fused_cnn()
-    assert fc is not None, "the explicit CNN path (fused_cnn) must run"
+    lrn = (PPOCLIP_Learner(pol, opt, sch, DEV, "./", vf, ent, clip, gn, True) if ppo else
+           A2C_Learner(pol, opt, sch, DEV, "./", vf, ent, gn))
+    fcn = lrn._fused_cnn()
+    assert fcn is not None, "the explicit CNN path (fused_cnn) must run"
     if filters[:2] == [32, 64]:   # the production first convs: K25 / K26 / K27
-        assert fc.trunk_.u8_conv1 and fc.trunk_._dgrad_ok(fc.trunk_.convs[1][0])
-    buf = DummyOnPolicyBuffer_Atari(_Box(), _Disc(), {}, N, T, True, True, 0.99, 0.95, device=DEV)
+        assert fcn.trunk_.u8_conv1 and fcn.trunk_._dgrad_ok(fcn.trunk_.convs[1][0])
+    buf = DummyOnPolicyBuffer_Atari(_Box(), _Disc(), {"old_logp": ()} if ppo else {}, N, T, True, True, 0.99, 0.95,
+                                    device=DEV)
     assert buf.observations.dtype == torch.uint8
     envs = [SynthAtariEnv(i, seed=seed, n_actions=K, max_episode_steps=max_ep) for i in range(N)]
     obs = np.stack([e.reset()[0] for e in envs])
     B = N * T // n_mb
     u = k = 0
+    keys = ["actor-loss", "critic-loss", "entropy", "learning_rate", "predict_value"] + (["clip_ratio"] if ppo else [])
     for it in range(g["act"].shape[0]):
         for t in range(T):
             acts = g["env_actions"][k]
@@ -177,37 +176,75 @@ def test_a2c_atari_replays_reference_agent(golden, fixture, conv_path):
                 if te or tr:
                     info["reset_obs"] = e.reset()[0]
                 raw[i] = o
-                # a2c_agent.py:88-92: a game over (truncation) continues from reset_obs, a life loss keeps the stack
+                # a2c_agent.py:88-92 / ppoclip_agent.py:89-101: a game over (truncation) continues from reset_obs, a
+                # life loss keeps the stack and the path
                 nxt[i] = info["reset_obs"] if tr else o
             # the reference stores after envs.step, and on train()'s first step `obs` still aliases the vec env's
-            # buf_obs, which the step overwrote (a2c_agent.py:59-66): that column holds the post-step frames
+            # buf_obs, which the step overwrote (a2c_agent.py:59-66, ppoclip_agent.py:60-68): that column holds the
+            # post-step frames
             stored = raw if (it, t) == (0, 0) else obs
             assert np.array_equal(stored.reshape(N, -1).astype(np.int64).sum(-1), g["frame_sum"][it][:, t])
-            buf.store(stored, g["act"][it][:, t], g["rew"][it][:, t], g["val"][it][:, t], g["term"][it][:, t])
+            aux = {"old_logp": g["old_logp"][it][:, t]} if ppo else None
+            buf.store(stored, g["act"][it][:, t], g["rew"][it][:, t], g["val"][it][:, t], g["term"][it][:, t], aux)
             for i in np.nonzero(g["closed"][it][:, t])[0]:
                 buf.finish_path(float(g["boot"][it][i, t]), i)
             obs = nxt
-        np.testing.assert_allclose(buf.advantages.cpu().numpy(), g["adv"][it], rtol=1e-5, atol=2e-5)
-        np.testing.assert_allclose(buf.returns.cpu().numpy(), g["ret"][it], rtol=1e-5, atol=2e-5)
+        _gae_close(buf.advantages.cpu().numpy(), g["adv"][it])
+        _gae_close(buf.returns.cpu().numpy(), g["ret"][it])
         for e in range(n_epoch):
             perm = g["perms"][it * n_epoch + e]
             for s in range(0, N * T, B):
-                o, a, r, _, ad, _ = buf.sample(perm[s:s + B])
+                o, a, r, v, ad, ax = buf.sample(perm[s:s + B])
                 assert o.dtype == torch.uint8
-                info = lrn.update(o, a, r, ad)
-                got = [info["actor-loss"], info["critic-loss"], info["entropy"], info["learning_rate"],
-                       info["predict_value"]]
-                atol = np.maximum(2e-5, efac * env["info"][u]) if env is not None else 2e-5
-                if env is not None and u == 0:
-                    assert (atol == 2e-5).all()   # the first update starts from identical weights: base tolerance
+                info = lrn.update(o, a, r, v, ad, ax["old_logp"]) if ppo else lrn.update(o, a, r, ad)
+                got = [float(info[kk]) for kk in keys]
+                ev = env["info"][u] if env is not None else np.zeros(len(keys))
+                atol = np.maximum(base_atol, efac * ev)
+                if u == 0:
+                    atol = np.full(len(keys), base_atol)   # identical starting weights: north_star's tolerance
+                if ppo:   # clip fraction: a count / B, exact at update 0 (ratios 1 within f32), then the envelope
+                    atol[-1] = 0.0 if u == 0 else max(efac * ev[-1], 2.0 / B)
                 if env is not None and os.environ.get("XPA_REPORT_ENVELOPE"):
                     dev = np.abs(np.asarray(got, np.float64) - g["infos"][u])
-                    print("ENVELOPE u=%d dev/env=%s" % (u, np.round(dev / np.maximum(env["info"][u], 1e-12), 2)))
-                _close(got, g["infos"][u], 2e-4, atol, "update %d" % u)
+                    print("ENVELOPE u=%d dev/env=%s" % (u, np.round(dev / np.maximum(ev, 1e-12), 2)))
+                _close(got, g["infos"][u], rtol, atol, "update %d" % u)
                 u += 1
         buf.clear()
     assert u == len(g["infos"])
     _check_sd1(pol, g, rtol=1e-3, atol=5e-5, env=env, efac=efac)
+
+
+@pytest.mark.parametrize("fixture", ["atari_a2c.npz", "atari_a2c_prod.npz"])
+def test_a2c_atari_replays_reference_agent(golden, fixture, conv_path):
+    """G8: the reference's two recorded A2C_Agent iterations on Atari-shaped frames (a2c_agent.py:57-107,
+    env_name "Atari": DummyOnPolicyBuffer_Atari memory_tools.py:526-560, AC_CNN_Atari cnn.py:45-93 +
+    Categorical_AC_Policy, life losses keep the path open) replayed through the device buffer (uint8 frames,
+    K1 GAE with the Atari closures, K4 sample + adv-norm) and A2C_Learner (CNN on K25-K29 or MIOpen per conv_path,
+    K2 categorical loss, K9 clip + Adam): GAE, every update's info dict, the final parameters.  The frames are
+    regenerated by stepping the oracle SynthAtari env with the recorded actions through the reference's
+    DummyVecEnv / agent observation flow and checked against the recorded per-step frame sums.
+    atari_a2c_prod.npz (G8P) is the production net (filters [32, 64, 64], kernels [8, 4, 3], strides [4, 2, 1], fc
+    512; 8 envs x 64 steps, minibatches of 256) replayed update by update.  A few Adam steps of an f32 net are
+    chaotic in the last bits (tests/golden/make_envelopes.py): the prod fixture carries, per update and per tensor, how
+    far the exact f64 replay lands from the reference, and the tolerances are max(base, 3 x that envelope) — update 0
+    (identical starting weights) is held to the base tolerances (1e-4 relative + 1e-5)."""
+    g = golden(fixture)
+    env = golden(fixture.replace(".npz", "_env.npz")) if "init_seed" in g else None
+    _replay_atari(g, env, conv_path)
+
+
+@pytest.mark.parametrize("fixture", ["atari_ppo.npz", "atari_ppo_prod.npz"])
+def test_ppo_atari_replays_reference_agent(golden, fixture, conv_path):
+    """G12 / G12P: examples/ppo/ppo_atari.py's agent — the reference's PPOCLIP_Agent with env_name
+    "Atari" (ppoclip_agent.py:24-25: DummyOnPolicyBuffer_Atari; :93-94: a life loss keeps the path open) over
+    DummyVecEnv_Atari of SynthAtari, ppo/atari.yaml's coefficients (lr 2.5e-4, clip 0.2, grad norm 0.5, vf 0.25,
+    ent 0.01; 4 epochs x 4 minibatches), two recorded iterations, small and production AC_CNN_Atari — replayed
+    through the device buffer (old_logp column), FusedCNNActorCritic and K2 in PPO mode (ratio / clip / old_logp,
+    clip fraction): GAE at 1e-5, update 0's loss scalars at 1e-4 relative + 1e-5, later updates within 3x the
+    fixture's measured f64 envelope (make_envelopes.py), the final weights likewise."""
+    g = golden(fixture)
+    env = golden(fixture.replace(".npz", "_env.npz"))
+    _replay_atari(g, env, conv_path)
 
 
 def test_atari_deferred_last_bootstrap_matches_per_step():

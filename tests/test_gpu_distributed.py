@@ -182,3 +182,31 @@ def test_bench_two_rank_rehearsal_one_gpu():
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["steps"] == 2 and r["value"] > 0
     assert r["config"]["global_envs"] == 512 and "dp2" in r["config"]["parallelism"]
+
+
+@pytest.mark.timeout(900)
+def test_bench_self_launch_two_ranks_one_gpu():
+    """`python bench.py --gpus 2` with no launcher (the driver's plain form): bench.py starts the 2 ranks itself, both
+    on the box's one GPU over gloo, and the line reports n_gpus 2 on the C2 and C4 legs with ONE all-reduce per
+    minibatch and the collective's measured time share."""
+    import json
+    import subprocess
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["XPA_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--n-envs", "512", "--horizon", "32", "--n-epoch", "2", "--n-minibatch", "2", "--no-sweep", "--no-per",
+           "--no-c1", "--no-c3", "--no-cpu-baseline", "--no-kernel-timing", "--no-pmc", "--no-rocprof"]
+    out = subprocess.run(cmd, cwd=repo, env=env, capture_output=True, text=True, timeout=860)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["config"]["global_envs"] == 1024 and "dp2" in r["config"]["parallelism"]
+    assert r["data_parallel"]["collectives_per_minibatch"] == 1.0
+    assert r["data_parallel"]["allreduce"]["bytes"] > 0 and r["data_parallel"]["allreduce_time_share"] > 0
+    c4 = r["c4_box376"]
+    assert c4["n_gpus"] == 2 and c4["collectives_per_minibatch"] == 1.0 and c4["value"] > 0

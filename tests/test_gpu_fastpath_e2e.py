@@ -144,14 +144,12 @@ def test_c4_shape_iteration_matches_oracle(mode, monkeypatch):
     assert agent.defer_boot and agent.n_slots == 1 and not agent._env_fused(fm)
     agent.train(T, log=False)
     agent.train(T - 1, log=False)
-    # tolerances (r05): over the iteration's 8 updates the f32 device path and the f64 oracle drift apart through Adam
-    # (near-zero gradients of the 376-wide layer normalised to +-lr steps), and the PPO actor loss is a cancellation
-    # (|mean| ~0.02 of O(1) terms): profiles/r05/c4_drift.jsonl shows the r04 library-GEMM path at 2.1e-4 on the actor
-    # loss and 2.4e-4 on weights for seed 18, the split path at 0 there and the reverse for seed 17 — 5e-4 / 5e-4 is
-    # ~2x the largest drift of the six runs (every trunk / rollout GEMM form); the drifted ratios move rows across the
-    # clip bounds (19 of 8192 at update 5 of one run), so the clip fraction is held to 5e-3 (41 rows)
+    # tolerances (r06): over the iteration's 8 updates the f32 device path and the oracle drift apart through Adam
+    # (near-zero gradients of the 376-wide layer normalised to +-lr steps; profiles/r05/c4_drift.jsonl).  Update 0
+    # starts from identical weights: every loss scalar at north_star's 1e-4.  Later updates: 3x the f32-vs-f64 distance
+    # of the oracle's own replay of the same inputs, measured in this test (the G8P envelope method), never below 1e-4
     replay_last_step_iteration(agent, D, A, [H], False, "ppo", 0.0, n_epoch, n_mb, expect_mid_truncations=True,
-                               loss_tol=5e-4, w_atol=5e-4, clip_tol=5e-3)
+                               loss_tol=1e-4, w_atol=1e-4, envelope=3.0)
     assert fm._wide_on() == wide
     keys = {k[0] for k in fm._partials if isinstance(k, tuple)}
     assert ("wide_bwd" in keys) == wide and ("wide_x" in keys) == (mode == "gather"), keys

@@ -64,3 +64,33 @@ def test_relu_critic_keeps_thin_plan():
     fm = FusedActorCritic(pol)
     assert fm.wide0 and fm.rep[0][1] == 1 and fm.rep[0][2] == 0.0
     assert isinstance(pol.representation.model[1], nn.ReLU)
+
+
+@pytest.mark.parametrize("d,B,direct", [(376, 65536, True), (1024, 65536, False), (1024, 49152, True),
+                                        (2048, 24576, True), (2048, 24577, False), (4096, 12289, False)])
+def test_wide_direct_respects_k41v_index_stage(d, B, direct):
+    """the row-index forms only where K41V-IDX's per-slice rows (ceil(B / S) to 32) fit its 1536-row LDS
+    index stage (csrc/sgemm3.hip kVIdxMax); beyond it the pitched gather (no limit) runs instead of a mid-update
+    hipErrorInvalidValue."""
+    from xuanpolicy_amd import buffer as bf
+    from xuanpolicy_amd.fused_mlp import FusedActorCritic, Rows
+    fm = FusedActorCritic(cpu_ref.build_actor_critic_ref(d, 6, [256], [256], [256]))
+    flat = torch.zeros(B + bf.OBS_SLACK // d + 2, d)[:B]   # slack after the last row, as the rollout buffer has
+    x = Rows(flat, torch.zeros(B, dtype=torch.int64))
+    assert fm._wide_direct_ok(x, d) == direct
+    S = fm._wide_slices(fm._wide_mpad(d))
+    per = -(-B // S)
+    assert (-(-per // 32) * 32 <= fm.WIDE_VIDX_MAX) == direct
+
+
+def test_trunk_backward_form_and_crit_plan_share_one_predicate():
+    """the factored critic is planned only where the fused trunk backward form applies (one predicate,
+    _trunk_bwd_form), and the planned backward raises instead of being stripped under python -O."""
+    import inspect
+    from xuanpolicy_amd.fused_mlp import FusedActorCritic
+    src = inspect.getsource(FusedActorCritic.loss_backward)
+    assert "assert self._trunk_bwd_fused" not in src and "RuntimeError" in src
+    assert "_trunk_bwd_form" in inspect.getsource(FusedActorCritic._crit_plan)
+    fm = FusedActorCritic(cpu_ref.build_actor_critic_ref(17, 6, [256], [256], [256]))
+    x = torch.zeros(8, 17)
+    assert fm._trunk_bwd_form(torch.zeros(8, 256), x, [torch.zeros(8, 256)]) is None   # no paired layer: no fused form

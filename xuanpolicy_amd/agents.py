@@ -125,9 +125,12 @@ class _OnPolicyAgent:
         self.fuse_gather = True     # minibatch gather + adv moments inside the update's K13 (fused_mlp.Rows)
         # r05: the next step's obs_rms.update folded into K8 (xpa_rollout_post_deferred_norm_rms) on the device-env
         # path; _rms_pending: the current observation's statistics are not merged yet (the first step, or after
-        # anything but a folded step produced env.obs), so that step runs the standalone update first
+        # anything but a folded step produced env.obs), so that step runs the standalone update first.  An env reset
+        # (envs.reset bumps envs.resets) re-arms it.  test() does not: its obs_rms.update merges other rows, and the
+        # folded merge of env.obs already happened (the Chan merge is order-independent up to rounding)
         self.fold_rms = FOLD_RMS
         self._rms_pending = True
+        self._rms_resets = getattr(envs, "resets", 0)
         self._rms_fold_part = None
         # K32: whole device env steps (RMS, normalise, forward, sample, env, post) in one launch (_small_rollout)
         self.fused_rollout = bool(_cfg(config, "fused_rollout", True))
@@ -433,6 +436,8 @@ class _OnPolicyAgent:
             ops.store_column(x, self.memory.observations, self.cursor)
             self._policy_in = x
         else:
+            if getattr(env, "resets", 0) != self._rms_resets:
+                self._rms_resets, self._rms_pending = getattr(env, "resets", 0), True
             if self.use_obsnorm and (self._rms_pending or not self._rms_fold_ok()):
                 self._rms_update(x)
                 self._rms_pending = False

@@ -82,6 +82,28 @@ class GradAllReduce:
         self.calls += 1
 
 
+class LocalGradSync:
+    """A world-size-1 stand-in for GradAllReduce (no collective): attached to a learner on one GPU it makes the update
+    take exactly the data-parallel code path — the clip norm from its own pass over the (synchronised) flat gradient
+    instead of the producers' partials, eager K9 instead of the device-scheduled / graphed step — so that path's
+    per-rank cost is measurable before a multi-GPU node exists (bench.py --dp-path)."""
+
+    early_slice = False
+
+    def __init__(self, flat_grads):
+        self.fg = flat_grads
+        self.avg = True
+        self.calls = 0
+        self.collectives = 0
+
+    def begin(self, region):
+        return False
+
+    def __call__(self, params):
+        self.fg.ensure_views()
+        self.calls += 1
+
+
 def attach_flat_grads(learner, allreduce=True, group=None, fused_optimizer=True, early_slice=False):
     """Give a learner flat parameters/gradients, the fused clip+Adam step when its optimizer allows,
     and the all-reduce hook when a process group of more than one rank is initialised (one collective per

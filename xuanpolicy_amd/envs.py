@@ -116,6 +116,7 @@ class SynthBoxVecEnv:
         return self.obs
 
     def reset(self):
+        self.resets = getattr(self, "resets", 0) + 1   # agents re-arm a folded obs-RMS merge (K8R)
         ids = np.arange(self.num_envs)
         s0 = synthbox_reset_states(self.noise_seed, ids, np.zeros(self.num_envs), self.D)
         self.X.zero_()
@@ -232,6 +233,7 @@ class SynthAtariVecEnv:
         return self.stack
 
     def reset(self):
+        self.resets = getattr(self, "resets", 0) + 1   # agents re-arm a folded obs-RMS merge (K8R)
         for t in (self.ep_step, self.ep_index, self.ep_score, self.ep_last_score, self.ep_last_len, self.rew,
                   self.term, self.trunc, self._act):
             t.zero_()
@@ -338,6 +340,7 @@ class CartPoleVecEnv:
         return self._obs
 
     def reset(self):
+        self.resets = getattr(self, "resets", 0) + 1   # agents re-arm a folded obs-RMS merge (K8R)
         s0 = cartpole_reset_states(self.noise_seed, np.arange(self.num_envs), np.zeros(self.num_envs))
         self.state.copy_(torch.as_tensor(s0, device=self.device))
         self._obs.copy_(self.state.float())

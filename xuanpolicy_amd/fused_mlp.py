@@ -205,13 +205,25 @@ class FusedActorCritic:
     def _wide_mpad(d):
         return (d + 127) // 128 * 128   # K41V's row tiles over the layer's inputs
 
+    WIDE_VIDX_MAX = 1536   # K41V-IDX's LDS index stage (csrc/sgemm3.hip kVIdxMax): rows per slice, rounded to 32
+
+    @classmethod
+    def _wide_slices(cls, kp):
+        return max(1, 256 // (kp // 128))
+
     def _wide_direct_ok(self, x, d):
         """The row-index forms apply: the flat buffer's rows are the layer width and readable, finite (zeroed) slack
-        follows its last row for the padded columns (buffer.OBS_SLACK)."""
+        follows its last row for the padded columns (buffer.OBS_SLACK), and K41V-IDX's per-slice row count fits its LDS
+        index stage (else the pitched gather, which has no such limit).  Input contract: the rows are finite — K40F
+        reads columns d .. kp - 1 of a row from the next row, multiplied by zero weight rows."""
         f = x.flat
-        need = max((d + 15) // 16 * 16, self._wide_mpad(d)) - d
+        mp = self._wide_mpad(d)
+        need = max((d + 15) // 16 * 16, mp) - d
+        S = self._wide_slices(mp)
+        per = (x.idx.shape[0] + S - 1) // S
+        per = (per + 31) // 32 * 32
         return (self.WIDE_DIRECT and f.dim() == 2 and f.is_contiguous() and f.shape[1] == d and d % 4 == 0
-                and f.data_ptr() % 16 == 0
+                and f.data_ptr() % 16 == 0 and per <= self.WIDE_VIDX_MAX
                 and f.untyped_storage().nbytes() // 4 >= f.storage_offset() + f.numel() + need)
 
     def _wide_forward(self, x, adv, adv_partials):
@@ -257,7 +269,7 @@ class FusedActorCritic:
         direct = getattr(x, "wide_direct", False)
         xp = x.gathered
         kp = self._wide_mpad(d) if direct else xp.shape[1]
-        S = max(1, 256 // (kp // 128))
+        S = self._wide_slices(kp)
         key = ("wide_bwd", B, kp, S)
         ws = self._partials.get(key)
         if ws is None:
@@ -533,7 +545,8 @@ class FusedActorCritic:
             if self.early_grad_sync is not None:
                 self._cq_early.flush(s.device)
                 self.early_grad_sync(self.pair[2])
-            assert self._trunk_bwd_fused(self._hws.dz_actor, x, rep_outs, crit=crit)
+            if not self._trunk_bwd_fused(self._hws.dz_actor, x, rep_outs, crit=crit):
+                raise RuntimeError("factored critic planned but the fused trunk backward did not apply")
             self._flush_with_norm(s.device)
             return scalars
         if paired:   # dW of both hidden layers and dX (K = 512, no accumulate pass) as single GEMMs
@@ -636,7 +649,7 @@ class FusedActorCritic:
         x_ok = self._wide_on() or (isinstance(xr, torch.Tensor) and xr.dim() == 2 and xr.stride(1) == 1)
         if not (x_ok and isinstance(h, torch.Tensor) and h.shape[1] == 256 and _vec4_rows(h)):
             return None
-        if self._hws is None or not _vec4_rows(self._hws.dz_actor):
+        if self._hws is None or self._trunk_bwd_form(self._hws.dz_actor, x, rep_outs) is None:
             return None
         key = ("crit", B)
         bufs = self._partials.get(key)
@@ -687,23 +700,37 @@ class FusedActorCritic:
             self._partials[key] = sign
         return sign
 
-    def _trunk_bwd_fused(self, dz, x, rep_outs, crit=None):
-        """K42: the dX GEMM and the one representation layer's backward (K13's) in one launch, g never stored.  Returns
-        False (nothing done) when it does not apply: not the split GEMMs, more than one representation layer, no K13
-        first layer, d_in > 32, or rows not given as the gathered minibatch.  The wide trunk layer: _wide_bwd."""
+    def _trunk_bwd_form(self, dz, x, rep_outs):
+        """Which fused trunk backward applies (no side effects): "wide" (_wide_bwd), "thin" (K42 over K13's layer) or
+        None.  _crit_plan plans the factored critic only where this is not None, and _trunk_bwd_fused runs exactly this
+        form, so the two cannot disagree."""
         if (self._wide_on() and isinstance(x, Rows) and getattr(x, "hsign", None) is not None
                 and (isinstance(x.gathered, torch.Tensor) or getattr(x, "wide_direct", False)) and _vec4_rows(dz)):
+            return "wide"
+        if not (self.FUSE_TRUNK_BWD and self.pair is not None and self._dx_split_ok(self.pair[0]) and len(self.rep) == 1
+                and self.thin0 and _vec4_rows(dz)):
+            return None
+        xr = x.gathered if isinstance(x, Rows) else x
+        if not isinstance(xr, torch.Tensor) or xr.dim() != 2 or xr.stride(1) != 1 or self.rep[0][0].in_features > 32:
+            return None
+        h = rep_outs[0] if rep_outs else None
+        if not isinstance(h, torch.Tensor) or h.stride(1) != 1 or h.shape[1] != 256:
+            return None
+        return "thin"
+
+    def _trunk_bwd_fused(self, dz, x, rep_outs, crit=None):
+        """K42: the dX GEMM and the one representation layer's backward (K13's) in one launch, g never stored.  Returns
+        False (nothing done) when it does not apply (_trunk_bwd_form): not the split GEMMs, more than one representation
+        layer, no K13 first layer, d_in > 32, or rows not given as the gathered minibatch.  The wide trunk layer:
+        _wide_bwd."""
+        form = self._trunk_bwd_form(dz, x, rep_outs)
+        if form == "wide":
             return self._wide_bwd(dz, x, crit)
-        if not (self.FUSE_TRUNK_BWD and self._dx_split_ok(self.pair[0]) and len(self.rep) == 1 and self.thin0
-                and _vec4_rows(dz)):
+        if form is None:
             return False
         lin, code, slope = self.rep[0]
         xr = x.gathered if isinstance(x, Rows) else x
-        if not isinstance(xr, torch.Tensor) or xr.dim() != 2 or xr.stride(1) != 1 or lin.in_features > 32:
-            return False
         h = rep_outs[0]
-        if not isinstance(h, torch.Tensor) or h.stride(1) != 1 or h.shape[1] != 256:
-            return False
         rows = dz.shape[0]
         key = ("k42", rows, lin.in_features)
         ws = self._partials.get(key)
