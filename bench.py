@@ -765,35 +765,53 @@ def c4_bench(device, rank, world, n_envs=4096, n_steps=128, steps=2, warmup=1):
     return res
 
 
-def dp_path_bench(device, args, steps=3, warmup=1):
+def dp_path_bench(device, args, steps=3, warmup=2):
     """C2 on one GPU with the data-parallel update path attached (distributed.LocalGradSync in place of the
-    all-reduce): the per-rank cost of world > 1 apart from the collective itself — the clip norm from its own pass
-    (the producers' partials are not the averaged gradient's), K9 launched eagerly per minibatch."""
+    all-reduce) and, in the same call, without it: the per-rank cost of world > 1 apart from the collective itself —
+    the clip norm from its own pass (the producers' partials are not the averaged gradient's), K9 launched from the
+    host per minibatch.  The two arms alternate (A B A B) so box drift hits both alike."""
     import torch
     from xuanpolicy_amd.distributed import LocalGradSync
     from xuanpolicy_amd.runner import build_synthbox_ppo
     N, T = args.n_envs, args.horizon
-    agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=args.obs_dim, act_dim=args.act_dim, hidden=args.hidden,
-                               n_epoch=args.n_epoch, n_minibatch=args.n_minibatch, seed=1, device=device)
-    agent.learner.enable_fast_path()
-    agent.fuse_value_gae = args.gae_form == "value"
-    hook = agent.learner.grad_sync = LocalGradSync(agent.learner.flat_grads)
-    for _ in range(warmup):
-        agent.train(T)
-    torch.cuda.synchronize()
-    c0 = hook.calls
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        agent.train(T)
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    res = {"what": "C2 with the world > 1 update path on one GPU (grad_sync hook without a collective: own clip-norm "
-                   "pass, eager K9 per minibatch)", "value": round(N * T * steps / el, 1), "unit": "env-steps/s",
-           "ms_per_iteration": round(el / steps * 1e3, 3), "iterations": steps,
-           "hook_calls_per_minibatch": (hook.calls - c0) / (steps * args.n_epoch * args.n_minibatch)}
-    del agent
-    torch.cuda.empty_cache()
-    return res
+
+    def arm(hooked):
+        agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=args.obs_dim, act_dim=args.act_dim,
+                                   hidden=args.hidden, n_epoch=args.n_epoch, n_minibatch=args.n_minibatch, seed=1,
+                                   device=device)
+        agent.learner.enable_fast_path()
+        agent.fuse_value_gae = args.gae_form == "value"
+        hook = None
+        if hooked:
+            hook = agent.learner.grad_sync = LocalGradSync(agent.learner.flat_grads)
+        for _ in range(warmup):
+            agent.train(T)
+        torch.cuda.synchronize()
+        c0 = hook.calls if hook else 0
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            agent.train(T)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        calls = (hook.calls - c0) if hook else 0
+        del agent
+        torch.cuda.empty_cache()
+        return el / steps * 1e3, calls
+    ms = {True: [], False: []}
+    calls = 0
+    for hooked in (False, True, False, True):
+        m, c = arm(hooked)
+        ms[hooked].append(m)
+        calls = max(calls, c)
+    on, off = min(ms[True]), min(ms[False])
+    return {"what": "C2 with the world > 1 update path on one GPU (grad_sync hook without a collective: own clip-norm "
+                    "pass, host-launched K9 per minibatch) against the world-1 path, arms alternated, best of 2 x %d "
+                    "iterations each" % steps,
+            "value": round(N * T / (on * 1e-3), 1), "unit": "env-steps/s", "ms_per_iteration": round(on, 3),
+            "world1_ms_per_iteration": round(off, 3), "delta_ms_per_iteration": round(on - off, 3),
+            "delta_us_per_minibatch": round((on - off) * 1e3 / (args.n_epoch * args.n_minibatch), 2),
+            "arms_ms": {"dp_path": [round(x, 3) for x in ms[True]], "world1": [round(x, 3) for x in ms[False]]},
+            "hook_calls_per_minibatch": calls / (steps * args.n_epoch * args.n_minibatch)}
 
 
 def _cpu_model():

@@ -162,6 +162,7 @@ def replay_updates(agent, pol, opt_state, lr0, sched_epoch, perm_counter, adv, r
     B = N * T // n_mb
     assert len(agent.update_log) == n_epoch * n_mb
     u = 0
+    run_max = {}
     for e in range(n_epoch):
         perm = agent.epoch_permutation(N * T, counter=perm_counter + e).cpu().numpy()
         for s in range(0, N * T, B):
@@ -173,8 +174,11 @@ def replay_updates(agent, pol, opt_state, lr0, sched_epoch, perm_counter, adv, r
             if lrn64 is not None:
                 i64 = lrn64.update(o, a, r, ad, ax.get("old_logp"))
                 l64 = i64["actor-loss"] - ent * i64["entropy"] + cfg.vf_coef * i64["critic-loss"]
-                env = {k: envelope * abs(info[k] - i64[k]) if u > 0 else 0.0 for k in i64 if k in info}
-                env["loss"] = envelope * abs(ref_loss - l64) if u > 0 else 0.0
+                d = {k: abs(float(info[k]) - float(i64[k])) for k in i64 if k in info}
+                d["loss"] = abs(ref_loss - l64)
+                for k, v in d.items():   # running maximum over the updates (make_envelopes.envelope_atari)
+                    run_max[k] = max(run_max.get(k, 0.0), v)
+                env = {k: envelope * v if u > 0 else 0.0 for k, v in run_max.items()}
             if report is not None:   # diagnostics (tools/c4_drift.py): record instead of asserting
                 report.append(("update", u, [float(got[j]) for j in range(6)],
                                [float(info[k]) for k in ("actor-loss", "critic-loss", "entropy")] + [float(ref_loss)]))
