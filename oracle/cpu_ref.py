@@ -492,7 +492,8 @@ class LearnerRef:
         self.clip_range, self.clip_grad_norm, self.use_grad_clip = clip_range, clip_grad_norm, use_grad_clip
         self.iterations = 0
 
-    def update(self, obs, act, ret, adv, old_logp=None):
+    def update(self, obs, act, ret, adv, old_logp=None, capture_grads=False):
+        """capture_grads: keep every parameter's gradient before clipping in self.last_grads (lock-step replays)."""
         torch = _torch()
         self.iterations += 1
         if not (isinstance(obs, np.ndarray) and obs.dtype == np.uint8):   # raw frames: the policy scales them
@@ -519,6 +520,8 @@ class LearnerRef:
         loss = a_loss - self.ent_coef * e_loss + self.vf_coef * c_loss
         self.optimizer.zero_grad()
         loss.backward()
+        if capture_grads:
+            self.last_grads = [p.grad.detach().clone() for p in self.policy.parameters()]
         if self.algo == "a2c" or self.use_grad_clip:
             torch.nn.utils.clip_grad_norm_(self.policy.parameters(), self.clip_grad_norm)
         self.optimizer.step()

@@ -10,8 +10,8 @@ import json
 import sys
 from collections import defaultdict
 
-KEYS = ("s3_wgrad", "s3_gemm_trunk_bwd", "head_gemm_kernel", "thin_fwd_kernel", "colsum_finalize", "clip_adam",
-        "split_batch", "gae_dpp", "rollout_policy_head", "Cijk")
+KEYS = ("s3_wgrad", "s3_gemm_trunk_bwd", "s3_trunk_bwd", "head_gemm_kernel", "thin_fwd", "colsum_finalize", "clip_adam",
+        "split_batch", "gae_dpp", "rollout_policy_head", "Cijk", "s3_gemm_r64", "rms_partials", "rollout_post")
 
 
 def main(pmc_dir, out):
@@ -37,6 +37,9 @@ def main(pmc_dir, out):
         if wave:
             d["wait_inst_lds_per_wave_cycle"] = round(d.get("SQ_WAIT_INST_LDS", 0.0) / wave, 4)
             d["wait_any_per_wave_cycle"] = round(d.get("SQ_WAIT_ANY", 0.0) / wave, 4)
+            for c in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_MISC"):
+                if c in d:   # issue quad-cycles of that instruction class per wave quad-cycle
+                    d[c.replace("SQ_ACTIVE_INST_", "").lower() + "_issue_per_wave_cycle"] = round(d[c] / wave, 4)
         res["kernels"][k] = d
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: {x: v.get(x) for x in ("mfma_busy_frac", "dispatches", "wait_inst_lds_per_wave_cycle")}

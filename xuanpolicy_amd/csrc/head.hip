@@ -167,7 +167,7 @@ struct RowIn {  // epilogue wave 0, lane = row of the tile
     float x, old, act[KMAX];
 };
 
-template <int MODE, int ALGO, int ACT, int KMAX, int NW = 4>
+template <int MODE, int ALGO, int ACT, int KMAX, int NW = 4, bool QOK = true>
 struct HeadEpi {
     static constexpr int KP = (KMAX + 3) & ~3;  // 16-B aligned d-head rows
     // phase-1 partials per pass: heads wider than 8 (C4's 17 / 18) go through s_part in two halves, so the K16 block
@@ -181,14 +181,28 @@ struct HeadEpi {
     // half the VALU issues)
     static constexpr bool kPk = KMAX <= 8;  // the wide heads (C4) keep scalar accumulators (packed pairs spill there)
     static constexpr int KH2 = (KMAX + 1) / 2;
-    float wc[CPT][KMAX], acc_dw[CPT][kPk ? 1 : KMAX], acc_dbh[CPT];
+    // r06, phase 2 of the actor heads (KMAX <= 6, the whole block): thread e owns the 4 consecutive columns 4 (e & 63) ..
+    // + 3 of rows r = e >> 6 (mod 4), so a wave reads a row of h with ONE ds_read_b128 per lane and writes its dz row as
+    // ONE 1-KiB store (16 B per lane) instead of 64 B-strided 4-B ones; each dz value is the same arithmetic as before
+    // (bit for bit), dW_out / db_hidden accumulate per wave and are summed over the 4 waves in a fixed order at finish
+    // Register budget (2 blocks per CU: 256 VGPRs): the quad layout's 4-column accumulators live only through a tile's
+    // epilogue (q_dw2 / q_dbh, zeroed in p2_quad, summed over the 4 waves into the one-column acc_dw2 / acc_dbh by
+    // quad_flush), and its output weights are loaded per tile (16-B loads from L2): kept across the k loop they took the
+    // K = 6 actor from 204 to 253 VGPRs and the K = 8 one into scratch
+    // (QOK: the kernel allows it — K12 keeps its next tile's z prefetched in 64 VGPRs through the epilogue; KMAX <= 6:
+    // the K = 8 bucket's packed accumulators and weights did not fit 256 VGPRs beside the rest)
+    static constexpr bool kQuad = QOK && MODE != 2 && NW == 4 && KMAX <= 6;
+    float wc[kQuad ? 1 : CPT][KMAX], acc_dw[CPT][kPk ? 1 : KMAX], acc_dbh[CPT];
     f2v acc_dw2[CPT][kPk ? KH2 : 1];
+    f2v q_dw2[kQuad ? 4 : 1][KH2];
+    float q_dbh[kQuad ? 4 : 1];
+    __device__ __forceinline__ int col_of(int j) const { return e + NT * j; }
     // the wide heads (C4) keep the Gaussian's per-output variance / log-scale in LDS (s_stats[2 ..], written by
     // init_a): 36 registers fewer where the kernel sits at the 256-register cap of 2 blocks per CU
     static constexpr bool kLdsVar = KMAX > 8;
     static constexpr int kStatN = kLdsVar ? 2 + 2 * KMAX : 2;   // floats of s_stats
     float acc_dbo[KMAX], acc_dls[KMAX], var_[kLdsVar ? 1 : KMAX], logsc[kLdsVar ? 1 : KMAX];
-    const float *s_var = nullptr;   // kLdsVar: var at s_var[o], log-scale at s_var[KMAX + o]
+    const float *s_var = nullptr;   // kLdsVar: 1 / var at s_var[o], log-scale at s_var[KMAX + o]
     float sum0, sum1, sum2, ent_const, inv_b, lo, hi, a_mean, a_inv, slope;
     float hd[KMAX];  // epilogue wave 0: the row's head outputs between the phase-1 passes and the loss
     int K, e;        // e: epilogue thread index
@@ -214,9 +228,9 @@ struct HeadEpi {
             s_stats[1] = 1.f;
         }
 #pragma unroll
-        for (int j = 0; j < CPT; ++j)
+        for (int j = 0; j < (kQuad ? 1 : CPT); ++j)
 #pragma unroll
-            for (int o = 0; o < KMAX; ++o) wc[j][o] = o < K ? W[o * kH + e + NT * j] : 0.f;
+            for (int o = 0; o < KMAX; ++o) wc[j][o] = (o < K && !kQuad) ? W[o * kH + col_of(j)] : 0.f;
 #pragma unroll
         for (int o = 0; o < KMAX; ++o) {
             acc_dbo[o] = acc_dls[o] = 0.f;
@@ -248,13 +262,16 @@ struct HeadEpi {
             for (int o = 0; o < KMAX; ++o) {
                 const float sc = o < K ? expf(logstd[o]) : 1.f;
                 const float ls = logf(sc);
+                // r06: the reciprocal of the variance, so the per-row loss multiplies where it divided (three IEEE
+                // divisions per output and row: ~half the loss's instructions); each product differs from the divide
+                // by at most one rounding
                 if constexpr (kLdsVar) {
                     if (e == o) {
-                        s_stats[2 + o] = sc * sc;
+                        s_stats[2 + o] = 1.0f / (sc * sc);
                         s_stats[2 + KMAX + o] = ls;
                     }
                 } else {
-                    var_[o] = sc * sc;
+                    var_[o] = 1.0f / (sc * sc);
                     logsc[o] = ls;
                 }
                 if (o < K) ent_const += kHalfLog2PiPlusHalf + ls;
@@ -269,7 +286,7 @@ struct HeadEpi {
         a_inv = s_stats[1];
         s_var = s_stats + 2;
     }
-    __device__ __forceinline__ float var_at(int o) const { return kLdsVar ? s_var[o] : var_[o]; }
+    __device__ __forceinline__ float ivar_at(int o) const { return kLdsVar ? s_var[o] : var_[o]; }   // 1 / var
     __device__ __forceinline__ float logsc_at(int o) const { return kLdsVar ? s_var[KMAX + o] : logsc[o]; }
 
     __device__ __forceinline__ RowIn<KMAX> rows(int64_t tile, int64_t batch, const int64_t *__restrict__ idx,
@@ -383,7 +400,7 @@ struct HeadEpi {
                         diff[o] = 0.f;
                         if (o < K) {
                             diff[o] = in.act[o] - hd[o];
-                            logp += -(diff[o] * diff[o]) / (2.0f * var_at(o)) - logsc_at(o) - kLogSqrt2Pi;
+                            logp += -(diff[o] * diff[o]) * (0.5f * ivar_at(o)) - logsc_at(o) - kLogSqrt2Pi;
                         }
                     }
                     ent = ent_const;
@@ -430,8 +447,8 @@ struct HeadEpi {
                 for (int o = 0; o < KMAX; ++o) {
                     if (o < K) {
                         if (MODE == 0) {
-                            dh_[o] = dlogp * diff[o] / var_at(o);
-                            acc_dls[o] += dlogp * (diff[o] * diff[o] / var_at(o) - 1.0f);
+                            dh_[o] = dlogp * diff[o] * ivar_at(o);
+                            acc_dls[o] += dlogp * (diff[o] * diff[o] * ivar_at(o) - 1.0f);
                         } else {
                             const float ln = hd[o] - lse;
                             const float p = expf(ln);
@@ -458,11 +475,15 @@ struct HeadEpi {
     // and db_hidden accumulated in registers; rows in groups of 4 (every LDS read of the group issued before the
     // arithmetic, the row order of the accumulations kept: bitwise the same sums as one row at a time).
     __device__ __forceinline__ void p2(const float *s_h, float (*s_dh)[KP], int64_t tile, int64_t batch, int r0, int r1,
-                                       float *__restrict__ dz, int64_t ld) {
+                                       float *__restrict__ dz, int64_t ld, const float *__restrict__ W = nullptr) {
 #if XPA_HEAD_PROBE == 5  // 5 = epilogue alone without phase 2
         r1 = r0;
 #endif
         const int nr = (int)min((int64_t)r1, batch - tile * kTile);
+        if constexpr (kQuad) {
+            p2_quad(s_h, s_dh, tile, r0, nr, dz, ld, W);
+            return;
+        }
         unsigned mlo = 0u, mhi = 0u;   // mask_out: lane r of each wave ends with row r's two words of its 64 columns
         auto ballot_row = [&](int rr, float h) {
             if constexpr (CPT == 1) {
@@ -523,6 +544,119 @@ struct HeadEpi {
             }
         }
     }
+    // kQuad phase 2: rows r0 <= r < nr with r = wave (mod 4), 4 rows' LDS reads issued before their arithmetic
+    __device__ __forceinline__ void p2_quad(const float *s_h, float (*s_dh)[KP], int64_t tile, int r0, int nr,
+                                            float *__restrict__ dz, int64_t ld, const float *__restrict__ W) {
+        const int w = e >> 6, l = e & 63;
+        float4 wq[KMAX];   // output o's weights of columns 4 l .. 4 l + 3 (rows o >= K: 0)
+#pragma unroll
+        for (int o = 0; o < KMAX; ++o) {
+            const float4 v = *reinterpret_cast<const float4 *>(W + (o < K ? o : 0) * kH + 4 * l);
+            wq[o] = o < K ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        f2v wc2[4][KH2];
+#pragma unroll
+        for (int o2 = 0; o2 < KH2; ++o2) {
+            const float4 a = wq[2 * o2];
+            const float4 b = 2 * o2 + 1 < KMAX ? wq[2 * o2 + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+            wc2[0][o2] = f2v{a.x, b.x};
+            wc2[1][o2] = f2v{a.y, b.y};
+            wc2[2][o2] = f2v{a.z, b.z};
+            wc2[3][o2] = f2v{a.w, b.w};
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+            for (int o2 = 0; o2 < KH2; ++o2) q_dw2[j][o2] = f2v{0.f, 0.f};
+            q_dbh[j] = 0.f;
+        }
+        int r = r0 + ((w - r0) & 3);
+        constexpr int RG = 4;   // rows per group: r, r + 4, r + 8, r + 12
+        for (; r + 4 * (RG - 1) < nr; r += 4 * RG) {
+            float4 hv[RG];
+            float gq[RG][KP];
+#pragma unroll
+            for (int u = 0; u < RG; ++u) {
+                hv[u] = *reinterpret_cast<const float4 *>(s_h + (r + 4 * u) * kS + 4 * l);
+#pragma unroll
+                for (int q = 0; q < KP; q += 4) {
+                    const float4 g4 = *reinterpret_cast<const float4 *>(&s_dh[r + 4 * u][q]);
+                    gq[u][q] = g4.x;
+                    gq[u][q + 1] = g4.y;
+                    gq[u][q + 2] = g4.z;
+                    gq[u][q + 3] = g4.w;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < RG; ++u) quad_row(hv[u], gq[u], wc2, dz + (tile * kTile + r + 4 * u) * ld);
+        }
+        for (; r < nr; r += 4) {
+            float gq[KP];
+#pragma unroll
+            for (int q = 0; q < KP; ++q) gq[q] = s_dh[r][q];
+            quad_row(*reinterpret_cast<const float4 *>(s_h + r * kS + 4 * l), gq, wc2, dz + (tile * kTile + r) * ld);
+        }
+    }
+    __device__ __forceinline__ void quad_row(const float4 &h4, const float (&g)[KP], const f2v (&wc2)[4][KH2],
+                                             float *__restrict__ dzrow) {
+#pragma clang fp contract(off)
+        const float hv[4] = {h4.x, h4.y, h4.z, h4.w};
+        float dv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            // col_row's arithmetic per element: d head . w as one packed chain over the output pairs, then their sum
+            f2v d2 = {0.f, 0.f};
+#pragma unroll
+            for (int o2 = 0; o2 < KH2; ++o2) d2 = __builtin_elementwise_fma(f2v{g[2 * o2], g[2 * o2 + 1]}, wc2[j][o2], d2);
+            float d = d2.x + d2.y;
+            const f2v hh = {hv[j], hv[j]};
+#pragma unroll
+            for (int o2 = 0; o2 < KH2; ++o2)
+                q_dw2[j][o2] = __builtin_elementwise_fma(f2v{g[2 * o2], g[2 * o2 + 1]}, hh, q_dw2[j][o2]);
+            d *= act_g<ACT>(hv[j], slope);
+            dv[j] = d;
+            q_dbh[j] += d;
+        }
+#if XPA_HEAD_PROBE != 4  // 4 = epilogue alone without the dz stores
+        if (dz_on) {
+            const f4v d4 = {dv[0], dv[1], dv[2], dv[3]};
+            f4v *dst = reinterpret_cast<f4v *>(dzrow + 4 * (e & 63));
+            if (g_head_dz_plain) *dst = d4;
+            else __builtin_nontemporal_store(d4, dst);
+        }
+#endif
+    }
+
+    // kQuad, after phase 2 and a block barrier (s_h free): the 4 waves' 16-row partials of each column through LDS, summed
+    // in wave order into column e's running dW_out / db_hidden; ends with a barrier (the LDS is the next tile's)
+    __device__ __forceinline__ void quad_flush(float *s_red) {
+        const int w = e >> 6, l = e & 63;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = 4 * l + j;
+#pragma unroll
+            for (int o2 = 0; o2 < KH2; ++o2) {
+                s_red[(w * (2 * KH2 + 1) + 2 * o2) * kH + c] = q_dw2[j][o2].x;
+                s_red[(w * (2 * KH2 + 1) + 2 * o2 + 1) * kH + c] = q_dw2[j][o2].y;
+            }
+            s_red[(w * (2 * KH2 + 1) + 2 * KH2) * kH + c] = q_dbh[j];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int o2 = 0; o2 < KH2; ++o2) {
+            f2v v = {s_red[(2 * o2) * kH + e], s_red[(2 * o2 + 1) * kH + e]};
+#pragma unroll
+            for (int ww = 1; ww < 4; ++ww)
+                v += f2v{s_red[(ww * (2 * KH2 + 1) + 2 * o2) * kH + e], s_red[(ww * (2 * KH2 + 1) + 2 * o2 + 1) * kH + e]};
+            acc_dw2[0][o2] += v;
+        }
+        float b = s_red[(2 * KH2) * kH + e];
+#pragma unroll
+        for (int ww = 1; ww < 4; ++ww) b += s_red[(ww * (2 * KH2 + 1) + 2 * KH2) * kH + e];
+        acc_dbh[0] += b;
+        __syncthreads();
+    }
+
     __device__ __forceinline__ void col_row(int j, float h, const float (&g)[KP], const f2v (&wc2)[KH2],
                                             float *__restrict__ dzrow) {
 #pragma clang fp contract(off)
@@ -567,15 +701,22 @@ struct HeadEpi {
 #pragma unroll
         for (int pass = 0; pass < NPASS; ++pass) {
             if (pass > 0) __syncthreads();  // wave 0 has read the previous pass
+#if XPA_HEAD_PROBE != 10  // 10 = epilogue alone without phase 1
             p1(pass, s_h, s_part, W);
+#endif
             __syncthreads();
+#if XPA_HEAD_PROBE != 10
             p1_sum(pass, s_part, bias);
+#endif
         }
+#if XPA_HEAD_PROBE != 11  // 11 = epilogue alone without the loss
         loss(s_dh, in, ent_coef, vf_coef);
+#endif
         __syncthreads();
         if (MODE == 2 && dv_out != nullptr && e < 64 && tile * kTile + e < batch) dv_out[tile * kTile + e] = s_dh[e][0];
-        p2(s_h, s_dh, tile, batch, 0, kTile, dz, ld);
+        p2(s_h, s_dh, tile, batch, 0, kTile, dz, ld, W);
         __syncthreads();  // s_h / s_dh reused by the next tile
+        if constexpr (kQuad) quad_flush(const_cast<float *>(s_h));
     }
 
     // Per-block partial row `blk`; with `zero_blk` >= 0 also a row of zeros (K16W: rows its grid does not own).
@@ -653,7 +794,7 @@ struct HeadEpi {
 // K12: z (the hidden pre-activations, row stride ld == ldx) streamed from HBM.
 template <int MODE, int ALGO, int ACT, int KMAX>
 __global__ __launch_bounds__(256, 2) void head_tile_kernel(XPA_HEAD_KERNEL_PARAMS) {
-    using Epi = HeadEpi<MODE, ALGO, ACT, KMAX>;
+    using Epi = HeadEpi<MODE, ALGO, ACT, KMAX, 4, false>;
     __shared__ __attribute__((aligned(16))) float s_h[kTile * kS];
     __shared__ __attribute__((aligned(16))) float s_part[kWaves][kTile][Epi::PH];
     __shared__ __attribute__((aligned(16))) float s_dh[kTile][Epi::KP];
@@ -1041,7 +1182,7 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
             xa = hout;
             lda = ldh;
         }
-#if XPA_HEAD_PROBE != 2 && XPA_HEAD_PROBE != 4 && XPA_HEAD_PROBE != 5  // tools/head_probe.py: 2 = epilogue alone (4, 5: parts of it)
+#if XPA_HEAD_PROBE != 2 && XPA_HEAD_PROBE != 4 && XPA_HEAD_PROBE != 5 && XPA_HEAD_PROBE != 10 && XPA_HEAD_PROBE != 11  // tools/head_probe.py: 2 = epilogue alone (4, 5, 10, 11: parts of it)
         if constexpr (S3 == 3) {   // K16R: B as K16P, A formed from the gathered rows (see trunk_chunk)
             const char *wsp = reinterpret_cast<const char *>(Wh);
             float *s_w0 = reinterpret_cast<float *>(reinterpret_cast<char *>(smem) + kROff);
@@ -1403,7 +1544,7 @@ int check_actor(int algo, int dist, int act_code, int64_t batch, int64_t act_dim
     if ((dist == XPA_DIST_GAUSSIAN && !logstd) || (algo == XPA_ALGO_PPO && !old_logp) ||
         (dist == XPA_DIST_CATEGORICAL && act_dim < 2))
         return (int)hipErrorInvalidValue;
-    if ((uintptr_t)w % 16) return (int)hipErrorInvalidValue;
+    if ((uintptr_t)w % 16 || (uintptr_t)dz % 16) return (int)hipErrorInvalidValue;   // r06: 16-B dz row stores (kQuad)
     return 0;
 }
 }  // namespace
@@ -1474,7 +1615,7 @@ int gemm_actor_entry(XPA_GEMM_ACTOR_PARAMS) {
                          partial_dw, partial_db_hidden, partial_db_out, loss_partials, loss_width);
     if (rc) return rc;
     if ((KIND == 3 && act_dim > 8) || !x || !w_hidden || !b_hidden || ((uintptr_t)x | (uintptr_t)w_hidden) % 16 ||
-        ldx < kKin || ldx % 4 || ld_dz < kH)
+        ldx < kKin || ldx % 4 || ld_dz < kH || ld_dz % 4)   // r06: 16-B dz row stores (kQuad)
         return (int)hipErrorInvalidValue;
     HeadArgs a{};
     a.batch = batch; a.K = (int)act_dim; a.ld = ld_dz; a.z = x; a.ldx = ldx; a.Wh = w_hidden; a.bh = b_hidden;
@@ -1565,7 +1706,7 @@ namespace {
 int check_trunk(int64_t d_in, const float *x_rows, int64_t ld_rows, const float *w_in, const float *b_in,
                 const float *w_hidden, const float *b_hidden, int64_t ld_dz) {
     if (d_in < 1 || d_in > kTrunkDMax || !x_rows || ld_rows < d_in || !w_in || !b_in || !w_hidden || !b_hidden ||
-        (uintptr_t)w_hidden % 16 || ld_dz < kH)
+        (uintptr_t)w_hidden % 16 || ld_dz < kH || ld_dz % 4)
         return (int)hipErrorInvalidValue;
     return 0;
 }
