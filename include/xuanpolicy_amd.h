@@ -702,6 +702,12 @@ int xpa_s3_gemm_bias_act_rows(const float *a, int64_t lda, const int64_t *ridx, 
                               unsigned *sign_out, xpa_stream_t stream);
 int xpa_s3_wgrad_rows(const float *a, int64_t lda, const int64_t *aidx, const float *b, int64_t ldb, int64_t rows,
                       int64_t m, int64_t n, int64_t slices, float *out, xpa_stream_t stream);
+/* r06 — K41V over rows narrower than its 128-row output tiles (C3's first fc layer: dW^T = flat^T g, flat [B, 3136]):
+ * m <= lda + 127; the last tile reads past each row, and after the last row into slack the caller keeps readable and
+ * finite; those output rows are garbage for the caller's finalize map to drop.  Replaces the fc weight gradient of
+ * loss.backward() through AC_CNN_Atari's first Linear (xuance/torch/representations/cnn.py:45-93). */
+int xpa_s3_wgrad_padded(const float *a, int64_t lda, const float *b, int64_t ldb, int64_t rows, int64_t m, int64_t n,
+                        int64_t slices, float *out, xpa_stream_t stream);
 /* K40R (r05): the rollout's paired hidden layer z [m, 512] = x [m, 256] . [B0 | B1] + bias on the split (B0 / B1 =
  * Wh_actor^T / Wh_critic^T split by xpa_s3_split_b, k = 256): 64-row x 128-column blocks for the rollout's few rows
  * (ppoclip_agent.py:63 self.action(obs) -> the policy's hidden layers); each output equals xpa_s3_gemm's + bias. */
@@ -862,6 +868,9 @@ int xpa_thin_linear_act_fwd_gather(int act, const float *x, int64_t ldx, int64_t
 int xpa_thin_probe(int mask);
 /* Diagnostics: 1 makes the head kernels store dz with plain (not non-temporal) stores. */
 int xpa_head_store_probe(int plain);
+/* r06 A/B: the K16 heads' second-slot blocks (blockIdx >= 256) start n x ~0.85 us late, so their k loop overlaps the
+ * first blocks' epilogue; 0 (the default) = off.  Returns a hipError. */
+int xpa_head_stagger(int n);
 /* The gather form writing h and its sign bits as well (r04; h_sign: 32 bytes per row, byte b bit j = h[row, 32 j + b]
  * > 0, the layout xpa_s3_gemm_trunk_bwd_sign reads); act 0 / 1. */
 int xpa_thin_linear_act_fwd_gather_sign(int act, const float *x, int64_t ldx, int64_t n_rows, const int64_t *idx,

@@ -331,3 +331,61 @@ def test_gemm_group_act_equals_group_then_k22(act, slope, channels, m):
     torch.cuda.synchronize()
     assert torch.equal(dz, dx)
     torch.testing.assert_close(db, db_ref, rtol=1e-5, atol=1e-5 * float(dx.abs().sum(0).max()) + 1e-9)
+
+
+@pytest.mark.parametrize("rows,width", [(16384, 3136), (2051, 3136), (300, 100)])
+def test_wgrad_padded_rows_match_f32_gemm_error(rows, width):
+    """r06, xpa_s3_wgrad_padded (a fc weight gradient whose input width is not a multiple of 128, e.g. the Nature CNN's 3136, read as 128-row tiles): the kept output
+    rows (< width) of the slices' sum against f64 within the f32 GEMM's error; the rows past the width read the next row
+    (or the slack after the last row, here filled with NaN: it may reach only the dropped rows)."""
+    from xuanpolicy_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(rows + width)
+    m = (width + 127) // 128 * 128
+    buf = torch.full((rows * width + (m - width),), float("nan"), device=DEV)
+    a = buf[:rows * width].view(rows, width)
+    a.copy_(_wide((rows, width), g))
+    b = torch.randn(rows, 2 * 256, device=DEV, generator=g)[:, 256:]   # a column half of g [rows, 512] (ld 512)
+    part = ops.s3_wgrad(a, b, m=m)
+    torch.cuda.synchronize()
+    got = part.double().sum(0)[:width]
+    ref = a.double().t() @ b.double()
+    native = torch.mm(a.t(), b)
+    scale = ref.abs().max().item()
+    err = (got - ref).abs().max().item()
+    err_f32 = (native.double() - ref).abs().max().item()
+    assert torch.isfinite(part[:, :width]).all()
+    assert err <= 2 * err_f32 + 2 ** -24 * scale, (err, err_f32, scale)
+    with pytest.raises(ValueError):   # no slack after the last row
+        ops.s3_wgrad(a.clone(), b, m=m)
+
+
+def test_fc_weight_gradient_split_matches_library(monkeypatch):
+    """r06: the C3 trunk's first fc weight gradient on K41V (fused_cnn._fc0_wgrad_split, at the update's B = 16384 and
+    the production AC_CNN_Atari) against the hipBLASLt f32 GEMM it replaces, both against f64: within 2x its error."""
+    from xuanpolicy_amd import fused_cnn
+    from xuanpolicy_amd.policies import AC_CNN_Atari, Categorical_AC_Policy
+
+    class _Disc:
+        n, shape = 6, ()
+    torch.manual_seed(0)
+    rep = AC_CNN_Atari((84, 84, 4), [8, 4, 3], [4, 2, 1], [32, 64, 64], None, torch.nn.init.orthogonal_, torch.nn.ReLU,
+                       DEV, [512])
+    pol = Categorical_AC_Policy(_Disc(), rep, [], [], None, torch.nn.init.orthogonal_, torch.nn.ReLU, DEV)
+    fc = fused_cnn.FusedCNNActorCritic(pol)
+    tr = fc.trunk_
+    B = 16384
+    x = torch.randint(0, 256, (B, 84, 84, 4), dtype=torch.int32, device=DEV).to(torch.uint8)
+    s, ctx = tr.forward(x)
+    hs, am, flat, fouts = ctx
+    assert tr._fc_wsplit_rows(B)
+    g = torch.randn(B, 512, device=DEV) * 1e-3
+    tr._dw_tmp = torch.empty_like(tr.fc[0][0].weight)
+    assert tr._fc0_wgrad_split(g, flat)
+    got = tr._dw_tmp.double().clone()
+    native = torch.mm(g.t(), flat)
+    torch.cuda.synchronize()
+    ref = g.double().t() @ flat.double()
+    scale = ref.abs().max().item()
+    err = (got - ref).abs().max().item()
+    err_f32 = (native.double() - ref).abs().max().item()
+    assert err <= 2 * err_f32 + 2 ** -24 * scale, (err, err_f32, scale)

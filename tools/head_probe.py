@@ -36,7 +36,8 @@ OUT = os.path.join(HERE, "_probe")
 VARIANTS = {0: "full", 1: "gemm only", 2: "epilogue only", 3: "staging only", 4: "epilogue without dz stores",
             5: "epilogue without phase 2", 6: "gemm without operand DMAs", 7: "K16P without its B-plane DMAs",
             8: "K16P without the A split (f32 bits as bf16)", 9: "K16P without the A split and without DMAs",
-            10: "epilogue without phase 1", 11: "epilogue without the loss"}
+            10: "epilogue without phase 1", 11: "epilogue without the loss",
+            12: "gemm only without the A split (f32 bits as bf16)"}
 # XPA_PROBE_FORM=s3p times the K16P entries (Wh as its bf16 planes, r04) instead of the f32 K16 ones
 FORM = os.environ.get("XPA_PROBE_FORM", "k16")
 FLAGS = {}   # variant -> hipcc defines, when not just -DXPA_HEAD_PROBE=<variant>

@@ -242,6 +242,7 @@ SIGNATURES = {
                                                            c_p, c_f32, c_p, c_i64, c_p, c_p, c_p, c_p, c_p]),
     "xpa_thin_probe": (ctypes.c_int, [ctypes.c_int]),
     "xpa_head_store_probe": (ctypes.c_int, [ctypes.c_int]),
+    "xpa_head_stagger": (ctypes.c_int, [ctypes.c_int]),
     "xpa_s3_probe": (ctypes.c_int, [ctypes.c_int]),
     "xpa_head_gemm_s3q_critic_mask": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p,
                                                      c_f32, c_p, c_i64, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64, c_p,
@@ -287,6 +288,7 @@ SIGNATURES = {
     "xpa_s3_gemm_trunk_bwd": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64, ctypes.c_int,
                                              c_f32, c_p, c_p, c_p]),
     "xpa_s3_wgrad": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
+    "xpa_s3_wgrad_padded": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
     "xpa_grad_norm_num_partials": (c_i64, [c_i64]),
     "xpa_clip_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_p, c_f32, c_f32, c_f32, c_f32, c_f32, c_i64, c_p,
                                           c_p]),

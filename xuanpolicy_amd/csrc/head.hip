@@ -147,6 +147,8 @@ __device__ __forceinline__ void load_tile(float4 (&zq)[16], const float *__restr
     }
 }
 
+__device__ int g_head_stagger = 0;   // r06: see head_gemm_kernel (xpa_head_stagger)
+
 // dz stores: non-temporal (0, the default) or plain (1: xpa_head_store_probe, r04 A/B — the update's dz is read next by
 // K41 and K42, and the 128 MiB of both halves fit the MALL)
 __device__ int g_head_dz_plain = 0;
@@ -1007,8 +1009,18 @@ __device__ __forceinline__ void gemm_chunk_s3q(const char *st, f32x16 (&acc)[2][
     const int sw = (i >> 2) & 3;
     const float *pa = A + ((wave & 1) * 32 + i) * kKC;
     xpa_bf16x8 ah, am, al;
+#if XPA_HEAD_PROBE == 8 || XPA_HEAD_PROBE == 9 || XPA_HEAD_PROBE == 12  // the A split's cost: f32 bits fed as bf16
+    {
+        const float4 lo = *reinterpret_cast<const float4 *>(pa + 4 * (h ^ sw)),
+                     hi = *reinterpret_cast<const float4 *>(pa + 4 * ((h + 2) ^ sw));
+        ah = __builtin_bit_cast(xpa_bf16x8, lo);
+        am = __builtin_bit_cast(xpa_bf16x8, hi);
+        al = __builtin_bit_cast(xpa_bf16x8, lo);
+    }
+#else
     xpa_split8(*reinterpret_cast<const float4 *>(pa + 4 * (h ^ sw)),
                *reinterpret_cast<const float4 *>(pa + 4 * ((h + 2) ^ sw)), ah, am, al);
+#endif
     const xpa_bf16x8 *bimg = reinterpret_cast<const xpa_bf16x8 *>(st + 4096) + lane;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -1153,6 +1165,11 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int64_t ntiles = (batch + kTile - 1) / kTile;
     if ((int64_t)blockIdx.x >= head_partials(batch)) return;  // no partial row of its own (see kGridMax)
+    // r06 (xpa_head_stagger, A/B): the second wave of resident blocks (blockIdx >= 256: the second block slot of each CU)
+    // starts g_head_stagger x ~0.85 us late, so that its k loop runs beside the first block's epilogue instead of in
+    // phase with it (both blocks' GEMMs sharing the matrix cores, then both epilogues sharing the VALU).  0: off.
+    if (g_head_stagger > 0 && blockIdx.x >= 256)
+        for (int i = 0; i < g_head_stagger; ++i) __builtin_amdgcn_s_sleep(32);
     Epi epi;
     epi.init_a(t, K_in, W, logstd, adv_partials, n_adv_partials, batch, clip_range, slope, s_stats);
     epi.mask_out = cmask;
@@ -1287,7 +1304,7 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
                     smem[row * kS + col] = act_f<ACT>(acc[rt][ct][r] + bc, slope);
                 }
             }
-#if XPA_HEAD_PROBE == 1 || XPA_HEAD_PROBE == 3 || XPA_HEAD_PROBE == 6  // the GEMM alone: keep its result live
+#if XPA_HEAD_PROBE == 1 || XPA_HEAD_PROBE == 3 || XPA_HEAD_PROBE == 6 || XPA_HEAD_PROBE == 12  // the GEMM alone: keep its result live
         __syncthreads();
         if (r0 + (t >> 2) < batch) dz[(r0 + (t >> 2)) * ld + (t & 3)] = smem[(t >> 2) * kS + (t & 3)];
 #else
@@ -1688,6 +1705,11 @@ XPA_API int xpa_lds_poison(xpa_stream_t stream) {
 
 XPA_API int xpa_head_store_probe(int plain) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_head_dz_plain), &plain, sizeof(int));
+}
+
+// r06 A/B: the K16 heads' second-slot blocks start n x ~0.85 us late (see head_gemm_kernel); 0 = off (the default)
+XPA_API int xpa_head_stagger(int n) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_head_stagger), &n, sizeof(int));
 }
 
 // diagnostics only (tools/k16w_ab.py --probe): see g_ws_probe

@@ -1958,6 +1958,23 @@ XPA_API int xpa_s3_wgrad(const float *a, int64_t lda, const float *b, int64_t ld
     return xpa_launch_status();
 }
 
+// K41V over rows narrower than the row tiles (r06: C3's first fc layer, dW^T = flat^T g with flat [B, 3136]): m may exceed
+// lda by < 128 — the last row tile reads past each row into the next (finite values of the same buffer) and, after the
+// last row, into slack the caller guarantees readable (and finite); those output rows are garbage, dropped by the
+// caller's finalize map.  No per-slice row limit (the rows are read in place, not through an index stage).
+XPA_API int xpa_s3_wgrad_padded(const float *a, int64_t lda, const float *b, int64_t ldb, int64_t rows, int64_t m,
+                                int64_t n, int64_t slices, float *out, xpa_stream_t stream) {
+    if (!a || !b || !out || rows <= 0 || m <= 0 || m % kWgM || n != kN || lda < 4 || m > lda + kWgM || ldb < n ||
+        slices < 1 || slices > 4096 || (lda & 3) || (ldb & 3) ||
+        ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15))
+        return (int)hipErrorInvalidValue;
+    int64_t per = (rows + slices - 1) / slices;
+    per = (per + kWgKC - 1) / kWgKC * kWgKC;
+    const dim3 grid((unsigned)(slices * (m / kWgM))), block(512);
+    s3_wgrad_v_kernel<1><<<grid, block, 0, stream>>>(a, lda, b, ldb, rows, m, (int)slices, per, out);
+    return xpa_launch_status();
+}
+
 // K41V's row-index form (r05): A's row r is row aidx[r] of a (C4's trunk dW straight from the rollout buffer); m may
 // exceed a's row width by < 128 (the last row tile reads past each row: the caller guarantees readable slack after the
 // buffer's last row; those output rows are garbage and dropped by the caller's finalize map); rows per slice <= 1536

@@ -237,7 +237,7 @@ class _Trunk:
             self._w_ver += 1
         return self._w_hwc
 
-    # r05: the first fc layer of the update's minibatches (C3: [16384, 3136] x [3136, 512]) on the bf16 matrix cores by
+    # r05: the first fc layer of the update's minibatches (C3: [16384, 6400] x [6400, 512]) on the bf16 matrix cores by
     # the three-way split (K40G: one launch per GEMM; forward in 2 k halves x 256-column blocks, summed in a fixed
     # order; the data gradient in 256-column blocks, the last one aligned to the end so no block is padded — the
     # columns it shares with its neighbour come out bit-identical from both).  The rollout's 1024-frame forwards stay
@@ -314,6 +314,38 @@ class _Trunk:
                    "colsum db (fc act)")
         return dz
 
+    # r06: the first fc layer's weight gradient on the split too (was hipBLASLt's f32 GEMM: 822 us per C3 minibatch,
+    # profiles/r05/r05k28b): dW^T = flat^T g as K41V slices per 256-column half of g (AC_CNN_Atari: flat [B, 6400] =
+    # 50 row tiles of 128; a width that is not a multiple of 128 takes the padded form, the columns past a row reading
+    # the next row or the slack the forward leaves after the last row, into output rows the finalize map drops); the
+    # batched f64 finalize writes the kept rows transposed into dW.  Same row rule as the forward's split
+    # (fc_split_min_rows).
+    fc_wsplit = True
+
+    def _fc_wsplit_rows(self, rows):
+        lin = self.fc[0][0] if self.fc else None
+        return (self.fc_wsplit and lin is not None and ops.S3_GEMMS and self.tail == "flatten"
+                and rows >= self.fc_split_min_rows and lin.out_features % 256 == 0 and lin.in_features % 4 == 0)
+
+    def _fc0_wgrad_split(self, g, flat):
+        """self._dw_tmp = g^T flat ([out, in], the forward's (H, W, C) column order) on K41V; False (nothing done) where it
+        does not apply."""
+        rows, in_f = flat.shape
+        m = (in_f + 127) // 128 * 128
+        if not (self._fc_wsplit_rows(rows) and g.is_contiguous() and flat.stride(1) == 1 and flat.stride(0) == in_f
+                and flat.untyped_storage().nbytes() // 4 >= flat.storage_offset() + (rows - 1) * in_f + m):
+            return False
+        out_f = g.shape[1]
+        S = ops.s3_wgrad_slices(rows, m)
+        if getattr(self, "_fcq", None) is None:
+            self._fcq = ops.ColsumQueue()
+        for h in range(out_f // 256):
+            part = self.parts.buf(("fcw", h, S, m), (S, m, 256), g.device)
+            ops.s3_wgrad(flat, g[:, 256 * h:256 * (h + 1)], out=part, slices=S, m=m if m != in_f else None)
+            self._fcq.add(part.view(S, -1), self._dw_tmp[256 * h:256 * (h + 1)], tmap=(256, in_f, in_f))
+        self._fcq.flush(g.device)
+        return True
+
     def _fc0_dgrad_split(self, g):
         rows = g.shape[0]
         _, _, bd, c0s = self._fc_planes()
@@ -358,9 +390,18 @@ class _Trunk:
             h = self.frames(xu)
             hs = [h]
             convs = self.convs
+        last = convs[-1][0] if convs else None
         for conv, code, slope in convs:
             if self._igemm_ok(conv, h.numel(), self._out_rows(conv, h.shape)):   # K28 (bias + activation fused)
-                y = self._conv_fwd(conv, code, slope, h)
+                # r06: the last block's output (the fc layer's flat input) with slack after it where the split weight
+                # gradient will read it as 128-row tiles (_fc0_wgrad_split)
+                slack = 0
+                if conv is last and self.tail == "flatten" and self._fc_wsplit_rows(B):
+                    oh = (h.shape[1] + 2 * conv.padding[0] - conv.kernel_size[0]) // conv.stride[0] + 1
+                    ow = (h.shape[2] + 2 * conv.padding[0] - conv.kernel_size[0]) // conv.stride[0] + 1
+                    width = oh * ow * conv.out_channels
+                    slack = (width + 127) // 128 * 128 - width   # 0 for AC_CNN_Atari's 10 x 10 x 64 = 6400
+                y = self._conv_fwd(conv, code, slope, h, slack=slack)
             else:
                 _library_conv_guard(conv)
                 z = F.conv2d(h.permute(0, 3, 1, 2), conv.weight, None, conv.stride, conv.padding)
@@ -430,13 +471,15 @@ class _Trunk:
         return B * ((H + 2 * pd - k) // st + 1) * ((W + 2 * pd - k) // st + 1)
 
     @staticmethod
-    def _conv_fwd(conv, code, slope, h):
-        """K28 forward: act(conv(h) + b), h NHWC f32 [B, H, W, C] -> NHWC [B, OH, OW, out]."""
+    def _conv_fwd(conv, code, slope, h, slack=0):
+        """K28 forward: act(conv(h) + b), h NHWC f32 [B, H, W, C] -> NHWC [B, OH, OW, out].  slack: floats of the same
+        allocation after the output (readable, never written: the padded K41 reads them into output rows it drops)."""
         B, H, W, C = h.shape
         k, st, pd = conv.kernel_size[0], conv.stride[0], conv.padding[0]
         OH, OW = (H + 2 * pd - k) // st + 1, (W + 2 * pd - k) // st + 1
         h = h if h.is_contiguous() else h.contiguous()
-        y = torch.empty((B, OH, OW, conv.out_channels), dtype=torch.float32, device=h.device)
+        n = B * OH * OW * conv.out_channels
+        y = torch.empty((n + slack,), dtype=torch.float32, device=h.device)[:n].view(B, OH, OW, conv.out_channels)
         _lib.check(ops.lib().xpa_conv_fwd(code, ops._p(h), B, H, W, C, ops._p(conv.weight), ops._p(conv.bias),
                                           conv.out_channels, k, st, pd, float(slope), ops._p(y), ops._stream(h.device)),
                    "xpa_conv_fwd")
@@ -539,7 +582,8 @@ class _Trunk:
                 if j == 0:
                     if self._dw_tmp is None:
                         self._dw_tmp = torch.empty_like(lin.weight)
-                    torch.mm(g.t(), x_in, out=self._dw_tmp)
+                    if not self._fc0_wgrad_split(g, x_in):
+                        torch.mm(g.t(), x_in, out=self._dw_tmp)
                     Cl, Hl, Wl = self._chw
                     lin.weight.grad.view(lin.out_features, Cl, Hl, Wl).copy_(
                         self._dw_tmp.view(lin.out_features, Hl, Wl, Cl).permute(0, 3, 1, 2))

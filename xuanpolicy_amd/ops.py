@@ -522,7 +522,8 @@ def s3_wgrad(a, b, out=None, slices=None, aidx=None, m=None):
     """K41: per-slice partials out [S, m, 256] of a^T b over the rows (a [rows, m] = dz, b [rows, 256] = the layer
     input; unit column strides), on the bf16 matrix cores by the three-way split.  The caller sums the S slices.
     aidx (int64 [rows], r05): a's row r is a[aidx[r]] of a [n_rows, width] (m given, m <= width + 127: output rows past
-    the width are garbage for the caller to drop; a needs readable slack after its last row; xpa_s3_wgrad_rows)."""
+    the width are garbage for the caller to drop; a needs readable slack after its last row; xpa_s3_wgrad_rows).
+    m > a.shape[1] without aidx (r06): the rows in place, the same padding rule (xpa_s3_wgrad_padded)."""
     if aidx is not None:
         _req(a, "a", torch.float32, contiguous=False)
         _req(b, "b", torch.float32, contiguous=False)
@@ -540,6 +541,25 @@ def s3_wgrad(a, b, out=None, slices=None, aidx=None, m=None):
         return out
     _req(a, "a", torch.float32, contiguous=False)
     _req(b, "b", torch.float32, contiguous=False)
+    if m is not None and m != a.shape[1]:
+        # r06 (xpa_s3_wgrad_padded): m output rows over a's narrower rows (m <= width + 127); the rows past the width
+        # read on into the next row and, after the last row, into slack of a's own storage, which must be readable
+        rows, width = a.shape
+        if a.dim() != 2 or a.stride(1) != 1 or not width < m <= width + 127:
+            raise ValueError("padded form: a [rows, width] with width < m <= width + 127")
+        lda, ldb = a.stride(0), _row_stride(b, "b", 256)
+        need = a.storage_offset() + (rows - 1) * lda + m
+        if a.untyped_storage().nbytes() // 4 < need:
+            raise ValueError("padded form: a needs %d floats of slack after its last row" % (m - width))
+        if b.shape[0] != rows:
+            raise ValueError("a and b must have the same rows")
+        S = slices or s3_wgrad_slices(rows, m)
+        if out is None:
+            out = torch.empty(S, m, 256, dtype=torch.float32, device=a.device)
+        _req(out, "out", torch.float32, (S, m, 256))
+        _lib.check(lib().xpa_s3_wgrad_padded(_p(a), lda, _p(b), ldb, rows, m, 256, S, _p(out), _stream(a.device)),
+                   "xpa_s3_wgrad_padded")
+        return out
     rows, m = a.shape
     lda, ldb = _row_stride(a, "a", m), _row_stride(b, "b", 256)
     if b.shape[0] != rows:
