@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--pair-sa", type=int, default=0, help="K41P's actor share of 128 slices (0: the default)")
     p.add_argument("--crit-factored", choices=("on", "off"), default="on",
                    help="the critic's factored backward (K41P / K42C, r05) or its dz_critic through K41V / K42S")
+    p.add_argument("--fuse-post", choices=("on", "off"), default="on",
+                   help="K14F: K8's post step + the next obs_rms.update inside the env-fused K14 launch (r06)")
     p.add_argument("--fold-rms", choices=("on", "off"), default="off",
                    help="the next step's obs-RMS update folded into K8 (r05 opt-in, measured neutral) or its own launch")
     p.add_argument("--rollout-h-store", choices=("plain", "nt"), default="nt",
@@ -1005,6 +1007,7 @@ def main():
     FusedActorCritic.ROLLOUT_SPLIT = args.rollout_split == "on"
     import xuanpolicy_amd.agents as _agents
     _agents.FOLD_RMS = args.fold_rms == "on"
+    _agents.FUSE_POST = args.fuse_post == "on"
     if args.pair_sa:
         ops.lib().xpa_s3_wgrad_pair_tune(args.pair_sa)
     thin_probe = (1 if args.thin_store == "plain" else 0) | (2 if args.rollout_h_store == "plain" else 0)

@@ -998,6 +998,31 @@ int xpa_conv_wgrad(int act, const float *g, const float *y, float slope, const f
  * the LDS-slab form applies (both give the same sums up to f32 association; process-global, not thread-safe). */
 void xpa_conv_wgrad_force_stream(int on);
 
+/* r06, K14F — one device env step's last launch: xpa_rollout_policy_head_synthbox (policy heads, sample, store, SynthBox
+ * env step) and K8's deferred + normalised post step (xpa_rollout_post_deferred_norm; with obs_count non-NULL also the
+ * next step's obs_rms.update, xpa_rollout_post_deferred_norm_rms) in ONE launch: the tail of ppoclip_agent.py:65-75
+ * (envs.step, reward normalisation, memory.store, the path closing of finish_path's callers) and the obs_rms.update of
+ * ppoclip_agent.py:62-63 for the next observation.  slot_from_next: kept truncation rows are the env's next observation
+ * (A2C's reset_obs bootstrap, a2c_agent.py:88-95) instead of its final one.  part / tickets: the workspace sized by
+ * xpa_rollout_step_workspace (f64 partials, returned in doubles; *n_tickets int32 tickets zeroed once, left zero by every
+ * launch).  The partial sums are taken in a fixed order (any block arrival order gives the same bits). */
+int64_t xpa_rollout_step_workspace(int64_t n_envs, int64_t obs_dim, int rms, int64_t *n_tickets);
+/* Diagnostics: bits 1 / 2 / 4 end K14F's tail after the block partials / the group tickets / the group sums (results
+ * then invalid: timing only; tools/k14f_probe.py); 0 = production. */
+int xpa_k14f_probe(int bits);
+int xpa_rollout_step_synthbox(
+    int act, int64_t n_envs, int64_t act_dim, int64_t horizon, int64_t hidden, int64_t ld, const float *z_actor,
+    const float *z_critic, float slope, const float *w_actor, const float *b_actor, const float *w_critic,
+    const float *b_critic, const float *logstd, xpa_cursor_t *cursor, uint32_t seed, float act_clip, float *buf_act,
+    float *buf_logp, float *buf_val, int64_t obs_dim, const float *wcat_t, uint32_t env_seed, int32_t max_episode_steps,
+    float noise, float term_thresh, float reset_scale, float *state, int64_t ld_state, float *final_obs, float *rew,
+    uint8_t *term, uint8_t *trunc, int32_t *ep_step, uint32_t *ep_index, float *ep_score, float *ep_last_score,
+    int32_t *ep_last_len, float *slot_obs, int32_t *slot_t, int64_t n_slots, int32_t *overflow, int slot_from_next,
+    float *obs_mean, float *obs_var, double *obs_count, float obs_clip, float *boot_norm, int64_t ld_norm,
+    float *ret_mean, float *ret_var, double *ret_count, float *returns, float *buf_rew, float *buf_term,
+    uint8_t *buf_closed, float *buf_boot, float gamma, int mask_returns, int use_rewnorm, float rew_range,
+    int atari_lifeloss, double *part, int32_t *tickets, xpa_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

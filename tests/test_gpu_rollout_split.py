@@ -66,6 +66,7 @@ def test_fold_rms_matches_standalone_update(monkeypatch):
     import xuanpolicy_amd.agents as ag
     from xuanpolicy_amd.runner import build_synthbox_ppo
     outs = []
+    monkeypatch.setattr(ag, "FUSE_POST", False)   # r06: K14F would fold the update in both arms
     for fold in (True, False):
         monkeypatch.setattr(ag, "FOLD_RMS", fold)
         agent = build_synthbox_ppo(n_envs=1000, n_steps=16, obs_dim=17, act_dim=6, hidden=256, n_epoch=1,

@@ -289,6 +289,15 @@ SIGNATURES = {
                                              c_f32, c_p, c_p, c_p]),
     "xpa_s3_wgrad": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
     "xpa_s3_wgrad_padded": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
+    "xpa_rollout_step_workspace": (c_i64, [c_i64, c_i64, ctypes.c_int, c_p]),
+    "xpa_k14f_probe": (ctypes.c_int, [ctypes.c_int]),
+    "xpa_rollout_step_synthbox": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f32,
+                                                 c_p, c_p, c_p, c_p, c_p, c_p, c_u32, c_f32, c_p, c_p, c_p,
+                                                 c_i64, c_p, c_u32, ctypes.c_int32, c_f32, c_f32, c_f32, c_p,
+                                                 c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                                                 c_p, c_p, c_i64, c_p, ctypes.c_int, c_p, c_p, c_p, c_f32, c_p, c_i64,
+                                                 c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, ctypes.c_int,
+                                                 ctypes.c_int, c_f32, ctypes.c_int, c_p, c_p, c_p]),
     "xpa_grad_norm_num_partials": (c_i64, [c_i64]),
     "xpa_clip_adam_step": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_p, c_f32, c_f32, c_f32, c_f32, c_f32, c_i64, c_p,
                                           c_p]),

@@ -52,6 +52,9 @@ def _cfg(config, name, default):
 # into K8, 6.5 + 7.7 -> 15.0 us), so it is an opt-in (bench.py --fold-rms on); off keeps the reference's update order
 # exactly, also around test() calls (which update obs_rms with the test observations, ppoclip_agent.py:125)
 FOLD_RMS = False
+# r06: K8's post step (and, with per-rank obs statistics, the next step's obs_rms.update) inside the env-fused K14 launch
+# (K14F, ops.rollout_policy_head_synthbox(post=)): a C2 env step in three launches instead of five
+FUSE_POST = True
 
 class _OnPolicyAgent:
     algo = "ppo"
@@ -129,6 +132,8 @@ class _OnPolicyAgent:
         # (envs.reset bumps envs.resets) re-arms it.  test() does not: its obs_rms.update merges other rows, and the
         # folded merge of env.obs already happened (the Chan merge is order-independent up to rounding)
         self.fold_rms = FOLD_RMS
+        self.fuse_post = FUSE_POST
+        self._k14f_ws = None
         self._rms_pending = True
         self._rms_resets = getattr(envs, "resets", 0)
         self._rms_fold_part = None
@@ -248,9 +253,10 @@ class _OnPolicyAgent:
         ok = getattr(self.envs, "fusable_with_policy_step", None)
         return bool(fm is not None and self.fuse_env_step and ok is not None and ok(self.dist))
 
-    def _sample_into_buffer(self, raw_x=None, fuse_env=False):
+    def _sample_into_buffer(self, raw_x=None, fuse_env=False, post=None):
         """raw_x: the raw observations, normalised inside the fused trunk (see _rollout_step_device).
-        fuse_env: also step the device env inside K14 (the caller then skips env.step_device())."""
+        fuse_env: also step the device env inside K14 (the caller then skips env.step_device()).
+        post (with fuse_env): K8's post step in the same launch (K14F, _k14f_post; the caller then skips _post)."""
         mem = self.memory
         logp_buf = mem.auxiliary_infos["old_logp"] if self.algo == "ppo" else self.logp_scratch
         env_in = self.envs.act_in if self.device_env else self._act_scratch()
@@ -260,12 +266,14 @@ class _OnPolicyAgent:
             T, D = self.n_steps, self.obs_dim
             fm.rollout_act(raw_x, self.dist, self.cursor, self.seed, mem.actions, logp_buf, mem.values, env_in,
                            act_clip=1.0, norm=(self.obs_mean, self.obs_var, self._obs_clip(), self.obs_norm,
-                                               mem.observations, T * D, self.cursor), env=env)
+                                               mem.observations, T * D, self.cursor), env=env, post=post)
             return
         if fm is not None:
             fm.rollout_act(self._policy_in, self.dist, self.cursor, self.seed, mem.actions, logp_buf, mem.values,
-                           env_in, act_clip=1.0, env=env)
+                           env_in, act_clip=1.0, env=env, post=post)
             return
+        if post is not None:
+            raise RuntimeError("K14F needs the fused rollout forward")
         head, logstd, v = self._heads(self._policy_in)
         ops.rollout_sample(self.dist, head.contiguous(), logstd, v.contiguous(), self.cursor, self.seed,
                            mem.actions, logp_buf, mem.values, env_in, act_clip=1.0)
@@ -345,10 +353,34 @@ class _OnPolicyAgent:
                          v_boot_mid=v_mid.contiguous() if v_mid is not None else None)
 
     def _rms_fold_ok(self):
-        """The next step's obs_rms.update rides in K8 (device env, per-rank statistics, deferred bootstraps, D <= 64)."""
-        return (self.fold_rms and self.device_env and self.use_obsnorm and not self.sync_obs_rms and self.defer_boot
-                and not self.raw_obs and self.obs_dim <= 64 and self.envs.obs.dim() == 2
+        """The next step's obs_rms.update rides in the step's last launch — K14F (_k14f_on) or, with FOLD_RMS, K8 —
+        (device env, per-rank statistics, deferred bootstraps, D <= 64)."""
+        return ((self.fold_rms or self._k14f_on()) and self.device_env and self.use_obsnorm and not self.sync_obs_rms
+                and self.defer_boot and not self.raw_obs and self.obs_dim <= 64 and self.envs.obs.dim() == 2
                 and self.envs.obs.stride(1) == 1)
+
+    def _k14f_on(self, fuse=None):
+        """K8's post step runs inside the env-fused K14 launch (K14F): fused env step, deferred bootstraps."""
+        if fuse is None:
+            fuse = self._env_fused(self._rollout_mlp())
+        return bool(fuse and self.fuse_post and self.defer_boot and not self.raw_obs)
+
+    def _k14f_post(self, fuse):
+        """K14F's post-step arguments (ops.rollout_policy_head_synthbox(post=)) — the deferred, normalised K8 call of
+        _post, with the next step's obs_rms.update where _rms_fold_ok — or None where K14F does not apply."""
+        if not self._k14f_on(fuse):
+            return None
+        rms = self._rms_fold_ok()
+        if self._k14f_ws is None or self._k14f_ws[0] != rms:   # graph-capture safe: allocated on the first (eager) step
+            self._k14f_ws = (rms, ops.rollout_step_workspace(self.n_envs, self.obs_dim, rms, self.device))
+        mem = self.memory
+        return dict(slot_obs=self.slot_obs, slot_t=self.slot_t, overflow=self.slot_overflow,
+                    slot_from_next=self.boot_from_reset, obs_mean=self.obs_mean, obs_var=self.obs_var,
+                    obs_count=self.obs_count if rms else None, obs_clip=self._obs_clip(), boot_norm=self.boot_obs,
+                    ret_mean=self.ret_mean, ret_var=self.ret_var, ret_count=self.ret_count, returns=self.returns,
+                    buf_rew=mem.rewards, buf_term=mem.terminals, buf_closed=mem.closed, buf_boot=mem.boot,
+                    gamma=self.gamma, mask_returns=(self.algo == "ppo"), use_rewnorm=self.use_rewnorm,
+                    rew_range=self.rewnorm_range, atari_lifeloss=self.atari, workspace=self._k14f_ws[1])
 
     def _rms_update(self, x):
         if self.sync_obs_rms:
@@ -444,17 +476,22 @@ class _OnPolicyAgent:
             fm = self._rollout_mlp()
             if fm is not None and fm.thin0 and x.stride(1) == 1:
                 fuse = self._env_fused(fm)
-                self._sample_into_buffer(raw_x=x, fuse_env=fuse)   # normalisation fused into the trunk's first layer
+                post = self._k14f_post(fuse)
+                # normalisation fused into the trunk's first layer
+                self._sample_into_buffer(raw_x=x, fuse_env=fuse, post=post)
                 if not fuse:
                     env.step_device()
-                self._post(env.rew, env.term, env.trunc, env.final_obs)
+                if post is None:
+                    self._post(env.rew, env.term, env.trunc, env.final_obs)
                 return
             self._normalize_into(x, self.obs_norm, True)
         fuse = self._env_fused(self._rollout_mlp())
-        self._sample_into_buffer(fuse_env=fuse)
+        post = self._k14f_post(fuse)
+        self._sample_into_buffer(fuse_env=fuse, post=post)
         if not fuse:
             env.step_device()
-        self._post(env.rew, env.term, env.trunc, env.final_obs)
+        if post is None:
+            self._post(env.rew, env.term, env.trunc, env.final_obs)
 
     def _rollout_step_graph(self):
         """The device env step captured once into a hipGraph and replayed: every per-step argument

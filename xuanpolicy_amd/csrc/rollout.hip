@@ -275,6 +275,21 @@ __global__ __launch_bounds__(1024) void rms_partials_cols_kernel(const float *__
 // the partials may come from other blocks of the same launch), then each column is summed over the
 // partials in block order (deterministic).
 constexpr int kMergeLds = 2048;  // doubles of LDS staging: np * dim <= 1024 (else per-column global loads)
+// column d of the merge: s / q = the batch's sums of (x - mean[d]) and its square over n rows, c0 = the running count
+__device__ __forceinline__ void rms_merge_col(double s, double q, double n, double c0, float *mean, float *var,
+                                              int64_t d) {
+    const double ms = s / n;
+    const double m0 = (double)mean[d], v0 = (double)var[d];
+    const double bm = m0 + ms;                        // batch mean
+    const double bvar = fmax(q / n - ms * ms, 0.0);   // np.std(x, axis=0)**2 (ddof 0)
+    const double tot = c0 + n;
+    const double delta = bm - m0;
+    const double new_mean = m0 + delta * n / tot;
+    const double m2 = v0 * c0 + bvar * n + delta * delta * c0 * n / tot;
+    mean[d] = (float)new_mean;
+    var[d] = (float)(m2 / tot);
+}
+
 __device__ void rms_merge_body(const double *part, int64_t np, int64_t n, int64_t dim, float *__restrict__ mean,
                                float *__restrict__ var, double *__restrict__ count) {
     __shared__ double s_part[kMergeLds];
@@ -289,16 +304,7 @@ __device__ void rms_merge_body(const double *part, int64_t np, int64_t n, int64_
             s += staged ? s_part[p * dim + d] : xpa_load_agent(part + p * dim + d);
             q += staged ? s_part[(np + p) * dim + d] : xpa_load_agent(part + (np + p) * dim + d);
         }
-        const double ms = s / (double)n;
-        const double m0 = (double)mean[d], v0 = (double)var[d];
-        const double bm = m0 + ms;                               // batch mean
-        const double bvar = fmax(q / (double)n - ms * ms, 0.0);  // np.std(x, axis=0)**2 (ddof 0)
-        const double tot = c0 + (double)n;
-        const double delta = bm - m0;
-        const double new_mean = m0 + delta * (double)n / tot;
-        const double m2 = v0 * c0 + bvar * (double)n + delta * delta * c0 * (double)n / tot;
-        mean[d] = (float)new_mean;
-        var[d] = (float)(m2 / tot);
+        rms_merge_col(s, q, (double)n, c0, mean, var, d);
     }
     __syncthreads();
     if (threadIdx.x == 0) *count = c0 + (double)n;
@@ -437,11 +443,19 @@ struct SynthEnvArgs {
     const float *wt;  // fused form: [W | U]^T, [D + A, D] row-major
 };
 
+// What K14F's post tail needs from the step, in registers: reward and flags (every lane), and lane d's final observation
+// (sv) and next state (sn) for d = lane < min(D, 64)
+struct EnvRowOut {
+    float r, sv, sn;
+    bool te, tr;
+};
+
 // t, ep, score0: the env's ep_step / ep_index / ep_score (loaded by the caller, early in the fused form)
 template <class PreFn>
-__device__ __forceinline__ void synthbox_env_row(int64_t n, int lane, const SynthEnvArgs &e, PreFn pre, int t,
-                                                 uint32_t ep, float score0) {
+__device__ __forceinline__ EnvRowOut synthbox_env_row(int64_t n, int lane, const SynthEnvArgs &e, PreFn pre, int t,
+                                                      uint32_t ep, float score0) {
     const int D = e.D;
+    EnvRowOut o{0.f, 0.f, 0.f, false, false};
     float sumsq = 0.f, s0 = 0.f;
     for (int d = lane; d < D; d += 64) {
         const uint32_t base = ((uint32_t)t * (uint32_t)D + (uint32_t)d) * 4u;
@@ -453,6 +467,7 @@ __device__ __forceinline__ void synthbox_env_row(int64_t n, int lane, const Synt
         e.final_obs[n * D + d] = sv;
         sumsq += sv * sv;
         if (d == 0) s0 = sv;
+        if (d == lane) o.sv = sv;
     }
     sumsq = xpa_wave_sum(sumsq);
     s0 = __shfl(s0, 0, 64);
@@ -471,7 +486,11 @@ __device__ __forceinline__ void synthbox_env_row(int64_t n, int lane, const Synt
             sn = e.final_obs[n * D + d];
         }
         e.state[n * e.ld_state + d] = sn;
+        if (d == lane) o.sn = sn;
     }
+    o.r = r;
+    o.te = te;
+    o.tr = tr;
     if (lane == 0) {
         e.rew[n] = r;
         e.term[n] = te ? 1 : 0;
@@ -487,12 +506,220 @@ __device__ __forceinline__ void synthbox_env_row(int64_t n, int lane, const Synt
             e.ep_score[n] = score;
         }
     }
+    return o;
 }
 
 __device__ __forceinline__ float wave_allsum_f(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
+}
+
+// obs_normalize_kernel's arithmetic on one element (K8's NORM form and K14F)
+__device__ __forceinline__ float obs_norm1(float x, float m, float v, float clip) {
+    const float sd = sqrtf(v);
+    const float y = (x - m) / (sd + 1e-8f);
+    return fminf(fmaxf(y, -clip), clip);
+}
+
+// ret_rms.update_from_moments (statistic_tools.py:86-112) from the summed (count, sum, sumsq) of the closed paths.
+__device__ __forceinline__ void ret_rms_merge_local(double c, double s1, double s2, float &m, float &v, double &cnt) {
+    if (c > 0.0) {
+        const double bm = s1 / c;
+        const double bvar = fmax(s2 / c - bm * bm, 0.0);
+        const double c0 = cnt, m0 = (double)m, v0 = (double)v;
+        const double tot = c0 + c;
+        const double delta = bm - m0;
+        m = (float)(m0 + delta * c / tot);
+        v = (float)((v0 * c0 + bvar * c + delta * delta * c0 * c / tot) / tot);
+        cnt = tot;
+    }
+}
+
+__device__ __forceinline__ void ret_rms_merge(double c, double s1, double s2, float *ret_mean, float *ret_var,
+                                              double *ret_count) {
+    if (c > 0.0) {
+        float m = *ret_mean, v = *ret_var;
+        double cnt = *ret_count;
+        ret_rms_merge_local(c, s1, s2, m, v, cnt);
+        *ret_mean = m;
+        *ret_var = v;
+        *ret_count = cnt;
+    }
+}
+
+// ---- K14F (r06): K8's deferred, normalised post step and the next step's obs_rms.update in K14E's launch ----------------
+// An env step of the C2 rollout then takes three launches (normalise + trunk, K40R, K14F) instead of five (+ K8 + K5).
+// Per env (one wave, lanes over the state dims) the tail does what post_env<true, true> does for it (reward
+// normalisation, buffer column t, closures, kept truncation rows, boot_norm at the last step, the return tracker) from the
+// step's results in registers (EnvRowOut) and forms the env's share of the ret_rms moments and of the next observation's
+// sums around the running mean; the 4 envs of a block are added in wave order.  The block partials (P = 3 + 2D f64) are
+// reduced in two ticketed levels, both in a fixed order (any arrival order gives the same bits): the last block of each
+// group of kPostGrp blocks sums its group's partials (4 contiguous chunks, then the chunks in order), and the last group
+// to finish sums the group partials in group order, merges obs_rms (rms_merge_col) and ret_rms (ret_rms_merge), advances
+// the cursor and resets the tickets.  Every block reads the statistics and the cursor before its ticket, the final block
+// writes them after every ticket was taken (K8's protocol).
+constexpr int kPostGrp = 64;
+// tickets 256 B apart: atomics on one line serialise, and 1024 blocks' tickets on the two lines of a packed [1 + 16]
+// array cost ~10 us per launch (tools/k14f_probe.py, r06: drain + group tickets 9.6 us packed)
+constexpr int kTicketStride = 64;
+// diagnostics (tools/k14f_probe.py, xpa_k14f_probe): bit 1 = the tail ends after the block partial stores, bit 2 = after
+// the group tickets, bit 4 = after the group sums (results then invalid: timing only); 0 in production
+__device__ int g_k14f_probe = 0;
+struct PostArgs {
+    xpa_cursor_t *cur;
+    float *ret_mean, *ret_var;
+    double *ret_count;
+    float *returns, *buf_rew, *buf_term;
+    uint8_t *buf_closed;
+    float *buf_boot;
+    float gamma, rew_range, obs_clip;
+    int mask_returns, use_rewnorm, atari_lifeloss, slot_from_next, n_slots;
+    float *slot_obs;
+    int32_t *slot_t, *overflow;
+    float *obs_mean, *obs_var;
+    double *obs_count;   // nullptr: no obs_rms update (P = 3)
+    float *boot_norm;
+    int64_t ld_norm;
+    double *part;        // f64 [(blocks + groups) * P]
+    unsigned *tickets;   // [(1 + groups) * kTicketStride] (ticket i at i * kTicketStride), zero between launches
+};
+
+__device__ __forceinline__ void k14f_tail(const PostArgs &pa, int D, const EnvRowOut &eo, bool valid, int64_t n,
+                                          int64_t n_envs, int64_t T, int lane, int wave) {
+    __shared__ double s_pp[4][3 + 2 * 64];
+    __shared__ double s_ch[4][3 + 2 * 64];
+    __shared__ bool s_last;
+    const bool rms = pa.obs_count != nullptr;
+    const int P = 3 + (rms ? 2 * D : 0);
+    const int32_t t = pa.cur->ptr;
+    double cnt = 0.0, sm = 0.0, sq = 0.0, rp = 0.0, rq = 0.0;
+    if (valid) {   // wave-uniform
+        const bool last = t == (int32_t)(T - 1);
+        const int64_t cell = n * T + t;
+        const bool done = eo.te || eo.tr;
+        const bool close = last || (done && !(pa.atari_lifeloss && !eo.tr));
+        const float m = lane < D ? pa.obs_mean[lane] : 0.f, v = lane < D ? pa.obs_var[lane] : 1.f;
+        if (lane == 0) {
+            const float rstd = fminf(fmaxf(sqrtf(*pa.ret_var), 0.1f), 100.0f);
+            pa.buf_rew[cell] = pa.use_rewnorm ? fminf(fmaxf(eo.r / rstd, -pa.rew_range), pa.rew_range) : eo.r;
+            pa.buf_term[cell] = eo.te ? 1.f : 0.f;
+            pa.buf_closed[cell] = close ? 1 : 0;
+            pa.buf_boot[cell] = 0.f;   // deferred: the bootstraps are written after the rollout
+            const float R = pa.returns[n];
+            float Rk = pa.mask_returns ? (eo.te ? 0.f : pa.gamma * R) + eo.r : pa.gamma * R + eo.r;
+            if (done) {
+                cnt = 1.0;
+                sm = (double)Rk;
+                sq = (double)Rk * (double)Rk;
+                Rk = 0.f;
+            }
+            pa.returns[n] = Rk;
+        }
+        if (close && !eo.te && !last) {   // mid-buffer truncation: keep the normalised row for later
+            int k = 0;
+            if (lane == 0) {
+                while (k < pa.n_slots && pa.slot_t[(int64_t)k * n_envs + n] >= 0) ++k;
+                if (k == pa.n_slots) {   // contract broken: counted (the agent raises), the last slot is reused
+                    atomicAdd(pa.overflow, 1);
+                    k = pa.n_slots - 1;
+                }
+                pa.slot_t[(int64_t)k * n_envs + n] = t;
+            }
+            k = __shfl(k, 0, 64);
+            if (lane < D)
+                pa.slot_obs[((int64_t)k * n_envs + n) * D + lane] =
+                    obs_norm1(pa.slot_from_next ? eo.sn : eo.sv, m, v, pa.obs_clip);
+        }
+        if (last && lane < D) pa.boot_norm[n * pa.ld_norm + lane] = obs_norm1(eo.sv, m, v, pa.obs_clip);
+        if (rms && lane < D) {
+            const double dv = (double)eo.sn - (double)m;
+            rp = dv;
+            rq = dv * dv;
+        }
+    }
+    if (lane == 0) {
+        s_pp[wave][0] = cnt;
+        s_pp[wave][1] = sm;
+        s_pp[wave][2] = sq;
+    }
+    if (rms && lane < D) {
+        s_pp[wave][3 + lane] = rp;
+        s_pp[wave][3 + D + lane] = rq;
+    }
+    __syncthreads();
+    const int tid = threadIdx.x;
+    const unsigned nblk = gridDim.x, G = (nblk + kPostGrp - 1) / kPostGrp;
+    const int probe = g_k14f_probe;
+    if (tid < P)
+        xpa_store_agent(pa.part + (int64_t)blockIdx.x * P + tid, ((s_pp[0][tid] + s_pp[1][tid]) + s_pp[2][tid]) + s_pp[3][tid]);
+    if (probe & 1) return;
+    xpa_drain();
+    __syncthreads();
+    const unsigned g = blockIdx.x / kPostGrp, g0 = g * kPostGrp;
+    const int gn = (int)min((unsigned)kPostGrp, nblk - g0);
+    if (tid == 0) s_last = xpa_ticket(pa.tickets + kTicketStride * (1 + g)) == (unsigned)(gn - 1);
+    __syncthreads();
+    if (!s_last) return;
+    if (probe & 2) {
+        if (tid == 0) pa.tickets[kTicketStride * (1 + g)] = 0u;
+        return;
+    }
+    // the group's partials: thread (chunk j, column i) sums a contiguous run of blocks in order, then the runs in order
+    const int nch = min(4, 256 / P);
+    const int i = tid % P, j = tid / P;
+    if (j < nch) {
+        const int per = (gn + nch - 1) / nch;
+        const int lo = j * per, hi = min(gn, lo + per);
+        double acc = 0.0;
+        for (int b0 = lo; b0 < hi; b0 += 16) {
+            double x[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                x[u] = b0 + u < hi ? xpa_load_agent(pa.part + (int64_t)(g0 + b0 + u) * P + i) : 0.0;
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (b0 + u < hi) acc += x[u];
+        }
+        s_ch[j][i] = acc;
+    }
+    __syncthreads();
+    if (tid < P) {
+        double a = s_ch[0][tid];
+        for (int jj = 1; jj < nch; ++jj) a += s_ch[jj][tid];
+        xpa_store_agent(pa.part + (int64_t)(nblk + g) * P + tid, a);
+    }
+    if (tid == 0) pa.tickets[kTicketStride * (1 + g)] = 0u;   // every block of the group has taken its ticket
+    if (probe & 4) return;
+    xpa_drain();
+    __syncthreads();
+    if (tid == 0) s_last = xpa_ticket(pa.tickets) == G - 1;
+    __syncthreads();
+    if (!s_last) return;
+    // the last group: the group partials in group order
+    if (tid < P) {
+        double a = 0.0;
+        for (unsigned b0 = 0; b0 < G; b0 += 16) {
+            double x[16];
+#pragma unroll
+            for (unsigned u = 0; u < 16; ++u)
+                x[u] = b0 + u < G ? xpa_load_agent(pa.part + (int64_t)(nblk + b0 + u) * P + tid) : 0.0;
+#pragma unroll
+            for (unsigned u = 0; u < 16; ++u)
+                if (b0 + u < G) a += x[u];
+        }
+        s_ch[0][tid] = a;
+    }
+    const double c0 = rms ? *pa.obs_count : 0.0;
+    __syncthreads();
+    if (rms && tid < D) rms_merge_col(s_ch[0][3 + tid], s_ch[0][3 + D + tid], (double)n_envs, c0, pa.obs_mean, pa.obs_var, tid);
+    if (tid == 0) {
+        if (rms) *pa.obs_count = c0 + (double)n_envs;
+        ret_rms_merge(s_ch[0][0], s_ch[0][1], s_ch[0][2], pa.ret_mean, pa.ret_var, pa.ret_count);
+        pa.cur->ptr = (int32_t)((t + 1) % T);
+        pa.cur->step = pa.cur->step + 1u;
+        pa.tickets[0] = 0u;
+    }
 }
 
 // MODE: 0 Gaussian sample, 1 Categorical sample, 2 value only (v_out[n]).
@@ -510,99 +737,107 @@ __device__ __forceinline__ int64_t xcd_env(int64_t b, int wave, int64_t n_envs) 
     return 8 * G + 4 * (m & 1) + wave;
 }
 
-template <int MODE, int ACT, bool ENV = false>
+// POST (K14F, r06, with MODE 0 + ENV): k14f_tail after the env step; every wave of the block reaches it (waves past
+// n_envs skip the env body only)
+template <int MODE, int ACT, bool ENV = false, bool POST = false>
 __global__ __launch_bounds__(256) void rollout_policy_head_kernel(
     int64_t n_envs, int K, int64_t T, const float *__restrict__ za, const float *__restrict__ zc, int64_t ld,
     float slope, const float *__restrict__ Wa, const float *__restrict__ ba, const float *__restrict__ Wc,
-    const float *__restrict__ bc, const float *__restrict__ logstd, const xpa_cursor_t *__restrict__ cur,
+    const float *__restrict__ bc, const float *__restrict__ logstd, const xpa_cursor_t *cur,   // POST: also pa.cur
     uint32_t seed, float act_clip, float *__restrict__ buf_act, float *__restrict__ buf_logp,
     float *__restrict__ buf_val, float *__restrict__ env_in, int64_t ld_env, float *__restrict__ v_out,
-    SynthEnvArgs env) {
+    SynthEnvArgs env, PostArgs pa = PostArgs{}) {
+    static_assert(!POST || (MODE == 0 && ENV), "K14F is the Gaussian env-fused form");
     __shared__ float s_head[4][kRolloutKMax];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t n = ENV ? xcd_env(blockIdx.x, wave, n_envs) : (int64_t)blockIdx.x * 4 + wave;
-    if (n >= n_envs) return;  // wave-uniform
-    // ENV: the env's state row, counters and the first kPreW rows of [W | U]^T are loaded first, so their
-    // latency hides under the head arithmetic
-    constexpr int kPreW = 24;
-    float xs = 0.f, wreg[ENV ? kPreW : 1];
-    int e_t = 0;
-    uint32_t e_ep = 0u;
-    float e_score = 0.f;
-    int dl = 0;
-    if constexpr (ENV) {
-        dl = lane < env.D ? lane : 0;
-        xs = lane < env.D ? env.state[n * env.ld_state + lane] : 0.f;
-        e_t = env.ep_step[n];
-        e_ep = env.ep_index[n];
-        e_score = env.ep_score[n];
+    const bool valid = n < n_envs;
+    if (!POST && !valid) return;  // wave-uniform
+    EnvRowOut eo{0.f, 0.f, 0.f, false, false};
+    if (valid) {
+        // ENV: the env's state row, counters and the first kPreW rows of [W | U]^T are loaded first, so their
+        // latency hides under the head arithmetic
+        constexpr int kPreW = 24;
+        float xs = 0.f, wreg[ENV ? kPreW : 1];
+        int e_t = 0;
+        uint32_t e_ep = 0u;
+        float e_score = 0.f;
+        int dl = 0;
+        if constexpr (ENV) {
+            dl = lane < env.D ? lane : 0;
+            xs = lane < env.D ? env.state[n * env.ld_state + lane] : 0.f;
+            e_t = env.ep_step[n];
+            e_ep = env.ep_index[n];
+            e_score = env.ep_score[n];
 #pragma unroll
-        for (int j = 0; j < kPreW; ++j) {  // unconditional loads (clamped row): no branch + wait per element
-            const int jj = j < env.D + K ? j : env.D + K - 1;
-            wreg[j] = env.wt[jj * env.D + dl];
-        }
-    }
-    const float4 hc = xpa_act4<ACT>(*reinterpret_cast<const float4 *>(zc + n * ld + 4 * lane), slope);
-    const float v = wave_allsum_f(xpa_dot4(hc, *reinterpret_cast<const float4 *>(Wc + 4 * lane))) + bc[0];
-    if (MODE == 2) {
-        if (lane == 0) v_out[n] = v;
-        return;
-    }
-    const float4 h = xpa_act4<ACT>(*reinterpret_cast<const float4 *>(za + n * ld + 4 * lane), slope);
-    float mine = 0.f;  // lane o keeps head[o]
-    for (int o = 0; o < K; ++o) {
-        const float p = wave_allsum_f(xpa_dot4(h, *reinterpret_cast<const float4 *>(Wa + o * 256 + 4 * lane))) + ba[o];
-        if (lane == o) mine = p;
-        if (MODE == 1 && lane == 0) s_head[wave][o] = p;
-    }
-    if (MODE == 1) {
-        if (lane == 0) cat_sample_store(n, K, T, s_head[wave], v, cur, seed, buf_act, buf_logp, buf_val, env_in, ld_env);
-        return;
-    }
-    // Gaussian: lane a draws dimension a (the K3 arithmetic); lane 0 adds the log-prob terms in
-    // dimension order, so the sum is bitwise K3's sequential one.
-    const int64_t cell = n * T + cur->ptr;
-    float term_a = 0.f, xclip = 0.f;
-    if (lane < K) {
-        const int a = lane;
-        const uint32_t step = cur->step;
-        const uint32_t h1 = xpa_hash4(seed ^ kSaltAct, step, (uint32_t)n, (uint32_t)(2 * a));
-        const uint32_t h2 = xpa_hash4(seed ^ kSaltAct, step, (uint32_t)n, (uint32_t)(2 * a + 1));
-        const float u1 = 1.0f - xpa_u01(h1);
-        const float u2 = xpa_u01(h2);
-        const float eps = sqrtf(-2.0f * logf(u1)) * cosf(6.28318530717958647692f * u2);
-        const float sc = expf(logstd[a]);
-        const float x = mine + sc * eps;
-        const float diff = x - mine;
-        term_a = -(diff * diff) / (2.0f * sc * sc) - logf(sc) - 0.91893853320467274178f;
-        buf_act[cell * K + a] = x;
-        xclip = fminf(fmaxf(x, -act_clip), act_clip);
-        env_in[n * ld_env + a] = xclip;
-    }
-    float logp = 0.f;
-    for (int a = 0; a < K; ++a) logp += __shfl(term_a, a, 64);
-    if (lane == 0) {
-        buf_logp[cell] = logp;
-        buf_val[cell] = v;
-    }
-    if constexpr (ENV) {
-        // pre = [W | U] (s | clip(a)) for state dim `lane`: one fmaf chain over j < D + K in order
-        const int D = env.D, J = D + K;
-        float pre = 0.f;
-#pragma unroll
-        for (int j = 0; j < kPreW; ++j) {
-            if (j < J) {  // uniform
-                const float v = __shfl(j < D ? xs : xclip, j < D ? j : j - D, 64);
-                if (lane < D) pre = fmaf(v, wreg[j], pre);
+            for (int j = 0; j < kPreW; ++j) {  // unconditional loads (clamped row): no branch + wait per element
+                const int jj = j < env.D + K ? j : env.D + K - 1;
+                wreg[j] = env.wt[jj * env.D + dl];
             }
         }
-        for (int j = kPreW; j < J; ++j) {
-            const float v = __shfl(j < D ? xs : xclip, j < D ? j : j - D, 64);
-            const float w = env.wt[j * D + dl];
-            if (lane < D) pre = fmaf(v, w, pre);
+        const float4 hc = xpa_act4<ACT>(*reinterpret_cast<const float4 *>(zc + n * ld + 4 * lane), slope);
+        const float v = wave_allsum_f(xpa_dot4(hc, *reinterpret_cast<const float4 *>(Wc + 4 * lane))) + bc[0];
+        if (MODE == 2) {
+            if (lane == 0) v_out[n] = v;
+            return;
         }
-        synthbox_env_row(n, lane, env, [&](int) { return pre; }, e_t, e_ep, e_score);
+        const float4 h = xpa_act4<ACT>(*reinterpret_cast<const float4 *>(za + n * ld + 4 * lane), slope);
+        float mine = 0.f;  // lane o keeps head[o]
+        for (int o = 0; o < K; ++o) {
+            const float p = wave_allsum_f(xpa_dot4(h, *reinterpret_cast<const float4 *>(Wa + o * 256 + 4 * lane))) + ba[o];
+            if (lane == o) mine = p;
+            if (MODE == 1 && lane == 0) s_head[wave][o] = p;
+        }
+        if (MODE == 1) {
+            if (lane == 0) cat_sample_store(n, K, T, s_head[wave], v, cur, seed, buf_act, buf_logp, buf_val, env_in, ld_env);
+            return;
+        }
+        // Gaussian: lane a draws dimension a (the K3 arithmetic); lane 0 adds the log-prob terms in
+        // dimension order, so the sum is bitwise K3's sequential one.
+        const int64_t cell = n * T + cur->ptr;
+        float term_a = 0.f, xclip = 0.f;
+        if (lane < K) {
+            const int a = lane;
+            const uint32_t step = cur->step;
+            const uint32_t h1 = xpa_hash4(seed ^ kSaltAct, step, (uint32_t)n, (uint32_t)(2 * a));
+            const uint32_t h2 = xpa_hash4(seed ^ kSaltAct, step, (uint32_t)n, (uint32_t)(2 * a + 1));
+            const float u1 = 1.0f - xpa_u01(h1);
+            const float u2 = xpa_u01(h2);
+            const float eps = sqrtf(-2.0f * logf(u1)) * cosf(6.28318530717958647692f * u2);
+            const float sc = expf(logstd[a]);
+            const float x = mine + sc * eps;
+            const float diff = x - mine;
+            term_a = -(diff * diff) / (2.0f * sc * sc) - logf(sc) - 0.91893853320467274178f;
+            buf_act[cell * K + a] = x;
+            xclip = fminf(fmaxf(x, -act_clip), act_clip);
+            env_in[n * ld_env + a] = xclip;
+        }
+        float logp = 0.f;
+        for (int a = 0; a < K; ++a) logp += __shfl(term_a, a, 64);
+        if (lane == 0) {
+            buf_logp[cell] = logp;
+            buf_val[cell] = v;
+        }
+        if constexpr (ENV) {
+            // pre = [W | U] (s | clip(a)) for state dim `lane`: one fmaf chain over j < D + K in order
+            const int D = env.D, J = D + K;
+            float pre = 0.f;
+#pragma unroll
+            for (int j = 0; j < kPreW; ++j) {
+                if (j < J) {  // uniform
+                    const float v = __shfl(j < D ? xs : xclip, j < D ? j : j - D, 64);
+                    if (lane < D) pre = fmaf(v, wreg[j], pre);
+                }
+            }
+            for (int j = kPreW; j < J; ++j) {
+                const float v = __shfl(j < D ? xs : xclip, j < D ? j : j - D, 64);
+                const float w = env.wt[j * D + dl];
+                if (lane < D) pre = fmaf(v, w, pre);
+            }
+            eo = synthbox_env_row(n, lane, env, [&](int) { return pre; }, e_t, e_ep, e_score);
+        }
     }
+    if constexpr (POST) k14f_tail(pa, env.D, eo, valid, n, n_envs, T, lane, wave);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -633,11 +868,6 @@ constexpr int kPostThreads = 256;
 // running statistics (obs_normalize_kernel's exact arithmetic) where it keeps a truncation row, and at the
 // rollout's last step writes every env's normalised final observation into boot_norm — the second
 // normalise launch of each env step is folded in here.
-__device__ __forceinline__ float obs_norm1(float x, float m, float v, float clip) {
-    const float sd = sqrtf(v);
-    const float y = (x - m) / (sd + 1e-8f);
-    return fminf(fmaxf(y, -clip), clip);
-}
 
 // K8's per-env body (shared with K32): reward normalisation, buffer column t, closures / kept truncation rows,
 // the return tracker (R in, the new running return out); (cnt, sum, sumsq) = the env's contribution to ret_rms's
@@ -687,31 +917,6 @@ __device__ __forceinline__ float post_env(
     return Rk;  // the env's running return
 }
 
-// ret_rms.update_from_moments (statistic_tools.py:86-112) from the summed (count, sum, sumsq) of the closed paths.
-__device__ __forceinline__ void ret_rms_merge_local(double c, double s1, double s2, float &m, float &v, double &cnt) {
-    if (c > 0.0) {
-        const double bm = s1 / c;
-        const double bvar = fmax(s2 / c - bm * bm, 0.0);
-        const double c0 = cnt, m0 = (double)m, v0 = (double)v;
-        const double tot = c0 + c;
-        const double delta = bm - m0;
-        m = (float)(m0 + delta * c / tot);
-        v = (float)((v0 * c0 + bvar * c + delta * delta * c0 * c / tot) / tot);
-        cnt = tot;
-    }
-}
-
-__device__ __forceinline__ void ret_rms_merge(double c, double s1, double s2, float *ret_mean, float *ret_var,
-                                              double *ret_count) {
-    if (c > 0.0) {
-        float m = *ret_mean, v = *ret_var;
-        double cnt = *ret_count;
-        ret_rms_merge_local(c, s1, s2, m, v, cnt);
-        *ret_mean = m;
-        *ret_var = v;
-        *ret_count = cnt;
-    }
-}
 
 // RMS (r05): the NEXT step's obs_rms.update folded in — each block also sums (x - mean) and its square over its envs'
 // rows of the observation the env step just produced (f64; the block's 4 waves' sums in order), in
@@ -1555,6 +1760,69 @@ XPA_API int xpa_rollout_policy_head_synthbox(int act, int64_t n_envs, int64_t ac
     else if (act == 1) XPA_K14E(1);
     else XPA_K14E(2);
 #undef XPA_K14E
+    return xpa_launch_status();
+}
+
+// ---- K14F (r06) ------------------------------------------------------------------------------------
+XPA_API int xpa_k14f_probe(int bits) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_k14f_probe), &bits, sizeof(int));
+}
+
+// Workspace of xpa_rollout_step_synthbox: f64 partials (returned, in doubles) and *n_tickets int32 tickets (zeroed once
+// by the caller; every launch leaves them zero).  rms: with the obs_rms update.
+XPA_API int64_t xpa_rollout_step_workspace(int64_t n_envs, int64_t obs_dim, int rms, int64_t *n_tickets) {
+    if (n_envs <= 0 || obs_dim < 1 || obs_dim > 64 || !n_tickets) return -1;
+    const int64_t blocks = (n_envs + 3) / 4, groups = (blocks + kPostGrp - 1) / kPostGrp;
+    *n_tickets = (1 + groups) * kTicketStride;
+    return (blocks + groups) * (3 + (rms ? 2 * obs_dim : 0));
+}
+
+// xpa_rollout_policy_head_synthbox and K8's deferred + normalised post step (xpa_rollout_post_deferred_norm, with
+// obs_count non-null also the next step's obs_rms.update: xpa_rollout_post_deferred_norm_rms) in ONE launch (K14F).
+// The post arguments mean what they mean there; slot_from_next (A2C's boot_from_reset): kept truncation rows are the
+// env's next observation instead of its final one; part / tickets: xpa_rollout_step_workspace.
+XPA_API int xpa_rollout_step_synthbox(
+    int act, int64_t n_envs, int64_t act_dim, int64_t horizon, int64_t hidden, int64_t ld, const float *z_actor,
+    const float *z_critic, float slope, const float *w_actor, const float *b_actor, const float *w_critic,
+    const float *b_critic, const float *logstd, xpa_cursor_t *cursor, uint32_t seed, float act_clip, float *buf_act,
+    float *buf_logp, float *buf_val, int64_t obs_dim, const float *wcat_t, uint32_t env_seed, int32_t max_episode_steps,
+    float noise, float term_thresh, float reset_scale, float *state, int64_t ld_state, float *final_obs, float *rew,
+    uint8_t *term, uint8_t *trunc, int32_t *ep_step, uint32_t *ep_index, float *ep_score, float *ep_last_score,
+    int32_t *ep_last_len, float *slot_obs, int32_t *slot_t, int64_t n_slots, int32_t *overflow, int slot_from_next,
+    float *obs_mean, float *obs_var, double *obs_count, float obs_clip, float *boot_norm, int64_t ld_norm,
+    float *ret_mean, float *ret_var, double *ret_count, float *returns, float *buf_rew, float *buf_term,
+    uint8_t *buf_closed, float *buf_boot, float gamma, int mask_returns, int use_rewnorm, float rew_range,
+    int atari_lifeloss, double *part, int32_t *tickets, xpa_stream_t stream) {
+    if (n_envs <= 0 || act_dim < 1 || act_dim > kRolloutKMax || horizon <= 0 || hidden != 256 || ld < 256 || ld % 4 ||
+        act < 0 || act > 2 || !z_actor || !z_critic || !w_actor || !b_actor || !w_critic || !b_critic || !cursor ||
+        !logstd || !buf_act || !buf_logp || !buf_val)
+        return (int)hipErrorInvalidValue;
+    if (((uintptr_t)z_actor | (uintptr_t)z_critic | (uintptr_t)w_actor | (uintptr_t)w_critic) % 16)
+        return (int)hipErrorInvalidValue;
+    if (obs_dim < 1 || obs_dim > 64 || !wcat_t || !state || ld_state < obs_dim + act_dim || !final_obs || !rew ||
+        !term || !trunc || !ep_step || !ep_index || !ep_score || !ep_last_score || !ep_last_len)
+        return (int)hipErrorInvalidValue;
+    if (n_slots < 1 || n_slots > horizon || !slot_obs || !slot_t || !overflow || !obs_mean || !obs_var || !boot_norm ||
+        ld_norm < obs_dim || !ret_mean || !ret_var || !ret_count || !returns || !buf_rew || !buf_term || !buf_closed ||
+        !buf_boot || !part || !tickets || (n_envs + 3) / 4 > 0x7fffffff)
+        return (int)hipErrorInvalidValue;
+    SynthEnvArgs e{(int)obs_dim, env_seed, max_episode_steps, noise, term_thresh, reset_scale, state, ld_state,
+                   final_obs, rew, term, trunc, ep_step, ep_index, ep_score, ep_last_score, ep_last_len, wcat_t};
+    PostArgs pa{cursor, ret_mean, ret_var, ret_count, returns, buf_rew, buf_term, buf_closed, buf_boot, gamma, rew_range,
+                obs_clip, mask_returns, use_rewnorm, atari_lifeloss, slot_from_next, (int)n_slots, slot_obs, slot_t,
+                overflow, obs_mean, obs_var, obs_count, boot_norm, ld_norm, part, (unsigned *)tickets};
+    float *env_in = state + obs_dim;
+    const unsigned blocks = (unsigned)((n_envs + 3) / 4);
+    hipStream_t s = (hipStream_t)stream;
+#define XPA_K14F(A_)                                                                                              \
+    hipLaunchKernelGGL((rollout_policy_head_kernel<0, A_, true, true>), dim3(blocks), dim3(256), 0, s, n_envs,     \
+                       (int)act_dim, horizon, z_actor, z_critic, ld, slope, w_actor, b_actor, w_critic, b_critic,     \
+                       logstd, cursor, seed, act_clip, buf_act, buf_logp, buf_val, env_in, ld_state, (float *)nullptr, \
+                       e, pa)
+    if (act == 0) XPA_K14F(0);
+    else if (act == 1) XPA_K14F(1);
+    else XPA_K14F(2);
+#undef XPA_K14F
     return xpa_launch_status();
 }
 

@@ -421,10 +421,11 @@ class FusedActorCritic:
 
     @torch.no_grad()
     def rollout_act(self, x, dist, cursor, seed, buf_act, buf_logp, buf_val, env_in, act_clip=1.0, norm=None,
-                    env=None):
+                    env=None, post=None):
         """Policy step of the rollout: trunk, paired hidden GEMM, then K14 (heads + sample + store).
         norm: see _rep_forward (x is then the raw observation).  env: a device SynthBox env whose step runs
-        inside the same K14 launch (ops.rollout_policy_head_synthbox; the caller skips env.step_device())."""
+        inside the same K14 launch (ops.rollout_policy_head_synthbox; the caller skips env.step_device()).
+        post (with env, r06): K8's post step in that launch too (K14F; ops.rollout_policy_head_synthbox(post=))."""
         rep_outs = self._rep_forward(x, norm=norm)
         s = rep_outs[-1] if rep_outs else x
         z = self._rollout_pair(s)
@@ -437,7 +438,7 @@ class FusedActorCritic:
         if env is not None:
             ops.rollout_policy_head_synthbox(z[:, :H], z[:, H:], (code, slope), lin_ao.weight, lin_ao.bias,
                                              lin_co.weight, lin_co.bias, self.logstd, cursor, seed, buf_act, buf_logp,
-                                             buf_val, env, act_clip)
+                                             buf_val, env, act_clip, post=post)
             return
         ops.rollout_policy_head(dist, z[:, :H], z[:, H:], (code, slope), lin_ao.weight, lin_ao.bias, lin_co.weight,
                                 lin_co.bias, self.logstd, cursor, seed, buf_act, buf_logp, buf_val, env_in, act_clip)

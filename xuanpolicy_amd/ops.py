@@ -1266,12 +1266,57 @@ def rollout_policy_head(dist, z_actor, z_critic, act, w_actor, b_actor, w_critic
     _lib.check(rc, "xpa_rollout_policy_head")
 
 
+def rollout_step_workspace(n_envs, obs_dim, rms, device):
+    """K14F workspace (xpa_rollout_step_workspace): (partials f64, tickets int32 zeroed once; launches leave them 0)."""
+    nt = ctypes.c_int64()
+    nd = int(lib().xpa_rollout_step_workspace(int(n_envs), int(obs_dim), int(bool(rms)), ctypes.byref(nt)))
+    if nd <= 0:
+        raise ValueError("K14F needs 1 <= obs_dim <= 64")
+    return (torch.empty(nd, dtype=torch.float64, device=device), torch.zeros(nt.value, dtype=torch.int32, device=device))
+
+
+def _rollout_step_post(post, N, T, D, device):
+    """The post-step argument tail of xpa_rollout_step_synthbox from `post` (a dict, see rollout_policy_head_synthbox)."""
+    p = dict(post)
+    S = _n_slots(p["slot_t"], N)
+    _req(p["slot_obs"], "slot_obs", torch.float32, (S * N, D))
+    _req(p["overflow"], "overflow", torch.int32, (1,))
+    _req(p["obs_mean"], "obs_mean", torch.float32, (D,))
+    _req(p["obs_var"], "obs_var", torch.float32, (D,))
+    if p.get("obs_count") is not None:
+        _req(p["obs_count"], "obs_count", torch.float64, (1,))
+    ldn = _row_stride(p["boot_norm"], "boot_norm", D)
+    for name in ("ret_mean", "ret_var"):
+        _req(p[name], name, torch.float32, (1,))
+    _req(p["ret_count"], "ret_count", torch.float64, (1,))
+    _req(p["returns"], "returns", torch.float32, (N,))
+    for name in ("buf_rew", "buf_term", "buf_boot"):
+        _req(p[name], name, torch.float32, (N, T))
+    _req(p["buf_closed"], "buf_closed", torch.uint8, (N, T))
+    part, tickets = p["workspace"]
+    nt = ctypes.c_int64()
+    nd = int(lib().xpa_rollout_step_workspace(N, D, int(p.get("obs_count") is not None), ctypes.byref(nt)))
+    _req(part, "part", torch.float64, (nd,))
+    _req(tickets, "tickets", torch.int32, (nt.value,))
+    return [_p(p["slot_obs"]), _p(p["slot_t"]), S, _p(p["overflow"]), int(bool(p.get("slot_from_next", False))),
+            _p(p["obs_mean"]), _p(p["obs_var"]), _p(p.get("obs_count")), float(p["obs_clip"]), _p(p["boot_norm"]), ldn,
+            _p(p["ret_mean"]), _p(p["ret_var"]), _p(p["ret_count"]), _p(p["returns"]), _p(p["buf_rew"]),
+            _p(p["buf_term"]), _p(p["buf_closed"]), _p(p["buf_boot"]), float(p["gamma"]),
+            int(bool(p.get("mask_returns", True))), int(bool(p.get("use_rewnorm", True))), float(p.get("rew_range", 5.0)),
+            int(bool(p.get("atari_lifeloss", False))), _p(part), _p(tickets)]
+
+
 def rollout_policy_head_synthbox(z_actor, z_critic, act, w_actor, b_actor, w_critic, b_critic, logstd, cursor, seed,
-                                 buf_act, buf_logp, buf_val, env, act_clip=1.0):
+                                 buf_act, buf_logp, buf_val, env, act_clip=1.0, post=None):
     """K14 (Gaussian) + the SynthBox env step of envs.SynthBoxVecEnv `env` in one launch
     (xpa_rollout_policy_head_synthbox): same buffers as rollout_policy_head, then the env's state, final
     obs, reward, flags and episode counters exactly as env.step_device() after K14 would write them (the
-    env pre-activation as a fixed-order chain instead of the GEMM: ulp-level differences)."""
+    env pre-activation as a fixed-order chain instead of the GEMM: ulp-level differences).
+    post (r06, K14F: xpa_rollout_step_synthbox): also K8's deferred, normalised post step in the same launch — a dict of
+    rollout_post's deferred-norm arguments (slot_obs, slot_t, overflow, obs_mean, obs_var, obs_clip, boot_norm, ret_mean,
+    ret_var, ret_count, returns, buf_rew, buf_term, buf_closed, buf_boot, gamma, mask_returns, use_rewnorm, rew_range,
+    atari_lifeloss), slot_from_next (A2C: kept rows from the next observation), obs_count (or None: with it the next
+    step's obs_rms.update as rollout_post(rms=...)), workspace = rollout_step_workspace(N, D, obs_count is not None)."""
     N, H = z_actor.shape
     ld = z_actor.stride(0)
     for name, z in (("z_actor", z_actor), ("z_critic", z_critic)):
@@ -1288,6 +1333,16 @@ def rollout_policy_head_synthbox(z_actor, z_critic, act, w_actor, b_actor, w_cri
     if env.num_envs != N or env.A != A or env.discrete:
         raise ValueError("the fused env step needs a continuous-action env of matching shape")
     from .envs import NOISE, TERM_THRESH, RESET_SCALE
+    if post is not None:
+        rc = lib().xpa_rollout_step_synthbox(
+            act[0], N, A, T, H, ld, _p(z_actor), _p(z_critic), float(act[1]), _p(w_actor), _p(b_actor), _p(w_critic),
+            _p(b_critic), _p(logstd), _p(cursor), int(seed) & 0xFFFFFFFF, float(act_clip), _p(buf_act), _p(buf_logp),
+            _p(buf_val), env.D, _p(env.Wcat_t), env.noise_seed, env.max_episode_steps, NOISE, TERM_THRESH,
+            RESET_SCALE, _p(env.X), env.X.stride(0), _p(env.final_obs), _p(env.rew), _p(env.term), _p(env.trunc),
+            _p(env.ep_step), _p(env.ep_index), _p(env.ep_score), _p(env.ep_last_score), _p(env.ep_last_len),
+            *_rollout_step_post(post, N, T, env.D, z_actor.device), _stream(z_actor.device))
+        _lib.check(rc, "xpa_rollout_step_synthbox")
+        return
     rc = lib().xpa_rollout_policy_head_synthbox(
         act[0], N, A, T, H, ld, _p(z_actor), _p(z_critic), float(act[1]), _p(w_actor), _p(b_actor), _p(w_critic),
         _p(b_critic), _p(logstd), _p(cursor), int(seed) & 0xFFFFFFFF, float(act_clip), _p(buf_act), _p(buf_logp),
