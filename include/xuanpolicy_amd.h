@@ -35,7 +35,11 @@ typedef struct ihipStream_t *xpa_stream_t; /* == hipStream_t */
  * NULL: final_obs as before); XpaSmallRolloutArgs gains slot_reset_obs (the same choice for K32); xpa_rollout_post
  * takes v_boot_mid after v_boot (nullable: the bootstrap values of closures before the rollout's last step, A2C's
  * V(norm(reset_obs)); the last step's closures use v_boot). */
-#define XPA_ABI_VERSION 3
+/* ABI 4 (round 6): the batched column-sum finalizes that take a ticket (xpa_colsum_finalize_batch_sq / _sq_loss / _map)
+ * need int32 [XPA_COLSUM_TICKET_INTS] there, zero-initialised and left at zero (two ticket levels on separate lines:
+ * ~300 blocks counting on one int serialised their atomics). */
+#define XPA_ABI_VERSION 4
+#define XPA_COLSUM_TICKET_INTS 4096
 
 /* Device-resident rollout cursor read by the per-step kernels, so a captured step replays
  * without host-side arguments changing: ptr = buffer column being written (DummyOnPolicyBuffer.ptr,
@@ -429,8 +433,8 @@ int xpa_colsum_finalize_batch(int n_segs, const float *const *partials, const in
 int64_t xpa_colsum_batch_tiles(int n_segs, const int64_t *n_partials, const int64_t *cols);
 /* xpa_colsum_finalize_batch that also produces the clip norm of its outputs: sq (nullable; tiles + 2
  * doubles) holds at sq[0] a share written beforehand (e.g. xpa_policy_loss_finalize_sq's d logstd); each
- * tile writes its sum of squared outputs to sq[1 + tile], and the last block to finish (atomic ticket,
- * int32 [1], zero-initialised and left at zero) writes the fixed-order total of sq[0 .. tiles] to
+ * tile writes its sum of squared outputs to sq[1 + tile], and the last block to finish (atomic tickets,
+ * int32 [XPA_COLSUM_TICKET_INTS], zero-initialised and left at zero) writes the fixed-order total of sq[0 .. tiles] to
  * sq[1 + tiles] — the single partial xpa_clip_adam_step_partials then reads. */
 int xpa_colsum_finalize_batch_sq(int n_segs, const float *const *partials, const int64_t *n_partials,
                                  const int64_t *cols, float *const *outs, double *sq, int32_t *ticket,

@@ -20,7 +20,8 @@ SOURCES = ["gae.hip", "loss.hip", "rollout.hip", "optim.hip", "mlp.hip", "head.h
            "classic.hip", "dqn.hip", "conv.hip", "igemm.hip", "smallmlp.hip", "sgemm3.hip"]
 HEADER = os.path.join(REPO_DIR, "include", "xuanpolicy_amd.h")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
+COLSUM_TICKET_INTS = 4096   # include/xuanpolicy_amd.h XPA_COLSUM_TICKET_INTS (ABI 4)
 
 c_i32, c_i64, c_u32, c_f32, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
 

@@ -309,6 +309,9 @@ __global__ __launch_bounds__(kColTile * kColGroups) void colsum_finalize_kernel(
 }
 
 constexpr int kMaxSegs = 16;
+// the batched finalize's ticket buffer (ABI 4): int32 [kColTicketStride (1 + kColTicketGroups)] = XPA_COLSUM_TICKET_INTS
+constexpr unsigned kColTicketStride = 64, kColTicketGroups = 63;
+static_assert(kColTicketStride * (1 + kColTicketGroups) == XPA_COLSUM_TICKET_INTS, "ticket buffer size (ABI 4)");
 // Segments with few partial rows (G <= kWideMaxG, e.g. the split-K slices of a weight gradient: G = 8,
 // C = 131 072) use 1024-column tiles, one column per thread summed over G in order; the others 64-column
 // tiles with 16 row groups (colsum_tile).
@@ -449,7 +452,21 @@ __global__ __launch_bounds__(kColTile * kColGroups) void colsum_finalize_batch_k
     if (!b.sq) return;
     xpa_drain();  // this block's partial (sc1 store) complete before its ticket
     __syncthreads();
-    if (threadIdx.x == 0) s_last = xpa_ticket(b.ticket) == gridDim.x - 1;
+    // r06 (ABI 4): two ticket levels on separate 256-B lines — the blocks of group g (kColTicketGroups groups of
+    // contiguous blocks) count on ticket[kColTicketStride (1 + g)], each group's last block on ticket[0]: one counter for
+    // all ~300 tiles of a C2 update serialised their atomics on one line (K14F measured ~19 ns per atomic per line)
+    if (threadIdx.x == 0) {
+        const unsigned nb = gridDim.x;
+        const unsigned gs = (nb + kColTicketGroups - 1) / kColTicketGroups, ng = (nb + gs - 1) / gs;
+        const unsigned g = blockIdx.x / gs, gn = min(gs, nb - g * gs);
+        unsigned *gt = b.ticket + kColTicketStride * (1 + g);
+        bool last = xpa_ticket(gt) == gn - 1;
+        if (last) {
+            *gt = 0u;   // every block of the group has taken its ticket
+            last = xpa_ticket(b.ticket) == ng - 1;
+        }
+        s_last = last;
+    }
     __syncthreads();
     if (!s_last) return;
     const int n = (int)gridDim.x + (b.has_loss ? 0 : 1);  // sq[0 .. tiles]

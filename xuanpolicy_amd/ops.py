@@ -930,7 +930,7 @@ class ColsumQueue:
             loss = None
         if one:
             if self._ticket is None:
-                self._ticket = torch.zeros((1,), dtype=torch.int32, device=dev)
+                self._ticket = torch.zeros((_lib.COLSUM_TICKET_INTS,), dtype=torch.int32, device=dev)
             n, _keep, args, tiles, tmap = plan[0]
             if tmap is not None:
                 la = loss if loss is not None else (0, 0, 0, 0, None, 0.0, 0.0, None, None)
