@@ -24,6 +24,10 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md; the 2:1-sparsity figure is not used)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # dense f32-input MFMA (= f32 vector rate; no xf32 on gfx950), same table
+# r06 (tools/clock_probe.hip, profiles/r06/clock/): the clock a dense v_mfma_f32_32x32x16_bf16 loop on random data holds
+# (in-kernel s_memtime / s_memrealtime, known-cycle and GRBM_GUI_ACTIVE methods agree on >= 20 ms dispatches) against the
+# 2.4 GHz the peak assumes; reported beside `frac` as the bf16 peak the split kernels can reach on this part
+BF16_MFMA_LOOP_CLOCK_GHZ, PEAK_CLOCK_GHZ = 1.86, 2.4
 
 
 def parse():
@@ -1114,7 +1118,10 @@ def main():
             # achieved / frac: SURVEY.md §8(d)'s algorithmic bytes (20 B per (env, step) + the bootstraps) over the
             # launch's duration, as the bench contract defines them; the value-fused launch also reads the critic's
             # hidden pre-activations (its extra bytes are reported beside, as launch_bytes_*)
-            traffic, traffic_note = (None, "skipped (--no-pmc)") if args.no_pmc else live_gae_traffic(form)
+            # the PMC child passes run at N = 1 only (at world > 1 the other ranks would wait on rank 0's children)
+            traffic, traffic_note = ((None, "skipped (--no-pmc)") if args.no_pmc else
+                                     (None, "skipped (world > 1: measured at N = 1)") if world > 1 else
+                                     live_gae_traffic(form))
             rp_us, rp_list, rp_note = (None, None, "skipped") if args.no_rocprof or world > 1 else \
                 live_gae_rocprof(args)
             # the other GAE form's in-loop launch under the profiler (split: the compact scan alone, exactly the §8(d)
@@ -1235,6 +1242,7 @@ def main():
                                        "unit": "TFLOP/s", "frac": h["frac"]}
                 h.update({"flops": 6 * fl, "achieved": round(6 * fl / heads_ms / 1e9, 1), "peak": BF16_MFMA_PEAK_TFLOPS,
                           "frac": round(6 * fl / heads_ms / 1e9 / BF16_MFMA_PEAK_TFLOPS, 4)})
+                h["frac_at_measured_bf16_clock"] = round(h["frac"] * PEAK_CLOCK_GHZ / BF16_MFMA_LOOP_CLOCK_GHZ, 4)
         elif heads_ms:
             hb = heads_bytes(B, args.act_dim, args.hidden)
             update_kernels["heads"] = {
@@ -1256,7 +1264,11 @@ def main():
                         "at the dense bf16 peak, vs the measured update (phase events incl. the iteration's one GAE "
                         "launch, / updates per iteration)" % ("6 actor + 3 critic" if per_bwd < 6 else "6"),
                 "bf16_mfma_gflop": round(bf / 1e9, 2), "floor_us": round(bf / BF16_MFMA_PEAK_TFLOPS / 1e6, 2),
-                "measured_us": round(upd_us, 2), "frac": round(bf / BF16_MFMA_PEAK_TFLOPS / 1e6 / upd_us, 4)}
+                "measured_us": round(upd_us, 2), "frac": round(bf / BF16_MFMA_PEAK_TFLOPS / 1e6 / upd_us, 4),
+                "frac_at_measured_bf16_clock": round(bf / BF16_MFMA_PEAK_TFLOPS / 1e6 / upd_us * PEAK_CLOCK_GHZ
+                                                     / BF16_MFMA_LOOP_CLOCK_GHZ, 4),
+                "clock_note": "a dense bf16 MFMA loop holds %.2f GHz on this part (tools/clock_probe.hip), not %.1f"
+                              % (BF16_MFMA_LOOP_CLOCK_GHZ, PEAK_CLOCK_GHZ)}
         if gemm_ms:
             fl = pair_gemm_flops(B, args.hidden, args.hidden)
             update_kernels["gemm_pair"] = {
