@@ -550,22 +550,20 @@ struct HeadEpi {
     __device__ __forceinline__ void p2_quad(const float *s_h, float (*s_dh)[KP], int64_t tile, int r0, int nr,
                                             float *__restrict__ dz, int64_t ld, const float *__restrict__ W) {
         const int w = e >> 6, l = e & 63;
-        float4 wq[KMAX];   // output o's weights of columns 4 l .. 4 l + 3 (rows o >= K: 0)
-#pragma unroll
-        for (int o = 0; o < KMAX; ++o) {
-            const float4 v = *reinterpret_cast<const float4 *>(W + (o < K ? o : 0) * kH + 4 * l);
-            wq[o] = o < K ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        // wc2[j][o2] = (w[2 o2][4 l + j], w[2 o2 + 1][4 l + j]), loaded straight into place; rows o >= K re-read row 0
+        // (finite) and their d head is 0 (loss() zeroes s_dh[.][o >= K]), so they add 0 to every chain.  r06: no select on
+        // o < K — with one, hipcc put each row's load under a uniform branch with its own vmcnt(0) (KMAX serial L2 round
+        // trips per tile); and no float4 staging array beside wc2 (its 4 KMAX registers made the kernel spill)
         f2v wc2[4][KH2];
 #pragma unroll
-        for (int o2 = 0; o2 < KH2; ++o2) {
-            const float4 a = wq[2 * o2];
-            const float4 b = 2 * o2 + 1 < KMAX ? wq[2 * o2 + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
-            wc2[0][o2] = f2v{a.x, b.x};
-            wc2[1][o2] = f2v{a.y, b.y};
-            wc2[2][o2] = f2v{a.z, b.z};
-            wc2[3][o2] = f2v{a.w, b.w};
-        }
+        for (int o2 = 0; o2 < KH2; ++o2)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int oa = 2 * o2, ob = 2 * o2 + 1;
+                const float a = W[(oa < K ? oa : 0) * kH + 4 * l + j];
+                const float b = ob < KMAX ? W[(ob < K ? ob : 0) * kH + 4 * l + j] : 0.f;
+                wc2[j][o2] = f2v{a, b};
+            }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
 #pragma unroll
@@ -1153,8 +1151,12 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
     constexpr int kStatsOff = kDhOff + kTile * Epi::KP;
     constexpr int kStatsEnd = kStatsOff + (Epi::kStatN > 4 ? Epi::kStatN : 4);
     static_assert(KMAX <= 8 || kStatsEnd * 4 <= 81920, "wide heads: 2 blocks per CU");
-    constexpr int kLdsFloats = S3 == 3 && kREnd / 4 > kStatsEnd ? kREnd / 4 : kStatsEnd;
-    static_assert(kLdsFloats * 4 <= 81920, "K16R: 2 blocks per CU");
+    constexpr int kLdsBase = S3 == 3 && kREnd / 4 > kStatsEnd ? kREnd / 4 : kStatsEnd;
+    // K16Q (r06): the hidden bias staged once per launch past everything else (the h conversion's bias reads, 4 per
+    // lane and tile, were serial L2 round trips after the k loop)
+    static_assert(kLdsBase * 4 <= 81920, "2 blocks per CU");
+    constexpr bool kBhLds = S3 == 4 && (kLdsBase + kH) * 4 <= 81920;   // the widest heads have no 1 KiB to spare
+    constexpr int kBhOff = kLdsBase, kLdsFloats = kLdsBase + (kBhLds ? kH : 0);
     __shared__ __attribute__((aligned(16))) float lds[kLdsFloats];
     float *smem = lds;
     auto s_part = reinterpret_cast<float(*)[kTile][Epi::PH]>(lds + kPartOff);
@@ -1175,6 +1177,7 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
     epi.mask_out = cmask;
     epi.dv_out = cdv;
     epi.dz_on = dz != nullptr;
+    if constexpr (kBhLds) lds[kBhOff + t] = bh[t];   // kH == 256 == blockDim.x
     __syncthreads();
     epi.init_b(s_stats);
     const float bh0 = bh[wave * 64 + (lane & 31)], bh1 = bh[wave * 64 + 32 + (lane & 31)];
@@ -1296,7 +1299,7 @@ __global__ __launch_bounds__(256, 2) void head_gemm_kernel(XPA_HEAD_KERNEL_PARAM
                 // K16Q: acc[a][b] is column block 2 a + b of the wave's 128 columns, rows of row tile wave & 1
                 const int col = S3 == 4 ? (wave >> 1) * 128 + (2 * rt + ct) * 32 + (lane & 31)
                                         : wave * 64 + ct * 32 + (lane & 31);
-                const float bc = S3 == 4 ? bh[col] : ct ? bh1 : bh0;
+                const float bc = kBhLds ? lds[kBhOff + col] : S3 == 4 ? bh[col] : ct ? bh1 : bh0;
                 const int row0 = S3 == 4 ? (wave & 1) * 32 : rt * 32;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
