@@ -180,3 +180,33 @@ def test_row_index_forms_equal_gathered(M, n_rows, d):
     torch.cuda.synchronize()
     assert torch.equal(h1, h2) and torch.equal(s1, s2)
     assert torch.equal(p1[:, :d], p2[:, :d])
+
+
+@pytest.mark.parametrize("d", [376, 100])
+def test_row_index_form_ignores_the_next_rows_values(d):
+    """r06: K40F's row-index form reads a row's padded columns d .. kp - 1 from the NEXT buffer row; those
+    columns are zeroed before the split, so a non-finite value there (inf / nan in the next observation) leaves this row's
+    outputs equal to the gathered form's — only the row that holds it goes non-finite, as in the reference."""
+    from xuanpolicy_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(d)
+    n_rows, M = 600, 512
+    kp = (d + 15) // 16 * 16
+    store = torch.zeros(n_rows * d + 128, device=DEV)
+    flat = store[:n_rows * d].view(n_rows, d)
+    flat.copy_(torch.randn(n_rows, d, device=DEV, generator=g))
+    flat[101, :16] = float("inf")     # the row after row 100
+    flat[201, :16] = float("nan")     # the row after row 200
+    idx = torch.randint(0, n_rows, (M,), device=DEV, generator=g)
+    idx[0], idx[1], idx[2] = 100, 200, 101
+    xp = torch.zeros(M, kp, device=DEV)
+    xp[:, :d] = flat[idx]
+    w = torch.randn(256, d, device=DEV, generator=g) / d ** 0.5
+    b = torch.randn(256, device=DEV, generator=g) * 0.1
+    ws = ops.s3_split_padded(w.t(), kp)
+    h1 = ops.s3_gemm_bias_act(flat, ws, kp, b, 1, 0.01, ridx=idx)
+    h2 = ops.s3_gemm_bias_act(xp, ws, kp, b, 1, 0.01)
+    torch.cuda.synchronize()
+    ok = (idx != 101) & (idx != 201)   # the rows that hold the inf / nan themselves go non-finite in both forms
+    assert torch.isfinite(h1[ok]).all(), "a row's outputs picked up the next row's non-finite values"
+    assert torch.equal(h1[ok], h2[ok])
+    assert not torch.isfinite(h1[2]).all()   # the row that holds the inf is non-finite, as in the gathered form

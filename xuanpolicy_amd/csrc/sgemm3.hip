@@ -209,14 +209,28 @@ __device__ __forceinline__ void issue_rows(unsigned st, const float *ar0, const 
     }
 }
 
+// kvalid (wave-uniform, r06): A's columns >= kvalid of this chunk are zeroed before the split — K40F's row-index form
+// reads the padded columns d .. kp - 1 of a row from the next buffer row, and 0 x a non-finite value there (the B rows
+// of those columns are zero) would make this row's outputs NaN where the reference's are finite
 template <int W, int PROBE>
-__device__ __forceinline__ void chunk(const char *st, f32x16 (&acc)[8], int lane, int wave) {
+__device__ __forceinline__ void chunk(const char *st, f32x16 (&acc)[8], int lane, int wave, int kvalid = kKC) {
     constexpr int kAImg = S3Geom<W>::kAImg;
     const int h = lane >> 5, i = lane & 31;
     const int sw = (i >> 2) & 3;
     const float *arow = reinterpret_cast<const float *>(st) + (wave * 32 + i) * kKC;
-    const float4 alo = *reinterpret_cast<const float4 *>(arow + 4 * (h ^ sw));
-    const float4 ahi = *reinterpret_cast<const float4 *>(arow + 4 * ((h + 2) ^ sw));
+    float4 alo = *reinterpret_cast<const float4 *>(arow + 4 * (h ^ sw));
+    float4 ahi = *reinterpret_cast<const float4 *>(arow + 4 * ((h + 2) ^ sw));
+    if (kvalid < kKC) {   // the LDS position h ^ sw holds the row's logical quad h (issue_rows' swizzle)
+        const int c0 = 4 * h, c1 = 4 * (h + 2);
+        alo.x = c0 < kvalid ? alo.x : 0.f;
+        alo.y = c0 + 1 < kvalid ? alo.y : 0.f;
+        alo.z = c0 + 2 < kvalid ? alo.z : 0.f;
+        alo.w = c0 + 3 < kvalid ? alo.w : 0.f;
+        ahi.x = c1 < kvalid ? ahi.x : 0.f;
+        ahi.y = c1 + 1 < kvalid ? ahi.y : 0.f;
+        ahi.z = c1 + 2 < kvalid ? ahi.z : 0.f;
+        ahi.w = c1 + 3 < kvalid ? ahi.w : 0.f;
+    }
     bf16x8 ah, am, al;
     xpa_split8(alo, ahi, ah, am, al);
     const bf16x8 *bimg = reinterpret_cast<const bf16x8 *>(st + kAImg) + lane;
@@ -333,6 +347,9 @@ __device__ __forceinline__ void s3_gemm_body(const float *__restrict__ a, int64_
         if (ch + S - 1 < nchunks && (PROBE & 2) == 0)
             issue_any(base + ((ch + S - 1) % S) * G::kStage, ch + S - 1);
         if constexpr (T64 != 0) chunk64(lds + (ch % S) * G::kStage, acc, lane, wave);
+        else if constexpr (EPI != 0)   // K40F: through ridx the row ends at column lda (the buffer's row width)
+            chunk<W, PROBE>(lds + (ch % S) * G::kStage, acc, lane, wave,
+                            ridx != nullptr && lda - (int64_t)ch * kKC < kKC ? (int)(lda - (int64_t)ch * kKC) : kKC);
         else chunk<W, PROBE>(lds + (ch % S) * G::kStage, acc, lane, wave);
     }
     // C/D map of 32x32 MFMA: row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col = lane & 31

@@ -214,8 +214,9 @@ class FusedActorCritic:
     def _wide_direct_ok(self, x, d):
         """The row-index forms apply: the flat buffer's rows are the layer width and readable, finite (zeroed) slack
         follows its last row for the padded columns (buffer.OBS_SLACK), and K41V-IDX's per-slice row count fits its LDS
-        index stage (else the pitched gather, which has no such limit).  Input contract: the rows are finite — K40F
-        reads columns d .. kp - 1 of a row from the next row, multiplied by zero weight rows."""
+        index stage (else the pitched gather, which has no such limit).  K40F reads columns d .. kp - 1 of a row from
+        the next row and zeroes them before the split (r06), so a non-finite next row does not reach this row's outputs
+        (tests/test_gpu_wide_trunk.py::test_row_index_form_ignores_the_next_rows_values)."""
         f = x.flat
         mp = self._wide_mpad(d)
         need = max((d + 15) // 16 * 16, mp) - d
