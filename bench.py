@@ -70,6 +70,10 @@ def parse():
     p.add_argument("--pair-sa", type=int, default=0, help="K41P's actor share of 128 slices (0: the default)")
     p.add_argument("--crit-factored", choices=("on", "off"), default="on",
                    help="the critic's factored backward (K41P / K42C, r05) or its dz_critic through K41V / K42S")
+    p.add_argument("--sync-obs-rms", choices=("off", "step", "rollout"), default="off",
+                   help="world > 1: obs_rms synchronised across ranks per env step (outside the graphs) or per rollout")
+    p.add_argument("--global-advnorm", choices=("on", "off"), default="off",
+                   help="world > 1: each minibatch's advantage moments averaged across ranks (a second collective)")
     p.add_argument("--fuse-post", choices=("on", "off"), default="on",
                    help="K14F: K8's post step + the next obs_rms.update inside the env-fused K14 launch (r06)")
     p.add_argument("--fold-rms", choices=("on", "off"), default="off",
@@ -1025,9 +1029,14 @@ def main():
     if args.dz_store == "plain":
         assert ops.lib().xpa_head_store_probe(1) == 0
     N, T = args.n_envs, args.horizon
+    dp_variants = {}   # SURVEY.md §8(e)'s global-statistics variants (world > 1 only; default: per-shard statistics)
+    if args.sync_obs_rms != "off":
+        dp_variants["sync_obs_rms"] = "rollout" if args.sync_obs_rms == "rollout" else True
+    if args.global_advnorm == "on":
+        dp_variants["global_advnorm"] = True
     agent = build_synthbox_ppo(n_envs=N, n_steps=T, obs_dim=args.obs_dim, act_dim=args.act_dim, hidden=args.hidden,
                                n_epoch=args.n_epoch, n_minibatch=args.n_minibatch, seed=1, device=device,
-                               shard=rank)
+                               shard=rank, **dp_variants)
     agent.learner.enable_fast_path()  # flat params/grads, fused clip+Adam, RCCL hook when world > 1
     agent.fuse_value_gae = args.gae_form == "value"
     fm0 = agent.learner._fused_mlp()
@@ -1296,7 +1305,9 @@ def main():
                        "parallelism": ("dp1 (one env shard, no collective)" if world == 1 else
                                        "dp%d (env shards; ONE all-reduce of the flat gradient per minibatch over "
                                        "%s)" % (
-                                           world, "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()))},
+                                           world, "RCCL" if dist.get_backend() == "nccl" else dist.get_backend())),
+                       "dp_statistics": {"sync_obs_rms": args.sync_obs_rms if world > 1 else "n/a (world 1)",
+                                         "global_advnorm": args.global_advnorm if world > 1 else "n/a (world 1)"}},
             "roofline": roofline,
             "phase_split_ms": phase_ms,
             "loss_kernel": loss_kernel,

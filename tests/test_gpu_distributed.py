@@ -210,3 +210,56 @@ def test_bench_self_launch_two_ranks_one_gpu():
     assert r["data_parallel"]["allreduce"]["bytes"] > 0 and r["data_parallel"]["allreduce_time_share"] > 0
     c4 = r["c4_box376"]
     assert c4["n_gpus"] == 2 and c4["collectives_per_minibatch"] == 1.0 and c4["value"] > 0
+
+
+def _rollout_sync_worker(rank, world, port, q):
+    """sync_obs_rms = "rollout" (r06): the rollout stays graph-captured with the obs-RMS merge folded into K14F, and the
+    ranks' statistics are merged once per rollout (agents.rms_rollout_sync): identical obs_rms and parameters on every
+    rank after each rollout, with the count = start + every rank's rows."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), XPA_DIST_BACKEND="gloo")
+    import torch.distributed as dist
+    try:
+        from xuanpolicy_amd.distributed import broadcast_parameters, init_from_env
+        from xuanpolicy_amd.runner import build_synthbox_ppo
+        init_from_env()
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        N, T = 256, 16
+        agent = build_synthbox_ppo(n_envs=N, n_steps=T, n_epoch=2, n_minibatch=2, device=dev, shard=rank,
+                                   sync_obs_rms="rollout", hidden=256)
+        broadcast_parameters(agent.policy)
+        assert agent.sync_obs_rms_rollout and not agent.sync_obs_rms and agent.use_graph and agent._k14f_on()
+        c_start = float(agent.obs_count)
+        agent.train(2 * T)
+        torch.cuda.synchronize()
+        for t in (agent.obs_mean, agent.obs_var, agent.obs_count,
+                  torch.cat([p.detach().reshape(-1) for p in agent.policy.parameters()])):
+            got = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(got, t.contiguous())
+            assert torch.equal(got[0], got[1])
+        # every row merged once: the first observation, then each step's next observation, on every rank
+        assert abs(float(agent.obs_count) - (c_start + world * N * (2 * T + 1))) < 1e-3, float(agent.obs_count)
+        q.put((rank, "ok"))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_sync_obs_rms_per_rollout_two_ranks_one_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rollout_sync_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=580) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: "ok", 1: "ok"}, res

@@ -56,6 +56,31 @@ FOLD_RMS = False
 # (K14F, ops.rollout_policy_head_synthbox(post=)): a C2 env step in three launches instead of five
 FUSE_POST = True
 
+
+def rms_rollout_sync(start, end, all_reduce_sum):
+    """sync_obs_rms = "rollout" (r06): the rank's rows of a rollout recovered from its running statistics — end = start
+    (+) B, Chan's merge being associative over the per-step merges (statistic_tools.py:86-112) — as (n, sum, sum of squares)
+    in f64, SUM-reduced over the ranks, and merged into start: the statistics one RunningMeanStd over every rank's rows
+    would hold, up to the f32 rounding of the stored mean / var.  start / end = (mean f32 [D], var f32 [D], count f64 [1]);
+    returns (mean f32, var f32, count f64)."""
+    m0, v0, c0 = start[0].double(), start[1].double(), start[2].double()
+    m1, v1, c1 = end[0].double(), end[1].double(), end[2].double()
+    n = c1 - c0
+    s1 = m1 * c1 - m0 * c0                                       # the rows' sum
+    mb = s1 / n
+    m2 = v1 * c1 - v0 * c0 - (mb - m0) ** 2 * c0 * n / c1       # the rows' squared deviations about their own mean
+    red = torch.cat([n, s1, m2 + s1 * mb])                      # (n, sum, sum of squares)
+    all_reduce_sum(red)
+    D = m0.shape[0]
+    N, S1, Q = red[:1], red[1:1 + D], red[1 + D:]
+    mB = S1 / N
+    m2B = torch.clamp(Q - S1 * mB, min=0.0)
+    tot = c0 + N
+    delta = mB - m0
+    mean = m0 + delta * N / tot
+    var = (v0 * c0 + m2B + delta * delta * c0 * N / tot) / tot
+    return mean.float(), var.float(), tot
+
 class _OnPolicyAgent:
     algo = "ppo"
 
@@ -160,7 +185,13 @@ class _OnPolicyAgent:
         import torch.distributed as tdist
         if tdist.is_available() and tdist.is_initialized():
             self.world = tdist.get_world_size()
-        self.sync_obs_rms = bool(_cfg(config, "sync_obs_rms", False)) and self.world > 1 and self.use_obsnorm
+        #   sync_obs_rms = "rollout" (r06): per-rank statistics inside a rollout (graph-captured, folded into K14F), merged
+        #                   across ranks once per rollout, before the update (rms_rollout_sync)
+        sync_mode = _cfg(config, "sync_obs_rms", False)
+        dp_rms = self.world > 1 and self.use_obsnorm
+        self.sync_obs_rms_rollout = dp_rms and isinstance(sync_mode, str) and sync_mode.lower() == "rollout"
+        self.sync_obs_rms = dp_rms and bool(sync_mode) and not self.sync_obs_rms_rollout
+        self._rms_c0 = None
         self.global_advnorm = bool(_cfg(config, "global_advnorm", False)) and self.world > 1
         if self.sync_obs_rms:
             self.use_graph = False  # the per-step collective runs outside a captured graph
@@ -390,6 +421,17 @@ class _OnPolicyAgent:
         else:
             ops.rms_update(x, self.obs_mean, self.obs_var, self.obs_count, partials=self.rms_part,
                            ticket=self._rms_ticket)
+
+    def _sync_rms_rollout(self):
+        """sync_obs_rms = "rollout": every rank's rollout rows merged into the common start statistics (rms_rollout_sync,
+        one all-reduce of 2 D + 1 doubles per rollout), so every rank leaves the rollout with the same obs_rms."""
+        import torch.distributed as tdist
+        m, v, c = rms_rollout_sync(self._rms_c0, (self.obs_mean, self.obs_var, self.obs_count),
+                                   lambda t: tdist.all_reduce(t, op=tdist.ReduceOp.SUM))
+        self.obs_mean.copy_(m)
+        self.obs_var.copy_(v)
+        self.obs_count.copy_(c)
+        self._rms_c0 = None
 
     def _small_rollout(self):
         """K32's argument block (xpa_small_rollout_cartpole) when whole device env steps run as one launch: a CartPole
@@ -812,6 +854,8 @@ class _OnPolicyAgent:
         while left > 0:
             t0 = time.perf_counter()
             if self._t == 0:
+                if self.sync_obs_rms_rollout:   # the common statistics every rank starts this rollout from
+                    self._rms_c0 = (self.obs_mean.clone(), self.obs_var.clone(), self.obs_count.clone())
                 fc = self._rollout_cnn()
                 if fc is not None:
                     fc.refresh()   # outside any captured graph: the replays read the refreshed weight copy
@@ -831,6 +875,8 @@ class _OnPolicyAgent:
             t1 = time.perf_counter()
             self.timers["rollout"] += t1 - t0
             if self._t == self.n_steps:
+                if self.sync_obs_rms_rollout and self._rms_c0 is not None:
+                    self._sync_rms_rollout()
                 if self.phase_events is not None:   # measurement hook (bench.py): rollout | update split
                     self.phase_events.append(("rollout_end", torch.cuda.Event(enable_timing=True)))
                     self.phase_events[-1][1].record()
