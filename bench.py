@@ -51,9 +51,11 @@ def parse():
     p.add_argument("--no-c4", action="store_true", help="skip the C4 Box(376,17) measurement")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
-    p.add_argument("--gae-form", choices=("value", "split"), default="value",
-                   help="value: the deferred bootstraps' value head fused into the GAE scan (K1V, one launch); "
-                        "split: value head (K14) then the compact GAE scan (K1)")
+    p.add_argument("--gae-form", choices=("k40v", "value", "split"), default="value",
+                   help="k40v (r06, opt-in): the deferred bootstraps' critic to the value on the split GEMM (K40V, the value "
+                        "head in its epilogue), then the compact GAE scan (K1) on exactly the §8(d) bytes; value: the "
+                        "value head fused into the GAE scan (K1V, one launch); split: hipBLASLt + value head (K14) "
+                        "then the compact GAE scan")
     p.add_argument("--trunk-heads", choices=("on", "off"), default="off",
                    help="K16X (trunk layer inside the head GEMM launches) or r03's K13 forward + K16 (A/B)")
     p.add_argument("--gemm", choices=("f32", "split3"), default="split3",
@@ -790,7 +792,8 @@ def dp_path_bench(device, args, steps=3, warmup=2):
                                    hidden=args.hidden, n_epoch=args.n_epoch, n_minibatch=args.n_minibatch, seed=1,
                                    device=device)
         agent.learner.enable_fast_path()
-        agent.fuse_value_gae = args.gae_form == "value"
+        agent.fuse_value_gae = args.gae_form in ("k40v", "value")
+        agent.value_gemm = args.gae_form == "k40v"
         hook = None
         if hooked:
             hook = agent.learner.grad_sync = LocalGradSync(agent.learner.flat_grads)
@@ -1038,7 +1041,8 @@ def main():
                                n_epoch=args.n_epoch, n_minibatch=args.n_minibatch, seed=1, device=device,
                                shard=rank, **dp_variants)
     agent.learner.enable_fast_path()  # flat params/grads, fused clip+Adam, RCCL hook when world > 1
-    agent.fuse_value_gae = args.gae_form == "value"
+    agent.fuse_value_gae = args.gae_form in ("k40v", "value")
+    agent.value_gemm = args.gae_form == "k40v"
     fm0 = agent.learner._fused_mlp()
     if fm0 is not None:
         fm0.use_trunk_heads = args.trunk_heads == "on"
@@ -1154,7 +1158,9 @@ def main():
                 kname = "xpa_gae_scan_value: critic output layer + bootstrap fixup + GAE (gae_dpp_kernel<5, 1, %d>)" \
                     % act_code
             else:
-                kname = "xpa_gae_scan_compact (gae_dpp_kernel<5, 1>)"
+                kname = "xpa_gae_scan_compact (gae_dpp_kernel<5, 1>)" + (
+                    "; the deferred bootstrap values from K40V (xpa_s3_gemm_value) in the launch before"
+                    if args.gae_form == "k40v" else "")
             roofline = {"kernel": kname, "bound": "hbm", "achieved": round(ach, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "traffic_note": traffic_note,

@@ -1011,6 +1011,13 @@ void xpa_conv_wgrad_force_stream(int on);
  * xpa_rollout_step_workspace (f64 partials, returned in doubles; *n_tickets int32 tickets zeroed once, left zero by every
  * launch).  The partial sums are taken in a fixed order (any block arrival order gives the same bits). */
 int64_t xpa_rollout_step_workspace(int64_t n_envs, int64_t obs_dim, int rms, int64_t *n_tickets);
+/* r06, K40V: v [m] = act(a [m, k] . B + bias) . w_out + b_out[0] (act 0 identity / 1 LeakyReLU (slope) / 2 tanh; B the
+ * 256-column planes of xpa_s3_split_b; a 16-B aligned, lda % 4 == 0, k % 16 == 0): the critic from its last hidden layer's
+ * input to the value in one launch — the rollout's deferred bootstrap rows (critic(x), ppoclip_agent.py:95-101), whose
+ * values then go to the compact GAE scan (xpa_gae_scan_compact). */
+int xpa_s3_gemm_value(const float *a, int64_t lda, const void *b_split, float *v, int64_t m, int64_t k,
+                      const float *bias, int act, float slope, const float *w_out, const float *b_out,
+                      xpa_stream_t stream);
 /* Diagnostics: bits 1 / 2 / 4 end K14F's tail after the block partials / the group tickets / the group sums (results
  * then invalid: timing only; tools/k14f_probe.py); 0 = production. */
 int xpa_k14f_probe(int bits);

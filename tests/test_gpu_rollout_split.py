@@ -84,3 +84,54 @@ def test_fold_rms_matches_standalone_update(monkeypatch):
     assert torch.allclose(m1, m0, rtol=1e-6, atol=1e-7) and torch.allclose(v1, v0, rtol=1e-6, atol=1e-7)
     assert torch.allclose(o1, o0, rtol=1e-5, atol=1e-6)
     assert torch.allclose(val1, val0, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,act", [(8192, 1), (777, 1), (64, 0), (5, 2), (65536, 1)])
+def test_gemm_value_matches_f64(M, act):
+    """r06, K40V: v = act(x Wh^T + bh) . w_out + b_out in one launch (the split GEMM with the value head in its
+    epilogue) against f64, within the f32 GEMM's error carried through the output layer."""
+    from xuanpolicy_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(M + act)
+    x = torch.randn(M, 256, device=DEV, generator=g)
+    wh = torch.randn(256, 256, device=DEV, generator=g) / 16
+    bh = torch.randn(256, device=DEV, generator=g) * 0.1
+    wo = torch.randn(1, 256, device=DEV, generator=g) / 16
+    bo = torch.randn(1, device=DEV, generator=g)
+    slope = 0.01
+    v = ops.s3_gemm_value(x, ops.s3_split(wh.t()), 256, bh, act, slope, wo.view(-1), bo)
+    torch.cuda.synchronize()
+    z = x.double() @ wh.double().t() + bh.double()
+    if act == 1:
+        hz = torch.where(z > 0, z, z * slope)
+    elif act == 2:
+        hz = torch.tanh(z)
+    else:
+        hz = z
+    ref = hz @ wo.double().view(-1) + bo.double()
+    # the hidden layer's f32 error (4e-6 of sum |x w| per element) through |w_out|, plus the 256-term output sum's
+    bound = (4e-6 * (x.double().abs() @ wh.double().abs().t())) @ wo.double().abs().view(-1) + \
+        1e-6 * (hz.abs() @ wo.double().abs().view(-1)) + 1e-6
+    err = (v.double() - ref).abs()
+    assert torch.isfinite(v).all()
+    assert bool((err <= bound).all()), (err / bound).max().item()
+
+
+def test_deferred_bootstraps_k40v_equal_reference_critic(monkeypatch):
+    """The deferred bootstrap rows through K40V (opt-in, agents.VALUE_GEMM) against the reference-shaped critic
+    (trunk, library GEMM, K14's value head) on the same rows with the rollout's weights, to f32 accuracy; the update
+    phase then takes the K40V + compact-scan form (the e2e oracle replays run it end to end)."""
+    from xuanpolicy_amd.runner import build_synthbox_ppo
+    agent = build_synthbox_ppo(n_envs=1024, n_steps=16, obs_dim=17, act_dim=6, hidden=256, n_epoch=1, n_minibatch=4,
+                               seed=21, device="cuda:0", max_episode_steps=20)   # one slot: the fused scans apply
+    agent.value_gemm = True
+    agent.train(15, log=False)   # stops one step before the update: the rollout's weights and planes still current
+    fm = agent._rollout_mlp()
+    agent._boot_pair.normal_()   # any rows
+    v_k40v = fm.rollout_value_split(agent._boot_pair)
+    v_ref = fm.rollout_value(agent._boot_pair)
+    torch.cuda.synchronize()
+    assert v_k40v is not None
+    scale = v_ref.abs().max().item()
+    assert (v_k40v - v_ref).abs().max().item() <= 2e-5 * max(scale, 1.0)
+    agent.train(1, log=False)    # the last step + the update phase: K40V + the compact scan is the form taken
+    assert agent.gae_form == "compact" and agent.value_gemm

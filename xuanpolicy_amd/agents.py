@@ -55,6 +55,9 @@ FOLD_RMS = False
 # r06: K8's post step (and, with per-rank obs statistics, the next step's obs_rms.update) inside the env-fused K14 launch
 # (K14F, ops.rollout_policy_head_synthbox(post=)): a C2 env step in three launches instead of five
 FUSE_POST = True
+# r06 (opt-in): the deferred bootstrap rows' critic on K40V (split GEMM + value-head epilogue) feeding the compact GAE
+# scan — GAE 5.18 vs 5.56 us in the loop; off by default; XPA_VALUE_GEMM=1 or bench --gae-form k40v
+VALUE_GEMM = os.environ.get("XPA_VALUE_GEMM", "0") == "1"
 
 
 def rms_rollout_sync(start, end, all_reduce_sum):
@@ -150,6 +153,9 @@ class _OnPolicyAgent:
         self.device_env = hasattr(envs, "step_device")
         self.fuse_env_step = True   # device SynthBox env stepped inside K14 when possible (_env_fused)
         self.fuse_value_gae = True  # deferred bootstraps' value head inside the GAE scan (xpa_gae_scan_value)
+        # r06 (K40V): with fuse_value_gae, the deferred bootstraps' critic to the value on the split GEMM (the value head in
+        # its epilogue) and the compact GAE scan on exactly SURVEY.md §8(d)'s bytes, where it applies
+        self.value_gemm = VALUE_GEMM
         self.fuse_gather = True     # minibatch gather + adv moments inside the update's K13 (fused_mlp.Rows)
         # r05: the next step's obs_rms.update folded into K8 (xpa_rollout_post_deferred_norm_rms) on the device-env
         # path; _rms_pending: the current observation's statistics are not merged yet (the first step, or after
@@ -713,12 +719,23 @@ class _OnPolicyAgent:
             self._raw_last_bootstraps()
         elif self.raw_mid_next:
             self._raw_mid_from_next()
-        zc = None
+        zc = vk = None
         one_slot = self.defer_boot and self.n_slots == 1   # the fused scans take one deferred truncation per env
-        if (one_slot and not self.atari and not mem._pending and self.fuse_value_gae
+        if (one_slot and not self.atari and not mem._pending and self.fuse_value_gae and self.value_gemm
+                and self._rollout_mlp() is not None):
+            if getattr(self, "_vboot", None) is None:
+                self._vboot = torch.empty(self._boot_pair.shape[0], dtype=torch.float32, device=self.device)
+            vk = self._rollout_mlp().rollout_value_split(self._boot_pair, out=self._vboot)
+        if (vk is None and one_slot and not self.atari and not mem._pending and self.fuse_value_gae
                 and ops.gae_value_ok(self.n_steps) and self._rollout_mlp() is not None):
             zc = self._deferred_bootstraps(hidden_only=True)
-        if zc is not None:
+        if vk is not None:
+            # K40V's values, then one launch: the fixup's bootstrap writes fused into the compact-closure GAE scan
+            ops.gae_scan_compact(mem.rewards, mem.values, mem.terminals, self.slot_t, vk, mem.gamma, mem.gae_lam,
+                                 mem.use_gae, adv=mem._advantages, ret=mem._returns, boot=mem.boot)
+            mem._dirty = False
+            self.gae_form = "compact"
+        elif zc is not None:
             # one launch: the critic's output layer, the fixup's bootstrap writes and the compact GAE scan
             fm = self._rollout_mlp()
             lin_co = fm.critic[-1][0]

@@ -304,7 +304,8 @@ __device__ __forceinline__ void s3_gemm_body(const float *__restrict__ a, int64_
                                              const float *__restrict__ bias, float slope,
                                              unsigned char *__restrict__ sign, const int64_t *__restrict__ ridx,
                                              int64_t blk, const float *__restrict__ yab = nullptr,
-                                             const S3ActBwd *abp = nullptr) {
+                                             const S3ActBwd *abp = nullptr, const float *__restrict__ wo = nullptr,
+                                             const float *__restrict__ bo = nullptr) {
     using G = S3Geom<W>;
     // ONE LDS array (the DMA target; see head.hip)
     __shared__ __attribute__((aligned(16))) char lds[S * G::kStage];
@@ -367,6 +368,34 @@ __device__ __forceinline__ void s3_gemm_body(const float *__restrict__ a, int64_
                     for (int j = 0; j < 4; ++j) crow[j * 32] = acc[rt * 4 + j][r];
                 }
             }
+        return;
+    }
+    if constexpr (EPI >= 4) {
+        // K40V (r06): the critic's value head in the epilogue — c[row] = act(z[row] + bias) . wo + bo[0] with act
+        // identity / LeakyReLU (slope) / tanh for EPI 4 / 5 / 6: each lane's 8 columns in column-block order (one fmaf
+        // chain), then the 32 lanes of its row half in a fixed butterfly; the hidden layer's output is never stored
+        float bv[8], wv[8];
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb) {
+            bv[cb] = bias[cb * 32 + col];
+            wv[cb] = wo[cb * 32 + col];
+        }
+        const float b_out = bo[0];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float p = 0.f;
+#pragma unroll
+            for (int cb = 0; cb < 8; ++cb) {
+                float x = acc[cb][r] + bv[cb];
+                if constexpr (EPI == 5) x = x > 0.f ? x : x * slope;
+                if constexpr (EPI == 6) x = tanhf(x);
+                p = fmaf(x, wv[cb], p);
+            }
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) p += __shfl_xor(p, o, 64);
+            const int64_t row = r0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (col == 0 && row < M) c[row] = p + b_out;
+        }
         return;
     }
     if constexpr (EPI != 0) {
@@ -451,6 +480,18 @@ __global__ __launch_bounds__(64 * W, 8 / W) void s3_gemm_kernel(const float *__r
                                                                unsigned char *__restrict__ sign = nullptr,
                                                                const int64_t *__restrict__ ridx = nullptr) {
     s3_gemm_body<W, S, PROBE, T64, EPI>(a, lda, bs, c, ldc, M, nchunks, bias, slope, sign, ridx, blockIdx.x);
+}
+
+// K40V (r06): K40 with the value-head epilogue (EPI 4 / 5 / 6), v [M] out
+template <int W, int EPI>
+__global__ __launch_bounds__(64 * W, 8 / W) void s3_gemm_value_kernel(const float *__restrict__ a, int64_t lda,
+                                                                     const __bf16 *__restrict__ bs,
+                                                                     float *__restrict__ v, int64_t M, int nchunks,
+                                                                     const float *__restrict__ bias, float slope,
+                                                                     const float *__restrict__ wo,
+                                                                     const float *__restrict__ bo) {
+    s3_gemm_body<W, 3, 0, 0, EPI>(a, lda, bs, v, 1, M, nchunks, bias, slope, nullptr, nullptr, blockIdx.x, nullptr,
+                                  nullptr, wo, bo);
 }
 
 // K40G (r05): up to kS3Groups independent K40 problems of one shape in one launch (blockIdx.y = the problem): the
@@ -2327,6 +2368,26 @@ int gemm_bias_act_impl(const float *a, int64_t lda, const int64_t *ridx, const v
     return xpa_launch_status();
 }
 }  // namespace
+
+// K40V (r06): v [m] = act(a [m, k] . B + bias) . w_out + b_out[0] (act 0 identity / 1 LeakyReLU (slope) / 2 tanh; B
+// split by xpa_s3_split_b, 256 columns): the critic of the rollout's deferred bootstrap rows up to its value in one
+// launch, 64-row blocks (two waves of 32 rows x 256 columns) so a few thousand rows still spread over the chip
+XPA_API int xpa_s3_gemm_value(const float *a, int64_t lda, const void *b_split, float *v, int64_t m, int64_t k,
+                              const float *bias, int act, float slope, const float *w_out, const float *b_out,
+                              xpa_stream_t stream) {
+    if (!a || !b_split || !v || !bias || !w_out || !b_out || m <= 0 || k <= 0 || k % kKC != 0 || lda < k ||
+        (reinterpret_cast<uintptr_t>(a) & 15) || (lda & 3) || act < 0 || act > 2 || k / kKC > (1 << 20) ||
+        (m + 63) / 64 > 0x7fffffff)
+        return (int)hipErrorInvalidValue;
+    const __bf16 *bs = static_cast<const __bf16 *>(b_split);
+    const int nch = (int)(k / kKC);
+    const dim3 grid((unsigned)((m + 63) / 64)), block(128);
+    hipStream_t s = (hipStream_t)stream;
+    if (act == 0) s3_gemm_value_kernel<2, 4><<<grid, block, 0, s>>>(a, lda, bs, v, m, nch, bias, slope, w_out, b_out);
+    else if (act == 1) s3_gemm_value_kernel<2, 5><<<grid, block, 0, s>>>(a, lda, bs, v, m, nch, bias, slope, w_out, b_out);
+    else s3_gemm_value_kernel<2, 6><<<grid, block, 0, s>>>(a, lda, bs, v, m, nch, bias, slope, w_out, b_out);
+    return xpa_launch_status();
+}
 
 // K40R (r05): z [m, 512] = x [m, 256] . [B0 | B1] + bias, B0 / B1 split by xpa_s3_split_b (k = 256): the rollout's
 // paired hidden layer; each output is xpa_s3_gemm's + bias bit for bit

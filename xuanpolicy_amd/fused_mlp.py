@@ -454,6 +454,24 @@ class FusedActorCritic:
         return F.linear(s, lin_ch.weight, lin_ch.bias)
 
     @torch.no_grad()
+    def rollout_value_split(self, x, out=None):
+        """K40V (r06): the critic from x to its value in two launches — the trunk, then the critic's hidden layer on the
+        split GEMM (the rollout's planes of Wh_critic^T, rollout_refresh) with act . w_out + b_out in its epilogue — or
+        None where that form does not apply (no rollout planes, a critic deeper than one hidden layer)."""
+        rs = getattr(self, "_roll_split", None)
+        if rs is None or len(self.critic) != 2:
+            return None
+        lin_ch, code, slope = self.critic[-2]
+        lin_co = self.critic[-1][0]
+        if lin_co.out_features != 1 or lin_ch.in_features != 256 or lin_ch.out_features != 256:
+            return None
+        rep_outs = self._rep_forward(x)
+        s = rep_outs[-1] if rep_outs else x
+        if not (isinstance(s, torch.Tensor) and s.dim() == 2 and s.shape[1] == 256 and _vec4_rows(s)):
+            return None
+        return ops.s3_gemm_value(s, rs[1], 256, lin_ch.bias, code, slope, lin_co.weight.view(-1), lin_co.bias, out=out)
+
+    @torch.no_grad()
     def rollout_value(self, x, out=None):
         """Critic only (bootstrap values): trunk, critic hidden GEMM, K14 value head."""
         rep_outs = self._rep_forward(x)

@@ -425,6 +425,25 @@ def s3_split_padded(b, k_pad, out=None):
     return out
 
 
+def s3_gemm_value(a, b_split, k, bias, act, slope, w_out, b_out, out=None):
+    """K40V (r06): v [m] = act(a [m, k] . B + bias) . w_out + b_out (act = code 0 identity / 1 LeakyReLU / 2 tanh; B =
+    s3_split(W^T) of the critic's last hidden layer, 256 columns; w_out [256] or [1, 256], b_out [1])."""
+    _req(a, "a", torch.float32, contiguous=False)
+    if a.dim() != 2 or a.stride(1) != 1 or a.shape[1] < k or k % 16:
+        raise ValueError("a must be [m, >= k] with unit column stride, k % 16 == 0")
+    m = a.shape[0]
+    _req(bias, "bias", torch.float32, (HEAD_HIDDEN,))
+    if w_out.numel() != HEAD_HIDDEN or not w_out.is_contiguous() or w_out.dtype != torch.float32:
+        raise ValueError("w_out must be 256 contiguous float32 values")
+    _req(b_out, "b_out", torch.float32, (1,))
+    if out is None:
+        out = torch.empty(m, dtype=torch.float32, device=a.device)
+    _req(out, "out", torch.float32, (m,))
+    _lib.check(lib().xpa_s3_gemm_value(_p(a), a.stride(0), _p(b_split), _p(out), m, k, _p(bias), int(act), float(slope),
+                                       _p(w_out), _p(b_out), _stream(a.device)), "xpa_s3_gemm_value")
+    return out
+
+
 def s3_gemm_bias_act(a, b_split, k, bias, act, slope, out=None, sign=None, ridx=None):
     """K40F (r05): out [m, 256] = act(a [m, k] . B + bias) (act 0 identity / 1 LeakyReLU / 2 tanh); sign (int32 [m, 8],
     act 0 / 1): the output's sign bits for K42W.  a's columns past the layer width must be zero (padded rows).
