@@ -1018,6 +1018,15 @@ int64_t xpa_rollout_step_workspace(int64_t n_envs, int64_t obs_dim, int rms, int
 int xpa_s3_gemm_value(const float *a, int64_t lda, const void *b_split, float *v, int64_t m, int64_t k,
                       const float *bias, int act, float slope, const float *w_out, const float *b_out,
                       xpa_stream_t stream);
+/* K40T (r06): the rollout's trunk and paired hidden layer in one launch — xpa_thin_linear_act_fwd_norm (d_in <= 18,
+ * d_out 256: obs normalisation + Basic_MLP's first layer, mlp.py:21-51; normalised rows to xn and the buffer column)
+ * followed by xpa_s3_gemm_rows_pair on its h, with h formed in LDS and never stored (ppoclip_agent.py:63
+ * self.action(obs) -> representation + the policy's hidden layers).  z equals the two-launch form's bit for bit. */
+int xpa_s3_gemm_rows_pair_trunk(int act, const float *x, int64_t ldx, int64_t d_in, const float *w, const float *b,
+                                float slope, const float *mean, const float *var, float clip, float *xn, int64_t ldn,
+                                float *col, int64_t col_ld, const xpa_cursor_t *cursor, const void *b0_split,
+                                const void *b1_split, const float *bias, float *c, int64_t ldc, int64_t m,
+                                xpa_stream_t stream);
 /* Diagnostics: bits 1 / 2 / 4 end K14F's tail after the block partials / the group tickets / the group sums (results
  * then invalid: timing only; tools/k14f_probe.py); 0 = production. */
 int xpa_k14f_probe(int bits);

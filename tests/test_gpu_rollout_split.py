@@ -135,3 +135,77 @@ def test_deferred_bootstraps_k40v_equal_reference_critic(monkeypatch):
     assert (v_k40v - v_ref).abs().max().item() <= 2e-5 * max(scale, 1.0)
     agent.train(1, log=False)    # the last step + the update phase: K40V + the compact scan is the form taken
     assert agent.gae_form == "compact" and agent.value_gemm
+
+
+@pytest.mark.parametrize("M,din,code,with_col", [(4096, 17, 1, True), (1000, 17, 1, False), (777, 5, 2, True),
+                                                 (37, 18, 0, True), (65536, 17, 1, True)])
+def test_rows_pair_trunk_equals_two_launches(M, din, code, with_col):
+    """r06, K40T: the trunk (obs normalisation + thin first layer) formed inside K40R's launch equals the two-launch form
+    (xpa_thin_linear_act_fwd_norm, then xpa_s3_gemm_rows_pair on its h) bit for bit: z, the normalised rows in xn and
+    the rollout buffer column; ragged and XCD-mapped (M % 512 == 0) row counts, d_in forms 8 / 18, every activation."""
+    from xuanpolicy_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(M + din)
+    X = torch.randn(M, din + 3, device=DEV, generator=g) * 3 + 1
+    x = X[:, :din]                       # strided rows, as the env's observation view
+    mean = torch.randn(din, device=DEV, generator=g)
+    var = torch.rand(din, device=DEV, generator=g) + 0.1
+    W = torch.randn(256, din, device=DEV, generator=g) * 0.2
+    b = torch.randn(256, device=DEV, generator=g) * 0.1
+    wa = torch.randn(256, 256, device=DEV, generator=g) / 16
+    wc = torch.randn(256, 256, device=DEV, generator=g) / 16
+    bias = torch.randn(512, device=DEV, generator=g)
+    sa, sc = ops.s3_split(wa.t()), ops.s3_split(wc.t())
+    T = 5
+    cur = torch.tensor([3, 0, 0, 0], dtype=torch.int32, device=DEV)
+    L = ops.lib()
+    outs = []
+    for fused in (False, True):
+        xn = torch.full((M, din), 55.0, device=DEV)
+        col = torch.full((M, T, din), 66.0, device=DEV) if with_col else None
+        if fused:
+            z = ops.s3_gemm_rows_pair_trunk(x, W, b, code, 0.01, mean, var, 5.0, xn, col, T * din, cur, sa, sc, bias)
+        else:
+            h = torch.empty(M, 256, device=DEV)
+            assert L.xpa_thin_linear_act_fwd_norm(code, ops._p(x), x.stride(0), M, din, 256, ops._p(W), ops._p(b),
+                                                   0.01, ops._p(h), 256, ops._p(mean), ops._p(var), 5.0, ops._p(xn),
+                                                   din, ops._p(col) if with_col else None, T * din, ops._p(cur),
+                                                   ops._stream()) == 0
+            z = ops.s3_gemm_rows_pair(h, sa, sc, bias)
+        outs.append((z, xn, col))
+    torch.cuda.synchronize()
+    (z0, xn0, c0), (z1, xn1, c1) = outs
+    assert torch.equal(z1, z0)
+    assert torch.equal(xn1, xn0)
+    if with_col:
+        assert torch.equal(c1, c0)
+
+
+def test_rollout_with_k40t_bit_equal(monkeypatch):
+    """A C2-shaped rollout with the trunk inside K40R's launch (FusedActorCritic.ROLLOUT_TRUNK, opt-in) and with
+    K13-norm + K40R: the rollout buffers (observations, actions, log-probs, values) and the obs statistics are equal."""
+    from xuanpolicy_amd import ops
+    from xuanpolicy_amd.fused_mlp import FusedActorCritic
+    from xuanpolicy_amd.runner import build_synthbox_ppo
+    calls = []
+    k40t = ops.s3_gemm_rows_pair_trunk
+
+    def counted(*a, **k):
+        calls.append(1)
+        return k40t(*a, **k)
+    monkeypatch.setattr(ops, "s3_gemm_rows_pair_trunk", counted)
+    outs = []
+    for trunk in (True, False):
+        monkeypatch.setattr(FusedActorCritic, "ROLLOUT_TRUNK", trunk)
+        n0 = len(calls)
+        agent = build_synthbox_ppo(n_envs=1024, n_steps=16, obs_dim=17, act_dim=6, hidden=256, n_epoch=1,
+                                   n_minibatch=4, seed=11, device="cuda:0", max_episode_steps=9)
+        agent.train(16 + 15, log=False)   # a rollout + update, then 15 steps of the next rollout
+        assert (len(calls) > n0) == trunk     # K40T is the form the rollout took (captured or eager)
+        m = agent.memory
+        torch.cuda.synchronize()
+        outs.append((m.observations[:, :15].clone(), m.actions[:, :15].clone(),
+                     m.auxiliary_infos["old_logp"][:, :15].clone(), m.values[:, :15].clone(), agent.obs_mean.clone(),
+                     agent.obs_var.clone()))
+        del agent
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

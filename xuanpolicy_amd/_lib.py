@@ -293,6 +293,9 @@ SIGNATURES = {
     "xpa_rollout_step_workspace": (c_i64, [c_i64, c_i64, ctypes.c_int, c_p]),
     "xpa_k14f_probe": (ctypes.c_int, [ctypes.c_int]),
     "xpa_s3_gemm_value": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_i64, c_i64, c_p, ctypes.c_int, c_f32, c_p, c_p, c_p]),
+    "xpa_s3_gemm_rows_pair_trunk": (ctypes.c_int, [ctypes.c_int, c_p, c_i64, c_i64, c_p, c_p, c_f32, c_p, c_p, c_f32,
+                                                   c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64,
+                                                   c_p]),
     "xpa_rollout_step_synthbox": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f32,
                                                  c_p, c_p, c_p, c_p, c_p, c_p, c_u32, c_f32, c_p, c_p, c_p,
                                                  c_i64, c_p, c_u32, ctypes.c_int32, c_f32, c_f32, c_f32, c_p,

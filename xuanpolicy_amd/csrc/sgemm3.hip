@@ -617,6 +617,232 @@ __global__ __launch_bounds__(256, 1) void s3_gemm_r64_kernel(const float *__rest
     }
 }
 
+// K40T (r06): the rollout's trunk in K40R's launch — the block's 64 raw observation rows are normalised (clip((x -
+// mean) / (sqrt(var) + 1e-8)), xpa_thin_linear_act_fwd_norm's arithmetic), their trunk layer act(x . W^T + b) is
+// formed in the block (thread t <-> trunk column t = GEMM k index t, the same k-ascending fmaf chain as
+// thin_fwd_norm_kernel, so h is that kernel's bit for bit) straight into a resident f32 A image of all 16 k chunks (K40R's
+// swizzled layout), and the k loop streams only B's planes.  The trunk's h never reaches HBM; the 4 column-quarter
+// blocks of a row tile each form it (4 x 64 x din x 256 FMAs, ~1 us of VALU before the first MFMA, overlapped with B's
+// prefetch); the quarter-0 block writes the normalised rows to xn and the rollout buffer column.  Every z is K40R's on
+// thin_fwd_norm's h, bit for bit.
+template <int ACT>
+__device__ __forceinline__ float trunk_act(float z, float slope) {
+    if (ACT == 1) return z > 0.f ? z : z * slope;
+    if (ACT == 2) return tanhf(z);
+    return z;
+}
+
+constexpr int kTAImg = kRRows * kN * 4;   // 64 KiB: the block's h rows, all k chunks
+// W's rows in LDS at this stride (d_in <= kTWst for the d_in-20 form: the whole K40T LDS then stays under 160 KiB)
+template <int DMAX>
+struct TrunkW { static constexpr int kSt = DMAX == 8 ? 8 : 18; };
+template <int S, int CPS, int ACT, int DMAX, int PROBE = 0>
+__global__ __launch_bounds__(256, 1) void s3_gemm_r64_trunk_kernel(
+    const float *__restrict__ x, int64_t ldx, int din, const float *__restrict__ tw, const float *__restrict__ tb,
+    float slope, const float *__restrict__ mean, const float *__restrict__ var, float clip, float *__restrict__ xn,
+    int64_t ldn, float *__restrict__ col, int64_t col_ld, const xpa_cursor_t *__restrict__ cursor,
+    const __bf16 *__restrict__ bs0, const __bf16 *__restrict__ bs1, float *__restrict__ c, int64_t ldc, int64_t M,
+    const float *__restrict__ bias) {
+    constexpr int kSt = CPS * kRBImg;
+    constexpr int kNch = kN / kKC;
+    constexpr int kWst = TrunkW<DMAX>::kSt;
+    static_assert(kNch % CPS == 0 && (4 / CPS) * CPS == 4, "stages of CPS chunks, a trunk phase per 4 chunks");
+    static_assert(DMAX % 2 == 0 && kWst % 2 == 0, "feature pairs");
+    constexpr int kLds = kTAImg + S * kSt + kRRows * DMAX * 4 + kN * kWst * 4;
+    static_assert(kLds <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(16))) char lds[kLds];
+    float *aimg = reinterpret_cast<float *>(lds);
+    float *s_x = reinterpret_cast<float *>(lds + kTAImg + S * kSt);
+    float *wl = s_x + kRRows * DMAX;
+    const unsigned bbase = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_char_t *)lds) + kTAImg;
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int64_t r0 = (int64_t)blockIdx.x * kRRows;
+    const bool xr = (M & 511) == 0;   // K40R's XCD-aware row map
+    auto grow = [&](int R) -> int64_t {
+        if (!xr) return r0 + R;
+        const int64_t tt = (int64_t)(blockIdx.x & 7) + 8 * (8 * (int64_t)(blockIdx.x >> 3) + (R >> 3));
+        return 8 * tt + (R & 7);
+    };
+    const int q = blockIdx.y;
+    const char *bsrc0 = reinterpret_cast<const char *>(q < 2 ? bs0 : bs1);
+    const int coff = (q & 1) * 4;
+    constexpr int nst = kNch / CPS;
+    auto issue = [&](unsigned st, int stage) {
+#pragma unroll
+        for (int u = 0; u < CPS; ++u) {
+            const int ch = stage * CPS + u;
+            const char *bsrc = bsrc0 + (int64_t)ch * kBImg;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const int piece = wave * 3 + k, plane = piece >> 2, j = piece & 3;
+                glds16(bsrc + (plane * 8 + coff + j) * 1024 + lane * 16, st + (unsigned)(u * kRBImg + piece * 1024));
+            }
+        }
+    };
+#pragma unroll
+    for (int d = 0; d < S - 1; ++d) issue(bbase + d * kSt, d);
+    // W [256, din] into LDS (coalesced: a thread's own weights straight from global memory are 68-B strided across the
+    // lanes, ~34 cache lines per load instruction) and the normalised rows into s_x; every load issued before the
+    // first use (a rolled loop waited for each round trip in turn)
+    {
+        const int nw = kN * din;
+        constexpr int kWPer = (kN * DMAX + 255) / 256;
+        float wv[kWPer];
+#pragma unroll
+        for (int u = 0; u < kWPer; ++u) wv[u] = tw[min(t + 256 * u, nw - 1)];
+        constexpr int kPer = (kRRows * DMAX + 255) / 256;
+        float xv[kPer], mv[kPer], vv[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int i = min(t + 256 * u, kRRows * DMAX - 1);
+            const int R = i / DMAX, k = i - R * DMAX;
+            const int64_t row = grow(R);
+            const int kc = k < din ? k : 0;
+            const int64_t rc = row < M ? row : M - 1;
+            xv[u] = x[rc * ldx + kc];
+            mv[u] = mean[kc];
+            vv[u] = var[kc];
+        }
+#pragma unroll
+        for (int u = 0; u < kWPer; ++u) {
+            const int i = t + 256 * u;
+            if (i < nw) wl[(i / din) * kWst + i % din] = wv[u];
+        }
+        const int64_t cof = col ? (int64_t)cursor->ptr * din : 0;
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int i = t + 256 * u;
+            if (i >= kRRows * DMAX) break;
+            const int R = i / DMAX, k = i - R * DMAX;
+            const int64_t row = grow(R);
+            const bool ok = k < din && row < M;
+            float y = 0.f;
+            if (ok) {
+                const float sd = sqrtf(vv[u]);
+                y = (xv[u] - mv[u]) / (sd + 1e-8f);
+                y = fminf(fmaxf(y, -clip), clip);
+                if (q == 0) {
+                    xn[row * ldn + k] = y;
+                    if (col) col[row * col_ld + cof + k] = y;
+                }
+            }
+            s_x[((R >> 1) * DMAX + k) * 2 + (R & 1)] = y;   // row pairs: one float4 = features k, k + 1 of rows R, R + 1
+        }
+    }
+    __syncthreads();
+    // trunk phase p: the h columns 64 p .. 64 p + 63 = A chunks 4 p .. 4 p + 3, all 64 rows.  Lane (cq = lane & 15,
+    // rq = lane >> 4) of wave w: columns 64 p + cq + 16 i (i < 4) of rows 16 w + 4 rq .. + 3 (two row pairs) — eight
+    // independent v_pk_fma_f32 chains, each row's chain the k-ascending fmaf sequence of thin_fwd_norm_kernel (h is
+    // that kernel's bit for bit).  Column cc lands at chunk cc / 16, logical quad (cc / 4) & 3 (stored at quad ^ sw(R)),
+    // element cc & 3.  Phases 1-3 run inside the k loop, in the stages' DMA waits.
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const int cq = lane & 15, rq = lane >> 4;
+    float bcs[4][4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bcs[p][i] = tb[64 * p + cq + 16 * i];
+    auto trunk_phase = [&](int p) {
+        if constexpr ((PROBE & 1) != 0) return;
+        const int P0 = 8 * wave + 2 * rq;
+        f2 acc[2][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[u][i] = f2{0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < DMAX; k += 2) {
+            f2 wk[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const f2 wv = *reinterpret_cast<const f2 *>(wl + (64 * p + cq + 16 * i) * kWst + (k < kWst ? k : 0));
+                wk[i] = f2{k < din ? wv.x : 0.f, k + 1 < din ? wv.y : 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const float4 xv = *reinterpret_cast<const float4 *>(s_x + ((P0 + u) * DMAX + k) * 2);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    acc[u][i] = __builtin_elementwise_fma(f2{xv.x, xv.y}, f2{wk[i].x, wk[i].x}, acc[u][i]);
+                    acc[u][i] = __builtin_elementwise_fma(f2{xv.z, xv.w}, f2{wk[i].y, wk[i].y}, acc[u][i]);
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int cc = 64 * p + cq + 16 * i;
+            float *dst = aimg + (cc >> 4) * (kRRows * kKC) + (cc & 3);
+            const int lq = (cc >> 2) & 3;
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int R = 2 * (P0 + u) + e;
+                    dst[R * kKC + 4 * (lq ^ ((R >> 2) & 3))] = trunk_act<ACT>(acc[u][i][e] + bcs[p][i], slope);
+                }
+        }
+    };
+    trunk_phase(0);
+    if constexpr ((PROBE & 2) != 0) {   // diagnostics: the prologue alone (every prefetched DMA drained)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+    }
+    f32x16 acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    const int wr = wave & 1, wc = wave >> 1;
+    const int h = lane >> 5, i = lane & 31, sw = (i >> 2) & 3;
+    constexpr int kPerSt = 3 * CPS;
+    constexpr int kStPerPhase = 4 / CPS;
+#pragma unroll 1
+    for (int sg = 0; sg < nst; ++sg) {
+        // own B DMAs of stage sg landed (the `ahead` stages after it may fly) and own LDS writes (the trunk phases)
+        // done, then every wave's; the slot stage sg + S - 1 refills was read in stage sg - 1
+        const int ahead = min(nst - 1 - sg, S - 2);
+        switch (ahead) {
+        case 5: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(5 * kPerSt) : "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(4 * kPerSt) : "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(3 * kPerSt) : "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * kPerSt) : "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(kPerSt) : "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        if (sg + S - 1 < nst) issue(bbase + ((sg + S - 1) % S) * kSt, sg + S - 1);
+#pragma unroll
+        for (int u = 0; u < CPS; ++u) {
+            const int ch = sg * CPS + u;
+            const char *st = lds + kTAImg + (sg % S) * kSt + u * kRBImg;
+            const float *arow = aimg + ch * (kRRows * kKC) + (32 * wr + i) * kKC;
+            bf16x8 ah, am, al;
+            xpa_split8(*reinterpret_cast<const float4 *>(arow + 4 * (h ^ sw)),
+                       *reinterpret_cast<const float4 *>(arow + 4 * ((h + 2) ^ sw)), ah, am, al);
+            const bf16x8 *bimg = reinterpret_cast<const bf16x8 *>(st) + lane;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int cbl = 2 * wc + j;
+                acc[j] = xpa_mfma_s3(ah, am, al, bimg[cbl * 64], bimg[(4 + cbl) * 64], bimg[(8 + cbl) * 64], acc[j]);
+            }
+        }
+        // the next trunk phase while this stage's MFMAs run: phase p + 1 is first read at stage (p + 1) kStPerPhase,
+        // at least one barrier (with its lgkmcnt(0)) later
+        if (sg % kStPerPhase == 0 && sg / kStPerPhase + 1 < 4) trunk_phase(sg / kStPerPhase + 1);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int cl = q * 128 + (2 * wc + j) * 32 + i;
+        const float bv = bias[cl];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t row = grow(32 * wr + (r & 3) + 8 * (r >> 2) + 4 * h);
+            if (row < M) c[row * ldc + cl] = acc[j][r] + bv;
+        }
+    }
+}
+
 // K40W: K40 with the roles split over the waves (as K41W): waves 4-7 (producers) DMA the operands of chunk c + 2 (their
 // own 32 A rows each + B's planes) and split chunk c + 1's A rows (own DMAs, so a vmcnt wait suffices) into the bf16
 // planes of the stage, while waves 0-3 (consumers, one per SIMD, 32 rows x 256 columns each) read ready planes and run
@@ -2405,6 +2631,44 @@ XPA_API int xpa_s3_gemm_rows_pair(const float *a, int64_t lda, const void *b0_sp
         s3_gemm_r64_kernel<3, 2><<<grid, dim3(256), 0, stream>>>(a, lda, b0, b1, c, ldc, m, kN / kKC, bias);
     else
         s3_gemm_r64_kernel<2, 4><<<grid, dim3(256), 0, stream>>>(a, lda, b0, b1, c, ldc, m, kN / kKC, bias);
+    return xpa_launch_status();
+}
+
+// K40T (r06): xpa_thin_linear_act_fwd_norm (d_out 256, d_in <= 20; h not stored) + xpa_s3_gemm_rows_pair in one launch
+XPA_API int xpa_s3_gemm_rows_pair_trunk(int act, const float *x, int64_t ldx, int64_t d_in, const float *w,
+                                        const float *b, float slope, const float *mean, const float *var, float clip,
+                                        float *xn, int64_t ldn, float *col, int64_t col_ld, const xpa_cursor_t *cursor,
+                                        const void *b0_split, const void *b1_split, const float *bias, float *c,
+                                        int64_t ldc, int64_t m, xpa_stream_t stream) {
+    if (!x || !w || !b || !mean || !var || !xn || !b0_split || !b1_split || !bias || !c || m <= 0 || d_in < 1 ||
+        d_in > TrunkW<20>::kSt || act < 0 || act > 2 || ldx < d_in || ldn < d_in || ldc < 2 * kN ||
+        (col && (!cursor || col_ld < d_in)) || (m + kRRows - 1) / kRRows > 0x7fffffff)
+        return (int)hipErrorInvalidValue;
+    const dim3 grid((unsigned)((m + kRRows - 1) / kRRows), 4);
+    const __bf16 *b0 = static_cast<const __bf16 *>(b0_split), *b1 = static_cast<const __bf16 *>(b1_split);
+    hipStream_t s = (hipStream_t)stream;
+    const int din = (int)d_in;
+#define XPA_K40T_P(A_, D_, P_)                                                                                        \
+    s3_gemm_r64_trunk_kernel<3, 2, A_, D_, P_><<<grid, dim3(256), 0, s>>>(x, ldx, din, w, b, slope, mean, var, clip,  \
+                                                                           xn, ldn, col, col_ld, cursor, b0, b1, c, ldc, \
+                                                                           m, bias)
+    // diagnostics (xpa_s3_probe, tools/k40t_probe.py; act 1, d_in 9-18): 4096 = no trunk FMAs, 8192 = the prologue
+    // (loads, staging, trunk phase 0) alone
+    if ((g_s3_probe & 12288) && act == 1 && din > 8) {
+        if (g_s3_probe & 4096) XPA_K40T_P(1, 20, 1);
+        else XPA_K40T_P(1, 20, 2);
+        return xpa_launch_status();
+    }
+    if (din <= 8) {
+        if (act == 0) XPA_K40T_P(0, 8, 0);
+        else if (act == 1) XPA_K40T_P(1, 8, 0);
+        else XPA_K40T_P(2, 8, 0);
+    } else {
+        if (act == 0) XPA_K40T_P(0, 20, 0);
+        else if (act == 1) XPA_K40T_P(1, 20, 0);
+        else XPA_K40T_P(2, 20, 0);
+    }
+#undef XPA_K40T_P
     return xpa_launch_status();
 }
 

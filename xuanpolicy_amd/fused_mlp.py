@@ -17,6 +17,8 @@ Forward: F.linear (GEMM + bias epilogue) then the activation in place; the activ
 kept (LeakyReLU/ReLU/tanh derivatives are functions of the output), no pre-activation copies.
 Every parameter gradient is overwritten each update, so no zeroing pass is needed.
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -420,6 +422,23 @@ class FusedActorCritic:
             return ops.s3_gemm_rows_pair(s, rs[0], rs[1], self.pair[1])
         return F.linear(s, self.pair[0], self.pair[1])
 
+    # r06 (K40T, opt-in: XPA_ROLLOUT_TRUNK=1): with the normalisation fused (norm given), a one-layer thin trunk
+    # (d_in <= 18) and K40R's planes, the trunk runs inside the paired hidden GEMM's launch (h never stored).  Measured
+    # no faster than K13-norm + K40R (20.4-22.4 vs 20.7 us per env step at C2), so off
+    ROLLOUT_TRUNK = os.environ.get("XPA_ROLLOUT_TRUNK", "0") == "1"
+
+    def _rollout_trunk_pair(self, x, norm):
+        rs = getattr(self, "_roll_split", None)
+        if (not self.ROLLOUT_TRUNK or norm is None or rs is None or not self.thin0 or len(self.rep) != 1
+                or x.dim() != 2 or x.dtype != torch.float32 or x.stride(1) != 1):
+            return None
+        lin, code, slope = self.rep[0]
+        if lin.in_features > 18 or lin.out_features != 256:
+            return None
+        mean, var, clip, xn, col, col_ld, cursor = norm
+        return ops.s3_gemm_rows_pair_trunk(x, lin.weight, lin.bias, code, slope, mean, var, clip, xn, col, col_ld,
+                                           cursor, rs[0], rs[1], self.pair[1])
+
     @torch.no_grad()
     def rollout_act(self, x, dist, cursor, seed, buf_act, buf_logp, buf_val, env_in, act_clip=1.0, norm=None,
                     env=None, post=None):
@@ -427,9 +446,11 @@ class FusedActorCritic:
         norm: see _rep_forward (x is then the raw observation).  env: a device SynthBox env whose step runs
         inside the same K14 launch (ops.rollout_policy_head_synthbox; the caller skips env.step_device()).
         post (with env, r06): K8's post step in that launch too (K14F; ops.rollout_policy_head_synthbox(post=))."""
-        rep_outs = self._rep_forward(x, norm=norm)
-        s = rep_outs[-1] if rep_outs else x
-        z = self._rollout_pair(s)
+        z = self._rollout_trunk_pair(x, norm)
+        if z is None:
+            rep_outs = self._rep_forward(x, norm=norm)
+            s = rep_outs[-1] if rep_outs else x
+            z = self._rollout_pair(s)
         H = ops.HEAD_HIDDEN
         lin_ao = self.actor[-1][0]
         lin_co = self.critic[-1][0]

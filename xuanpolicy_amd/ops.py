@@ -405,6 +405,37 @@ def s3_gemm_rows_pair(a, b0_split, b1_split, bias, out=None):
     return out
 
 
+def s3_gemm_rows_pair_trunk(x, w, b, act, slope, mean, var, clip, xn, col, col_ld, cursor, b0_split, b1_split, bias,
+                            out=None):
+    """K40T (r06): the rollout's trunk (obs normalisation + Linear(d_in, 256) + act, d_in <= 18; xn and the buffer column
+    col (nullable) get the normalised rows as xpa_thin_linear_act_fwd_norm writes them) and K40R on its h in one launch;
+    h stays in LDS.  out [m, 512] equals the two-launch form's bit for bit."""
+    _req(x, "x", torch.float32, contiguous=False)
+    m, d_in = x.shape
+    if x.stride(1) != 1 or not 1 <= d_in <= 18:
+        raise ValueError("x must be [m, d_in <= 18] with unit column stride")
+    _req(w, "w", torch.float32, (256, d_in))
+    _req(b, "b", torch.float32, (256,))
+    _req(mean, "mean", torch.float32, (d_in,))
+    _req(var, "var", torch.float32, (d_in,))
+    _req(bias, "bias", torch.float32, (512,))
+    if xn.dtype != torch.float32 or xn.shape[0] != m or xn.shape[1] != d_in or xn.stride(1) != 1:
+        raise ValueError("xn must be float32 [m, d_in] with unit column stride")
+    if out is None:
+        out = torch.empty(m, 512, dtype=torch.float32, device=x.device)
+    ldc = _row_stride(out, "out", 512)
+    if out.shape[0] != m:
+        raise ValueError("out must have %d rows" % m)
+    nb = int(lib().xpa_s3_split_bytes(256, 256))
+    for bb in (b0_split, b1_split):
+        _req(bb, "b_split", torch.uint8, (nb,))
+    _lib.check(lib().xpa_s3_gemm_rows_pair_trunk(
+        int(act), _p(x), x.stride(0), d_in, _p(w), _p(b), float(slope), _p(mean), _p(var), float(clip), _p(xn),
+        xn.stride(0), _p(col) if col is not None else None, int(col_ld), _p(cursor) if col is not None else None,
+        _p(b0_split), _p(b1_split), _p(bias), _p(out), ldc, m, _stream(x.device)), "xpa_s3_gemm_rows_pair_trunk")
+    return out
+
+
 def s3_split_padded(b, k_pad, out=None):
     """The split of b [kv, 256] (any strides) padded with zero rows to k_pad (a multiple of 16): K40F's operand for a
     layer width that is not a multiple of 16 (xpa_s3_split_batch_padded)."""
