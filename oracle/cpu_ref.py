@@ -492,10 +492,59 @@ class LearnerRef:
         self.clip_range, self.clip_grad_norm, self.use_grad_clip = clip_range, clip_grad_norm, use_grad_clip
         self.iterations = 0
 
+    def _kink_hooks_arm(self):
+        """Forward hooks recording every (Linear -> LeakyReLU / ReLU) pair's input, pre-activation and activation (the
+        activation with retain_grad) for _kink_rows."""
+        torch = _torch()
+        nn = torch.nn
+        self._kink_rec, self._kink_handles = [], []
+        for m in self.policy.modules():
+            if not isinstance(m, nn.Sequential):
+                continue
+            mods = list(m)
+            for a, b in zip(mods, mods[1:]):
+                if isinstance(a, nn.Linear) and isinstance(b, (nn.LeakyReLU, nn.ReLU)):
+                    slope = float(b.negative_slope) if isinstance(b, nn.LeakyReLU) else 0.0
+                    rec = {"lin": a, "slope": slope}
+                    self._kink_rec.append(rec)
+
+                    def lin_hook(mod, inp, out, rec=rec):
+                        rec["a"], rec["z"] = inp[0], out
+
+                    def act_hook(mod, inp, out, rec=rec):
+                        if out.requires_grad:
+                            out.retain_grad()
+                        rec["h"] = out
+                    self._kink_handles += [a.register_forward_hook(lin_hook), b.register_forward_hook(act_hook)]
+
+    def _kink_hooks_clear(self):
+        for hd in getattr(self, "_kink_handles", []):
+            hd.remove()
+        self._kink_handles, self._kink_rec = [], []
+
+    def _kink_rows(self, cap=16):
+        """The (row, unit) pre-activations within 4e-6 of sum |a w| (the split GEMM's f32 error bound) of zero, the
+        closest first: [(z, h, row, unit, slope)]."""
+        torch = _torch()
+        cands = []
+        for rec in getattr(self, "_kink_rec", []):
+            if "z" not in rec or rec["z"].dim() != 2:
+                continue
+            z, a, W = rec["z"].detach(), rec["a"].detach(), rec["lin"].weight.detach()
+            bound = 4e-6 * (a.abs() @ W.abs().t())
+            r = z.abs() / (bound + 1e-30)
+            idx = ((r <= 1.0) & (bound > 1e-20)).nonzero()   # (an all-zero input row: z is exact on every side)
+            for i, u in idx.tolist():
+                cands.append((float(r[i, u]), rec["z"], rec["h"], i, u, rec["slope"]))
+        cands.sort(key=lambda c: c[0])
+        return [c[1:] for c in cands[:cap]]
+
     def update(self, obs, act, ret, adv, old_logp=None, capture_grads=False):
         """capture_grads: keep every parameter's gradient before clipping in self.last_grads (lock-step replays)."""
         torch = _torch()
         self.iterations += 1
+        if capture_grads:
+            self._kink_hooks_arm()
         if not (isinstance(obs, np.ndarray) and obs.dtype == np.uint8):   # raw frames: the policy scales them
             # f32 observations; an f64 replay (precision envelopes) takes them exactly in its parameters' dtype
             obs = torch.as_tensor(obs, dtype=torch.float32).to(next(self.policy.parameters()).dtype)
@@ -520,6 +569,7 @@ class LearnerRef:
         loss = a_loss - self.ent_coef * e_loss + self.vf_coef * c_loss
         self.optimizer.zero_grad()
         boundary = []
+        kinks = self._kink_rows() if capture_grads else []
         if capture_grads and self.algo == "ppo":
             # rows whose ratio sits within f32 rounding of a clip bound (the window below): which branch of min() /
             # clamp() they take is not decided by the math, so a correct f32 implementation may include or drop their
@@ -532,9 +582,22 @@ class LearnerRef:
                 g = torch.autograd.grad(-(adv[i] * ratio[i]) / ratio.shape[0], params, retain_graph=True,
                                         allow_unused=True)
                 boundary.append([torch.zeros_like(p) if x is None else x.detach().clone() for p, x in zip(params, g)])
-        loss.backward()
+        loss.backward(retain_graph=bool(kinks))
         if capture_grads:
             self.last_grads = [p.grad.detach().clone() for p in self.policy.parameters()]
+            # (row, unit) pre-activations within the f32 GEMM's rounding of a (Leaky)ReLU kink: the side the device's
+            # z lands on is not decided by the math either; flipping it changes that row's gradient by
+            # (s_other - s) dL/dh(row, unit) grad_theta z(row, unit).  Kept per candidate (at most 16) beside the
+            # clip-bound rows.
+            params = list(self.policy.parameters())
+            for z, h, i, u, slope in kinks:
+                if h.grad is None:
+                    continue
+                s_cur = 1.0 if float(z[i, u].detach()) > 0 else slope
+                g = torch.autograd.grad(z[i, u], params, retain_graph=True, allow_unused=True)
+                f = ((slope if s_cur == 1.0 else 1.0) - s_cur) * float(h.grad[i, u])
+                boundary.append([torch.zeros_like(p) if x is None else f * x.detach() for p, x in zip(params, g)])
+            self._kink_hooks_clear()
             self.boundary_grads = boundary
         if self.algo == "a2c" or self.use_grad_clip:
             torch.nn.utils.clip_grad_norm_(self.policy.parameters(), self.clip_grad_norm)

@@ -55,9 +55,10 @@ FOLD_RMS = False
 # r06: K8's post step (and, with per-rank obs statistics, the next step's obs_rms.update) inside the env-fused K14 launch
 # (K14F, ops.rollout_policy_head_synthbox(post=)): a C2 env step in three launches instead of five
 FUSE_POST = True
-# r06 (opt-in): the deferred bootstrap rows' critic on K40V (split GEMM + value-head epilogue) feeding the compact GAE
-# scan — GAE 5.18 vs 5.56 us in the loop; off by default; XPA_VALUE_GEMM=1 or bench --gae-form k40v
-VALUE_GEMM = os.environ.get("XPA_VALUE_GEMM", "0") == "1"
+# r06: the deferred bootstrap rows' critic on K40V (split GEMM + value-head epilogue) feeding the compact GAE scan —
+# GAE 5.18 vs 5.56 us in the loop; XPA_VALUE_GEMM=0 / bench --gae-form value: the value-fused
+# scan (K1V)
+VALUE_GEMM = os.environ.get("XPA_VALUE_GEMM", "1") != "0"
 
 
 def rms_rollout_sync(start, end, all_reduce_sum):
