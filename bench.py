@@ -51,8 +51,8 @@ def parse():
     p.add_argument("--no-c4", action="store_true", help="skip the C4 Box(376,17) measurement")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--out", default=None, help="also write the JSON line to this file")
-    p.add_argument("--gae-form", choices=("k40v", "value", "split"), default="k40v",
-                   help="k40v (r06, the default): the deferred bootstraps' critic to the value on the split GEMM (K40V, the value "
+    p.add_argument("--gae-form", choices=("k40v", "value", "split"), default="value",
+                   help="k40v (r06, opt-in: the scan faster, the K40V launch before it slower than value's GEMM): the deferred bootstraps' critic to the value on the split GEMM (K40V, the value "
                         "head in its epilogue), then the compact GAE scan (K1) on exactly the §8(d) bytes; value: the "
                         "value head fused into the GAE scan (K1V, one launch); split: hipBLASLt + value head (K14) "
                         "then the compact GAE scan")

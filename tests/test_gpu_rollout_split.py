@@ -117,7 +117,7 @@ def test_gemm_value_matches_f64(M, act):
 
 
 def test_deferred_bootstraps_k40v_equal_reference_critic(monkeypatch):
-    """The deferred bootstrap rows through K40V (the default, agents.VALUE_GEMM) against the reference-shaped critic
+    """The deferred bootstrap rows through K40V (opt-in, agents.VALUE_GEMM) against the reference-shaped critic
     (trunk, library GEMM, K14's value head) on the same rows with the rollout's weights, to f32 accuracy; the update
     phase then takes the K40V + compact-scan form (the e2e oracle replays run it end to end)."""
     from xuanpolicy_amd.runner import build_synthbox_ppo

@@ -55,10 +55,11 @@ FOLD_RMS = False
 # r06: K8's post step (and, with per-rank obs statistics, the next step's obs_rms.update) inside the env-fused K14 launch
 # (K14F, ops.rollout_policy_head_synthbox(post=)): a C2 env step in three launches instead of five
 FUSE_POST = True
-# r06: the deferred bootstrap rows' critic on K40V (split GEMM + value-head epilogue) feeding the compact GAE scan —
-# GAE 5.18 vs 5.56 us in the loop; XPA_VALUE_GEMM=0 / bench --gae-form value: the value-fused
-# scan (K1V)
-VALUE_GEMM = os.environ.get("XPA_VALUE_GEMM", "1") != "0"
+# r06 (opt-in, XPA_VALUE_GEMM=1 / bench --gae-form k40v): the deferred bootstrap rows' critic on K40V (split GEMM +
+# value-head epilogue) feeding the compact GAE scan.  The scan is faster (5.3 vs 6.0 us) but K40V's launch, 64 blocks
+# each streaming all of B, costs 25.6 us against the library GEMM's 15.1 for the value form: 30.9 vs 21.1 us per
+# iteration, so the value-fused scan (K1V) stays the default
+VALUE_GEMM = os.environ.get("XPA_VALUE_GEMM", "0") == "1"
 
 
 def rms_rollout_sync(start, end, all_reduce_sum):
